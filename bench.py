@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Headline benchmark: additive NFFT kernel matvecs/s (+ PCG wall time to 1e-6) on MI355X.
+
+Workload (BASELINE.json configs[2], "headline single-GPU"): n = 1e6 points, d = 32 features, 32 1-D
+additive windows {0},{1},...,{31}, Gaussian kernel f = 1, l = 1, mu = 0.01; points i.i.d. U[0,1)^d,
+vector x ~ U(-0.5, 0.5) (TESTS/TEST1/foo.cpp:243-247), numpy PCG64 seed 906 (synthetic data).
+One "step" = one Nfft4GPAdditiveNFFTMatSymv(y = K x) with x and y resident in HBM.
+
+N = 1:  the matvec on one GPU.
+N > 1:  one process per GPU (torch.distributed, RCCL).  Rows are sharded: each rank spreads its own
+        n/N points for all 32 windows, the 32x64 oversampled grids (16 KB) are all-reduced over
+        xGMI, and each rank interpolates its own rows.  Total work is fixed -> "scaling": "strong".
+
+Printed (rank 0): one JSON line with value = whole-job matvecs/s, the roofline of the dominant kernel
+(measured live with hipEvents on the library stream), the CPU baseline (this repo's C/OpenMP
+restatement of the reference NFFT path = oracle/, "kind": "port", on a bounded sample), and PCG
+time to 1e-6 (unpreconditioned, N = 1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def make_problem(n, d, seed=906):
+    rng = np.random.default_rng(seed)
+    X = rng.random((n, d))
+    x = rng.random(n) - 0.5
+    return X, x
+
+
+def algorithmic_bytes(info, n, nw, beta_zero=True):
+    """Bytes each kernel must move with this layout ('Roofline'):
+    spread: 6 B per (point, window) [u16 index + u32 fixed-point coordinate] + 8n (alpha)
+            + nblocks*nw*64*8 (partial grids);
+    interp: 6 B per (point, window) + 8n (x for the mu term) + 8n (y write) [+ 8n y read if beta != 0]."""
+    pc = n * nw
+    parts = info["nblocks"] * nw * 64 * 8
+    spread = 6 * pc + 8 * n + parts
+    interp = 6 * pc + 16 * n + (0 if beta_zero else 8 * n)
+    return spread, interp
+
+
+def cpu_baseline(n, d, X, x, max_seconds=25.0):
+    """Oracle (C + OpenMP restatement of nfft_interface.c + NFFT3 fastsum) on this host."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc_mod
+    lib = None
+    # prefer a -march=native build of the oracle for this host (built into a scratch dir)
+    try:
+        out_dir = os.path.join(ROOT, "gpurun_out", "oracle_native")
+        os.makedirs(out_dir, exist_ok=True)
+        so = os.path.join(out_dir, "liboracle_native.so")
+        subprocess.run(["gcc", "-O3", "-march=native", "-fPIC", "-fopenmp", "-std=gnu11", "-shared",
+                        os.path.join(ROOT, "oracle", "nfft4gp_oracle.c"), "-o", so, "-lm"],
+                       check=True, capture_output=True, timeout=120)
+        lib = orc_mod.oracle_lib(so)
+        native = True
+    except Exception:
+        lib = orc_mod.oracle_lib()
+        native = False
+    win = np.arange(d, dtype=np.int32)
+    o = orc_mod.OracleAdditiveNFFT(X, win, d, 1, lib=lib)
+    t0 = time.time()
+    o.setup(0, 1.0, 1.0, 0.01)
+    t_setup = time.time() - t0
+    o.matsymv(x)  # warm
+    reps, t_total = 0, 0.0
+    while t_total < max_seconds and reps < 20:
+        t0 = time.time()
+        o.matsymv(x)
+        t_total += time.time() - t0
+        reps += 1
+        if t_total > 0.5 * max_seconds:
+            break
+    threads = int(lib.orc_num_threads())
+    return {
+        "value": reps / t_total,
+        "unit": "matvecs/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{reps} matvecs of the full workload (n={n}, {d} windows) after one warm-up; "
+                  f"setup (PRE_PSI taps, bhat) {t_setup:.1f}s untimed; -march=native={native}; "
+                  f"OMP threads={threads}",
+    }
+
+
+def run_pcg_single(op, torch, n, rng_seed=906, tol=1e-6, maxits=3000):
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    rng = np.random.default_rng(rng_seed + 1)
+    b = torch.tensor(rng.random(n) - 0.5, device="cuda")
+    x = torch.zeros(n, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    t0 = time.time()
+    _, relres, hist, iters = amd.pcg(op, b, x, maxits=maxits, tol=tol)
+    torch.cuda.synchronize()
+    t = time.time() - t0
+    return {"pcg_time_s": t, "pcg_iters": iters, "pcg_rel_res": relres, "pcg_converged": iters > 0,
+            "pcg_precond": "none", "pcg_tol": tol}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--d", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcg", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local_rank)
+    L = amd.lib()
+    L.Nfft4GPAmdSetStream(torch.cuda.current_stream().cuda_stream)
+
+    n, d = args.n, args.d
+    X, x_host = make_problem(n, d)
+    win = np.arange(d, dtype=np.int32)
+    if world == 1:
+        op = amd.NFFTAdditiveKernel(X, win, d, 1)
+        rb, re = 0, n
+    else:
+        per = (n + world - 1) // world
+        rb, re = min(n, rank * per), min(n, (rank + 1) * per)
+        op = amd.NFFTAdditiveKernel(X, win, d, 1, shard=(rb, re))
+    t0 = time.time()
+    rc = op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01)
+    setup_s = time.time() - t0
+    if rc != 0:
+        raise SystemExit("setup failed")
+    xd = torch.tensor(x_host[rb:re], device="cuda")
+    yd = torch.zeros(re - rb, dtype=torch.float64, device="cuda")
+    grid = torch.zeros(d * 64, dtype=torch.float64, device="cuda")
+
+    def step():
+        if world == 1:
+            op.matsymv(xd, 1.0, 0.0, yd)
+        else:
+            op.shard_spread(xd, grid)
+            dist.all_reduce(grid)
+            op.shard_finish(grid, xd, 1.0, 0.0, yd)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    if world == 1:
+        op.timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    result = {
+        "metric": "kernel matvecs/sec (additive NFFT (K+sigma^2 I)v, n=1e6, d=32 1-D windows)",
+        "value": args.steps / elapsed,
+        "unit": "matvecs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: X ~ U[0,1)^d, x ~ U(-0.5,0.5), numpy PCG64 seed 906",
+        "config": {"workload": f"additive NFFT matvec, n={n}, d={d}, {d} x 1-D windows, Gaussian f=1 l=1 "
+                               "mu=0.01 (BASELINE configs[2]); N>1: rows sharded, 32x64 grid all-reduce",
+                   "n": n, "d": d, "nwindows": d, "setup_s": setup_s,
+                   "parallelism": f"rows{world}" if world > 1 else "single"},
+    }
+    if world == 1:
+        tq = op.timing_query()
+        op.timing(False)
+        info = op.layout_info()
+        b_spread, b_interp = algorithmic_bytes(info, n, d)
+        avg = {k: (v[0] / max(v[1], 1)) for k, v in tq.items()}  # ms
+        dom = "spread" if avg["spread"] >= avg["interp"] else "interp"
+        bytes_dom = b_spread if dom == "spread" else b_interp
+        achieved = bytes_dom / (avg[dom] * 1e-3) / 1e9
+        result["roofline"] = {"bound": "hbm", "kernel": f"k_{dom}", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                              "algorithmic_bytes_per_launch": bytes_dom,
+                              "avg_launch_ms": avg[dom]}
+        result["kernels_ms"] = avg
+        result["layout"] = info
+        # survey-defined whole-matvec bytes (fp64 coords: 8n(2d+2)) for reference
+        result["matvec_bytes_survey_def"] = 8 * n * (2 * d + 2)
+        if not args.no_pcg:
+            result.update(run_pcg_single(op, torch, n))
+        if not args.no_cpu_baseline:
+            try:
+                result["cpu_baseline"] = cpu_baseline(n, d, X, x_host)
+            except Exception as e:  # report, do not fail the GPU measurement
+                result["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

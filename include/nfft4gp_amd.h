@@ -1,0 +1,191 @@
+/*
+ * nfft4gp_amd.h -- C ABI of the MI355X-native NFFT additive-kernel operator.
+ *
+ * Drop-in replacement for the hot-path subset of the reference header
+ *   INC/nfft4gp_headers.h:9-23  (aggregating INC/_linearalg.h, _solvers.h, _preconds.h, _external.h)
+ * of Hitenze/Preconditioned_Additive_Gaussian_Processes_with_Fourier_Acceleration.
+ *
+ * Differences from the reference header, all deliberate:
+ *  - no NFFT3/FFTW includes (INC/_external.h:4-20): str_adj's fastsum_plan members are internal;
+ *  - vectors x, y, rhs may be HOST or DEVICE (hipMalloc) pointers; the library detects which with
+ *    hipPointerGetAttributes.  Device pointers run with no PCIe traffic and no host sync, enqueued
+ *    on the stream set by Nfft4GPAmdSetStream (default: the null stream, ordered with torch's
+ *    default stream).  Host pointers are staged through device buffers and the call is synchronous.
+ *  - every computation runs on the GPU; there is no CPU fallback.  If no HIP device is present the
+ *    operator entry points print an error and return -1.
+ *  - callbacks handed to Nfft4GPSolverPcg receive DEVICE pointers (all operators in this library
+ *    accept them).
+ *
+ * Precision: NFFT4GP_DOUBLE is double (the reference default, SRC/utils/utils.h:28-31).
+ */
+#ifndef NFFT4GP_AMD_H
+#define NFFT4GP_AMD_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef NFFT4GP_DOUBLE
+#define NFFT4GP_DOUBLE double
+#endif
+
+#ifndef NFFT4GP_KERNEL_MAX_PARAMS
+#define NFFT4GP_KERNEL_MAX_PARAMS 5 /* SRC/linearalg/kernels.h:59-61 */
+#endif
+
+/* ---- function-pointer types (unchanged) ------------------------------------------------------ */
+/* SRC/linearalg/kernels.h:49 */
+typedef int (*func_kernel)(void *str, NFFT4GP_DOUBLE *data, int n, int ldim, int d, int *permr, int kr,
+                           int *permc, int kc, NFFT4GP_DOUBLE **Kp, NFFT4GP_DOUBLE **dKp);
+/* SRC/solvers/solvers.h:21 */
+typedef int (*func_solve)(void *precond, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
+/* SRC/solvers/solvers.h:49 */
+typedef int (*func_symmatvec)(void *matrix, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x,
+                              NFFT4GP_DOUBLE beta, NFFT4GP_DOUBLE *y);
+/* SRC/utils/utils.h (func_free) */
+typedef void (*func_free)(void *str);
+
+/* ---- kernel handle: field layout identical to SRC/linearalg/kernels.h:65-95 -------------------
+ * Callers write _params[0] (f), _params[1] (l) and _noise_level (mu) directly
+ * (SRC/optimizer/gp_loss.c:143-150, TESTS/TEST1/foo.cpp:222-224).  _external points at the
+ * library's device-side plan (opaque). */
+typedef struct NFFT4GP_KERNEL_STRUCT
+{
+   NFFT4GP_DOUBLE _params[NFFT4GP_KERNEL_MAX_PARAMS];
+   int _iparams[NFFT4GP_KERNEL_MAX_PARAMS];
+   int _max_n;
+   int _omp;
+   NFFT4GP_DOUBLE _noise_level;
+   int _own_buffer;
+   NFFT4GP_DOUBLE *_buffer;
+   int _own_dbuffer;
+   NFFT4GP_DOUBLE *_dbuffer;
+   func_kernel _fkernel_buffer;
+   int **_ibufferp;
+   size_t *_libufferp;
+   int _own_fkernel_buffer_params;
+   void *_fkernel_buffer_params;
+   size_t _ldwork;
+   NFFT4GP_DOUBLE *_dwork;
+   void *_external;
+} nfft4gp_kernel, *pnfft4gp_kernel;
+
+/* ---- generic kernel parameter struct --------------------------------------------------------- */
+/* replaces SRC/linearalg/kernels.c:404-436 */
+void *Nfft4GPKernelParamCreate(int max_n, int omp);
+/* replaces SRC/linearalg/kernels.c:438-470 */
+void Nfft4GPKernelParamFree(void *str);
+
+/* ---- NFFT single-component operator (INC/_external.h:60-200) ----------------------------------- */
+/* replaces SRC/external/nfft_interface.c:3-42 */
+void *Nfft4GPNFFTKernelParamCreate(int max_n, int dim);
+/* replaces SRC/external/nfft_interface.c:44-77 */
+void Nfft4GPNFFTKernelParamFree(void *kernel);
+/* replaces SRC/external/nfft_interface.c:79-82 (no-op, used as func_free) */
+void Nfft4GPNFFTKernelFree(void *str);
+/* replaces SRC/external/nfft_interface.c:84-101 */
+int Nfft4GPNFFTKernelParamFreeNFFTKernel(void *kernel);
+/* replaces SRC/external/nfft_interface.c:103-127 */
+int Nfft4GPNFFTKernelParamRemovePoints(void *kernel);
+/* replaces SRC/external/nfft_interface.c:129-263 (func_kernel; *Kp = *dKp = component handle) */
+int Nfft4GPNFFTKernelGaussianKernel(void *str, NFFT4GP_DOUBLE *data, int n, int ldim, int d, int *permr, int kr,
+                                    int *permc, int kc, NFFT4GP_DOUBLE **Kp, NFFT4GP_DOUBLE **dKp);
+/* replaces SRC/external/nfft_interface.c:265-398 */
+int Nfft4GPNFFTKernelMatern12Kernel(void *str, NFFT4GP_DOUBLE *data, int n, int ldim, int d, int *permr, int kr,
+                                    int *permc, int kc, NFFT4GP_DOUBLE **Kp, NFFT4GP_DOUBLE **dKp);
+/* replaces SRC/external/nfft_interface.c:400-497 (func_symmatvec on the component handle) */
+int Nfft4GPNFFTMatSymv(void *data, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE beta,
+                       NFFT4GP_DOUBLE *y);
+/* replaces SRC/external/nfft_interface.c:499-620 (y is 3n: dK/df, dK/dl, dK/dmu) */
+int Nfft4GPNFFTGradMatSymv(void *data, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE beta,
+                           NFFT4GP_DOUBLE *y);
+
+/* ---- NFFT additive operator (the north-star path) ---------------------------------------------- */
+/* replaces SRC/external/nfft_interface.c:622-674 */
+void *Nfft4GPNFFTAdditiveKernelParamCreate(NFFT4GP_DOUBLE *data, int n, int ldim, int d, int *windows, int nwindows,
+                                           int dwindows);
+/* replaces SRC/external/nfft_interface.c:676-734 (func_kernel; *Kp = *dKp = str) */
+int Nfft4GPNFFTAdditiveKernelGaussianKernel(void *str, NFFT4GP_DOUBLE *data, int n, int ldim, int d, int *permr,
+                                            int kr, int *permc, int kc, NFFT4GP_DOUBLE **Kp, NFFT4GP_DOUBLE **dKp);
+/* replaces SRC/external/nfft_interface.c:736-794 */
+int Nfft4GPNFFTAdditiveKernelMatern12Kernel(void *str, NFFT4GP_DOUBLE *data, int n, int ldim, int d, int *permr,
+                                            int kr, int *permc, int kc, NFFT4GP_DOUBLE **Kp, NFFT4GP_DOUBLE **dKp);
+/* replaces SRC/external/nfft_interface.c:796-817: y = beta*y + alpha*f^2*((1/nw) sum_c K_c + mu I) x */
+int Nfft4GPAdditiveNFFTMatSymv(void *data, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE beta,
+                               NFFT4GP_DOUBLE *y);
+/* replaces SRC/external/nfft_interface.c:819-840 */
+int Nfft4GPAdditiveNFFTGradMatSymv(void *data, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE beta,
+                                   NFFT4GP_DOUBLE *y);
+/* replaces SRC/external/nfft_interface.c:842-856 */
+void Nfft4GPAdditiveNFFTKernelFree(void *str);
+/* replaces SRC/external/nfft_interface.c:858-871 (host memory, caller frees with free()) */
+NFFT4GP_DOUBLE *Nfft4GPNFFTAppendData(NFFT4GP_DOUBLE *X1, int n1, int ldim1, int d, NFFT4GP_DOUBLE *X2, int n2,
+                                      int ldim2);
+
+/* ---- BLAS-1 vector ops (SRC/linearalg/vecops.c:3-155), host or device pointers ------------------ */
+NFFT4GP_DOUBLE Nfft4GPVecNorm2(NFFT4GP_DOUBLE *x, int n);                       /* vecops.c:3-7 */
+NFFT4GP_DOUBLE Nfft4GPVecDdot(NFFT4GP_DOUBLE *x, int n, NFFT4GP_DOUBLE *y);     /* vecops.c:9-13 */
+void Nfft4GPVecFill(NFFT4GP_DOUBLE *x, size_t n, NFFT4GP_DOUBLE val);           /* vecops.c:47-69 */
+void Nfft4GPVecScale(NFFT4GP_DOUBLE *x, size_t n, NFFT4GP_DOUBLE scale);        /* vecops.c:71-100 */
+void Nfft4GPVecAxpy(NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, size_t n, NFFT4GP_DOUBLE *y); /* vecops.c:102-155 */
+
+/* ---- PCG (SRC/solvers/pcg.c:3-206), device-resident ------------------------------------------- */
+int Nfft4GPSolverPcg(void *mat_data, int n, func_symmatvec matvec, void *prec_data, func_solve precondfunc,
+                     NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs, int maxits, int atol, NFFT4GP_DOUBLE tol,
+                     NFFT4GP_DOUBLE *prel_res, NFFT4GP_DOUBLE **prel_res_v, int *piter, int print_level);
+
+/* length of the rel_res_v array returned by the last Nfft4GPSolverPcg call on this process
+ * (1 for the early exits of pcg.c:32-41 / :70-84, maxits+1 otherwise) */
+int Nfft4GPAmdPcgHistoryLength(void);
+
+/* ---- Nystrom ("RAN") preconditioner apply (SRC/preconds/nys.c:115-173) ----------------------------
+ * The reference builds U (n x k), s, eta in Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660);
+ * Nfft4GPAmdNysCreate takes those factors (host or device arrays) and keeps them in HBM with U's rows
+ * already un-permuted, so the apply needs no gather. */
+void *Nfft4GPAmdNysCreate(int n, int k, const NFFT4GP_DOUBLE *U, const NFFT4GP_DOUBLE *s, NFFT4GP_DOUBLE eta,
+                          const int *perm);
+/* same signature as Nfft4GPPrecondNysSolve (nys.c:115): x = M^{-1} rhs, func_solve */
+int Nfft4GPAmdNysSolve(void *nys, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
+void Nfft4GPAmdNysFree(void *nys);
+
+/* ---- MI355X extensions --------------------------------------------------------------------------- */
+/* stream every kernel of this library is enqueued on (hipStream_t; NULL = null stream) */
+void Nfft4GPAmdSetStream(void *hip_stream);
+void *Nfft4GPAmdGetStream(void);
+/* 1 if a HIP device is visible */
+int Nfft4GPAmdDeviceAvailable(void);
+/* library version string */
+const char *Nfft4GPAmdVersion(void);
+
+/* layout statistics of an additive handle after its first setup:
+ * out[0]=n, [1]=nwindows, [2]=block size, [3]=#blocks, [4]=#tiles, [5]=slots (incl. padding),
+ * [6]=points per chunk R, [7]=comps per group, [8]=#groups, [9]=device bytes of the layout */
+int Nfft4GPAmdAdditiveLayoutInfo(void *str, long long *out, int nout);
+
+/* per-kernel timing with hipEvents on the library stream (0 disables; resets counters when enabled).
+ * After enabling, every additive matvec records events around its spread / grid / interp launches.
+ * Nfft4GPAmdTimingQuery writes total milliseconds and launch counts for the three kernels:
+ * ms[0..2] = spread, grid, interp;  cnt[0..2] likewise.  Returns 0. */
+int Nfft4GPAmdTimingEnable(void *str, int enable);
+int Nfft4GPAmdTimingQuery(void *str, double *ms, long long *cnt);
+
+/* split-phase additive matvec for row-sharded multi-GPU use (one process per GPU):
+ *   phase 1 (spread): per-component oversampled-grid partial sums of this rank's points into grid
+ *                     (device, nwindows*64 doubles, overwritten);
+ *   -- caller all-reduces grid across ranks (RCCL) --
+ *   phase 2 (finish): circulant + interpolation + epilogue for this rank's points.
+ * The handle must have been created with Nfft4GPAmdAdditiveShardCreate.  x, y are device pointers to
+ * this rank's rows.  grad = 0: y has n_local entries; grad = 1: y has 3*n_local (y0|y1|y2). */
+void *Nfft4GPAmdAdditiveShardCreate(NFFT4GP_DOUBLE *data, int n_global, int ldim, int d, int *windows,
+                                    int nwindows, int dwindows, int row_begin, int row_end);
+int Nfft4GPAmdShardSpread(void *str, const NFFT4GP_DOUBLE *x_local, NFFT4GP_DOUBLE *grid);
+int Nfft4GPAmdShardFinish(void *str, const NFFT4GP_DOUBLE *grid, int grad, NFFT4GP_DOUBLE alpha,
+                          const NFFT4GP_DOUBLE *x_local, NFFT4GP_DOUBLE beta, NFFT4GP_DOUBLE *y_local);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NFFT4GP_AMD_H */

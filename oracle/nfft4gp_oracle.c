@@ -1,0 +1,664 @@
+/*
+ * nfft4gp_oracle.c -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * CPU restatement of the reference's NFFT-accelerated additive-kernel operator
+ * (Hitenze/Preconditioned_Additive_Gaussian_Processes_with_Fourier_Acceleration,
+ * SRC/external/nfft_interface.c) together with the third-party algorithm it calls,
+ * NFFT3 `applications/fastsum` (fastsum_precompute / fastsum_trafo) + NFFT3 nfft_adjoint /
+ * nfft_trafo with the Kaiser-Bessel window and PRE_PSI precomputed taps.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this file's
+ * library.  The product path (preconditioned_..._amd/csrc) never links or calls it.
+ *
+ * Third-party dependency restated here (absent from /root/reference and from this image):
+ *   NFFT3 (github NFFT/nfft), version UNPINNED by the reference (README.md:12 says "install nfft
+ *   --enable-all --enable-openmp"; the API used -- fastsum_init_guru_kernel/_source_nodes/
+ *   _target_nodes, STORE_PERMUTATION_X_ALPHA, kernels xx_gaussian / der_laplacian_rbf -- implies
+ *   NFFT >= 3.5.x).  Restated from the published algorithm:
+ *     * Kaiser-Bessel window, b = pi*(2 - 1/sigma), sigma = n_os/N = 2:
+ *         PHI(t)  = sinh(b*sqrt(m^2-t^2))/(pi*sqrt(m^2-t^2))  if m^2 > t^2   (t = n_os*x)
+ *                 = sin (b*sqrt(t^2-m^2))/(pi*sqrt(t^2-m^2))  if m^2 < t^2
+ *                 = b/pi                                      otherwise (continuous limit)
+ *         PHI_HUT(k) = I0(m*sqrt(b^2 - (2*pi*k/n_os)^2))
+ *     * PRE_PSI taps: u = floor(n_os*x) - m, 2m+2 taps l = u..u+2m+1, psi = PHI(n_os*x - l).
+ *     * adjoint: g_l = sum_j alpha_j psi_jl ; fhat_k = (sum_l g_l e^{+2 pi i k l/n_os})/PHI_HUT(k)
+ *     * trafo  : h_l = sum_k (fhat_k/PHI_HUT(k)) e^{-2 pi i k l/n_os} ; f_j = sum_l h_l psi_jl
+ *     * fastsum (eps_I = eps_B = 0 so no near field, regkern = kernel clamped at r = 1/2):
+ *         bhat_k = N^{-d} sum_{l in I_N^d} K(min(|l/N|, 1/2)) e^{-2 pi i k.l/N}
+ *         f = trafo( bhat .* adjoint(alpha) )
+ *     * kernels: gaussian K(r)=exp(-r^2/c^2); xx_gaussian (r^2/c^2)exp(-r^2/c^2);
+ *       laplacian_rbf exp(-r/c); der_laplacian_rbf (r/c)exp(-r/c)  -- the derivative forms are
+ *       the ones under which nfft_interface.c:536 yields dK/dl; the tests pin this against the
+ *       reference's own dense gradient (kernels.c:490-678) compiled in oracle/_ref.
+ *
+ * Parity status: the NFFT arithmetic itself has NO golden vectors in the reference (TEST1 prints
+ * NFFT-vs-dense errors but asserts nothing and its notebook holds no outputs).  This
+ * restatement is pinned (a) against the reference's dense operator compiled from its own sources
+ * (oracle/_ref, kernels.c/matops.c) within the N=32 truncation error -- exactly TEST1's criterion
+ * (TESTS/TEST1/foo.cpp:250-293) -- and (b) against an exact NDFT of the same bhat within the KB
+ * window error (~1e-8).  The NFFT3 window details (the sin branch, the 2m+2 taps) are therefore
+ * "restated, not pinned" (Parity).
+ *
+ * Reference call sites followed line by line:
+ *   ParamCreate          nfft_interface.c:3-42, :622-674 (window gathering, skip_last :630-636)
+ *   Gaussian/Matern setup :129-263 / :265-398 (first-call centring + scaling :150-213, c = l*scale*sqrt2
+ *                          :219 (Matern :355), mu :221, ff :256)
+ *   MatSymv               :400-497 (alpha_c = a*x, y = beta*y + ff*(Re f + mu*Re alpha_c))
+ *   GradMatSymv           :499-620 (scale :536)
+ *   AdditiveMatSymv       :796-817 (1/nwindows, sequential components into _dwork)
+ *   AdditiveGradMatSymv   :819-840
+ */
+#include <complex.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_N 32    /* bandwidth, nfft_interface.c:18 */
+#define ORC_M 4     /* window cutoff, nfft_interface.c:20 */
+#define ORC_NOS 64  /* oversampled grid, nfft_interface.c:25-27 */
+#define ORC_T (2 * ORC_M + 2)
+
+typedef double complex cplx;
+
+static const double ORC_PI = 3.141592653589793238462643383279502884;
+
+/* ---------------------------------------------------------------------------------------------
+ * Window (NFFT3 Kaiser-Bessel, see header)
+ * -------------------------------------------------------------------------------------------*/
+static double orc_kb_b(void) { return ORC_PI * (2.0 - 1.0 / ((double)ORC_NOS / (double)ORC_N)); }
+
+/* PHI as a function of t = n_os * x (grid units) */
+static double orc_phi(double t)
+{
+   const double b = orc_kb_b();
+   const double a = (double)(ORC_M * ORC_M) - t * t;
+   if (a > 0.0)
+   {
+      const double s = sqrt(a);
+      return sinh(b * s) / (ORC_PI * s);
+   }
+   else if (a < 0.0)
+   {
+      const double s = sqrt(-a);
+      return sin(b * s) / (ORC_PI * s);
+   }
+   return b / ORC_PI;
+}
+
+/* modified Bessel I0 by its power series (converges for all arguments used here, z < 20) */
+static double orc_bessel_i0(double z)
+{
+   double sum = 1.0, term = 1.0, q = 0.25 * z * z;
+   for (int k = 1; k < 200; k++)
+   {
+      term *= q / ((double)k * (double)k);
+      sum += term;
+      if (term < 1e-18 * sum) break;
+   }
+   return sum;
+}
+
+static double orc_phi_hut(int k)
+{
+   const double b = orc_kb_b();
+   const double w = 2.0 * ORC_PI * (double)k / (double)ORC_NOS;
+   return orc_bessel_i0((double)ORC_M * sqrt(b * b - w * w));
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Kernels (NFFT3 applications/fastsum/kernels.c semantics, see header)
+ * -------------------------------------------------------------------------------------------*/
+static double orc_kern(int kind, double r, double c)
+{
+   r = fabs(r);
+   switch (kind)
+   {
+   case 0: return exp(-r * r / (c * c));                     /* gaussian */
+   case 1: return (r * r / (c * c)) * exp(-r * r / (c * c)); /* xx_gaussian */
+   case 2: return exp(-r / c);                               /* laplacian_rbf */
+   case 3: return (r / c) * exp(-r / c);                     /* der_laplacian_rbf */
+   }
+   return 0.0;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * One additive component (the reference's str_adj + two fastsum plans)
+ * -------------------------------------------------------------------------------------------*/
+typedef struct
+{
+   int d;          /* window dimension */
+   int n;
+   double *x;      /* n*d point-major, centred and scaled (str_adj::_x after :150-213) */
+   double scale;   /* str_adj::_scale, -1 until first setup */
+   int kernel;     /* 0 gaussian, 1 matern12 (str_adj::_kernel) */
+   double sigma0;  /* kernel param c (str_adj::_sigma[0]) */
+   double mu;
+   double kscale;  /* str_adj::_kernel_scale = f */
+   int ngrid;      /* n_os^d */
+   int nmodes;     /* N^d */
+   double *bhat;   /* N^d, real (imag parts vanish for even kernels) */
+   double *bhat_d; /* derivative kernel */
+   double *phihut_inv; /* [d][N] 1/PHI_HUT(k), k = -N/2..N/2-1 (same per dim) */
+   int *u;         /* [n][d] floor(n_os*x)-m */
+   double *psi;    /* [n][d][T] PRE_PSI taps */
+} orc_comp;
+
+typedef struct
+{
+   int n, nw, dw, skip_last;
+   double f, l, mu;        /* _params[0], _params[1], _noise_level */
+   double *buffer;         /* gathered window columns, n x (sum dims) col-major */
+   orc_comp *comps;
+   double *work;           /* 3n accumulator (_dwork) */
+} orc_additive;
+
+/* bhat for a kernel (fastsum_precompute, kernel part) */
+static void orc_bhat(int d, int kind, double c, double *bhat)
+{
+   const int N = ORC_N;
+   int nm = 1;
+   for (int t = 0; t < d; t++) nm *= N;
+   /* samples K(min(|l/N|,1/2)), l in I_N^d; index j = sum_t (l_t + N/2) N^t */
+   double *s = (double *)malloc(sizeof(double) * nm);
+   for (int j = 0; j < nm; j++)
+   {
+      int jj = j;
+      double r2 = 0.0;
+      for (int t = 0; t < d; t++)
+      {
+         const double lt = (double)(jj % N) / (double)N - 0.5;
+         r2 += lt * lt;
+         jj /= N;
+      }
+      double r = sqrt(r2);
+      if (r > 0.5) r = 0.5;
+      s[j] = orc_kern(kind, r, c) / (double)nm;
+   }
+   /* separable DFT (real even data -> real even result; compute in complex, keep real part) */
+   cplx *a = (cplx *)malloc(sizeof(cplx) * nm);
+   cplx *b = (cplx *)malloc(sizeof(cplx) * nm);
+   for (int j = 0; j < nm; j++) a[j] = s[j];
+   int stride = 1;
+   for (int t = 0; t < d; t++)
+   {
+      for (int j = 0; j < nm; j++)
+      {
+         const int lo = j % stride;
+         const int kt = (j / stride) % N;
+         const int hi = j / (stride * N);
+         cplx acc = 0.0;
+         for (int lt = 0; lt < N; lt++)
+         {
+            const double ph = -2.0 * ORC_PI * (double)((kt - N / 2) * (lt - N / 2)) / (double)N;
+            acc += a[lo + stride * (lt + N * hi)] * cexp(I * ph);
+         }
+         b[j] = acc;
+      }
+      memcpy(a, b, sizeof(cplx) * nm);
+      stride *= N;
+   }
+   for (int j = 0; j < nm; j++) bhat[j] = creal(a[j]);
+   free(a);
+   free(b);
+   free(s);
+}
+
+/* grid index helpers: grid multi-index (g_0..g_{d-1}), linear = sum g_t * n_os^t */
+static void orc_comp_fastsum(const orc_comp *cp, const double *bh, const cplx *alpha, cplx *fout)
+{
+   const int d = cp->d, n = cp->n, NOS = ORC_NOS, N = ORC_N, T = ORC_T;
+   const int ng = cp->ngrid, nm = cp->nmodes;
+   int ntap = 1;
+   for (int t = 0; t < d; t++) ntap *= T;
+
+   /* ---- adjoint B^T: spread onto the oversampled grid (per-thread private grids) ---- */
+   cplx *g = (cplx *)calloc((size_t)ng, sizeof(cplx));
+#pragma omp parallel
+   {
+      cplx *gl = (cplx *)calloc((size_t)ng, sizeof(cplx));
+#pragma omp for schedule(static)
+      for (int j = 0; j < n; j++)
+      {
+         for (int tt = 0; tt < ntap; tt++)
+         {
+            int rem = tt, gi = 0, gs = 1;
+            double w = 1.0;
+            for (int t = 0; t < d; t++)
+            {
+               const int lt = rem % T;
+               rem /= T;
+               int gidx = cp->u[(size_t)j * d + t] + lt;
+               gidx = ((gidx % NOS) + NOS) % NOS;
+               gi += gidx * gs;
+               gs *= NOS;
+               w *= cp->psi[((size_t)j * d + t) * T + lt];
+            }
+            gl[gi] += alpha[j] * w;
+         }
+      }
+#pragma omp critical
+      for (int i = 0; i < ng; i++) g[i] += gl[i];
+      free(gl);
+   }
+
+   /* ---- F^H + D: fhat_k = phihut_inv(k) * sum_l g_l e^{+2 pi i k l / n_os} (separable) ---- */
+   /* stage 1: reduce each grid dim NOS -> N, in place order over dims */
+   cplx *a = g;
+   int cur = ng; /* current array size */
+   int len_before = 1;
+   cplx *buf = NULL;
+   for (int t = 0; t < d; t++)
+   {
+      /* layout: [lower dims already N][dim t NOS][higher dims NOS] */
+      int hi = 1;
+      for (int s = t + 1; s < d; s++) hi *= NOS;
+      const int newsz = len_before * N * hi;
+      buf = (cplx *)malloc(sizeof(cplx) * newsz);
+      for (int h = 0; h < hi; h++)
+         for (int k = 0; k < N; k++)
+            for (int lo = 0; lo < len_before; lo++)
+            {
+               cplx acc = 0.0;
+               for (int l = 0; l < NOS; l++)
+               {
+                  const double ph = 2.0 * ORC_PI * (double)((k - N / 2) * l) / (double)NOS;
+                  acc += a[lo + len_before * (l + NOS * h)] * cexp(I * ph);
+               }
+               buf[lo + len_before * (k + N * h)] = acc * cp->phihut_inv[t * N + k];
+            }
+      if (a != g) free(a);
+      a = buf;
+      cur = newsz;
+      len_before *= N;
+   }
+   /* ---- multiply by bhat (fastsum_trafo step 2) and D of the trafo ---- */
+   for (int j = 0; j < nm; j++)
+   {
+      int jj = j;
+      double di = 1.0;
+      for (int t = 0; t < d; t++)
+      {
+         di *= cp->phihut_inv[t * N + (jj % N)];
+         jj /= N;
+      }
+      a[j] *= bh[j] * di;
+   }
+   (void)cur;
+   /* ---- F: h_l = sum_k a_k e^{-2 pi i k l/n_os}, expand each dim N -> NOS ---- */
+   int len_after = 1; /* dims > t still N; dims < t already NOS */
+   for (int t = 0; t < d; t++)
+   {
+      int lo_n = 1, hi_n = 1;
+      for (int s = 0; s < t; s++) lo_n *= NOS;
+      for (int s = t + 1; s < d; s++) hi_n *= N;
+      buf = (cplx *)malloc(sizeof(cplx) * lo_n * NOS * hi_n);
+      for (int h = 0; h < hi_n; h++)
+         for (int l = 0; l < NOS; l++)
+            for (int lo = 0; lo < lo_n; lo++)
+            {
+               cplx acc = 0.0;
+               for (int k = 0; k < N; k++)
+               {
+                  const double ph = -2.0 * ORC_PI * (double)((k - N / 2) * l) / (double)NOS;
+                  acc += a[lo + lo_n * (k + N * h)] * cexp(I * ph);
+               }
+               buf[lo + lo_n * (l + NOS * h)] = acc;
+            }
+      free(a);
+      a = buf;
+      (void)len_after;
+   }
+   free(g);
+
+   /* ---- B: interpolate ---- */
+#pragma omp parallel for schedule(static)
+   for (int j = 0; j < n; j++)
+   {
+      cplx acc = 0.0;
+      for (int tt = 0; tt < ntap; tt++)
+      {
+         int rem = tt, gi = 0, gs = 1;
+         double w = 1.0;
+         for (int t = 0; t < d; t++)
+         {
+            const int lt = rem % T;
+            rem /= T;
+            int gidx = cp->u[(size_t)j * d + t] + lt;
+            gidx = ((gidx % NOS) + NOS) % NOS;
+            gi += gidx * gs;
+            gs *= NOS;
+            w *= cp->psi[((size_t)j * d + t) * T + lt];
+         }
+         acc += a[gi] * w;
+      }
+      fout[j] = acc;
+   }
+   free(a);
+}
+
+/* exact NDFT with the same bhat: f_i = sum_k bhat_k e^{-2pi i k.y_i} sum_j alpha_j e^{2 pi i k.x_j} */
+static void orc_comp_ndft(const orc_comp *cp, const double *bh, const cplx *alpha, cplx *fout)
+{
+   const int d = cp->d, n = cp->n, N = ORC_N, nm = cp->nmodes;
+   cplx *fh = (cplx *)calloc((size_t)nm, sizeof(cplx));
+#pragma omp parallel for schedule(static)
+   for (int k = 0; k < nm; k++)
+   {
+      int kk[3] = {0, 0, 0}, rem = k;
+      for (int t = 0; t < d; t++)
+      {
+         kk[t] = rem % N - N / 2;
+         rem /= N;
+      }
+      cplx acc = 0.0;
+      for (int j = 0; j < n; j++)
+      {
+         double ph = 0.0;
+         for (int t = 0; t < d; t++) ph += (double)kk[t] * cp->x[(size_t)j * d + t];
+         acc += alpha[j] * cexp(I * 2.0 * ORC_PI * ph);
+      }
+      fh[k] = acc * bh[k];
+   }
+#pragma omp parallel for schedule(static)
+   for (int j = 0; j < n; j++)
+   {
+      cplx acc = 0.0;
+      for (int k = 0; k < nm; k++)
+      {
+         int rem = k;
+         double ph = 0.0;
+         for (int t = 0; t < d; t++)
+         {
+            ph += (double)(rem % N - N / 2) * cp->x[(size_t)j * d + t];
+            rem /= N;
+         }
+         acc += fh[k] * cexp(-I * 2.0 * ORC_PI * ph);
+      }
+      fout[j] = acc;
+   }
+   free(fh);
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Setup (nfft_interface.c:129-263 / :265-398)
+ * -------------------------------------------------------------------------------------------*/
+static void orc_comp_setup(orc_comp *cp, const double *data, int kernel, double f, double l, double mu)
+{
+   const int n = cp->n, d = cp->d;
+   cp->kernel = kernel;
+   if (cp->scale < 0.0)
+   {
+      /* first call: centre, scale to radius in [0.125, 0.25], transpose to point-major */
+      double *xc = (double *)malloc(sizeof(double) * (size_t)n * d);
+      memcpy(xc, data, sizeof(double) * (size_t)n * d);
+      for (int i = 0; i < d; i++)
+      {
+         double center = 0.0;
+         for (int j = 0; j < n; j++) center += xc[(size_t)i * n + j];
+         center /= (double)n;
+         for (int j = 0; j < n; j++) xc[(size_t)i * n + j] -= center;
+      }
+      double radius = 0.0;
+      for (int j = 0; j < n; j++)
+      {
+         double ri = 0.0;
+         for (int i = 0; i < d; i++) ri += xc[(size_t)i * n + j] * xc[(size_t)i * n + j];
+         ri = sqrt(ri);
+         if (ri > radius) radius = ri;
+      }
+      if (radius > 0.25 || radius < 0.125)
+      {
+         cp->scale = 0.25 / radius;
+         for (size_t j = 0; j < (size_t)n * d; j++) xc[j] *= cp->scale;
+      }
+      else
+      {
+         cp->scale = 1.0;
+      }
+      for (int i = 0; i < d; i++)
+         for (int j = 0; j < n; j++) cp->x[(size_t)j * d + i] = xc[(size_t)i * n + j];
+      free(xc);
+
+      /* PRE_PSI taps (depend only on the nodes) */
+#pragma omp parallel for schedule(static)
+      for (int j = 0; j < n; j++)
+         for (int t = 0; t < d; t++)
+         {
+            const double xj = cp->x[(size_t)j * d + t];
+            const int c = (int)floor(xj * (double)ORC_NOS);
+            const int u = c - ORC_M;
+            cp->u[(size_t)j * d + t] = u;
+            for (int lt = 0; lt < ORC_T; lt++)
+            {
+               const double tx = xj - (double)(u + lt) / (double)ORC_NOS;
+               cp->psi[((size_t)j * d + t) * ORC_T + lt] = orc_phi(tx * (double)ORC_NOS);
+            }
+         }
+   }
+   if (kernel == 0)
+      cp->sigma0 = l * cp->scale * sqrt(2.0);
+   else
+      cp->sigma0 = l * cp->scale;
+   cp->mu = mu;
+   cp->kscale = f;
+   orc_bhat(d, kernel == 0 ? 0 : 2, cp->sigma0, cp->bhat);
+   orc_bhat(d, kernel == 0 ? 1 : 3, cp->sigma0, cp->bhat_d);
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Public (ctypes) API
+ * -------------------------------------------------------------------------------------------*/
+void *orc_additive_create(const double *data, int n, int ldim, int d, const int *windows, int nwindows, int dwindows)
+{
+   (void)d;
+   orc_additive *h = (orc_additive *)calloc(1, sizeof(orc_additive));
+   h->n = n;
+   h->nw = nwindows;
+   h->dw = dwindows;
+   /* skip_last: trailing -1 count in the last window (nfft_interface.c:630-636) */
+   int skip_window = 1;
+   h->skip_last = 0;
+   while (skip_window < dwindows && windows[nwindows * dwindows - skip_window] < 0)
+   {
+      skip_window++;
+      h->skip_last++;
+   }
+   h->buffer = (double *)malloc(sizeof(double) * (size_t)n * nwindows * dwindows);
+   h->comps = (orc_comp *)calloc((size_t)nwindows, sizeof(orc_comp));
+   h->work = (double *)malloc(sizeof(double) * 3 * (size_t)n);
+   /* gather (nfft_interface.c:648-670) */
+   double *dst = h->buffer;
+   const int *fw = windows;
+   for (int i = 0; i < nwindows; i++)
+   {
+      int actual = 0;
+      for (int j = 0; j < dwindows; j++)
+      {
+         if (fw[0] >= 0)
+         {
+            memcpy(dst, data + (size_t)fw[0] * ldim, sizeof(double) * n);
+            fw++;
+            dst += n;
+            actual++;
+         }
+      }
+      orc_comp *cp = &h->comps[i];
+      cp->d = actual;
+      cp->n = n;
+      cp->scale = -1.0;
+      cp->x = (double *)malloc(sizeof(double) * (size_t)n * actual);
+      cp->ngrid = 1;
+      cp->nmodes = 1;
+      for (int t = 0; t < actual; t++)
+      {
+         cp->ngrid *= ORC_NOS;
+         cp->nmodes *= ORC_N;
+      }
+      cp->bhat = (double *)malloc(sizeof(double) * cp->nmodes);
+      cp->bhat_d = (double *)malloc(sizeof(double) * cp->nmodes);
+      cp->phihut_inv = (double *)malloc(sizeof(double) * ORC_N * (actual > 0 ? actual : 1));
+      for (int t = 0; t < actual; t++)
+         for (int k = 0; k < ORC_N; k++) cp->phihut_inv[t * ORC_N + k] = 1.0 / orc_phi_hut(k - ORC_N / 2);
+      cp->u = (int *)malloc(sizeof(int) * (size_t)n * actual);
+      cp->psi = (double *)malloc(sizeof(double) * (size_t)n * actual * ORC_T);
+   }
+   return h;
+}
+
+/* func_kernel analogue: nfft_interface.c:676-734 (kernel=0) / :736-794 (kernel=1).
+ * As in the reference, windows are consumed at a stride of n*dwindows from _buffer. */
+int orc_additive_setup(void *vh, int kernel, double f, double l, double mu)
+{
+   orc_additive *h = (orc_additive *)vh;
+   h->f = f;
+   h->l = l;
+   h->mu = mu;
+   const double *dw = h->buffer;
+   for (int i = 0; i < h->nw; i++)
+   {
+      orc_comp_setup(&h->comps[i], dw, kernel, f, l, mu);
+      dw += (size_t)h->n * h->dw;
+   }
+   return 0;
+}
+
+static void orc_comp_apply(orc_comp *cp, int exact, int which, const cplx *alpha, cplx *fout)
+{
+   const double *bh = which ? cp->bhat_d : cp->bhat;
+   if (exact)
+      orc_comp_ndft(cp, bh, alpha, fout);
+   else
+      orc_comp_fastsum(cp, bh, alpha, fout);
+}
+
+/* Nfft4GPNFFTMatSymv (:400-497) for one component, accumulating with beta = 1 */
+static void orc_comp_matsymv_acc(orc_comp *cp, int exact, double a, const double *x, double *y)
+{
+   const int n = cp->n;
+   const double ff = cp->kscale * cp->kscale;
+   cplx *al = (cplx *)malloc(sizeof(cplx) * n);
+   cplx *fo = (cplx *)malloc(sizeof(cplx) * n);
+   for (int i = 0; i < n; i++) al[i] = a * x[i];
+   orc_comp_apply(cp, exact, 0, al, fo);
+   for (int i = 0; i < n; i++) y[i] += ff * (creal(fo[i]) + cp->mu * creal(al[i]));
+   free(al);
+   free(fo);
+}
+
+/* Nfft4GPNFFTGradMatSymv (:499-620), beta = 1 branch */
+static void orc_comp_gradmatsymv_acc(orc_comp *cp, int exact, double a, const double *x, double *y)
+{
+   const int n = cp->n;
+   const double ff = cp->kscale * cp->kscale;
+   const double f2 = cp->kscale * 2.0;
+   cplx *al = (cplx *)malloc(sizeof(cplx) * n);
+   cplx *fo = (cplx *)malloc(sizeof(cplx) * n);
+   cplx *fd = (cplx *)malloc(sizeof(cplx) * n);
+   for (int i = 0; i < n; i++) al[i] = a * x[i];
+   orc_comp_apply(cp, exact, 0, al, fo);
+   orc_comp_apply(cp, exact, 1, al, fd);
+   double scale = cp->kernel == 0 ? 2.0 * cp->scale * sqrt(2.0) / cp->sigma0 : cp->scale / cp->sigma0;
+   scale *= ff;
+   for (int i = 0; i < n; i++)
+   {
+      y[i] += f2 * (creal(fo[i]) + cp->mu * creal(al[i]));
+      y[n + i] += scale * creal(fd[i]);
+      y[2 * n + i] += ff * creal(al[i]);
+   }
+   free(al);
+   free(fo);
+   free(fd);
+}
+
+static void orc_scale_vec(double *y, size_t n, double beta)
+{
+   /* Nfft4GPVecScale (vecops.c:71-100): beta == 0 fills with zeros */
+   if (beta == 0.0)
+      for (size_t i = 0; i < n; i++) y[i] = 0.0;
+   else
+      for (size_t i = 0; i < n; i++) y[i] *= beta;
+}
+
+/* Nfft4GPAdditiveNFFTMatSymv (:796-817); exact=1 swaps fastsum for the exact NDFT */
+int orc_additive_matsymv(void *vh, int n, double alpha, const double *x, double beta, double *y, int exact)
+{
+   orc_additive *h = (orc_additive *)vh;
+   memset(h->work, 0, sizeof(double) * n);
+   const double scale = 1.0 / (double)h->nw * alpha;
+   for (int i = 0; i < h->nw; i++) orc_comp_matsymv_acc(&h->comps[i], exact, scale, x, h->work);
+   orc_scale_vec(y, n, beta);
+   for (int i = 0; i < n; i++) y[i] += h->work[i];
+   return 0;
+}
+
+/* Nfft4GPAdditiveNFFTGradMatSymv (:819-840) */
+int orc_additive_gradmatsymv(void *vh, int n, double alpha, const double *x, double beta, double *y, int exact)
+{
+   orc_additive *h = (orc_additive *)vh;
+   memset(h->work, 0, sizeof(double) * 3 * n);
+   const double scale = 1.0 / (double)h->nw * alpha;
+   for (int i = 0; i < h->nw; i++) orc_comp_gradmatsymv_acc(&h->comps[i], exact, scale, x, h->work);
+   orc_scale_vec(y, 3 * (size_t)n, beta);
+   for (int i = 0; i < 3 * n; i++) y[i] += h->work[i];
+   return 0;
+}
+
+/* introspection for tests: per-component scale, kernel parameter, dims, bhat */
+int orc_additive_comp_info(void *vh, int c, int *d, double *scale, double *sigma0, double *bhat_out, double *bhat_d_out)
+{
+   orc_additive *h = (orc_additive *)vh;
+   if (c < 0 || c >= h->nw) return -1;
+   orc_comp *cp = &h->comps[c];
+   *d = cp->d;
+   *scale = cp->scale;
+   *sigma0 = cp->sigma0;
+   if (bhat_out) memcpy(bhat_out, cp->bhat, sizeof(double) * cp->nmodes);
+   if (bhat_d_out) memcpy(bhat_d_out, cp->bhat_d, sizeof(double) * cp->nmodes);
+   return 0;
+}
+
+/* scaled, point-major coordinates of component c (after the first setup) */
+int orc_additive_comp_points(void *vh, int c, double *xout)
+{
+   orc_additive *h = (orc_additive *)vh;
+   if (c < 0 || c >= h->nw) return -1;
+   orc_comp *cp = &h->comps[c];
+   memcpy(xout, cp->x, sizeof(double) * (size_t)cp->n * cp->d);
+   return 0;
+}
+
+double orc_window_phi(double t) { return orc_phi(t); }
+double orc_window_phi_hut(int k) { return orc_phi_hut(k); }
+
+void orc_additive_free(void *vh)
+{
+   orc_additive *h = (orc_additive *)vh;
+   if (!h) return;
+   for (int i = 0; i < h->nw; i++)
+   {
+      orc_comp *cp = &h->comps[i];
+      free(cp->x);
+      free(cp->bhat);
+      free(cp->bhat_d);
+      free(cp->phihut_inv);
+      free(cp->u);
+      free(cp->psi);
+   }
+   free(h->comps);
+   free(h->buffer);
+   free(h->work);
+   free(h);
+}
+
+int orc_num_threads(void)
+{
+#ifdef _OPENMP
+   return omp_get_max_threads();
+#else
+   return 1;
+#endif
+}

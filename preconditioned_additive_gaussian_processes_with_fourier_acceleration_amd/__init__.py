@@ -1,0 +1,11 @@
+"""MI355X-native NFFT-accelerated additive Gaussian-process kernel operator.
+
+Drop-in for the hot path of Hitenze/Preconditioned_Additive_Gaussian_Processes_with_Fourier_Acceleration
+(SRC/external/nfft_interface.c + SRC/solvers/pcg.c + SRC/preconds/nys.c apply): hand-written HIP
+kernels for gfx950 behind the C ABI of include/nfft4gp_amd.h (libnfft4gp_amd.so, built in-tree).
+"""
+from ._lib import ExtensionMissing, header_symbols, lib  # noqa: F401
+from .nfft import GAUSSIAN, MATERN12, NFFTAdditiveKernel, NFFTKernel  # noqa: F401
+from .solvers import NystromPrecond, pcg  # noqa: F401
+
+__version__ = "0.1.0"

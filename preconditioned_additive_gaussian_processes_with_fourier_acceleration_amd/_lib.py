@@ -1,0 +1,128 @@
+"""ctypes binding of ``libnfft4gp_amd.so`` (the C ABI declared in ``include/nfft4gp_amd.h``).
+
+The library is built in-tree by ``csrc/Makefile`` (``__graft_entry__.build()``).  Importing this
+module never falls back to anything: if the shared object is missing, ``lib()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libnfft4gp_amd.so")
+HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "nfft4gp_amd.h")
+
+dp = C.POINTER(C.c_double)
+ip = C.POINTER(C.c_int)
+vp = C.c_void_p
+
+SYMMATVEC = C.CFUNCTYPE(C.c_int, vp, C.c_int, C.c_double, vp, C.c_double, vp)
+SOLVE = C.CFUNCTYPE(C.c_int, vp, C.c_int, vp, vp)
+
+
+class NfftKernelStruct(C.Structure):
+    """nfft4gp_kernel, field layout of SRC/linearalg/kernels.h:65-95."""
+    _fields_ = [
+        ("_params", C.c_double * 5),
+        ("_iparams", C.c_int * 5),
+        ("_max_n", C.c_int),
+        ("_omp", C.c_int),
+        ("_noise_level", C.c_double),
+        ("_own_buffer", C.c_int),
+        ("_buffer", dp),
+        ("_own_dbuffer", C.c_int),
+        ("_dbuffer", dp),
+        ("_fkernel_buffer", vp),
+        ("_ibufferp", vp),
+        ("_libufferp", vp),
+        ("_own_fkernel_buffer_params", C.c_int),
+        ("_fkernel_buffer_params", vp),
+        ("_ldwork", C.c_size_t),
+        ("_dwork", dp),
+        ("_external", vp),
+    ]
+
+
+_SIGS = {
+    # name: (restype, argtypes)
+    "Nfft4GPKernelParamCreate": (vp, [C.c_int, C.c_int]),
+    "Nfft4GPKernelParamFree": (None, [vp]),
+    "Nfft4GPNFFTKernelParamCreate": (vp, [C.c_int, C.c_int]),
+    "Nfft4GPNFFTKernelParamFree": (None, [vp]),
+    "Nfft4GPNFFTKernelFree": (None, [vp]),
+    "Nfft4GPNFFTKernelParamFreeNFFTKernel": (C.c_int, [vp]),
+    "Nfft4GPNFFTKernelParamRemovePoints": (C.c_int, [vp]),
+    "Nfft4GPNFFTKernelGaussianKernel": (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, ip, C.c_int, ip, C.c_int,
+                                                  C.POINTER(vp), C.POINTER(vp)]),
+    "Nfft4GPNFFTKernelMatern12Kernel": (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, ip, C.c_int, ip, C.c_int,
+                                                  C.POINTER(vp), C.POINTER(vp)]),
+    "Nfft4GPNFFTMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),
+    "Nfft4GPNFFTGradMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),
+    "Nfft4GPNFFTAdditiveKernelParamCreate": (vp, [vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int]),
+    "Nfft4GPNFFTAdditiveKernelGaussianKernel": (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, ip, C.c_int, ip,
+                                                          C.c_int, C.POINTER(vp), C.POINTER(vp)]),
+    "Nfft4GPNFFTAdditiveKernelMatern12Kernel": (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, ip, C.c_int, ip,
+                                                          C.c_int, C.POINTER(vp), C.POINTER(vp)]),
+    "Nfft4GPAdditiveNFFTMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),
+    "Nfft4GPAdditiveNFFTGradMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),
+    "Nfft4GPAdditiveNFFTKernelFree": (None, [vp]),
+    "Nfft4GPNFFTAppendData": (vp, [vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int]),
+    "Nfft4GPVecNorm2": (C.c_double, [vp, C.c_int]),
+    "Nfft4GPVecDdot": (C.c_double, [vp, C.c_int, vp]),
+    "Nfft4GPVecFill": (None, [vp, C.c_size_t, C.c_double]),
+    "Nfft4GPVecScale": (None, [vp, C.c_size_t, C.c_double]),
+    "Nfft4GPVecAxpy": (None, [C.c_double, vp, C.c_size_t, vp]),
+    "Nfft4GPSolverPcg": (C.c_int, [vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_double, dp,
+                                   C.POINTER(dp), ip, C.c_int]),
+    "Nfft4GPAmdPcgHistoryLength": (C.c_int, []),
+    "Nfft4GPAmdNysCreate": (vp, [C.c_int, C.c_int, vp, vp, C.c_double, vp]),
+    "Nfft4GPAmdNysSolve": (C.c_int, [vp, C.c_int, vp, vp]),
+    "Nfft4GPAmdNysFree": (None, [vp]),
+    "Nfft4GPAmdSetStream": (None, [vp]),
+    "Nfft4GPAmdGetStream": (vp, []),
+    "Nfft4GPAmdDeviceAvailable": (C.c_int, []),
+    "Nfft4GPAmdVersion": (C.c_char_p, []),
+    "Nfft4GPAmdAdditiveLayoutInfo": (C.c_int, [vp, C.POINTER(C.c_longlong), C.c_int]),
+    "Nfft4GPAmdTimingEnable": (C.c_int, [vp, C.c_int]),
+    "Nfft4GPAmdTimingQuery": (C.c_int, [vp, dp, C.POINTER(C.c_longlong)]),
+    "Nfft4GPAmdAdditiveShardCreate": (vp, [vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "Nfft4GPAmdShardSpread": (C.c_int, [vp, vp, vp]),
+    "Nfft4GPAmdShardFinish": (C.c_int, [vp, vp, C.c_int, C.c_double, vp, C.c_double, vp]),
+}
+
+_lib = None
+
+
+class ExtensionMissing(RuntimeError):
+    pass
+
+
+def header_symbols(path: str = HEADER) -> list[str]:
+    """Every function name declared in include/nfft4gp_amd.h."""
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = re.findall(r"\b(Nfft4GP\w+)\s*\(", txt)
+    return sorted(set(names))
+
+
+def lib():
+    """Load the HIP C-ABI library (raises ExtensionMissing if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ExtensionMissing(
+                f"{LIB_PATH} not found: build it with `make -C {os.path.join(PKG_DIR, 'csrc')}` "
+                "(or __graft_entry__.build()). There is no CPU fallback.")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def fnptr(name: str) -> int:
+    """Address of an exported C function (to pass as func_symmatvec / func_solve)."""
+    return C.cast(getattr(lib(), name), vp).value

@@ -1,0 +1,130 @@
+// internal.h -- private types of the MI355X NFFT additive-kernel operator.
+//
+// Algorithm (1-D additive components, the BASELINE configurations B-E):
+//   The reference (nfft_interface.c:400-497 -> NFFT3 fastsum_trafo) computes per component
+//     f = B diag(1/phihut) F^T [bhat] F diag(1/phihut) B^T alpha
+//   with B the 2m+2 = 10-tap Kaiser-Bessel spreading matrix onto a 64-cell periodic grid and F the
+//   32-mode DFT.  For one component the middle factor is a real 64x64 circulant W (only Re f is used,
+//   nfft_interface.c:436) and each tap is an entire function of the point's offset u in its cell.
+//   We write the 10 taps as degree-11 polynomials in u (max error 3e-13 of the window peak), so
+//     spread : M[cell][d] = sum_{j in cell} alpha_j u_j^d        (per-cell moments)
+//              g[(cell-4+t) mod 64] += sum_d C[t][d] M[cell][d]
+//     grid   : h = W g,   H[cell][d] = sum_t h[(cell-4+t) mod 64] C[t][d]
+//     interp : f_j = sum_d H[cell_j][d] u_j^d                     (Horner)
+//   Points are bucketed by cell at setup (the nodes are fixed after the first setup call,
+//   nfft_interface.c:150) so a lane owns a run of R points of one cell: moments accumulate in
+//   registers and the interpolation coefficients are loaded once per run.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/nfft4gp_amd.h"
+
+namespace nfft4gp_amd {
+
+constexpr int kNos = 64;            // oversampled grid n_os (nfft_interface.c:25-27)
+constexpr int kBand = 32;           // bandwidth N (nfft_interface.c:18)
+constexpr int kM = 4;               // window cutoff m (nfft_interface.c:20)
+constexpr int kTaps = 2 * kM + 2;   // PRE_PSI taps per dim
+constexpr int kDeg = 11;            // tap polynomial degree
+constexpr int kNC = kDeg + 1;       // coefficients per cell
+constexpr int kR = 16;              // points per lane-run (chunk)
+constexpr int kWave = 64;
+
+#define NFFT4GP_HIP_CHECK(expr)                                                                    \
+   do {                                                                                            \
+      hipError_t _e = (expr);                                                                      \
+      if (_e != hipSuccess) {                                                                      \
+         fprintf(stderr, "nfft4gp_amd: HIP error %s at %s:%d (%s)\n", hipGetErrorString(_e),      \
+                 __FILE__, __LINE__, #expr);                                                       \
+         return -1;                                                                                \
+      }                                                                                            \
+   } while (0)
+
+// ---- host math (window.cpp) --------------------------------------------------------------------
+double kb_phi(double t);         // NFFT3 Kaiser-Bessel PHI in grid units
+double kb_phi_hut(int k);        // NFFT3 PHI_HUT
+// tap polynomial coefficients C[t*kNC + d] (monomials in u = frac - 1/2)
+const std::vector<double>& tap_poly_coeffs();
+// fastsum kernel Fourier coefficients for a 1-D component, k = -N/2..N/2-1 (index k+N/2)
+// kind: 0 gaussian, 1 xx_gaussian, 2 laplacian_rbf, 3 der_laplacian_rbf
+void bhat_1d(int kind, double c, double* bhat);
+// real circulant first column: w[s] = weight * sum_k bhat_k / phihut_k^2 cos(2 pi k s / n_os)
+void circulant_1d(const double* bhat, double weight, double* w);
+
+// ---- layout (layout.cpp) -----------------------------------------------------------------------
+struct Layout {
+   int n = 0;           // local points
+   int nw = 0;          // components
+   int B = 4096;        // block size (points)
+   int CG = 8;          // components per spread group
+   int ngroups = 0;
+   int nblocks = 0;
+   long long ntiles = 0;
+   std::vector<uint16_t> meta;     // [ntiles*64]      comp<<6 | cell
+   std::vector<uint32_t> perm2;    // [ntiles*R/2*64]  two 16-bit local indices
+   std::vector<uint32_t> q;        // [ntiles*R*64]    32-bit fixed-point coordinate (x mod 1)
+   std::vector<int> tile_off;      // [nblocks*ngroups+1]
+};
+// build from per-component quantized coordinates qc[c*n + j]
+void build_layout(const std::vector<uint32_t>& qc, int n, int nw, int B, int CG, Layout& L);
+
+// ---- device plan --------------------------------------------------------------------------------
+struct DevLayout {
+   uint16_t* meta = nullptr;
+   uint32_t* perm2 = nullptr;
+   uint32_t* q = nullptr;
+   int* tile_off = nullptr;
+   long long ntiles = 0;
+   size_t bytes = 0;
+};
+
+struct AdditivePlan {
+   // geometry
+   int n_global = 0, row_begin = 0, row_end = 0, n = 0;  // n = local rows
+   int nw = 0, dw = 0, skip_last = 0;
+   std::vector<int> comp_dims;
+   // per-component cached first-setup state (nfft_interface.c:150-213)
+   bool points_ready = false;
+   std::vector<double> comp_scale;
+   std::vector<double> comp_sigma;
+   int kernel = 0;  // 0 gaussian, 1 matern12
+   double f = 1.0, l = 1.0, mu = 0.0;
+   double weight = 1.0;  // 1/nwindows
+   // layout
+   int B = 4096, CG = 8, ngroups = 0, nblocks = 0;
+   DevLayout dl;
+   // device buffers
+   double* d_part = nullptr;  // [nblocks][nw][64]
+   double* d_grid = nullptr;  // [nw][64]
+   double* d_w = nullptr;     // [nw][64] circulant, kernel
+   double* d_wd = nullptr;    // [nw][64] circulant, derivative kernel
+   double* d_H = nullptr;     // [nw][64][kNC]
+   double* d_Hd = nullptr;
+   double* d_C = nullptr;     // [kTaps][kNC]
+   double* d_xs = nullptr;    // staging (host pointer calls)
+   double* d_ys = nullptr;    // staging 3n
+   // timing
+   bool timing = false;
+   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+   double ms[3] = {0, 0, 0};
+   long long cnt[3] = {0, 0, 0};
+};
+
+// launchers (nfft_kernels.hip); all enqueue on `stream`
+int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream);
+int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream);
+int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream);
+int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream);
+int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, double beta, double* d_y,
+                  hipStream_t stream);
+
+hipStream_t current_stream();
+bool is_device_ptr(const void* p);
+int device_ok();
+
+}  // namespace nfft4gp_amd

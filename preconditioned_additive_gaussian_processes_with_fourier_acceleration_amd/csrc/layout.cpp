@@ -1,0 +1,147 @@
+// layout.cpp -- cell-bucketed chunk layout of the fixed NFFT nodes (host, built once per handle).
+//
+// The reference fixes the nodes at the first setup call and only refreshes the kernel
+// coefficients afterwards (nfft_interface.c:150 `_scale < 0` test, :216-254).  We exploit that by
+// bucketing, once, every block of B consecutive points by oversampled-grid cell, per component:
+//
+//   block b = points [b*B, (b+1)*B)           (B <= 65535 so a local index fits 16 bits)
+//   group g = components [g*CG, (g+1)*CG)
+//   chunk   = up to R points of ONE (component, cell), padded with dummies (local index B, which
+//             the kernels map to a zero alpha / a discarded output slot)
+//   tile    = 64 chunks, one per lane; stored lane-fastest so every load is coalesced:
+//               meta [tile][lane]            u16  comp << 6 | cell
+//               perm2[tile][r/2][lane]       u32  local index of points r and r+1 (16 bits each)
+//               q    [tile][r][lane]         u32  fixed-point x mod 1 (cell = q >> 26)
+//   tile_off[b*ngroups + g] = first tile of (b, g); the spread kernel gets one workgroup per (b, g),
+//   the interpolation kernel one workgroup per b (all groups).
+#include <algorithm>
+#include <thread>
+
+#include "internal.h"
+
+namespace nfft4gp_amd {
+
+namespace {
+
+struct ChunkSink {
+   // count-only pass when arrays are null
+   uint16_t* meta;
+   uint32_t* perm2;
+   uint32_t* q;
+};
+
+// enumerate the chunks of (block b, group g); returns the number of chunks; if `out` has arrays,
+// writes tiles starting at tile index t0
+long long emit_block_group(const std::vector<uint32_t>& qc, int n, int nw, int B, int CG, int b, int g,
+                           const ChunkSink* out, long long t0, std::vector<int>& cnt, std::vector<int>& off,
+                           std::vector<uint16_t>& sorted)
+{
+   const int base = b * B;
+   const int nloc = std::min(B, n - base);
+   const int c0 = g * CG, c1 = std::min(nw, c0 + CG);
+   long long nchunks = 0;
+   for (int c = c0; c < c1; c++) {
+      const uint32_t* qq = qc.data() + (size_t)c * n + base;
+      std::fill(cnt.begin(), cnt.end(), 0);
+      for (int j = 0; j < nloc; j++) cnt[qq[j] >> 26]++;
+      off[0] = 0;
+      for (int cell = 0; cell < kNos; cell++) off[cell + 1] = off[cell] + cnt[cell];
+      if (out) {
+         std::vector<int> pos(off.begin(), off.end() - 1);
+         for (int j = 0; j < nloc; j++) sorted[pos[qq[j] >> 26]++] = (uint16_t)j;  // stable
+      }
+      for (int cell = 0; cell < kNos; cell++) {
+         for (int s = off[cell]; s < off[cell + 1]; s += kR) {
+            if (out) {
+               const long long chunk = nchunks;
+               const long long tile = t0 + chunk / kWave;
+               const int lane = (int)(chunk % kWave);
+               out->meta[tile * kWave + lane] = (uint16_t)((c << 6) | cell);
+               uint16_t loc[kR];
+               uint32_t qv[kR];
+               for (int r = 0; r < kR; r++) {
+                  const int sidx = s + r;
+                  if (sidx < off[cell + 1]) {
+                     loc[r] = sorted[sidx];
+                     qv[r] = qq[loc[r]];
+                  } else {
+                     loc[r] = (uint16_t)B;  // dummy: zero alpha / discarded output
+                     qv[r] = (uint32_t)cell << 26;
+                  }
+               }
+               for (int r2 = 0; r2 < kR / 2; r2++)
+                  out->perm2[(tile * (kR / 2) + r2) * kWave + lane] =
+                      (uint32_t)loc[2 * r2] | ((uint32_t)loc[2 * r2 + 1] << 16);
+               for (int r = 0; r < kR; r++) out->q[(tile * kR + r) * kWave + lane] = qv[r];
+            }
+            nchunks++;
+         }
+      }
+   }
+   const long long ntiles = (nchunks + kWave - 1) / kWave;
+   if (out) {
+      // pad the last tile with dummy chunks of the group's first component, cell 0
+      for (long long chunk = nchunks; chunk < ntiles * kWave; chunk++) {
+         const long long tile = t0 + chunk / kWave;
+         const int lane = (int)(chunk % kWave);
+         out->meta[tile * kWave + lane] = (uint16_t)(c0 << 6);
+         for (int r2 = 0; r2 < kR / 2; r2++)
+            out->perm2[(tile * (kR / 2) + r2) * kWave + lane] = (uint32_t)B | ((uint32_t)B << 16);
+         for (int r = 0; r < kR; r++) out->q[(tile * kR + r) * kWave + lane] = 0u;
+      }
+   }
+   return ntiles;
+}
+
+template <class F>
+void parallel_for(int nitems, F&& f)
+{
+   unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+   if (nitems < 4) nt = 1;
+   std::vector<std::thread> th;
+   for (unsigned t = 0; t < nt; t++)
+      th.emplace_back([&, t] {
+         for (int i = (int)t; i < nitems; i += (int)nt) f(i);
+      });
+   for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+void build_layout(const std::vector<uint32_t>& qc, int n, int nw, int B, int CG, Layout& L)
+{
+   L.n = n;
+   L.nw = nw;
+   L.B = B;
+   L.CG = CG;
+   L.ngroups = (nw + CG - 1) / CG;
+   L.nblocks = (n + B - 1) / B;
+   const int nbg = L.nblocks * L.ngroups;
+   std::vector<long long> tiles(nbg, 0);
+   parallel_for(L.nblocks, [&](int b) {
+      std::vector<int> cnt(kNos), off(kNos + 1);
+      std::vector<uint16_t> sorted(B);
+      for (int g = 0; g < L.ngroups; g++)
+         tiles[b * L.ngroups + g] = emit_block_group(qc, n, nw, B, CG, b, g, nullptr, 0, cnt, off, sorted);
+   });
+   L.tile_off.assign(nbg + 1, 0);
+   long long acc = 0;
+   for (int i = 0; i < nbg; i++) {
+      L.tile_off[i] = (int)acc;
+      acc += tiles[i];
+   }
+   L.tile_off[nbg] = (int)acc;
+   L.ntiles = acc;
+   L.meta.assign((size_t)acc * kWave, 0);
+   L.perm2.assign((size_t)acc * (kR / 2) * kWave, 0);
+   L.q.assign((size_t)acc * kR * kWave, 0);
+   ChunkSink sink{L.meta.data(), L.perm2.data(), L.q.data()};
+   parallel_for(L.nblocks, [&](int b) {
+      std::vector<int> cnt(kNos), off(kNos + 1);
+      std::vector<uint16_t> sorted(B);
+      for (int g = 0; g < L.ngroups; g++)
+         emit_block_group(qc, n, nw, B, CG, b, g, &sink, L.tile_off[b * L.ngroups + g], cnt, off, sorted);
+   });
+}
+
+}  // namespace nfft4gp_amd

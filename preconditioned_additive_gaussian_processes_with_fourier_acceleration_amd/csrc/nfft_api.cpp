@@ -1,0 +1,641 @@
+// nfft_api.cpp -- C ABI of the NFFT additive-kernel operator (drop-in for nfft_interface.c).
+//
+// Handle model (mirrors nfft_interface.c:3-42, :622-674): a nfft4gp_kernel struct with the
+// reference's exact field layout; _iparams[0..2] = nwindows, dwindows, skip_last; _buffer = the
+// gathered window columns (host); _dwork = 3n host doubles as in the reference; _external = our
+// device plan.  Hyperparameters are read from _params / _noise_level at setup time and cached,
+// as the reference caches them in str_adj (nfft_interface.c:219-256).
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "internal.h"
+
+using namespace nfft4gp_amd;
+
+namespace nfft4gp_amd {
+
+static hipStream_t g_stream = nullptr;
+
+hipStream_t current_stream() { return g_stream; }
+
+int device_ok()
+{
+   static int ok = -1;
+   if (ok < 0) {
+      int cnt = 0;
+      if (hipGetDeviceCount(&cnt) != hipSuccess) cnt = 0;
+      (void)hipGetLastError();
+      ok = cnt > 0 ? 1 : 0;
+   }
+   return ok;
+}
+
+bool is_device_ptr(const void* p)
+{
+   if (!p) return false;
+   hipPointerAttribute_t attr;
+   hipError_t e = hipPointerGetAttributes(&attr, p);
+   if (e != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+   }
+   return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+}  // namespace nfft4gp_amd
+
+namespace {
+
+struct TimingRec {
+   std::array<hipEvent_t, 4> ev;
+};
+
+struct PlanExt {
+   AdditivePlan P;
+   std::vector<TimingRec> pending;
+   std::vector<TimingRec> pool;
+};
+
+// single-component handle (the reference's str_adj): *Kp of the single-component setup points here
+struct SingleAdj {
+   nfft4gp_kernel* owner = nullptr;
+   int dim = 1;
+   int max_n = 0;
+   std::vector<double> data;  // first-setup copy of the points (n x dim, column-major)
+   PlanExt* plan = nullptr;
+};
+
+void dfree(void* p)
+{
+   if (p) (void)hipFree(p);
+}
+
+void free_layout(AdditivePlan& P)
+{
+   dfree(P.dl.meta);
+   dfree(P.dl.perm2);
+   dfree(P.dl.q);
+   dfree(P.dl.tile_off);
+   P.dl = DevLayout();
+   dfree(P.d_part);
+   P.d_part = nullptr;
+}
+
+void free_plan(PlanExt* E)
+{
+   if (!E) return;
+   AdditivePlan& P = E->P;
+   free_layout(P);
+   dfree(P.d_grid);
+   dfree(P.d_w);
+   dfree(P.d_wd);
+   dfree(P.d_H);
+   dfree(P.d_Hd);
+   dfree(P.d_C);
+   dfree(P.d_xs);
+   dfree(P.d_ys);
+   for (auto& r : E->pending)
+      for (auto e : r.ev) (void)hipEventDestroy(e);
+   for (auto& r : E->pool)
+      for (auto e : r.ev) (void)hipEventDestroy(e);
+   delete E;
+}
+
+template <class T>
+int upload(T** dptr, const std::vector<T>& h)
+{
+   if (*dptr) {
+      (void)hipFree(*dptr);
+      *dptr = nullptr;
+   }
+   if (h.empty()) return 0;
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)dptr, sizeof(T) * h.size()));
+   NFFT4GP_HIP_CHECK(hipMemcpy(*dptr, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+   return 0;
+}
+
+// nfft_interface.c:150-213: centre by the mean, scale to radius 0.25 unless already in
+// [0.125, 0.25], computed once from all n_global points (same operation order as the reference).
+double centre_and_scale(const double* col, int n_global, int d, std::vector<double>& xs)
+{
+   xs.assign(col, col + (size_t)n_global * d);
+   for (int i = 0; i < d; i++) {
+      double c = 0.0;
+      for (int j = 0; j < n_global; j++) c += xs[(size_t)i * n_global + j];
+      c /= (double)n_global;
+      for (int j = 0; j < n_global; j++) xs[(size_t)i * n_global + j] -= c;
+   }
+   double radius = 0.0;
+   for (int j = 0; j < n_global; j++) {
+      double r = 0.0;
+      for (int i = 0; i < d; i++) r += xs[(size_t)i * n_global + j] * xs[(size_t)i * n_global + j];
+      r = std::sqrt(r);
+      if (r > radius) radius = r;
+   }
+   double scale;
+   if (radius > 0.25 || radius < 0.125) {
+      scale = 0.25 / radius;
+      for (auto& v : xs) v *= scale;
+   } else {
+      scale = 1.0;
+   }
+   return scale;
+}
+
+uint32_t quantize(double x)
+{
+   // x in [-0.5, 0.5): 32-bit fixed point of x mod 1 (exact power-of-two scaling, one rounding)
+   const long long v = std::llround(x * 4294967296.0);
+   return (uint32_t)(unsigned long long)v;
+}
+
+// first setup: nodes -> layout on the device
+int plan_build_points(AdditivePlan& P, const double* buffer)
+{
+   const int ng = P.n_global;
+   std::vector<uint32_t> qc((size_t)P.nw * P.n);
+   P.comp_scale.assign(P.nw, 1.0);
+   std::vector<double> xs;
+   for (int c = 0; c < P.nw; c++) {
+      if (P.comp_dims[c] != 1) {
+         fprintf(stderr,
+                 "nfft4gp_amd: window %d has %d features; the MI355X path implements 1-D additive windows "
+                 "(BASELINE configs B-E). Multi-dimensional windows are not supported yet.\n",
+                 c, P.comp_dims[c]);
+         return -1;
+      }
+      const double* col = buffer + (size_t)c * ng * P.dw;  // nfft_interface.c:703 stride n*dwindows
+      P.comp_scale[c] = centre_and_scale(col, ng, 1, xs);
+      for (int j = 0; j < P.n; j++) qc[(size_t)c * P.n + j] = quantize(xs[(size_t)P.row_begin + j]);
+   }
+   Layout L;
+   build_layout(qc, P.n, P.nw, P.B, P.CG, L);
+   P.ngroups = L.ngroups;
+   P.nblocks = L.nblocks;
+   free_layout(P);
+   if (upload(&P.dl.meta, L.meta) || upload(&P.dl.perm2, L.perm2) || upload(&P.dl.q, L.q) ||
+       upload(&P.dl.tile_off, L.tile_off))
+      return -1;
+   P.dl.ntiles = L.ntiles;
+   P.dl.bytes = L.meta.size() * 2 + L.perm2.size() * 4 + L.q.size() * 4 + L.tile_off.size() * 4;
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part, sizeof(double) * (size_t)std::max(1, P.nblocks) * P.nw * kNos));
+   if (!P.d_grid) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_grid, sizeof(double) * (size_t)P.nw * kNos));
+   if (!P.d_H) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_H, sizeof(double) * (size_t)P.nw * kNos * kNC));
+   if (!P.d_Hd) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_Hd, sizeof(double) * (size_t)P.nw * kNos * kNC));
+   if (!P.d_C && upload(&P.d_C, tap_poly_coeffs())) return -1;
+   P.points_ready = true;
+   return 0;
+}
+
+// every setup: kernel coefficients (nfft_interface.c:216-256)
+int plan_setup(AdditivePlan& P, const double* buffer, int kernel, double f, double l, double mu)
+{
+   if (!device_ok()) {
+      fprintf(stderr, "nfft4gp_amd: no HIP device visible; the operator has no CPU fallback.\n");
+      return -1;
+   }
+   if (!P.points_ready && plan_build_points(P, buffer)) return -1;
+   P.kernel = kernel;
+   P.f = f;
+   P.l = l;
+   P.mu = mu;
+   P.comp_sigma.assign(P.nw, 0.0);
+   std::vector<double> w((size_t)P.nw * kNos), wd((size_t)P.nw * kNos);
+   double bh[kBand], bhd[kBand];
+   for (int c = 0; c < P.nw; c++) {
+      const double sc = P.comp_scale[c];
+      const double sig = (kernel == 0) ? l * sc * std::sqrt(2.0) : l * sc;  // :219 / :355
+      P.comp_sigma[c] = sig;
+      bhat_1d(kernel == 0 ? 0 : 2, sig, bh);
+      bhat_1d(kernel == 0 ? 1 : 3, sig, bhd);
+      const double dscale = (kernel == 0) ? 2.0 * sc * std::sqrt(2.0) / sig : sc / sig;  // :536
+      circulant_1d(bh, P.weight, w.data() + (size_t)c * kNos);
+      circulant_1d(bhd, P.weight * dscale, wd.data() + (size_t)c * kNos);
+   }
+   if (upload(&P.d_w, w) || upload(&P.d_wd, wd)) return -1;
+   return 0;
+}
+
+TimingRec get_rec(PlanExt* E)
+{
+   if (!E->pool.empty()) {
+      TimingRec r = E->pool.back();
+      E->pool.pop_back();
+      return r;
+   }
+   TimingRec r;
+   for (auto& e : r.ev) (void)hipEventCreate(&e);
+   return r;
+}
+
+// y = beta*y + alpha*(op) x  on device pointers
+int plan_apply_dev(PlanExt* E, int grad, double alpha, const double* d_x, double beta, double* d_y)
+{
+   AdditivePlan& P = E->P;
+   hipStream_t s = current_stream();
+   TimingRec rec;
+   if (P.timing) {
+      rec = get_rec(E);
+      (void)hipEventRecord(rec.ev[0], s);
+   }
+   if (launch_spread(P, d_x, P.d_part, s)) return -1;
+   if (P.timing) (void)hipEventRecord(rec.ev[1], s);
+   if (launch_grid(P, P.d_part, P.nblocks, grad, s)) return -1;
+   if (P.timing) (void)hipEventRecord(rec.ev[2], s);
+   if (launch_interp(P, grad, alpha, d_x, beta, d_y, s)) return -1;
+   if (P.timing) {
+      (void)hipEventRecord(rec.ev[3], s);
+      E->pending.push_back(rec);
+   }
+   return 0;
+}
+
+int plan_apply(PlanExt* E, int n, int grad, double alpha, const double* x, double beta, double* y)
+{
+   AdditivePlan& P = E->P;
+   if (!P.points_ready) {
+      fprintf(stderr, "nfft4gp_amd: matvec called before the kernel setup (func_kernel) call.\n");
+      return -1;
+   }
+   if (n != P.n) {
+      fprintf(stderr, "nfft4gp_amd: matvec size %d does not match the handle (%d).\n", n, P.n);
+      return -1;
+   }
+   const size_t ny = (size_t)n * (grad ? 3 : 1);
+   const bool dx = is_device_ptr(x), dy = is_device_ptr(y);
+   if (dx && dy) return plan_apply_dev(E, grad, alpha, x, beta, y);
+   // host staging (PCIe), synchronous
+   hipStream_t s = current_stream();
+   if (!P.d_xs) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_xs, sizeof(double) * (size_t)n));
+   if (!P.d_ys) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_ys, sizeof(double) * (size_t)n * 3));
+   const double* xd = x;
+   double* yd = y;
+   if (!dx) {
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(P.d_xs, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
+      xd = P.d_xs;
+   }
+   if (!dy) {
+      yd = P.d_ys;
+      if (beta != 0.0) NFFT4GP_HIP_CHECK(hipMemcpyAsync(yd, y, sizeof(double) * ny, hipMemcpyHostToDevice, s));
+   }
+   if (plan_apply_dev(E, grad, alpha, xd, beta, yd)) return -1;
+   if (!dy) NFFT4GP_HIP_CHECK(hipMemcpyAsync(y, yd, sizeof(double) * ny, hipMemcpyDeviceToHost, s));
+   NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
+   return 0;
+}
+
+PlanExt* additive_plan(void* str)
+{
+   if (!str) return nullptr;
+   return (PlanExt*)((nfft4gp_kernel*)str)->_external;
+}
+
+nfft4gp_kernel* kernel_struct_create(int max_n)
+{
+   nfft4gp_kernel* k = (nfft4gp_kernel*)calloc(1, sizeof(nfft4gp_kernel));
+   k->_max_n = max_n;
+   k->_omp = 0;
+   k->_ldwork = (size_t)max_n;
+   k->_dwork = (double*)malloc(sizeof(double) * (size_t)std::max(1, max_n));
+   return k;
+}
+
+int setup_common(void* str, int kernel, int n, int ldim, double** Kp, double** dKp)
+{
+   if (Kp == NULL || dKp == NULL) {
+      printf("Error: NFFT kernel requires Kp and dKp to be not NULL.\n");
+      return -1;
+   }
+   nfft4gp_kernel* kd = (nfft4gp_kernel*)str;
+   PlanExt* E = additive_plan(str);
+   if (!E) return -1;
+   (void)n;
+   (void)ldim;
+   if (plan_setup(E->P, kd->_buffer, kernel, kd->_params[0], kd->_params[1], kd->_noise_level)) return -1;
+   *Kp = (double*)str;
+   *dKp = (double*)str;
+   return 0;
+}
+
+void* additive_create(double* data, int n_global, int ldim, int* windows, int nwindows, int dwindows, int rb, int re)
+{
+   nfft4gp_kernel* kd = kernel_struct_create(3 * n_global);  // nfft_interface.c:624
+   kd->_iparams[0] = nwindows;
+   kd->_iparams[1] = dwindows;
+   int skip_window = 1;
+   kd->_iparams[2] = 0;
+   while (skip_window < dwindows && windows[nwindows * dwindows - skip_window] < 0) {  // :630-636
+      skip_window++;
+      kd->_iparams[2]++;
+   }
+   kd->_ibufferp = (int**)malloc(sizeof(int*));
+   kd->_ibufferp[0] = windows;
+   kd->_buffer = (double*)malloc(sizeof(double) * (size_t)n_global * nwindows * dwindows);
+   kd->_own_buffer = 1;
+   PlanExt* E = new PlanExt();
+   AdditivePlan& P = E->P;
+   P.n_global = n_global;
+   P.row_begin = rb;
+   P.row_end = re;
+   P.n = re - rb;
+   P.nw = nwindows;
+   P.dw = dwindows;
+   P.skip_last = kd->_iparams[2];
+   P.weight = 1.0 / (double)nwindows;  // nfft_interface.c:806
+   double* dst = kd->_buffer;
+   const int* fw = windows;
+   for (int i = 0; i < nwindows; i++) {  // :648-670
+      int actual = 0;
+      for (int j = 0; j < dwindows; j++) {
+         if (fw[0] >= 0) {
+            memcpy(dst, data + (size_t)fw[0] * ldim, sizeof(double) * n_global);
+            fw++;
+            dst += n_global;
+            actual++;
+         }
+      }
+      P.comp_dims.push_back(actual);
+   }
+   kd->_external = E;
+   return kd;
+}
+
+}  // namespace
+
+extern "C" {
+
+static const char* kVersion = "nfft4gp_amd 0.1.0 (gfx950)";
+
+const char* Nfft4GPAmdVersion(void) { return kVersion; }
+int Nfft4GPAmdDeviceAvailable(void) { return device_ok(); }
+void Nfft4GPAmdSetStream(void* s) { g_stream = (hipStream_t)s; }
+void* Nfft4GPAmdGetStream(void) { return (void*)g_stream; }
+
+void* Nfft4GPKernelParamCreate(int max_n, int omp)
+{
+   nfft4gp_kernel* k = kernel_struct_create(max_n);
+   k->_omp = omp;
+   return k;
+}
+
+void Nfft4GPKernelParamFree(void* str)
+{
+   nfft4gp_kernel* k = (nfft4gp_kernel*)str;
+   if (!k) return;
+   free(k->_dwork);
+   if (k->_own_buffer) free(k->_buffer);
+   if (k->_own_dbuffer) free(k->_dbuffer);
+   free(k->_ibufferp);
+   if (k->_own_fkernel_buffer_params) Nfft4GPKernelParamFree(k->_fkernel_buffer_params);
+   free(k);
+}
+
+/* ------------------------------- additive ----------------------------------------------------- */
+void* Nfft4GPNFFTAdditiveKernelParamCreate(double* data, int n, int ldim, int d, int* windows, int nwindows,
+                                           int dwindows)
+{
+   (void)d;
+   return additive_create(data, n, ldim, windows, nwindows, dwindows, 0, n);
+}
+
+void* Nfft4GPAmdAdditiveShardCreate(double* data, int n_global, int ldim, int d, int* windows, int nwindows,
+                                    int dwindows, int row_begin, int row_end)
+{
+   (void)d;
+   if (row_begin < 0 || row_end > n_global || row_begin > row_end) {
+      fprintf(stderr, "nfft4gp_amd: invalid shard rows [%d, %d) of %d\n", row_begin, row_end, n_global);
+      return NULL;
+   }
+   return additive_create(data, n_global, ldim, windows, nwindows, dwindows, row_begin, row_end);
+}
+
+int Nfft4GPNFFTAdditiveKernelGaussianKernel(void* str, double* data, int n, int ldim, int d, int* permr, int kr,
+                                            int* permc, int kc, double** Kp, double** dKp)
+{
+   (void)data, (void)d, (void)permr, (void)kr, (void)permc, (void)kc;
+   return setup_common(str, 0, n, ldim, Kp, dKp);
+}
+
+int Nfft4GPNFFTAdditiveKernelMatern12Kernel(void* str, double* data, int n, int ldim, int d, int* permr, int kr,
+                                            int* permc, int kc, double** Kp, double** dKp)
+{
+   (void)data, (void)d, (void)permr, (void)kr, (void)permc, (void)kc;
+   return setup_common(str, 1, n, ldim, Kp, dKp);
+}
+
+int Nfft4GPAdditiveNFFTMatSymv(void* data, int n, double alpha, double* x, double beta, double* y)
+{
+   PlanExt* E = additive_plan(data);
+   if (!E) return -1;
+   return plan_apply(E, n, 0, alpha, x, beta, y);
+}
+
+int Nfft4GPAdditiveNFFTGradMatSymv(void* data, int n, double alpha, double* x, double beta, double* y)
+{
+   PlanExt* E = additive_plan(data);
+   if (!E) return -1;
+   return plan_apply(E, n, 1, alpha, x, beta, y);
+}
+
+void Nfft4GPAdditiveNFFTKernelFree(void* str)
+{
+   if (!str) return;
+   free_plan(additive_plan(str));
+   ((nfft4gp_kernel*)str)->_external = NULL;
+   Nfft4GPKernelParamFree(str);
+}
+
+double* Nfft4GPNFFTAppendData(double* X1, int n1, int ldim1, int d, double* X2, int n2, int ldim2)
+{
+   double* X = (double*)malloc(sizeof(double) * (size_t)(n1 + n2) * d);
+   for (int i = 0; i < d; i++) {
+      memcpy(X + (size_t)i * (n1 + n2), X1 + (size_t)i * ldim1, sizeof(double) * n1);
+      memcpy(X + (size_t)i * (n1 + n2) + n1, X2 + (size_t)i * ldim2, sizeof(double) * n2);
+   }
+   return X;
+}
+
+int Nfft4GPAmdAdditiveLayoutInfo(void* str, long long* out, int nout)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !out) return -1;
+   const AdditivePlan& P = E->P;
+   long long v[10] = {P.n, P.nw, P.B, P.nblocks, P.dl.ntiles, P.dl.ntiles * kWave * kR, kR, P.CG, P.ngroups,
+                      (long long)P.dl.bytes};
+   for (int i = 0; i < nout && i < 10; i++) out[i] = v[i];
+   return 0;
+}
+
+int Nfft4GPAmdTimingEnable(void* str, int enable)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E) return -1;
+   E->P.timing = enable != 0;
+   if (enable) {
+      (void)hipStreamSynchronize(current_stream());
+      for (auto& r : E->pending) E->pool.push_back(r);
+      E->pending.clear();
+      for (int i = 0; i < 3; i++) {
+         E->P.ms[i] = 0;
+         E->P.cnt[i] = 0;
+      }
+   }
+   return 0;
+}
+
+int Nfft4GPAmdTimingQuery(void* str, double* ms, long long* cnt)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E) return -1;
+   AdditivePlan& P = E->P;
+   for (auto& r : E->pending) {
+      NFFT4GP_HIP_CHECK(hipEventSynchronize(r.ev[3]));
+      for (int i = 0; i < 3; i++) {
+         float t = 0.f;
+         NFFT4GP_HIP_CHECK(hipEventElapsedTime(&t, r.ev[i], r.ev[i + 1]));
+         P.ms[i] += t;
+         P.cnt[i]++;
+      }
+      E->pool.push_back(r);
+   }
+   E->pending.clear();
+   for (int i = 0; i < 3; i++) {
+      if (ms) ms[i] = P.ms[i];
+      if (cnt) cnt[i] = P.cnt[i];
+   }
+   return 0;
+}
+
+int Nfft4GPAmdShardSpread(void* str, const double* x_local, double* grid)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready) return -1;
+   AdditivePlan& P = E->P;
+   hipStream_t s = current_stream();
+   if (launch_spread(P, x_local, P.d_part, s)) return -1;
+   if (P.nblocks == 0) {
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * P.nw * kNos, s));
+      return 0;
+   }
+   return launch_reduce_parts(P, P.d_part, grid, s);
+}
+
+int Nfft4GPAmdShardFinish(void* str, const double* grid, int grad, double alpha, const double* x_local, double beta,
+                          double* y_local)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready) return -1;
+   AdditivePlan& P = E->P;
+   hipStream_t s = current_stream();
+   if (launch_grid_from_sum(P, grid, grad, s)) return -1;
+   return launch_interp(P, grad, alpha, x_local, beta, y_local, s);
+}
+
+/* ------------------------------- single component --------------------------------------------- */
+void* Nfft4GPNFFTKernelParamCreate(int max_n, int dim)
+{
+   nfft4gp_kernel* kd = kernel_struct_create(max_n);  // nfft_interface.c:5
+   SingleAdj* adj = new SingleAdj();
+   adj->owner = kd;
+   adj->dim = dim;
+   adj->max_n = max_n;
+   kd->_external = adj;
+   return kd;
+}
+
+int Nfft4GPNFFTKernelParamRemovePoints(void* kernel)
+{
+   nfft4gp_kernel* kd = (nfft4gp_kernel*)kernel;
+   SingleAdj* adj = kd ? (SingleAdj*)kd->_external : nullptr;
+   if (adj && adj->plan) {
+      free_layout(adj->plan->P);
+      adj->plan->P.points_ready = false;
+   }
+   return 0;
+}
+
+int Nfft4GPNFFTKernelParamFreeNFFTKernel(void* kernel) { return Nfft4GPNFFTKernelParamRemovePoints(kernel); }
+
+void Nfft4GPNFFTKernelParamFree(void* kernel)
+{
+   nfft4gp_kernel* kd = (nfft4gp_kernel*)kernel;
+   if (!kd) return;
+   SingleAdj* adj = (SingleAdj*)kd->_external;
+   if (adj) {
+      free_plan(adj->plan);
+      delete adj;
+   }
+   kd->_external = NULL;
+   Nfft4GPKernelParamFree(kd);
+}
+
+void Nfft4GPNFFTKernelFree(void* str) { (void)str; }
+
+static int single_setup(void* str, int kernel, double* data, int n, int ldim, int d, double** Kp, double** dKp)
+{
+   nfft4gp_kernel* kd = (nfft4gp_kernel*)str;
+   SingleAdj* adj = (SingleAdj*)kd->_external;
+   if (Kp == NULL || dKp == NULL) {
+      printf("Error: NFFT kernel requires Kp and dKp to be not NULL.\n");
+      return -1;
+   }
+   if (n != ldim) {
+      printf("Error: NFFT kernel requires n == ldim.\n");
+      return -1;
+   }
+   if (!adj->plan) {
+      adj->data.assign(data, data + (size_t)n * d);  // first call fixes the points (:150-153)
+      adj->plan = new PlanExt();
+      AdditivePlan& P = adj->plan->P;
+      P.n_global = n;
+      P.row_begin = 0;
+      P.row_end = n;
+      P.n = n;
+      P.nw = 1;
+      P.dw = d;
+      P.weight = 1.0;
+      P.comp_dims.assign(1, d);
+   }
+   AdditivePlan& P = adj->plan->P;
+   if (plan_setup(P, adj->data.data(), kernel, kd->_params[0], kd->_params[1], kd->_noise_level)) return -1;
+   *Kp = (double*)adj;
+   *dKp = (double*)adj;
+   return 0;
+}
+
+int Nfft4GPNFFTKernelGaussianKernel(void* str, double* data, int n, int ldim, int d, int* permr, int kr, int* permc,
+                                    int kc, double** Kp, double** dKp)
+{
+   (void)permr, (void)kr, (void)permc, (void)kc;
+   return single_setup(str, 0, data, n, ldim, d, Kp, dKp);
+}
+
+int Nfft4GPNFFTKernelMatern12Kernel(void* str, double* data, int n, int ldim, int d, int* permr, int kr, int* permc,
+                                    int kc, double** Kp, double** dKp)
+{
+   (void)permr, (void)kr, (void)permc, (void)kc;
+   return single_setup(str, 1, data, n, ldim, d, Kp, dKp);
+}
+
+int Nfft4GPNFFTMatSymv(void* data, int n, double alpha, double* x, double beta, double* y)
+{
+   SingleAdj* adj = (SingleAdj*)data;
+   if (!adj || !adj->plan) return -1;
+   return plan_apply(adj->plan, n, 0, alpha, x, beta, y);
+}
+
+int Nfft4GPNFFTGradMatSymv(void* data, int n, double alpha, double* x, double beta, double* y)
+{
+   SingleAdj* adj = (SingleAdj*)data;
+   if (!adj || !adj->plan) return -1;
+   return plan_apply(adj->plan, n, 1, alpha, x, beta, y);
+}
+
+}  // extern "C"

@@ -1,0 +1,371 @@
+// nfft_kernels.hip -- CDNA4 (gfx950) kernels of the additive NFFT matvec.
+//
+// Per matvec three launches on one stream (see internal.h for the algebra):
+//   k_spread  grid = nblocks x ngroups workgroups of 512 threads (8 waves).  The workgroup stages
+//             the block's alpha slice (B doubles) in LDS once for all its components, each lane
+//             walks one R-point run of a single (component, cell) accumulating the 12 moments
+//             alpha*u^d in registers, flushes them with ds_add_f64 into an LDS moment table, and
+//             the workgroup finally folds moments into its 64-cell partial grids (taps = C * M).
+//             HBM: 6 B per point-component (u16 index + u32 fixed-point coordinate) + alpha once.
+//   k_grid    one workgroup per component: sum of the partial grids, the 64x64 real circulant
+//             (= FFT . diag(bhat/phihut^2) . IFFT restricted to Re), and the per-cell
+//             interpolation polynomials H = C^T h.
+//   k_interp  one workgroup per block: lanes walk the same runs, load H[comp][cell] once per run,
+//             Horner per point, ds_add_f64 into an LDS y-block; the epilogue applies
+//             y = beta*y + alpha*ff*(sum + mu*x) (grad: the three outputs of
+//             nfft_interface.c:547-549) with one coalesced pass.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+
+#include "internal.h"
+
+namespace nfft4gp_amd {
+
+constexpr int kSpreadThreads = 512;
+constexpr int kInterpThreads = 512;
+constexpr int kGridThreads = 256;
+
+__device__ __forceinline__ double q_to_u(uint32_t q)
+{
+   // offset inside the cell minus one half: exact in fp64
+   return (double)(q & 0x3FFFFFFu) * 0x1p-26 - 0.5;
+}
+
+// ------------------------------------------------------------------------------------------------
+// spread
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kSpreadThreads) void k_spread(
+    const uint16_t* __restrict__ meta, const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
+    const int* __restrict__ tile_off, const double* __restrict__ x, const double* __restrict__ Cg, int n, int B,
+    int nblocks, int ngroups, int CG, int nw, double* __restrict__ part)
+{
+   extern __shared__ __attribute__((aligned(16))) double smem[];
+   const int Bp = (B + 2) & ~1;
+   double* s_alpha = smem;              // Bp
+   double* s_C = smem + Bp;             // kTaps*kNC = 120
+   double* s_mom = s_C + kTaps * kNC;   // CG*64*kNC
+
+   // XCD-aware decode: the ngroups workgroups of one block land on one XCD (blockIdx % 8), so its
+   // alpha slice is fetched into one L2.  Speed only; correctness does not depend on placement.
+   const int xcd = blockIdx.x & 7;
+   const int rest = blockIdx.x >> 3;
+   const int g = rest % ngroups;
+   const int b = (rest / ngroups) * 8 + xcd;
+   if (b >= nblocks) return;
+
+   const int tid = threadIdx.x;
+   const int base = b * B;
+   const int nloc = min(B, n - base);
+   for (int i = tid; i < Bp; i += kSpreadThreads) s_alpha[i] = (i < nloc) ? x[base + i] : 0.0;
+   for (int i = tid; i < kTaps * kNC; i += kSpreadThreads) s_C[i] = Cg[i];
+   for (int i = tid; i < CG * kNos * kNC; i += kSpreadThreads) s_mom[i] = 0.0;
+   __syncthreads();
+
+   const int lane = tid & 63;
+   const int wave = tid >> 6;
+   const int nwaves = kSpreadThreads / 64;
+   const int c0 = g * CG;
+   const int t0 = tile_off[b * ngroups + g];
+   const int t1 = tile_off[b * ngroups + g + 1];
+   for (int t = t0 + wave; t < t1; t += nwaves) {
+      const uint32_t mt = meta[(size_t)t * 64 + lane];
+      uint32_t pp[kR / 2];
+      uint32_t qq[kR];
+#pragma unroll
+      for (int r2 = 0; r2 < kR / 2; r2++) pp[r2] = perm2[((size_t)t * (kR / 2) + r2) * 64 + lane];
+#pragma unroll
+      for (int r = 0; r < kR; r++) qq[r] = qarr[((size_t)t * kR + r) * 64 + lane];
+      double acc[kNC];
+#pragma unroll
+      for (int d = 0; d < kNC; d++) acc[d] = 0.0;
+#pragma unroll 2
+      for (int r = 0; r < kR; r++) {
+         const uint32_t loc = (r & 1) ? (pp[r >> 1] >> 16) : (pp[r >> 1] & 0xFFFFu);
+         const double u = q_to_u(qq[r]);
+         double tpow = s_alpha[loc];
+         acc[0] += tpow;
+#pragma unroll
+         for (int d = 1; d < kNC; d++) {
+            tpow *= u;
+            acc[d] += tpow;
+         }
+      }
+      const int comp_local = (int)(mt >> 6) - c0;
+      const int cell = (int)(mt & 63u);
+      double* dst = s_mom + ((size_t)comp_local * kNos + cell) * kNC;
+#pragma unroll
+      for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
+   }
+   __syncthreads();
+
+   // fold moments into the 64-cell partial grid of every component of this group:
+   //   g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
+   const int ncomp = min(CG, nw - c0);
+   for (int idx = tid; idx < ncomp * kNos; idx += kSpreadThreads) {
+      const int cl = idx / kNos;
+      const int gi = idx % kNos;
+      double v = 0.0;
+#pragma unroll 1
+      for (int tp = 0; tp < kTaps; tp++) {
+         const double* mrow = s_mom + ((size_t)cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kNC;
+#pragma unroll
+         for (int d = 0; d < kNC; d++) v = fma(s_C[tp * kNC + d], mrow[d], v);
+      }
+      part[((size_t)b * nw + c0 + cl) * kNos + gi] = v;
+   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// grid: sum partial grids, circulant, interpolation polynomials
+// ------------------------------------------------------------------------------------------------
+__device__ void grid_tail(int comp, const double* __restrict__ s_g, const double* __restrict__ w,
+                          const double* __restrict__ Cg, double* __restrict__ H, double* s_h)
+{
+   const int tid = threadIdx.x;
+   if (tid < kNos) {
+      const double* wc = w + (size_t)comp * kNos;
+      double h = 0.0;
+      for (int l2 = 0; l2 < kNos; l2++) h = fma(wc[(tid - l2) & (kNos - 1)], s_g[l2], h);
+      s_h[tid] = h;
+   }
+   __syncthreads();
+   for (int idx = tid; idx < kNos * kNC; idx += blockDim.x) {
+      const int cell = idx / kNC;
+      const int d = idx % kNC;
+      double v = 0.0;
+#pragma unroll
+      for (int tp = 0; tp < kTaps; tp++) v = fma(s_h[(cell - kM + tp) & (kNos - 1)], Cg[tp * kNC + d], v);
+      H[((size_t)comp * kNos + cell) * kNC + d] = v;
+   }
+   __syncthreads();
+}
+
+__global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict__ part, int nparts, int nw,
+                                                      const double* __restrict__ w, const double* __restrict__ wd,
+                                                      const double* __restrict__ Cg, double* __restrict__ H,
+                                                      double* __restrict__ Hd, int grad, int from_sum)
+{
+   __shared__ double s_red[kGridThreads];
+   __shared__ double s_g[kNos];
+   __shared__ double s_h[kNos];
+   const int comp = blockIdx.x;
+   const int tid = threadIdx.x;
+   if (from_sum) {
+      if (tid < kNos) s_g[tid] = part[(size_t)comp * kNos + tid];
+   } else {
+      // kGridThreads/64 lanes per cell stride over the partial grids (fixed order: deterministic)
+      const int cell = tid & 63;
+      const int strand = tid >> 6;
+      const int nstr = kGridThreads / 64;
+      double s = 0.0;
+      for (int p = strand; p < nparts; p += nstr) s += part[((size_t)p * nw + comp) * kNos + cell];
+      s_red[tid] = s;
+      __syncthreads();
+      if (tid < kNos) {
+         double v = 0.0;
+         for (int k = 0; k < nstr; k++) v += s_red[k * 64 + tid];
+         s_g[tid] = v;
+      }
+   }
+   __syncthreads();
+   grid_tail(comp, s_g, w, Cg, H, s_h);
+   if (grad) grid_tail(comp, s_g, wd, Cg, Hd, s_h);
+}
+
+__global__ __launch_bounds__(kGridThreads) void k_reduce_parts(const double* __restrict__ part, int nparts, int nw,
+                                                              double* __restrict__ gsum)
+{
+   // one thread per (comp, cell)
+   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+   if (idx >= nw * kNos) return;
+   double s = 0.0;
+   for (int p = 0; p < nparts; p++) s += part[(size_t)p * nw * kNos + idx];
+   gsum[idx] = s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// interpolation + epilogue
+// ------------------------------------------------------------------------------------------------
+template <bool GRAD>
+__global__ __launch_bounds__(kInterpThreads) void k_interp(
+    const uint16_t* __restrict__ meta, const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
+    const int* __restrict__ tile_off, const double* __restrict__ H, const double* __restrict__ Hd,
+    const double* __restrict__ x, double* __restrict__ y, int n, int B, int ngroups, double alpha, double beta,
+    double f, double mu)
+{
+   extern __shared__ __attribute__((aligned(16))) double smem[];
+   const int Bp = (B + 2) & ~1;
+   double* s_y = smem;
+   double* s_yd = smem + Bp;  // GRAD only
+   const int b = blockIdx.x;
+   const int tid = threadIdx.x;
+   const int base = b * B;
+   const int nloc = min(B, n - base);
+   for (int i = tid; i < Bp; i += kInterpThreads) {
+      s_y[i] = 0.0;
+      if (GRAD) s_yd[i] = 0.0;
+   }
+   __syncthreads();
+
+   const int lane = tid & 63;
+   const int wave = tid >> 6;
+   const int nwaves = kInterpThreads / 64;
+   const int t0 = tile_off[b * ngroups];
+   const int t1 = tile_off[(b + 1) * ngroups];
+   for (int t = t0 + wave; t < t1; t += nwaves) {
+      const uint32_t mt = meta[(size_t)t * 64 + lane];
+      uint32_t pp[kR / 2];
+      uint32_t qq[kR];
+#pragma unroll
+      for (int r2 = 0; r2 < kR / 2; r2++) pp[r2] = perm2[((size_t)t * (kR / 2) + r2) * 64 + lane];
+#pragma unroll
+      for (int r = 0; r < kR; r++) qq[r] = qarr[((size_t)t * kR + r) * 64 + lane];
+      const size_t hoff = (size_t)mt * kNC;  // (comp*64 + cell) * kNC: meta is comp<<6|cell
+      double hc[kNC], hdc[GRAD ? kNC : 1];
+#pragma unroll
+      for (int d = 0; d < kNC; d += 2) {
+         const double2 v = *reinterpret_cast<const double2*>(H + hoff + d);
+         hc[d] = v.x;
+         hc[d + 1] = v.y;
+         if (GRAD) {
+            const double2 vd = *reinterpret_cast<const double2*>(Hd + hoff + d);
+            hdc[d] = vd.x;
+            hdc[d + 1] = vd.y;
+         }
+      }
+#pragma unroll
+      for (int r = 0; r < kR; r++) {
+         const uint32_t loc = (r & 1) ? (pp[r >> 1] >> 16) : (pp[r >> 1] & 0xFFFFu);
+         const double u = q_to_u(qq[r]);
+         double v = hc[kNC - 1];
+#pragma unroll
+         for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
+         atomicAdd(s_y + loc, v);
+         if (GRAD) {
+            double vd = hdc[kNC - 1];
+#pragma unroll
+            for (int d = kNC - 2; d >= 0; d--) vd = fma(vd, u, hdc[d]);
+            atomicAdd(s_yd + loc, vd);
+         }
+      }
+   }
+   __syncthreads();
+
+   const double ff = f * f;
+   for (int j = tid; j < nloc; j += kInterpThreads) {
+      const size_t gj = (size_t)base + j;
+      const double xj = x[gj];
+      if (!GRAD) {
+         const double v = ff * (s_y[j] + mu * xj);
+         y[gj] = (beta == 0.0) ? alpha * v : fma(beta, y[gj], alpha * v);
+      } else {
+         // nfft_interface.c:547-549 summed over components: (2f)(Kx + mu x), ff*dscale*K'x, ff*x
+         const double v0 = 2.0 * f * (s_y[j] + mu * xj);
+         const double v1 = ff * s_yd[j];
+         const double v2 = ff * xj;
+         double* y0 = y;
+         double* y1 = y + n;
+         double* y2 = y + 2 * (size_t)n;
+         if (beta == 0.0) {
+            y0[gj] = alpha * v0;
+            y1[gj] = alpha * v1;
+            y2[gj] = alpha * v2;
+         } else {
+            y0[gj] = fma(beta, y0[gj], alpha * v0);
+            y1[gj] = fma(beta, y1[gj], alpha * v1);
+            y2[gj] = fma(beta, y2[gj], alpha * v2);
+         }
+      }
+   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+static size_t spread_lds_bytes(const AdditivePlan& P)
+{
+   const int Bp = (P.B + 2) & ~1;
+   return sizeof(double) * ((size_t)Bp + kTaps * kNC + (size_t)P.CG * kNos * kNC);
+}
+
+static size_t interp_lds_bytes(const AdditivePlan& P, int grad)
+{
+   const int Bp = (P.B + 2) & ~1;
+   return sizeof(double) * (size_t)Bp * (grad ? 2 : 1);
+}
+
+static void raise_lds_limit(const void* fn, size_t bytes)
+{
+   if (bytes > 64 * 1024) {
+      (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+      (void)hipGetLastError();
+   }
+}
+
+int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream)
+{
+   if (P.dl.ntiles == 0 || P.n == 0) return 0;
+   const size_t lds = spread_lds_bytes(P);
+   static bool raised = false;
+   if (!raised) {
+      raise_lds_limit((const void*)k_spread, 160 * 1024);
+      raised = true;
+   }
+   const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
+   hipLaunchKernelGGL(k_spread, dim3(gridx), dim3(kSpreadThreads), lds, stream, P.dl.meta, P.dl.perm2, P.dl.q,
+                      P.dl.tile_off, d_x, P.d_C, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream)
+{
+   hipLaunchKernelGGL(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, d_part, nparts, P.nw, P.d_w, P.d_wd,
+                      P.d_C, P.d_H, P.d_Hd, grad, 0);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream)
+{
+   hipLaunchKernelGGL(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, d_gridsum, 1, P.nw, P.d_w, P.d_wd,
+                      P.d_C, P.d_H, P.d_Hd, grad, 1);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream)
+{
+   const int total = P.nw * kNos;
+   hipLaunchKernelGGL(k_reduce_parts, dim3((total + kGridThreads - 1) / kGridThreads), dim3(kGridThreads), 0,
+                      stream, d_part, P.nblocks, P.nw, d_gridsum);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, double beta, double* d_y,
+                  hipStream_t stream)
+{
+   if (P.n == 0) return 0;
+   const size_t lds = interp_lds_bytes(P, grad);
+   static bool raised = false;
+   if (!raised) {
+      raise_lds_limit((const void*)k_interp<false>, 160 * 1024);
+      raise_lds_limit((const void*)k_interp<true>, 160 * 1024);
+      raised = true;
+   }
+   if (grad)
+      hipLaunchKernelGGL(k_interp<true>, dim3(P.nblocks), dim3(kInterpThreads), lds, stream, P.dl.meta, P.dl.perm2,
+                         P.dl.q, P.dl.tile_off, P.d_H, P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups, alpha, beta, P.f,
+                         P.mu);
+   else
+      hipLaunchKernelGGL(k_interp<false>, dim3(P.nblocks), dim3(kInterpThreads), lds, stream, P.dl.meta,
+                         P.dl.perm2, P.dl.q, P.dl.tile_off, P.d_H, P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups, alpha,
+                         beta, P.f, P.mu);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+}  // namespace nfft4gp_amd

@@ -1,0 +1,75 @@
+"""Krylov solve and preconditioner front-ends over the C ABI.
+
+``pcg``         Nfft4GPSolverPcg (SRC/solvers/pcg.c:3-206) with an NFFT operator and an optional
+                Nystrom preconditioner, both passed to the C solver as C function pointers (no
+                Python in the iteration loop).
+``NystromPrecond``  Nfft4GPAmdNys* -- the apply of SRC/preconds/nys.c:115-173 on factors U, s, eta,
+                perm produced by the reference's Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .nfft import _ptr
+
+
+class NystromPrecond:
+    def __init__(self, U, s, eta: float, perm=None):
+        U = np.asfortranarray(np.asarray(U, dtype=np.float64))
+        n, k = U.shape
+        s = np.ascontiguousarray(np.asarray(s, dtype=np.float64))
+        p = None if perm is None else np.ascontiguousarray(np.asarray(perm, dtype=np.int32))
+        self.n, self.k, self.eta = n, k, float(eta)
+        self.h = _lib.lib().Nfft4GPAmdNysCreate(n, k, U.ctypes.data, s.ctypes.data, float(eta),
+                                                p.ctypes.data if p is not None else None)
+        if not self.h:
+            raise RuntimeError("Nfft4GPAmdNysCreate failed")
+
+    def solve(self, x, rhs):
+        rc = _lib.lib().Nfft4GPAmdNysSolve(self.h, self.n, _ptr(x)[0], _ptr(rhs)[0])
+        if rc:
+            raise RuntimeError("Nfft4GPAmdNysSolve failed")
+        return x
+
+    @property
+    def solve_fnptr(self) -> int:
+        return _lib.fnptr("Nfft4GPAmdNysSolve")
+
+    def free(self):
+        if getattr(self, "h", None):
+            _lib.lib().Nfft4GPAmdNysFree(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def pcg(op, b, x=None, maxits=1000, tol=1e-6, atol=False, precond=None, print_level=0):
+    """Nfft4GPSolverPcg(op, n, matvec, precond, precondfunc, x, b, maxits, atol, tol, ...).
+
+    ``op`` is an NFFTAdditiveKernel (its C matvec is used) and ``precond`` a NystromPrecond or None.
+    ``b``/``x`` are numpy arrays or torch GPU tensors.  Returns (x, rel_res, rel_res_v, iters) with the
+    reference's reporting semantics (iters = 0 when not converged, pcg.c:19,197).
+    """
+    if x is None:
+        x = b * 0
+    n = op.n
+    rel = C.c_double()
+    relv = _lib.dp()
+    it = C.c_int()
+    L = _lib.lib()
+    rc = L.Nfft4GPSolverPcg(op.h, n, op.matvec_fnptr, precond.h if precond else None,
+                            precond.solve_fnptr if precond else None, _ptr(x)[0], _ptr(b)[0], int(maxits),
+                            int(bool(atol)), float(tol), C.byref(rel), C.byref(relv), C.byref(it), int(print_level))
+    if rc:
+        raise RuntimeError("Nfft4GPSolverPcg failed")
+    length = L.Nfft4GPAmdPcgHistoryLength()
+    hist = np.ctypeslib.as_array(relv, shape=(length,)).copy()
+    C.CDLL(None).free(relv)
+    return x, rel.value, hist, it.value
