@@ -96,8 +96,12 @@ def cpu_baseline(n, d, X, x, max_seconds=25.0):
     }
 
 
-def run_pcg_single(op, torch, n, rng_seed=906, tol=1e-6, maxits=3000):
+def run_pcg_single(op, torch, n, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1):
+    """PCG to 1e-6 on the same points.  At l = 1 the NFFT-approximated kernel of this data is
+    indefinite (bhat_k < 0 for a Gaussian truncated at r = 1/2; DESIGN.md 'SPD'), which is why the
+    reference solves with FGMRES; CG needs an SPD operator, so it runs at l = 0.1 (all bhat_k > 0)."""
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    assert op.setup(amd.GAUSSIAN, f=1.0, l=l_pcg, mu=0.01) == 0
     rng = np.random.default_rng(rng_seed + 1)
     b = torch.tensor(rng.random(n) - 0.5, device="cuda")
     x = torch.zeros(n, dtype=torch.float64, device="cuda")
@@ -107,7 +111,8 @@ def run_pcg_single(op, torch, n, rng_seed=906, tol=1e-6, maxits=3000):
     torch.cuda.synchronize()
     t = time.time() - t0
     return {"pcg_time_s": t, "pcg_iters": iters, "pcg_rel_res": relres, "pcg_converged": iters > 0,
-            "pcg_precond": "none", "pcg_tol": tol}
+            "pcg_precond": "none", "pcg_tol": tol, "pcg_l": l_pcg,
+            "pcg_ms_per_iter": 1e3 * t / max(iters if iters > 0 else len(hist) - 1, 1)}
 
 
 def main():

@@ -184,6 +184,23 @@ int Nfft4GPAmdShardSpread(void *str, const NFFT4GP_DOUBLE *x_local, NFFT4GP_DOUB
 int Nfft4GPAmdShardFinish(void *str, const NFFT4GP_DOUBLE *grid, int grad, NFFT4GP_DOUBLE alpha,
                           const NFFT4GP_DOUBLE *x_local, NFFT4GP_DOUBLE beta, NFFT4GP_DOUBLE *y_local);
 
+/* ---- host-only helpers (no GPU needed): the setup math of the device plan, exported so the CPU
+ * test-suite can check it and emulate the kernels against the oracle ------------------------------- */
+/* tap polynomial coefficients C[t*12 + d], t = 0..9, d = 0..11 (monomials in u = frac - 1/2) */
+int Nfft4GPAmdHostTapPoly(NFFT4GP_DOUBLE *C);
+/* kernel kind 0 gaussian, 1 xx_gaussian, 2 laplacian_rbf, 3 der_laplacian_rbf with parameter c:
+ * bhat[32] (k = -16..15) and the 64-point real circulant w = weight * sum_k bhat_k/phihut_k^2 cos(...) */
+int Nfft4GPAmdHostCirculant(int kind, NFFT4GP_DOUBLE c, NFFT4GP_DOUBLE weight, NFFT4GP_DOUBLE *bhat,
+                            NFFT4GP_DOUBLE *w);
+/* centre + scale one 1-D window exactly as nfft_interface.c:150-213 and quantize to 32-bit fixed point;
+ * returns the scale (or -1 if all points coincide) */
+NFFT4GP_DOUBLE Nfft4GPAmdHostPrepare(const NFFT4GP_DOUBLE *col, int n, unsigned int *q);
+/* chunk layout of per-window quantized coordinates qc[c*n + j]; call with NULL arrays to get
+ * counts[0] = ntiles, counts[1] = ngroups, counts[2] = nblocks, then with arrays of
+ * ntiles*64 (meta), ntiles*8*64 (perm2), ntiles*16*64 (q), nblocks*ngroups+1 (tile_off) */
+int Nfft4GPAmdHostLayout(const unsigned int *qc, int n, int nw, int B, int CG, long long *counts,
+                         unsigned short *meta, unsigned int *perm2, unsigned int *q, int *tile_off);
+
 #ifdef __cplusplus
 }
 #endif

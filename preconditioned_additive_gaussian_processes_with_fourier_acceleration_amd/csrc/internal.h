@@ -115,6 +115,8 @@ struct AdditivePlan {
    long long cnt[3] = {0, 0, 0};
 };
 
+// copy the tap polynomial table into constant memory of the current device
+int upload_tap_coeffs();
 // launchers (nfft_kernels.hip); all enqueue on `stream`
 int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream);
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream);

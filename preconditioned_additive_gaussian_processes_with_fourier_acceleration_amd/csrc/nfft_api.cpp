@@ -140,6 +140,7 @@ double centre_and_scale(const double* col, int n_global, int d, std::vector<doub
       if (r > radius) radius = r;
    }
    double scale;
+   if (radius == 0.0) return -1.0;  // all points coincide: the reference divides by zero (:190)
    if (radius > 0.25 || radius < 0.125) {
       scale = 0.25 / radius;
       for (auto& v : xs) v *= scale;
@@ -173,6 +174,12 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
       }
       const double* col = buffer + (size_t)c * ng * P.dw;  // nfft_interface.c:703 stride n*dwindows
       P.comp_scale[c] = centre_and_scale(col, ng, 1, xs);
+      if (P.comp_scale[c] < 0.0) {
+         fprintf(stderr,
+                 "nfft4gp_amd: all points of window %d coincide (radius 0); the reference's scaling "
+                 "0.25/radius (nfft_interface.c:190) is undefined there.\n", c);
+         return -1;
+      }
       for (int j = 0; j < P.n; j++) qc[(size_t)c * P.n + j] = quantize(xs[(size_t)P.row_begin + j]);
    }
    Layout L;
@@ -189,7 +196,7 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
    if (!P.d_grid) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_grid, sizeof(double) * (size_t)P.nw * kNos));
    if (!P.d_H) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_H, sizeof(double) * (size_t)P.nw * kNos * kNC));
    if (!P.d_Hd) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_Hd, sizeof(double) * (size_t)P.nw * kNos * kNC));
-   if (!P.d_C && upload(&P.d_C, tap_poly_coeffs())) return -1;
+   if (upload_tap_coeffs()) return -1;
    P.points_ready = true;
    return 0;
 }
@@ -536,6 +543,49 @@ int Nfft4GPAmdShardFinish(void* str, const double* grid, int grad, double alpha,
    hipStream_t s = current_stream();
    if (launch_grid_from_sum(P, grid, grad, s)) return -1;
    return launch_interp(P, grad, alpha, x_local, beta, y_local, s);
+}
+
+/* ------------------------------- host-only helpers -------------------------------------------- */
+int Nfft4GPAmdHostTapPoly(double* C)
+{
+   const std::vector<double>& T = tap_poly_coeffs();
+   memcpy(C, T.data(), sizeof(double) * T.size());
+   return 0;
+}
+
+int Nfft4GPAmdHostCirculant(int kind, double c, double weight, double* bhat, double* w)
+{
+   double bh[kBand];
+   bhat_1d(kind, c, bh);
+   if (bhat) memcpy(bhat, bh, sizeof(bh));
+   if (w) circulant_1d(bh, weight, w);
+   return 0;
+}
+
+double Nfft4GPAmdHostPrepare(const double* col, int n, unsigned int* q)
+{
+   std::vector<double> xs;
+   const double sc = centre_and_scale(col, n, 1, xs);
+   if (sc < 0.0) return sc;
+   for (int j = 0; j < n; j++) q[j] = quantize(xs[j]);
+   return sc;
+}
+
+int Nfft4GPAmdHostLayout(const unsigned int* qc, int n, int nw, int B, int CG, long long* counts,
+                         unsigned short* meta, unsigned int* perm2, unsigned int* q, int* tile_off)
+{
+   if (B <= 0 || B > 65535 || CG <= 0 || n < 0 || nw <= 0 || nw > 1023) return -1;
+   std::vector<uint32_t> v(qc, qc + (size_t)n * nw);
+   Layout L;
+   build_layout(v, n, nw, B, CG, L);
+   counts[0] = L.ntiles;
+   counts[1] = L.ngroups;
+   counts[2] = L.nblocks;
+   if (meta) memcpy(meta, L.meta.data(), L.meta.size() * sizeof(uint16_t));
+   if (perm2) memcpy(perm2, L.perm2.data(), L.perm2.size() * sizeof(uint32_t));
+   if (q) memcpy(q, L.q.data(), L.q.size() * sizeof(uint32_t));
+   if (tile_off) memcpy(tile_off, L.tile_off.data(), L.tile_off.size() * sizeof(int));
+   return 0;
 }
 
 /* ------------------------------- single component --------------------------------------------- */

@@ -24,7 +24,7 @@
 namespace nfft4gp_amd {
 
 constexpr int kSpreadThreads = 512;
-constexpr int kInterpThreads = 512;
+constexpr int kInterpThreads = 1024;
 constexpr int kGridThreads = 256;
 
 __device__ __forceinline__ double q_to_u(uint32_t q)
@@ -36,16 +36,35 @@ __device__ __forceinline__ double q_to_u(uint32_t q)
 // ------------------------------------------------------------------------------------------------
 // spread
 // ------------------------------------------------------------------------------------------------
+// tap polynomial coefficients C[t][d] in constant memory: wave-uniform reads become scalar loads
+__constant__ double c_taps[kTaps * kNC];
+
+struct TileRegs {
+   uint32_t mt;
+   uint32_t pp[kR / 2];
+   uint32_t qq[kR];
+};
+
+__device__ __forceinline__ void load_tile(TileRegs& T, const uint16_t* __restrict__ meta,
+                                          const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
+                                          int t, int lane)
+{
+   T.mt = meta[(size_t)t * 64 + lane];
+#pragma unroll
+   for (int r2 = 0; r2 < kR / 2; r2++) T.pp[r2] = perm2[((size_t)t * (kR / 2) + r2) * 64 + lane];
+#pragma unroll
+   for (int r = 0; r < kR; r++) T.qq[r] = qarr[((size_t)t * kR + r) * 64 + lane];
+}
+
 __global__ __launch_bounds__(kSpreadThreads) void k_spread(
     const uint16_t* __restrict__ meta, const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
-    const int* __restrict__ tile_off, const double* __restrict__ x, const double* __restrict__ Cg, int n, int B,
-    int nblocks, int ngroups, int CG, int nw, double* __restrict__ part)
+    const int* __restrict__ tile_off, const double* __restrict__ x, int n, int B, int nblocks, int ngroups, int CG,
+    int nw, double* __restrict__ part)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = (B + 2) & ~1;
-   double* s_alpha = smem;              // Bp
-   double* s_C = smem + Bp;             // kTaps*kNC = 120
-   double* s_mom = s_C + kTaps * kNC;   // CG*64*kNC
+   double* s_alpha = smem;      // Bp
+   double* s_grid = smem + Bp;  // CG*64 partial grids
 
    // XCD-aware decode: the ngroups workgroups of one block land on one XCD (blockIdx % 8), so its
    // alpha slice is fetched into one L2.  Speed only; correctness does not depend on placement.
@@ -56,34 +75,35 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
    if (b >= nblocks) return;
 
    const int tid = threadIdx.x;
-   const int base = b * B;
-   const int nloc = min(B, n - base);
-   for (int i = tid; i < Bp; i += kSpreadThreads) s_alpha[i] = (i < nloc) ? x[base + i] : 0.0;
-   for (int i = tid; i < kTaps * kNC; i += kSpreadThreads) s_C[i] = Cg[i];
-   for (int i = tid; i < CG * kNos * kNC; i += kSpreadThreads) s_mom[i] = 0.0;
-   __syncthreads();
-
    const int lane = tid & 63;
    const int wave = tid >> 6;
    const int nwaves = kSpreadThreads / 64;
    const int c0 = g * CG;
    const int t0 = tile_off[b * ngroups + g];
    const int t1 = tile_off[b * ngroups + g + 1];
-   for (int t = t0 + wave; t < t1; t += nwaves) {
-      const uint32_t mt = meta[(size_t)t * 64 + lane];
-      uint32_t pp[kR / 2];
-      uint32_t qq[kR];
-#pragma unroll
-      for (int r2 = 0; r2 < kR / 2; r2++) pp[r2] = perm2[((size_t)t * (kR / 2) + r2) * 64 + lane];
-#pragma unroll
-      for (int r = 0; r < kR; r++) qq[r] = qarr[((size_t)t * kR + r) * 64 + lane];
+
+   // issue the first tile's loads before the alpha staging so both are in flight together
+   TileRegs cur;
+   int t = t0 + wave;
+   if (t < t1) load_tile(cur, meta, perm2, qarr, t, lane);
+
+   const int base = b * B;
+   const int nloc = min(B, n - base);
+   for (int i = tid; i < Bp; i += kSpreadThreads) s_alpha[i] = (i < nloc) ? x[base + i] : 0.0;
+   for (int i = tid; i < CG * kNos; i += kSpreadThreads) s_grid[i] = 0.0;
+   __syncthreads();
+
+   for (; t < t1; t += nwaves) {
+      TileRegs nxt;
+      const int tn = t + nwaves;
+      if (tn < t1) load_tile(nxt, meta, perm2, qarr, tn, lane);  // prefetch the next tile
       double acc[kNC];
 #pragma unroll
       for (int d = 0; d < kNC; d++) acc[d] = 0.0;
 #pragma unroll 2
       for (int r = 0; r < kR; r++) {
-         const uint32_t loc = (r & 1) ? (pp[r >> 1] >> 16) : (pp[r >> 1] & 0xFFFFu);
-         const double u = q_to_u(qq[r]);
+         const uint32_t loc = (r & 1) ? (cur.pp[r >> 1] >> 16) : (cur.pp[r >> 1] & 0xFFFFu);
+         const double u = q_to_u(cur.qq[r]);
          double tpow = s_alpha[loc];
          acc[0] += tpow;
 #pragma unroll
@@ -92,42 +112,39 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
             acc[d] += tpow;
          }
       }
-      const int comp_local = (int)(mt >> 6) - c0;
-      const int cell = (int)(mt & 63u);
-      double* dst = s_mom + ((size_t)comp_local * kNos + cell) * kNC;
+      // fold the run's moments into its 10 taps and add them to the component's LDS grid:
+      //   grid[(cell - m + tp) mod 64] += sum_d C[tp][d] * M[d]
+      const int comp_local = (int)(cur.mt >> 6) - c0;
+      const int cell = (int)(cur.mt & 63u);
+      double* gdst = s_grid + comp_local * kNos;
 #pragma unroll
-      for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
+      for (int tp = 0; tp < kTaps; tp++) {
+         double v = 0.0;
+#pragma unroll
+         for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], acc[d], v);
+         atomicAdd(gdst + ((cell - kM + tp) & (kNos - 1)), v);  // ds_add_f64
+      }
+      if (tn < t1) cur = nxt;
    }
    __syncthreads();
-
-   // fold moments into the 64-cell partial grid of every component of this group:
-   //   g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
    const int ncomp = min(CG, nw - c0);
-   for (int idx = tid; idx < ncomp * kNos; idx += kSpreadThreads) {
-      const int cl = idx / kNos;
-      const int gi = idx % kNos;
-      double v = 0.0;
-#pragma unroll 1
-      for (int tp = 0; tp < kTaps; tp++) {
-         const double* mrow = s_mom + ((size_t)cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kNC;
-#pragma unroll
-         for (int d = 0; d < kNC; d++) v = fma(s_C[tp * kNC + d], mrow[d], v);
-      }
-      part[((size_t)b * nw + c0 + cl) * kNos + gi] = v;
-   }
+   for (int idx = tid; idx < ncomp * kNos; idx += kSpreadThreads)
+      part[((size_t)b * nw + c0) * kNos + idx] = s_grid[idx];
 }
 
 // ------------------------------------------------------------------------------------------------
 // grid: sum partial grids, circulant, interpolation polynomials
 // ------------------------------------------------------------------------------------------------
 __device__ void grid_tail(int comp, const double* __restrict__ s_g, const double* __restrict__ w,
-                          const double* __restrict__ Cg, double* __restrict__ H, double* s_h)
+                          double* __restrict__ H, double* s_w, double* s_h)
 {
    const int tid = threadIdx.x;
+   if (tid < kNos) s_w[tid] = w[(size_t)comp * kNos + tid];
+   __syncthreads();
    if (tid < kNos) {
-      const double* wc = w + (size_t)comp * kNos;
       double h = 0.0;
-      for (int l2 = 0; l2 < kNos; l2++) h = fma(wc[(tid - l2) & (kNos - 1)], s_g[l2], h);
+#pragma unroll 8
+      for (int l2 = 0; l2 < kNos; l2++) h = fma(s_w[(tid - l2) & (kNos - 1)], s_g[l2], h);
       s_h[tid] = h;
    }
    __syncthreads();
@@ -136,7 +153,7 @@ __device__ void grid_tail(int comp, const double* __restrict__ s_g, const double
       const int d = idx % kNC;
       double v = 0.0;
 #pragma unroll
-      for (int tp = 0; tp < kTaps; tp++) v = fma(s_h[(cell - kM + tp) & (kNos - 1)], Cg[tp * kNC + d], v);
+      for (int tp = 0; tp < kTaps; tp++) v = fma(s_h[(cell - kM + tp) & (kNos - 1)], c_taps[tp * kNC + d], v);
       H[((size_t)comp * kNos + cell) * kNC + d] = v;
    }
    __syncthreads();
@@ -144,24 +161,35 @@ __device__ void grid_tail(int comp, const double* __restrict__ s_g, const double
 
 __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict__ part, int nparts, int nw,
                                                       const double* __restrict__ w, const double* __restrict__ wd,
-                                                      const double* __restrict__ Cg, double* __restrict__ H,
-                                                      double* __restrict__ Hd, int grad, int from_sum)
+                                                      double* __restrict__ H, double* __restrict__ Hd, int grad,
+                                                      int from_sum)
 {
    __shared__ double s_red[kGridThreads];
    __shared__ double s_g[kNos];
    __shared__ double s_h[kNos];
+   __shared__ double s_w[kNos];
    const int comp = blockIdx.x;
    const int tid = threadIdx.x;
    if (from_sum) {
       if (tid < kNos) s_g[tid] = part[(size_t)comp * kNos + tid];
    } else {
-      // kGridThreads/64 lanes per cell stride over the partial grids (fixed order: deterministic)
+      // kGridThreads/64 strands per cell over the partial grids, 4 independent accumulators each;
+      // fixed order -> deterministic
       const int cell = tid & 63;
       const int strand = tid >> 6;
       const int nstr = kGridThreads / 64;
-      double s = 0.0;
-      for (int p = strand; p < nparts; p += nstr) s += part[((size_t)p * nw + comp) * kNos + cell];
-      s_red[tid] = s;
+      double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+      int p = strand;
+      const size_t stride = (size_t)nw * kNos;
+      const double* src = part + (size_t)comp * kNos + cell;
+      for (; p + 3 * nstr < nparts; p += 4 * nstr) {
+         s0 += src[(size_t)p * stride];
+         s1 += src[(size_t)(p + nstr) * stride];
+         s2 += src[(size_t)(p + 2 * nstr) * stride];
+         s3 += src[(size_t)(p + 3 * nstr) * stride];
+      }
+      for (; p < nparts; p += nstr) s0 += src[(size_t)p * stride];
+      s_red[tid] = (s0 + s1) + (s2 + s3);
       __syncthreads();
       if (tid < kNos) {
          double v = 0.0;
@@ -170,8 +198,8 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
       }
    }
    __syncthreads();
-   grid_tail(comp, s_g, w, Cg, H, s_h);
-   if (grad) grid_tail(comp, s_g, wd, Cg, Hd, s_h);
+   grid_tail(comp, s_g, w, H, s_w, s_h);
+   if (grad) grid_tail(comp, s_g, wd, Hd, s_w, s_h);
 }
 
 __global__ __launch_bounds__(kGridThreads) void k_reduce_parts(const double* __restrict__ part, int nparts, int nw,
@@ -214,14 +242,16 @@ __global__ __launch_bounds__(kInterpThreads) void k_interp(
    const int nwaves = kInterpThreads / 64;
    const int t0 = tile_off[b * ngroups];
    const int t1 = tile_off[(b + 1) * ngroups];
-   for (int t = t0 + wave; t < t1; t += nwaves) {
-      const uint32_t mt = meta[(size_t)t * 64 + lane];
-      uint32_t pp[kR / 2];
-      uint32_t qq[kR];
-#pragma unroll
-      for (int r2 = 0; r2 < kR / 2; r2++) pp[r2] = perm2[((size_t)t * (kR / 2) + r2) * 64 + lane];
-#pragma unroll
-      for (int r = 0; r < kR; r++) qq[r] = qarr[((size_t)t * kR + r) * 64 + lane];
+   TileRegs cur;
+   int t = t0 + wave;
+   if (t < t1) load_tile(cur, meta, perm2, qarr, t, lane);
+   for (; t < t1; t += nwaves) {
+      TileRegs nxt;
+      const int tn = t + nwaves;
+      if (tn < t1) load_tile(nxt, meta, perm2, qarr, tn, lane);  // prefetch the next tile
+      const uint32_t mt = cur.mt;
+      const uint32_t* pp = cur.pp;
+      const uint32_t* qq = cur.qq;
       const size_t hoff = (size_t)mt * kNC;  // (comp*64 + cell) * kNC: meta is comp<<6|cell
       double hc[kNC], hdc[GRAD ? kNC : 1];
 #pragma unroll
@@ -250,6 +280,7 @@ __global__ __launch_bounds__(kInterpThreads) void k_interp(
             atomicAdd(s_yd + loc, vd);
          }
       }
+      if (tn < t1) cur = nxt;
    }
    __syncthreads();
 
@@ -287,7 +318,7 @@ __global__ __launch_bounds__(kInterpThreads) void k_interp(
 static size_t spread_lds_bytes(const AdditivePlan& P)
 {
    const int Bp = (P.B + 2) & ~1;
-   return sizeof(double) * ((size_t)Bp + kTaps * kNC + (size_t)P.CG * kNos * kNC);
+   return sizeof(double) * ((size_t)Bp + (size_t)P.CG * kNos);
 }
 
 static size_t interp_lds_bytes(const AdditivePlan& P, int grad)
@@ -304,6 +335,21 @@ static void raise_lds_limit(const void* fn, size_t bytes)
    }
 }
 
+int upload_tap_coeffs()
+{
+   // constant memory is per device: upload once per device this process uses
+   static bool done[64] = {false};
+   int dev = 0;
+   NFFT4GP_HIP_CHECK(hipGetDevice(&dev));
+   if (dev < 0 || dev >= 64) return -1;
+   if (!done[dev]) {
+      const std::vector<double>& C = tap_poly_coeffs();
+      NFFT4GP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_taps), C.data(), sizeof(double) * kTaps * kNC));
+      done[dev] = true;
+   }
+   return 0;
+}
+
 int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream)
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
@@ -315,7 +361,7 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
    }
    const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
    hipLaunchKernelGGL(k_spread, dim3(gridx), dim3(kSpreadThreads), lds, stream, P.dl.meta, P.dl.perm2, P.dl.q,
-                      P.dl.tile_off, d_x, P.d_C, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part);
+                      P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -323,7 +369,7 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream)
 {
    hipLaunchKernelGGL(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, d_part, nparts, P.nw, P.d_w, P.d_wd,
-                      P.d_C, P.d_H, P.d_Hd, grad, 0);
+                      P.d_H, P.d_Hd, grad, 0);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -331,7 +377,7 @@ int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int gra
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream)
 {
    hipLaunchKernelGGL(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, d_gridsum, 1, P.nw, P.d_w, P.d_wd,
-                      P.d_C, P.d_H, P.d_Hd, grad, 1);
+                      P.d_H, P.d_Hd, grad, 1);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

@@ -1,0 +1,152 @@
+"""CPU tests of the product's host logic (no GPU): C-ABI library, setup math, chunk layout, and a
+numpy replay of the kernels' arithmetic against the oracle."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+from emulate import EmulatedPlan, circulant, layout, prepare, tap_poly
+from oracle import OracleAdditiveNFFT, oracle_lib
+
+
+def rel(a, b):
+    return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / np.linalg.norm(np.asarray(b)))
+
+
+def test_library_exports_every_header_symbol():
+    syms = amd.header_symbols()
+    assert len(syms) >= 40
+    out = subprocess.run(["nm", "-D", "--defined-only", amd._lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+    L = amd.lib()
+    for s in syms:
+        assert getattr(L, s) is not None
+    assert b"gfx950" in L.Nfft4GPAmdVersion()
+
+
+def test_library_is_gfx950_code_object():
+    blob = open(amd._lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"gfx942" not in blob and b"gfx90a" not in blob
+
+
+def test_struct_layout_matches_reference():
+    # SRC/linearalg/kernels.h:65-95 on LP64
+    st = amd._lib.NfftKernelStruct
+    assert st._params.offset == 0 and st._iparams.offset == 40
+    assert st._noise_level.offset == 72 and st._buffer.offset == 88
+    assert st._external.offset == 168 and C.sizeof(st) == 176
+
+
+@pytest.mark.skipif(os.environ.get("HIP_VISIBLE_DEVICES") is None and amd.lib().Nfft4GPAmdDeviceAvailable(),
+                    reason="a GPU is visible")
+def test_no_device_fails_loudly():
+    L = amd.lib()
+    assert L.Nfft4GPAmdDeviceAvailable() == 0
+    rng = np.random.default_rng(0)
+    X = rng.random((100, 2))
+    op = amd.NFFTAdditiveKernel(X, np.array([0, 1], np.int32), 2, 1)
+    assert op.setup(amd.GAUSSIAN, 1.0, 1.0, 0.01) == -1
+    with pytest.raises(RuntimeError):
+        op.matsymv(np.zeros(100))
+
+
+def test_tap_polynomials_match_window():
+    Cm = tap_poly()
+    lib = oracle_lib()
+    u = np.linspace(-0.5, 0.5, 2001)
+    peak = lib.orc_window_phi(0.0)
+    err = 0.0
+    for t in range(10):
+        exact = np.array([lib.orc_window_phi(uu + 0.5 + 4 - t) for uu in u])
+        approx = np.polynomial.polynomial.polyval(u, Cm[t])
+        err = max(err, np.max(np.abs(exact - approx)) / peak)
+    assert err < 1e-12, err
+
+
+def test_bhat_and_circulant_match_oracle():
+    rng = np.random.default_rng(1)
+    X = rng.random((500, 1))
+    orc = OracleAdditiveNFFT(X, np.array([0], np.int32), 1, 1)
+    for kernel in (0, 1):
+        orc.setup(kernel, 1.0, 0.7, 0.01)
+        info = orc.comp_info(0)
+        bh, _ = circulant(0 if kernel == 0 else 2, info["sigma0"], 1.0)
+        np.testing.assert_allclose(bh, info["bhat"], rtol=1e-12, atol=1e-15)
+        bhd, _ = circulant(1 if kernel == 0 else 3, info["sigma0"], 1.0)
+        np.testing.assert_allclose(bhd, info["bhat_d"], rtol=1e-12, atol=1e-15)
+
+
+def test_prepare_matches_reference_scaling():
+    rng = np.random.default_rng(2)
+    X = rng.random((3000, 1)) * 7.0 - 2.0
+    orc = OracleAdditiveNFFT(X, np.array([0], np.int32), 1, 1)
+    orc.setup(0, 1.0, 1.0, 0.01)
+    sc, q = prepare(X[:, 0])
+    assert sc == orc.comp_info(0)["scale"]
+    xs = orc.comp_points(0)[:, 0]
+    # 32-bit fixed point of x mod 1: error <= 2^-33
+    back = (q.astype(np.int64) - (q >= 2 ** 31) * 2 ** 32) / 2.0 ** 32
+    assert np.max(np.abs(back - xs)) <= 2.0 ** -33
+    # radius already in [0.125, 0.25] -> scale 1 (nfft_interface.c:188-196)
+    sc2, _ = prepare(np.linspace(-0.2, 0.2, 101) + 5.0)
+    assert sc2 == 1.0
+    assert prepare(np.full(10, 3.0))[0] == -1.0
+
+
+@pytest.mark.parametrize("n,B,CG", [(10000, 4096, 8), (5000, 1000, 3), (777, 4096, 2)])
+def test_layout_invariants(n, B, CG):
+    nw = 5
+    rng = np.random.default_rng(n)
+    qc = np.zeros((nw, n), np.uint32)
+    for c in range(nw):
+        x = rng.beta(0.5, 2.0, n) if c == 0 else rng.random(n)
+        _, qc[c] = prepare(x)
+    L = layout(qc.ravel(), n, nw, B, CG)
+    meta, loc, q = L["meta"], L["loc"], L["q"]
+    comp, cell = meta >> 6, meta & 63
+    seen = np.zeros((nw, n), np.int64)
+    ng = L["ngroups"]
+    assert ng == (nw + CG - 1) // CG and L["nblocks"] == (n + B - 1) // B
+    assert np.all(np.diff(L["tile_off"]) >= 0) and L["tile_off"][-1] == L["ntiles"]
+    for b in range(L["nblocks"]):
+        for g in range(ng):
+            t0, t1 = L["tile_off"][b * ng + g], L["tile_off"][b * ng + g + 1]
+            cc = comp[t0:t1]
+            assert np.all((cc >= g * CG) & (cc < min(nw, (g + 1) * CG)))
+            real = loc[t0:t1] < B
+            # every real slot: its coordinate is the point's and lies in the chunk's cell
+            tt, ll, rr = np.nonzero(real)
+            j = b * B + loc[t0:t1][tt, ll, rr]
+            c = cc[tt, ll]
+            assert np.all(q[t0:t1][tt, ll, rr] == qc[c, j])
+            assert np.all((qc[c, j] >> 26) == cell[t0:t1][tt, ll])
+            np.add.at(seen, (c, j), 1)
+    assert np.all(seen == 1)  # every (window, point) exactly once
+
+
+@pytest.mark.parametrize("kernel", [0, 1])
+def test_emulated_kernels_match_oracle(kernel):
+    rng = np.random.default_rng(3)
+    n, d = 6000, 4
+    X = rng.random((n, d))
+    x = rng.random(n) - 0.5
+    y0 = rng.random(3 * n)
+    win = np.arange(d, dtype=np.int32)
+    orc = OracleAdditiveNFFT(X, win, d, 1)
+    orc.setup(kernel, 1.2, 0.8, 0.02)
+    em = EmulatedPlan(X, [[c] for c in range(d)], B=1024, CG=3)
+    em.setup(kernel, 1.2, 0.8, 0.02)
+    assert rel(em.matsymv(x), orc.matsymv(x)) < 1e-8
+    assert rel(em.matsymv(x, -1.0, 0.5, y0[:n]), orc.matsymv(x, -1.0, 0.5, y0[:n])) < 1e-8
+    g = em.matsymv(x, 0.3, 2.0, y0, grad=True)
+    gr = orc.gradmatsymv(x, 0.3, 2.0, y0)
+    for k in range(3):
+        s = slice(k * n, (k + 1) * n)
+        assert rel(g[s], gr[s]) < 1e-8

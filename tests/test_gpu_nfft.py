@@ -112,7 +112,14 @@ def test_hyperparameter_update_reuses_nodes(torch_cuda):
         assert rel(op.matsymv(x), orc.matsymv(x)) <= TOL_TIGHT
 
 
-@pytest.mark.parametrize("n", [1, 63, 4095, 4096, 4097, 20001])
+def test_coincident_points_fail_loudly(torch_cuda):
+    # the reference's scale 0.25/radius divides by zero when every point coincides (:188-191)
+    X = np.full((10, 1), 0.3)
+    op = amd.NFFTAdditiveKernel(X, np.array([0], np.int32), 1, 1)
+    assert op.setup(amd.GAUSSIAN, 1.0, 1.0, 0.01) == -1
+
+
+@pytest.mark.parametrize("n", [2, 63, 4095, 4096, 4097, 20001])
 def test_ragged_sizes(torch_cuda, n):
     d = 3
     X, x = make(n, d, seed=n)
