@@ -255,3 +255,49 @@ def ref_pcg(matvec_py, n, b, x0=None, maxits=1000, tol=1e-6, atol=0, precond_py=
     m = min(maxits, n)
     hist = np.ctypeslib.as_array(relv, shape=(m + 1,)).copy()
     return x, rel.value, hist, it.value
+
+
+# ----------------------------------------------------------------------------------------------
+# Nystrom preconditioner of the reference (SRC/preconds/nys.c), driven through oracle/_ref
+# ----------------------------------------------------------------------------------------------
+class PrecondNysStruct(C.Structure):
+    """precond_nys, SRC/preconds/nys.h:24-55."""
+    _fields_ = [
+        ("_k_setup", C.c_int), ("_own_perm", C.c_int), ("_perm", _ip), ("_n", C.c_int), ("_tits", C.c_int),
+        ("_titt", C.c_double), ("_tset", C.c_double), ("_tlogdet", C.c_double), ("_tdvp", C.c_double),
+        ("_nys_opt", C.c_int), ("_k", C.c_int), ("_eta", C.c_double), ("_f2", C.c_double),
+        ("_U", _dp), ("_s", _dp), ("_work", _dp), ("_K", _dp), ("_dU", _dp), ("_dK", _dp),
+        ("_chol_K11", C.c_void_p), ("_dvp_nosolve", C.c_int),
+    ]
+
+
+class RefNystrom:
+    """Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660) on the reference's dense additive kernel."""
+
+    def __init__(self, dense: "RefDenseAdditive", f, l, mu, k, perm):
+        lib = ref_lib()
+        self.lib = lib
+        st = dense.st
+        st._params[0] = f
+        st._params[1] = l
+        st._noise_level = mu
+        self.perm = np.ascontiguousarray(np.asarray(perm, dtype=np.int32))
+        self.h = lib.Nfft4GPPrecondNysCreate()
+        lib.Nfft4GPPrecondNysSetRank(self.h, k)
+        lib.Nfft4GPPrecondNysSetPerm(self.h, _i(self.perm), 0)
+        fk = C.cast(lib.Nfft4GPKernelAdditiveKernel, C.c_void_p)
+        rc = lib.Nfft4GPPrecondNysSetupWithKernel(_d(dense._data), dense.n, dense.n, dense.d, fk, dense.h, 0,
+                                                  self.h)
+        assert rc == 0
+        self.st = PrecondNysStruct.from_address(self.h)
+        self.n, self.k = dense.n, k
+
+    def factors(self):
+        n, k = self.n, self.k
+        U = np.ctypeslib.as_array(self.st._U, shape=(n * k,)).reshape(n, k, order="F").copy()
+        s = np.ctypeslib.as_array(self.st._s, shape=(k,)).copy()
+        return U, s, self.st._eta, self.perm.copy()
+
+    def solve(self, x, rhs):
+        self.lib.Nfft4GPPrecondNysSolve(C.c_void_p(self.h), self.n, _d(x), _d(rhs))
+        return x

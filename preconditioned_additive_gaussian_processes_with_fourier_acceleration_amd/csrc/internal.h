@@ -96,7 +96,7 @@ struct AdditivePlan {
    double f = 1.0, l = 1.0, mu = 0.0;
    double weight = 1.0;  // 1/nwindows
    // layout
-   int B = 4096, CG = 8, ngroups = 0, nblocks = 0;
+   int B = 4096, CG = 4, ngroups = 0, nblocks = 0;
    DevLayout dl;
    // device buffers
    double* d_part = nullptr;  // [nblocks][nw][64]

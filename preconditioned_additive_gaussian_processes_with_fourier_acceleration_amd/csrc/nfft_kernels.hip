@@ -63,8 +63,8 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = (B + 2) & ~1;
-   double* s_alpha = smem;      // Bp
-   double* s_grid = smem + Bp;  // CG*64 partial grids
+   double* s_alpha = smem;     // Bp
+   double* s_mom = smem + Bp;  // CG*64*kNC per-cell moments
 
    // XCD-aware decode: the ngroups workgroups of one block land on one XCD (blockIdx % 8), so its
    // alpha slice is fetched into one L2.  Speed only; correctness does not depend on placement.
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
    const int base = b * B;
    const int nloc = min(B, n - base);
    for (int i = tid; i < Bp; i += kSpreadThreads) s_alpha[i] = (i < nloc) ? x[base + i] : 0.0;
-   for (int i = tid; i < CG * kNos; i += kSpreadThreads) s_grid[i] = 0.0;
+   for (int i = tid; i < CG * kNos * kNC; i += kSpreadThreads) s_mom[i] = 0.0;
    __syncthreads();
 
    for (; t < t1; t += nwaves) {
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
       double acc[kNC];
 #pragma unroll
       for (int d = 0; d < kNC; d++) acc[d] = 0.0;
-#pragma unroll 2
+#pragma unroll
       for (int r = 0; r < kR; r++) {
          const uint32_t loc = (r & 1) ? (cur.pp[r >> 1] >> 16) : (cur.pp[r >> 1] & 0xFFFFu);
          const double u = q_to_u(cur.qq[r]);
@@ -112,24 +112,30 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
             acc[d] += tpow;
          }
       }
-      // fold the run's moments into its 10 taps and add them to the component's LDS grid:
-      //   grid[(cell - m + tp) mod 64] += sum_d C[tp][d] * M[d]
       const int comp_local = (int)(cur.mt >> 6) - c0;
       const int cell = (int)(cur.mt & 63u);
-      double* gdst = s_grid + comp_local * kNos;
+      double* dst = s_mom + (comp_local * kNos + cell) * kNC;
 #pragma unroll
-      for (int tp = 0; tp < kTaps; tp++) {
-         double v = 0.0;
-#pragma unroll
-         for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], acc[d], v);
-         atomicAdd(gdst + ((cell - kM + tp) & (kNos - 1)), v);  // ds_add_f64
-      }
+      for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
       if (tn < t1) cur = nxt;
    }
    __syncthreads();
+
+   // fold moments into the 64-cell partial grid of every component of this group:
+   //   g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
    const int ncomp = min(CG, nw - c0);
-   for (int idx = tid; idx < ncomp * kNos; idx += kSpreadThreads)
-      part[((size_t)b * nw + c0) * kNos + idx] = s_grid[idx];
+   for (int idx = tid; idx < ncomp * kNos; idx += kSpreadThreads) {
+      const int cl = idx / kNos;
+      const int gi = idx % kNos;
+      double v = 0.0;
+#pragma unroll 1
+      for (int tp = 0; tp < kTaps; tp++) {
+         const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kNC;
+#pragma unroll
+         for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
+      }
+      part[((size_t)b * nw + c0 + cl) * kNos + gi] = v;
+   }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -318,7 +324,7 @@ __global__ __launch_bounds__(kInterpThreads) void k_interp(
 static size_t spread_lds_bytes(const AdditivePlan& P)
 {
    const int Bp = (P.B + 2) & ~1;
-   return sizeof(double) * ((size_t)Bp + (size_t)P.CG * kNos);
+   return sizeof(double) * ((size_t)Bp + (size_t)P.CG * kNos * kNC);
 }
 
 static size_t interp_lds_bytes(const AdditivePlan& P, int grad)

@@ -1,0 +1,138 @@
+"""GPU tests of the device-resident PCG, vector ops and the Nystrom apply against the reference's own
+compiled code (oracle/_ref: pcg.c, vecops.c, nys.c) driven with the oracle's NFFT matvec."""
+import numpy as np
+import pytest
+
+import oracle as O
+from oracle import OracleAdditiveNFFT
+
+import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+
+pytestmark = pytest.mark.gpu
+needs_ref = pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref not built")
+
+
+def rel(a, b):
+    return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / np.linalg.norm(np.asarray(b)))
+
+
+def problem(n=4000, d=4, seed=906, l=0.1, mu=0.01):
+    rng = np.random.default_rng(seed)
+    X = rng.random((n, d))
+    b = rng.random(n) - 0.5
+    win = np.arange(d, dtype=np.int32)
+    op = amd.NFFTAdditiveKernel(X, win, d, 1)
+    assert op.setup(amd.GAUSSIAN, 1.0, l, mu) == 0
+    orc = OracleAdditiveNFFT(X, win, d, 1)
+    orc.setup(0, 1.0, l, mu)
+    return X, b, win, op, orc
+
+
+def test_vecops_host_and_device(torch_cuda):
+    torch = torch_cuda
+    L = amd.lib()
+    rng = np.random.default_rng(0)
+    n = 100_003
+    x = rng.random(n)
+    y = rng.random(n)
+    assert abs(L.Nfft4GPVecDdot(x.ctypes.data, n, y.ctypes.data) - x @ y) <= 1e-12 * abs(x @ y)
+    assert abs(L.Nfft4GPVecNorm2(x.ctypes.data, n) - np.linalg.norm(x)) <= 1e-12 * np.linalg.norm(x)
+    xd = torch.tensor(x, device="cuda")
+    yd = torch.tensor(y, device="cuda")
+    assert abs(L.Nfft4GPVecDdot(xd.data_ptr(), n, yd.data_ptr()) - x @ y) <= 1e-12 * abs(x @ y)
+    L.Nfft4GPVecAxpy(0.5, xd.data_ptr(), n, yd.data_ptr())
+    np.testing.assert_allclose(yd.cpu().numpy(), y + 0.5 * x, rtol=1e-15)
+    L.Nfft4GPVecScale(yd.data_ptr(), n, 2.0)
+    np.testing.assert_allclose(yd.cpu().numpy(), 2 * (y + 0.5 * x), rtol=1e-15)
+    yd.fill_(float("nan"))
+    L.Nfft4GPVecScale(yd.data_ptr(), n, 0.0)  # scale 0 fills zeros (vecops.c:74-77)
+    assert float(yd.abs().sum()) == 0.0
+    h = x.copy()
+    L.Nfft4GPVecFill(h.ctypes.data, n, 3.0)
+    assert np.all(h == 3.0)
+    h2 = y.copy()
+    L.Nfft4GPVecAxpy(-1.5, x.ctypes.data, n, h2.ctypes.data)
+    np.testing.assert_allclose(h2, y - 1.5 * x, rtol=1e-15)
+
+
+@needs_ref
+@pytest.mark.parametrize("ptrs", ["host", "device"])
+def test_pcg_matches_reference_pcg(torch_cuda, ptrs):
+    torch = torch_cuda
+    n = 4000
+    X, b, win, op, orc = problem(n)
+
+    def mv(alpha, xv, beta, yv):
+        yv[:] = orc.matsymv(np.array(xv), alpha, beta, np.array(yv))
+
+    x_ref, rr_ref, hist_ref, it_ref = O.ref_pcg(mv, n, b, maxits=2000, tol=1e-6)
+    assert it_ref > 0
+    if ptrs == "host":
+        x, rr, hist, it = amd.pcg(op, b.copy(), np.zeros(n), maxits=2000, tol=1e-6)
+    else:
+        xd = torch.zeros(n, dtype=torch.float64, device="cuda")
+        x, rr, hist, it = amd.pcg(op, torch.tensor(b, device="cuda"), xd, maxits=2000, tol=1e-6)
+        x = x.cpu().numpy()
+    assert it > 0 and rr <= 1e-6
+    assert abs(it - it_ref) <= max(2, int(0.05 * it_ref)), (it, it_ref)
+    k = min(20, it, it_ref)
+    np.testing.assert_allclose(hist[:k], hist_ref[:k], rtol=1e-5)
+    assert rel(x, x_ref) <= 1e-4
+
+
+def test_pcg_early_exits(torch_cuda):
+    n = 2000
+    X, b, win, op, orc = problem(n)
+    x, rr, hist, it = amd.pcg(op, np.zeros(n), np.ones(n), maxits=100, tol=1e-6)
+    assert it == 0 and rr == 0.0 and len(hist) == 1 and np.all(x == 0)   # pcg.c:32-41
+    xs, _, _, it1 = amd.pcg(op, b.copy(), np.zeros(n), maxits=2000, tol=1e-8)
+    assert it1 > 0
+    x2, rr2, hist2, it2 = amd.pcg(op, b.copy(), xs.copy(), maxits=100, tol=1e-6)
+    assert it2 == 0 and len(hist2) == 1 and rr2 < 1e-6                   # pcg.c:70-84
+    # not converged within maxits -> iter stays 0 (pcg.c:19,197)
+    _, rr3, hist3, it3 = amd.pcg(op, b.copy(), np.zeros(n), maxits=3, tol=1e-12)
+    assert it3 == 0 and len(hist3) == 4 and rr3 > 1e-12
+
+
+@needs_ref
+def test_nystrom_apply_matches_reference(torch_cuda):
+    torch = torch_cuda
+    n, d, k = 3000, 4, 64
+    rng = np.random.default_rng(5)
+    X = rng.random((n, d))
+    win = np.arange(d, dtype=np.int32)
+    dense = O.RefDenseAdditive(X, win, d, 1, kernel=0)
+    perm = rng.permutation(n).astype(np.int32)
+    nys = O.RefNystrom(dense, 1.0, 0.1, 0.01, k, perm)
+    U, s, eta, p = nys.factors()
+    pre = amd.NystromPrecond(U, s, eta, p)
+    r = rng.random(n) - 0.5
+    x_ref = nys.solve(np.zeros(n), r.copy())
+    x = pre.solve(np.zeros(n), r.copy())
+    assert rel(x, x_ref) <= 1e-12
+    xd = torch.zeros(n, dtype=torch.float64, device="cuda")
+    pre.solve(xd, torch.tensor(r, device="cuda"))
+    assert rel(xd.cpu().numpy(), x_ref) <= 1e-12
+
+
+@needs_ref
+def test_preconditioned_pcg_matches_reference(torch_cuda):
+    n, d, k = 4000, 4, 128
+    X, b, win, op, orc = problem(n)
+    rng = np.random.default_rng(6)
+    dense = O.RefDenseAdditive(X, win, d, 1, kernel=0)
+    nys = O.RefNystrom(dense, 1.0, 0.1, 0.01, k, rng.permutation(n).astype(np.int32))
+    U, s, eta, p = nys.factors()
+    pre = amd.NystromPrecond(U, s, eta, p)
+
+    def mv(alpha, xv, beta, yv):
+        yv[:] = orc.matsymv(np.array(xv), alpha, beta, np.array(yv))
+
+    def pc(xv, rv):
+        xv[:] = nys.solve(np.zeros(n), np.array(rv))
+
+    x_ref, rr_ref, hist_ref, it_ref = O.ref_pcg(mv, n, b, maxits=2000, tol=1e-6, precond_py=pc)
+    x, rr, hist, it = amd.pcg(op, b.copy(), np.zeros(n), maxits=2000, tol=1e-6, precond=pre)
+    assert it_ref > 0 and it > 0
+    assert abs(it - it_ref) <= max(2, int(0.05 * it_ref)), (it, it_ref)
+    assert rel(x, x_ref) <= 1e-4
