@@ -8,7 +8,8 @@
 //   group g = components [g*CG, (g+1)*CG)
 //   chunk   = up to R points of ONE (component, cell), padded with dummies (local index B, which
 //             the kernels map to a zero alpha / a discarded output slot)
-//   tile    = 64 chunks, one per lane; stored lane-fastest so every load is coalesced:
+//   tile    = 64 chunks, one per lane (dealt column-wise, see emit_block_group); stored lane-fastest
+//             so every load is coalesced:
 //               meta [tile][lane]            u16  comp << 6 | cell
 //               perm2[tile][r/2][lane]       u32  local index of points r and r+1 (16 bits each)
 //               q    [tile][r][lane]         u32  fixed-point x mod 1 (cell = q >> 26)
@@ -30,15 +31,27 @@ struct ChunkSink {
    uint32_t* q;
 };
 
-// enumerate the chunks of (block b, group g); returns the number of chunks; if `out` has arrays,
-// writes tiles starting at tile index t0
+// enumerate the chunks of (block b, group g) in (component, cell) order; returns the number of
+// tiles.  With arrays, writes them into tiles [t0, t0 + T) where T = ntiles: chunk k goes to tile
+// t0 + k % T, lane k / T ("dealt" column-wise), so the 64 lanes of a tile hold chunks T apart in the
+// sorted order -- different cells -- and their LDS flushes do not collide on one address.
 long long emit_block_group(const std::vector<uint32_t>& qc, int n, int nw, int B, int CG, int b, int g,
-                           const ChunkSink* out, long long t0, std::vector<int>& cnt, std::vector<int>& off,
-                           std::vector<uint16_t>& sorted)
+                           const ChunkSink* out, long long t0, long long T, std::vector<int>& cnt,
+                           std::vector<int>& off, std::vector<uint16_t>& sorted)
 {
    const int base = b * B;
    const int nloc = std::min(B, n - base);
    const int c0 = g * CG, c1 = std::min(nw, c0 + CG);
+   if (out) {
+      // every slot of the group's tiles starts as a dummy chunk of the group's first component
+      for (long long tile = t0; tile < t0 + T; tile++)
+         for (int lane = 0; lane < kWave; lane++) {
+            out->meta[tile * kWave + lane] = (uint16_t)(c0 << 6);
+            for (int r2 = 0; r2 < kR / 2; r2++)
+               out->perm2[(tile * (kR / 2) + r2) * kWave + lane] = (uint32_t)B | ((uint32_t)B << 16);
+            for (int r = 0; r < kR; r++) out->q[(tile * kR + r) * kWave + lane] = 0u;
+         }
+   }
    long long nchunks = 0;
    for (int c = c0; c < c1; c++) {
       const uint32_t* qq = qc.data() + (size_t)c * n + base;
@@ -54,8 +67,8 @@ long long emit_block_group(const std::vector<uint32_t>& qc, int n, int nw, int B
          for (int s = off[cell]; s < off[cell + 1]; s += kR) {
             if (out) {
                const long long chunk = nchunks;
-               const long long tile = t0 + chunk / kWave;
-               const int lane = (int)(chunk % kWave);
+               const long long tile = t0 + chunk % T;
+               const int lane = (int)(chunk / T);
                out->meta[tile * kWave + lane] = (uint16_t)((c << 6) | cell);
                uint16_t loc[kR];
                uint32_t qv[kR];
@@ -78,19 +91,7 @@ long long emit_block_group(const std::vector<uint32_t>& qc, int n, int nw, int B
          }
       }
    }
-   const long long ntiles = (nchunks + kWave - 1) / kWave;
-   if (out) {
-      // pad the last tile with dummy chunks of the group's first component, cell 0
-      for (long long chunk = nchunks; chunk < ntiles * kWave; chunk++) {
-         const long long tile = t0 + chunk / kWave;
-         const int lane = (int)(chunk % kWave);
-         out->meta[tile * kWave + lane] = (uint16_t)(c0 << 6);
-         for (int r2 = 0; r2 < kR / 2; r2++)
-            out->perm2[(tile * (kR / 2) + r2) * kWave + lane] = (uint32_t)B | ((uint32_t)B << 16);
-         for (int r = 0; r < kR; r++) out->q[(tile * kR + r) * kWave + lane] = 0u;
-      }
-   }
-   return ntiles;
+   return (nchunks + kWave - 1) / kWave;
 }
 
 template <class F>
@@ -122,7 +123,7 @@ void build_layout(const std::vector<uint32_t>& qc, int n, int nw, int B, int CG,
       std::vector<int> cnt(kNos), off(kNos + 1);
       std::vector<uint16_t> sorted(B);
       for (int g = 0; g < L.ngroups; g++)
-         tiles[b * L.ngroups + g] = emit_block_group(qc, n, nw, B, CG, b, g, nullptr, 0, cnt, off, sorted);
+         tiles[b * L.ngroups + g] = emit_block_group(qc, n, nw, B, CG, b, g, nullptr, 0, 0, cnt, off, sorted);
    });
    L.tile_off.assign(nbg + 1, 0);
    long long acc = 0;
@@ -140,7 +141,8 @@ void build_layout(const std::vector<uint32_t>& qc, int n, int nw, int B, int CG,
       std::vector<int> cnt(kNos), off(kNos + 1);
       std::vector<uint16_t> sorted(B);
       for (int g = 0; g < L.ngroups; g++)
-         emit_block_group(qc, n, nw, B, CG, b, g, &sink, L.tile_off[b * L.ngroups + g], cnt, off, sorted);
+         emit_block_group(qc, n, nw, B, CG, b, g, &sink, L.tile_off[b * L.ngroups + g],
+                          L.tile_off[b * L.ngroups + g + 1] - L.tile_off[b * L.ngroups + g], cnt, off, sorted);
    });
 }
 

@@ -331,6 +331,19 @@ int setup_common(void* str, int kernel, int n, int ldim, double** Kp, double** d
    return 0;
 }
 
+// tuning overrides (layout only; results are independent of them up to rounding)
+void env_layout(AdditivePlan& P)
+{
+   if (const char* e = getenv("NFFT4GP_AMD_BLOCK")) {
+      const int v = atoi(e);
+      if (v >= 256 && v <= 16384) P.B = v;
+   }
+   if (const char* e = getenv("NFFT4GP_AMD_CG")) {
+      const int v = atoi(e);
+      if (v >= 1 && v <= 64) P.CG = v;
+   }
+}
+
 void* additive_create(double* data, int n_global, int ldim, int* windows, int nwindows, int dwindows, int rb, int re)
 {
    nfft4gp_kernel* kd = kernel_struct_create(3 * n_global);  // nfft_interface.c:624
@@ -356,6 +369,7 @@ void* additive_create(double* data, int n_global, int ldim, int* windows, int nw
    P.dw = dwindows;
    P.skip_last = kd->_iparams[2];
    P.weight = 1.0 / (double)nwindows;  // nfft_interface.c:806
+   env_layout(P);
    double* dst = kd->_buffer;
    const int* fw = windows;
    for (int i = 0; i < nwindows; i++) {  // :648-670
@@ -652,6 +666,7 @@ static int single_setup(void* str, int kernel, double* data, int n, int ldim, in
       P.dw = d;
       P.weight = 1.0;
       P.comp_dims.assign(1, d);
+      env_layout(P);
    }
    AdditivePlan& P = adj->plan->P;
    if (plan_setup(P, adj->data.data(), kernel, kd->_params[0], kd->_params[1], kd->_noise_level)) return -1;

@@ -26,6 +26,9 @@ namespace nfft4gp_amd {
 constexpr int kSpreadThreads = 512;
 constexpr int kInterpThreads = 1024;
 constexpr int kGridThreads = 256;
+// LDS row stride of the moment table: 13 doubles (26 banks) so rows of different cells spread over
+// the 64 banks instead of repeating every 8 cells (stride 12 -> 24 banks)
+constexpr int kMomStride = kNC + 1;
 
 __device__ __forceinline__ double q_to_u(uint32_t q)
 {
@@ -64,7 +67,7 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = (B + 2) & ~1;
    double* s_alpha = smem;     // Bp
-   double* s_mom = smem + Bp;  // CG*64*kNC per-cell moments
+   double* s_mom = smem + Bp;  // CG*64*kMomStride per-cell moments
 
    // XCD-aware decode: the ngroups workgroups of one block land on one XCD (blockIdx % 8), so its
    // alpha slice is fetched into one L2.  Speed only; correctness does not depend on placement.
@@ -90,7 +93,7 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
    const int base = b * B;
    const int nloc = min(B, n - base);
    for (int i = tid; i < Bp; i += kSpreadThreads) s_alpha[i] = (i < nloc) ? x[base + i] : 0.0;
-   for (int i = tid; i < CG * kNos * kNC; i += kSpreadThreads) s_mom[i] = 0.0;
+   for (int i = tid; i < CG * kNos * kMomStride; i += kSpreadThreads) s_mom[i] = 0.0;
    __syncthreads();
 
    for (; t < t1; t += nwaves) {
@@ -114,7 +117,7 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
       }
       const int comp_local = (int)(cur.mt >> 6) - c0;
       const int cell = (int)(cur.mt & 63u);
-      double* dst = s_mom + (comp_local * kNos + cell) * kNC;
+      double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
 #pragma unroll
       for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
       if (tn < t1) cur = nxt;
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
       double v = 0.0;
 #pragma unroll 1
       for (int tp = 0; tp < kTaps; tp++) {
-         const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kNC;
+         const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
 #pragma unroll
          for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
       }
@@ -324,7 +327,7 @@ __global__ __launch_bounds__(kInterpThreads) void k_interp(
 static size_t spread_lds_bytes(const AdditivePlan& P)
 {
    const int Bp = (P.B + 2) & ~1;
-   return sizeof(double) * ((size_t)Bp + (size_t)P.CG * kNos * kNC);
+   return sizeof(double) * ((size_t)Bp + (size_t)P.CG * kNos * kMomStride);
 }
 
 static size_t interp_lds_bytes(const AdditivePlan& P, int grad)

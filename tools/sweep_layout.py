@@ -1,0 +1,31 @@
+"""Sweep layout knobs (block size B, components per spread group CG) for the config-C matvec.
+Each setting runs in a fresh subprocess (env vars are read at handle creation)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r'''
+import json, sys, time, numpy as np, torch
+sys.path.insert(0, %r)
+import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+n, d = 1000000, 32
+rng = np.random.default_rng(906); X = rng.random((n, d)); x = rng.random(n) - 0.5
+op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+assert op.setup(amd.GAUSSIAN, 1.0, 1.0, 0.01) == 0
+xd = torch.tensor(x, device="cuda"); yd = torch.zeros(n, dtype=torch.float64, device="cuda")
+for _ in range(10): op.matsymv(xd, 1.0, 0.0, yd)
+torch.cuda.synchronize(); op.timing(True); t = time.perf_counter()
+for _ in range(100): op.matsymv(xd, 1.0, 0.0, yd)
+torch.cuda.synchronize(); el = time.perf_counter() - t
+tq = op.timing_query(); info = op.layout_info()
+print(json.dumps({"ms": el * 10, "spread": tq["spread"][0] / tq["spread"][1], "grid": tq["grid"][0] / tq["grid"][1],
+                  "interp": tq["interp"][0] / tq["interp"][1], "slots": info["slots"], "tiles": info["ntiles"]}))
+''' % ROOT
+for B in [2048, 4096, 8192]:
+    for CG in [2, 4, 8, 16]:
+        env = dict(os.environ, NFFT4GP_AMD_BLOCK=str(B), NFFT4GP_AMD_CG=str(CG))
+        r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
+        line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr[-300:]
+        print(f"B={B} CG={CG} {line}", flush=True)
