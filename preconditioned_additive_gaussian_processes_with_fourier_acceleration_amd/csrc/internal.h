@@ -97,6 +97,7 @@ struct AdditivePlan {
    double weight = 1.0;  // 1/nwindows
    // layout
    int B = 4096, CG = 4, ngroups = 0, nblocks = 0;
+   int spread_variant = 0, interp_variant = 0;  // kernel shape variants (nfft_kernels.hip)
    DevLayout dl;
    // device buffers
    double* d_part = nullptr;  // [nblocks][nw][64]

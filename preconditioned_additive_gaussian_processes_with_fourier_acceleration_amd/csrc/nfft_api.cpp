@@ -342,6 +342,8 @@ void env_layout(AdditivePlan& P)
       const int v = atoi(e);
       if (v >= 1 && v <= 64) P.CG = v;
    }
+   if (const char* e = getenv("NFFT4GP_AMD_SPREAD_VARIANT")) P.spread_variant = atoi(e);
+   if (const char* e = getenv("NFFT4GP_AMD_INTERP_VARIANT")) P.interp_variant = atoi(e);
 }
 
 void* additive_create(double* data, int n_global, int ldim, int* windows, int nwindows, int dwindows, int rb, int re)

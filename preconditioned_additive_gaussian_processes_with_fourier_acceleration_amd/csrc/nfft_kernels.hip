@@ -1,19 +1,21 @@
 // nfft_kernels.hip -- CDNA4 (gfx950) kernels of the additive NFFT matvec.
 //
 // Per matvec three launches on one stream (see internal.h for the algebra):
-//   k_spread  grid = nblocks x ngroups workgroups of 512 threads (8 waves).  The workgroup stages
-//             the block's alpha slice (B doubles) in LDS once for all its components, each lane
-//             walks one R-point run of a single (component, cell) accumulating the 12 moments
-//             alpha*u^d in registers, flushes them with ds_add_f64 into an LDS moment table, and
-//             the workgroup finally folds moments into its 64-cell partial grids (taps = C * M).
-//             HBM: 6 B per point-component (u16 index + u32 fixed-point coordinate) + alpha once.
-//   k_grid    one workgroup per component: sum of the partial grids, the 64x64 real circulant
-//             (= FFT . diag(bhat/phihut^2) . IFFT restricted to Re), and the per-cell
-//             interpolation polynomials H = C^T h.
+//   k_spread  one workgroup per (block of B points, group of CG windows).  The workgroup stages the
+//             block's alpha slice (B doubles) in LDS once for its windows; each lane walks one R-point
+//             run of a single (window, cell), accumulates the 12 moments alpha*u^d in registers and
+//             flushes them with ds_add_f64 into an LDS moment table; the workgroup finally folds the
+//             moments into 64-cell partial grids (taps = C * M) and writes them to part[comp][block].
+//             HBM: 6 B per (point, window) -- u16 local index + u32 fixed-point coordinate -- + alpha.
+//   k_grid    one workgroup per window: sum of the partial grids (fixed order, deterministic), the
+//             64x64 real circulant (= FFT . diag(bhat/phihut^2) . IFFT restricted to Re), and the
+//             per-cell interpolation polynomials H = C^T h.
 //   k_interp  one workgroup per block: lanes walk the same runs, load H[comp][cell] once per run,
 //             Horner per point, ds_add_f64 into an LDS y-block; the epilogue applies
-//             y = beta*y + alpha*ff*(sum + mu*x) (grad: the three outputs of
-//             nfft_interface.c:547-549) with one coalesced pass.
+//             y = beta*y + alpha*ff*(sum + mu*x) (grad: the three outputs of nfft_interface.c:547-549)
+//             in one coalesced pass.
+// Kernel shapes (threads per workgroup, occupancy hint, next-run prefetch) are template parameters;
+// the launchers pick a variant from AdditivePlan (env NFFT4GP_AMD_SPREAD_VARIANT / _INTERP_VARIANT).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -23,9 +25,7 @@
 
 namespace nfft4gp_amd {
 
-constexpr int kSpreadThreads = 512;
-constexpr int kInterpThreads = 1024;
-constexpr int kGridThreads = 256;
+constexpr int kGridThreads = 1024;
 // LDS row stride of the moment table: 13 doubles (26 banks) so rows of different cells spread over
 // the 64 banks instead of repeating every 8 cells (stride 12 -> 24 banks)
 constexpr int kMomStride = kNC + 1;
@@ -36,9 +36,6 @@ __device__ __forceinline__ double q_to_u(uint32_t q)
    return (double)(q & 0x3FFFFFFu) * 0x1p-26 - 0.5;
 }
 
-// ------------------------------------------------------------------------------------------------
-// spread
-// ------------------------------------------------------------------------------------------------
 // tap polynomial coefficients C[t][d] in constant memory: wave-uniform reads become scalar loads
 __constant__ double c_taps[kTaps * kNC];
 
@@ -59,7 +56,11 @@ __device__ __forceinline__ void load_tile(TileRegs& T, const uint16_t* __restric
    for (int r = 0; r < kR; r++) T.qq[r] = qarr[((size_t)t * kR + r) * 64 + lane];
 }
 
-__global__ __launch_bounds__(kSpreadThreads) void k_spread(
+// ------------------------------------------------------------------------------------------------
+// spread
+// ------------------------------------------------------------------------------------------------
+template <int THREADS, int MINW, bool PREFETCH>
+__global__ __launch_bounds__(THREADS, MINW) void k_spread(
     const uint16_t* __restrict__ meta, const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
     const int* __restrict__ tile_off, const double* __restrict__ x, int n, int B, int nblocks, int ngroups, int CG,
     int nw, double* __restrict__ part)
@@ -80,26 +81,26 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
    const int tid = threadIdx.x;
    const int lane = tid & 63;
    const int wave = tid >> 6;
-   const int nwaves = kSpreadThreads / 64;
+   constexpr int nwaves = THREADS / 64;
    const int c0 = g * CG;
    const int t0 = tile_off[b * ngroups + g];
    const int t1 = tile_off[b * ngroups + g + 1];
 
-   // issue the first tile's loads before the alpha staging so both are in flight together
+   // issue the first run's loads before the alpha staging so both are in flight together
    TileRegs cur;
    int t = t0 + wave;
    if (t < t1) load_tile(cur, meta, perm2, qarr, t, lane);
 
    const int base = b * B;
    const int nloc = min(B, n - base);
-   for (int i = tid; i < Bp; i += kSpreadThreads) s_alpha[i] = (i < nloc) ? x[base + i] : 0.0;
-   for (int i = tid; i < CG * kNos * kMomStride; i += kSpreadThreads) s_mom[i] = 0.0;
+   for (int i = tid; i < Bp; i += THREADS) s_alpha[i] = (i < nloc) ? x[base + i] : 0.0;
+   for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
    __syncthreads();
 
    for (; t < t1; t += nwaves) {
       TileRegs nxt;
       const int tn = t + nwaves;
-      if (tn < t1) load_tile(nxt, meta, perm2, qarr, tn, lane);  // prefetch the next tile
+      if (PREFETCH && tn < t1) load_tile(nxt, meta, perm2, qarr, tn, lane);  // prefetch the next run
       double acc[kNC];
 #pragma unroll
       for (int d = 0; d < kNC; d++) acc[d] = 0.0;
@@ -120,14 +121,18 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
       double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
 #pragma unroll
       for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
-      if (tn < t1) cur = nxt;
+      if (PREFETCH) {
+         if (tn < t1) cur = nxt;
+      } else if (tn < t1) {
+         load_tile(cur, meta, perm2, qarr, tn, lane);
+      }
    }
    __syncthreads();
 
-   // fold moments into the 64-cell partial grid of every component of this group:
+   // fold moments into the 64-cell partial grid of every window of this group:
    //   g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
    const int ncomp = min(CG, nw - c0);
-   for (int idx = tid; idx < ncomp * kNos; idx += kSpreadThreads) {
+   for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
       const int cl = idx / kNos;
       const int gi = idx % kNos;
       double v = 0.0;
@@ -137,7 +142,7 @@ __global__ __launch_bounds__(kSpreadThreads) void k_spread(
 #pragma unroll
          for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
       }
-      part[((size_t)b * nw + c0 + cl) * kNos + gi] = v;
+      part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
    }
 }
 
@@ -168,7 +173,8 @@ __device__ void grid_tail(int comp, const double* __restrict__ s_g, const double
    __syncthreads();
 }
 
-__global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict__ part, int nparts, int nw,
+// part: [nw][nparts][64] (from_sum = 0) or the summed grids [nw][64] (from_sum = 1)
+__global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict__ part, int nparts,
                                                       const double* __restrict__ w, const double* __restrict__ wd,
                                                       double* __restrict__ H, double* __restrict__ Hd, int grad,
                                                       int from_sum)
@@ -182,22 +188,21 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
    if (from_sum) {
       if (tid < kNos) s_g[tid] = part[(size_t)comp * kNos + tid];
    } else {
-      // kGridThreads/64 strands per cell over the partial grids, 4 independent accumulators each;
-      // fixed order -> deterministic
+      // 16 strands per cell over this window's contiguous partial grids; 4 independent accumulators
+      // per strand keep loads in flight; fixed order -> deterministic
       const int cell = tid & 63;
       const int strand = tid >> 6;
-      const int nstr = kGridThreads / 64;
+      constexpr int nstr = kGridThreads / 64;
+      const double* src = part + (size_t)comp * nparts * kNos + cell;
       double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
       int p = strand;
-      const size_t stride = (size_t)nw * kNos;
-      const double* src = part + (size_t)comp * kNos + cell;
       for (; p + 3 * nstr < nparts; p += 4 * nstr) {
-         s0 += src[(size_t)p * stride];
-         s1 += src[(size_t)(p + nstr) * stride];
-         s2 += src[(size_t)(p + 2 * nstr) * stride];
-         s3 += src[(size_t)(p + 3 * nstr) * stride];
+         s0 += src[(size_t)p * kNos];
+         s1 += src[(size_t)(p + nstr) * kNos];
+         s2 += src[(size_t)(p + 2 * nstr) * kNos];
+         s3 += src[(size_t)(p + 3 * nstr) * kNos];
       }
-      for (; p < nparts; p += nstr) s0 += src[(size_t)p * stride];
+      for (; p < nparts; p += nstr) s0 += src[(size_t)p * kNos];
       s_red[tid] = (s0 + s1) + (s2 + s3);
       __syncthreads();
       if (tid < kNos) {
@@ -211,22 +216,24 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
    if (grad) grid_tail(comp, s_g, wd, Hd, s_w, s_h);
 }
 
-__global__ __launch_bounds__(kGridThreads) void k_reduce_parts(const double* __restrict__ part, int nparts, int nw,
-                                                              double* __restrict__ gsum)
+// gsum[comp][cell] = sum_b part[comp][b][cell]   (row-sharded path: before the all-reduce)
+__global__ __launch_bounds__(256) void k_reduce_parts(const double* __restrict__ part, int nparts, int nw,
+                                                     double* __restrict__ gsum)
 {
-   // one thread per (comp, cell)
    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
    if (idx >= nw * kNos) return;
+   const int comp = idx / kNos, cell = idx % kNos;
+   const double* src = part + (size_t)comp * nparts * kNos + cell;
    double s = 0.0;
-   for (int p = 0; p < nparts; p++) s += part[(size_t)p * nw * kNos + idx];
+   for (int p = 0; p < nparts; p++) s += src[(size_t)p * kNos];
    gsum[idx] = s;
 }
 
 // ------------------------------------------------------------------------------------------------
 // interpolation + epilogue
 // ------------------------------------------------------------------------------------------------
-template <bool GRAD>
-__global__ __launch_bounds__(kInterpThreads) void k_interp(
+template <bool GRAD, int THREADS, bool PREFETCH>
+__global__ __launch_bounds__(THREADS) void k_interp(
     const uint16_t* __restrict__ meta, const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
     const int* __restrict__ tile_off, const double* __restrict__ H, const double* __restrict__ Hd,
     const double* __restrict__ x, double* __restrict__ y, int n, int B, int ngroups, double alpha, double beta,
@@ -240,28 +247,25 @@ __global__ __launch_bounds__(kInterpThreads) void k_interp(
    const int tid = threadIdx.x;
    const int base = b * B;
    const int nloc = min(B, n - base);
-   for (int i = tid; i < Bp; i += kInterpThreads) {
-      s_y[i] = 0.0;
-      if (GRAD) s_yd[i] = 0.0;
-   }
-   __syncthreads();
-
    const int lane = tid & 63;
    const int wave = tid >> 6;
-   const int nwaves = kInterpThreads / 64;
+   constexpr int nwaves = THREADS / 64;
    const int t0 = tile_off[b * ngroups];
    const int t1 = tile_off[(b + 1) * ngroups];
    TileRegs cur;
    int t = t0 + wave;
    if (t < t1) load_tile(cur, meta, perm2, qarr, t, lane);
+   for (int i = tid; i < Bp; i += THREADS) {
+      s_y[i] = 0.0;
+      if (GRAD) s_yd[i] = 0.0;
+   }
+   __syncthreads();
+
    for (; t < t1; t += nwaves) {
       TileRegs nxt;
       const int tn = t + nwaves;
-      if (tn < t1) load_tile(nxt, meta, perm2, qarr, tn, lane);  // prefetch the next tile
-      const uint32_t mt = cur.mt;
-      const uint32_t* pp = cur.pp;
-      const uint32_t* qq = cur.qq;
-      const size_t hoff = (size_t)mt * kNC;  // (comp*64 + cell) * kNC: meta is comp<<6|cell
+      if (PREFETCH && tn < t1) load_tile(nxt, meta, perm2, qarr, tn, lane);  // prefetch the next run
+      const size_t hoff = (size_t)cur.mt * kNC;  // (comp*64 + cell) * kNC: meta is comp<<6|cell
       double hc[kNC], hdc[GRAD ? kNC : 1];
 #pragma unroll
       for (int d = 0; d < kNC; d += 2) {
@@ -276,8 +280,8 @@ __global__ __launch_bounds__(kInterpThreads) void k_interp(
       }
 #pragma unroll
       for (int r = 0; r < kR; r++) {
-         const uint32_t loc = (r & 1) ? (pp[r >> 1] >> 16) : (pp[r >> 1] & 0xFFFFu);
-         const double u = q_to_u(qq[r]);
+         const uint32_t loc = (r & 1) ? (cur.pp[r >> 1] >> 16) : (cur.pp[r >> 1] & 0xFFFFu);
+         const double u = q_to_u(cur.qq[r]);
          double v = hc[kNC - 1];
 #pragma unroll
          for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
@@ -289,19 +293,23 @@ __global__ __launch_bounds__(kInterpThreads) void k_interp(
             atomicAdd(s_yd + loc, vd);
          }
       }
-      if (tn < t1) cur = nxt;
+      if (PREFETCH) {
+         if (tn < t1) cur = nxt;
+      } else if (tn < t1) {
+         load_tile(cur, meta, perm2, qarr, tn, lane);
+      }
    }
    __syncthreads();
 
    const double ff = f * f;
-   for (int j = tid; j < nloc; j += kInterpThreads) {
+   for (int j = tid; j < nloc; j += THREADS) {
       const size_t gj = (size_t)base + j;
       const double xj = x[gj];
       if (!GRAD) {
          const double v = ff * (s_y[j] + mu * xj);
          y[gj] = (beta == 0.0) ? alpha * v : fma(beta, y[gj], alpha * v);
       } else {
-         // nfft_interface.c:547-549 summed over components: (2f)(Kx + mu x), ff*dscale*K'x, ff*x
+         // nfft_interface.c:547-549 summed over windows: (2f)(Kx + mu x), ff*dscale*K'x, ff*x
          const double v0 = 2.0 * f * (s_y[j] + mu * xj);
          const double v1 = ff * s_yd[j];
          const double v2 = ff * xj;
@@ -336,14 +344,6 @@ static size_t interp_lds_bytes(const AdditivePlan& P, int grad)
    return sizeof(double) * (size_t)Bp * (grad ? 2 : 1);
 }
 
-static void raise_lds_limit(const void* fn, size_t bytes)
-{
-   if (bytes > 64 * 1024) {
-      (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-      (void)hipGetLastError();
-   }
-}
-
 int upload_tap_coeffs()
 {
    // constant memory is per device: upload once per device this process uses
@@ -359,17 +359,59 @@ int upload_tap_coeffs()
    return 0;
 }
 
+typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, int, int, int,
+                         int, int, int, double*);
+struct SpreadVariant {
+   SpreadFn fn;
+   int threads;
+};
+static const SpreadVariant kSpreadVariants[] = {
+    {k_spread<512, 1, true>, 512},   // 0: 8 waves, next-run prefetch
+    {k_spread<512, 1, false>, 512},  // 1: 8 waves, no prefetch
+    {k_spread<256, 1, true>, 256},   // 2: 4 waves, prefetch
+    {k_spread<512, 3, false>, 512},  // 3: 8 waves, >= 3 waves/SIMD register budget, no prefetch
+    {k_spread<1024, 1, false>, 1024},  // 4: 16 waves, no prefetch
+};
+constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
+
+typedef void (*InterpFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*,
+                         const double*, const double*, double*, int, int, int, double, double, double, double);
+struct InterpVariant {
+   InterpFn fn, fn_grad;
+   int threads;
+};
+static const InterpVariant kInterpVariants[] = {
+    {k_interp<false, 1024, true>, k_interp<true, 1024, true>, 1024},  // 0
+    {k_interp<false, 1024, false>, k_interp<true, 1024, false>, 1024},  // 1
+    {k_interp<false, 512, true>, k_interp<true, 512, true>, 512},  // 2
+};
+constexpr int kNumInterpVariants = sizeof(kInterpVariants) / sizeof(kInterpVariants[0]);
+
+static void raise_lds_limit_once()
+{
+   static bool raised = false;
+   if (raised) return;
+   for (int i = 0; i < kNumSpreadVariants; i++)
+      (void)hipFuncSetAttribute((const void*)kSpreadVariants[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+   for (int i = 0; i < kNumInterpVariants; i++) {
+      (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn_grad,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+   }
+   (void)hipGetLastError();
+   raised = true;
+}
+
 int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream)
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
+   raise_lds_limit_once();
+   const SpreadVariant& V = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
    const size_t lds = spread_lds_bytes(P);
-   static bool raised = false;
-   if (!raised) {
-      raise_lds_limit((const void*)k_spread, 160 * 1024);
-      raised = true;
-   }
    const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
-   hipLaunchKernelGGL(k_spread, dim3(gridx), dim3(kSpreadThreads), lds, stream, P.dl.meta, P.dl.perm2, P.dl.q,
+   hipLaunchKernelGGL(V.fn, dim3(gridx), dim3(V.threads), lds, stream, P.dl.meta, P.dl.perm2, P.dl.q,
                       P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
@@ -377,16 +419,16 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream)
 {
-   hipLaunchKernelGGL(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, d_part, nparts, P.nw, P.d_w, P.d_wd,
-                      P.d_H, P.d_Hd, grad, 0);
+   hipLaunchKernelGGL(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, d_part, nparts, P.d_w, P.d_wd, P.d_H,
+                      P.d_Hd, grad, 0);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
 
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream)
 {
-   hipLaunchKernelGGL(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, d_gridsum, 1, P.nw, P.d_w, P.d_wd,
-                      P.d_H, P.d_Hd, grad, 1);
+   hipLaunchKernelGGL(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, d_gridsum, 1, P.d_w, P.d_wd, P.d_H,
+                      P.d_Hd, grad, 1);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -394,8 +436,8 @@ int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int gra
 int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream)
 {
    const int total = P.nw * kNos;
-   hipLaunchKernelGGL(k_reduce_parts, dim3((total + kGridThreads - 1) / kGridThreads), dim3(kGridThreads), 0,
-                      stream, d_part, P.nblocks, P.nw, d_gridsum);
+   hipLaunchKernelGGL(k_reduce_parts, dim3((total + 255) / 256), dim3(256), 0, stream, d_part, P.nblocks, P.nw,
+                      d_gridsum);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -404,21 +446,11 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
                   hipStream_t stream)
 {
    if (P.n == 0) return 0;
+   raise_lds_limit_once();
+   const InterpVariant& V = kInterpVariants[std::min(std::max(P.interp_variant, 0), kNumInterpVariants - 1)];
    const size_t lds = interp_lds_bytes(P, grad);
-   static bool raised = false;
-   if (!raised) {
-      raise_lds_limit((const void*)k_interp<false>, 160 * 1024);
-      raise_lds_limit((const void*)k_interp<true>, 160 * 1024);
-      raised = true;
-   }
-   if (grad)
-      hipLaunchKernelGGL(k_interp<true>, dim3(P.nblocks), dim3(kInterpThreads), lds, stream, P.dl.meta, P.dl.perm2,
-                         P.dl.q, P.dl.tile_off, P.d_H, P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups, alpha, beta, P.f,
-                         P.mu);
-   else
-      hipLaunchKernelGGL(k_interp<false>, dim3(P.nblocks), dim3(kInterpThreads), lds, stream, P.dl.meta,
-                         P.dl.perm2, P.dl.q, P.dl.tile_off, P.d_H, P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups, alpha,
-                         beta, P.f, P.mu);
+   hipLaunchKernelGGL(grad ? V.fn_grad : V.fn, dim3(P.nblocks), dim3(V.threads), lds, stream, P.dl.meta, P.dl.perm2,
+                      P.dl.q, P.dl.tile_off, P.d_H, P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups, alpha, beta, P.f, P.mu);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

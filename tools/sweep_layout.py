@@ -1,6 +1,6 @@
-"""Sweep layout knobs (block size B, components per spread group CG) for the config-C matvec.
-Each setting runs in a fresh subprocess (env vars are read at handle creation)."""
-import json
+"""Sweep layout knobs (block size B, windows per spread group CG) and kernel variants for the config-C
+matvec.  Each setting runs in a fresh subprocess (env vars are read at handle creation).
+usage: python tools/sweep_layout.py "B,CG,SV,IV" ..."""
 import os
 import subprocess
 import sys
@@ -19,13 +19,14 @@ for _ in range(10): op.matsymv(xd, 1.0, 0.0, yd)
 torch.cuda.synchronize(); op.timing(True); t = time.perf_counter()
 for _ in range(100): op.matsymv(xd, 1.0, 0.0, yd)
 torch.cuda.synchronize(); el = time.perf_counter() - t
-tq = op.timing_query(); info = op.layout_info()
-print(json.dumps({"ms": el * 10, "spread": tq["spread"][0] / tq["spread"][1], "grid": tq["grid"][0] / tq["grid"][1],
-                  "interp": tq["interp"][0] / tq["interp"][1], "slots": info["slots"], "tiles": info["ntiles"]}))
+tq = op.timing_query()
+print(json.dumps({"ms": round(el * 10, 4), **{k: round(v[0] / v[1], 4) for k, v in tq.items()}}))
 ''' % ROOT
-for B in [2048, 4096, 8192]:
-    for CG in [2, 4, 8, 16]:
-        env = dict(os.environ, NFFT4GP_AMD_BLOCK=str(B), NFFT4GP_AMD_CG=str(CG))
-        r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
-        line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr[-300:]
-        print(f"B={B} CG={CG} {line}", flush=True)
+configs = sys.argv[1:] or ["4096,4,0,0"]
+for cfg in configs:
+    B, CG, SV, IV = cfg.split(",")
+    env = dict(os.environ, NFFT4GP_AMD_BLOCK=B, NFFT4GP_AMD_CG=CG, NFFT4GP_AMD_SPREAD_VARIANT=SV,
+               NFFT4GP_AMD_INTERP_VARIANT=IV)
+    r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
+    line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr[-300:]
+    print(f"B={B} CG={CG} SV={SV} IV={IV} {line}", flush=True)
