@@ -59,7 +59,7 @@ __device__ __forceinline__ void load_tile(TileRegs& T, const uint16_t* __restric
 // ------------------------------------------------------------------------------------------------
 // spread
 // ------------------------------------------------------------------------------------------------
-template <int THREADS, int MINW, bool PREFETCH>
+template <int THREADS, int MINW, bool PREFETCH, int ABL = 0, bool CONTIG = false>
 __global__ __launch_bounds__(THREADS, MINW) void k_spread(
     const uint16_t* __restrict__ meta, const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
     const int* __restrict__ tile_off, const double* __restrict__ x, int n, int B, int nblocks, int ngroups, int CG,
@@ -86,6 +86,57 @@ __global__ __launch_bounds__(THREADS, MINW) void k_spread(
    const int t0 = tile_off[b * ngroups + g];
    const int t1 = tile_off[b * ngroups + g + 1];
 
+   if (CONTIG) {
+      // each wave takes a contiguous range of the group's tiles; with the column-dealt layout a lane
+      // then walks CONSECUTIVE chunks of the sorted (window, cell) list, keeps its moments in registers
+      // while the key stays the same and flushes to LDS only when the key changes
+      const int T = t1 - t0;
+      const int ta = t0 + (int)(((long long)wave * T) / nwaves);
+      const int tb = t0 + (int)(((long long)(wave + 1) * T) / nwaves);
+      TileRegs cur;
+      if (ta < tb) load_tile(cur, meta, perm2, qarr, ta, lane);
+      const int base = b * B;
+      const int nloc = min(B, n - base);
+      for (int i = tid; i < Bp; i += THREADS) s_alpha[i] = (i < nloc) ? x[base + i] : 0.0;
+      for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
+      __syncthreads();
+      double acc[kNC];
+#pragma unroll
+      for (int d = 0; d < kNC; d++) acc[d] = 0.0;
+      uint32_t key = (ta < tb) ? cur.mt : 0u;
+      for (int t = ta; t < tb; t++) {
+         TileRegs nxt;
+         if (t + 1 < tb) load_tile(nxt, meta, perm2, qarr, t + 1, lane);  // prefetch the next run
+         if (cur.mt != key) {  // divergent: only lanes whose (window, cell) changed flush
+            double* dst = s_mom + ((int)(key >> 6) - c0) * kNos * kMomStride + (int)(key & 63u) * kMomStride;
+#pragma unroll
+            for (int d = 0; d < kNC; d++) {
+               atomicAdd(dst + d, acc[d]);
+               acc[d] = 0.0;
+            }
+            key = cur.mt;
+         }
+#pragma unroll
+         for (int r = 0; r < kR; r++) {
+            const uint32_t loc = (r & 1) ? (cur.pp[r >> 1] >> 16) : (cur.pp[r >> 1] & 0xFFFFu);
+            const double u = q_to_u(cur.qq[r]);
+            double tpow = s_alpha[loc];
+            acc[0] += tpow;
+#pragma unroll
+            for (int d = 1; d < kNC; d++) {
+               tpow *= u;
+               acc[d] += tpow;
+            }
+         }
+         if (t + 1 < tb) cur = nxt;
+      }
+      if (ta < tb) {
+         double* dst = s_mom + ((int)(key >> 6) - c0) * kNos * kMomStride + (int)(key & 63u) * kMomStride;
+#pragma unroll
+         for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);
+      }
+      __syncthreads();
+   } else {
    // issue the first run's loads before the alpha staging so both are in flight together
    TileRegs cur;
    int t = t0 + wave;
@@ -108,19 +159,28 @@ __global__ __launch_bounds__(THREADS, MINW) void k_spread(
       for (int r = 0; r < kR; r++) {
          const uint32_t loc = (r & 1) ? (cur.pp[r >> 1] >> 16) : (cur.pp[r >> 1] & 0xFFFFu);
          const double u = q_to_u(cur.qq[r]);
-         double tpow = s_alpha[loc];
+         // ABL (timing experiments only, wrong results): 1 = no alpha gather, 2 = no moment powers
+         double tpow = (ABL == 1) ? (double)loc : s_alpha[loc];
          acc[0] += tpow;
+         if (ABL == 2) {
+            acc[1] += u;
+         } else {
 #pragma unroll
-         for (int d = 1; d < kNC; d++) {
-            tpow *= u;
-            acc[d] += tpow;
+            for (int d = 1; d < kNC; d++) {
+               tpow *= u;
+               acc[d] += tpow;
+            }
          }
       }
       const int comp_local = (int)(cur.mt >> 6) - c0;
       const int cell = (int)(cur.mt & 63u);
       double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
+      if (ABL == 3) {  // no flush atomics: one plain store
+         if (acc[0] == 12345.0) dst[0] = acc[1] + acc[11];
+      } else {
 #pragma unroll
-      for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
+         for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
+      }
       if (PREFETCH) {
          if (tn < t1) cur = nxt;
       } else if (tn < t1) {
@@ -128,6 +188,7 @@ __global__ __launch_bounds__(THREADS, MINW) void k_spread(
       }
    }
    __syncthreads();
+   }
 
    // fold moments into the 64-cell partial grid of every window of this group:
    //   g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
@@ -232,7 +293,7 @@ __global__ __launch_bounds__(256) void k_reduce_parts(const double* __restrict__
 // ------------------------------------------------------------------------------------------------
 // interpolation + epilogue
 // ------------------------------------------------------------------------------------------------
-template <bool GRAD, int THREADS, bool PREFETCH>
+template <bool GRAD, int THREADS, bool PREFETCH, int ABL = 0>
 __global__ __launch_bounds__(THREADS) void k_interp(
     const uint16_t* __restrict__ meta, const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
     const int* __restrict__ tile_off, const double* __restrict__ H, const double* __restrict__ Hd,
@@ -283,9 +344,17 @@ __global__ __launch_bounds__(THREADS) void k_interp(
          const uint32_t loc = (r & 1) ? (cur.pp[r >> 1] >> 16) : (cur.pp[r >> 1] & 0xFFFFu);
          const double u = q_to_u(cur.qq[r]);
          double v = hc[kNC - 1];
+         if (ABL == 1) {
+            v = u;
+         } else {
 #pragma unroll
-         for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
-         atomicAdd(s_y + loc, v);
+            for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
+         }
+         if (ABL == 2) {
+            if (v == 12345.0) s_y[loc] = v;
+         } else {
+            atomicAdd(s_y + loc, v);
+         }
          if (GRAD) {
             double vd = hdc[kNC - 1];
 #pragma unroll
@@ -371,6 +440,14 @@ static const SpreadVariant kSpreadVariants[] = {
     {k_spread<256, 1, true>, 256},   // 2: 4 waves, prefetch
     {k_spread<512, 3, false>, 512},  // 3: 8 waves, >= 3 waves/SIMD register budget, no prefetch
     {k_spread<1024, 1, false>, 1024},  // 4: 16 waves, no prefetch
+    // ablations for timing experiments only (WRONG results): 5 no alpha gather, 6 no powers, 7 no flush
+    {k_spread<512, 1, false, 1>, 512},
+    {k_spread<512, 1, false, 2>, 512},
+    {k_spread<512, 1, false, 3>, 512},
+    // contiguous wave ranges + flush on key change: 8 contig 512 thr, 9 contig 256 thr, 10 contig 1024 thr
+    {k_spread<512, 1, true, 0, true>, 512},
+    {k_spread<256, 1, true, 0, true>, 256},
+    {k_spread<1024, 1, true, 0, true>, 1024},
 };
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
@@ -384,6 +461,9 @@ static const InterpVariant kInterpVariants[] = {
     {k_interp<false, 1024, true>, k_interp<true, 1024, true>, 1024},  // 0
     {k_interp<false, 1024, false>, k_interp<true, 1024, false>, 1024},  // 1
     {k_interp<false, 512, true>, k_interp<true, 512, true>, 512},  // 2
+    // ablations (WRONG results): 3 no H gather/Horner, 4 no LDS atomics
+    {k_interp<false, 1024, false, 1>, k_interp<true, 1024, false, 1>, 1024},
+    {k_interp<false, 1024, false, 2>, k_interp<true, 1024, false, 2>, 1024},
 };
 constexpr int kNumInterpVariants = sizeof(kInterpVariants) / sizeof(kInterpVariants[0]);
 
