@@ -155,6 +155,46 @@ __global__ __launch_bounds__(THREADS, MINW) void k_spread(
       double acc[kNC];
 #pragma unroll
       for (int d = 0; d < kNC; d++) acc[d] = 0.0;
+      if (ABL == 4) {
+         // mixed precision: moments d <= 5 in fp64; d = 6..11 (<= 2.4e-4 of the window peak in the taps,
+         // so fp32 rounding contributes ~1e-11 relative) as packed fp32 on point pairs; all 16 alpha
+         // gathers are issued before the arithmetic
+         double a[kR];
+#pragma unroll
+         for (int r = 0; r < kR; r++) {
+            const uint32_t loc = (r & 1) ? (cur.pp[r >> 1] >> 16) : (cur.pp[r >> 1] & 0xFFFFu);
+            a[r] = s_alpha[loc];
+         }
+         typedef float f2 __attribute__((ext_vector_type(2)));
+         f2 hi[kNC - 6];
+#pragma unroll
+         for (int d = 0; d < kNC - 6; d++) hi[d] = f2{0.f, 0.f};
+#pragma unroll
+         for (int r = 0; r < kR; r += 2) {
+            const double u0 = q_to_u(cur.qq[r]);
+            const double u1 = q_to_u(cur.qq[r + 1]);
+            double p0 = a[r], p1 = a[r + 1];
+            acc[0] += p0;
+            acc[0] += p1;
+#pragma unroll
+            for (int d = 1; d < 6; d++) {
+               p0 *= u0;
+               p1 *= u1;
+               acc[d] += p0;
+               acc[d] += p1;
+            }
+            f2 tp = f2{(float)(p0 * u0), (float)(p1 * u1)};
+            const f2 uu = f2{(float)u0, (float)u1};
+            hi[0] += tp;
+#pragma unroll
+            for (int d = 1; d < kNC - 6; d++) {
+               tp *= uu;
+               hi[d] += tp;
+            }
+         }
+#pragma unroll
+         for (int d = 0; d < kNC - 6; d++) acc[6 + d] = (double)hi[d].x + (double)hi[d].y;
+      } else
 #pragma unroll
       for (int r = 0; r < kR; r++) {
          const uint32_t loc = (r & 1) ? (cur.pp[r >> 1] >> 16) : (cur.pp[r >> 1] & 0xFFFFu);
@@ -448,6 +488,9 @@ static const SpreadVariant kSpreadVariants[] = {
     {k_spread<512, 1, true, 0, true>, 512},
     {k_spread<256, 1, true, 0, true>, 256},
     {k_spread<1024, 1, true, 0, true>, 1024},
+    // 11/12: mixed-precision high moments + up-front alpha gathers (prefetch / no prefetch)
+    {k_spread<512, 1, true, 4>, 512},
+    {k_spread<512, 1, false, 4>, 512},
 };
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
