@@ -57,6 +57,12 @@ void bhat_1d(int kind, double c, double* bhat);
 void circulant_1d(const double* bhat, double weight, double* w);
 
 // ---- layout (layout.cpp) -----------------------------------------------------------------------
+// element index of word w (of nwords per lane) of `lane` in tile t: [t][w/4][lane][w%4]
+__host__ __device__ inline size_t quad_index(long long t, int w, int lane, int nwords)
+{
+   return (((size_t)t * (size_t)(nwords / 4) + (size_t)(w >> 2)) * kWave + (size_t)lane) * 4 + (size_t)(w & 3);
+}
+
 struct Layout {
    int n = 0;           // local points
    int nw = 0;          // components

@@ -8,11 +8,12 @@
 //   group g = components [g*CG, (g+1)*CG)
 //   chunk   = up to R points of ONE (component, cell), padded with dummies (local index B, which
 //             the kernels map to a zero alpha / a discarded output slot)
-//   tile    = 64 chunks, one per lane (dealt column-wise, see emit_block_group); stored lane-fastest
-//             so every load is coalesced:
-//               meta [tile][lane]            u16  comp << 6 | cell
-//               perm2[tile][r/2][lane]       u32  local index of points r and r+1 (16 bits each)
-//               q    [tile][r][lane]         u32  fixed-point x mod 1 (cell = q >> 26)
+//   tile    = 64 chunks, one per lane (dealt column-wise, see emit_block_group); a lane's words are
+//             grouped in 16-byte quads, quads lane-fastest, so each lane loads 16 B per instruction
+//             and a wave instruction reads 1 KiB contiguous (quad_index in internal.h):
+//               meta [tile][lane]              u16  comp << 6 | cell
+//               perm2[tile][r/8][lane][r/2%4]  u32  local index of points r and r+1 (16 bits each)
+//               q    [tile][r/4][lane][r%4]    u32  fixed-point x mod 1 (cell = q >> 26)
 //   tile_off[b*ngroups + g] = first tile of (b, g); the spread kernel gets one workgroup per (b, g),
 //   the interpolation kernel one workgroup per b (all groups).
 #include <algorithm>
@@ -48,8 +49,8 @@ long long emit_block_group(const std::vector<uint32_t>& qc, int n, int nw, int B
          for (int lane = 0; lane < kWave; lane++) {
             out->meta[tile * kWave + lane] = (uint16_t)(c0 << 6);
             for (int r2 = 0; r2 < kR / 2; r2++)
-               out->perm2[(tile * (kR / 2) + r2) * kWave + lane] = (uint32_t)B | ((uint32_t)B << 16);
-            for (int r = 0; r < kR; r++) out->q[(tile * kR + r) * kWave + lane] = 0u;
+               out->perm2[quad_index(tile, r2, lane, kR / 2)] = (uint32_t)B | ((uint32_t)B << 16);
+            for (int r = 0; r < kR; r++) out->q[quad_index(tile, r, lane, kR)] = 0u;
          }
    }
    long long nchunks = 0;
@@ -83,9 +84,9 @@ long long emit_block_group(const std::vector<uint32_t>& qc, int n, int nw, int B
                   }
                }
                for (int r2 = 0; r2 < kR / 2; r2++)
-                  out->perm2[(tile * (kR / 2) + r2) * kWave + lane] =
+                  out->perm2[quad_index(tile, r2, lane, kR / 2)] =
                       (uint32_t)loc[2 * r2] | ((uint32_t)loc[2 * r2 + 1] << 16);
-               for (int r = 0; r < kR; r++) out->q[(tile * kR + r) * kWave + lane] = qv[r];
+               for (int r = 0; r < kR; r++) out->q[quad_index(tile, r, lane, kR)] = qv[r];
             }
             nchunks++;
          }

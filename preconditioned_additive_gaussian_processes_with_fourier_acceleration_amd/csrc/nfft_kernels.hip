@@ -49,11 +49,26 @@ __device__ __forceinline__ void load_tile(TileRegs& T, const uint16_t* __restric
                                           const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
                                           int t, int lane)
 {
+   // 16 B per lane per load: perm2 quads [t][2][lane], q quads [t][4][lane] (layout.cpp)
    T.mt = meta[(size_t)t * 64 + lane];
+   const uint4* p4 = reinterpret_cast<const uint4*>(perm2) + (size_t)t * (kR / 8) * 64 + lane;
+   const uint4* q4 = reinterpret_cast<const uint4*>(qarr) + (size_t)t * (kR / 4) * 64 + lane;
 #pragma unroll
-   for (int r2 = 0; r2 < kR / 2; r2++) T.pp[r2] = perm2[((size_t)t * (kR / 2) + r2) * 64 + lane];
+   for (int k = 0; k < kR / 8; k++) {
+      const uint4 v = p4[k * 64];
+      T.pp[4 * k + 0] = v.x;
+      T.pp[4 * k + 1] = v.y;
+      T.pp[4 * k + 2] = v.z;
+      T.pp[4 * k + 3] = v.w;
+   }
 #pragma unroll
-   for (int r = 0; r < kR; r++) T.qq[r] = qarr[((size_t)t * kR + r) * 64 + lane];
+   for (int k = 0; k < kR / 4; k++) {
+      const uint4 v = q4[k * 64];
+      T.qq[4 * k + 0] = v.x;
+      T.qq[4 * k + 1] = v.y;
+      T.qq[4 * k + 2] = v.z;
+      T.qq[4 * k + 3] = v.w;
+   }
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -53,12 +53,12 @@ def layout(qc, n, nw, B=4096, CG=8):
     toff = np.zeros(nblocks * ngroups + 1, np.int32)
     assert L.Nfft4GPAmdHostLayout(qc.ctypes.data, n, nw, B, CG, cnt, meta.ctypes.data, perm2.ctypes.data,
                                   q.ctypes.data, toff.ctypes.data) == 0
-    # unpack to [tile][lane][r]
-    p2 = perm2.reshape(ntiles, R // 2, 64)
+    # unpack the 16-byte-quad layout [tile][w/4][lane][w%4] (layout.cpp) to [tile][lane][w]
+    p2 = perm2.reshape(ntiles, R // 8, 64, 4).transpose(0, 2, 1, 3).reshape(ntiles, 64, R // 2)
     loc = np.empty((ntiles, 64, R), np.int64)
-    loc[:, :, 0::2] = (p2 & 0xFFFF).transpose(0, 2, 1)
-    loc[:, :, 1::2] = (p2 >> 16).transpose(0, 2, 1)
-    qq = q.reshape(ntiles, R, 64).transpose(0, 2, 1).astype(np.int64)
+    loc[:, :, 0::2] = p2 & 0xFFFF
+    loc[:, :, 1::2] = p2 >> 16
+    qq = q.reshape(ntiles, R // 4, 64, 4).transpose(0, 2, 1, 3).reshape(ntiles, 64, R).astype(np.int64)
     return dict(ntiles=ntiles, ngroups=ngroups, nblocks=nblocks, meta=meta.reshape(ntiles, 64).astype(np.int64),
                 loc=loc, q=qq, tile_off=toff, B=B, CG=CG)
 
