@@ -39,6 +39,17 @@ __device__ __forceinline__ double q_to_u(uint32_t q)
 // tap polynomial coefficients C[t][d] in constant memory: wave-uniform reads become scalar loads
 __constant__ double c_taps[kTaps * kNC];
 
+// diagnostic timeline (ABL == 5 builds only): per workgroup 4 s_memrealtime stamps (100 MHz)
+constexpr int kMaxStampWG = 16384;
+__device__ unsigned long long g_stamps[kMaxStampWG * 4];
+
+template <int ABL>
+__device__ __forceinline__ void stamp(int slot)
+{
+   if (ABL == 5 && threadIdx.x == 0 && blockIdx.x < kMaxStampWG)
+      g_stamps[blockIdx.x * 4 + slot] = __builtin_amdgcn_s_memrealtime();
+}
+
 struct TileRegs {
    uint32_t mt;
    uint32_t pp[kR / 2];
@@ -92,6 +103,7 @@ __global__ __launch_bounds__(THREADS, MINW) void k_spread(
    const int g = rest % ngroups;
    const int b = (rest / ngroups) * 8 + xcd;
    if (b >= nblocks) return;
+   stamp<ABL>(0);
 
    const int tid = threadIdx.x;
    const int lane = tid & 63;
@@ -162,6 +174,7 @@ __global__ __launch_bounds__(THREADS, MINW) void k_spread(
    for (int i = tid; i < Bp; i += THREADS) s_alpha[i] = (i < nloc) ? x[base + i] : 0.0;
    for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
    __syncthreads();
+   stamp<ABL>(1);
 
    for (; t < t1; t += nwaves) {
       TileRegs nxt;
@@ -244,6 +257,7 @@ __global__ __launch_bounds__(THREADS, MINW) void k_spread(
    }
    __syncthreads();
    }
+   stamp<ABL>(2);
 
    // fold moments into the 64-cell partial grid of every window of this group:
    //   g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
@@ -260,6 +274,19 @@ __global__ __launch_bounds__(THREADS, MINW) void k_spread(
       }
       part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
    }
+   if (ABL == 5) {
+      __syncthreads();
+      stamp<ABL>(3);
+   }
+}
+
+// copy the diagnostic timeline out (tools/ only)
+extern "C" int Nfft4GPAmdDebugStamps(unsigned long long* out, int nwg)
+{
+   if (nwg > kMaxStampWG) nwg = kMaxStampWG;
+   NFFT4GP_HIP_CHECK(hipDeviceSynchronize());
+   NFFT4GP_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 4 * nwg));
+   return nwg;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -506,6 +533,8 @@ static const SpreadVariant kSpreadVariants[] = {
     // 11/12: mixed-precision high moments + up-front alpha gathers (prefetch / no prefetch)
     {k_spread<512, 1, true, 4>, 512},
     {k_spread<512, 1, false, 4>, 512},
+    // 13: diagnostic timeline build of variant 1 (s_memrealtime stamps per workgroup)
+    {k_spread<512, 1, false, 5>, 512},
 };
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
