@@ -280,6 +280,154 @@ __global__ __launch_bounds__(THREADS, MINW) void k_spread(
    }
 }
 
+// ------------------------------------------------------------------------------------------------
+// persistent spread: a resident workgroup walks items (block, group) = it, it + G, it + 2G, ...
+// The next item's alpha slice is loaded into registers and its first runs into the tile registers
+// while the current item is processed, so the per-item prologue no longer waits on HBM; the fold uses
+// every thread with independent per-tap accumulators.
+// ------------------------------------------------------------------------------------------------
+template <int THREADS, int BMAX>
+__global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void k_spread_persist(
+    const uint16_t* __restrict__ meta, const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
+    const int* __restrict__ tile_off, const double* __restrict__ x, int n, int B, int nblocks, int ngroups, int CG,
+    int nw, double* __restrict__ part)
+{
+   extern __shared__ __attribute__((aligned(16))) double smem[];
+   constexpr int kPer = (BMAX + 2 + THREADS - 1) / THREADS;  // alpha values per thread (B + pad slot)
+   const int Bp = (B + 2) & ~1;
+   double* s_alpha = smem;
+   double* s_mom = smem + Bp;
+   const int tid = threadIdx.x;
+   const int lane = tid & 63;
+   const int wave = tid >> 6;
+   constexpr int nwaves = THREADS / 64;
+   const int nitems = ((nblocks + 7) / 8) * 8 * ngroups;
+   const int G = gridDim.x;
+
+   auto decode = [&](int it, int& b, int& g) {
+      const int xcd = it & 7;
+      const int rest = it >> 3;
+      g = rest % ngroups;
+      b = (rest / ngroups) * 8 + xcd;
+   };
+   auto next_valid = [&](int it) {
+      while (it < nitems) {
+         int bb, gg;
+         decode(it, bb, gg);
+         if (bb < nblocks) return it;
+         it += G;
+      }
+      return nitems;
+   };
+
+   int it = next_valid(blockIdx.x);
+   if (it >= nitems) return;
+   int b, g;
+   decode(it, b, g);
+   // prologue of the first item: alpha into registers, first run into tile registers
+   double areg[kPer];
+   auto load_alpha = [&](int bb) {
+      const int base = bb * B;
+      const int nloc = min(B, n - base);
+#pragma unroll
+      for (int k = 0; k < kPer; k++) {
+         const int i = tid + k * THREADS;
+         areg[k] = (i < nloc) ? x[base + i] : 0.0;
+      }
+   };
+   load_alpha(b);
+   TileRegs cur;
+   int t = tile_off[b * ngroups + g] + wave;
+   if (t < tile_off[b * ngroups + g + 1]) load_tile(cur, meta, perm2, qarr, t, lane);
+
+   while (true) {
+      const int c0 = g * CG;
+      const int t1 = tile_off[b * ngroups + g + 1];
+      // stage alpha, clear moments
+#pragma unroll
+      for (int k = 0; k < kPer; k++) {
+         const int i = tid + k * THREADS;
+         if (i < Bp) s_alpha[i] = areg[k];
+      }
+      for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
+      __syncthreads();
+      // next item: alpha loads in flight during this item's runs
+      const int it_next = next_valid(it + G);
+      int bn = 0, gn = 0;
+      if (it_next < nitems) {
+         decode(it_next, bn, gn);
+         load_alpha(bn);
+      }
+      const int tfirst_next = (it_next < nitems) ? tile_off[bn * ngroups + gn] + wave : 0;
+      const int tend_next = (it_next < nitems) ? tile_off[bn * ngroups + gn + 1] : 0;
+
+      for (; t < t1; t += nwaves) {
+         TileRegs nxt;
+         const int tn = t + nwaves;
+         // prefetch the next run: in this item, or the first run of the next item
+         const int tpre = (tn < t1) ? tn : tfirst_next;
+         const bool has_pre = (tn < t1) || (tfirst_next < tend_next);
+         if (has_pre) load_tile(nxt, meta, perm2, qarr, tpre, lane);
+         double acc[kNC];
+#pragma unroll
+         for (int d = 0; d < kNC; d++) acc[d] = 0.0;
+#pragma unroll
+         for (int r = 0; r < kR; r++) {
+            const uint32_t loc = (r & 1) ? (cur.pp[r >> 1] >> 16) : (cur.pp[r >> 1] & 0xFFFFu);
+            const double u = q_to_u(cur.qq[r]);
+            double tpow = s_alpha[loc];
+            acc[0] += tpow;
+#pragma unroll
+            for (int d = 1; d < kNC; d++) {
+               tpow *= u;
+               acc[d] += tpow;
+            }
+         }
+         double* dst = s_mom + (((int)(cur.mt >> 6) - c0) * kNos + (int)(cur.mt & 63u)) * kMomStride;
+#pragma unroll
+         for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
+         if (has_pre) cur = nxt;
+      }
+      // a wave whose run list of this item was empty still has to pick up the next item's first run
+      if (t == tile_off[b * ngroups + g] + wave && t >= t1 && tfirst_next < tend_next)
+         load_tile(cur, meta, perm2, qarr, tfirst_next, lane);
+      __syncthreads();
+
+      // fold: every thread, two partial sums of 5 taps each (independent chains), combined in LDS-free
+      // registers via the pair lane (tid ^ 1 holds the other half of the same output)
+      const int ncomp = min(CG, nw - c0);
+      for (int idx = tid; idx < 2 * ncomp * kNos; idx += THREADS) {
+         const int o = idx >> 1;
+         const int half = idx & 1;
+         const int cl = o / kNos;
+         const int gi = o % kNos;
+         // taps half*5 .. half*5+4; two interleaved accumulators (even / odd degree) per tap
+         double s = 0.0;
+#pragma unroll 1
+         for (int j = 0; j < 5; j++) {
+            const int tp = half * 5 + j;
+            const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
+            const double* crow = c_taps + tp * kNC;
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int d = 0; d < kNC; d += 2) {
+               a0 = fma(crow[d], mrow[d], a0);
+               a1 = fma(crow[d + 1], mrow[d + 1], a1);
+            }
+            s += a0 + a1;
+         }
+         s += __shfl_xor(s, 1, 64);
+         if (half == 0) part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = s;
+      }
+      if (it_next >= nitems) break;
+      __syncthreads();  // s_alpha / s_mom are overwritten by the next item
+      it = it_next;
+      b = bn;
+      g = gn;
+      t = tfirst_next;
+   }
+}
+
 // copy the diagnostic timeline out (tools/ only)
 extern "C" int Nfft4GPAmdDebugStamps(unsigned long long* out, int nwg)
 {
@@ -515,6 +663,7 @@ typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, cons
 struct SpreadVariant {
    SpreadFn fn;
    int threads;
+   int persistent_bmax = 0;  // > 0: persistent kernel for blocks up to this size
 };
 static const SpreadVariant kSpreadVariants[] = {
     {k_spread<512, 1, true>, 512},   // 0: 8 waves, next-run prefetch
@@ -535,6 +684,10 @@ static const SpreadVariant kSpreadVariants[] = {
     {k_spread<512, 1, false, 4>, 512},
     // 13: diagnostic timeline build of variant 1 (s_memrealtime stamps per workgroup)
     {k_spread<512, 1, false, 5>, 512},
+    // 14: persistent workgroups, next-item alpha/run prefetch (B <= 4096)
+    {k_spread_persist<512, 4096>, 512, 4096},
+    // 15: persistent, 256 threads
+    {k_spread_persist<256, 4096>, 256, 4096},
 };
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
@@ -577,7 +730,27 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
    raise_lds_limit_once();
    const SpreadVariant& V = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
    const size_t lds = spread_lds_bytes(P);
-   const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
+   int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
+   if (V.persistent_bmax > 0) {
+      if (P.B > V.persistent_bmax) {
+         fprintf(stderr, "nfft4gp_amd: block size %d exceeds the persistent spread kernel's %d\n", P.B,
+                 V.persistent_bmax);
+         return -1;
+      }
+      // resident workgroups: occupancy x CUs, a multiple of 8 (item -> XCD affinity), at most the items
+      static int cached_dev = -1, cached_cus = 0;
+      int dev = 0;
+      NFFT4GP_HIP_CHECK(hipGetDevice(&dev));
+      if (dev != cached_dev) {
+         NFFT4GP_HIP_CHECK(hipDeviceGetAttribute(&cached_cus, hipDeviceAttributeMultiprocessorCount, dev));
+         cached_dev = dev;
+      }
+      int per_cu = 0;
+      NFFT4GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)V.fn, V.threads, lds));
+      int G = std::max(1, per_cu) * cached_cus;
+      G = std::max(8, (G / 8) * 8);
+      gridx = std::min(gridx, G);
+   }
    hipLaunchKernelGGL(V.fn, dim3(gridx), dim3(V.threads), lds, stream, P.dl.meta, P.dl.perm2, P.dl.q,
                       P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part);
    NFFT4GP_HIP_CHECK(hipGetLastError());
