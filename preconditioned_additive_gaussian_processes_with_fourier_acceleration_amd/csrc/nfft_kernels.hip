@@ -428,6 +428,200 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void k_spread_persist(
    }
 }
 
+// ------------------------------------------------------------------------------------------------
+// three-deep register ring: every wave keeps its next TWO runs in flight while it computes one
+// (bytes in flight per CU, not VALU or LDS, bound the streaming rate of the one-deep kernels)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void spread_run(const TileRegs& T, const double* __restrict__ s_alpha,
+                                           double* __restrict__ s_mom, int c0)
+{
+   double acc[kNC];
+#pragma unroll
+   for (int d = 0; d < kNC; d++) acc[d] = 0.0;
+#pragma unroll
+   for (int r = 0; r < kR; r++) {
+      const uint32_t loc = (r & 1) ? (T.pp[r >> 1] >> 16) : (T.pp[r >> 1] & 0xFFFFu);
+      const double u = q_to_u(T.qq[r]);
+      double tpow = s_alpha[loc];
+      acc[0] += tpow;
+#pragma unroll
+      for (int d = 1; d < kNC; d++) {
+         tpow *= u;
+         acc[d] += tpow;
+      }
+   }
+   double* dst = s_mom + (((int)(T.mt >> 6) - c0) * kNos + (int)(T.mt & 63u)) * kMomStride;
+#pragma unroll
+   for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
+   // keep the scheduler from hoisting the next run's 16 LDS gathers above this one (register blow-up)
+   __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_spread3(
+    const uint16_t* __restrict__ meta, const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
+    const int* __restrict__ tile_off, const double* __restrict__ x, int n, int B, int nblocks, int ngroups, int CG,
+    int nw, double* __restrict__ part)
+{
+   extern __shared__ __attribute__((aligned(16))) double smem[];
+   const int Bp = (B + 2) & ~1;
+   double* s_alpha = smem;
+   double* s_mom = smem + Bp;
+   const int xcd = blockIdx.x & 7;
+   const int rest = blockIdx.x >> 3;
+   const int g = rest % ngroups;
+   const int b = (rest / ngroups) * 8 + xcd;
+   if (b >= nblocks) return;
+   const int tid = threadIdx.x;
+   const int lane = tid & 63;
+   const int wave = tid >> 6;
+   constexpr int nwv = THREADS / 64;
+   const int c0 = g * CG;
+   const int t1 = tile_off[b * ngroups + g + 1];
+   int t = tile_off[b * ngroups + g] + wave;
+   TileRegs A, Bq, Cq;
+   if (t < t1) load_tile(A, meta, perm2, qarr, t, lane);
+   if (t + nwv < t1) load_tile(Bq, meta, perm2, qarr, t + nwv, lane);
+   const int base = b * B;
+   const int nloc = min(B, n - base);
+   for (int i = tid; i < Bp; i += THREADS) s_alpha[i] = (i < nloc) ? x[base + i] : 0.0;
+   for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
+   __syncthreads();
+   while (true) {
+      if (t + 2 * nwv < t1) load_tile(Cq, meta, perm2, qarr, t + 2 * nwv, lane);
+      if (t >= t1) break;
+      spread_run(A, s_alpha, s_mom, c0);
+      t += nwv;
+      if (t + 2 * nwv < t1) load_tile(A, meta, perm2, qarr, t + 2 * nwv, lane);
+      if (t >= t1) break;
+      spread_run(Bq, s_alpha, s_mom, c0);
+      t += nwv;
+      if (t + 2 * nwv < t1) load_tile(Bq, meta, perm2, qarr, t + 2 * nwv, lane);
+      if (t >= t1) break;
+      spread_run(Cq, s_alpha, s_mom, c0);
+      t += nwv;
+   }
+   __syncthreads();
+   const int ncomp = min(CG, nw - c0);
+   for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
+      const int cl = idx / kNos;
+      const int gi = idx % kNos;
+      double v = 0.0;
+#pragma unroll 1
+      for (int tp = 0; tp < kTaps; tp++) {
+         const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
+#pragma unroll
+         for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
+      }
+      part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
+   }
+}
+
+template <bool GRAD>
+__device__ __forceinline__ void interp_run(const TileRegs& T, const double* __restrict__ H,
+                                           const double* __restrict__ Hd, double* __restrict__ s_y,
+                                           double* __restrict__ s_yd)
+{
+   const size_t hoff = (size_t)T.mt * kNC;  // (comp*64 + cell) * kNC
+   double hc[kNC], hdc[GRAD ? kNC : 1];
+#pragma unroll
+   for (int d = 0; d < kNC; d += 2) {
+      const double2 v = *reinterpret_cast<const double2*>(H + hoff + d);
+      hc[d] = v.x;
+      hc[d + 1] = v.y;
+      if (GRAD) {
+         const double2 vd = *reinterpret_cast<const double2*>(Hd + hoff + d);
+         hdc[d] = vd.x;
+         hdc[d + 1] = vd.y;
+      }
+   }
+#pragma unroll
+   for (int r = 0; r < kR; r++) {
+      const uint32_t loc = (r & 1) ? (T.pp[r >> 1] >> 16) : (T.pp[r >> 1] & 0xFFFFu);
+      const double u = q_to_u(T.qq[r]);
+      double v = hc[kNC - 1];
+#pragma unroll
+      for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
+      atomicAdd(s_y + loc, v);
+      if (GRAD) {
+         double vd = hdc[kNC - 1];
+#pragma unroll
+         for (int d = kNC - 2; d >= 0; d--) vd = fma(vd, u, hdc[d]);
+         atomicAdd(s_yd + loc, vd);
+      }
+   }
+}
+
+template <bool GRAD, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_interp3(
+    const uint16_t* __restrict__ meta, const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
+    const int* __restrict__ tile_off, const double* __restrict__ H, const double* __restrict__ Hd,
+    const double* __restrict__ x, double* __restrict__ y, int n, int B, int ngroups, double alpha, double beta,
+    double f, double mu)
+{
+   extern __shared__ __attribute__((aligned(16))) double smem[];
+   const int Bp = (B + 2) & ~1;
+   double* s_y = smem;
+   double* s_yd = smem + Bp;
+   const int b = blockIdx.x;
+   const int tid = threadIdx.x;
+   const int base = b * B;
+   const int nloc = min(B, n - base);
+   const int lane = tid & 63;
+   const int wave = tid >> 6;
+   constexpr int nwv = THREADS / 64;
+   const int t1 = tile_off[(b + 1) * ngroups];
+   int t = tile_off[b * ngroups] + wave;
+   TileRegs A, Bq, Cq;
+   if (t < t1) load_tile(A, meta, perm2, qarr, t, lane);
+   if (t + nwv < t1) load_tile(Bq, meta, perm2, qarr, t + nwv, lane);
+   for (int i = tid; i < Bp; i += THREADS) {
+      s_y[i] = 0.0;
+      if (GRAD) s_yd[i] = 0.0;
+   }
+   __syncthreads();
+   while (true) {
+      if (t + 2 * nwv < t1) load_tile(Cq, meta, perm2, qarr, t + 2 * nwv, lane);
+      if (t >= t1) break;
+      interp_run<GRAD>(A, H, Hd, s_y, s_yd);
+      t += nwv;
+      if (t + 2 * nwv < t1) load_tile(A, meta, perm2, qarr, t + 2 * nwv, lane);
+      if (t >= t1) break;
+      interp_run<GRAD>(Bq, H, Hd, s_y, s_yd);
+      t += nwv;
+      if (t + 2 * nwv < t1) load_tile(Bq, meta, perm2, qarr, t + 2 * nwv, lane);
+      if (t >= t1) break;
+      interp_run<GRAD>(Cq, H, Hd, s_y, s_yd);
+      t += nwv;
+   }
+   __syncthreads();
+   const double ff = f * f;
+   for (int j = tid; j < nloc; j += THREADS) {
+      const size_t gj = (size_t)base + j;
+      const double xj = x[gj];
+      if (!GRAD) {
+         const double v = ff * (s_y[j] + mu * xj);
+         y[gj] = (beta == 0.0) ? alpha * v : fma(beta, y[gj], alpha * v);
+      } else {
+         const double v0 = 2.0 * f * (s_y[j] + mu * xj);
+         const double v1 = ff * s_yd[j];
+         const double v2 = ff * xj;
+         double* y0 = y;
+         double* y1 = y + n;
+         double* y2 = y + 2 * (size_t)n;
+         if (beta == 0.0) {
+            y0[gj] = alpha * v0;
+            y1[gj] = alpha * v1;
+            y2[gj] = alpha * v2;
+         } else {
+            y0[gj] = fma(beta, y0[gj], alpha * v0);
+            y1[gj] = fma(beta, y1[gj], alpha * v1);
+            y2[gj] = fma(beta, y2[gj], alpha * v2);
+         }
+      }
+   }
+}
+
 // copy the diagnostic timeline out (tools/ only)
 extern "C" int Nfft4GPAmdDebugStamps(unsigned long long* out, int nwg)
 {
@@ -688,6 +882,9 @@ static const SpreadVariant kSpreadVariants[] = {
     {k_spread_persist<512, 4096>, 512, 4096},
     // 15: persistent, 256 threads
     {k_spread_persist<256, 4096>, 256, 4096},
+    // 16/17: three-deep run ring
+    {k_spread3<512>, 512},
+    {k_spread3<256>, 256},
 };
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
@@ -704,6 +901,9 @@ static const InterpVariant kInterpVariants[] = {
     // ablations (WRONG results): 3 no H gather/Horner, 4 no LDS atomics
     {k_interp<false, 1024, false, 1>, k_interp<true, 1024, false, 1>, 1024},
     {k_interp<false, 1024, false, 2>, k_interp<true, 1024, false, 2>, 1024},
+    // 5/6: three-deep run ring
+    {k_interp3<false, 1024>, k_interp3<true, 1024>, 1024},
+    {k_interp3<false, 512>, k_interp3<true, 512>, 512},
 };
 constexpr int kNumInterpVariants = sizeof(kInterpVariants) / sizeof(kInterpVariants[0]);
 
