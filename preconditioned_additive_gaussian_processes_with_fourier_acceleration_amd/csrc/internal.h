@@ -103,7 +103,9 @@ struct AdditivePlan {
    double weight = 1.0;  // 1/nwindows
    // layout
    int B = 4096, CG = 4, ngroups = 0, nblocks = 0;
-   int spread_variant = 0, interp_variant = 0;  // kernel shape variants (nfft_kernels.hip)
+   int spread_variant = 1, interp_variant = 1;  // kernel shape variants (nfft_kernels.hip)
+   bool fused = true;                           // grid step fused into the spread tail
+   unsigned int* d_tickets = nullptr;           // [ngroups] arrival tickets of the fused spread
    DevLayout dl;
    // device buffers
    double* d_part = nullptr;  // [nblocks][nw][64]
@@ -126,6 +128,8 @@ struct AdditivePlan {
 int upload_tap_coeffs();
 // launchers (nfft_kernels.hip); all enqueue on `stream`
 int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream);
+// spread + grid in one launch (uses d_grid as the self-clearing accumulator and d_tickets)
+int launch_spread_fused(const AdditivePlan& P, const double* d_x, int grad, hipStream_t stream);
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream);
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream);
 int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream);

@@ -453,8 +453,6 @@ __device__ __forceinline__ void spread_run(const TileRegs& T, const double* __re
    double* dst = s_mom + (((int)(T.mt >> 6) - c0) * kNos + (int)(T.mt & 63u)) * kMomStride;
 #pragma unroll
    for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
-   // keep the scheduler from hoisting the next run's 16 LDS gathers above this one (register blow-up)
-   __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int THREADS>
@@ -620,6 +618,138 @@ __global__ __launch_bounds__(THREADS) void k_interp3(
          }
       }
    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// spread with the grid step fused into its tail (default single-GPU path)
+//   every workgroup adds its 64-cell partial grids into gsum[comp][64] with memory-side fp64 atomics,
+//   then takes an arrival ticket for its window group; the LAST workgroup of the group reads the
+//   sums back with returning atomics (coherent across XCDs), applies the circulant, writes the
+//   interpolation polynomials H (and Hd), and clears gsum / the ticket for the next launch.
+//   Protocol per MI355X_MICROARCH.md "Workgroup dispatch ... visibility": every adding wave drains
+//   its atomics (s_waitcnt vmcnt(0)) before the workgroup barrier, one lane releases at agent scope
+//   and takes the ticket; the last arriver acquires before reading.
+// ------------------------------------------------------------------------------------------------
+__device__ void fused_grid_tail(int comp, const double* __restrict__ s_g, const double* __restrict__ w,
+                                double* __restrict__ H, double* s_w, double* s_h, int tid, int nthreads)
+{
+   // s_g: this component's summed grid (LDS); computes H[comp] with threads [0, nthreads)
+   if (tid < kNos) s_w[tid] = w[(size_t)comp * kNos + tid];
+   __syncthreads();
+   if (tid < kNos) {
+      double h = 0.0;
+#pragma unroll 8
+      for (int l2 = 0; l2 < kNos; l2++) h = fma(s_w[(tid - l2) & (kNos - 1)], s_g[l2], h);
+      s_h[tid] = h;
+   }
+   __syncthreads();
+   for (int idx = tid; idx < kNos * kNC; idx += nthreads) {
+      const int cell = idx / kNC;
+      const int d = idx % kNC;
+      double v = 0.0;
+#pragma unroll
+      for (int tp = 0; tp < kTaps; tp++) v = fma(s_h[(cell - kM + tp) & (kNos - 1)], c_taps[tp * kNC + d], v);
+      H[((size_t)comp * kNos + cell) * kNC + d] = v;
+   }
+   __syncthreads();
+}
+
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_spread_fused(
+    const uint16_t* __restrict__ meta, const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
+    const int* __restrict__ tile_off, const double* __restrict__ x, int n, int B, int nblocks, int ngroups, int CG,
+    int nw, double* __restrict__ gsum, unsigned int* __restrict__ tickets, const double* __restrict__ w,
+    const double* __restrict__ wd, double* __restrict__ H, double* __restrict__ Hd, int grad)
+{
+   extern __shared__ __attribute__((aligned(16))) double smem[];
+   __shared__ int s_last;
+   __shared__ double s_w[kNos], s_h[kNos];
+   const int Bp = (B + 2) & ~1;
+   double* s_alpha = smem;
+   double* s_mom = smem + Bp;
+   const int xcd = blockIdx.x & 7;
+   const int rest = blockIdx.x >> 3;
+   const int g = rest % ngroups;
+   const int b = (rest / ngroups) * 8 + xcd;
+   if (b >= nblocks) return;
+   const int tid = threadIdx.x;
+   const int lane = tid & 63;
+   const int wave = tid >> 6;
+   constexpr int nwaves = THREADS / 64;
+   const int c0 = g * CG;
+   const int t0 = tile_off[b * ngroups + g];
+   const int t1 = tile_off[b * ngroups + g + 1];
+   TileRegs cur;
+   int t = t0 + wave;
+   if (t < t1) load_tile(cur, meta, perm2, qarr, t, lane);
+   const int base = b * B;
+   const int nloc = min(B, n - base);
+   for (int i = tid; i < Bp; i += THREADS) s_alpha[i] = (i < nloc) ? x[base + i] : 0.0;
+   for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
+   __syncthreads();
+   for (; t < t1; t += nwaves) {
+      double acc[kNC];
+#pragma unroll
+      for (int d = 0; d < kNC; d++) acc[d] = 0.0;
+#pragma unroll
+      for (int r = 0; r < kR; r++) {
+         const uint32_t loc = (r & 1) ? (cur.pp[r >> 1] >> 16) : (cur.pp[r >> 1] & 0xFFFFu);
+         const double u = q_to_u(cur.qq[r]);
+         double tpow = s_alpha[loc];
+         acc[0] += tpow;
+#pragma unroll
+         for (int d = 1; d < kNC; d++) {
+            tpow *= u;
+            acc[d] += tpow;
+         }
+      }
+      double* dst = s_mom + (((int)(cur.mt >> 6) - c0) * kNos + (int)(cur.mt & 63u)) * kMomStride;
+#pragma unroll
+      for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
+      if (t + nwaves < t1) load_tile(cur, meta, perm2, qarr, t + nwaves, lane);
+   }
+   __syncthreads();
+
+   // fold into partial grids and add them to gsum (memory-side fp64 atomics, no return)
+   const int ncomp = min(CG, nw - c0);
+   for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
+      const int cl = idx / kNos;
+      const int gi = idx % kNos;
+      double v = 0.0;
+#pragma unroll 1
+      for (int tp = 0; tp < kTaps; tp++) {
+         const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
+#pragma unroll
+         for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
+      }
+      atomicAdd(gsum + (size_t)(c0 + cl) * kNos + gi, v);
+   }
+   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every adding wave drains its atomics
+   __syncthreads();
+   if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned old = __hip_atomic_fetch_add(tickets + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = (old == (unsigned)(nblocks - 1)) ? 1 : 0;
+   }
+   __syncthreads();
+   if (!s_last) return;
+   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+   __syncthreads();
+   // last arriver of group g: summed grids -> LDS (returning atomics read the memory-side value and
+   // clear it for the next launch), circulant, polynomials
+   double* s_g = s_mom;  // reuse: ncomp*64 doubles
+   for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
+      double* p = gsum + (size_t)c0 * kNos + idx;
+      s_g[idx] = __hip_atomic_exchange(p, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+   }
+   __syncthreads();
+   for (int cl = 0; cl < ncomp; cl++) {
+      fused_grid_tail(c0 + cl, s_g + cl * kNos, w, H, s_w, s_h, tid, THREADS);
+      if (grad) fused_grid_tail(c0 + cl, s_g + cl * kNos, wd, Hd, s_w, s_h, tid, THREADS);
+   }
+   if (tid == 0) __hip_atomic_store(tickets + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // copy the diagnostic timeline out (tools/ only)
@@ -953,6 +1083,26 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
    }
    hipLaunchKernelGGL(V.fn, dim3(gridx), dim3(V.threads), lds, stream, P.dl.meta, P.dl.perm2, P.dl.q,
                       P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int launch_spread_fused(const AdditivePlan& P, const double* d_x, int grad, hipStream_t stream)
+{
+   if (P.n == 0) return 0;
+   raise_lds_limit_once();
+   static bool raised = false;
+   if (!raised) {
+      (void)hipFuncSetAttribute((const void*)k_spread_fused<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      (void)hipGetLastError();
+      raised = true;
+   }
+   const size_t lds = spread_lds_bytes(P);
+   const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
+   hipLaunchKernelGGL(k_spread_fused<512>, dim3(gridx), dim3(512), lds, stream, P.dl.meta, P.dl.perm2, P.dl.q,
+                      P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, P.d_grid, P.d_tickets, P.d_w,
+                      P.d_wd, P.d_H, P.d_Hd, grad);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
