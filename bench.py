@@ -96,6 +96,66 @@ def cpu_baseline(n, d, X, x, max_seconds=25.0):
     }
 
 
+def kernel_only(n, d):
+    """Child mode for the PMC passes: setup + one matvec + a few launches of each kernel."""
+    import torch
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    X, x_host = make_problem(n, d)
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    assert op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) == 0
+    xd = torch.tensor(x_host, device="cuda")
+    yd = torch.zeros(n, dtype=torch.float64, device="cuda")
+    op.matsymv(xd, 1.0, 0.0, yd)
+    for k in op.KERNELS:
+        op.kernel_bench(k, xd, yd, reps=5)
+    torch.cuda.synchronize()
+
+
+def pmc_traffic(n, d, timeout=600):
+    """HBM bytes per launch of k_spread / k_interp from rocprofv3 PMC counters, one counter per pass
+    (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass), on a child process running --kernel-only.
+    FETCH_SIZE is doubled (gfx950 tallies 128-B reads at 64 B, MI355X_MICROARCH.md 'HBM');
+    both counters are in KiB.  Returns {kernel: {"fetch": B, "write": B, "traffic": B}} or None."""
+    import csv
+    import shutil
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None
+    out = {}
+    base = os.path.join(ROOT, "gpurun_out", "bench_pmc")
+    env = dict(os.environ, TMPDIR="/tmp")
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d_out = os.path.join(base, counter.lower())
+        shutil.rmtree(d_out, ignore_errors=True)
+        cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", d_out, "-o", "pmc", "--",
+               sys.executable, os.path.abspath(__file__), "--kernel-only", "--n", str(n), "--d", str(d)]
+        r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=timeout)
+        if r.returncode != 0:
+            return None
+        path = os.path.join(d_out, "pmc_counter_collection.csv")
+        sums = {}
+        with open(path) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] != counter:
+                    continue
+                name = row["Kernel_Name"]
+                key = "spread" if "k_spread" in name else "interp" if "k_interp" in name else \
+                      "grid" if "k_grid" in name else None
+                if key is None:
+                    continue
+                s = sums.setdefault(key, [0.0, 0])
+                s[0] += float(row["Counter_Value"])
+                s[1] += 1
+        for key, (tot, cnt) in sums.items():
+            kib = tot / cnt
+            rec = out.setdefault(key, {})
+            rec["fetch" if counter == "FETCH_SIZE" else "write"] = \
+                kib * 1024 * (2 if counter == "FETCH_SIZE" else 1)
+    for rec in out.values():
+        rec["traffic"] = rec.get("fetch", 0.0) + rec.get("write", 0.0)
+    return out
+
+
 def run_pcg_single(op, torch, n, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1):
     """PCG to 1e-6 on the same points.  At l = 1 the NFFT-approximated kernel of this data is
     indefinite (bhat_k < 0 for a Gaussian truncated at r = 1/2; DESIGN.md 'SPD'), which is why the
@@ -124,7 +184,12 @@ def main():
     ap.add_argument("--d", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcg", action="store_true")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
+    ap.add_argument("--kernel-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.kernel_only:
+        kernel_only(args.n, args.d)
+        return
 
     import torch
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
@@ -173,8 +238,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if world == 1:
-        op.timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -207,16 +270,30 @@ def main():
                    "parallelism": f"rows{world}" if world > 1 else "single"},
     }
     if world == 1:
-        tq = op.timing_query()
-        op.timing(False)
+        # per-kernel durations: one hipEvent pair around `reps` back-to-back launches of each kernel
+        # on the library stream (the timed loop above carries no per-launch events: a pair costs
+        # several microseconds, ~5% of a matvec)
         info = op.layout_info()
         b_spread, b_interp = algorithmic_bytes(info, n, d)
-        avg = {k: (v[0] / max(v[1], 1)) for k, v in tq.items()}  # ms
+        reps = max(20, min(args.steps, 200))
+        avg = {k: op.kernel_bench(k, xd, yd, reps=reps) for k in op.KERNELS}  # ms
+        torch.cuda.synchronize()
         dom = "spread" if avg["spread"] >= avg["interp"] else "interp"
         bytes_dom = b_spread if dom == "spread" else b_interp
         achieved = bytes_dom / (avg[dom] * 1e-3) / 1e9
+        traffic = None
+        if not args.no_traffic:
+            try:
+                pmc = pmc_traffic(n, d)
+            except Exception as e:  # report, do not fail the GPU measurement
+                pmc = None
+                result["pmc_error"] = repr(e)
+            if pmc:
+                result["pmc_bytes_per_launch"] = pmc
+                traffic = pmc.get(dom, {}).get("traffic")
         result["roofline"] = {"bound": "hbm", "kernel": f"k_{dom}", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                              "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                              "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                              "traffic_unit": "bytes per launch (2 x FETCH_SIZE + WRITE_SIZE)",
                               "algorithmic_bytes_per_launch": bytes_dom,
                               "avg_launch_ms": avg[dom]}
         result["kernels_ms"] = avg

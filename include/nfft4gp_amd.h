@@ -170,6 +170,12 @@ int Nfft4GPAmdAdditiveLayoutInfo(void *str, long long *out, int nout);
  * ms[0..2] = spread, grid, interp;  cnt[0..2] likewise.  Returns 0. */
 int Nfft4GPAmdTimingEnable(void *str, int enable);
 int Nfft4GPAmdTimingQuery(void *str, double *ms, long long *cnt);
+/* average duration of ONE kernel of the additive matvec (which: 0 spread, 1 grid, 2 interp), measured
+ * with a single hipEvent pair around `reps` back-to-back launches on the library stream (per-launch
+ * event pairs add several microseconds each).  x, y: device vectors of the handle's size (y: 3n if
+ * grad).  Writes the mean milliseconds per launch. */
+int Nfft4GPAmdKernelBench(void *str, int which, int grad, int reps, const NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *y,
+                          double *ms_avg);
 
 /* split-phase additive matvec for row-sharded multi-GPU use (one process per GPU):
  *   phase 1 (spread): per-component oversampled-grid partial sums of this rank's points into grid

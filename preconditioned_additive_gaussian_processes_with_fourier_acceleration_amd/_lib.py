@@ -86,6 +86,7 @@ _SIGS = {
     "Nfft4GPAmdAdditiveLayoutInfo": (C.c_int, [vp, C.POINTER(C.c_longlong), C.c_int]),
     "Nfft4GPAmdTimingEnable": (C.c_int, [vp, C.c_int]),
     "Nfft4GPAmdTimingQuery": (C.c_int, [vp, dp, C.POINTER(C.c_longlong)]),
+    "Nfft4GPAmdKernelBench": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, vp, dp]),
     "Nfft4GPAmdAdditiveShardCreate": (vp, [vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int]),
     "Nfft4GPAmdShardSpread": (C.c_int, [vp, vp, vp]),
     "Nfft4GPAmdShardFinish": (C.c_int, [vp, vp, C.c_int, C.c_double, vp, C.c_double, vp]),

@@ -104,7 +104,9 @@ struct AdditivePlan {
    // layout
    int B = 4096, CG = 4, ngroups = 0, nblocks = 0;
    int spread_variant = 1, interp_variant = 1;  // kernel shape variants (nfft_kernels.hip)
-   bool fused = true;                           // grid step fused into the spread tail
+   // grid step fused into the spread tail via global fp64 atomics: measured 1.6x SLOWER at config C
+   // (245 workgroups add into each accumulator address), so off unless NFFT4GP_AMD_FUSED=1
+   bool fused = false;
    unsigned int* d_tickets = nullptr;           // [ngroups] arrival tickets of the fused spread
    DevLayout dl;
    // device buffers

@@ -555,6 +555,41 @@ int Nfft4GPAmdTimingQuery(void* str, double* ms, long long* cnt)
    return 0;
 }
 
+int Nfft4GPAmdKernelBench(void* str, int which, int grad, int reps, const double* x, double* y, double* ms_avg)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready || reps <= 0 || !ms_avg) return -1;
+   AdditivePlan& P = E->P;
+   if (!is_device_ptr(x) || !is_device_ptr(y)) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdKernelBench needs device vectors\n");
+      return -1;
+   }
+   hipStream_t s = current_stream();
+   hipEvent_t e0, e1;
+   NFFT4GP_HIP_CHECK(hipEventCreate(&e0));
+   NFFT4GP_HIP_CHECK(hipEventCreate(&e1));
+   // one warm launch, then `reps` back-to-back launches of the one kernel between a single event pair
+   for (int rep = -1; rep < reps; rep++) {
+      if (rep == 0) NFFT4GP_HIP_CHECK(hipEventRecord(e0, s));
+      int rc = 0;
+      if (which == 0)
+         rc = launch_spread(P, x, P.d_part, s);
+      else if (which == 1)
+         rc = launch_grid(P, P.d_part, P.nblocks, grad, s);
+      else
+         rc = launch_interp(P, grad, 1.0, x, 0.0, y, s);
+      if (rc) return -1;
+   }
+   NFFT4GP_HIP_CHECK(hipEventRecord(e1, s));
+   NFFT4GP_HIP_CHECK(hipEventSynchronize(e1));
+   float t = 0.f;
+   NFFT4GP_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+   *ms_avg = (double)t / reps;
+   (void)hipEventDestroy(e0);
+   (void)hipEventDestroy(e1);
+   return 0;
+}
+
 int Nfft4GPAmdShardSpread(void* str, const double* x_local, double* grid)
 {
    PlanExt* E = additive_plan(str);

@@ -175,6 +175,23 @@ class NFFTAdditiveKernel:
         names = ["spread", "grid", "interp"]
         return {nm: (ms[i], int(cnt[i])) for i, nm in enumerate(names)}
 
+    KERNELS = ("spread", "grid", "interp")
+
+    def kernel_bench(self, kernel: str, x, y, reps: int = 50, grad: bool = False) -> float:
+        """Mean ms of one launch of `kernel` ("spread" | "grid" | "interp"), timed with a single event
+        pair around `reps` back-to-back launches on the library stream.  x, y: device vectors
+        (y of length 3n when grad).  Call after a matvec (or gradmatsymv when grad) of the same setup."""
+        px, dx = _ptr(x)
+        py, dy = _ptr(y)
+        if not (dx and dy):
+            raise ValueError("kernel_bench needs device vectors")
+        ms = C.c_double()
+        rc = _lib.lib().Nfft4GPAmdKernelBench(self.h, self.KERNELS.index(kernel), int(grad), reps, px, py,
+                                               C.byref(ms))
+        if rc != 0:
+            raise RuntimeError("Nfft4GPAmdKernelBench failed")
+        return ms.value
+
     @property
     def matvec_fnptr(self) -> int:
         return _lib.fnptr("Nfft4GPAdditiveNFFTMatSymv")
