@@ -5,6 +5,7 @@ Drop-in for the hot path of Hitenze/Preconditioned_Additive_Gaussian_Processes_w
 kernels for gfx950 behind the C ABI of include/nfft4gp_amd.h (libnfft4gp_amd.so, built in-tree).
 """
 from ._lib import ExtensionMissing, header_symbols, lib  # noqa: F401
+from .data import read_features, read_labels, read_windows  # noqa: F401
 from .nfft import GAUSSIAN, MATERN12, NFFTAdditiveKernel, NFFTKernel  # noqa: F401
 from .solvers import NystromPrecond, pcg  # noqa: F401
 

@@ -76,37 +76,225 @@ __global__ void k_axpy(double a, const double* __restrict__ x, size_t n, double*
       y[i] += a * x[i];
 }
 
-// p = beta*p + z  (pcg.c:145-146: Scale then Axpy)
-__global__ void k_pupdate(double* __restrict__ p, const double* __restrict__ z, size_t n, double beta)
+// ---------------------------------------------------------------------------------------------
+// Device-controlled PCG (pcg.c:3-206).  The iteration's scalars (rho, pq, ||r||) and its control
+// decisions (the rho/beta/pq breakdown tests and the convergence test) live on the device, so the
+// host enqueues iterations back to back and only polls a status slot in pinned host memory a few
+// iterations behind.  Once a kernel flags a stop, every later PCG kernel of the launched-ahead
+// iterations is a no-op, so the state the host finds is exactly the state at the flagged iteration.
+// ---------------------------------------------------------------------------------------------
+struct PcgState {
+   double normb, tolb, pq, normr2;
+   int status;     // 0 running, 1 converged candidate, 2 rho == 0, 3 beta == 0, 4 pq <= 0
+   int flag_iter;  // iteration that set status
+};
+
+struct PcgSlot {   // pinned host memory, written by the last kernel of each iteration
+   double normr;
+   int status, flag_iter, seq, pad;
+};
+
+// PCG vector kernels: kEPT independent elements per thread (all loads issued before use), so each
+// lane keeps several HBM requests in flight; grid = ceil(n / (kVecThreads * kEPT)) <= kPcgMaxBlocks.
+constexpr int kEPT = 4;
+constexpr int kPcgMaxBlocks = 2048;
+constexpr int kXcds = 8;
+constexpr int kTicketStride = 64;  // unsigned ints: 256 B between arrival counters
+
+int pcg_grid(size_t n)
 {
-   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-      const double t = beta * p[i];
-      p[i] = t + z[i];
-   }
+   size_t g = (n + (size_t)kVecThreads * kEPT - 1) / ((size_t)kVecThreads * kEPT);
+   if (g > (size_t)kPcgMaxBlocks) g = kPcgMaxBlocks;
+   return (int)(g == 0 ? 1 : g);
 }
 
-// x += a p ; r -= a q ; partial ||r||^2   (pcg.c:168-172 fused into one pass)
-__global__ __launch_bounds__(kVecThreads) void k_xr_update(double* __restrict__ x, double* __restrict__ r,
-                                                           const double* __restrict__ p,
-                                                           const double* __restrict__ q, size_t n, double a,
-                                                           double* __restrict__ part)
+// partial of this block -> memory-side store, arrival ticket; returns true in every thread of the
+// last arriving block, with the fixed-order total of all partials in *total.  Thread 0 holds `v`.
+__device__ bool grid_total(double v, double* __restrict__ part, unsigned int* __restrict__ ticket, double* total)
+{
+   __shared__ int s_last;
+   __shared__ double s_red[kVecThreads / 64];
+   // hand-off without L2 write-back fences (a release fence here writes back every dirty line the
+   // kernel produced -- measured +15-20 us per launch): the partial goes out as an agent-scope
+   // (sc1, memory-side) store, drained with vmcnt(0) before the ticket RMW; the last arriver reads
+   // the partials with agent-scope loads (MI355X_MICROARCH.md, handoff-flag)
+   // Arrival is counted per XCD first (block b runs on XCD b % 8; 8 counters 256 B apart), then
+   // once per XCD on a top counter: one counter taking every block's RMW serialises ~1000 atomics
+   // at one memory channel (measured ~13 us per launch).
+   if (threadIdx.x == 0) {
+      __hip_atomic_store(part + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned G = gridDim.x;
+      const unsigned xcd = blockIdx.x % kXcds;
+      const unsigned members = (G - xcd + kXcds - 1) / kXcds;
+      const unsigned groups = G < kXcds ? G : kXcds;
+      int last = 0;
+      const unsigned old = __hip_atomic_fetch_add(ticket + (1 + xcd) * kTicketStride, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      if (old == members - 1) {
+         const unsigned top = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+         last = (top == groups - 1);
+      }
+      s_last = last;
+   }
+   __syncthreads();
+   if (!s_last) return false;
+   constexpr int kPer = kPcgMaxBlocks / kVecThreads;
+   double pv[kPer];
+#pragma unroll
+   for (int u = 0; u < kPer; u++) {
+      const unsigned i = threadIdx.x + u * kVecThreads;
+      pv[u] = i < gridDim.x ? __hip_atomic_load(part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+   }
+   double acc = 0.0;
+#pragma unroll
+   for (int u = 0; u < kPer; u++) acc += pv[u];
+   for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+   if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = acc;
+   __syncthreads();
+   double t = 0.0;
+   for (int w = 0; w < kVecThreads / 64; w++) t += s_red[w];
+   *total = t;
+   if (threadIdx.x <= (unsigned)kXcds)
+      __hip_atomic_store(ticket + threadIdx.x * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+   return true;
+}
+
+__device__ double block_sum0(double acc)
 {
    __shared__ double s[kVecThreads / 64];
-   double acc = 0.0;
-   for (size_t i = (size_t)blockIdx.x * kVecThreads + threadIdx.x; i < n; i += (size_t)gridDim.x * kVecThreads) {
-      x[i] += a * p[i];
-      const double ri = r[i] + (-a) * q[i];
-      r[i] = ri;
-      acc = fma(ri, ri, acc);
-   }
    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
    __syncthreads();
-   if (threadIdx.x == 0) {
-      double v = 0.0;
+   double v = 0.0;
+   if (threadIdx.x == 0)
       for (int w = 0; w < kVecThreads / 64; w++) v += s[w];
-      part[blockIdx.x] = v;
+   return v;  // valid in thread 0
+}
+
+// which = 0: rhos[ii] = (z, r) with the rho == 0 test;  which = 1: pq = (q, p) with the pq <= 0 test
+__global__ __launch_bounds__(kVecThreads) void k_pcg_dot(const double* __restrict__ a, const double* __restrict__ b,
+                                                         size_t n, double* __restrict__ part,
+                                                         unsigned int* __restrict__ ticket, PcgState* st,
+                                                         double* __restrict__ rhos, int ii, int which)
+{
+   if (st->status) return;
+   double acc = 0.0;
+   const size_t stride = (size_t)gridDim.x * kVecThreads * kEPT;
+   for (size_t i0 = (size_t)blockIdx.x * kVecThreads * kEPT + threadIdx.x; i0 < n; i0 += stride) {
+      double av[kEPT], bv[kEPT];
+#pragma unroll
+      for (int u = 0; u < kEPT; u++) {
+         const size_t i = i0 + (size_t)u * kVecThreads;
+         av[u] = i < n ? a[i] : 0.0;
+         bv[u] = i < n ? b[i] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kEPT; u++) acc = fma(av[u], bv[u], acc);
    }
+   acc = block_sum0(acc);
+   double tot;
+   if (!grid_total(acc, part, ticket, &tot) || threadIdx.x != 0) return;
+   if (which == 0) {
+      rhos[ii] = tot;
+      if (tot == 0.0) { st->status = 2; st->flag_iter = ii; }
+   } else {
+      st->pq = tot;
+      if (tot <= 0.0) { st->status = 4; st->flag_iter = ii; }
+   }
+}
+
+// p = z (ii == 1) or p = beta p + z, beta = rhos[ii]/rhos[ii-1] (pcg.c:131-147: Scale then Axpy)
+__global__ __launch_bounds__(kVecThreads) void k_pcg_pupdate(double* __restrict__ p, const double* __restrict__ z,
+                                                             size_t n, PcgState* st, const double* __restrict__ rhos,
+                                                             int ii)
+{
+   if (st->status) return;
+   const double rho = rhos[ii];
+   if (rho == 0.0) {  // no-preconditioner path: rho came from the previous iteration's norm
+      if (blockIdx.x == 0 && threadIdx.x == 0) { st->status = 2; st->flag_iter = ii; }
+      return;
+   }
+   double beta = 0.0;
+   if (ii > 1) {
+      beta = rho / rhos[ii - 1];
+      if (beta == 0.0) {
+         if (blockIdx.x == 0 && threadIdx.x == 0) { st->status = 3; st->flag_iter = ii; }
+         return;
+      }
+   }
+   const size_t stride = (size_t)gridDim.x * kVecThreads * kEPT;
+   for (size_t i0 = (size_t)blockIdx.x * kVecThreads * kEPT + threadIdx.x; i0 < n; i0 += stride) {
+      double pv[kEPT], zv[kEPT];
+#pragma unroll
+      for (int u = 0; u < kEPT; u++) {
+         const size_t i = i0 + (size_t)u * kVecThreads;
+         zv[u] = i < n ? z[i] : 0.0;
+         pv[u] = (ii > 1 && i < n) ? p[i] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kEPT; u++) {
+         const size_t i = i0 + (size_t)u * kVecThreads;
+         if (i < n) p[i] = (ii > 1) ? beta * pv[u] + zv[u] : zv[u];
+      }
+   }
+}
+
+// x += alpha p ; r -= alpha q ; ||r|| ; convergence test ; status slot  (pcg.c:168-182)
+__global__ __launch_bounds__(kVecThreads) void k_pcg_xr(double* __restrict__ x, double* __restrict__ r,
+                                                        const double* __restrict__ p, const double* __restrict__ q,
+                                                        size_t n, double* __restrict__ part,
+                                                        unsigned int* __restrict__ ticket, PcgState* st,
+                                                        double* __restrict__ rhos, double* __restrict__ hist, int ii,
+                                                        int rho_from_norm, PcgSlot* slot)
+{
+   if (st->status) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+         slot->normr = st->normr2;
+         slot->status = st->status;
+         slot->flag_iter = st->flag_iter;
+         __hip_atomic_store(&slot->seq, ii, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      return;
+   }
+   const double a = rhos[ii] / st->pq;
+   double acc = 0.0;
+   const size_t stride = (size_t)gridDim.x * kVecThreads * kEPT;
+   for (size_t i0 = (size_t)blockIdx.x * kVecThreads * kEPT + threadIdx.x; i0 < n; i0 += stride) {
+      double xv[kEPT], rv[kEPT], pv[kEPT], qv[kEPT];
+#pragma unroll
+      for (int u = 0; u < kEPT; u++) {
+         const size_t i = i0 + (size_t)u * kVecThreads;
+         const bool ok = i < n;
+         xv[u] = ok ? x[i] : 0.0;
+         rv[u] = ok ? r[i] : 0.0;
+         pv[u] = ok ? p[i] : 0.0;
+         qv[u] = ok ? q[i] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kEPT; u++) {
+         const size_t i = i0 + (size_t)u * kVecThreads;
+         const double xi = xv[u] + a * pv[u];
+         const double ri = rv[u] + (-a) * qv[u];
+         acc = fma(ri, ri, acc);
+         if (i < n) {
+            x[i] = xi;
+            r[i] = ri;
+         }
+      }
+   }
+   acc = block_sum0(acc);
+   double tot;
+   if (!grid_total(acc, part, ticket, &tot) || threadIdx.x != 0) return;
+   const double normr = sqrt(tot);
+   st->normr2 = normr;
+   hist[ii] = normr / st->normb;
+   if (rho_from_norm) rhos[ii + 1] = tot;  // z = r next iteration: rho = (r, r)
+   if (normr <= st->tolb) { st->status = 1; st->flag_iter = ii; }
+   slot->normr = normr;
+   slot->status = st->status;
+   slot->flag_iter = st->flag_iter;
+   __hip_atomic_store(&slot->seq, ii, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 int grid_for(size_t n)
@@ -266,6 +454,30 @@ struct NysDev {
    int nblk = 0;
 };
 
+// PCG scratch: reduction partials + arrival ticket (device), status slots (pinned host, mapped)
+struct PcgScratch {
+   static constexpr int kSlots = 4;
+   double* part = nullptr;
+   unsigned int* ticket = nullptr;
+   PcgSlot* slots_h = nullptr;
+   PcgSlot* slots_d = nullptr;
+   int ensure()
+   {
+      if (!part) {
+         NFFT4GP_HIP_CHECK(hipMalloc((void**)&part, sizeof(double) * kPcgMaxBlocks));
+         const size_t tb = sizeof(unsigned int) * (kXcds + 1) * kTicketStride;
+         NFFT4GP_HIP_CHECK(hipMalloc((void**)&ticket, tb));
+         NFFT4GP_HIP_CHECK(hipMemset(ticket, 0, tb));
+         NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&slots_h, sizeof(PcgSlot) * kSlots,
+                                         hipHostMallocMapped | hipHostMallocCoherent));
+         NFFT4GP_HIP_CHECK(hipHostGetDevicePointer((void**)&slots_d, slots_h, 0));
+         memset(slots_h, 0, sizeof(PcgSlot) * kSlots);
+      }
+      return 0;
+   }
+};
+PcgScratch g_pcg;
+
 int g_last_hist_len = 0;
 
 }  // namespace
@@ -334,17 +546,24 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
    Vec vx, vb;
    if (vx.open(x, N, true) || vb.open(rhs, N, true)) return -1;
    double *r = nullptr, *z = nullptr, *p = nullptr, *q = nullptr;
-   int iter = 0, ii;
-   double rho = 1.0, alpha, beta, normb, normr, normr2, tolb;
+   double *rhos = nullptr, *hist_d = nullptr;
+   PcgState* st = nullptr;
+   PcgSlot* slots_h = nullptr;  // pinned, device-visible
+   PcgSlot* slots_d = nullptr;
+   int iter = 0;
+   double normb, normr, normr2, tolb;
    double* rel_res_v = nullptr;
    const double EPSILON = DBL_EPSILON;
-   if (g_red.ensure()) return -1;
+   if (g_red.ensure() || g_pcg.ensure()) return -1;
 
    auto cleanup = [&](bool copy_x) {
       if (r) (void)hipFree(r);
       if (z) (void)hipFree(z);
       if (p) (void)hipFree(p);
       if (q) (void)hipFree(q);
+      if (rhos) (void)hipFree(rhos);
+      if (hist_d) (void)hipFree(hist_d);
+      if (st) (void)hipFree(st);
       vx.close(copy_x);
       vb.close(false);
    };
@@ -365,17 +584,18 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
    if (maxits > n) maxits = n;
 
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&r, sizeof(double) * N));
-   NFFT4GP_HIP_CHECK(hipMalloc((void**)&z, sizeof(double) * N));
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&p, sizeof(double) * N));
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&q, sizeof(double) * N));
+   if (prec_data) NFFT4GP_HIP_CHECK(hipMalloc((void**)&z, sizeof(double) * N));
 
    NFFT4GP_HIP_CHECK(hipMemcpyAsync(r, vb.d, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
    if (matvec(mat_data, n, -1.0, vx.d, 1.0, r)) {
       cleanup(false);
       return -1;
    }
-   if (dev_dot(r, r, N, &normr)) return -1;
-   normr = std::sqrt(normr);
+   double rr0;
+   if (dev_dot(r, r, N, &rr0)) return -1;
+   normr = std::sqrt(rr0);
    if (normr < tolb) {  // pcg.c:70-84
       *prel_res = normr / normb;
       *piter = 0;
@@ -398,57 +618,139 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
       printf("Step    Residual norm  Relative res.  Convergence Rate\n");
       printf("%5d   %8e   %8e   N/A\n", 0, normr, rel_res_v[0]);
    }
-   const int g = grid_for(N);
-   for (ii = 1; ii <= maxits; ii++) {
-      if (prec_data) {
-         if (precondfunc(prec_data, n, z, r)) break;
-      } else {
-         NFFT4GP_HIP_CHECK(hipMemcpyAsync(z, r, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
-      }
-      const double rho1 = rho;
-      if (dev_dot(z, r, N, &rho)) break;
-      if (rho == 0.0) {
-         if (print_level > 1) printf("rho = %.16e\n", rho);
-         break;
-      }
-      if (ii == 1) {
-         NFFT4GP_HIP_CHECK(hipMemcpyAsync(p, z, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
-      } else {
-         beta = rho / rho1;
-         if (beta == 0.0) {
-            if (print_level > 1) printf("beta = %.16e\n", beta);
-            break;
-         }
-         hipLaunchKernelGGL(k_pupdate, dim3(elem_grid(N)), dim3(256), 0, s, p, z, N, beta);
-      }
-      if (matvec(mat_data, n, 1.0, p, 0.0, q)) break;
-      double pq;
-      if (dev_dot(q, p, N, &pq)) break;
-      if (pq <= 0) {
-         if (print_level > 1) printf("pq = %.16e\n", pq);
-         break;
-      }
-      alpha = rho / pq;
-      hipLaunchKernelGGL(k_xr_update, dim3(g), dim3(kVecThreads), 0, s, vx.d, r, p, q, N, alpha, g_red.part);
-      hipLaunchKernelGGL(k_sum_final, dim3(1), dim3(kVecThreads), 0, s, g_red.part, g, g_red.res);
-      NFFT4GP_HIP_CHECK(hipMemcpyAsync(g_red.host, g_red.res, sizeof(double), hipMemcpyDeviceToHost, s));
+
+   // device state
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&rhos, sizeof(double) * ((size_t)maxits + 2)));
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&hist_d, sizeof(double) * ((size_t)maxits + 1)));
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&st, sizeof(PcgState)));
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(hist_d, 0, sizeof(double) * ((size_t)maxits + 1), s));
+   {
+      PcgState h{};
+      h.normb = normb;
+      h.tolb = tolb;
+      h.normr2 = normr;
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(st, &h, sizeof(h), hipMemcpyHostToDevice, s));
+      // no preconditioner: z = r, so iteration 1's rho is (r, r)  (pcg.c:103-119)
+      if (!prec_data) NFFT4GP_HIP_CHECK(hipMemcpyAsync(rhos + 1, &rr0, sizeof(double), hipMemcpyHostToDevice, s));
       NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
-      normr = std::sqrt(g_red.host[0]);
-      normr2 = normr;
-      rel_res_v[ii] = normr / normb;
-      if (print_level > 0)
-         printf("%5d   %8e   %8e   %8.6f\n", ii, normr, rel_res_v[ii], rel_res_v[ii] / rel_res_v[ii - 1]);
-      if (normr <= tolb) {  // pcg.c:181-193: true residual recheck
-         NFFT4GP_HIP_CHECK(hipMemcpyAsync(r, vb.d, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
-         if (matvec(mat_data, n, -1.0, vx.d, 1.0, r)) break;
-         if (dev_dot(r, r, N, &normr2)) break;
-         normr2 = std::sqrt(normr2);
-         rel_res_v[ii] = normr2;
-         if (normr2 <= tolb) {
-            iter = ii;
-            break;
+   }
+   slots_h = g_pcg.slots_h;
+   slots_d = g_pcg.slots_d;
+   for (int i = 0; i < PcgScratch::kSlots; i++) __atomic_store_n(&slots_h[i].seq, 0, __ATOMIC_RELAXED);
+
+   const int g = pcg_grid(N);
+   const int ge = g;
+   // iterations in flight ahead of the host's status check (1 when printing every step)
+   const int lag = print_level > 0 ? 1 : PcgScratch::kSlots;
+   double prev_rel = rel_res_v[0];
+   int next_check = 1;   // next iteration whose slot the host reads
+   int ii = 1;
+   bool stop = false;
+   int rc = 0;
+   while (!stop) {
+      // enqueue iterations until `lag` are unchecked or maxits is reached
+      while (ii <= maxits && ii - next_check < lag) {
+         double* zz = r;
+         if (prec_data) {
+            if (precondfunc(prec_data, n, z, r)) { rc = -1; break; }
+            hipLaunchKernelGGL(k_pcg_dot, dim3(g), dim3(kVecThreads), 0, s, z, r, N, g_pcg.part, g_pcg.ticket, st,
+                               rhos, ii, 0);
+            zz = z;
+         }
+         hipLaunchKernelGGL(k_pcg_pupdate, dim3(ge), dim3(kVecThreads), 0, s, p, zz, N, st, rhos, ii);
+         if (matvec(mat_data, n, 1.0, p, 0.0, q)) { rc = -1; break; }
+         hipLaunchKernelGGL(k_pcg_dot, dim3(g), dim3(kVecThreads), 0, s, q, p, N, g_pcg.part, g_pcg.ticket, st,
+                            rhos, ii, 1);
+         hipLaunchKernelGGL(k_pcg_xr, dim3(g), dim3(kVecThreads), 0, s, vx.d, r, p, q, N, g_pcg.part, g_pcg.ticket,
+                            st, rhos, hist_d, ii, prec_data ? 0 : 1, slots_d + (ii % PcgScratch::kSlots));
+         ii++;
+      }
+      if (rc) break;
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      if (next_check >= ii) break;  // nothing in flight: maxits reached
+      // wait for iteration next_check's status slot
+      PcgSlot* sl = slots_h + (next_check % PcgScratch::kSlots);
+      long spins = 0;
+      while (__atomic_load_n(&sl->seq, __ATOMIC_ACQUIRE) != next_check) {
+         if ((++spins & 0xFFFF) == 0) {
+            const hipError_t qe = hipStreamQuery(s);
+            if (qe == hipSuccess && __atomic_load_n(&sl->seq, __ATOMIC_ACQUIRE) != next_check) {
+               fprintf(stderr, "nfft4gp_amd: PCG status slot %d never arrived\n", next_check);
+               rc = -1;
+               break;
+            }
+            if (qe != hipSuccess && qe != hipErrorNotReady) {
+               fprintf(stderr, "nfft4gp_amd: PCG stream error %s\n", hipGetErrorString(qe));
+               rc = -1;
+               break;
+            }
          }
       }
+      if (rc) break;
+      const int status = sl->status;
+      const int fi = sl->flag_iter;
+      if (print_level > 0 && (status == 0 || status == 1) && (status == 0 || fi == next_check)) {
+         const double rel = sl->normr / normb;
+         printf("%5d   %8e   %8e   %8.6f\n", next_check, sl->normr, rel, rel / prev_rel);
+         prev_rel = rel;
+      }
+      if (status == 0) {
+         next_check++;
+         continue;
+      }
+      // a kernel stopped the iteration at fi <= next_check: drain the no-op'd tail, then act as pcg.c
+      NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
+      PcgState h;
+      NFFT4GP_HIP_CHECK(hipMemcpy(&h, st, sizeof(h), hipMemcpyDeviceToHost));
+      NFFT4GP_HIP_CHECK(hipMemcpy(rel_res_v + 1, hist_d + 1, sizeof(double) * (size_t)fi, hipMemcpyDeviceToHost));
+      normr2 = h.normr2;
+      if (status != 1) {
+         if (print_level > 1) {
+            if (status == 2) printf("rho = %.16e\n", 0.0);
+            if (status == 3) printf("beta = %.16e\n", 0.0);
+            if (status == 4) printf("pq = %.16e\n", h.pq);
+         }
+         break;
+      }
+      // pcg.c:181-193: recompute the true residual
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(r, vb.d, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
+      if (matvec(mat_data, n, -1.0, vx.d, 1.0, r)) { rc = -1; break; }
+      double rr;
+      if (dev_dot(r, r, N, &rr)) { rc = -1; break; }
+      normr2 = std::sqrt(rr);
+      rel_res_v[fi] = normr2;
+      if (normr2 <= tolb) {
+         iter = fi;
+         break;
+      }
+      // keep iterating from fi + 1 with the true residual
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(hist_d + fi, &rel_res_v[fi], sizeof(double), hipMemcpyHostToDevice, s));
+      if (!prec_data) NFFT4GP_HIP_CHECK(hipMemcpyAsync(rhos + fi + 1, &rr, sizeof(double), hipMemcpyHostToDevice, s));
+      h.status = 0;
+      h.normr2 = normr2;
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(st, &h, sizeof(h), hipMemcpyHostToDevice, s));
+      NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
+      for (int i = 0; i < PcgScratch::kSlots; i++) __atomic_store_n(&slots_h[i].seq, 0, __ATOMIC_RELAXED);
+      prev_rel = rel_res_v[fi];
+      ii = fi + 1;
+      next_check = fi + 1;
+   }
+   if (!rc && iter == 0) {
+      // not converged (maxits or breakdown): the history of the completed iterations
+      (void)hipStreamSynchronize(s);
+      PcgState h;
+      if (hipMemcpy(&h, st, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
+         normr2 = h.normr2;
+         const int last = h.status ? h.flag_iter : std::min(ii - 1, maxits);
+         if (last > 0) (void)hipMemcpy(rel_res_v + 1, hist_d + 1, sizeof(double) * (size_t)last, hipMemcpyDeviceToHost);
+         if (h.status == 1) rel_res_v[h.flag_iter] = normr2;
+      }
+   }
+   if (rc) {
+      (void)hipStreamSynchronize(s);
+      free(rel_res_v);
+      cleanup(false);
+      return -1;
    }
    *prel_res = normr2 / normb;
    *piter = iter;

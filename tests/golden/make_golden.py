@@ -1,0 +1,127 @@
+"""Generate the committed golden fixtures (tests/golden/*.npz).  TEST INFRASTRUCTURE.
+
+Run here (the container that has /root/reference) after `make -C oracle && make -C oracle ref`:
+    python tests/golden/make_golden.py
+Inputs are data files the reference's own tests hold (TESTS/TEST2/data/foo.*, TESTS/TEST1/data/bike.*)
+plus seeded synthetic points.  Expected outputs come from
+  * the reference's DENSE operator compiled from its own sources (oracle/_ref: kernels.c:3046-3494
+    additive kernel, matops.c:3-29 SYMV, pcg.c:3-206 PCG, nys.c:518-660 Nystrom setup/apply), and
+  * the oracle's CPU restatement of the reference's NFFT path (oracle/nfft4gp_oracle.c), NFFT and
+    exact-NDFT modes, kept so that later oracle edits are caught.
+Every array is stored in an .npz without pickles (np.load(..., allow_pickle=False) reads it back).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+from oracle import OracleAdditiveNFFT, RefDenseAdditive, RefNystrom, ref_available, ref_pcg  # noqa: E402
+from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.data import (  # noqa: E402
+    read_features, read_labels, read_windows)
+
+REF = os.environ.get("NFFT4GP_REF", "/root/reference")
+
+
+def operator_case(X, win, nw, dw, kernel, f, l, mu, x, dense=True):
+    out = {}
+    o = OracleAdditiveNFFT(X, win, nw, dw)
+    o.setup(kernel, f, l, mu)
+    out["nfft_y"] = o.matsymv(x)
+    out["nfft_grad"] = o.gradmatsymv(x)
+    out["ndft_y"] = o.matsymv(x, exact=True)
+    out["ndft_grad"] = o.gradmatsymv(x, exact=True)
+    out["nfft_y_ab"] = o.matsymv(x, alpha=0.7, beta=-1.5, y=np.cos(np.arange(X.shape[0])))
+    if dense:
+        r = RefDenseAdditive(X, win, nw, dw, kernel=kernel)
+        r.matrices(f, l, mu)
+        out["dense_y"] = r.matsymv(x)
+        out["dense_grad"] = r.gradmatsymv(x)
+    return out
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print(f"wrote {path} ({os.path.getsize(path)} bytes)")
+
+
+def main():
+    if not ref_available():
+        raise SystemExit("build oracle/_ref first: make -C oracle ref")
+    f, mu = 1.3, 0.01
+
+    # (1) TEST2's 1-D dataset, one window {0} (TESTS/TEST2/data/foo.window)
+    X = read_features(os.path.join(REF, "TESTS/TEST2/data/foo.train.feature"))
+    lab = read_labels(os.path.join(REF, "TESTS/TEST2/data/foo.train.label"))
+    win, nw, dw = read_windows(os.path.join(REF, "TESTS/TEST2/data/foo.window"))
+    x = np.random.default_rng(11).random(X.shape[0]) - 0.5
+    arrays = dict(X=X, labels=lab, windows=win, nw=nw, dw=dw, x=x, f=f, mu=mu)
+    for kernel, kname in ((0, "gauss"), (1, "matern")):
+        for l in (0.1, 1.0):
+            for k, v in operator_case(X, win, nw, dw, kernel, f, l, mu, x).items():
+                arrays[f"{kname}_l{l}_{k}"] = v
+    save("foo1d", **arrays)
+
+    # (2) synthetic additive 1-D windows (the BASELINE configs' shape, small n)
+    rng = np.random.default_rng(906)
+    n, d = 2000, 4
+    Xs = rng.random((n, d))
+    xs = rng.random(n) - 0.5
+    wins = np.arange(d, dtype=np.int32)
+    arrays = dict(X=Xs, windows=wins, nw=d, dw=1, x=xs, f=f, mu=mu)
+    for kernel, kname, l in ((0, "gauss", 0.3), (1, "matern", 1.0)):
+        for k, v in operator_case(Xs, wins, d, 1, kernel, f, l, mu, xs).items():
+            arrays[f"{kname}_l{l}_{k}"] = v
+    save("synth1d", **arrays)
+
+    # (3) TEST1's bike dataset, 3 windows x 3 features (bike.g.window), first 400 rows: multi-D windows
+    Xb = read_features(os.path.join(REF, "TESTS/TEST1/data/bike.train.feature"))[:400].copy(order="F")
+    winb, nwb, dwb = read_windows(os.path.join(REF, "TESTS/TEST1/data/bike.g.window"))
+    xb = np.random.default_rng(12).random(Xb.shape[0]) - 0.5
+    arrays = dict(X=Xb, windows=winb, nw=nwb, dw=dwb, x=xb, f=1.0, mu=mu)
+    for k, v in operator_case(Xb, winb, nwb, dwb, 0, 1.0, 1.0, mu, xb).items():
+        arrays[f"gauss_l1.0_{k}"] = v
+    save("bike3d", **arrays)
+
+    # (4) the reference's PCG (pcg.c) on its dense additive operator (synthetic 4 x 1-D windows,
+    #     f = 1, l = 0.1), without and with its Nystrom preconditioner (nys.c), fixed permutation.
+    #     (On TEST2's single 1-D window the reference's rank-32 Nystrom setup degenerates -- s ~ 1e-17
+    #     and a NaN PCG -- so the preconditioned fixture uses the additive data.)
+    f1, l = 1.0, 0.1
+    Xp, winp = Xs[:1500].copy(order="F"), wins
+    n1 = Xp.shape[0]
+    b = np.random.default_rng(15).random(n1) - 0.5
+    r = RefDenseAdditive(Xp, winp, d, 1, kernel=0)
+    r.matrices(f1, l, mu, grad=False)
+
+    def mv(alpha, xv, beta, yv):
+        yv[:] = r.matsymv(xv, alpha, beta, yv.copy())
+
+    xp, relres, hist, its = ref_pcg(mv, n1, b, maxits=1000, tol=1e-6)
+    k = 32
+    perm = np.random.default_rng(13).permutation(n1).astype(np.int32)
+    nys = RefNystrom(r, f1, l, mu, k, perm)
+    U, s, eta, _ = nys.factors()
+    nys_rhs = np.random.default_rng(14).random(n1) - 0.5
+    nys_out = nys.solve(np.zeros(n1), nys_rhs.copy())
+
+    def pc(xo, rhs):
+        nys.solve(xo, rhs.copy())
+
+    xq, relq, histq, itq = ref_pcg(mv, n1, b, maxits=1000, tol=1e-6, precond_py=pc)
+    assert its > 0 and itq > 0 and np.all(np.isfinite(U))
+    save("pcg_synth", X=Xp, windows=winp, nw=d, dw=1, b=b, f=f1, l=l, mu=mu,
+         pcg_x=xp, pcg_relres=relres, pcg_hist=hist, pcg_iters=its,
+         nys_k=k, nys_perm=perm, nys_U=U, nys_s=s, nys_eta=eta, nys_rhs=nys_rhs, nys_out=nys_out,
+         pcgnys_x=xq, pcgnys_relres=relq, pcgnys_hist=histq, pcgnys_iters=itq)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,116 @@
+"""GPU parity against the committed golden fixtures (tests/golden/*.npz), through the C ABI:
+the HIP additive matvec / grad matvec vs the oracle's NFFT outputs, the HIP Nystrom apply vs the
+reference's nys.c output, and the device-controlled PCG vs the reference's pcg.c runs (dense operator
+of the fixture supplied as a C callback, so both solvers see the same operator)."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd import _lib
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+ONE_D = [("foo1d", "gauss_l0.1", 0, 0.1), ("foo1d", "gauss_l1.0", 0, 1.0), ("foo1d", "matern_l0.1", 1, 0.1),
+         ("foo1d", "matern_l1.0", 1, 1.0), ("synth1d", "gauss_l0.3", 0, 0.3), ("synth1d", "matern_l1.0", 1, 1.0)]
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+
+
+def rel(a, b):
+    return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / np.linalg.norm(np.asarray(b)))
+
+
+@pytest.mark.parametrize("name,pre,kernel,l", ONE_D)
+def test_matvec_matches_golden(torch_cuda, name, pre, kernel, l):
+    torch = torch_cuda
+    z = load(name)
+    X = np.asarray(z["X"])
+    op = amd.NFFTAdditiveKernel(X, np.asarray(z["windows"], np.int32), int(z["nw"]), int(z["dw"]))
+    assert op.setup(kernel, float(z["f"]), l, float(z["mu"])) == 0
+    x = np.asarray(z["x"])
+    n = x.size
+    xd = torch.tensor(x, device="cuda")
+    yd = torch.zeros(n, dtype=torch.float64, device="cuda")
+    op.matsymv(xd, 1.0, 0.0, yd)
+    # the product's design error (tap polynomials, fixed-point coordinates): <= 1e-9 at l = 0.1
+    assert rel(yd.cpu().numpy(), z[pre + "_nfft_y"]) < 1e-8
+    y0 = torch.tensor(np.cos(np.arange(n)), device="cuda")
+    op.matsymv(xd, 0.7, -1.5, y0)
+    assert rel(y0.cpu().numpy(), z[pre + "_nfft_y_ab"]) < 1e-8
+    g = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
+    op.gradmatsymv(xd, 1.0, 0.0, g)
+    g = g.cpu().numpy()
+    gz = z[pre + "_nfft_grad"]
+    for i in range(3):
+        assert rel(g[i * n:(i + 1) * n], gz[i * n:(i + 1) * n]) < 1e-8, i
+
+
+# ---- dense operator of a fixture as a C callback on device vectors --------------------------------
+class DenseDeviceOp:
+    """func_symmatvec over device pointers: y = alpha*K x + beta*y with K the reference's dense additive
+    Gaussian f^2 ((1/nw) sum_c exp(-|x_c - x_c'|^2 / 2 l^2) + mu I) (kernels.c:680-1289, 3099-3494)."""
+
+    def __init__(self, z):
+        X, f, l, mu = np.asarray(z["X"]), float(z["f"]), float(z["l"]), float(z["mu"])
+        n, nw = X.shape
+        K = np.zeros((n, n))
+        for c in range(nw):
+            d = X[:, c][:, None] - X[:, c][None, :]
+            K += np.exp(-d * d / (2 * l * l))
+        self.K = f * f * (K / nw + mu * np.eye(n))
+        self.n = n
+        self.h = None
+        hip = C.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        self.hip = hip
+
+        def mv(_m, nn, alpha, xp, beta, yp):
+            self.hip.hipDeviceSynchronize()
+            xv = np.empty(nn)
+            yv = np.empty(nn)
+            self.hip.hipMemcpy(xv.ctypes.data, xp, 8 * nn, 2)  # D2H
+            self.hip.hipMemcpy(yv.ctypes.data, yp, 8 * nn, 2)
+            out = alpha * (self.K @ xv) + (beta * yv if beta != 0.0 else 0.0)
+            out = np.ascontiguousarray(out, dtype=np.float64)
+            self.hip.hipMemcpy(yp, out.ctypes.data, 8 * nn, 1)  # H2D
+            return 0
+
+        self._cb = _lib.SYMMATVEC(mv)
+        self.matvec_fnptr = C.cast(self._cb, C.c_void_p).value
+
+
+def test_nystrom_apply_matches_golden(torch_cuda):
+    torch = torch_cuda
+    z = load("pcg_synth")
+    pre = amd.NystromPrecond(z["nys_U"], z["nys_s"], float(z["nys_eta"]), z["nys_perm"])
+    r = np.asarray(z["nys_rhs"])
+    xd = torch.zeros(r.size, dtype=torch.float64, device="cuda")
+    pre.solve(xd, torch.tensor(r, device="cuda"))
+    assert rel(xd.cpu().numpy(), z["nys_out"]) <= 1e-12
+
+
+@pytest.mark.parametrize("with_nys", [False, True])
+def test_pcg_matches_golden(torch_cuda, with_nys):
+    torch = torch_cuda
+    z = load("pcg_synth")
+    op = DenseDeviceOp(z)
+    pre = amd.NystromPrecond(z["nys_U"], z["nys_s"], float(z["nys_eta"]), z["nys_perm"]) if with_nys else None
+    key = "pcgnys" if with_nys else "pcg"
+    b = torch.tensor(np.asarray(z["b"]), device="cuda")
+    x = torch.zeros(op.n, dtype=torch.float64, device="cuda")
+    x, rr, hist, it = amd.pcg(op, b, x, maxits=1000, tol=1e-6, precond=pre)
+    it_ref = int(z[key + "_iters"])
+    assert it > 0 and abs(it - it_ref) <= max(2, it_ref // 20), (it, it_ref)
+    assert rr <= 1e-6
+    assert rel(x.cpu().numpy(), z[key + "_x"]) < 1e-5
+    h_ref = np.asarray(z[key + "_hist"])
+    k = min(10, it, it_ref)
+    np.testing.assert_allclose(hist[:k], h_ref[:k], rtol=1e-6)
+    # pcg.c:188: the converged entry holds the ABSOLUTE true-residual norm
+    assert hist[it] == pytest.approx(rr * np.linalg.norm(np.asarray(z["b"])), rel=1e-12)
