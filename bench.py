@@ -300,6 +300,15 @@ def main():
         result["layout"] = info
         # survey-defined whole-matvec bytes (fp64 coords: 8n(2d+2)) for reference
         result["matvec_bytes_survey_def"] = 8 * n * (2 * d + 2)
+        # host-pointer calls (the reference's calling convention): x and y staged over PCIe each call
+        xh = np.ascontiguousarray(x_host)
+        yh = np.zeros(n)
+        op.matsymv(xh, 1.0, 0.0, yh)
+        reps_h = 20
+        t0 = time.perf_counter()
+        for _ in range(reps_h):
+            op.matsymv(xh, 1.0, 0.0, yh)
+        result["pcie_inclusive_matvecs_per_s"] = reps_h / (time.perf_counter() - t0)
         if not args.no_pcg:
             result.update(run_pcg_single(op, torch, n))
         if not args.no_cpu_baseline:

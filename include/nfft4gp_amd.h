@@ -13,8 +13,10 @@
  *    default stream).  Host pointers are staged through device buffers and the call is synchronous.
  *  - every computation runs on the GPU; there is no CPU fallback.  If no HIP device is present the
  *    operator entry points print an error and return -1.
- *  - callbacks handed to Nfft4GPSolverPcg receive DEVICE pointers (all operators in this library
- *    accept them).
+ *  - Nfft4GPSolverPcg keeps its vectors in HBM.  Callbacks of this library (the NFFT matvecs,
+ *    Nfft4GPAmdNysSolve) receive device pointers; any other callback -- e.g. the reference's own
+ *    Nfft4GPDenseMatSymv -- is called with HOST vectors staged around the call, exactly as the
+ *    reference calls it (see Nfft4GPAmdSetCallbackPointerMode).
  *
  * Precision: NFFT4GP_DOUBLE is double (the reference default, SRC/utils/utils.h:28-31).
  */
@@ -139,6 +141,10 @@ int Nfft4GPSolverPcg(void *mat_data, int n, func_symmatvec matvec, void *prec_da
 /* length of the rel_res_v array returned by the last Nfft4GPSolverPcg call on this process
  * (1 for the early exits of pcg.c:32-41 / :70-84, maxits+1 otherwise) */
 int Nfft4GPAmdPcgHistoryLength(void);
+/* how Nfft4GPSolverPcg hands vectors to its matvec / preconditioner callbacks:
+ * -1 (default) device pointers for this library's own operators, host-staged vectors for any other
+ *  function; 0 always host-staged; 1 always device pointers (for user callbacks written for HBM). */
+void Nfft4GPAmdSetCallbackPointerMode(int mode);
 
 /* ---- Nystrom ("RAN") preconditioner apply (SRC/preconds/nys.c:115-173) ----------------------------
  * The reference builds U (n x k), s, eta in Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660);

@@ -76,6 +76,7 @@ _SIGS = {
     "Nfft4GPSolverPcg": (C.c_int, [vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_double, dp,
                                    C.POINTER(dp), ip, C.c_int]),
     "Nfft4GPAmdPcgHistoryLength": (C.c_int, []),
+    "Nfft4GPAmdSetCallbackPointerMode": (None, [C.c_int]),
     "Nfft4GPAmdNysCreate": (vp, [C.c_int, C.c_int, vp, vp, C.c_double, vp]),
     "Nfft4GPAmdNysSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdNysFree": (None, [vp]),

@@ -478,6 +478,63 @@ struct PcgScratch {
 };
 PcgScratch g_pcg;
 
+// ---- operator / preconditioner callbacks of Nfft4GPSolverPcg ----------------------------------
+// The library's own operators take device pointers.  Any other callback (e.g. the reference's
+// Nfft4GPDenseMatSymv on a host matrix) is called the reference's way, with HOST vectors: the
+// adapter stages its input and output through pinned host buffers around the call.  Mode -1 (auto)
+// decides per function pointer; 0 forces host staging, 1 forces device pointers.
+int g_cb_mode = -1;
+
+struct Callbacks {
+   func_symmatvec matvec;
+   void* mat;
+   func_solve prec;
+   void* pdata;
+   bool mv_dev, pc_dev;
+   size_t n;
+   double *h_in = nullptr, *h_out = nullptr;
+   int ensure_host()
+   {
+      if (!h_in) {
+         NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&h_in, sizeof(double) * (n ? n : 1)));
+         NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&h_out, sizeof(double) * (n ? n : 1)));
+      }
+      return 0;
+   }
+   ~Callbacks()
+   {
+      if (h_in) (void)hipHostFree(h_in);
+      if (h_out) (void)hipHostFree(h_out);
+   }
+   // y = alpha A x + beta y on device vectors
+   int apply(double alpha, double* dx, double beta, double* dy)
+   {
+      if (mv_dev) return matvec(mat, (int)n, alpha, dx, beta, dy);
+      if (ensure_host()) return -1;
+      hipStream_t s = current_stream();
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(h_in, dx, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+      if (beta != 0.0) NFFT4GP_HIP_CHECK(hipMemcpyAsync(h_out, dy, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+      NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
+      if (matvec(mat, (int)n, alpha, h_in, beta, h_out)) return -1;
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(dy, h_out, sizeof(double) * n, hipMemcpyHostToDevice, s));
+      return 0;
+   }
+   // z = M^{-1} r on device vectors
+   int solve(double* dz, double* dr)
+   {
+      if (pc_dev) return prec(pdata, (int)n, dz, dr);
+      if (ensure_host()) return -1;
+      hipStream_t s = current_stream();
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(h_in, dr, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+      NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
+      if (prec(pdata, (int)n, h_out, h_in)) return -1;
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(dz, h_out, sizeof(double) * n, hipMemcpyHostToDevice, s));
+      return 0;
+   }
+};
+
+bool library_operator(const void* fn);
+
 int g_last_hist_len = 0;
 
 }  // namespace
@@ -543,6 +600,14 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
    if (!need_device("Nfft4GPSolverPcg")) return -1;
    hipStream_t s = current_stream();
    const size_t N = (size_t)n;
+   Callbacks cb;
+   cb.matvec = matvec;
+   cb.mat = mat_data;
+   cb.prec = precondfunc;
+   cb.pdata = prec_data;
+   cb.n = N;
+   cb.mv_dev = g_cb_mode == 1 || (g_cb_mode == -1 && library_operator((const void*)matvec));
+   cb.pc_dev = g_cb_mode == 1 || (g_cb_mode == -1 && library_operator((const void*)precondfunc));
    Vec vx, vb;
    if (vx.open(x, N, true) || vb.open(rhs, N, true)) return -1;
    double *r = nullptr, *z = nullptr, *p = nullptr, *q = nullptr;
@@ -589,7 +654,7 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
    if (prec_data) NFFT4GP_HIP_CHECK(hipMalloc((void**)&z, sizeof(double) * N));
 
    NFFT4GP_HIP_CHECK(hipMemcpyAsync(r, vb.d, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
-   if (matvec(mat_data, n, -1.0, vx.d, 1.0, r)) {
+   if (cb.apply(-1.0, vx.d, 1.0, r)) {
       cleanup(false);
       return -1;
    }
@@ -652,13 +717,13 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
       while (ii <= maxits && ii - next_check < lag) {
          double* zz = r;
          if (prec_data) {
-            if (precondfunc(prec_data, n, z, r)) { rc = -1; break; }
+            if (cb.solve(z, r)) { rc = -1; break; }
             hipLaunchKernelGGL(k_pcg_dot, dim3(g), dim3(kVecThreads), 0, s, z, r, N, g_pcg.part, g_pcg.ticket, st,
                                rhos, ii, 0);
             zz = z;
          }
          hipLaunchKernelGGL(k_pcg_pupdate, dim3(ge), dim3(kVecThreads), 0, s, p, zz, N, st, rhos, ii);
-         if (matvec(mat_data, n, 1.0, p, 0.0, q)) { rc = -1; break; }
+         if (cb.apply(1.0, p, 0.0, q)) { rc = -1; break; }
          hipLaunchKernelGGL(k_pcg_dot, dim3(g), dim3(kVecThreads), 0, s, q, p, N, g_pcg.part, g_pcg.ticket, st,
                             rhos, ii, 1);
          hipLaunchKernelGGL(k_pcg_xr, dim3(g), dim3(kVecThreads), 0, s, vx.d, r, p, q, N, g_pcg.part, g_pcg.ticket,
@@ -714,7 +779,7 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
       }
       // pcg.c:181-193: recompute the true residual
       NFFT4GP_HIP_CHECK(hipMemcpyAsync(r, vb.d, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
-      if (matvec(mat_data, n, -1.0, vx.d, 1.0, r)) { rc = -1; break; }
+      if (cb.apply(-1.0, vx.d, 1.0, r)) { rc = -1; break; }
       double rr;
       if (dev_dot(r, r, N, &rr)) { rc = -1; break; }
       normr2 = std::sqrt(rr);
@@ -829,3 +894,13 @@ void Nfft4GPAmdNysFree(void* nys)
 }
 
 }  // extern "C"
+
+namespace {
+bool library_operator(const void* fn)
+{
+   return fn == (const void*)&Nfft4GPAdditiveNFFTMatSymv || fn == (const void*)&Nfft4GPNFFTMatSymv ||
+          fn == (const void*)&Nfft4GPAmdNysSolve;
+}
+}  // namespace
+
+extern "C" void Nfft4GPAmdSetCallbackPointerMode(int mode) { g_cb_mode = (mode < -1 || mode > 1) ? -1 : mode; }

@@ -51,10 +51,11 @@ def test_matvec_matches_golden(torch_cuda, name, pre, kernel, l):
         assert rel(g[i * n:(i + 1) * n], gz[i * n:(i + 1) * n]) < 1e-8, i
 
 
-# ---- dense operator of a fixture as a C callback on device vectors --------------------------------
-class DenseDeviceOp:
-    """func_symmatvec over device pointers: y = alpha*K x + beta*y with K the reference's dense additive
-    Gaussian f^2 ((1/nw) sum_c exp(-|x_c - x_c'|^2 / 2 l^2) + mu I) (kernels.c:680-1289, 3099-3494)."""
+# ---- dense operator of a fixture as a plain host C callback -------------------------------------
+class DenseHostOp:
+    """func_symmatvec on HOST vectors (how the reference calls every operator): y = alpha*K x + beta*y
+    with K the reference's dense additive Gaussian f^2 ((1/nw) sum_c exp(-|x_c - x_c'|^2 / 2 l^2) + mu I)
+    (kernels.c:680-1289, 3099-3494).  Nfft4GPSolverPcg stages vectors for it (callback mode -1)."""
 
     def __init__(self, z):
         X, f, l, mu = np.asarray(z["X"]), float(z["f"]), float(z["l"]), float(z["mu"])
@@ -66,23 +67,30 @@ class DenseDeviceOp:
         self.K = f * f * (K / nw + mu * np.eye(n))
         self.n = n
         self.h = None
-        hip = C.CDLL("libamdhip64.so")
-        hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-        self.hip = hip
 
         def mv(_m, nn, alpha, xp, beta, yp):
-            self.hip.hipDeviceSynchronize()
-            xv = np.empty(nn)
-            yv = np.empty(nn)
-            self.hip.hipMemcpy(xv.ctypes.data, xp, 8 * nn, 2)  # D2H
-            self.hip.hipMemcpy(yv.ctypes.data, yp, 8 * nn, 2)
-            out = alpha * (self.K @ xv) + (beta * yv if beta != 0.0 else 0.0)
-            out = np.ascontiguousarray(out, dtype=np.float64)
-            self.hip.hipMemcpy(yp, out.ctypes.data, 8 * nn, 1)  # H2D
+            xv = np.ctypeslib.as_array(C.cast(xp, _lib.dp), shape=(nn,))
+            yv = np.ctypeslib.as_array(C.cast(yp, _lib.dp), shape=(nn,))
+            yv[:] = alpha * (self.K @ xv) + (beta * yv if beta != 0.0 else 0.0)
             return 0
 
         self._cb = _lib.SYMMATVEC(mv)
         self.matvec_fnptr = C.cast(self._cb, C.c_void_p).value
+
+
+class RefDenseOp:
+    """The reference's own Nfft4GPDenseMatSymv (matops.c:3-13, compiled in oracle/_ref) on the dense
+    additive matrix built by its Nfft4GPKernelAdditiveKernel: the drop-in scenario of a reference
+    caller handing its host operator to this library's PCG."""
+
+    def __init__(self, z):
+        import oracle as O
+        self.dense = O.RefDenseAdditive(np.asarray(z["X"]), np.asarray(z["windows"], np.int32), int(z["nw"]),
+                                        int(z["dw"]), kernel=0)
+        self.dense.matrices(float(z["f"]), float(z["l"]), float(z["mu"]), grad=False)
+        self.n = self.dense.n
+        self.h = C.cast(self.dense._K, C.c_void_p).value
+        self.matvec_fnptr = C.cast(self.dense.lib.Nfft4GPDenseMatSymv, C.c_void_p).value
 
 
 def test_nystrom_apply_matches_golden(torch_cuda):
@@ -95,11 +103,15 @@ def test_nystrom_apply_matches_golden(torch_cuda):
     assert rel(xd.cpu().numpy(), z["nys_out"]) <= 1e-12
 
 
+@pytest.mark.parametrize("opkind", ["numpy", "reference"])
 @pytest.mark.parametrize("with_nys", [False, True])
-def test_pcg_matches_golden(torch_cuda, with_nys):
+def test_pcg_matches_golden(torch_cuda, with_nys, opkind):
     torch = torch_cuda
+    import oracle as O
+    if opkind == "reference" and not O.ref_available():
+        pytest.skip("oracle/_ref not built")
     z = load("pcg_synth")
-    op = DenseDeviceOp(z)
+    op = DenseHostOp(z) if opkind == "numpy" else RefDenseOp(z)
     pre = amd.NystromPrecond(z["nys_U"], z["nys_s"], float(z["nys_eta"]), z["nys_perm"]) if with_nys else None
     key = "pcgnys" if with_nys else "pcg"
     b = torch.tensor(np.asarray(z["b"]), device="cuda")
@@ -114,3 +126,16 @@ def test_pcg_matches_golden(torch_cuda, with_nys):
     np.testing.assert_allclose(hist[:k], h_ref[:k], rtol=1e-6)
     # pcg.c:188: the converged entry holds the ABSOLUTE true-residual norm
     assert hist[it] == pytest.approx(rr * np.linalg.norm(np.asarray(z["b"])), rel=1e-12)
+
+
+def test_pcg_host_vectors_with_reference_operator(torch_cuda):
+    """Host b / x (the reference's convention end to end) with the reference's dense operator."""
+    import oracle as O
+    if not O.ref_available():
+        pytest.skip("oracle/_ref not built")
+    z = load("pcg_synth")
+    op = RefDenseOp(z)
+    x = np.zeros(op.n)
+    x, rr, hist, it = amd.pcg(op, np.asarray(z["b"]).copy(), x, maxits=1000, tol=1e-6)
+    assert it > 0 and abs(it - int(z["pcg_iters"])) <= max(2, int(z["pcg_iters"]) // 20)
+    assert rel(x, z["pcg_x"]) < 1e-5
