@@ -175,6 +175,27 @@ def run_pcg_single(op, torch, n, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1)
             "pcg_ms_per_iter": 1e3 * t / max(iters if iters > 0 else len(hist) - 1, 1)}
 
 
+def run_pcg_sharded(op, sop, torch, dist, n, rb, re, tol=1e-6, maxits=3000, l_pcg=0.1):
+    """Row-sharded CG (dist.py, pcg.c semantics): local HIP BLAS-1 + scalar all-reduces."""
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import GpuVecOps
+    assert op.setup(amd.GAUSSIAN, f=1.0, l=l_pcg, mu=0.01) == 0
+    rng = np.random.default_rng(906 + 1)
+    b = torch.tensor((rng.random(n) - 0.5)[rb:re], device="cuda")
+    x = torch.zeros(re - rb, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.time()
+    _, relres, hist, iters = sop.pcg(b, x, maxits=maxits, tol=tol, vec=GpuVecOps())
+    torch.cuda.synchronize()
+    t = torch.tensor([time.time() - t0], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = float(t.item())
+    return {"pcg_time_s": t, "pcg_iters": iters, "pcg_rel_res": relres, "pcg_converged": iters > 0,
+            "pcg_precond": "none", "pcg_tol": tol, "pcg_l": l_pcg, "pcg_impl": "row-sharded (dist.py)",
+            "pcg_ms_per_iter": 1e3 * t / max(iters if iters > 0 else len(hist) - 1, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -197,11 +218,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; NFFT4GP_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on
+    # one GPU (RCCL refuses duplicate devices); the driver's multi-GPU runs use the default, nccl (RCCL)
+    dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local_rank)
+        dist.init_process_group(os.environ.get("NFFT4GP_BENCH_BACKEND", "nccl"))
     L = amd.lib()
     L.Nfft4GPAmdSetStream(torch.cuda.current_stream().cuda_stream)
 
@@ -212,8 +235,9 @@ def main():
         op = amd.NFFTAdditiveKernel(X, win, d, 1)
         rb, re = 0, n
     else:
-        per = (n + world - 1) // world
-        rb, re = min(n, rank * per), min(n, (rank + 1) * per)
+        from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import (
+            RowShardedAdditiveKernel, row_range)
+        rb, re = row_range(n, rank, world)
         op = amd.NFFTAdditiveKernel(X, win, d, 1, shard=(rb, re))
     t0 = time.time()
     rc = op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01)
@@ -222,15 +246,13 @@ def main():
         raise SystemExit("setup failed")
     xd = torch.tensor(x_host[rb:re], device="cuda")
     yd = torch.zeros(re - rb, dtype=torch.float64, device="cuda")
-    grid = torch.zeros(d * 64, dtype=torch.float64, device="cuda")
+    sop = RowShardedAdditiveKernel(op, d, n, rb, re) if world > 1 else None
 
     def step():
         if world == 1:
             op.matsymv(xd, 1.0, 0.0, yd)
         else:
-            op.shard_spread(xd, grid)
-            dist.all_reduce(grid)
-            op.shard_finish(grid, xd, 1.0, 0.0, yd)
+            sop.matsymv(xd, 1.0, 0.0, yd)  # local spread -> all-reduce of the 32x64 grids -> local interp
 
     for _ in range(args.warmup):
         step()
@@ -316,6 +338,8 @@ def main():
                 result["cpu_baseline"] = cpu_baseline(n, d, X, x_host)
             except Exception as e:  # report, do not fail the GPU measurement
                 result["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if world > 1 and not args.no_pcg:
+        result.update(run_pcg_sharded(op, sop, torch, dist, n, rb, re))
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -1,0 +1,127 @@
+"""world_size-2 gloo tests (CPU) of the row-sharded multi-GPU path: the product's distributed operator
+and CG (dist.py) driving the numpy replay of the HIP shard kernels, against the oracle and the
+reference's own pcg.c (oracle/_ref)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def problem(n=3000, d=3, seed=41):
+    rng = np.random.default_rng(seed)
+    X = rng.random((n, d))
+    x = rng.random(n) - 0.5
+    return X, x
+
+
+class EmulatedShard:
+    """shard_spread / shard_finish of the HIP shard handle, replayed in numpy (tests/emulate.py)."""
+
+    def __init__(self, X, windows, rb, re):
+        from emulate import EmulatedPlan
+        self.E = EmulatedPlan(X, windows, shard=(rb, re))
+        self.nw = len(windows)
+
+    def setup(self, kernel, f, l, mu):
+        self.E.setup(kernel, f, l, mu)
+
+    def shard_spread(self, x_local, grid):
+        grid[:] = self.E.spread(np.asarray(x_local)).ravel()
+
+    def shard_finish(self, grid, x_local, alpha=1.0, beta=0.0, y_local=None, grad=False):
+        out = self.E.finish(np.asarray(grid).reshape(self.nw, 64), np.asarray(x_local), alpha, beta,
+                            y_local, grad)
+        if y_local is not None:
+            y_local[:] = out
+        return out
+
+
+def _worker(rank, world, port, outdir, l):
+    import sys
+    for p in (os.path.dirname(HERE), HERE, os.path.join(os.path.dirname(HERE), "oracle")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import (
+        NumpyVecOps, RowShardedAdditiveKernel, row_range)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X, x = problem()
+    n, d = X.shape
+    rb, re = row_range(n, rank, world)
+    eng = EmulatedShard(X, list(range(d)), rb, re)
+    eng.setup(0, 1.0, l, 0.01)
+    op = RowShardedAdditiveKernel(eng, d, n, rb, re)
+    y = np.zeros(re - rb)
+    op.matsymv(x[rb:re].copy(), 1.0, 0.0, y)
+    g = op.matsymv(x[rb:re].copy(), 1.0, 0.0, None, grad=True)
+    b = x[rb:re].copy()
+    xs = np.zeros(re - rb)
+    xs, rr, hist, it = op.pcg(b, xs, maxits=1000, tol=1e-6, vec=NumpyVecOps())
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), y=y, g=g, x=xs, rr=rr, hist=hist, it=it, rb=rb, re=re)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def gloo_run(tmp_path_factory):
+    out = tmp_path_factory.mktemp("gloo")
+    mp.spawn(_worker, args=(2, _free_port(), str(out), 0.1), nprocs=2, join=True)
+    return [dict(np.load(os.path.join(out, f"rank{r}.npz"))) for r in range(2)]
+
+
+def test_row_sharded_matvec_matches_oracle(gloo_run):
+    from oracle import OracleAdditiveNFFT
+    X, x = problem()
+    n, d = X.shape
+    o = OracleAdditiveNFFT(X, np.arange(d, dtype=np.int32), d, 1)
+    o.setup(0, 1.0, 0.1, 0.01)
+    y = np.concatenate([r["y"] for r in gloo_run])
+    assert np.linalg.norm(y - o.matsymv(x)) / np.linalg.norm(o.matsymv(x)) < 1e-8
+    gref = o.gradmatsymv(x)
+    for part in range(3):
+        gp = np.concatenate([r["g"][part * (r["re"] - r["rb"]):(part + 1) * (r["re"] - r["rb"])] for r in gloo_run])
+        gr = gref[part * n:(part + 1) * n]
+        assert np.linalg.norm(gp - gr) / np.linalg.norm(gr) < 1e-8, part
+
+
+def test_row_sharded_pcg_matches_reference_pcg(gloo_run):
+    import oracle as O
+    X, x = problem()
+    n, d = X.shape
+    assert all(int(r["it"]) == int(gloo_run[0]["it"]) for r in gloo_run)
+    xs = np.concatenate([r["x"] for r in gloo_run])
+    assert int(gloo_run[0]["it"]) > 0 and float(gloo_run[0]["rr"]) <= 1e-6
+    o = O.OracleAdditiveNFFT(X, np.arange(d, dtype=np.int32), d, 1)
+    o.setup(0, 1.0, 0.1, 0.01)
+    res = np.linalg.norm(x - o.matsymv(xs)) / np.linalg.norm(x)
+    assert res < 2e-6
+    if O.ref_available():
+        def mv(alpha, xv, beta, yv):
+            yv[:] = o.matsymv(np.array(xv), alpha, beta, np.array(yv))
+        x_ref, rr_ref, hist_ref, it_ref = O.ref_pcg(mv, n, x, maxits=1000, tol=1e-6)
+        it = int(gloo_run[0]["it"])
+        assert abs(it - it_ref) <= max(2, it_ref // 20), (it, it_ref)
+        np.testing.assert_allclose(gloo_run[0]["hist"][:8], hist_ref[:8], rtol=1e-6)
+        assert np.linalg.norm(xs - x_ref) / np.linalg.norm(x_ref) < 1e-4
+
+
+def test_row_range_covers_rows():
+    from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import row_range
+    for n, w in [(10, 3), (7, 8), (1000000, 8), (5, 1)]:
+        rs = [row_range(n, r, w) for r in range(w)]
+        assert rs[0][0] == 0 and rs[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
