@@ -198,7 +198,8 @@ int Nfft4GPAmdShardFinish(void *str, const NFFT4GP_DOUBLE *grid, int grad, NFFT4
 
 /* ---- host-only helpers (no GPU needed): the setup math of the device plan, exported so the CPU
  * test-suite can check it and emulate the kernels against the oracle ------------------------------- */
-/* tap polynomial coefficients C[t*12 + d], t = 0..9, d = 0..11 (monomials in u = frac - 1/2) */
+/* tap polynomial coefficients C[t*NC + d], t = 0..9, d = 0..NC-1 (monomials in u = frac - 1/2);
+ * returns NC, the coefficients per tap (C == NULL: only returns NC) */
 int Nfft4GPAmdHostTapPoly(NFFT4GP_DOUBLE *C);
 /* kernel kind 0 gaussian, 1 xx_gaussian, 2 laplacian_rbf, 3 der_laplacian_rbf with parameter c:
  * bhat[32] (k = -16..15) and the 64-point real circulant w = weight * sum_k bhat_k/phihut_k^2 cos(...) */

@@ -121,6 +121,14 @@ def lib():
             raise ExtensionMissing(
                 f"{LIB_PATH} not found: build it with `make -C {os.path.join(PKG_DIR, 'csrc')}` "
                 "(or __graft_entry__.build()). There is no CPU fallback.")
+        # One HIP runtime per process.  PyTorch-ROCm bundles its own libamdhip64.so.7; when torch is
+        # installed it is loaded FIRST, so this library's libamdhip64.so.7 dependency binds to that
+        # already-loaded runtime.  Loading /opt/rocm's copy first instead puts two HIP/HSA runtimes in
+        # the process and whichever initialises second loses the device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)

@@ -6,7 +6,8 @@
 //   with B the 2m+2 = 10-tap Kaiser-Bessel spreading matrix onto a 64-cell periodic grid and F the
 //   32-mode DFT.  For one component the middle factor is a real 64x64 circulant W (only Re f is used,
 //   nfft_interface.c:436) and each tap is an entire function of the point's offset u in its cell.
-//   We write the 10 taps as degree-11 polynomials in u (max error 3e-13 of the window peak), so
+//   We write the 10 taps as degree-9 polynomials in u (max error 2.5e-10 of the window peak, below
+//   the KB window's own 5e-8 truncation; degree 11 would give 8e-13 at 20 % more VALU work), so
 //     spread : M[cell][d] = sum_{j in cell} alpha_j u_j^d        (per-cell moments)
 //              g[(cell-4+t) mod 64] += sum_d C[t][d] M[cell][d]
 //     grid   : h = W g,   H[cell][d] = sum_t h[(cell-4+t) mod 64] C[t][d]
@@ -30,7 +31,7 @@ constexpr int kNos = 64;            // oversampled grid n_os (nfft_interface.c:2
 constexpr int kBand = 32;           // bandwidth N (nfft_interface.c:18)
 constexpr int kM = 4;               // window cutoff m (nfft_interface.c:20)
 constexpr int kTaps = 2 * kM + 2;   // PRE_PSI taps per dim
-constexpr int kDeg = 11;            // tap polynomial degree
+constexpr int kDeg = 9;             // tap polynomial degree
 constexpr int kNC = kDeg + 1;       // coefficients per cell
 constexpr int kR = 16;              // points per lane-run (chunk)
 constexpr int kWave = 64;
@@ -102,16 +103,11 @@ struct AdditivePlan {
    double f = 1.0, l = 1.0, mu = 0.0;
    double weight = 1.0;  // 1/nwindows
    // layout
-   int B = 4096, CG = 4, ngroups = 0, nblocks = 0;
+   int B = 4096, CG = 3, ngroups = 0, nblocks = 0;  // CG = 3: 3 spread workgroups fit a CU's LDS
    int spread_variant = 1, interp_variant = 1;  // kernel shape variants (nfft_kernels.hip)
-   // grid step fused into the spread tail via global fp64 atomics: measured 1.6x SLOWER at config C
-   // (245 workgroups add into each accumulator address), so off unless NFFT4GP_AMD_FUSED=1
-   bool fused = false;
-   unsigned int* d_tickets = nullptr;           // [ngroups] arrival tickets of the fused spread
    DevLayout dl;
    // device buffers
    double* d_part = nullptr;  // [nblocks][nw][64]
-   double* d_grid = nullptr;  // [nw][64]
    double* d_w = nullptr;     // [nw][64] circulant, kernel
    double* d_wd = nullptr;    // [nw][64] circulant, derivative kernel
    double* d_H = nullptr;     // [nw][64][kNC]
@@ -130,8 +126,6 @@ struct AdditivePlan {
 int upload_tap_coeffs();
 // launchers (nfft_kernels.hip); all enqueue on `stream`
 int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream);
-// spread + grid in one launch (uses d_grid as the self-clearing accumulator and d_tickets)
-int launch_spread_fused(const AdditivePlan& P, const double* d_x, int grad, hipStream_t stream);
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream);
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream);
 int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream);

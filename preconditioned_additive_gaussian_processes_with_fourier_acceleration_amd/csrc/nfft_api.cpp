@@ -27,10 +27,15 @@ hipStream_t current_stream() { return g_stream; }
 
 int device_ok()
 {
-   static int ok = -1;
-   if (ok < 0) {
+   // a positive answer is cached; a negative one is re-queried (and explained) on every call
+   static int ok = 0;
+   if (!ok) {
       int cnt = 0;
-      if (hipGetDeviceCount(&cnt) != hipSuccess) cnt = 0;
+      const hipError_t e = hipGetDeviceCount(&cnt);
+      if (e != hipSuccess) {
+         fprintf(stderr, "nfft4gp_amd: hipGetDeviceCount failed: %s\n", hipGetErrorString(e));
+         cnt = 0;
+      }
       (void)hipGetLastError();
       ok = cnt > 0 ? 1 : 0;
    }
@@ -93,8 +98,6 @@ void free_plan(PlanExt* E)
    if (!E) return;
    AdditivePlan& P = E->P;
    free_layout(P);
-   dfree(P.d_grid);
-   dfree(P.d_tickets);
    dfree(P.d_w);
    dfree(P.d_wd);
    dfree(P.d_H);
@@ -194,13 +197,6 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
    P.dl.ntiles = L.ntiles;
    P.dl.bytes = L.meta.size() * 2 + L.perm2.size() * 4 + L.q.size() * 4 + L.tile_off.size() * 4;
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part, sizeof(double) * (size_t)std::max(1, P.nblocks) * P.nw * kNos));
-   if (!P.d_grid) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_grid, sizeof(double) * (size_t)P.nw * kNos));
-   // the fused spread's accumulator and tickets start at zero and are cleared by each launch's last
-   // arriver, so they need no per-call memset
-   NFFT4GP_HIP_CHECK(hipMemset(P.d_grid, 0, sizeof(double) * (size_t)P.nw * kNos));
-   dfree(P.d_tickets);
-   NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_tickets, sizeof(unsigned int) * (size_t)std::max(1, P.ngroups)));
-   NFFT4GP_HIP_CHECK(hipMemset(P.d_tickets, 0, sizeof(unsigned int) * (size_t)std::max(1, P.ngroups)));
    if (!P.d_H) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_H, sizeof(double) * (size_t)P.nw * kNos * kNC));
    if (!P.d_Hd) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_Hd, sizeof(double) * (size_t)P.nw * kNos * kNC));
    if (upload_tap_coeffs()) return -1;
@@ -259,18 +255,10 @@ int plan_apply_dev(PlanExt* E, int grad, double alpha, const double* d_x, double
       rec = get_rec(E);
       (void)hipEventRecord(rec.ev[0], s);
    }
-   if (P.fused) {
-      if (launch_spread_fused(P, d_x, grad, s)) return -1;
-      if (P.timing) {
-         (void)hipEventRecord(rec.ev[1], s);
-         (void)hipEventRecord(rec.ev[2], s);
-      }
-   } else {
-      if (launch_spread(P, d_x, P.d_part, s)) return -1;
-      if (P.timing) (void)hipEventRecord(rec.ev[1], s);
-      if (launch_grid(P, P.d_part, P.nblocks, grad, s)) return -1;
-      if (P.timing) (void)hipEventRecord(rec.ev[2], s);
-   }
+   if (launch_spread(P, d_x, P.d_part, s)) return -1;
+   if (P.timing) (void)hipEventRecord(rec.ev[1], s);
+   if (launch_grid(P, P.d_part, P.nblocks, grad, s)) return -1;
+   if (P.timing) (void)hipEventRecord(rec.ev[2], s);
    if (launch_interp(P, grad, alpha, d_x, beta, d_y, s)) return -1;
    if (P.timing) {
       (void)hipEventRecord(rec.ev[3], s);
@@ -351,17 +339,13 @@ void env_layout(AdditivePlan& P)
 {
    if (const char* e = getenv("NFFT4GP_AMD_BLOCK")) {
       const int v = atoi(e);
-      if (v >= 256 && v <= 16384) P.B = v;
+      if (v >= 256 && v <= 16384) P.B = v & ~1;  // even: the LDS slice is staged in 16-byte pairs
    }
    if (const char* e = getenv("NFFT4GP_AMD_CG")) {
       const int v = atoi(e);
       if (v >= 1 && v <= 64) P.CG = v;
    }
-   if (const char* e = getenv("NFFT4GP_AMD_SPREAD_VARIANT")) {
-      P.spread_variant = atoi(e);
-      P.fused = false;  // an explicit variant selects the three-launch path
-   }
-   if (const char* e = getenv("NFFT4GP_AMD_FUSED")) P.fused = atoi(e) != 0;
+   if (const char* e = getenv("NFFT4GP_AMD_SPREAD_VARIANT")) P.spread_variant = atoi(e);
    if (const char* e = getenv("NFFT4GP_AMD_INTERP_VARIANT")) P.interp_variant = atoi(e);
 }
 
@@ -618,9 +602,11 @@ int Nfft4GPAmdShardFinish(void* str, const double* grid, int grad, double alpha,
 /* ------------------------------- host-only helpers -------------------------------------------- */
 int Nfft4GPAmdHostTapPoly(double* C)
 {
-   const std::vector<double>& T = tap_poly_coeffs();
-   memcpy(C, T.data(), sizeof(double) * T.size());
-   return 0;
+   if (C) {
+      const std::vector<double>& T = tap_poly_coeffs();
+      memcpy(C, T.data(), sizeof(double) * T.size());
+   }
+   return kNC;
 }
 
 int Nfft4GPAmdHostCirculant(int kind, double c, double weight, double* bhat, double* w)

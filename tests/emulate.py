@@ -18,12 +18,12 @@ R = 16
 NOS = 64
 M = 4
 NTAP = 10
-NC = 12
+NC = amd.lib().Nfft4GPAmdHostTapPoly(None)  # coefficients per tap polynomial (degree + 1)
 
 
 def tap_poly():
     Cm = np.zeros(NTAP * NC)
-    amd.lib().Nfft4GPAmdHostTapPoly(Cm.ctypes.data)
+    assert amd.lib().Nfft4GPAmdHostTapPoly(Cm.ctypes.data) == NC
     return Cm.reshape(NTAP, NC)
 
 

@@ -67,7 +67,9 @@ def test_tap_polynomials_match_window():
         exact = np.array([lib.orc_window_phi(uu + 0.5 + 4 - t) for uu in u])
         approx = np.polynomial.polynomial.polyval(u, Cm[t])
         err = max(err, np.max(np.abs(exact - approx)) / peak)
-    assert err < 1e-12, err
+    # Chebyshev-node interpolation error of the degree-(NC-1) tap polynomials (window.cpp)
+    bound = {12: 1e-12, 10: 5e-10}[Cm.shape[1]]
+    assert err < bound, err
 
 
 def test_bhat_and_circulant_match_oracle():

@@ -16,17 +16,20 @@ op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
 assert op.setup(amd.GAUSSIAN, 1.0, 1.0, 0.01) == 0
 xd = torch.tensor(x, device="cuda"); yd = torch.zeros(n, dtype=torch.float64, device="cuda")
 for _ in range(10): op.matsymv(xd, 1.0, 0.0, yd)
-torch.cuda.synchronize(); op.timing(True); t = time.perf_counter()
-for _ in range(100): op.matsymv(xd, 1.0, 0.0, yd)
+torch.cuda.synchronize(); t = time.perf_counter()
+for _ in range(200): op.matsymv(xd, 1.0, 0.0, yd)
 torch.cuda.synchronize(); el = time.perf_counter() - t
-tq = op.timing_query()
-print(json.dumps({"ms": round(el * 10, 4), **{k: round(v[0] / v[1], 4) for k, v in tq.items()}}))
+kb = {k: round(op.kernel_bench(k, xd, yd, reps=100), 4) for k in op.KERNELS}
+print(json.dumps({"ms": round(el * 5, 4), **kb}))
 ''' % ROOT
 configs = sys.argv[1:] or ["4096,4,0,0"]
 for cfg in configs:
     B, CG, SV, IV = cfg.split(",")
-    env = dict(os.environ, NFFT4GP_AMD_BLOCK=B, NFFT4GP_AMD_CG=CG, NFFT4GP_AMD_SPREAD_VARIANT=SV,
-               NFFT4GP_AMD_INTERP_VARIANT=IV)
+    env = dict(os.environ, NFFT4GP_AMD_BLOCK=B, NFFT4GP_AMD_CG=CG)
+    if SV != "-":
+        env["NFFT4GP_AMD_SPREAD_VARIANT"] = SV
+    if IV != "-":
+        env["NFFT4GP_AMD_INTERP_VARIANT"] = IV
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr[-300:]
     print(f"B={B} CG={CG} SV={SV} IV={IV} {line}", flush=True)

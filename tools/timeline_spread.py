@@ -1,4 +1,4 @@
-"""Per-workgroup timeline of k_spread (diagnostic variant 13, s_memrealtime stamps at 100 MHz)."""
+"""Per-workgroup timeline of k_spread (diagnostic variant 4, s_memrealtime stamps at 100 MHz)."""
 import ctypes as C
 import os
 import sys
@@ -6,7 +6,7 @@ import sys
 import numpy as np
 import torch
 
-os.environ["NFFT4GP_AMD_SPREAD_VARIANT"] = "13"
+os.environ["NFFT4GP_AMD_SPREAD_VARIANT"] = "4"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd  # noqa: E402
 
