@@ -41,14 +41,14 @@ def make_problem(n, d, seed=906):
 
 
 def algorithmic_bytes(info, n, nw, beta_zero=True):
-    """Bytes each kernel must move with this layout ('Roofline'):
-    spread: 6 B per (point, window) [u16 index + u32 fixed-point coordinate] + 8n (alpha)
+    """Bytes each kernel must move with this layout:
+    spread: 5 B per (point, window) [12-bit local index + 26-bit offset in the cell] + 8n (alpha)
             + nblocks*nw*64*8 (partial grids);
-    interp: 6 B per (point, window) + 8n (x for the mu term) + 8n (y write) [+ 8n y read if beta != 0]."""
+    interp: 5 B per (point, window) + 8n (x for the mu term) + 8n (y write) [+ 8n y read if beta != 0]."""
     pc = n * nw
     parts = info["nblocks"] * nw * 64 * 8
-    spread = 6 * pc + 8 * n + parts
-    interp = 6 * pc + 16 * n + (0 if beta_zero else 8 * n)
+    spread = 5 * pc + 8 * n + parts
+    interp = 5 * pc + 16 * n + (0 if beta_zero else 8 * n)
     return spread, interp
 
 

@@ -35,6 +35,7 @@ constexpr int kDeg = 9;             // tap polynomial degree
 constexpr int kNC = kDeg + 1;       // coefficients per cell
 constexpr int kR = 16;              // points per lane-run (chunk)
 constexpr int kWave = 64;
+constexpr int kMaxBlock = 4094;     // points per block: local index and the dummy index B fit 12 bits
 
 #define NFFT4GP_HIP_CHECK(expr)                                                                    \
    do {                                                                                            \
@@ -67,14 +68,14 @@ __host__ __device__ inline size_t quad_index(long long t, int w, int lane, int n
 struct Layout {
    int n = 0;           // local points
    int nw = 0;          // components
-   int B = 4096;        // block size (points)
+   int B = kMaxBlock;   // block size (points)
    int CG = 8;          // components per spread group
    int ngroups = 0;
    int nblocks = 0;
    long long ntiles = 0;
    std::vector<uint16_t> meta;     // [ntiles*64]      comp<<6 | cell
-   std::vector<uint32_t> perm2;    // [ntiles*R/2*64]  two 16-bit local indices
-   std::vector<uint32_t> q;        // [ntiles*R*64]    32-bit fixed-point coordinate (x mod 1)
+   std::vector<uint32_t> lo;       // [ntiles*R/4*64]  local index bits 0-5, one byte per point
+   std::vector<uint32_t> q;        // [ntiles*R*64]    offset in cell (26 bits) | index bits 6-11
    std::vector<int> tile_off;      // [nblocks*ngroups+1]
 };
 // build from per-component quantized coordinates qc[c*n + j]
@@ -83,7 +84,7 @@ void build_layout(const std::vector<uint32_t>& qc, int n, int nw, int B, int CG,
 // ---- device plan --------------------------------------------------------------------------------
 struct DevLayout {
    uint16_t* meta = nullptr;
-   uint32_t* perm2 = nullptr;
+   uint32_t* lo = nullptr;
    uint32_t* q = nullptr;
    int* tile_off = nullptr;
    long long ntiles = 0;
@@ -103,8 +104,9 @@ struct AdditivePlan {
    double f = 1.0, l = 1.0, mu = 0.0;
    double weight = 1.0;  // 1/nwindows
    // layout
-   int B = 4096, CG = 3, ngroups = 0, nblocks = 0;  // CG = 3: 3 spread workgroups fit a CU's LDS
+   int B = kMaxBlock, CG = 3, ngroups = 0, nblocks = 0;  // CG = 3: 3 spread workgroups fit a CU's LDS
    int spread_variant = 1, interp_variant = 1;  // kernel shape variants (nfft_kernels.hip)
+   int gpw = 1;                                  // window groups per spread workgroup (alpha staged once)
    DevLayout dl;
    // device buffers
    double* d_part = nullptr;  // [nblocks][nw][64]

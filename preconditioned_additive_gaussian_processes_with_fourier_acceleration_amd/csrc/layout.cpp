@@ -4,16 +4,19 @@
 // coefficients afterwards (nfft_interface.c:150 `_scale < 0` test, :216-254).  We exploit that by
 // bucketing, once, every block of B consecutive points by oversampled-grid cell, per component:
 //
-//   block b = points [b*B, (b+1)*B)           (B <= 65535 so a local index fits 16 bits)
+//   block b = points [b*B, (b+1)*B)           (B <= kMaxBlock = 4094: local index + dummy < 2^12)
 //   group g = components [g*CG, (g+1)*CG)
 //   chunk   = up to R points of ONE (component, cell), padded with dummies (local index B, which
 //             the kernels map to a zero alpha / a discarded output slot)
 //   tile    = 64 chunks, one per lane (dealt column-wise, see emit_block_group); a lane's words are
 //             grouped in 16-byte quads, quads lane-fastest, so each lane loads 16 B per instruction
 //             and a wave instruction reads 1 KiB contiguous (quad_index in internal.h):
-//               meta [tile][lane]              u16  comp << 6 | cell
-//               perm2[tile][r/8][lane][r/2%4]  u32  local index of points r and r+1 (16 bits each)
-//               q    [tile][r/4][lane][r%4]    u32  fixed-point x mod 1 (cell = q >> 26)
+//               meta [tile][lane]            u16  comp << 6 | cell
+//               q    [tile][r/4][lane][r%4]  u32  bits 0-25: offset in the cell (2^-26 units),
+//                                                 bits 26-31: local index bits 6-11
+//               lo   [tile][0][lane][r/4]    u32  byte r%4 = local index bits 0-5
+//             5 bytes per (point, window): the chunk's cell lives in meta, so the coordinate word's
+//             top 6 bits carry half of the 12-bit local index instead.
 //   tile_off[b*ngroups + g] = first tile of (b, g); the spread kernel gets one workgroup per (b, g),
 //   the interpolation kernel one workgroup per b (all groups).
 #include <algorithm>
@@ -28,9 +31,15 @@ namespace {
 struct ChunkSink {
    // count-only pass when arrays are null
    uint16_t* meta;
-   uint32_t* perm2;
+   uint32_t* lo;
    uint32_t* q;
 };
+
+inline uint32_t slot_word(uint32_t loc, uint32_t frac) { return ((loc >> 6) << 26) | (frac & 0x3FFFFFFu); }
+inline uint32_t lo_word(const uint32_t* loc4)
+{
+   return (loc4[0] & 63u) | ((loc4[1] & 63u) << 8) | ((loc4[2] & 63u) << 16) | ((loc4[3] & 63u) << 24);
+}
 
 // enumerate the chunks of (block b, group g) in (component, cell) order; returns the number of
 // tiles.  With arrays, writes them into tiles [t0, t0 + T) where T = ntiles: chunk k goes to tile
@@ -48,9 +57,9 @@ long long emit_block_group(const std::vector<uint32_t>& qc, int n, int nw, int B
       for (long long tile = t0; tile < t0 + T; tile++)
          for (int lane = 0; lane < kWave; lane++) {
             out->meta[tile * kWave + lane] = (uint16_t)(c0 << 6);
-            for (int r2 = 0; r2 < kR / 2; r2++)
-               out->perm2[quad_index(tile, r2, lane, kR / 2)] = (uint32_t)B | ((uint32_t)B << 16);
-            for (int r = 0; r < kR; r++) out->q[quad_index(tile, r, lane, kR)] = 0u;
+            const uint32_t dummy4[4] = {(uint32_t)B, (uint32_t)B, (uint32_t)B, (uint32_t)B};
+            for (int r4 = 0; r4 < kR / 4; r4++) out->lo[quad_index(tile, r4, lane, kR / 4)] = lo_word(dummy4);
+            for (int r = 0; r < kR; r++) out->q[quad_index(tile, r, lane, kR)] = slot_word((uint32_t)B, 0u);
          }
    }
    long long nchunks = 0;
@@ -71,21 +80,19 @@ long long emit_block_group(const std::vector<uint32_t>& qc, int n, int nw, int B
                const long long tile = t0 + chunk % T;
                const int lane = (int)(chunk / T);
                out->meta[tile * kWave + lane] = (uint16_t)((c << 6) | cell);
-               uint16_t loc[kR];
+               uint32_t loc[kR];
                uint32_t qv[kR];
                for (int r = 0; r < kR; r++) {
                   const int sidx = s + r;
                   if (sidx < off[cell + 1]) {
                      loc[r] = sorted[sidx];
-                     qv[r] = qq[loc[r]];
+                     qv[r] = slot_word(loc[r], qq[loc[r]]);
                   } else {
-                     loc[r] = (uint16_t)B;  // dummy: zero alpha / discarded output
-                     qv[r] = (uint32_t)cell << 26;
+                     loc[r] = (uint32_t)B;  // dummy: zero alpha / discarded output
+                     qv[r] = slot_word(loc[r], 0u);
                   }
                }
-               for (int r2 = 0; r2 < kR / 2; r2++)
-                  out->perm2[quad_index(tile, r2, lane, kR / 2)] =
-                      (uint32_t)loc[2 * r2] | ((uint32_t)loc[2 * r2 + 1] << 16);
+               for (int r4 = 0; r4 < kR / 4; r4++) out->lo[quad_index(tile, r4, lane, kR / 4)] = lo_word(loc + 4 * r4);
                for (int r = 0; r < kR; r++) out->q[quad_index(tile, r, lane, kR)] = qv[r];
             }
             nchunks++;
@@ -135,9 +142,9 @@ void build_layout(const std::vector<uint32_t>& qc, int n, int nw, int B, int CG,
    L.tile_off[nbg] = (int)acc;
    L.ntiles = acc;
    L.meta.assign((size_t)acc * kWave, 0);
-   L.perm2.assign((size_t)acc * (kR / 2) * kWave, 0);
+   L.lo.assign((size_t)acc * (kR / 4) * kWave, 0);
    L.q.assign((size_t)acc * kR * kWave, 0);
-   ChunkSink sink{L.meta.data(), L.perm2.data(), L.q.data()};
+   ChunkSink sink{L.meta.data(), L.lo.data(), L.q.data()};
    parallel_for(L.nblocks, [&](int b) {
       std::vector<int> cnt(kNos), off(kNos + 1);
       std::vector<uint16_t> sorted(B);

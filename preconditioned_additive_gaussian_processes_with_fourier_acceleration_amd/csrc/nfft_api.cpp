@@ -85,7 +85,7 @@ void dfree(void* p)
 void free_layout(AdditivePlan& P)
 {
    dfree(P.dl.meta);
-   dfree(P.dl.perm2);
+   dfree(P.dl.lo);
    dfree(P.dl.q);
    dfree(P.dl.tile_off);
    P.dl = DevLayout();
@@ -191,11 +191,11 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
    P.ngroups = L.ngroups;
    P.nblocks = L.nblocks;
    free_layout(P);
-   if (upload(&P.dl.meta, L.meta) || upload(&P.dl.perm2, L.perm2) || upload(&P.dl.q, L.q) ||
+   if (upload(&P.dl.meta, L.meta) || upload(&P.dl.lo, L.lo) || upload(&P.dl.q, L.q) ||
        upload(&P.dl.tile_off, L.tile_off))
       return -1;
    P.dl.ntiles = L.ntiles;
-   P.dl.bytes = L.meta.size() * 2 + L.perm2.size() * 4 + L.q.size() * 4 + L.tile_off.size() * 4;
+   P.dl.bytes = L.meta.size() * 2 + L.lo.size() * 4 + L.q.size() * 4 + L.tile_off.size() * 4;
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part, sizeof(double) * (size_t)std::max(1, P.nblocks) * P.nw * kNos));
    if (!P.d_H) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_H, sizeof(double) * (size_t)P.nw * kNos * kNC));
    if (!P.d_Hd) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_Hd, sizeof(double) * (size_t)P.nw * kNos * kNC));
@@ -339,13 +339,14 @@ void env_layout(AdditivePlan& P)
 {
    if (const char* e = getenv("NFFT4GP_AMD_BLOCK")) {
       const int v = atoi(e);
-      if (v >= 256 && v <= 16384) P.B = v & ~1;  // even: the LDS slice is staged in 16-byte pairs
+      if (v >= 256) P.B = std::min(v, kMaxBlock) & ~1;  // even: the LDS slice is staged in 16-byte pairs
    }
    if (const char* e = getenv("NFFT4GP_AMD_CG")) {
       const int v = atoi(e);
       if (v >= 1 && v <= 64) P.CG = v;
    }
    if (const char* e = getenv("NFFT4GP_AMD_SPREAD_VARIANT")) P.spread_variant = atoi(e);
+   if (const char* e = getenv("NFFT4GP_AMD_GPW")) P.gpw = std::max(1, atoi(e));
    if (const char* e = getenv("NFFT4GP_AMD_INTERP_VARIANT")) P.interp_variant = atoi(e);
 }
 
@@ -628,9 +629,9 @@ double Nfft4GPAmdHostPrepare(const double* col, int n, unsigned int* q)
 }
 
 int Nfft4GPAmdHostLayout(const unsigned int* qc, int n, int nw, int B, int CG, long long* counts,
-                         unsigned short* meta, unsigned int* perm2, unsigned int* q, int* tile_off)
+                         unsigned short* meta, unsigned int* lo, unsigned int* q, int* tile_off)
 {
-   if (B <= 0 || B > 65535 || CG <= 0 || n < 0 || nw <= 0 || nw > 1023) return -1;
+   if (B <= 0 || B > kMaxBlock || CG <= 0 || n < 0 || nw <= 0 || nw > 1023) return -1;
    std::vector<uint32_t> v(qc, qc + (size_t)n * nw);
    Layout L;
    build_layout(v, n, nw, B, CG, L);
@@ -638,7 +639,7 @@ int Nfft4GPAmdHostLayout(const unsigned int* qc, int n, int nw, int B, int CG, l
    counts[1] = L.ngroups;
    counts[2] = L.nblocks;
    if (meta) memcpy(meta, L.meta.data(), L.meta.size() * sizeof(uint16_t));
-   if (perm2) memcpy(perm2, L.perm2.data(), L.perm2.size() * sizeof(uint32_t));
+   if (lo) memcpy(lo, L.lo.data(), L.lo.size() * sizeof(uint32_t));
    if (q) memcpy(q, L.q.data(), L.q.size() * sizeof(uint32_t));
    if (tile_off) memcpy(tile_off, L.tile_off.data(), L.tile_off.size() * sizeof(int));
    return 0;

@@ -6,7 +6,7 @@
 //             run of a single (window, cell), accumulates the kNC = 10 moments alpha*u^d in registers and
 //             flushes them with ds_add_f64 into an LDS moment table; the workgroup finally folds the
 //             moments into 64-cell partial grids (taps = C * M) and writes them to part[comp][block].
-//             HBM: 6 B per (point, window) -- u16 local index + u32 fixed-point coordinate -- + alpha.
+//             HBM: 5 B per (point, window) -- 12-bit local index + 26-bit offset in the cell -- + alpha.
 //   k_grid    one workgroup per window: sum of the partial grids (fixed order, deterministic), the
 //             64x64 real circulant (= FFT . diag(bhat/phihut^2) . IFFT restricted to Re), and the
 //             per-cell interpolation polynomials H = C^T h.
@@ -53,25 +53,25 @@ __device__ __forceinline__ void stamp(int slot)
 
 struct TileRegs {
    uint32_t mt;
-   uint32_t pp[kR / 2];
-   uint32_t qq[kR];
+   uint32_t lo[kR / 4];  // local index bits 0-5, one byte per point
+   uint32_t qq[kR];      // offset in the cell (bits 0-25) | local index bits 6-11 (bits 26-31)
 };
 
 __device__ __forceinline__ void load_tile(TileRegs& T, const uint16_t* __restrict__ meta,
-                                          const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
+                                          const uint32_t* __restrict__ lo, const uint32_t* __restrict__ qarr,
                                           int t, int lane)
 {
-   // 16 B per lane per load: perm2 quads [t][2][lane], q quads [t][4][lane] (layout.cpp)
+   // 16 B per lane per load: lo quads [t][1][lane], q quads [t][4][lane] (layout.cpp)
    T.mt = meta[(size_t)t * 64 + lane];
-   const uint4* p4 = reinterpret_cast<const uint4*>(perm2) + (size_t)t * (kR / 8) * 64 + lane;
+   const uint4* l4 = reinterpret_cast<const uint4*>(lo) + (size_t)t * (kR / 16) * 64 + lane;
    const uint4* q4 = reinterpret_cast<const uint4*>(qarr) + (size_t)t * (kR / 4) * 64 + lane;
 #pragma unroll
-   for (int k = 0; k < kR / 8; k++) {
-      const uint4 v = p4[k * 64];
-      T.pp[4 * k + 0] = v.x;
-      T.pp[4 * k + 1] = v.y;
-      T.pp[4 * k + 2] = v.z;
-      T.pp[4 * k + 3] = v.w;
+   for (int k = 0; k < kR / 16; k++) {
+      const uint4 v = l4[k * 64];
+      T.lo[4 * k + 0] = v.x;
+      T.lo[4 * k + 1] = v.y;
+      T.lo[4 * k + 2] = v.z;
+      T.lo[4 * k + 3] = v.w;
    }
 #pragma unroll
    for (int k = 0; k < kR / 4; k++) {
@@ -81,6 +81,12 @@ __device__ __forceinline__ void load_tile(TileRegs& T, const uint16_t* __restric
       T.qq[4 * k + 2] = v.z;
       T.qq[4 * k + 3] = v.w;
    }
+}
+
+// local index of point r of the run (0..B-1, or B for a dummy slot)
+__device__ __forceinline__ uint32_t slot_loc(const TileRegs& T, int r)
+{
+   return ((T.qq[r] >> 26) << 6) | ((T.lo[r >> 2] >> (8 * (r & 3))) & 63u);
 }
 
 // Stage x[base, base + nloc) of a block into LDS (zero beyond nloc, up to B), plus two zero pad
@@ -124,10 +130,10 @@ __device__ __forceinline__ void stage_block(double* __restrict__ s, const double
 // ------------------------------------------------------------------------------------------------
 template <int THREADS, bool PREFETCH, bool TIMELINE = false>
 __global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__ meta,
-                                                    const uint32_t* __restrict__ perm2,
+                                                    const uint32_t* __restrict__ lo,
                                                     const uint32_t* __restrict__ qarr,
                                                     const int* __restrict__ tile_off, const double* __restrict__ x,
-                                                    int n, int B, int nblocks, int ngroups, int CG, int nw,
+                                                    int n, int B, int nblocks, int ngroups, int CG, int nw, int gpw,
                                                     double* __restrict__ part)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -135,80 +141,100 @@ __global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__
    double* s_alpha = smem;     // Bp
    double* s_mom = smem + Bp;  // CG*64*kMomStride per-cell moments
 
-   // XCD-aware decode: the ngroups workgroups of one block land on one XCD (blockIdx % 8), so its
-   // alpha slice is fetched into one L2.  Speed only; correctness does not depend on placement.
+   // One workgroup = one block of points x a slice of gpw consecutive window groups: the block's
+   // alpha slice is staged ONCE and reused for every group of the slice, and the next group's first
+   // run is fetched while the current group folds.  XCD-aware decode: the slices of one block land
+   // on one XCD (blockIdx % 8), so its alpha slice is read into one L2.  Placement is speed only.
+   const int nslices = (ngroups + gpw - 1) / gpw;
    const int xcd = blockIdx.x & 7;
    const int rest = blockIdx.x >> 3;
-   const int g = rest % ngroups;
-   const int b = (rest / ngroups) * 8 + xcd;
+   const int slice = rest % nslices;
+   const int b = (rest / nslices) * 8 + xcd;
    if (b >= nblocks) return;
+   const int g_begin = slice * gpw;
+   const int g_end = min(ngroups, g_begin + gpw);
    if (TIMELINE) stamp(0);
 
    const int tid = threadIdx.x;
    const int lane = tid & 63;
    const int wave = tid >> 6;
    constexpr int nwaves = THREADS / 64;
-   const int c0 = g * CG;
-   const int t0 = tile_off[b * ngroups + g];
-   const int t1 = tile_off[b * ngroups + g + 1];
 
    // the first run's loads and the alpha slice are in flight together
    TileRegs cur;
+   int t0 = tile_off[b * ngroups + g_begin];
+   int t1 = tile_off[b * ngroups + g_begin + 1];
    int t = t0 + wave;
-   if (t < t1) load_tile(cur, meta, perm2, qarr, t, lane);
+   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
    const int base = b * B;
    stage_block<THREADS>(s_alpha, x, base, min(B, n - base), B);
    for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
    __syncthreads();
    if (TIMELINE) stamp(1);
 
-   for (; t < t1; t += nwaves) {
-      TileRegs nxt;
-      const int tn = t + nwaves;
-      if (PREFETCH && tn < t1) load_tile(nxt, meta, perm2, qarr, tn, lane);  // prefetch the next run
-      double acc[kNC];
+   for (int g = g_begin; g < g_end; g++) {
+      const int c0 = g * CG;
+      for (; t < t1; t += nwaves) {
+         TileRegs nxt;
+         const int tn = t + nwaves;
+         if (PREFETCH && tn < t1) load_tile(nxt, meta, lo, qarr, tn, lane);  // prefetch the next run
+         double acc[kNC];
 #pragma unroll
-      for (int d = 0; d < kNC; d++) acc[d] = 0.0;
+         for (int d = 0; d < kNC; d++) acc[d] = 0.0;
 #pragma unroll
-      for (int r = 0; r < kR; r++) {
-         const uint32_t loc = (r & 1) ? (cur.pp[r >> 1] >> 16) : (cur.pp[r >> 1] & 0xFFFFu);
-         const double u = q_to_u(cur.qq[r]);
-         double tpow = s_alpha[loc];
-         acc[0] += tpow;
+         for (int r = 0; r < kR; r++) {
+            const uint32_t loc = slot_loc(cur, r);
+            const double u = q_to_u(cur.qq[r]);
+            double tpow = s_alpha[loc];
+            acc[0] += tpow;
 #pragma unroll
-         for (int d = 1; d < kNC; d++) {
-            tpow *= u;
-            acc[d] += tpow;
+            for (int d = 1; d < kNC; d++) {
+               tpow *= u;
+               acc[d] += tpow;
+            }
+         }
+         const int comp_local = (int)(cur.mt >> 6) - c0;
+         const int cell = (int)(cur.mt & 63u);
+         double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
+#pragma unroll
+         for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
+         if (PREFETCH) {
+            if (tn < t1) cur = nxt;
+         } else if (tn < t1) {
+            load_tile(cur, meta, lo, qarr, tn, lane);
          }
       }
-      const int comp_local = (int)(cur.mt >> 6) - c0;
-      const int cell = (int)(cur.mt & 63u);
-      double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
-#pragma unroll
-      for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
-      if (PREFETCH) {
-         if (tn < t1) cur = nxt;
-      } else if (tn < t1) {
-         load_tile(cur, meta, perm2, qarr, tn, lane);
-      }
-   }
-   __syncthreads();
-   if (TIMELINE) stamp(2);
+      __syncthreads();
+      if (TIMELINE && g == g_begin) stamp(2);
 
-   // fold moments into the 64-cell partial grid of every window of this group:
-   //   g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
-   const int ncomp = min(CG, nw - c0);
-   for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
-      const int cl = idx / kNos;
-      const int gi = idx % kNos;
-      double v = 0.0;
-#pragma unroll 1
-      for (int tp = 0; tp < kTaps; tp++) {
-         const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
-#pragma unroll
-         for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
+      // the next group's first run is loaded while this group folds
+      if (g + 1 < g_end) {
+         t0 = t1;
+         t1 = tile_off[b * ngroups + g + 2];
+         t = t0 + wave;
+         if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
       }
-      part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
+
+      // fold moments into the 64-cell partial grid of every window of this group:
+      //   g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
+      const int ncomp = min(CG, nw - c0);
+      for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
+         const int cl = idx / kNos;
+         const int gi = idx % kNos;
+         double v = 0.0;
+#pragma unroll 1
+         for (int tp = 0; tp < kTaps; tp++) {
+            const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
+#pragma unroll
+            for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
+         }
+         part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
+      }
+      if (g + 1 < g_end) {
+         __syncthreads();  // every fold read done before the table is cleared
+         for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
+         __syncthreads();
+      }
    }
    if (TIMELINE) {
       __syncthreads();
@@ -267,22 +293,26 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
    if (from_sum) {
       if (tid < kNos) s_g[tid] = part[(size_t)comp * kNos + tid];
    } else {
-      // 16 strands per cell over this window's contiguous partial grids; 4 independent accumulators
-      // per strand keep loads in flight; fixed order -> deterministic
+      // 16 strands per cell over this window's contiguous partial grids; each strand issues up to
+      // kPer loads before its first add (one memory latency for nparts <= 256); fixed order ->
+      // deterministic
+      constexpr int kPer = 16;
       const int cell = tid & 63;
       const int strand = tid >> 6;
       constexpr int nstr = kGridThreads / 64;
       const double* src = part + (size_t)comp * nparts * kNos + cell;
-      double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-      int p = strand;
-      for (; p + 3 * nstr < nparts; p += 4 * nstr) {
-         s0 += src[(size_t)p * kNos];
-         s1 += src[(size_t)(p + nstr) * kNos];
-         s2 += src[(size_t)(p + 2 * nstr) * kNos];
-         s3 += src[(size_t)(p + 3 * nstr) * kNos];
+      double acc = 0.0;
+      for (int p0 = strand; p0 < nparts; p0 += kPer * nstr) {
+         double v[kPer];
+#pragma unroll
+         for (int k = 0; k < kPer; k++) {
+            const int p = p0 + k * nstr;
+            v[k] = p < nparts ? src[(size_t)p * kNos] : 0.0;
+         }
+#pragma unroll
+         for (int k = 0; k < kPer; k++) acc += v[k];
       }
-      for (; p < nparts; p += nstr) s0 += src[(size_t)p * kNos];
-      s_red[tid] = (s0 + s1) + (s2 + s3);
+      s_red[tid] = acc;
       __syncthreads();
       if (tid < kNos) {
          double v = 0.0;
@@ -315,7 +345,7 @@ constexpr int kEpMax = 8;  // epilogue values per thread held in registers (B <=
 
 template <bool GRAD, int THREADS, bool PREFETCH>
 __global__ __launch_bounds__(THREADS) void k_interp(
-    const uint16_t* __restrict__ meta, const uint32_t* __restrict__ perm2, const uint32_t* __restrict__ qarr,
+    const uint16_t* __restrict__ meta, const uint32_t* __restrict__ lo, const uint32_t* __restrict__ qarr,
     const int* __restrict__ tile_off, const double* __restrict__ H, const double* __restrict__ Hd,
     const double* __restrict__ x, double* __restrict__ y, int n, int B, int ngroups, double alpha, double beta,
     double f, double mu)
@@ -335,7 +365,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
    const int t1 = tile_off[(b + 1) * ngroups];
    TileRegs cur;
    int t = t0 + wave;
-   if (t < t1) load_tile(cur, meta, perm2, qarr, t, lane);
+   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
    // the epilogue's x (mu term) and, when beta != 0, y are fetched now, behind the first run
    const bool ep_regs = B <= kEpMax * THREADS;
    double xe[kEpMax], ye[kEpMax];
@@ -356,7 +386,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
    for (; t < t1; t += nwaves) {
       TileRegs nxt;
       const int tn = t + nwaves;
-      if (PREFETCH && tn < t1) load_tile(nxt, meta, perm2, qarr, tn, lane);  // prefetch the next run
+      if (PREFETCH && tn < t1) load_tile(nxt, meta, lo, qarr, tn, lane);  // prefetch the next run
       const size_t hoff = (size_t)cur.mt * kNC;  // (comp*64 + cell) * kNC: meta is comp<<6|cell
       double hc[kNC], hdc[GRAD ? kNC : 1];
 #pragma unroll
@@ -372,7 +402,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
       }
 #pragma unroll
       for (int r = 0; r < kR; r++) {
-         const uint32_t loc = (r & 1) ? (cur.pp[r >> 1] >> 16) : (cur.pp[r >> 1] & 0xFFFFu);
+         const uint32_t loc = slot_loc(cur, r);
          const double u = q_to_u(cur.qq[r]);
          double v = hc[kNC - 1];
 #pragma unroll
@@ -388,7 +418,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
       if (PREFETCH) {
          if (tn < t1) cur = nxt;
       } else if (tn < t1) {
-         load_tile(cur, meta, perm2, qarr, tn, lane);
+         load_tile(cur, meta, lo, qarr, tn, lane);
       }
    }
    __syncthreads();
@@ -478,7 +508,7 @@ int upload_tap_coeffs()
 }
 
 typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, int, int, int,
-                         int, int, int, double*);
+                         int, int, int, int, double*);
 struct SpreadVariant {
    SpreadFn fn;
    int threads;
@@ -528,9 +558,11 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
    raise_lds_limit_once();
    const SpreadVariant& V = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
-   const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
-   hipLaunchKernelGGL(V.fn, dim3(gridx), dim3(V.threads), spread_lds_bytes(P), stream, P.dl.meta, P.dl.perm2,
-                      P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part);
+   const int gpw = std::min(std::max(P.gpw, 1), P.ngroups);
+   const int nslices = (P.ngroups + gpw - 1) / gpw;
+   const int gridx = ((P.nblocks + 7) / 8) * 8 * nslices;
+   hipLaunchKernelGGL(V.fn, dim3(gridx), dim3(V.threads), spread_lds_bytes(P), stream, P.dl.meta, P.dl.lo,
+                      P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, gpw, d_part);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -567,7 +599,7 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
    raise_lds_limit_once();
    const InterpVariant& V = kInterpVariants[std::min(std::max(P.interp_variant, 0), kNumInterpVariants - 1)];
    hipLaunchKernelGGL(grad ? V.fn_grad : V.fn, dim3(P.nblocks), dim3(V.threads), interp_lds_bytes(P, grad), stream,
-                      P.dl.meta, P.dl.perm2, P.dl.q, P.dl.tile_off, P.d_H, P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups,
+                      P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, P.d_H, P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups,
                       alpha, beta, P.f, P.mu);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;

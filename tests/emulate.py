@@ -41,32 +41,34 @@ def prepare(col):
     return sc, q
 
 
-def layout(qc, n, nw, B=4096, CG=8):
+def layout(qc, n, nw, B=4094, CG=8):
     qc = np.ascontiguousarray(qc, dtype=np.uint32)
     cnt = (C.c_longlong * 3)()
     L = amd.lib()
     assert L.Nfft4GPAmdHostLayout(qc.ctypes.data, n, nw, B, CG, cnt, None, None, None, None) == 0
     ntiles, ngroups, nblocks = cnt[0], cnt[1], cnt[2]
     meta = np.zeros(ntiles * 64, np.uint16)
-    perm2 = np.zeros(ntiles * (R // 2) * 64, np.uint32)
+    lo = np.zeros(ntiles * (R // 4) * 64, np.uint32)
     q = np.zeros(ntiles * R * 64, np.uint32)
     toff = np.zeros(nblocks * ngroups + 1, np.int32)
-    assert L.Nfft4GPAmdHostLayout(qc.ctypes.data, n, nw, B, CG, cnt, meta.ctypes.data, perm2.ctypes.data,
+    assert L.Nfft4GPAmdHostLayout(qc.ctypes.data, n, nw, B, CG, cnt, meta.ctypes.data, lo.ctypes.data,
                                   q.ctypes.data, toff.ctypes.data) == 0
     # unpack the 16-byte-quad layout [tile][w/4][lane][w%4] (layout.cpp) to [tile][lane][w]
-    p2 = perm2.reshape(ntiles, R // 8, 64, 4).transpose(0, 2, 1, 3).reshape(ntiles, 64, R // 2)
-    loc = np.empty((ntiles, 64, R), np.int64)
-    loc[:, :, 0::2] = p2 & 0xFFFF
-    loc[:, :, 1::2] = p2 >> 16
+    lw = lo.reshape(ntiles, R // 16, 64, 4).transpose(0, 2, 1, 3).reshape(ntiles, 64, R // 4).astype(np.int64)
     qq = q.reshape(ntiles, R // 4, 64, 4).transpose(0, 2, 1, 3).reshape(ntiles, 64, R).astype(np.int64)
+    lob = np.empty((ntiles, 64, R), np.int64)
+    for k in range(4):
+        lob[:, :, k::4] = (lw >> (8 * k)) & 63
+    loc = ((qq >> 26) << 6) | lob                      # 12-bit local index (B for dummies)
+    frac = qq & 0x3FFFFFF                              # offset in the cell, 2^-26 units
     return dict(ntiles=ntiles, ngroups=ngroups, nblocks=nblocks, meta=meta.reshape(ntiles, 64).astype(np.int64),
-                loc=loc, q=qq, tile_off=toff, B=B, CG=CG)
+                loc=loc, q=frac, tile_off=toff, B=B, CG=CG)
 
 
 class EmulatedPlan:
     """Host setup + numpy replay of the device plan for 1-D windows (rows [rb, re) of n_global)."""
 
-    def __init__(self, X, windows, B=4096, CG=8, shard=None):
+    def __init__(self, X, windows, B=4094, CG=8, shard=None):
         X = np.asarray(X, dtype=np.float64)
         self.n_global = X.shape[0]
         self.windows = list(windows)

@@ -102,7 +102,7 @@ def test_prepare_matches_reference_scaling():
     assert prepare(np.full(10, 3.0))[0] == -1.0
 
 
-@pytest.mark.parametrize("n,B,CG", [(10000, 4096, 8), (5000, 1000, 3), (777, 4096, 2)])
+@pytest.mark.parametrize("n,B,CG", [(10000, 4094, 8), (5000, 1000, 3), (777, 4094, 2), (9000, 256, 3)])
 def test_layout_invariants(n, B, CG):
     nw = 5
     rng = np.random.default_rng(n)
@@ -127,8 +127,9 @@ def test_layout_invariants(n, B, CG):
             tt, ll, rr = np.nonzero(real)
             j = b * B + loc[t0:t1][tt, ll, rr]
             c = cc[tt, ll]
-            assert np.all(q[t0:t1][tt, ll, rr] == qc[c, j])
-            assert np.all((qc[c, j] >> 26) == cell[t0:t1][tt, ll])
+            assert np.all(q[t0:t1][tt, ll, rr] == (qc[c, j] & 0x3FFFFFF))   # offset in the cell
+            assert np.all((qc[c, j] >> 26) == cell[t0:t1][tt, ll])          # the chunk's cell
+            assert np.all(loc[t0:t1][~real] == B)                            # dummies -> pad slot
             np.add.at(seen, (c, j), 1)
     assert np.all(seen == 1)  # every (window, point) exactly once
 

@@ -1,6 +1,6 @@
 """Sweep layout knobs (block size B, windows per spread group CG) and kernel variants for the config-C
 matvec.  Each setting runs in a fresh subprocess (env vars are read at handle creation).
-usage: python tools/sweep_layout.py "B,CG,SV,IV" ..."""
+usage: python tools/sweep_layout.py "B,CG,SV,IV[,GPW]" ...   ("-" keeps the library default)"""
 import os
 import subprocess
 import sys
@@ -24,12 +24,16 @@ print(json.dumps({"ms": round(el * 5, 4), **kb}))
 ''' % ROOT
 configs = sys.argv[1:] or ["4096,4,0,0"]
 for cfg in configs:
-    B, CG, SV, IV = cfg.split(",")
+    parts = cfg.split(",")
+    B, CG, SV, IV = parts[:4]
+    GPW = parts[4] if len(parts) > 4 else "-"
     env = dict(os.environ, NFFT4GP_AMD_BLOCK=B, NFFT4GP_AMD_CG=CG)
+    if GPW != "-":
+        env["NFFT4GP_AMD_GPW"] = GPW
     if SV != "-":
         env["NFFT4GP_AMD_SPREAD_VARIANT"] = SV
     if IV != "-":
         env["NFFT4GP_AMD_INTERP_VARIANT"] = IV
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr[-300:]
-    print(f"B={B} CG={CG} SV={SV} IV={IV} {line}", flush=True)
+    print(f"B={B} CG={CG} SV={SV} IV={IV} GPW={GPW} {line}", flush=True)
