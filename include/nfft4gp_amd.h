@@ -208,7 +208,7 @@ int Nfft4GPAmdHostCirculant(int kind, NFFT4GP_DOUBLE c, NFFT4GP_DOUBLE weight, N
 /* centre + scale one 1-D window exactly as nfft_interface.c:150-213 and quantize to 32-bit fixed point;
  * returns the scale (or -1 if all points coincide) */
 NFFT4GP_DOUBLE Nfft4GPAmdHostPrepare(const NFFT4GP_DOUBLE *col, int n, unsigned int *q);
-/* chunk layout of per-window quantized coordinates qc[c*n + j] (B <= 4094); call with NULL arrays to
+/* chunk layout of per-window quantized coordinates qc[c*n + j] (B <= 4064); call with NULL arrays to
  * get counts[0] = ntiles, counts[1] = ngroups, counts[2] = nblocks, then with arrays of
  * ntiles*64 (meta), ntiles*4*64 (lo: local index bits 0-5, a byte per point), ntiles*16*64 (q: offset
  * in the cell in bits 0-25, local index bits 6-11 in bits 26-31), nblocks*ngroups+1 (tile_off) */

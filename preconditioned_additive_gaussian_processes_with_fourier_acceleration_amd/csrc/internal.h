@@ -35,7 +35,8 @@ constexpr int kDeg = 9;             // tap polynomial degree
 constexpr int kNC = kDeg + 1;       // coefficients per cell
 constexpr int kR = 16;              // points per lane-run (chunk)
 constexpr int kWave = 64;
-constexpr int kMaxBlock = 4094;     // points per block: local index and the dummy index B fit 12 bits
+constexpr int kPad = 32;            // pad entries after a block's B points (dummy slots, one per bank)
+constexpr int kMaxBlock = 4096 - kPad;  // points per block: local index and pad entries fit 12 bits
 
 #define NFFT4GP_HIP_CHECK(expr)                                                                    \
    do {                                                                                            \

@@ -4,10 +4,12 @@
 // coefficients afterwards (nfft_interface.c:150 `_scale < 0` test, :216-254).  We exploit that by
 // bucketing, once, every block of B consecutive points by oversampled-grid cell, per component:
 //
-//   block b = points [b*B, (b+1)*B)           (B <= kMaxBlock = 4094: local index + dummy < 2^12)
+//   block b = points [b*B, (b+1)*B)           (B <= kMaxBlock = 4064: local index and the 32 pad
+//                                               entries B .. B+31 used by dummies fit 12 bits)
 //   group g = components [g*CG, (g+1)*CG)
-//   chunk   = up to R points of ONE (component, cell), padded with dummies (local index B, which
-//             the kernels map to a zero alpha / a discarded output slot)
+//   chunk   = up to R points of ONE (component, cell), padded with dummies (local index B + lane%32,
+//             pad entries the kernels hold at zero alpha / discard as output); the points of a chunk
+//             are ordered per tile to spread the lanes over LDS banks (balance_tile)
 //   tile    = 64 chunks, one per lane (dealt column-wise, see emit_block_group); a lane's words are
 //             grouped in 16-byte quads, quads lane-fastest, so each lane loads 16 B per instruction
 //             and a wave instruction reads 1 KiB contiguous (quad_index in internal.h):
@@ -41,6 +43,36 @@ inline uint32_t lo_word(const uint32_t* loc4)
    return (loc4[0] & 63u) | ((loc4[1] & 63u) << 8) | ((loc4[2] & 63u) << 16) | ((loc4[3] & 63u) << 24);
 }
 
+// Order the 16 points of every lane's run so that, at each point slot r, the 64 lanes of a tile hit
+// different LDS banks: the spread gathers alpha[loc] with ds_read_b64 (bank pair = loc mod 32 within
+// each 32-lane half) and the interpolation adds into y[loc] with ds_add_f64 (loc mod 16 within each
+// 16-lane quarter).  Random order costs ~4-way conflicts; a greedy pass per slot gets close to
+// conflict-free.  Dummy slots point at pad entry B + lane % 32 (distinct banks, no same-address
+// atomics).  Any order is correct: the sums over a run are order-independent up to rounding.
+void balance_tile(uint32_t (*loc)[kR], uint32_t (*fr)[kR])
+{
+   for (int r = 0; r < kR; r++) {
+      int c32[2][32] = {};
+      int c16[4][16] = {};
+      for (int lane = 0; lane < kWave; lane++) {
+         int best = r, best_cost = 1 << 30;
+         for (int k = r; k < kR; k++) {
+            const uint32_t v = loc[lane][k];
+            const int cost = 2 * c32[lane >> 5][v & 31] + c16[lane >> 4][v & 15];
+            if (cost < best_cost) {
+               best_cost = cost;
+               best = k;
+               if (cost == 0) break;
+            }
+         }
+         std::swap(loc[lane][r], loc[lane][best]);
+         std::swap(fr[lane][r], fr[lane][best]);
+         c32[lane >> 5][loc[lane][r] & 31]++;
+         c16[lane >> 4][loc[lane][r] & 15]++;
+      }
+   }
+}
+
 // enumerate the chunks of (block b, group g) in (component, cell) order; returns the number of
 // tiles.  With arrays, writes them into tiles [t0, t0 + T) where T = ntiles: chunk k goes to tile
 // t0 + k % T, lane k / T ("dealt" column-wise), so the 64 lanes of a tile hold chunks T apart in the
@@ -52,14 +84,16 @@ long long emit_block_group(const std::vector<uint32_t>& qc, int n, int nw, int B
    const int base = b * B;
    const int nloc = std::min(B, n - base);
    const int c0 = g * CG, c1 = std::min(nw, c0 + CG);
+   // staging of the group's tiles: [tile][lane][r] local index and offset-in-cell
+   std::vector<uint32_t> sloc, sfr;
    if (out) {
-      // every slot of the group's tiles starts as a dummy chunk of the group's first component
-      for (long long tile = t0; tile < t0 + T; tile++)
+      // every slot starts as a dummy chunk of the group's first component
+      sloc.resize((size_t)T * kWave * kR);
+      sfr.assign((size_t)T * kWave * kR, 0u);
+      for (long long tile = 0; tile < T; tile++)
          for (int lane = 0; lane < kWave; lane++) {
-            out->meta[tile * kWave + lane] = (uint16_t)(c0 << 6);
-            const uint32_t dummy4[4] = {(uint32_t)B, (uint32_t)B, (uint32_t)B, (uint32_t)B};
-            for (int r4 = 0; r4 < kR / 4; r4++) out->lo[quad_index(tile, r4, lane, kR / 4)] = lo_word(dummy4);
-            for (int r = 0; r < kR; r++) out->q[quad_index(tile, r, lane, kR)] = slot_word((uint32_t)B, 0u);
+            out->meta[(t0 + tile) * kWave + lane] = (uint16_t)(c0 << 6);
+            for (int r = 0; r < kR; r++) sloc[((size_t)tile * kWave + lane) * kR + r] = (uint32_t)(B + (lane & 31));
          }
    }
    long long nchunks = 0;
@@ -77,25 +111,30 @@ long long emit_block_group(const std::vector<uint32_t>& qc, int n, int nw, int B
          for (int s = off[cell]; s < off[cell + 1]; s += kR) {
             if (out) {
                const long long chunk = nchunks;
-               const long long tile = t0 + chunk % T;
+               const long long tile = chunk % T;
                const int lane = (int)(chunk / T);
-               out->meta[tile * kWave + lane] = (uint16_t)((c << 6) | cell);
-               uint32_t loc[kR];
-               uint32_t qv[kR];
+               out->meta[(t0 + tile) * kWave + lane] = (uint16_t)((c << 6) | cell);
                for (int r = 0; r < kR; r++) {
                   const int sidx = s + r;
+                  const size_t k = ((size_t)tile * kWave + lane) * kR + r;
                   if (sidx < off[cell + 1]) {
-                     loc[r] = sorted[sidx];
-                     qv[r] = slot_word(loc[r], qq[loc[r]]);
-                  } else {
-                     loc[r] = (uint32_t)B;  // dummy: zero alpha / discarded output
-                     qv[r] = slot_word(loc[r], 0u);
-                  }
+                     sloc[k] = sorted[sidx];
+                     sfr[k] = qq[sorted[sidx]] & 0x3FFFFFFu;
+                  }  // else: stays a dummy (pad entry B + lane % 32: zero alpha / discarded output)
                }
-               for (int r4 = 0; r4 < kR / 4; r4++) out->lo[quad_index(tile, r4, lane, kR / 4)] = lo_word(loc + 4 * r4);
-               for (int r = 0; r < kR; r++) out->q[quad_index(tile, r, lane, kR)] = qv[r];
             }
             nchunks++;
+         }
+      }
+   }
+   if (out) {
+      for (long long tile = 0; tile < T; tile++) {
+         auto* L = reinterpret_cast<uint32_t(*)[kR]>(sloc.data() + (size_t)tile * kWave * kR);
+         auto* F = reinterpret_cast<uint32_t(*)[kR]>(sfr.data() + (size_t)tile * kWave * kR);
+         balance_tile(L, F);
+         for (int lane = 0; lane < kWave; lane++) {
+            for (int r4 = 0; r4 < kR / 4; r4++) out->lo[quad_index(t0 + tile, r4, lane, kR / 4)] = lo_word(L[lane] + 4 * r4);
+            for (int r = 0; r < kR; r++) out->q[quad_index(t0 + tile, r, lane, kR)] = slot_word(L[lane][r], F[lane][r]);
          }
       }
    }

@@ -90,7 +90,7 @@ __device__ __forceinline__ uint32_t slot_loc(const TileRegs& T, int r)
 }
 
 // Stage x[base, base + nloc) of a block into LDS (zero beyond nloc, up to B), plus two zero pad
-// entries s[B], s[B+1] that the layout's dummy slots point at.  Every thread issues ALL its 16-byte
+// entries s[B .. B+kPad) that the layout's dummy slots point at.  Every thread issues ALL its 16-byte
 // loads before its first LDS write, so the slice costs one memory latency instead of B/THREADS.
 template <int THREADS>
 __device__ __forceinline__ void stage_block(double* __restrict__ s, const double* __restrict__ x, int base, int nloc,
@@ -119,10 +119,7 @@ __device__ __forceinline__ void stage_block(double* __restrict__ s, const double
          if (i < npair) reinterpret_cast<double2*>(s)[i] = v[u];
       }
    }
-   if (tid == 0) {
-      s[B] = 0.0;
-      s[B + 1] = 0.0;
-   }
+   if (tid < kPad) s[B + tid] = 0.0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -137,7 +134,7 @@ __global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__
                                                     double* __restrict__ part)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
-   const int Bp = B + 2;
+   const int Bp = B + kPad;
    double* s_alpha = smem;     // Bp
    double* s_mom = smem + Bp;  // CG*64*kMomStride per-cell moments
 
@@ -351,7 +348,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
     double f, double mu)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
-   const int Bp = B + 2;
+   const int Bp = B + kPad;
    double* s_y = smem;
    double* s_yd = smem + Bp;  // GRAD only
    const int b = blockIdx.x;
@@ -484,12 +481,12 @@ __global__ __launch_bounds__(THREADS) void k_interp(
 // ------------------------------------------------------------------------------------------------
 static size_t spread_lds_bytes(const AdditivePlan& P)
 {
-   return sizeof(double) * ((size_t)P.B + 2 + (size_t)P.CG * kNos * kMomStride);
+   return sizeof(double) * ((size_t)P.B + kPad + (size_t)P.CG * kNos * kMomStride);
 }
 
 static size_t interp_lds_bytes(const AdditivePlan& P, int grad)
 {
-   return sizeof(double) * ((size_t)P.B + 2) * (grad ? 2 : 1);
+   return sizeof(double) * ((size_t)P.B + kPad) * (grad ? 2 : 1);
 }
 
 int upload_tap_coeffs()

@@ -41,7 +41,7 @@ def prepare(col):
     return sc, q
 
 
-def layout(qc, n, nw, B=4094, CG=8):
+def layout(qc, n, nw, B=4064, CG=8):
     qc = np.ascontiguousarray(qc, dtype=np.uint32)
     cnt = (C.c_longlong * 3)()
     L = amd.lib()
@@ -53,13 +53,17 @@ def layout(qc, n, nw, B=4094, CG=8):
     toff = np.zeros(nblocks * ngroups + 1, np.int32)
     assert L.Nfft4GPAmdHostLayout(qc.ctypes.data, n, nw, B, CG, cnt, meta.ctypes.data, lo.ctypes.data,
                                   q.ctypes.data, toff.ctypes.data) == 0
-    # unpack the 16-byte-quad layout [tile][w/4][lane][w%4] (layout.cpp) to [tile][lane][w]
-    lw = lo.reshape(ntiles, R // 16, 64, 4).transpose(0, 2, 1, 3).reshape(ntiles, 64, R // 4).astype(np.int64)
-    qq = q.reshape(ntiles, R // 4, 64, 4).transpose(0, 2, 1, 3).reshape(ntiles, 64, R).astype(np.int64)
+
+    def quads(a, words):  # the 16-byte-quad layout [tile][w/4][lane][w%4] (layout.cpp) -> [tile][lane][w]
+        return a.reshape(ntiles, words // 4, 64, 4).transpose(0, 2, 1, 3).reshape(ntiles, 64, words)
+
+    # 12-bit local index split over q (bits 26-31) and lo (a byte per point)
+    lw = quads(lo, R // 4).astype(np.int64)
+    qq = quads(q, R).astype(np.int64)
     lob = np.empty((ntiles, 64, R), np.int64)
     for k in range(4):
         lob[:, :, k::4] = (lw >> (8 * k)) & 63
-    loc = ((qq >> 26) << 6) | lob                      # 12-bit local index (B for dummies)
+    loc = ((qq >> 26) << 6) | lob                      # local index (B + lane % 32 for dummies)
     frac = qq & 0x3FFFFFF                              # offset in the cell, 2^-26 units
     return dict(ntiles=ntiles, ngroups=ngroups, nblocks=nblocks, meta=meta.reshape(ntiles, 64).astype(np.int64),
                 loc=loc, q=frac, tile_off=toff, B=B, CG=CG)
@@ -68,7 +72,7 @@ def layout(qc, n, nw, B=4094, CG=8):
 class EmulatedPlan:
     """Host setup + numpy replay of the device plan for 1-D windows (rows [rb, re) of n_global)."""
 
-    def __init__(self, X, windows, B=4094, CG=8, shard=None):
+    def __init__(self, X, windows, B=4064, CG=8, shard=None):
         X = np.asarray(X, dtype=np.float64)
         self.n_global = X.shape[0]
         self.windows = list(windows)
@@ -108,7 +112,7 @@ class EmulatedPlan:
         for b in range(L["nblocks"]):
             base = b * B
             nloc = min(B, self.n - base)
-            alpha = np.zeros(B + 1)
+            alpha = np.zeros(B + 32)  # 32 zero pad entries for the dummy slots
             alpha[:nloc] = x_local[base:base + nloc]
             t0, t1 = L["tile_off"][b * ng], L["tile_off"][(b + 1) * ng]
             a = alpha[L["loc"][t0:t1]]                       # [t][lane][r]
