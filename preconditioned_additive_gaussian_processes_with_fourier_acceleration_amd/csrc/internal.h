@@ -116,6 +116,8 @@ struct AdditivePlan {
    double* d_H = nullptr;     // [nw][64][kNC]
    double* d_Hd = nullptr;
    double* d_C = nullptr;     // [kTaps][kNC]
+   double* d_dot_part = nullptr;         // [nblocks] fused matvec-dot partials
+   unsigned int* d_dot_ticket = nullptr; // arrival counters (reduce.hpp)
    double* d_xs = nullptr;    // staging (host pointer calls)
    double* d_ys = nullptr;    // staging 3n
    // timing
@@ -132,8 +134,12 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream);
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream);
 int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream);
+// d_dot != nullptr (non-grad): also writes (y, x) to *d_dot (device), one grid-wide reduction in the launch
 int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, double beta, double* d_y,
-                  hipStream_t stream);
+                  hipStream_t stream, double* d_dot = nullptr);
+// y = A x (alpha = 1, beta = 0) and *d_dot = (y, x) on device pointers: the matvec + dot of a CG step in
+// the matvec's own three launches (used by Nfft4GPSolverPcg when its operator is this library's)
+int additive_matvec_dot(void* str, const double* d_x, double* d_y, double* d_dot);
 
 hipStream_t current_stream();
 bool is_device_ptr(const void* p);

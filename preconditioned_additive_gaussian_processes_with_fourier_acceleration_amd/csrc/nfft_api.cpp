@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "internal.h"
+#include "reduce.hpp"
 
 using namespace nfft4gp_amd;
 
@@ -90,7 +91,11 @@ void free_layout(AdditivePlan& P)
    dfree(P.dl.tile_off);
    P.dl = DevLayout();
    dfree(P.d_part);
+   dfree(P.d_dot_part);
+   dfree(P.d_dot_ticket);
    P.d_part = nullptr;
+   P.d_dot_part = nullptr;
+   P.d_dot_ticket = nullptr;
 }
 
 void free_plan(PlanExt* E)
@@ -197,6 +202,12 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
    P.dl.ntiles = L.ntiles;
    P.dl.bytes = L.meta.size() * 2 + L.lo.size() * 4 + L.q.size() * 4 + L.tile_off.size() * 4;
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part, sizeof(double) * (size_t)std::max(1, P.nblocks) * P.nw * kNos));
+   dfree(P.d_dot_part);
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_dot_part, sizeof(double) * (size_t)std::max(1, P.nblocks)));
+   if (!P.d_dot_ticket) {
+      NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_dot_ticket, sizeof(unsigned int) * kTicketWords));
+      NFFT4GP_HIP_CHECK(hipMemset(P.d_dot_ticket, 0, sizeof(unsigned int) * kTicketWords));
+   }
    if (!P.d_H) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_H, sizeof(double) * (size_t)P.nw * kNos * kNC));
    if (!P.d_Hd) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_Hd, sizeof(double) * (size_t)P.nw * kNos * kNC));
    if (upload_tap_coeffs()) return -1;
@@ -307,6 +318,7 @@ PlanExt* additive_plan(void* str)
    return (PlanExt*)((nfft4gp_kernel*)str)->_external;
 }
 
+
 nfft4gp_kernel* kernel_struct_create(int max_n)
 {
    nfft4gp_kernel* k = (nfft4gp_kernel*)calloc(1, sizeof(nfft4gp_kernel));
@@ -395,6 +407,19 @@ void* additive_create(double* data, int n_global, int ldim, int* windows, int nw
 }
 
 }  // namespace
+
+namespace nfft4gp_amd {
+int additive_matvec_dot(void* str, const double* d_x, double* d_y, double* d_dot)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready) return -1;
+   AdditivePlan& P = E->P;
+   hipStream_t s = current_stream();
+   if (launch_spread(P, d_x, P.d_part, s)) return -1;
+   if (launch_grid(P, P.d_part, P.nblocks, 0, s)) return -1;
+   return launch_interp(P, 0, 1.0, d_x, 0.0, d_y, s, d_dot);
+}
+}  // namespace nfft4gp_amd
 
 extern "C" {
 

@@ -24,6 +24,7 @@
 #include <cstdio>
 
 #include "internal.h"
+#include "reduce.hpp"
 
 namespace nfft4gp_amd {
 
@@ -340,12 +341,15 @@ __global__ __launch_bounds__(256) void k_reduce_parts(const double* __restrict__
 // ------------------------------------------------------------------------------------------------
 constexpr int kEpMax = 8;  // epilogue values per thread held in registers (B <= kEpMax * THREADS)
 
-template <bool GRAD, int THREADS, bool PREFETCH>
+// DOT (non-GRAD only): also forms (y_out, x) -- the (q, p) of a CG step when y = A p -- with a
+// deterministic grid-wide sum written to *dot_out by the last block (reduce.hpp)
+template <bool GRAD, int THREADS, bool PREFETCH, bool DOT = false>
 __global__ __launch_bounds__(THREADS) void k_interp(
     const uint16_t* __restrict__ meta, const uint32_t* __restrict__ lo, const uint32_t* __restrict__ qarr,
     const int* __restrict__ tile_off, const double* __restrict__ H, const double* __restrict__ Hd,
     const double* __restrict__ x, double* __restrict__ y, int n, int B, int ngroups, double alpha, double beta,
-    double f, double mu)
+    double f, double mu, double* __restrict__ dot_part, unsigned int* __restrict__ dot_ticket,
+    double* __restrict__ dot_out)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = B + kPad;
@@ -421,6 +425,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
    __syncthreads();
 
    const double ff = f * f;
+   double dacc = 0.0;
    double* y0 = y;
    double* y1 = y + n;
    double* y2 = y + 2 * (size_t)n;
@@ -434,7 +439,9 @@ __global__ __launch_bounds__(THREADS) void k_interp(
       const double xj = xe[k];
       if (!GRAD) {
          const double v = ff * (s_y[j] + mu * xj);
-         y[gj] = (beta == 0.0) ? alpha * v : fma(beta, ye[k], alpha * v);
+         const double yo = (beta == 0.0) ? alpha * v : fma(beta, ye[k], alpha * v);
+         y[gj] = yo;
+         if (DOT) dacc = fma(yo, xj, dacc);
       } else {
          // nfft_interface.c:547-549 summed over windows: (2f)(Kx + mu x), ff*dscale*K'x, ff*x
          const double v0 = 2.0 * f * (s_y[j] + mu * xj);
@@ -457,7 +464,9 @@ __global__ __launch_bounds__(THREADS) void k_interp(
          const double xj = x[gj];
          if (!GRAD) {
             const double v = ff * (s_y[j] + mu * xj);
-            y[gj] = (beta == 0.0) ? alpha * v : fma(beta, y[gj], alpha * v);
+            const double yo = (beta == 0.0) ? alpha * v : fma(beta, y[gj], alpha * v);
+            y[gj] = yo;
+            if (DOT) dacc = fma(yo, xj, dacc);
          } else {
             const double v0 = 2.0 * f * (s_y[j] + mu * xj);
             const double v1 = ff * s_yd[j];
@@ -473,6 +482,11 @@ __global__ __launch_bounds__(THREADS) void k_interp(
             }
          }
       }
+   }
+   if (DOT && !GRAD) {
+      dacc = block_sum0<THREADS>(dacc);
+      double tot;
+      if (grid_total<THREADS>(dacc, dot_part, dot_ticket, &tot) && threadIdx.x == 0) *dot_out = tot;
    }
 }
 
@@ -520,16 +534,18 @@ static const SpreadVariant kSpreadVariants[] = {
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
 typedef void (*InterpFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*,
-                         const double*, const double*, double*, int, int, int, double, double, double, double);
+                         const double*, const double*, double*, int, int, int, double, double, double, double,
+                         double*, unsigned int*, double*);
 struct InterpVariant {
-   InterpFn fn, fn_grad;
+   InterpFn fn, fn_grad, fn_dot;
    int threads;
 };
 static const InterpVariant kInterpVariants[] = {
-    {k_interp<false, 1024, true>, k_interp<true, 1024, true>, 1024},    // 0: 16 waves, prefetch
-    {k_interp<false, 1024, false>, k_interp<true, 1024, false>, 1024},  // 1: 16 waves (default)
-    {k_interp<false, 512, true>, k_interp<true, 512, true>, 512},       // 2: 8 waves, prefetch
-    {k_interp<false, 512, false>, k_interp<true, 512, false>, 512},     // 3: 8 waves
+    {k_interp<false, 1024, true>, k_interp<true, 1024, true>, k_interp<false, 1024, true, true>, 1024},  // 0
+    {k_interp<false, 1024, false>, k_interp<true, 1024, false>, k_interp<false, 1024, false, true>,
+     1024},                                                                                            // 1 (default)
+    {k_interp<false, 512, true>, k_interp<true, 512, true>, k_interp<false, 512, true, true>, 512},      // 2
+    {k_interp<false, 512, false>, k_interp<true, 512, false>, k_interp<false, 512, false, true>, 512},   // 3
 };
 constexpr int kNumInterpVariants = sizeof(kInterpVariants) / sizeof(kInterpVariants[0]);
 
@@ -544,6 +560,8 @@ static void raise_lds_limit_once()
       (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
       (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn_grad,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn_dot,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
    }
    (void)hipGetLastError();
@@ -590,14 +608,19 @@ int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_g
 }
 
 int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, double beta, double* d_y,
-                  hipStream_t stream)
+                  hipStream_t stream, double* d_dot)
 {
    if (P.n == 0) return 0;
    raise_lds_limit_once();
    const InterpVariant& V = kInterpVariants[std::min(std::max(P.interp_variant, 0), kNumInterpVariants - 1)];
-   hipLaunchKernelGGL(grad ? V.fn_grad : V.fn, dim3(P.nblocks), dim3(V.threads), interp_lds_bytes(P, grad), stream,
-                      P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, P.d_H, P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups,
-                      alpha, beta, P.f, P.mu);
+   if (d_dot && (grad || P.nblocks > kRedMaxBlocks)) {
+      fprintf(stderr, "nfft4gp_amd: fused matvec-dot needs a plain matvec and <= %d blocks\n", kRedMaxBlocks);
+      return -1;
+   }
+   const InterpFn fn = grad ? V.fn_grad : (d_dot ? V.fn_dot : V.fn);
+   hipLaunchKernelGGL(fn, dim3(P.nblocks), dim3(V.threads), interp_lds_bytes(P, grad), stream, P.dl.meta, P.dl.lo,
+                      P.dl.q, P.dl.tile_off, P.d_H, P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups, alpha, beta, P.f, P.mu,
+                      P.d_dot_part, P.d_dot_ticket, d_dot);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "internal.h"
+#include "reduce.hpp"
 
 using namespace nfft4gp_amd;
 
@@ -97,79 +98,13 @@ struct PcgSlot {   // pinned host memory, written by the last kernel of each ite
 // PCG vector kernels: kEPT independent elements per thread (all loads issued before use), so each
 // lane keeps several HBM requests in flight; grid = ceil(n / (kVecThreads * kEPT)) <= kPcgMaxBlocks.
 constexpr int kEPT = 4;
-constexpr int kPcgMaxBlocks = 2048;
-constexpr int kXcds = 8;
-constexpr int kTicketStride = 64;  // unsigned ints: 256 B between arrival counters
+constexpr int kPcgMaxBlocks = 2048;  // <= kRedMaxBlocks (reduce.hpp)
 
 int pcg_grid(size_t n)
 {
    size_t g = (n + (size_t)kVecThreads * kEPT - 1) / ((size_t)kVecThreads * kEPT);
    if (g > (size_t)kPcgMaxBlocks) g = kPcgMaxBlocks;
    return (int)(g == 0 ? 1 : g);
-}
-
-// partial of this block -> memory-side store, arrival ticket; returns true in every thread of the
-// last arriving block, with the fixed-order total of all partials in *total.  Thread 0 holds `v`.
-__device__ bool grid_total(double v, double* __restrict__ part, unsigned int* __restrict__ ticket, double* total)
-{
-   __shared__ int s_last;
-   __shared__ double s_red[kVecThreads / 64];
-   // hand-off without L2 write-back fences (a release fence here writes back every dirty line the
-   // kernel produced -- measured +15-20 us per launch): the partial goes out as an agent-scope
-   // (sc1, memory-side) store, drained with vmcnt(0) before the ticket RMW; the last arriver reads
-   // the partials with agent-scope loads (MI355X_MICROARCH.md, handoff-flag)
-   // Arrival is counted per XCD first (block b runs on XCD b % 8; 8 counters 256 B apart), then
-   // once per XCD on a top counter: one counter taking every block's RMW serialises ~1000 atomics
-   // at one memory channel (measured ~13 us per launch).
-   if (threadIdx.x == 0) {
-      __hip_atomic_store(part + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned G = gridDim.x;
-      const unsigned xcd = blockIdx.x % kXcds;
-      const unsigned members = (G - xcd + kXcds - 1) / kXcds;
-      const unsigned groups = G < kXcds ? G : kXcds;
-      int last = 0;
-      const unsigned old = __hip_atomic_fetch_add(ticket + (1 + xcd) * kTicketStride, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-      if (old == members - 1) {
-         const unsigned top = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-         last = (top == groups - 1);
-      }
-      s_last = last;
-   }
-   __syncthreads();
-   if (!s_last) return false;
-   constexpr int kPer = kPcgMaxBlocks / kVecThreads;
-   double pv[kPer];
-#pragma unroll
-   for (int u = 0; u < kPer; u++) {
-      const unsigned i = threadIdx.x + u * kVecThreads;
-      pv[u] = i < gridDim.x ? __hip_atomic_load(part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-   }
-   double acc = 0.0;
-#pragma unroll
-   for (int u = 0; u < kPer; u++) acc += pv[u];
-   for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
-   if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = acc;
-   __syncthreads();
-   double t = 0.0;
-   for (int w = 0; w < kVecThreads / 64; w++) t += s_red[w];
-   *total = t;
-   if (threadIdx.x <= (unsigned)kXcds)
-      __hip_atomic_store(ticket + threadIdx.x * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-   return true;
-}
-
-__device__ double block_sum0(double acc)
-{
-   __shared__ double s[kVecThreads / 64];
-   for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
-   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
-   __syncthreads();
-   double v = 0.0;
-   if (threadIdx.x == 0)
-      for (int w = 0; w < kVecThreads / 64; w++) v += s[w];
-   return v;  // valid in thread 0
 }
 
 // which = 0: rhos[ii] = (z, r) with the rho == 0 test;  which = 1: pq = (q, p) with the pq <= 0 test
@@ -192,9 +127,9 @@ __global__ __launch_bounds__(kVecThreads) void k_pcg_dot(const double* __restric
 #pragma unroll
       for (int u = 0; u < kEPT; u++) acc = fma(av[u], bv[u], acc);
    }
-   acc = block_sum0(acc);
+   acc = block_sum0<kVecThreads>(acc);
    double tot;
-   if (!grid_total(acc, part, ticket, &tot) || threadIdx.x != 0) return;
+   if (!grid_total<kVecThreads>(acc, part, ticket, &tot) || threadIdx.x != 0) return;
    if (which == 0) {
       rhos[ii] = tot;
       if (tot == 0.0) { st->status = 2; st->flag_iter = ii; }
@@ -246,10 +181,16 @@ __global__ __launch_bounds__(kVecThreads) void k_pcg_xr(double* __restrict__ x, 
                                                         size_t n, double* __restrict__ part,
                                                         unsigned int* __restrict__ ticket, PcgState* st,
                                                         double* __restrict__ rhos, double* __restrict__ hist, int ii,
-                                                        int rho_from_norm, PcgSlot* slot)
+                                                        int rho_from_norm, int check_pq, PcgSlot* slot)
 {
-   if (st->status) {
+   // check_pq: (q, p) came from the fused matvec-dot, so the pq <= 0 breakdown test (pcg.c:158) is here
+   const int status = st->status ? st->status : ((check_pq && st->pq <= 0.0) ? 4 : 0);
+   if (status) {
       if (blockIdx.x == 0 && threadIdx.x == 0) {
+         if (!st->status) {
+            st->status = status;
+            st->flag_iter = ii;
+         }
          slot->normr = st->normr2;
          slot->status = st->status;
          slot->flag_iter = st->flag_iter;
@@ -283,9 +224,9 @@ __global__ __launch_bounds__(kVecThreads) void k_pcg_xr(double* __restrict__ x, 
          }
       }
    }
-   acc = block_sum0(acc);
+   acc = block_sum0<kVecThreads>(acc);
    double tot;
-   if (!grid_total(acc, part, ticket, &tot) || threadIdx.x != 0) return;
+   if (!grid_total<kVecThreads>(acc, part, ticket, &tot) || threadIdx.x != 0) return;
    const double normr = sqrt(tot);
    st->normr2 = normr;
    hist[ii] = normr / st->normb;
@@ -465,7 +406,7 @@ struct PcgScratch {
    {
       if (!part) {
          NFFT4GP_HIP_CHECK(hipMalloc((void**)&part, sizeof(double) * kPcgMaxBlocks));
-         const size_t tb = sizeof(unsigned int) * (kXcds + 1) * kTicketStride;
+         const size_t tb = sizeof(unsigned int) * kTicketWords;
          NFFT4GP_HIP_CHECK(hipMalloc((void**)&ticket, tb));
          NFFT4GP_HIP_CHECK(hipMemset(ticket, 0, tb));
          NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&slots_h, sizeof(PcgSlot) * kSlots,
@@ -705,6 +646,8 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
 
    const int g = pcg_grid(N);
    const int ge = g;
+   // this library's additive operator forms (q, p) in its own interpolation launch
+   const bool fused_dot = cb.mv_dev && matvec == &Nfft4GPAdditiveNFFTMatSymv;
    // iterations in flight ahead of the host's status check (1 when printing every step)
    const int lag = print_level > 0 ? 1 : PcgScratch::kSlots;
    double prev_rel = rel_res_v[0];
@@ -723,11 +666,17 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
             zz = z;
          }
          hipLaunchKernelGGL(k_pcg_pupdate, dim3(ge), dim3(kVecThreads), 0, s, p, zz, N, st, rhos, ii);
-         if (cb.apply(1.0, p, 0.0, q)) { rc = -1; break; }
-         hipLaunchKernelGGL(k_pcg_dot, dim3(g), dim3(kVecThreads), 0, s, q, p, N, g_pcg.part, g_pcg.ticket, st,
-                            rhos, ii, 1);
+         if (fused_dot) {
+            // q = A p with (q, p) formed inside the interpolation kernel's epilogue
+            if (additive_matvec_dot(mat_data, p, q, &st->pq)) { rc = -1; break; }
+         } else {
+            if (cb.apply(1.0, p, 0.0, q)) { rc = -1; break; }
+            hipLaunchKernelGGL(k_pcg_dot, dim3(g), dim3(kVecThreads), 0, s, q, p, N, g_pcg.part, g_pcg.ticket, st,
+                               rhos, ii, 1);
+         }
          hipLaunchKernelGGL(k_pcg_xr, dim3(g), dim3(kVecThreads), 0, s, vx.d, r, p, q, N, g_pcg.part, g_pcg.ticket,
-                            st, rhos, hist_d, ii, prec_data ? 0 : 1, slots_d + (ii % PcgScratch::kSlots));
+                            st, rhos, hist_d, ii, prec_data ? 0 : 1, fused_dot ? 1 : 0,
+                            slots_d + (ii % PcgScratch::kSlots));
          ii++;
       }
       if (rc) break;
