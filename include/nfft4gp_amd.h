@@ -155,6 +155,23 @@ void *Nfft4GPAmdNysCreate(int n, int k, const NFFT4GP_DOUBLE *U, const NFFT4GP_D
 /* same signature as Nfft4GPPrecondNysSolve (nys.c:115): x = M^{-1} rhs, func_solve */
 int Nfft4GPAmdNysSolve(void *nys, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
 void Nfft4GPAmdNysFree(void *nys);
+/* Nystrom preconditioner SETUP on the GPU: Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660, require_grad
+ * = 0) for the DENSE additive kernel (kernels.c:3099-3494; Gaussian :680-1289 or Matern-1/2 :2390-3033, as
+ * set up last) over the data, windows and hyperparameters (_params[0] = f, _params[1] = l, _noise_level
+ * = mu) of the additive handle `str`, landmarks perm[0..k-1] of the permutation perm[0..n-1]:
+ * K11 + sqrt(k) ulp(|K11|_F) I = L L^T (chol.c:446-466), U1 = K(perm, perm[:k]) L^{-T},
+ * U1^T U1 = V diag(w) V^T, U = U1 V w^{-1/2} (descending w), s = max(1/(w + eta), 0), eta = mu f^2.
+ * The n x k panel and the n x k x k products run on the GPU (v_mfma_f64_16x16x4), the k x k Cholesky,
+ * inverse and eigensolve on the host.  Returns a handle for Nfft4GPAmdNysSolve / Nfft4GPAmdNysFree, or
+ * NULL (message on stderr) if K11 is not positive definite or the handle is unsuitable.
+ * k11_mode 0 reproduces the reference's K11 exactly: nys.c:569 passes the k x d sub-data to the additive
+ * kernel, which ignores it and reads its own gathered buffer at window stride k*dwindows (kernels.c:3160),
+ * so K11 is built from buffer slices, not from the landmarks.  k11_mode 1 uses K(perm[:k], perm[:k]). */
+void *Nfft4GPAmdNysSetupAdditive(void *str, const int *perm, int k, int k11_mode);
+/* copy a Nystrom handle's factors to the host: U (n x k column-major) with rows in the order of perm
+ * (pass the setup's perm to get the reference's permuted row order, NULL for natural order), s (k),
+ * eta; any output may be NULL */
+int Nfft4GPAmdNysFactors(void *nys, const int *perm, NFFT4GP_DOUBLE *U, NFFT4GP_DOUBLE *s, NFFT4GP_DOUBLE *eta);
 
 /* ---- MI355X extensions --------------------------------------------------------------------------- */
 /* stream every kernel of this library is enqueued on (hipStream_t; NULL = null stream) */
@@ -214,6 +231,11 @@ NFFT4GP_DOUBLE Nfft4GPAmdHostPrepare(const NFFT4GP_DOUBLE *col, int n, unsigned 
  * in the cell in bits 0-25, local index bits 6-11 in bits 26-31), nblocks*ngroups+1 (tile_off) */
 int Nfft4GPAmdHostLayout(const unsigned int *qc, int n, int nw, int B, int CG, long long *counts,
                          unsigned short *meta, unsigned int *lo, unsigned int *q, int *tile_off);
+/* the Nystrom setup's host k x k steps: symmetric eigensolve (dsyev 'V' semantics: ascending w,
+ * eigenvectors as the columns of V, column-major) and L^{-1} of the lower Cholesky factor of A + shift I
+ * (returns 0, or the failing column + 1 if A + shift I is not positive definite) */
+int Nfft4GPAmdHostSymEig(const NFFT4GP_DOUBLE *A, int n, NFFT4GP_DOUBLE *w, NFFT4GP_DOUBLE *V);
+int Nfft4GPAmdHostCholInverse(const NFFT4GP_DOUBLE *A, int k, NFFT4GP_DOUBLE shift, NFFT4GP_DOUBLE *G);
 
 #ifdef __cplusplus
 }

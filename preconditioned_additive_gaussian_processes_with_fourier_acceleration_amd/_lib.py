@@ -80,6 +80,8 @@ _SIGS = {
     "Nfft4GPAmdNysCreate": (vp, [C.c_int, C.c_int, vp, vp, C.c_double, vp]),
     "Nfft4GPAmdNysSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdNysFree": (None, [vp]),
+    "Nfft4GPAmdNysSetupAdditive": (vp, [vp, vp, C.c_int, C.c_int]),
+    "Nfft4GPAmdNysFactors": (C.c_int, [vp, vp, vp, vp, dp]),
     "Nfft4GPAmdSetStream": (None, [vp]),
     "Nfft4GPAmdGetStream": (vp, []),
     "Nfft4GPAmdDeviceAvailable": (C.c_int, []),
@@ -94,6 +96,8 @@ _SIGS = {
     "Nfft4GPAmdHostTapPoly": (C.c_int, [vp]),
     "Nfft4GPAmdHostCirculant": (C.c_int, [C.c_int, C.c_double, C.c_double, vp, vp]),
     "Nfft4GPAmdHostPrepare": (C.c_double, [vp, C.c_int, vp]),
+    "Nfft4GPAmdHostSymEig": (C.c_int, [vp, C.c_int, vp, vp]),
+    "Nfft4GPAmdHostCholInverse": (C.c_int, [vp, C.c_int, C.c_double, vp]),
     "Nfft4GPAmdHostLayout": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_longlong), vp, vp,
                                        vp, vp]),
 }

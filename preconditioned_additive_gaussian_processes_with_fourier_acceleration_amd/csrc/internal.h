@@ -141,6 +141,26 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
 // the matvec's own three launches (used by Nfft4GPSolverPcg when its operator is this library's)
 int additive_matvec_dot(void* str, const double* d_x, double* d_y, double* d_dot);
 
+// Nystrom preconditioner M = U S U^T + eta (I - U U^T) in HBM (nys.c:115-173 apply)
+struct NysDev {
+   int n = 0, k = 0;
+   double eta = 0.0;
+   double* U = nullptr;  // n x k column-major, natural row order
+   double* s = nullptr;  // k
+   double* w = nullptr;  // apply scratch, k
+   double* part = nullptr;
+   int nblk = 0;
+};
+constexpr int kNysRows = 2048;  // rows per workgroup of the apply's U^T r pass
+int nys_alloc_scratch(NysDev* N);
+// GPU Nystrom setup (nystrom.hip) from gathered window coordinates xw (n x packed dims, host)
+int gemm_f64(bool transA, int M, int N, int K, const double* A, long long lda, const double* B, long long ldb,
+             double* C, long long ldc, const int* out_row, hipStream_t s);
+int sym_eig_host(const std::vector<double>& A, int n, std::vector<double>& w, std::vector<double>& V);
+int chol_inverse_host(std::vector<double>& A, int k);
+NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int skip_last, int kernel, double f,
+                           double l, double mu, const int* perm, int k, int k11_mode);
+
 hipStream_t current_stream();
 bool is_device_ptr(const void* p);
 int device_ok();

@@ -600,6 +600,27 @@ int Nfft4GPAmdKernelBench(void* str, int which, int grad, int reps, const double
    return 0;
 }
 
+void* Nfft4GPAmdNysSetupAdditive(void* str, const int* perm, int k, int k11_mode)
+{
+   if (!device_ok()) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdNysSetupAdditive: no HIP device visible (no CPU fallback).\n");
+      return nullptr;
+   }
+   nfft4gp_kernel* kd = (nfft4gp_kernel*)str;
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready || !perm) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdNysSetupAdditive needs an additive handle after its kernel setup\n");
+      return nullptr;
+   }
+   const AdditivePlan& P = E->P;
+   if (P.row_begin != 0 || P.row_end != P.n_global) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdNysSetupAdditive: row-sharded handles are not supported\n");
+      return nullptr;
+   }
+   return nys_setup_additive(kd->_buffer, P.n_global, P.nw, P.dw, P.skip_last, P.kernel, kd->_params[0],
+                             kd->_params[1], kd->_noise_level, perm, k, k11_mode);
+}
+
 int Nfft4GPAmdShardSpread(void* str, const double* x_local, double* grid)
 {
    PlanExt* E = additive_plan(str);

@@ -1,0 +1,597 @@
+// nystrom.hip -- Nystrom ("RAN") preconditioner setup on the GPU.
+//
+// Restates Nfft4GPPrecondNysSetupWithKernel (SRC/preconds/nys.c:518-660) for the dense additive kernel
+// of an additive handle's data / windows / hyperparameters (SRC/linearalg/kernels.c:3099-3494, Gaussian
+// kernels.c:680-1289 and Matern-1/2 :2390-3033, "when have permc we do not add noise"):
+//
+//   Kp  = K(perm, perm[:k])                   n x k panel, rows in permuted order   (k_nys_panel, VALU)
+//   K11 (see below), + sqrt(k) ulp(|K11|_F) I, L = chol(K11), G = L^{-1}     (host, k x k; chol.c:428-467)
+//   U1  = Kp G^T                              (k_gemm_f64, MFMA; matops.c Nfft4GPTrilNystromMm)
+//   AA  = U1^T U1 = V diag(w1) V^T            (k_gemm_f64 split over rows, MFMA; host eigensolve;
+//                                              matops.c Nfft4GPTrilNystromSvd)
+//   U   = U1 V(:, reversed) diag(1/sqrt(w1 reversed))   (k_gemm_f64, rows scattered to natural order)
+//   s   = max(1/(w + eta), 0), eta = mu f^2   (nys.c:641-647)
+//
+// The three n x k x k products (6 n k^2 flops, 1.6 TFLOP at n = 1e6, k = 512) run on v_mfma_f64_16x16x4;
+// the k x k Cholesky / inverse / eigensolve (O(k^3), ~0.1-0.5 s at k = 512) run on the host.
+//
+// K11: the reference builds it by calling the additive kernel on the k x d sub-data, but that kernel
+// reads its own gathered buffer with the stride of the n it is given (kernels.c:3160), so its K11 is the
+// kernel matrix of buffer slices, not of the landmarks perm[:k] (checked against the compiled reference
+// to 1e-11).  k11_mode 0 reproduces that (parity); k11_mode 1 uses K(perm[:k], perm[:k]), the matrix the
+// method intends, which is what makes the preconditioner effective.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "internal.h"
+
+namespace nfft4gp_amd {
+
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ---- panel: Kp[jj + ii*n] = (f^2/nw) sum_c kern(|x_c[perm[jj]] - x_c[perm[ii]]|), jj < n, ii < k --------
+constexpr int kPanelRows = 64, kPanelCols = 64, kPanelThreads = 256;
+constexpr int kPanelMaxDims = 128;  // window dimensions summed over all windows (nw * dw)
+
+template <int KERNEL>  // 0 Gaussian exp(-r^2 / 2l^2), 1 Matern-1/2 exp(-r / l)
+__global__ __launch_bounds__(kPanelThreads) void k_nys_panel(const double* __restrict__ xw, int n, int nw, int dw,
+                                                             int last_dw, const int* __restrict__ perm, int k,
+                                                             double scale, double inv, double* __restrict__ Kp)
+{
+   extern __shared__ double sm[];
+   const int D = (nw - 1) * dw + last_dw;
+   double* s_r = sm;                     // [D][kPanelRows]
+   double* s_c = sm + D * kPanelRows;    // [D][kPanelCols]
+   const int r0 = blockIdx.x * kPanelRows, c0 = blockIdx.y * kPanelCols;
+   for (int e = threadIdx.x; e < D * kPanelRows; e += kPanelThreads) {
+      const int t = e / kPanelRows, i = e % kPanelRows;
+      const int w = min(t / dw, nw - 1), dd = t - w * dw;  // window w, its dimension dd
+      const size_t col = (size_t)w * dw + dd;               // windows packed at stride n*dw (kernels.c:3160)
+      s_r[e] = (r0 + i < n) ? xw[col * n + perm[r0 + i]] : 0.0;
+      s_c[e] = (c0 + i < k) ? xw[col * n + perm[c0 + i]] : 0.0;
+   }
+   __syncthreads();
+   // thread -> 4 rows x 4 columns, rows fastest so stores are coalesced per column
+   const int tr = threadIdx.x & 15, tc = threadIdx.x >> 4;
+   double acc[4][4] = {};
+   for (int w = 0; w < nw; w++) {
+      const int dims = (w == nw - 1) ? last_dw : dw;
+      double r2[4][4] = {};
+      for (int dd = 0; dd < dims; dd++) {
+         const int t = w * dw + dd;
+         double xr[4], xc[4];
+#pragma unroll
+         for (int a = 0; a < 4; a++) xr[a] = s_r[t * kPanelRows + tr + 16 * a];
+#pragma unroll
+         for (int b = 0; b < 4; b++) xc[b] = s_c[t * kPanelCols + tc + 16 * b];
+#pragma unroll
+         for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+               const double df = xr[a] - xc[b];
+               r2[a][b] = fma(df, df, r2[a][b]);
+            }
+      }
+#pragma unroll
+      for (int a = 0; a < 4; a++)
+#pragma unroll
+         for (int b = 0; b < 4; b++) acc[a][b] += (KERNEL == 0) ? exp(-r2[a][b] * inv) : exp(-sqrt(r2[a][b]) * inv);
+   }
+#pragma unroll
+   for (int b = 0; b < 4; b++) {
+      const int c = c0 + tc + 16 * b;
+      if (c >= k) continue;
+#pragma unroll
+      for (int a = 0; a < 4; a++) {
+         const int r = r0 + tr + 16 * a;
+         if (r < n) Kp[(size_t)c * n + r] = scale * acc[a][b];
+      }
+   }
+}
+
+// ---- C = op(A) B on MFMA f64 ---------------------------------------------------------------------
+// op(A) is M x K: A column-major (lda) or, with TRANSA, A^T of a column-major K x M array.  B is K x N
+// column-major (ldb).  64 x 64 output tile per workgroup (4 waves, 32 x 32 each = 2 x 2 tiles of
+// v_mfma_f64_16x16x4_f64), K in steps of 16 through LDS.  gridDim.z > 1 splits K into chunks of
+// ksplit; chunk z writes its partial product at C + z * split_stride (summed by k_sum_splits).
+// out_row (optional) scatters output row r to row out_row[r].
+constexpr int kGemmTile = 64, kGemmK = 16, kGemmThreads = 256;
+
+template <bool TRANSA>
+__global__ __launch_bounds__(kGemmThreads) void k_gemm_f64(int M, int N, int K, const double* __restrict__ A,
+                                                           long long lda, const double* __restrict__ B,
+                                                           long long ldb, double* __restrict__ C, long long ldc,
+                                                           long long split_stride, int ksplit,
+                                                           const int* __restrict__ out_row)
+{
+   __shared__ double As[kGemmK][kGemmTile + 1];  // As[kk][row]
+   __shared__ double Bs[kGemmK][kGemmTile + 1];  // Bs[kk][col]
+   const int m0 = blockIdx.x * kGemmTile, n0 = blockIdx.y * kGemmTile;
+   const int kbeg = blockIdx.z * ksplit, kend = min(K, kbeg + ksplit);
+   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+   const int wr = (wave & 1) * 32, wc = (wave >> 1) * 32;
+   d4 acc[2][2];
+#pragma unroll
+   for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+   for (int k0 = kbeg; k0 < kend; k0 += kGemmK) {
+      double av[4], bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+         const int e = tid + u * kGemmThreads;
+         int r, kk;
+         if (!TRANSA) {
+            r = e & 63;
+            kk = e >> 6;
+         } else {
+            kk = e & 15;
+            r = e >> 4;
+         }
+         const int gr = m0 + r, gk = k0 + kk;
+         av[u] = (gr < M && gk < kend) ? (TRANSA ? A[gk + gr * lda] : A[gr + gk * lda]) : 0.0;
+         const int bk = e & 15, bc = e >> 4;
+         const int gbk = k0 + bk, gbc = n0 + bc;
+         bv[u] = (gbk < kend && gbc < N) ? B[gbk + gbc * ldb] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+         const int e = tid + u * kGemmThreads;
+         if (!TRANSA)
+            As[e >> 6][e & 63] = av[u];
+         else
+            As[e & 15][e >> 4] = av[u];
+         Bs[e & 15][e >> 4] = bv[u];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k4 = 0; k4 < kGemmK / 4; k4++) {
+         const int kk = 4 * k4 + (lane >> 4);
+         const double a0 = As[kk][wr + (lane & 15)], a1 = As[kk][wr + 16 + (lane & 15)];
+         const double b0 = Bs[kk][wc + (lane & 15)], b1 = Bs[kk][wc + 16 + (lane & 15)];
+         acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+         acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+         acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+         acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+      }
+      __syncthreads();
+   }
+   // C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
+   double* Cz = C + (size_t)blockIdx.z * split_stride;
+#pragma unroll
+   for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+#pragma unroll
+         for (int rg = 0; rg < 4; rg++) {
+            const int gr = m0 + wr + 16 * i + (lane >> 4) + 4 * rg;
+            const int gc = n0 + wc + 16 * j + (lane & 15);
+            if (gr < M && gc < N) {
+               const long long orow = out_row ? out_row[gr] : gr;
+               Cz[orow + gc * ldc] = acc[i][j][rg];
+            }
+         }
+}
+
+// C[i] = sum_z part[z * stride + i] in z order
+__global__ void k_sum_splits(const double* __restrict__ part, int nsplit, long long stride, long long count,
+                             double* __restrict__ C)
+{
+   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= count) return;
+   double v = 0.0;
+   for (int z = 0; z < nsplit; z++) v += part[z * stride + i];
+   C[i] = v;
+}
+
+int gemm(bool transA, int M, int N, int K, const double* A, long long lda, const double* B, long long ldb, double* C,
+         long long ldc, const int* out_row, hipStream_t s)
+{
+   dim3 grid((M + kGemmTile - 1) / kGemmTile, (N + kGemmTile - 1) / kGemmTile, 1);
+   if (transA)
+      hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(kGemmThreads), 0, s, M, N, K, A, lda, B, ldb, C, ldc, 0LL, K,
+                         out_row);
+   else
+      hipLaunchKernelGGL(k_gemm_f64<false>, grid, dim3(kGemmThreads), 0, s, M, N, K, A, lda, B, ldb, C, ldc, 0LL, K,
+                         out_row);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+// ---- host k x k linear algebra (column-major, k <= a few thousand) --------------------------------
+// lower Cholesky in place (LAPACK dpotrf 'L' semantics); returns 0 or the failing column + 1
+int chol_lower(std::vector<double>& a, int k)
+{
+   for (int j = 0; j < k; j++) {
+      double d = a[j + (size_t)j * k];
+      for (int p = 0; p < j; p++) d -= a[j + (size_t)p * k] * a[j + (size_t)p * k];
+      if (!(d > 0.0)) return j + 1;
+      d = std::sqrt(d);
+      a[j + (size_t)j * k] = d;
+      for (int i = j + 1; i < k; i++) {
+         double v = a[i + (size_t)j * k];
+         for (int p = 0; p < j; p++) v -= a[i + (size_t)p * k] * a[j + (size_t)p * k];
+         a[i + (size_t)j * k] = v / d;
+      }
+   }
+   for (int j = 0; j < k; j++)
+      for (int i = 0; i < j; i++) a[i + (size_t)j * k] = 0.0;
+   return 0;
+}
+
+// inverse of a lower-triangular matrix in place (dtrtri 'L' 'N')
+void trtri_lower(std::vector<double>& L, int k)
+{
+   std::vector<double> G((size_t)k * k, 0.0);
+   for (int j = 0; j < k; j++) {
+      G[j + (size_t)j * k] = 1.0 / L[j + (size_t)j * k];
+      for (int i = j + 1; i < k; i++) {
+         double v = 0.0;
+         for (int m = j; m < i; m++) v += L[i + (size_t)m * k] * G[m + (size_t)j * k];
+         G[i + (size_t)j * k] = -v / L[i + (size_t)i * k];
+      }
+   }
+   L.swap(G);
+}
+
+// symmetric eigensolve (dsyev 'V' semantics: ascending w, orthonormal eigenvectors as columns of V):
+// Householder tridiagonalisation, then implicit-shift QL with the transformations accumulated
+int sym_eig(const std::vector<double>& A, int n, std::vector<double>& w, std::vector<double>& V)
+{
+   std::vector<double> a(A);  // a[i + j*n] = a(i, j); symmetric, so a(i, j) = a[i*n + j] too
+   auto at = [&](int i, int j) -> double& { return a[(size_t)i * n + j]; };
+   std::vector<double> d(n), e(n);
+   for (int i = n - 1; i > 0; i--) {
+      const int l = i - 1;
+      double h = 0.0, scale = 0.0;
+      if (l > 0) {
+         for (int kk = 0; kk <= l; kk++) scale += std::fabs(at(i, kk));
+         if (scale == 0.0) {
+            e[i] = at(i, l);
+         } else {
+            for (int kk = 0; kk <= l; kk++) {
+               at(i, kk) /= scale;
+               h += at(i, kk) * at(i, kk);
+            }
+            double f = at(i, l);
+            double g = (f >= 0.0) ? -std::sqrt(h) : std::sqrt(h);
+            e[i] = scale * g;
+            h -= f * g;
+            at(i, l) = f - g;
+            f = 0.0;
+            for (int j = 0; j <= l; j++) {
+               at(j, i) = at(i, j) / h;
+               g = 0.0;
+               for (int kk = 0; kk <= j; kk++) g += at(j, kk) * at(i, kk);
+               for (int kk = j + 1; kk <= l; kk++) g += at(kk, j) * at(i, kk);
+               e[j] = g / h;
+               f += e[j] * at(i, j);
+            }
+            const double hh = f / (h + h);
+            for (int j = 0; j <= l; j++) {
+               f = at(i, j);
+               e[j] = g = e[j] - hh * f;
+               for (int kk = 0; kk <= j; kk++) at(j, kk) -= (f * e[kk] + g * at(i, kk));
+            }
+         }
+      } else {
+         e[i] = at(i, l);
+      }
+      d[i] = h;
+   }
+   d[0] = 0.0;
+   e[0] = 0.0;
+   for (int i = 0; i < n; i++) {
+      const int l = i - 1;
+      if (d[i] != 0.0) {
+         for (int j = 0; j <= l; j++) {
+            double g = 0.0;
+            for (int kk = 0; kk <= l; kk++) g += at(i, kk) * at(kk, j);
+            for (int kk = 0; kk <= l; kk++) at(kk, j) -= g * at(kk, i);
+         }
+      }
+      d[i] = at(i, i);
+      at(i, i) = 1.0;
+      for (int j = 0; j <= l; j++) at(j, i) = at(i, j) = 0.0;
+   }
+   // z^T (rows = eigenvector slots) so the QL rotations touch contiguous memory
+   std::vector<double> zt((size_t)n * n);
+   for (int i = 0; i < n; i++)
+      for (int kk = 0; kk < n; kk++) zt[(size_t)i * n + kk] = at(kk, i);
+   for (int i = 1; i < n; i++) e[i - 1] = e[i];
+   if (n > 0) e[n - 1] = 0.0;
+   for (int l = 0; l < n; l++) {
+      int iter = 0, m;
+      do {
+         for (m = l; m < n - 1; m++) {
+            const double dd = std::fabs(d[m]) + std::fabs(d[m + 1]);
+            if (std::fabs(e[m]) <= DBL_EPSILON * dd) break;
+         }
+         if (m != l) {
+            if (iter++ == 200) return -1;
+            double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
+            double r = std::hypot(g, 1.0);
+            g = d[m] - d[l] + e[l] / (g + std::copysign(r, g));
+            double s = 1.0, c = 1.0, p = 0.0;
+            int i;
+            for (i = m - 1; i >= l; i--) {
+               double f = s * e[i];
+               const double b = c * e[i];
+               e[i + 1] = (r = std::hypot(f, g));
+               if (r == 0.0) {
+                  d[i + 1] -= p;
+                  e[m] = 0.0;
+                  break;
+               }
+               s = f / r;
+               c = g / r;
+               g = d[i + 1] - p;
+               r = (d[i] - g) * s + 2.0 * c * b;
+               d[i + 1] = g + (p = s * r);
+               g = c * r - b;
+               double* z0 = zt.data() + (size_t)i * n;
+               double* z1 = zt.data() + (size_t)(i + 1) * n;
+               for (int kk = 0; kk < n; kk++) {
+                  f = z1[kk];
+                  z1[kk] = s * z0[kk] + c * f;
+                  z0[kk] = c * z0[kk] - s * f;
+               }
+            }
+            if (r == 0.0 && i >= l) continue;
+            d[l] -= p;
+            e[l] = g;
+            e[m] = 0.0;
+         }
+      } while (m != l);
+   }
+   std::vector<int> order(n);
+   for (int i = 0; i < n; i++) order[i] = i;
+   std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return d[x] < d[y]; });
+   w.resize(n);
+   V.assign((size_t)n * n, 0.0);
+   for (int c = 0; c < n; c++) {
+      w[c] = d[order[c]];
+      memcpy(V.data() + (size_t)c * n, zt.data() + (size_t)order[c] * n, sizeof(double) * n);
+   }
+   return 0;
+}
+
+template <class T>
+int dalloc(T** p, size_t count)
+{
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)p, sizeof(T) * std::max<size_t>(1, count)));
+   return 0;
+}
+
+}  // namespace
+
+int gemm_f64(bool transA, int M, int N, int K, const double* A, long long lda, const double* B, long long ldb,
+             double* C, long long ldc, const int* out_row, hipStream_t s)
+{
+   return gemm(transA, M, N, K, A, lda, B, ldb, C, ldc, out_row, s);
+}
+
+int sym_eig_host(const std::vector<double>& A, int n, std::vector<double>& w, std::vector<double>& V)
+{
+   return sym_eig(A, n, w, V);
+}
+
+// L^{-1} of chol(A) (lower) in place; returns 0 or the failing column + 1
+int chol_inverse_host(std::vector<double>& A, int k)
+{
+   if (int info = chol_lower(A, k)) return info;
+   trtri_lower(A, k);
+   return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int skip_last, int kernel, double f,
+                           double l, double mu, const int* perm, int k, int k11_mode)
+{
+   const int last_dw = dw - skip_last;
+   const int D = (nw - 1) * dw + last_dw;
+   if (k <= 0 || k > n || D > kPanelMaxDims || last_dw <= 0) {
+      fprintf(stderr, "nfft4gp_amd: Nystrom setup needs 0 < k <= n and <= %d window dimensions\n", kPanelMaxDims);
+      return nullptr;
+   }
+   hipStream_t s = current_stream();
+   double *d_xw = nullptr, *d_Kp = nullptr, *d_U1 = nullptr, *d_B = nullptr, *d_part = nullptr, *d_AA = nullptr;
+   int* d_perm = nullptr;
+   NysDev* N = nullptr;
+   auto fail = [&](const char* what) -> NysDev* {
+      if (what) fprintf(stderr, "nfft4gp_amd: Nystrom setup: %s\n", what);
+      (void)hipStreamSynchronize(s);
+      for (double* p : {d_xw, d_U1, d_B, d_part, d_AA}) (void)hipFree(p);
+      (void)hipFree(d_perm);
+      if (N) {
+         (void)hipFree(N->U);
+         (void)hipFree(N->s);
+         (void)hipFree(N->w);
+         (void)hipFree(N->part);
+         delete N;
+      } else {
+         (void)hipFree(d_Kp);
+      }
+      return nullptr;
+   };
+   const size_t nk = (size_t)n * k;
+   if (dalloc(&d_xw, (size_t)n * nw * dw) || dalloc(&d_perm, (size_t)n) || dalloc(&d_Kp, nk) ||
+       dalloc(&d_U1, nk) || dalloc(&d_B, (size_t)k * k) || dalloc(&d_AA, (size_t)k * k))
+      return fail("allocation");
+   if (hipMemcpy(d_xw, xw_host, sizeof(double) * (size_t)n * ((nw - 1) * dw + last_dw), hipMemcpyHostToDevice) ||
+       hipMemcpy(d_perm, perm, sizeof(int) * (size_t)n, hipMemcpyHostToDevice))
+      return fail("upload");
+
+   // 1. panel K(perm, perm[:k]) (noise-free, nys.c:566-567 / kernels.c "when have permc")
+   const double f2 = f * f;
+   const double inv = (kernel == 0) ? 1.0 / (2.0 * l * l) : 1.0 / l;
+   const size_t lds = sizeof(double) * (size_t)D * (kPanelRows + kPanelCols);
+   dim3 pgrid((n + kPanelRows - 1) / kPanelRows, (k + kPanelCols - 1) / kPanelCols);
+   if (kernel == 0)
+      hipLaunchKernelGGL(k_nys_panel<0>, pgrid, dim3(kPanelThreads), lds, s, d_xw, n, nw, dw, last_dw, d_perm, k,
+                         f2 / nw, inv, d_Kp);
+   else
+      hipLaunchKernelGGL(k_nys_panel<1>, pgrid, dim3(kPanelThreads), lds, s, d_xw, n, nw, dw, last_dw, d_perm, k,
+                         f2 / nw, inv, d_Kp);
+   if (hipGetLastError() != hipSuccess) return fail("panel launch");
+
+   // 2. K11, stable shift + Cholesky + inverse on the host (chol.c:446-466)
+   std::vector<double> K11((size_t)k * k);
+   if (k11_mode == 1) {
+      // landmarks: K(perm[:k], perm[:k]) = the first k rows of the panel
+      if (hipMemcpy2DAsync(K11.data(), sizeof(double) * k, d_Kp, sizeof(double) * n, sizeof(double) * k, k,
+                           hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+         return fail("K11 download");
+   } else {
+      // the reference: nys.c:569 hands the k x d sub-data to Nfft4GPKernelAdditiveKernel, which ignores
+      // its data argument and reads window i of its own gathered buffer at offset i*n*dwindows with
+      // n = k (kernels.c:3160), i.e. coordinate t of "point" p of window i is buffer[i*k*dw + t*k + p]
+      for (int j = 0; j < k; j++)
+         for (int i = j; i < k; i++) {
+            double acc = 0.0;
+            for (int w = 0; w < nw; w++) {
+               const int dims = (w == nw - 1) ? last_dw : dw;
+               const double* base = xw_host + (size_t)w * k * dw;
+               double r2 = 0.0;
+               for (int t = 0; t < dims; t++) {
+                  const double df = base[(size_t)t * k + i] - base[(size_t)t * k + j];
+                  r2 += df * df;
+               }
+               acc += (kernel == 0) ? std::exp(-r2 * inv) : std::exp(-std::sqrt(r2) * inv);
+            }
+            K11[i + (size_t)j * k] = K11[j + (size_t)i * k] = (f2 / nw) * acc;
+         }
+   }
+   double fro = 0.0;  // dlansy('F', 'L'): the lower triangle, off-diagonals counted twice
+   for (int j = 0; j < k; j++) {
+      fro += K11[j + (size_t)j * k] * K11[j + (size_t)j * k];
+      for (int i = j + 1; i < k; i++) fro += 2.0 * K11[i + (size_t)j * k] * K11[i + (size_t)j * k];
+   }
+   fro = std::sqrt(fro);
+   const double nu = std::sqrt((double)k) * (std::nextafter(fro, fro + 1.0) - fro);
+   for (int j = 0; j < k; j++) K11[j + (size_t)j * k] += nu;
+   if (int info = chol_lower(K11, k)) {
+      fprintf(stderr, "nfft4gp_amd: Nystrom setup: K11 + shift is not positive definite (column %d)\n", info);
+      return fail(nullptr);
+   }
+   trtri_lower(K11, k);  // G = L^{-1}
+   std::vector<double> Gt((size_t)k * k);
+   for (int j = 0; j < k; j++)
+      for (int i = 0; i < k; i++) Gt[i + (size_t)j * k] = K11[j + (size_t)i * k];
+   if (hipMemcpy(d_B, Gt.data(), sizeof(double) * Gt.size(), hipMemcpyHostToDevice)) return fail("upload");
+
+   // 3. U1 = Kp G^T  (dtrmm 'R' 'L' 'T', matops.c Nfft4GPTrilNystromMm)
+   if (gemm(false, n, k, k, d_Kp, n, d_B, k, d_U1, n, nullptr, s)) return fail("gemm");
+
+   // 4. AA = U1^T U1, K = n split over row chunks (fixed order sum -> deterministic)
+   const int nsplit = std::max(1, std::min(256, n / 8192));
+   const int ksplit = ((n + nsplit - 1) / nsplit + kGemmK - 1) / kGemmK * kGemmK;
+   const int nsplit_used = (n + ksplit - 1) / ksplit;
+   if (dalloc(&d_part, (size_t)nsplit_used * k * k)) return fail("allocation");
+   {
+      dim3 grid((k + kGemmTile - 1) / kGemmTile, (k + kGemmTile - 1) / kGemmTile, nsplit_used);
+      hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(kGemmThreads), 0, s, k, k, n, d_U1, (long long)n, d_U1,
+                         (long long)n, d_part, (long long)k, (long long)k * k, ksplit, (const int*)nullptr);
+      const long long cnt = (long long)k * k;
+      hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, d_part, nsplit_used, cnt,
+                         cnt, d_AA);
+      if (hipGetLastError() != hipSuccess) return fail("gram launch");
+   }
+   std::vector<double> AA((size_t)k * k);
+   if (hipMemcpyAsync(AA.data(), d_AA, sizeof(double) * AA.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess)
+      return fail("gram download");
+
+   // 5. eig(AA) (dsyev: ascending); U = U1 V diag(w1^-1/2), columns in descending w1 order, with the
+   //    reference's 1e12 factor for sqrt(w1) < 1e-12 (matops.c Nfft4GPTrilNystromSvd)
+   std::vector<double> w1, V;
+   if (sym_eig(AA, k, w1, V)) return fail("eigensolver did not converge");
+   std::vector<double> W((size_t)k * k), sv(k);
+   for (int c = 0; c < k; c++) {
+      const int src = k - 1 - c;
+      const double wi = std::sqrt(w1[src]);
+      sv[c] = wi;
+      const double scale = (wi < 1e-12) ? 1e12 : 1.0 / wi;
+      for (int i = 0; i < k; i++) W[i + (size_t)c * k] = V[i + (size_t)src * k] * scale;
+   }
+   if (hipMemcpy(d_B, W.data(), sizeof(double) * W.size(), hipMemcpyHostToDevice)) return fail("upload");
+   N = new NysDev();
+   N->n = n;
+   N->k = k;
+   N->U = d_Kp;  // the panel's storage is reused for U (rows scattered back to natural order)
+   d_Kp = nullptr;
+   if (gemm(false, n, k, k, d_U1, n, d_B, k, N->U, n, d_perm, s)) return fail("gemm");
+
+   // 6. s = max(1/(w^2 + eta), 0), eta = mu f^2 (nys.c:641-647)
+   N->eta = mu * f2;
+   std::vector<double> sh(k);
+   for (int c = 0; c < k; c++) sh[c] = std::max(1.0 / (sv[c] * sv[c] + N->eta), 0.0);
+   if (dalloc(&N->s, (size_t)k) || hipMemcpyAsync(N->s, sh.data(), sizeof(double) * k, hipMemcpyHostToDevice, s) ||
+       nys_alloc_scratch(N))
+      return fail("allocation");
+   if (hipStreamSynchronize(s) != hipSuccess) return fail("sync");
+   for (double* p : {d_xw, d_U1, d_B, d_part, d_AA}) (void)hipFree(p);
+   (void)hipFree(d_perm);
+   return N;
+}
+
+}  // namespace nfft4gp_amd
+
+extern "C" {
+
+int Nfft4GPAmdNysFactors(void* nys, const int* perm, double* U, double* s, double* eta)
+{
+   nfft4gp_amd::NysDev* N = (nfft4gp_amd::NysDev*)nys;
+   if (!N) return -1;
+   const int n = N->n, k = N->k;
+   if (U) {
+      std::vector<double> h((size_t)n * k);
+      NFFT4GP_HIP_CHECK(hipMemcpy(h.data(), N->U, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
+      for (int c = 0; c < k; c++)
+         for (int i = 0; i < n; i++) U[i + (size_t)c * n] = h[(perm ? perm[i] : i) + (size_t)c * n];
+   }
+   if (s) NFFT4GP_HIP_CHECK(hipMemcpy(s, N->s, sizeof(double) * k, hipMemcpyDeviceToHost));
+   if (eta) *eta = N->eta;
+   return 0;
+}
+
+}  // extern "C"
+
+// ---- host-only helpers for the CPU test-suite (no GPU needed) ------------------------------------
+extern "C" int Nfft4GPAmdHostSymEig(const double* A, int n, double* w, double* V)
+{
+   std::vector<double> a(A, A + (size_t)n * n), wv, Vv;
+   if (nfft4gp_amd::sym_eig_host(a, n, wv, Vv)) return -1;
+   memcpy(w, wv.data(), sizeof(double) * n);
+   memcpy(V, Vv.data(), sizeof(double) * (size_t)n * n);
+   return 0;
+}
+
+extern "C" int Nfft4GPAmdHostCholInverse(const double* A, int k, double shift, double* G)
+{
+   std::vector<double> a(A, A + (size_t)k * k);
+   for (int j = 0; j < k; j++) a[j + (size_t)j * k] += shift;
+   const int info = nfft4gp_amd::chol_inverse_host(a, k);
+   if (info) return info;
+   memcpy(G, a.data(), sizeof(double) * (size_t)k * k);
+   return 0;
+}
+
+// ---- device test hooks (tests/ only): the MFMA GEMM and the panel kernel in isolation ---------------
+extern "C" int Nfft4GPAmdDebugGemm(int transA, int M, int N, int K, const double* A, long long lda, const double* B,
+                                   long long ldb, double* C, long long ldc)
+{
+   if (nfft4gp_amd::gemm_f64(transA != 0, M, N, K, A, lda, B, ldb, C, ldc, nullptr, nfft4gp_amd::current_stream()))
+      return -1;
+   NFFT4GP_HIP_CHECK(hipStreamSynchronize(nfft4gp_amd::current_stream()));
+   return 0;
+}

@@ -20,6 +20,16 @@
 
 using namespace nfft4gp_amd;
 
+namespace nfft4gp_amd {
+int nys_alloc_scratch(NysDev* N)
+{
+   N->nblk = (N->n + kNysRows - 1) / kNysRows;
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&N->w, sizeof(double) * std::max(1, N->k)));
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&N->part, sizeof(double) * (size_t)N->nblk * std::max(1, N->k)));
+   return 0;
+}
+}  // namespace nfft4gp_amd
+
 namespace {
 
 constexpr int kVecThreads = 256;
@@ -327,7 +337,6 @@ bool need_device(const char* who)
 // ---------------------------------------------------------------------------------------------
 // Nystrom apply kernels
 // ---------------------------------------------------------------------------------------------
-constexpr int kNysRows = 2048;   // rows per workgroup in U^T r
 constexpr int kNysThreads = 256;
 
 // partial[blk][j] = sum_{i in blk rows} U[i, j] r[i]; one wave per column at a time, the block's
@@ -384,16 +393,6 @@ __global__ __launch_bounds__(kNysThreads) void k_nys_u(const double* __restrict_
    for (int j = 0; j < k; j++) acc = fma(U[(size_t)j * ldu + i], s_w[j], acc);
    x[i] = r[i] / eta + acc;
 }
-
-struct NysDev {
-   int n = 0, k = 0;
-   double eta = 0.0;
-   double* U = nullptr;  // natural row order
-   double* s = nullptr;
-   double* w = nullptr;
-   double* part = nullptr;
-   int nblk = 0;
-};
 
 // PCG scratch: reduction partials + arrival ticket (device), status slots (pinned host, mapped)
 struct PcgScratch {
@@ -801,11 +800,8 @@ void* Nfft4GPAmdNysCreate(int n, int k, const double* U, const double* s, double
    } else {
       memcpy(hs.data(), s, sizeof(double) * k);
    }
-   N->nblk = (n + kNysRows - 1) / kNysRows;
    if (hipMalloc((void**)&N->U, sizeof(double) * hU.size()) != hipSuccess ||
-       hipMalloc((void**)&N->s, sizeof(double) * k) != hipSuccess ||
-       hipMalloc((void**)&N->w, sizeof(double) * k) != hipSuccess ||
-       hipMalloc((void**)&N->part, sizeof(double) * (size_t)N->nblk * k) != hipSuccess) {
+       hipMalloc((void**)&N->s, sizeof(double) * k) != hipSuccess || nys_alloc_scratch(N)) {
       fprintf(stderr, "nfft4gp_amd: Nystrom allocation failed\n");
       return nullptr;
    }

@@ -17,6 +17,40 @@ from .nfft import _ptr
 
 
 class NystromPrecond:
+    """M^{-1} of the reference's Nystrom preconditioner (nys.c:115-173) held in HBM.
+
+    ``NystromPrecond(U, s, eta, perm)`` takes factors from anywhere (e.g. the reference's own setup);
+    ``NystromPrecond.from_additive(op, perm, k)`` builds them on the GPU from the dense additive kernel of
+    an NFFTAdditiveKernel's data and hyperparameters (Nfft4GPAmdNysSetupAdditive, nys.c:518-660)."""
+
+    @classmethod
+    def from_additive(cls, op, perm, k: int, k11: str = "reference"):
+        """k11 = "reference": the reference's K11 exactly (built from slices of the kernel's window
+        buffer, see include/nfft4gp_amd.h); "landmarks": K(perm[:k], perm[:k]) as the method intends."""
+        mode = {"reference": 0, "landmarks": 1}[k11]
+        perm = np.ascontiguousarray(np.asarray(perm, dtype=np.int32))
+        if perm.size != op.n:
+            raise ValueError("perm must be a permutation of the handle's n points")
+        self = cls.__new__(cls)
+        self.n, self.k = op.n, int(k)
+        self.h = _lib.lib().Nfft4GPAmdNysSetupAdditive(op.h, perm.ctypes.data, int(k), mode)
+        if not self.h:
+            raise RuntimeError("Nfft4GPAmdNysSetupAdditive failed (see stderr)")
+        eta = C.c_double()
+        _lib.lib().Nfft4GPAmdNysFactors(self.h, None, None, None, C.byref(eta))
+        self.eta = eta.value
+        return self
+
+    def factors(self, perm=None):
+        """(U, s, eta) with U's rows in the order of ``perm`` (the reference keeps them permuted)."""
+        U = np.zeros((self.n, self.k), order="F")
+        s = np.zeros(self.k)
+        eta = C.c_double()
+        p = None if perm is None else np.ascontiguousarray(np.asarray(perm, dtype=np.int32))
+        _lib.lib().Nfft4GPAmdNysFactors(self.h, p.ctypes.data if p is not None else None, U.ctypes.data,
+                                        s.ctypes.data, C.byref(eta))
+        return U, s, eta.value
+
     def __init__(self, U, s, eta: float, perm=None):
         U = np.asfortranarray(np.asarray(U, dtype=np.float64))
         n, k = U.shape

@@ -140,3 +140,75 @@ def test_preconditioned_pcg_matches_reference(torch_cuda):
     assert it_ref > 0 and it > 0
     assert abs(it - it_ref) <= max(2, int(0.05 * it_ref)), (it, it_ref)
     assert rel(x, x_ref) <= 1e-4
+
+
+# ---- GPU Nystrom setup (Nfft4GPAmdNysSetupAdditive) vs the reference's nys.c setup -------------------
+@needs_ref
+@pytest.mark.parametrize("kernel,l,k", [(0, 0.1, 32), (0, 0.3, 64), (1, 1.0, 48)])
+def test_gpu_nystrom_setup_matches_reference(torch_cuda, kernel, l, k):
+    torch = torch_cuda
+    n, d = 3000, 4
+    rng = np.random.default_rng(21)
+    X = rng.random((n, d))
+    win = np.arange(d, dtype=np.int32)
+    f, mu = 1.2, 0.02
+    perm = rng.permutation(n).astype(np.int32)
+    dense = O.RefDenseAdditive(X, win, d, 1, kernel=kernel)
+    ref = O.RefNystrom(dense, f, l, mu, k, perm)
+    U_ref, s_ref, eta_ref, _ = ref.factors()
+    op = amd.NFFTAdditiveKernel(X, win, d, 1)
+    assert op.setup(kernel, f, l, mu) == 0
+    pre = amd.NystromPrecond.from_additive(op, perm, k, k11="reference")
+    U, s, eta = pre.factors(perm)
+    assert eta == pytest.approx(eta_ref, rel=1e-15)
+    np.testing.assert_allclose(s, s_ref, rtol=1e-7)
+    # eigenvector signs are arbitrary: compare columns up to sign, and the sign-free apply
+    sign = np.sign(np.sum(U * U_ref, axis=0))
+    np.testing.assert_allclose(U * sign, U_ref, rtol=0, atol=1e-7 * np.abs(U_ref).max())
+    r = rng.random(n) - 0.5
+    x_ref = ref.solve(np.zeros(n), r.copy())
+    xd = torch.zeros(n, dtype=torch.float64, device="cuda")
+    pre.solve(xd, torch.tensor(r, device="cuda"))
+    assert rel(xd.cpu().numpy(), x_ref) < 1e-7
+
+
+def test_gpu_nystrom_setup_orthonormal_large(torch_cuda):
+    """Full-size property: U = U1 V w^{-1/2} has orthonormal columns (n = 2e5, k = 256, 8 windows)."""
+    n, d, k = 200_000, 8, 256
+    rng = np.random.default_rng(22)
+    X = rng.random((n, d))
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    assert op.setup(amd.GAUSSIAN, 1.0, 0.1, 0.01) == 0
+    pre = amd.NystromPrecond.from_additive(op, rng.permutation(n).astype(np.int32), k, k11="landmarks")
+    U, s, eta = pre.factors()
+    assert np.all(np.isfinite(U)) and np.all(s > 0) and np.all(np.diff(s) >= -1e-12 * s.max())
+    G = U.T @ U
+    assert np.abs(G - np.eye(k)).max() < 1e-6
+
+
+@pytest.mark.parametrize("kernel,l", [(0, 0.1), (1, 1.0)])
+def test_gpu_nystrom_landmarks_matches_numpy(torch_cuda, kernel, l):
+    """k11 = "landmarks": the same pipeline with K11 = K(perm[:k], perm[:k]), restated in numpy."""
+    n, d, k, f, mu = 2500, 3, 40, 1.1, 0.05
+    rng = np.random.default_rng(23)
+    X = rng.random((n, d))
+    perm = rng.permutation(n).astype(np.int32)
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    assert op.setup(kernel, f, l, mu) == 0
+    pre = amd.NystromPrecond.from_additive(op, perm, k, k11="landmarks")
+    U, s, eta = pre.factors(perm)
+
+    def kern(r2):
+        return np.exp(-r2 / (2 * l * l)) if kernel == 0 else np.exp(-np.sqrt(r2) / l)
+
+    Kp = sum(kern((X[perm, w][:, None] - X[perm[:k], w][None, :]) ** 2) for w in range(d)) * f * f / d
+    K11 = Kp[:k].copy()
+    fro = np.linalg.norm(K11)
+    Lc = np.linalg.cholesky(K11 + np.sqrt(k) * (np.nextafter(fro, fro + 1) - fro) * np.eye(k))
+    U1 = Kp @ np.linalg.inv(Lc).T
+    w1, V = np.linalg.eigh(U1.T @ U1)
+    Ur = (U1 @ V[:, ::-1]) / np.sqrt(w1[::-1])
+    s_r = 1.0 / (w1[::-1] + mu * f * f)
+    np.testing.assert_allclose(s, s_r, rtol=1e-7)
+    sign = np.sign(np.sum(U * Ur, axis=0))
+    np.testing.assert_allclose(U * sign, Ur, rtol=0, atol=1e-7 * np.abs(Ur).max())
