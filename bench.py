@@ -175,6 +175,29 @@ def run_pcg_single(op, torch, n, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1)
             "pcg_ms_per_iter": 1e3 * t / max(iters if iters > 0 else len(hist) - 1, 1)}
 
 
+def run_pcg_nystrom(op, torch, n, k, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1):
+    """PCG to 1e-6 with a rank-k Nystrom preconditioner set up on the GPU (nys.c:518-660 restated,
+    K11 = K(perm[:k], perm[:k]) -- the reference's own K11 is built from the wrong points)."""
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    assert op.setup(amd.GAUSSIAN, f=1.0, l=l_pcg, mu=0.01) == 0
+    perm = np.random.default_rng(rng_seed + 2).permutation(n).astype(np.int32)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    pre = amd.NystromPrecond.from_additive(op, perm, k, k11="landmarks")
+    torch.cuda.synchronize()
+    t_setup = time.time() - t0
+    b = torch.tensor(np.random.default_rng(rng_seed + 1).random(n) - 0.5, device="cuda")
+    x = torch.zeros(n, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    t0 = time.time()
+    _, relres, hist, iters = amd.pcg(op, b, x, maxits=maxits, tol=tol, precond=pre)
+    torch.cuda.synchronize()
+    t = time.time() - t0
+    pre.free()
+    return {"pcg_nys_rank": k, "pcg_nys_setup_s": t_setup, "pcg_nys_time_s": t, "pcg_nys_iters": iters,
+            "pcg_nys_rel_res": relres, "pcg_nys_total_s": t_setup + t}
+
+
 def run_pcg_sharded(op, sop, torch, dist, n, rb, re, tol=1e-6, maxits=3000, l_pcg=0.1):
     """Row-sharded CG (dist.py, pcg.c semantics): local HIP BLAS-1 + scalar all-reduces."""
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
@@ -206,6 +229,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcg", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
+    ap.add_argument("--nys-rank", type=int, default=512, help="rank of the Nystrom-preconditioned PCG (0: off)")
     ap.add_argument("--kernel-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.kernel_only:
@@ -333,6 +357,11 @@ def main():
         result["pcie_inclusive_matvecs_per_s"] = reps_h / (time.perf_counter() - t0)
         if not args.no_pcg:
             result.update(run_pcg_single(op, torch, n))
+            if args.nys_rank > 0:
+                try:
+                    result.update(run_pcg_nystrom(op, torch, n, args.nys_rank))
+                except Exception as e:  # report, do not fail the GPU measurement
+                    result["pcg_nys_error"] = repr(e)
         if not args.no_cpu_baseline:
             try:
                 result["cpu_baseline"] = cpu_baseline(n, d, X, x_host)

@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -398,6 +399,17 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
 {
    const int last_dw = dw - skip_last;
    const int D = (nw - 1) * dw + last_dw;
+   // NFFT4GP_AMD_VERBOSE=1: per-phase wall times on stderr
+   const bool verbose = getenv("NFFT4GP_AMD_VERBOSE") && atoi(getenv("NFFT4GP_AMD_VERBOSE")) > 0;
+   auto tic = std::chrono::steady_clock::now();
+   auto phase = [&](const char* name) {
+      if (!verbose) return;
+      (void)hipStreamSynchronize(current_stream());
+      const auto now = std::chrono::steady_clock::now();
+      fprintf(stderr, "nfft4gp_amd: nystrom %-10s %8.3f ms\n", name,
+              std::chrono::duration<double, std::milli>(now - tic).count());
+      tic = now;
+   };
    if (k <= 0 || k > n || D > kPanelMaxDims || last_dw <= 0) {
       fprintf(stderr, "nfft4gp_amd: Nystrom setup needs 0 < k <= n and <= %d window dimensions\n", kPanelMaxDims);
       return nullptr;
@@ -443,6 +455,7 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
                          f2 / nw, inv, d_Kp);
    if (hipGetLastError() != hipSuccess) return fail("panel launch");
 
+   phase("panel");
    // 2. K11, stable shift + Cholesky + inverse on the host (chol.c:446-466)
    std::vector<double> K11((size_t)k * k);
    if (k11_mode == 1) {
@@ -489,9 +502,11 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
       for (int i = 0; i < k; i++) Gt[i + (size_t)j * k] = K11[j + (size_t)i * k];
    if (hipMemcpy(d_B, Gt.data(), sizeof(double) * Gt.size(), hipMemcpyHostToDevice)) return fail("upload");
 
+   phase("k11+chol");
    // 3. U1 = Kp G^T  (dtrmm 'R' 'L' 'T', matops.c Nfft4GPTrilNystromMm)
    if (gemm(false, n, k, k, d_Kp, n, d_B, k, d_U1, n, nullptr, s)) return fail("gemm");
 
+   phase("gemm1");
    // 4. AA = U1^T U1, K = n split over row chunks (fixed order sum -> deterministic)
    const int nsplit = std::max(1, std::min(256, n / 8192));
    const int ksplit = ((n + nsplit - 1) / nsplit + kGemmK - 1) / kGemmK * kGemmK;
@@ -506,6 +521,7 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
                          cnt, d_AA);
       if (hipGetLastError() != hipSuccess) return fail("gram launch");
    }
+   phase("gram");
    std::vector<double> AA((size_t)k * k);
    if (hipMemcpyAsync(AA.data(), d_AA, sizeof(double) * AA.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
        hipStreamSynchronize(s) != hipSuccess)
@@ -515,6 +531,7 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    //    reference's 1e12 factor for sqrt(w1) < 1e-12 (matops.c Nfft4GPTrilNystromSvd)
    std::vector<double> w1, V;
    if (sym_eig(AA, k, w1, V)) return fail("eigensolver did not converge");
+   phase("eig");
    std::vector<double> W((size_t)k * k), sv(k);
    for (int c = 0; c < k; c++) {
       const int src = k - 1 - c;
@@ -531,6 +548,7 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    d_Kp = nullptr;
    if (gemm(false, n, k, k, d_U1, n, d_B, k, N->U, n, d_perm, s)) return fail("gemm");
 
+   phase("gemm2");
    // 6. s = max(1/(w^2 + eta), 0), eta = mu f^2 (nys.c:641-647)
    N->eta = mu * f2;
    std::vector<double> sh(k);

@@ -163,3 +163,27 @@ def test_emulated_kernels_match_oracle(kernel):
     for k in range(3):
         s = slice(k * n, (k + 1) * n)
         assert rel(g[s], gr[s]) < 1e-8
+
+
+def test_host_eigensolver_and_cholesky_inverse():
+    """The Nystrom setup's host k x k steps (nystrom.hip) against numpy/LAPACK."""
+    L = amd.lib()
+    rng = np.random.default_rng(8)
+    for n in (1, 7, 96, 300):
+        B = rng.standard_normal((n, n))
+        A = np.asfortranarray(B @ B.T + 0.5 * np.eye(n))
+        w = np.zeros(n)
+        V = np.zeros((n, n), order="F")
+        assert L.Nfft4GPAmdHostSymEig(A.ctypes.data, n, w.ctypes.data, V.ctypes.data) == 0
+        wr = np.linalg.eigvalsh(A)
+        assert np.all(np.diff(w) >= 0)                                  # ascending, as dsyev
+        assert np.abs(w - wr).max() <= 1e-13 * wr.max()
+        assert np.abs(A @ V - V * w).max() <= 1e-12 * wr.max()
+        assert np.abs(V.T @ V - np.eye(n)).max() <= 1e-13
+        G = np.zeros((n, n), order="F")
+        assert L.Nfft4GPAmdHostCholInverse(A.ctypes.data, n, 0.25, G.ctypes.data) == 0
+        Lc = np.linalg.cholesky(A + 0.25 * np.eye(n))
+        np.testing.assert_allclose(G, np.linalg.inv(Lc), rtol=0, atol=1e-12 * np.abs(np.linalg.inv(Lc)).max())
+    # not positive definite: the failing column is reported
+    A = np.asfortranarray(np.diag([1.0, -1.0, 2.0]))
+    assert L.Nfft4GPAmdHostCholInverse(A.ctypes.data, 3, 0.0, np.zeros(9).ctypes.data) == 2

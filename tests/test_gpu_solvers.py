@@ -144,7 +144,9 @@ def test_preconditioned_pcg_matches_reference(torch_cuda):
 
 # ---- GPU Nystrom setup (Nfft4GPAmdNysSetupAdditive) vs the reference's nys.c setup -------------------
 @needs_ref
-@pytest.mark.parametrize("kernel,l,k", [(0, 0.1, 32), (0, 0.3, 64), (1, 1.0, 48)])
+# cases where the reference's own factors are finite and moderately conditioned (its K11 quirk makes
+# e.g. a Gaussian at l = 0.3 with k = 64 produce s ~ 1e-16 and NaN columns)
+@pytest.mark.parametrize("kernel,l,k", [(0, 0.1, 32), (0, 0.05, 64), (0, 0.03, 128), (1, 1.0, 48), (1, 0.3, 96)])
 def test_gpu_nystrom_setup_matches_reference(torch_cuda, kernel, l, k):
     torch = torch_cuda
     n, d = 3000, 4
@@ -173,8 +175,9 @@ def test_gpu_nystrom_setup_matches_reference(torch_cuda, kernel, l, k):
 
 
 def test_gpu_nystrom_setup_orthonormal_large(torch_cuda):
-    """Full-size property: U = U1 V w^{-1/2} has orthonormal columns (n = 2e5, k = 256, 8 windows)."""
-    n, d, k = 200_000, 8, 256
+    """Full-size property: U = U1 V w^{-1/2} has orthonormal columns (n = 2e5, k = 256, 16 windows; the
+    additive kernel's numerical rank, ~30 per 1-D window at l = 0.1, stays above k)."""
+    n, d, k = 200_000, 16, 256
     rng = np.random.default_rng(22)
     X = rng.random((n, d))
     op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
