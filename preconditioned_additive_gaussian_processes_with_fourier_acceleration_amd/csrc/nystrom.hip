@@ -20,7 +20,9 @@
 // kernel matrix of buffer slices, not of the landmarks perm[:k] (checked against the compiled reference
 // to 1e-11).  k11_mode 0 reproduces that (parity); k11_mode 1 uses K(perm[:k], perm[:k]), the matrix the
 // method intends, which is what makes the preconditioner effective.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rocsolver/rocsolver.h>  // types and prototypes only: the library is dlopen'ed on first use
 
 #include <algorithm>
 #include <cfloat>
@@ -365,6 +367,76 @@ int sym_eig(const std::vector<double>& A, int n, std::vector<double>& w, std::ve
    return 0;
 }
 
+// ---- k x k helpers on the device -------------------------------------------------------------------
+__global__ void k_add_diag(double* A, int k, double nu)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < k) A[i + (size_t)i * k] += nu;
+}
+
+// Gt = (lower part of G)^T
+__global__ void k_transpose_lower(const double* __restrict__ G, int k, double* __restrict__ Gt)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
+   if (i < k) Gt[i + (size_t)j * k] = (j >= i) ? G[j + (size_t)i * k] : 0.0;
+}
+
+// W[:, c] = V[:, k-1-c] / sqrt(w1[k-1-c]) (x 1e12 when sqrt(w1) < 1e-12), s[c] = max(1/(w^2 + eta), 0)
+// (matops.c Nfft4GPTrilNystromSvd, nys.c:641-647; NFFT4GP_MAX maps NaN to 0)
+__global__ void k_nys_scale(const double* __restrict__ V, const double* __restrict__ w1, int k, double eta,
+                            double* __restrict__ W, double* __restrict__ s)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y;
+   const int src = k - 1 - c;
+   const double wi = sqrt(w1[src]);
+   if (i < k) W[i + (size_t)c * k] = V[i + (size_t)src * k] * ((wi < 1e-12) ? 1e12 : 1.0 / wi);
+   if (i == 0) {
+      const double v = 1.0 / (wi * wi + eta);
+      s[c] = (v >= 0.0) ? v : 0.0;
+   }
+}
+
+__global__ void k_iota(int* p, int k)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < k) p[i] = i;
+}
+
+// rocSOLVER (dpotrf / dtrtri / dsyevd) loaded on first use: with PyTorch in the process it binds to the
+// copy PyTorch already loaded (one ROCm runtime per process); without it, to /opt/rocm.  If it cannot be
+// loaded the k x k steps run on the host instead (NFFT4GP_AMD_NO_ROCSOLVER=1 forces that).
+struct RocSolver {
+   bool ok = false;
+   rocblas_handle h = nullptr;
+   decltype(&rocblas_set_stream) set_stream = nullptr;
+   decltype(&rocsolver_dpotrf) potrf = nullptr;
+   decltype(&rocsolver_dtrtri) trtri = nullptr;
+   decltype(&rocsolver_dsyevd) syevd = nullptr;
+};
+
+RocSolver& rocsolver()
+{
+   static RocSolver R;
+   static bool tried = false;
+   if (tried) return R;
+   tried = true;
+   if (getenv("NFFT4GP_AMD_NO_ROCSOLVER") && atoi(getenv("NFFT4GP_AMD_NO_ROCSOLVER")) > 0) return R;
+   void* hb = dlopen("librocblas.so.5", RTLD_NOW | RTLD_GLOBAL);
+   if (!hb) hb = dlopen("/opt/rocm/lib/librocblas.so.5", RTLD_NOW | RTLD_GLOBAL);
+   void* hs = dlopen("librocsolver.so.0", RTLD_NOW | RTLD_GLOBAL);
+   if (!hs) hs = dlopen("/opt/rocm/lib/librocsolver.so.0", RTLD_NOW | RTLD_GLOBAL);
+   if (!hb || !hs) return R;
+   auto create = (decltype(&rocblas_create_handle))dlsym(hb, "rocblas_create_handle");
+   R.set_stream = (decltype(&rocblas_set_stream))dlsym(hb, "rocblas_set_stream");
+   R.potrf = (decltype(&rocsolver_dpotrf))dlsym(hs, "rocsolver_dpotrf");
+   R.trtri = (decltype(&rocsolver_dtrtri))dlsym(hs, "rocsolver_dtrtri");
+   R.syevd = (decltype(&rocsolver_dsyevd))dlsym(hs, "rocsolver_dsyevd");
+   if (!create || !R.set_stream || !R.potrf || !R.trtri || !R.syevd) return R;
+   if (create(&R.h) != rocblas_status_success) return R;
+   R.ok = true;
+   return R;
+}
+
 template <class T>
 int dalloc(T** p, size_t count)
 {
@@ -416,13 +488,17 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    }
    hipStream_t s = current_stream();
    double *d_xw = nullptr, *d_Kp = nullptr, *d_U1 = nullptr, *d_B = nullptr, *d_part = nullptr, *d_AA = nullptr;
-   int* d_perm = nullptr;
+   double *d_K11 = nullptr, *d_w1 = nullptr, *d_e = nullptr, *d_s = nullptr;
+   int *d_perm = nullptr, *d_iota = nullptr, *d_info = nullptr;
    NysDev* N = nullptr;
+   auto release = [&]() {
+      for (double* p : {d_xw, d_U1, d_B, d_part, d_AA, d_K11, d_w1, d_e, d_s}) (void)hipFree(p);
+      for (int* p : {d_perm, d_iota, d_info}) (void)hipFree(p);
+   };
    auto fail = [&](const char* what) -> NysDev* {
       if (what) fprintf(stderr, "nfft4gp_amd: Nystrom setup: %s\n", what);
       (void)hipStreamSynchronize(s);
-      for (double* p : {d_xw, d_U1, d_B, d_part, d_AA}) (void)hipFree(p);
-      (void)hipFree(d_perm);
+      release();
       if (N) {
          (void)hipFree(N->U);
          (void)hipFree(N->s);
@@ -435,7 +511,7 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
       return nullptr;
    };
    const size_t nk = (size_t)n * k;
-   if (dalloc(&d_xw, (size_t)n * nw * dw) || dalloc(&d_perm, (size_t)n) || dalloc(&d_Kp, nk) ||
+   if (dalloc(&d_xw, (size_t)n * nw * dw) || dalloc(&d_perm, (size_t)n) || dalloc(&d_info, 1) || dalloc(&d_Kp, nk) ||
        dalloc(&d_U1, nk) || dalloc(&d_B, (size_t)k * k) || dalloc(&d_AA, (size_t)k * k))
       return fail("allocation");
    if (hipMemcpy(d_xw, xw_host, sizeof(double) * (size_t)n * ((nw - 1) * dw + last_dw), hipMemcpyHostToDevice) ||
@@ -456,51 +532,66 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    if (hipGetLastError() != hipSuccess) return fail("panel launch");
 
    phase("panel");
-   // 2. K11, stable shift + Cholesky + inverse on the host (chol.c:446-466)
-   std::vector<double> K11((size_t)k * k);
+   // 2. K11 on the device: the landmark block of the panel (mode 1), or the reference's K11 (mode 0:
+   //    nys.c:569 hands the k x d sub-data to Nfft4GPKernelAdditiveKernel, which ignores it and reads
+   //    window i of its own gathered buffer at offset i*n*dwindows with n = k, kernels.c:3160 -- the
+   //    panel kernel over that buffer with n = k and the identity permutation)
+   if (dalloc(&d_K11, (size_t)k * k) || dalloc(&d_iota, (size_t)k)) return fail("allocation");
    if (k11_mode == 1) {
-      // landmarks: K(perm[:k], perm[:k]) = the first k rows of the panel
-      if (hipMemcpy2DAsync(K11.data(), sizeof(double) * k, d_Kp, sizeof(double) * n, sizeof(double) * k, k,
-                           hipMemcpyDeviceToHost, s) != hipSuccess ||
-          hipStreamSynchronize(s) != hipSuccess)
-         return fail("K11 download");
+      if (hipMemcpy2DAsync(d_K11, sizeof(double) * k, d_Kp, sizeof(double) * n, sizeof(double) * k, k,
+                           hipMemcpyDeviceToDevice, s) != hipSuccess)
+         return fail("K11 copy");
    } else {
-      // the reference: nys.c:569 hands the k x d sub-data to Nfft4GPKernelAdditiveKernel, which ignores
-      // its data argument and reads window i of its own gathered buffer at offset i*n*dwindows with
-      // n = k (kernels.c:3160), i.e. coordinate t of "point" p of window i is buffer[i*k*dw + t*k + p]
-      for (int j = 0; j < k; j++)
-         for (int i = j; i < k; i++) {
-            double acc = 0.0;
-            for (int w = 0; w < nw; w++) {
-               const int dims = (w == nw - 1) ? last_dw : dw;
-               const double* base = xw_host + (size_t)w * k * dw;
-               double r2 = 0.0;
-               for (int t = 0; t < dims; t++) {
-                  const double df = base[(size_t)t * k + i] - base[(size_t)t * k + j];
-                  r2 += df * df;
-               }
-               acc += (kernel == 0) ? std::exp(-r2 * inv) : std::exp(-std::sqrt(r2) * inv);
-            }
-            K11[i + (size_t)j * k] = K11[j + (size_t)i * k] = (f2 / nw) * acc;
-         }
+      hipLaunchKernelGGL(k_iota, dim3((k + 255) / 256), dim3(256), 0, s, d_iota, k);
+      dim3 kgrid((k + kPanelRows - 1) / kPanelRows, (k + kPanelCols - 1) / kPanelCols);
+      if (kernel == 0)
+         hipLaunchKernelGGL(k_nys_panel<0>, kgrid, dim3(kPanelThreads), lds, s, d_xw, k, nw, dw, last_dw, d_iota, k,
+                            f2 / nw, inv, d_K11);
+      else
+         hipLaunchKernelGGL(k_nys_panel<1>, kgrid, dim3(kPanelThreads), lds, s, d_xw, k, nw, dw, last_dw, d_iota, k,
+                            f2 / nw, inv, d_K11);
    }
-   double fro = 0.0;  // dlansy('F', 'L'): the lower triangle, off-diagonals counted twice
+   // stable shift nu = sqrt(k) ulp(|K11|_F) (chol.c:449-465; dlansy 'F' 'L' = the full-matrix norm)
+   std::vector<double> K11((size_t)k * k);
+   if (hipMemcpyAsync(K11.data(), d_K11, sizeof(double) * K11.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess)
+      return fail("K11 download");
+   double fro = 0.0;
    for (int j = 0; j < k; j++) {
       fro += K11[j + (size_t)j * k] * K11[j + (size_t)j * k];
       for (int i = j + 1; i < k; i++) fro += 2.0 * K11[i + (size_t)j * k] * K11[i + (size_t)j * k];
    }
    fro = std::sqrt(fro);
    const double nu = std::sqrt((double)k) * (std::nextafter(fro, fro + 1.0) - fro);
-   for (int j = 0; j < k; j++) K11[j + (size_t)j * k] += nu;
-   if (int info = chol_lower(K11, k)) {
-      fprintf(stderr, "nfft4gp_amd: Nystrom setup: K11 + shift is not positive definite (column %d)\n", info);
-      return fail(nullptr);
+   RocSolver& R = rocsolver();
+   if (R.ok) {
+      // L = chol(K11 + nu I), G = L^{-1}, Gt = G^T, all on the device
+      int info = 0;
+      R.set_stream(R.h, s);
+      hipLaunchKernelGGL(k_add_diag, dim3((k + 255) / 256), dim3(256), 0, s, d_K11, k, nu);
+      if (R.potrf(R.h, rocblas_fill_lower, k, d_K11, k, d_info) != rocblas_status_success ||
+          hipMemcpyAsync(&info, d_info, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+         return fail("rocsolver_dpotrf");
+      if (info) {
+         fprintf(stderr, "nfft4gp_amd: Nystrom setup: K11 + shift is not positive definite (column %d)\n", info);
+         return fail(nullptr);
+      }
+      if (R.trtri(R.h, rocblas_fill_lower, rocblas_diagonal_non_unit, k, d_K11, k, d_info) != rocblas_status_success)
+         return fail("rocsolver_dtrtri");
+      hipLaunchKernelGGL(k_transpose_lower, dim3((k + 255) / 256, k), dim3(256), 0, s, d_K11, k, d_B);
+   } else {
+      for (int j = 0; j < k; j++) K11[j + (size_t)j * k] += nu;
+      if (int info = chol_lower(K11, k)) {
+         fprintf(stderr, "nfft4gp_amd: Nystrom setup: K11 + shift is not positive definite (column %d)\n", info);
+         return fail(nullptr);
+      }
+      trtri_lower(K11, k);  // G = L^{-1}
+      std::vector<double> Gt((size_t)k * k);
+      for (int j = 0; j < k; j++)
+         for (int i = 0; i < k; i++) Gt[i + (size_t)j * k] = (j >= i) ? K11[j + (size_t)i * k] : 0.0;
+      if (hipMemcpy(d_B, Gt.data(), sizeof(double) * Gt.size(), hipMemcpyHostToDevice)) return fail("upload");
    }
-   trtri_lower(K11, k);  // G = L^{-1}
-   std::vector<double> Gt((size_t)k * k);
-   for (int j = 0; j < k; j++)
-      for (int i = 0; i < k; i++) Gt[i + (size_t)j * k] = K11[j + (size_t)i * k];
-   if (hipMemcpy(d_B, Gt.data(), sizeof(double) * Gt.size(), hipMemcpyHostToDevice)) return fail("upload");
 
    phase("k11+chol");
    // 3. U1 = Kp G^T  (dtrmm 'R' 'L' 'T', matops.c Nfft4GPTrilNystromMm)
@@ -522,43 +613,43 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
       if (hipGetLastError() != hipSuccess) return fail("gram launch");
    }
    phase("gram");
-   std::vector<double> AA((size_t)k * k);
-   if (hipMemcpyAsync(AA.data(), d_AA, sizeof(double) * AA.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
-       hipStreamSynchronize(s) != hipSuccess)
-      return fail("gram download");
-
-   // 5. eig(AA) (dsyev: ascending); U = U1 V diag(w1^-1/2), columns in descending w1 order, with the
-   //    reference's 1e12 factor for sqrt(w1) < 1e-12 (matops.c Nfft4GPTrilNystromSvd)
-   std::vector<double> w1, V;
-   if (sym_eig(AA, k, w1, V)) return fail("eigensolver did not converge");
-   phase("eig");
-   std::vector<double> W((size_t)k * k), sv(k);
-   for (int c = 0; c < k; c++) {
-      const int src = k - 1 - c;
-      const double wi = std::sqrt(w1[src]);
-      sv[c] = wi;
-      const double scale = (wi < 1e-12) ? 1e12 : 1.0 / wi;
-      for (int i = 0; i < k; i++) W[i + (size_t)c * k] = V[i + (size_t)src * k] * scale;
+   // 5. eig(AA) = V diag(w1) V^T (dsyev: ascending); W = V(:, reversed) diag(w1^-1/2) with the
+   //    reference's 1e12 factor for sqrt(w1) < 1e-12 (matops.c Nfft4GPTrilNystromSvd); s (nys.c:641-647)
+   const double eta = mu * f2;
+   if (dalloc(&d_w1, (size_t)k) || dalloc(&d_e, (size_t)k) || dalloc(&d_s, (size_t)k)) return fail("allocation");
+   if (R.ok) {
+      int info = 0;
+      if (R.syevd(R.h, rocblas_evect_original, rocblas_fill_lower, k, d_AA, k, d_w1, d_e, d_info) !=
+              rocblas_status_success ||
+          hipMemcpyAsync(&info, d_info, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess || info)
+         return fail("rocsolver_dsyevd");
+   } else {
+      std::vector<double> AA((size_t)k * k);
+      if (hipMemcpyAsync(AA.data(), d_AA, sizeof(double) * AA.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+         return fail("gram download");
+      std::vector<double> w1, V;
+      if (sym_eig(AA, k, w1, V)) return fail("eigensolver did not converge");
+      if (hipMemcpy(d_AA, V.data(), sizeof(double) * V.size(), hipMemcpyHostToDevice) ||
+          hipMemcpy(d_w1, w1.data(), sizeof(double) * k, hipMemcpyHostToDevice))
+         return fail("upload");
    }
-   if (hipMemcpy(d_B, W.data(), sizeof(double) * W.size(), hipMemcpyHostToDevice)) return fail("upload");
+   hipLaunchKernelGGL(k_nys_scale, dim3((k + 255) / 256, k), dim3(256), 0, s, d_AA, d_w1, k, eta, d_B, d_s);
+   phase("eig");
    N = new NysDev();
    N->n = n;
    N->k = k;
    N->U = d_Kp;  // the panel's storage is reused for U (rows scattered back to natural order)
    d_Kp = nullptr;
    if (gemm(false, n, k, k, d_U1, n, d_B, k, N->U, n, d_perm, s)) return fail("gemm");
-
-   phase("gemm2");
-   // 6. s = max(1/(w^2 + eta), 0), eta = mu f^2 (nys.c:641-647)
-   N->eta = mu * f2;
-   std::vector<double> sh(k);
-   for (int c = 0; c < k; c++) sh[c] = std::max(1.0 / (sv[c] * sv[c] + N->eta), 0.0);
-   if (dalloc(&N->s, (size_t)k) || hipMemcpyAsync(N->s, sh.data(), sizeof(double) * k, hipMemcpyHostToDevice, s) ||
-       nys_alloc_scratch(N))
-      return fail("allocation");
+   N->eta = eta;
+   N->s = d_s;
+   d_s = nullptr;
+   if (nys_alloc_scratch(N)) return fail("allocation");
    if (hipStreamSynchronize(s) != hipSuccess) return fail("sync");
-   for (double* p : {d_xw, d_U1, d_B, d_part, d_AA}) (void)hipFree(p);
-   (void)hipFree(d_perm);
+   phase("gemm2");
+   release();
    return N;
 }
 
