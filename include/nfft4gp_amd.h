@@ -14,7 +14,7 @@
  *  - every computation runs on the GPU; there is no CPU fallback.  If no HIP device is present the
  *    operator entry points print an error and return -1.
  *  - Nfft4GPSolverPcg keeps its vectors in HBM.  Callbacks of this library (the NFFT matvecs,
- *    Nfft4GPAmdNysSolve) receive device pointers; any other callback -- e.g. the reference's own
+ *    Nfft4GPAmdNysSolve, Nfft4GPAmdFsaiSolve, Nfft4GPAmdAfnSolve) receive device pointers; any other callback -- e.g. the reference's own
  *    Nfft4GPDenseMatSymv -- is called with HOST vectors staged around the call, exactly as the
  *    reference calls it (see Nfft4GPAmdSetCallbackPointerMode).
  *
@@ -172,6 +172,28 @@ void *Nfft4GPAmdNysSetupAdditive(void *str, const int *perm, int k, int k11_mode
  * (pass the setup's perm to get the reference's permuted row order, NULL for natural order), s (k),
  * eta; any output may be NULL */
 int Nfft4GPAmdNysFactors(void *nys, const int *perm, NFFT4GP_DOUBLE *U, NFFT4GP_DOUBLE *s, NFFT4GP_DOUBLE *eta);
+
+/* ---- FSAI preconditioner apply (SRC/preconds/fsai.c:106-123) --------------------------------------
+ * The reference's Nfft4GPPrecondFsaiSetupWithKernel (fsai.c:333-...) produces the lower-triangular
+ * factor L in CSR (precond_fsai _L_i, _L_j, _L_a; fsai.h:11-58).  Nfft4GPAmdFsaiCreate takes those
+ * three host arrays (n+1, nnz, nnz) and keeps L and L^T in HBM. */
+void *Nfft4GPAmdFsaiCreate(int n, const int *L_i, const int *L_j, const NFFT4GP_DOUBLE *L_a);
+/* same signature and result as Nfft4GPPrecondFsaiSolve (fsai.c:106): x = L^T (L rhs); each row is summed
+ * in the reference's order with unfused multiply-adds, so x is bitwise the reference's */
+int Nfft4GPAmdFsaiSolve(void *fsai, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
+void Nfft4GPAmdFsaiFree(void *fsai);
+
+/* ---- AFN preconditioner apply (SRC/preconds/afn.c:82-143) -----------------------------------------
+ * precond_afn (afn.h:14-85) holds perm (n), the Cholesky factor of A11 = K(perm[:k], perm[:k]) + noise
+ * (k x k lower, column-major), K12 = K(perm[:k], perm[k:]) (k x (n-k) column-major) and the FSAI of the
+ * Schur complement (an Nfft4GPAmdFsaiCreate handle of size n-k, not owned).  0 <= k <= n: k = 0 applies
+ * the FSAI alone, k = n solves with A11 on the unpermuted rhs, as afn.c:101-110 does.  AFN is not in the
+ * reference's build (Makefile:3-26 lists chol, fsai, nys only); this is its apply. */
+void *Nfft4GPAmdAfnCreate(int n, int k, const int *perm, const NFFT4GP_DOUBLE *L11, const NFFT4GP_DOUBLE *K12,
+                          void *fsai_schur);
+/* same signature as Nfft4GPPrecondAFNSolve (afn.c:82) */
+int Nfft4GPAmdAfnSolve(void *afn, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
+void Nfft4GPAmdAfnFree(void *afn);
 
 /* ---- MI355X extensions --------------------------------------------------------------------------- */
 /* stream every kernel of this library is enqueued on (hipStream_t; NULL = null stream) */

@@ -301,3 +301,154 @@ class RefNystrom:
     def solve(self, x, rhs):
         self.lib.Nfft4GPPrecondNysSolve(C.c_void_p(self.h), self.n, _d(x), _d(rhs))
         return x
+
+
+# ----------------------------------------------------------------------------------------------
+# FSAI preconditioner of the reference (SRC/preconds/fsai.c), driven through oracle/_ref, and the
+# AFN apply (SRC/preconds/afn.c:82-143, not in the reference build) restated in numpy on top of it
+# ----------------------------------------------------------------------------------------------
+class PrecondFsaiStruct(C.Structure):
+    """precond_fsai, SRC/preconds/fsai.h:22-39."""
+    _fields_ = [
+        ("_lfil", C.c_int), ("_n", C.c_int), ("_tits", C.c_int), ("_titt", C.c_double), ("_tset", C.c_double),
+        ("_tlogdet", C.c_double), ("_tdvp", C.c_double), ("_L_i", _ip), ("_L_j", _ip), ("_L_a", _dp),
+        ("_dL_a", _dp), ("_work", _dp),
+    ]
+
+
+def ref_gaussian_params(f, l, mu, max_n):
+    """Nfft4GPKernelParamCreate (kernels.c:404-440) with _params = (f, l), _noise_level = mu; omp = 1 gives
+    each OpenMP thread its own _dwork (the FSAI setup calls the kernel inside a parallel region)."""
+    lib = ref_lib()
+    h = lib.Nfft4GPKernelParamCreate(int(max_n), 1)
+    st = NfftKernelStruct.from_address(h)
+    st._params[0] = f
+    st._params[1] = l
+    st._noise_level = mu
+    return h
+
+
+def ref_gaussian_matrix(params, data, permr=None, permc=None):
+    """The reference's Nfft4GPKernelGaussianKernel (kernels.c:680-1289): K(permr, permc) (no noise),
+    K(permr, permr) + noise when permc is None (only its lower triangle is written), the full matrix f^2 (exp(-|xi - xj|^2 / 2 l^2) + mu I)
+    when no permutation is given."""
+    lib = ref_lib()
+    data = np.asfortranarray(data, dtype=np.float64)
+    n, d = data.shape
+    K = _dp()
+    if permr is None:
+        lib.Nfft4GPKernelGaussianKernel(params, _d(data), n, n, d, None, 0, None, 0, C.byref(K), None)
+        kr = kc = n
+    elif permc is None:
+        pr = np.ascontiguousarray(permr, dtype=np.int32)
+        kr = kc = pr.size
+        lib.Nfft4GPKernelGaussianKernel(params, _d(data), n, n, d, _i(pr), kr, None, 0, C.byref(K), None)
+    else:
+        pr = np.ascontiguousarray(permr, dtype=np.int32)
+        pc = np.ascontiguousarray(permc, dtype=np.int32)
+        kr, kc = pr.size, pc.size
+        lib.Nfft4GPKernelGaussianKernel(params, _d(data), n, n, d, _i(pr), kr, _i(pc), kc, C.byref(K), None)
+    out = np.ctypeslib.as_array(K, shape=(kr * kc,)).reshape(kr, kc, order="F").copy()
+    C.CDLL(None).free(K)
+    return out
+
+
+class RefFsai:
+    """Nfft4GPPrecondFsaiSetupWithKernel (fsai.c:302-312: KNN pattern of `data`, per-row Cholesky solves
+    on kernel submatrices) and its apply Nfft4GPPrecondFsaiSolve (fsai.c:106-123), via oracle/_ref.
+    ``kernel`` names a func_kernel of the reference (default its dense Gaussian kernel, kernels.c:680)
+    and ``params`` its parameter handle."""
+
+    def __init__(self, data, params, lfil, kernel="Nfft4GPKernelGaussianKernel"):
+        lib = ref_lib()
+        self.lib = lib
+        lib.Nfft4GPPrecondFsaiCreate.restype = C.c_void_p
+        lib.Nfft4GPPrecondFsaiSetLfil.argtypes = [C.c_void_p, C.c_int]
+        lib.Nfft4GPPrecondFsaiSetupWithKernel.argtypes = [_dp, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                                          C.c_void_p, C.c_int, C.c_void_p]
+        lib.Nfft4GPPrecondFsaiSolve.argtypes = [C.c_void_p, C.c_int, _dp, _dp]
+        self._data = np.asfortranarray(data, dtype=np.float64)
+        n, d = self._data.shape
+        self.n = n
+        self.h = lib.Nfft4GPPrecondFsaiCreate()
+        lib.Nfft4GPPrecondFsaiSetLfil(self.h, lfil)
+        fk = C.cast(getattr(lib, kernel), C.c_void_p)
+        rc = lib.Nfft4GPPrecondFsaiSetupWithKernel(_d(self._data), n, n, d, fk, params, 0, self.h)
+        assert rc == 0
+        self.st = PrecondFsaiStruct.from_address(self.h)
+
+    def csr(self):
+        n = self.n
+        ia = np.ctypeslib.as_array(self.st._L_i, shape=(n + 1,)).copy()
+        nnz = int(ia[n])
+        ja = np.ctypeslib.as_array(self.st._L_j, shape=(nnz,)).copy()
+        aa = np.ctypeslib.as_array(self.st._L_a, shape=(nnz,)).copy()
+        return ia, ja, aa
+
+    def solve(self, rhs):
+        rhs = np.ascontiguousarray(rhs, dtype=np.float64)
+        x = np.zeros(self.n)
+        self.lib.Nfft4GPPrecondFsaiSolve(C.c_void_p(self.h), self.n, _d(x), _d(rhs))
+        return x
+
+
+def ref_schur_params(data, perm, k, chol_K11, gauss_params):
+    """Nfft4GPKernelSchurCombineKernelParamCreate (kernels.c:3496-3596, no gradient): the kernel of the
+    Schur complement K22 - K21 K11^{-1} K12 the reference's AFN setup hands to FSAI (afn.c:473)."""
+    lib = ref_lib()
+    f = lib.Nfft4GPKernelSchurCombineKernelParamCreate
+    f.restype = C.c_void_p
+    f.argtypes = [_dp, C.c_int, C.c_int, C.c_int, _ip, C.c_int, _dp, _dp, C.c_void_p, C.c_void_p, C.c_int,
+                  C.c_int]
+    data = np.asfortranarray(data, dtype=np.float64)
+    n, d = data.shape
+    perm = np.ascontiguousarray(perm, dtype=np.int32)
+    L = np.asfortranarray(chol_K11, dtype=np.float64)
+    fk = C.cast(lib.Nfft4GPKernelGaussianKernel, C.c_void_p)
+    keep = (data, perm, L)
+    return f(_d(data), n, n, d, _i(perm), k, _d(L), None, fk, gauss_params, 1, 0), keep
+
+
+def csr_mv(ia, ja, aa, x, trans=False):
+    """Nfft4GPCsrMv (matops.c:139-272) with alpha = 1, beta = 0: y = L x ('N') or L^T x ('T')."""
+    n = ia.size - 1
+    rows = np.repeat(np.arange(n), np.diff(ia))
+    nnz = int(ia[n])
+    prod = aa[:nnz] * (x[rows] if trans else x[ja[:nnz]])
+    y = np.zeros(n)
+    np.add.at(y, ja[:nnz] if trans else rows, prod)
+    return y
+
+
+def fsai_apply(ia, ja, aa, rhs):
+    """Nfft4GPPrecondFsaiSolve (fsai.c:106-123): x = L^T (L rhs)."""
+    return csr_mv(ia, ja, aa, csr_mv(ia, ja, aa, rhs), trans=True)
+
+
+def gaussian_block(X, f, l, rows, cols):
+    """f^2 exp(-|x_r - x_c|^2 / 2 l^2), the off-diagonal blocks of kernels.c:680-1289."""
+    A, B = X[rows], X[cols]
+    D = ((A[:, None, :] - B[None, :, :]) ** 2).sum(-1)
+    return f * f * np.exp(-D / (2.0 * l * l))
+
+
+def afn_apply(perm, L11, K12, schur_solve, rhs):
+    """Nfft4GPPrecondAFNSolve (afn.c:82-143) restated: [rp; rp2] = rhs(perm); y = A11 \\ rp (A11 = L11
+    L11^T); rp2 -= K12^T y; y2 = S^{-1} rp2; rp -= K12 y2; y = A11 \\ rp; x(perm) = [y; y2].
+    k = 0 applies schur_solve to rhs; k = n solves with A11 on the unpermuted rhs (afn.c:101-110)."""
+    import scipy.linalg as sl
+    n = rhs.shape[0]
+    k = L11.shape[0]
+    if k == 0:
+        return schur_solve(rhs)
+    if k == n:
+        return sl.cho_solve((L11, True), rhs)
+    rp = rhs[perm].copy()
+    y = sl.cho_solve((L11, True), rp[:k])
+    rp2 = rp[k:] - K12.T @ y
+    y2 = schur_solve(rp2)
+    r1 = rp[:k] - K12 @ y2
+    y = sl.cho_solve((L11, True), r1)
+    x = np.empty(n)
+    x[perm] = np.concatenate([y, y2])
+    return x

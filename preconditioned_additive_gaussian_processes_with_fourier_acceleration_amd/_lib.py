@@ -82,6 +82,12 @@ _SIGS = {
     "Nfft4GPAmdNysFree": (None, [vp]),
     "Nfft4GPAmdNysSetupAdditive": (vp, [vp, vp, C.c_int, C.c_int]),
     "Nfft4GPAmdNysFactors": (C.c_int, [vp, vp, vp, vp, dp]),
+    "Nfft4GPAmdFsaiCreate": (vp, [C.c_int, vp, vp, vp]),
+    "Nfft4GPAmdFsaiSolve": (C.c_int, [vp, C.c_int, vp, vp]),
+    "Nfft4GPAmdFsaiFree": (None, [vp]),
+    "Nfft4GPAmdAfnCreate": (vp, [C.c_int, C.c_int, vp, vp, vp, vp]),
+    "Nfft4GPAmdAfnSolve": (C.c_int, [vp, C.c_int, vp, vp]),
+    "Nfft4GPAmdAfnFree": (None, [vp]),
     "Nfft4GPAmdSetStream": (None, [vp]),
     "Nfft4GPAmdGetStream": (vp, []),
     "Nfft4GPAmdDeviceAvailable": (C.c_int, []),

@@ -1,0 +1,322 @@
+// fsai_afn.hip -- FSAI and AFN preconditioner applies in HBM.
+//
+//   Nfft4GPAmdFsai*  SRC/preconds/fsai.c:106-123  x = L^T (L rhs), L lower CSR (diagonal
+//                    last), both products through Nfft4GPCsrMv (matops.c:139-272).  L^T is kept as its
+//                    own CSR (built at create, entries in ascending row order) so both products are
+//                    row-parallel gathers; each row sums in the reference's order with unfused multiply
+//                    and add, so the result is bitwise the reference's.
+//   Nfft4GPAmdAfn*   SRC/preconds/afn.c:82-143 (not part of the reference build): with [rp; rp2] =
+//                    rhs(perm), y = A11 \ rp, rp2 -= A12^T y, y2 = FSAI(rp2), rp -= A12 y2, y = A11 \ rp,
+//                    x(perm) = [y; y2].  A11 \ . uses L11^{-1} (two triangular products) instead of the
+//                    reference's Cholesky solves.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "internal.h"
+
+namespace nfft4gp_amd {
+
+namespace {
+
+struct FsaiDev {
+   int n = 0;
+   int *ia = nullptr, *ja = nullptr;  // L
+   double* aa = nullptr;
+   int *tia = nullptr, *tja = nullptr;  // L^T
+   double* taa = nullptr;
+   double* work = nullptr;
+};
+
+struct AfnDev {
+   int n = 0, k = 0, n2 = 0;
+   int* perm = nullptr;
+   double* Linv = nullptr;  // k x k, inverse of the lower Cholesky factor of A11
+   double* K12 = nullptr;   // k x n2 column-major
+   FsaiDev* S = nullptr;    // FSAI of the Schur complement (n2)
+   bool own_S = false;
+   double *rp = nullptr, *y = nullptr, *t = nullptr, *part = nullptr;
+   int nblk = 0;
+};
+
+// y[i] = sum_j a[j] x[ja[j]] in the row's stored order, unfused (matops.c:239-248)
+__global__ void k_csr_rows(const int* __restrict__ ia, const int* __restrict__ ja, const double* __restrict__ a,
+                           const double* __restrict__ x, double* __restrict__ y, int n)
+{
+#pragma clang fp contract(off)  // the reference's host build multiplies and adds separately (no FMA)
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= n) return;
+   double r = 0.0;
+   for (int j = ia[i]; j < ia[i + 1]; j++) r += a[j] * x[ja[j]];
+   y[i] = r;
+}
+
+__global__ void k_gather(const double* __restrict__ src, const int* __restrict__ perm, int n, double* __restrict__ dst)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) dst[i] = src[perm[i]];
+}
+
+__global__ void k_scatter(const double* __restrict__ src, const int* __restrict__ perm, int n, double* __restrict__ dst)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) dst[perm[i]] = src[i];
+}
+
+// out = Linv v (lower) or Linv^T v
+__global__ void k_trmv(const double* __restrict__ Linv, int k, const double* __restrict__ v, double* __restrict__ out,
+                       int trans)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= k) return;
+   double r = 0.0;
+   if (!trans)
+      for (int j = 0; j <= i; j++) r = fma(Linv[i + (size_t)j * k], v[j], r);
+   else
+      for (int j = i; j < k; j++) r = fma(Linv[j + (size_t)i * k], v[j], r);
+   out[i] = r;
+}
+
+// rp2[j] -= sum_i K12[i + j*k] y[i]  (one wave per column)
+__global__ __launch_bounds__(256) void k_a12t(const double* __restrict__ K12, int k, int n2, const double* __restrict__ y,
+                                              double* __restrict__ rp2)
+{
+   const int lane = threadIdx.x & 63;
+   const long long j = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+   if (j >= n2) return;
+   const double* col = K12 + j * k;
+   double r = 0.0;
+   for (int i = lane; i < k; i += 64) r = fma(col[i], y[i], r);
+   for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off, 64);
+   if (lane == 0) rp2[j] -= r;
+}
+
+// part[blk][i] = sum_{j in blk} K12[i + j*k] y2[j]
+constexpr int kA12Cols = 1024;
+__global__ void k_a12_part(const double* __restrict__ K12, int k, int n2, const double* __restrict__ y2,
+                           double* __restrict__ part)
+{
+   const int j0 = blockIdx.x * kA12Cols, j1 = min(n2, j0 + kA12Cols);
+   for (int i = threadIdx.x; i < k; i += blockDim.x) {
+      double r = 0.0;
+      for (int j = j0; j < j1; j++) r = fma(K12[i + (size_t)j * k], y2[j], r);
+      part[(size_t)blockIdx.x * k + i] = r;
+   }
+}
+
+// rp[i] -= sum_blk part[blk][i]
+__global__ void k_a12_reduce(const double* __restrict__ part, int nblk, int k, double* __restrict__ rp)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= k) return;
+   double r = 0.0;
+   for (int b = 0; b < nblk; b++) r += part[(size_t)b * k + i];
+   rp[i] -= r;
+}
+
+template <class T>
+int up(T** d, const T* h, size_t count)
+{
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)d, sizeof(T) * std::max<size_t>(1, count)));
+   if (count) NFFT4GP_HIP_CHECK(hipMemcpy(*d, h, sizeof(T) * count, hipMemcpyHostToDevice));
+   return 0;
+}
+
+void fsai_free(FsaiDev* F)
+{
+   if (!F) return;
+   for (void* p : {(void*)F->ia, (void*)F->ja, (void*)F->aa, (void*)F->tia, (void*)F->tja, (void*)F->taa,
+                   (void*)F->work})
+      (void)hipFree(p);
+   delete F;
+}
+
+FsaiDev* fsai_create(int n, const int* ia, const int* ja, const double* aa)
+{
+   if (n <= 0 || !ia || !ja || !aa) return nullptr;
+   const int nnz = ia[n];
+   // L^T as CSR: column c's entries in ascending row order, i.e. Nfft4GPCsrMv('T')'s accumulation order
+   std::vector<int> tia(n + 1, 0), tja(nnz);
+   std::vector<double> taa(nnz);
+   for (int j = 0; j < nnz; j++) tia[ja[j] + 1]++;
+   for (int c = 0; c < n; c++) tia[c + 1] += tia[c];
+   std::vector<int> pos(tia.begin(), tia.end() - 1);
+   for (int i = 0; i < n; i++)
+      for (int j = ia[i]; j < ia[i + 1]; j++) {
+         const int p = pos[ja[j]]++;
+         tja[p] = i;
+         taa[p] = aa[j];
+      }
+   FsaiDev* F = new FsaiDev();
+   F->n = n;
+   if (up(&F->ia, ia, (size_t)n + 1) || up(&F->ja, ja, (size_t)nnz) || up(&F->aa, aa, (size_t)nnz) ||
+       up(&F->tia, tia.data(), (size_t)n + 1) || up(&F->tja, tja.data(), (size_t)nnz) ||
+       up(&F->taa, taa.data(), (size_t)nnz) || hipMalloc((void**)&F->work, sizeof(double) * n) != hipSuccess) {
+      fsai_free(F);
+      return nullptr;
+   }
+   return F;
+}
+
+int fsai_apply_dev(FsaiDev* F, double* dx, const double* drhs, hipStream_t s)
+{
+   const int g = (F->n + 255) / 256;
+   hipLaunchKernelGGL(k_csr_rows, dim3(g), dim3(256), 0, s, F->ia, F->ja, F->aa, drhs, F->work, F->n);
+   hipLaunchKernelGGL(k_csr_rows, dim3(g), dim3(256), 0, s, F->tia, F->tja, F->taa, F->work, dx, F->n);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+// host or device vectors, like the library's other applies
+int with_device_vectors(int n, double* x, double* rhs, int (*fn)(void*, double*, const double*, hipStream_t),
+                        void* obj)
+{
+   hipStream_t s = current_stream();
+   const bool dx = is_device_ptr(x), dr = is_device_ptr(rhs);
+   double *xd = x, *rd = rhs;
+   if (!dx) NFFT4GP_HIP_CHECK(hipMalloc((void**)&xd, sizeof(double) * std::max(1, n)));
+   if (!dr) {
+      NFFT4GP_HIP_CHECK(hipMalloc((void**)&rd, sizeof(double) * std::max(1, n)));
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(rd, rhs, sizeof(double) * n, hipMemcpyHostToDevice, s));
+   }
+   int rc = fn(obj, xd, rd, s);
+   if (!dx) {
+      if (!rc) NFFT4GP_HIP_CHECK(hipMemcpyAsync(x, xd, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+      NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
+      (void)hipFree(xd);
+   }
+   if (!dr) {
+      NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
+      (void)hipFree(rd);
+   }
+   return rc;
+}
+
+int fsai_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
+{
+   return fsai_apply_dev((FsaiDev*)obj, dx, drhs, s);
+}
+
+int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
+{
+   AfnDev* A = (AfnDev*)obj;
+   const int n = A->n, k = A->k, n2 = A->n2;
+   const int g = (n + 255) / 256, gk = (k + 255) / 256;
+   double* rp2 = A->rp + k;
+   double* y2 = A->y + k;
+   if (k == 0) return fsai_apply_dev(A->S, dx, drhs, s);  // afn.c:106-110
+   if (n2 == 0) {                                          // afn.c:101-105: A11 solve on the unpermuted rhs
+      hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, drhs, A->t, 0);
+      hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, dx, 1);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   }
+   hipLaunchKernelGGL(k_gather, dim3(g), dim3(256), 0, s, drhs, A->perm, n, A->rp);
+   // y = A11 \ rp = L^{-T} (L^{-1} rp)
+   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->rp, A->t, 0);
+   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y, 1);
+   // rp2 -= A12^T y
+   hipLaunchKernelGGL(k_a12t, dim3((n2 + 3) / 4), dim3(256), 0, s, A->K12, k, n2, A->y, rp2);
+   // y2 = FSAI(rp2)
+   if (fsai_apply_dev(A->S, y2, rp2, s)) return -1;
+   // rp -= A12 y2
+   hipLaunchKernelGGL(k_a12_part, dim3(A->nblk), dim3(256), 0, s, A->K12, k, n2, y2, A->part);
+   hipLaunchKernelGGL(k_a12_reduce, dim3(gk), dim3(256), 0, s, A->part, A->nblk, k, A->rp);
+   // y = A11 \ rp
+   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->rp, A->t, 0);
+   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y, 1);
+   hipLaunchKernelGGL(k_scatter, dim3(g), dim3(256), 0, s, A->y, A->perm, n, dx);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+}  // namespace
+
+}  // namespace nfft4gp_amd
+
+using namespace nfft4gp_amd;
+
+extern "C" {
+
+void* Nfft4GPAmdFsaiCreate(int n, const int* ia, const int* ja, const double* aa)
+{
+   if (!device_ok()) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdFsaiCreate: no HIP device visible (no CPU fallback).\n");
+      return nullptr;
+   }
+   return fsai_create(n, ia, ja, aa);
+}
+
+int Nfft4GPAmdFsaiSolve(void* fsai, int n, double* x, double* rhs)
+{
+   FsaiDev* F = (FsaiDev*)fsai;
+   if (!F || n != F->n) return -1;
+   return with_device_vectors(n, x, rhs, &fsai_apply_obj, F);
+}
+
+void Nfft4GPAmdFsaiFree(void* fsai) { fsai_free((FsaiDev*)fsai); }
+
+void* Nfft4GPAmdAfnCreate(int n, int k, const int* perm, const double* L11, const double* K12, void* fsai_schur)
+{
+   if (!device_ok()) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnCreate: no HIP device visible (no CPU fallback).\n");
+      return nullptr;
+   }
+   FsaiDev* S = (FsaiDev*)fsai_schur;
+   const bool ok = n > 0 && k >= 0 && k <= n && (k == 0 || L11) && (k == n || (S && S->n == n - k)) &&
+                   (k == 0 || k == n || (perm && K12));
+   if (!ok) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnCreate: needs 0 <= k <= n, L11 (k > 0), an FSAI of size n - k "
+                      "(k < n), perm and K12 (0 < k < n)\n");
+      return nullptr;
+   }
+   // L11^{-1} on the host (k x k lower triangular inverse)
+   std::vector<double> L(L11, L11 + (size_t)k * k), G((size_t)k * k, 0.0);
+   for (int j = 0; j < k; j++) {
+      G[j + (size_t)j * k] = 1.0 / L[j + (size_t)j * k];
+      for (int i = j + 1; i < k; i++) {
+         double v = 0.0;
+         for (int m = j; m < i; m++) v += L[i + (size_t)m * k] * G[m + (size_t)j * k];
+         G[i + (size_t)j * k] = -v / L[i + (size_t)i * k];
+      }
+   }
+   AfnDev* A = new AfnDev();
+   A->n = n;
+   A->k = k;
+   A->n2 = n - k;
+   A->S = S;
+   A->nblk = (A->n2 + kA12Cols - 1) / kA12Cols;
+   const bool mid = k > 0 && k < n;
+   if ((mid && up(&A->perm, perm, (size_t)n)) || up(&A->Linv, G.data(), G.size()) ||
+       (mid && up(&A->K12, K12, (size_t)k * A->n2)) || hipMalloc((void**)&A->rp, sizeof(double) * n) != hipSuccess ||
+       hipMalloc((void**)&A->y, sizeof(double) * n) != hipSuccess ||
+       hipMalloc((void**)&A->t, sizeof(double) * std::max(1, k)) != hipSuccess ||
+       hipMalloc((void**)&A->part, sizeof(double) * std::max<size_t>(1, (size_t)A->nblk * k)) != hipSuccess) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnCreate: allocation failed\n");
+      Nfft4GPAmdAfnFree(A);
+      return nullptr;
+   }
+   return A;
+}
+
+int Nfft4GPAmdAfnSolve(void* afn, int n, double* x, double* rhs)
+{
+   AfnDev* A = (AfnDev*)afn;
+   if (!A || n != A->n) return -1;
+   return with_device_vectors(n, x, rhs, &afn_apply_obj, A);
+}
+
+void Nfft4GPAmdAfnFree(void* afn)
+{
+   AfnDev* A = (AfnDev*)afn;
+   if (!A) return;
+   for (void* p : {(void*)A->perm, (void*)A->Linv, (void*)A->K12, (void*)A->rp, (void*)A->y, (void*)A->t,
+                   (void*)A->part})
+      (void)hipFree(p);
+   delete A;  // the Schur complement's FSAI handle stays with its creator (Nfft4GPAmdFsaiFree)
+}
+
+}  // extern "C"

@@ -844,7 +844,8 @@ namespace {
 bool library_operator(const void* fn)
 {
    return fn == (const void*)&Nfft4GPAdditiveNFFTMatSymv || fn == (const void*)&Nfft4GPNFFTMatSymv ||
-          fn == (const void*)&Nfft4GPAmdNysSolve;
+          fn == (const void*)&Nfft4GPAmdNysSolve || fn == (const void*)&Nfft4GPAmdFsaiSolve ||
+          fn == (const void*)&Nfft4GPAmdAfnSolve;
 }
 }  // namespace
 

@@ -5,6 +5,8 @@
                 Python in the iteration loop).
 ``NystromPrecond``  Nfft4GPAmdNys* -- the apply of SRC/preconds/nys.c:115-173 on factors U, s, eta,
                 perm produced by the reference's Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660).
+``FsaiPrecond`` Nfft4GPAmdFsai* -- the apply of SRC/preconds/fsai.c:106-123 on the reference's CSR factor.
+``AfnPrecond``  Nfft4GPAmdAfn* -- the apply of SRC/preconds/afn.c:82-143.
 """
 from __future__ import annotations
 
@@ -84,10 +86,83 @@ class NystromPrecond:
             pass
 
 
+class _Apply:
+    """Common part of the HBM-resident preconditioner handles (func_solve + free)."""
+
+    _solve = _free = ""
+
+    def solve(self, x, rhs):
+        rc = getattr(_lib.lib(), self._solve)(self.h, self.n, _ptr(x)[0], _ptr(rhs)[0])
+        if rc:
+            raise RuntimeError(f"{self._solve} failed")
+        return x
+
+    @property
+    def solve_fnptr(self) -> int:
+        return _lib.fnptr(self._solve)
+
+    def free(self):
+        if getattr(self, "h", None):
+            getattr(_lib.lib(), self._free)(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class FsaiPrecond(_Apply):
+    """M^{-1} = L^T L of the reference's FSAI preconditioner (fsai.c:106-123) held in HBM.
+
+    ``L_i, L_j, L_a`` are precond_fsai's CSR arrays (fsai.h:22-39) as produced by
+    Nfft4GPPrecondFsaiSetupWithKernel (fsai.c:302-...)."""
+
+    _solve, _free = "Nfft4GPAmdFsaiSolve", "Nfft4GPAmdFsaiFree"
+
+    def __init__(self, L_i, L_j, L_a):
+        ia = np.ascontiguousarray(np.asarray(L_i, dtype=np.int32))
+        ja = np.ascontiguousarray(np.asarray(L_j, dtype=np.int32))
+        aa = np.ascontiguousarray(np.asarray(L_a, dtype=np.float64))
+        n = ia.size - 1
+        if n <= 0 or ja.size < ia[-1] or aa.size < ia[-1]:
+            raise ValueError("L_i must have n+1 entries and L_j, L_a at least L_i[n]")
+        if ia[-1] and (ja[: ia[-1]].min() < 0 or ja[: ia[-1]].max() >= n):
+            raise ValueError("L_j has column indices outside [0, n)")
+        self.n = n
+        self.h = _lib.lib().Nfft4GPAmdFsaiCreate(n, ia.ctypes.data, ja.ctypes.data, aa.ctypes.data)
+        if not self.h:
+            raise RuntimeError("Nfft4GPAmdFsaiCreate failed (see stderr)")
+
+
+class AfnPrecond(_Apply):
+    """The reference's AFN apply (afn.c:82-143) held in HBM: perm (n), L11 the lower Cholesky factor of
+    A11 = K(perm[:k], perm[:k]) (k x k), K12 = K(perm[:k], perm[k:]) (k x (n-k)) and ``schur`` an
+    FsaiPrecond of size n-k (kept alive by this object)."""
+
+    _solve, _free = "Nfft4GPAmdAfnSolve", "Nfft4GPAmdAfnFree"
+
+    def __init__(self, perm, L11, K12, schur: FsaiPrecond | None):
+        L11 = np.asfortranarray(np.asarray(L11, dtype=np.float64))
+        k = L11.shape[0]
+        p = np.ascontiguousarray(np.asarray(perm, dtype=np.int32))
+        n = p.size
+        K12 = np.asfortranarray(np.asarray(K12, dtype=np.float64).reshape(k, n - k))
+        if schur is not None and schur.n != n - k:
+            raise ValueError("schur must be an FsaiPrecond of size n - k")
+        self.n, self.k, self.schur = n, k, schur
+        self.h = _lib.lib().Nfft4GPAmdAfnCreate(n, k, p.ctypes.data, L11.ctypes.data, K12.ctypes.data,
+                                                schur.h if schur is not None else None)
+        if not self.h:
+            raise RuntimeError("Nfft4GPAmdAfnCreate failed (see stderr)")
+
+
 def pcg(op, b, x=None, maxits=1000, tol=1e-6, atol=False, precond=None, print_level=0):
     """Nfft4GPSolverPcg(op, n, matvec, precond, precondfunc, x, b, maxits, atol, tol, ...).
 
-    ``op`` is an NFFTAdditiveKernel (its C matvec is used) and ``precond`` a NystromPrecond or None.
+    ``op`` is an NFFTAdditiveKernel (its C matvec is used) and ``precond`` a NystromPrecond, FsaiPrecond,
+    AfnPrecond or None.
     ``b``/``x`` are numpy arrays or torch GPU tensors.  Returns (x, rel_res, rel_res_v, iters) with the
     reference's reporting semantics (iters = 0 when not converged, pcg.c:19,197).
     """

@@ -22,7 +22,8 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
-from oracle import OracleAdditiveNFFT, RefDenseAdditive, RefNystrom, ref_available, ref_pcg  # noqa: E402
+from oracle import (OracleAdditiveNFFT, RefDenseAdditive, RefFsai, RefNystrom, afn_apply,  # noqa: E402
+                    ref_available, ref_gaussian_matrix, ref_gaussian_params, ref_pcg, ref_schur_params)
 from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.data import (  # noqa: E402
     read_features, read_labels, read_windows)
 
@@ -52,9 +53,65 @@ def save(name, **arrays):
     print(f"wrote {path} ({os.path.getsize(path)} bytes)")
 
 
+def make_precond_synth():
+    """(5) the reference's FSAI (fsai.c:302-..., KNN pattern, lfil 20) on its dense Gaussian kernel
+    (kernels.c:680) over seeded 3-D points, its apply (fsai.c:106) and PCG with it; the AFN apply
+    (afn.c:82-143, restated in oracle.afn_apply) with the pieces the reference's kernel-FSAI AFN setup
+    builds (afn.c:430-473): Cholesky of K11 = K(perm[:k], perm[:k]) + noise, K12 = K(perm[:k], perm[k:]),
+    the FSAI of the Schur complement through Nfft4GPKernelSchurCombineKernel (kernels.c:3496-3760), and
+    PCG with it."""
+    rng = np.random.default_rng(21)
+    n, d, f, l, mu, lfil = 2000, 3, 1.1, 0.25, 0.01, 20
+    X = np.asfortranarray(rng.random((n, d)))
+    P = ref_gaussian_params(f, l, mu, n)
+    K = ref_gaussian_matrix(P, X)
+    b = rng.random(n) - 0.5
+
+    def mv(alpha, xv, beta, yv):
+        yv[:] = alpha * (K @ xv) + (beta * yv if beta != 0.0 else 0.0)
+
+    fs = RefFsai(X, P, lfil)
+    fs_i, fs_j, fs_a = fs.csr()
+    fs_rhs = rng.random(n) - 0.5
+    fs_out = fs.solve(fs_rhs)
+
+    def pc_fsai(xo, rhs):
+        xo[:] = fs.solve(rhs.copy())
+
+    xf, relf, histf, itf = ref_pcg(mv, n, b, maxits=1000, tol=1e-6, precond_py=pc_fsai)
+
+    k = 100
+    perm = rng.permutation(n).astype(np.int32)
+    K11 = ref_gaussian_matrix(P, X, perm[:k])
+    K11 = np.tril(K11) + np.tril(K11, -1).T
+    L11 = np.linalg.cholesky(K11)
+    K12 = ref_gaussian_matrix(P, X, perm[:k], perm[k:])  # not stored: f^2 exp(-|xi - xj|^2 / 2 l^2)
+    SP, _keep = ref_schur_params(X, perm, k, L11, P)
+    X2 = np.asfortranarray(X[perm[k:]])
+    sf = RefFsai(X2, SP, lfil, kernel="Nfft4GPKernelSchurCombineKernel")
+    s_i, s_j, s_a = sf.csr()
+    afn_rhs = rng.random(n) - 0.5
+    afn_out = afn_apply(perm, L11, K12, sf.solve, afn_rhs)
+
+    def pc_afn(xo, rhs):
+        xo[:] = afn_apply(perm, L11, K12, sf.solve, rhs.copy())
+
+    xa, rela, hista, ita = ref_pcg(mv, n, b, maxits=1000, tol=1e-6, precond_py=pc_afn)
+    assert itf > 0 and ita > 0
+    print(f"precond_synth: PCG iterations fsai {itf}, afn {ita}")
+    save("precond_synth", X=X, f=f, l=l, mu=mu, lfil=lfil, b=b,
+         fsai_i=fs_i, fsai_j=fs_j, fsai_a=fs_a, fsai_rhs=fs_rhs, fsai_out=fs_out,
+         pcgfsai_x=xf, pcgfsai_relres=relf, pcgfsai_hist=histf, pcgfsai_iters=itf,
+         afn_k=k, afn_perm=perm, afn_L11=L11, schur_i=s_i, schur_j=s_j, schur_a=s_a,
+         afn_rhs=afn_rhs, afn_out=afn_out,
+         pcgafn_x=xa, pcgafn_relres=rela, pcgafn_hist=hista, pcgafn_iters=ita)
+
+
 def main():
     if not ref_available():
         raise SystemExit("build oracle/_ref first: make -C oracle ref")
+    if sys.argv[1:] == ["precond"]:
+        return make_precond_synth()
     f, mu = 1.3, 0.01
 
     # (1) TEST2's 1-D dataset, one window {0} (TESTS/TEST2/data/foo.window)
@@ -121,6 +178,8 @@ def main():
          pcg_x=xp, pcg_relres=relres, pcg_hist=hist, pcg_iters=its,
          nys_k=k, nys_perm=perm, nys_U=U, nys_s=s, nys_eta=eta, nys_rhs=nys_rhs, nys_out=nys_out,
          pcgnys_x=xq, pcgnys_relres=relq, pcgnys_hist=histq, pcgnys_iters=itq)
+
+    make_precond_synth()
 
 
 if __name__ == "__main__":

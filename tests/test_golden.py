@@ -8,7 +8,7 @@ import pytest
 
 import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
 from emulate import EmulatedPlan
-from oracle import OracleAdditiveNFFT, RefDenseAdditive, ref_available
+from oracle import OracleAdditiveNFFT, RefDenseAdditive, afn_apply, fsai_apply, gaussian_block, ref_available
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -113,6 +113,51 @@ def test_pcg_fixture_is_consistent():
     b = z["b"]
     assert np.linalg.norm(b - K @ z["pcg_x"]) / np.linalg.norm(b) < 1e-6
     assert np.linalg.norm(b - K @ z["pcgnys_x"]) / np.linalg.norm(b) < 1e-6
+
+
+def _afn_pieces(z):
+    X, f, l = np.asarray(z["X"]), float(z["f"]), float(z["l"])
+    k, perm = int(z["afn_k"]), np.asarray(z["afn_perm"])
+    return perm, np.asarray(z["afn_L11"]), gaussian_block(X, f, l, perm[:k], perm[k:])
+
+
+def test_fsai_afn_restatements_reproduce_golden():
+    """oracle.fsai_apply (fsai.c:106-123) and oracle.afn_apply (afn.c:82-143) against the reference's
+    own FSAI apply and the AFN fixture (precond_synth.npz)."""
+    z = load("precond_synth")
+    ia, ja, aa = (np.asarray(z[k]) for k in ("fsai_i", "fsai_j", "fsai_a"))
+    n = ia.size - 1
+    # the reference's factor: lower triangular, diagonal last in every row, positive diagonal
+    last = ia[1:] - 1
+    assert np.array_equal(ja[last], np.arange(n)) and np.all(aa[last] > 0)
+    assert np.all(ja[: ia[-1]] <= np.repeat(np.arange(n), np.diff(ia)))
+    assert rel(fsai_apply(ia, ja, aa, np.asarray(z["fsai_rhs"])), z["fsai_out"]) < 1e-14
+    si, sj, sa = (np.asarray(z[k]) for k in ("schur_i", "schur_j", "schur_a"))
+    perm, L11, K12 = _afn_pieces(z)
+    out = afn_apply(perm, L11, K12, lambda r: fsai_apply(si, sj, sa, r), np.asarray(z["afn_rhs"]))
+    assert rel(out, z["afn_out"]) < 1e-12
+    # AFN is the stronger preconditioner on this problem, both converge
+    assert 0 < int(z["pcgafn_iters"]) < int(z["pcgfsai_iters"])
+
+
+@pytest.mark.skipif(not ref_available(), reason="oracle/_ref not built")
+def test_compiled_reference_reproduces_fsai_fixture():
+    """Re-run the reference's FSAI setups (fsai.c:302-..., plain Gaussian kernel and the Schur
+    complement kernel kernels.c:3496-3760) from the fixture's inputs."""
+    import oracle as O
+    z = load("precond_synth")
+    X, f, l, mu, lfil = np.asarray(z["X"]), float(z["f"]), float(z["l"]), float(z["mu"]), int(z["lfil"])
+    P = O.ref_gaussian_params(f, l, mu, X.shape[0])
+    ia, ja, aa = O.RefFsai(X, P, lfil).csr()
+    assert np.array_equal(ia, z["fsai_i"]) and np.array_equal(ja, z["fsai_j"])
+    np.testing.assert_allclose(aa, z["fsai_a"], rtol=1e-12, atol=0)
+    perm, L11, K12 = _afn_pieces(z)
+    k = int(z["afn_k"])
+    np.testing.assert_allclose(O.ref_gaussian_matrix(P, X, perm[:k], perm[k:]), K12, rtol=1e-13, atol=1e-15)
+    SP, _keep = O.ref_schur_params(X, perm, k, L11, P)
+    si, sj, sa = O.RefFsai(np.asfortranarray(X[perm[k:]]), SP, lfil, kernel="Nfft4GPKernelSchurCombineKernel").csr()
+    assert np.array_equal(si, z["schur_i"]) and np.array_equal(sj, z["schur_j"])
+    np.testing.assert_allclose(sa, z["schur_a"], rtol=1e-10, atol=0)
 
 
 def test_data_readers(tmp_path):

@@ -139,3 +139,116 @@ def test_pcg_host_vectors_with_reference_operator(torch_cuda):
     x, rr, hist, it = amd.pcg(op, np.asarray(z["b"]).copy(), x, maxits=1000, tol=1e-6)
     assert it > 0 and abs(it - int(z["pcg_iters"])) <= max(2, int(z["pcg_iters"]) // 20)
     assert rel(x, z["pcg_x"]) < 1e-5
+
+
+# ---- FSAI (fsai.c:106-123) and AFN (afn.c:82-143) applies ----------------------------------------
+class DenseGaussHostOp(DenseHostOp):
+    """func_symmatvec on host vectors for the precond_synth fixture: the reference's dense Gaussian
+    kernel f^2 (exp(-|xi - xj|^2 / 2 l^2) + mu I) (kernels.c:680-1289) over its 3-D points."""
+
+    def __init__(self, z):
+        from oracle import gaussian_block
+        X, f, l, mu = np.asarray(z["X"]), float(z["f"]), float(z["l"]), float(z["mu"])
+        n = X.shape[0]
+        idx = np.arange(n)
+        self.K = gaussian_block(X, f, l, idx, idx) + f * f * mu * np.eye(n)
+        self.n = n
+        self.h = None
+
+        def mv(_m, nn, alpha, xp, beta, yp):
+            xv = np.ctypeslib.as_array(C.cast(xp, _lib.dp), shape=(nn,))
+            yv = np.ctypeslib.as_array(C.cast(yp, _lib.dp), shape=(nn,))
+            yv[:] = alpha * (self.K @ xv) + (beta * yv if beta != 0.0 else 0.0)
+            return 0
+
+        self._cb = _lib.SYMMATVEC(mv)
+        self.matvec_fnptr = C.cast(self._cb, C.c_void_p).value
+
+
+def _fsai(z, pre="fsai"):
+    return amd.FsaiPrecond(z[pre + "_i"], z[pre + "_j"], z[pre + "_a"])
+
+
+def _afn(z):
+    from oracle import gaussian_block
+    X, f, l = np.asarray(z["X"]), float(z["f"]), float(z["l"])
+    k, perm = int(z["afn_k"]), np.asarray(z["afn_perm"])
+    S = _fsai(z, "schur")
+    return amd.AfnPrecond(perm, z["afn_L11"], gaussian_block(X, f, l, perm[:k], perm[k:]), S)
+
+
+def test_fsai_apply_is_bitwise_reference(torch_cuda):
+    """Each CSR row is summed in Nfft4GPCsrMv's order with unfused multiply and add (matops.c:231-262):
+    the result equals the reference's Nfft4GPPrecondFsaiSolve bit for bit, device and host vectors."""
+    torch = torch_cuda
+    z = load("precond_synth")
+    pre = _fsai(z)
+    r = np.asarray(z["fsai_rhs"])
+    xd = torch.zeros(r.size, dtype=torch.float64, device="cuda")
+    pre.solve(xd, torch.tensor(r, device="cuda"))
+    np.testing.assert_array_equal(xd.cpu().numpy(), z["fsai_out"])
+    xh = np.zeros(r.size)
+    pre.solve(xh, r.copy())
+    np.testing.assert_array_equal(xh, z["fsai_out"])
+
+
+def test_afn_apply_matches_golden(torch_cuda):
+    torch = torch_cuda
+    z = load("precond_synth")
+    pre = _afn(z)
+    r = np.asarray(z["afn_rhs"])
+    xd = torch.zeros(r.size, dtype=torch.float64, device="cuda")
+    pre.solve(xd, torch.tensor(r, device="cuda"))
+    assert rel(xd.cpu().numpy(), z["afn_out"]) <= 1e-12
+    xh = np.zeros(r.size)
+    pre.solve(xh, r.copy())
+    assert rel(xh, z["afn_out"]) <= 1e-12
+
+
+@pytest.mark.parametrize("k", [0, "n"])
+def test_afn_apply_edge_ranks(torch_cuda, k):
+    """afn.c:101-110: k = n solves with A11 on the UNPERMUTED rhs, k = 0 is the Schur FSAI alone."""
+    import scipy.linalg as sl
+    from oracle import afn_apply, fsai_apply, gaussian_block
+    torch = torch_cuda
+    rng = np.random.default_rng(5)
+    n = 300
+    X = rng.random((n, 2))
+    perm = rng.permutation(n).astype(np.int32)
+    r = rng.random(n) - 0.5
+    if k == 0:
+        z = load("precond_synth")
+        ia, ja, aa = (np.asarray(z[c]) for c in ("fsai_i", "fsai_j", "fsai_a"))
+        n = ia.size - 1
+        r = rng.random(n) - 0.5
+        S = amd.FsaiPrecond(ia, ja, aa)
+        pre = amd.AfnPrecond(np.arange(n), np.zeros((0, 0)), np.zeros((0, n)), S)
+        ref = afn_apply(np.arange(n), np.zeros((0, 0)), None, lambda v: fsai_apply(ia, ja, aa, v), r)
+    else:
+        A = gaussian_block(X, 1.0, 0.3, perm, perm) + 0.05 * np.eye(n)
+        L = sl.cholesky(A, lower=True)
+        pre = amd.AfnPrecond(perm, L, np.zeros((n, 0)), None)
+        ref = afn_apply(perm, L, None, None, r)
+    xd = torch.zeros(n, dtype=torch.float64, device="cuda")
+    pre.solve(xd, torch.tensor(r, device="cuda"))
+    assert rel(xd.cpu().numpy(), ref) <= 1e-11
+
+
+@pytest.mark.parametrize("kind", ["fsai", "afn"])
+def test_pcg_with_fsai_afn_matches_golden(torch_cuda, kind):
+    """This library's PCG (device vectors, the preconditioner called with device pointers) against the
+    reference's pcg.c with the reference's FSAI / the restated AFN on the same dense operator."""
+    torch = torch_cuda
+    z = load("precond_synth")
+    op = DenseGaussHostOp(z)
+    pre = _fsai(z) if kind == "fsai" else _afn(z)
+    key = "pcg" + kind
+    b = torch.tensor(np.asarray(z["b"]), device="cuda")
+    x = torch.zeros(op.n, dtype=torch.float64, device="cuda")
+    x, rr, hist, it = amd.pcg(op, b, x, maxits=1000, tol=1e-6, precond=pre)
+    it_ref = int(z[key + "_iters"])
+    assert it > 0 and abs(it - it_ref) <= max(2, it_ref // 20), (it, it_ref)
+    assert rr <= 1e-6
+    assert rel(x.cpu().numpy(), z[key + "_x"]) < 1e-5
+    k = min(10, it, it_ref)
+    np.testing.assert_allclose(hist[:k], np.asarray(z[key + "_hist"])[:k], rtol=1e-6)
