@@ -224,7 +224,7 @@ int Nfft4GPAmdKernelBench(void *str, int which, int grad, int reps, const NFFT4G
 
 /* split-phase additive matvec for row-sharded multi-GPU use (one process per GPU):
  *   phase 1 (spread): per-component oversampled-grid partial sums of this rank's points into grid
- *                     (device, nwindows*64 doubles, overwritten);
+ *                     (device, Nfft4GPAmdShardGridSize doubles, overwritten);
  *   -- caller all-reduces grid across ranks (RCCL) --
  *   phase 2 (finish): circulant + interpolation + epilogue for this rank's points.
  * The handle must have been created with Nfft4GPAmdAdditiveShardCreate.  x, y are device pointers to
@@ -234,6 +234,9 @@ void *Nfft4GPAmdAdditiveShardCreate(NFFT4GP_DOUBLE *data, int n_global, int ldim
 int Nfft4GPAmdShardSpread(void *str, const NFFT4GP_DOUBLE *x_local, NFFT4GP_DOUBLE *grid);
 int Nfft4GPAmdShardFinish(void *str, const NFFT4GP_DOUBLE *grid, int grad, NFFT4GP_DOUBLE alpha,
                           const NFFT4GP_DOUBLE *x_local, NFFT4GP_DOUBLE beta, NFFT4GP_DOUBLE *y_local);
+/* elements of the grid Nfft4GPAmdShardSpread writes and Nfft4GPAmdShardFinish reads: nwindows * 64 when
+ * every window is 1-D, nwindows * 64^dmax otherwise (the real spread grids of multi-feature windows) */
+long long Nfft4GPAmdShardGridSize(void *str);
 
 /* ---- host-only helpers (no GPU needed): the setup math of the device plan, exported so the CPU
  * test-suite can check it and emulate the kernels against the oracle ------------------------------- */

@@ -99,6 +99,7 @@ _SIGS = {
     "Nfft4GPAmdAdditiveShardCreate": (vp, [vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int]),
     "Nfft4GPAmdShardSpread": (C.c_int, [vp, vp, vp]),
     "Nfft4GPAmdShardFinish": (C.c_int, [vp, vp, C.c_int, C.c_double, vp, C.c_double, vp]),
+    "Nfft4GPAmdShardGridSize": (C.c_longlong, [vp]),
     "Nfft4GPAmdHostTapPoly": (C.c_int, [vp]),
     "Nfft4GPAmdHostCirculant": (C.c_int, [C.c_int, C.c_double, C.c_double, vp, vp]),
     "Nfft4GPAmdHostPrepare": (C.c_double, [vp, C.c_int, vp]),

@@ -92,6 +92,34 @@ struct DevLayout {
    size_t bytes = 0;
 };
 
+// multi-dimensional windows (nfft_md.hip): per-component 64^d grids, dims <= kMdMaxDim
+constexpr int kMdMaxDim = 3;
+struct MdComp {
+   int d = 0;
+   int hicount = 1;          // kTaps^(d-1): tap rows per point
+   long long u_off = 0;      // this component's first entry in u ([point][d]); psi starts at u_off * kTaps
+};
+struct MdPlan {
+   bool on = false;
+   int maxd = 1;
+   long long G = 0;          // 64^maxd: real grid stride per component
+   long long Cmax = 0;       // 32 * 64^(maxd-1): complex pass buffer stride per component
+   long long M = 0;          // 32^maxd: mode stride per component
+   std::vector<MdComp> comps;
+   MdComp* d_comps = nullptr;
+   int* d_u = nullptr;       // [comp][point][d]  floor(64 x) - m
+   double* d_psi = nullptr;  // [comp][point][d][kTaps]  PHI taps (PRE_PSI)
+   double* d_grid = nullptr; // [nw][G] spread grid
+   double2* d_F[2] = {nullptr, nullptr};  // forward ping-pong [nw][Cmax]
+   double2* d_Mo[2] = {nullptr, nullptr}; // modes x bhat (chain 0: K, chain 1: K') [nw][M]
+   double2* d_B[4] = {nullptr, nullptr, nullptr, nullptr};  // backward ping-pong, 2 per chain
+   double* d_h[2] = {nullptr, nullptr};   // interpolation grids [nw][G]
+   double* d_bh = nullptr;   // [nw][M]  weight * bhat * prod 1/phihut (second deconvolution)
+   double* d_bhd = nullptr;  // [nw][M]  the same for the derivative kernel, times dscale
+   double* d_dot_part = nullptr;
+   unsigned int* d_dot_ticket = nullptr;
+};
+
 struct AdditivePlan {
    // geometry
    int n_global = 0, row_begin = 0, row_end = 0, n = 0;  // n = local rows
@@ -120,6 +148,7 @@ struct AdditivePlan {
    unsigned int* d_dot_ticket = nullptr; // arrival counters (reduce.hpp)
    double* d_xs = nullptr;    // staging (host pointer calls)
    double* d_ys = nullptr;    // staging 3n
+   MdPlan md;  // used instead of the 1-D layout when any window has more than one feature
    // timing
    bool timing = false;
    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -160,6 +189,17 @@ int sym_eig_host(const std::vector<double>& A, int n, std::vector<double>& w, st
 int chol_inverse_host(std::vector<double>& A, int k);
 NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int skip_last, int kernel, double f,
                            double l, double mu, const int* perm, int k, int k11_mode);
+
+// multi-dimensional windows (nfft_md.hip).  xs[c] = component c's centred, scaled coordinates
+// (n_global x d column-major); the plan keeps rows [row_begin, row_end).
+int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs);
+int md_setup(AdditivePlan& P);  // kernel coefficients for P.kernel, P.comp_sigma, P.comp_scale
+int md_spread(const AdditivePlan& P, const double* d_x, double* d_grid, hipStream_t s);
+int md_grid(const AdditivePlan& P, const double* d_grid, int grad, hipStream_t s);
+int md_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, double beta, double* d_y,
+              hipStream_t s, double* d_dot = nullptr);
+void md_free(AdditivePlan& P);
+void bhat_nd(int kind, int d, double c, std::vector<double>& bhat);  // window.cpp, 32^d real
 
 hipStream_t current_stream();
 bool is_device_ptr(const void* p);

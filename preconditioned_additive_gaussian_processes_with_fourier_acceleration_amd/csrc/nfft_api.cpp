@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -103,6 +104,7 @@ void free_plan(PlanExt* E)
    if (!E) return;
    AdditivePlan& P = E->P;
    free_layout(P);
+   md_free(P);
    dfree(P.d_w);
    dfree(P.d_wd);
    dfree(P.d_H);
@@ -173,14 +175,23 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
    std::vector<uint32_t> qc((size_t)P.nw * P.n);
    P.comp_scale.assign(P.nw, 1.0);
    std::vector<double> xs;
-   for (int c = 0; c < P.nw; c++) {
-      if (P.comp_dims[c] != 1) {
-         fprintf(stderr,
-                 "nfft4gp_amd: window %d has %d features; the MI355X path implements 1-D additive windows "
-                 "(BASELINE configs B-E). Multi-dimensional windows are not supported yet.\n",
-                 c, P.comp_dims[c]);
-         return -1;
+   if (std::any_of(P.comp_dims.begin(), P.comp_dims.end(), [](int d) { return d != 1; })) {
+      // windows of several features: 64^d grids (nfft_md.hip)
+      std::vector<std::vector<double>> xsc(P.nw);
+      for (int c = 0; c < P.nw; c++) {
+         const double* col = buffer + (size_t)c * ng * P.dw;  // nfft_interface.c:703 stride n*dwindows
+         P.comp_scale[c] = centre_and_scale(col, ng, P.comp_dims[c], xsc[c]);
+         if (P.comp_scale[c] < 0.0) {
+            fprintf(stderr, "nfft4gp_amd: all points of window %d coincide (radius 0); the reference's scaling "
+                            "0.25/radius (nfft_interface.c:190) is undefined there.\n", c);
+            return -1;
+         }
       }
+      if (md_build_points(P, xsc)) return -1;
+      P.points_ready = true;
+      return 0;
+   }
+   for (int c = 0; c < P.nw; c++) {
       const double* col = buffer + (size_t)c * ng * P.dw;  // nfft_interface.c:703 stride n*dwindows
       P.comp_scale[c] = centre_and_scale(col, ng, 1, xs);
       if (P.comp_scale[c] < 0.0) {
@@ -228,6 +239,11 @@ int plan_setup(AdditivePlan& P, const double* buffer, int kernel, double f, doub
    P.l = l;
    P.mu = mu;
    P.comp_sigma.assign(P.nw, 0.0);
+   if (P.md.on) {
+      for (int c = 0; c < P.nw; c++)
+         P.comp_sigma[c] = (kernel == 0) ? l * P.comp_scale[c] * std::sqrt(2.0) : l * P.comp_scale[c];  // :219/:355
+      return md_setup(P);
+   }
    std::vector<double> w((size_t)P.nw * kNos), wd((size_t)P.nw * kNos);
    double bh[kBand], bhd[kBand];
    for (int c = 0; c < P.nw; c++) {
@@ -266,11 +282,12 @@ int plan_apply_dev(PlanExt* E, int grad, double alpha, const double* d_x, double
       rec = get_rec(E);
       (void)hipEventRecord(rec.ev[0], s);
    }
-   if (launch_spread(P, d_x, P.d_part, s)) return -1;
+   if (P.md.on ? md_spread(P, d_x, P.md.d_grid, s) : launch_spread(P, d_x, P.d_part, s)) return -1;
    if (P.timing) (void)hipEventRecord(rec.ev[1], s);
-   if (launch_grid(P, P.d_part, P.nblocks, grad, s)) return -1;
+   if (P.md.on ? md_grid(P, P.md.d_grid, grad, s) : launch_grid(P, P.d_part, P.nblocks, grad, s)) return -1;
    if (P.timing) (void)hipEventRecord(rec.ev[2], s);
-   if (launch_interp(P, grad, alpha, d_x, beta, d_y, s)) return -1;
+   if (P.md.on ? md_interp(P, grad, alpha, d_x, beta, d_y, s) : launch_interp(P, grad, alpha, d_x, beta, d_y, s))
+      return -1;
    if (P.timing) {
       (void)hipEventRecord(rec.ev[3], s);
       E->pending.push_back(rec);
@@ -415,6 +432,10 @@ int additive_matvec_dot(void* str, const double* d_x, double* d_y, double* d_dot
    if (!E || !E->P.points_ready) return -1;
    AdditivePlan& P = E->P;
    hipStream_t s = current_stream();
+   if (P.md.on) {
+      if (md_spread(P, d_x, P.md.d_grid, s) || md_grid(P, P.md.d_grid, 0, s)) return -1;
+      return md_interp(P, 0, 1.0, d_x, 0.0, d_y, s, d_dot);
+   }
    if (launch_spread(P, d_x, P.d_part, s)) return -1;
    if (launch_grid(P, P.d_part, P.nblocks, 0, s)) return -1;
    return launch_interp(P, 0, 1.0, d_x, 0.0, d_y, s, d_dot);
@@ -582,7 +603,11 @@ int Nfft4GPAmdKernelBench(void* str, int which, int grad, int reps, const double
    for (int rep = -1; rep < reps; rep++) {
       if (rep == 0) NFFT4GP_HIP_CHECK(hipEventRecord(e0, s));
       int rc = 0;
-      if (which == 0)
+      if (P.md.on)
+         rc = which == 0 ? md_spread(P, x, P.md.d_grid, s)
+              : which == 1 ? md_grid(P, P.md.d_grid, grad, s)
+                           : md_interp(P, grad, 1.0, x, 0.0, y, s);
+      else if (which == 0)
          rc = launch_spread(P, x, P.d_part, s);
       else if (which == 1)
          rc = launch_grid(P, P.d_part, P.nblocks, grad, s);
@@ -627,6 +652,7 @@ int Nfft4GPAmdShardSpread(void* str, const double* x_local, double* grid)
    if (!E || !E->P.points_ready) return -1;
    AdditivePlan& P = E->P;
    hipStream_t s = current_stream();
+   if (P.md.on) return md_spread(P, x_local, grid, s);
    if (launch_spread(P, x_local, P.d_part, s)) return -1;
    if (P.nblocks == 0) {
       NFFT4GP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * P.nw * kNos, s));
@@ -642,8 +668,20 @@ int Nfft4GPAmdShardFinish(void* str, const double* grid, int grad, double alpha,
    if (!E || !E->P.points_ready) return -1;
    AdditivePlan& P = E->P;
    hipStream_t s = current_stream();
+   if (P.md.on) {
+      if (md_grid(P, grid, grad, s)) return -1;
+      return md_interp(P, grad, alpha, x_local, beta, y_local, s);
+   }
    if (launch_grid_from_sum(P, grid, grad, s)) return -1;
    return launch_interp(P, grad, alpha, x_local, beta, y_local, s);
+}
+
+long long Nfft4GPAmdShardGridSize(void* str)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready) return -1;
+   const AdditivePlan& P = E->P;
+   return P.md.on ? (long long)P.nw * P.md.G : (long long)P.nw * kNos;
 }
 
 /* ------------------------------- host-only helpers -------------------------------------------- */

@@ -1,0 +1,466 @@
+// nfft_md.hip -- the additive operator for windows of 2 or 3 features (TEST1's bike / poletele windows,
+// BASELINE config A), and any handle mixing them with 1-D windows.
+//
+// Same algorithm as the 1-D path (NFFT3 fastsum with N = 32, n_os = 64, m = 4, nfft_interface.c:216-256,
+// :426, :533-534; see window.cpp), on 64^d grids:
+//   spread    g = B^T x         each point adds x_j * prod_t PHI taps to 10^d cells (PRE_PSI taps from the
+//                               first setup, fp64 atomics into the component's grid, which stays in L2)
+//   forward   a = (E x ... x E) g   E = [e^{+2 pi i (k-16) l / 64} / PHI_HUT(k-16)]  (32 x 64), one axis
+//                                   per launch, then a *= weight * bhat_k * prod_t 1/PHI_HUT(k_t - 16)
+//   backward  h = Re (E^* x ... x E^*) a   (the reference keeps Re f, nfft_interface.c:436)
+//   interp    (K x)_j = sum over the point's 10^d cells of h * taps, one wave per point, all components
+//             of the point in the same wave (the per-point sum over windows is in a fixed order)
+// and the 1-D path's epilogue (y = beta y + alpha f^2 (sum + mu x), or the three gradient outputs of
+// nfft_interface.c:547-549).  The grid work per component is 3 x 32 x 64^2 x 64 complex MACs in 3-D
+// (tiny); the spread/interp are 1000 taps per point and component.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "internal.h"
+#include "reduce.hpp"
+
+namespace nfft4gp_amd {
+
+namespace {
+
+__constant__ double2 c_tw[kNos];       // e^{+2 pi i m / 64}
+__constant__ double c_phinv[kBand];    // 1 / PHI_HUT(k - 16)
+
+constexpr int kMdThreads = 256;
+constexpr int kMdInterpBlocks = 2048;  // grid-stride interp (grid_total handles <= kRedMaxBlocks)
+
+__device__ __forceinline__ int ipow_i(int b, int e)
+{
+   int r = 1;
+   for (int i = 0; i < e; i++) r *= b;
+   return r;
+}
+
+// tap row `hi` (digits over axes 1..d-1) of point j: grid row offset and the product of its taps
+__device__ __forceinline__ double tap_row(const int* uj, const double* pj, int d, int hi, long long* base)
+{
+   double w = 1.0;
+   long long b = 0, stride = kNos;
+   int rem = hi;
+   for (int t = 1; t < d; t++) {
+      const int lt = rem % kTaps;
+      rem /= kTaps;
+      b += (long long)((uj[t] + lt) & (kNos - 1)) * stride;
+      stride *= kNos;
+      w *= pj[t * kTaps + lt];
+   }
+   *base = b;
+   return w;
+}
+
+// thread = (point, tap row); the row's 10 cells along axis 0 get fp64 atomic adds
+__global__ __launch_bounds__(kMdThreads) void k_md_spread(const MdComp* __restrict__ comps,
+                                                          const int* __restrict__ u, const double* __restrict__ psi,
+                                                          const double* __restrict__ x, int n, int hi_max,
+                                                          double* __restrict__ grid, long long G)
+{
+   const MdComp cp = comps[blockIdx.y];
+   const long long idx = (long long)blockIdx.x * kMdThreads + threadIdx.x;
+   if (idx >= (long long)n * hi_max) return;
+   const int j = (int)(idx / hi_max), hi = (int)(idx % hi_max);
+   if (hi >= cp.hicount) return;
+   const int* uj = u + cp.u_off + (long long)j * cp.d;
+   const double* pj = psi + (cp.u_off + (long long)j * cp.d) * kTaps;
+   long long base;
+   const double w = x[j] * tap_row(uj, pj, cp.d, hi, &base);
+   double* g = grid + (long long)blockIdx.y * G + base;
+   const int u0 = uj[0];
+#pragma unroll
+   for (int lt = 0; lt < kTaps; lt++) atomicAdd(g + ((u0 + lt) & (kNos - 1)), w * pj[lt]);
+}
+
+// forward pass along axis t: in [32^t][64][64^(d-t-1)] (real grid when t == 0) -> out [32^t][32][...]
+__global__ __launch_bounds__(kMdThreads) void k_md_fwd(const MdComp* __restrict__ comps, int t,
+                                                       const double* __restrict__ grid, long long G,
+                                                       double2* __restrict__ F0, double2* __restrict__ F1,
+                                                       long long Cmax)
+{
+   const int c = blockIdx.y;
+   const int d = comps[c].d;
+   if (t >= d) return;
+   const int lo = ipow_i(kBand, t), hi = ipow_i(kNos, d - t - 1);
+   const int e = blockIdx.x * kMdThreads + threadIdx.x;
+   if (e >= lo * kBand * hi) return;
+   const int lo_i = e % lo, r = e / lo, k = r % kBand, h = r / kBand;
+   double2 acc = {0.0, 0.0};
+   if (t == 0) {
+      const double* in = grid + (long long)c * G;
+      for (int l = 0; l < kNos; l++) {
+         const double v = in[lo_i + (long long)lo * (l + kNos * h)];
+         const double2 w = c_tw[((k - kBand / 2) * l) & (kNos - 1)];
+         acc.x = fma(v, w.x, acc.x);
+         acc.y = fma(v, w.y, acc.y);
+      }
+   } else {
+      const double2* in = ((t - 1) & 1 ? F1 : F0) + (long long)c * Cmax;
+      for (int l = 0; l < kNos; l++) {
+         const double2 v = in[lo_i + (long long)lo * (l + kNos * h)];
+         const double2 w = c_tw[((k - kBand / 2) * l) & (kNos - 1)];
+         acc.x = fma(v.x, w.x, fma(-v.y, w.y, acc.x));
+         acc.y = fma(v.x, w.y, fma(v.y, w.x, acc.y));
+      }
+   }
+   double2* out = (t & 1 ? F1 : F0) + (long long)c * Cmax;
+   const double s = c_phinv[k];
+   out[lo_i + (long long)lo * (k + kBand * h)] = make_double2(acc.x * s, acc.y * s);
+}
+
+// modes: chain 0 = a * bh, chain 1 = a * bhd
+__global__ __launch_bounds__(kMdThreads) void k_md_modes(const MdComp* __restrict__ comps,
+                                                         const double2* __restrict__ F0,
+                                                         const double2* __restrict__ F1, long long Cmax,
+                                                         const double* __restrict__ bh,
+                                                         const double* __restrict__ bhd, long long M, int grad,
+                                                         double2* __restrict__ M0, double2* __restrict__ M1)
+{
+   const int c = blockIdx.y;
+   const int d = comps[c].d;
+   const int e = blockIdx.x * kMdThreads + threadIdx.x;
+   if (e >= ipow_i(kBand, d)) return;
+   const double2 a = (((d - 1) & 1) ? F1 : F0)[(long long)c * Cmax + e];
+   const long long o = (long long)c * M + e;
+   const double b0 = bh[o];
+   M0[o] = make_double2(a.x * b0, a.y * b0);
+   if (grad) {
+      const double b1 = bhd[o];
+      M1[o] = make_double2(a.x * b1, a.y * b1);
+   }
+}
+
+// backward pass along axis t for chain blockIdx.z: in [64^t][32][32^(d-t-1)] -> out [64^t][64][...];
+// the last axis writes the real part only, to the interpolation grid
+__global__ __launch_bounds__(kMdThreads) void k_md_bwd(const MdComp* __restrict__ comps, int t,
+                                                       const double2* __restrict__ M0,
+                                                       const double2* __restrict__ M1, long long M,
+                                                       double2* __restrict__ B0, double2* __restrict__ B1,
+                                                       double2* __restrict__ B2, double2* __restrict__ B3,
+                                                       long long Cmax, double* __restrict__ h0,
+                                                       double* __restrict__ h1, long long G)
+{
+   const int c = blockIdx.y, chain = blockIdx.z;
+   const int d = comps[c].d;
+   if (t >= d) return;
+   const int lo = ipow_i(kNos, t), hi = ipow_i(kBand, d - t - 1);
+   const int e = blockIdx.x * kMdThreads + threadIdx.x;
+   if (e >= lo * kNos * hi) return;
+   const int lo_i = e % lo, r = e / lo, l = r % kNos, h = r / kNos;
+   double2* Ba = chain ? B2 : B0;
+   double2* Bb = chain ? B3 : B1;
+   const double2* in = (t == 0) ? (chain ? M1 : M0) + (long long)c * M : ((t - 1) & 1 ? Bb : Ba) + (long long)c * Cmax;
+   double2 acc = {0.0, 0.0};
+   for (int k = 0; k < kBand; k++) {
+      const double2 v = in[lo_i + (long long)lo * (k + kBand * h)];
+      const double2 w = c_tw[((k - kBand / 2) * l) & (kNos - 1)];  // conjugated below
+      acc.x = fma(v.x, w.x, fma(v.y, w.y, acc.x));
+      acc.y = fma(v.y, w.x, fma(-v.x, w.y, acc.y));
+   }
+   const long long o = lo_i + (long long)lo * (l + kNos * h);
+   if (t == d - 1)
+      (chain ? h1 : h0)[(long long)c * G + o] = acc.x;
+   else
+      ((t & 1) ? Bb : Ba)[(long long)c * Cmax + o] = acc;
+}
+
+// one wave per point (grid-stride), every component of the point in the wave; 1-D path epilogue
+template <int GRAD, int DOT>
+__global__ __launch_bounds__(kMdThreads) void k_md_interp(const MdComp* __restrict__ comps, int nw,
+                                                          const int* __restrict__ u,
+                                                          const double* __restrict__ psi,
+                                                          const double* __restrict__ h0,
+                                                          const double* __restrict__ h1, long long G,
+                                                          const double* __restrict__ x, double* __restrict__ y,
+                                                          int n, double alpha, double beta, double f, double mu,
+                                                          double* __restrict__ dot_part,
+                                                          unsigned int* __restrict__ dot_ticket,
+                                                          double* __restrict__ dot_out)
+{
+   const int lane = threadIdx.x & 63;
+   const int waves = gridDim.x * (kMdThreads / 64);
+   const double ff = f * f;
+   double dacc = 0.0;
+   for (int j = blockIdx.x * (kMdThreads / 64) + (threadIdx.x >> 6); j < n; j += waves) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int c = 0; c < nw; c++) {
+         const MdComp cp = comps[c];
+         const int* uj = u + cp.u_off + (long long)j * cp.d;
+         const double* pj = psi + (cp.u_off + (long long)j * cp.d) * kTaps;
+         const int u0 = uj[0];
+         double a0 = 0.0, a1 = 0.0;
+         for (int hi = lane; hi < cp.hicount; hi += 64) {
+            long long base;
+            const double w = tap_row(uj, pj, cp.d, hi, &base);
+            const double* r0 = h0 + (long long)c * G + base;
+            double v0 = 0.0;
+#pragma unroll
+            for (int lt = 0; lt < kTaps; lt++) v0 = fma(r0[(u0 + lt) & (kNos - 1)], pj[lt], v0);
+            a0 = fma(w, v0, a0);
+            if (GRAD) {
+               const double* r1 = h1 + (long long)c * G + base;
+               double v1 = 0.0;
+#pragma unroll
+               for (int lt = 0; lt < kTaps; lt++) v1 = fma(r1[(u0 + lt) & (kNos - 1)], pj[lt], v1);
+               a1 = fma(w, v1, a1);
+            }
+         }
+         for (int off = 32; off > 0; off >>= 1) {
+            a0 += __shfl_xor(a0, off, 64);
+            if (GRAD) a1 += __shfl_xor(a1, off, 64);
+         }
+         s0 += a0;
+         s1 += a1;
+      }
+      if (lane == 0) {
+         const double xj = x[j];
+         if (!GRAD) {
+            const double v = ff * (s0 + mu * xj);
+            const double yo = (beta == 0.0) ? alpha * v : fma(beta, y[j], alpha * v);
+            y[j] = yo;
+            if (DOT) dacc = fma(yo, xj, dacc);
+         } else {
+            // nfft_interface.c:547-549 summed over windows: (2f)(Kx + mu x), ff*dscale*K'x, ff*x
+            const double v0 = 2.0 * f * (s0 + mu * xj), v1 = ff * s1, v2 = ff * xj;
+            double* y1 = y + n;
+            double* y2 = y + 2 * (size_t)n;
+            if (beta == 0.0) {
+               y[j] = alpha * v0;
+               y1[j] = alpha * v1;
+               y2[j] = alpha * v2;
+            } else {
+               y[j] = fma(beta, y[j], alpha * v0);
+               y1[j] = fma(beta, y1[j], alpha * v1);
+               y2[j] = fma(beta, y2[j], alpha * v2);
+            }
+         }
+      }
+   }
+   if (DOT) {
+      dacc = block_sum0<kMdThreads>(dacc);
+      double tot;
+      if (grid_total<kMdThreads>(dacc, dot_part, dot_ticket, &tot) && threadIdx.x == 0) *dot_out = tot;
+   }
+}
+
+template <class T>
+int dalloc(T** p, size_t count)
+{
+   if (*p) {
+      (void)hipFree(*p);
+      *p = nullptr;
+   }
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)p, sizeof(T) * std::max<size_t>(1, count)));
+   return 0;
+}
+
+template <class T>
+void dfree_md(T*& p)
+{
+   if (p) (void)hipFree(p);
+   p = nullptr;
+}
+
+int upload_md_constants()
+{
+   double2 tw[kNos];
+   for (int m = 0; m < kNos; m++) {
+      const double a = 2.0 * 3.141592653589793238462643383279502884 * (double)m / (double)kNos;
+      tw[m] = make_double2(std::cos(a), std::sin(a));
+   }
+   // exact values where the angle is a multiple of pi/4 (cos/sin of those are not exact in libm)
+   for (int m = 0; m < kNos; m += kNos / 4) {
+      const int q = m / (kNos / 4);
+      tw[m] = make_double2(q == 0 ? 1.0 : q == 2 ? -1.0 : 0.0, q == 1 ? 1.0 : q == 3 ? -1.0 : 0.0);
+   }
+   double ph[kBand];
+   for (int k = 0; k < kBand; k++) ph[k] = 1.0 / kb_phi_hut(k - kBand / 2);
+   NFFT4GP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_tw), tw, sizeof(tw)));
+   NFFT4GP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_phinv), ph, sizeof(ph)));
+   return 0;
+}
+
+}  // namespace
+
+void md_free(AdditivePlan& P)
+{
+   MdPlan& D = P.md;
+   dfree_md(D.d_comps);
+   dfree_md(D.d_u);
+   dfree_md(D.d_psi);
+   dfree_md(D.d_grid);
+   for (auto& p : D.d_F) dfree_md(p);
+   for (auto& p : D.d_Mo) dfree_md(p);
+   for (auto& p : D.d_B) dfree_md(p);
+   for (auto& p : D.d_h) dfree_md(p);
+   dfree_md(D.d_bh);
+   dfree_md(D.d_bhd);
+   dfree_md(D.d_dot_part);
+   dfree_md(D.d_dot_ticket);
+}
+
+// first setup: PRE_PSI taps of the kept rows (nfft_interface.c:150-213 then fastsum's PRE_PSI), buffers
+int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
+{
+   MdPlan& D = P.md;
+   md_free(P);
+   D.on = true;
+   D.maxd = 1;
+   for (int c = 0; c < P.nw; c++) {
+      if (P.comp_dims[c] < 1 || P.comp_dims[c] > kMdMaxDim) {
+         fprintf(stderr, "nfft4gp_amd: window %d has %d features; windows of 1 to %d features are supported.\n", c,
+                 P.comp_dims[c], kMdMaxDim);
+         return -1;
+      }
+      D.maxd = std::max(D.maxd, P.comp_dims[c]);
+   }
+   D.G = 1;
+   D.M = 1;
+   for (int t = 0; t < D.maxd; t++) {
+      D.G *= kNos;
+      D.M *= kBand;
+   }
+   D.Cmax = D.G / 2;  // 32 * 64^(maxd-1)
+   D.comps.assign(P.nw, MdComp());
+   long long off = 0;
+   for (int c = 0; c < P.nw; c++) {
+      MdComp& cp = D.comps[c];
+      cp.d = P.comp_dims[c];
+      cp.hicount = 1;
+      for (int t = 1; t < cp.d; t++) cp.hicount *= kTaps;
+      cp.u_off = off;
+      off += (long long)P.n * cp.d;
+   }
+   const int n = P.n, ng = P.n_global;
+   std::vector<int> u;
+   std::vector<double> psi;
+   for (int c = 0; c < P.nw; c++) {
+      const int d = P.comp_dims[c];
+      for (int j = 0; j < n; j++)
+         for (int t = 0; t < d; t++) {
+            const double xj = xs[c][(size_t)t * ng + P.row_begin + j];
+            const int uj = (int)std::floor(xj * (double)kNos) - kM;
+            u.push_back(uj);
+            for (int lt = 0; lt < kTaps; lt++) {
+               const double tx = xj - (double)(uj + lt) / (double)kNos;
+               psi.push_back(kb_phi(tx * (double)kNos));
+            }
+         }
+   }
+   const size_t nw = (size_t)P.nw;
+   if (dalloc(&D.d_comps, nw) || dalloc(&D.d_u, u.size()) || dalloc(&D.d_psi, psi.size()) ||
+       dalloc(&D.d_grid, nw * D.G) || dalloc(&D.d_F[0], nw * D.Cmax) || dalloc(&D.d_F[1], nw * D.Cmax) ||
+       dalloc(&D.d_Mo[0], nw * D.M) || dalloc(&D.d_Mo[1], nw * D.M) || dalloc(&D.d_B[0], nw * D.Cmax) ||
+       dalloc(&D.d_B[1], nw * D.Cmax) || dalloc(&D.d_B[2], nw * D.Cmax) || dalloc(&D.d_B[3], nw * D.Cmax) ||
+       dalloc(&D.d_h[0], nw * D.G) || dalloc(&D.d_h[1], nw * D.G) || dalloc(&D.d_bh, nw * D.M) ||
+       dalloc(&D.d_bhd, nw * D.M) || dalloc(&D.d_dot_part, (size_t)kMdInterpBlocks) ||
+       dalloc(&D.d_dot_ticket, (size_t)kTicketWords))
+      return -1;
+   NFFT4GP_HIP_CHECK(hipMemcpy(D.d_comps, D.comps.data(), sizeof(MdComp) * nw, hipMemcpyHostToDevice));
+   if (!u.empty()) {
+      NFFT4GP_HIP_CHECK(hipMemcpy(D.d_u, u.data(), sizeof(int) * u.size(), hipMemcpyHostToDevice));
+      NFFT4GP_HIP_CHECK(hipMemcpy(D.d_psi, psi.data(), sizeof(double) * psi.size(), hipMemcpyHostToDevice));
+   }
+   NFFT4GP_HIP_CHECK(hipMemset(D.d_dot_ticket, 0, sizeof(unsigned int) * kTicketWords));
+   return upload_md_constants();
+}
+
+// every setup: weight * bhat * prod 1/PHI_HUT per component (nfft_interface.c:216-256, :536)
+int md_setup(AdditivePlan& P)
+{
+   MdPlan& D = P.md;
+   std::vector<double> bh((size_t)P.nw * D.M, 0.0), bhd((size_t)P.nw * D.M, 0.0), b0, b1;
+   double phinv[kBand];
+   for (int k = 0; k < kBand; k++) phinv[k] = 1.0 / kb_phi_hut(k - kBand / 2);
+   for (int c = 0; c < P.nw; c++) {
+      const int d = D.comps[c].d;
+      const double sc = P.comp_scale[c], sig = P.comp_sigma[c];
+      bhat_nd(P.kernel == 0 ? 0 : 2, d, sig, b0);
+      bhat_nd(P.kernel == 0 ? 1 : 3, d, sig, b1);
+      const double dscale = (P.kernel == 0) ? 2.0 * sc * std::sqrt(2.0) / sig : sc / sig;  // :536
+      for (size_t j = 0; j < b0.size(); j++) {
+         double di = 1.0;
+         size_t jj = j;
+         for (int t = 0; t < d; t++) {
+            di *= phinv[jj % kBand];
+            jj /= kBand;
+         }
+         bh[(size_t)c * D.M + j] = P.weight * b0[j] * di;
+         bhd[(size_t)c * D.M + j] = P.weight * dscale * b1[j] * di;
+      }
+   }
+   NFFT4GP_HIP_CHECK(hipMemcpy(D.d_bh, bh.data(), sizeof(double) * bh.size(), hipMemcpyHostToDevice));
+   NFFT4GP_HIP_CHECK(hipMemcpy(D.d_bhd, bhd.data(), sizeof(double) * bhd.size(), hipMemcpyHostToDevice));
+   return 0;
+}
+
+int md_spread(const AdditivePlan& P, const double* d_x, double* d_grid, hipStream_t s)
+{
+   const MdPlan& D = P.md;
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(d_grid, 0, sizeof(double) * (size_t)P.nw * D.G, s));
+   if (P.n == 0) return 0;
+   int hi_max = 1;
+   for (int t = 1; t < D.maxd; t++) hi_max *= kTaps;
+   const long long work = (long long)P.n * hi_max;
+   hipLaunchKernelGGL(k_md_spread, dim3((unsigned)((work + kMdThreads - 1) / kMdThreads), P.nw), dim3(kMdThreads), 0,
+                      s, D.d_comps, D.d_u, D.d_psi, d_x, P.n, hi_max, d_grid, D.G);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int md_grid(const AdditivePlan& P, const double* d_grid, int grad, hipStream_t s)
+{
+   const MdPlan& D = P.md;
+   for (int t = 0; t < D.maxd; t++) {
+      // largest pass over the components: 32^(t+1) 64^(maxd-t-1) outputs
+      long long outs = 1;
+      for (int a = 0; a <= t; a++) outs *= kBand;
+      for (int a = t + 1; a < D.maxd; a++) outs *= kNos;
+      hipLaunchKernelGGL(k_md_fwd, dim3((unsigned)((outs + kMdThreads - 1) / kMdThreads), P.nw), dim3(kMdThreads), 0,
+                         s, D.d_comps, t, d_grid, D.G, D.d_F[0], D.d_F[1], D.Cmax);
+   }
+   hipLaunchKernelGGL(k_md_modes, dim3((unsigned)((D.M + kMdThreads - 1) / kMdThreads), P.nw), dim3(kMdThreads), 0, s,
+                      D.d_comps, D.d_F[0], D.d_F[1], D.Cmax, D.d_bh, D.d_bhd, D.M, grad, D.d_Mo[0], D.d_Mo[1]);
+   for (int t = 0; t < D.maxd; t++) {
+      long long outs = 1;
+      for (int a = 0; a <= t; a++) outs *= kNos;
+      for (int a = t + 1; a < D.maxd; a++) outs *= kBand;
+      hipLaunchKernelGGL(k_md_bwd, dim3((unsigned)((outs + kMdThreads - 1) / kMdThreads), P.nw, grad ? 2 : 1),
+                         dim3(kMdThreads), 0, s, D.d_comps, t, D.d_Mo[0], D.d_Mo[1], D.M, D.d_B[0], D.d_B[1],
+                         D.d_B[2], D.d_B[3], D.Cmax, D.d_h[0], D.d_h[1], D.G);
+   }
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int md_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, double beta, double* d_y,
+              hipStream_t s, double* d_dot)
+{
+   const MdPlan& D = P.md;
+   if (P.n == 0) {
+      if (d_dot) NFFT4GP_HIP_CHECK(hipMemsetAsync(d_dot, 0, sizeof(double), s));
+      return 0;
+   }
+   const int blocks = std::min(kMdInterpBlocks, (P.n + kMdThreads / 64 - 1) / (kMdThreads / 64));
+#define NFFT4GP_MD_INTERP(G_, D_)                                                                              \
+   hipLaunchKernelGGL((k_md_interp<G_, D_>), dim3(blocks), dim3(kMdThreads), 0, s, D.d_comps, P.nw, D.d_u, D.d_psi, \
+                      D.d_h[0], D.d_h[1], D.G, d_x, d_y, P.n, alpha, beta, P.f, P.mu, D.d_dot_part, D.d_dot_ticket, \
+                      d_dot)
+   if (grad)
+      NFFT4GP_MD_INTERP(1, 0);
+   else if (d_dot)
+      NFFT4GP_MD_INTERP(0, 1);
+   else
+      NFFT4GP_MD_INTERP(0, 0);
+#undef NFFT4GP_MD_INTERP
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+}  // namespace nfft4gp_amd

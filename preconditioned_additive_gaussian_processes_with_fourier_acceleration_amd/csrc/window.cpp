@@ -10,6 +10,7 @@
 //     keeps (nfft_interface.c:436), the circulant
 //       w[s] = sum_{k=-N/2}^{N/2-1} bhat_k / phihut_k^2 cos(2 pi k s / n_os).
 #include <cmath>
+#include <complex>
 #include <mutex>
 #include <vector>
 
@@ -128,6 +129,48 @@ void bhat_1d(int kind, double c, double* bhat)
       }
       bhat[k] = acc;
    }
+}
+
+// d-dimensional bhat on the N^d modes (index sum_t (k_t + N/2) N^t): the N^-d scaled samples
+// K(min(|l/N|, 1/2)) transformed one axis at a time in complex arithmetic, real part kept (the
+// imaginary part cancels: the samples are even apart from the unpaired l_t = -N/2 planes, whose
+// phase factors are +-1)
+void bhat_nd(int kind, int d, double c, std::vector<double>& bhat)
+{
+   const int N = kBand;
+   int nm = 1;
+   for (int t = 0; t < d; t++) nm *= N;
+   std::vector<std::complex<double>> a(nm), b(nm);
+   for (int j = 0; j < nm; j++) {
+      int jj = j;
+      double r2 = 0.0;
+      for (int t = 0; t < d; t++) {
+         const double lt = (double)(jj % N - N / 2) / (double)N;
+         r2 += lt * lt;
+         jj /= N;
+      }
+      double r = std::sqrt(r2);
+      if (r > 0.5) r = 0.5;
+      a[j] = kern(kind, r, c) / (double)nm;
+   }
+   std::complex<double> tw[kBand];
+   for (int m = 0; m < N; m++) tw[m] = std::polar(1.0, -2.0 * kPi * (double)m / (double)N);
+   int stride = 1;
+   for (int t = 0; t < d; t++) {
+      for (int j = 0; j < nm; j++) {
+         const int lo = j % stride, kt = (j / stride) % N, hi = j / (stride * N);
+         std::complex<double> acc = 0.0;
+         for (int l = 0; l < N; l++) {
+            const int m = ((((kt - N / 2) * (l - N / 2)) % N) + N) % N;  // exact phase reduction
+            acc += a[lo + stride * (l + N * hi)] * tw[m];
+         }
+         b[j] = acc;
+      }
+      a.swap(b);
+      stride *= N;
+   }
+   bhat.resize(nm);
+   for (int j = 0; j < nm; j++) bhat[j] = a[j].real();
 }
 
 void circulant_1d(const double* bhat, double weight, double* w)

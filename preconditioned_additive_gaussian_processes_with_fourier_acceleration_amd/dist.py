@@ -82,7 +82,10 @@ class RowShardedAdditiveKernel:
             # the HIP shard handle writes the grid from a kernel: keep it in HBM (RCCL reduces it in
             # place); a host engine (the numpy replay in the tests) keeps it in host memory
             dev = "cuda" if hasattr(engine, "h") else "cpu"
-            grid = torch.zeros(nwindows * 64, dtype=torch.float64, device=dev)
+            size = engine.shard_grid_size() if hasattr(engine, "shard_grid_size") else nwindows * 64
+            if size <= 0:
+                raise RuntimeError("run the kernel setup on the shard handle before sharding its matvec")
+            grid = torch.zeros(size, dtype=torch.float64, device=dev)
         self.grid = grid
         if hasattr(engine, "h"):
             # the HIP kernels and the collectives must be ordered on torch's current stream

@@ -147,6 +147,11 @@ class NFFTAdditiveKernel:
             raise RuntimeError("shard spread failed")
         return grid
 
+    def shard_grid_size(self) -> int:
+        """Doubles in the grid shard_spread writes (nw*64, or nw*64^dmax with multi-feature windows);
+        -1 before the kernel setup."""
+        return int(_lib.lib().Nfft4GPAmdShardGridSize(self.h))
+
     def shard_finish(self, grid, x_local, alpha=1.0, beta=0.0, y_local=None, grad=False):
         if y_local is None:
             y_local = _empty_like(x_local, (3 if grad else 1) * self.n)
