@@ -48,6 +48,21 @@ typedef int (*func_symmatvec)(void *matrix, int n, NFFT4GP_DOUBLE alpha, NFFT4GP
                               NFFT4GP_DOUBLE beta, NFFT4GP_DOUBLE *y);
 /* SRC/utils/utils.h (func_free) */
 typedef void (*func_free)(void *str);
+/* SRC/solvers/solvers.h:58, :66, :79: preconditioner trace / logdet / dM/dtheta x (GP loss gradient) */
+typedef int (*func_trace)(void *str, NFFT4GP_DOUBLE **tracesp);
+typedef NFFT4GP_DOUBLE (*func_logdet)(void *str);
+typedef int (*func_dvp)(void *str, int n, int *mask, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE **yp);
+/* SRC/preconds/precond.h:39-47 */
+typedef int (*precond_kernel_setup)(NFFT4GP_DOUBLE *data, int n, int ldim, int d, func_kernel fkernel,
+                                    void *fkernel_params, int require_grad, void *precond_data);
+/* SRC/optimizer/transform.h:15-20 */
+typedef enum
+{
+   NFFT4GP_TRANSFORM_SOFTPLUS = 0,
+   NFFT4GP_TRANSFORM_SIGMOID,
+   NFFT4GP_TRANSFORM_EXP,
+   NFFT4GP_TRANSFORM_IDENTITY
+} nfft4gp_transform_type;
 
 /* ---- kernel handle: field layout identical to SRC/linearalg/kernels.h:65-95 -------------------
  * Callers write _params[0] (f), _params[1] (l) and _noise_level (mu) directly
@@ -132,6 +147,9 @@ NFFT4GP_DOUBLE Nfft4GPVecDdot(NFFT4GP_DOUBLE *x, int n, NFFT4GP_DOUBLE *y);     
 void Nfft4GPVecFill(NFFT4GP_DOUBLE *x, size_t n, NFFT4GP_DOUBLE val);           /* vecops.c:47-69 */
 void Nfft4GPVecScale(NFFT4GP_DOUBLE *x, size_t n, NFFT4GP_DOUBLE scale);        /* vecops.c:71-100 */
 void Nfft4GPVecAxpy(NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, size_t n, NFFT4GP_DOUBLE *y); /* vecops.c:102-155 */
+/* vecops.c:15-46: serial libc rand() / RAND_MAX (Rademacher: < 0.5 -> -1, else 1), as the reference */
+void Nfft4GPVecRand(NFFT4GP_DOUBLE *x, int n);
+void Nfft4GPVecRadamacher(NFFT4GP_DOUBLE *x, int n);
 
 /* ---- PCG (SRC/solvers/pcg.c:3-206), device-resident ------------------------------------------- */
 int Nfft4GPSolverPcg(void *mat_data, int n, func_symmatvec matvec, void *prec_data, func_solve precondfunc,
@@ -141,6 +159,40 @@ int Nfft4GPSolverPcg(void *mat_data, int n, func_symmatvec matvec, void *prec_da
 /* length of the rel_res_v array returned by the last Nfft4GPSolverPcg call on this process
  * (1 for the early exits of pcg.c:32-41 / :70-84, maxits+1 otherwise) */
 int Nfft4GPAmdPcgHistoryLength(void);
+
+/* ---- FGMRES, Lanczos, stochastic Lanczos quadrature, GP loss ------------------------------------
+ * Same signatures and results as the reference; every n-vector lives in HBM, callbacks follow the PCG
+ * rules above (this library's operators/preconditioners get device pointers, others host vectors).
+ * prel_res_v / TDp / TEp are malloc'ed (free with free()). */
+/* SRC/solvers/fgmres.c:3-252 (MGS without re-orthogonalisation; kdim <= 4094) */
+int Nfft4GPSolverFgmres(void *mat_data, int n, func_symmatvec matvec, void *prec_data, func_solve precondfunc,
+                        NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs, int kdim, int maxits, int atol, NFFT4GP_DOUBLE tol,
+                        NFFT4GP_DOUBLE *prel_res, NFFT4GP_DOUBLE **prel_res_v, int *piter, int print_level);
+/* SRC/solvers/lanczos.c:3-419 (preconditioned Lanczos, MGS2 re-orthogonalisation; maxits <= 4094) */
+int Nfft4GPSolverLanczos(void *mat_data, int n, func_symmatvec matvec, void *prec_data, func_solve precondfunc,
+                         NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs, int wsize, int maxits, int atol, NFFT4GP_DOUBLE tol,
+                         NFFT4GP_DOUBLE *prel_res, NFFT4GP_DOUBLE **prel_res_v, int *piter, int *tsize,
+                         NFFT4GP_DOUBLE **TDp, NFFT4GP_DOUBLE **TEp, int print_level);
+/* SRC/solvers/lanczos.c:421-610: logdet(K)/n and its hyperparameter gradient; radamacher (n x nvecs,
+ * host or device) or NULL for Nfft4GPVecRadamacher probes */
+int Nfft4GPLanczosQuadratureLogdet(void *mat_data, void *dmat_data, int n, func_symmatvec matvec,
+                                   func_symmatvec dmatvec, void *prec_data, func_solve precondfunc,
+                                   func_trace tracefunc, func_logdet logdetfunc, func_dvp dvpfunc, int maxits,
+                                   int nvecs, NFFT4GP_DOUBLE *radamacher, int print_level, NFFT4GP_DOUBLE *logdet,
+                                   NFFT4GP_DOUBLE **dlogdetp);
+/* SRC/optimizer/transform.c:4-89 */
+int Nfft4GPTransform(nfft4gp_transform_type type, NFFT4GP_DOUBLE val, int inverse, NFFT4GP_DOUBLE *tvalp,
+                     NFFT4GP_DOUBLE *dtvalp);
+/* SRC/optimizer/gp_loss.c:96-307: loss = (y^T K^{-1} y + logdet K + log 2 pi) / (2n) and its gradient in
+ * the transformed hyperparameters x = (f, l, mu) */
+int Nfft4GPGpLoss(NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *data, NFFT4GP_DOUBLE *label, int n, int ldim, int d,
+                  func_kernel fkernel, void *vfkernel_data, func_free kernel_data_free, func_symmatvec matvec,
+                  func_symmatvec dmatvec, func_kernel precond_fkernel, void *precond_vfkernel_data,
+                  func_free precond_vfkernel_data_free, precond_kernel_setup precond_setup, func_solve precond_solve,
+                  func_trace precond_trace, func_logdet precond_logdet, func_dvp precond_dvp, func_free precond_reset,
+                  void *precond_data, int atol, NFFT4GP_DOUBLE tol, int wsize, int maxits, int nvecs,
+                  NFFT4GP_DOUBLE *radamacher, nfft4gp_transform_type transform, int *mask, int print_level,
+                  NFFT4GP_DOUBLE *dwork, NFFT4GP_DOUBLE *loss, NFFT4GP_DOUBLE *grad);
 /* how Nfft4GPSolverPcg hands vectors to its matvec / preconditioner callbacks:
  * -1 (default) device pointers for this library's own operators, host-staged vectors for any other
  *  function; 0 always host-staged; 1 always device pointers (for user callbacks written for HBM). */

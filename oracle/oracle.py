@@ -452,3 +452,161 @@ def afn_apply(perm, L11, K12, schur_solve, rhs):
     x = np.empty(n)
     x[perm] = np.concatenate([y, y2])
     return x
+
+
+# ----------------------------------------------------------------------------------------------
+# FGMRES (fgmres.c), Lanczos quadrature (lanczos.c:421-610) and the GP loss (gp_loss.c:96-307) of the
+# reference, driven through oracle/_ref with its dense operator and Nystrom preconditioner
+# ----------------------------------------------------------------------------------------------
+def _host_cb(matvec_py, nout=1):
+    def _mv(_m, nn, alpha, xp, beta, yp):
+        xv = np.ctypeslib.as_array(xp, shape=(nn,))
+        yv = np.ctypeslib.as_array(yp, shape=(nout * nn,))
+        matvec_py(alpha, xv, beta, yv)
+        return 0
+    return SYMMATVEC(_mv)
+
+
+def ref_fgmres(matvec_py, n, b, kdim, maxits, tol, atol=0, precond_py=None, x0=None):
+    """Nfft4GPSolverFgmres (fgmres.c:3-252) with Python callbacks; returns (x, rel_res, hist, iters)."""
+    lib = ref_lib()
+    lib.Nfft4GPSolverFgmres.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _dp, _dp, C.c_int,
+                                        C.c_int, C.c_int, C.c_double, _dp, C.POINTER(_dp), _ip, C.c_int]
+    mv_cb = _host_cb(matvec_py)
+
+    def _pc(_p, nn, xp, rp):
+        precond_py(np.ctypeslib.as_array(xp, shape=(nn,)), np.ctypeslib.as_array(rp, shape=(nn,)))
+        return 0
+
+    pc_cb = SOLVE(_pc) if precond_py is not None else None
+    x = np.zeros(n) if x0 is None else np.array(x0, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    rel, relv, it, dummy = C.c_double(), _dp(), C.c_int(), C.c_int(1)
+    lib.Nfft4GPSolverFgmres(None, n, C.cast(mv_cb, C.c_void_p), C.byref(dummy) if pc_cb else None,
+                            C.cast(pc_cb, C.c_void_p) if pc_cb else None, _d(x), _d(b), kdim, maxits, atol, tol,
+                            C.byref(rel), C.byref(relv), C.byref(it), -1)
+    hist = np.ctypeslib.as_array(relv, shape=(maxits + 1,)).copy()
+    return x, rel.value, hist, it.value
+
+
+def ref_logdet_quadrature(matvec_py, dmatvec_py, n, maxits, nvecs, radamacher):
+    """Nfft4GPLanczosQuadratureLogdet (lanczos.c:421-610), no preconditioner, fixed Rademacher probes."""
+    lib = ref_lib()
+    f = lib.Nfft4GPLanczosQuadratureLogdet
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                  C.c_void_p, C.c_void_p, C.c_int, C.c_int, _dp, C.c_int, _dp, C.POINTER(_dp)]
+    mv_cb = _host_cb(matvec_py)
+    dmv_cb = _host_cb(dmatvec_py, 3)
+    R = np.asfortranarray(radamacher, dtype=np.float64)
+    val = C.c_double()
+    dval = _dp()
+    rc = f(None, None, n, C.cast(mv_cb, C.c_void_p), C.cast(dmv_cb, C.c_void_p), None, None, None, None, None,
+           maxits, nvecs, _d(R), -1, C.byref(val), C.byref(dval))
+    assert rc == 0
+    return val.value, np.ctypeslib.as_array(dval, shape=(3,)).copy()
+
+
+class RefGpLoss:
+    """Nfft4GPGpLoss (gp_loss.c:96-307) of the reference on its dense additive kernel (kernels.c:3099-3494,
+    Gaussian), Nfft4GPDenseMatSymv / Nfft4GPDenseGradMatSymv (matops.c:3-29) and, optionally, its Nystrom
+    preconditioner with gradients (nys.c:175-660).  ``args(lib_fn)`` gives the argument tuple with the
+    reference's own function pointers, so the same call can be made on this library's Nfft4GPGpLoss."""
+
+    def __init__(self, X, windows, nw, dw, k=0, perm=None):
+        lib = ref_lib()
+        self.lib = lib
+        self.X = np.asfortranarray(X, dtype=np.float64)
+        self.n, self.d = self.X.shape
+        self.win = np.ascontiguousarray(np.asarray(windows, dtype=np.int32).ravel())
+        fk = C.cast(lib.Nfft4GPKernelGaussianKernel, C.c_void_p)
+        mk = lambda: lib.Nfft4GPKernelAdditiveKernelParamCreate(_d(self.X), self.n, self.n, self.d, _i(self.win),
+                                                                  nw, dw, fk)
+        self.kh = mk()
+        self.pkh = mk()
+        self.k = k
+        self.nys = None
+        if k > 0:
+            self.perm = np.ascontiguousarray(np.asarray(perm, dtype=np.int32))
+            self.nys = lib.Nfft4GPPrecondNysCreate()
+            lib.Nfft4GPPrecondNysSetRank(self.nys, k)
+            lib.Nfft4GPPrecondNysSetPerm(self.nys, _i(self.perm), 0)
+        self.dwork = np.zeros(4 * self.n * self.n + 4 * self.n)
+
+    def fn(self, name):
+        return C.cast(getattr(self.lib, name), C.c_void_p).value
+
+    def args(self, hyper, label, maxits, nvecs, radamacher, tol=1e-8, transform=0):
+        x = np.ascontiguousarray(hyper, dtype=np.float64)
+        lab = np.ascontiguousarray(label, dtype=np.float64)
+        R = np.asfortranarray(radamacher, dtype=np.float64)
+        self._keep = (x, lab, R)
+        nys = self.k > 0
+        P = lambda name: self.fn(name) if nys else None
+        return (x.ctypes.data, self.X.ctypes.data, lab.ctypes.data, self.n, self.n, self.d,
+                self.fn("Nfft4GPKernelAdditiveKernel"), self.kh, None, self.fn("Nfft4GPDenseMatSymv"),
+                self.fn("Nfft4GPDenseGradMatSymv"), self.fn("Nfft4GPKernelAdditiveKernel"), self.pkh, None,
+                P("Nfft4GPPrecondNysSetupWithKernel"), P("Nfft4GPPrecondNysSolve"), P("Nfft4GPPrecondNysTrace"),
+                P("Nfft4GPPrecondNysLogdet"), P("Nfft4GPPrecondNysDvp"), P("Nfft4GPPrecondNysReset"),
+                self.nys if nys else None, 0, tol, maxits, maxits, nvecs, R.ctypes.data, transform, None, 0,
+                self.dwork.ctypes.data)
+
+    ARGTYPES = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.c_int, C.c_int, C.c_int,
+                C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, _dp, _dp]
+
+    def run(self, fn, *a, **kw):
+        """fn = a Nfft4GPGpLoss entry point (the reference's, or this library's); returns (loss, grad)."""
+        fn.argtypes = self.ARGTYPES
+        fn.restype = C.c_int
+        loss = np.zeros(1)
+        grad = np.zeros(3)
+        rc = fn(*self.args(*a, **kw), _d(loss), _d(grad))
+        assert rc == 0, rc
+        return float(loss[0]), grad
+
+    def reference(self, *a, **kw):
+        return self.run(self.lib.Nfft4GPGpLoss, *a, **kw)
+
+
+FUNC_KERNEL = C.CFUNCTYPE(C.c_int, C.c_void_p, _dp, C.c_int, C.c_int, C.c_int, _ip, C.c_int, _ip, C.c_int,
+                          C.POINTER(_dp), C.POINTER(_dp))
+
+
+def ref_gp_loss_nfft(X, windows, nw, dw, label, hyper, maxits, nvecs, radamacher, tol=1e-8):
+    """The reference's Nfft4GPGpLoss (gp_loss.c:96-307, compiled in oracle/_ref) driven by this oracle's
+    NFFT operator (the CPU restatement of nfft_interface.c): the kernel setup callback reads f, l, mu from
+    the kernel struct the loss writes (gp_loss.c:143-150) and sets the oracle up; matvec / grad matvec
+    are the oracle's (no preconditioner).  Returns (loss, grad)."""
+    lib = ref_lib()
+    X = np.asfortranarray(X, dtype=np.float64)
+    n, d = X.shape
+    o = OracleAdditiveNFFT(X, np.asarray(windows, dtype=np.int32), nw, dw)
+    kh = lib.Nfft4GPKernelParamCreate(n, 0)
+    st = NfftKernelStruct.from_address(kh)
+
+    def fk(_s, _data, _n, _ldim, _d, _pr, _kr, _pc, _kc, Kp, dKp):
+        o.setup(0, st._params[0], st._params[1], st._noise_level)
+        Kp[0] = C.cast(C.c_void_p(kh), _dp)
+        dKp[0] = C.cast(C.c_void_p(kh), _dp)
+        return 0
+
+    fk_cb = FUNC_KERNEL(fk)
+    mv_cb = _host_cb(lambda a, xv, b, yv: yv.__setitem__(slice(None), o.matsymv(xv.copy(), a, b, yv.copy())))
+    dmv_cb = _host_cb(lambda a, xv, b, yv: yv.__setitem__(slice(None), o.gradmatsymv(xv.copy(), a, b, yv.copy())),
+                      3)
+    x = np.ascontiguousarray(hyper, dtype=np.float64)
+    lab = np.ascontiguousarray(label, dtype=np.float64)
+    R = np.asfortranarray(radamacher, dtype=np.float64)
+    loss = np.zeros(1)
+    grad = np.zeros(3)
+    fn = lib.Nfft4GPGpLoss
+    fn.argtypes = RefGpLoss.ARGTYPES
+    fn.restype = C.c_int
+    V = lambda cb: C.cast(cb, C.c_void_p).value
+    pkh = lib.Nfft4GPKernelParamCreate(n, 0)  # gp_loss.c:145-150 writes the preconditioner's kernel struct too
+    rc = fn(x.ctypes.data, X.ctypes.data, lab.ctypes.data, n, n, d, V(fk_cb), kh, None, V(mv_cb), V(dmv_cb),
+            None, pkh, None, None, None, None, None, None, None, None, 0, tol, maxits, maxits, nvecs,
+            R.ctypes.data, 0, None, -1, None, _d(loss), _d(grad))
+    assert rc == 0
+    return float(loss[0]), grad

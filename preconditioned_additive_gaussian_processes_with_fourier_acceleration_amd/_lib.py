@@ -76,6 +76,15 @@ _SIGS = {
     "Nfft4GPSolverPcg": (C.c_int, [vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_double, dp,
                                    C.POINTER(dp), ip, C.c_int]),
     "Nfft4GPAmdPcgHistoryLength": (C.c_int, []),
+    "Nfft4GPSolverFgmres": (C.c_int, [vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_double, dp,
+                                      C.POINTER(dp), ip, C.c_int]),
+    "Nfft4GPSolverLanczos": (C.c_int, [vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_double, dp,
+                                       C.POINTER(dp), ip, ip, C.POINTER(dp), C.POINTER(dp), C.c_int]),
+    "Nfft4GPLanczosQuadratureLogdet": (C.c_int, [vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int, C.c_int, vp,
+                                                 C.c_int, dp, C.POINTER(dp)]),
+    "Nfft4GPTransform": (C.c_int, [C.c_int, C.c_double, C.c_int, dp, dp]),
+    "Nfft4GPVecRand": (None, [vp, C.c_int]),
+    "Nfft4GPVecRadamacher": (None, [vp, C.c_int]),
     "Nfft4GPAmdSetCallbackPointerMode": (None, [C.c_int]),
     "Nfft4GPAmdNysCreate": (vp, [C.c_int, C.c_int, vp, vp, C.c_double, vp]),
     "Nfft4GPAmdNysSolve": (C.c_int, [vp, C.c_int, vp, vp]),

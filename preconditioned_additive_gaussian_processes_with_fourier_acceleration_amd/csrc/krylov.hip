@@ -1,0 +1,909 @@
+// krylov.hip -- FGMRES, preconditioned Lanczos, stochastic Lanczos quadrature and the GP loss, with
+// every n-vector (Krylov bases, iterates, probes) in HBM.
+//
+//   Nfft4GPSolverFgmres            SRC/solvers/fgmres.c:3-252   restarted flexible GMRES, MGS without
+//                                                               re-orthogonalisation, the reference's
+//                                                               restart and breakdown behaviour
+//   Nfft4GPSolverLanczos           SRC/solvers/lanczos.c:3-419  M-inner-product Lanczos with full MGS2
+//                                                               re-orthogonalisation (matops.c:348-440)
+//   Nfft4GPLanczosQuadratureLogdet SRC/solvers/lanczos.c:421-610
+//   Nfft4GPGpLoss                  SRC/optimizer/gp_loss.c:96-307
+//   Nfft4GPTransform               SRC/optimizer/transform.c:4-89
+//
+// The small dense work (Givens rotations, the Cholesky of T, the tridiagonal eigensolve) runs on the
+// host on scalars read back once per iteration; each Gram-Schmidt step is one fused launch (apply the
+// previous projection, then the next inner product, reduced on the device in a fixed order).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "callbacks.hpp"
+#include "internal.h"
+#include "reduce.hpp"
+
+using namespace nfft4gp_amd;
+
+namespace {
+
+constexpr int kKThreads = 256;
+constexpr int kKEPT = 4;
+constexpr int kKMaxBlocks = 2048;  // <= kRedMaxBlocks
+
+int kgrid(size_t n)
+{
+   size_t g = (n + (size_t)kKThreads * kKEPT - 1) / ((size_t)kKThreads * kKEPT);
+   g = std::min<size_t>(g, kKMaxBlocks);
+   return (int)(g == 0 ? 1 : g);
+}
+
+// w -= (*hprev) * u (when u != nullptr); then *out = (w, v) (v != nullptr) or ||w||^2 (v == nullptr)
+__global__ __launch_bounds__(kKThreads) void k_gs_step(double* __restrict__ w, const double* __restrict__ u,
+                                                       const double* __restrict__ hprev,
+                                                       const double* __restrict__ v, size_t n,
+                                                       double* __restrict__ part, unsigned int* __restrict__ ticket,
+                                                       double* __restrict__ out)
+{
+   const double h = u ? *hprev : 0.0;
+   double acc = 0.0;
+   const size_t stride = (size_t)gridDim.x * kKThreads * kKEPT;
+   for (size_t i0 = (size_t)blockIdx.x * kKThreads * kKEPT + threadIdx.x; i0 < n; i0 += stride) {
+      double wv[kKEPT], uv[kKEPT], vv[kKEPT];
+#pragma unroll
+      for (int e = 0; e < kKEPT; e++) {
+         const size_t i = i0 + (size_t)e * kKThreads;
+         wv[e] = i < n ? w[i] : 0.0;
+         uv[e] = (u && i < n) ? u[i] : 0.0;
+         vv[e] = (v && i < n) ? v[i] : 0.0;
+      }
+#pragma unroll
+      for (int e = 0; e < kKEPT; e++) {
+         const size_t i = i0 + (size_t)e * kKThreads;
+         if (u) {
+            wv[e] = fma(-h, uv[e], wv[e]);
+            if (i < n) w[i] = wv[e];
+         }
+         acc = v ? fma(wv[e], vv[e], acc) : fma(wv[e], wv[e], acc);
+      }
+   }
+   acc = block_sum0<kKThreads>(acc);
+   double tot;
+   if (grid_total<kKThreads>(acc, part, ticket, &tot) && threadIdx.x == 0) *out = tot;
+}
+
+// out[0] = (a, b), out[1] = (b, b): the Lanczos (v, z) and ||z||^2 in one pass
+__global__ __launch_bounds__(kKThreads) void k_dot2(const double* __restrict__ a, const double* __restrict__ b,
+                                                    size_t n, double* __restrict__ part,
+                                                    unsigned int* __restrict__ ticket, double* __restrict__ part2,
+                                                    unsigned int* __restrict__ ticket2, double* __restrict__ out)
+{
+   double ab = 0.0, bb = 0.0;
+   const size_t stride = (size_t)gridDim.x * kKThreads * kKEPT;
+   for (size_t i0 = (size_t)blockIdx.x * kKThreads * kKEPT + threadIdx.x; i0 < n; i0 += stride) {
+      double av[kKEPT], bv[kKEPT];
+#pragma unroll
+      for (int e = 0; e < kKEPT; e++) {
+         const size_t i = i0 + (size_t)e * kKThreads;
+         av[e] = i < n ? a[i] : 0.0;
+         bv[e] = i < n ? b[i] : 0.0;
+      }
+#pragma unroll
+      for (int e = 0; e < kKEPT; e++) {
+         ab = fma(av[e], bv[e], ab);
+         bb = fma(bv[e], bv[e], bb);
+      }
+   }
+   ab = block_sum0<kKThreads>(ab);
+   double tot;
+   if (grid_total<kKThreads>(ab, part, ticket, &tot) && threadIdx.x == 0) out[0] = tot;
+   __syncthreads();
+   bb = block_sum0<kKThreads>(bb);
+   if (grid_total<kKThreads>(bb, part2, ticket2, &tot) && threadIdx.x == 0) out[1] = tot;
+}
+
+__global__ void k_scale2(double* __restrict__ a, double* __restrict__ b, size_t n, double s)
+{
+   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+      a[i] *= s;
+      if (b) b[i] *= s;
+   }
+}
+
+// x += sum_j c[j] B[:, j] (columns in order, ld = n)
+__global__ void k_combine(double* __restrict__ x, const double* __restrict__ B, size_t ld, size_t n,
+                          const double* __restrict__ c, int m)
+{
+   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+      double v = x[i];
+      for (int j = 0; j < m; j++) v = fma(c[j], B[(size_t)j * ld + i], v);
+      x[i] = v;
+   }
+}
+
+// y = a - b
+__global__ void k_sub(double* __restrict__ y, const double* __restrict__ a, const double* __restrict__ b, size_t n)
+{
+   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+      y[i] = a[i] - b[i];
+}
+
+int egrid(size_t n)
+{
+   size_t g = (n + 255) / 256;
+   return (int)std::max<size_t>(1, std::min<size_t>(g, 4096));
+}
+
+// device scratch of the Krylov solvers: two reduction pairs, device scalars, pinned read-back
+struct KScratch {
+   static constexpr int kScal = 4096;
+   double *part = nullptr, *part2 = nullptr, *scal = nullptr, *hscal = nullptr, *coef = nullptr;
+   unsigned int *ticket = nullptr, *ticket2 = nullptr;
+   int ensure()
+   {
+      if (part) return 0;
+      NFFT4GP_HIP_CHECK(hipMalloc((void**)&part, sizeof(double) * kKMaxBlocks));
+      NFFT4GP_HIP_CHECK(hipMalloc((void**)&part2, sizeof(double) * kKMaxBlocks));
+      NFFT4GP_HIP_CHECK(hipMalloc((void**)&scal, sizeof(double) * kScal));
+      NFFT4GP_HIP_CHECK(hipMalloc((void**)&coef, sizeof(double) * kScal));
+      NFFT4GP_HIP_CHECK(hipMalloc((void**)&ticket, sizeof(unsigned int) * kTicketWords));
+      NFFT4GP_HIP_CHECK(hipMalloc((void**)&ticket2, sizeof(unsigned int) * kTicketWords));
+      NFFT4GP_HIP_CHECK(hipMemset(ticket, 0, sizeof(unsigned int) * kTicketWords));
+      NFFT4GP_HIP_CHECK(hipMemset(ticket2, 0, sizeof(unsigned int) * kTicketWords));
+      NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&hscal, sizeof(double) * kScal));
+      return 0;
+   }
+};
+KScratch g_k;
+
+struct Ctx {
+   hipStream_t s;
+   size_t n;
+   // w -= h u (u optional), *out = (w, v) or ||w||^2
+   int gs(double* w, const double* u, const double* hprev, const double* v, double* out)
+   {
+      hipLaunchKernelGGL(k_gs_step, dim3(kgrid(n)), dim3(kKThreads), 0, s, w, u, hprev, v, n, g_k.part, g_k.ticket,
+                         out);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   }
+   int read(const double* d, int count, double* h)
+   {
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(g_k.hscal, d, sizeof(double) * count, hipMemcpyDeviceToHost, s));
+      NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
+      memcpy(h, g_k.hscal, sizeof(double) * count);
+      return 0;
+   }
+   double dot(const double* a, const double* b)
+   {
+      if (gs(const_cast<double*>(a), nullptr, nullptr, b, g_k.scal + KScratch::kScal - 1)) return NAN;
+      double v;
+      if (read(g_k.scal + KScratch::kScal - 1, 1, &v)) return NAN;
+      return v;
+   }
+   double norm(const double* a) { return std::sqrt(dot(a, a)); }
+   void scale(double* a, double* b, double f)
+   {
+      hipLaunchKernelGGL(k_scale2, dim3(egrid(n)), dim3(256), 0, s, a, b, n, f);
+   }
+   int combine(double* x, const double* B, int m, const double* c)
+   {
+      if (m <= 0) return 0;
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(g_k.coef, c, sizeof(double) * m, hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(k_combine, dim3(egrid(n)), dim3(256), 0, s, x, B, n, n, g_k.coef, m);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   }
+   int copy(double* dst, const double* src)
+   {
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+      return 0;
+   }
+};
+
+double* rel_hist(int len)
+{
+   return (double*)calloc((size_t)std::max(1, len), sizeof(double));
+}
+
+template <class T>
+int dmalloc(T** p, size_t count)
+{
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)p, sizeof(T) * std::max<size_t>(1, count)));
+   return 0;
+}
+
+// host tridiagonal eigensolve: dstev 'V' (ascending eigenvalues, eigenvectors in columns of TV)
+int tridiag_eig(int m, const double* d, const double* e, std::vector<double>& w, std::vector<double>& V)
+{
+   std::vector<double> A((size_t)m * m, 0.0);
+   for (int i = 0; i < m; i++) {
+      A[(size_t)i * m + i] = d[i];
+      if (i + 1 < m) {
+         A[(size_t)i * m + i + 1] = e[i];
+         A[(size_t)(i + 1) * m + i] = e[i];
+      }
+   }
+   return sym_eig_host(A, m, w, V);
+}
+
+}  // namespace
+
+namespace nfft4gp_amd {
+
+// ---- FGMRES (fgmres.c:3-252) on device vectors ----------------------------------------------------
+int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits, int atol, double tol,
+               double* prel_res, double** prel_res_v, int* piter, int print_level)
+{
+   const size_t n = cb.n;
+   Ctx c{current_stream(), n};
+   const double EPS = DBL_EPSILON;
+   if (n == 0) {
+      *prel_res = 0.0;
+      *piter = 0;
+      *prel_res_v = rel_hist(1);
+      return 0;
+   }
+   const double normb = c.norm(rhs);
+   if (normb < EPS) {
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(x, 0, sizeof(double) * n, c.s));
+      *prel_res = 0.0;
+      *piter = 0;
+      *prel_res_v = rel_hist(1);
+      return 0;
+   }
+   if (kdim + 2 > KScratch::kScal) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPSolverFgmres: restart dimension %d above %d\n", kdim, KScratch::kScal - 2);
+      return -1;
+   }
+   double *V = nullptr, *Z = nullptr;
+   if (dmalloc(&V, n * (size_t)(kdim + 1)) || dmalloc(&Z, n * (size_t)(kdim + 1))) return -1;
+   auto cleanup = [&]() {
+      (void)hipStreamSynchronize(c.s);
+      (void)hipFree(V);
+      (void)hipFree(Z);
+   };
+   std::vector<double> H((size_t)kdim * (kdim + 1), 0.0), cs(kdim), sn(kdim), rs(kdim + 1);
+   double* v = V;
+   c.copy(v, rhs);
+   if (cb.apply(-1.0, x, 1.0, v)) {
+      cleanup();
+      return -1;
+   }
+   double normr = c.norm(v);
+   if (normr < EPS) {
+      *prel_res = 0.0;
+      *piter = 0;
+      *prel_res_v = rel_hist(1);
+      cleanup();
+      return 0;
+   }
+   const double tolr = atol ? tol : tol * normb;
+   double* rel = rel_hist(maxits + 1);
+   rel[0] = normr / normb;
+   int iter = 0, i = 0;
+   double* w = V;
+   if (print_level > 0) {
+      printf("--------------------------------------------------------------------------------\n");
+      printf("Start FlexGMRES(%d)\n", kdim);
+      printf("Residual Tol: %e\nMax number of inner iterations: %d\n", tolr, maxits);
+      printf("--------------------------------------------------------------------------------\n");
+      printf("Step    Residual norm  Relative res.  Convergence Rate\n");
+      printf("%5d   %8e   %8e   N/A\n", 0, normr, rel[0]);
+   }
+   bool broke = false;
+   while (iter < maxits) {
+      rs[0] = normr;
+      c.scale(v, nullptr, 1.0 / normr);
+      i = 0;
+      while (i < kdim && iter < maxits) {
+         i++;
+         iter++;
+         v = V + (size_t)(i - 1) * n;
+         double* z = Z + (size_t)(i - 1) * n;
+         w = V + (size_t)i * n;
+         if (cb.prec) {
+            if (cb.solve(z, v) || cb.apply(1.0, z, 0.0, w)) {
+               free(rel);
+               cleanup();
+               return -1;
+            }
+         } else {
+            c.copy(z, v);
+            if (cb.apply(1.0, v, 0.0, w)) {
+               free(rel);
+               cleanup();
+               return -1;
+            }
+         }
+         // Nfft4GPModifiedGS (matops.c:274-346) with k = i-1, no re-orthogonalisation
+         double* hd = g_k.scal;
+         for (int j = 0; j < i; j++)
+            if (c.gs(w, j ? V + (size_t)(j - 1) * n : nullptr, j ? hd + j - 1 : nullptr, V + (size_t)j * n, hd + j))
+               return -1;
+         if (c.gs(w, V + (size_t)(i - 1) * n, hd + i - 1, nullptr, hd + i)) return -1;
+         std::vector<double> hcol(i + 1);
+         if (c.read(hd, i + 1, hcol.data())) return -1;
+         const double t = std::sqrt(hcol[i]);
+         double* Hc = H.data() + (size_t)(i - 1) * (kdim + 1);
+         for (int j = 0; j < i; j++) Hc[j] = hcol[j];
+         Hc[i] = t;
+         c.scale(w, nullptr, 1.0 / t);
+         for (int j = 1; j < i; j++) {
+            const double hii = Hc[j - 1];
+            Hc[j - 1] = cs[j - 1] * hii + sn[j - 1] * Hc[j];
+            Hc[j] = -sn[j - 1] * hii + cs[j - 1] * Hc[j];
+         }
+         const double hii = Hc[i - 1], hii1 = Hc[i];
+         const double gam = std::sqrt(hii * hii + hii1 * hii1);
+         if (std::fabs(gam) < EPS) {
+            broke = true;  // fgmres.c:179-182: leave without updating x
+            break;
+         }
+         cs[i - 1] = hii / gam;
+         sn[i - 1] = hii1 / gam;
+         rs[i] = -sn[i - 1] * rs[i - 1];
+         rs[i - 1] = cs[i - 1] * rs[i - 1];
+         Hc[i - 1] = cs[i - 1] * hii + sn[i - 1] * hii1;
+         normr = std::fabs(rs[i]);
+         rel[iter] = normr / normb;
+         if (print_level > 0)
+            printf("%5d   %8e   %8e   %8.6f\n", iter, normr, rel[iter], rel[iter] / rel[iter - 1]);
+         if (normr <= tolr) break;
+      }
+      if (broke) break;
+      if (print_level == 0)
+         printf("Rel. residual at the end of current cycle (# of steps per cycle/total its: %d/%d): %e \n", kdim,
+                iter, rel[iter]);
+      rs[i - 1] /= H[(size_t)(i - 1) * (kdim + 1) + i - 1];
+      for (int k = i - 2; k >= 0; k--) {
+         for (int j = k + 1; j < i; j++) rs[k] -= H[(size_t)j * (kdim + 1) + k] * rs[j];
+         rs[k] /= H[(size_t)k * (kdim + 1) + k];
+      }
+      if (c.combine(x, Z, i, rs.data())) return -1;
+      if (normr <= tolr) break;
+      // restart (fgmres.c:236-243): v = rhs - A x through w; normr keeps the Givens estimate
+      v = V;
+      c.copy(v, rhs);
+      if (cb.apply(1.0, x, 0.0, w)) {
+         free(rel);
+         cleanup();
+         return -1;
+      }
+      hipLaunchKernelGGL(k_sub, dim3(egrid(n)), dim3(256), 0, c.s, v, v, w, n);
+   }
+   *prel_res = normr / normb;
+   *piter = iter;
+   *prel_res_v = rel;
+   cleanup();
+   return 0;
+}
+
+// ---- Lanczos (lanczos.c:3-419) on device vectors ----------------------------------------------------
+// MGS2 (matops.c:348-440) of w against V[0..k] (dots) / Z[0..k] (updates), re-orthogonalised while
+// ||w|| < 0.7071 * its previous norm; returns ||w|| and adds the last two projections to td / te
+static int mgs2(Ctx& c, double* w, const double* V, const double* Z, int k, double* td, double* te, double* t)
+{
+   const size_t n = c.n;
+   double normw = c.norm(w);
+   double* hd = g_k.scal;
+   for (int pass = 0;; pass++) {
+      for (int i = 0; i <= k; i++)
+         if (c.gs(w, i ? Z + (size_t)(i - 1) * n : nullptr, i ? hd + i - 1 : nullptr, V + (size_t)i * n, hd + i))
+            return -1;
+      if (c.gs(w, Z + (size_t)k * n, hd + k, nullptr, hd + k + 1)) return -1;
+      std::vector<double> h(k + 2);
+      if (c.read(hd, k + 2, h.data())) return -1;
+      if (pass == 0) {
+         if (k >= 1 && te) *te = h[k - 1];
+         if (td) *td = h[k];
+      } else {
+         if (k >= 1 && te) *te += h[k - 1];
+         if (td) *td += h[k];
+      }
+      *t = std::sqrt(h[k + 1]);
+      if (!(*t < normw * 0.7071 && *t >= DBL_EPSILON)) break;
+      normw = *t;
+   }
+   return 0;
+}
+
+int lanczos_dev(Callbacks& cb, double* x, const double* rhs, int wsize, int maxits, int atol, double tol,
+                double* prel_res, double** prel_res_v, int* piter, int* tsize, double** TDp, double** TEp,
+                int print_level)
+{
+   const size_t n = cb.n;
+   Ctx c{current_stream(), n};
+   const double EPS = DBL_EPSILON;
+   if (wsize <= 0) wsize = maxits;
+   wsize = std::min(wsize, maxits);
+   if (n == 0) {
+      *prel_res = 0.0;
+      *piter = 0;
+      *prel_res_v = rel_hist(1);
+      return 0;
+   }
+   const double normb = c.norm(rhs);
+   if (normb < EPS) {
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(x, 0, sizeof(double) * n, c.s));
+      *prel_res = 0.0;
+      *piter = 0;
+      *prel_res_v = rel_hist(1);
+      return 0;
+   }
+   if (maxits + 2 > KScratch::kScal) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPSolverLanczos: maxits %d above %d\n", maxits, KScratch::kScal - 2);
+      return -1;
+   }
+   double *V = nullptr, *Z = nullptr;
+   if (dmalloc(&V, n * (size_t)(maxits + 1)) || dmalloc(&Z, n * (size_t)(maxits + 1))) return -1;
+   auto cleanup = [&]() {
+      (void)hipStreamSynchronize(c.s);
+      (void)hipFree(V);
+      (void)hipFree(Z);
+   };
+   std::vector<double> TLD(maxits + 1, 0.0), TLE(maxits + 1, 0.0), y(maxits + 1, 0.0);
+   double* TD = *TDp ? *TDp : (double*)calloc((size_t)maxits + 1, sizeof(double));
+   double* TE = *TEp ? *TEp : (double*)calloc((size_t)std::max(1, maxits), sizeof(double));
+   double* z = Z;
+   double* v = V;
+   c.copy(z, rhs);
+   if (cb.apply(-1.0, x, 1.0, z)) {
+      cleanup();
+      return -1;
+   }
+   if (cb.prec) {
+      if (cb.solve(v, z)) {
+         cleanup();
+         return -1;
+      }
+   } else {
+      c.copy(v, z);
+   }
+   double normr = c.norm(z);
+   const double beta = std::sqrt(c.dot(v, z));
+   if (beta < EPS) {
+      *prel_res = 0.0;
+      *piter = 0;
+      *prel_res_v = rel_hist(1);
+      if (!*TDp) free(TD);
+      if (!*TEp) free(TE);
+      cleanup();
+      return 0;
+   }
+   const double tolr = atol ? tol / beta : tol;
+   double* rel = rel_hist(maxits + 1);
+   rel[0] = normr / normb;
+   int iter = 0, chol_size = 0;
+   double ls = 0.0, t = 0.0, dotvz = 0.0;
+   if (print_level > 0) {
+      printf("--------------------------------------------------------------------------------\n");
+      printf("Start Lanczos(%d)\n", maxits);
+      printf("Residual Tol: %e\nMax number of inner iterations: %d\n", tolr, maxits);
+      printf("--------------------------------------------------------------------------------\n");
+      printf("Step    Residual norm  Relative res.  Convergence Rate\n");
+      printf("%5d   %8e   %8e   N/A\n", 0, normr, rel[0]);
+   }
+   c.scale(v, z, 1.0 / beta);
+   auto step = [&](bool first_loop) -> int {
+      iter++;
+      z = Z + (size_t)iter * n;
+      double* wv = V + (size_t)(iter - 1) * n;
+      v = V + (size_t)iter * n;
+      if (cb.apply(1.0, wv, 0.0, z)) return -1;
+      const int k = first_loop ? std::min(iter - 1, wsize) : iter - 1;
+      double te_dummy;
+      if (mgs2(c, z, V, Z, k, TD + iter - 1, iter >= 2 ? TE + iter - 2 : &te_dummy, &t)) return -1;
+      if (t < EPS) return 1;
+      if (cb.prec) {
+         if (cb.solve(v, z)) return -1;
+      } else {
+         c.copy(v, z);
+      }
+      double* o = g_k.scal + KScratch::kScal - 2;
+      hipLaunchKernelGGL(k_dot2, dim3(kgrid(n)), dim3(kKThreads), 0, c.s, v, z, n, g_k.part, g_k.ticket, g_k.part2,
+                         g_k.ticket2, o);
+      double vz[2];
+      if (c.read(o, 2, vz)) return -1;
+      dotvz = std::sqrt(vz[0]);
+      if (dotvz < EPS) return 1;
+      c.scale(v, z, 1.0 / dotvz);
+      if (first_loop) {
+         const double normz = std::sqrt(vz[1]) / dotvz;
+         if (iter != 1) {
+            TLE[iter - 2] = TE[iter - 2] / TLD[iter - 2];
+            TLD[iter - 1] = std::sqrt(TD[iter - 1] - TLE[iter - 2] * TLE[iter - 2]);
+            const double le = 1.0 / TLD[iter - 1];
+            ls = -ls * TLE[iter - 2] * le;
+            normr = std::fabs(le * ls) * dotvz * beta * normz;
+         } else {
+            TLD[0] = std::sqrt(TD[0]);
+            ls = 1.0 / TLD[0];
+            normr = dotvz / TD[0] * beta * normz;
+         }
+         chol_size++;
+         rel[iter] = normr / normb;
+         if (print_level > 0)
+            printf("%5d   %8e   %8e   %8.6f\n", iter, normr, rel[iter], rel[iter] / rel[iter - 1]);
+         if (normr <= tolr) return 1;
+      } else if (print_level > 0) {
+         printf("%5d   Building T\n", iter);
+      }
+      return 0;
+   };
+   while (iter < maxits) {
+      const int r = step(true);
+      if (r < 0) {
+         free(rel);
+         cleanup();
+         return -1;
+      }
+      if (r) break;
+   }
+   if (print_level == 0)
+      printf("Rel. residual at the end of the iteration (# of its: %d): %e \n", iter, rel[iter]);
+   // solution from the Cholesky factor of T (lanczos.c:258-273)
+   if (chol_size > 0) {
+      y[0] = beta / TLD[0];
+      for (int k = 1; k < chol_size; k++) y[k] = (-y[k - 1] * TLE[k - 1]) / TLD[k];
+      y[chol_size - 1] /= TLD[chol_size - 1];
+      for (int k = chol_size - 2; k >= 0; k--) y[k] = (y[k] - TLE[k] * y[k + 1]) / TLD[k];
+      if (c.combine(x, V, chol_size, y.data())) return -1;
+   }
+   *prel_res = normr / normb;
+   *piter = iter;
+   *prel_res_v = rel;
+   // second loop: complete T up to wsize, restarting from a random vector after a breakdown
+   while (iter < wsize) {
+      if (t < EPS || dotvz < EPS) {
+         z = Z + (size_t)iter * n;
+         v = V + (size_t)iter * n;
+         std::vector<double> rnd(n);
+         for (size_t i = 0; i < n; i++) rnd[i] = (double)rand() / (double)RAND_MAX;  // Nfft4GPVecRand
+         NFFT4GP_HIP_CHECK(hipMemcpy(z, rnd.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+         double td, te;
+         if (mgs2(c, z, V, Z, iter - 1, &td, &te, &t)) return -1;
+         if (t < EPS) break;
+         if (cb.prec) {
+            if (cb.solve(v, z)) return -1;
+         } else {
+            c.copy(v, z);
+         }
+         dotvz = std::sqrt(c.dot(v, z));
+         if (dotvz < EPS) break;
+         c.scale(v, z, 1.0 / dotvz);
+      }
+      while (iter < wsize) {
+         const int r = step(false);
+         if (r < 0) return -1;
+         if (r) break;
+      }
+   }
+   *tsize = iter;
+   if (!*TDp) *TDp = TD;
+   if (!*TEp) *TEp = TE;
+   cleanup();
+   return 0;
+}
+
+
+// ---- stochastic Lanczos quadrature (lanczos.c:421-610) --------------------------------------------
+int lanczos_logdet_dev(Callbacks& cb, Callbacks& dcb, func_trace tracefunc, func_logdet logdetfunc,
+                       func_dvp dvpfunc, int maxits, int nvecs, const double* radamacher, int print_level,
+                       double* logdet, double** dlogdetp)
+{
+   const size_t n = cb.n;
+   Ctx c{current_stream(), n};
+   void* prec_data = cb.prec ? cb.pdata : nullptr;
+   double* dval = *dlogdetp ? *dlogdetp : (double*)calloc(3, sizeof(double));
+   double traces_precond[3] = {0.0, 0.0, 0.0}, logdet_precond = 0.0;
+   if (prec_data) {
+      double* tp = traces_precond;
+      if (tracefunc(prec_data, &tp)) return -1;
+      for (int i = 0; i < 3; i++) traces_precond[i] /= (double)n;
+      logdet_precond = logdetfunc(prec_data) / (double)n;
+   }
+   const bool dvp_dev = g_cb_mode == 1 || (g_cb_mode == -1 && library_operator((const void*)dvpfunc));
+   double *z = nullptr, *x = nullptr, *dAz = nullptr, *px = nullptr;
+   std::vector<double> hz, hpx;
+   if (dmalloc(&z, n) || dmalloc(&x, n) || dmalloc(&dAz, 3 * n) || dmalloc(&px, 3 * n)) return -1;
+   auto cleanup = [&]() {
+      (void)hipStreamSynchronize(c.s);
+      for (double* p : {z, x, dAz, px}) (void)hipFree(p);
+   };
+   const bool rad_dev = radamacher && is_device_ptr(radamacher);
+   double val = 0.0;
+   for (int j = 0; j < 3; j++) dval[j] = 0.0;
+   for (int i = 0; i < nvecs; i++) {
+      if (radamacher) {
+         NFFT4GP_HIP_CHECK(hipMemcpyAsync(z, radamacher + (size_t)i * n, sizeof(double) * n,
+                                          rad_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c.s));
+      } else {
+         hz.resize(n);
+         Nfft4GPVecRadamacher(hz.data(), (int)n);
+         NFFT4GP_HIP_CHECK(hipMemcpyAsync(z, hz.data(), sizeof(double) * n, hipMemcpyHostToDevice, c.s));
+      }
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(x, 0, sizeof(double) * n, c.s));
+      if (dcb.apply(1.0, z, 0.0, dAz)) {
+         cleanup();
+         return -1;
+      }
+      double rel_res, *rel_res_v = nullptr, *TD = nullptr, *TE = nullptr;
+      int niter = 0, tsize = 0;
+      if (lanczos_dev(cb, x, z, maxits, maxits, 0, DBL_EPSILON, &rel_res, &rel_res_v, &niter, &tsize, &TD, &TE,
+                      print_level)) {
+         cleanup();
+         return -1;
+      }
+      free(rel_res_v);
+      while (tsize > 0 && std::isnan(TD[tsize - 1])) tsize--;
+      if (tsize == 0) {
+         printf("Warning: empty tridiagonal matrix\n");  // lanczos.c:525-529 returns without a result
+         free(TD);
+         free(TE);
+         cleanup();
+         return 0;
+      }
+      std::vector<double> w, TV;
+      if (tridiag_eig(tsize, TD, TE, w, TV)) {
+         printf("Warning: DSTEV failed at iteration %d/%d\n", i, nvecs);
+         free(TD);
+         free(TE);
+         cleanup();
+         return -1;
+      }
+      // sum_j TV(0, j)^2 log|lambda_j|  (TV column-major, eigenvector j in column j)
+      for (int j = 0; j < tsize; j++) val += TV[(size_t)j * tsize] * TV[(size_t)j * tsize] * std::log(std::fabs(w[j]));
+      if (prec_data) {
+         if (dvp_dev) {
+            double* pp = px;
+            if (dvpfunc(prec_data, (int)n, nullptr, z, &pp)) {
+               cleanup();
+               return -1;
+            }
+         } else {
+            hz.resize(n);
+            hpx.assign(3 * n, 0.0);
+            NFFT4GP_HIP_CHECK(hipMemcpy(hz.data(), z, sizeof(double) * n, hipMemcpyDeviceToHost));
+            double* pp = hpx.data();
+            if (dvpfunc(prec_data, (int)n, nullptr, hz.data(), &pp)) {
+               cleanup();
+               return -1;
+            }
+            NFFT4GP_HIP_CHECK(hipMemcpy(px, hpx.data(), sizeof(double) * 3 * n, hipMemcpyHostToDevice));
+         }
+      }
+      for (int j = 0; j < 3; j++) {
+         dval[j] += c.dot(dAz + (size_t)j * n, x);
+         if (prec_data) dval[j] -= c.dot(px + (size_t)j * n, z);
+      }
+      free(TD);
+      free(TE);
+   }
+   cleanup();
+   double scale = 1.0 / (double)nvecs;
+   val *= scale;
+   scale /= (double)n;
+   for (int j = 0; j < 3; j++) dval[j] *= scale;
+   val += logdet_precond;
+   for (int j = 0; j < 3; j++) dval[j] += traces_precond[j];
+   *logdet = val;
+   if (!*dlogdetp) *dlogdetp = dval;
+   return 0;
+}
+
+}  // namespace nfft4gp_amd
+
+// ---------------------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------------------
+namespace {
+
+bool make_callbacks(Callbacks& cb, int n, func_symmatvec matvec, void* mat, func_solve prec, void* pdata)
+{
+   cb.matvec = matvec;
+   cb.mat = mat;
+   cb.prec = pdata ? prec : nullptr;  // the reference tests prec_data, not the function (fgmres.c:148)
+   cb.pdata = pdata;
+   cb.n = (size_t)n;
+   cb.mv_dev = g_cb_mode == 1 || (g_cb_mode == -1 && library_operator((const void*)matvec));
+   cb.pc_dev = g_cb_mode == 1 || (g_cb_mode == -1 && library_operator((const void*)prec));
+   return g_k.ensure() == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int Nfft4GPSolverFgmres(void* mat_data, int n, func_symmatvec matvec, void* prec_data, func_solve precondfunc,
+                        double* x, double* rhs, int kdim, int maxits, int atol, double tol, double* prel_res,
+                        double** prel_res_v, int* piter, int print_level)
+{
+   if (!need_device("Nfft4GPSolverFgmres")) return -1;
+   Callbacks cb;
+   if (!make_callbacks(cb, n, matvec, mat_data, precondfunc, prec_data)) return -1;
+   Vec vx, vb;
+   if (vx.open(x, n, true) || vb.open(rhs, n, true)) return -1;
+   const int rc = fgmres_dev(cb, vx.d, vb.d, kdim, maxits, atol, tol, prel_res, prel_res_v, piter, print_level);
+   vb.close(false);
+   vx.close(rc == 0);
+   return rc;
+}
+
+int Nfft4GPSolverLanczos(void* mat_data, int n, func_symmatvec matvec, void* prec_data, func_solve precondfunc,
+                         double* x, double* rhs, int wsize, int maxits, int atol, double tol, double* prel_res,
+                         double** prel_res_v, int* piter, int* tsize, double** TDp, double** TEp, int print_level)
+{
+   if (!need_device("Nfft4GPSolverLanczos")) return -1;
+   Callbacks cb;
+   if (!make_callbacks(cb, n, matvec, mat_data, precondfunc, prec_data)) return -1;
+   Vec vx, vb;
+   if (vx.open(x, n, true) || vb.open(rhs, n, true)) return -1;
+   const int rc = lanczos_dev(cb, vx.d, vb.d, wsize, maxits, atol, tol, prel_res, prel_res_v, piter, tsize, TDp, TEp,
+                              print_level);
+   vb.close(false);
+   vx.close(rc == 0);
+   return rc;
+}
+
+int Nfft4GPLanczosQuadratureLogdet(void* mat_data, void* dmat_data, int n, func_symmatvec matvec,
+                                   func_symmatvec dmatvec, void* prec_data, func_solve precondfunc,
+                                   func_trace tracefunc, func_logdet logdetfunc, func_dvp dvpfunc, int maxits,
+                                   int nvecs, double* radamacher, int print_level, double* logdet, double** dlogdetp)
+{
+   if (!need_device("Nfft4GPLanczosQuadratureLogdet")) return -1;
+   Callbacks cb, dcb;
+   if (!make_callbacks(cb, n, matvec, mat_data, precondfunc, prec_data) ||
+       !make_callbacks(dcb, n, dmatvec, dmat_data, nullptr, nullptr))
+      return -1;
+   dcb.out_mult = 3;
+   return lanczos_logdet_dev(cb, dcb, tracefunc, logdetfunc, dvpfunc, maxits, nvecs, radamacher, print_level, logdet,
+                             dlogdetp);
+}
+
+int Nfft4GPTransform(nfft4gp_transform_type type, double val, int inverse, double* tvalp, double* dtvalp)
+{
+   switch (type) {
+   case 1:  // NFFT4GP_TRANSFORM_SIGMOID
+      if (!inverse) {
+         *tvalp = 1.0 / (exp(-val) + 1.0);
+         *dtvalp = *tvalp * (1 - *tvalp);
+      } else {
+         *tvalp = log(val / (1.0 - val));
+      }
+      break;
+   case 0:  // NFFT4GP_TRANSFORM_SOFTPLUS
+      if (!inverse) {
+         if (val > 20.0) {
+            *tvalp = val;
+            *dtvalp = 1.0;
+         } else if (val < -20.0) {
+            *tvalp = exp(val);
+            *dtvalp = exp(val);
+         } else {
+            *tvalp = log(1.0 + exp(val));
+            *dtvalp = exp(val) / (1.0 + exp(val));
+         }
+      } else {
+         if (val > 20.0)
+            *tvalp = val;
+         else if (val < 2.06115362243856e-09)
+            *tvalp = log(val);
+         else
+            *tvalp = log(exp(val) - 1.0);
+      }
+      break;
+   case 2:  // NFFT4GP_TRANSFORM_EXP
+      if (!inverse) {
+         *tvalp = exp(val);
+         *dtvalp = exp(val);
+      } else {
+         *tvalp = log(val);
+      }
+      break;
+   case 3:  // NFFT4GP_TRANSFORM_IDENTITY
+      *tvalp = val;
+      if (!inverse) *dtvalp = 1.0;
+      break;
+   default:
+      printf("Error: unknown transform type.\n");
+      return -1;
+   }
+   return 0;
+}
+
+int Nfft4GPGpLoss(double* x, double* data, double* label, int n, int ldim, int d, func_kernel fkernel,
+                  void* vfkernel_data, func_free kernel_data_free, func_symmatvec matvec, func_symmatvec dmatvec,
+                  func_kernel precond_fkernel, void* precond_vfkernel_data, func_free precond_vfkernel_data_free,
+                  precond_kernel_setup precond_setup, func_solve precond_solve, func_trace precond_trace,
+                  func_logdet precond_logdet, func_dvp precond_dvp, func_free precond_reset, void* precond_data,
+                  int atol, double tol, int wsize, int maxits, int nvecs, double* radamacher,
+                  nfft4gp_transform_type transform,
+                  int* mask, int print_level, double* dwork, double* loss, double* grad)
+{
+   (void)precond_vfkernel_data_free;
+   (void)wsize;
+   if (!need_device("Nfft4GPGpLoss")) return -1;
+   double tvals[3], dtvals[3];
+   for (int i = 0; i < 3; i++)
+      if (Nfft4GPTransform(transform, x[i], 0, tvals + i, dtvals + i)) return -1;
+   printf("Transform %e %e %e into %e %e %e with grad %e %e %e\n", x[0], x[1], x[2], tvals[0], tvals[1], tvals[2],
+          dtvals[0], dtvals[1], dtvals[2]);
+   nfft4gp_kernel* kd = (nfft4gp_kernel*)vfkernel_data;
+   nfft4gp_kernel* pkd = (nfft4gp_kernel*)precond_vfkernel_data;
+   kd->_params[0] = tvals[0];
+   kd->_params[1] = tvals[1];
+   kd->_noise_level = tvals[2];
+   if (pkd) {
+      pkd->_params[0] = tvals[0];
+      pkd->_params[1] = tvals[1];
+      pkd->_noise_level = tvals[2];
+   }
+   double* kernel_mat = nullptr;
+   double* dkernel_mat = nullptr;
+   if (dwork) {
+      kernel_mat = dwork;
+      dkernel_mat = dwork + (size_t)n * n;
+   }
+   if (fkernel(vfkernel_data, data, n, ldim, d, nullptr, 0, nullptr, 0, &kernel_mat, &dkernel_mat)) return -1;
+   if (precond_setup)
+      precond_setup(data, n, ldim, d, precond_fkernel, precond_vfkernel_data, 1, precond_data);
+   else
+      precond_data = nullptr;
+
+   Callbacks cb, dcb;
+   if (!make_callbacks(cb, n, matvec, kernel_mat, precond_solve, precond_data) ||
+       !make_callbacks(dcb, n, dmatvec, dkernel_mat, nullptr, nullptr))
+      return -1;
+   dcb.out_mult = 3;
+   hipStream_t s = current_stream();
+   Ctx c{s, (size_t)n};
+   double *iKY = nullptr, *dKiKY = nullptr;
+   Vec vl;
+   if (dmalloc(&iKY, (size_t)n) || dmalloc(&dKiKY, 3 * (size_t)n) || vl.open(label, n, true)) return -1;
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(iKY, 0, sizeof(double) * n, s));
+   const int solve_kdim = std::min(n, maxits * 2), solve_maxits = std::min(n, maxits * 2);
+   double rel_res, *rel_res_v = nullptr;
+   int niter = 0;
+   if (fgmres_dev(cb, iKY, vl.d, solve_kdim, solve_maxits, atol, tol, &rel_res, &rel_res_v, &niter, print_level))
+      return -1;
+   if (rel_res > 1e10) {
+      printf("Warning: FGMRES unstable, rel_res = %f\n", rel_res);
+      printf("Current parameters (after transform): f = %f, l = %f, mu = %f\n", tvals[0], tvals[1], tvals[2]);
+   }
+   free(rel_res_v);
+   const double L1 = c.dot(vl.d, iKY) / (double)n;
+   if (dcb.apply(1.0, iKY, 0.0, dKiKY)) return -1;
+   double L1_grad[3];
+   for (int i = 0; i < 3; i++) L1_grad[i] = c.dot(dKiKY + (size_t)i * n, iKY) / (double)n * dtvals[i];
+   double L2 = 0.0, *L2_grad = nullptr;
+   const int qits = std::min(n, maxits);
+   const int err = lanczos_logdet_dev(cb, dcb, precond_trace, precond_logdet, precond_dvp, qits, nvecs, radamacher,
+                                      print_level, &L2, &L2_grad);
+   (void)hipStreamSynchronize(s);
+   (void)hipFree(iKY);
+   (void)hipFree(dKiKY);
+   vl.close(false);
+   if (err != 0) {
+      printf("Error in Nfft4GPLanczosQuadratureLogdet\n");
+      return err;
+   }
+   loss[0] = 0.5 * (L1 + L2 + log(2.0 * 3.1415926535897932384626));
+   for (int i = 0; i < 3; i++) {
+      const double g = L2_grad ? 0.5 * (-L1_grad[i] + L2_grad[i] * dtvals[i]) : 0.0;
+      grad[i] = (mask && !mask[i]) ? 0.0 : g;
+   }
+   free(L2_grad);
+   if (!dwork && kernel_data_free) {
+      kernel_data_free(kernel_mat);
+      kernel_data_free(dkernel_mat);
+   }
+   if (precond_data && precond_reset) precond_reset(precond_data);
+   return 0;
+}
+
+}  // extern "C"

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "internal.h"
+#include "callbacks.hpp"
 #include "reduce.hpp"
 
 using namespace nfft4gp_amd;
@@ -293,46 +294,6 @@ int elem_grid(size_t n)
    return (int)(g == 0 ? 1 : g);
 }
 
-// host-or-device view of a vector: host pointers are staged through device memory
-struct Vec {
-   double* d = nullptr;
-   double* h = nullptr;
-   size_t n = 0;
-   bool staged = false;
-   int open(double* p, size_t nn, bool copy_in)
-   {
-      n = nn;
-      if (is_device_ptr(p)) {
-         d = p;
-         return 0;
-      }
-      h = p;
-      staged = true;
-      NFFT4GP_HIP_CHECK(hipMalloc((void**)&d, sizeof(double) * (n ? n : 1)));
-      if (copy_in && n) NFFT4GP_HIP_CHECK(hipMemcpy(d, h, sizeof(double) * n, hipMemcpyHostToDevice));
-      return 0;
-   }
-   int close(bool copy_out)
-   {
-      if (staged) {
-         hipStream_t s = current_stream();
-         NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
-         if (copy_out && n) NFFT4GP_HIP_CHECK(hipMemcpy(h, d, sizeof(double) * n, hipMemcpyDeviceToHost));
-         NFFT4GP_HIP_CHECK(hipFree(d));
-         d = nullptr;
-      }
-      return 0;
-   }
-};
-
-bool need_device(const char* who)
-{
-   if (!device_ok()) {
-      fprintf(stderr, "nfft4gp_amd: %s: no HIP device visible (no CPU fallback).\n", who);
-      return false;
-   }
-   return true;
-}
 
 // ---------------------------------------------------------------------------------------------
 // Nystrom apply kernels
@@ -418,62 +379,6 @@ struct PcgScratch {
 };
 PcgScratch g_pcg;
 
-// ---- operator / preconditioner callbacks of Nfft4GPSolverPcg ----------------------------------
-// The library's own operators take device pointers.  Any other callback (e.g. the reference's
-// Nfft4GPDenseMatSymv on a host matrix) is called the reference's way, with HOST vectors: the
-// adapter stages its input and output through pinned host buffers around the call.  Mode -1 (auto)
-// decides per function pointer; 0 forces host staging, 1 forces device pointers.
-int g_cb_mode = -1;
-
-struct Callbacks {
-   func_symmatvec matvec;
-   void* mat;
-   func_solve prec;
-   void* pdata;
-   bool mv_dev, pc_dev;
-   size_t n;
-   double *h_in = nullptr, *h_out = nullptr;
-   int ensure_host()
-   {
-      if (!h_in) {
-         NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&h_in, sizeof(double) * (n ? n : 1)));
-         NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&h_out, sizeof(double) * (n ? n : 1)));
-      }
-      return 0;
-   }
-   ~Callbacks()
-   {
-      if (h_in) (void)hipHostFree(h_in);
-      if (h_out) (void)hipHostFree(h_out);
-   }
-   // y = alpha A x + beta y on device vectors
-   int apply(double alpha, double* dx, double beta, double* dy)
-   {
-      if (mv_dev) return matvec(mat, (int)n, alpha, dx, beta, dy);
-      if (ensure_host()) return -1;
-      hipStream_t s = current_stream();
-      NFFT4GP_HIP_CHECK(hipMemcpyAsync(h_in, dx, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-      if (beta != 0.0) NFFT4GP_HIP_CHECK(hipMemcpyAsync(h_out, dy, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-      NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
-      if (matvec(mat, (int)n, alpha, h_in, beta, h_out)) return -1;
-      NFFT4GP_HIP_CHECK(hipMemcpyAsync(dy, h_out, sizeof(double) * n, hipMemcpyHostToDevice, s));
-      return 0;
-   }
-   // z = M^{-1} r on device vectors
-   int solve(double* dz, double* dr)
-   {
-      if (pc_dev) return prec(pdata, (int)n, dz, dr);
-      if (ensure_host()) return -1;
-      hipStream_t s = current_stream();
-      NFFT4GP_HIP_CHECK(hipMemcpyAsync(h_in, dr, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-      NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
-      if (prec(pdata, (int)n, h_out, h_in)) return -1;
-      NFFT4GP_HIP_CHECK(hipMemcpyAsync(dz, h_out, sizeof(double) * n, hipMemcpyHostToDevice, s));
-      return 0;
-   }
-};
-
-bool library_operator(const void* fn);
 
 int g_last_hist_len = 0;
 
@@ -508,6 +413,24 @@ void Nfft4GPVecFill(double* x, size_t n, double val)
    hipLaunchKernelGGL(k_fill, dim3(elem_grid(n)), dim3(256), 0, current_stream(), v.d, n, val);
    v.close(true);
 }
+
+// vecops.c:15-46: serial libc rand() (the reference's sequence for a given srand seed); device vectors
+// get the same host-generated values
+static void vec_random(double* x, int n, bool rademacher)
+{
+   std::vector<double> h(std::max(0, n));
+   for (int i = 0; i < n; i++) {
+      h[i] = (double)rand() / (double)RAND_MAX;
+      if (rademacher) h[i] = h[i] < 0.5 ? -1.0 : 1.0;
+   }
+   if (n > 0 && is_device_ptr(x))
+      (void)hipMemcpy(x, h.data(), sizeof(double) * n, hipMemcpyHostToDevice);
+   else if (n > 0)
+      memcpy(x, h.data(), sizeof(double) * n);
+}
+
+void Nfft4GPVecRand(double* x, int n) { vec_random(x, n, false); }
+void Nfft4GPVecRadamacher(double* x, int n) { vec_random(x, n, true); }
 
 void Nfft4GPVecScale(double* x, size_t n, double scale)
 {
@@ -840,13 +763,15 @@ void Nfft4GPAmdNysFree(void* nys)
 
 }  // extern "C"
 
-namespace {
+namespace nfft4gp_amd {
+int g_cb_mode = -1;
 bool library_operator(const void* fn)
 {
    return fn == (const void*)&Nfft4GPAdditiveNFFTMatSymv || fn == (const void*)&Nfft4GPNFFTMatSymv ||
+          fn == (const void*)&Nfft4GPAdditiveNFFTGradMatSymv || fn == (const void*)&Nfft4GPNFFTGradMatSymv ||
           fn == (const void*)&Nfft4GPAmdNysSolve || fn == (const void*)&Nfft4GPAmdFsaiSolve ||
           fn == (const void*)&Nfft4GPAmdAfnSolve;
 }
-}  // namespace
+}  // namespace nfft4gp_amd
 
 extern "C" void Nfft4GPAmdSetCallbackPointerMode(int mode) { g_cb_mode = (mode < -1 || mode > 1) ? -1 : mode; }

@@ -201,6 +201,10 @@ class NFFTAdditiveKernel:
     def matvec_fnptr(self) -> int:
         return _lib.fnptr("Nfft4GPAdditiveNFFTMatSymv")
 
+    @property
+    def gradmatvec_fnptr(self) -> int:
+        return _lib.fnptr("Nfft4GPAdditiveNFFTGradMatSymv")
+
     def free(self):
         if getattr(self, "h", None):
             _lib.lib().Nfft4GPAdditiveNFFTKernelFree(self.h)

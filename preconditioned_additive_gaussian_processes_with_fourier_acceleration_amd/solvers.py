@@ -7,6 +7,8 @@
                 perm produced by the reference's Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660).
 ``FsaiPrecond`` Nfft4GPAmdFsai* -- the apply of SRC/preconds/fsai.c:106-123 on the reference's CSR factor.
 ``AfnPrecond``  Nfft4GPAmdAfn* -- the apply of SRC/preconds/afn.c:82-143.
+``fgmres``      Nfft4GPSolverFgmres (SRC/solvers/fgmres.c:3-252).
+``logdet``      Nfft4GPLanczosQuadratureLogdet (SRC/solvers/lanczos.c:421-610), no preconditioner.
 """
 from __future__ import annotations
 
@@ -182,3 +184,41 @@ def pcg(op, b, x=None, maxits=1000, tol=1e-6, atol=False, precond=None, print_le
     hist = np.ctypeslib.as_array(relv, shape=(length,)).copy()
     C.CDLL(None).free(relv)
     return x, rel.value, hist, it.value
+
+
+def fgmres(op, b, x=None, kdim=50, maxits=1000, tol=1e-6, atol=False, precond=None, print_level=-1):
+    """Nfft4GPSolverFgmres(op, n, matvec, precond, precondfunc, x, b, kdim, maxits, atol, tol, ...).
+    Returns (x, rel_res, rel_res_v, iters)."""
+    if x is None:
+        x = b * 0
+    n = op.n
+    rel = C.c_double()
+    relv = _lib.dp()
+    it = C.c_int()
+    L = _lib.lib()
+    rc = L.Nfft4GPSolverFgmres(op.h, n, op.matvec_fnptr, precond.h if precond else None,
+                               precond.solve_fnptr if precond else None, _ptr(x)[0], _ptr(b)[0], int(kdim),
+                               int(maxits), int(bool(atol)), float(tol), C.byref(rel), C.byref(relv), C.byref(it),
+                               int(print_level))
+    if rc:
+        raise RuntimeError("Nfft4GPSolverFgmres failed")
+    hist = np.ctypeslib.as_array(relv, shape=(int(maxits) + 1,)).copy()
+    C.CDLL(None).free(relv)
+    return x, rel.value, hist, it.value
+
+
+def logdet(op, maxits, nvecs, rademacher=None, print_level=-1):
+    """Stochastic Lanczos quadrature of logdet(K)/n and its gradient (Nfft4GPLanczosQuadratureLogdet,
+    lanczos.c:421-610) for an operator with ``matvec_fnptr`` and ``gradmatvec_fnptr``."""
+    val = C.c_double()
+    dval = _lib.dp()
+    R = None if rademacher is None else np.asfortranarray(np.asarray(rademacher, dtype=np.float64))
+    rc = _lib.lib().Nfft4GPLanczosQuadratureLogdet(op.h, op.h, op.n, op.matvec_fnptr, op.gradmatvec_fnptr, None,
+                                                   None, None, None, None, int(maxits), int(nvecs),
+                                                   R.ctypes.data if R is not None else None, int(print_level),
+                                                   C.byref(val), C.byref(dval))
+    if rc:
+        raise RuntimeError("Nfft4GPLanczosQuadratureLogdet failed")
+    g = np.ctypeslib.as_array(dval, shape=(3,)).copy()
+    C.CDLL(None).free(dval)
+    return val.value, g

@@ -22,8 +22,9 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
-from oracle import (OracleAdditiveNFFT, RefDenseAdditive, RefFsai, RefNystrom, afn_apply,  # noqa: E402
-                    ref_available, ref_gaussian_matrix, ref_gaussian_params, ref_pcg, ref_schur_params)
+from oracle import (OracleAdditiveNFFT, RefDenseAdditive, RefFsai, RefGpLoss, RefNystrom, afn_apply,  # noqa: E402
+                    ref_available, ref_fgmres, ref_gaussian_matrix, ref_gaussian_params, ref_gp_loss_nfft,
+                    ref_logdet_quadrature, ref_pcg, ref_schur_params)
 from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.data import (  # noqa: E402
     read_features, read_labels, read_windows)
 
@@ -107,11 +108,60 @@ def make_precond_synth():
          pcgafn_x=xa, pcgafn_relres=rela, pcgafn_hist=hista, pcgafn_iters=ita)
 
 
+def make_krylov_synth():
+    """(6) the reference's FGMRES (fgmres.c), Lanczos quadrature (lanczos.c:421-610) and GP loss
+    (gp_loss.c:96-307) on pcg_synth's dense additive operator (4 x 1-D windows, n = 1500), with fixed
+    Rademacher probes; FGMRES also with restarts and with the Nystrom preconditioner of pcg_synth."""
+    z = np.load(os.path.join(HERE, "pcg_synth.npz"), allow_pickle=False)
+    X, win, nw, dw = np.asarray(z["X"]), np.asarray(z["windows"]), int(z["nw"]), int(z["dw"])
+    n = X.shape[0]
+    b = np.asarray(z["b"])
+    f, l, mu = 1.0, 0.1, 0.01
+    r = RefDenseAdditive(X, win, nw, dw, kernel=0)
+    r.matrices(f, l, mu, grad=True)
+
+    def mv(alpha, xv, beta, yv):
+        yv[:] = r.matsymv(xv, alpha, beta, yv.copy())
+
+    def dmv(alpha, xv, beta, yv):
+        yv[:] = r.gradmatsymv(xv, alpha, beta, yv.copy())
+
+    out = {}
+    xg, relg, histg, itg = ref_fgmres(mv, n, b, 100, 400, 1e-8)
+    out.update(fg_x=xg, fg_relres=relg, fg_hist=histg, fg_iters=itg)
+    xr, relr, histr, itr = ref_fgmres(mv, n, b, 10, 60, 1e-8)  # restarts every 10 steps, stops at maxits
+    out.update(fgr_x=xr, fgr_relres=relr, fgr_hist=histr, fgr_iters=itr)
+    nys = RefNystrom(r, f, l, mu, int(z["nys_k"]), np.asarray(z["nys_perm"]))
+
+    def pc(xo, rhs):
+        nys.solve(xo, rhs.copy())
+
+    xn, reln, histn, itn = ref_fgmres(mv, n, b, 100, 400, 1e-8, precond_py=pc)
+    out.update(fgn_x=xn, fgn_relres=reln, fgn_hist=histn, fgn_iters=itn)
+    rng = np.random.default_rng(31)
+    nvecs, maxits = 4, 20
+    R = np.where(rng.random((n, nvecs)) < 0.5, -1, 1).astype(np.int8)
+    ld, dld = ref_logdet_quadrature(mv, dmv, n, maxits, nvecs, R.astype(np.float64))
+    out.update(ld_val=ld, ld_grad=dld)
+    hyper = np.array([0.5, -1.0, -3.0])
+    g0 = RefGpLoss(X, win, nw, dw)
+    loss0, grad0 = g0.reference(hyper, b, maxits, nvecs, R.astype(np.float64))
+    g8 = RefGpLoss(X, win, nw, dw, k=8, perm=np.asarray(z["nys_perm"]))
+    loss8, grad8 = g8.reference(hyper, b, maxits, nvecs, R.astype(np.float64))
+    # the reference's loss code on the NFFT operator (the oracle's restatement of nfft_interface.c)
+    lossn, gradn = ref_gp_loss_nfft(X, win, nw, dw, b, hyper, maxits, nvecs, R.astype(np.float64))
+    print(f"krylov_synth: fgmres its {itg}/{itr}/{itn}, logdet {ld}, loss {loss0} / nys8 {loss8} / nfft {lossn}")
+    save("krylov_synth", f=f, l=l, mu=mu, rademacher=R, nvecs=nvecs, maxits=maxits, hyper=hyper,
+         loss=loss0, grad=grad0, loss_nys8=loss8, grad_nys8=grad8, loss_nfft=lossn, grad_nfft=gradn, **out)
+
+
 def main():
     if not ref_available():
         raise SystemExit("build oracle/_ref first: make -C oracle ref")
     if sys.argv[1:] == ["precond"]:
         return make_precond_synth()
+    if sys.argv[1:] == ["krylov"]:
+        return make_krylov_synth()
     f, mu = 1.3, 0.01
 
     # (1) TEST2's 1-D dataset, one window {0} (TESTS/TEST2/data/foo.window)
@@ -180,6 +230,7 @@ def main():
          pcgnys_x=xq, pcgnys_relres=relq, pcgnys_hist=histq, pcgnys_iters=itq)
 
     make_precond_synth()
+    make_krylov_synth()
 
 
 if __name__ == "__main__":

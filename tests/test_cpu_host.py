@@ -187,3 +187,73 @@ def test_host_eigensolver_and_cholesky_inverse():
     # not positive definite: the failing column is reported
     A = np.asfortranarray(np.diag([1.0, -1.0, 2.0]))
     assert L.Nfft4GPAmdHostCholInverse(A.ctypes.data, 3, 0.0, np.zeros(9).ctypes.data) == 2
+
+
+def test_transform_matches_reference_formulas():
+    """Nfft4GPTransform (transform.c:4-89): softplus (with the +-20 thresholds), sigmoid, exp, identity,
+    forward with derivative and inverse (host code, no device needed)."""
+    L = amd.lib()
+    t, dt = C.c_double(), C.c_double()
+    for v in (-25.0, -3.0, 0.0, 0.7, 19.0, 25.0):
+        assert L.Nfft4GPTransform(0, v, 0, C.byref(t), C.byref(dt)) == 0
+        if v > 20:
+            exp_t, exp_dt = v, 1.0
+        elif v < -20:
+            exp_t, exp_dt = np.exp(v), np.exp(v)
+        else:
+            exp_t, exp_dt = np.log1p(np.exp(v)), np.exp(v) / (1 + np.exp(v))
+        assert t.value == pytest.approx(exp_t, rel=1e-15) and dt.value == pytest.approx(exp_dt, rel=1e-15)
+        assert L.Nfft4GPTransform(0, t.value, 1, C.byref(t), None) == 0
+        if -20 <= v <= 20:
+            assert t.value == pytest.approx(v, rel=1e-9, abs=1e-9)
+    assert L.Nfft4GPTransform(1, 0.3, 0, C.byref(t), C.byref(dt)) == 0
+    s = 1 / (1 + np.exp(-0.3))
+    assert t.value == pytest.approx(s) and dt.value == pytest.approx(s * (1 - s))
+    assert L.Nfft4GPTransform(2, 0.3, 0, C.byref(t), C.byref(dt)) == 0
+    assert t.value == pytest.approx(np.exp(0.3)) and dt.value == pytest.approx(np.exp(0.3))
+    assert L.Nfft4GPTransform(3, 0.3, 0, C.byref(t), C.byref(dt)) == 0
+    assert t.value == 0.3 and dt.value == 1.0
+    assert L.Nfft4GPTransform(7, 0.3, 0, C.byref(t), C.byref(dt)) == -1
+
+
+def test_random_vectors_follow_libc_rand():
+    """Nfft4GPVecRand / Nfft4GPVecRadamacher (vecops.c:15-46): libc rand() / RAND_MAX in order, so a
+    srand seed reproduces the reference's probes."""
+    libc = C.CDLL(None)
+    L = amd.lib()
+    libc.srand(807)
+    expect = np.array([libc.rand() for _ in range(1000)], dtype=np.float64) / 2147483647.0
+    libc.srand(807)
+    x = np.zeros(1000)
+    L.Nfft4GPVecRand(x.ctypes.data, 1000)
+    np.testing.assert_array_equal(x, expect)
+    libc.srand(807)
+    L.Nfft4GPVecRadamacher(x.ctypes.data, 1000)
+    np.testing.assert_array_equal(x, np.where(expect < 0.5, -1.0, 1.0))
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                    "oracle", "_ref", "libnfft4gp_ref.so")),
+                    reason="oracle/_ref not built")
+def test_compiled_reference_reproduces_krylov_fixture():
+    """Re-run the reference's FGMRES and logdet quadrature (oracle/_ref) from the krylov_synth inputs."""
+    import oracle as O
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    z = np.load(os.path.join(gold, "pcg_synth.npz"))
+    k = np.load(os.path.join(gold, "krylov_synth.npz"))
+    r = O.RefDenseAdditive(z["X"], z["windows"], int(z["nw"]), int(z["dw"]), kernel=0)
+    r.matrices(float(k["f"]), float(k["l"]), float(k["mu"]), grad=True)
+
+    def mv(a, xv, b, yv):
+        yv[:] = r.matsymv(xv, a, b, yv.copy())
+
+    def dmv(a, xv, b, yv):
+        yv[:] = r.gradmatsymv(xv, a, b, yv.copy())
+
+    n = z["X"].shape[0]
+    x, rr, hist, it = O.ref_fgmres(mv, n, z["b"], 100, 400, 1e-8)
+    assert it == int(k["fg_iters"])
+    np.testing.assert_allclose(x, k["fg_x"], rtol=1e-9, atol=1e-12)
+    val, g = O.ref_logdet_quadrature(mv, dmv, n, int(k["maxits"]), int(k["nvecs"]), k["rademacher"].astype(float))
+    assert val == pytest.approx(float(k["ld_val"]), rel=1e-12)
+    np.testing.assert_allclose(g, k["ld_grad"], rtol=1e-10)

@@ -1,0 +1,178 @@
+"""GPU parity of FGMRES (fgmres.c), the Lanczos logdet quadrature (lanczos.c:421-610) and the GP loss
+(gp_loss.c:96-307) against the reference's own runs (tests/golden/krylov_synth.npz, made from
+oracle/_ref on pcg_synth's dense additive operator with fixed Rademacher probes).
+
+The operator is handed over the way a reference caller would: a host func_symmatvec (numpy dense
+matrix, or the reference's Nfft4GPDenseMatSymv from oracle/_ref), so both solvers see the same
+operator and differ only in floating-point summation order.  Tolerances are written per test.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd import _lib
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+
+
+def rel(a, b):
+    return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / np.linalg.norm(np.asarray(b)))
+
+
+class HostDenseOp:
+    """func_symmatvec / grad func_symmatvec on host vectors for pcg_synth's dense additive Gaussian
+    f^2 ((1/nw) sum_c exp(-|x_c - x_c'|^2 / 2 l^2) + mu I) and its three derivative matrices
+    (kernels.c:680-1289, 3099-3494; matops.c:3-29)."""
+
+    def __init__(self, X, f, l, mu):
+        n, nw = X.shape
+        E = np.zeros((n, n))
+        D = np.zeros((n, n))
+        for c in range(nw):
+            d2 = (X[:, c][:, None] - X[:, c][None, :]) ** 2
+            e = np.exp(-d2 / (2 * l * l))
+            E += e
+            D += d2 / (l ** 3) * e
+        E /= nw
+        D /= nw
+        self.K = f * f * (E + mu * np.eye(n))
+        self.dK = [2 * f * (E + mu * np.eye(n)), f * f * D, f * f * np.eye(n)]
+        self.n = n
+        self.h = None
+
+        def mv(_m, nn, alpha, xp, beta, yp):
+            xv = np.ctypeslib.as_array(C.cast(xp, _lib.dp), shape=(nn,))
+            yv = np.ctypeslib.as_array(C.cast(yp, _lib.dp), shape=(nn,))
+            yv[:] = alpha * (self.K @ xv) + (beta * yv if beta != 0.0 else 0.0)
+            return 0
+
+        def dmv(_m, nn, alpha, xp, beta, yp):
+            xv = np.ctypeslib.as_array(C.cast(xp, _lib.dp), shape=(nn,))
+            yv = np.ctypeslib.as_array(C.cast(yp, _lib.dp), shape=(3 * nn,))
+            for i in range(3):
+                seg = yv[i * nn:(i + 1) * nn]
+                seg[:] = alpha * (self.dK[i] @ xv) + (beta * seg if beta != 0.0 else 0.0)
+            return 0
+
+        self._cb = _lib.SYMMATVEC(mv)
+        self._dcb = _lib.SYMMATVEC(dmv)
+        self.matvec_fnptr = C.cast(self._cb, C.c_void_p).value
+        self.gradmatvec_fnptr = C.cast(self._dcb, C.c_void_p).value
+
+
+@pytest.fixture(scope="module")
+def case():
+    z = load("pcg_synth")
+    k = load("krylov_synth")
+    op = HostDenseOp(np.asarray(z["X"]), float(k["f"]), float(k["l"]), float(k["mu"]))
+    return z, k, op
+
+
+# (key, kdim, maxits, Nystrom, history rtol, solution rtol).  The restarted case (kdim 10) stagnates at
+# |r| ~ 0.86 |b| on this ill-conditioned operator (l = 0.1) and its restart vector is not re-normalised
+# (fgmres.c:236-243 scales by the Givens estimate): measured, 1e-16 operator rounding grows to ~5e-5 in
+# the history within two cycles, so that case is held to 1e-3.
+FG_CASES = [("fg", 100, 400, False, 1e-5, 1e-6), ("fgr", 10, 60, False, 1e-3, 1e-3),
+            ("fgn", 100, 400, True, 1e-5, 1e-6)]
+
+
+@pytest.mark.parametrize("key,kdim,maxits,nys,htol,xtol", FG_CASES)
+def test_fgmres_matches_reference(torch_cuda, case, key, kdim, maxits, nys, htol, xtol):
+    """Same iteration count (+-1), residual history (restarts included: fgmres.c:236-243 keeps the
+    Givens estimate as the restart norm) and solution."""
+    torch = torch_cuda
+    z, k, op = case
+    pre = amd.NystromPrecond(z["nys_U"], z["nys_s"], float(z["nys_eta"]), z["nys_perm"]) if nys else None
+    b = torch.tensor(np.asarray(z["b"]), device="cuda")
+    x = torch.zeros(op.n, dtype=torch.float64, device="cuda")
+    x, rr, hist, it = amd.fgmres(op, b, x, kdim=kdim, maxits=maxits, tol=1e-8, precond=pre)
+    it_ref = int(k[key + "_iters"])
+    assert abs(it - it_ref) <= 1, (it, it_ref)
+    m = min(it, it_ref)
+    np.testing.assert_allclose(hist[:m + 1], np.asarray(k[key + "_hist"])[:m + 1], rtol=htol)
+    assert rel(x.cpu().numpy(), k[key + "_x"]) < xtol
+    assert rr == pytest.approx(float(k[key + "_relres"]), rel=1e-3)
+
+
+def test_fgmres_host_vectors_match_device(torch_cuda, case):
+    torch = torch_cuda
+    z, k, op = case
+    b = np.asarray(z["b"])
+    xh, rh, hh, ih = amd.fgmres(op, b.copy(), np.zeros(op.n), kdim=10, maxits=60, tol=1e-8)
+    xd, rd, hd, idv = amd.fgmres(op, torch.tensor(b, device="cuda"), torch.zeros(op.n, dtype=torch.float64,
+                                                                             device="cuda"), kdim=10, maxits=60, tol=1e-8)
+    assert ih == idv
+    np.testing.assert_array_equal(xh, xd.cpu().numpy())
+
+
+def test_logdet_quadrature_matches_reference(torch_cuda, case):
+    """Lanczos with full MGS2 re-orthogonalisation: T agrees to rounding, so the quadrature does."""
+    z, k, op = case
+    R = np.asarray(k["rademacher"], dtype=np.float64)
+    val, g = amd.logdet(op, int(k["maxits"]), int(k["nvecs"]), R)
+    assert val == pytest.approx(float(k["ld_val"]), rel=1e-9)
+    np.testing.assert_allclose(g, k["ld_grad"], rtol=1e-8)
+
+
+def _ref_gp(z, k, nys):
+    import oracle as O
+    if not O.ref_available():
+        pytest.skip("oracle/_ref not built")
+    if nys:
+        return O.RefGpLoss(np.asarray(z["X"]), np.asarray(z["windows"]), int(z["nw"]), int(z["dw"]), k=8,
+                           perm=np.asarray(z["nys_perm"]))
+    return O.RefGpLoss(np.asarray(z["X"]), np.asarray(z["windows"]), int(z["nw"]), int(z["dw"]))
+
+
+@pytest.mark.parametrize("nys", [False, True])
+def test_gp_loss_matches_reference(torch_cuda, case, nys):
+    """This library's Nfft4GPGpLoss called with the reference's own dense kernel, SYMV and (nys=True) its
+    Nystrom preconditioner with trace / logdet / dvp (all host callbacks): the reference's loss and
+    gradient."""
+    z, k, op = case
+    g = _ref_gp(z, k, nys)
+    R = np.asarray(k["rademacher"], dtype=np.float64)
+    loss, grad = g.run(_lib.lib().Nfft4GPGpLoss, np.asarray(k["hyper"]), np.asarray(z["b"]), int(k["maxits"]),
+                       int(k["nvecs"]), R)
+    sfx = "_nys8" if nys else ""
+    assert loss == pytest.approx(float(k["loss" + sfx]), rel=1e-8)
+    np.testing.assert_allclose(grad, k["grad" + sfx], rtol=1e-6, atol=1e-9)
+
+
+def test_gp_loss_on_nfft_operator(torch_cuda, case):
+    """The north-star operator inside the GP loss (device pointers end to end) against the reference's
+    loss code driven by the oracle's NFFT operator."""
+    z, k, op = case
+    X = np.asfortranarray(np.asarray(z["X"]))
+    n, d = X.shape
+    nf = amd.NFFTAdditiveKernel(X, np.asarray(z["windows"], np.int32), int(z["nw"]), int(z["dw"]))
+    L = _lib.lib()
+    fn = L.Nfft4GPGpLoss
+    import oracle as O
+    fn.argtypes = O.RefGpLoss.ARGTYPES
+    fn.restype = C.c_int
+    x = np.asarray(k["hyper"], dtype=np.float64).copy()
+    lab = np.ascontiguousarray(np.asarray(z["b"]))
+    R = np.asfortranarray(np.asarray(k["rademacher"], dtype=np.float64))
+    loss = np.zeros(1)
+    grad = np.zeros(3)
+    rc = fn(x.ctypes.data, X.ctypes.data, lab.ctypes.data, n, n, d,
+            _lib.fnptr("Nfft4GPNFFTAdditiveKernelGaussianKernel"), nf.h, None, nf.matvec_fnptr, nf.gradmatvec_fnptr,
+            None, None, None, None, None, None, None, None, None, None, 0, 1e-8, int(k["maxits"]), int(k["maxits"]),
+            int(k["nvecs"]), R.ctypes.data, 0, None, -1, None, loss.ctypes.data_as(_lib.dp),
+            grad.ctypes.data_as(_lib.dp))
+    assert rc == 0
+    # the reference's gp_loss.c / fgmres.c / lanczos.c on the oracle's NFFT operator
+    assert loss[0] == pytest.approx(float(k["loss_nfft"]), rel=1e-8)
+    np.testing.assert_allclose(grad, k["grad_nfft"], rtol=1e-6, atol=1e-9)
+    # and the dense operator's loss within the NFFT truncation (about 3e-5 per matvec at l = 0.31),
+    # amplified by K^{-1}: measured 2.2e-3
+    assert loss[0] == pytest.approx(float(k["loss"]), rel=5e-3)
