@@ -137,6 +137,20 @@ int Nfft4GPAdditiveNFFTGradMatSymv(void *data, int n, NFFT4GP_DOUBLE alpha, NFFT
                                    NFFT4GP_DOUBLE *y);
 /* replaces SRC/external/nfft_interface.c:842-856 */
 void Nfft4GPAdditiveNFFTKernelFree(void *str);
+/* replaces SRC/external/nfft_interface.c:873-1068: posterior mean at the n_predict points of data_all
+ * (rows n..n+n_predict-1; vfkernel_data_l is a kernel handle over data_all) and, if std_predictp is not
+ * NULL, the predictive standard deviation sqrt|K22_ii - K21_i K11^{-1} K12_i|.  *label_predictp /
+ * *std_predictp: caller arrays (host or device) or NULL to get malloc'ed host arrays. */
+int Nfft4GPAdditiveNFFTGpPredict(NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *data, NFFT4GP_DOUBLE *label, int n, int ldim,
+                                 int d, NFFT4GP_DOUBLE *data_predict, int n_predict, int ldim_predict,
+                                 NFFT4GP_DOUBLE *data_all, func_kernel fkernel, void *vfkernel_data,
+                                 void *vfkernel_data_l, func_free kernel_data_free, func_symmatvec matvec,
+                                 func_kernel precond_fkernel, void *precond_vfkernel_data,
+                                 func_free precond_kernel_data_free, precond_kernel_setup precond_setup,
+                                 func_solve precond_solve, void *precond_data, int atol, NFFT4GP_DOUBLE tol,
+                                 int maxits, nfft4gp_transform_type transform, int print_level,
+                                 NFFT4GP_DOUBLE *dwork, NFFT4GP_DOUBLE **label_predictp,
+                                 NFFT4GP_DOUBLE **std_predictp);
 /* replaces SRC/external/nfft_interface.c:858-871 (host memory, caller frees with free()) */
 NFFT4GP_DOUBLE *Nfft4GPNFFTAppendData(NFFT4GP_DOUBLE *X1, int n1, int ldim1, int d, NFFT4GP_DOUBLE *X2, int n2,
                                       int ldim2);

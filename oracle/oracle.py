@@ -610,3 +610,37 @@ def ref_gp_loss_nfft(X, windows, nw, dw, label, hyper, maxits, nvecs, radamacher
             R.ctypes.data, 0, None, -1, None, _d(loss), _d(grad))
     assert rc == 0
     return float(loss[0]), grad
+
+
+def ref_nfft_gp_predict(X, Xp, windows, nw, dw, label, hyper, maxits, tol, with_std=True, atol=0):
+    """Nfft4GPAdditiveNFFTGpPredict (nfft_interface.c:873-1068) restated over the reference's own FGMRES
+    (fgmres.c, oracle/_ref) and this oracle's NFFT operator, softplus transform (transform.c:20-37):
+    mean = (K_all [K11^{-1} y; 0])[n:], std_i = sqrt|K22_ii - K21_i K11^{-1} K12_i| with one FGMRES
+    (restart n, maxits n) per prediction point.  Returns (mean, std or None)."""
+    tv = np.where(np.asarray(hyper) > 20, hyper, np.log1p(np.exp(np.minimum(hyper, 20))))
+    f, l, mu = (float(v) for v in tv)
+    X = np.asfortranarray(X, dtype=np.float64)
+    n = X.shape[0]
+    Xa = np.asfortranarray(np.vstack([X, np.asarray(Xp, dtype=np.float64)]))
+    na = Xa.shape[0]
+    o11 = OracleAdditiveNFFT(X, windows, nw, dw)
+    o11.setup(0, f, l, mu)
+    oa = OracleAdditiveNFFT(Xa, windows, nw, dw)
+    oa.setup(0, f, l, mu)
+
+    def mv11(a, xv, b, yv):
+        yv[:] = o11.matsymv(xv.copy(), a, b, yv.copy())
+
+    iKY, _, _, _ = ref_fgmres(mv11, n, np.asarray(label, dtype=np.float64), maxits, maxits, tol, atol=atol)
+    helper = oa.matsymv(np.concatenate([iKY, np.zeros(na - n)]))
+    mean = helper[n:].copy()
+    if not with_std:
+        return mean, None
+    std = np.zeros(na - n)
+    for i in range(na - n):
+        e = np.zeros(na)
+        e[n + i] = 1.0
+        h = oa.matsymv(e)
+        sol, _, _, _ = ref_fgmres(mv11, n, h[:n].copy(), n, n, tol, atol=atol)
+        std[i] = np.sqrt(abs(h[n + i] - np.dot(h[:n], sol)))
+    return mean, std

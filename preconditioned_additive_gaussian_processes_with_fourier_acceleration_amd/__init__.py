@@ -6,6 +6,7 @@ kernels for gfx950 behind the C ABI of include/nfft4gp_amd.h (libnfft4gp_amd.so,
 """
 from ._lib import ExtensionMissing, header_symbols, lib  # noqa: F401
 from .data import read_features, read_labels, read_windows  # noqa: F401
+from .gp import gp_loss, gp_predict  # noqa: F401
 from .nfft import GAUSSIAN, MATERN12, NFFTAdditiveKernel, NFFTKernel  # noqa: F401
 from .solvers import AfnPrecond, FsaiPrecond, NystromPrecond, fgmres, logdet, pcg  # noqa: F401
 

@@ -9,6 +9,8 @@
 //   Nfft4GPLanczosQuadratureLogdet SRC/solvers/lanczos.c:421-610
 //   Nfft4GPGpLoss                  SRC/optimizer/gp_loss.c:96-307
 //   Nfft4GPTransform               SRC/optimizer/transform.c:4-89
+//   Nfft4GPAdditiveNFFTGpPredict   SRC/external/nfft_interface.c:873-1068 (posterior mean, and the
+//                                  predictive standard deviation by one solve per prediction point)
 //
 // The small dense work (Givens rotations, the Cholesky of T, the tridiagonal eigensolve) runs on the
 // host on scalars read back once per iteration; each Gram-Schmidt step is one fused launch (apply the
@@ -903,6 +905,102 @@ int Nfft4GPGpLoss(double* x, double* data, double* label, int n, int ldim, int d
       kernel_data_free(dkernel_mat);
    }
    if (precond_data && precond_reset) precond_reset(precond_data);
+   return 0;
+}
+
+int Nfft4GPAdditiveNFFTGpPredict(double* x, double* data, double* label, int n, int ldim, int d,
+                                 double* data_predict, int n_predict, int ldim_predict, double* data_all,
+                                 func_kernel fkernel, void* vfkernel_data, void* vfkernel_data_l,
+                                 func_free kernel_data_free, func_symmatvec matvec, func_kernel precond_fkernel,
+                                 void* precond_vfkernel_data, func_free precond_kernel_data_free,
+                                 precond_kernel_setup precond_setup, func_solve precond_solve, void* precond_data,
+                                 int atol, double tol, int maxits, nfft4gp_transform_type transform,
+                                 int print_level, double* dwork, double** label_predictp, double** std_predictp)
+{
+   (void)data_predict, (void)ldim_predict, (void)kernel_data_free, (void)precond_kernel_data_free, (void)dwork;
+   if (!need_device("Nfft4GPAdditiveNFFTGpPredict")) return -1;
+   double tvals[3], dtvals[3];
+   for (int i = 0; i < 3; i++)
+      if (Nfft4GPTransform(transform, x[i], 0, tvals + i, dtvals + i)) return -1;
+   nfft4gp_kernel* kd = (nfft4gp_kernel*)vfkernel_data;
+   nfft4gp_kernel* kl = (nfft4gp_kernel*)vfkernel_data_l;
+   for (nfft4gp_kernel* k : {kd, kl}) {
+      k->_params[0] = tvals[0];
+      k->_params[1] = tvals[1];
+      k->_noise_level = tvals[2];
+   }
+   double *K11 = nullptr, *dK11 = nullptr, *K = nullptr, *dK = nullptr;
+   const int na = n + n_predict;
+   if (fkernel(vfkernel_data, data, n, ldim, d, nullptr, 0, nullptr, 0, &K11, &dK11) ||
+       fkernel(vfkernel_data_l, data_all, na, na, d, nullptr, 0, nullptr, 0, &K, &dK))
+      return -1;
+   if (precond_setup)
+      precond_setup(data, n, ldim, d, precond_fkernel, precond_vfkernel_data, 1, precond_data);
+   else
+      precond_data = nullptr;
+   Callbacks cb11, cba;
+   if (!make_callbacks(cb11, n, matvec, K11, precond_solve, precond_data) ||
+       !make_callbacks(cba, na, matvec, K, nullptr, nullptr))
+      return -1;
+   hipStream_t s = current_stream();
+   Ctx c{s, (size_t)n};
+   double *iKY = nullptr, *helper = nullptr;
+   Vec vl;
+   if (dmalloc(&iKY, (size_t)na) || dmalloc(&helper, (size_t)na) || vl.open(label, n, true)) return -1;
+   auto cleanup = [&]() {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(iKY);
+      (void)hipFree(helper);
+      vl.close(false);
+   };
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(iKY, 0, sizeof(double) * na, s));
+   double rel_res, *rel_res_v = nullptr;
+   int niter = 0;
+   if (fgmres_dev(cb11, iKY, vl.d, maxits, maxits, atol, tol, &rel_res, &rel_res_v, &niter, print_level)) {
+      cleanup();
+      return -1;
+   }
+   free(rel_res_v);
+   // label_predict = (K_all [iKY; 0])[n:]  (nfft_interface.c:973-979)
+   if (cba.apply(1.0, iKY, 0.0, helper)) {
+      cleanup();
+      return -1;
+   }
+   double* lp = *label_predictp ? *label_predictp : (double*)malloc(sizeof(double) * std::max(1, n_predict));
+   const bool lp_dev = is_device_ptr(lp);
+   NFFT4GP_HIP_CHECK(hipMemcpyAsync(lp, helper + n, sizeof(double) * n_predict,
+                                    lp_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+   NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
+   if (!*label_predictp) *label_predictp = lp;
+   if (std_predictp) {
+      // diag of K22 - K21 K11^{-1} K12, one column at a time (nfft_interface.c:993-1060)
+      double* sp = *std_predictp ? *std_predictp : (double*)malloc(sizeof(double) * std::max(1, n_predict));
+      std::vector<double> hs(n_predict);
+      const double one = 1.0;
+      for (int i = 0; i < n_predict; i++) {
+         NFFT4GP_HIP_CHECK(hipMemsetAsync(iKY, 0, sizeof(double) * na, s));
+         NFFT4GP_HIP_CHECK(hipMemcpyAsync(iKY + n + i, &one, sizeof(double), hipMemcpyHostToDevice, s));
+         if (cba.apply(1.0, iKY, 0.0, helper)) {
+            cleanup();
+            return -1;
+         }
+         double K22i;
+         if (c.read(helper + n + i, 1, &K22i)) return -1;
+         NFFT4GP_HIP_CHECK(hipMemsetAsync(iKY + n + i, 0, sizeof(double), s));
+         if (fgmres_dev(cb11, iKY, helper, n, n, atol, tol, &rel_res, &rel_res_v, &niter, print_level)) {
+            cleanup();
+            return -1;
+         }
+         free(rel_res_v);
+         hs[i] = std::sqrt(std::fabs(K22i - c.dot(helper, iKY)));
+      }
+      if (is_device_ptr(sp))
+         NFFT4GP_HIP_CHECK(hipMemcpy(sp, hs.data(), sizeof(double) * n_predict, hipMemcpyHostToDevice));
+      else
+         memcpy(sp, hs.data(), sizeof(double) * n_predict);
+      if (!*std_predictp) *std_predictp = sp;
+   }
+   cleanup();
    return 0;
 }
 

@@ -1,0 +1,81 @@
+"""GP loss and prediction on the NFFT additive operator, over the C ABI.
+
+``gp_loss``     Nfft4GPGpLoss (SRC/optimizer/gp_loss.c:96-307) with Nfft4GPNFFTAdditiveKernelGaussianKernel /
+                Nfft4GPAdditiveNFFTMatSymv / Nfft4GPAdditiveNFFTGradMatSymv as kernel, matvec and grad matvec,
+                no preconditioner (TEST1-style call of the north-star operator inside the loss).
+``gp_predict``  Nfft4GPAdditiveNFFTGpPredict (SRC/external/nfft_interface.c:873-1068): posterior mean and,
+                optionally, standard deviation at new points (a second handle over [X; Xp], as TEST4 does).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .nfft import NFFTAdditiveKernel
+
+_vp = C.c_void_p
+_GPLOSS_ARGS = [_vp, _vp, _vp, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                _vp, _vp, _vp, _vp, C.c_int, C.c_double, C.c_int, C.c_int, C.c_int, _vp, C.c_int, _vp, C.c_int, _vp,
+                _lib.dp, _lib.dp]
+_PREDICT_ARGS = [_vp, _vp, _vp, C.c_int, C.c_int, C.c_int, _vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                 _vp, _vp, _vp, _vp, _vp, C.c_int, C.c_double, C.c_int, C.c_int, C.c_int, _vp, C.POINTER(_lib.dp),
+                 C.POINTER(_lib.dp)]
+
+
+def gp_loss(X, windows, nwindows, dwindows, y, hyper, maxits=50, nvecs=10, rademacher=None, tol=1e-6,
+            transform=0, mask=None, print_level=-1):
+    """(loss, grad) of Nfft4GPGpLoss for the additive NFFT Gaussian kernel; ``hyper`` = (f, l, mu) before
+    the transform (0 softplus, 1 sigmoid, 2 exp, 3 identity)."""
+    X = np.asfortranarray(np.asarray(X, dtype=np.float64))
+    n, d = X.shape
+    op = NFFTAdditiveKernel(X, windows, nwindows, dwindows)
+    L = _lib.lib()
+    fn = L.Nfft4GPGpLoss
+    fn.argtypes = _GPLOSS_ARGS
+    fn.restype = C.c_int
+    x = np.ascontiguousarray(np.asarray(hyper, dtype=np.float64))
+    lab = np.ascontiguousarray(np.asarray(y, dtype=np.float64))
+    R = None if rademacher is None else np.asfortranarray(np.asarray(rademacher, dtype=np.float64))
+    m = None if mask is None else np.ascontiguousarray(np.asarray(mask, dtype=np.int32))
+    loss = np.zeros(1)
+    grad = np.zeros(3)
+    rc = fn(x.ctypes.data, X.ctypes.data, lab.ctypes.data, n, n, d,
+            _lib.fnptr("Nfft4GPNFFTAdditiveKernelGaussianKernel"), op.h, None, op.matvec_fnptr, op.gradmatvec_fnptr,
+            None, None, None, None, None, None, None, None, None, None, 0, float(tol), int(maxits), int(maxits),
+            int(nvecs), R.ctypes.data if R is not None else None, int(transform),
+            m.ctypes.data if m is not None else None, int(print_level), None, loss.ctypes.data_as(_lib.dp),
+            grad.ctypes.data_as(_lib.dp))
+    if rc:
+        raise RuntimeError("Nfft4GPGpLoss failed")
+    return float(loss[0]), grad
+
+
+def gp_predict(X, Xp, windows, nwindows, dwindows, y, hyper, maxits=100, tol=1e-8, with_std=False,
+               transform=0, print_level=-1):
+    """(mean, std or None) of Nfft4GPAdditiveNFFTGpPredict at the rows of Xp."""
+    X = np.asfortranarray(np.asarray(X, dtype=np.float64))
+    Xp = np.asfortranarray(np.asarray(Xp, dtype=np.float64))
+    n, d = X.shape
+    npred = Xp.shape[0]
+    Xa = np.asfortranarray(np.vstack([X, Xp]))
+    op = NFFTAdditiveKernel(X, windows, nwindows, dwindows)
+    opa = NFFTAdditiveKernel(Xa, windows, nwindows, dwindows)
+    L = _lib.lib()
+    fn = L.Nfft4GPAdditiveNFFTGpPredict
+    fn.argtypes = _PREDICT_ARGS
+    fn.restype = C.c_int
+    x = np.ascontiguousarray(np.asarray(hyper, dtype=np.float64))
+    lab = np.ascontiguousarray(np.asarray(y, dtype=np.float64))
+    mean = np.zeros(npred)
+    std = np.zeros(npred)
+    mp = C.cast(mean.ctypes.data, _lib.dp)
+    sp = C.cast(std.ctypes.data, _lib.dp)
+    rc = fn(x.ctypes.data, X.ctypes.data, lab.ctypes.data, n, n, d, Xp.ctypes.data, npred, npred, Xa.ctypes.data,
+            _lib.fnptr("Nfft4GPNFFTAdditiveKernelGaussianKernel"), op.h, opa.h, None, op.matvec_fnptr, None, None,
+            None, None, None, None, 0, float(tol), int(maxits), int(transform), int(print_level), None,
+            C.byref(mp), C.byref(sp) if with_std else None)
+    if rc:
+        raise RuntimeError("Nfft4GPAdditiveNFFTGpPredict failed")
+    return mean, (std if with_std else None)

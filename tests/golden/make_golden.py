@@ -24,7 +24,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 from oracle import (OracleAdditiveNFFT, RefDenseAdditive, RefFsai, RefGpLoss, RefNystrom, afn_apply,  # noqa: E402
                     ref_available, ref_fgmres, ref_gaussian_matrix, ref_gaussian_params, ref_gp_loss_nfft,
-                    ref_logdet_quadrature, ref_pcg, ref_schur_params)
+                    ref_logdet_quadrature, ref_nfft_gp_predict, ref_pcg, ref_schur_params)
 from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.data import (  # noqa: E402
     read_features, read_labels, read_windows)
 
@@ -155,6 +155,21 @@ def make_krylov_synth():
          loss=loss0, grad=grad0, loss_nys8=loss8, grad_nys8=grad8, loss_nfft=lossn, grad_nfft=gradn, **out)
 
 
+def make_predict_synth():
+    """(7) Nfft4GPAdditiveNFFTGpPredict (nfft_interface.c:873-1068) restated over the reference's FGMRES
+    and the oracle NFFT operator: 4 x 1-D windows, 800 training and 40 prediction points."""
+    rng = np.random.default_rng(41)
+    n, npred, d = 800, 40, 4
+    X = rng.random((n, d))
+    Xp = rng.random((npred, d))
+    y = np.sin(6 * X).sum(1) + 0.05 * rng.standard_normal(n)
+    win = np.arange(d, dtype=np.int32)
+    hyper = np.array([0.3, -0.5, -2.5])
+    mean, std = ref_nfft_gp_predict(X, Xp, win, d, 1, y, hyper, 200, 1e-10)
+    print(f"predict_synth: mean[:3] {mean[:3]}, std[:3] {std[:3]}")
+    save("predict_synth", X=X, Xp=Xp, y=y, windows=win, hyper=hyper, maxits=200, tol=1e-10, mean=mean, std=std)
+
+
 def main():
     if not ref_available():
         raise SystemExit("build oracle/_ref first: make -C oracle ref")
@@ -162,6 +177,8 @@ def main():
         return make_precond_synth()
     if sys.argv[1:] == ["krylov"]:
         return make_krylov_synth()
+    if sys.argv[1:] == ["predict"]:
+        return make_predict_synth()
     f, mu = 1.3, 0.01
 
     # (1) TEST2's 1-D dataset, one window {0} (TESTS/TEST2/data/foo.window)
@@ -231,6 +248,7 @@ def main():
 
     make_precond_synth()
     make_krylov_synth()
+    make_predict_synth()
 
 
 if __name__ == "__main__":

@@ -176,3 +176,25 @@ def test_gp_loss_on_nfft_operator(torch_cuda, case):
     # and the dense operator's loss within the NFFT truncation (about 3e-5 per matvec at l = 0.31),
     # amplified by K^{-1}: measured 2.2e-3
     assert loss[0] == pytest.approx(float(k["loss"]), rel=5e-3)
+
+
+def test_gp_predict_matches_restated_reference(torch_cuda):
+    """Nfft4GPAdditiveNFFTGpPredict (nfft_interface.c:873-1068): mean and standard deviation against the
+    reference's orchestration restated over its own FGMRES and the oracle NFFT operator
+    (tests/golden/predict_synth.npz).  FGMRES runs to 1e-10, so the means agree to ~1e-9."""
+    z = load("predict_synth")
+    mean, std = amd.gp_predict(z["X"], z["Xp"], z["windows"], 4, 1, z["y"], z["hyper"], maxits=int(z["maxits"]),
+                               tol=float(z["tol"]), with_std=True)
+    assert rel(mean, z["mean"]) < 1e-8
+    np.testing.assert_allclose(std, z["std"], rtol=1e-6)
+    m2, s2 = amd.gp_predict(z["X"], z["Xp"], z["windows"], 4, 1, z["y"], z["hyper"], maxits=int(z["maxits"]),
+                            tol=float(z["tol"]))
+    assert s2 is None and rel(m2, mean) < 1e-12  # LDS atomics in the spread: not bitwise run to run
+
+
+def test_gp_loss_wrapper(torch_cuda, case):
+    z, k, op = case
+    loss, grad = amd.gp_loss(z["X"], z["windows"], int(z["nw"]), int(z["dw"]), z["b"], k["hyper"],
+                             maxits=int(k["maxits"]), nvecs=int(k["nvecs"]), rademacher=k["rademacher"], tol=1e-8)
+    assert loss == pytest.approx(float(k["loss_nfft"]), rel=1e-8)
+    np.testing.assert_allclose(grad, k["grad_nfft"], rtol=1e-6, atol=1e-9)
