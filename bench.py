@@ -31,6 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+F64_MFMA_PEAK_TFS = 78.6  # MI355X dense FP64 matrix peak (spec; gfx950 runs v_mfma_f64_16x16x4 at half of MI300X)
 
 
 def make_problem(n, d, seed=906):
@@ -186,6 +187,13 @@ def run_pcg_nystrom(op, torch, n, k, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=
     pre = amd.NystromPrecond.from_additive(op, perm, k, k11="landmarks")
     torch.cuda.synchronize()
     t_setup = time.time() - t0
+    ms = pre.setup_times()
+    flops = 2.0 * n * k * k  # each of the three n x k x k products
+    mfma = {"kernel": "k_gemm_f64 (v_mfma_f64_16x16x4)", "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+            "flops_per_product": flops, "panel_ms": ms["panel"]}
+    for key in ("gemm1", "gram", "gemm2"):
+        tf = flops / (ms[key] * 1e-3) / 1e12 if ms[key] > 0 else None
+        mfma[key] = {"ms": ms[key], "achieved": tf, "frac": tf / F64_MFMA_PEAK_TFS if tf else None}
     b = torch.tensor(np.random.default_rng(rng_seed + 1).random(n) - 0.5, device="cuda")
     x = torch.zeros(n, dtype=torch.float64, device="cuda")
     torch.cuda.synchronize()
@@ -195,7 +203,7 @@ def run_pcg_nystrom(op, torch, n, k, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=
     t = time.time() - t0
     pre.free()
     return {"pcg_nys_rank": k, "pcg_nys_setup_s": t_setup, "pcg_nys_time_s": t, "pcg_nys_iters": iters,
-            "pcg_nys_rel_res": relres, "pcg_nys_total_s": t_setup + t}
+            "pcg_nys_rel_res": relres, "pcg_nys_total_s": t_setup + t, "nys_setup_mfma": mfma}
 
 
 def run_pcg_sharded(op, sop, torch, dist, n, rb, re, tol=1e-6, maxits=3000, l_pcg=0.1):

@@ -228,7 +228,7 @@ void Nfft4GPAmdNysFree(void *nys);
  * K11 + sqrt(k) ulp(|K11|_F) I = L L^T (chol.c:446-466), U1 = K(perm, perm[:k]) L^{-T},
  * U1^T U1 = V diag(w) V^T, U = U1 V w^{-1/2} (descending w), s = max(1/(w + eta), 0), eta = mu f^2.
  * The n x k panel and the n x k x k products run on the GPU (v_mfma_f64_16x16x4), the k x k Cholesky,
- * inverse and eigensolve on the host.  Returns a handle for Nfft4GPAmdNysSolve / Nfft4GPAmdNysFree, or
+ * inverse and eigensolve on the GPU through rocSOLVER (dlopen'ed; host fallback when it is absent).  Returns a handle for Nfft4GPAmdNysSolve / Nfft4GPAmdNysFree, or
  * NULL (message on stderr) if K11 is not positive definite or the handle is unsuitable.
  * k11_mode 0 reproduces the reference's K11 exactly: nys.c:569 passes the k x d sub-data to the additive
  * kernel, which ignores it and reads its own gathered buffer at window stride k*dwindows (kernels.c:3160),
@@ -238,6 +238,9 @@ void *Nfft4GPAmdNysSetupAdditive(void *str, const int *perm, int k, int k11_mode
  * (pass the setup's perm to get the reference's permuted row order, NULL for natural order), s (k),
  * eta; any output may be NULL */
 int Nfft4GPAmdNysFactors(void *nys, const int *perm, NFFT4GP_DOUBLE *U, NFFT4GP_DOUBLE *s, NFFT4GP_DOUBLE *eta);
+/* hipEvent durations (ms) of a GPU setup's four big kernels: the panel, U1 = Kp G^T, the Gram U1^T U1 and
+ * U = U1 W (the three MFMA products, 2 n k^2 flops each); zeros for a handle from Nfft4GPAmdNysCreate */
+int Nfft4GPAmdNysSetupTimes(void *nys, NFFT4GP_DOUBLE *ms4);
 
 /* ---- FSAI preconditioner apply (SRC/preconds/fsai.c:106-123) --------------------------------------
  * The reference's Nfft4GPPrecondFsaiSetupWithKernel (fsai.c:333-...) produces the lower-triangular

@@ -91,6 +91,7 @@ _SIGS = {
     "Nfft4GPAmdNysFree": (None, [vp]),
     "Nfft4GPAmdNysSetupAdditive": (vp, [vp, vp, C.c_int, C.c_int]),
     "Nfft4GPAmdNysFactors": (C.c_int, [vp, vp, vp, vp, dp]),
+    "Nfft4GPAmdNysSetupTimes": (C.c_int, [vp, vp]),
     "Nfft4GPAmdFsaiCreate": (vp, [C.c_int, vp, vp, vp]),
     "Nfft4GPAmdFsaiSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdFsaiFree": (None, [vp]),

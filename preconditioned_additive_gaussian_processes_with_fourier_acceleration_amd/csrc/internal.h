@@ -179,12 +179,15 @@ struct NysDev {
    double* w = nullptr;  // apply scratch, k
    double* part = nullptr;
    int nblk = 0;
+   // GPU setup only: hipEvent durations of the setup's kernels (ms): panel, U1 = Kp G^T, the Gram
+   // U1^T U1 (+ split sum), U = U1 W (Nfft4GPAmdNysSetupTimes)
+   double setup_ms[4] = {0.0, 0.0, 0.0, 0.0};
 };
 constexpr int kNysRows = 2048;  // rows per workgroup of the apply's U^T r pass
 int nys_alloc_scratch(NysDev* N);
 // GPU Nystrom setup (nystrom.hip) from gathered window coordinates xw (n x packed dims, host)
 int gemm_f64(bool transA, int M, int N, int K, const double* A, long long lda, const double* B, long long ldb,
-             double* C, long long ldc, const int* out_row, hipStream_t s);
+             double* C, long long ldc, hipStream_t s);
 int sym_eig_host(const std::vector<double>& A, int n, std::vector<double>& w, std::vector<double>& V);
 int chol_inverse_host(std::vector<double>& A, int k);
 NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int skip_last, int kernel, double f,

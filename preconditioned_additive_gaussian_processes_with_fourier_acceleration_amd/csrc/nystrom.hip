@@ -40,14 +40,18 @@ namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// ---- panel: Kp[jj + ii*n] = (f^2/nw) sum_c kern(|x_c[perm[jj]] - x_c[perm[ii]]|), jj < n, ii < k --------
+// ---- panel: Kp[jj + ii*n] = (f^2/nw) sum_c kern(|x_c[rperm[jj]] - x_c[cperm[ii]]|), jj < n, ii < k -------
+// rperm = NULL: rows in natural order.  The reference's panel rows are perm-ordered (nys.c:566-567); a
+// natural-order panel gives the same U1^T U1 (a sum over rows) and lands U in natural row order
+// directly, so the final product needs no row scatter and the apply reads U as stored.
 constexpr int kPanelRows = 64, kPanelCols = 64, kPanelThreads = 256;
 constexpr int kPanelMaxDims = 128;  // window dimensions summed over all windows (nw * dw)
 
 template <int KERNEL>  // 0 Gaussian exp(-r^2 / 2l^2), 1 Matern-1/2 exp(-r / l)
 __global__ __launch_bounds__(kPanelThreads) void k_nys_panel(const double* __restrict__ xw, int n, int nw, int dw,
-                                                             int last_dw, const int* __restrict__ perm, int k,
-                                                             double scale, double inv, double* __restrict__ Kp)
+                                                             int last_dw, const int* __restrict__ rperm,
+                                                             const int* __restrict__ cperm, int k, double scale,
+                                                             double inv, double* __restrict__ Kp)
 {
    extern __shared__ double sm[];
    const int D = (nw - 1) * dw + last_dw;
@@ -58,8 +62,8 @@ __global__ __launch_bounds__(kPanelThreads) void k_nys_panel(const double* __res
       const int t = e / kPanelRows, i = e % kPanelRows;
       const int w = min(t / dw, nw - 1), dd = t - w * dw;  // window w, its dimension dd
       const size_t col = (size_t)w * dw + dd;               // windows packed at stride n*dw (kernels.c:3160)
-      s_r[e] = (r0 + i < n) ? xw[col * n + perm[r0 + i]] : 0.0;
-      s_c[e] = (c0 + i < k) ? xw[col * n + perm[c0 + i]] : 0.0;
+      s_r[e] = (r0 + i < n) ? xw[col * n + (rperm ? rperm[r0 + i] : r0 + i)] : 0.0;
+      s_c[e] = (c0 + i < k) ? xw[col * n + cperm[c0 + i]] : 0.0;
    }
    __syncthreads();
    // thread -> 4 rows x 4 columns, rows fastest so stores are coalesced per column
@@ -102,109 +106,125 @@ __global__ __launch_bounds__(kPanelThreads) void k_nys_panel(const double* __res
 
 // ---- C = op(A) B on MFMA f64 ---------------------------------------------------------------------
 // op(A) is M x K: A column-major (lda) or, with TRANSA, A^T of a column-major K x M array.  B is K x N
-// column-major (ldb).  64 x 64 output tile per workgroup (4 waves, 32 x 32 each = 2 x 2 tiles of
-// v_mfma_f64_16x16x4_f64), K in steps of 16 through LDS.  gridDim.z > 1 splits K into chunks of
-// ksplit; chunk z writes its partial product at C + z * split_stride (summed by k_sum_splits).
-// out_row (optional) scatters output row r to row out_row[r].
-constexpr int kGemmTile = 64, kGemmK = 16, kGemmThreads = 256;
+// column-major (ldb).  128 x 128 output tile per workgroup: 4 waves in 2 x 2, each 64 x 64 = 4 x 4
+// blocks of v_mfma_f64_16x16x4_f64 (64 doubles of accumulator per lane).  K advances in steps of 16
+// through LDS; the next step's global loads are issued before the current step's 64 MFMAs per wave,
+// so their latency hides behind ~4k MFMA cycles.  The MFMA operands are swapped (B feeds the
+// A-operand slot) so a lane's accumulators hold 16 consecutive ROWS of C: every store instruction
+// writes 4 full 128-B column segments of the column-major C instead of 16 scattered 32-B pieces.
+// gridDim.z > 1 splits K into chunks of ksplit; chunk z writes its partial product at
+// C + z * split_stride (summed by k_sum_splits).  sym: C is symmetric (the Gram U^T U), only tiles
+// with tile_n <= tile_m are computed (k_sum_splits mirrors the rest).
+constexpr int kGemmTile = 128, kGemmK = 16, kGemmThreads = 256, kGemmPad = 1;
+constexpr int kGemmLd = kGemmTile + kGemmPad;
 
 template <bool TRANSA>
 __global__ __launch_bounds__(kGemmThreads) void k_gemm_f64(int M, int N, int K, const double* __restrict__ A,
                                                            long long lda, const double* __restrict__ B,
                                                            long long ldb, double* __restrict__ C, long long ldc,
-                                                           long long split_stride, int ksplit,
-                                                           const int* __restrict__ out_row)
+                                                           long long split_stride, int ksplit, int sym)
 {
-   __shared__ double As[kGemmK][kGemmTile + 1];  // As[kk][row]
-   __shared__ double Bs[kGemmK][kGemmTile + 1];  // Bs[kk][col]
+   if (sym && blockIdx.y > blockIdx.x) return;
+   __shared__ double As[kGemmK * kGemmLd];  // As[kk][row]
+   __shared__ double Bs[kGemmK * kGemmLd];  // Bs[kk][col]
    const int m0 = blockIdx.x * kGemmTile, n0 = blockIdx.y * kGemmTile;
    const int kbeg = blockIdx.z * ksplit, kend = min(K, kbeg + ksplit);
    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-   const int wr = (wave & 1) * 32, wc = (wave >> 1) * 32;
-   d4 acc[2][2];
+   const int wm = (wave & 1) * 64, wn = (wave >> 1) * 64;
+   constexpr int kPer = kGemmK * kGemmTile / kGemmThreads;  // 8 elements of each operand per thread
+   d4 acc[4][4];
 #pragma unroll
-   for (int i = 0; i < 2; i++)
+   for (int i = 0; i < 4; i++)
 #pragma unroll
-      for (int j = 0; j < 2; j++) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
-   for (int k0 = kbeg; k0 < kend; k0 += kGemmK) {
-      double av[4], bv[4];
+      for (int j = 0; j < 4; j++) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+   double av[kPer], bv[kPer];
+   auto fetch = [&](int k0) {
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < kPer; u++) {
          const int e = tid + u * kGemmThreads;
          int r, kk;
          if (!TRANSA) {
-            r = e & 63;
-            kk = e >> 6;
+            r = e & (kGemmTile - 1);
+            kk = e >> 7;
          } else {
-            kk = e & 15;
+            kk = e & (kGemmK - 1);
             r = e >> 4;
          }
          const int gr = m0 + r, gk = k0 + kk;
-         av[u] = (gr < M && gk < kend) ? (TRANSA ? A[gk + gr * lda] : A[gr + gk * lda]) : 0.0;
-         const int bk = e & 15, bc = e >> 4;
+         av[u] = (gr < M && gk < kend) ? (TRANSA ? A[gk + (long long)gr * lda] : A[gr + (long long)gk * lda]) : 0.0;
+         const int bk = e & (kGemmK - 1), bc = e >> 4;
          const int gbk = k0 + bk, gbc = n0 + bc;
-         bv[u] = (gbk < kend && gbc < N) ? B[gbk + gbc * ldb] : 0.0;
+         bv[u] = (gbk < kend && gbc < N) ? B[gbk + (long long)gbc * ldb] : 0.0;
       }
+   };
+   fetch(kbeg);
+   for (int k0 = kbeg; k0 < kend; k0 += kGemmK) {
+      __syncthreads();  // the previous step's LDS reads are done
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < kPer; u++) {
          const int e = tid + u * kGemmThreads;
          if (!TRANSA)
-            As[e >> 6][e & 63] = av[u];
+            As[(e >> 7) * kGemmLd + (e & (kGemmTile - 1))] = av[u];
          else
-            As[e & 15][e >> 4] = av[u];
-         Bs[e & 15][e >> 4] = bv[u];
+            As[(e & (kGemmK - 1)) * kGemmLd + (e >> 4)] = av[u];
+         Bs[(e & (kGemmK - 1)) * kGemmLd + (e >> 4)] = bv[u];
       }
       __syncthreads();
+      if (k0 + kGemmK < kend) fetch(k0 + kGemmK);  // in flight during this step's MFMAs
 #pragma unroll
       for (int k4 = 0; k4 < kGemmK / 4; k4++) {
          const int kk = 4 * k4 + (lane >> 4);
-         const double a0 = As[kk][wr + (lane & 15)], a1 = As[kk][wr + 16 + (lane & 15)];
-         const double b0 = Bs[kk][wc + (lane & 15)], b1 = Bs[kk][wc + 16 + (lane & 15)];
-         acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-         acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-         acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-         acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+         double a[4], b[4];
+#pragma unroll
+         for (int i = 0; i < 4; i++) a[i] = As[kk * kGemmLd + wm + 16 * i + (lane & 15)];
+#pragma unroll
+         for (int j = 0; j < 4; j++) b[j] = Bs[kk * kGemmLd + wn + 16 * j + (lane & 15)];
+#pragma unroll
+         for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(b[j], a[i], acc[i][j], 0, 0, 0);
       }
-      __syncthreads();
    }
-   // C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
+   // D map of v_mfma_f64_16x16x4_f64: D col = lane & 15 (B-operand index = row of C here),
+   // D row = (lane >> 4) + 4 * reg (A-operand index = column of C here)
    double* Cz = C + (size_t)blockIdx.z * split_stride;
 #pragma unroll
-   for (int i = 0; i < 2; i++)
+   for (int i = 0; i < 4; i++)
 #pragma unroll
-      for (int j = 0; j < 2; j++)
+      for (int j = 0; j < 4; j++)
 #pragma unroll
          for (int rg = 0; rg < 4; rg++) {
-            const int gr = m0 + wr + 16 * i + (lane >> 4) + 4 * rg;
-            const int gc = n0 + wc + 16 * j + (lane & 15);
-            if (gr < M && gc < N) {
-               const long long orow = out_row ? out_row[gr] : gr;
-               Cz[orow + gc * ldc] = acc[i][j][rg];
-            }
+            const int gr = m0 + wm + 16 * i + (lane & 15);
+            const int gc = n0 + wn + 16 * j + (lane >> 4) + 4 * rg;
+            if (gr < M && gc < N) Cz[gr + (long long)gc * ldc] = acc[i][j][rg];
          }
 }
 
-// C[i] = sum_z part[z * stride + i] in z order
+// C[i] = sum_z part[z * stride + i] in z order.  sym (square C of order ld): elements of tiles above the
+// tile diagonal were not computed and are read from the transposed position.
 __global__ void k_sum_splits(const double* __restrict__ part, int nsplit, long long stride, long long count,
-                             double* __restrict__ C)
+                             double* __restrict__ C, int sym, int ld)
 {
    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
    if (i >= count) return;
+   long long src = i;
+   if (sym) {
+      const long long r = i % ld, c = i / ld;
+      if (c / kGemmTile > r / kGemmTile) src = c + r * ld;
+   }
    double v = 0.0;
-   for (int z = 0; z < nsplit; z++) v += part[z * stride + i];
+   for (int z = 0; z < nsplit; z++) v += part[z * stride + src];
    C[i] = v;
 }
 
 int gemm(bool transA, int M, int N, int K, const double* A, long long lda, const double* B, long long ldb, double* C,
-         long long ldc, const int* out_row, hipStream_t s)
+         long long ldc, hipStream_t s)
 {
    dim3 grid((M + kGemmTile - 1) / kGemmTile, (N + kGemmTile - 1) / kGemmTile, 1);
    if (transA)
-      hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(kGemmThreads), 0, s, M, N, K, A, lda, B, ldb, C, ldc, 0LL, K,
-                         out_row);
+      hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(kGemmThreads), 0, s, M, N, K, A, lda, B, ldb, C, ldc, 0LL, K, 0);
    else
-      hipLaunchKernelGGL(k_gemm_f64<false>, grid, dim3(kGemmThreads), 0, s, M, N, K, A, lda, B, ldb, C, ldc, 0LL, K,
-                         out_row);
+      hipLaunchKernelGGL(k_gemm_f64<false>, grid, dim3(kGemmThreads), 0, s, M, N, K, A, lda, B, ldb, C, ldc, 0LL, K, 0);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -396,6 +416,14 @@ __global__ void k_nys_scale(const double* __restrict__ V, const double* __restri
    }
 }
 
+// K11[a + b k] = Kp[perm[a] + b n]
+__global__ void k_gather_rows(const double* __restrict__ Kp, long long n, const int* __restrict__ perm, int k,
+                              double* __restrict__ K11)
+{
+   const int a = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
+   if (a < k) K11[a + (size_t)b * k] = Kp[perm[a] + b * n];
+}
+
 __global__ void k_iota(int* p, int k)
 {
    const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -447,9 +475,9 @@ int dalloc(T** p, size_t count)
 }  // namespace
 
 int gemm_f64(bool transA, int M, int N, int K, const double* A, long long lda, const double* B, long long ldb,
-             double* C, long long ldc, const int* out_row, hipStream_t s)
+             double* C, long long ldc, hipStream_t s)
 {
-   return gemm(transA, M, N, K, A, lda, B, ldb, C, ldc, out_row, s);
+   return gemm(transA, M, N, K, A, lda, B, ldb, C, ldc, s);
 }
 
 int sym_eig_host(const std::vector<double>& A, int n, std::vector<double>& w, std::vector<double>& V)
@@ -510,6 +538,16 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
       }
       return nullptr;
    };
+   // hipEvents around the four big kernels (panel, gemm1, gram, gemm2) for the MFMA report
+   hipEvent_t ev[8];
+   for (auto& e : ev) (void)hipEventCreate(&e);
+   struct EvGuard {
+      hipEvent_t* e;
+      ~EvGuard()
+      {
+         for (int i = 0; i < 8; i++) (void)hipEventDestroy(e[i]);
+      }
+   } ev_guard{ev};
    const size_t nk = (size_t)n * k;
    if (dalloc(&d_xw, (size_t)n * nw * dw) || dalloc(&d_perm, (size_t)n) || dalloc(&d_info, 1) || dalloc(&d_Kp, nk) ||
        dalloc(&d_U1, nk) || dalloc(&d_B, (size_t)k * k) || dalloc(&d_AA, (size_t)k * k))
@@ -523,13 +561,15 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    const double inv = (kernel == 0) ? 1.0 / (2.0 * l * l) : 1.0 / l;
    const size_t lds = sizeof(double) * (size_t)D * (kPanelRows + kPanelCols);
    dim3 pgrid((n + kPanelRows - 1) / kPanelRows, (k + kPanelCols - 1) / kPanelCols);
+   (void)hipEventRecord(ev[0], s);
    if (kernel == 0)
-      hipLaunchKernelGGL(k_nys_panel<0>, pgrid, dim3(kPanelThreads), lds, s, d_xw, n, nw, dw, last_dw, d_perm, k,
-                         f2 / nw, inv, d_Kp);
+      hipLaunchKernelGGL(k_nys_panel<0>, pgrid, dim3(kPanelThreads), lds, s, d_xw, n, nw, dw, last_dw,
+                         (const int*)nullptr, d_perm, k, f2 / nw, inv, d_Kp);
    else
-      hipLaunchKernelGGL(k_nys_panel<1>, pgrid, dim3(kPanelThreads), lds, s, d_xw, n, nw, dw, last_dw, d_perm, k,
-                         f2 / nw, inv, d_Kp);
+      hipLaunchKernelGGL(k_nys_panel<1>, pgrid, dim3(kPanelThreads), lds, s, d_xw, n, nw, dw, last_dw,
+                         (const int*)nullptr, d_perm, k, f2 / nw, inv, d_Kp);
    if (hipGetLastError() != hipSuccess) return fail("panel launch");
+   (void)hipEventRecord(ev[1], s);
 
    phase("panel");
    // 2. K11 on the device: the landmark block of the panel (mode 1), or the reference's K11 (mode 0:
@@ -538,18 +578,18 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    //    panel kernel over that buffer with n = k and the identity permutation)
    if (dalloc(&d_K11, (size_t)k * k) || dalloc(&d_iota, (size_t)k)) return fail("allocation");
    if (k11_mode == 1) {
-      if (hipMemcpy2DAsync(d_K11, sizeof(double) * k, d_Kp, sizeof(double) * n, sizeof(double) * k, k,
-                           hipMemcpyDeviceToDevice, s) != hipSuccess)
-         return fail("K11 copy");
+      // the landmark rows perm[:k] of the natural-order panel
+      hipLaunchKernelGGL(k_gather_rows, dim3((k + 255) / 256, k), dim3(256), 0, s, d_Kp, (long long)n, d_perm, k,
+                         d_K11);
    } else {
       hipLaunchKernelGGL(k_iota, dim3((k + 255) / 256), dim3(256), 0, s, d_iota, k);
       dim3 kgrid((k + kPanelRows - 1) / kPanelRows, (k + kPanelCols - 1) / kPanelCols);
       if (kernel == 0)
-         hipLaunchKernelGGL(k_nys_panel<0>, kgrid, dim3(kPanelThreads), lds, s, d_xw, k, nw, dw, last_dw, d_iota, k,
-                            f2 / nw, inv, d_K11);
+         hipLaunchKernelGGL(k_nys_panel<0>, kgrid, dim3(kPanelThreads), lds, s, d_xw, k, nw, dw, last_dw,
+                            (const int*)nullptr, d_iota, k, f2 / nw, inv, d_K11);
       else
-         hipLaunchKernelGGL(k_nys_panel<1>, kgrid, dim3(kPanelThreads), lds, s, d_xw, k, nw, dw, last_dw, d_iota, k,
-                            f2 / nw, inv, d_K11);
+         hipLaunchKernelGGL(k_nys_panel<1>, kgrid, dim3(kPanelThreads), lds, s, d_xw, k, nw, dw, last_dw,
+                            (const int*)nullptr, d_iota, k, f2 / nw, inv, d_K11);
    }
    // stable shift nu = sqrt(k) ulp(|K11|_F) (chol.c:449-465; dlansy 'F' 'L' = the full-matrix norm)
    std::vector<double> K11((size_t)k * k);
@@ -595,7 +635,9 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
 
    phase("k11+chol");
    // 3. U1 = Kp G^T  (dtrmm 'R' 'L' 'T', matops.c Nfft4GPTrilNystromMm)
-   if (gemm(false, n, k, k, d_Kp, n, d_B, k, d_U1, n, nullptr, s)) return fail("gemm");
+   (void)hipEventRecord(ev[2], s);
+   if (gemm(false, n, k, k, d_Kp, n, d_B, k, d_U1, n, s)) return fail("gemm");
+   (void)hipEventRecord(ev[3], s);
 
    phase("gemm1");
    // 4. AA = U1^T U1, K = n split over row chunks (fixed order sum -> deterministic)
@@ -604,13 +646,15 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    const int nsplit_used = (n + ksplit - 1) / ksplit;
    if (dalloc(&d_part, (size_t)nsplit_used * k * k)) return fail("allocation");
    {
+      (void)hipEventRecord(ev[4], s);
       dim3 grid((k + kGemmTile - 1) / kGemmTile, (k + kGemmTile - 1) / kGemmTile, nsplit_used);
       hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(kGemmThreads), 0, s, k, k, n, d_U1, (long long)n, d_U1,
-                         (long long)n, d_part, (long long)k, (long long)k * k, ksplit, (const int*)nullptr);
+                         (long long)n, d_part, (long long)k, (long long)k * k, ksplit, 1);
       const long long cnt = (long long)k * k;
       hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, d_part, nsplit_used, cnt,
-                         cnt, d_AA);
+                         cnt, d_AA, 1, k);
       if (hipGetLastError() != hipSuccess) return fail("gram launch");
+      (void)hipEventRecord(ev[5], s);
    }
    phase("gram");
    // 5. eig(AA) = V diag(w1) V^T (dsyev: ascending); W = V(:, reversed) diag(w1^-1/2) with the
@@ -642,13 +686,19 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    N->k = k;
    N->U = d_Kp;  // the panel's storage is reused for U (rows scattered back to natural order)
    d_Kp = nullptr;
-   if (gemm(false, n, k, k, d_U1, n, d_B, k, N->U, n, d_perm, s)) return fail("gemm");
+   (void)hipEventRecord(ev[6], s);
+   if (gemm(false, n, k, k, d_U1, n, d_B, k, N->U, n, s)) return fail("gemm");
+   (void)hipEventRecord(ev[7], s);
    N->eta = eta;
    N->s = d_s;
    d_s = nullptr;
    if (nys_alloc_scratch(N)) return fail("allocation");
    if (hipStreamSynchronize(s) != hipSuccess) return fail("sync");
    phase("gemm2");
+   for (int i = 0; i < 4; i++) {
+      float ms = 0.0f;
+      if (hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]) == hipSuccess) N->setup_ms[i] = ms;
+   }
    release();
    return N;
 }
@@ -656,6 +706,14 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
 }  // namespace nfft4gp_amd
 
 extern "C" {
+
+int Nfft4GPAmdNysSetupTimes(void* nys, double* ms4)
+{
+   nfft4gp_amd::NysDev* N = (nfft4gp_amd::NysDev*)nys;
+   if (!N || !ms4) return -1;
+   for (int i = 0; i < 4; i++) ms4[i] = N->setup_ms[i];
+   return 0;
+}
 
 int Nfft4GPAmdNysFactors(void* nys, const int* perm, double* U, double* s, double* eta)
 {
@@ -699,7 +757,7 @@ extern "C" int Nfft4GPAmdHostCholInverse(const double* A, int k, double shift, d
 extern "C" int Nfft4GPAmdDebugGemm(int transA, int M, int N, int K, const double* A, long long lda, const double* B,
                                    long long ldb, double* C, long long ldc)
 {
-   if (nfft4gp_amd::gemm_f64(transA != 0, M, N, K, A, lda, B, ldb, C, ldc, nullptr, nfft4gp_amd::current_stream()))
+   if (nfft4gp_amd::gemm_f64(transA != 0, M, N, K, A, lda, B, ldb, C, ldc, nfft4gp_amd::current_stream()))
       return -1;
    NFFT4GP_HIP_CHECK(hipStreamSynchronize(nfft4gp_amd::current_stream()));
    return 0;

@@ -300,44 +300,80 @@ int elem_grid(size_t n)
 // ---------------------------------------------------------------------------------------------
 constexpr int kNysThreads = 256;
 
-// partial[blk][j] = sum_{i in blk rows} U[i, j] r[i]; one wave per column at a time, the block's
-// r segment kept in registers (kNysRows/64 = 32 values per lane)
+// partial[blk][j] = sum_{i in blk rows} U[i, j] r[i].  The block's r segment is staged in LDS; each
+// wave walks its columns four at a time with 32 loads per lane in flight, row indices clamped to
+// n - 1 (and r zero-padded) so the loads need no predication.
+constexpr int kNysUtCols = 4;
 __global__ __launch_bounds__(kNysThreads) void k_nys_ut(const double* __restrict__ U, size_t ldu, int n, int k,
                                                        const double* __restrict__ r, double* __restrict__ part)
 {
    constexpr int kPer = kNysRows / 64;
+   constexpr int kChunk = 8;
+   __shared__ double s_r[kNysRows];
    const int lane = threadIdx.x & 63;
    const int wave = threadIdx.x >> 6;
-   const int nw = kNysThreads / 64;
+   const int nwv = kNysThreads / 64;
    const size_t r0 = (size_t)blockIdx.x * kNysRows;
-   double rv[kPer];
-#pragma unroll
-   for (int t = 0; t < kPer; t++) {
-      const size_t i = r0 + (size_t)t * 64 + lane;
-      rv[t] = (i < (size_t)n) ? r[i] : 0.0;
+   for (int t = threadIdx.x; t < kNysRows; t += kNysThreads) {
+      const size_t i = r0 + t;
+      s_r[t] = (i < (size_t)n) ? r[i] : 0.0;
    }
-   for (int j = wave; j < k; j += nw) {
-      const double* col = U + (size_t)j * ldu;
-      double acc = 0.0;
+   __syncthreads();
+   const size_t last = (size_t)n - 1;
+   for (int j0 = wave * kNysUtCols; j0 < k; j0 += nwv * kNysUtCols) {
+      const double* col[kNysUtCols];
 #pragma unroll
-      for (int t = 0; t < kPer; t++) {
-         const size_t i = r0 + (size_t)t * 64 + lane;
-         if (i < (size_t)n) acc = fma(col[i], rv[t], acc);
+      for (int c = 0; c < kNysUtCols; c++) col[c] = U + (size_t)min(j0 + c, k - 1) * ldu;
+      double acc[kNysUtCols] = {};
+#pragma unroll
+      for (int t = 0; t < kPer; t += kChunk) {
+         double v[kNysUtCols][kChunk];
+#pragma unroll
+         for (int c = 0; c < kNysUtCols; c++)
+#pragma unroll
+            for (int u = 0; u < kChunk; u++) {
+               const size_t i = r0 + (size_t)(t + u) * 64 + lane;
+               v[c][u] = __builtin_nontemporal_load(col[c] + (i < last ? i : last));
+            }
+#pragma unroll
+         for (int u = 0; u < kChunk; u++) {
+            const double rr = s_r[(t + u) * 64 + lane];
+#pragma unroll
+            for (int c = 0; c < kNysUtCols; c++) acc[c] = fma(v[c][u], rr, acc[c]);
+         }
       }
-      for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
-      if (lane == 0) part[(size_t)blockIdx.x * k + j] = acc;
+#pragma unroll
+      for (int c = 0; c < kNysUtCols; c++) {
+         double a = acc[c];
+         for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off, 64);
+         if (lane == 0 && j0 + c < k) part[(size_t)blockIdx.x * k + j0 + c] = a;
+      }
    }
 }
 
-// w[j] = (s[j] - 1/eta) * sum_blk part[blk][j]
-__global__ void k_nys_w(const double* __restrict__ part, int nblk, int k, const double* __restrict__ s, double eta,
-                        double* __restrict__ w)
+// w[j] = (s[j] - 1/eta) * sum_blk part[blk][j].  A workgroup owns 64 columns; its 16 wave-rows
+// each sum every 16th block (coalesced over j), then one fixed-order pass over the 16 sums.
+constexpr int kNysWRows = 16;
+__global__ __launch_bounds__(64 * kNysWRows) void k_nys_w(const double* __restrict__ part, int nblk, int k,
+                                                          const double* __restrict__ s, double eta,
+                                                          double* __restrict__ w)
 {
-   const int j = blockIdx.x * blockDim.x + threadIdx.x;
-   if (j >= k) return;
-   double z = 0.0;
-   for (int b = 0; b < nblk; b++) z += part[(size_t)b * k + j];
-   w[j] = s[j] * z - z / eta;
+   __shared__ double s_sum[kNysWRows][64];
+   const int lane = threadIdx.x & 63;
+   const int g = threadIdx.x >> 6;
+   const int j = blockIdx.x * 64 + lane;
+   const int jj = j < k ? j : k - 1;
+   double z[4] = {};
+   int b = g, u = 0;
+   for (; b < nblk; b += kNysWRows, u = (u + 1) & 3) z[u] += part[(size_t)b * k + jj];
+   s_sum[g][lane] = (z[0] + z[1]) + (z[2] + z[3]);
+   __syncthreads();
+   if (g == 0 && j < k) {
+      double t = 0.0;
+#pragma unroll
+      for (int q = 0; q < kNysWRows; q++) t += s_sum[q][lane];
+      w[j] = s[j] * t - t / eta;
+   }
 }
 
 // x[i] = r[i]/eta + sum_j U[i, j] w[j]
@@ -741,7 +777,7 @@ int Nfft4GPAmdNysSolve(void* nys, int n, double* x, double* rhs)
    Vec vx, vr;
    if (vx.open(x, n, false) || vr.open(rhs, n, true)) return -1;
    hipLaunchKernelGGL(k_nys_ut, dim3(N->nblk), dim3(kNysThreads), 0, s, N->U, (size_t)n, n, N->k, vr.d, N->part);
-   hipLaunchKernelGGL(k_nys_w, dim3((N->k + 255) / 256), dim3(256), 0, s, N->part, N->nblk, N->k, N->s, N->eta, N->w);
+   hipLaunchKernelGGL(k_nys_w, dim3((N->k + 63) / 64), dim3(64 * kNysWRows), 0, s, N->part, N->nblk, N->k, N->s, N->eta, N->w);
    hipLaunchKernelGGL(k_nys_u, dim3((n + kNysThreads - 1) / kNysThreads), dim3(kNysThreads),
                       sizeof(double) * N->k, s, N->U, (size_t)n, n, N->k, N->w, vr.d, N->eta, vx.d);
    NFFT4GP_HIP_CHECK(hipGetLastError());

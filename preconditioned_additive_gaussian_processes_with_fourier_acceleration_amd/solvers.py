@@ -45,6 +45,12 @@ class NystromPrecond:
         self.eta = eta.value
         return self
 
+    def setup_times(self):
+        """hipEvent ms of the GPU setup's panel, U1 = Kp G^T, Gram U1^T U1 and U = U1 W kernels."""
+        ms = np.zeros(4)
+        _lib.lib().Nfft4GPAmdNysSetupTimes(self.h, ms.ctypes.data)
+        return {"panel": ms[0], "gemm1": ms[1], "gram": ms[2], "gemm2": ms[3]}
+
     def factors(self, perm=None):
         """(U, s, eta) with U's rows in the order of ``perm`` (the reference keeps them permuted)."""
         U = np.zeros((self.n, self.k), order="F")

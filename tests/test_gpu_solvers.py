@@ -215,3 +215,25 @@ def test_gpu_nystrom_landmarks_matches_numpy(torch_cuda, kernel, l):
     np.testing.assert_allclose(s, s_r, rtol=1e-7)
     sign = np.sign(np.sum(U * Ur, axis=0))
     np.testing.assert_allclose(U * sign, Ur, rtol=0, atol=1e-7 * np.abs(Ur).max())
+
+
+@pytest.mark.parametrize("tA,M,N,K", [(0, 128, 128, 16), (0, 300, 200, 37), (0, 1000, 512, 512),
+                                      (1, 128, 128, 16), (1, 130, 70, 300), (1, 256, 256, 4099)])
+def test_mfma_gemm_f64_ragged(torch_cuda, tA, M, N, K):
+    """The MFMA f64 GEMM behind the Nystrom setup (128 x 128 tiles, K steps of 16, swapped operands)
+    on ragged shapes in both A layouts, against numpy."""
+    import ctypes as C
+    torch = torch_cuda
+    f = amd.lib().Nfft4GPAmdDebugGemm
+    f.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_longlong, C.c_void_p, C.c_longlong,
+                  C.c_void_p, C.c_longlong]
+    rng = np.random.default_rng(M + N + K)
+    A = rng.standard_normal((K, M) if tA else (M, K))
+    Bm = rng.standard_normal((K, N))
+    ref = (A.T if tA else A) @ Bm
+    Ad = torch.tensor(A.ravel(order="F"), device="cuda")
+    Bd = torch.tensor(Bm.ravel(order="F"), device="cuda")
+    Cd = torch.full((M * N,), np.nan, dtype=torch.float64, device="cuda")
+    assert f(tA, M, N, K, Ad.data_ptr(), A.shape[0], Bd.data_ptr(), K, Cd.data_ptr(), M) == 0
+    Cm = Cd.cpu().numpy().reshape(N, M).T
+    assert np.abs(Cm - ref).max() <= 1e-12 * np.sqrt(K) * np.abs(ref).max()
