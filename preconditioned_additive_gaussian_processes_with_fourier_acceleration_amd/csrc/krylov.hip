@@ -134,6 +134,121 @@ __global__ void k_sub(double* __restrict__ y, const double* __restrict__ a, cons
       y[i] = a[i] - b[i];
 }
 
+// ---- block (classical) Gram-Schmidt passes for the Lanczos re-orthogonalisation -------------------
+// One pass = two launches over the whole basis: h = V^T w (kBD basis vectors per workgroup, every
+// block's partials reduced in a fixed order), then w -= Z h with ||w||^2 fused.  This reads the basis
+// twice per pass instead of streaming w, z_i and v_i once per basis vector (MGS: 4 vectors moved per
+// projection): 2x fewer bytes and 2 launches instead of k + 2.
+constexpr int kBD = 8;
+constexpr int kBDThreads = 256;
+constexpr int kBDMaxBlocks = 512;
+
+int bd_grid(size_t n)
+{
+   size_t g = (n + (size_t)kBDThreads * 16 - 1) / ((size_t)kBDThreads * 16);
+   return (int)std::max<size_t>(1, std::min<size_t>(g, kBDMaxBlocks));
+}
+
+// part[blockIdx.x * ldp + i] = sum over this block's rows r of w[r] V[i n + r], i in [g0, g0 + kBD) & < m;
+// with_norm: column m is w itself (part[.. + m] sums ||w||^2)
+__global__ __launch_bounds__(kBDThreads) void k_block_dots(const double* __restrict__ w, const double* __restrict__ V,
+                                                           size_t n, int m, int with_norm, double* __restrict__ part,
+                                                           int ldp)
+{
+   __shared__ double s[kBDThreads / 64][kBD];
+   const int g0 = blockIdx.y * kBD;
+   const int cnt = min(kBD, m + with_norm - g0);
+   const int nv = m - g0;  // columns of this group that come from V; the next one (if counted) is w
+   double acc[kBD];
+#pragma unroll
+   for (int j = 0; j < kBD; j++) acc[j] = 0.0;
+   const size_t stride = (size_t)gridDim.x * kBDThreads;
+   for (size_t r = (size_t)blockIdx.x * kBDThreads + threadIdx.x; r < n; r += stride) {
+      const double wr = w[r];
+      double v[kBD];
+#pragma unroll
+      for (int j = 0; j < kBD; j++) v[j] = j < nv && j < cnt ? V[(size_t)(g0 + j) * n + r] : (j < cnt ? wr : 0.0);
+#pragma unroll
+      for (int j = 0; j < kBD; j++) acc[j] = fma(v[j], wr, acc[j]);
+   }
+   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+   for (int j = 0; j < kBD; j++) {
+      double a = acc[j];
+      for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off, 64);
+      if (lane == 0) s[wave][j] = a;
+   }
+   __syncthreads();
+   if (threadIdx.x < cnt) {
+      double t = 0.0;
+#pragma unroll
+      for (int q = 0; q < kBDThreads / 64; q++) t += s[q][threadIdx.x];
+      part[(size_t)blockIdx.x * ldp + g0 + threadIdx.x] = t;
+   }
+}
+
+// h[i] = sum_b part[b ldp + i] (fixed order: 16 strands over blocks b = g mod 16, then the strands) for
+// i < m; column i = m (the norm column of k_block_dots, when mc = m + 1) lands in h[m + 1]
+__global__ __launch_bounds__(1024) void k_block_reduce(const double* __restrict__ part, int nblk, int ldp, int mc,
+                                                      int m, double* __restrict__ h)
+{
+   __shared__ double s_sum[16][64];
+   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+   const int i = blockIdx.x * 64 + lane;
+   const int ii = i < mc ? i : mc - 1;
+   double z[4] = {0.0, 0.0, 0.0, 0.0};
+   int u = 0;
+   for (int b = g; b < nblk; b += 16, u = (u + 1) & 3) z[u] += part[(size_t)b * ldp + ii];
+   s_sum[g][lane] = (z[0] + z[1]) + (z[2] + z[3]);
+   __syncthreads();
+   if (g == 0 && i < mc) {
+      double t = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; q++) t += s_sum[q][lane];
+      h[i < m ? i : m + 1] = t;
+   }
+}
+
+// w -= sum_{j < m} h[j] Z[j n + .] (j in order), then *out = ||w||^2 (fixed-order grid reduction)
+__global__ __launch_bounds__(kKThreads) void k_block_update(double* __restrict__ w, const double* __restrict__ Z,
+                                                            size_t n, const double* __restrict__ h, int m,
+                                                            double* __restrict__ part,
+                                                            unsigned int* __restrict__ ticket,
+                                                            double* __restrict__ out)
+{
+   extern __shared__ double s_h[];
+   for (int j = threadIdx.x; j < m; j += kKThreads) s_h[j] = h[j];
+   __syncthreads();
+   double acc = 0.0;
+   const size_t stride = (size_t)gridDim.x * kKThreads * kKEPT;
+   for (size_t i0 = (size_t)blockIdx.x * kKThreads * kKEPT + threadIdx.x; i0 < n; i0 += stride) {
+      double wv[kKEPT];
+#pragma unroll
+      for (int e = 0; e < kKEPT; e++) {
+         const size_t i = i0 + (size_t)e * kKThreads;
+         wv[e] = i < n ? w[i] : 0.0;
+      }
+      for (int j = 0; j < m; j++) {
+         const double hj = s_h[j];
+         const double* zj = Z + (size_t)j * n;
+#pragma unroll
+         for (int e = 0; e < kKEPT; e++) {
+            const size_t i = i0 + (size_t)e * kKThreads;
+            wv[e] = fma(-hj, i < n ? zj[i] : 0.0, wv[e]);
+         }
+      }
+#pragma unroll
+      for (int e = 0; e < kKEPT; e++) {
+         const size_t i = i0 + (size_t)e * kKThreads;
+         if (i < n) w[i] = wv[e];
+         acc = fma(wv[e], wv[e], acc);
+      }
+   }
+   acc = block_sum0<kKThreads>(acc);
+   double tot;
+   if (grid_total<kKThreads>(acc, part, ticket, &tot) && threadIdx.x == 0) *out = tot;
+}
+
 int egrid(size_t n)
 {
    size_t g = (n + 255) / 256;
@@ -144,7 +259,13 @@ int egrid(size_t n)
 struct KScratch {
    static constexpr int kScal = 4096;
    double *part = nullptr, *part2 = nullptr, *scal = nullptr, *hscal = nullptr, *coef = nullptr;
+   double* bpart = nullptr;  // block Gram-Schmidt partials [kBDMaxBlocks][kScal]
    unsigned int *ticket = nullptr, *ticket2 = nullptr;
+   int ensure_bpart()
+   {
+      if (!bpart) NFFT4GP_HIP_CHECK(hipMalloc((void**)&bpart, sizeof(double) * kBDMaxBlocks * kScal));
+      return 0;
+   }
    int ensure()
    {
       if (part) return 0;
@@ -188,6 +309,23 @@ struct Ctx {
       return v;
    }
    double norm(const double* a) { return std::sqrt(dot(a, a)); }
+   // one classical Gram-Schmidt pass: h[0..m) = V^T w, w -= Z h, h[m] = ||w||^2 afterwards (device
+   // scalars); with_norm: also h[m + 1] = ||w||^2 before the update (from the dot pass)
+   int block_gs(double* w, const double* V, const double* Z, int m, double* h, int with_norm = 0)
+   {
+      if (m <= 0 || m + 2 > KScratch::kScal) return -1;
+      if (g_k.ensure_bpart()) return -1;
+      const int nb = bd_grid(n);
+      const int mc = m + with_norm;
+      hipLaunchKernelGGL(k_block_dots, dim3(nb, (mc + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m, with_norm,
+                         g_k.bpart, KScratch::kScal);
+      hipLaunchKernelGGL(k_block_reduce, dim3((mc + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, mc, m,
+                         h);
+      hipLaunchKernelGGL(k_block_update, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, Z, n, h, m,
+                         g_k.part, g_k.ticket, h + m);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   }
    void scale(double* a, double* b, double f)
    {
       hipLaunchKernelGGL(k_scale2, dim3(egrid(n)), dim3(256), 0, s, a, b, n, f);
@@ -386,20 +524,22 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
 }
 
 // ---- Lanczos (lanczos.c:3-419) on device vectors ----------------------------------------------------
-// MGS2 (matops.c:348-440) of w against V[0..k] (dots) / Z[0..k] (updates), re-orthogonalised while
-// ||w|| < 0.7071 * its previous norm; returns ||w|| and adds the last two projections to td / te
+// Re-orthogonalisation of w against V[0..k] (dots) / Z[0..k] (updates), repeated while ||w|| < 0.7071 *
+// its previous norm and >= eps, adding the last two projections to td / te (Nfft4GPModifiedGS2,
+// matops.c:348-440).  Each pass is a block classical Gram-Schmidt step (Ctx::block_gs) rather than the
+// reference's vector-by-vector MGS: the repeat-while-the-norm-drops rule is the "twice is enough"
+// criterion that makes the classical form as orthogonal as MGS, and a pass then moves the basis twice
+// instead of four vectors per basis vector.  Projections differ from MGS's only by rounding.
 static int mgs2(Ctx& c, double* w, const double* V, const double* Z, int k, double* td, double* te, double* t)
 {
-   const size_t n = c.n;
-   double normw = c.norm(w);
+   double normw = 0.0;
    double* hd = g_k.scal;
    for (int pass = 0;; pass++) {
-      for (int i = 0; i <= k; i++)
-         if (c.gs(w, i ? Z + (size_t)(i - 1) * n : nullptr, i ? hd + i - 1 : nullptr, V + (size_t)i * n, hd + i))
-            return -1;
-      if (c.gs(w, Z + (size_t)k * n, hd + k, nullptr, hd + k + 1)) return -1;
-      std::vector<double> h(k + 2);
-      if (c.read(hd, k + 2, h.data())) return -1;
+      // the first pass also returns ||w|| before the projections (hd[k + 2])
+      if (c.block_gs(w, V, Z, k + 1, hd, pass == 0)) return -1;
+      std::vector<double> h(k + 3);
+      if (c.read(hd, pass == 0 ? k + 3 : k + 2, h.data())) return -1;
+      if (pass == 0) normw = std::sqrt(h[k + 2]);
       if (pass == 0) {
          if (k >= 1 && te) *te = h[k - 1];
          if (td) *td = h[k];

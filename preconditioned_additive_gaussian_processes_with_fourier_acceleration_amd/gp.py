@@ -25,26 +25,37 @@ _PREDICT_ARGS = [_vp, _vp, _vp, C.c_int, C.c_int, C.c_int, _vp, C.c_int, C.c_int
 
 
 def gp_loss(X, windows, nwindows, dwindows, y, hyper, maxits=50, nvecs=10, rademacher=None, tol=1e-6,
-            transform=0, mask=None, print_level=-1):
+            transform=0, mask=None, print_level=-1, op=None):
     """(loss, grad) of Nfft4GPGpLoss for the additive NFFT Gaussian kernel; ``hyper`` = (f, l, mu) before
-    the transform (0 softplus, 1 sigmoid, 2 exp, 3 identity)."""
+    the transform (0 softplus, 1 sigmoid, 2 exp, 3 identity).  ``op``: an existing NFFTAdditiveKernel over
+    the same X to reuse, as the reference's optimizer loop reuses its kernel handle across loss calls
+    (its points, centring and scale stay those of its first setup, nfft_interface.c:150)."""
     X = np.asfortranarray(np.asarray(X, dtype=np.float64))
     n, d = X.shape
-    op = NFFTAdditiveKernel(X, windows, nwindows, dwindows)
+    if op is None:
+        op = NFFTAdditiveKernel(X, windows, nwindows, dwindows)
+    elif op.n != n:
+        raise ValueError("op was created over a different number of points")
     L = _lib.lib()
     fn = L.Nfft4GPGpLoss
     fn.argtypes = _GPLOSS_ARGS
     fn.restype = C.c_int
     x = np.ascontiguousarray(np.asarray(hyper, dtype=np.float64))
     lab = np.ascontiguousarray(np.asarray(y, dtype=np.float64))
-    R = None if rademacher is None else np.asfortranarray(np.asarray(rademacher, dtype=np.float64))
+    if rademacher is None:
+        R, r_ptr = None, None
+    elif hasattr(rademacher, "data_ptr"):  # a torch tensor (n * nvecs, column-major probes); device OK
+        R, r_ptr = rademacher, rademacher.data_ptr()
+    else:
+        R = np.asfortranarray(np.asarray(rademacher, dtype=np.float64))
+        r_ptr = R.ctypes.data
     m = None if mask is None else np.ascontiguousarray(np.asarray(mask, dtype=np.int32))
     loss = np.zeros(1)
     grad = np.zeros(3)
     rc = fn(x.ctypes.data, X.ctypes.data, lab.ctypes.data, n, n, d,
             _lib.fnptr("Nfft4GPNFFTAdditiveKernelGaussianKernel"), op.h, None, op.matvec_fnptr, op.gradmatvec_fnptr,
             None, None, None, None, None, None, None, None, None, None, 0, float(tol), int(maxits), int(maxits),
-            int(nvecs), R.ctypes.data if R is not None else None, int(transform),
+            int(nvecs), r_ptr, int(transform),
             m.ctypes.data if m is not None else None, int(print_level), None, loss.ctypes.data_as(_lib.dp),
             grad.ctypes.data_as(_lib.dp))
     if rc:
