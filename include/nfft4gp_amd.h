@@ -242,6 +242,32 @@ int Nfft4GPAmdNysFactors(void *nys, const int *perm, NFFT4GP_DOUBLE *U, NFFT4GP_
  * U = U1 W (the three MFMA products, 2 n k^2 flops each); zeros for a handle from Nfft4GPAmdNysCreate */
 int Nfft4GPAmdNysSetupTimes(void *nys, NFFT4GP_DOUBLE *ms4);
 
+/* ---- Nystrom preconditioner with gradients, the reference's interface (SRC/preconds/nys.h:62-179) -----
+ * Drop-ins for Nfft4GPPrecondNysCreate / Free / Reset / SetRank / SetPerm (nys.c:3-113),
+ * Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660, a precond_kernel_setup), Nfft4GPPrecondNysSolve
+ * (func_solve, nys.c:115-173), Nfft4GPPrecondNysDvp (func_dvp, nys.c:175-330), Nfft4GPPrecondNysTrace
+ * (func_trace, nys.c:332-474) and Nfft4GPPrecondNysLogdet (func_logdet, nys.c:476-500), for
+ * Nfft4GPGpLoss's precond_* arguments (gp_loss.c:96-307).  The setup's fkernel must be this library's
+ * Nfft4GPNFFTAdditiveKernelGaussianKernel / ...Matern12Kernel and fkernel_params an additive handle of this
+ * library (its gathered windows _buffer and _params / _noise_level play the role of the reference's dense
+ * additive kernel data, kernels.c:3099-3494; the reference's own Nfft4GPKernelAdditiveKernel is not part of
+ * this library).  Factors, panels and gradients stay in HBM; Solve / Dvp take host or device vectors
+ * (Dvp allocates *yp like the reference when it is NULL, on the side x lives on).
+ * Nfft4GPAmdPrecondNysSetK11Mode: 0 (default) = the reference's K11 (see Nfft4GPAmdNysSetupAdditive),
+ * 1 = K(perm[:k], perm[:k]) with the gradient panels over every window. */
+void *Nfft4GPAmdPrecondNysCreate(void);
+void Nfft4GPAmdPrecondNysFree(void *str);
+void Nfft4GPAmdPrecondNysReset(void *str);
+void Nfft4GPAmdPrecondNysSetRank(void *str, int k);
+void Nfft4GPAmdPrecondNysSetPerm(void *str, int *perm, int own_perm);
+void Nfft4GPAmdPrecondNysSetK11Mode(void *str, int mode);
+int Nfft4GPAmdPrecondNysSetupWithKernel(NFFT4GP_DOUBLE *data, int n, int ldim, int d, func_kernel fkernel,
+                                        void *fkernel_params, int require_grad, void *vnys_mat);
+int Nfft4GPAmdPrecondNysSolve(void *vnys_mat, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
+int Nfft4GPAmdPrecondNysDvp(void *vnys_mat, int n, int *mask, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE **yp);
+int Nfft4GPAmdPrecondNysTrace(void *vnys_mat, NFFT4GP_DOUBLE **tracesp);
+NFFT4GP_DOUBLE Nfft4GPAmdPrecondNysLogdet(void *vnys_mat);
+
 /* ---- FSAI preconditioner apply (SRC/preconds/fsai.c:106-123) --------------------------------------
  * The reference's Nfft4GPPrecondFsaiSetupWithKernel (fsai.c:333-...) produces the lower-triangular
  * factor L in CSR (precond_fsai _L_i, _L_j, _L_a; fsai.h:11-58).  Nfft4GPAmdFsaiCreate takes those

@@ -170,6 +170,10 @@ def ref_lib():
         lib.Nfft4GPPrecondNysSetupWithKernel.argtypes = [_dp, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                                          C.c_void_p, C.c_int, C.c_void_p]
         lib.Nfft4GPPrecondNysSolve.argtypes = [C.c_void_p, C.c_int, _dp, _dp]
+        lib.Nfft4GPPrecondNysDvp.argtypes = [C.c_void_p, C.c_int, _ip, _dp, C.POINTER(_dp)]
+        lib.Nfft4GPPrecondNysTrace.argtypes = [C.c_void_p, C.POINTER(_dp)]
+        lib.Nfft4GPPrecondNysLogdet.argtypes = [C.c_void_p]
+        lib.Nfft4GPPrecondNysLogdet.restype = C.c_double
         _rlib = lib
     return _rlib
 
@@ -272,9 +276,10 @@ class PrecondNysStruct(C.Structure):
 
 
 class RefNystrom:
-    """Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660) on the reference's dense additive kernel."""
+    """Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660) on the reference's dense additive kernel; with
+    grad=True (require_grad) also its Dvp / Trace / Logdet (nys.c:175-516)."""
 
-    def __init__(self, dense: "RefDenseAdditive", f, l, mu, k, perm):
+    def __init__(self, dense: "RefDenseAdditive", f, l, mu, k, perm, grad=False):
         lib = ref_lib()
         self.lib = lib
         st = dense.st
@@ -286,8 +291,8 @@ class RefNystrom:
         lib.Nfft4GPPrecondNysSetRank(self.h, k)
         lib.Nfft4GPPrecondNysSetPerm(self.h, _i(self.perm), 0)
         fk = C.cast(lib.Nfft4GPKernelAdditiveKernel, C.c_void_p)
-        rc = lib.Nfft4GPPrecondNysSetupWithKernel(_d(dense._data), dense.n, dense.n, dense.d, fk, dense.h, 0,
-                                                  self.h)
+        rc = lib.Nfft4GPPrecondNysSetupWithKernel(_d(dense._data), dense.n, dense.n, dense.d, fk, dense.h,
+                                                  1 if grad else 0, self.h)
         assert rc == 0
         self.st = PrecondNysStruct.from_address(self.h)
         self.n, self.k = dense.n, k
@@ -301,6 +306,24 @@ class RefNystrom:
     def solve(self, x, rhs):
         self.lib.Nfft4GPPrecondNysSolve(C.c_void_p(self.h), self.n, _d(x), _d(rhs))
         return x
+
+    def dvp(self, x, mask=None):
+        """[M^{-1} dM/df x; M^{-1} dM/dl x; M^{-1} dM/dmu x] (3n), nys.c:175-330."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros(3 * self.n)
+        yp = _d(y)
+        m = None if mask is None else _i(np.ascontiguousarray(mask, dtype=np.int32))
+        assert self.lib.Nfft4GPPrecondNysDvp(C.c_void_p(self.h), self.n, m, _d(x), C.byref(yp)) == 0
+        return y
+
+    def trace(self):
+        t = np.zeros(3)
+        tp = _d(t)
+        assert self.lib.Nfft4GPPrecondNysTrace(C.c_void_p(self.h), C.byref(tp)) == 0
+        return t
+
+    def logdet(self):
+        return float(self.lib.Nfft4GPPrecondNysLogdet(C.c_void_p(self.h)))
 
 
 # ----------------------------------------------------------------------------------------------

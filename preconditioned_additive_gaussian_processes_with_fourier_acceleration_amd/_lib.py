@@ -92,6 +92,17 @@ _SIGS = {
     "Nfft4GPAmdNysSetupAdditive": (vp, [vp, vp, C.c_int, C.c_int]),
     "Nfft4GPAmdNysFactors": (C.c_int, [vp, vp, vp, vp, dp]),
     "Nfft4GPAmdNysSetupTimes": (C.c_int, [vp, vp]),
+    "Nfft4GPAmdPrecondNysCreate": (vp, []),
+    "Nfft4GPAmdPrecondNysFree": (None, [vp]),
+    "Nfft4GPAmdPrecondNysReset": (None, [vp]),
+    "Nfft4GPAmdPrecondNysSetRank": (None, [vp, C.c_int]),
+    "Nfft4GPAmdPrecondNysSetPerm": (None, [vp, vp, C.c_int]),
+    "Nfft4GPAmdPrecondNysSetK11Mode": (None, [vp, C.c_int]),
+    "Nfft4GPAmdPrecondNysSetupWithKernel": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp]),
+    "Nfft4GPAmdPrecondNysSolve": (C.c_int, [vp, C.c_int, vp, vp]),
+    "Nfft4GPAmdPrecondNysDvp": (C.c_int, [vp, C.c_int, vp, vp, vp]),
+    "Nfft4GPAmdPrecondNysTrace": (C.c_int, [vp, vp]),
+    "Nfft4GPAmdPrecondNysLogdet": (C.c_double, [vp]),
     "Nfft4GPAmdFsaiCreate": (vp, [C.c_int, vp, vp, vp]),
     "Nfft4GPAmdFsaiSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdFsaiFree": (None, [vp]),

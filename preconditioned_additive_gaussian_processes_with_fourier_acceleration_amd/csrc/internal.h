@@ -182,7 +182,16 @@ struct NysDev {
    // GPU setup only: hipEvent durations of the setup's kernels (ms): panel, U1 = Kp G^T, the Gram
    // U1^T U1 (+ split sum), U = U1 W (Nfft4GPAmdNysSetupTimes)
    double setup_ms[4] = {0.0, 0.0, 0.0, 0.0};
+   std::vector<double> hs;  // s on the host (logdet)
+   // setups with gradients (nys.c:518-660 with require_grad, for Dvp / Trace / Logdet, nys.c:175-516):
+   // Kall = [K | dK/df | dK/dl] (n x 3k, natural row order), dU = K L^{-T} (n x k), G = L^{-1} and G^T,
+   // GdKG = [L^{-1} dK11_f L^{-T} | L^{-1} dK11_l L^{-T}] (k x 2k), D = dU^T dU, scratch vk (8k), vn (n)
+   bool grad = false;
+   double f2 = 0.0;
+   double *Kall = nullptr, *dU = nullptr, *G = nullptr, *Gt = nullptr, *GdKG = nullptr, *D = nullptr;
+   double *vk = nullptr, *vn = nullptr;
 };
+void nys_free(NysDev* N);
 constexpr int kNysRows = 2048;  // rows per workgroup of the apply's U^T r pass
 int nys_alloc_scratch(NysDev* N);
 // GPU Nystrom setup (nystrom.hip) from gathered window coordinates xw (n x packed dims, host)
@@ -191,7 +200,7 @@ int gemm_f64(bool transA, int M, int N, int K, const double* A, long long lda, c
 int sym_eig_host(const std::vector<double>& A, int n, std::vector<double>& w, std::vector<double>& V);
 int chol_inverse_host(std::vector<double>& A, int k);
 NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int skip_last, int kernel, double f,
-                           double l, double mu, const int* perm, int k, int k11_mode);
+                           double l, double mu, const int* perm, int k, int k11_mode, bool with_grad = false);
 
 // multi-dimensional windows (nfft_md.hip).  xs[c] = component c's centred, scaled coordinates
 // (n_global x d column-major); the plan keeps rows [row_begin, row_end).

@@ -442,6 +442,26 @@ int additive_matvec_dot(void* str, const double* d_x, double* d_y, double* d_dot
 }
 }  // namespace nfft4gp_amd
 
+namespace nfft4gp_amd {
+// the gathered window buffer of an additive handle (kernels.h:65-95 _buffer / _iparams) and its plan's
+// kernel type (-1 before the first kernel setup); returns -1 for a handle that is not an additive one
+int additive_buffer_info(void* str, const double** xw, int* n, int* nw, int* dw, int* skip_last, int* kernel)
+{
+   nfft4gp_kernel* kd = (nfft4gp_kernel*)str;
+   PlanExt* E = additive_plan(str);
+   if (!kd || !E || !kd->_buffer) return -1;
+   const AdditivePlan& P = E->P;
+   if (P.row_begin != 0 || P.row_end != P.n_global) return -1;
+   *xw = kd->_buffer;
+   *n = P.n_global;
+   *nw = kd->_iparams[0];
+   *dw = kd->_iparams[1];
+   *skip_last = kd->_iparams[2];
+   *kernel = P.points_ready ? P.kernel : -1;
+   return 0;
+}
+}  // namespace nfft4gp_amd
+
 extern "C" {
 
 static const char* kVersion = "nfft4gp_amd 0.1.0 (gfx950)";
@@ -624,6 +644,7 @@ int Nfft4GPAmdKernelBench(void* str, int which, int grad, int reps, const double
    (void)hipEventDestroy(e1);
    return 0;
 }
+
 
 void* Nfft4GPAmdNysSetupAdditive(void* str, const int* perm, int k, int k11_mode)
 {

@@ -1,0 +1,412 @@
+// nys_grad.hip -- the Nystrom preconditioner with gradients on the GPU, behind the reference's
+// preconditioner interface (SRC/preconds/nys.h:62-179):
+//
+//   Nfft4GPAmdPrecondNysCreate / SetRank / SetPerm / Reset / Free      nys.c:3-113
+//   Nfft4GPAmdPrecondNysSetupWithKernel (precond_kernel_setup)          nys.c:518-660 (+ chol.c:428-560 for
+//                                                                       the gradient blocks of K11)
+//   Nfft4GPAmdPrecondNysSolve    (func_solve)                           nys.c:115-173
+//   Nfft4GPAmdPrecondNysDvp      (func_dvp)   y_g = M^{-1} dM/dtheta_g x nys.c:175-330
+//   Nfft4GPAmdPrecondNysTrace    (func_trace) tr(M^{-1} dM/dtheta_g)    nys.c:332-474
+//   Nfft4GPAmdPrecondNysLogdet   (func_logdet) log det M                nys.c:476-500
+//
+// M = K L^{-T} L^{-1} K^T + eta I with K = K(:, perm[:k]) (n x k, noise-free), L = chol(K11 + nu I),
+// eta = mu f^2.  Everything n-sized is in HBM in natural row order; the reference keeps rows permuted, so
+// its x(perm) / y(perm) gathers disappear.
+//
+// Dvp per gradient g (f, l): a = K^T x and b = dK_g^T x (two GEMV^T passes), the k x k chain
+// a'' = G^T G a, d = G^T G b - G^T GdKG_g G a (one workgroup), y_g = dK_g a'' + K d (one fused GEMV pass over
+// both panels), then y_g = M^{-1} y_g.  The mu gradient is f^2 M^{-1} x.
+//
+// Trace: the reference loops Dvp over the k columns of dU = K L^{-T} (k times four n x k GEMVs) and forms
+// dU (dU^T dU + eta I)^{-1} and 2 dK_g L^{-T} - dU GdKG_g as n x k matrices.  Every one of its sums of
+// n x k elementwise products is a trace of k x k products, so this restates it with ONE n x k x 3k MFMA
+// Gram P = [K dK_f dK_l]^T dU plus k x k MFMA products:
+//   sum (2 dK_g G^T - dU GdKG_g) o dU  = 2 sum G o P_g^T - sum GdKG_g o D          (D = dU^T dU)
+//   sum Dvp_g(dU) o dU W               = sum (P_g W) o (K11i P_K) - sum (P_K W) o (G^T GdKG_g G P_K)
+//                                        + sum (P_K W) o (K11i P_g)                 (W = (D + eta I)^{-1},
+//   sum Dvp_mu(dU) o dU W              = f^2 sum D o W                               K11i = G^T G)
+// Identical in exact arithmetic; sums differ from the reference's only by association (rounding).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "callbacks.hpp"
+#include "internal.h"
+
+namespace nfft4gp_amd {
+int additive_buffer_info(void* str, const double** xw, int* n, int* nw, int* dw, int* skip_last, int* kernel);
+int nys_gemv_t(const double* A, size_t lda, int n, int k, const double* x, double* out, double* part, hipStream_t s);
+int nys_apply_dev(NysDev* N, double* x, const double* rhs, hipStream_t s);
+int chol_inverse_dev(double* A, int k, double shift, double* G, double* Gt, int* d_info, hipStream_t s);
+int gram_tn(int M, int N, int K, const double* A, long long lda, const double* B, long long ldb, double* C, int sym,
+            hipStream_t s);
+}  // namespace nfft4gp_amd
+
+using namespace nfft4gp_amd;
+
+namespace {
+
+constexpr int kChainThreads = 1024;
+
+// out = op(A) v for a k x k column-major A held in global memory; op = A (trans = 0) or A^T (1).
+// Called by a whole workgroup; v and out in LDS.
+__device__ void small_gemv(const double* __restrict__ A, int k, int trans, const double* v, double* out)
+{
+   for (int i = threadIdx.x; i < k; i += blockDim.x) {
+      double acc = 0.0;
+      if (!trans)
+         for (int j = 0; j < k; j++) acc = fma(A[i + (size_t)j * k], v[j], acc);
+      else
+         for (int j = 0; j < k; j++) acc = fma(A[j + (size_t)i * k], v[j], acc);
+      out[i] = acc;
+   }
+   __syncthreads();
+}
+
+// ab = [a; b] (2k): a'' = G^T G a, d = G^T G b - G^T GdKG G a -> out = [a''; d]   (nys.c:262-282)
+__global__ __launch_bounds__(kChainThreads) void k_dvp_chain(const double* __restrict__ ab, int k,
+                                                             const double* __restrict__ G,
+                                                             const double* __restrict__ Gt,
+                                                             const double* __restrict__ GdKG,
+                                                             double* __restrict__ out)
+{
+   extern __shared__ double sm[];
+   double *a = sm, *b = sm + k, *t1 = sm + 2 * k, *t2 = sm + 3 * k, *t3 = sm + 4 * k;
+   for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) sm[i] = ab[i];
+   __syncthreads();
+   small_gemv(G, k, 0, a, t1);      // a' = L^{-1} K^T x
+   small_gemv(G, k, 0, b, t2);      // b' = L^{-1} dK^T x
+   small_gemv(GdKG, k, 0, t1, t3);  // c = GdKG a'
+   small_gemv(Gt, k, 0, t1, a);     // a'' = L^{-T} a'
+   small_gemv(Gt, k, 0, t2, b);     // b'' = L^{-T} b'
+   small_gemv(Gt, k, 0, t3, t1);    // c'' = L^{-T} c
+   for (int i = threadIdx.x; i < k; i += blockDim.x) {
+      out[i] = a[i];
+      out[k + i] = b[i] - t1[i];
+   }
+}
+
+// y[i] = sum_j A1[i + j n] c1[j] + A2[i + j n] c2[j]   (nys.c:286-288, the two K terms merged)
+constexpr int kGemvThreads = 256;
+__global__ __launch_bounds__(kGemvThreads) void k_gemv_n2(const double* __restrict__ A1,
+                                                          const double* __restrict__ A2, size_t n, int k,
+                                                          const double* __restrict__ c, double* __restrict__ y)
+{
+   extern __shared__ double s_c[];
+   for (int j = threadIdx.x; j < 2 * k; j += kGemvThreads) s_c[j] = c[j];
+   __syncthreads();
+   const size_t i = (size_t)blockIdx.x * kGemvThreads + threadIdx.x;
+   if (i >= n) return;
+   double acc = 0.0;
+   for (int j = 0; j < k; j++) {
+      acc = fma(A1[i + (size_t)j * n], s_c[j], acc);
+      acc = fma(A2[i + (size_t)j * n], s_c[k + j], acc);
+   }
+   y[i] = acc;
+}
+
+__global__ void k_scale_copy(double* __restrict__ y, const double* __restrict__ x, size_t n, double a)
+{
+   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+      y[i] = a * x[i];
+}
+
+// out[t] = sum_{i,j < k} A_t[i + j lda_t] * B_t[(trans_t ? j + i ldb_t : i + j ldb_t)], fixed order (one
+// workgroup per term)
+struct ProdTerm {
+   const double* A;
+   const double* B;
+   int lda, ldb, trans;
+};
+constexpr int kMaxTerms = 12;
+struct ProdTerms {
+   ProdTerm t[kMaxTerms];
+};
+__global__ __launch_bounds__(1024) void k_sum_prods(ProdTerms terms, int k, double* __restrict__ out)
+{
+   __shared__ double s[16];
+   const ProdTerm T = terms.t[blockIdx.x];
+   double acc = 0.0;
+   for (long long e = threadIdx.x; e < (long long)k * k; e += 1024) {
+      const int i = (int)(e % k), j = (int)(e / k);
+      const double bv = T.trans ? T.B[j + (size_t)i * T.ldb] : T.B[i + (size_t)j * T.ldb];
+      acc = fma(T.A[i + (size_t)j * T.lda], bv, acc);
+   }
+   for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+   __syncthreads();
+   if (threadIdx.x == 0) {
+      double v = 0.0;
+      for (int w = 0; w < 16; w++) v += s[w];
+      out[blockIdx.x] = v;
+   }
+}
+
+// the reference's precond_nys, restated: rank / permutation knobs plus the device factors
+struct PrecondNysAmd {
+   int k_setup = 50;  // nys.c:7 default
+   int* perm = nullptr;
+   int own_perm = 0;
+   int k11_mode = 0;
+   NysDev* dev = nullptr;
+};
+
+int dvp_dev(NysDev* N, const int* mask, const double* x, double* y, bool nosolve, hipStream_t s)
+{
+   const int n = N->n, k = N->k;
+   const size_t nk = (size_t)n * k;
+   const double* K = N->Kall;
+   double* ab = N->vk;          // [a; b]
+   double* cd = N->vk + 2 * k;  // [a''; d]
+   for (int g = 0; g < 2; g++) {
+      if (mask && !mask[g]) continue;
+      const double* dK = N->Kall + (size_t)(g + 1) * nk;
+      if (nys_gemv_t(K, n, n, k, x, ab, N->part, s) || nys_gemv_t(dK, n, n, k, x, ab + k, N->part, s)) return -1;
+      hipLaunchKernelGGL(k_dvp_chain, dim3(1), dim3(kChainThreads), sizeof(double) * 5 * k, s, ab, k, N->G,
+                         N->Gt, N->GdKG + (size_t)g * k * k, cd);
+      double* yg = y + (size_t)g * n;
+      double* dst = nosolve ? yg : N->vn;
+      hipLaunchKernelGGL(k_gemv_n2, dim3((n + kGemvThreads - 1) / kGemvThreads), dim3(kGemvThreads),
+                         sizeof(double) * 2 * k, s, dK, K, (size_t)n, k, cd, dst);
+      if (!nosolve && nys_apply_dev(N, yg, N->vn, s)) return -1;
+   }
+   if (!mask || mask[2]) {
+      double* y2 = y + 2 * (size_t)n;
+      if (nosolve) {
+         hipLaunchKernelGGL(k_scale_copy, dim3(1024), dim3(256), 0, s, y2, x, (size_t)n, N->f2);
+      } else {
+         if (nys_apply_dev(N, N->vn, x, s)) return -1;
+         hipLaunchKernelGGL(k_scale_copy, dim3(1024), dim3(256), 0, s, y2, N->vn, (size_t)n, N->f2);
+      }
+   }
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int trace_dev(NysDev* N, double* traces, hipStream_t s)
+{
+   const int n = N->n, k = N->k;
+   const size_t kk = (size_t)k * k;
+   const int k3 = 3 * k;
+   double *P = nullptr, *W = nullptr, *Wt = nullptr, *K11i = nullptr, *T = nullptr, *Q = nullptr, *R = nullptr,
+          *out = nullptr;
+   int* d_info = nullptr;
+   auto cleanup = [&]() {
+      (void)hipStreamSynchronize(s);
+      for (double* p : {P, W, Wt, K11i, T, Q, R, out}) (void)hipFree(p);
+      (void)hipFree(d_info);
+   };
+   auto dal = [](double** p, size_t c) { return hipMalloc((void**)p, sizeof(double) * c) != hipSuccess; };
+   if (dal(&P, 3 * kk) || dal(&W, kk) || dal(&Wt, kk) || dal(&K11i, kk) || dal(&T, kk) || dal(&Q, 3 * kk) ||
+       dal(&R, 4 * kk) || dal(&out, kMaxTerms) || hipMalloc((void**)&d_info, sizeof(int)) != hipSuccess) {
+      cleanup();
+      return -1;
+   }
+   // P = [K dK_f dK_l]^T dU (3k x k): the one n-sized product (MFMA, split over rows)
+   if (gram_tn(k3, k, n, N->Kall, n, N->dU, n, P, 0, s)) {
+      cleanup();
+      return -1;
+   }
+   // W = (D + eta I)^{-1} = C^{-T} C^{-1} (nys.c:380-409: UU = dU^T dU + eta I, potrf, two trsm);
+   // K11i = G^T G = (K11 + nu I)^{-1}
+   if (hipMemcpyAsync(T, N->D, sizeof(double) * kk, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+       chol_inverse_dev(T, k, N->eta, W, Wt, d_info, s) != 0 || gemm_f64(true, k, k, k, W, k, W, k, Q, k, s) ||
+       hipMemcpyAsync(W, Q, sizeof(double) * kk, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+       gemm_f64(true, k, k, k, N->G, k, N->G, k, K11i, k, s)) {
+      cleanup();
+      return -1;
+   }
+   const double* PK = P;  // rows [0, k) of P: K^T dU (ld 3k)
+   // Q = [P_K W | P_f W | P_l W] and R = [K11i P_K | K11i P_f | K11i P_l | scratch]  (k x k blocks, ld k)
+   for (int b = 0; b < 3; b++)
+      if (gemm_f64(false, k, k, k, P + b * k, k3, W, k, Q + b * kk, k, s) ||
+          gemm_f64(false, k, k, k, K11i, k, P + b * k, k3, R + b * kk, k, s)) {
+         cleanup();
+         return -1;
+      }
+   ProdTerms terms{};
+   double tr[3];
+   std::vector<double> h(kMaxTerms);
+   for (int g = 0; g < 2; g++) {
+      double* C = R + 3 * kk;  // G^T GdKG_g G P_K, built through T
+      if (gemm_f64(false, k, k, k, N->G, k, PK, k3, T, k, s) ||
+          gemm_f64(false, k, k, k, N->GdKG + g * kk, k, T, k, C, k, s) ||
+          gemm_f64(true, k, k, k, N->G, k, C, k, T, k, s)) {
+         cleanup();
+         return -1;
+      }
+      int nt = 0;
+      terms.t[nt++] = {N->G, P + (g + 1) * k, k, k3, 1};  // sum G o P_g^T
+      terms.t[nt++] = {N->GdKG + g * kk, N->D, k, k, 0};  // sum GdKG_g o D
+      terms.t[nt++] = {Q + (g + 1) * kk, R, k, k, 0};     // sum (P_g W) o (K11i P_K)
+      terms.t[nt++] = {Q, T, k, k, 0};                    // sum (P_K W) o (G^T GdKG_g G P_K)
+      terms.t[nt++] = {Q, R + (g + 1) * kk, k, k, 0};     // sum (P_K W) o (K11i P_g)
+      hipLaunchKernelGGL(k_sum_prods, dim3(nt), dim3(1024), 0, s, terms, k, out);
+      if (hipMemcpyAsync(h.data(), out, sizeof(double) * nt, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess) {
+         cleanup();
+         return -1;
+      }
+      tr[g] = 2.0 * h[0] - h[1] - (h[2] - h[3] + h[4]);
+   }
+   terms.t[0] = {N->D, W, k, k, 0};  // sum D o W
+   hipLaunchKernelGGL(k_sum_prods, dim3(1), dim3(1024), 0, s, terms, k, out);
+   if (hipMemcpyAsync(h.data(), out, sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess) {
+      cleanup();
+      return -1;
+   }
+   tr[2] = (double)n * N->f2 - N->f2 * h[0];
+   for (int g = 0; g < 3; g++) traces[g] = tr[g] / N->eta;
+   cleanup();
+   return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+void* Nfft4GPAmdPrecondNysCreate(void) { return new PrecondNysAmd(); }
+
+void Nfft4GPAmdPrecondNysSetRank(void* str, int k)
+{
+   if (str) ((PrecondNysAmd*)str)->k_setup = k;
+}
+
+void Nfft4GPAmdPrecondNysSetPerm(void* str, int* perm, int own_perm)
+{
+   if (!str) return;
+   PrecondNysAmd* P = (PrecondNysAmd*)str;
+   P->perm = perm;
+   P->own_perm = own_perm;
+}
+
+void Nfft4GPAmdPrecondNysSetK11Mode(void* str, int mode)
+{
+   if (str) ((PrecondNysAmd*)str)->k11_mode = mode ? 1 : 0;
+}
+
+void Nfft4GPAmdPrecondNysReset(void* str)
+{
+   PrecondNysAmd* P = (PrecondNysAmd*)str;
+   if (!P) return;
+   nys_free(P->dev);  // keep the permutation (nys.c:76-100)
+   P->dev = nullptr;
+}
+
+void Nfft4GPAmdPrecondNysFree(void* str)
+{
+   PrecondNysAmd* P = (PrecondNysAmd*)str;
+   if (!P) return;
+   nys_free(P->dev);
+   if (P->own_perm) free(P->perm);
+   delete P;
+}
+
+int Nfft4GPAmdPrecondNysSetupWithKernel(double* data, int n, int ldim, int d, func_kernel fkernel,
+                                        void* fkernel_params, int require_grad, void* vnys_mat)
+{
+   (void)data;
+   (void)ldim;
+   (void)d;
+   PrecondNysAmd* P = (PrecondNysAmd*)vnys_mat;
+   if (!P || !need_device("Nfft4GPAmdPrecondNysSetupWithKernel")) return -1;
+   const double* xw = nullptr;
+   int nn = 0, nw = 0, dw = 0, skip = 0, kernel = -1;
+   if (additive_buffer_info(fkernel_params, &xw, &nn, &nw, &dw, &skip, &kernel)) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondNysSetupWithKernel: fkernel_params must be an additive NFFT "
+                      "handle of this library (Nfft4GPNFFTAdditiveKernelParamCreate)\n");
+      return -1;
+   }
+   if (fkernel == &Nfft4GPNFFTAdditiveKernelGaussianKernel) kernel = 0;
+   else if (fkernel == &Nfft4GPNFFTAdditiveKernelMatern12Kernel) kernel = 1;
+   if (kernel < 0 || nn != n || !P->perm) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondNysSetupWithKernel: needs this library's additive Gaussian / "
+                      "Matern-1/2 setup function (or a handle set up with one), n = the handle's n and a "
+                      "permutation (Nfft4GPAmdPrecondNysSetPerm)\n");
+      return -1;
+   }
+   nfft4gp_kernel* kd = (nfft4gp_kernel*)fkernel_params;
+   nys_free(P->dev);
+   const int k = std::min(P->k_setup, n);
+   P->dev = nys_setup_additive(xw, n, nw, dw, skip, kernel, kd->_params[0], kd->_params[1], kd->_noise_level,
+                               P->perm, k, P->k11_mode, require_grad != 0);
+   return P->dev ? 0 : -1;
+}
+
+int Nfft4GPAmdPrecondNysSolve(void* vnys_mat, int n, double* x, double* rhs)
+{
+   PrecondNysAmd* P = (PrecondNysAmd*)vnys_mat;
+   if (!P || !P->dev) return -1;
+   return Nfft4GPAmdNysSolve(P->dev, n, x, rhs);
+}
+
+int Nfft4GPAmdPrecondNysDvp(void* vnys_mat, int n, int* mask, double* x, double** yp)
+{
+   PrecondNysAmd* P = (PrecondNysAmd*)vnys_mat;
+   if (!P || !P->dev || n != P->dev->n) return -1;
+   NysDev* N = P->dev;
+   if (!N->grad) {
+      printf("Setup NYS without gradient, dvp not supported.\n");  // nys.c:190-194
+      return -1;
+   }
+   if (!yp) {
+      printf("output pointer cannot be NULL\n");
+      return -1;
+   }
+   const bool dev_x = is_device_ptr(x);
+   if (!*yp) {
+      // allocated like the reference's output (calloc'ed 3n), on the side x lives on
+      if (dev_x) {
+         if (hipMalloc((void**)yp, sizeof(double) * 3 * (size_t)n) != hipSuccess) return -1;
+         NFFT4GP_HIP_CHECK(hipMemset(*yp, 0, sizeof(double) * 3 * (size_t)n));
+      } else {
+         *yp = (double*)calloc(3 * (size_t)n, sizeof(double));
+      }
+   }
+   hipStream_t s = current_stream();
+   Vec vx, vy;
+   if (vx.open(x, n, true) || vy.open(*yp, 3 * (size_t)n, true)) return -1;
+   const int rc = dvp_dev(N, mask, vx.d, vy.d, false, s);
+   vx.close(false);
+   vy.close(rc == 0);
+   return rc;
+}
+
+int Nfft4GPAmdPrecondNysTrace(void* vnys_mat, double** tracesp)
+{
+   PrecondNysAmd* P = (PrecondNysAmd*)vnys_mat;
+   if (!P || !P->dev) return -1;
+   if (!P->dev->grad) {
+      printf("Setup Nys without gradient, trace not supported.\n");  // nys.c:340-344
+      return -1;
+   }
+   if (!tracesp) {
+      printf("Trace pointer cannot be NULL\n");
+      return -1;
+   }
+   double* traces = *tracesp ? *tracesp : (double*)calloc(3, sizeof(double));
+   if (trace_dev(P->dev, traces, current_stream())) {
+      if (!*tracesp) free(traces);
+      return -1;
+   }
+   *tracesp = traces;
+   return 0;
+}
+
+double Nfft4GPAmdPrecondNysLogdet(void* vnys_mat)
+{
+   PrecondNysAmd* P = (PrecondNysAmd*)vnys_mat;
+   if (!P || !P->dev) return NAN;
+   const NysDev* N = P->dev;
+   const double val0 = std::log(N->eta);
+   double val = val0 * (double)(N->n - N->k);
+   for (int i = 0; i < N->k; i++) val += (N->hs[i] > 0) ? std::log(1.0 / N->hs[i]) : val0;
+   return val;
+}
+
+}  // extern "C"

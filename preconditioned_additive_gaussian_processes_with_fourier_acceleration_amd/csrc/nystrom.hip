@@ -47,11 +47,19 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int kPanelRows = 64, kPanelCols = 64, kPanelThreads = 256;
 constexpr int kPanelMaxDims = 128;  // window dimensions summed over all windows (nw * dw)
 
-template <int KERNEL>  // 0 Gaussian exp(-r^2 / 2l^2), 1 Matern-1/2 exp(-r / l)
+// GRAD: also the two hyperparameter derivatives of the noise-free panel (kernels.c:680-1289 Gaussian,
+// :2390-3033 Matern-1/2, averaged over windows by kernels.c:3099-3494), written as blocks 2 and 3 at
+// Kp + n k and Kp + 2 n k:  dK/df = (2/f) K,  dK/dl = (f^2/nw) sum_c r_c^2/l^3 e^{-r_c^2/2l^2} (Gaussian)
+// or (f^2/nw) sum_c r_c/l^2 e^{-r_c/l} (Matern-1/2), over the first grad_nw windows: with a padded last
+// window (skip_last > 0) the reference's rectangular K(permr, permc) adds the last window to K but not to
+// dK (kernels.c:3169 passes NULL for its dK), while its square no-permutation matrix (the K11 of
+// nys.c:569) keeps it (kernels.c:3398); grad_nw = nw - 1 reproduces the former.
+template <int KERNEL, bool GRAD>  // KERNEL 0 Gaussian exp(-r^2 / 2l^2), 1 Matern-1/2 exp(-r / l)
 __global__ __launch_bounds__(kPanelThreads) void k_nys_panel(const double* __restrict__ xw, int n, int nw, int dw,
                                                              int last_dw, const int* __restrict__ rperm,
                                                              const int* __restrict__ cperm, int k, double scale,
-                                                             double inv, double* __restrict__ Kp)
+                                                             double inv, double* __restrict__ Kp, int grad_nw,
+                                                             double df_scale, double dl_scale)
 {
    extern __shared__ double sm[];
    const int D = (nw - 1) * dw + last_dw;
@@ -68,7 +76,7 @@ __global__ __launch_bounds__(kPanelThreads) void k_nys_panel(const double* __res
    __syncthreads();
    // thread -> 4 rows x 4 columns, rows fastest so stores are coalesced per column
    const int tr = threadIdx.x & 15, tc = threadIdx.x >> 4;
-   double acc[4][4] = {};
+   double acc[4][4] = {}, accf[4][4] = {}, accl[4][4] = {};
    for (int w = 0; w < nw; w++) {
       const int dims = (w == nw - 1) ? last_dw : dw;
       double r2[4][4] = {};
@@ -87,11 +95,21 @@ __global__ __launch_bounds__(kPanelThreads) void k_nys_panel(const double* __res
                r2[a][b] = fma(df, df, r2[a][b]);
             }
       }
+      const bool gw = GRAD && w < grad_nw;
 #pragma unroll
       for (int a = 0; a < 4; a++)
 #pragma unroll
-         for (int b = 0; b < 4; b++) acc[a][b] += (KERNEL == 0) ? exp(-r2[a][b] * inv) : exp(-sqrt(r2[a][b]) * inv);
+         for (int b = 0; b < 4; b++) {
+            const double r = (KERNEL == 0) ? r2[a][b] : sqrt(r2[a][b]);
+            const double e = (KERNEL == 0) ? exp(-r * inv) : exp(-r * inv);
+            acc[a][b] += e;
+            if (gw) {
+               accf[a][b] += e;
+               accl[a][b] = fma(r, e, accl[a][b]);
+            }
+         }
    }
+   const size_t blk = (size_t)n * k;
 #pragma unroll
    for (int b = 0; b < 4; b++) {
       const int c = c0 + tc + 16 * b;
@@ -99,9 +117,33 @@ __global__ __launch_bounds__(kPanelThreads) void k_nys_panel(const double* __res
 #pragma unroll
       for (int a = 0; a < 4; a++) {
          const int r = r0 + tr + 16 * a;
-         if (r < n) Kp[(size_t)c * n + r] = scale * acc[a][b];
+         if (r >= n) continue;
+         Kp[(size_t)c * n + r] = scale * acc[a][b];
+         if (GRAD) {
+            Kp[blk + (size_t)c * n + r] = df_scale * accf[a][b];
+            Kp[2 * blk + (size_t)c * n + r] = dl_scale * accl[a][b];
+         }
       }
    }
+}
+
+// launch the panel variant for (kernel, grad)
+void launch_panel(int kernel, bool grad, dim3 grid, size_t lds, hipStream_t s, const double* xw, int n, int nw, int dw,
+                  int last_dw, const int* rperm, const int* cperm, int k, double f, double l, double* Kp, int grad_nw)
+{
+   const double f2nw = f * f / nw;
+   const double inv = (kernel == 0) ? 1.0 / (2.0 * l * l) : 1.0 / l;
+   const double df_scale = 2.0 / f * f2nw;
+   const double dl_scale = (kernel == 0) ? f2nw / (l * l * l) : f2nw / (l * l);
+#define NYS_PANEL(KK, GG)                                                                                        \
+   hipLaunchKernelGGL((k_nys_panel<KK, GG>), grid, dim3(kPanelThreads), lds, s, xw, n, nw, dw, last_dw, rperm, \
+                      cperm, k, f2nw, inv, Kp, grad_nw, df_scale, dl_scale)
+   if (kernel == 0) {
+      if (grad) NYS_PANEL(0, true); else NYS_PANEL(0, false);
+   } else {
+      if (grad) NYS_PANEL(1, true); else NYS_PANEL(1, false);
+   }
+#undef NYS_PANEL
 }
 
 // ---- C = op(A) B on MFMA f64 ---------------------------------------------------------------------
@@ -394,6 +436,13 @@ __global__ void k_add_diag(double* A, int k, double nu)
    if (i < k) A[i + (size_t)i * k] += nu;
 }
 
+// G = lower part of A (strict upper zeroed)
+__global__ void k_clean_lower(const double* __restrict__ A, int k, double* __restrict__ G)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
+   if (i < k) G[i + (size_t)j * k] = (i >= j) ? A[i + (size_t)j * k] : 0.0;
+}
+
 // Gt = (lower part of G)^T
 __global__ void k_transpose_lower(const double* __restrict__ G, int k, double* __restrict__ Gt)
 {
@@ -493,9 +542,70 @@ int chol_inverse_host(std::vector<double>& A, int k)
    return 0;
 }
 
+// G = L^{-1} (clean lower triangle) and Gt = G^T of L = chol(A + shift I), A k x k on the device (A is
+// overwritten).  rocSOLVER potrf + trtri when it loaded, the host Cholesky otherwise.  Returns 0, the
+// failing column + 1 when A + shift is not positive definite, or -1.
+int chol_inverse_dev(double* A, int k, double shift, double* G, double* Gt, int* d_info, hipStream_t s)
+{
+   RocSolver& R = rocsolver();
+   if (R.ok) {
+      int info = 0;
+      R.set_stream(R.h, s);
+      if (shift != 0.0) hipLaunchKernelGGL(k_add_diag, dim3((k + 255) / 256), dim3(256), 0, s, A, k, shift);
+      if (R.potrf(R.h, rocblas_fill_lower, k, A, k, d_info) != rocblas_status_success ||
+          hipMemcpyAsync(&info, d_info, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+         return -1;
+      if (info) return info;
+      if (R.trtri(R.h, rocblas_fill_lower, rocblas_diagonal_non_unit, k, A, k, d_info) != rocblas_status_success)
+         return -1;
+      hipLaunchKernelGGL(k_transpose_lower, dim3((k + 255) / 256, k), dim3(256), 0, s, A, k, Gt);
+      if (G) hipLaunchKernelGGL(k_clean_lower, dim3((k + 255) / 256, k), dim3(256), 0, s, A, k, G);
+      return hipGetLastError() == hipSuccess ? 0 : -1;
+   }
+   std::vector<double> h((size_t)k * k);
+   if (hipMemcpyAsync(h.data(), A, sizeof(double) * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess)
+      return -1;
+   for (int j = 0; j < k; j++) h[j + (size_t)j * k] += shift;
+   if (int info = chol_lower(h, k)) return info;
+   trtri_lower(h, k);
+   std::vector<double> ht((size_t)k * k);
+   for (int j = 0; j < k; j++)
+      for (int i = 0; i < k; i++) {
+         ht[i + (size_t)j * k] = (j >= i) ? h[j + (size_t)i * k] : 0.0;
+         if (i < j) h[i + (size_t)j * k] = 0.0;
+      }
+   if (hipMemcpy(Gt, ht.data(), sizeof(double) * ht.size(), hipMemcpyHostToDevice)) return -1;
+   if (G && hipMemcpy(G, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice)) return -1;
+   return 0;
+}
+
+// C (M x N, ld ldc) = A^T B with A K x M (lda) and B K x N (ldb), K split over row chunks (fixed-order sum,
+// deterministic); sym: C symmetric with A == B (only tiles on and below the diagonal are computed)
+int gram_tn(int M, int N, int K, const double* A, long long lda, const double* B, long long ldb, double* C, int sym,
+            hipStream_t s)
+{
+   const int nsplit = std::max(1, std::min(256, K / 8192));
+   const int ksplit = ((K + nsplit - 1) / nsplit + kGemmK - 1) / kGemmK * kGemmK;
+   const int nsplit_used = (K + ksplit - 1) / ksplit;
+   double* part = nullptr;
+   if (dalloc(&part, (size_t)nsplit_used * M * N)) return -1;
+   dim3 grid((M + kGemmTile - 1) / kGemmTile, (N + kGemmTile - 1) / kGemmTile, nsplit_used);
+   hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(kGemmThreads), 0, s, M, N, K, A, lda, B, ldb, part, (long long)M,
+                      (long long)M * N, ksplit, sym);
+   const long long cnt = (long long)M * N;
+   hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, part, nsplit_used, cnt, cnt,
+                      C, sym, M);
+   const bool ok = hipGetLastError() == hipSuccess;
+   (void)hipStreamSynchronize(s);
+   (void)hipFree(part);
+   return ok ? 0 : -1;
+}
+
 // ------------------------------------------------------------------------------------------------
 NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int skip_last, int kernel, double f,
-                           double l, double mu, const int* perm, int k, int k11_mode)
+                           double l, double mu, const int* perm, int k, int k11_mode, bool with_grad)
 {
    const int last_dw = dw - skip_last;
    const int D = (nw - 1) * dw + last_dw;
@@ -515,27 +625,22 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
       return nullptr;
    }
    hipStream_t s = current_stream();
-   double *d_xw = nullptr, *d_Kp = nullptr, *d_U1 = nullptr, *d_B = nullptr, *d_part = nullptr, *d_AA = nullptr;
-   double *d_K11 = nullptr, *d_w1 = nullptr, *d_e = nullptr, *d_s = nullptr;
+   const int nblk = with_grad ? 3 : 1;  // panel blocks: K (and dK/df, dK/dl)
+   double *d_xw = nullptr, *d_Kp = nullptr, *d_U1 = nullptr, *d_B = nullptr, *d_AA = nullptr;
+   double *d_K11 = nullptr, *d_w1 = nullptr, *d_e = nullptr, *d_s = nullptr, *d_T = nullptr;
    int *d_perm = nullptr, *d_iota = nullptr, *d_info = nullptr;
-   NysDev* N = nullptr;
+   NysDev* N = new NysDev();
+   N->n = n;
+   N->k = k;
    auto release = [&]() {
-      for (double* p : {d_xw, d_U1, d_B, d_part, d_AA, d_K11, d_w1, d_e, d_s}) (void)hipFree(p);
+      for (double* p : {d_xw, d_Kp, d_U1, d_B, d_AA, d_K11, d_w1, d_e, d_s, d_T}) (void)hipFree(p);
       for (int* p : {d_perm, d_iota, d_info}) (void)hipFree(p);
    };
    auto fail = [&](const char* what) -> NysDev* {
       if (what) fprintf(stderr, "nfft4gp_amd: Nystrom setup: %s\n", what);
       (void)hipStreamSynchronize(s);
       release();
-      if (N) {
-         (void)hipFree(N->U);
-         (void)hipFree(N->s);
-         (void)hipFree(N->w);
-         (void)hipFree(N->part);
-         delete N;
-      } else {
-         (void)hipFree(d_Kp);
-      }
+      nys_free(N);
       return nullptr;
    };
    // hipEvents around the four big kernels (panel, gemm1, gram, gemm2) for the MFMA report
@@ -548,52 +653,44 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
          for (int i = 0; i < 8; i++) (void)hipEventDestroy(e[i]);
       }
    } ev_guard{ev};
-   const size_t nk = (size_t)n * k;
-   if (dalloc(&d_xw, (size_t)n * nw * dw) || dalloc(&d_perm, (size_t)n) || dalloc(&d_info, 1) || dalloc(&d_Kp, nk) ||
-       dalloc(&d_U1, nk) || dalloc(&d_B, (size_t)k * k) || dalloc(&d_AA, (size_t)k * k))
+   const size_t nk = (size_t)n * k, kk = (size_t)k * k;
+   if (dalloc(&d_xw, (size_t)n * nw * dw) || dalloc(&d_perm, (size_t)n) || dalloc(&d_info, 1) ||
+       dalloc(&d_Kp, nk * nblk) || dalloc(&d_U1, nk) || dalloc(&d_B, kk) || dalloc(&d_AA, kk))
       return fail("allocation");
    if (hipMemcpy(d_xw, xw_host, sizeof(double) * (size_t)n * ((nw - 1) * dw + last_dw), hipMemcpyHostToDevice) ||
        hipMemcpy(d_perm, perm, sizeof(int) * (size_t)n, hipMemcpyHostToDevice))
       return fail("upload");
 
-   // 1. panel K(perm, perm[:k]) (noise-free, nys.c:566-567 / kernels.c "when have permc")
+   // 1. panel K(perm, perm[:k]) (noise-free, nys.c:566-567 / kernels.c "when have permc"), rows in natural
+   //    order; with gradients also dK/df and dK/dl (nys.c:597-601)
    const double f2 = f * f;
-   const double inv = (kernel == 0) ? 1.0 / (2.0 * l * l) : 1.0 / l;
+   const int nw_grad_panel = (k11_mode == 0 && skip_last > 0) ? nw - 1 : nw;
    const size_t lds = sizeof(double) * (size_t)D * (kPanelRows + kPanelCols);
    dim3 pgrid((n + kPanelRows - 1) / kPanelRows, (k + kPanelCols - 1) / kPanelCols);
    (void)hipEventRecord(ev[0], s);
-   if (kernel == 0)
-      hipLaunchKernelGGL(k_nys_panel<0>, pgrid, dim3(kPanelThreads), lds, s, d_xw, n, nw, dw, last_dw,
-                         (const int*)nullptr, d_perm, k, f2 / nw, inv, d_Kp);
-   else
-      hipLaunchKernelGGL(k_nys_panel<1>, pgrid, dim3(kPanelThreads), lds, s, d_xw, n, nw, dw, last_dw,
-                         (const int*)nullptr, d_perm, k, f2 / nw, inv, d_Kp);
+   launch_panel(kernel, with_grad, pgrid, lds, s, d_xw, n, nw, dw, last_dw, nullptr, d_perm, k, f, l, d_Kp,
+                nw_grad_panel);
    if (hipGetLastError() != hipSuccess) return fail("panel launch");
    (void)hipEventRecord(ev[1], s);
 
    phase("panel");
-   // 2. K11 on the device: the landmark block of the panel (mode 1), or the reference's K11 (mode 0:
-   //    nys.c:569 hands the k x d sub-data to Nfft4GPKernelAdditiveKernel, which ignores it and reads
-   //    window i of its own gathered buffer at offset i*n*dwindows with n = k, kernels.c:3160 -- the
-   //    panel kernel over that buffer with n = k and the identity permutation)
-   if (dalloc(&d_K11, (size_t)k * k) || dalloc(&d_iota, (size_t)k)) return fail("allocation");
+   // 2. K11 (and dK11) on the device: the landmark rows of the panel (mode 1), or the reference's K11
+   //    (mode 0: nys.c:569 hands the k x d sub-data to Nfft4GPKernelAdditiveKernel, which ignores it and
+   //    reads window i of its own gathered buffer at offset i*n*dwindows with n = k, kernels.c:3160 --
+   //    the panel kernel over that buffer with n = k and the identity permutation)
+   if (dalloc(&d_K11, kk * nblk) || dalloc(&d_iota, (size_t)k)) return fail("allocation");
    if (k11_mode == 1) {
-      // the landmark rows perm[:k] of the natural-order panel
-      hipLaunchKernelGGL(k_gather_rows, dim3((k + 255) / 256, k), dim3(256), 0, s, d_Kp, (long long)n, d_perm, k,
-                         d_K11);
+      for (int b = 0; b < nblk; b++)
+         hipLaunchKernelGGL(k_gather_rows, dim3((k + 255) / 256, k), dim3(256), 0, s, d_Kp + b * nk, (long long)n,
+                            d_perm, k, d_K11 + b * kk);
    } else {
       hipLaunchKernelGGL(k_iota, dim3((k + 255) / 256), dim3(256), 0, s, d_iota, k);
       dim3 kgrid((k + kPanelRows - 1) / kPanelRows, (k + kPanelCols - 1) / kPanelCols);
-      if (kernel == 0)
-         hipLaunchKernelGGL(k_nys_panel<0>, kgrid, dim3(kPanelThreads), lds, s, d_xw, k, nw, dw, last_dw,
-                            (const int*)nullptr, d_iota, k, f2 / nw, inv, d_K11);
-      else
-         hipLaunchKernelGGL(k_nys_panel<1>, kgrid, dim3(kPanelThreads), lds, s, d_xw, k, nw, dw, last_dw,
-                            (const int*)nullptr, d_iota, k, f2 / nw, inv, d_K11);
+      launch_panel(kernel, with_grad, kgrid, lds, s, d_xw, k, nw, dw, last_dw, nullptr, d_iota, k, f, l, d_K11, nw);
    }
    // stable shift nu = sqrt(k) ulp(|K11|_F) (chol.c:449-465; dlansy 'F' 'L' = the full-matrix norm)
-   std::vector<double> K11((size_t)k * k);
-   if (hipMemcpyAsync(K11.data(), d_K11, sizeof(double) * K11.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+   std::vector<double> K11(kk);
+   if (hipMemcpyAsync(K11.data(), d_K11, sizeof(double) * kk, hipMemcpyDeviceToHost, s) != hipSuccess ||
        hipStreamSynchronize(s) != hipSuccess)
       return fail("K11 download");
    double fro = 0.0;
@@ -603,34 +700,26 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    }
    fro = std::sqrt(fro);
    const double nu = std::sqrt((double)k) * (std::nextafter(fro, fro + 1.0) - fro);
-   RocSolver& R = rocsolver();
-   if (R.ok) {
-      // L = chol(K11 + nu I), G = L^{-1}, Gt = G^T, all on the device
-      int info = 0;
-      R.set_stream(R.h, s);
-      hipLaunchKernelGGL(k_add_diag, dim3((k + 255) / 256), dim3(256), 0, s, d_K11, k, nu);
-      if (R.potrf(R.h, rocblas_fill_lower, k, d_K11, k, d_info) != rocblas_status_success ||
-          hipMemcpyAsync(&info, d_info, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
-          hipStreamSynchronize(s) != hipSuccess)
-         return fail("rocsolver_dpotrf");
-      if (info) {
+   // L = chol(K11 + nu I), G = L^{-1} (kept with gradients), Gt = G^T in d_B
+   if (with_grad && (dalloc(&N->G, kk) || dalloc(&N->Gt, kk))) return fail("allocation");
+   {
+      const int info = chol_inverse_dev(d_K11, k, nu, with_grad ? N->G : nullptr, d_B, d_info, s);
+      if (info > 0) {
          fprintf(stderr, "nfft4gp_amd: Nystrom setup: K11 + shift is not positive definite (column %d)\n", info);
          return fail(nullptr);
       }
-      if (R.trtri(R.h, rocblas_fill_lower, rocblas_diagonal_non_unit, k, d_K11, k, d_info) != rocblas_status_success)
-         return fail("rocsolver_dtrtri");
-      hipLaunchKernelGGL(k_transpose_lower, dim3((k + 255) / 256, k), dim3(256), 0, s, d_K11, k, d_B);
-   } else {
-      for (int j = 0; j < k; j++) K11[j + (size_t)j * k] += nu;
-      if (int info = chol_lower(K11, k)) {
-         fprintf(stderr, "nfft4gp_amd: Nystrom setup: K11 + shift is not positive definite (column %d)\n", info);
-         return fail(nullptr);
+      if (info < 0) return fail("Cholesky / triangular inverse of K11");
+   }
+   if (with_grad) {
+      // GdKG_g = L^{-1} dK11_g L^{-T} for g = f, l (chol.c:512-523)
+      if (hipMemcpyAsync(N->Gt, d_B, sizeof(double) * kk, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+          dalloc(&N->GdKG, 2 * kk) || dalloc(&d_T, kk))
+         return fail("allocation");
+      for (int g = 0; g < 2; g++) {
+         if (gemm(false, k, k, k, d_K11 + (g + 1) * kk, k, N->Gt, k, d_T, k, s) ||
+             gemm(false, k, k, k, N->G, k, d_T, k, N->GdKG + g * kk, k, s))
+            return fail("gemm");
       }
-      trtri_lower(K11, k);  // G = L^{-1}
-      std::vector<double> Gt((size_t)k * k);
-      for (int j = 0; j < k; j++)
-         for (int i = 0; i < k; i++) Gt[i + (size_t)j * k] = (j >= i) ? K11[j + (size_t)i * k] : 0.0;
-      if (hipMemcpy(d_B, Gt.data(), sizeof(double) * Gt.size(), hipMemcpyHostToDevice)) return fail("upload");
    }
 
    phase("k11+chol");
@@ -640,37 +729,32 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    (void)hipEventRecord(ev[3], s);
 
    phase("gemm1");
-   // 4. AA = U1^T U1, K = n split over row chunks (fixed order sum -> deterministic)
-   const int nsplit = std::max(1, std::min(256, n / 8192));
-   const int ksplit = ((n + nsplit - 1) / nsplit + kGemmK - 1) / kGemmK * kGemmK;
-   const int nsplit_used = (n + ksplit - 1) / ksplit;
-   if (dalloc(&d_part, (size_t)nsplit_used * k * k)) return fail("allocation");
-   {
-      (void)hipEventRecord(ev[4], s);
-      dim3 grid((k + kGemmTile - 1) / kGemmTile, (k + kGemmTile - 1) / kGemmTile, nsplit_used);
-      hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(kGemmThreads), 0, s, k, k, n, d_U1, (long long)n, d_U1,
-                         (long long)n, d_part, (long long)k, (long long)k * k, ksplit, 1);
-      const long long cnt = (long long)k * k;
-      hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, d_part, nsplit_used, cnt,
-                         cnt, d_AA, 1, k);
-      if (hipGetLastError() != hipSuccess) return fail("gram launch");
-      (void)hipEventRecord(ev[5], s);
+   // 4. AA = U1^T U1, split over rows (fixed-order sum, deterministic); with gradients D = AA is kept
+   (void)hipEventRecord(ev[4], s);
+   if (gram_tn(k, k, n, d_U1, n, d_U1, n, d_AA, 1, s)) return fail("gram");
+   (void)hipEventRecord(ev[5], s);
+   if (with_grad) {
+      if (dalloc(&N->D, kk) ||
+          hipMemcpyAsync(N->D, d_AA, sizeof(double) * kk, hipMemcpyDeviceToDevice, s) != hipSuccess)
+         return fail("allocation");
    }
    phase("gram");
    // 5. eig(AA) = V diag(w1) V^T (dsyev: ascending); W = V(:, reversed) diag(w1^-1/2) with the
    //    reference's 1e12 factor for sqrt(w1) < 1e-12 (matops.c Nfft4GPTrilNystromSvd); s (nys.c:641-647)
    const double eta = mu * f2;
    if (dalloc(&d_w1, (size_t)k) || dalloc(&d_e, (size_t)k) || dalloc(&d_s, (size_t)k)) return fail("allocation");
+   RocSolver& R = rocsolver();
    if (R.ok) {
       int info = 0;
+      R.set_stream(R.h, s);
       if (R.syevd(R.h, rocblas_evect_original, rocblas_fill_lower, k, d_AA, k, d_w1, d_e, d_info) !=
               rocblas_status_success ||
           hipMemcpyAsync(&info, d_info, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
           hipStreamSynchronize(s) != hipSuccess || info)
          return fail("rocsolver_dsyevd");
    } else {
-      std::vector<double> AA((size_t)k * k);
-      if (hipMemcpyAsync(AA.data(), d_AA, sizeof(double) * AA.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      std::vector<double> AA(kk);
+      if (hipMemcpyAsync(AA.data(), d_AA, sizeof(double) * kk, hipMemcpyDeviceToHost, s) != hipSuccess ||
           hipStreamSynchronize(s) != hipSuccess)
          return fail("gram download");
       std::vector<double> w1, V;
@@ -681,19 +765,33 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    }
    hipLaunchKernelGGL(k_nys_scale, dim3((k + 255) / 256, k), dim3(256), 0, s, d_AA, d_w1, k, eta, d_B, d_s);
    phase("eig");
-   N = new NysDev();
-   N->n = n;
-   N->k = k;
-   N->U = d_Kp;  // the panel's storage is reused for U (rows scattered back to natural order)
-   d_Kp = nullptr;
+   // 6. U = U1 W.  Without gradients the panel's storage is reused for U; with them the panel (K, dK/df,
+   //    dK/dl) and U1 (= dU, nys.c:611-615) stay, for Dvp and Trace.
+   if (with_grad) {
+      if (dalloc(&N->U, nk)) return fail("allocation");
+   } else {
+      N->U = d_Kp;
+      d_Kp = nullptr;
+   }
    (void)hipEventRecord(ev[6], s);
    if (gemm(false, n, k, k, d_U1, n, d_B, k, N->U, n, s)) return fail("gemm");
    (void)hipEventRecord(ev[7], s);
    N->eta = eta;
    N->s = d_s;
    d_s = nullptr;
-   if (nys_alloc_scratch(N)) return fail("allocation");
-   if (hipStreamSynchronize(s) != hipSuccess) return fail("sync");
+   if (with_grad) {
+      N->grad = true;
+      N->f2 = f2;
+      N->Kall = d_Kp;
+      d_Kp = nullptr;
+      N->dU = d_U1;
+      d_U1 = nullptr;
+      if (dalloc(&N->vk, 8 * (size_t)k) || dalloc(&N->vn, (size_t)n)) return fail("allocation");
+   }
+   N->hs.resize(k);
+   if (hipMemcpyAsync(N->hs.data(), N->s, sizeof(double) * k, hipMemcpyDeviceToHost, s) != hipSuccess ||
+       nys_alloc_scratch(N) || hipStreamSynchronize(s) != hipSuccess)
+      return fail("sync");
    phase("gemm2");
    for (int i = 0; i < 4; i++) {
       float ms = 0.0f;

@@ -22,6 +22,15 @@
 using namespace nfft4gp_amd;
 
 namespace nfft4gp_amd {
+void nys_free(NysDev* N)
+{
+   if (!N) return;
+   (void)hipStreamSynchronize(current_stream());
+   for (double* p : {N->U, N->s, N->w, N->part, N->Kall, N->dU, N->G, N->Gt, N->GdKG, N->D, N->vk, N->vn})
+      (void)hipFree(p);
+   delete N;
+}
+
 int nys_alloc_scratch(NysDev* N)
 {
    N->nblk = (N->n + kNysRows - 1) / kNysRows;
@@ -372,7 +381,7 @@ __global__ __launch_bounds__(64 * kNysWRows) void k_nys_w(const double* __restri
       double t = 0.0;
 #pragma unroll
       for (int q = 0; q < kNysWRows; q++) t += s_sum[q][lane];
-      w[j] = s[j] * t - t / eta;
+      w[j] = s ? s[j] * t - t / eta : t;  // s == NULL: the plain column sums (A^T x)
    }
 }
 
@@ -419,6 +428,33 @@ PcgScratch g_pcg;
 int g_last_hist_len = 0;
 
 }  // namespace
+
+namespace nfft4gp_amd {
+// out[0..k) = A^T x for A n x k column-major (lda), fixed-order reduction over kNysRows row blocks;
+// part holds ceil(n / kNysRows) * k doubles
+int nys_gemv_t(const double* A, size_t lda, int n, int k, const double* x, double* out, double* part, hipStream_t s)
+{
+   const int nblk = (n + kNysRows - 1) / kNysRows;
+   hipLaunchKernelGGL(k_nys_ut, dim3(nblk), dim3(kNysThreads), 0, s, A, lda, n, k, x, part);
+   hipLaunchKernelGGL(k_nys_w, dim3((k + 63) / 64), dim3(64 * kNysWRows), 0, s, part, nblk, k, (const double*)nullptr,
+                      1.0, out);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+// x = M^{-1} rhs on device vectors (nys.c:115-173 in natural row order)
+int nys_apply_dev(NysDev* N, double* x, const double* rhs, hipStream_t s)
+{
+   const int n = N->n;
+   hipLaunchKernelGGL(k_nys_ut, dim3(N->nblk), dim3(kNysThreads), 0, s, N->U, (size_t)n, n, N->k, rhs, N->part);
+   hipLaunchKernelGGL(k_nys_w, dim3((N->k + 63) / 64), dim3(64 * kNysWRows), 0, s, N->part, N->nblk, N->k, N->s, N->eta,
+                      N->w);
+   hipLaunchKernelGGL(k_nys_u, dim3((n + kNysThreads - 1) / kNysThreads), dim3(kNysThreads), sizeof(double) * N->k, s,
+                      N->U, (size_t)n, n, N->k, N->w, rhs, N->eta, x);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+}  // namespace nfft4gp_amd
 
 extern "C" {
 
@@ -769,6 +805,7 @@ void* Nfft4GPAmdNysCreate(int n, int k, const double* U, const double* s, double
    return N;
 }
 
+
 int Nfft4GPAmdNysSolve(void* nys, int n, double* x, double* rhs)
 {
    NysDev* N = (NysDev*)nys;
@@ -776,26 +813,13 @@ int Nfft4GPAmdNysSolve(void* nys, int n, double* x, double* rhs)
    hipStream_t s = current_stream();
    Vec vx, vr;
    if (vx.open(x, n, false) || vr.open(rhs, n, true)) return -1;
-   hipLaunchKernelGGL(k_nys_ut, dim3(N->nblk), dim3(kNysThreads), 0, s, N->U, (size_t)n, n, N->k, vr.d, N->part);
-   hipLaunchKernelGGL(k_nys_w, dim3((N->k + 63) / 64), dim3(64 * kNysWRows), 0, s, N->part, N->nblk, N->k, N->s, N->eta, N->w);
-   hipLaunchKernelGGL(k_nys_u, dim3((n + kNysThreads - 1) / kNysThreads), dim3(kNysThreads),
-                      sizeof(double) * N->k, s, N->U, (size_t)n, n, N->k, N->w, vr.d, N->eta, vx.d);
-   NFFT4GP_HIP_CHECK(hipGetLastError());
+   if (nys_apply_dev(N, vx.d, vr.d, s)) return -1;
    vr.close(false);
    vx.close(true);
    return 0;
 }
 
-void Nfft4GPAmdNysFree(void* nys)
-{
-   NysDev* N = (NysDev*)nys;
-   if (!N) return;
-   (void)hipFree(N->U);
-   (void)hipFree(N->s);
-   (void)hipFree(N->w);
-   (void)hipFree(N->part);
-   delete N;
-}
+void Nfft4GPAmdNysFree(void* nys) { nys_free((NysDev*)nys); }
 
 }  // extern "C"
 
@@ -806,7 +830,8 @@ bool library_operator(const void* fn)
    return fn == (const void*)&Nfft4GPAdditiveNFFTMatSymv || fn == (const void*)&Nfft4GPNFFTMatSymv ||
           fn == (const void*)&Nfft4GPAdditiveNFFTGradMatSymv || fn == (const void*)&Nfft4GPNFFTGradMatSymv ||
           fn == (const void*)&Nfft4GPAmdNysSolve || fn == (const void*)&Nfft4GPAmdFsaiSolve ||
-          fn == (const void*)&Nfft4GPAmdAfnSolve;
+          fn == (const void*)&Nfft4GPAmdAfnSolve || fn == (const void*)&Nfft4GPAmdPrecondNysSolve ||
+          fn == (const void*)&Nfft4GPAmdPrecondNysDvp;
 }
 }  // namespace nfft4gp_amd
 
