@@ -238,6 +238,11 @@ void *Nfft4GPAmdNysSetupAdditive(void *str, const int *perm, int k, int k11_mode
  * (pass the setup's perm to get the reference's permuted row order, NULL for natural order), s (k),
  * eta; any output may be NULL */
 int Nfft4GPAmdNysFactors(void *nys, const int *perm, NFFT4GP_DOUBLE *U, NFFT4GP_DOUBLE *s, NFFT4GP_DOUBLE *eta);
+/* storage of U read by Nfft4GPAmdNysSolve: 64 (default, the reference's fp64) or 32 (an fp32 copy, half the
+ * bytes of the two HBM-bound passes; accumulation stays fp64).  The preconditioner only steers PCG, whose
+ * stopping test is on the true fp64 residual (pcg.c:181-193), so fp32 storage changes the iteration
+ * count at most, not the accuracy of the solution.  Returns 0 or -1. */
+int Nfft4GPAmdNysSetStorage(void *nys, int bits);
 /* hipEvent durations (ms) of a GPU setup's four big kernels: the panel, U1 = Kp G^T, the Gram U1^T U1 and
  * U = U1 W (the three MFMA products, 2 n k^2 flops each); zeros for a handle from Nfft4GPAmdNysCreate */
 int Nfft4GPAmdNysSetupTimes(void *nys, NFFT4GP_DOUBLE *ms4);

@@ -92,6 +92,7 @@ _SIGS = {
     "Nfft4GPAmdNysSetupAdditive": (vp, [vp, vp, C.c_int, C.c_int]),
     "Nfft4GPAmdNysFactors": (C.c_int, [vp, vp, vp, vp, dp]),
     "Nfft4GPAmdNysSetupTimes": (C.c_int, [vp, vp]),
+    "Nfft4GPAmdNysSetStorage": (C.c_int, [vp, C.c_int]),
     "Nfft4GPAmdPrecondNysCreate": (vp, []),
     "Nfft4GPAmdPrecondNysFree": (None, [vp]),
     "Nfft4GPAmdPrecondNysReset": (None, [vp]),

@@ -175,6 +175,7 @@ struct NysDev {
    int n = 0, k = 0;
    double eta = 0.0;
    double* U = nullptr;  // n x k column-major, natural row order
+   float* Uf = nullptr;  // optional fp32 copy the apply reads instead (Nfft4GPAmdNysSetStorage)
    double* s = nullptr;  // k
    double* w = nullptr;  // apply scratch, k
    double* part = nullptr;

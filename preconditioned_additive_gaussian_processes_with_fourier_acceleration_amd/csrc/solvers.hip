@@ -28,6 +28,7 @@ void nys_free(NysDev* N)
    (void)hipStreamSynchronize(current_stream());
    for (double* p : {N->U, N->s, N->w, N->part, N->Kall, N->dU, N->G, N->Gt, N->GdKG, N->D, N->vk, N->vn})
       (void)hipFree(p);
+   (void)hipFree(N->Uf);
    delete N;
 }
 
@@ -312,8 +313,10 @@ constexpr int kNysThreads = 256;
 // partial[blk][j] = sum_{i in blk rows} U[i, j] r[i].  The block's r segment is staged in LDS; each
 // wave walks its columns four at a time with 32 loads per lane in flight, row indices clamped to
 // n - 1 (and r zero-padded) so the loads need no predication.
+// T = float: the fp32 copy of U (Nfft4GPAmdNysSetStorage), widened to fp64 before the fp64 accumulation
 constexpr int kNysUtCols = 4;
-__global__ __launch_bounds__(kNysThreads) void k_nys_ut(const double* __restrict__ U, size_t ldu, int n, int k,
+template <class T>
+__global__ __launch_bounds__(kNysThreads) void k_nys_ut(const T* __restrict__ U, size_t ldu, int n, int k,
                                                        const double* __restrict__ r, double* __restrict__ part)
 {
    constexpr int kPer = kNysRows / 64;
@@ -330,7 +333,7 @@ __global__ __launch_bounds__(kNysThreads) void k_nys_ut(const double* __restrict
    __syncthreads();
    const size_t last = (size_t)n - 1;
    for (int j0 = wave * kNysUtCols; j0 < k; j0 += nwv * kNysUtCols) {
-      const double* col[kNysUtCols];
+      const T* col[kNysUtCols];
 #pragma unroll
       for (int c = 0; c < kNysUtCols; c++) col[c] = U + (size_t)min(j0 + c, k - 1) * ldu;
       double acc[kNysUtCols] = {};
@@ -342,7 +345,7 @@ __global__ __launch_bounds__(kNysThreads) void k_nys_ut(const double* __restrict
 #pragma unroll
             for (int u = 0; u < kChunk; u++) {
                const size_t i = r0 + (size_t)(t + u) * 64 + lane;
-               v[c][u] = __builtin_nontemporal_load(col[c] + (i < last ? i : last));
+               v[c][u] = (double)__builtin_nontemporal_load(col[c] + (i < last ? i : last));
             }
 #pragma unroll
          for (int u = 0; u < kChunk; u++) {
@@ -386,7 +389,8 @@ __global__ __launch_bounds__(64 * kNysWRows) void k_nys_w(const double* __restri
 }
 
 // x[i] = r[i]/eta + sum_j U[i, j] w[j]
-__global__ __launch_bounds__(kNysThreads) void k_nys_u(const double* __restrict__ U, size_t ldu, int n, int k,
+template <class T>
+__global__ __launch_bounds__(kNysThreads) void k_nys_u(const T* __restrict__ U, size_t ldu, int n, int k,
                                                       const double* __restrict__ w, const double* __restrict__ r,
                                                       double eta, double* __restrict__ x)
 {
@@ -396,7 +400,7 @@ __global__ __launch_bounds__(kNysThreads) void k_nys_u(const double* __restrict_
    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
    if (i >= (size_t)n) return;
    double acc = 0.0;
-   for (int j = 0; j < k; j++) acc = fma(U[(size_t)j * ldu + i], s_w[j], acc);
+   for (int j = 0; j < k; j++) acc = fma((double)U[(size_t)j * ldu + i], s_w[j], acc);
    x[i] = r[i] / eta + acc;
 }
 
@@ -435,7 +439,7 @@ namespace nfft4gp_amd {
 int nys_gemv_t(const double* A, size_t lda, int n, int k, const double* x, double* out, double* part, hipStream_t s)
 {
    const int nblk = (n + kNysRows - 1) / kNysRows;
-   hipLaunchKernelGGL(k_nys_ut, dim3(nblk), dim3(kNysThreads), 0, s, A, lda, n, k, x, part);
+   hipLaunchKernelGGL(k_nys_ut<double>, dim3(nblk), dim3(kNysThreads), 0, s, A, lda, n, k, x, part);
    hipLaunchKernelGGL(k_nys_w, dim3((k + 63) / 64), dim3(64 * kNysWRows), 0, s, part, nblk, k, (const double*)nullptr,
                       1.0, out);
    NFFT4GP_HIP_CHECK(hipGetLastError());
@@ -446,13 +450,28 @@ int nys_gemv_t(const double* A, size_t lda, int n, int k, const double* x, doubl
 int nys_apply_dev(NysDev* N, double* x, const double* rhs, hipStream_t s)
 {
    const int n = N->n;
-   hipLaunchKernelGGL(k_nys_ut, dim3(N->nblk), dim3(kNysThreads), 0, s, N->U, (size_t)n, n, N->k, rhs, N->part);
+   if (N->Uf)
+      hipLaunchKernelGGL(k_nys_ut<float>, dim3(N->nblk), dim3(kNysThreads), 0, s, N->Uf, (size_t)n, n, N->k, rhs,
+                         N->part);
+   else
+      hipLaunchKernelGGL(k_nys_ut<double>, dim3(N->nblk), dim3(kNysThreads), 0, s, N->U, (size_t)n, n, N->k, rhs,
+                         N->part);
    hipLaunchKernelGGL(k_nys_w, dim3((N->k + 63) / 64), dim3(64 * kNysWRows), 0, s, N->part, N->nblk, N->k, N->s, N->eta,
                       N->w);
-   hipLaunchKernelGGL(k_nys_u, dim3((n + kNysThreads - 1) / kNysThreads), dim3(kNysThreads), sizeof(double) * N->k, s,
-                      N->U, (size_t)n, n, N->k, N->w, rhs, N->eta, x);
+   if (N->Uf)
+      hipLaunchKernelGGL(k_nys_u<float>, dim3((n + kNysThreads - 1) / kNysThreads), dim3(kNysThreads),
+                         sizeof(double) * N->k, s, N->Uf, (size_t)n, n, N->k, N->w, rhs, N->eta, x);
+   else
+      hipLaunchKernelGGL(k_nys_u<double>, dim3((n + kNysThreads - 1) / kNysThreads), dim3(kNysThreads),
+                         sizeof(double) * N->k, s, N->U, (size_t)n, n, N->k, N->w, rhs, N->eta, x);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
+}
+
+__global__ void k_to_f32(const double* __restrict__ a, size_t count, float* __restrict__ b)
+{
+   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x)
+      b[i] = (float)a[i];
 }
 }  // namespace nfft4gp_amd
 
@@ -805,6 +824,27 @@ void* Nfft4GPAmdNysCreate(int n, int k, const double* U, const double* s, double
    return N;
 }
 
+
+int Nfft4GPAmdNysSetStorage(void* nys, int bits)
+{
+   NysDev* N = (NysDev*)nys;
+   if (!N || (bits != 32 && bits != 64)) return -1;
+   hipStream_t s = current_stream();
+   if (bits == 64) {
+      if (N->Uf) {
+         NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
+         NFFT4GP_HIP_CHECK(hipFree(N->Uf));
+         N->Uf = nullptr;
+      }
+      return 0;
+   }
+   if (N->Uf) return 0;
+   const size_t count = (size_t)N->n * N->k;
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&N->Uf, sizeof(float) * std::max<size_t>(1, count)));
+   hipLaunchKernelGGL(k_to_f32, dim3(4096), dim3(256), 0, s, N->U, count, N->Uf);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
 
 int Nfft4GPAmdNysSolve(void* nys, int n, double* x, double* rhs)
 {

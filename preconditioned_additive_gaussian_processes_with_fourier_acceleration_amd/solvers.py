@@ -45,6 +45,12 @@ class NystromPrecond:
         self.eta = eta.value
         return self
 
+    def set_storage(self, bits: int):
+        """U read by the apply in fp64 (64, the reference's) or as an fp32 copy (32; fp64 accumulation)."""
+        if _lib.lib().Nfft4GPAmdNysSetStorage(self.h, int(bits)):
+            raise ValueError("storage bits must be 32 or 64")
+        return self
+
     def setup_times(self):
         """hipEvent ms of the GPU setup's panel, U1 = Kp G^T, Gram U1^T U1 and U = U1 W kernels."""
         ms = np.zeros(4)

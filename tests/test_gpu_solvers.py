@@ -237,3 +237,35 @@ def test_mfma_gemm_f64_ragged(torch_cuda, tA, M, N, K):
     assert f(tA, M, N, K, Ad.data_ptr(), A.shape[0], Bd.data_ptr(), K, Cd.data_ptr(), M) == 0
     Cm = Cd.cpu().numpy().reshape(N, M).T
     assert np.abs(Cm - ref).max() <= 1e-12 * np.sqrt(K) * np.abs(ref).max()
+
+
+def test_nystrom_fp32_storage_pcg(torch_cuda):
+    """Nfft4GPAmdNysSetStorage(32): the apply reads an fp32 copy of U (fp64 accumulation).  The apply moves
+    by ~1e-7 relative; PCG still stops on its fp64 true residual (pcg.c:181-193), so it reaches the same
+    tolerance, in about as many iterations."""
+    torch = torch_cuda
+    n, d, k = 20000, 8, 64
+    rng = np.random.default_rng(51)
+    X = rng.random((n, d))
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    assert op.setup(amd.GAUSSIAN, 1.0, 0.1, 0.01) == 0
+    pre = amd.NystromPrecond.from_additive(op, rng.permutation(n).astype(np.int32), k, k11="landmarks")
+    r = torch.tensor(rng.random(n) - 0.5, device="cuda")
+    z64 = torch.zeros(n, dtype=torch.float64, device="cuda")
+    pre.solve(z64, r)
+    b = torch.tensor(rng.random(n) - 0.5, device="cuda")
+    x64 = torch.zeros(n, dtype=torch.float64, device="cuda")
+    _, rel64, _, it64 = amd.pcg(op, b, x64, maxits=2000, tol=1e-6, precond=pre)
+    pre.set_storage(32)
+    z32 = torch.zeros(n, dtype=torch.float64, device="cuda")
+    pre.solve(z32, r)
+    assert rel(z32.cpu().numpy(), z64.cpu().numpy()) < 1e-6
+    x32 = torch.zeros(n, dtype=torch.float64, device="cuda")
+    _, rel32, _, it32 = amd.pcg(op, b, x32, maxits=2000, tol=1e-6, precond=pre)
+    assert it64 > 0 and it32 > 0 and rel32 <= 1e-6
+    assert abs(it32 - it64) <= max(2, it64 // 10), (it32, it64)
+    pre.set_storage(64)
+    z = torch.zeros(n, dtype=torch.float64, device="cuda")
+    pre.solve(z, r)
+    assert torch.equal(z, z64)
+    pre.free()
