@@ -273,6 +273,36 @@ int Nfft4GPAmdPrecondNysDvp(void *vnys_mat, int n, int *mask, NFFT4GP_DOUBLE *x,
 int Nfft4GPAmdPrecondNysTrace(void *vnys_mat, NFFT4GP_DOUBLE **tracesp);
 NFFT4GP_DOUBLE Nfft4GPAmdPrecondNysLogdet(void *vnys_mat);
 
+/* ---- FSAI preconditioner built on the GPU, with gradients (SRC/preconds/fsai.h:46-207) ----------------
+ * Drop-ins for Nfft4GPPrecondFsaiCreate / Free / Reset / SetLfil (fsai.c:3-104),
+ * Nfft4GPPrecondFsaiSetupWithKernel (fsai.c:302-673: KNN pattern kernels.c:121-278, per-row Cholesky
+ * solves, gradients), Nfft4GPPrecondFsaiSolve (func_solve, :106-123), Nfft4GPPrecondFsaiDvp (func_dvp,
+ * :125-216), Nfft4GPPrecondFsaiTrace (func_trace, :218-276), Nfft4GPPrecondFsaiLogdet (func_logdet,
+ * :278-301) and the CSR triangular solves Nfft4GPPrecondFsaiInvL / InvLT (:675-728), level-scheduled on
+ * the device.  The setup's kernel is the plain Gaussian (default, or fkernel ==
+ * Nfft4GPNFFTAdditiveKernelGaussianKernel) or Matern-1/2 (Nfft4GPAmdPrecondFsaiSetKernel(.., 1), or fkernel
+ * == Nfft4GPNFFTAdditiveKernelMatern12Kernel) kernel of all d columns of data, with _params[0] = f,
+ * _params[1] = l, _noise_level = mu read from fkernel_params (any struct with the nfft4gp_kernel layout,
+ * the reference's Nfft4GPKernelParamCreate handle included); lfil <= 64, d <= 256.
+ * Nfft4GPAmdPrecondFsaiSetCsr loads given factors (e.g. the reference's _L_i, _L_j, _L_a, _dL_a; da may be
+ * NULL); Nfft4GPAmdPrecondFsaiCsr copies them out (any output may be NULL) and returns nnz. */
+void *Nfft4GPAmdPrecondFsaiCreate(void);
+void Nfft4GPAmdPrecondFsaiFree(void *str);
+void Nfft4GPAmdPrecondFsaiReset(void *str);
+void Nfft4GPAmdPrecondFsaiSetLfil(void *str, int lfil);
+void Nfft4GPAmdPrecondFsaiSetKernel(void *str, int kernel);
+int Nfft4GPAmdPrecondFsaiSetupWithKernel(NFFT4GP_DOUBLE *data, int n, int ldim, int d, func_kernel fkernel,
+                                         void *fkernel_params, int require_grad, void *vfsai_mat);
+int Nfft4GPAmdPrecondFsaiSetCsr(void *vfsai_mat, int n, const int *ia, const int *ja, const NFFT4GP_DOUBLE *aa,
+                                const NFFT4GP_DOUBLE *da);
+int Nfft4GPAmdPrecondFsaiCsr(void *vfsai_mat, int *ia, int *ja, NFFT4GP_DOUBLE *aa, NFFT4GP_DOUBLE *da);
+int Nfft4GPAmdPrecondFsaiSolve(void *vfsai_mat, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
+int Nfft4GPAmdPrecondFsaiInvL(void *vfsai_mat, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
+int Nfft4GPAmdPrecondFsaiInvLT(void *vfsai_mat, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
+int Nfft4GPAmdPrecondFsaiDvp(void *vfsai_mat, int n, int *mask, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE **yp);
+int Nfft4GPAmdPrecondFsaiTrace(void *vfsai_mat, NFFT4GP_DOUBLE **tracesp);
+NFFT4GP_DOUBLE Nfft4GPAmdPrecondFsaiLogdet(void *vfsai_mat);
+
 /* ---- FSAI preconditioner apply (SRC/preconds/fsai.c:106-123) --------------------------------------
  * The reference's Nfft4GPPrecondFsaiSetupWithKernel (fsai.c:333-...) produces the lower-triangular
  * factor L in CSR (precond_fsai _L_i, _L_j, _L_a; fsai.h:11-58).  Nfft4GPAmdFsaiCreate takes those

@@ -382,7 +382,7 @@ class RefFsai:
     ``kernel`` names a func_kernel of the reference (default its dense Gaussian kernel, kernels.c:680)
     and ``params`` its parameter handle."""
 
-    def __init__(self, data, params, lfil, kernel="Nfft4GPKernelGaussianKernel"):
+    def __init__(self, data, params, lfil, kernel="Nfft4GPKernelGaussianKernel", grad=False):
         lib = ref_lib()
         self.lib = lib
         lib.Nfft4GPPrecondFsaiCreate.restype = C.c_void_p
@@ -396,9 +396,17 @@ class RefFsai:
         self.h = lib.Nfft4GPPrecondFsaiCreate()
         lib.Nfft4GPPrecondFsaiSetLfil(self.h, lfil)
         fk = C.cast(getattr(lib, kernel), C.c_void_p)
-        rc = lib.Nfft4GPPrecondFsaiSetupWithKernel(_d(self._data), n, n, d, fk, params, 0, self.h)
+        rc = lib.Nfft4GPPrecondFsaiSetupWithKernel(_d(self._data), n, n, d, fk, params, 1 if grad else 0, self.h)
         assert rc == 0
         self.st = PrecondFsaiStruct.from_address(self.h)
+        self.grad = grad
+        for name, args in (("Nfft4GPPrecondFsaiDvp", [C.c_void_p, C.c_int, _ip, _dp, C.POINTER(_dp)]),
+                           ("Nfft4GPPrecondFsaiTrace", [C.c_void_p, C.POINTER(_dp)]),
+                           ("Nfft4GPPrecondFsaiLogdet", [C.c_void_p]),
+                           ("Nfft4GPPrecondFsaiInvL", [C.c_void_p, C.c_int, _dp, _dp]),
+                           ("Nfft4GPPrecondFsaiInvLT", [C.c_void_p, C.c_int, _dp, _dp])):
+            getattr(lib, name).argtypes = args
+        lib.Nfft4GPPrecondFsaiLogdet.restype = C.c_double
 
     def csr(self):
         n = self.n
@@ -413,6 +421,34 @@ class RefFsai:
         x = np.zeros(self.n)
         self.lib.Nfft4GPPrecondFsaiSolve(C.c_void_p(self.h), self.n, _d(x), _d(rhs))
         return x
+
+    def dl(self):
+        """the gradient factors dL_a (3 nnz: f, l, mu), fsai.c:472-476"""
+        nnz = int(np.ctypeslib.as_array(self.st._L_i, shape=(self.n + 1,))[self.n])
+        return np.ctypeslib.as_array(self.st._dL_a, shape=(3 * nnz,)).copy()
+
+    def inv_l(self, rhs, trans=False):
+        rhs = np.ascontiguousarray(rhs, dtype=np.float64)
+        x = np.zeros(self.n)
+        fn = self.lib.Nfft4GPPrecondFsaiInvLT if trans else self.lib.Nfft4GPPrecondFsaiInvL
+        fn(C.c_void_p(self.h), self.n, _d(x), _d(rhs))
+        return x
+
+    def dvp(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros(3 * self.n)
+        yp = _d(y)
+        assert self.lib.Nfft4GPPrecondFsaiDvp(C.c_void_p(self.h), self.n, None, _d(x), C.byref(yp)) == 0
+        return y
+
+    def trace(self):
+        t = np.zeros(3)
+        tp = _d(t)
+        assert self.lib.Nfft4GPPrecondFsaiTrace(C.c_void_p(self.h), C.byref(tp)) == 0
+        return t
+
+    def logdet(self):
+        return float(self.lib.Nfft4GPPrecondFsaiLogdet(C.c_void_p(self.h)))
 
 
 def ref_schur_params(data, perm, k, chol_K11, gauss_params):

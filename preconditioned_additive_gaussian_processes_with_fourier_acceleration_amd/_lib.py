@@ -93,6 +93,20 @@ _SIGS = {
     "Nfft4GPAmdNysFactors": (C.c_int, [vp, vp, vp, vp, dp]),
     "Nfft4GPAmdNysSetupTimes": (C.c_int, [vp, vp]),
     "Nfft4GPAmdNysSetStorage": (C.c_int, [vp, C.c_int]),
+    "Nfft4GPAmdPrecondFsaiCreate": (vp, []),
+    "Nfft4GPAmdPrecondFsaiFree": (None, [vp]),
+    "Nfft4GPAmdPrecondFsaiReset": (None, [vp]),
+    "Nfft4GPAmdPrecondFsaiSetLfil": (None, [vp, C.c_int]),
+    "Nfft4GPAmdPrecondFsaiSetKernel": (None, [vp, C.c_int]),
+    "Nfft4GPAmdPrecondFsaiSetupWithKernel": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp]),
+    "Nfft4GPAmdPrecondFsaiSetCsr": (C.c_int, [vp, C.c_int, vp, vp, vp, vp]),
+    "Nfft4GPAmdPrecondFsaiCsr": (C.c_int, [vp, vp, vp, vp, vp]),
+    "Nfft4GPAmdPrecondFsaiSolve": (C.c_int, [vp, C.c_int, vp, vp]),
+    "Nfft4GPAmdPrecondFsaiInvL": (C.c_int, [vp, C.c_int, vp, vp]),
+    "Nfft4GPAmdPrecondFsaiInvLT": (C.c_int, [vp, C.c_int, vp, vp]),
+    "Nfft4GPAmdPrecondFsaiDvp": (C.c_int, [vp, C.c_int, vp, vp, vp]),
+    "Nfft4GPAmdPrecondFsaiTrace": (C.c_int, [vp, vp]),
+    "Nfft4GPAmdPrecondFsaiLogdet": (C.c_double, [vp]),
     "Nfft4GPAmdPrecondNysCreate": (vp, []),
     "Nfft4GPAmdPrecondNysFree": (None, [vp]),
     "Nfft4GPAmdPrecondNysReset": (None, [vp]),

@@ -1,0 +1,750 @@
+// fsai_setup.hip -- the FSAI preconditioner built on the GPU, with gradients, behind the reference's
+// interface (SRC/preconds/fsai.h:46-207):
+//
+//   Nfft4GPAmdPrecondFsaiCreate / SetLfil / Reset / Free          fsai.c:3-104
+//   Nfft4GPAmdPrecondFsaiSetupWithKernel (precond_kernel_setup)   fsai.c:302-312 -> :314-673
+//       pattern  Nfft4GPDistanceEuclidKnn (kernels.c:121-278): row i < lfil is dense (0..i); row i >= lfil
+//                holds the lfil-1 nearest points among 0..i-1, then i.  k_knn: one workgroup per row, an
+//                MSB-first radix select on the bits of the squared distances (non-negative doubles order
+//                like their bit patterns), then a rank sort of the survivors by (distance, index).
+//       values   per row, the kernel submatrix K_a of its points, L_a = chol(K_a), A_ai = K_a^{-1} e_k /
+//                sqrt(e_k' K_a^{-1} e_k); with gradients dA_g = K_a^{-1}(-dK_g A_ai) - 1/2 (.)_k dd A_ai
+//                (fsai.c:530-563).  k_fsai_rows: one wave per row, K_a in LDS.
+//   Nfft4GPAmdPrecondFsaiSolve  (func_solve)   x = L^T (L rhs)                 fsai.c:106-123
+//   Nfft4GPAmdPrecondFsaiInvL / InvLT          L^{-1} rhs, L^{-T} rhs          fsai.c:675-728
+//   Nfft4GPAmdPrecondFsaiDvp    (func_dvp)                                     fsai.c:125-216
+//   Nfft4GPAmdPrecondFsaiTrace  (func_trace)   2 sum_i dL_g(i,i) / L(i,i)      fsai.c:218-276
+//   Nfft4GPAmdPrecondFsaiLogdet (func_logdet)  2 sum_i log(1 / L(i,i))         fsai.c:278-301
+//
+// The triangular solves are CSR SpTRSVs over level sets computed once at setup (a row's level is one
+// more than its dependencies'; ~250 levels for 2e4 KNN rows): ONE workgroup walks the levels with a
+// barrier between them, so there is no grid-wide synchronisation and no spinning.  Each row sums in the
+// reference's order with unfused multiply-add, so given the same factors the solves, products and Dvp
+// are bitwise the reference's.
+//
+// Kernel: the plain (non-additive) Gaussian or Matern-1/2 kernel of all d columns of `data` with the
+// parameters of `fkernel_params` (_params[0] = f, _params[1] = l, _noise_level = mu; kernels.c:680-1289,
+// :2390-3033), as the reference's FSAI runs on Nfft4GPKernelGaussianKernel.  The reference's FSAI on its
+// additive kernel would evaluate buffer rows instead of the pattern's points (kernels.c:3160 ignores
+// the data argument); this library does not reproduce that.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "callbacks.hpp"
+#include "internal.h"
+
+using namespace nfft4gp_amd;
+
+namespace {
+
+constexpr int kFsaiMaxK = 64;      // entries per row (lfil) the per-row kernel holds in LDS
+constexpr int kKnnThreads = 256;
+constexpr int kKnnGather = 256;    // survivors of the radix select sorted directly
+constexpr int kMaxDims = 256;      // features of `data`
+constexpr int kTrsvThreads = 1024;
+
+__device__ __forceinline__ double sqdist(const double* __restrict__ X, int ldim, int d, const double* xi, int j)
+{
+   double s = 0.0;
+   for (int c = 0; c < d; c++) {
+      const double t = X[(size_t)c * ldim + j] - xi[c];
+      s = fma(t, t, s);
+   }
+   return s;
+}
+
+// pattern rows i in [lfil, n): ja[ia[i] .. ia[i] + lfil - 2] = the lfil-1 nearest of 0..i-1 by
+// (squared distance, index), ja[ia[i] + lfil - 1] = i.  Grid-stride over rows.
+__global__ __launch_bounds__(kKnnThreads) void k_knn(const double* __restrict__ X, int ldim, int n, int d, int lfil,
+                                                     const int* __restrict__ ia, int* __restrict__ ja)
+{
+   __shared__ unsigned int hist[256];
+   __shared__ double s_xi[kMaxDims];
+   __shared__ unsigned long long s_key[kKnnGather + kFsaiMaxK];
+   __shared__ int s_idx[kKnnGather + kFsaiMaxK];
+   __shared__ int s_nsel, s_ngat;
+   __shared__ unsigned long long s_prefix;
+   __shared__ int s_bits, s_need, s_eq;
+   const int tid = threadIdx.x;
+   const int K = lfil - 1;
+   for (int i = lfil + blockIdx.x; i < n; i += gridDim.x) {
+      for (int c = tid; c < d; c += kKnnThreads) s_xi[c] = X[(size_t)c * ldim + i];
+      if (tid == 0) {
+         s_prefix = 0ull;
+         s_bits = 0;
+         s_need = K;
+         s_eq = i;
+      }
+      __syncthreads();
+      // MSB-first radix select: narrow the prefix of the K-th smallest key byte by byte until the
+      // candidates that share it fit the gather buffer
+      while (s_bits < 64 && s_eq > kKnnGather) {
+         const int bits = s_bits;
+         const unsigned long long prefix = s_prefix;
+         for (int b = tid; b < 256; b += kKnnThreads) hist[b] = 0u;
+         __syncthreads();
+         for (int j = tid; j < i; j += kKnnThreads) {
+            const unsigned long long u = (unsigned long long)__double_as_longlong(sqdist(X, ldim, d, s_xi, j));
+            if (bits == 0 || (u >> (64 - bits)) == prefix) atomicAdd(&hist[(u >> (56 - bits)) & 255ull], 1u);
+         }
+         __syncthreads();
+         if (tid == 0) {
+            unsigned int cum = 0;
+            int b = 0;
+            for (; b < 255; b++) {
+               if (cum + hist[b] >= (unsigned)s_need) break;
+               cum += hist[b];
+            }
+            s_need -= (int)cum;
+            s_eq = (int)hist[b];
+            s_prefix = (prefix << 8) | (unsigned long long)b;
+            s_bits = bits + 8;
+         }
+         __syncthreads();
+      }
+      // collect: keys below the prefix are in; keys equal to it compete for the remaining s_need slots
+      if (tid == 0) {
+         s_nsel = 0;
+         s_ngat = 0;
+      }
+      __syncthreads();
+      {
+         const int bits = s_bits;
+         const unsigned long long prefix = s_prefix;
+         for (int j = tid; j < i; j += kKnnThreads) {
+            const unsigned long long u = (unsigned long long)__double_as_longlong(sqdist(X, ldim, d, s_xi, j));
+            const unsigned long long top = bits == 0 ? 0ull : (u >> (64 - bits));
+            if (bits > 0 && top < prefix) {
+               const int p = atomicAdd(&s_nsel, 1);
+               s_key[kKnnGather + p] = u;
+               s_idx[kKnnGather + p] = j;
+            } else if (bits == 0 || top == prefix) {
+               const int p = atomicAdd(&s_ngat, 1);
+               if (p < kKnnGather) {
+                  s_key[p] = u;
+                  s_idx[p] = j;
+               }
+            }
+         }
+      }
+      __syncthreads();
+      // rank the gathered candidates by (key, index); the first s_need join the selection
+      const int ng = min(s_ngat, kKnnGather);
+      const int nsel0 = s_nsel;
+      __syncthreads();
+      for (int e = tid; e < ng; e += kKnnThreads) {
+         const unsigned long long ke = s_key[e];
+         const int ie = s_idx[e];
+         int rank = 0;
+         for (int o = 0; o < ng; o++) {
+            const unsigned long long ko = s_key[o];
+            rank += (ko < ke || (ko == ke && s_idx[o] < ie)) ? 1 : 0;
+         }
+         if (rank < K - nsel0) {
+            s_key[kKnnGather + nsel0 + rank] = ke;
+            s_idx[kKnnGather + nsel0 + rank] = ie;
+         }
+      }
+      __syncthreads();
+      // final order of the K neighbours: by (key, index), then the point itself
+      const int row = ia[i];
+      for (int e = tid; e < K; e += kKnnThreads) {
+         const unsigned long long ke = s_key[kKnnGather + e];
+         const int ie = s_idx[kKnnGather + e];
+         int rank = 0;
+         for (int o = 0; o < K; o++) {
+            const unsigned long long ko = s_key[kKnnGather + o];
+            rank += (ko < ke || (ko == ke && s_idx[kKnnGather + o] < ie)) ? 1 : 0;
+         }
+         ja[row + rank] = ie;
+      }
+      if (tid == 0) ja[row + K] = i;
+      __syncthreads();
+   }
+}
+
+struct KernelParams {
+   int kernel;  // 0 Gaussian, 1 Matern-1/2
+   double f2, inv, mu;
+   double df_scale;  // 2/f
+   double dl_scale;  // f^2 / l^3 (Gaussian) or f^2 / l^2 (Matern)
+};
+
+// K entry from the squared distance (off-diagonal) and the three derivative entries (fsai.c:530 dK_a)
+__device__ __forceinline__ void kern_entry(const KernelParams& P, double s, bool diag, double& K, double* dK)
+{
+   if (diag) {
+      K = P.f2 + P.f2 * P.mu;  // f^2 + noise_level (kernels.c:695)
+      dK[0] = P.df_scale * K;
+      dK[1] = 0.0;
+      dK[2] = P.f2;
+      return;
+   }
+   const double r = (P.kernel == 0) ? s : sqrt(s);
+   const double e = exp(-r * P.inv);
+   K = P.f2 * e;
+   dK[0] = P.df_scale * K;
+   dK[1] = P.dl_scale * r * e;
+   dK[2] = 0.0;
+}
+
+// In place on the wave's LDS vector b: b = L^{-1} b (trans = 0) or L^{-T} b (trans = 1), L lower in A.
+__device__ void wave_trsv(double (*A)[kFsaiMaxK + 1], int k, double* b, int trans)
+{
+   const int lane = threadIdx.x;
+   if (!trans) {
+      for (int m = 0; m < k; m++) {
+         if (lane == 0) b[m] /= A[m][m];
+         __syncthreads();
+         if (lane > m && lane < k) b[lane] -= A[lane][m] * b[m];
+         __syncthreads();
+      }
+   } else {
+      for (int m = k - 1; m >= 0; m--) {
+         if (lane == 0) b[m] /= A[m][m];
+         __syncthreads();
+         if (lane < m) b[lane] -= A[m][lane] * b[m];
+         __syncthreads();
+      }
+   }
+}
+
+// one wave per row i: A_ai (and dA_ai for the three gradients) into aa / da (fsai.c:353-398, :493-563)
+__global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, int ldim, int d,
+                                                  const int* __restrict__ ia, const int* __restrict__ ja,
+                                                  KernelParams P, int grad, int nnz, double* __restrict__ aa,
+                                                  double* __restrict__ da)
+{
+   __shared__ double A[kFsaiMaxK][kFsaiMaxK + 1];
+   __shared__ double a[kFsaiMaxK], u[kFsaiMaxK];
+   __shared__ int idx[kFsaiMaxK];
+   const int i = blockIdx.x;
+   const int lane = threadIdx.x;
+   const int j1 = ia[i];
+   const int k = ia[i + 1] - j1;
+   if (lane < k) idx[lane] = ja[j1 + lane];
+   __syncthreads();
+   // K_a (lower triangle is all the factorisation reads)
+   for (int e = lane; e < k * k; e += 64) {
+      const int r = e % k, c = e / k;
+      if (c > r) continue;
+      double s = 0.0;
+      for (int dd = 0; dd < d; dd++) {
+         const double t = X[(size_t)dd * ldim + idx[r]] - X[(size_t)dd * ldim + idx[c]];
+         s = fma(t, t, s);
+      }
+      double K, dK[3];
+      kern_entry(P, s, r == c, K, dK);
+      A[r][c] = K;
+   }
+   __syncthreads();
+   // Cholesky, lower (dpotrf 'L')
+   for (int j = 0; j < k; j++) {
+      if (lane == 0) A[j][j] = sqrt(A[j][j]);
+      __syncthreads();
+      if (lane > j && lane < k) A[lane][j] /= A[j][j];
+      __syncthreads();
+      if (lane > j && lane < k) {
+         const double arj = A[lane][j];
+         for (int c = j + 1; c <= lane; c++) A[lane][c] -= arj * A[c][j];
+      }
+      __syncthreads();
+   }
+   // A_ai = K_a^{-1} e_k, scaled by 1/sqrt(its last entry)
+   if (lane < k) a[lane] = (lane == k - 1) ? 1.0 : 0.0;
+   __syncthreads();
+   wave_trsv(A, k, a, 0);
+   wave_trsv(A, k, a, 1);
+   const double dd_scale = 1.0 / sqrt(a[k - 1]);
+   __syncthreads();
+   if (lane < k) {
+      a[lane] *= dd_scale;
+      aa[j1 + lane] = a[lane];
+   }
+   __syncthreads();
+   if (!grad) return;
+   for (int g = 0; g < 3; g++) {
+      // u = -dK_g A_ai (dK_g recomputed from the coordinates: K_a's storage now holds its factor)
+      if (lane < k) {
+         double acc = 0.0;
+         for (int c = 0; c < k; c++) {
+            double s = 0.0;
+            for (int dd = 0; dd < d; dd++) {
+               const double t = X[(size_t)dd * ldim + idx[lane]] - X[(size_t)dd * ldim + idx[c]];
+               s = fma(t, t, s);
+            }
+            double K, dK[3];
+            kern_entry(P, s, lane == c, K, dK);
+            acc = fma(dK[g], a[c], acc);
+         }
+         u[lane] = -acc;
+      }
+      __syncthreads();
+      wave_trsv(A, k, u, 0);
+      wave_trsv(A, k, u, 1);
+      const double t = -0.5 * u[k - 1] * dd_scale;
+      __syncthreads();
+      if (lane < k) da[(size_t)g * nnz + j1 + lane] = fma(t, a[lane], u[lane]);
+      __syncthreads();
+   }
+}
+
+// ---- level-scheduled CSR triangular solves: one workgroup, a barrier between levels ----------------
+// x = L^{-1} rhs (fsai.c:675-699): x[i] = (rhs[i] - sum_{j < diag} L_ij x_j) / L_ii in the row's order
+__global__ __launch_bounds__(kTrsvThreads) void k_trsv_lower(const int* __restrict__ lev_ptr, int nlev,
+                                                             const int* __restrict__ lev_rows,
+                                                             const int* __restrict__ ia, const int* __restrict__ ja,
+                                                             const double* __restrict__ aa,
+                                                             const double* __restrict__ rhs, double* x)
+{
+#pragma clang fp contract(off)  // the reference's host build: separate multiply and subtract
+   for (int lv = 0; lv < nlev; lv++) {
+      for (int e = lev_ptr[lv] + threadIdx.x; e < lev_ptr[lv + 1]; e += kTrsvThreads) {
+         const int i = lev_rows[e];
+         const int j2 = ia[i + 1] - 1;
+         double s = rhs[i];
+         for (int j = ia[i]; j < j2; j++) s -= aa[j] * x[ja[j]];
+         x[i] = s / aa[j2];
+      }
+      __syncthreads();
+   }
+}
+
+// x = L^{-T} rhs (fsai.c:701-728) through L^T stored as CSR (tia/tja/taa: column c of L, rows ascending,
+// diagonal first): the reference subtracts L_ic x_i from x[c] for i descending, then divides by L_cc
+__global__ __launch_bounds__(kTrsvThreads) void k_trsv_upper(const int* __restrict__ lev_ptr, int nlev,
+                                                             const int* __restrict__ lev_rows,
+                                                             const int* __restrict__ tia,
+                                                             const int* __restrict__ tja,
+                                                             const double* __restrict__ taa,
+                                                             const double* __restrict__ rhs, double* x)
+{
+#pragma clang fp contract(off)
+   for (int lv = 0; lv < nlev; lv++) {
+      for (int e = lev_ptr[lv] + threadIdx.x; e < lev_ptr[lv + 1]; e += kTrsvThreads) {
+         const int c = lev_rows[e];
+         const int p0 = tia[c];
+         double s = rhs[c];
+         for (int p = tia[c + 1] - 1; p > p0; p--) s -= taa[p] * x[tja[p]];
+         x[c] = s / taa[p0];
+      }
+      __syncthreads();
+   }
+}
+
+// y = beta y + A x for a CSR A (matops.c:139-272 with alpha = 1, beta in {0, 1}): the row accumulates
+// into y[i] itself (matops.c:247), in row order, unfused
+__global__ void k_csr_mv(const int* __restrict__ ia, const int* __restrict__ ja, const double* __restrict__ a,
+                         const double* __restrict__ x, double* __restrict__ y, int n, int beta_one)
+{
+#pragma clang fp contract(off)
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= n) return;
+   double r = beta_one ? y[i] : 0.0;
+   for (int j = ia[i]; j < ia[i + 1]; j++) r += a[j] * x[ja[j]];
+   y[i] = r;
+}
+
+// out[blk] = sum over the block's rows of num[diag_i] / den[diag_i] (or log(1 / den[diag_i]) when num is
+// NULL), diag_i = ia[i+1] - 1; the host sums the blocks in order
+__global__ __launch_bounds__(256) void k_diag_sum(const int* __restrict__ ia, int n, const double* __restrict__ num,
+                                                  const double* __restrict__ den, double* __restrict__ out)
+{
+   __shared__ double s[4];
+   const int i = blockIdx.x * 256 + threadIdx.x;
+   double v = 0.0;
+   if (i < n) {
+      const int p = ia[i + 1] - 1;
+      v = num ? num[p] / den[p] : log(1.0 / den[p]);
+   }
+   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+   __syncthreads();
+   if (threadIdx.x == 0) out[blockIdx.x] = (s[0] + s[1]) + (s[2] + s[3]);
+}
+
+__global__ void k_gather_vals(const double* __restrict__ src, const int* __restrict__ map, int count,
+                              double* __restrict__ dst)
+{
+   const int p = blockIdx.x * blockDim.x + threadIdx.x;
+   if (p < count) dst[p] = src[map[p]];
+}
+
+// the reference's precond_fsai, restated, with the device factors
+struct PrecondFsaiAmd {
+   int lfil = 50;  // fsai.c:12
+   int kernel = 0;
+   int n = 0, nnz = 0;
+   bool grad = false;
+   int *ia = nullptr, *ja = nullptr, *tia = nullptr, *tja = nullptr, *tmap = nullptr;
+   double *aa = nullptr, *taa = nullptr, *da = nullptr, *tda = nullptr;  // da, tda: 3 nnz
+   int *lev_ptr = nullptr, *lev_rows = nullptr, *rlev_ptr = nullptr, *rlev_rows = nullptr;
+   int nlev = 0, nrlev = 0;
+   double *work = nullptr, *part = nullptr;
+   void release()
+   {
+      (void)hipStreamSynchronize(current_stream());
+      for (int* p : {ia, ja, tia, tja, tmap, lev_ptr, lev_rows, rlev_ptr, rlev_rows}) (void)hipFree(p);
+      for (double* p : {aa, taa, da, tda, work, part}) (void)hipFree(p);
+      ia = ja = tia = tja = tmap = lev_ptr = lev_rows = rlev_ptr = rlev_rows = nullptr;
+      aa = taa = da = tda = work = part = nullptr;
+      n = nnz = nlev = nrlev = 0;
+      grad = false;
+   }
+};
+
+template <class T>
+int upload(T** d, const T* h, size_t count)
+{
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)d, sizeof(T) * std::max<size_t>(1, count)));
+   if (count && h) NFFT4GP_HIP_CHECK(hipMemcpy(*d, h, sizeof(T) * count, hipMemcpyHostToDevice));
+   return 0;
+}
+
+// level sets of the lower solve (a row after all its dependencies) and of the transposed solve
+void level_sets(int n, const std::vector<int>& ia, const std::vector<int>& ja, std::vector<int>& ptr,
+                std::vector<int>& rows, bool transposed)
+{
+   std::vector<int> lev(n, 0);
+   int maxlev = 0;
+   if (!transposed) {
+      for (int i = 0; i < n; i++) {
+         int l = 0;
+         for (int p = ia[i]; p < ia[i + 1] - 1; p++) l = std::max(l, lev[ja[p]] + 1);
+         lev[i] = l;
+         maxlev = std::max(maxlev, l);
+      }
+   } else {
+      for (int j = n - 1; j >= 0; j--)
+         for (int p = ia[j]; p < ia[j + 1] - 1; p++) lev[ja[p]] = std::max(lev[ja[p]], lev[j] + 1);
+      for (int i = 0; i < n; i++) maxlev = std::max(maxlev, lev[i]);
+   }
+   ptr.assign(maxlev + 2, 0);
+   for (int i = 0; i < n; i++) ptr[lev[i] + 1]++;
+   for (int l = 0; l <= maxlev; l++) ptr[l + 1] += ptr[l];
+   rows.assign(n, 0);
+   std::vector<int> pos(ptr.begin(), ptr.end() - 1);
+   for (int i = 0; i < n; i++) rows[pos[lev[i]]++] = i;
+}
+
+// device factors from host CSR (ia, ja, aa [, da 3 nnz]): L, L^T (column entries in ascending row order,
+// the order Nfft4GPCsrMv('T') accumulates in), the map between them, the level sets
+int fsai_load(PrecondFsaiAmd* F, int n, const int* ia, const int* ja, const double* aa, const double* da)
+{
+   F->release();
+   const int nnz = ia[n];
+   std::vector<int> hia(ia, ia + n + 1), hja(ja, ja + nnz);
+   std::vector<int> tcnt(n + 1, 0), tia(n + 1, 0), tja(nnz), tmap(nnz);
+   for (int p = 0; p < nnz; p++) tcnt[ja[p] + 1]++;
+   for (int c = 0; c < n; c++) tia[c + 1] = tia[c] + tcnt[c + 1];
+   std::vector<int> pos(tia.begin(), tia.end() - 1);
+   for (int i = 0; i < n; i++)
+      for (int p = ia[i]; p < ia[i + 1]; p++) {
+         const int q = pos[ja[p]]++;
+         tja[q] = i;
+         tmap[q] = p;
+      }
+   std::vector<int> lp, lr, rp, rr;
+   level_sets(n, hia, hja, lp, lr, false);
+   level_sets(n, hia, hja, rp, rr, true);
+   F->n = n;
+   F->nnz = nnz;
+   F->nlev = (int)lp.size() - 1;
+   F->nrlev = (int)rp.size() - 1;
+   // reverse the transposed levels: the first processed holds the rows with no later dependents
+   if (upload(&F->ia, hia.data(), hia.size()) || upload(&F->ja, hja.data(), hja.size()) ||
+       upload(&F->tia, tia.data(), tia.size()) || upload(&F->tja, tja.data(), tja.size()) ||
+       upload(&F->tmap, tmap.data(), tmap.size()) || upload(&F->lev_ptr, lp.data(), lp.size()) ||
+       upload(&F->lev_rows, lr.data(), lr.size()) || upload(&F->rlev_ptr, rp.data(), rp.size()) ||
+       upload(&F->rlev_rows, rr.data(), rr.size()) || upload(&F->aa, aa, (size_t)nnz) ||
+       upload(&F->taa, (const double*)nullptr, (size_t)nnz) || upload(&F->work, (const double*)nullptr, 3 * (size_t)n) ||
+       upload(&F->part, (const double*)nullptr, (size_t)(n + 255) / 256 + 1))
+      return -1;
+   hipStream_t s = current_stream();
+   hipLaunchKernelGGL(k_gather_vals, dim3((nnz + 255) / 256), dim3(256), 0, s, F->aa, F->tmap, nnz, F->taa);
+   if (da) {
+      if (upload(&F->da, da, 3 * (size_t)nnz) || upload(&F->tda, (const double*)nullptr, 3 * (size_t)nnz)) return -1;
+      for (int g = 0; g < 3; g++)
+         hipLaunchKernelGGL(k_gather_vals, dim3((nnz + 255) / 256), dim3(256), 0, s, F->da + (size_t)g * nnz, F->tmap,
+                            nnz, F->tda + (size_t)g * nnz);
+      F->grad = true;
+   }
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int inv_l(PrecondFsaiAmd* F, double* x, const double* rhs, hipStream_t s)
+{
+   hipLaunchKernelGGL(k_trsv_lower, dim3(1), dim3(kTrsvThreads), 0, s, F->lev_ptr, F->nlev, F->lev_rows, F->ia, F->ja,
+                      F->aa, rhs, x);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int inv_lt(PrecondFsaiAmd* F, double* x, const double* rhs, hipStream_t s)
+{
+   hipLaunchKernelGGL(k_trsv_upper, dim3(1), dim3(kTrsvThreads), 0, s, F->rlev_ptr, F->nrlev, F->rlev_rows, F->tia,
+                      F->tja, F->taa, rhs, x);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+void csr_mv(const int* ia, const int* ja, const double* a, const double* x, double* y, int n, int beta_one,
+            hipStream_t s)
+{
+   hipLaunchKernelGGL(k_csr_mv, dim3((n + 255) / 256), dim3(256), 0, s, ia, ja, a, x, y, n, beta_one);
+}
+
+// fsai.c:163-200 for gradient g on device vectors; y: n entries
+int dvp_one(PrecondFsaiAmd* F, int g, const double* x, double* y, hipStream_t s)
+{
+   const int n = F->n;
+   double* w1 = F->work;
+   double* w2 = F->work + n;
+   const double* dl = F->da + (size_t)g * F->nnz;
+   const double* tdl = F->tda + (size_t)g * F->nnz;
+   if (inv_lt(F, w1, x, s)) return -1;            // work = L^{-T} x
+   csr_mv(F->tia, F->tja, tdl, w1, y, n, 0, s);   // y = dL^T work
+   if (inv_lt(F, w2, y, s)) return -1;            // work2 = L^{-T} y
+   if (inv_l(F, y, w1, s)) return -1;             // y = L^{-1} work
+   csr_mv(F->ia, F->ja, dl, y, w2, n, 1, s);      // work2 += dL y
+   csr_mv(F->tia, F->tja, F->taa, w2, y, n, 0, s);  // y = L^T work2
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+double diag_sum(PrecondFsaiAmd* F, const double* num, hipStream_t s)
+{
+   const int nb = (F->n + 255) / 256;
+   hipLaunchKernelGGL(k_diag_sum, dim3(nb), dim3(256), 0, s, F->ia, F->n, num, F->aa, F->part);
+   std::vector<double> h(nb);
+   if (hipMemcpyAsync(h.data(), F->part, sizeof(double) * nb, hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess)
+      return NAN;
+   double v = 0.0;
+   for (double t : h) v += t;
+   return v;
+}
+
+}  // namespace
+
+extern "C" {
+
+void* Nfft4GPAmdPrecondFsaiCreate(void) { return new PrecondFsaiAmd(); }
+
+void Nfft4GPAmdPrecondFsaiSetLfil(void* str, int lfil)
+{
+   if (str) ((PrecondFsaiAmd*)str)->lfil = lfil;
+}
+
+void Nfft4GPAmdPrecondFsaiSetKernel(void* str, int kernel)
+{
+   if (str) ((PrecondFsaiAmd*)str)->kernel = kernel ? 1 : 0;
+}
+
+void Nfft4GPAmdPrecondFsaiReset(void* str)
+{
+   if (str) ((PrecondFsaiAmd*)str)->release();  // keeps lfil (fsai.c:60-98)
+}
+
+void Nfft4GPAmdPrecondFsaiFree(void* str)
+{
+   PrecondFsaiAmd* F = (PrecondFsaiAmd*)str;
+   if (!F) return;
+   F->release();
+   delete F;
+}
+
+int Nfft4GPAmdPrecondFsaiSetupWithKernel(double* data, int n, int ldim, int d, func_kernel fkernel,
+                                         void* fkernel_params, int require_grad, void* vfsai_mat)
+{
+   PrecondFsaiAmd* F = (PrecondFsaiAmd*)vfsai_mat;
+   if (!F || !need_device("Nfft4GPAmdPrecondFsaiSetupWithKernel")) return -1;
+   const nfft4gp_kernel* kp = (const nfft4gp_kernel*)fkernel_params;
+   const int lfil = F->lfil;
+   if (!kp || !data || n <= 0 || ldim < n || d <= 0 || d > kMaxDims || lfil < 1 || lfil > kFsaiMaxK) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondFsaiSetupWithKernel needs kernel parameters, 1 <= lfil <= %d "
+                      "and at most %d features\n", kFsaiMaxK, kMaxDims);
+      return -1;
+   }
+   int kernel = F->kernel;
+   if (fkernel == &Nfft4GPNFFTAdditiveKernelGaussianKernel) kernel = 0;
+   else if (fkernel == &Nfft4GPNFFTAdditiveKernelMatern12Kernel) kernel = 1;
+   // pattern row pointers (kernels.c:133-168): dense rows below lfil, lfil entries after
+   std::vector<int> hia(n + 1, 0);
+   for (int i = 0; i < n; i++) hia[i + 1] = hia[i] + ((n <= lfil || i < lfil) ? i + 1 : lfil);
+   const int nnz = hia[n];
+   std::vector<int> hja((size_t)nnz);
+   for (int i = 0; i < std::min(n, n <= lfil ? n : lfil); i++)
+      for (int j = 0; j <= i; j++) hja[hia[i] + j] = j;
+   hipStream_t s = current_stream();
+   double *dX = nullptr, *daa = nullptr, *dda = nullptr;
+   int *dia = nullptr, *dja = nullptr;
+   auto cleanup = [&]() {
+      (void)hipStreamSynchronize(s);
+      for (double* p : {dX, daa, dda}) (void)hipFree(p);
+      for (int* p : {dia, dja}) (void)hipFree(p);
+   };
+   if (upload(&dX, (const double*)nullptr, (size_t)ldim * d) ||
+       hipMemcpy(dX, data, sizeof(double) * (size_t)ldim * d, hipMemcpyHostToDevice) != hipSuccess ||
+       upload(&dia, hia.data(), hia.size()) || upload(&dja, hja.data(), hja.size()) ||
+       upload(&daa, (const double*)nullptr, (size_t)nnz) ||
+       (require_grad && upload(&dda, (const double*)nullptr, 3 * (size_t)nnz))) {
+      cleanup();
+      return -1;
+   }
+   if (n > lfil) {
+      const int grid = std::min(n - lfil, 4096);
+      hipLaunchKernelGGL(k_knn, dim3(grid), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia, dja);
+   }
+   KernelParams P;
+   const double f = kp->_params[0], l = kp->_params[1];
+   P.kernel = kernel;
+   P.f2 = f * f;
+   P.inv = (kernel == 0) ? 1.0 / (2.0 * l * l) : 1.0 / l;
+   P.mu = kp->_noise_level;
+   P.df_scale = 2.0 / f;
+   P.dl_scale = (kernel == 0) ? P.f2 / (l * l * l) : P.f2 / (l * l);
+   hipLaunchKernelGGL(k_fsai_rows, dim3(n), dim3(64), 0, s, dX, ldim, d, dia, dja, P, require_grad ? 1 : 0, nnz,
+                      daa, dda);
+   if (hipGetLastError() != hipSuccess ||
+       hipMemcpyAsync(hja.data(), dja, sizeof(int) * nnz, hipMemcpyDeviceToHost, s) != hipSuccess) {
+      cleanup();
+      return -1;
+   }
+   std::vector<double> haa((size_t)nnz), hda(require_grad ? 3 * (size_t)nnz : 0);
+   if (hipMemcpyAsync(haa.data(), daa, sizeof(double) * nnz, hipMemcpyDeviceToHost, s) != hipSuccess ||
+       (require_grad &&
+        hipMemcpyAsync(hda.data(), dda, sizeof(double) * hda.size(), hipMemcpyDeviceToHost, s) != hipSuccess) ||
+       hipStreamSynchronize(s) != hipSuccess) {
+      cleanup();
+      return -1;
+   }
+   cleanup();
+   return fsai_load(F, n, hia.data(), hja.data(), haa.data(), require_grad ? hda.data() : nullptr);
+}
+
+int Nfft4GPAmdPrecondFsaiSetCsr(void* vfsai_mat, int n, const int* ia, const int* ja, const double* aa,
+                                const double* da)
+{
+   PrecondFsaiAmd* F = (PrecondFsaiAmd*)vfsai_mat;
+   if (!F || !ia || !ja || !aa || !need_device("Nfft4GPAmdPrecondFsaiSetCsr")) return -1;
+   return fsai_load(F, n, ia, ja, aa, da);
+}
+
+int Nfft4GPAmdPrecondFsaiCsr(void* vfsai_mat, int* ia, int* ja, double* aa, double* da)
+{
+   PrecondFsaiAmd* F = (PrecondFsaiAmd*)vfsai_mat;
+   if (!F || !F->ia) return -1;
+   const int n = F->n, nnz = F->nnz;
+   if (ia) NFFT4GP_HIP_CHECK(hipMemcpy(ia, F->ia, sizeof(int) * (n + 1), hipMemcpyDeviceToHost));
+   if (ja) NFFT4GP_HIP_CHECK(hipMemcpy(ja, F->ja, sizeof(int) * nnz, hipMemcpyDeviceToHost));
+   if (aa) NFFT4GP_HIP_CHECK(hipMemcpy(aa, F->aa, sizeof(double) * nnz, hipMemcpyDeviceToHost));
+   if (da && F->da) NFFT4GP_HIP_CHECK(hipMemcpy(da, F->da, sizeof(double) * 3 * nnz, hipMemcpyDeviceToHost));
+   return nnz;
+}
+
+int Nfft4GPAmdPrecondFsaiSolve(void* vfsai_mat, int n, double* x, double* rhs)
+{
+   PrecondFsaiAmd* F = (PrecondFsaiAmd*)vfsai_mat;
+   if (!F || !F->ia || n != F->n) return -1;
+   hipStream_t s = current_stream();
+   Vec vx, vr;
+   if (vx.open(x, n, false) || vr.open(rhs, n, true)) return -1;
+   csr_mv(F->ia, F->ja, F->aa, vr.d, F->work, n, 0, s);    // work = L rhs
+   csr_mv(F->tia, F->tja, F->taa, F->work, vx.d, n, 0, s);  // x = L^T work
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   vr.close(false);
+   vx.close(true);
+   return 0;
+}
+
+int Nfft4GPAmdPrecondFsaiInvL(void* vfsai_mat, int n, double* x, double* rhs)
+{
+   PrecondFsaiAmd* F = (PrecondFsaiAmd*)vfsai_mat;
+   if (!F || !F->ia || n != F->n) return -1;
+   Vec vx, vr;
+   if (vx.open(x, n, false) || vr.open(rhs, n, true)) return -1;
+   const int rc = inv_l(F, vx.d, vr.d, current_stream());
+   vr.close(false);
+   vx.close(rc == 0);
+   return rc;
+}
+
+int Nfft4GPAmdPrecondFsaiInvLT(void* vfsai_mat, int n, double* x, double* rhs)
+{
+   PrecondFsaiAmd* F = (PrecondFsaiAmd*)vfsai_mat;
+   if (!F || !F->ia || n != F->n) return -1;
+   Vec vx, vr;
+   if (vx.open(x, n, false) || vr.open(rhs, n, true)) return -1;
+   const int rc = inv_lt(F, vx.d, vr.d, current_stream());
+   vr.close(false);
+   vx.close(rc == 0);
+   return rc;
+}
+
+int Nfft4GPAmdPrecondFsaiDvp(void* vfsai_mat, int n, int* mask, double* x, double** yp)
+{
+   PrecondFsaiAmd* F = (PrecondFsaiAmd*)vfsai_mat;
+   if (!F || !F->ia || n != F->n) return -1;
+   if (!F->grad) {
+      printf("Setup FSAI without gradient, trace not supported.\n");  // fsai.c:139-143
+      return -1;
+   }
+   if (!yp) {
+      printf("output pointer cannot be NULL\n");
+      return -1;
+   }
+   if (!*yp) {
+      if (is_device_ptr(x)) {
+         if (hipMalloc((void**)yp, sizeof(double) * 3 * (size_t)n) != hipSuccess) return -1;
+         NFFT4GP_HIP_CHECK(hipMemset(*yp, 0, sizeof(double) * 3 * (size_t)n));
+      } else {
+         *yp = (double*)calloc(3 * (size_t)n, sizeof(double));
+      }
+   }
+   hipStream_t s = current_stream();
+   Vec vx, vy;
+   if (vx.open(x, n, true) || vy.open(*yp, 3 * (size_t)n, true)) return -1;
+   int rc = 0;
+   for (int g = 0; g < 3 && !rc; g++)
+      if (!mask || mask[g]) rc = dvp_one(F, g, vx.d, vy.d + (size_t)g * n, s);
+   vx.close(false);
+   vy.close(rc == 0);
+   return rc;
+}
+
+int Nfft4GPAmdPrecondFsaiTrace(void* vfsai_mat, double** tracesp)
+{
+   PrecondFsaiAmd* F = (PrecondFsaiAmd*)vfsai_mat;
+   if (!F || !F->ia) return -1;
+   if (!F->grad) {
+      printf("Setup FSAI without gradient, trace not supported.\n");  // fsai.c:225-229
+      return -1;
+   }
+   if (!tracesp) {
+      printf("Trace pointer cannot be NULL\n");
+      return -1;
+   }
+   double* traces = *tracesp ? *tracesp : (double*)calloc(3, sizeof(double));
+   hipStream_t s = current_stream();
+   // the reference adds to what the array holds, then doubles (fsai.c:256-265)
+   for (int g = 0; g < 3; g++) traces[g] = 2.0 * (traces[g] + diag_sum(F, F->da + (size_t)g * F->nnz, s));
+   *tracesp = traces;
+   return 0;
+}
+
+double Nfft4GPAmdPrecondFsaiLogdet(void* vfsai_mat)
+{
+   PrecondFsaiAmd* F = (PrecondFsaiAmd*)vfsai_mat;
+   if (!F || !F->ia) return NAN;
+   return 2.0 * diag_sum(F, nullptr, current_stream());
+}
+
+}  // extern "C"

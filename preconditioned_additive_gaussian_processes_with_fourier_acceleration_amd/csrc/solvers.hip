@@ -871,7 +871,8 @@ bool library_operator(const void* fn)
           fn == (const void*)&Nfft4GPAdditiveNFFTGradMatSymv || fn == (const void*)&Nfft4GPNFFTGradMatSymv ||
           fn == (const void*)&Nfft4GPAmdNysSolve || fn == (const void*)&Nfft4GPAmdFsaiSolve ||
           fn == (const void*)&Nfft4GPAmdAfnSolve || fn == (const void*)&Nfft4GPAmdPrecondNysSolve ||
-          fn == (const void*)&Nfft4GPAmdPrecondNysDvp;
+          fn == (const void*)&Nfft4GPAmdPrecondNysDvp || fn == (const void*)&Nfft4GPAmdPrecondFsaiSolve ||
+          fn == (const void*)&Nfft4GPAmdPrecondFsaiDvp;
 }
 }  // namespace nfft4gp_amd
 
