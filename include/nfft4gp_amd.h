@@ -324,6 +324,27 @@ void *Nfft4GPAmdAfnCreate(int n, int k, const int *perm, const NFFT4GP_DOUBLE *L
 /* same signature as Nfft4GPPrecondAFNSolve (afn.c:82) */
 int Nfft4GPAmdAfnSolve(void *afn, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
 void Nfft4GPAmdAfnFree(void *afn);
+/* AFN setup on the device: Nfft4GPPrecondAFNSetup (afn.c:161-489) with rank k given (its rank estimation,
+ * afn.c:178-243 / rankest.c, is the caller's), schur_opt 3 (kernel FSAI of the Schur complement through
+ * Nfft4GPKernelSchurCombineKernel, kernels.c:3496-3760; lfil = schur_lfil <= 64) and the ordering
+ * perm_opt 0: identity (afn.c:245-256), 1: farthest points (Nfft4GPAmdSortFps, afn.c:196-209), 2: perm (n
+ * entries, e.g. the reference's Nfft4GPRandPerm expanded, afn.c:210-218).  kernel: 0 Gaussian
+ * (Nfft4GPKernelGaussianKernel), 1 Matern-1/2; fkernel_params: an nfft4gp_kernel (_params[0] = f,
+ * _params[1] = l, _noise_level = mu).  data: host or device, n x d column-major (ldim).  Returns a handle
+ * for Nfft4GPAmdAfnSolve / Nfft4GPAmdAfnFree (which then also frees the Schur FSAI), NULL on error. */
+void *Nfft4GPAmdAfnSetup(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int k, int perm_opt, const int *perm,
+                         int schur_lfil, int kernel, void *fkernel_params);
+/* the AFN handle's rank, permutation (n) and Schur-complement FSAI (CSR, n - k rows); any output may be
+ * NULL; returns the FSAI's nnz (0 without one), -1 on error */
+int Nfft4GPAmdAfnInfo(void *afn, int *k, int *perm, int *ia, int *ja, NFFT4GP_DOUBLE *aa);
+
+/* ---- farthest point sampling (SRC/linearalg/ordering.c) -------------------------------------------
+ * Nfft4GPSortFps with kFpsAlgorithmParallel1 (ordering.c:422-739): *k in: the number of points to select
+ * (<= 0: all n), out: the number selected (fewer when the fill distance falls below tol); perm and dist
+ * (may be NULL): host arrays of *k entries receiving the selected points and their fill distances
+ * (the reference's _dist).  data: host or device, n x d column-major (ldim), d <= 256. */
+int Nfft4GPAmdSortFps(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int *k, NFFT4GP_DOUBLE tol, int *perm,
+                      NFFT4GP_DOUBLE *dist);
 
 /* ---- MI355X extensions --------------------------------------------------------------------------- */
 /* stream every kernel of this library is enqueued on (hipStream_t; NULL = null stream) */

@@ -451,6 +451,98 @@ class RefFsai:
         return float(self.lib.Nfft4GPPrecondFsaiLogdet(C.c_void_p(self.h)))
 
 
+class FpsStruct(C.Structure):
+    """ordering_fps, SRC/linearalg/ordering.h:27-61."""
+    _fields_ = [
+        ("_algorithm", C.c_int), ("_tol", C.c_double), ("_rho", C.c_double), ("_fdist", C.c_void_p),
+        ("_fdist_params", C.c_void_p), ("_dist", _dp), ("_build_pattern", C.c_int), ("_pattern_lfil", C.c_int),
+        ("_pattern_opt", C.c_int), ("_S_i", _ip), ("_S_j", _ip),
+    ]
+
+
+def ref_sort_fps(data, k, tol=0.0):
+    """Nfft4GPSortFps with kFpsAlgorithmParallel1 (ordering.c:422-739) via oracle/_ref: the selected points
+    and their fill distances (_dist).  k <= 0 selects until the fill distance drops below tol."""
+    lib = ref_lib()
+    lib.Nfft4GPOrdFpsCreate.restype = C.c_void_p
+    lib.Nfft4GPOrdFpsFree.argtypes = [C.c_void_p]
+    lib.Nfft4GPSortFps.argtypes = [C.c_void_p, _dp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
+                                   C.POINTER(_ip)]
+    data = np.asfortranarray(data, dtype=np.float64)
+    n, d = data.shape
+    h = lib.Nfft4GPOrdFpsCreate()
+    st = FpsStruct.from_address(h)
+    st._algorithm = 0  # kFpsAlgorithmParallel1
+    st._tol = tol
+    kk = C.c_int(k)
+    perm = _ip()
+    assert lib.Nfft4GPSortFps(h, _d(data), n, n, d, C.byref(kk), C.byref(perm)) == 0
+    m = kk.value
+    p = np.ctypeslib.as_array(perm, shape=(m,)).copy()
+    dist = np.ctypeslib.as_array(st._dist, shape=(m,)).copy()
+    C.CDLL(None).free(perm)
+    lib.Nfft4GPOrdFpsFree(h)
+    return p, dist
+
+
+def fps_par1(data, k, tol=0.0):
+    """Nfft4GPSortFpsPar1 (ordering.c:422-711) restated in numpy: start at the point closest to the mean
+    (ordering.c:467-538), give it the largest distance to it (:594-599), then repeatedly append the
+    unselected point farthest from the selected set (strict >, lowest index on ties, (0, 0) when no
+    distance is positive, :617-690) while fewer than k are selected and the newest one's distance is
+    >= tol.  Distances as Nfft4GPDistanceEuclid (kernels.c:5-15): sqrt of the squares summed in feature
+    order."""
+    X = np.asarray(data, dtype=np.float64)
+    n, d = X.shape
+    k = n if k <= 0 else k
+
+    def dist_to(q):
+        v = np.zeros(n)
+        for c in range(d):
+            t = X[:, c] - q[c]
+            v = v + t * t
+        return np.sqrt(v)
+
+    mean = np.zeros(d)
+    for c in range(d):
+        mean[c] = np.sum(X[:, c] / n)
+    i1 = int(np.argmin(dist_to(mean)))
+    dc = dist_to(X[i1])
+    i2 = int(np.argmax(dc)) if dc.max() > 0 else 0
+    dmax = dc[i2] if dc.max() > 0 else 0.0
+    marker = np.full(n, -1)
+    perm, dist = [i1], [dmax]
+    dc[i1] = dmax
+    marker[i1] = 0
+    if dmax < tol or len(perm) >= k:
+        return np.array(perm, dtype=np.int32), np.array(dist)
+    i1 = i2
+    marker[i1] = 1
+    perm.append(i1)
+    dist.append(dmax)
+    while len(perm) < k and dc[i1] >= tol:
+        free = marker < 0
+        dc[free] = np.minimum(dc[free], dist_to(X[i1])[free])
+        cand = np.where(free, dc, -1.0)
+        i2 = int(np.argmax(cand))
+        if cand[i2] > 0:
+            dmax = cand[i2]
+        else:
+            i2, dmax = 0, 0.0
+        i1 = i2
+        marker[i1] = len(perm)
+        perm.append(i1)
+        dist.append(dmax)
+    return np.array(perm, dtype=np.int32), np.array(dist)
+
+
+def expand_perm(perm, n):
+    """Nfft4GPExpandPerm (utils.c:208-245): perm, then the unused indices in ascending order."""
+    used = np.zeros(n, dtype=bool)
+    used[perm] = True
+    return np.concatenate([np.asarray(perm, dtype=np.int32), np.flatnonzero(~used).astype(np.int32)])
+
+
 def ref_schur_params(data, perm, k, chol_K11, gauss_params):
     """Nfft4GPKernelSchurCombineKernelParamCreate (kernels.c:3496-3596, no gradient): the kernel of the
     Schur complement K22 - K21 K11^{-1} K12 the reference's AFN setup hands to FSAI (afn.c:473)."""

@@ -124,6 +124,9 @@ _SIGS = {
     "Nfft4GPAmdAfnCreate": (vp, [C.c_int, C.c_int, vp, vp, vp, vp]),
     "Nfft4GPAmdAfnSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdAfnFree": (None, [vp]),
+    "Nfft4GPAmdAfnSetup": (vp, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, vp]),
+    "Nfft4GPAmdAfnInfo": (C.c_int, [vp, vp, vp, vp, vp, vp]),
+    "Nfft4GPAmdSortFps": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, C.c_double, vp, vp]),
     "Nfft4GPAmdSetStream": (None, [vp]),
     "Nfft4GPAmdGetStream": (vp, []),
     "Nfft4GPAmdDeviceAvailable": (C.c_int, []),
@@ -188,3 +191,15 @@ def lib():
 def fnptr(name: str) -> int:
     """Address of an exported C function (to pass as func_symmatvec / func_solve)."""
     return C.cast(getattr(lib(), name), vp).value
+
+
+def kernel_params(f: float, l: float, mu: float, max_n: int) -> int:
+    """An nfft4gp_kernel (Nfft4GPKernelParamCreate, kernels.c:404-440) with _params = (f, l) and
+    _noise_level = mu, as the reference's callers fill it (gp_loss.c:143-150).  Free with
+    Nfft4GPKernelParamFree."""
+    h = lib().Nfft4GPKernelParamCreate(int(max_n), 0)
+    st = NfftKernelStruct.from_address(h)
+    st._params[0] = f
+    st._params[1] = l
+    st._noise_level = mu
+    return h

@@ -235,6 +235,30 @@ int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
 
 }  // namespace
 
+// an AFN apply object from factors already in HBM (afn_setup.hip); takes ownership of d_perm, d_Linv,
+// d_K12 (hipMalloc'ed) and of the Schur FSAI handle S (an Nfft4GPAmdFsaiCreate handle of size n - k)
+void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_K12, void* S)
+{
+   AfnDev* A = new AfnDev();
+   A->n = n;
+   A->k = k;
+   A->n2 = n - k;
+   A->S = (FsaiDev*)S;
+   A->own_S = true;
+   A->perm = d_perm;
+   A->Linv = d_Linv;
+   A->K12 = d_K12;
+   A->nblk = (A->n2 + kA12Cols - 1) / kA12Cols;
+   if (hipMalloc((void**)&A->rp, sizeof(double) * n) != hipSuccess ||
+       hipMalloc((void**)&A->y, sizeof(double) * n) != hipSuccess ||
+       hipMalloc((void**)&A->t, sizeof(double) * std::max(1, k)) != hipSuccess ||
+       hipMalloc((void**)&A->part, sizeof(double) * std::max<size_t>(1, (size_t)A->nblk * k)) != hipSuccess) {
+      Nfft4GPAmdAfnFree(A);
+      return nullptr;
+   }
+   return A;
+}
+
 }  // namespace nfft4gp_amd
 
 using namespace nfft4gp_amd;
@@ -316,7 +340,26 @@ void Nfft4GPAmdAfnFree(void* afn)
    for (void* p : {(void*)A->perm, (void*)A->Linv, (void*)A->K12, (void*)A->rp, (void*)A->y, (void*)A->t,
                    (void*)A->part})
       (void)hipFree(p);
-   delete A;  // the Schur complement's FSAI handle stays with its creator (Nfft4GPAmdFsaiFree)
+   // the Schur complement's FSAI handle stays with its creator (Nfft4GPAmdFsaiFree) unless the AFN was
+   // set up on the device (Nfft4GPAmdAfnSetup), which owns it
+   if (A->own_S) fsai_free(A->S);
+   delete A;
+}
+
+int Nfft4GPAmdAfnInfo(void* afn, int* k, int* perm, int* ia, int* ja, double* aa)
+{
+   AfnDev* A = (AfnDev*)afn;
+   if (!A) return -1;
+   if (k) *k = A->k;
+   if (perm && A->perm) NFFT4GP_HIP_CHECK(hipMemcpy(perm, A->perm, sizeof(int) * A->n, hipMemcpyDeviceToHost));
+   if (!A->S) return 0;
+   const int n2 = A->S->n;
+   int nnz = 0;
+   NFFT4GP_HIP_CHECK(hipMemcpy(&nnz, A->S->ia + n2, sizeof(int), hipMemcpyDeviceToHost));
+   if (ia) NFFT4GP_HIP_CHECK(hipMemcpy(ia, A->S->ia, sizeof(int) * (n2 + 1), hipMemcpyDeviceToHost));
+   if (ja) NFFT4GP_HIP_CHECK(hipMemcpy(ja, A->S->ja, sizeof(int) * nnz, hipMemcpyDeviceToHost));
+   if (aa) NFFT4GP_HIP_CHECK(hipMemcpy(aa, A->S->aa, sizeof(double) * nnz, hipMemcpyDeviceToHost));
+   return nnz;
 }
 
 }  // extern "C"

@@ -216,12 +216,18 @@ __device__ void wave_trsv(double (*A)[kFsaiMaxK + 1], int k, double* b, int tran
 }
 
 // one wave per row i: A_ai (and dA_ai for the three gradients) into aa / da (fsai.c:353-398, :493-563)
+//
+// W (kw x n column-major, optional): the Schur-complement kernel K(x_r, x_c) - W(:, r)' W(:, c) of the AFN
+// setup (Nfft4GPKernelSchurCombineKernel, kernels.c:3599-3760, with W = L11^{-1} K12), staged through LDS
+// kSchurChunk rows of W at a time so each row reads its lfil columns of W once.
+constexpr int kSchurChunk = 32;
 __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, int ldim, int d,
                                                   const int* __restrict__ ia, const int* __restrict__ ja,
-                                                  KernelParams P, int grad, int nnz, double* __restrict__ aa,
-                                                  double* __restrict__ da)
+                                                  KernelParams P, const double* __restrict__ W, int kw, int grad,
+                                                  int nnz, double* __restrict__ aa, double* __restrict__ da)
 {
    __shared__ double A[kFsaiMaxK][kFsaiMaxK + 1];
+   __shared__ double Ws[kFsaiMaxK][kSchurChunk + 1];
    __shared__ double a[kFsaiMaxK], u[kFsaiMaxK];
    __shared__ int idx[kFsaiMaxK];
    const int i = blockIdx.x;
@@ -244,6 +250,24 @@ __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, 
       A[r][c] = K;
    }
    __syncthreads();
+   if (W) {
+      for (int t0 = 0; t0 < kw; t0 += kSchurChunk) {
+         const int tc = min(kSchurChunk, kw - t0);
+         for (int e = lane; e < k * tc; e += 64) {
+            const int r = e / tc, tt = e % tc;
+            Ws[r][tt] = W[(size_t)idx[r] * kw + t0 + tt];
+         }
+         __syncthreads();
+         for (int e = lane; e < k * k; e += 64) {
+            const int r = e % k, c = e / k;
+            if (c > r) continue;
+            double acc = 0.0;
+            for (int tt = 0; tt < tc; tt++) acc = fma(Ws[r][tt], Ws[c][tt], acc);
+            A[r][c] -= acc;
+         }
+         __syncthreads();
+      }
+   }
    // Cholesky, lower (dpotrf 'L')
    for (int j = 0; j < k; j++) {
       if (lane == 0) A[j][j] = sqrt(A[j][j]);
@@ -534,6 +558,69 @@ double diag_sum(PrecondFsaiAmd* F, const double* num, hipStream_t s)
 
 }  // namespace
 
+namespace nfft4gp_amd {
+
+// The FSAI of a kernel matrix (fsai.c:314-673) from device coordinates: KNN pattern, per-row values (and
+// gradients), copied to host CSR.  dW (kw x n, optional): the Schur-complement kernel of the AFN setup.
+int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, int kernel, double f, double l, double mu,
+                    const double* dW, int kw, int require_grad, std::vector<int>& hia, std::vector<int>& hja,
+                    std::vector<double>& haa, std::vector<double>& hda, hipStream_t s)
+{
+   if (n <= 0 || ldim < n || d <= 0 || d > kMaxDims || lfil < 1 || lfil > kFsaiMaxK || (dW && kw <= 0)) {
+      fprintf(stderr, "nfft4gp_amd: FSAI setup needs 1 <= lfil <= %d and at most %d features\n", kFsaiMaxK,
+              kMaxDims);
+      return -1;
+   }
+   if (require_grad && dW) {
+      fprintf(stderr, "nfft4gp_amd: FSAI setup: gradients of the Schur-complement kernel are not supported\n");
+      return -1;
+   }
+   // pattern row pointers (kernels.c:133-168): dense rows below lfil, lfil entries after
+   hia.assign(n + 1, 0);
+   for (int i = 0; i < n; i++) hia[i + 1] = hia[i] + ((n <= lfil || i < lfil) ? i + 1 : lfil);
+   const int nnz = hia[n];
+   hja.assign((size_t)nnz, 0);
+   for (int i = 0; i < std::min(n, n <= lfil ? n : lfil); i++)
+      for (int j = 0; j <= i; j++) hja[hia[i] + j] = j;
+   double *daa = nullptr, *dda = nullptr;
+   int *dia = nullptr, *dja = nullptr;
+   auto cleanup = [&](int rc) {
+      (void)hipStreamSynchronize(s);
+      for (double* p : {daa, dda}) (void)hipFree(p);
+      for (int* p : {dia, dja}) (void)hipFree(p);
+      return rc;
+   };
+   if (upload(&dia, hia.data(), hia.size()) || upload(&dja, hja.data(), hja.size()) ||
+       upload(&daa, (const double*)nullptr, (size_t)nnz) ||
+       (require_grad && upload(&dda, (const double*)nullptr, 3 * (size_t)nnz)))
+      return cleanup(-1);
+   if (n > lfil) {
+      const int grid = std::min(n - lfil, 4096);
+      hipLaunchKernelGGL(k_knn, dim3(grid), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia, dja);
+   }
+   KernelParams P;
+   P.kernel = kernel;
+   P.f2 = f * f;
+   P.inv = (kernel == 0) ? 1.0 / (2.0 * l * l) : 1.0 / l;
+   P.mu = mu;
+   P.df_scale = 2.0 / f;
+   P.dl_scale = (kernel == 0) ? P.f2 / (l * l * l) : P.f2 / (l * l);
+   hipLaunchKernelGGL(k_fsai_rows, dim3(n), dim3(64), 0, s, dX, ldim, d, dia, dja, P, dW, kw, require_grad ? 1 : 0,
+                      nnz, daa, dda);
+   haa.assign((size_t)nnz, 0.0);
+   hda.assign(require_grad ? 3 * (size_t)nnz : 0, 0.0);
+   if (hipGetLastError() != hipSuccess ||
+       hipMemcpyAsync(hja.data(), dja, sizeof(int) * nnz, hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipMemcpyAsync(haa.data(), daa, sizeof(double) * nnz, hipMemcpyDeviceToHost, s) != hipSuccess ||
+       (require_grad &&
+        hipMemcpyAsync(hda.data(), dda, sizeof(double) * hda.size(), hipMemcpyDeviceToHost, s) != hipSuccess) ||
+       hipStreamSynchronize(s) != hipSuccess)
+      return cleanup(-1);
+   return cleanup(0);
+}
+
+}  // namespace nfft4gp_amd
+
 extern "C" {
 
 void* Nfft4GPAmdPrecondFsaiCreate(void) { return new PrecondFsaiAmd(); }
@@ -567,66 +654,27 @@ int Nfft4GPAmdPrecondFsaiSetupWithKernel(double* data, int n, int ldim, int d, f
    PrecondFsaiAmd* F = (PrecondFsaiAmd*)vfsai_mat;
    if (!F || !need_device("Nfft4GPAmdPrecondFsaiSetupWithKernel")) return -1;
    const nfft4gp_kernel* kp = (const nfft4gp_kernel*)fkernel_params;
-   const int lfil = F->lfil;
-   if (!kp || !data || n <= 0 || ldim < n || d <= 0 || d > kMaxDims || lfil < 1 || lfil > kFsaiMaxK) {
-      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondFsaiSetupWithKernel needs kernel parameters, 1 <= lfil <= %d "
-                      "and at most %d features\n", kFsaiMaxK, kMaxDims);
+   if (!kp || !data || n <= 0 || ldim < n || d <= 0) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondFsaiSetupWithKernel needs data and kernel parameters\n");
       return -1;
    }
    int kernel = F->kernel;
    if (fkernel == &Nfft4GPNFFTAdditiveKernelGaussianKernel) kernel = 0;
    else if (fkernel == &Nfft4GPNFFTAdditiveKernelMatern12Kernel) kernel = 1;
-   // pattern row pointers (kernels.c:133-168): dense rows below lfil, lfil entries after
-   std::vector<int> hia(n + 1, 0);
-   for (int i = 0; i < n; i++) hia[i + 1] = hia[i] + ((n <= lfil || i < lfil) ? i + 1 : lfil);
-   const int nnz = hia[n];
-   std::vector<int> hja((size_t)nnz);
-   for (int i = 0; i < std::min(n, n <= lfil ? n : lfil); i++)
-      for (int j = 0; j <= i; j++) hja[hia[i] + j] = j;
    hipStream_t s = current_stream();
-   double *dX = nullptr, *daa = nullptr, *dda = nullptr;
-   int *dia = nullptr, *dja = nullptr;
-   auto cleanup = [&]() {
-      (void)hipStreamSynchronize(s);
-      for (double* p : {dX, daa, dda}) (void)hipFree(p);
-      for (int* p : {dia, dja}) (void)hipFree(p);
-   };
+   double* dX = nullptr;
    if (upload(&dX, (const double*)nullptr, (size_t)ldim * d) ||
-       hipMemcpy(dX, data, sizeof(double) * (size_t)ldim * d, hipMemcpyHostToDevice) != hipSuccess ||
-       upload(&dia, hia.data(), hia.size()) || upload(&dja, hja.data(), hja.size()) ||
-       upload(&daa, (const double*)nullptr, (size_t)nnz) ||
-       (require_grad && upload(&dda, (const double*)nullptr, 3 * (size_t)nnz))) {
-      cleanup();
+       hipMemcpy(dX, data, sizeof(double) * (size_t)ldim * d, hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(dX);
       return -1;
    }
-   if (n > lfil) {
-      const int grid = std::min(n - lfil, 4096);
-      hipLaunchKernelGGL(k_knn, dim3(grid), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia, dja);
-   }
-   KernelParams P;
-   const double f = kp->_params[0], l = kp->_params[1];
-   P.kernel = kernel;
-   P.f2 = f * f;
-   P.inv = (kernel == 0) ? 1.0 / (2.0 * l * l) : 1.0 / l;
-   P.mu = kp->_noise_level;
-   P.df_scale = 2.0 / f;
-   P.dl_scale = (kernel == 0) ? P.f2 / (l * l * l) : P.f2 / (l * l);
-   hipLaunchKernelGGL(k_fsai_rows, dim3(n), dim3(64), 0, s, dX, ldim, d, dia, dja, P, require_grad ? 1 : 0, nnz,
-                      daa, dda);
-   if (hipGetLastError() != hipSuccess ||
-       hipMemcpyAsync(hja.data(), dja, sizeof(int) * nnz, hipMemcpyDeviceToHost, s) != hipSuccess) {
-      cleanup();
-      return -1;
-   }
-   std::vector<double> haa((size_t)nnz), hda(require_grad ? 3 * (size_t)nnz : 0);
-   if (hipMemcpyAsync(haa.data(), daa, sizeof(double) * nnz, hipMemcpyDeviceToHost, s) != hipSuccess ||
-       (require_grad &&
-        hipMemcpyAsync(hda.data(), dda, sizeof(double) * hda.size(), hipMemcpyDeviceToHost, s) != hipSuccess) ||
-       hipStreamSynchronize(s) != hipSuccess) {
-      cleanup();
-      return -1;
-   }
-   cleanup();
+   std::vector<int> hia, hja;
+   std::vector<double> haa, hda;
+   const int rc = fsai_kernel_csr(dX, n, ldim, d, F->lfil, kernel, kp->_params[0], kp->_params[1], kp->_noise_level,
+                                  nullptr, 0, require_grad, hia, hja, haa, hda, s);
+   (void)hipStreamSynchronize(s);
+   (void)hipFree(dX);
+   if (rc) return -1;
    return fsai_load(F, n, hia.data(), hja.data(), haa.data(), require_grad ? hda.data() : nullptr);
 }
 

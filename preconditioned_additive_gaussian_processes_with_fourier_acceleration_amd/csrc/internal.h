@@ -214,6 +214,16 @@ int md_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, 
 void md_free(AdditivePlan& P);
 void bhat_nd(int kind, int d, double c, std::vector<double>& bhat);  // window.cpp, 32^d real
 
+// k x k lower Cholesky of A (+ shift I) and its inverse (rocSOLVER potrf/trtri, host fallback): G = L^{-1}
+// (lower, cleaned; may be NULL), Gt = L^{-T}.  A is overwritten.  >0: not positive definite (nystrom.hip)
+int chol_inverse_dev(double* A, int k, double shift, double* G, double* Gt, int* d_info, hipStream_t s);
+// FSAI of a kernel matrix from device coordinates (fsai_setup.hip), host CSR out; dW: Schur kernel
+int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, int kernel, double f, double l, double mu,
+                    const double* dW, int kw, int require_grad, std::vector<int>& ia, std::vector<int>& ja,
+                    std::vector<double>& aa, std::vector<double>& da, hipStream_t s);
+// AFN apply object from device factors (fsai_afn.hip); owns all of them and S
+void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_K12, void* S);
+
 hipStream_t current_stream();
 bool is_device_ptr(const void* p);
 int device_ok();

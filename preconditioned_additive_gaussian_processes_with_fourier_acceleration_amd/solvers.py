@@ -171,6 +171,67 @@ class AfnPrecond(_Apply):
         if not self.h:
             raise RuntimeError("Nfft4GPAmdAfnCreate failed (see stderr)")
 
+    @classmethod
+    def setup(cls, X, k: int, f: float, l: float, mu: float, perm_opt: str = "fps", perm=None,
+              schur_lfil: int = 20, kernel: int = 0):
+        """Nfft4GPAmdAfnSetup: the AFN of the plain Gaussian (kernel 0) / Matern-1/2 (1) kernel of the
+        points X (n x d) built on the GPU with rank k (afn.c:161-489, schur_opt 3).  perm_opt: "identity"
+        (afn.c:245-256), "fps" (farthest points, afn.c:196-209) or "perm" (``perm`` given, n entries)."""
+        L = _lib.lib()
+        X = np.asfortranarray(np.asarray(X, dtype=np.float64))
+        n, d = X.shape
+        opt = {"identity": 0, "fps": 1, "perm": 2}[perm_opt]
+        p = None if perm is None else np.ascontiguousarray(np.asarray(perm, dtype=np.int32))
+        if opt == 2 and (p is None or p.size != n):
+            raise ValueError("perm_opt 'perm' needs a permutation of the n points")
+        params = _lib.kernel_params(f, l, mu, n)
+        self = cls.__new__(cls)
+        self.n, self.schur = n, None
+        self.h = L.Nfft4GPAmdAfnSetup(X.ctypes.data, n, n, d, int(k), opt, None if p is None else p.ctypes.data,
+                                      int(schur_lfil), int(kernel), params)
+        L.Nfft4GPKernelParamFree(params)
+        if not self.h:
+            raise RuntimeError("Nfft4GPAmdAfnSetup failed (see stderr)")
+        kk = C.c_int()
+        L.Nfft4GPAmdAfnInfo(self.h, C.byref(kk), None, None, None, None)
+        self.k = kk.value
+        return self
+
+    def info(self):
+        """(k, perm, (ia, ja, aa) of the Schur complement's FSAI or None)"""
+        L = _lib.lib()
+        perm = np.zeros(self.n, np.int32)
+        nnz = L.Nfft4GPAmdAfnInfo(self.h, None, perm.ctypes.data, None, None, None)
+        if nnz <= 0:
+            return self.k, perm, None
+        ia = np.zeros(self.n - self.k + 1, np.int32)
+        ja = np.zeros(nnz, np.int32)
+        aa = np.zeros(nnz)
+        L.Nfft4GPAmdAfnInfo(self.h, None, None, ia.ctypes.data, ja.ctypes.data, aa.ctypes.data)
+        return self.k, perm, (ia, ja, aa)
+
+
+def sort_fps(X, k: int, tol: float = 0.0):
+    """Nfft4GPAmdSortFps -- Nfft4GPSortFps with kFpsAlgorithmParallel1 (ordering.c:422-739) on the GPU:
+    (selected points, fill distances).  X: n x d numpy array or a torch GPU tensor of shape (d, n)
+    (column-major n x d).  k <= 0 selects until the fill distance drops below tol."""
+    L = _lib.lib()
+    if hasattr(X, "data_ptr"):
+        d, n = X.shape
+        src, keep = X.data_ptr(), X
+    else:
+        keep = np.asfortranarray(np.asarray(X, dtype=np.float64))
+        n, d = keep.shape
+        src = keep.ctypes.data
+    m = n if k <= 0 else min(k, n)
+    kk = C.c_int(int(k))
+    perm = np.zeros(m, np.int32)
+    dist = np.zeros(m)
+    if L.Nfft4GPAmdSortFps(src, n, n, d, C.byref(kk), float(tol), perm.ctypes.data, dist.ctypes.data):
+        raise RuntimeError("Nfft4GPAmdSortFps failed (see stderr)")
+    del keep
+    return perm[:kk.value], dist[:kk.value]
+
 
 def pcg(op, b, x=None, maxits=1000, tol=1e-6, atol=False, precond=None, print_level=0):
     """Nfft4GPSolverPcg(op, n, matvec, precond, precondfunc, x, b, maxits, atol, tol, ...).

@@ -24,7 +24,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 from oracle import (OracleAdditiveNFFT, RefDenseAdditive, RefFsai, RefGpLoss, RefNystrom, afn_apply,  # noqa: E402
                     ref_available, ref_fgmres, ref_gaussian_matrix, ref_gaussian_params, ref_gp_loss_nfft,
-                    ref_logdet_quadrature, ref_nfft_gp_predict, ref_pcg, ref_schur_params)
+                    ref_logdet_quadrature, ref_nfft_gp_predict, ref_pcg, ref_schur_params, ref_sort_fps)
 from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.data import (  # noqa: E402
     read_features, read_labels, read_windows)
 
@@ -106,6 +106,17 @@ def make_precond_synth():
          afn_k=k, afn_perm=perm, afn_L11=L11, schur_i=s_i, schur_j=s_j, schur_a=s_a,
          afn_rhs=afn_rhs, afn_out=afn_out,
          pcgafn_x=xa, pcgafn_relres=rela, pcgafn_hist=hista, pcgafn_iters=ita)
+
+
+def make_fps_synth():
+    """(8) the reference's farthest point sampling (Nfft4GPSortFps, kFpsAlgorithmParallel1,
+    ordering.c:422-739) on seeded points: a fixed count, and a fill-distance tolerance (k = 0)."""
+    rng = np.random.default_rng(31)
+    Xa = np.asfortranarray(rng.random((1500, 3)))
+    pa, da = ref_sort_fps(Xa, 120)
+    Xb = np.asfortranarray(rng.random((800, 6)))
+    pb, db = ref_sort_fps(Xb, 0, tol=0.45)
+    save("fps_synth", Xa=Xa, ka=120, perm_a=pa, dist_a=da, Xb=Xb, tol_b=0.45, perm_b=pb, dist_b=db)
 
 
 def make_krylov_synth():
@@ -249,7 +260,11 @@ def main():
     make_precond_synth()
     make_krylov_synth()
     make_predict_synth()
+    make_fps_synth()
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["fps"]:
+        make_fps_synth()
+    else:
+        main()

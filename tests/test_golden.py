@@ -174,3 +174,17 @@ def test_data_readers(tmp_path):
     (tmp_path / "bad.feature").write_text("3 2\n1 2 3\n")
     with pytest.raises(ValueError):
         amd.read_features(str(tmp_path / "bad.feature"))
+
+
+def test_fps_restatement_matches_golden():
+    """oracle.fps_par1 (ordering.c:422-711 restated) reproduces the reference's FPS order and fill
+    distances bit for bit (fixture from the compiled reference, tests/golden/make_golden.py)."""
+    from oracle import fps_par1
+    z = load("fps_synth")
+    p, d = fps_par1(z["Xa"], int(z["ka"]))
+    np.testing.assert_array_equal(p, z["perm_a"])
+    np.testing.assert_array_equal(d, z["dist_a"])
+    p, d = fps_par1(z["Xb"], 0, float(z["tol_b"]))
+    np.testing.assert_array_equal(p, z["perm_b"])
+    np.testing.assert_array_equal(d, z["dist_b"])
+    assert d[-1] < float(z["tol_b"]) <= d[-2]

@@ -1,0 +1,212 @@
+"""GPU farthest point sampling (Nfft4GPAmdSortFps) and AFN setup (Nfft4GPAmdAfnSetup, afn_setup.hip).
+
+* FPS against the reference's Nfft4GPSortFps (kFpsAlgorithmParallel1, ordering.c:422-739): the golden
+  fixture and oracle/_ref on fresh inputs, order and fill distances bitwise.
+* AFN setup (afn.c:161-489, rank given, schur_opt 3) against the pieces the reference's setup builds:
+  the golden precond_synth AFN (its permutation, Cholesky of K11, Schur-complement FSAI through
+  Nfft4GPKernelSchurCombineKernel, kernels.c:3496-3760, apply restated in oracle.afn_apply since afn.c is
+  not in the reference build).  Schur FSAI rows compared as sets (the KNN ranks exact distances, the
+  reference |x|^2 + |y|^2 - 2 x.y) with values to 1e-8 of the row norm; applies to 1e-9.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd import _lib
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+need_ref = pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref not built")
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+
+
+def rel(a, b):
+    return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / np.linalg.norm(np.asarray(b)))
+
+
+def gpu_fps(X, k, tol=0.0, device=None):
+    L = _lib.lib()
+    X = np.asfortranarray(X, dtype=np.float64)
+    n, d = X.shape
+    kk = C.c_int(k)
+    m = n if k <= 0 else k
+    perm = np.zeros(m, np.int32)
+    dist = np.zeros(m)
+    src = X.ctypes.data
+    if device is not None:
+        t = device.tensor(X.T.copy(), dtype=device.float64, device="cuda")  # row-major d x n == column-major n x d
+        src = t.data_ptr()
+    assert L.Nfft4GPAmdSortFps(src, n, n, d, C.byref(kk), tol, perm.ctypes.data, dist.ctypes.data) == 0
+    return perm[:kk.value], dist[:kk.value]
+
+
+class GpuAfn:
+    def __init__(self, X, k, perm_opt, perm, lfil, params, kernel=0):
+        self.L = _lib.lib()
+        X = np.asfortranarray(X, dtype=np.float64)
+        self.n, d = X.shape
+        p = None if perm is None else np.ascontiguousarray(perm, dtype=np.int32)
+        self.h = self.L.Nfft4GPAmdAfnSetup(X.ctypes.data, self.n, self.n, d, k, perm_opt,
+                                           None if p is None else p.ctypes.data, lfil, kernel, params)
+        assert self.h
+
+    def info(self):
+        k = C.c_int()
+        perm = np.zeros(self.n, np.int32)
+        nnz = self.L.Nfft4GPAmdAfnInfo(self.h, C.byref(k), perm.ctypes.data, None, None, None)
+        assert nnz >= 0
+        n2 = self.n - k.value
+        ia = np.zeros(n2 + 1, np.int32)
+        ja = np.zeros(max(nnz, 1), np.int32)
+        aa = np.zeros(max(nnz, 1))
+        if nnz:
+            assert self.L.Nfft4GPAmdAfnInfo(self.h, None, None, ia.ctypes.data, ja.ctypes.data, aa.ctypes.data) == nnz
+        return k.value, perm, (ia, ja[:nnz], aa[:nnz])
+
+    def solve(self, rhs):
+        x = np.zeros(self.n)
+        r = np.ascontiguousarray(rhs, dtype=np.float64).copy()
+        assert self.L.Nfft4GPAmdAfnSolve(self.h, self.n, x.ctypes.data, r.ctypes.data) == 0
+        return x
+
+    def free(self):
+        self.L.Nfft4GPAmdAfnFree(self.h)
+
+
+def compare_csr(got, ref, max_bad_frac=0.005):
+    ia, ja, aa = got
+    ria, rja, raa = ref
+    np.testing.assert_array_equal(ia, ria)
+    bad = 0
+    for i in range(ia.size - 1):
+        s, rs = slice(ia[i], ia[i + 1]), slice(ria[i], ria[i + 1])
+        o, ro = np.argsort(ja[s]), np.argsort(rja[rs])
+        if not np.array_equal(ja[s][o], rja[rs][ro]):
+            bad += 1
+            continue
+        assert np.abs(aa[s][o] - raa[rs][ro]).max() <= 1e-8 * np.linalg.norm(raa[rs]), i
+    assert bad <= max(1, int(max_bad_frac * (ia.size - 1))), bad
+
+
+def test_fps_matches_golden(torch_cuda):
+    z = load("fps_synth")
+    p, d = gpu_fps(z["Xa"], int(z["ka"]))
+    np.testing.assert_array_equal(p, z["perm_a"])
+    np.testing.assert_array_equal(d, z["dist_a"])
+    p, d = gpu_fps(z["Xb"], 0, float(z["tol_b"]), device=torch_cuda)
+    np.testing.assert_array_equal(p, z["perm_b"])
+    np.testing.assert_array_equal(d, z["dist_b"])
+
+
+@need_ref
+@pytest.mark.parametrize("n,d,k,tol", [(20000, 3, 300, 0.0), (5000, 17, 0, 0.9), (300, 2, 300, 0.0), (7, 2, 1, 0.0)])
+def test_fps_matches_reference(torch_cuda, n, d, k, tol):
+    X = np.random.default_rng(n + d).random((n, d))
+    p_ref, d_ref = O.ref_sort_fps(X, k, tol)
+    p, dist = gpu_fps(X, k, tol)
+    np.testing.assert_array_equal(p, p_ref)
+    np.testing.assert_array_equal(dist, d_ref)
+
+
+def test_afn_setup_matches_golden(torch_cuda):
+    """The golden AFN (seeded permutation, k = 100, lfil 20) rebuilt on the GPU from the points."""
+    z = load("precond_synth")
+    X, f, l, mu = np.asarray(z["X"]), float(z["f"]), float(z["l"]), float(z["mu"])
+    n = X.shape[0]
+    k, perm, lfil = int(z["afn_k"]), np.asarray(z["afn_perm"]), int(z["lfil"])
+    params = _lib.kernel_params(f, l, mu, n)
+    A = GpuAfn(X, k, 2, perm, lfil, params)
+    _lib.lib().Nfft4GPKernelParamFree(params)
+    kk, p, csr = A.info()
+    assert kk == k
+    np.testing.assert_array_equal(p, perm)
+    compare_csr(csr, tuple(np.asarray(z[c]) for c in ("schur_i", "schur_j", "schur_a")))
+    r = np.asarray(z["afn_rhs"])
+    assert rel(A.solve(r), z["afn_out"]) <= 1e-9
+    A.free()
+
+
+@need_ref
+@pytest.mark.parametrize("kernel_l", [0.3, 0.15])
+def test_afn_setup_with_fps_matches_reference_pieces(torch_cuda, kernel_l):
+    """perm_opt 1: the GPU FPS order, then the same pieces the reference builds for it (afn.c:425-473)
+    through oracle/_ref: the Schur FSAI and the restated apply."""
+    import scipy.linalg as sl
+    rng = np.random.default_rng(int(kernel_l * 100))
+    n, d, k, lfil, f, mu = 3000, 3, 150, 15, 1.0, 0.01
+    X = np.asfortranarray(rng.random((n, d)))
+    P = O.ref_gaussian_params(f, kernel_l, mu, n)
+    A = GpuAfn(X, k, 1, None, lfil, P)
+    kk, perm, csr = A.info()
+    sel, _ = O.ref_sort_fps(X, k)
+    np.testing.assert_array_equal(perm, O.expand_perm(sel, n))
+    K11 = O.ref_gaussian_matrix(P, X, perm[:k])
+    K11 = np.tril(K11) + np.tril(K11, -1).T
+    L11 = sl.cholesky(K11, lower=True)
+    K12 = O.ref_gaussian_matrix(P, X, perm[:k], perm[k:])
+    SP, _keep = O.ref_schur_params(X, perm, k, L11, P)
+    sf = O.RefFsai(np.asfortranarray(X[perm[k:]]), SP, lfil, kernel="Nfft4GPKernelSchurCombineKernel")
+    compare_csr(csr, sf.csr())
+    for _ in range(2):
+        r = rng.random(n) - 0.5
+        assert rel(A.solve(r), O.afn_apply(perm, L11, K12, sf.solve, r.copy())) <= 1e-9
+    A.free()
+
+
+@need_ref
+def test_afn_setup_edge_ranks(torch_cuda):
+    """k = 0: the FSAI of the whole kernel (afn.c:270-281); k = n: A11 \\ rhs on the unpermuted data."""
+    rng = np.random.default_rng(3)
+    n, d, f, l, mu = 400, 2, 1.0, 0.3, 0.05
+    X = np.asfortranarray(rng.random((n, d)))
+    P = O.ref_gaussian_params(f, l, mu, n)
+    r = rng.random(n) - 0.5
+    A0 = GpuAfn(X, 0, 1, None, 12, P)
+    ref = O.RefFsai(X, P, 12)
+    kk, _, csr = A0.info()
+    assert kk == 0
+    compare_csr(csr, ref.csr())
+    assert rel(A0.solve(r), ref.solve(r)) <= 1e-9
+    A0.free()
+    An = GpuAfn(X, n, 1, None, 12, P)
+    K = O.ref_gaussian_matrix(P, X)
+    K = np.tril(K) + np.tril(K, -1).T
+    assert rel(An.solve(r), np.linalg.solve(K, r)) <= 1e-8
+    An.free()
+
+
+def test_pcg_with_gpu_afn_matches_golden_iterations(torch_cuda):
+    """This library's PCG with the GPU-built AFN (AfnPrecond.setup) needs as many iterations as the
+    reference's PCG with the golden AFN on the same dense operator (within 5 %)."""
+    from test_gpu_golden import DenseGaussHostOp
+    torch = torch_cuda
+    z = load("precond_synth")
+    X, f, l, mu = np.asarray(z["X"]), float(z["f"]), float(z["l"]), float(z["mu"])
+    pre = amd.AfnPrecond.setup(X, int(z["afn_k"]), f, l, mu, perm_opt="perm", perm=np.asarray(z["afn_perm"]),
+                               schur_lfil=int(z["lfil"]))
+    assert pre.k == int(z["afn_k"])
+    op = DenseGaussHostOp(z)
+    b = torch.tensor(np.asarray(z["b"]), device="cuda")
+    x = torch.zeros(op.n, dtype=torch.float64, device="cuda")
+    x, rr, hist, it = amd.pcg(op, b, x, maxits=1000, tol=1e-6, precond=pre)
+    it_ref = int(z["pcgafn_iters"])
+    assert it > 0 and abs(it - it_ref) <= max(2, it_ref // 20), (it, it_ref)
+    assert rr <= 1e-6
+
+
+def test_sort_fps_front_end_device_tensor(torch_cuda):
+    """amd.sort_fps on a device tensor (column-major n x d as a (d, n) tensor) equals the host call."""
+    torch = torch_cuda
+    X = np.random.default_rng(9).random((4000, 4))
+    p_host, d_host = amd.sort_fps(X, 64)
+    p_dev, d_dev = amd.sort_fps(torch.tensor(X.T.copy(), device="cuda"), 64)
+    np.testing.assert_array_equal(p_host, p_dev)
+    np.testing.assert_array_equal(d_host, d_dev)
