@@ -97,6 +97,37 @@ __device__ void block_best(double& v, int& i, bool max_mode)
    }
 }
 
+// the last workgroup to finish (ticket) reduces every workgroup's (value, index) with all its threads;
+// returns true in that workgroup, with the winner in (v, i) on thread 0
+__device__ bool last_block_best(double bv, int bi, double* pv, int* pi, unsigned int* ticket, bool max_mode,
+                                double& v, int& i)
+{
+   __shared__ int s_last;
+   block_best(bv, bi, max_mode);
+   if (threadIdx.x == 0) {
+      pv[blockIdx.x] = bv;
+      pi[blockIdx.x] = bi;
+      __threadfence();
+      s_last = (atomicAdd(ticket, 1u) == gridDim.x - 1) ? 1 : 0;
+   }
+   __syncthreads();
+   if (!s_last) return false;
+   __threadfence();
+   v = 0.0;
+   i = -1;
+   for (int g = threadIdx.x; g < (int)gridDim.x; g += kFpsThreads) {
+      const double gv = __hip_atomic_load(&pv[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int gi = __hip_atomic_load(&pi[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (beats(gv, gi, v, i, max_mode)) {
+         v = gv;
+         i = gi;
+      }
+   }
+   __syncthreads();  // block_best's LDS is reused
+   block_best(v, i, max_mode);
+   return true;
+}
+
 // per-column mean of data / n (ordering.c:467-506), blocked fixed-order sums
 __global__ __launch_bounds__(kFpsThreads) void k_col_mean(const double* __restrict__ X, long long ldim, int n,
                                                           double* __restrict__ mean)
@@ -131,28 +162,11 @@ __global__ __launch_bounds__(kFpsThreads) void k_fps_center(const double* __rest
          bi = i;
       }
    }
-   block_best(bv, bi, false);
-   if (threadIdx.x == 0) {
-      pv[blockIdx.x] = bv;
-      pi[blockIdx.x] = bi;
-      __threadfence();
-      const unsigned int t = atomicAdd(&st->ticket, 1u);
-      if (t == gridDim.x - 1) {
-         __threadfence();
-         double v = 0.0;
-         int b = -1;
-         for (int g = 0; g < (int)gridDim.x; g++) {
-            const double gv = __hip_atomic_load(&pv[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int gi = __hip_atomic_load(&pi[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (beats(gv, gi, v, b, false)) {
-               v = gv;
-               b = gi;
-            }
-         }
-         st->i1 = b;
-         st->ticket = 0u;
-      }
-   }
+   double v;
+   int b;
+   if (!last_block_best(bv, bi, pv, pi, &st->ticket, false, v, b) || threadIdx.x != 0) return;
+   st->i1 = b;
+   st->ticket = 0u;
 }
 
 // one FPS pass against the newest point st->i1 (ordering.c:545-694)
@@ -186,24 +200,9 @@ __global__ __launch_bounds__(kFpsThreads) void k_fps_step(const double* __restri
          bi = i;
       }
    }
-   block_best(bv, bi, true);
-   if (threadIdx.x != 0) return;
-   pv[blockIdx.x] = bv;
-   pi[blockIdx.x] = bi;
-   __threadfence();
-   const unsigned int t = atomicAdd(&st->ticket, 1u);
-   if (t != gridDim.x - 1) return;
-   __threadfence();
-   double v = 0.0;
-   int b = -1;
-   for (int g = 0; g < (int)gridDim.x; g++) {
-      const double gv = __hip_atomic_load(&pv[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int gi = __hip_atomic_load(&pi[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (beats(gv, gi, v, b, true)) {
-         v = gv;
-         b = gi;
-      }
-   }
+   double v;
+   int b;
+   if (!last_block_best(bv, bi, pv, pi, &st->ticket, true, v, b) || threadIdx.x != 0) return;
    // the reference keeps (dmax, i2) = (0, 0) unless some distance is strictly positive
    double dmax = 0.0;
    int i2 = 0;
@@ -451,10 +450,10 @@ void* Nfft4GPAmdAfnSetup(const double* data, int n, int ldim, int d, int k, int 
       if (!S) return fail("FSAI upload");
    }
    (void)hipStreamSynchronize(s);
-   for (void* p : {(void*)dX, (void*)Xp, (void*)K11, (void*)Gt, (void*)W, (void*)dinfo}) (void)hipFree(p);
-   dX = Xp = K11 = Gt = W = nullptr;
+   for (void* p : {(void*)dX, (void*)Xp, (void*)K11, (void*)W, (void*)dinfo}) (void)hipFree(p);
+   dX = Xp = K11 = W = nullptr;
    dinfo = nullptr;
-   void* A = afn_create_device(n, k, dperm, G, K12, S);
+   void* A = afn_create_device(n, k, dperm, G, Gt, K12, S);
    if (!A) {
       fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: allocation failed\n");
       return nullptr;  // afn_create_device released the factors and S

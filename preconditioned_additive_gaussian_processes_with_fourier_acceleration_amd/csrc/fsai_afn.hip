@@ -34,12 +34,13 @@ struct FsaiDev {
 struct AfnDev {
    int n = 0, k = 0, n2 = 0;
    int* perm = nullptr;
-   double* Linv = nullptr;  // k x k, inverse of the lower Cholesky factor of A11
+   double* Linv = nullptr;   // k x k, inverse of the lower Cholesky factor of A11 (column j: rows >= j)
+   double* LinvT = nullptr;  // its transpose (column i = row i of Linv)
    double* K12 = nullptr;   // k x n2 column-major
    FsaiDev* S = nullptr;    // FSAI of the Schur complement (n2)
    bool own_S = false;
    double *rp = nullptr, *y = nullptr, *t = nullptr, *part = nullptr;
-   int nblk = 0;
+   int nblk = 0, cols = 1;  // A12 y2: workgroups, columns per workgroup
 };
 
 // y[i] = sum_j a[j] x[ja[j]] in the row's stored order, unfused (matops.c:239-248)
@@ -66,18 +67,19 @@ __global__ void k_scatter(const double* __restrict__ src, const int* __restrict_
    if (i < n) dst[perm[i]] = src[i];
 }
 
-// out = Linv v (lower) or Linv^T v
-__global__ void k_trmv(const double* __restrict__ Linv, int k, const double* __restrict__ v, double* __restrict__ out,
-                       int trans)
+// out[i] = sum_j M[j + i*k] v[j]: one wave per output over a contiguous column of M.  M = LinvT gives
+// Linv v, M = Linv gives Linv^T v (the other triangle holds zeros)
+__global__ __launch_bounds__(256) void k_trmv(const double* __restrict__ M, int k, const double* __restrict__ v,
+                                              double* __restrict__ out)
 {
-   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   const int lane = threadIdx.x & 63;
+   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
    if (i >= k) return;
+   const double* col = M + (size_t)i * k;
    double r = 0.0;
-   if (!trans)
-      for (int j = 0; j <= i; j++) r = fma(Linv[i + (size_t)j * k], v[j], r);
-   else
-      for (int j = i; j < k; j++) r = fma(Linv[j + (size_t)i * k], v[j], r);
-   out[i] = r;
+   for (int j = lane; j < k; j += 64) r = fma(col[j], v[j], r);
+   for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off, 64);
+   if (lane == 0) out[i] = r;
 }
 
 // rp2[j] -= sum_i K12[i + j*k] y[i]  (one wave per column)
@@ -94,27 +96,44 @@ __global__ __launch_bounds__(256) void k_a12t(const double* __restrict__ K12, in
    if (lane == 0) rp2[j] -= r;
 }
 
-// part[blk][i] = sum_{j in blk} K12[i + j*k] y2[j]
-constexpr int kA12Cols = 1024;
-__global__ void k_a12_part(const double* __restrict__ K12, int k, int n2, const double* __restrict__ y2,
-                           double* __restrict__ part)
+// part[blk][i] = sum_{j in blk} K12[i + j*k] y2[j]; `cols` columns per workgroup, sized at create so
+// that ~2048 workgroups stream K12 (one HBM pass over k x n2)
+constexpr int kA12Blocks = 2048;
+__global__ __launch_bounds__(256) void k_a12_part(const double* __restrict__ K12, int k, int n2, int cols,
+                                                  const double* __restrict__ y2, double* __restrict__ part)
 {
-   const int j0 = blockIdx.x * kA12Cols, j1 = min(n2, j0 + kA12Cols);
+   const int j0 = blockIdx.x * cols, j1 = min(n2, j0 + cols);
    for (int i = threadIdx.x; i < k; i += blockDim.x) {
-      double r = 0.0;
-      for (int j = j0; j < j1; j++) r = fma(K12[i + (size_t)j * k], y2[j], r);
-      part[(size_t)blockIdx.x * k + i] = r;
+      double r0 = 0.0, r1 = 0.0;
+      int j = j0;
+      for (; j + 1 < j1; j += 2) {
+         r0 = fma(K12[i + (size_t)j * k], y2[j], r0);
+         r1 = fma(K12[i + (size_t)(j + 1) * k], y2[j + 1], r1);
+      }
+      if (j < j1) r0 = fma(K12[i + (size_t)j * k], y2[j], r0);
+      part[(size_t)blockIdx.x * k + i] = r0 + r1;
    }
 }
 
-// rp[i] -= sum_blk part[blk][i]
-__global__ void k_a12_reduce(const double* __restrict__ part, int nblk, int k, double* __restrict__ rp)
+// rp[i] -= sum_blk part[blk][i]: 4 waves split the workgroups, fixed order
+__global__ __launch_bounds__(256) void k_a12_reduce(const double* __restrict__ part, int nblk, int k,
+                                                    double* __restrict__ rp)
 {
-   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-   if (i >= k) return;
+   __shared__ double s[4][64];
+   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+   const int i = blockIdx.x * 64 + lane;
    double r = 0.0;
-   for (int b = 0; b < nblk; b++) r += part[(size_t)b * k + i];
-   rp[i] -= r;
+   if (i < k)
+      for (int b = w; b < nblk; b += 4) r += part[(size_t)b * k + i];
+   s[w][lane] = r;
+   __syncthreads();
+   if (w == 0 && i < k) rp[i] -= (s[0][lane] + s[1][lane]) + (s[2][lane] + s[3][lane]);
+}
+
+void a12_shape(int n2, int& cols, int& nblk)
+{
+   cols = std::max(16, std::min(1024, (n2 + kA12Blocks - 1) / kA12Blocks));
+   nblk = (n2 + cols - 1) / cols;
 }
 
 template <class T>
@@ -204,30 +223,30 @@ int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
 {
    AfnDev* A = (AfnDev*)obj;
    const int n = A->n, k = A->k, n2 = A->n2;
-   const int g = (n + 255) / 256, gk = (k + 255) / 256;
+   const int g = (n + 255) / 256, gk = (k + 3) / 4;
    double* rp2 = A->rp + k;
    double* y2 = A->y + k;
    if (k == 0) return fsai_apply_dev(A->S, dx, drhs, s);  // afn.c:106-110
    if (n2 == 0) {                                          // afn.c:101-105: A11 solve on the unpermuted rhs
-      hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, drhs, A->t, 0);
-      hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, dx, 1);
+      hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->LinvT, k, drhs, A->t);
+      hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, dx);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return 0;
    }
    hipLaunchKernelGGL(k_gather, dim3(g), dim3(256), 0, s, drhs, A->perm, n, A->rp);
    // y = A11 \ rp = L^{-T} (L^{-1} rp)
-   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->rp, A->t, 0);
-   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y, 1);
+   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->LinvT, k, A->rp, A->t);
+   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y);
    // rp2 -= A12^T y
    hipLaunchKernelGGL(k_a12t, dim3((n2 + 3) / 4), dim3(256), 0, s, A->K12, k, n2, A->y, rp2);
    // y2 = FSAI(rp2)
    if (fsai_apply_dev(A->S, y2, rp2, s)) return -1;
    // rp -= A12 y2
-   hipLaunchKernelGGL(k_a12_part, dim3(A->nblk), dim3(256), 0, s, A->K12, k, n2, y2, A->part);
-   hipLaunchKernelGGL(k_a12_reduce, dim3(gk), dim3(256), 0, s, A->part, A->nblk, k, A->rp);
+   hipLaunchKernelGGL(k_a12_part, dim3(A->nblk), dim3(256), 0, s, A->K12, k, n2, A->cols, y2, A->part);
+   hipLaunchKernelGGL(k_a12_reduce, dim3((k + 63) / 64), dim3(256), 0, s, A->part, A->nblk, k, A->rp);
    // y = A11 \ rp
-   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->rp, A->t, 0);
-   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y, 1);
+   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->LinvT, k, A->rp, A->t);
+   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y);
    hipLaunchKernelGGL(k_scatter, dim3(g), dim3(256), 0, s, A->y, A->perm, n, dx);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
@@ -237,7 +256,7 @@ int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
 
 // an AFN apply object from factors already in HBM (afn_setup.hip); takes ownership of d_perm, d_Linv,
 // d_K12 (hipMalloc'ed) and of the Schur FSAI handle S (an Nfft4GPAmdFsaiCreate handle of size n - k)
-void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_K12, void* S)
+void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_LinvT, double* d_K12, void* S)
 {
    AfnDev* A = new AfnDev();
    A->n = n;
@@ -247,8 +266,9 @@ void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_K12
    A->own_S = true;
    A->perm = d_perm;
    A->Linv = d_Linv;
+   A->LinvT = d_LinvT;
    A->K12 = d_K12;
-   A->nblk = (A->n2 + kA12Cols - 1) / kA12Cols;
+   a12_shape(A->n2, A->cols, A->nblk);
    if (hipMalloc((void**)&A->rp, sizeof(double) * n) != hipSuccess ||
        hipMalloc((void**)&A->y, sizeof(double) * n) != hipSuccess ||
        hipMalloc((void**)&A->t, sizeof(double) * std::max(1, k)) != hipSuccess ||
@@ -307,14 +327,18 @@ void* Nfft4GPAmdAfnCreate(int n, int k, const int* perm, const double* L11, cons
          G[i + (size_t)j * k] = -v / L[i + (size_t)i * k];
       }
    }
+   std::vector<double> GT((size_t)k * k);
+   for (int j = 0; j < k; j++)
+      for (int i = 0; i < k; i++) GT[j + (size_t)i * k] = G[i + (size_t)j * k];
    AfnDev* A = new AfnDev();
    A->n = n;
    A->k = k;
    A->n2 = n - k;
    A->S = S;
-   A->nblk = (A->n2 + kA12Cols - 1) / kA12Cols;
+   a12_shape(A->n2, A->cols, A->nblk);
    const bool mid = k > 0 && k < n;
    if ((mid && up(&A->perm, perm, (size_t)n)) || up(&A->Linv, G.data(), G.size()) ||
+       up(&A->LinvT, GT.data(), GT.size()) ||
        (mid && up(&A->K12, K12, (size_t)k * A->n2)) || hipMalloc((void**)&A->rp, sizeof(double) * n) != hipSuccess ||
        hipMalloc((void**)&A->y, sizeof(double) * n) != hipSuccess ||
        hipMalloc((void**)&A->t, sizeof(double) * std::max(1, k)) != hipSuccess ||
@@ -337,8 +361,8 @@ void Nfft4GPAmdAfnFree(void* afn)
 {
    AfnDev* A = (AfnDev*)afn;
    if (!A) return;
-   for (void* p : {(void*)A->perm, (void*)A->Linv, (void*)A->K12, (void*)A->rp, (void*)A->y, (void*)A->t,
-                   (void*)A->part})
+   for (void* p : {(void*)A->perm, (void*)A->Linv, (void*)A->LinvT, (void*)A->K12, (void*)A->rp, (void*)A->y,
+                   (void*)A->t, (void*)A->part})
       (void)hipFree(p);
    // the Schur complement's FSAI handle stays with its creator (Nfft4GPAmdFsaiFree) unless the AFN was
    // set up on the device (Nfft4GPAmdAfnSetup), which owns it

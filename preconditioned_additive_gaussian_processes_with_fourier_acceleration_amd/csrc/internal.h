@@ -222,7 +222,7 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, int kern
                     const double* dW, int kw, int require_grad, std::vector<int>& ia, std::vector<int>& ja,
                     std::vector<double>& aa, std::vector<double>& da, hipStream_t s);
 // AFN apply object from device factors (fsai_afn.hip); owns all of them and S
-void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_K12, void* S);
+void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_LinvT, double* d_K12, void* S);
 
 hipStream_t current_stream();
 bool is_device_ptr(const void* p);
