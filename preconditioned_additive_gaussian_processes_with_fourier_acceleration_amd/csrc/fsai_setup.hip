@@ -48,6 +48,7 @@ constexpr int kKnnThreads = 256;
 constexpr int kKnnGather = 256;    // survivors of the radix select sorted directly
 constexpr int kMaxDims = 256;      // features of `data`
 constexpr int kTrsvThreads = 1024;
+int knn_fallback_rows = 0;  // rows of the last FSAI setup that k_knn_bounded handed to k_knn
 
 __device__ __forceinline__ double sqdist(const double* __restrict__ X, int ldim, int d, const double* xi, int j)
 {
@@ -60,9 +61,11 @@ __device__ __forceinline__ double sqdist(const double* __restrict__ X, int ldim,
 }
 
 // pattern rows i in [lfil, n): ja[ia[i] .. ia[i] + lfil - 2] = the lfil-1 nearest of 0..i-1 by
-// (squared distance, index), ja[ia[i] + lfil - 1] = i.  Grid-stride over rows.
+// (squared distance, index), ja[ia[i] + lfil - 1] = i.  Grid-stride over rows, or over the rows of
+// `rows` (nrows of them) when given: the rows k_knn_bounded could not settle.
 __global__ __launch_bounds__(kKnnThreads) void k_knn(const double* __restrict__ X, int ldim, int n, int d, int lfil,
-                                                     const int* __restrict__ ia, int* __restrict__ ja)
+                                                     const int* __restrict__ ia, int* __restrict__ ja,
+                                                     const int* __restrict__ rows, int nrows)
 {
    __shared__ unsigned int hist[256];
    __shared__ double s_xi[kMaxDims];
@@ -73,7 +76,9 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn(const double* __restrict__ 
    __shared__ int s_bits, s_need, s_eq;
    const int tid = threadIdx.x;
    const int K = lfil - 1;
-   for (int i = lfil + blockIdx.x; i < n; i += gridDim.x) {
+   const int nloop = rows ? nrows : n - lfil;
+   for (int it = blockIdx.x; it < nloop; it += gridDim.x) {
+      const int i = rows ? rows[it] : lfil + it;
       for (int c = tid; c < d; c += kKnnThreads) s_xi[c] = X[(size_t)c * ldim + i];
       if (tid == 0) {
          s_prefix = 0ull;
@@ -165,6 +170,224 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn(const double* __restrict__ 
          ja[row + rank] = ie;
       }
       if (tid == 0) ja[row + K] = i;
+      __syncthreads();
+   }
+}
+
+// The same pattern rows, kKnnRows consecutive rows per workgroup sharing every load of a point (the
+// scan is bound by the on-chip bandwidth of re-reading the earlier points, so the rows per workgroup
+// set the speed), in two passes over the earlier points instead of k_knn's three to four:
+//   sample  the squared distances to points 0..S-1 (S = min(i0, 4096)) histogrammed by exponent (256
+//           bins over 2^-224 .. 2^31, clamped) give the bin of the sample's (lfil-1)-th smallest, so
+//           every true neighbour has a key below tau = the bin's upper end;
+//   count   keys below tau, binned by (exponent - (E-16), 4 top mantissa bits) with tau = 2^E -- 256
+//           monotone bins over [2^(E-16), tau), smaller keys in bin 0 -- locate the bin b* of the
+//           (lfil-1)-th key;
+//   collect keys in bins below b* are in, keys in b* (at most kKnnGather2) are ranked by (key, index).
+// Only keys below tau touch the LDS histograms (a few percent of them).  A row whose bin b* holds more
+// than kKnnGather2 keys (duplicates, pathological data) is appended to `fail` for k_knn.  d <= 64.
+constexpr int kKnnRows = 16;
+constexpr int kKnnSample = 4096;
+constexpr int kKnnGather2 = 128;
+constexpr int kKnnMaxDims2 = 64;
+constexpr int kExpBase = 1023 - 224;
+__device__ __forceinline__ int knn_bin(unsigned long long u, int base)
+{
+   const int e = (int)(u >> 52);
+   return (e < base) ? 0 : (((e - base) << 4) | (int)((u >> 48) & 15ull));
+}
+
+__global__ __launch_bounds__(kKnnThreads) void k_knn_bounded(const double* __restrict__ X, int ldim, int n, int d,
+                                                             int lfil, const int* __restrict__ ia,
+                                                             int* __restrict__ ja, int* __restrict__ fail,
+                                                             int* __restrict__ nfail)
+{
+   constexpr int R = kKnnRows;
+   __shared__ double q[kKnnMaxDims2][R];
+   __shared__ unsigned int h0[R][256];
+   __shared__ unsigned int h1[R][256];
+   __shared__ unsigned long long s_key[R][kKnnGather2 + kFsaiMaxK];
+   __shared__ int s_idx[R][kKnnGather2 + kFsaiMaxK];
+   __shared__ unsigned long long s_tau[R];
+   __shared__ int s_base[R], s_bstar[R], s_ok[R];
+   __shared__ int s_nsel[R], s_ngat[R];
+   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+   const int K = lfil - 1;
+   const int ngroups = (n - lfil + R - 1) / R;
+   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+      const int i0 = lfil + g * R;
+      const int nr = min(R, n - i0);
+      for (int e = tid; e < R * d; e += kKnnThreads) {
+         const int r = e / d, c = e % d;
+         q[c][r] = (r < nr) ? X[(size_t)c * ldim + i0 + r] : 0.0;
+      }
+      for (int e = tid; e < R * 256; e += kKnnThreads) {
+         h0[e / 256][e % 256] = 0u;
+         h1[e / 256][e % 256] = 0u;
+      }
+      if (tid < R) {
+         s_nsel[tid] = 0;
+         s_ngat[tid] = 0;
+      }
+      __syncthreads();
+      // sample: exponent histogram of keys to points 0..S-1 (S <= i0 <= every row's i)
+      const int S = min(i0, kKnnSample);
+      for (int j = tid; j < S; j += kKnnThreads) {
+         double acc[R];
+#pragma unroll
+         for (int r = 0; r < R; r++) acc[r] = 0.0;
+         for (int c = 0; c < d; c++) {
+            const double xj = X[(size_t)c * ldim + j];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+               const double t = xj - q[c][r];
+               acc[r] = fma(t, t, acc[r]);
+            }
+         }
+#pragma unroll
+         for (int r = 0; r < R; r++)
+            if (r < nr) {
+               const int e = (int)((unsigned long long)__double_as_longlong(acc[r]) >> 52);
+               atomicAdd(&h0[r][min(255, max(0, e - kExpBase))], 1u);
+            }
+      }
+      __syncthreads();
+      // one wave per row: the first bin where the cumulative count reaches K
+      for (int r = wave; r < nr; r += kKnnThreads / 64) {
+         unsigned int loc = 0;
+         for (int b = 0; b < 4; b++) loc += h0[r][lane * 4 + b];
+         unsigned int incl = loc;
+         for (int off = 1; off < 64; off <<= 1) {
+            const unsigned int o = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += o;
+         }
+         const unsigned long long hit = __ballot(incl >= (unsigned)K);
+         const int first = __ffsll((long long)hit) - 1;
+         if (lane == first) {
+            unsigned int cum = incl - loc;
+            int b = lane * 4;
+            for (;; b++) {
+               cum += h0[r][b];
+               if (cum >= (unsigned)K) break;
+            }
+            const int E = b + kExpBase + 1;  // keys of bin b have exponents < E (bin 255: any)
+            s_tau[r] = (b == 255) ? ~0ull : ((unsigned long long)E << 52);
+            s_base[r] = ((b == 255) ? 2047 : E) - 16;
+         }
+      }
+      __syncthreads();
+      // count: keys below tau by (exponent, 4 mantissa bits)
+      const int jmax = i0 + nr - 1;
+      for (int j = tid; j < jmax; j += kKnnThreads) {
+         double acc[R];
+#pragma unroll
+         for (int r = 0; r < R; r++) acc[r] = 0.0;
+         for (int c = 0; c < d; c++) {
+            const double xj = X[(size_t)c * ldim + j];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+               const double t = xj - q[c][r];
+               acc[r] = fma(t, t, acc[r]);
+            }
+         }
+#pragma unroll
+         for (int r = 0; r < R; r++) {
+            const unsigned long long u = (unsigned long long)__double_as_longlong(acc[r]);
+            if (r < nr && j < i0 + r && u < s_tau[r]) atomicAdd(&h1[r][knn_bin(u, s_base[r])], 1u);
+         }
+      }
+      __syncthreads();
+      for (int r = wave; r < nr; r += kKnnThreads / 64) {
+         unsigned int loc = 0;
+         for (int b = 0; b < 4; b++) loc += h1[r][lane * 4 + b];
+         unsigned int incl = loc;
+         for (int off = 1; off < 64; off <<= 1) {
+            const unsigned int o = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += o;
+         }
+         const unsigned long long hit = __ballot(incl >= (unsigned)K);
+         const int first = __ffsll((long long)hit) - 1;
+         if (lane == first) {
+            unsigned int cum = incl - loc;
+            int b = lane * 4;
+            for (;; b++) {
+               if (cum + h1[r][b] >= (unsigned)K) break;
+               cum += h1[r][b];
+            }
+            s_bstar[r] = b;
+            s_ok[r] = (h1[r][b] <= (unsigned)kKnnGather2) ? 1 : 0;
+         }
+      }
+      __syncthreads();
+      // collect
+      for (int j = tid; j < jmax; j += kKnnThreads) {
+         double acc[R];
+#pragma unroll
+         for (int r = 0; r < R; r++) acc[r] = 0.0;
+         for (int c = 0; c < d; c++) {
+            const double xj = X[(size_t)c * ldim + j];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+               const double t = xj - q[c][r];
+               acc[r] = fma(t, t, acc[r]);
+            }
+         }
+#pragma unroll
+         for (int r = 0; r < R; r++) {
+            const unsigned long long u = (unsigned long long)__double_as_longlong(acc[r]);
+            if (r < nr && s_ok[r] && j < i0 + r && u < s_tau[r]) {
+               const int b = knn_bin(u, s_base[r]);
+               if (b < s_bstar[r]) {
+                  const int p = atomicAdd(&s_nsel[r], 1);
+                  s_key[r][kKnnGather2 + p] = u;
+                  s_idx[r][kKnnGather2 + p] = j;
+               } else if (b == s_bstar[r]) {
+                  const int p = atomicAdd(&s_ngat[r], 1);
+                  s_key[r][p] = u;
+                  s_idx[r][p] = j;
+               }
+            }
+         }
+      }
+      __syncthreads();
+      // rank the bin-b* keys by (key, index); the first K - below join (one wave per row)
+      for (int r = wave; r < nr; r += kKnnThreads / 64) {
+         if (!s_ok[r]) continue;
+         const int ng = s_ngat[r], nsel0 = s_nsel[r];
+         for (int e = lane; e < ng; e += 64) {
+            const unsigned long long ke = s_key[r][e];
+            const int ie = s_idx[r][e];
+            int rank = 0;
+            for (int o = 0; o < ng; o++) {
+               const unsigned long long ko = s_key[r][o];
+               rank += (ko < ke || (ko == ke && s_idx[r][o] < ie)) ? 1 : 0;
+            }
+            if (rank < K - nsel0) {
+               s_key[r][kKnnGather2 + nsel0 + rank] = ke;
+               s_idx[r][kKnnGather2 + nsel0 + rank] = ie;
+            }
+         }
+      }
+      __syncthreads();
+      for (int r = wave; r < nr; r += kKnnThreads / 64) {
+         const int i = i0 + r;
+         if (!s_ok[r]) {
+            if (lane == 0) fail[atomicAdd(nfail, 1)] = i;
+            continue;
+         }
+         const int row = ia[i];
+         for (int e = lane; e < K; e += 64) {
+            const unsigned long long ke = s_key[r][kKnnGather2 + e];
+            const int ie = s_idx[r][kKnnGather2 + e];
+            int rank = 0;
+            for (int o = 0; o < K; o++) {
+               const unsigned long long ko = s_key[r][kKnnGather2 + o];
+               rank += (ko < ke || (ko == ke && s_idx[r][kKnnGather2 + o] < ie)) ? 1 : 0;
+            }
+            ja[row + rank] = ie;
+         }
+         if (lane == 0) ja[row + K] = i;
+      }
       __syncthreads();
    }
 }
@@ -595,8 +818,33 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, int kern
        (require_grad && upload(&dda, (const double*)nullptr, 3 * (size_t)nnz)))
       return cleanup(-1);
    if (n > lfil) {
-      const int grid = std::min(n - lfil, 4096);
-      hipLaunchKernelGGL(k_knn, dim3(grid), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia, dja);
+      // bounded two-pass KNN, then the radix-select kernel on the rows it could not settle
+      int* dfail = nullptr;
+      if (upload(&dfail, (const int*)nullptr, (size_t)(n - lfil) + 1) ||
+          hipMemsetAsync(dfail + (n - lfil), 0, sizeof(int), s) != hipSuccess) {
+         (void)hipFree(dfail);
+         return cleanup(-1);
+      }
+      const int ngroups = (n - lfil + kKnnRows - 1) / kKnnRows;
+      int nfail = 0;
+      if (d <= kKnnMaxDims2) {
+         hipLaunchKernelGGL(k_knn_bounded, dim3(std::min(ngroups, 8192)), dim3(kKnnThreads), 0, s, dX, ldim, n, d,
+                            lfil, dia, dja, dfail, dfail + (n - lfil));
+         if (hipMemcpyAsync(&nfail, dfail + (n - lfil), sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+             hipStreamSynchronize(s) != hipSuccess) {
+            (void)hipFree(dfail);
+            return cleanup(-1);
+         }
+         if (nfail > 0)
+            hipLaunchKernelGGL(k_knn, dim3(std::min(nfail, 4096)), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia,
+                               dja, dfail, nfail);
+      } else {
+         hipLaunchKernelGGL(k_knn, dim3(std::min(n - lfil, 4096)), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia,
+                            dja, nullptr, 0);
+      }
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(dfail);
+      knn_fallback_rows = nfail;
    }
    KernelParams P;
    P.kernel = kernel;

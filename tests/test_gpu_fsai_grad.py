@@ -168,3 +168,24 @@ def test_fsai_pcg_on_dense_operator(torch_cuda):
     assert it > 0 and it_ref > 0 and rr <= 1e-8
     assert abs(it - it_ref) <= max(2, it_ref // 20), (it, it_ref)
     ours.free()
+
+
+@pytest.mark.parametrize("n,d,lfil", [(3000, 2, 20), (1500, 3, 40)])
+def test_fsai_pattern_exact_order_with_ties(torch_cuda, n, d, lfil):
+    """Points on a coarse lattice: exact squared distances (any summation order), many duplicates and
+    ties.  Every row must hold the lfil-1 smallest (distance, index) of the earlier points in that order,
+    then the point itself (kernels.c:121-278 with ties broken by index).  Duplicates overflow the
+    bounded KNN's bins, so this also runs its radix-select fallback."""
+    rng = np.random.default_rng(n)
+    X = rng.integers(0, 4, (n, d)) / 4.0
+    params = O.ref_gaussian_params(1.0, 0.5, 0.1, n) if O.ref_available() else None
+    ours = AmdFsai(lfil)
+    ours.setup(X, params, grad=False)
+    ia, ja, _, _ = ours.csr()
+    K = lfil - 1
+    for i in range(lfil, n, 7):
+        d2 = ((X[:i] - X[i]) ** 2).sum(axis=1)
+        expect = np.lexsort((np.arange(i), d2))[:K]
+        np.testing.assert_array_equal(ja[ia[i]:ia[i + 1] - 1], expect, err_msg=f"row {i}")
+        assert ja[ia[i + 1] - 1] == i
+    ours.free()
