@@ -189,3 +189,45 @@ def test_fsai_pattern_exact_order_with_ties(torch_cuda, n, d, lfil):
         np.testing.assert_array_equal(ja[ia[i]:ia[i + 1] - 1], expect, err_msg=f"row {i}")
         assert ja[ia[i + 1] - 1] == i
     ours.free()
+
+
+def test_gp_loss_with_gpu_fsai(torch_cuda):
+    """Nfft4GPGpLoss (this library's) with the reference's dense Gaussian operator and THIS library's
+    FSAI with gradients (setup / solve / trace / logdet / dvp on the GPU) against the reference's
+    Nfft4GPGpLoss with its own FSAI (fsai.c) on the same inputs and probes."""
+    lib = O.ref_lib()
+    rng = np.random.default_rng(4)
+    n, d, lfil, nvecs, maxits = 600, 3, 20, 6, 30
+    X = np.asfortranarray(rng.random((n, d)))
+    y = rng.random(n) - 0.5
+    hyper = np.array([1.1, 0.3, 0.02])
+    R = np.asfortranarray(np.sign(rng.random((n, nvecs)) - 0.5))
+    kh = O.ref_gaussian_params(1.0, 1.0, 0.01, n)
+    pkh = O.ref_gaussian_params(1.0, 1.0, 0.01, n)
+    lib.Nfft4GPPrecondFsaiCreate.restype = C.c_void_p
+    lib.Nfft4GPPrecondFsaiSetLfil.argtypes = [C.c_void_p, C.c_int]
+    lib.Nfft4GPPrecondFsaiFree.argtypes = [C.c_void_p]
+    ref_fs = lib.Nfft4GPPrecondFsaiCreate()
+    lib.Nfft4GPPrecondFsaiSetLfil(ref_fs, lfil)
+    ours = AmdFsai(lfil)
+    f = lambda name: C.cast(getattr(lib, name), C.c_void_p).value  # noqa: E731
+    dwork = np.zeros(4 * n * n + 4 * n)
+
+    def run(fn, prefix, getp, h):
+        args = (hyper.ctypes.data, X.ctypes.data, y.ctypes.data, n, n, d, f("Nfft4GPKernelGaussianKernel"), kh, None,
+                f("Nfft4GPDenseMatSymv"), f("Nfft4GPDenseGradMatSymv"), f("Nfft4GPKernelGaussianKernel"), pkh, None,
+                *[getp(prefix + s) for s in ("SetupWithKernel", "Solve", "Trace", "Logdet", "Dvp", "Reset")], h, 0,
+                1e-8, maxits, maxits, nvecs, R.ctypes.data, 0, None, 0, dwork.ctypes.data)
+        fn.argtypes = O.RefGpLoss.ARGTYPES
+        fn.restype = C.c_int
+        loss = np.zeros(1)
+        grad = np.zeros(3)
+        assert fn(*args, loss.ctypes.data_as(_lib.dp), grad.ctypes.data_as(_lib.dp)) == 0
+        return loss[0], grad
+
+    loss_ref, grad_ref = run(lib.Nfft4GPGpLoss, "Nfft4GPPrecondFsai", f, ref_fs)
+    loss, grad = run(_lib.lib().Nfft4GPGpLoss, "Nfft4GPAmdPrecondFsai", _lib.fnptr, ours.h)
+    lib.Nfft4GPPrecondFsaiFree(ref_fs)
+    ours.free()
+    assert loss == pytest.approx(loss_ref, rel=1e-8)
+    np.testing.assert_allclose(grad, grad_ref, rtol=1e-6, atol=1e-9)
