@@ -338,6 +338,28 @@ void *Nfft4GPAmdAfnSetup(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int
  * NULL; returns the FSAI's nnz (0 without one), -1 on error */
 int Nfft4GPAmdAfnInfo(void *afn, int *k, int *perm, int *ia, int *ja, NFFT4GP_DOUBLE *aa);
 
+/* ---- rank estimation (SRC/linearalg/rankest.c) -----------------------------------------------------
+ * Drop-ins for Nfft4GPRankestNysScaled (rankest.c:248-391: nsample_r scaled subsamples of nsample points
+ * drawn with libc rand() as Nfft4GPRandPerm does, FPS-ordered, the Nystrom error of ranks 0, ngap, ... on
+ * each) and Nfft4GPRankestDefault (rankest.c:30-181: fill-distance / eigenvalue tolerance from
+ * subsamples, then FPS of the full data up to max_rank; perm receives the selected points), with the
+ * rankest struct's fields as arguments (reference defaults: max_rank 2000, nsample 500, nsample_r 5,
+ * full_tol 0.9).  kernel 0 Gaussian, 1 Matern-1/2; fkernel_params an nfft4gp_kernel.  The FPS passes,
+ * kernel matrices, Cholesky / inverse / eigenvalues (rocSOLVER) and Nystrom products (MFMA GEMM) run on
+ * the device; they consume rand() exactly as the reference does, so after the same srand() both pick the
+ * same subsamples.  A rank-k factor of a subsample that is not positive definite counts as error
+ * infinity (the reference continues on the partial factor).  Return the rank, -1 on error. */
+int Nfft4GPAmdRankestNysScaled(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int kernel, void *fkernel_params,
+                               int max_rank, int nsample, int nsample_r);
+int Nfft4GPAmdRankestDefault(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int kernel, void *fkernel_params,
+                             int max_rank, int nsample, int nsample_r, NFFT4GP_DOUBLE full_tol, int *perm);
+/* The rank and ordering step of Nfft4GPPrecondAFNSetup (afn.c:165-256) with max_k, perm_opt (0 random,
+ * 1 FPS) and nsamples as there: returns k and writes the full permutation (n entries, the k selected
+ * points first).  k == max_k: pass k and perm to Nfft4GPAmdAfnSetup (perm_opt 2); 0 < k < max_k: the
+ * reference builds a rank-k Nystrom instead (afn.c:287-296). */
+int Nfft4GPAmdAfnRankEstimate(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int max_k, int perm_opt,
+                              int nsamples, int kernel, void *fkernel_params, int *perm);
+
 /* ---- farthest point sampling (SRC/linearalg/ordering.c) -------------------------------------------
  * Nfft4GPSortFps with kFpsAlgorithmParallel1 (ordering.c:422-739): *k in: the number of points to select
  * (<= 0: all n), out: the number selected (fewer when the fill distance falls below tol); perm and dist

@@ -543,6 +543,43 @@ def expand_perm(perm, n):
     return np.concatenate([np.asarray(perm, dtype=np.int32), np.flatnonzero(~used).astype(np.int32)])
 
 
+class RankestStruct(C.Structure):
+    """rankest, SRC/linearalg/rankest.h:13-23."""
+    _fields_ = [
+        ("_nsample", C.c_int), ("_nsample_r", C.c_int), ("_max_rank", C.c_int), ("_full_tol", C.c_double),
+        ("_kernel_func", C.c_void_p), ("_kernel_str", C.c_void_p), ("_ordering_str", C.c_void_p), ("_perm", _ip),
+    ]
+
+
+def ref_rankest(data, params, max_rank, nsample=500, nsample_r=5, which="scaled", seed=None):
+    """Nfft4GPRankestNysScaled (rankest.c:354-391) or Nfft4GPRankestDefault (:132-181) of the reference on its
+    dense Gaussian kernel (params: an nfft4gp_kernel handle), via oracle/_ref; srand(seed) first when given.
+    Returns the rank (and, for "default", the selected points)."""
+    lib = ref_lib()
+    lib.Nfft4GPRankestStrCreate.restype = C.c_void_p
+    lib.Nfft4GPRankestStrFree.argtypes = [C.c_void_p]
+    fn = lib.Nfft4GPRankestNysScaled if which == "scaled" else lib.Nfft4GPRankestDefault
+    fn.argtypes = [C.c_void_p, _dp, C.c_int, C.c_int, C.c_int]
+    fn.restype = C.c_int
+    data = np.asfortranarray(data, dtype=np.float64)
+    n, d = data.shape
+    h = lib.Nfft4GPRankestStrCreate()
+    st = RankestStruct.from_address(h)
+    st._max_rank = max_rank
+    st._nsample = nsample
+    st._nsample_r = nsample_r
+    st._kernel_func = C.cast(lib.Nfft4GPKernelGaussianKernel, C.c_void_p).value
+    st._kernel_str = params
+    if seed is not None:
+        C.CDLL(None).srand(seed)
+    r = fn(h, _d(data), n, n, d)
+    perm = None
+    if which != "scaled":
+        perm = np.ctypeslib.as_array(st._perm, shape=(r,)).copy() if r > 0 else np.zeros(0, np.int32)
+    lib.Nfft4GPRankestStrFree(h)
+    return r if which == "scaled" else (r, perm)
+
+
 def ref_schur_params(data, perm, k, chol_K11, gauss_params):
     """Nfft4GPKernelSchurCombineKernelParamCreate (kernels.c:3496-3596, no gradient): the kernel of the
     Schur complement K22 - K21 K11^{-1} K12 the reference's AFN setup hands to FSAI (afn.c:473)."""

@@ -127,6 +127,11 @@ _SIGS = {
     "Nfft4GPAmdAfnSetup": (vp, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, vp]),
     "Nfft4GPAmdAfnInfo": (C.c_int, [vp, vp, vp, vp, vp, vp]),
     "Nfft4GPAmdSortFps": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, C.c_double, vp, vp]),
+    "Nfft4GPAmdRankestNysScaled": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int]),
+    "Nfft4GPAmdRankestDefault": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int,
+                                           C.c_double, vp]),
+    "Nfft4GPAmdAfnRankEstimate": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp,
+                                            vp]),
     "Nfft4GPAmdSetStream": (None, [vp]),
     "Nfft4GPAmdGetStream": (vp, []),
     "Nfft4GPAmdDeviceAvailable": (C.c_int, []),

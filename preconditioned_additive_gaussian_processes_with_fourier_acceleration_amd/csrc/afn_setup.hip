@@ -328,6 +328,281 @@ std::vector<int> expand_perm(const int* perm, int k, int n)
    return out;
 }
 
+
+// ---- rank estimation (rankest.c) ------------------------------------------------------------------
+
+__global__ void k_scale(double* __restrict__ x, size_t count, double a)
+{
+   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < count) x[i] *= a;
+}
+
+__global__ void k_add_diag_n(double* __restrict__ A, int n, double v)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) A[i + (size_t)i * n] += v;
+}
+
+__global__ void k_copy_block(const double* __restrict__ A, long long lda, int m, double* __restrict__ B)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
+   if (i < m) B[i + (size_t)j * m] = A[i + (size_t)j * lda];
+}
+
+// sum over the lower triangle (off-diagonal entries twice) of (A - B - shift I)^2 (B may be NULL):
+// dlansy('F', 'L')^2 of A - B - shift I, one workgroup, fixed order
+__global__ __launch_bounds__(1024) void k_sumsq_lower(const double* __restrict__ A, const double* __restrict__ B,
+                                                      double shift, int n, double* __restrict__ out)
+{
+   __shared__ double s[1024];
+   double acc = 0.0;
+   const size_t nn = (size_t)n * n;
+   for (size_t e = threadIdx.x; e < nn; e += 1024) {
+      const int i = (int)(e % n), j = (int)(e / n);
+      if (i < j) continue;
+      double v = A[e];
+      if (B) v -= B[e] + (i == j ? shift : 0.0);
+      acc += (i == j ? 1.0 : 2.0) * v * v;
+   }
+   s[threadIdx.x] = acc;
+   __syncthreads();
+   for (int w = 512; w > 0; w >>= 1) {
+      if (threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+      __syncthreads();
+   }
+   if (threadIdx.x == 0) *out = s[0];
+}
+
+// Nfft4GPRandPerm (utils.c:72-105): n draws of libc rand(), the indices of the k smallest (their order
+// within the k is the reference's quick-split's; here ascending by (draw, index) -- the sample is used
+// as a set)
+std::vector<int> rand_perm(int n, int k)
+{
+   std::vector<std::pair<double, int>> v(n);
+   for (int i = 0; i < n; i++) v[i] = {(double)rand(), i};
+   std::partial_sort(v.begin(), v.begin() + k, v.end());
+   std::vector<int> out(k);
+   for (int i = 0; i < k; i++) out[i] = v[i].second;
+   return out;
+}
+
+struct RankCtx {
+   const double* dX = nullptr;  // device, n x d column-major (ldim)
+   long long ldim = 0;
+   int n = 0, d = 0, kernel = 0;
+   double f = 1.0, l = 1.0, mu = 0.0;
+   hipStream_t s = nullptr;
+   double f2() const { return f * f; }
+   double inv() const { return kernel == 0 ? 1.0 / (2.0 * l * l) : 1.0 / l; }
+};
+
+// the subsample rows (device, n1 x d) of Nfft4GPSubData(data, RandPerm(n, n1)), scaled by `scale`
+int sample_points(const RankCtx& C, int n1, double scale, double* Xs)
+{
+   std::vector<int> rows = rand_perm(C.n, n1);
+   int* drows = nullptr;
+   if (dalloc(&drows, n1) || hipMemcpy(drows, rows.data(), sizeof(int) * n1, hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(drows);
+      return -1;
+   }
+   hipLaunchKernelGGL(k_gather_points, dim3((n1 + 255) / 256, C.d), dim3(256), 0, C.s, C.dX, C.ldim, n1, C.d, drows, Xs);
+   if (scale != 1.0)
+      hipLaunchKernelGGL(k_scale, dim3((unsigned)(((size_t)n1 * C.d + 255) / 256)), dim3(256), 0, C.s, Xs,
+                         (size_t)n1 * C.d, scale);
+   (void)hipStreamSynchronize(C.s);
+   (void)hipFree(drows);
+   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+double device_scalar(const double* d, hipStream_t s)
+{
+   double h = NAN;
+   if (hipMemcpyAsync(&h, d, sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+      return NAN;
+   return h;
+}
+
+// Nfft4GPRankestNysScaledEstimateRank (rankest.c:248-352)
+int nys_scaled_estimate(const RankCtx& C, int max_rank, int nsample)
+{
+   const int n = C.n, d = C.d;
+   const int n1 = std::min(nsample, n);
+   double *Xs = nullptr, *Xp = nullptr, *K0 = nullptr, *K11 = nullptr, *G = nullptr, *Gt = nullptr, *W = nullptr,
+          *Kn = nullptr, *dsum = nullptr;
+   int *dperm = nullptr, *dinfo = nullptr;
+   auto done = [&](int rc) {
+      (void)hipStreamSynchronize(C.s);
+      for (void* p : {(void*)Xs, (void*)Xp, (void*)K0, (void*)K11, (void*)G, (void*)Gt, (void*)W, (void*)Kn,
+                      (void*)dsum, (void*)dperm, (void*)dinfo})
+         (void)hipFree(p);
+      return rc;
+   };
+   const size_t nn = (size_t)n1 * n1;
+   if (dalloc(&Xs, (size_t)n1 * d) || dalloc(&Xp, (size_t)n1 * d) || dalloc(&K0, nn) || dalloc(&K11, nn) ||
+       dalloc(&G, nn) || dalloc(&Gt, nn) || dalloc(&W, nn) || dalloc(&Kn, nn) || dalloc(&dsum, 1) ||
+       dalloc(&dperm, n1) || dalloc(&dinfo, 1))
+      return done(-1);
+   // scale so that the sample's spacing resembles the full data's: (n1 / n)^(1/d)
+   if (sample_points(C, n1, pow((double)n1 / n, 1.0 / d), Xs)) return done(-1);
+   std::vector<int> perm(n1);
+   if (fps_device(Xs, n1, n1, d, n1, 0.0, perm.data(), nullptr, C.s) != n1) return done(-1);
+   if (hipMemcpy(dperm, perm.data(), sizeof(int) * n1, hipMemcpyHostToDevice) != hipSuccess) return done(-1);
+   hipLaunchKernelGGL(k_gather_points, dim3((n1 + 255) / 256, d), dim3(256), 0, C.s, Xs, (long long)n1, n1, d, dperm, Xp);
+   // K(perm, perm) without noise (rankest.c:307-309)
+   hipLaunchKernelGGL(k_kmat, dim3((n1 + 255) / 256, n1), dim3(256), 0, C.s, Xp, (long long)n1, n1, Xp, (long long)n1, n1,
+                      d, C.kernel, C.f2(), C.inv(), 0.0, 1, K0, (long long)n1);
+   hipLaunchKernelGGL(k_sumsq_lower, dim3(1), dim3(1024), 0, C.s, K0, nullptr, 0.0, n1, dsum);
+   double a_fro = sqrt(device_scalar(dsum, C.s));
+   const double nu = sqrt((double)n) * (nextafter(a_fro, a_fro + 1.0) - a_fro);  // rankest.c:318-322
+   // A_fro of K + nu I (rankest.c:323-329); K0 itself stays noise-free for K1 = K0(1:k, :)
+   hipLaunchKernelGGL(k_copy_block, dim3((n1 + 255) / 256, n1), dim3(256), 0, C.s, K0, (long long)n1, n1, Kn);
+   hipLaunchKernelGGL(k_add_diag_n, dim3((n1 + 255) / 256), dim3(256), 0, C.s, Kn, n1, nu);
+   hipLaunchKernelGGL(k_sumsq_lower, dim3(1), dim3(1024), 0, C.s, Kn, nullptr, 0.0, n1, dsum);
+   a_fro = sqrt(device_scalar(dsum, C.s));
+   const double tol = 0.1;
+   const int npoints = 50;  // NFFT4GP_RANKEST_NPOINTS
+   const int ngap = std::max(n1 / npoints, 1);
+   int rank = n1;
+   for (int i = 0; i < npoints; i++) {
+      // rankest.c:334: for i = 0 the reference's (size_t)(i - 1) * ngap wraps, and the int conversion of
+      // the huge double gives INT_MIN on x86, so only i >= 1 can stop here
+      if (i * ngap >= n1 || (i >= 1 && (long long)floor(((double)(i - 1) * ngap) * (double)n / n1) > 2LL * max_rank)) {
+         rank = (i - 1) * ngap;
+         break;
+      }
+      const int k = i * ngap;
+      double err;
+      if (k == 0) {
+         err = 1.0;
+      } else {
+         // Nfft4GPRankestNysError (rankest.c:183-240): K1 = K(perm[:k], perm), L = chol(K1(:, :k)),
+         // |L^{-1}K1)^T (L^{-1}K1) - (K + nu I)|_F / A_fro
+         hipLaunchKernelGGL(k_copy_block, dim3((k + 255) / 256, k), dim3(256), 0, C.s, K0, (long long)n1, k, K11);
+         const int info = chol_inverse_dev(K11, k, 0.0, G, Gt, dinfo, C.s);
+         if (info < 0) return done(-1);
+         if (info > 0) {
+            err = INFINITY;  // K11 not positive definite: the reference continues on a partial factor
+         } else {
+            if (gemm_f64(false, k, n1, k, G, k, K0, n1, W, k, C.s) || gram_tn(n1, n1, k, W, k, W, k, Kn, 0, C.s))
+               return done(-1);
+            hipLaunchKernelGGL(k_sumsq_lower, dim3(1), dim3(1024), 0, C.s, Kn, K0, nu, n1, dsum);
+            err = sqrt(device_scalar(dsum, C.s)) / a_fro;
+         }
+      }
+      if (err < tol) {
+         rank = k;
+         break;
+      }
+   }
+   return done((int)floor(rank * (double)n / n1));
+}
+
+// Nfft4GPRankestDefaultToleranceEstimation (rankest.c:30-130): returns h, *pk = the estimated rank
+double default_tolerance(const RankCtx& C, int nsamples, int* pk)
+{
+   const int n = C.n, d = C.d;
+   const int n1 = std::min(nsamples, n);
+   double *Xs = nullptr, *K = nullptr;
+   auto done = [&](double v) {
+      (void)hipStreamSynchronize(C.s);
+      (void)hipFree(Xs);
+      (void)hipFree(K);
+      return v;
+   };
+   if (dalloc(&Xs, (size_t)n1 * d) || dalloc(&K, (size_t)n1 * n1) || sample_points(C, n1, 1.0, Xs)) return done(NAN);
+   std::vector<int> perm(n1);
+   std::vector<double> dist(n1);
+   if (fps_device(Xs, n1, n1, d, n1, 0.0, perm.data(), dist.data(), C.s) != n1) return done(NAN);
+   // K of the sample with noise (kernels.c:1198) and its eigenvalues (dsyev 'N')
+   hipLaunchKernelGGL(k_kmat, dim3((n1 + 255) / 256, n1), dim3(256), 0, C.s, Xs, (long long)n1, n1, Xs, (long long)n1, n1,
+                      d, C.kernel, C.f2(), C.inv(), C.f2() * C.mu, 1, K, (long long)n1);
+   std::vector<double> eig;
+   if (sym_eigvals_dev(K, n1, eig, C.s)) return done(NAN);
+   const double tol = 0.41, tol2 = 0.2, tol3 = 1.1 * C.mu;
+   int rank = 0;
+   for (int i = n1 - 1; i >= 0; i--) {
+      if (eig[i] < tol3) break;
+      rank++;
+   }
+   const int rank2 = rank - 1;
+   while (rank > 1) {
+      rank--;
+      if ((dist[rank - 1] - dist[rank]) / dist[rank] > tol || dist[rank] <= (1.0 + tol2) * dist[rank2]) break;
+   }
+   if (pk) *pk = rank + 1;
+   return done(dist[rank]);
+}
+
+// Nfft4GPRankestNysScaled (rankest.c:354-391)
+int rankest_nys_scaled(const RankCtx& C, int max_rank, int nsample, int nsample_r)
+{
+   long long total = 0;
+   for (int i = 0; i < nsample_r; i++) {
+      const int r = nys_scaled_estimate(C, max_rank, nsample);
+      if (r < 0) return -1;
+      total += r;
+   }
+   int rank = (int)floor((double)total / nsample_r);
+   const int n1 = std::min(nsample, C.n);
+   const int ngap = std::max(n1 / 50, 1);
+   if (rank <= (int)floor(ngap * (double)C.n / n1)) rank = 0;  // "extra check needed" (rankest.c:380-385)
+   return rank;
+}
+
+// Nfft4GPRankestDefault (rankest.c:132-181): the rank and the FPS order it selected
+int rankest_default(const RankCtx& C, int max_rank, int nsample, int nsample_r, double full_tol, std::vector<int>& perm)
+{
+   int est = 0, total = 0;
+   double tol = default_tolerance(C, nsample, &est);
+   if (std::isnan(tol)) return -1;
+   total += est;
+   for (int i = 1; i < nsample_r; i++) {
+      const double t1 = default_tolerance(C, nsample, &est);
+      if (std::isnan(t1)) return -1;
+      tol += t1;
+      total += est;
+   }
+   tol /= nsample_r;
+   const bool full = total / (double)((long long)nsample * nsample_r) > full_tol;
+   const int kmax = std::min(max_rank, C.n);
+   perm.assign(kmax, 0);
+   const int rank = fps_device(C.dX, C.ldim, C.n, C.d, kmax, full ? 0.0 : tol, perm.data(), nullptr, C.s);
+   if (rank < 0) return -1;
+   perm.resize(rank);
+   return rank;
+}
+
+int rank_ctx(RankCtx& C, const double* data, int n, int ldim, int d, int kernel, const void* params, double** owned)
+{
+   const nfft4gp_kernel* kp = (const nfft4gp_kernel*)params;
+   *owned = nullptr;
+   if (!data || !kp || n <= 0 || ldim < n || d <= 0 || d > kFpsMaxDims) {
+      fprintf(stderr, "nfft4gp_amd: rank estimation needs data (ldim >= n, d <= %d) and kernel parameters\n",
+              kFpsMaxDims);
+      return -1;
+   }
+   C.n = n;
+   C.d = d;
+   C.ldim = ldim;
+   C.kernel = kernel ? 1 : 0;
+   C.f = kp->_params[0];
+   C.l = kp->_params[1];
+   C.mu = kp->_noise_level;
+   C.s = current_stream();
+   if (is_device_ptr(data)) {
+      C.dX = data;
+      return 0;
+   }
+   if (dalloc(owned, (size_t)ldim * d) ||
+       hipMemcpy(*owned, data, sizeof(double) * (size_t)ldim * d, hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(*owned);
+      *owned = nullptr;
+      return -1;
+   }
+   C.dX = *owned;
+   return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -459,6 +734,71 @@ void* Nfft4GPAmdAfnSetup(const double* data, int n, int ldim, int d, int k, int 
       return nullptr;  // afn_create_device released the factors and S
    }
    return A;
+}
+
+
+int Nfft4GPAmdRankestNysScaled(const double* data, int n, int ldim, int d, int kernel, void* fkernel_params,
+                               int max_rank, int nsample, int nsample_r)
+{
+   if (!need_device("Nfft4GPAmdRankestNysScaled")) return -1;
+   RankCtx C;
+   double* owned = nullptr;
+   if (rank_ctx(C, data, n, ldim, d, kernel, fkernel_params, &owned)) return -1;
+   const int r = rankest_nys_scaled(C, max_rank, nsample, nsample_r);
+   (void)hipFree(owned);
+   return r;
+}
+
+int Nfft4GPAmdRankestDefault(const double* data, int n, int ldim, int d, int kernel, void* fkernel_params,
+                             int max_rank, int nsample, int nsample_r, double full_tol, int* perm)
+{
+   if (!need_device("Nfft4GPAmdRankestDefault")) return -1;
+   RankCtx C;
+   double* owned = nullptr;
+   if (rank_ctx(C, data, n, ldim, d, kernel, fkernel_params, &owned)) return -1;
+   std::vector<int> p;
+   const int r = rankest_default(C, max_rank, nsample, nsample_r, full_tol, p);
+   (void)hipFree(owned);
+   if (r > 0 && perm) std::copy(p.begin(), p.end(), perm);
+   return r;
+}
+
+int Nfft4GPAmdAfnRankEstimate(const double* data, int n, int ldim, int d, int max_k, int perm_opt, int nsamples,
+                              int kernel, void* fkernel_params, int* perm)
+{
+   if (!need_device("Nfft4GPAmdAfnRankEstimate")) return -1;
+   if (!perm) return -1;
+   max_k = std::min(max_k, n);  // afn.c:167
+   if (max_k <= 0) {            // afn.c:245-256: the predefined rank -max_k, natural order
+      for (int i = 0; i < n; i++) perm[i] = i;
+      return std::min(-max_k, n);
+   }
+   RankCtx C;
+   double* owned = nullptr;
+   if (rank_ctx(C, data, n, ldim, d, kernel, fkernel_params, &owned)) return -1;
+   int k = -1;
+   std::vector<int> sel;
+   const int rank = rankest_nys_scaled(C, max_k, nsamples, 5);  // _nsample_r = 5 (rankest.c:11)
+   if (rank >= 0) {
+      if (rank >= max_k) {  // afn.c:193-219: not low rank
+         k = max_k;
+         if (perm_opt == 1) {
+            sel.assign(k, 0);
+            k = fps_device(C.dX, C.ldim, n, d, k, 0.0, sel.data(), nullptr, C.s);
+            if (k >= 0) sel.resize(k);
+         } else {
+            sel = rand_perm(n, k);
+         }
+      } else {  // afn.c:220-242
+         k = rankest_default(C, max_k, nsamples, 5, 0.9, sel);
+         if (k == max_k && perm_opt == 0) sel = rand_perm(n, k);
+      }
+   }
+   (void)hipFree(owned);
+   if (k < 0) return -1;
+   const std::vector<int> full = expand_perm(sel.data(), (int)sel.size(), n);
+   std::copy(full.begin(), full.end(), perm);
+   return k;
 }
 
 }  // extern "C"

@@ -217,6 +217,11 @@ void bhat_nd(int kind, int d, double c, std::vector<double>& bhat);  // window.c
 // k x k lower Cholesky of A (+ shift I) and its inverse (rocSOLVER potrf/trtri, host fallback): G = L^{-1}
 // (lower, cleaned; may be NULL), Gt = L^{-T}.  A is overwritten.  >0: not positive definite (nystrom.hip)
 int chol_inverse_dev(double* A, int k, double shift, double* G, double* Gt, int* d_info, hipStream_t s);
+// C (M x N) = A^T B, A K x M (lda), B K x N (ldb), split over K with a fixed-order sum (nystrom.hip)
+int gram_tn(int M, int N, int K, const double* A, long long lda, const double* B, long long ldb, double* C, int sym,
+            hipStream_t s);
+// ascending eigenvalues of a symmetric device matrix (rocSOLVER dsyevd, no vectors; nystrom.hip)
+int sym_eigvals_dev(double* A, int n, std::vector<double>& w, hipStream_t s);
 // FSAI of a kernel matrix from device coordinates (fsai_setup.hip), host CSR out; dW: Schur kernel
 int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, int kernel, double f, double l, double mu,
                     const double* dW, int kw, int require_grad, std::vector<int>& ia, std::vector<int>& ja,

@@ -534,6 +534,39 @@ int sym_eig_host(const std::vector<double>& A, int n, std::vector<double>& w, st
    return sym_eig(A, n, w, V);
 }
 
+// eigenvalues (ascending) of the symmetric n x n device matrix A (lower triangle read, A overwritten):
+// rocSOLVER dsyevd without vectors; the host tridiagonal QL when rocSOLVER did not load
+int sym_eigvals_dev(double* A, int n, std::vector<double>& w, hipStream_t s)
+{
+   w.assign(n, 0.0);
+   RocSolver& R = rocsolver();
+   if (R.ok) {
+      double *d_w = nullptr, *d_e = nullptr;
+      int* d_info = nullptr;
+      int info = 0;
+      int rc = -1;
+      if (dalloc(&d_w, n) == 0 && dalloc(&d_e, n) == 0 && dalloc(&d_info, 1) == 0) {
+         R.set_stream(R.h, s);
+         if (R.syevd(R.h, rocblas_evect_none, rocblas_fill_lower, n, A, n, d_w, d_e, d_info) == rocblas_status_success &&
+             hipMemcpyAsync(w.data(), d_w, sizeof(double) * n, hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipMemcpyAsync(&info, d_info, sizeof(int), hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipStreamSynchronize(s) == hipSuccess)
+            rc = info ? -1 : 0;
+      }
+      (void)hipFree(d_w);
+      (void)hipFree(d_e);
+      (void)hipFree(d_info);
+      return rc;
+   }
+   std::vector<double> h((size_t)n * n), V;
+   if (hipMemcpyAsync(h.data(), A, sizeof(double) * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess)
+      return -1;
+   for (int j = 0; j < n; j++)
+      for (int i = 0; i < j; i++) h[i + (size_t)j * n] = h[j + (size_t)i * n];
+   return sym_eig(h, n, w, V);
+}
+
 // L^{-1} of chol(A) (lower) in place; returns 0 or the failing column + 1
 int chol_inverse_host(std::vector<double>& A, int k)
 {

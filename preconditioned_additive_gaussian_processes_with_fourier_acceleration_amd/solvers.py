@@ -211,6 +211,24 @@ class AfnPrecond(_Apply):
         return self.k, perm, (ia, ja, aa)
 
 
+def afn_rank_estimate(X, max_k: int, f: float, l: float, mu: float, perm_opt: str = "fps", nsamples: int = 500,
+                      kernel: int = 0):
+    """Nfft4GPAmdAfnRankEstimate -- the rank / ordering step of Nfft4GPPrecondAFNSetup (afn.c:165-256) on
+    the GPU: (k, perm).  k == max_k: build ``AfnPrecond.setup(X, k, ..., perm_opt="perm", perm=perm)``;
+    0 < k < max_k: the reference switches to a rank-k Nystrom (afn.c:287-296).  Draws libc rand()."""
+    L = _lib.lib()
+    X = np.asfortranarray(np.asarray(X, dtype=np.float64))
+    n, d = X.shape
+    perm = np.zeros(n, np.int32)
+    params = _lib.kernel_params(f, l, mu, n)
+    k = L.Nfft4GPAmdAfnRankEstimate(X.ctypes.data, n, n, d, int(max_k), {"random": 0, "fps": 1}[perm_opt],
+                                    int(nsamples), int(kernel), params, perm.ctypes.data)
+    L.Nfft4GPKernelParamFree(params)
+    if k < 0:
+        raise RuntimeError("Nfft4GPAmdAfnRankEstimate failed (see stderr)")
+    return k, perm
+
+
 def sort_fps(X, k: int, tol: float = 0.0):
     """Nfft4GPAmdSortFps -- Nfft4GPSortFps with kFpsAlgorithmParallel1 (ordering.c:422-739) on the GPU:
     (selected points, fill distances).  X: n x d numpy array or a torch GPU tensor of shape (d, n)
