@@ -32,6 +32,7 @@
 
 #include "callbacks.hpp"
 #include "internal.h"
+#include "kernel_eval.hpp"
 
 using namespace nfft4gp_amd;
 
@@ -235,28 +236,17 @@ __global__ __launch_bounds__(kFpsThreads) void k_fps_step(const double* __restri
    st->ticket = 0u;
 }
 
-// out[i + j*ldo] = K(A_i, B_j) (+ f^2 mu on the diagonal when diag_noise), A: ma points (lda), B: nb
-// points (ldb), both column-major with d features.  The plain Gaussian / Matern-1/2 of kernels.c:680-1289,
-// :2390-3033 (f^2 exp(-r^2 / 2 l^2), f^2 exp(-r / l)).
-__global__ __launch_bounds__(256) void k_kmat(const double* __restrict__ A, long long lda, int ma,
-                                              const double* __restrict__ B, long long ldb, int nb, int d, int kernel,
-                                              double f2, double inv, double noise, int diag_noise,
-                                              double* __restrict__ out, long long ldo)
+// out[i + j*ldo] = K(x_{row0+i}, x_{col0+j}) for i < m, j < gridDim.y over the kernel coordinates X (ld
+// ldx); the noise goes on entries where the two are one point when diag_noise (kernel_eval.hpp)
+__global__ __launch_bounds__(256) void k_kmat(const double* __restrict__ X, long long ldx, int row0, int m, int col0,
+                                              KernelParams P, int diag_noise, double* __restrict__ out, long long ldo)
 {
    const int i = blockIdx.x * 256 + threadIdx.x;
    const int j = blockIdx.y;
-   if (i >= ma) return;
-   double s = 0.0;
-   for (int c = 0; c < d; c++) {
-      const double t = A[(size_t)c * lda + i] - B[(size_t)c * ldb + j];
-      s = fma(t, t, s);
-   }
-   double v;
-   if (diag_noise && i == j)
-      v = f2 + noise;
-   else
-      v = f2 * exp(-(kernel == 0 ? s : sqrt(s)) * inv);
-   out[(size_t)j * ldo + i] = v;
+   if (i >= m) return;
+   double K, dK[3];
+   kern_pair(P, X, ldx, row0 + i, col0 + j, diag_noise && row0 + i == col0 + j, K, dK);
+   out[(size_t)j * ldo + i] = K;
 }
 
 __global__ void k_gather_points(const double* __restrict__ X, long long ldim, int n, int d, const int* __restrict__ perm,
@@ -392,8 +382,15 @@ struct RankCtx {
    int n = 0, d = 0, kernel = 0;
    double f = 1.0, l = 1.0, mu = 0.0;
    hipStream_t s = nullptr;
-   double f2() const { return f * f; }
-   double inv() const { return kernel == 0 ? 1.0 / (2.0 * l * l) : 1.0 / l; }
+   KernelParams params(int dims, double noise) const
+   {
+      KernelSpec K;
+      K.kernel = kernel;
+      K.f = f;
+      K.l = l;
+      K.mu = noise;
+      return kernel_params_of(K, dims);
+   }
 };
 
 // the subsample rows (device, n1 x d) of Nfft4GPSubData(data, RandPerm(n, n1)), scaled by `scale`
@@ -449,8 +446,8 @@ int nys_scaled_estimate(const RankCtx& C, int max_rank, int nsample)
    if (hipMemcpy(dperm, perm.data(), sizeof(int) * n1, hipMemcpyHostToDevice) != hipSuccess) return done(-1);
    hipLaunchKernelGGL(k_gather_points, dim3((n1 + 255) / 256, d), dim3(256), 0, C.s, Xs, (long long)n1, n1, d, dperm, Xp);
    // K(perm, perm) without noise (rankest.c:307-309)
-   hipLaunchKernelGGL(k_kmat, dim3((n1 + 255) / 256, n1), dim3(256), 0, C.s, Xp, (long long)n1, n1, Xp, (long long)n1, n1,
-                      d, C.kernel, C.f2(), C.inv(), 0.0, 1, K0, (long long)n1);
+   hipLaunchKernelGGL(k_kmat, dim3((n1 + 255) / 256, n1), dim3(256), 0, C.s, Xp, (long long)n1, 0, n1, 0,
+                      C.params(d, 0.0), 1, K0, (long long)n1);
    hipLaunchKernelGGL(k_sumsq_lower, dim3(1), dim3(1024), 0, C.s, K0, nullptr, 0.0, n1, dsum);
    double a_fro = sqrt(device_scalar(dsum, C.s));
    const double nu = sqrt((double)n) * (nextafter(a_fro, a_fro + 1.0) - a_fro);  // rankest.c:318-322
@@ -514,8 +511,8 @@ double default_tolerance(const RankCtx& C, int nsamples, int* pk)
    std::vector<double> dist(n1);
    if (fps_device(Xs, n1, n1, d, n1, 0.0, perm.data(), dist.data(), C.s) != n1) return done(NAN);
    // K of the sample with noise (kernels.c:1198) and its eigenvalues (dsyev 'N')
-   hipLaunchKernelGGL(k_kmat, dim3((n1 + 255) / 256, n1), dim3(256), 0, C.s, Xs, (long long)n1, n1, Xs, (long long)n1, n1,
-                      d, C.kernel, C.f2(), C.inv(), C.f2() * C.mu, 1, K, (long long)n1);
+   hipLaunchKernelGGL(k_kmat, dim3((n1 + 255) / 256, n1), dim3(256), 0, C.s, Xs, (long long)n1, 0, n1, 0,
+                      C.params(d, C.mu), 1, K, (long long)n1);
    std::vector<double> eig;
    if (sym_eigvals_dev(K, n1, eig, C.s)) return done(NAN);
    const double tol = 0.41, tol2 = 0.2, tol3 = 1.1 * C.mu;
@@ -636,26 +633,29 @@ void* Nfft4GPAmdAfnSetup(const double* data, int n, int ldim, int d, int k, int 
                          int schur_lfil, int kernel, void* fkernel_params)
 {
    if (!need_device("Nfft4GPAmdAfnSetup")) return nullptr;
-   const nfft4gp_kernel* kp = (const nfft4gp_kernel*)fkernel_params;
-   if (!data || !kp || n <= 0 || ldim < n || d <= 0 || k < 0 || k > n || perm_opt < 0 || perm_opt > 2 ||
+   if (!data || !fkernel_params || n <= 0 || ldim < n || d <= 0 || k < 0 || k > n || perm_opt < 0 || perm_opt > 2 ||
        (perm_opt == 2 && !perm)) {
       fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup needs data (ldim >= n), kernel parameters, 0 <= k <= n, "
                       "perm_opt 0 (identity), 1 (FPS) or 2 (perm given)\n");
       return nullptr;
    }
-   kernel = kernel ? 1 : 0;
-   const double f = kp->_params[0], l = kp->_params[1], mu = kp->_noise_level;
-   const double f2 = f * f, inv = (kernel == 0) ? 1.0 / (2.0 * l * l) : 1.0 / l;
+   // the kernel: plain (data's coordinates) or this library's additive handle (its window buffer)
+   KernelSpec K;
+   double* dXk = nullptr;
+   const int additive = kernel_spec_of(fkernel_params, nullptr, kernel, n, K, &dXk);
+   if (additive < 0) return nullptr;
+   const int D = additive ? (K.nw - 1) * K.dw + K.last_dw : d;  // kernel coordinates per point
    hipStream_t s = current_stream();
    const int n2 = n - k;
-   double *dX = nullptr, *Xp = nullptr, *K11 = nullptr, *G = nullptr, *Gt = nullptr, *K12 = nullptr, *W = nullptr;
+   double *dX = nullptr, *Xp = nullptr, *Xkp = nullptr, *K11 = nullptr, *G = nullptr, *Gt = nullptr, *K12 = nullptr,
+          *W = nullptr;
    int *dperm = nullptr, *dinfo = nullptr;
    void* S = nullptr;
    auto fail = [&](const char* what) -> void* {
       if (what) fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: %s failed\n", what);
       (void)hipStreamSynchronize(s);
-      for (void* p : {(void*)dX, (void*)Xp, (void*)K11, (void*)G, (void*)Gt, (void*)K12, (void*)W, (void*)dperm,
-                      (void*)dinfo})
+      for (void* p : {(void*)dX, (void*)Xp, (void*)Xkp, (void*)dXk, (void*)K11, (void*)G, (void*)Gt, (void*)K12,
+                      (void*)W, (void*)dperm, (void*)dinfo})
          (void)hipFree(p);
       if (S) Nfft4GPAmdFsaiFree(S);
       return nullptr;
@@ -681,12 +681,22 @@ void* Nfft4GPAmdAfnSetup(const double* data, int n, int ldim, int d, int k, int 
        dalloc(&Xp, (size_t)n * d))
       return fail("allocation");
    hipLaunchKernelGGL(k_gather_points, dim3((n + 255) / 256, d), dim3(256), 0, s, dX, (long long)ldim, n, d, dperm, Xp);
+   if (additive) {
+      if (dalloc(&Xkp, (size_t)n * D)) return fail("allocation");
+      hipLaunchKernelGGL(k_gather_points, dim3((n + 255) / 256, D), dim3(256), 0, s, dXk, (long long)n, n, D, dperm,
+                         Xkp);
+   }
+   const double* Xk = additive ? Xkp : Xp;  // kernel coordinates in the permuted order, ld n
+   KernelSpec Kp = K;
+   Kp.Xk = additive ? Xkp : nullptr;
+   Kp.ldk = n;
+   const KernelParams P = kernel_params_of(Kp, d);
    const size_t kk = (size_t)k * k;
    if (k > 0) {
       // A11 = K(X1) + noise; L11^{-1} (afn.c:425-428: AfnPrecondCholSetupWithKernel)
       if (dalloc(&K11, kk) || dalloc(&G, kk) || dalloc(&Gt, kk) || dalloc(&dinfo, 1)) return fail("allocation");
-      hipLaunchKernelGGL(k_kmat, dim3((k + 255) / 256, k), dim3(256), 0, s, Xp, (long long)n, k, Xp, (long long)n, k,
-                         d, kernel, f2, inv, f2 * mu, 1, K11, (long long)k);
+      hipLaunchKernelGGL(k_kmat, dim3((k + 255) / 256, k), dim3(256), 0, s, Xk, (long long)n, 0, k, 0, P, 1, K11,
+                         (long long)k);
       const int info = chol_inverse_dev(K11, k, 0.0, G, Gt, dinfo, s);
       if (info > 0) {
          fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: K11 is not positive definite (column %d)\n", info);
@@ -699,13 +709,14 @@ void* Nfft4GPAmdAfnSetup(const double* data, int n, int ldim, int d, int k, int 
       if (dalloc(&K12, (size_t)k * n2) || dalloc(&W, (size_t)k * n2)) return fail("allocation");
       for (int j0 = 0; j0 < n2; j0 += 65535) {
          const int nb = std::min(65535, n2 - j0);
-         hipLaunchKernelGGL(k_kmat, dim3((k + 255) / 256, nb), dim3(256), 0, s, Xp, (long long)n, k, Xp + k + j0,
-                            (long long)n, nb, d, kernel, f2, inv, 0.0, 0, K12 + (size_t)j0 * k, (long long)k);
+         hipLaunchKernelGGL(k_kmat, dim3((k + 255) / 256, nb), dim3(256), 0, s, Xk, (long long)n, 0, k, k + j0, P, 0,
+                            K12 + (size_t)j0 * k, (long long)k);
       }
       if (gemm_f64(false, k, n2, k, G, k, K12, k, W, k, s)) return fail("gemm");
    }
    if (n2 > 0) {
-      // FSAI of the Schur complement on X2 (afn.c:445-473)
+      // FSAI of the Schur complement on X2 (afn.c:445-473): KNN on the points' coordinates, values of the
+      // Schur-complement kernel on the kernel coordinates
       std::vector<int> ia, ja;
       std::vector<double> aa, da;
       double* X2 = nullptr;
@@ -716,8 +727,9 @@ void* Nfft4GPAmdAfnSetup(const double* data, int n, int ldim, int d, int k, int 
             (void)hipFree(X2);
             return fail("copy");
          }
-      const int rc = fsai_kernel_csr(X2, n2, n2, d, schur_lfil, kernel, f, l, mu, W, k > 0 ? k : 0, 0, ia, ja, aa, da,
-                                     s);
+      KernelSpec K2 = Kp;
+      K2.Xk = additive ? Xkp + k : nullptr;  // column c of the last n2 points: Xkp + c*n + k + i
+      const int rc = fsai_kernel_csr(X2, n2, n2, d, schur_lfil, K2, W, k > 0 ? k : 0, 0, ia, ja, aa, da, s);
       (void)hipStreamSynchronize(s);
       (void)hipFree(X2);
       if (rc) return fail("Schur-complement FSAI");
@@ -725,8 +737,8 @@ void* Nfft4GPAmdAfnSetup(const double* data, int n, int ldim, int d, int k, int 
       if (!S) return fail("FSAI upload");
    }
    (void)hipStreamSynchronize(s);
-   for (void* p : {(void*)dX, (void*)Xp, (void*)K11, (void*)W, (void*)dinfo}) (void)hipFree(p);
-   dX = Xp = K11 = W = nullptr;
+   for (void* p : {(void*)dX, (void*)Xp, (void*)Xkp, (void*)dXk, (void*)K11, (void*)W, (void*)dinfo}) (void)hipFree(p);
+   dX = Xp = Xkp = dXk = K11 = W = nullptr;
    dinfo = nullptr;
    void* A = afn_create_device(n, k, dperm, G, Gt, K12, S);
    if (!A) {

@@ -38,6 +38,7 @@
 
 #include "callbacks.hpp"
 #include "internal.h"
+#include "kernel_eval.hpp"
 
 using namespace nfft4gp_amd;
 
@@ -392,31 +393,6 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn_bounded(const double* __res
    }
 }
 
-struct KernelParams {
-   int kernel;  // 0 Gaussian, 1 Matern-1/2
-   double f2, inv, mu;
-   double df_scale;  // 2/f
-   double dl_scale;  // f^2 / l^3 (Gaussian) or f^2 / l^2 (Matern)
-};
-
-// K entry from the squared distance (off-diagonal) and the three derivative entries (fsai.c:530 dK_a)
-__device__ __forceinline__ void kern_entry(const KernelParams& P, double s, bool diag, double& K, double* dK)
-{
-   if (diag) {
-      K = P.f2 + P.f2 * P.mu;  // f^2 + noise_level (kernels.c:695)
-      dK[0] = P.df_scale * K;
-      dK[1] = 0.0;
-      dK[2] = P.f2;
-      return;
-   }
-   const double r = (P.kernel == 0) ? s : sqrt(s);
-   const double e = exp(-r * P.inv);
-   K = P.f2 * e;
-   dK[0] = P.df_scale * K;
-   dK[1] = P.dl_scale * r * e;
-   dK[2] = 0.0;
-}
-
 // In place on the wave's LDS vector b: b = L^{-1} b (trans = 0) or L^{-T} b (trans = 1), L lower in A.
 __device__ void wave_trsv(double (*A)[kFsaiMaxK + 1], int k, double* b, int trans)
 {
@@ -444,7 +420,7 @@ __device__ void wave_trsv(double (*A)[kFsaiMaxK + 1], int k, double* b, int tran
 // setup (Nfft4GPKernelSchurCombineKernel, kernels.c:3599-3760, with W = L11^{-1} K12), staged through LDS
 // kSchurChunk rows of W at a time so each row reads its lfil columns of W once.
 constexpr int kSchurChunk = 32;
-__global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, int ldim, int d,
+__global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, long long ldim,
                                                   const int* __restrict__ ia, const int* __restrict__ ja,
                                                   KernelParams P, const double* __restrict__ W, int kw, int grad,
                                                   int nnz, double* __restrict__ aa, double* __restrict__ da)
@@ -463,13 +439,8 @@ __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, 
    for (int e = lane; e < k * k; e += 64) {
       const int r = e % k, c = e / k;
       if (c > r) continue;
-      double s = 0.0;
-      for (int dd = 0; dd < d; dd++) {
-         const double t = X[(size_t)dd * ldim + idx[r]] - X[(size_t)dd * ldim + idx[c]];
-         s = fma(t, t, s);
-      }
       double K, dK[3];
-      kern_entry(P, s, r == c, K, dK);
+      kern_pair(P, X, ldim, idx[r], idx[c], r == c, K, dK);
       A[r][c] = K;
    }
    __syncthreads();
@@ -521,13 +492,8 @@ __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, 
       if (lane < k) {
          double acc = 0.0;
          for (int c = 0; c < k; c++) {
-            double s = 0.0;
-            for (int dd = 0; dd < d; dd++) {
-               const double t = X[(size_t)dd * ldim + idx[lane]] - X[(size_t)dd * ldim + idx[c]];
-               s = fma(t, t, s);
-            }
             double K, dK[3];
-            kern_entry(P, s, lane == c, K, dK);
+            kern_pair(P, X, ldim, idx[lane], idx[c], lane == c, K, dK);
             acc = fma(dK[g], a[c], acc);
          }
          u[lane] = -acc;
@@ -783,11 +749,50 @@ double diag_sum(PrecondFsaiAmd* F, const double* num, hipStream_t s)
 
 namespace nfft4gp_amd {
 
+int additive_buffer_info(void* str, const double** xw, int* n, int* nw, int* dw, int* skip_last, int* kernel);
+
+// The kernel a setup evaluates: this library's additive NFFT handle as fkernel_params gives the dense
+// additive kernel of its gathered window buffer (uploaded to *owned), anything else the plain kernel of
+// the points with _params / _noise_level of the nfft4gp_kernel.  The kernel type comes from fkernel
+// when it is one of this library's setup functions, else from `kernel`.  Returns 1 (additive), 0
+// (plain) or -1.
+int kernel_spec_of(void* fkernel_params, func_kernel fkernel, int kernel, int n, KernelSpec& K, double** owned)
+{
+   *owned = nullptr;
+   const nfft4gp_kernel* kp = (const nfft4gp_kernel*)fkernel_params;
+   if (!kp) return -1;
+   K.kernel = kernel ? 1 : 0;
+   if (fkernel == &Nfft4GPNFFTAdditiveKernelGaussianKernel) K.kernel = 0;
+   else if (fkernel == &Nfft4GPNFFTAdditiveKernelMatern12Kernel) K.kernel = 1;
+   K.f = kp->_params[0];
+   K.l = kp->_params[1];
+   K.mu = kp->_noise_level;
+   K.Xk = nullptr;
+   const double* xw = nullptr;
+   int nn = 0, nw = 0, dw = 0, skip = 0, pk = -1;
+   if (additive_buffer_info(fkernel_params, &xw, &nn, &nw, &dw, &skip, &pk)) return 0;
+   if (nn != n || nw <= 0 || dw <= 0 || skip >= dw) {
+      fprintf(stderr, "nfft4gp_amd: the additive handle holds %d points, the setup got %d\n", nn, n);
+      return -1;
+   }
+   if (fkernel != &Nfft4GPNFFTAdditiveKernelGaussianKernel && fkernel != &Nfft4GPNFFTAdditiveKernelMatern12Kernel &&
+       pk >= 0)
+      K.kernel = pk;
+   const size_t D = (size_t)(nw - 1) * dw + (dw - skip);
+   if (upload(owned, xw, D * (size_t)n)) return -1;
+   K.Xk = *owned;
+   K.ldk = n;
+   K.nw = nw;
+   K.dw = dw;
+   K.last_dw = dw - skip;
+   return 1;
+}
+
 // The FSAI of a kernel matrix (fsai.c:314-673) from device coordinates: KNN pattern, per-row values (and
 // gradients), copied to host CSR.  dW (kw x n, optional): the Schur-complement kernel of the AFN setup.
-int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, int kernel, double f, double l, double mu,
-                    const double* dW, int kw, int require_grad, std::vector<int>& hia, std::vector<int>& hja,
-                    std::vector<double>& haa, std::vector<double>& hda, hipStream_t s)
+int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const KernelSpec& Ks, const double* dW, int kw,
+                    int require_grad, std::vector<int>& hia, std::vector<int>& hja, std::vector<double>& haa,
+                    std::vector<double>& hda, hipStream_t s)
 {
    if (n <= 0 || ldim < n || d <= 0 || d > kMaxDims || lfil < 1 || lfil > kFsaiMaxK || (dW && kw <= 0)) {
       fprintf(stderr, "nfft4gp_amd: FSAI setup needs 1 <= lfil <= %d and at most %d features\n", kFsaiMaxK,
@@ -846,15 +851,11 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, int kern
       (void)hipFree(dfail);
       knn_fallback_rows = nfail;
    }
-   KernelParams P;
-   P.kernel = kernel;
-   P.f2 = f * f;
-   P.inv = (kernel == 0) ? 1.0 / (2.0 * l * l) : 1.0 / l;
-   P.mu = mu;
-   P.df_scale = 2.0 / f;
-   P.dl_scale = (kernel == 0) ? P.f2 / (l * l * l) : P.f2 / (l * l);
-   hipLaunchKernelGGL(k_fsai_rows, dim3(n), dim3(64), 0, s, dX, ldim, d, dia, dja, P, dW, kw, require_grad ? 1 : 0,
-                      nnz, daa, dda);
+   const KernelParams P = kernel_params_of(Ks, d);
+   const double* Xk = Ks.Xk ? Ks.Xk : dX;
+   const long long ldk = Ks.Xk ? Ks.ldk : ldim;
+   hipLaunchKernelGGL(k_fsai_rows, dim3(n), dim3(64), 0, s, Xk, ldk, dia, dja, P, dW, kw, require_grad ? 1 : 0, nnz,
+                      daa, dda);
    haa.assign((size_t)nnz, 0.0);
    hda.assign(require_grad ? 3 * (size_t)nnz : 0, 0.0);
    if (hipGetLastError() != hipSuccess ||
@@ -901,27 +902,27 @@ int Nfft4GPAmdPrecondFsaiSetupWithKernel(double* data, int n, int ldim, int d, f
 {
    PrecondFsaiAmd* F = (PrecondFsaiAmd*)vfsai_mat;
    if (!F || !need_device("Nfft4GPAmdPrecondFsaiSetupWithKernel")) return -1;
-   const nfft4gp_kernel* kp = (const nfft4gp_kernel*)fkernel_params;
-   if (!kp || !data || n <= 0 || ldim < n || d <= 0) {
+   if (!fkernel_params || !data || n <= 0 || ldim < n || d <= 0) {
       fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondFsaiSetupWithKernel needs data and kernel parameters\n");
       return -1;
    }
-   int kernel = F->kernel;
-   if (fkernel == &Nfft4GPNFFTAdditiveKernelGaussianKernel) kernel = 0;
-   else if (fkernel == &Nfft4GPNFFTAdditiveKernelMatern12Kernel) kernel = 1;
+   KernelSpec K;
+   double* dXk = nullptr;
+   if (kernel_spec_of(fkernel_params, fkernel, F->kernel, n, K, &dXk) < 0) return -1;
    hipStream_t s = current_stream();
    double* dX = nullptr;
    if (upload(&dX, (const double*)nullptr, (size_t)ldim * d) ||
        hipMemcpy(dX, data, sizeof(double) * (size_t)ldim * d, hipMemcpyHostToDevice) != hipSuccess) {
       (void)hipFree(dX);
+      (void)hipFree(dXk);
       return -1;
    }
    std::vector<int> hia, hja;
    std::vector<double> haa, hda;
-   const int rc = fsai_kernel_csr(dX, n, ldim, d, F->lfil, kernel, kp->_params[0], kp->_params[1], kp->_noise_level,
-                                  nullptr, 0, require_grad, hia, hja, haa, hda, s);
+   const int rc = fsai_kernel_csr(dX, n, ldim, d, F->lfil, K, nullptr, 0, require_grad, hia, hja, haa, hda, s);
    (void)hipStreamSynchronize(s);
    (void)hipFree(dX);
+   (void)hipFree(dXk);
    if (rc) return -1;
    return fsai_load(F, n, hia.data(), hja.data(), haa.data(), require_grad ? hda.data() : nullptr);
 }

@@ -222,10 +222,24 @@ int gram_tn(int M, int N, int K, const double* A, long long lda, const double* B
             hipStream_t s);
 // ascending eigenvalues of a symmetric device matrix (rocSOLVER dsyevd, no vectors; nystrom.hip)
 int sym_eigvals_dev(double* A, int n, std::vector<double>& w, hipStream_t s);
-// FSAI of a kernel matrix from device coordinates (fsai_setup.hip), host CSR out; dW: Schur kernel
-int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, int kernel, double f, double l, double mu,
-                    const double* dW, int kw, int require_grad, std::vector<int>& ia, std::vector<int>& ja,
-                    std::vector<double>& aa, std::vector<double>& da, hipStream_t s);
+// the kernel of a preconditioner setup: plain Gaussian / Matern-1/2 of the points' coordinates
+// (Xk == NULL), or the dense additive kernel of the device coordinates Xk (column c of window w at
+// c = w*dw + t, ld ldk; the last window has last_dw of them) -- kernel_eval.hpp
+struct KernelSpec {
+   int kernel = 0;
+   double f = 1.0, l = 1.0, mu = 0.0;
+   const double* Xk = nullptr;
+   long long ldk = 0;
+   int nw = 1, dw = 0, last_dw = 0;
+};
+// FSAI of a kernel matrix (fsai_setup.hip): KNN pattern on dX (n x d, ld ldim), values of the kernel
+// K; host CSR out; dW (kw x n): the Schur-complement kernel K - W'W
+int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const KernelSpec& K, const double* dW, int kw,
+                    int require_grad, std::vector<int>& ia, std::vector<int>& ja, std::vector<double>& aa,
+                    std::vector<double>& da, hipStream_t s);
+// the KernelSpec of fkernel_params (this library's additive handle: its window buffer, uploaded to
+// *owned; else the plain kernel); 1 additive, 0 plain, -1 error (fsai_setup.hip)
+int kernel_spec_of(void* fkernel_params, func_kernel fkernel, int kernel, int n, KernelSpec& K, double** owned);
 // AFN apply object from device factors (fsai_afn.hip); owns all of them and S
 void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_LinvT, double* d_K12, void* S);
 

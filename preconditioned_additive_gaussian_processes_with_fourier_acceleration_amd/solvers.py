@@ -173,10 +173,12 @@ class AfnPrecond(_Apply):
 
     @classmethod
     def setup(cls, X, k: int, f: float, l: float, mu: float, perm_opt: str = "fps", perm=None,
-              schur_lfil: int = 20, kernel: int = 0):
+              schur_lfil: int = 20, kernel: int = 0, op=None):
         """Nfft4GPAmdAfnSetup: the AFN of the plain Gaussian (kernel 0) / Matern-1/2 (1) kernel of the
         points X (n x d) built on the GPU with rank k (afn.c:161-489, schur_opt 3).  perm_opt: "identity"
-        (afn.c:245-256), "fps" (farthest points, afn.c:196-209) or "perm" (``perm`` given, n entries)."""
+        (afn.c:245-256), "fps" (farthest points, afn.c:196-209) or "perm" (``perm`` given, n entries).
+        With ``op`` (an NFFTAdditiveKernel after its setup) the kernel is the dense additive kernel of
+        op's windows and hyperparameters (f, l, mu are then op's)."""
         L = _lib.lib()
         X = np.asfortranarray(np.asarray(X, dtype=np.float64))
         n, d = X.shape
@@ -184,12 +186,13 @@ class AfnPrecond(_Apply):
         p = None if perm is None else np.ascontiguousarray(np.asarray(perm, dtype=np.int32))
         if opt == 2 and (p is None or p.size != n):
             raise ValueError("perm_opt 'perm' needs a permutation of the n points")
-        params = _lib.kernel_params(f, l, mu, n)
+        params = op.h if op is not None else _lib.kernel_params(f, l, mu, n)
         self = cls.__new__(cls)
         self.n, self.schur = n, None
         self.h = L.Nfft4GPAmdAfnSetup(X.ctypes.data, n, n, d, int(k), opt, None if p is None else p.ctypes.data,
                                       int(schur_lfil), int(kernel), params)
-        L.Nfft4GPKernelParamFree(params)
+        if op is None:
+            L.Nfft4GPKernelParamFree(params)
         if not self.h:
             raise RuntimeError("Nfft4GPAmdAfnSetup failed (see stderr)")
         kk = C.c_int()
