@@ -224,6 +224,48 @@ def run_pcg_nystrom(op, torch, n, k, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=
             "nys_setup_mfma": mfma}
 
 
+def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1, schur="fsai",
+                order="random"):
+    """PCG to 1e-6 with the AFN preconditioner (BASELINE configs[1-2]: "AFN rank=512") of the same dense
+    additive kernel, set up on the GPU (afn.c:161-489 with rank k: FPS order, K11 Cholesky, K12,
+    W = L11^-1 K12 on MFMA, FSAI of the Schur complement with lfil entries per row)."""
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    assert op.setup(amd.GAUSSIAN, f=1.0, l=l_pcg, mu=0.01) == 0
+    torch.cuda.synchronize()
+    t0 = time.time()
+    # the reference's perm_opt 0 (afn.c:210-218, random order: the Nystrom leg's permutation) or 1 (FPS)
+    if order == "random":
+        perm = np.random.default_rng(rng_seed + 2).permutation(n).astype(np.int32)
+        pre = amd.AfnPrecond.setup(X, k, 1.0, l_pcg, 0.01, perm_opt="perm", perm=perm, schur_lfil=lfil, op=op,
+                                   schur=schur)
+    else:
+        pre = amd.AfnPrecond.setup(X, k, 1.0, l_pcg, 0.01, perm_opt="fps", schur_lfil=lfil, op=op, schur=schur)
+    torch.cuda.synchronize()
+    t_setup = time.time() - t0
+    b = torch.tensor(np.random.default_rng(rng_seed + 1).random(n) - 0.5, device="cuda")
+    x = torch.zeros(n, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    t0 = time.time()
+    _, relres, hist, iters = amd.pcg(op, b, x, maxits=maxits, tol=tol, precond=pre)
+    torch.cuda.synchronize()
+    t = time.time() - t0
+    r = torch.rand(n, dtype=torch.float64, device="cuda")
+    pre.solve(x, r)
+    torch.cuda.synchronize()
+    t1 = time.time()
+    for _ in range(10):
+        pre.solve(x, r)
+    torch.cuda.synchronize()
+    t_apply = (time.time() - t1) / 10
+    pre.free()
+    key = "pcg_afn" if schur == "fsai" else "pcg_afn_" + schur
+    if order != "random":
+        key += "_" + order
+    return {key + "_rank": k, key + "_order": order, key + "_schur": schur, key + "_schur_lfil": lfil if schur == "fsai" else None,
+            key + "_setup_s": t_setup, key + "_time_s": t, key + "_iters": iters, key + "_rel_res": relres,
+            key + "_total_s": t_setup + t, key + "_apply_ms": 1e3 * t_apply}
+
+
 def run_pcg_sharded(op, sop, torch, dist, n, rb, re, tol=1e-6, maxits=3000, l_pcg=0.1):
     """Row-sharded CG (dist.py, pcg.c semantics): local HIP BLAS-1 + scalar all-reduces."""
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
@@ -256,6 +298,11 @@ def main():
     ap.add_argument("--no-pcg", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
     ap.add_argument("--nys-rank", type=int, default=512, help="rank of the Nystrom-preconditioned PCG (0: off)")
+    ap.add_argument("--afn-rank", type=int, default=512, help="rank of the AFN-preconditioned PCG (0: off)")
+    ap.add_argument("--afn-schur", default="both", choices=["fsai", "noise", "both"],
+                    help="AFN Schur-complement solve: kernel FSAI (schur_opt 3), I/mu (0) or both")
+    ap.add_argument("--afn-order", default="random", choices=["random", "fps", "both"],
+                    help="AFN landmark order: random (perm_opt 0) or farthest points (1)")
     ap.add_argument("--kernel-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.kernel_only:
@@ -398,6 +445,13 @@ def main():
                     result.update(run_pcg_nystrom(op, torch, n, args.nys_rank))
                 except Exception as e:  # report, do not fail the GPU measurement
                     result["pcg_nys_error"] = repr(e)
+            if args.afn_rank > 0:
+                for schur in (["noise", "fsai"] if args.afn_schur == "both" else [args.afn_schur]):
+                    for order in (["random", "fps"] if args.afn_order == "both" else [args.afn_order]):
+                        try:
+                            result.update(run_pcg_afn(op, X, torch, n, args.afn_rank, schur=schur, order=order))
+                        except Exception as e:  # report, do not fail the GPU measurement
+                            result["pcg_afn_" + schur + "_" + order + "_error"] = repr(e)
         if not args.no_cpu_baseline:
             try:
                 result["cpu_baseline"] = cpu_baseline(n, d, X, x_host)

@@ -334,6 +334,13 @@ void Nfft4GPAmdAfnFree(void *afn);
  * for Nfft4GPAmdAfnSolve / Nfft4GPAmdAfnFree (which then also frees the Schur FSAI), NULL on error. */
 void *Nfft4GPAmdAfnSetup(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int k, int perm_opt, const int *perm,
                          int schur_lfil, int kernel, void *fkernel_params);
+/* the same with the reference's schur_opt (afn.c:449-480): 3 as above, 0 the scaled identity
+ * S^{-1} = I / _noise_level (afn.c:451-459, k > 0).  fkernel_params may also be this library's additive
+ * NFFT handle (after its setup): the kernel is then the dense additive kernel of its window buffer and
+ * hyperparameters (kernels.c:3099-3494, the points' K(perm[:k], .) -- not the reference's buffer-row
+ * quirk), the FPS order and the KNN pattern still come from data. */
+void *Nfft4GPAmdAfnSetupSchur(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int k, int perm_opt,
+                              const int *perm, int schur_opt, int schur_lfil, int kernel, void *fkernel_params);
 /* the AFN handle's rank, permutation (n) and Schur-complement FSAI (CSR, n - k rows); any output may be
  * NULL; returns the FSAI's nnz (0 without one), -1 on error */
 int Nfft4GPAmdAfnInfo(void *afn, int *k, int *perm, int *ia, int *ja, NFFT4GP_DOUBLE *aa);

@@ -125,6 +125,8 @@ _SIGS = {
     "Nfft4GPAmdAfnSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdAfnFree": (None, [vp]),
     "Nfft4GPAmdAfnSetup": (vp, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, vp]),
+    "Nfft4GPAmdAfnSetupSchur": (vp, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int,
+                                     vp]),
     "Nfft4GPAmdAfnInfo": (C.c_int, [vp, vp, vp, vp, vp, vp]),
     "Nfft4GPAmdSortFps": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, C.c_double, vp, vp]),
     "Nfft4GPAmdRankestNysScaled": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int]),

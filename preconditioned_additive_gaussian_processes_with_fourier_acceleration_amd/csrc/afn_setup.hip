@@ -632,11 +632,17 @@ int Nfft4GPAmdSortFps(const double* data, int n, int ldim, int d, int* k, double
 void* Nfft4GPAmdAfnSetup(const double* data, int n, int ldim, int d, int k, int perm_opt, const int* perm,
                          int schur_lfil, int kernel, void* fkernel_params)
 {
+   return Nfft4GPAmdAfnSetupSchur(data, n, ldim, d, k, perm_opt, perm, 3, schur_lfil, kernel, fkernel_params);
+}
+
+void* Nfft4GPAmdAfnSetupSchur(const double* data, int n, int ldim, int d, int k, int perm_opt, const int* perm,
+                              int schur_opt, int schur_lfil, int kernel, void* fkernel_params)
+{
    if (!need_device("Nfft4GPAmdAfnSetup")) return nullptr;
    if (!data || !fkernel_params || n <= 0 || ldim < n || d <= 0 || k < 0 || k > n || perm_opt < 0 || perm_opt > 2 ||
-       (perm_opt == 2 && !perm)) {
+       (perm_opt == 2 && !perm) || (schur_opt != 0 && schur_opt != 3) || (schur_opt == 0 && k == 0)) {
       fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup needs data (ldim >= n), kernel parameters, 0 <= k <= n, "
-                      "perm_opt 0 (identity), 1 (FPS) or 2 (perm given)\n");
+                      "perm_opt 0 (identity), 1 (FPS) or 2 (perm given), schur_opt 0 (k > 0) or 3\n");
       return nullptr;
    }
    // the kernel: plain (data's coordinates) or this library's additive handle (its window buffer)
@@ -705,16 +711,16 @@ void* Nfft4GPAmdAfnSetup(const double* data, int n, int ldim, int d, int k, int 
       if (info < 0) return fail("Cholesky / triangular inverse of K11");
    }
    if (n2 > 0 && k > 0) {
-      // K12 = K(X1, X2) (afn.c:436), W = L11^{-1} K12 (afn.c:443, dtrtrs)
-      if (dalloc(&K12, (size_t)k * n2) || dalloc(&W, (size_t)k * n2)) return fail("allocation");
+      // K12 = K(X1, X2) (afn.c:436), W = L11^{-1} K12 (afn.c:443, dtrtrs; the Schur FSAI's kernel)
+      if (dalloc(&K12, (size_t)k * n2) || (schur_opt == 3 && dalloc(&W, (size_t)k * n2))) return fail("allocation");
       for (int j0 = 0; j0 < n2; j0 += 65535) {
          const int nb = std::min(65535, n2 - j0);
          hipLaunchKernelGGL(k_kmat, dim3((k + 255) / 256, nb), dim3(256), 0, s, Xk, (long long)n, 0, k, k + j0, P, 0,
                             K12 + (size_t)j0 * k, (long long)k);
       }
-      if (gemm_f64(false, k, n2, k, G, k, K12, k, W, k, s)) return fail("gemm");
+      if (schur_opt == 3 && gemm_f64(false, k, n2, k, G, k, K12, k, W, k, s)) return fail("gemm");
    }
-   if (n2 > 0) {
+   if (n2 > 0 && schur_opt == 3) {
       // FSAI of the Schur complement on X2 (afn.c:445-473): KNN on the points' coordinates, values of the
       // Schur-complement kernel on the kernel coordinates
       std::vector<int> ia, ja;
@@ -740,7 +746,8 @@ void* Nfft4GPAmdAfnSetup(const double* data, int n, int ldim, int d, int k, int 
    for (void* p : {(void*)dX, (void*)Xp, (void*)Xkp, (void*)dXk, (void*)K11, (void*)W, (void*)dinfo}) (void)hipFree(p);
    dX = Xp = Xkp = dXk = K11 = W = nullptr;
    dinfo = nullptr;
-   void* A = afn_create_device(n, k, dperm, G, Gt, K12, S);
+   // schur_opt 0 (afn.c:451-459): S^{-1} = I / _noise_level
+   void* A = afn_create_device(n, k, dperm, G, Gt, K12, S, schur_opt == 0 ? 1.0 / K.mu : 0.0);
    if (!A) {
       fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: allocation failed\n");
       return nullptr;  // afn_create_device released the factors and S

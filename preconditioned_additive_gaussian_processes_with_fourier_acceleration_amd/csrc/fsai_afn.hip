@@ -38,6 +38,7 @@ struct AfnDev {
    double* LinvT = nullptr;  // its transpose (column i = row i of Linv)
    double* K12 = nullptr;   // k x n2 column-major
    FsaiDev* S = nullptr;    // FSAI of the Schur complement (n2)
+   double schur_scale = 0.0;  // S == NULL, n2 > 0: S^{-1} = schur_scale I (schur_opt 0, afn.c:451-459)
    bool own_S = false;
    double *rp = nullptr, *y = nullptr, *t = nullptr, *part = nullptr;
    int nblk = 0, cols = 1;  // A12 y2: workgroups, columns per workgroup
@@ -53,6 +54,12 @@ __global__ void k_csr_rows(const int* __restrict__ ia, const int* __restrict__ j
    double r = 0.0;
    for (int j = ia[i]; j < ia[i + 1]; j++) r += a[j] * x[ja[j]];
    y[i] = r;
+}
+
+__global__ void k_scale_into(const double* __restrict__ src, int n, double a, double* __restrict__ dst)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) dst[i] = a * src[i];
 }
 
 __global__ void k_gather(const double* __restrict__ src, const int* __restrict__ perm, int n, double* __restrict__ dst)
@@ -239,8 +246,12 @@ int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y);
    // rp2 -= A12^T y
    hipLaunchKernelGGL(k_a12t, dim3((n2 + 3) / 4), dim3(256), 0, s, A->K12, k, n2, A->y, rp2);
-   // y2 = FSAI(rp2)
-   if (fsai_apply_dev(A->S, y2, rp2, s)) return -1;
+   // y2 = FSAI(rp2), or rp2 / noise (schur_opt 0)
+   if (A->S) {
+      if (fsai_apply_dev(A->S, y2, rp2, s)) return -1;
+   } else {
+      hipLaunchKernelGGL(k_scale_into, dim3((n2 + 255) / 256), dim3(256), 0, s, rp2, n2, A->schur_scale, y2);
+   }
    // rp -= A12 y2
    hipLaunchKernelGGL(k_a12_part, dim3(A->nblk), dim3(256), 0, s, A->K12, k, n2, A->cols, y2, A->part);
    hipLaunchKernelGGL(k_a12_reduce, dim3((k + 63) / 64), dim3(256), 0, s, A->part, A->nblk, k, A->rp);
@@ -256,9 +267,11 @@ int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
 
 // an AFN apply object from factors already in HBM (afn_setup.hip); takes ownership of d_perm, d_Linv,
 // d_K12 (hipMalloc'ed) and of the Schur FSAI handle S (an Nfft4GPAmdFsaiCreate handle of size n - k)
-void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_LinvT, double* d_K12, void* S)
+void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_LinvT, double* d_K12, void* S,
+                        double schur_scale)
 {
    AfnDev* A = new AfnDev();
+   A->schur_scale = schur_scale;
    A->n = n;
    A->k = k;
    A->n2 = n - k;

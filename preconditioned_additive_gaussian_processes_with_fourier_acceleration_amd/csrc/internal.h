@@ -241,7 +241,9 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const Ke
 // *owned; else the plain kernel); 1 additive, 0 plain, -1 error (fsai_setup.hip)
 int kernel_spec_of(void* fkernel_params, func_kernel fkernel, int kernel, int n, KernelSpec& K, double** owned);
 // AFN apply object from device factors (fsai_afn.hip); owns all of them and S
-void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_LinvT, double* d_K12, void* S);
+// S == NULL with n - k > 0: the Schur complement solve is schur_scale * I (schur_opt 0)
+void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_LinvT, double* d_K12, void* S,
+                        double schur_scale = 0.0);
 
 hipStream_t current_stream();
 bool is_device_ptr(const void* p);

@@ -173,12 +173,13 @@ class AfnPrecond(_Apply):
 
     @classmethod
     def setup(cls, X, k: int, f: float, l: float, mu: float, perm_opt: str = "fps", perm=None,
-              schur_lfil: int = 20, kernel: int = 0, op=None):
+              schur_lfil: int = 20, kernel: int = 0, op=None, schur: str = "fsai"):
         """Nfft4GPAmdAfnSetup: the AFN of the plain Gaussian (kernel 0) / Matern-1/2 (1) kernel of the
         points X (n x d) built on the GPU with rank k (afn.c:161-489, schur_opt 3).  perm_opt: "identity"
         (afn.c:245-256), "fps" (farthest points, afn.c:196-209) or "perm" (``perm`` given, n entries).
         With ``op`` (an NFFTAdditiveKernel after its setup) the kernel is the dense additive kernel of
-        op's windows and hyperparameters (f, l, mu are then op's)."""
+        op's windows and hyperparameters (f, l, mu are then op's).  ``schur``: "fsai" (schur_opt 3, the
+        reference's default) or "noise" (schur_opt 0: S^{-1} = I / mu, afn.c:451-459)."""
         L = _lib.lib()
         X = np.asfortranarray(np.asarray(X, dtype=np.float64))
         n, d = X.shape
@@ -189,8 +190,8 @@ class AfnPrecond(_Apply):
         params = op.h if op is not None else _lib.kernel_params(f, l, mu, n)
         self = cls.__new__(cls)
         self.n, self.schur = n, None
-        self.h = L.Nfft4GPAmdAfnSetup(X.ctypes.data, n, n, d, int(k), opt, None if p is None else p.ctypes.data,
-                                      int(schur_lfil), int(kernel), params)
+        self.h = L.Nfft4GPAmdAfnSetupSchur(X.ctypes.data, n, n, d, int(k), opt, None if p is None else p.ctypes.data,
+                                           {"fsai": 3, "noise": 0}[schur], int(schur_lfil), int(kernel), params)
         if op is None:
             L.Nfft4GPKernelParamFree(params)
         if not self.h:

@@ -282,3 +282,20 @@ def test_pcg_nfft_operator_with_additive_afn(torch_cuda, k):
     _, rr0, _, it0 = amd.pcg(op, b, x0.clone(), maxits=3000, tol=1e-8)
     print(f"PCG n={n} d={d} l={l}: AFN rank {k}: {it} iterations, none: {it0}")
     assert rr <= 1e-8 and 0 < it, (it, it0)
+
+
+def test_afn_setup_schur_noise_matches_restatement(torch_cuda):
+    """schur_opt 0 (afn.c:451-459): the Schur-complement solve is I / _noise_level."""
+    import scipy.linalg as sl
+    z = load("precond_synth")
+    X, f, l, mu = np.asarray(z["X"]), float(z["f"]), float(z["l"]), float(z["mu"])
+    k, perm = int(z["afn_k"]), np.asarray(z["afn_perm"])
+    pre = amd.AfnPrecond.setup(X, k, f, l, mu, perm_opt="perm", perm=perm, schur="noise")
+    kk, p, csr = pre.info()
+    assert kk == k and csr is None
+    L11 = np.asarray(z["afn_L11"])
+    K12 = O.gaussian_block(X, f, l, perm[:k], perm[k:])
+    r = np.random.default_rng(3).random(X.shape[0]) - 0.5
+    x = np.zeros_like(r)
+    pre.solve(x, r.copy())
+    assert rel(x, O.afn_apply(perm, L11, K12, lambda v: v / mu, r.copy())) <= 1e-9

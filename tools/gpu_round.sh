@@ -8,7 +8,7 @@ timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.er
 cat gpurun_out/bench.json
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 rm -rf gpurun_out/prof
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-traffic > gpurun_out/prof_bench.log 2>&1 || { echo PROF_FAIL; tail -20 gpurun_out/prof_bench.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-traffic --afn-rank 0 > gpurun_out/prof_bench.log 2>&1 || { echo PROF_FAIL; tail -20 gpurun_out/prof_bench.log; exit 1; }
 find gpurun_out/prof -name "*stats*"
 timeout -k 10 400 python -u tools/setup_bench.py --out gpurun_out/setup_bench.json > gpurun_out/setup_bench.log 2>&1 || { echo SETUP_BENCH_FAIL; tail -20 gpurun_out/setup_bench.log; exit 1; }
 grep -v "^Using\|KNN time\|amdgpu.ids" gpurun_out/setup_bench.log | tail -12
