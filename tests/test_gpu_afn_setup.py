@@ -107,6 +107,27 @@ def test_fps_matches_golden(torch_cuda):
 
 
 @need_ref
+def test_fps_duplicates_match_reference(torch_cuda):
+    """Lattice points with many duplicates, k past the number of distinct points: once every remaining
+    distance is 0 the reference appends point 0 again ((dmax, i2) = (0, 0), ordering.c:624-690).  Ties
+    go to the lowest index as in the reference's serial loops; its OpenMP reductions merge the threads'
+    winners in arrival order, so the reference runs on one thread here."""
+    X = np.random.default_rng(4).integers(0, 3, (400, 2)) / 2.0  # 9 distinct points
+    gomp = C.CDLL("libgomp.so.1")
+    nthreads = gomp.omp_get_max_threads()
+    gomp.omp_set_num_threads(1)
+    try:
+        p_ref, d_ref = O.ref_sort_fps(X, 20)
+    finally:
+        gomp.omp_set_num_threads(nthreads)
+    np.testing.assert_array_equal(O.fps_par1(X, 20)[0], p_ref)
+    p, dist = gpu_fps(X, 20)
+    np.testing.assert_array_equal(p, p_ref)
+    np.testing.assert_array_equal(dist, d_ref)
+    assert (dist[9:] == 0).all()
+
+
+@need_ref
 @pytest.mark.parametrize("n,d,k,tol", [(20000, 3, 300, 0.0), (5000, 17, 0, 0.9), (300, 2, 300, 0.0), (7, 2, 1, 0.0)])
 def test_fps_matches_reference(torch_cuda, n, d, k, tol):
     X = np.random.default_rng(n + d).random((n, d))
