@@ -452,11 +452,18 @@ __global__ void k_transpose_lower(const double* __restrict__ G, int k, double* _
 
 // W[:, c] = V[:, k-1-c] / sqrt(w1[k-1-c]) (x 1e12 when sqrt(w1) < 1e-12), s[c] = max(1/(w^2 + eta), 0)
 // (matops.c Nfft4GPTrilNystromSvd, nys.c:641-647; NFFT4GP_MAX maps NaN to 0)
+// robust (k11_mode 1): eigenvalues of U1'U1 at rounding level (<= k eps max w1, or negative from
+// rounding, where the reference's sqrt gives NaN factors) drop their column instead
 __global__ void k_nys_scale(const double* __restrict__ V, const double* __restrict__ w1, int k, double eta,
-                            double* __restrict__ W, double* __restrict__ s)
+                            double* __restrict__ W, double* __restrict__ s, int robust)
 {
    const int i = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y;
    const int src = k - 1 - c;
+   if (robust && !(w1[src] > (double)k * 2.220446049250313e-16 * w1[k - 1])) {
+      if (i < k) W[i + (size_t)c * k] = 0.0;
+      if (i == 0) s[c] = 0.0;
+      return;
+   }
    const double wi = sqrt(w1[src]);
    if (i < k) W[i + (size_t)c * k] = V[i + (size_t)src * k] * ((wi < 1e-12) ? 1e12 : 1.0 / wi);
    if (i == 0) {
@@ -796,7 +803,8 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
           hipMemcpy(d_w1, w1.data(), sizeof(double) * k, hipMemcpyHostToDevice))
          return fail("upload");
    }
-   hipLaunchKernelGGL(k_nys_scale, dim3((k + 255) / 256, k), dim3(256), 0, s, d_AA, d_w1, k, eta, d_B, d_s);
+   hipLaunchKernelGGL(k_nys_scale, dim3((k + 255) / 256, k), dim3(256), 0, s, d_AA, d_w1, k, eta, d_B, d_s,
+                      k11_mode == 1 ? 1 : 0);
    phase("eig");
    // 6. U = U1 W.  Without gradients the panel's storage is reused for U; with them the panel (K, dK/df,
    //    dK/dl) and U1 (= dU, nys.c:611-615) stay, for Dvp and Trace.

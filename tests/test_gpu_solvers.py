@@ -269,3 +269,23 @@ def test_nystrom_fp32_storage_pcg(torch_cuda):
     pre.solve(z, r)
     assert torch.equal(z, z64)
     pre.free()
+
+
+def test_nystrom_landmarks_rank_above_numerical_rank(torch_cuda):
+    """k11 = "landmarks" with k above the kernel's numerical rank: eigenvalues of U1'U1 at rounding level
+    (negative ones would give NaN factors through sqrt, as in the reference's Nfft4GPTrilNystromSvd) drop
+    their columns; the factors stay finite and PCG converges in a few iterations."""
+    torch = torch_cuda
+    rng = np.random.default_rng(8)
+    n, d, k = 20000, 2, 300
+    X = rng.random((n, d))
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    assert op.setup(amd.GAUSSIAN, 1.0, 0.1, 0.01) == 0  # l = 0.1: the NFFT operator is SPD (DESIGN 3.4)
+    pre = amd.NystromPrecond.from_additive(op, rng.permutation(n).astype(np.int32), k, k11="landmarks")
+    b = torch.tensor(rng.random(n) - 0.5, device="cuda")
+    x = torch.zeros(n, dtype=torch.float64, device="cuda")
+    z = torch.zeros(n, dtype=torch.float64, device="cuda")
+    pre.solve(z, b)
+    assert torch.isfinite(z).all()
+    _, rr, _, it = amd.pcg(op, b, x, maxits=500, tol=1e-8, precond=pre)
+    assert 0 < it <= 20 and rr <= 1e-8, (it, rr)
