@@ -351,7 +351,8 @@ int Nfft4GPAmdAfnInfo(void *afn, int *k, int *perm, int *ia, int *ja, NFFT4GP_DO
  * each) and Nfft4GPRankestDefault (rankest.c:30-181: fill-distance / eigenvalue tolerance from
  * subsamples, then FPS of the full data up to max_rank; perm receives the selected points), with the
  * rankest struct's fields as arguments (reference defaults: max_rank 2000, nsample 500, nsample_r 5,
- * full_tol 0.9).  kernel 0 Gaussian, 1 Matern-1/2; fkernel_params an nfft4gp_kernel.  The FPS passes,
+ * full_tol 0.9).  kernel 0 Gaussian, 1 Matern-1/2; fkernel_params an nfft4gp_kernel, or this library's
+ * additive NFFT handle (the subsamples' kernel matrices are then its dense additive kernel).  The FPS passes,
  * kernel matrices, Cholesky / inverse / eigenvalues (rocSOLVER) and Nystrom products (MFMA GEMM) run on
  * the device; they consume rand() exactly as the reference does, so after the same srand() both pick the
  * same subsamples.  A rank-k factor of a subsample that is not positive definite counts as error

@@ -379,22 +379,23 @@ std::vector<int> rand_perm(int n, int k)
 struct RankCtx {
    const double* dX = nullptr;  // device, n x d column-major (ldim)
    long long ldim = 0;
-   int n = 0, d = 0, kernel = 0;
-   double f = 1.0, l = 1.0, mu = 0.0;
+   int n = 0, d = 0;
+   KernelSpec ks;  // plain, or the additive kernel of ks.Xk (n x D, ld n) -- kernel_spec_of
+   int D = 0;      // kernel coordinates per point
    hipStream_t s = nullptr;
-   KernelParams params(int dims, double noise) const
+   // the kernel on sample coordinates Xk_sample (additive) with noise `noise`
+   KernelParams params(const double* Xk_sample, double noise) const
    {
-      KernelSpec K;
-      K.kernel = kernel;
-      K.f = f;
-      K.l = l;
+      KernelSpec K = ks;
+      K.Xk = ks.Xk ? Xk_sample : nullptr;
       K.mu = noise;
-      return kernel_params_of(K, dims);
+      return kernel_params_of(K, d);
    }
 };
 
-// the subsample rows (device, n1 x d) of Nfft4GPSubData(data, RandPerm(n, n1)), scaled by `scale`
-int sample_points(const RankCtx& C, int n1, double scale, double* Xs)
+// the subsample rows of Nfft4GPSubData(data, RandPerm(n, n1)) into Xs (n1 x d) and, for an additive
+// kernel, of its coordinates into Xks (n1 x D), both scaled by `scale`
+int sample_points(const RankCtx& C, int n1, double scale, double* Xs, double* Xks)
 {
    std::vector<int> rows = rand_perm(C.n, n1);
    int* drows = nullptr;
@@ -403,9 +404,16 @@ int sample_points(const RankCtx& C, int n1, double scale, double* Xs)
       return -1;
    }
    hipLaunchKernelGGL(k_gather_points, dim3((n1 + 255) / 256, C.d), dim3(256), 0, C.s, C.dX, C.ldim, n1, C.d, drows, Xs);
-   if (scale != 1.0)
+   if (C.ks.Xk)
+      hipLaunchKernelGGL(k_gather_points, dim3((n1 + 255) / 256, C.D), dim3(256), 0, C.s, C.ks.Xk, C.ks.ldk, n1, C.D,
+                         drows, Xks);
+   if (scale != 1.0) {
       hipLaunchKernelGGL(k_scale, dim3((unsigned)(((size_t)n1 * C.d + 255) / 256)), dim3(256), 0, C.s, Xs,
                          (size_t)n1 * C.d, scale);
+      if (C.ks.Xk)
+         hipLaunchKernelGGL(k_scale, dim3((unsigned)(((size_t)n1 * C.D + 255) / 256)), dim3(256), 0, C.s, Xks,
+                            (size_t)n1 * C.D, scale);
+   }
    (void)hipStreamSynchronize(C.s);
    (void)hipFree(drows);
    return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -424,30 +432,34 @@ int nys_scaled_estimate(const RankCtx& C, int max_rank, int nsample)
 {
    const int n = C.n, d = C.d;
    const int n1 = std::min(nsample, n);
-   double *Xs = nullptr, *Xp = nullptr, *K0 = nullptr, *K11 = nullptr, *G = nullptr, *Gt = nullptr, *W = nullptr,
-          *Kn = nullptr, *dsum = nullptr;
+   double *Xs = nullptr, *Xp = nullptr, *Xks = nullptr, *Xkp = nullptr, *K0 = nullptr, *K11 = nullptr, *G = nullptr,
+          *Gt = nullptr, *W = nullptr, *Kn = nullptr, *dsum = nullptr;
    int *dperm = nullptr, *dinfo = nullptr;
    auto done = [&](int rc) {
       (void)hipStreamSynchronize(C.s);
-      for (void* p : {(void*)Xs, (void*)Xp, (void*)K0, (void*)K11, (void*)G, (void*)Gt, (void*)W, (void*)Kn,
-                      (void*)dsum, (void*)dperm, (void*)dinfo})
+      for (void* p : {(void*)Xs, (void*)Xp, (void*)Xks, (void*)Xkp, (void*)K0, (void*)K11, (void*)G, (void*)Gt,
+                      (void*)W, (void*)Kn, (void*)dsum, (void*)dperm, (void*)dinfo})
          (void)hipFree(p);
       return rc;
    };
    const size_t nn = (size_t)n1 * n1;
-   if (dalloc(&Xs, (size_t)n1 * d) || dalloc(&Xp, (size_t)n1 * d) || dalloc(&K0, nn) || dalloc(&K11, nn) ||
+   if ((C.ks.Xk && (dalloc(&Xks, (size_t)n1 * C.D) || dalloc(&Xkp, (size_t)n1 * C.D))) ||
+       dalloc(&Xs, (size_t)n1 * d) || dalloc(&Xp, (size_t)n1 * d) || dalloc(&K0, nn) || dalloc(&K11, nn) ||
        dalloc(&G, nn) || dalloc(&Gt, nn) || dalloc(&W, nn) || dalloc(&Kn, nn) || dalloc(&dsum, 1) ||
        dalloc(&dperm, n1) || dalloc(&dinfo, 1))
       return done(-1);
    // scale so that the sample's spacing resembles the full data's: (n1 / n)^(1/d)
-   if (sample_points(C, n1, pow((double)n1 / n, 1.0 / d), Xs)) return done(-1);
+   if (sample_points(C, n1, pow((double)n1 / n, 1.0 / d), Xs, Xks)) return done(-1);
    std::vector<int> perm(n1);
    if (fps_device(Xs, n1, n1, d, n1, 0.0, perm.data(), nullptr, C.s) != n1) return done(-1);
    if (hipMemcpy(dperm, perm.data(), sizeof(int) * n1, hipMemcpyHostToDevice) != hipSuccess) return done(-1);
    hipLaunchKernelGGL(k_gather_points, dim3((n1 + 255) / 256, d), dim3(256), 0, C.s, Xs, (long long)n1, n1, d, dperm, Xp);
+   if (C.ks.Xk)
+      hipLaunchKernelGGL(k_gather_points, dim3((n1 + 255) / 256, C.D), dim3(256), 0, C.s, Xks, (long long)n1, n1, C.D,
+                         dperm, Xkp);
    // K(perm, perm) without noise (rankest.c:307-309)
-   hipLaunchKernelGGL(k_kmat, dim3((n1 + 255) / 256, n1), dim3(256), 0, C.s, Xp, (long long)n1, 0, n1, 0,
-                      C.params(d, 0.0), 1, K0, (long long)n1);
+   hipLaunchKernelGGL(k_kmat, dim3((n1 + 255) / 256, n1), dim3(256), 0, C.s, C.ks.Xk ? Xkp : Xp, (long long)n1, 0, n1,
+                      0, C.params(Xkp, 0.0), 1, K0, (long long)n1);
    hipLaunchKernelGGL(k_sumsq_lower, dim3(1), dim3(1024), 0, C.s, K0, nullptr, 0.0, n1, dsum);
    double a_fro = sqrt(device_scalar(dsum, C.s));
    const double nu = sqrt((double)n) * (nextafter(a_fro, a_fro + 1.0) - a_fro);  // rankest.c:318-322
@@ -499,23 +511,26 @@ double default_tolerance(const RankCtx& C, int nsamples, int* pk)
 {
    const int n = C.n, d = C.d;
    const int n1 = std::min(nsamples, n);
-   double *Xs = nullptr, *K = nullptr;
+   double *Xs = nullptr, *Xks = nullptr, *K = nullptr;
    auto done = [&](double v) {
       (void)hipStreamSynchronize(C.s);
       (void)hipFree(Xs);
+      (void)hipFree(Xks);
       (void)hipFree(K);
       return v;
    };
-   if (dalloc(&Xs, (size_t)n1 * d) || dalloc(&K, (size_t)n1 * n1) || sample_points(C, n1, 1.0, Xs)) return done(NAN);
+   if ((C.ks.Xk && dalloc(&Xks, (size_t)n1 * C.D)) || dalloc(&Xs, (size_t)n1 * d) || dalloc(&K, (size_t)n1 * n1) ||
+       sample_points(C, n1, 1.0, Xs, Xks))
+      return done(NAN);
    std::vector<int> perm(n1);
    std::vector<double> dist(n1);
    if (fps_device(Xs, n1, n1, d, n1, 0.0, perm.data(), dist.data(), C.s) != n1) return done(NAN);
    // K of the sample with noise (kernels.c:1198) and its eigenvalues (dsyev 'N')
-   hipLaunchKernelGGL(k_kmat, dim3((n1 + 255) / 256, n1), dim3(256), 0, C.s, Xs, (long long)n1, 0, n1, 0,
-                      C.params(d, C.mu), 1, K, (long long)n1);
+   hipLaunchKernelGGL(k_kmat, dim3((n1 + 255) / 256, n1), dim3(256), 0, C.s, C.ks.Xk ? Xks : Xs, (long long)n1, 0, n1, 0,
+                      C.params(Xks, C.ks.mu), 1, K, (long long)n1);
    std::vector<double> eig;
    if (sym_eigvals_dev(K, n1, eig, C.s)) return done(NAN);
-   const double tol = 0.41, tol2 = 0.2, tol3 = 1.1 * C.mu;
+   const double tol = 0.41, tol2 = 0.2, tol3 = 1.1 * C.ks.mu;
    int rank = 0;
    for (int i = n1 - 1; i >= 0; i--) {
       if (eig[i] < tol3) break;
@@ -569,11 +584,11 @@ int rankest_default(const RankCtx& C, int max_rank, int nsample, int nsample_r, 
    return rank;
 }
 
-int rank_ctx(RankCtx& C, const double* data, int n, int ldim, int d, int kernel, const void* params, double** owned)
+int rank_ctx(RankCtx& C, const double* data, int n, int ldim, int d, int kernel, void* params, double** owned,
+             double** owned_k)
 {
-   const nfft4gp_kernel* kp = (const nfft4gp_kernel*)params;
-   *owned = nullptr;
-   if (!data || !kp || n <= 0 || ldim < n || d <= 0 || d > kFpsMaxDims) {
+   *owned = *owned_k = nullptr;
+   if (!data || !params || n <= 0 || ldim < n || d <= 0 || d > kFpsMaxDims) {
       fprintf(stderr, "nfft4gp_amd: rank estimation needs data (ldim >= n, d <= %d) and kernel parameters\n",
               kFpsMaxDims);
       return -1;
@@ -581,11 +596,10 @@ int rank_ctx(RankCtx& C, const double* data, int n, int ldim, int d, int kernel,
    C.n = n;
    C.d = d;
    C.ldim = ldim;
-   C.kernel = kernel ? 1 : 0;
-   C.f = kp->_params[0];
-   C.l = kp->_params[1];
-   C.mu = kp->_noise_level;
    C.s = current_stream();
+   const int additive = kernel_spec_of(params, nullptr, kernel, n, C.ks, owned_k);
+   if (additive < 0) return -1;
+   C.D = additive ? (C.ks.nw - 1) * C.ks.dw + C.ks.last_dw : d;
    if (is_device_ptr(data)) {
       C.dX = data;
       return 0;
@@ -761,10 +775,11 @@ int Nfft4GPAmdRankestNysScaled(const double* data, int n, int ldim, int d, int k
 {
    if (!need_device("Nfft4GPAmdRankestNysScaled")) return -1;
    RankCtx C;
-   double* owned = nullptr;
-   if (rank_ctx(C, data, n, ldim, d, kernel, fkernel_params, &owned)) return -1;
+   double *owned = nullptr, *owned_k = nullptr;
+   if (rank_ctx(C, data, n, ldim, d, kernel, fkernel_params, &owned, &owned_k)) return -1;
    const int r = rankest_nys_scaled(C, max_rank, nsample, nsample_r);
    (void)hipFree(owned);
+   (void)hipFree(owned_k);
    return r;
 }
 
@@ -773,11 +788,12 @@ int Nfft4GPAmdRankestDefault(const double* data, int n, int ldim, int d, int ker
 {
    if (!need_device("Nfft4GPAmdRankestDefault")) return -1;
    RankCtx C;
-   double* owned = nullptr;
-   if (rank_ctx(C, data, n, ldim, d, kernel, fkernel_params, &owned)) return -1;
+   double *owned = nullptr, *owned_k = nullptr;
+   if (rank_ctx(C, data, n, ldim, d, kernel, fkernel_params, &owned, &owned_k)) return -1;
    std::vector<int> p;
    const int r = rankest_default(C, max_rank, nsample, nsample_r, full_tol, p);
    (void)hipFree(owned);
+   (void)hipFree(owned_k);
    if (r > 0 && perm) std::copy(p.begin(), p.end(), perm);
    return r;
 }
@@ -793,8 +809,8 @@ int Nfft4GPAmdAfnRankEstimate(const double* data, int n, int ldim, int d, int ma
       return std::min(-max_k, n);
    }
    RankCtx C;
-   double* owned = nullptr;
-   if (rank_ctx(C, data, n, ldim, d, kernel, fkernel_params, &owned)) return -1;
+   double *owned = nullptr, *owned_k = nullptr;
+   if (rank_ctx(C, data, n, ldim, d, kernel, fkernel_params, &owned, &owned_k)) return -1;
    int k = -1;
    std::vector<int> sel;
    const int rank = rankest_nys_scaled(C, max_k, nsamples, 5);  // _nsample_r = 5 (rankest.c:11)
@@ -814,6 +830,7 @@ int Nfft4GPAmdAfnRankEstimate(const double* data, int n, int ldim, int d, int ma
       }
    }
    (void)hipFree(owned);
+   (void)hipFree(owned_k);
    if (k < 0) return -1;
    const std::vector<int> full = expand_perm(sel.data(), (int)sel.size(), n);
    std::copy(full.begin(), full.end(), perm);

@@ -99,3 +99,24 @@ def test_afn_rank_estimate_front_end_then_setup(torch_cuda):
     _, rr, _, it = amd.pcg(op, b, x0.clone(), maxits=2000, tol=1e-8, precond=pre)
     _, rr0, _, it0 = amd.pcg(op, b, x0.clone(), maxits=2000, tol=1e-8)
     assert rr <= 1e-8 and it > 0 and (it0 == 0 or it < it0), (it, it0)
+
+
+def test_afn_rank_estimate_additive_kernel(torch_cuda):
+    """With this library's additive NFFT handle as the kernel, the subsamples' kernel matrices are the dense
+    additive kernel of their window coordinates: a 1-D-window additive kernel in 6 features has a much
+    smaller numerical rank than the 6-D Gaussian of the same length scale, so the estimate is smaller."""
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    rng = np.random.default_rng(6)
+    n, d, f, l, mu = 20000, 6, 1.0, 0.3, 0.001
+    X = np.asfortranarray(rng.random((n, d)))
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    op.setup(amd.GAUSSIAN, f, l, mu)
+    L = _lib.lib()
+    P = _lib.kernel_params(f, l, mu, n)
+    LIBC.srand(3)
+    r_plain = L.Nfft4GPAmdRankestNysScaled(X.ctypes.data, n, n, d, 0, P, 2000, 500, 5)
+    LIBC.srand(3)
+    r_add = L.Nfft4GPAmdRankestNysScaled(X.ctypes.data, n, n, d, 0, op.h, 2000, 500, 5)
+    L.Nfft4GPKernelParamFree(P)
+    assert r_plain >= 0 and r_add >= 0
+    assert r_add < r_plain, (r_add, r_plain)
