@@ -188,3 +188,16 @@ def test_fps_restatement_matches_golden():
     np.testing.assert_array_equal(p, z["perm_b"])
     np.testing.assert_array_equal(d, z["dist_b"])
     assert d[-1] < float(z["tol_b"]) <= d[-2]
+
+
+@pytest.mark.skipif(not ref_available(), reason="oracle/_ref not built")
+@pytest.mark.parametrize("n,d,k,tol", [(3000, 3, 200, 0.0), (2000, 9, 0, 0.6)])
+def test_fps_restatement_matches_compiled_reference(n, d, k, tol):
+    """oracle.fps_par1 against the reference's Nfft4GPSortFps (ordering.c, compiled in oracle/_ref) on
+    fresh random points (no ties): order and fill distances bitwise."""
+    from oracle import fps_par1, ref_sort_fps
+    X = np.random.default_rng(n + d).random((n, d))
+    p_ref, d_ref = ref_sort_fps(X, k, tol)
+    p, dist = fps_par1(X, k, tol)
+    np.testing.assert_array_equal(p, p_ref)
+    np.testing.assert_array_equal(dist, d_ref)
