@@ -30,6 +30,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+BASELINE_METRIC = "kernel matvecs/sec + PCG wall-time to 1e-6, n=1e6 d=32 additive, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 F64_MFMA_PEAK_TFS = 78.6  # MI355X dense FP64 matrix peak (spec; gfx950 runs v_mfma_f64_16x16x4 at half of MI300X)
 
@@ -97,8 +98,9 @@ def cpu_baseline(n, d, X, x, max_seconds=25.0):
     }
 
 
-def kernel_only(n, d):
-    """Child mode for the PMC passes: setup + one matvec + a few launches of each kernel."""
+def kernel_only(n, d, nys_rank=0):
+    """Child mode for the PMC passes: setup + one matvec + a few launches of each kernel (and, with
+    nys_rank > 0, one rank-k Nystrom setup for its MFMA GEMM k_gemm_f64)."""
     import torch
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
     X, x_host = make_problem(n, d)
@@ -109,6 +111,10 @@ def kernel_only(n, d):
     op.matsymv(xd, 1.0, 0.0, yd)
     for k in op.KERNELS:
         op.kernel_bench(k, xd, yd, reps=5)
+    if nys_rank > 0:
+        assert op.setup(amd.GAUSSIAN, f=1.0, l=0.1, mu=0.01) == 0
+        perm = np.random.default_rng(908).permutation(n).astype(np.int32)
+        amd.NystromPrecond.from_additive(op, perm, nys_rank, k11="landmarks").free()
     torch.cuda.synchronize()
 
 
@@ -304,9 +310,10 @@ def main():
     ap.add_argument("--afn-order", default="random", choices=["random", "fps", "both"],
                     help="AFN landmark order: random (perm_opt 0) or farthest points (1)")
     ap.add_argument("--kernel-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--kernel-only-nys", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.kernel_only:
-        kernel_only(args.n, args.d)
+        kernel_only(args.n, args.d, args.kernel_only_nys)
         return
 
     import torch
@@ -351,58 +358,112 @@ def main():
         else:
             sop.matsymv(xd, 1.0, 0.0, yd)  # local spread -> all-reduce of the 32x64 grids -> local interp
 
+    # The PCG legs (the metric's second half) run first: their ~1e3 matvecs also bring the GPU out of its
+    # idle clock state, which otherwise costs the first few hundred matvecs ~15 % (tools/warm_probe.py:
+    # 100 us per matvec cold, 85 us warm, back to 100 us after 2 s idle).  Then the kernel is set up again
+    # at the matvec workload's l = 1 and the W warmup + K timed steps follow immediately.
+    pcg = {}
+    pcie_rate = None
+    if world == 1:
+        # host-pointer calls (the reference's calling convention): x and y staged over PCIe each call
+        xh = np.ascontiguousarray(x_host)
+        yh = np.zeros(n)
+        op.matsymv(xh, 1.0, 0.0, yh)
+        reps_h = 20
+        t0 = time.perf_counter()
+        for _ in range(reps_h):
+            op.matsymv(xh, 1.0, 0.0, yh)
+        pcie_rate = reps_h / (time.perf_counter() - t0)
+    if world == 1 and not args.no_pcg:
+        pcg.update(run_pcg_single(op, torch, n))
+        if args.nys_rank > 0:
+            try:
+                pcg.update(run_pcg_nystrom(op, torch, n, args.nys_rank))
+            except Exception as e:  # report, do not fail the GPU measurement
+                pcg["pcg_nys_error"] = repr(e)
+        if args.afn_rank > 0:
+            for schur in (["noise", "fsai"] if args.afn_schur == "both" else [args.afn_schur]):
+                for order in (["random", "fps"] if args.afn_order == "both" else [args.afn_order]):
+                    try:
+                        pcg.update(run_pcg_afn(op, X, torch, n, args.afn_rank, schur=schur, order=order))
+                    except Exception as e:  # report, do not fail the GPU measurement
+                        pcg["pcg_afn_" + schur + "_" + order + "_error"] = repr(e)
+        if op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) != 0:
+            raise SystemExit("setup failed")
+
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
 
+    def timed(instrumented):
+        """K steps bracketed by barrier + synchronize; with `instrumented` every spread / grid / interp
+        dispatch of the loop carries start / stop hipEvents (Nfft4GPAmdTimingEnable), so the per-kernel
+        durations are measured over this same timed region."""
+        if instrumented:
+            op.timing(True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        per = None
+        if instrumented:
+            per = {k: ms / max(c, 1) for k, (ms, c) in op.timing_query().items()}
+            op.timing(False)
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el, per
+
+    # the headline timed region is uninstrumented; it is repeated at once with dispatch-attached events on
+    # every kernel (about 13 us per matvec of event overhead, reported as ms_per_step_instrumented) for the
+    # per-kernel durations of the roofline
+    elapsed, _ = timed(False)
+    elapsed_inst, kern_avg = timed(True) if world == 1 else (None, None)
+    headline = n == 1_000_000 and d == 32
+    cfg_tag = "BASELINE configs[2]" if headline else "reduced size, not a BASELINE config" \
+        if (n, d) != (100_000, 8) else "BASELINE configs[1] sizes"
     result = {
-        "metric": "kernel matvecs/sec (additive NFFT (K+sigma^2 I)v, n=1e6, d=32 1-D windows)",
+        # BASELINE.json's metric at its headline config; a descriptive name at other sizes
+        "metric": BASELINE_METRIC if headline else f"kernel matvecs/sec (additive NFFT matvec, n={n}, d={d})",
         "value": args.steps / elapsed,
         "unit": "matvecs/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed / args.steps,
+        "ms_per_step_instrumented": 1e3 * elapsed_inst / args.steps if elapsed_inst else None,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: X ~ U[0,1)^d, x ~ U(-0.5,0.5), numpy PCG64 seed 906",
         "config": {"workload": f"additive NFFT matvec, n={n}, d={d}, {d} x 1-D windows, Gaussian f=1 l=1 "
-                               "mu=0.01 (BASELINE configs[2]); N>1: rows sharded, 32x64 grid all-reduce",
+                               f"mu=0.01 ({cfg_tag}); N>1: rows sharded, {d}x64 grid all-reduce",
                    "n": n, "d": d, "nwindows": d, "setup_s": setup_s,
                    "parallelism": f"rows{world}" if world > 1 else "single"},
     }
     if world == 1:
-        # per-kernel durations: one hipEvent pair around `reps` back-to-back launches of each kernel
-        # on the library stream (the timed loop above carries no per-launch events: a pair costs
-        # several microseconds, ~5% of a matvec)
+        result.update(pcg)
+        # per-kernel durations: dispatch-attached hipEvents over the instrumented repeat of the timed region
+        # (the same begin / end timestamps rocprofv3's kernel trace reports; profiles/ holds that trace of
+        # this command)
         info = op.layout_info()
         b_spread, b_interp = algorithmic_bytes(info, n, d)
-        reps = max(20, min(args.steps, 200))
-        avg = {k: op.kernel_bench(k, xd, yd, reps=reps) for k in op.KERNELS}  # ms
-        torch.cuda.synchronize()
+        avg = kern_avg
         dom = "spread" if avg["spread"] >= avg["interp"] else "interp"
         # achieved = SURVEY.md 8(d)'s algorithmic bytes: one matvec moves 8n(2d+2) (fp64 coordinates and
         # vectors), of which the spread pass reads coords + v = 8n(d+1) and the interpolation pass reads
         # coords and writes y = 8n(d+1).  This layout stores the same information in 5 B per
         # (point, window) (DESIGN.md 3.2), so it moves fewer bytes than that; the rate on the bytes it
-        # actually moves is reported beside it (achieved_layout / frac_layout).
+        # actually moves is reported beside it (achieved_layout / frac_layout, and frac_pmc on the PMC
+        # HBM bytes).
         survey_bytes = 8 * n * (d + 1)
         bytes_dom = b_spread if dom == "spread" else b_interp
         achieved = survey_bytes / (avg[dom] * 1e-3) / 1e9
@@ -424,34 +485,16 @@ def main():
                               "algorithmic_bytes_def": "SURVEY 8(d): 8n(d+1) per pass (fp64 coords + vector)",
                               "layout_bytes_per_launch": bytes_dom,
                               "achieved_layout": achieved_layout, "frac_layout": achieved_layout / HBM_PEAK_GBS,
-                              "avg_launch_ms": avg[dom]}
+                              "achieved_pmc": (traffic / (avg[dom] * 1e-3) / 1e9) if traffic else None,
+                              "frac_pmc": (traffic / (avg[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                              "avg_launch_ms": avg[dom],
+                              "avg_launch_source": f"dispatch-attached hipEvents over a repeat of the {args.steps} timed steps"}
         result["kernels_ms"] = avg
+        result["kernels_ms_sum"] = sum(avg.values())
         result["layout"] = info
         # survey-defined whole-matvec bytes (fp64 coords: 8n(2d+2)) for reference
         result["matvec_bytes_survey_def"] = 8 * n * (2 * d + 2)
-        # host-pointer calls (the reference's calling convention): x and y staged over PCIe each call
-        xh = np.ascontiguousarray(x_host)
-        yh = np.zeros(n)
-        op.matsymv(xh, 1.0, 0.0, yh)
-        reps_h = 20
-        t0 = time.perf_counter()
-        for _ in range(reps_h):
-            op.matsymv(xh, 1.0, 0.0, yh)
-        result["pcie_inclusive_matvecs_per_s"] = reps_h / (time.perf_counter() - t0)
-        if not args.no_pcg:
-            result.update(run_pcg_single(op, torch, n))
-            if args.nys_rank > 0:
-                try:
-                    result.update(run_pcg_nystrom(op, torch, n, args.nys_rank))
-                except Exception as e:  # report, do not fail the GPU measurement
-                    result["pcg_nys_error"] = repr(e)
-            if args.afn_rank > 0:
-                for schur in (["noise", "fsai"] if args.afn_schur == "both" else [args.afn_schur]):
-                    for order in (["random", "fps"] if args.afn_order == "both" else [args.afn_order]):
-                        try:
-                            result.update(run_pcg_afn(op, X, torch, n, args.afn_rank, schur=schur, order=order))
-                        except Exception as e:  # report, do not fail the GPU measurement
-                            result["pcg_afn_" + schur + "_" + order + "_error"] = repr(e)
+        result["pcie_inclusive_matvecs_per_s"] = pcie_rate
         if not args.no_cpu_baseline:
             try:
                 result["cpu_baseline"] = cpu_baseline(n, d, X, x_host)

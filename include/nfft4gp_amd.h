@@ -391,7 +391,10 @@ const char *Nfft4GPAmdVersion(void);
 int Nfft4GPAmdAdditiveLayoutInfo(void *str, long long *out, int nout);
 
 /* per-kernel timing with hipEvents on the library stream (0 disables; resets counters when enabled).
- * After enabling, every additive matvec records events around its spread / grid / interp launches.
+ * After enabling, every additive matvec launches its spread / grid / interp kernels with start / stop
+ * events attached to the dispatches (hipExtLaunchKernelGGL: the dispatch packet's own begin / end
+ * timestamps, the durations rocprofv3's kernel trace reports; multi-feature windows: events recorded
+ * around each launch).
  * Nfft4GPAmdTimingQuery writes total milliseconds and launch counts for the three kernels:
  * ms[0..2] = spread, grid, interp;  cnt[0..2] likewise.  Returns 0. */
 int Nfft4GPAmdTimingEnable(void *str, int enable);

@@ -149,9 +149,11 @@ struct AdditivePlan {
    double* d_xs = nullptr;    // staging (host pointer calls)
    double* d_ys = nullptr;    // staging 3n
    MdPlan md;  // used instead of the 1-D layout when any window has more than one feature
-   // timing
+   // timing (Nfft4GPAmdTimingEnable): while on, plan_apply_dev points kev at 6 events and the launchers
+   // attach them to the spread / grid / interp dispatches themselves (hipExtLaunchKernelGGL start and stop
+   // events = the dispatch packet's begin / end timestamps, the quantity rocprofv3's kernel trace reports)
    bool timing = false;
-   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+   hipEvent_t* kev = nullptr;
    double ms[3] = {0, 0, 0};
    long long cnt[3] = {0, 0, 0};
 };
@@ -169,6 +171,9 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
 // y = A x (alpha = 1, beta = 0) and *d_dot = (y, x) on device pointers: the matvec + dot of a CG step in
 // the matvec's own three launches (used by Nfft4GPSolverPcg when its operator is this library's)
 int additive_matvec_dot(void* str, const double* d_x, double* d_y, double* d_dot);
+// true when additive_matvec_dot can serve this handle: points set up, whole-row (not a row shard) handle,
+// and a 1-D layout whose block count the fused grid reduction can sum (nblocks <= kRedMaxBlocks)
+bool additive_fused_dot_ok(void* str);
 
 // Nystrom preconditioner M = U S U^T + eta (I - U U^T) in HBM (nys.c:115-173 apply)
 struct NysDev {

@@ -61,7 +61,7 @@ bool is_device_ptr(const void* p)
 namespace {
 
 struct TimingRec {
-   std::array<hipEvent_t, 4> ev;
+   std::array<hipEvent_t, 6> ev;  // start / stop of the spread, grid and interp dispatches
 };
 
 struct PlanExt {
@@ -280,19 +280,32 @@ int plan_apply_dev(PlanExt* E, int grad, double alpha, const double* d_x, double
    TimingRec rec;
    if (P.timing) {
       rec = get_rec(E);
-      (void)hipEventRecord(rec.ev[0], s);
+      if (!P.md.on) P.kev = rec.ev.data();  // 1-D launchers attach the events to the dispatches
    }
-   if (P.md.on ? md_spread(P, d_x, P.md.d_grid, s) : launch_spread(P, d_x, P.d_part, s)) return -1;
-   if (P.timing) (void)hipEventRecord(rec.ev[1], s);
-   if (P.md.on ? md_grid(P, P.md.d_grid, grad, s) : launch_grid(P, P.d_part, P.nblocks, grad, s)) return -1;
-   if (P.timing) (void)hipEventRecord(rec.ev[2], s);
-   if (P.md.on ? md_interp(P, grad, alpha, d_x, beta, d_y, s) : launch_interp(P, grad, alpha, d_x, beta, d_y, s))
-      return -1;
-   if (P.timing) {
+   const bool mdt = P.timing && P.md.on;  // multi-feature windows: events recorded around each launch
+   int rc = 0;
+   if (mdt) (void)hipEventRecord(rec.ev[0], s);
+   rc = P.md.on ? md_spread(P, d_x, P.md.d_grid, s) : launch_spread(P, d_x, P.d_part, s);
+   if (mdt) {
+      (void)hipEventRecord(rec.ev[1], s);
+      (void)hipEventRecord(rec.ev[2], s);
+   }
+   if (!rc) rc = P.md.on ? md_grid(P, P.md.d_grid, grad, s) : launch_grid(P, P.d_part, P.nblocks, grad, s);
+   if (mdt) {
       (void)hipEventRecord(rec.ev[3], s);
-      E->pending.push_back(rec);
+      (void)hipEventRecord(rec.ev[4], s);
    }
-   return 0;
+   if (!rc)
+      rc = P.md.on ? md_interp(P, grad, alpha, d_x, beta, d_y, s) : launch_interp(P, grad, alpha, d_x, beta, d_y, s);
+   if (mdt) (void)hipEventRecord(rec.ev[5], s);
+   P.kev = nullptr;
+   if (P.timing) {
+      if (rc)
+         E->pool.push_back(rec);
+      else
+         E->pending.push_back(rec);
+   }
+   return rc ? -1 : 0;
 }
 
 int plan_apply(PlanExt* E, int n, int grad, double alpha, const double* x, double beta, double* y)
@@ -304,6 +317,13 @@ int plan_apply(PlanExt* E, int n, int grad, double alpha, const double* x, doubl
    }
    if (n != P.n) {
       fprintf(stderr, "nfft4gp_amd: matvec size %d does not match the handle (%d).\n", n, P.n);
+      return -1;
+   }
+   if (P.row_begin != 0 || P.row_end != P.n_global) {
+      // a row shard holds only its rows' share of the grids: its operator is the split-phase pair
+      // Nfft4GPAmdShardSpread -> (sum over shards) -> Nfft4GPAmdShardFinish, never a whole matvec
+      fprintf(stderr, "nfft4gp_amd: rows [%d, %d) of %d form a row shard; use Nfft4GPAmdShardSpread/ShardFinish.\n",
+              P.row_begin, P.row_end, P.n_global);
       return -1;
    }
    const size_t ny = (size_t)n * (grad ? 3 : 1);
@@ -426,6 +446,15 @@ void* additive_create(double* data, int n_global, int ldim, int* windows, int nw
 }  // namespace
 
 namespace nfft4gp_amd {
+bool additive_fused_dot_ok(void* str)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready) return false;
+   const AdditivePlan& P = E->P;
+   if (P.row_begin != 0 || P.row_end != P.n_global) return false;
+   return P.md.on || P.nblocks <= kRedMaxBlocks;
+}
+
 int additive_matvec_dot(void* str, const double* d_x, double* d_y, double* d_dot)
 {
    PlanExt* E = additive_plan(str);
@@ -589,10 +618,10 @@ int Nfft4GPAmdTimingQuery(void* str, double* ms, long long* cnt)
    if (!E) return -1;
    AdditivePlan& P = E->P;
    for (auto& r : E->pending) {
-      NFFT4GP_HIP_CHECK(hipEventSynchronize(r.ev[3]));
+      NFFT4GP_HIP_CHECK(hipEventSynchronize(r.ev[5]));
       for (int i = 0; i < 3; i++) {
          float t = 0.f;
-         NFFT4GP_HIP_CHECK(hipEventElapsedTime(&t, r.ev[i], r.ev[i + 1]));
+         NFFT4GP_HIP_CHECK(hipEventElapsedTime(&t, r.ev[2 * i], r.ev[2 * i + 1]));
          P.ms[i] += t;
          P.cnt[i]++;
       }

@@ -18,6 +18,7 @@
 // the launchers pick a variant from AdditivePlan (env NFFT4GP_AMD_SPREAD_VARIANT / _INTERP_VARIANT).
 // Rejected experiments (persistent workgroups, three-deep run rings, mixed-precision moments, the grid
 // step fused into the spread tail via global atomics) are in the git history; DESIGN.md has numbers.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -493,6 +494,16 @@ __global__ __launch_bounds__(THREADS) void k_interp(
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
+// plain launch, or (timing mode) a launch whose start / stop events are the dispatch's own timestamps
+template <typename F, typename... A>
+static void launch_ev(F fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, const hipEvent_t* ev, A... args)
+{
+   if (ev)
+      hipExtLaunchKernelGGL(fn, grid, block, (std::uint32_t)lds, s, ev[0], ev[1], 0u, args...);
+   else
+      hipLaunchKernelGGL(fn, grid, block, lds, s, args...);
+}
+
 static size_t spread_lds_bytes(const AdditivePlan& P)
 {
    return sizeof(double) * ((size_t)P.B + kPad + (size_t)P.CG * kNos * kMomStride);
@@ -576,24 +587,24 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
    const int gpw = std::min(std::max(P.gpw, 1), P.ngroups);
    const int nslices = (P.ngroups + gpw - 1) / gpw;
    const int gridx = ((P.nblocks + 7) / 8) * 8 * nslices;
-   hipLaunchKernelGGL(V.fn, dim3(gridx), dim3(V.threads), spread_lds_bytes(P), stream, P.dl.meta, P.dl.lo,
-                      P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, gpw, d_part);
+   launch_ev(V.fn, dim3(gridx), dim3(V.threads), spread_lds_bytes(P), stream, P.kev ? P.kev + 0 : nullptr, P.dl.meta,
+             P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, gpw, d_part);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
 
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream)
 {
-   hipLaunchKernelGGL(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, d_part, nparts, P.d_w, P.d_wd, P.d_H,
-                      P.d_Hd, grad, 0);
+   launch_ev(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, P.kev ? P.kev + 2 : nullptr, d_part, nparts,
+             (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 0);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
 
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream)
 {
-   hipLaunchKernelGGL(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, d_gridsum, 1, P.d_w, P.d_wd, P.d_H,
-                      P.d_Hd, grad, 1);
+   launch_ev(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, P.kev ? P.kev + 2 : nullptr, d_gridsum, 1,
+             (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 1);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -618,9 +629,9 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
       return -1;
    }
    const InterpFn fn = grad ? V.fn_grad : (d_dot ? V.fn_dot : V.fn);
-   hipLaunchKernelGGL(fn, dim3(P.nblocks), dim3(V.threads), interp_lds_bytes(P, grad), stream, P.dl.meta, P.dl.lo,
-                      P.dl.q, P.dl.tile_off, P.d_H, P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups, alpha, beta, P.f, P.mu,
-                      P.d_dot_part, P.d_dot_ticket, d_dot);
+   launch_ev(fn, dim3(P.nblocks), dim3(V.threads), interp_lds_bytes(P, grad), stream, P.kev ? P.kev + 4 : nullptr,
+             P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H, (const double*)P.d_Hd, d_x, d_y, P.n,
+             P.B, P.ngroups, alpha, beta, P.f, P.mu, P.d_dot_part, P.d_dot_ticket, d_dot);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

@@ -660,7 +660,7 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
    const int g = pcg_grid(N);
    const int ge = g;
    // this library's additive operator forms (q, p) in its own interpolation launch
-   const bool fused_dot = cb.mv_dev && matvec == &Nfft4GPAdditiveNFFTMatSymv;
+   const bool fused_dot = cb.mv_dev && matvec == &Nfft4GPAdditiveNFFTMatSymv && additive_fused_dot_ok(mat_data);
    // iterations in flight ahead of the host's status check (1 when printing every step)
    const int lag = print_level > 0 ? 1 : PcgScratch::kSlots;
    double prev_rel = rel_res_v[0];

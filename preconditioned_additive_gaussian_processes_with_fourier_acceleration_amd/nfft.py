@@ -37,6 +37,18 @@ def _ptr(a):
     return a.data_ptr(), a.is_cuda
 
 
+def _numel(a) -> int:
+    return int(a.size) if isinstance(a, np.ndarray) else int(a.numel())
+
+
+def _check_len(name, a, need, exact=True):
+    """The C entry points take raw pointers plus n: a short buffer would be read or written past its end
+    (a host heap overflow through the staging copy, or an out-of-bounds device write)."""
+    got = _numel(a)
+    if (got != need) if exact else (got < need):
+        raise ValueError(f"{name} has {got} entries; this call needs {'exactly' if exact else 'at least'} {need}")
+
+
 def _empty_like(x, n):
     if isinstance(x, np.ndarray):
         return np.zeros(n)
@@ -122,8 +134,12 @@ class NFFTAdditiveKernel:
         return rc
 
     def _apply(self, fn, x, alpha, beta, y, mult):
+        if self.row_begin != 0 or self.row_end != self.n_global:
+            raise ValueError("a row-shard handle has no whole matvec: use shard_spread / shard_finish")
+        _check_len("x", x, self.n)
         if y is None:
             y = _empty_like(x, mult * self.n)
+        _check_len("y", y, mult * self.n)
         xp, xd = _ptr(x)
         yp, yd = _ptr(y)
         rc = fn(self.h, self.n, float(alpha), xp, float(beta), yp)
@@ -141,6 +157,11 @@ class NFFTAdditiveKernel:
 
     # ---- split phase for row-sharded multi-GPU use -------------------------------------------
     def shard_spread(self, x_local, grid):
+        _check_len("x_local", x_local, self.n)
+        size = self.shard_grid_size()
+        if size < 0:
+            raise RuntimeError("run the kernel setup before shard_spread")
+        _check_len("grid", grid, size, exact=False)
         xp, _ = _ptr(x_local)
         gp, _ = _ptr(grid)
         if _lib.lib().Nfft4GPAmdShardSpread(self.h, xp, gp) != 0:
@@ -153,8 +174,14 @@ class NFFTAdditiveKernel:
         return int(_lib.lib().Nfft4GPAmdShardGridSize(self.h))
 
     def shard_finish(self, grid, x_local, alpha=1.0, beta=0.0, y_local=None, grad=False):
+        _check_len("x_local", x_local, self.n)
         if y_local is None:
             y_local = _empty_like(x_local, (3 if grad else 1) * self.n)
+        _check_len("y_local", y_local, (3 if grad else 1) * self.n)
+        size = self.shard_grid_size()
+        if size < 0:
+            raise RuntimeError("run the kernel setup before shard_finish")
+        _check_len("grid", grid, size, exact=False)
         gp, _ = _ptr(grid)
         xp, _ = _ptr(x_local)
         yp, _ = _ptr(y_local)
@@ -246,16 +273,20 @@ class NFFTKernel:
         return rc
 
     def matsymv(self, x, alpha=1.0, beta=0.0, y=None):
+        _check_len("x", x, self.n)
         if y is None:
             y = _empty_like(x, self.n)
+        _check_len("y", y, self.n)
         rc = _lib.lib().Nfft4GPNFFTMatSymv(self.adj, self.n, float(alpha), _ptr(x)[0], float(beta), _ptr(y)[0])
         if rc:
             raise RuntimeError("Nfft4GPNFFTMatSymv failed")
         return y
 
     def gradmatsymv(self, x, alpha=1.0, beta=0.0, y=None):
+        _check_len("x", x, self.n)
         if y is None:
             y = _empty_like(x, 3 * self.n)
+        _check_len("y", y, 3 * self.n)
         rc = _lib.lib().Nfft4GPNFFTGradMatSymv(self.adj, self.n, float(alpha), _ptr(x)[0], float(beta),
                                                _ptr(y)[0])
         if rc:

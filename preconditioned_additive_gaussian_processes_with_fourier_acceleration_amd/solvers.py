@@ -17,7 +17,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from .nfft import _ptr
+from .nfft import _check_len, _ptr
 
 
 class NystromPrecond:
@@ -79,6 +79,8 @@ class NystromPrecond:
             raise RuntimeError("Nfft4GPAmdNysCreate failed")
 
     def solve(self, x, rhs):
+        _check_len("x", x, self.n)
+        _check_len("rhs", rhs, self.n)
         rc = _lib.lib().Nfft4GPAmdNysSolve(self.h, self.n, _ptr(x)[0], _ptr(rhs)[0])
         if rc:
             raise RuntimeError("Nfft4GPAmdNysSolve failed")
@@ -106,6 +108,8 @@ class _Apply:
     _solve = _free = ""
 
     def solve(self, x, rhs):
+        _check_len("x", x, self.n)
+        _check_len("rhs", rhs, self.n)
         rc = getattr(_lib.lib(), self._solve)(self.h, self.n, _ptr(x)[0], _ptr(rhs)[0])
         if rc:
             raise RuntimeError(f"{self._solve} failed")
@@ -266,6 +270,8 @@ def pcg(op, b, x=None, maxits=1000, tol=1e-6, atol=False, precond=None, print_le
     if x is None:
         x = b * 0
     n = op.n
+    _check_len("b", b, n)
+    _check_len("x", x, n)
     rel = C.c_double()
     relv = _lib.dp()
     it = C.c_int()
@@ -287,6 +293,8 @@ def fgmres(op, b, x=None, kdim=50, maxits=1000, tol=1e-6, atol=False, precond=No
     if x is None:
         x = b * 0
     n = op.n
+    _check_len("b", b, n)
+    _check_len("x", x, n)
     rel = C.c_double()
     relv = _lib.dp()
     it = C.c_int()

@@ -181,9 +181,39 @@ def make_predict_synth():
     save("predict_synth", X=X, Xp=Xp, y=y, windows=win, hyper=hyper, maxits=200, tol=1e-10, mean=mean, std=std)
 
 
+def config_e_inputs(n, d, nvecs, seed=906):
+    """Seeded inputs of the reduced config-E loss case (regenerated identically by the GPU test):
+    X ~ U[0,1)^(n x d), labels ~ U(-0.5, 0.5), Rademacher probes (n x nvecs, +-1)."""
+    rng = np.random.default_rng(seed)
+    X = np.asfortranarray(rng.random((n, d)))
+    y = rng.random(n) - 0.5
+    R = np.where(np.random.default_rng(seed + 1).random((n, nvecs)) < 0.5, -1.0, 1.0)
+    return X, y, np.asfortranarray(R)
+
+
+def inv_softplus(v):
+    return float(np.log(np.expm1(v)))
+
+
+def make_config_e_reduced():
+    """(9) BASELINE configs[4] (n = 1e7, 64 additive 1-D windows, loss + gradient by stochastic trace
+    estimation) at a reduced n: the reference's Nfft4GPGpLoss (gp_loss.c:96-307, fgmres.c, lanczos.c in
+    oracle/_ref) on the oracle's NFFT operator, softplus transform, f = 1, l = 0.1, mu = 0.01.  Only
+    scalars are stored: the inputs come back from config_e_inputs(n, d, nvecs, seed)."""
+    n, d, nvecs, maxits, seed = 20000, 64, 4, 20, 906
+    X, y, R = config_e_inputs(n, d, nvecs, seed)
+    hyper = np.array([inv_softplus(1.0), inv_softplus(0.1), inv_softplus(0.01)])
+    win = np.arange(d, dtype=np.int32)
+    loss, grad = ref_gp_loss_nfft(X, win, d, 1, y, hyper, maxits, nvecs, R)
+    print(f"config_e_reduced: loss {loss!r} grad {grad!r}")
+    save("config_e_reduced", n=n, d=d, nvecs=nvecs, maxits=maxits, seed=seed, hyper=hyper, loss=loss, grad=grad)
+
+
 def main():
     if not ref_available():
         raise SystemExit("build oracle/_ref first: make -C oracle ref")
+    if sys.argv[1:] == ["config_e"]:
+        return make_config_e_reduced()
     if sys.argv[1:] == ["precond"]:
         return make_precond_synth()
     if sys.argv[1:] == ["krylov"]:
