@@ -498,26 +498,53 @@ struct RocSolver {
    decltype(&rocsolver_dsyevd) syevd = nullptr;
 };
 
+// first loadable of the given sonames (unversioned first: the ROCm install's own link), or nullptr with the
+// dlerror of each attempt appended to `why`
+void* dlopen_first(const char* const* names, std::string& why)
+{
+   for (const char* const* p = names; *p; ++p) {
+      if (void* h = dlopen(*p, RTLD_NOW | RTLD_GLOBAL)) return h;
+      const char* e = dlerror();
+      why += std::string("\n  ") + (e ? e : *p);
+   }
+   return nullptr;
+}
+
 RocSolver& rocsolver()
 {
    static RocSolver R;
    static bool tried = false;
    if (tried) return R;
    tried = true;
-   if (getenv("NFFT4GP_AMD_NO_ROCSOLVER") && atoi(getenv("NFFT4GP_AMD_NO_ROCSOLVER")) > 0) return R;
-   void* hb = dlopen("librocblas.so.5", RTLD_NOW | RTLD_GLOBAL);
-   if (!hb) hb = dlopen("/opt/rocm/lib/librocblas.so.5", RTLD_NOW | RTLD_GLOBAL);
-   void* hs = dlopen("librocsolver.so.0", RTLD_NOW | RTLD_GLOBAL);
-   if (!hs) hs = dlopen("/opt/rocm/lib/librocsolver.so.0", RTLD_NOW | RTLD_GLOBAL);
-   if (!hb || !hs) return R;
-   auto create = (decltype(&rocblas_create_handle))dlsym(hb, "rocblas_create_handle");
-   R.set_stream = (decltype(&rocblas_set_stream))dlsym(hb, "rocblas_set_stream");
-   R.potrf = (decltype(&rocsolver_dpotrf))dlsym(hs, "rocsolver_dpotrf");
-   R.trtri = (decltype(&rocsolver_dtrtri))dlsym(hs, "rocsolver_dtrtri");
-   R.syevd = (decltype(&rocsolver_dsyevd))dlsym(hs, "rocsolver_dsyevd");
-   if (!create || !R.set_stream || !R.potrf || !R.trtri || !R.syevd) return R;
-   if (create(&R.h) != rocblas_status_success) return R;
-   R.ok = true;
+   if (getenv("NFFT4GP_AMD_NO_ROCSOLVER") && atoi(getenv("NFFT4GP_AMD_NO_ROCSOLVER")) > 0) {
+      fprintf(stderr, "nfft4gp_amd: NFFT4GP_AMD_NO_ROCSOLVER set: k x k Cholesky / inverse / eigensolves run on "
+                      "the host.\n");
+      return R;
+   }
+   static const char* const blas_names[] = {"librocblas.so", "librocblas.so.5", "librocblas.so.4",
+                                            "/opt/rocm/lib/librocblas.so", "/opt/rocm/lib/librocblas.so.5", nullptr};
+   static const char* const solver_names[] = {"librocsolver.so", "librocsolver.so.0",
+                                              "/opt/rocm/lib/librocsolver.so", "/opt/rocm/lib/librocsolver.so.0",
+                                              nullptr};
+   std::string why;
+   void* hb = dlopen_first(blas_names, why);
+   void* hs = hb ? dlopen_first(solver_names, why) : nullptr;
+   auto create = hb ? (decltype(&rocblas_create_handle))dlsym(hb, "rocblas_create_handle") : nullptr;
+   if (hb && hs) {
+      R.set_stream = (decltype(&rocblas_set_stream))dlsym(hb, "rocblas_set_stream");
+      R.potrf = (decltype(&rocsolver_dpotrf))dlsym(hs, "rocsolver_dpotrf");
+      R.trtri = (decltype(&rocsolver_dtrtri))dlsym(hs, "rocsolver_dtrtri");
+      R.syevd = (decltype(&rocsolver_dsyevd))dlsym(hs, "rocsolver_dsyevd");
+      if (!create || !R.set_stream || !R.potrf || !R.trtri || !R.syevd)
+         why += "\n  a rocBLAS / rocSOLVER entry point is missing";
+      else if (create(&R.h) != rocblas_status_success)
+         why += "\n  rocblas_create_handle failed";
+      else
+         R.ok = true;
+   }
+   if (!R.ok)
+      fprintf(stderr, "nfft4gp_amd: rocSOLVER could not be loaded; k x k Cholesky / inverse / eigensolves run on "
+                      "the host (slower, same results to rounding):%s\n", why.c_str());
    return R;
 }
 

@@ -8,6 +8,7 @@ Writes one CSV row per (kernel, counter): the mean value per dispatch.  Counter 
 """
 import argparse
 import csv
+import re
 import os
 import shutil
 import subprocess
@@ -72,7 +73,8 @@ def main():
                 if key is None:
                     continue
                 # template instances: keep the variant in the key (interp plain / grad / dot)
-                variant = name.split("(")[0].split("::")[-1]
+                m = re.search(r"(k_\w+(?:<[^()]*>)?)", name)
+                variant = m.group(1) if m else key
                 s = sums.setdefault((variant, row["Counter_Name"]), {})
                 s.setdefault(row.get("Dispatch_Id", len(s)), 0.0)
                 s[row.get("Dispatch_Id", len(s))] += float(row["Counter_Value"])
