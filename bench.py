@@ -7,9 +7,12 @@ vector x ~ U(-0.5, 0.5) (TESTS/TEST1/foo.cpp:243-247), numpy PCG64 seed 906 (syn
 One "step" = one Nfft4GPAdditiveNFFTMatSymv(y = K x) with x and y resident in HBM.
 
 N = 1:  the matvec on one GPU.
-N > 1:  one process per GPU (torch.distributed, RCCL).  Rows are sharded: each rank spreads its own
-        n/N points for all 32 windows, the 32x64 oversampled grids (16 KB) are all-reduced over
-        xGMI, and each rank interpolates its own rows.  Total work is fixed -> "scaling": "strong".
+N > 1:  one process per GPU (torch.distributed launches the ranks; the library's own RCCL communicator
+        does the all-reduces over xGMI, enqueued on the stream by dist.hip).  The headline splits ROWS:
+        each rank spreads its own n/N points for all 32 windows, the 32x64 oversampled grids (16 KB) are
+        all-reduced, each rank interpolates its own rows.  The line also carries the split BASELINE
+        configs[3] names, 4 COMPONENTS per GPU (y, 8 MB, all-reduced), timed the same way
+        ("partition_components").  Total work is fixed -> "scaling": "strong".
 
 Printed (rank 0): one JSON line with value = whole-job matvecs/s, the roofline of the dominant kernel
 (measured live with hipEvents on the library stream), the CPU baseline (this repo's C/OpenMP
@@ -163,23 +166,36 @@ def pmc_traffic(n, d, timeout=600):
     return out
 
 
-def run_pcg_single(op, torch, n, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1):
+def run_pcg_single(op, torch, n, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1, rows=None, dist=None,
+                   prefix="pcg"):
     """PCG to 1e-6 on the same points.  At l = 1 the NFFT-approximated kernel of this data is
     indefinite (bhat_k < 0 for a Gaussian truncated at r = 1/2; DESIGN.md 'SPD'), which is why the
-    reference solves with FGMRES; CG needs an SPD operator, so it runs at l = 0.1 (all bhat_k > 0)."""
+    reference solves with FGMRES; CG needs an SPD operator, so it runs at l = 0.1 (all bhat_k > 0).
+    With a distributed operator (N > 1) the same Nfft4GPSolverPcg runs on this rank's rows (rows =
+    (rb, re)); the time is the max over ranks."""
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
     assert op.setup(amd.GAUSSIAN, f=1.0, l=l_pcg, mu=0.01) == 0
+    rb, re = rows if rows is not None else (0, n)
     rng = np.random.default_rng(rng_seed + 1)
-    b = torch.tensor(rng.random(n) - 0.5, device="cuda")
-    x = torch.zeros(n, dtype=torch.float64, device="cuda")
+    b = torch.tensor((rng.random(n) - 0.5)[rb:re], device="cuda")
+    x = torch.zeros(re - rb, dtype=torch.float64, device="cuda")
     torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
     t0 = time.time()
     _, relres, hist, iters = amd.pcg(op, b, x, maxits=maxits, tol=tol)
     torch.cuda.synchronize()
     t = time.time() - t0
-    return {"pcg_time_s": t, "pcg_iters": iters, "pcg_rel_res": relres, "pcg_converged": iters > 0,
-            "pcg_precond": "none", "pcg_tol": tol, "pcg_l": l_pcg,
-            "pcg_ms_per_iter": 1e3 * t / max(iters if iters > 0 else len(hist) - 1, 1)}
+    if dist is not None:
+        tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    out = {"_time_s": t, "_iters": iters, "_rel_res": relres, "_converged": iters > 0, "_tol": tol, "_l": l_pcg,
+           "_ms_per_iter": 1e3 * t / max(iters if iters > 0 else len(hist) - 1, 1)}
+    out = {prefix + k: v for k, v in out.items()}
+    if prefix == "pcg":
+        out["pcg_precond"] = "none"
+    return out
 
 
 def run_pcg_nystrom(op, torch, n, k, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1):
@@ -272,27 +288,6 @@ def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000
             key + "_total_s": t_setup + t, key + "_apply_ms": 1e3 * t_apply}
 
 
-def run_pcg_sharded(op, sop, torch, dist, n, rb, re, tol=1e-6, maxits=3000, l_pcg=0.1):
-    """Row-sharded CG (dist.py, pcg.c semantics): local HIP BLAS-1 + scalar all-reduces."""
-    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
-    from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import GpuVecOps
-    assert op.setup(amd.GAUSSIAN, f=1.0, l=l_pcg, mu=0.01) == 0
-    rng = np.random.default_rng(906 + 1)
-    b = torch.tensor((rng.random(n) - 0.5)[rb:re], device="cuda")
-    x = torch.zeros(re - rb, dtype=torch.float64, device="cuda")
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.time()
-    _, relres, hist, iters = sop.pcg(b, x, maxits=maxits, tol=tol, vec=GpuVecOps())
-    torch.cuda.synchronize()
-    t = torch.tensor([time.time() - t0], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    t = float(t.item())
-    return {"pcg_time_s": t, "pcg_iters": iters, "pcg_rel_res": relres, "pcg_converged": iters > 0,
-            "pcg_precond": "none", "pcg_tol": tol, "pcg_l": l_pcg, "pcg_impl": "row-sharded (dist.py)",
-            "pcg_ms_per_iter": 1e3 * t / max(iters if iters > 0 else len(hist) - 1, 1)}
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -309,6 +304,8 @@ def main():
                     help="AFN Schur-complement solve: kernel FSAI (schur_opt 3), I/mu (0) or both")
     ap.add_argument("--afn-order", default="random", choices=["random", "fps", "both"],
                     help="AFN landmark order: random (perm_opt 0) or farthest points (1)")
+    ap.add_argument("--partition", default="rows", choices=["rows", "components"],
+                    help="N > 1: the headline split (the other one is timed too)")
     ap.add_argument("--kernel-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--kernel-only-nys", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -335,14 +332,19 @@ def main():
     n, d = args.n, args.d
     X, x_host = make_problem(n, d)
     win = np.arange(d, dtype=np.int32)
+    comm = None
     if world == 1:
         op = amd.NFFTAdditiveKernel(X, win, d, 1)
         rb, re = 0, n
     else:
         from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import (
-            RowShardedAdditiveKernel, row_range)
-        rb, re = row_range(n, rank, world)
-        op = amd.NFFTAdditiveKernel(X, win, d, 1, shard=(rb, re))
+            Communicator, DistributedAdditiveKernel)
+        # RCCL; the gloo rehearsal of several ranks on one GPU (RCCL refuses that) uses the group's own
+        # all-reduce through a staging buffer instead
+        gloo = os.environ.get("NFFT4GP_BENCH_BACKEND", "nccl") == "gloo"
+        comm = Communicator.callback() if gloo else Communicator.rccl()
+        op = DistributedAdditiveKernel(X, win, d, 1, comm, partition=args.partition)
+        rb, re = op.row_begin, op.row_end
     t0 = time.time()
     rc = op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01)
     setup_s = time.time() - t0
@@ -350,13 +352,11 @@ def main():
         raise SystemExit("setup failed")
     xd = torch.tensor(x_host[rb:re], device="cuda")
     yd = torch.zeros(re - rb, dtype=torch.float64, device="cuda")
-    sop = RowShardedAdditiveKernel(op, d, n, rb, re) if world > 1 else None
 
     def step():
-        if world == 1:
-            op.matsymv(xd, 1.0, 0.0, yd)
-        else:
-            sop.matsymv(xd, 1.0, 0.0, yd)  # local spread -> all-reduce of the 32x64 grids -> local interp
+        # N = 1: the whole matvec.  N > 1, rows: local spread -> all-reduce of the 32x64 grids -> local
+        # interpolation; components: local windows -> all-reduce of y
+        op.matsymv(xd, 1.0, 0.0, yd)
 
     # The PCG legs (the metric's second half) run first: their ~1e3 matvecs also bring the GPU out of its
     # idle clock state, which otherwise costs the first few hundred matvecs ~15 % (tools/warm_probe.py:
@@ -426,6 +426,26 @@ def main():
     # per-kernel durations of the roofline
     elapsed, _ = timed(False)
     elapsed_inst, kern_avg = timed(True) if world == 1 else (None, None)
+    alt = None
+    if world > 1:
+        # the other split, timed the same way (W warmup + K steps between barriers, max over ranks)
+        other = "components" if args.partition == "rows" else "rows"
+        op2 = DistributedAdditiveKernel(X, win, d, 1, comm, partition=other)
+        if op2.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) != 0:
+            raise SystemExit("setup failed")
+        x2 = torch.tensor(x_host[op2.row_begin:op2.row_end], device="cuda")
+        y2 = torch.zeros(op2.n, dtype=torch.float64, device="cuda")
+        op_main, xd_main, yd_main = op, xd, yd
+        op, xd, yd = op2, x2, y2
+        for _ in range(args.warmup):
+            step()
+        el2, _ = timed(False)
+        alt = {"partition": other, "value": args.steps / el2, "ms_per_step": 1e3 * el2 / args.steps,
+               "all_reduce_bytes_per_matvec": 8 * (op2.n if other == "components" else d * 64)}
+        if not args.no_pcg:
+            alt.update(run_pcg_single(op2, torch, n, rows=(op2.row_begin, op2.row_end), dist=dist))
+        op2.free()
+        op, xd, yd = op_main, xd_main, yd_main
     headline = n == 1_000_000 and d == 32
     cfg_tag = "BASELINE configs[2]" if headline else "reduced size, not a BASELINE config" \
         if (n, d) != (100_000, 8) else "BASELINE configs[1] sizes"
@@ -445,9 +465,9 @@ def main():
         "dtype": "f64",
         "data": "synthetic: X ~ U[0,1)^d, x ~ U(-0.5,0.5), numpy PCG64 seed 906",
         "config": {"workload": f"additive NFFT matvec, n={n}, d={d}, {d} x 1-D windows, Gaussian f=1 l=1 "
-                               f"mu=0.01 ({cfg_tag}); N>1: rows sharded, {d}x64 grid all-reduce",
+                               f"mu=0.01 ({cfg_tag})" + (f"; {world} GPUs, {args.partition} sharded" if world > 1 else ""),
                    "n": n, "d": d, "nwindows": d, "setup_s": setup_s,
-                   "parallelism": f"rows{world}" if world > 1 else "single"},
+                   "parallelism": f"{args.partition}{world}" if world > 1 else "single"},
     }
     if world == 1:
         result.update(pcg)
@@ -500,11 +520,19 @@ def main():
                 result["cpu_baseline"] = cpu_baseline(n, d, X, x_host)
             except Exception as e:  # report, do not fail the GPU measurement
                 result["cpu_baseline"] = {"value": None, "error": repr(e)}
-    if world > 1 and not args.no_pcg:
-        result.update(run_pcg_sharded(op, sop, torch, dist, n, rb, re))
+    if world > 1:
+        result["config"]["all_reduce_bytes_per_matvec"] = 8 * (op.n if args.partition == "components" else d * 64)
+        result["config"]["communicator"] = ("gloo rehearsal (host all-reduce)" if gloo else
+                                            "RCCL (library-owned ncclComm, all-reduce enqueued by dist.hip)")
+        if not args.no_pcg:
+            result.update(run_pcg_single(op, torch, n, rows=(rb, re), dist=dist))
+            result["pcg_impl"] = f"Nfft4GPSolverPcg on Nfft4GPAmdDistMatSymv ({args.partition}), device-controlled"
+        result["partition_" + alt["partition"]] = alt
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
+        op.free()
+        comm.free()
         dist.destroy_process_group()
 
 

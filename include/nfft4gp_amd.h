@@ -422,6 +422,51 @@ int Nfft4GPAmdShardFinish(void *str, const NFFT4GP_DOUBLE *grid, int grad, NFFT4
  * every window is 1-D, nwindows * 64^dmax otherwise (the real spread grids of multi-feature windows) */
 long long Nfft4GPAmdShardGridSize(void *str);
 
+/* ---- multi-GPU operators (one process per GPU) ----------------------------------------
+ * The reference is single-process: its additive matvec loops the components sequentially into _dwork
+ * (nfft_interface.c:796-817) and its PCG (pcg.c:3-206) works on whole vectors.  Here the operator is
+ * split over a communicator and stays a func_symmatvec, so Nfft4GPSolverPcg drives it unchanged.
+ *
+ * Communicators.  Nfft4GPAmdCommCreateRccl: RCCL over xGMI (librccl, the copy PyTorch mapped), every
+ * all-reduce enqueued on the library stream; rank 0 makes the id with Nfft4GPAmdCommUniqueId (128 bytes)
+ * and the caller broadcasts it.  Nfft4GPAmdCommCreateCallback: the caller's all-reduce (e.g. a gloo
+ * process group), called with a device staging buffer of `capacity` doubles it owns; it must leave the
+ * elementwise sum over the ranks in place.  Both return NULL on failure. */
+typedef int (*Nfft4GPAmdAllreduceFn)(void *ctx, NFFT4GP_DOUBLE *d_buf, long long count);
+int Nfft4GPAmdCommUniqueId(void *id128);
+void *Nfft4GPAmdCommCreateRccl(int rank, int world, const void *id128);
+void *Nfft4GPAmdCommCreateCallback(int rank, int world, Nfft4GPAmdAllreduceFn fn, void *ctx,
+                                   NFFT4GP_DOUBLE *d_stage, long long capacity);
+/* sum of count doubles at d_buf (device) over the ranks, in place, on the library stream */
+int Nfft4GPAmdCommAllreduce(void *comm, NFFT4GP_DOUBLE *d_buf, long long count);
+void Nfft4GPAmdCommFree(void *comm);
+
+/* Component shard: a whole-row additive handle over a subset of the windows, weighted 1/nw_global (the
+ * whole operator's 1/nwindows, nfft_interface.c:806); own_diag = 1 on exactly one rank, which adds the
+ * mu x term (and the gradient's f^2 x block).  Call before the kernel setup.  The ranks' y sum to the
+ * whole operator's. */
+int Nfft4GPAmdAdditiveComponentShard(void *str, int nw_global, int own_diag);
+/* Distributed operator over `comm`.  kind 0 (rows): `handle` from Nfft4GPAmdAdditiveShardCreate; x, y
+ * hold this rank's rows; one all-reduce of the Nfft4GPAmdShardGridSize grid per matvec.  kind 1
+ * (components): `handle` a component shard; x, y are whole (replicated) vectors; one all-reduce of y
+ * (n, 3n for the gradient) per matvec.  Free it before its handle and communicator. */
+void *Nfft4GPAmdDistCreate(void *handle, int kind, void *comm);
+void Nfft4GPAmdDistFree(void *dop);
+/* func_symmatvec on device vectors (n = this rank's rows for kind 0, n_global for kind 1).  Given to
+ * Nfft4GPSolverPcg, the solver sums its dot products over the communicator (kind 0) and clamps maxits
+ * to the global n, so its iterations equal the single-GPU solver's up to rounding. */
+int Nfft4GPAmdDistMatSymv(void *dop, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE beta,
+                          NFFT4GP_DOUBLE *y);
+int Nfft4GPAmdDistGradMatSymv(void *dop, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE beta,
+                              NFFT4GP_DOUBLE *y);
+/* Row-sharded Nystrom apply (nys.c:115-173 over row shards): keeps rows [row_begin, row_end) of a
+ * Nystrom preconditioner's U (Nfft4GPAmdNysCreate / Nfft4GPAmdNysSetupAdditive; copied, the source may
+ * be freed); the apply is a local U^T r, a k-vector all-reduce and a local U w + r/eta.  func_solve on
+ * this rank's rows (device). */
+void *Nfft4GPAmdNysShard(void *nys, int row_begin, int row_end, void *comm);
+int Nfft4GPAmdDistNysSolve(void *dnys, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
+void Nfft4GPAmdDistNysFree(void *dnys);
+
 /* ---- host-only helpers (no GPU needed): the setup math of the device plan, exported so the CPU
  * test-suite can check it and emulate the kernels against the oracle ------------------------------- */
 /* tap polynomial coefficients C[t*NC + d], t = 0..9, d = 0..NC-1 (monomials in u = frac - 1/2);

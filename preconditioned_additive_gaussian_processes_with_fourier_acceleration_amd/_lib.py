@@ -19,6 +19,7 @@ vp = C.c_void_p
 
 SYMMATVEC = C.CFUNCTYPE(C.c_int, vp, C.c_int, C.c_double, vp, C.c_double, vp)
 SOLVE = C.CFUNCTYPE(C.c_int, vp, C.c_int, vp, vp)
+ALLREDUCE = C.CFUNCTYPE(C.c_int, vp, vp, C.c_longlong)  # Nfft4GPAmdAllreduceFn
 
 
 class NfftKernelStruct(C.Structure):
@@ -146,6 +147,19 @@ _SIGS = {
     "Nfft4GPAmdShardSpread": (C.c_int, [vp, vp, vp]),
     "Nfft4GPAmdShardFinish": (C.c_int, [vp, vp, C.c_int, C.c_double, vp, C.c_double, vp]),
     "Nfft4GPAmdShardGridSize": (C.c_longlong, [vp]),
+    "Nfft4GPAmdCommUniqueId": (C.c_int, [vp]),
+    "Nfft4GPAmdCommCreateRccl": (vp, [C.c_int, C.c_int, vp]),
+    "Nfft4GPAmdCommCreateCallback": (vp, [C.c_int, C.c_int, ALLREDUCE, vp, vp, C.c_longlong]),
+    "Nfft4GPAmdCommAllreduce": (C.c_int, [vp, vp, C.c_longlong]),
+    "Nfft4GPAmdCommFree": (None, [vp]),
+    "Nfft4GPAmdAdditiveComponentShard": (C.c_int, [vp, C.c_int, C.c_int]),
+    "Nfft4GPAmdDistCreate": (vp, [vp, C.c_int, vp]),
+    "Nfft4GPAmdDistFree": (None, [vp]),
+    "Nfft4GPAmdDistMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),
+    "Nfft4GPAmdDistGradMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),
+    "Nfft4GPAmdNysShard": (vp, [vp, C.c_int, C.c_int, vp]),
+    "Nfft4GPAmdDistNysSolve": (C.c_int, [vp, C.c_int, vp, vp]),
+    "Nfft4GPAmdDistNysFree": (None, [vp]),
     "Nfft4GPAmdHostTapPoly": (C.c_int, [vp]),
     "Nfft4GPAmdHostCirculant": (C.c_int, [C.c_int, C.c_double, C.c_double, vp, vp]),
     "Nfft4GPAmdHostPrepare": (C.c_double, [vp, C.c_int, vp]),

@@ -1,0 +1,398 @@
+// dist.hip -- the additive operator and the Nystrom apply split over one process per GPU.
+//
+// The reference is one process: Nfft4GPAdditiveNFFTMatSymv runs its components one after another into
+// _dwork (nfft_interface.c:796-817) and Nfft4GPSolverPcg (pcg.c:3-206) works on whole vectors.  The sum
+// over components and the sum over points are both independent, so the operator splits two ways
+// (DESIGN 6):
+//   rows        each rank spreads its own points for every window, the nw x 64 grids (16 KB at config D;
+//               nw x 64^d for multi-feature windows) are all-reduced, each rank interpolates its rows.
+//               PCG vectors stay row-sharded, so Nfft4GPSolverPcg sums its dots over the communicator.
+//   components  each rank holds a subset of the windows for all points; y (n doubles) is all-reduced and
+//               the vectors are replicated (the dots need no communication).
+// Communicators: RCCL (librccl.so.1 dlopen'ed -- the copy PyTorch maps -- one ncclComm per process, every
+// all-reduce enqueued on the library stream, no host synchronisation), or a caller's all-reduce callback
+// on a device staging buffer (the gloo process group of the one-GPU tests).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types and prototypes only: the library is dlopen'ed on first use
+
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "internal.h"
+
+using namespace nfft4gp_amd;
+
+namespace {
+
+struct RcclApi {
+   bool ok = false;
+   decltype(&ncclGetUniqueId) get_id = nullptr;
+   decltype(&ncclCommInitRank) init_rank = nullptr;
+   decltype(&ncclAllReduce) all_reduce = nullptr;
+   decltype(&ncclCommDestroy) destroy = nullptr;
+   decltype(&ncclGetErrorString) err = nullptr;
+};
+
+RcclApi& rccl()
+{
+   static RcclApi R;
+   static bool tried = false;
+   if (tried) return R;
+   tried = true;
+   // the soname first: it matches the copy PyTorch's nccl process group already mapped (one RCCL per process)
+   static const char* const names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1", nullptr};
+   std::string why;
+   void* h = nullptr;
+   for (const char* const* p = names; *p && !h; ++p) {
+      h = dlopen(*p, RTLD_NOW | RTLD_GLOBAL);
+      if (!h) {
+         const char* e = dlerror();
+         why += std::string("\n  ") + (e ? e : *p);
+      }
+   }
+   if (h) {
+      R.get_id = (decltype(&ncclGetUniqueId))dlsym(h, "ncclGetUniqueId");
+      R.init_rank = (decltype(&ncclCommInitRank))dlsym(h, "ncclCommInitRank");
+      R.all_reduce = (decltype(&ncclAllReduce))dlsym(h, "ncclAllReduce");
+      R.destroy = (decltype(&ncclCommDestroy))dlsym(h, "ncclCommDestroy");
+      R.err = (decltype(&ncclGetErrorString))dlsym(h, "ncclGetErrorString");
+      R.ok = R.get_id && R.init_rank && R.all_reduce && R.destroy && R.err;
+      if (!R.ok) why += "\n  an RCCL entry point is missing";
+   }
+   if (!R.ok) fprintf(stderr, "nfft4gp_amd: RCCL could not be loaded:%s\n", why.c_str());
+   return R;
+}
+
+struct CommRccl : Comm {
+   ncclComm_t c = nullptr;
+   int allreduce(double* d_buf, size_t count, hipStream_t s) override
+   {
+      if (count == 0) return 0;
+      const ncclResult_t r = rccl().all_reduce(d_buf, d_buf, count, ncclDouble, ncclSum, c, s);
+      if (r != ncclSuccess) {
+         fprintf(stderr, "nfft4gp_amd: ncclAllReduce: %s\n", rccl().err(r));
+         return -1;
+      }
+      return 0;
+   }
+   ~CommRccl() override
+   {
+      if (c) rccl().destroy(c);
+   }
+};
+
+struct CommCallback : Comm {
+   Nfft4GPAmdAllreduceFn fn = nullptr;
+   void* ctx = nullptr;
+   double* stage = nullptr;  // the caller's device buffer
+   size_t cap = 0;
+   int allreduce(double* d_buf, size_t count, hipStream_t s) override
+   {
+      for (size_t off = 0; off < count; off += cap) {
+         const size_t m = std::min(cap, count - off);
+         NFFT4GP_HIP_CHECK(hipMemcpyAsync(stage, d_buf + off, sizeof(double) * m, hipMemcpyDeviceToDevice, s));
+         if (fn(ctx, stage, (long long)m)) {
+            fprintf(stderr, "nfft4gp_amd: the all-reduce callback failed\n");
+            return -1;
+         }
+         NFFT4GP_HIP_CHECK(hipMemcpyAsync(d_buf + off, stage, sizeof(double) * m, hipMemcpyDeviceToDevice, s));
+      }
+      return 0;
+   }
+};
+
+// y = beta y + t  (component shards with beta != 0)
+__global__ void k_axpby_add(double beta, double* __restrict__ y, const double* __restrict__ t, size_t n)
+{
+   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+      y[i] = (beta == 0.0 ? 0.0 : beta * y[i]) + t[i];
+}
+
+struct DistOp {
+   int kind = 0;  // 0 rows, 1 components
+   void* h = nullptr;
+   Comm* comm = nullptr;
+   int n_local = 0, n_global = 0;
+   double* d_grid = nullptr;
+   size_t grid_count = 0;
+   double* d_tmp = nullptr;  // components, beta != 0: 3 n
+};
+
+int grid_ready(DistOp* D)
+{
+   const long long g = Nfft4GPAmdShardGridSize(D->h);
+   if (g < 0) {
+      fprintf(stderr, "nfft4gp_amd: distributed matvec before the kernel setup\n");
+      return -1;
+   }
+   if (D->d_grid && D->grid_count == (size_t)g) return 0;
+   if (D->d_grid) (void)hipFree(D->d_grid);
+   D->d_grid = nullptr;
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&D->d_grid, sizeof(double) * std::max<size_t>(1, (size_t)g)));
+   D->grid_count = (size_t)g;
+   return 0;
+}
+
+int dist_apply(DistOp* D, int n, int grad, double alpha, double* x, double beta, double* y)
+{
+   if (!D) return -1;
+   const int want = D->kind == 0 ? D->n_local : D->n_global;
+   if (n != want) {
+      fprintf(stderr, "nfft4gp_amd: distributed matvec size %d, this rank holds %d\n", n, want);
+      return -1;
+   }
+   if ((n > 0 && (!is_device_ptr(x) || !is_device_ptr(y)))) {
+      fprintf(stderr, "nfft4gp_amd: the distributed operators take device vectors\n");
+      return -1;
+   }
+   hipStream_t s = current_stream();
+   if (D->kind == 0) {
+      if (grid_ready(D)) return -1;
+      if (Nfft4GPAmdShardSpread(D->h, x, D->d_grid)) return -1;
+      if (D->comm->allreduce(D->d_grid, D->grid_count, s)) return -1;
+      return Nfft4GPAmdShardFinish(D->h, D->d_grid, grad, alpha, x, beta, y);
+   }
+   const size_t ny = (size_t)n * (grad ? 3 : 1);
+   double* out = y;
+   if (beta != 0.0) {
+      if (!D->d_tmp) NFFT4GP_HIP_CHECK(hipMalloc((void**)&D->d_tmp, sizeof(double) * 3 * std::max<size_t>(1, n)));
+      out = D->d_tmp;
+   }
+   const int rc = grad ? Nfft4GPAdditiveNFFTGradMatSymv(D->h, n, alpha, x, 0.0, out)
+                       : Nfft4GPAdditiveNFFTMatSymv(D->h, n, alpha, x, 0.0, out);
+   if (rc || D->comm->allreduce(out, ny, s)) return -1;
+   if (beta != 0.0) {
+      const int g = (int)std::min<size_t>(4096, (ny + 255) / 256);
+      hipLaunchKernelGGL(k_axpby_add, dim3(std::max(g, 1)), dim3(256), 0, s, beta, y, (const double*)D->d_tmp, ny);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+   }
+   return 0;
+}
+
+// ---- row-sharded Nystrom apply ----------------------------------------------------------------------
+__global__ void k_dnys_scale(double* __restrict__ w, const double* __restrict__ s, int k, double eta)
+{
+   const int j = blockIdx.x * blockDim.x + threadIdx.x;
+   if (j < k) {
+      const double t = w[j];
+      w[j] = s[j] * t - t / eta;  // the expression of the one-GPU apply (solvers.hip k_nys_w)
+   }
+}
+
+struct DistNys {
+   NysDev* N = nullptr;  // this rank's rows of U (n = local rows), s, eta, scratch
+   Comm* comm = nullptr;
+};
+
+}  // namespace
+
+namespace nfft4gp_amd {
+int dist_pcg_info(void* dop, DistPcgInfo& info)
+{
+   DistOp* D = (DistOp*)dop;
+   if (!D) return -1;
+   info.n_global = D->n_global;
+   info.dot_comm = D->kind == 0 ? D->comm : nullptr;
+   info.fused_dot = D->kind == 0 && shard_fused_dot_ok(D->h);
+   return 0;
+}
+
+int dist_matvec_dot(void* dop, const double* d_p, double* d_q, double* d_dot)
+{
+   DistOp* D = (DistOp*)dop;
+   if (!D || D->kind != 0 || grid_ready(D)) return -1;
+   if (Nfft4GPAmdShardSpread(D->h, d_p, D->d_grid)) return -1;
+   if (D->comm->allreduce(D->d_grid, D->grid_count, current_stream())) return -1;
+   return shard_finish_dot(D->h, D->d_grid, d_p, d_q, d_dot);
+}
+
+// the row-sharded apply (nys.c:115-173 over row shards); implemented with the one-GPU apply's kernels
+int nys_apply_rows(NysDev* N, Comm* comm, double* x, const double* rhs, hipStream_t s);
+}  // namespace nfft4gp_amd
+
+extern "C" {
+
+int Nfft4GPAmdCommUniqueId(void* id128)
+{
+   RcclApi& R = rccl();
+   if (!R.ok || !id128) return -1;
+   ncclUniqueId id;
+   const ncclResult_t r = R.get_id(&id);
+   if (r != ncclSuccess) {
+      fprintf(stderr, "nfft4gp_amd: ncclGetUniqueId: %s\n", R.err(r));
+      return -1;
+   }
+   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+   memcpy(id128, &id, sizeof(id));
+   return 0;
+}
+
+void* Nfft4GPAmdCommCreateRccl(int rank, int world, const void* id128)
+{
+   if (!device_ok() || !id128 || world < 1 || rank < 0 || rank >= world) return nullptr;
+   RcclApi& R = rccl();
+   if (!R.ok) return nullptr;
+   ncclUniqueId id;
+   memcpy(&id, id128, sizeof(id));
+   CommRccl* C = new CommRccl();
+   C->rank = rank;
+   C->world = world;
+   const ncclResult_t r = R.init_rank(&C->c, world, id, rank);
+   if (r != ncclSuccess) {
+      fprintf(stderr, "nfft4gp_amd: ncclCommInitRank (rank %d of %d): %s\n", rank, world, R.err(r));
+      C->c = nullptr;
+      delete C;
+      return nullptr;
+   }
+   return C;
+}
+
+void* Nfft4GPAmdCommCreateCallback(int rank, int world, Nfft4GPAmdAllreduceFn fn, void* ctx, double* d_stage,
+                                   long long capacity)
+{
+   if (!fn || !d_stage || capacity <= 0 || world < 1 || rank < 0 || rank >= world) return nullptr;
+   if (!is_device_ptr(d_stage)) {
+      fprintf(stderr, "nfft4gp_amd: the all-reduce staging buffer must be device memory\n");
+      return nullptr;
+   }
+   CommCallback* C = new CommCallback();
+   C->rank = rank;
+   C->world = world;
+   C->fn = fn;
+   C->ctx = ctx;
+   C->stage = d_stage;
+   C->cap = (size_t)capacity;
+   return C;
+}
+
+int Nfft4GPAmdCommAllreduce(void* comm, double* d_buf, long long count)
+{
+   if (!comm || count < 0) return -1;
+   return ((Comm*)comm)->allreduce(d_buf, (size_t)count, current_stream());
+}
+
+void Nfft4GPAmdCommFree(void* comm)
+{
+   if (!comm) return;
+   (void)hipStreamSynchronize(current_stream());
+   delete (Comm*)comm;
+}
+
+void* Nfft4GPAmdDistCreate(void* handle, int kind, void* comm)
+{
+   int nl = 0, ng = 0, rb = 0;
+   if (!comm || (kind != 0 && kind != 1) || additive_rows(handle, &nl, &ng, &rb)) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdDistCreate needs an additive handle, kind 0 or 1 and a communicator\n");
+      return nullptr;
+   }
+   if (kind == 1 && nl != ng) {
+      fprintf(stderr, "nfft4gp_amd: a component-sharded operator needs a whole-row handle\n");
+      return nullptr;
+   }
+   DistOp* D = new DistOp();
+   D->kind = kind;
+   D->h = handle;
+   D->comm = (Comm*)comm;
+   D->n_local = nl;
+   D->n_global = ng;
+   return D;
+}
+
+void Nfft4GPAmdDistFree(void* dop)
+{
+   DistOp* D = (DistOp*)dop;
+   if (!D) return;
+   (void)hipStreamSynchronize(current_stream());
+   if (D->d_grid) (void)hipFree(D->d_grid);
+   if (D->d_tmp) (void)hipFree(D->d_tmp);
+   delete D;
+}
+
+int Nfft4GPAmdDistMatSymv(void* dop, int n, double alpha, double* x, double beta, double* y)
+{
+   return dist_apply((DistOp*)dop, n, 0, alpha, x, beta, y);
+}
+
+int Nfft4GPAmdDistGradMatSymv(void* dop, int n, double alpha, double* x, double beta, double* y)
+{
+   return dist_apply((DistOp*)dop, n, 1, alpha, x, beta, y);
+}
+
+void* Nfft4GPAmdNysShard(void* nys, int row_begin, int row_end, void* comm)
+{
+   NysDev* S = (NysDev*)nys;
+   if (!S || !comm || row_begin < 0 || row_end > S->n || row_begin > row_end) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdNysShard: invalid rows [%d, %d)\n", row_begin, row_end);
+      return nullptr;
+   }
+   hipStream_t s = current_stream();
+   NysDev* N = new NysDev();
+   N->n = row_end - row_begin;
+   N->k = S->k;
+   N->eta = S->eta;
+   const size_t nl = (size_t)N->n;
+   if (hipMalloc((void**)&N->U, sizeof(double) * std::max<size_t>(1, nl * N->k)) != hipSuccess ||
+       hipMalloc((void**)&N->s, sizeof(double) * std::max(1, N->k)) != hipSuccess || nys_alloc_scratch(N)) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdNysShard: allocation failed\n");
+      nys_free(N);
+      return nullptr;
+   }
+   // rows [row_begin, row_end) of every column of the n x k column-major U
+   if ((nl && hipMemcpy2DAsync(N->U, sizeof(double) * nl, S->U + row_begin, sizeof(double) * (size_t)S->n,
+                               sizeof(double) * nl, (size_t)N->k, hipMemcpyDeviceToDevice, s) != hipSuccess) ||
+       hipMemcpyAsync(N->s, S->s, sizeof(double) * N->k, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdNysShard: copy failed\n");
+      nys_free(N);
+      return nullptr;
+   }
+   DistNys* D = new DistNys();
+   D->N = N;
+   D->comm = (Comm*)comm;
+   return D;
+}
+
+int Nfft4GPAmdDistNysSolve(void* dnys, int n, double* x, double* rhs)
+{
+   DistNys* D = (DistNys*)dnys;
+   if (!D || n != D->N->n) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdDistNysSolve: size %d, this rank holds %d rows\n", n,
+              D ? D->N->n : -1);
+      return -1;
+   }
+   if (n > 0 && (!is_device_ptr(x) || !is_device_ptr(rhs))) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdDistNysSolve takes device vectors\n");
+      return -1;
+   }
+   return nys_apply_rows(D->N, D->comm, x, rhs, current_stream());
+}
+
+void Nfft4GPAmdDistNysFree(void* dnys)
+{
+   DistNys* D = (DistNys*)dnys;
+   if (!D) return;
+   nys_free(D->N);
+   delete D;
+}
+
+}  // extern "C"
+
+namespace nfft4gp_amd {
+// k_dnys_scale is this file's; the U passes are solvers.hip's (nys_gemv_t_local / nys_u_local)
+int nys_ut_local(NysDev* N, const double* rhs, double* w, hipStream_t s);
+int nys_u_local(NysDev* N, const double* w, const double* rhs, double* x, hipStream_t s);
+
+int nys_apply_rows(NysDev* N, Comm* comm, double* x, const double* rhs, hipStream_t s)
+{
+   // w = U_loc^T r_loc (k), summed over the row shards, then w = s w - w / eta, then x = U_loc w + r / eta
+   if (nys_ut_local(N, rhs, N->w, s)) return -1;
+   if (comm->allreduce(N->w, (size_t)N->k, s)) return -1;
+   hipLaunchKernelGGL(k_dnys_scale, dim3((N->k + 255) / 256), dim3(256), 0, s, N->w, (const double*)N->s, N->k, N->eta);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return nys_u_local(N, N->w, rhs, x, s);
+}
+}  // namespace nfft4gp_amd

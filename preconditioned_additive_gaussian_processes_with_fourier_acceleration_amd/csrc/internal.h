@@ -131,7 +131,8 @@ struct AdditivePlan {
    std::vector<double> comp_sigma;
    int kernel = 0;  // 0 gaussian, 1 matern12
    double f = 1.0, l = 1.0, mu = 0.0;
-   double weight = 1.0;  // 1/nwindows
+   double weight = 1.0;  // 1/nwindows (1/nwindows of the whole operator on a component shard)
+   double diag = 1.0;    // 1: this handle adds the mu x (and grad f^2 x) terms; 0: a component shard without them
    // layout
    int B = kMaxBlock, CG = 3, ngroups = 0, nblocks = 0;  // CG = 3: 3 spread workgroups fit a CU's LDS
    int spread_variant = 1, interp_variant = 1;  // kernel shape variants (nfft_kernels.hip)
@@ -253,5 +254,29 @@ void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_Lin
 hipStream_t current_stream();
 bool is_device_ptr(const void* p);
 int device_ok();
+
+// ---- multi-GPU (dist.hip) -----------------------------------------------------------------------
+// a process group: in-place sum of count device doubles over the ranks, ordered on stream s
+struct Comm {
+   int rank = 0, world = 1;
+   virtual ~Comm() {}
+   virtual int allreduce(double* d_buf, size_t count, hipStream_t s) = 0;
+};
+// additive handle rows (nfft_api.cpp): local, global, first row; -1 if not an additive handle
+int additive_rows(void* str, int* n_local, int* n_global, int* row_begin);
+bool shard_fused_dot_ok(void* str);
+// row shard: grid (summed over the shards) -> y_local = A x_local and *d_dot = (y_local, x_local) locally
+int shard_finish_dot(void* str, const double* grid, const double* x_local, double* y_local, double* d_dot);
+// what Nfft4GPSolverPcg needs to know about a distributed operator (matvec == Nfft4GPAmdDistMatSymv):
+// the communicator its dot products are summed over (NULL when the vectors are replicated), the global
+// n, and whether q = A p can also form the local (q, p) in its interpolation launch
+struct DistPcgInfo {
+   Comm* dot_comm = nullptr;
+   int n_global = 0;
+   bool fused_dot = false;
+};
+int dist_pcg_info(void* dop, DistPcgInfo& info);
+// q = A p with the local (q, p) in *d_dot (row shards; the caller all-reduces it)
+int dist_matvec_dot(void* dop, const double* d_p, double* d_q, double* d_dot);
 
 }  // namespace nfft4gp_amd

@@ -472,6 +472,46 @@ int additive_matvec_dot(void* str, const double* d_x, double* d_y, double* d_dot
 }  // namespace nfft4gp_amd
 
 namespace nfft4gp_amd {
+// rows of an additive handle: local (this shard) and global; -1 when str is not an additive handle
+int additive_rows(void* str, int* n_local, int* n_global, int* row_begin)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E) return -1;
+   *n_local = E->P.n;
+   *n_global = E->P.n_global;
+   if (row_begin) *row_begin = E->P.row_begin;
+   return 0;
+}
+
+// the row-sharded matvec's local interpolation with the fused (y, x) partial dot of these rows
+// (not yet summed over the shards): the q = A p, (q, p) step of a distributed CG
+bool shard_fused_dot_ok(void* str)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready) return false;
+   return E->P.md.on || E->P.nblocks <= kRedMaxBlocks;
+}
+
+int shard_finish_dot(void* str, const double* grid, const double* x_local, double* y_local, double* d_dot)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready) return -1;
+   AdditivePlan& P = E->P;
+   hipStream_t s = current_stream();
+   if (P.n == 0) {  // a shard without rows contributes 0 to the dot
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(d_dot, 0, sizeof(double), s));
+      return 0;
+   }
+   if (P.md.on) {
+      if (md_grid(P, grid, 0, s)) return -1;
+      return md_interp(P, 0, 1.0, x_local, 0.0, y_local, s, d_dot);
+   }
+   if (launch_grid_from_sum(P, grid, 0, s)) return -1;
+   return launch_interp(P, 0, 1.0, x_local, 0.0, y_local, s, d_dot);
+}
+}  // namespace nfft4gp_amd
+
+namespace nfft4gp_amd {
 // the gathered window buffer of an additive handle (kernels.h:65-95 _buffer / _iparams) and its plan's
 // kernel type (-1 before the first kernel setup); returns -1 for a handle that is not an additive one
 int additive_buffer_info(void* str, const double** xw, int* n, int* nw, int* dw, int* skip_last, int* kernel)
@@ -694,6 +734,19 @@ void* Nfft4GPAmdNysSetupAdditive(void* str, const int* perm, int k, int k11_mode
    }
    return nys_setup_additive(kd->_buffer, P.n_global, P.nw, P.dw, P.skip_last, P.kernel, kd->_params[0],
                              kd->_params[1], kd->_noise_level, perm, k, k11_mode);
+}
+
+int Nfft4GPAmdAdditiveComponentShard(void* str, int nw_global, int own_diag)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || nw_global < E->P.nw || E->P.row_begin != 0 || E->P.row_end != E->P.n_global) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAdditiveComponentShard needs a whole-row additive handle and "
+                      "nw_global >= its %d windows\n", E ? E->P.nw : 0);
+      return -1;
+   }
+   E->P.weight = 1.0 / (double)nw_global;  // the whole operator's 1/nwindows (nfft_interface.c:806)
+   E->P.diag = own_diag ? 1.0 : 0.0;
+   return 0;
 }
 
 int Nfft4GPAmdShardSpread(void* str, const double* x_local, double* grid)

@@ -349,7 +349,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
     const uint16_t* __restrict__ meta, const uint32_t* __restrict__ lo, const uint32_t* __restrict__ qarr,
     const int* __restrict__ tile_off, const double* __restrict__ H, const double* __restrict__ Hd,
     const double* __restrict__ x, double* __restrict__ y, int n, int B, int ngroups, double alpha, double beta,
-    double f, double mu, double* __restrict__ dot_part, unsigned int* __restrict__ dot_ticket,
+    double f, double mu, double dg, double* __restrict__ dot_part, unsigned int* __restrict__ dot_ticket,
     double* __restrict__ dot_out)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
          // nfft_interface.c:547-549 summed over windows: (2f)(Kx + mu x), ff*dscale*K'x, ff*x
          const double v0 = 2.0 * f * (s_y[j] + mu * xj);
          const double v1 = ff * s_yd[j];
-         const double v2 = ff * xj;
+         const double v2 = dg * ff * xj;  // dg: 0 on component shards without the diagonal
          if (beta == 0.0) {
             y0[gj] = alpha * v0;
             y1[gj] = alpha * v1;
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
          } else {
             const double v0 = 2.0 * f * (s_y[j] + mu * xj);
             const double v1 = ff * s_yd[j];
-            const double v2 = ff * xj;
+            const double v2 = dg * ff * xj;  // dg: 0 on component shards without the diagonal
             if (beta == 0.0) {
                y0[gj] = alpha * v0;
                y1[gj] = alpha * v1;
@@ -546,7 +546,7 @@ constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVaria
 
 typedef void (*InterpFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*,
                          const double*, const double*, double*, int, int, int, double, double, double, double,
-                         double*, unsigned int*, double*);
+                         double, double*, unsigned int*, double*);
 struct InterpVariant {
    InterpFn fn, fn_grad, fn_dot;
    int threads;
@@ -631,7 +631,7 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
    const InterpFn fn = grad ? V.fn_grad : (d_dot ? V.fn_dot : V.fn);
    launch_ev(fn, dim3(P.nblocks), dim3(V.threads), interp_lds_bytes(P, grad), stream, P.kev ? P.kev + 4 : nullptr,
              P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H, (const double*)P.d_Hd, d_x, d_y, P.n,
-             P.B, P.ngroups, alpha, beta, P.f, P.mu, P.d_dot_part, P.d_dot_ticket, d_dot);
+             P.B, P.ngroups, alpha, beta, P.f, P.mu * P.diag, P.diag, P.d_dot_part, P.d_dot_ticket, d_dot);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

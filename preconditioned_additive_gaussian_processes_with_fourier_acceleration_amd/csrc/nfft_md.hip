@@ -179,7 +179,7 @@ __global__ __launch_bounds__(kMdThreads) void k_md_interp(const MdComp* __restri
                                                           const double* __restrict__ h1, long long G,
                                                           const double* __restrict__ x, double* __restrict__ y,
                                                           int n, double alpha, double beta, double f, double mu,
-                                                          double* __restrict__ dot_part,
+                                                          double dg, double* __restrict__ dot_part,
                                                           unsigned int* __restrict__ dot_ticket,
                                                           double* __restrict__ dot_out)
 {
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(kMdThreads) void k_md_interp(const MdComp* __restri
             if (DOT) dacc = fma(yo, xj, dacc);
          } else {
             // nfft_interface.c:547-549 summed over windows: (2f)(Kx + mu x), ff*dscale*K'x, ff*x
-            const double v0 = 2.0 * f * (s0 + mu * xj), v1 = ff * s1, v2 = ff * xj;
+            const double v0 = 2.0 * f * (s0 + mu * xj), v1 = ff * s1, v2 = dg * ff * xj;
             double* y1 = y + n;
             double* y2 = y + 2 * (size_t)n;
             if (beta == 0.0) {
@@ -450,7 +450,8 @@ int md_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, 
    const int blocks = std::min(kMdInterpBlocks, (P.n + kMdThreads / 64 - 1) / (kMdThreads / 64));
 #define NFFT4GP_MD_INTERP(G_, D_)                                                                              \
    hipLaunchKernelGGL((k_md_interp<G_, D_>), dim3(blocks), dim3(kMdThreads), 0, s, D.d_comps, P.nw, D.d_u, D.d_psi, \
-                      D.d_h[0], D.d_h[1], D.G, d_x, d_y, P.n, alpha, beta, P.f, P.mu, D.d_dot_part, D.d_dot_ticket, \
+                      D.d_h[0], D.d_h[1], D.G, d_x, d_y, P.n, alpha, beta, P.f, P.mu * P.diag, P.diag, D.d_dot_part,          \
+                      D.d_dot_ticket, \
                       d_dot)
    if (grad)
       NFFT4GP_MD_INTERP(1, 0);

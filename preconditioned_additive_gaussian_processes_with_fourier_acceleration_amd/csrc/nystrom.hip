@@ -498,8 +498,9 @@ struct RocSolver {
    decltype(&rocsolver_dsyevd) syevd = nullptr;
 };
 
-// first loadable of the given sonames (unversioned first: the ROCm install's own link), or nullptr with the
-// dlerror of each attempt appended to `why`
+// first loadable of the given names, or nullptr with the dlerror of each attempt appended to `why`.  The
+// versioned sonames come first: they match a copy already mapped into the process (PyTorch's bundled
+// rocBLAS / rocSOLVER carry the sonames librocblas.so.5 / librocsolver.so.0), so the process keeps one copy
 void* dlopen_first(const char* const* names, std::string& why)
 {
    for (const char* const* p = names; *p; ++p) {
@@ -521,10 +522,10 @@ RocSolver& rocsolver()
                       "the host.\n");
       return R;
    }
-   static const char* const blas_names[] = {"librocblas.so", "librocblas.so.5", "librocblas.so.4",
-                                            "/opt/rocm/lib/librocblas.so", "/opt/rocm/lib/librocblas.so.5", nullptr};
-   static const char* const solver_names[] = {"librocsolver.so", "librocsolver.so.0",
-                                              "/opt/rocm/lib/librocsolver.so", "/opt/rocm/lib/librocsolver.so.0",
+   static const char* const blas_names[] = {"librocblas.so.5", "librocblas.so.4", "librocblas.so",
+                                            "/opt/rocm/lib/librocblas.so.5", "/opt/rocm/lib/librocblas.so", nullptr};
+   static const char* const solver_names[] = {"librocsolver.so.0", "librocsolver.so",
+                                              "/opt/rocm/lib/librocsolver.so.0", "/opt/rocm/lib/librocsolver.so",
                                               nullptr};
    std::string why;
    void* hb = dlopen_first(blas_names, why);

@@ -109,6 +109,7 @@ struct PcgState {
    double normb, tolb, pq, normr2;
    int status;     // 0 running, 1 converged candidate, 2 rho == 0, 3 beta == 0, 4 pq <= 0
    int flag_iter;  // iteration that set status
+   double loc[2];  // distributed PCG: this rank's partial dot (0) / ||r||^2 (1), all-reduced in place
 };
 
 struct PcgSlot {   // pinned host memory, written by the last kernel of each iteration
@@ -129,10 +130,24 @@ int pcg_grid(size_t n)
 }
 
 // which = 0: rhos[ii] = (z, r) with the rho == 0 test;  which = 1: pq = (q, p) with the pq <= 0 test
+__device__ void pcg_dot_store(double tot, PcgState* st, double* __restrict__ rhos, int ii, int which)
+{
+   if (which == 0) {
+      rhos[ii] = tot;
+      if (tot == 0.0) { st->status = 2; st->flag_iter = ii; }
+   } else {
+      st->pq = tot;
+      if (tot <= 0.0) { st->status = 4; st->flag_iter = ii; }
+   }
+}
+
+// loc != NULL (distributed PCG): only this rank's partial is written there; k_pcg_dot_fin applies it after
+// the all-reduce
 __global__ __launch_bounds__(kVecThreads) void k_pcg_dot(const double* __restrict__ a, const double* __restrict__ b,
                                                          size_t n, double* __restrict__ part,
                                                          unsigned int* __restrict__ ticket, PcgState* st,
-                                                         double* __restrict__ rhos, int ii, int which)
+                                                         double* __restrict__ rhos, int ii, int which,
+                                                         double* __restrict__ loc)
 {
    if (st->status) return;
    double acc = 0.0;
@@ -151,13 +166,16 @@ __global__ __launch_bounds__(kVecThreads) void k_pcg_dot(const double* __restric
    acc = block_sum0<kVecThreads>(acc);
    double tot;
    if (!grid_total<kVecThreads>(acc, part, ticket, &tot) || threadIdx.x != 0) return;
-   if (which == 0) {
-      rhos[ii] = tot;
-      if (tot == 0.0) { st->status = 2; st->flag_iter = ii; }
-   } else {
-      st->pq = tot;
-      if (tot <= 0.0) { st->status = 4; st->flag_iter = ii; }
+   if (loc) {
+      *loc = tot;
+      return;
    }
+   pcg_dot_store(tot, st, rhos, ii, which);
+}
+
+__global__ void k_pcg_dot_fin(PcgState* st, double* __restrict__ rhos, int ii, int which, const double* __restrict__ loc)
+{
+   if (threadIdx.x == 0 && !st->status) pcg_dot_store(*loc, st, rhos, ii, which);
 }
 
 // p = z (ii == 1) or p = beta p + z, beta = rhos[ii]/rhos[ii-1] (pcg.c:131-147: Scale then Axpy)
@@ -196,14 +214,37 @@ __global__ __launch_bounds__(kVecThreads) void k_pcg_pupdate(double* __restrict_
    }
 }
 
+__device__ void pcg_slot_write(const PcgState* st, PcgSlot* slot, double normr, int ii)
+{
+   slot->normr = normr;
+   slot->status = st->status;
+   slot->flag_iter = st->flag_iter;
+   __hip_atomic_store(&slot->seq, ii, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ||r||^2 = tot of iteration ii: history, next rho (no preconditioner), convergence test, status slot
+__device__ void pcg_xr_tail(double tot, PcgState* st, double* __restrict__ rhos, double* __restrict__ hist, int ii,
+                            int rho_from_norm, PcgSlot* slot)
+{
+   const double normr = sqrt(tot);
+   st->normr2 = normr;
+   hist[ii] = normr / st->normb;
+   if (rho_from_norm) rhos[ii + 1] = tot;  // z = r next iteration: rho = (r, r)
+   if (normr <= st->tolb) { st->status = 1; st->flag_iter = ii; }
+   pcg_slot_write(st, slot, normr, ii);
+}
+
 // x += alpha p ; r -= alpha q ; ||r|| ; convergence test ; status slot  (pcg.c:168-182)
 __global__ __launch_bounds__(kVecThreads) void k_pcg_xr(double* __restrict__ x, double* __restrict__ r,
                                                         const double* __restrict__ p, const double* __restrict__ q,
                                                         size_t n, double* __restrict__ part,
                                                         unsigned int* __restrict__ ticket, PcgState* st,
                                                         double* __restrict__ rhos, double* __restrict__ hist, int ii,
-                                                        int rho_from_norm, int check_pq, PcgSlot* slot)
+                                                        int rho_from_norm, int check_pq, PcgSlot* slot,
+                                                        double* __restrict__ loc)
 {
+   // loc != NULL (distributed PCG): the local ||r||^2 goes to *loc and k_pcg_xr_fin, after the all-reduce,
+   // makes the convergence test and writes the status slot
    // check_pq: (q, p) came from the fused matvec-dot, so the pq <= 0 breakdown test (pcg.c:158) is here
    const int status = st->status ? st->status : ((check_pq && st->pq <= 0.0) ? 4 : 0);
    if (status) {
@@ -212,10 +253,7 @@ __global__ __launch_bounds__(kVecThreads) void k_pcg_xr(double* __restrict__ x, 
             st->status = status;
             st->flag_iter = ii;
          }
-         slot->normr = st->normr2;
-         slot->status = st->status;
-         slot->flag_iter = st->flag_iter;
-         __hip_atomic_store(&slot->seq, ii, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+         if (!loc) pcg_slot_write(st, slot, st->normr2, ii);
       }
       return;
    }
@@ -248,15 +286,21 @@ __global__ __launch_bounds__(kVecThreads) void k_pcg_xr(double* __restrict__ x, 
    acc = block_sum0<kVecThreads>(acc);
    double tot;
    if (!grid_total<kVecThreads>(acc, part, ticket, &tot) || threadIdx.x != 0) return;
-   const double normr = sqrt(tot);
-   st->normr2 = normr;
-   hist[ii] = normr / st->normb;
-   if (rho_from_norm) rhos[ii + 1] = tot;  // z = r next iteration: rho = (r, r)
-   if (normr <= st->tolb) { st->status = 1; st->flag_iter = ii; }
-   slot->normr = normr;
-   slot->status = st->status;
-   slot->flag_iter = st->flag_iter;
-   __hip_atomic_store(&slot->seq, ii, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+   if (loc) {
+      *loc = tot;
+      return;
+   }
+   pcg_xr_tail(tot, st, rhos, hist, ii, rho_from_norm, slot);
+}
+
+__global__ void k_pcg_xr_fin(PcgState* st, double* __restrict__ rhos, double* __restrict__ hist, int ii,
+                             int rho_from_norm, PcgSlot* slot, const double* __restrict__ loc)
+{
+   if (threadIdx.x != 0) return;
+   if (st->status)
+      pcg_slot_write(st, slot, st->normr2, ii);
+   else
+      pcg_xr_tail(*loc, st, rhos, hist, ii, rho_from_norm, slot);
 }
 
 int grid_for(size_t n)
@@ -284,13 +328,15 @@ struct RedScratch {
 };
 RedScratch g_red;
 
-int dev_dot(const double* x, const double* y, size_t n, double* out)
+// comm != NULL: the local dot summed over the ranks (row-sharded vectors)
+int dev_dot(const double* x, const double* y, size_t n, double* out, Comm* comm = nullptr)
 {
    if (g_red.ensure()) return -1;
    hipStream_t s = current_stream();
    const int g = grid_for(n);
    hipLaunchKernelGGL(k_dot_partial, dim3(g), dim3(kVecThreads), 0, s, x, y, n, g_red.part);
    hipLaunchKernelGGL(k_sum_final, dim3(1), dim3(kVecThreads), 0, s, g_red.part, g, g_red.res);
+   if (comm && comm->allreduce(g_red.res, 1, s)) return -1;
    NFFT4GP_HIP_CHECK(hipMemcpyAsync(g_red.host, g_red.res, sizeof(double), hipMemcpyDeviceToHost, s));
    NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
    *out = g_red.host[0];
@@ -468,6 +514,31 @@ int nys_apply_dev(NysDev* N, double* x, const double* rhs, hipStream_t s)
    return 0;
 }
 
+// the two U passes of the apply on this rank's rows, for the row-sharded apply (dist.hip): w = U^T r
+// (column sums, not yet scaled) and x = U w + r / eta
+int nys_ut_local(NysDev* N, const double* rhs, double* w, hipStream_t s)
+{
+   if (N->n == 0) {
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(w, 0, sizeof(double) * N->k, s));
+      return 0;
+   }
+   hipLaunchKernelGGL(k_nys_ut<double>, dim3(N->nblk), dim3(kNysThreads), 0, s, (const double*)N->U, (size_t)N->n,
+                      N->n, N->k, rhs, N->part);
+   hipLaunchKernelGGL(k_nys_w, dim3((N->k + 63) / 64), dim3(64 * kNysWRows), 0, s, (const double*)N->part, N->nblk,
+                      N->k, (const double*)nullptr, N->eta, w);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int nys_u_local(NysDev* N, const double* w, const double* rhs, double* x, hipStream_t s)
+{
+   if (N->n == 0) return 0;
+   hipLaunchKernelGGL(k_nys_u<double>, dim3((N->n + kNysThreads - 1) / kNysThreads), dim3(kNysThreads),
+                      sizeof(double) * N->k, s, (const double*)N->U, (size_t)N->n, N->n, N->k, w, rhs, N->eta, x);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
 __global__ void k_to_f32(const double* __restrict__ a, size_t count, float* __restrict__ b)
 {
    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x)
@@ -587,7 +658,14 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
       vb.close(false);
    };
 
-   if (dev_dot(vb.d, vb.d, N, &normb)) return -1;
+   // a distributed operator (dist.hip): row-sharded vectors sum every dot over its communicator (red), and
+   // maxits is clamped to the global n; component-sharded (replicated) vectors need neither
+   const bool is_dist = cb.mv_dev && matvec == &Nfft4GPAmdDistMatSymv;
+   DistPcgInfo dinfo;
+   if (is_dist && dist_pcg_info(mat_data, dinfo)) return -1;
+   Comm* red = is_dist ? dinfo.dot_comm : nullptr;
+   const int n_all = is_dist ? dinfo.n_global : n;
+   if (dev_dot(vb.d, vb.d, N, &normb, red)) return -1;
    normb = std::sqrt(normb);
    if (normb < EPSILON) {  // pcg.c:32-41
       hipLaunchKernelGGL(k_fill, dim3(elem_grid(N)), dim3(256), 0, s, vx.d, N, 0.0);
@@ -600,7 +678,7 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
       return 0;
    }
    tolb = atol ? tol : tol * normb;
-   if (maxits > n) maxits = n;
+   if (maxits > n_all) maxits = n_all;
 
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&r, sizeof(double) * N));
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&p, sizeof(double) * N));
@@ -613,7 +691,7 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
       return -1;
    }
    double rr0;
-   if (dev_dot(r, r, N, &rr0)) return -1;
+   if (dev_dot(r, r, N, &rr0, red)) return -1;
    normr = std::sqrt(rr0);
    if (normr < tolb) {  // pcg.c:70-84
       *prel_res = normr / normb;
@@ -660,7 +738,10 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
    const int g = pcg_grid(N);
    const int ge = g;
    // this library's additive operator forms (q, p) in its own interpolation launch
-   const bool fused_dot = cb.mv_dev && matvec == &Nfft4GPAdditiveNFFTMatSymv && additive_fused_dot_ok(mat_data);
+   const bool fused_dot = cb.mv_dev && ((matvec == &Nfft4GPAdditiveNFFTMatSymv && additive_fused_dot_ok(mat_data)) ||
+                                        (is_dist && dinfo.fused_dot));
+   double* loc0 = red ? &st->loc[0] : nullptr;  // device addresses inside st
+   double* loc1 = red ? &st->loc[1] : nullptr;
    // iterations in flight ahead of the host's status check (1 when printing every step)
    const int lag = print_level > 0 ? 1 : PcgScratch::kSlots;
    double prev_rel = rel_res_v[0];
@@ -675,21 +756,42 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
          if (prec_data) {
             if (cb.solve(z, r)) { rc = -1; break; }
             hipLaunchKernelGGL(k_pcg_dot, dim3(g), dim3(kVecThreads), 0, s, z, r, N, g_pcg.part, g_pcg.ticket, st,
-                               rhos, ii, 0);
+                               rhos, ii, 0, loc0);
+            if (red) {
+               if (red->allreduce(loc0, 1, s)) { rc = -1; break; }
+               hipLaunchKernelGGL(k_pcg_dot_fin, dim3(1), dim3(64), 0, s, st, rhos, ii, 0, (const double*)loc0);
+            }
             zz = z;
          }
          hipLaunchKernelGGL(k_pcg_pupdate, dim3(ge), dim3(kVecThreads), 0, s, p, zz, N, st, rhos, ii);
          if (fused_dot) {
             // q = A p with (q, p) formed inside the interpolation kernel's epilogue
-            if (additive_matvec_dot(mat_data, p, q, &st->pq)) { rc = -1; break; }
+            if (is_dist) {
+               if (dist_matvec_dot(mat_data, p, q, &st->pq) || (red && red->allreduce(&st->pq, 1, s))) {
+                  rc = -1;
+                  break;
+               }
+            } else if (additive_matvec_dot(mat_data, p, q, &st->pq)) {
+               rc = -1;
+               break;
+            }
          } else {
             if (cb.apply(1.0, p, 0.0, q)) { rc = -1; break; }
             hipLaunchKernelGGL(k_pcg_dot, dim3(g), dim3(kVecThreads), 0, s, q, p, N, g_pcg.part, g_pcg.ticket, st,
-                               rhos, ii, 1);
+                               rhos, ii, 1, loc0);
+            if (red) {
+               if (red->allreduce(loc0, 1, s)) { rc = -1; break; }
+               hipLaunchKernelGGL(k_pcg_dot_fin, dim3(1), dim3(64), 0, s, st, rhos, ii, 1, (const double*)loc0);
+            }
          }
+         PcgSlot* slot = slots_d + (ii % PcgScratch::kSlots);
          hipLaunchKernelGGL(k_pcg_xr, dim3(g), dim3(kVecThreads), 0, s, vx.d, r, p, q, N, g_pcg.part, g_pcg.ticket,
-                            st, rhos, hist_d, ii, prec_data ? 0 : 1, fused_dot ? 1 : 0,
-                            slots_d + (ii % PcgScratch::kSlots));
+                            st, rhos, hist_d, ii, prec_data ? 0 : 1, fused_dot ? 1 : 0, slot, loc1);
+         if (red) {
+            if (red->allreduce(loc1, 1, s)) { rc = -1; break; }
+            hipLaunchKernelGGL(k_pcg_xr_fin, dim3(1), dim3(64), 0, s, st, rhos, hist_d, ii, prec_data ? 0 : 1, slot,
+                               (const double*)loc1);
+         }
          ii++;
       }
       if (rc) break;
@@ -743,7 +845,7 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
       NFFT4GP_HIP_CHECK(hipMemcpyAsync(r, vb.d, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
       if (cb.apply(-1.0, vx.d, 1.0, r)) { rc = -1; break; }
       double rr;
-      if (dev_dot(r, r, N, &rr)) { rc = -1; break; }
+      if (dev_dot(r, r, N, &rr, red)) { rc = -1; break; }
       normr2 = std::sqrt(rr);
       rel_res_v[fi] = normr2;
       if (normr2 <= tolb) {
@@ -872,7 +974,8 @@ bool library_operator(const void* fn)
           fn == (const void*)&Nfft4GPAmdNysSolve || fn == (const void*)&Nfft4GPAmdFsaiSolve ||
           fn == (const void*)&Nfft4GPAmdAfnSolve || fn == (const void*)&Nfft4GPAmdPrecondNysSolve ||
           fn == (const void*)&Nfft4GPAmdPrecondNysDvp || fn == (const void*)&Nfft4GPAmdPrecondFsaiSolve ||
-          fn == (const void*)&Nfft4GPAmdPrecondFsaiDvp;
+          fn == (const void*)&Nfft4GPAmdPrecondFsaiDvp || fn == (const void*)&Nfft4GPAmdDistMatSymv ||
+          fn == (const void*)&Nfft4GPAmdDistGradMatSymv || fn == (const void*)&Nfft4GPAmdDistNysSolve;
 }
 }  // namespace nfft4gp_amd
 

@@ -1,14 +1,21 @@
-"""Row-sharded multi-GPU operator and CG over torch.distributed (one process per GPU, RCCL).
+"""Multi-GPU additive operator, Nystrom apply and CG (one process per GPU).
 
-The reference is single-process (SRC/external/nfft_interface.c, SRC/solvers/pcg.c).  Across GPUs the
-additive matvec shards by ROWS: every rank spreads its own n/N points for all
-windows into the nw x 64 oversampled grids, the grids (16 KB at nw = 32) are summed with ONE
-all-reduce, and every rank interpolates its own rows.  CG keeps x, r, p, q row-sharded, so each dot
-product becomes a local dot plus a scalar all-reduce.
+The reference is single-process (SRC/external/nfft_interface.c:796-817 runs the components one after
+another; SRC/solvers/pcg.c works on whole vectors).  The operator splits two ways:
 
-``engine`` is anything with ``shard_spread(x_local, grid)`` / ``shard_finish(grid, x_local, alpha,
-beta, y_local, grad)`` -- the HIP shard handle (NFFTAdditiveKernel(..., shard=...)) in production; the
-CPU tests plug in the numpy replay of the same kernels to exercise the gloo path.
+* rows (``partition="rows"``): every rank spreads its own n/N points for all windows, the nw x 64
+  oversampled grids (16 KB at nw = 32) are summed with ONE all-reduce, every rank interpolates its rows;
+  CG vectors stay row-sharded and every dot is summed over the ranks.
+* components (``partition="components"``, the split BASELINE configs[3] names): every rank holds a
+  contiguous block of the windows for all points, y (n doubles) is all-reduced, vectors are replicated.
+
+``DistributedAdditiveKernel`` / ``RowShardedNystrom`` are the library's distributed operators
+(dist.hip): the all-reduces are enqueued by the C++ code on the library stream (RCCL) and
+``solvers.pcg`` drives them through the reference's own Nfft4GPSolverPcg entry point, with the
+scalars and control decisions on the device (no per-iteration host synchronisation).
+
+``RowShardedAdditiveKernel`` is the host-controlled mirror of the same CG over any engine with
+``shard_spread`` / ``shard_finish`` (the CPU tests drive it with the numpy replay of the HIP kernels).
 """
 from __future__ import annotations
 
@@ -21,6 +28,212 @@ def row_range(n: int, rank: int, world: int) -> tuple[int, int]:
     """Contiguous row block of `rank` (ceil-divided, the last ranks may get fewer or zero rows)."""
     per = (n + world - 1) // world
     return min(n, rank * per), min(n, (rank + 1) * per)
+
+
+def component_range(nw: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous block of windows of `rank` (balanced: sizes differ by at most one; every rank gets at
+    least one window when nw >= world).  Config D: 32 windows on 8 GPUs -> 4 per GPU."""
+    return rank * nw // world, (rank + 1) * nw // world
+
+
+class Communicator:
+    """The process group of the library's distributed operators (Nfft4GPAmdComm*).
+
+    ``Communicator.rccl()``: RCCL over xGMI, one communicator per process created from an id that rank 0
+    makes and torch.distributed broadcasts; all-reduces are enqueued on the library stream.
+    ``Communicator.callback()``: the all-reduce of a torch.distributed group (e.g. gloo, for several
+    ranks on one GPU, which RCCL refuses), through a device staging buffer; the sum goes through host
+    memory, so it synchronises -- a test path, not a fast one."""
+
+    def __init__(self, h, rank, world, keep=()):
+        self.h, self.rank, self.world, self._keep = h, rank, world, keep
+
+    @staticmethod
+    def _bind_stream():
+        import torch
+        from . import _lib
+        _lib.lib().Nfft4GPAmdSetStream(torch.cuda.current_stream().cuda_stream)
+
+    @classmethod
+    def rccl(cls, group=None):
+        import torch
+        import torch.distributed as dist
+        from . import _lib
+        L = _lib.lib()
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        buf = np.zeros(128, dtype=np.uint8)
+        if rank == 0 and L.Nfft4GPAmdCommUniqueId(buf.ctypes.data) != 0:
+            raise RuntimeError("Nfft4GPAmdCommUniqueId failed (RCCL not loadable, see stderr)")
+        t = torch.from_numpy(buf)
+        if dist.get_backend(group) == "nccl":
+            t = t.cuda()
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        buf = np.ascontiguousarray(t.cpu().numpy())
+        cls._bind_stream()
+        h = L.Nfft4GPAmdCommCreateRccl(rank, world, buf.ctypes.data)
+        if not h:
+            raise RuntimeError("Nfft4GPAmdCommCreateRccl failed (see stderr)")
+        return cls(h, rank, world)
+
+    @classmethod
+    def callback(cls, group=None, capacity: int = 1 << 20):
+        import torch
+        import torch.distributed as dist
+        from . import _lib
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        stage = torch.zeros(capacity, dtype=torch.float64, device="cuda")
+
+        def _allreduce(ctx, ptr, count):
+            try:
+                host = stage[:count].cpu()  # on torch's current stream = the library stream
+                dist.all_reduce(host, group=group)
+                stage[:count].copy_(host)
+                return 0
+            except Exception:  # a C caller cannot take a Python exception
+                return -1
+
+        fn = _lib.ALLREDUCE(_allreduce)
+        cls._bind_stream()
+        h = _lib.lib().Nfft4GPAmdCommCreateCallback(rank, world, fn, None, stage.data_ptr(), capacity)
+        if not h:
+            raise RuntimeError("Nfft4GPAmdCommCreateCallback failed")
+        return cls(h, rank, world, keep=(stage, fn))
+
+    def allreduce(self, t):
+        """In-place sum of a float64 device tensor over the ranks."""
+        from . import _lib
+        if _lib.lib().Nfft4GPAmdCommAllreduce(self.h, t.data_ptr(), t.numel()) != 0:
+            raise RuntimeError("Nfft4GPAmdCommAllreduce failed")
+        return t
+
+    def free(self):
+        if getattr(self, "h", None):
+            from . import _lib
+            _lib.lib().Nfft4GPAmdCommFree(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class DistributedAdditiveKernel:
+    """The additive operator split over a Communicator (Nfft4GPAmdDist*, dist.hip).
+
+    rows:       x, y hold this rank's rows [row_begin, row_end); ``n`` is their count.
+    components: this rank's windows [comp_begin, comp_end) for all n points, x and y whole (replicated).
+    ``solvers.pcg(self, b, x)`` runs Nfft4GPSolverPcg on it (device-controlled, dots summed over the ranks
+    for rows)."""
+
+    def __init__(self, data, windows, nwindows: int, dwindows: int, comm: Communicator, partition: str = "rows"):
+        from . import _lib
+        from .nfft import NFFTAdditiveKernel
+        data = np.asfortranarray(np.asarray(data, dtype=np.float64))
+        n = data.shape[0]
+        self.comm, self.partition = comm, partition
+        self.n_global, self.nwindows = n, nwindows
+        L = _lib.lib()
+        if partition == "rows":
+            self.row_begin, self.row_end = row_range(n, comm.rank, comm.world)
+            self.comp_begin, self.comp_end = 0, nwindows
+            self.local = NFFTAdditiveKernel(data, windows, nwindows, dwindows, shard=(self.row_begin, self.row_end))
+            kind = 0
+        elif partition == "components":
+            if nwindows < comm.world:
+                raise ValueError(f"{nwindows} windows cannot be split over {comm.world} ranks")
+            self.row_begin, self.row_end = 0, n
+            self.comp_begin, self.comp_end = component_range(nwindows, comm.rank, comm.world)
+            win = np.asarray(windows, dtype=np.int32).reshape(nwindows, dwindows)[self.comp_begin:self.comp_end]
+            self.local = NFFTAdditiveKernel(data, win, self.comp_end - self.comp_begin, dwindows)
+            if L.Nfft4GPAmdAdditiveComponentShard(self.local.h, nwindows, int(comm.rank == 0)) != 0:
+                raise RuntimeError("Nfft4GPAmdAdditiveComponentShard failed")
+            kind = 1
+        else:
+            raise ValueError("partition is 'rows' or 'components'")
+        self.n = self.row_end - self.row_begin
+        self.h = L.Nfft4GPAmdDistCreate(self.local.h, kind, comm.h)
+        if not self.h:
+            raise RuntimeError("Nfft4GPAmdDistCreate failed")
+
+    def setup(self, kernel=0, f=None, l=None, mu=None) -> int:
+        return self.local.setup(kernel, f, l, mu)
+
+    def _apply(self, name, x, alpha, beta, y, mult):
+        from . import _lib
+        from .nfft import _check_len, _empty_like, _ptr
+        _check_len("x", x, self.n)
+        if y is None:
+            y = _empty_like(x, mult * self.n)
+        _check_len("y", y, mult * self.n)
+        if getattr(_lib.lib(), name)(self.h, self.n, float(alpha), _ptr(x)[0], float(beta), _ptr(y)[0]) != 0:
+            raise RuntimeError(f"{name} failed")
+        return y
+
+    def matsymv(self, x, alpha=1.0, beta=0.0, y=None):
+        return self._apply("Nfft4GPAmdDistMatSymv", x, alpha, beta, y, 1)
+
+    def gradmatsymv(self, x, alpha=1.0, beta=0.0, y=None):
+        return self._apply("Nfft4GPAmdDistGradMatSymv", x, alpha, beta, y, 3)
+
+    @property
+    def matvec_fnptr(self) -> int:
+        from . import _lib
+        return _lib.fnptr("Nfft4GPAmdDistMatSymv")
+
+    def free(self):
+        from . import _lib
+        if getattr(self, "h", None):
+            _lib.lib().Nfft4GPAmdDistFree(self.h)
+            self.h = None
+        if getattr(self, "local", None) is not None:
+            self.local.free()
+            self.local = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class RowShardedNystrom:
+    """Rows [row_begin, row_end) of a NystromPrecond's U (Nfft4GPAmdNysShard): the apply of nys.c:115-173
+    as a local U^T r, a k-vector all-reduce and a local U w + r / eta."""
+
+    def __init__(self, nys, row_begin: int, row_end: int, comm: Communicator):
+        from . import _lib
+        self.n, self.k, self.comm = row_end - row_begin, nys.k, comm
+        self.h = _lib.lib().Nfft4GPAmdNysShard(nys.h, int(row_begin), int(row_end), comm.h)
+        if not self.h:
+            raise RuntimeError("Nfft4GPAmdNysShard failed")
+
+    def solve(self, x, rhs):
+        from . import _lib
+        from .nfft import _check_len, _ptr
+        _check_len("x", x, self.n)
+        _check_len("rhs", rhs, self.n)
+        if _lib.lib().Nfft4GPAmdDistNysSolve(self.h, self.n, _ptr(x)[0], _ptr(rhs)[0]) != 0:
+            raise RuntimeError("Nfft4GPAmdDistNysSolve failed")
+        return x
+
+    @property
+    def solve_fnptr(self) -> int:
+        from . import _lib
+        return _lib.fnptr("Nfft4GPAmdDistNysSolve")
+
+    def free(self):
+        from . import _lib
+        if getattr(self, "h", None):
+            _lib.lib().Nfft4GPAmdDistNysFree(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class GpuVecOps:
