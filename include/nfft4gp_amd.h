@@ -6,7 +6,7 @@
  * of Hitenze/Preconditioned_Additive_Gaussian_Processes_with_Fourier_Acceleration.
  *
  * Differences from the reference header, all deliberate:
- *  - no NFFT3/FFTW includes (INC/_external.h:4-20): str_adj's fastsum_plan members are internal;
+ *  - no NFFT3/FFTW includes (INC/_external.h:4-20): str_adj is declared with fastsum_plan opaque;
  *  - vectors x, y, rhs may be HOST or DEVICE (hipMalloc) pointers; the library detects which with
  *    hipPointerGetAttributes.  Device pointers run with no PCIe traffic and no host sync, enqueued
  *    on the stream set by Nfft4GPAmdSetStream (default: the null stream, ordered with torch's
@@ -88,6 +88,32 @@ typedef struct NFFT4GP_KERNEL_STRUCT
    NFFT4GP_DOUBLE *_dwork;
    void *_external;
 } nfft4gp_kernel, *pnfft4gp_kernel;
+
+/* ---- per-component NFFT state: field layout identical to INC/_external.h:28-51 ----------------
+ * Declared for source compatibility (a caller naming str_adj compiles).  NFFT3's fastsum_plan stays
+ * opaque: no fastsum.h is needed, and the typedef below is the same one fastsum.h makes.  The
+ * single-component handle's *Kp (Nfft4GPNFFTKernel{Gaussian,Matern12}Kernel) points at a str_adj that
+ * holds the cached scalars of the reference (_kernel, _d, _sigma, _mu, _N, _p, _m, _eps, _n, _NN, _scale,
+ * _kernel_scale); _x and the two plans are NULL: the centred points and the plans live in HBM. */
+typedef struct fastsum_plan_ fastsum_plan;
+typedef struct
+{
+   int _kernel; /* 0: Gauss, 1: Matern 1/2 */
+   int _d;
+   NFFT4GP_DOUBLE *_sigma;
+   NFFT4GP_DOUBLE _mu;
+   int _N;
+   int _p;
+   int _m;
+   NFFT4GP_DOUBLE _eps;
+   int _n;
+   int _NN;
+   NFFT4GP_DOUBLE *_x;
+   NFFT4GP_DOUBLE _scale;
+   NFFT4GP_DOUBLE _kernel_scale;
+   fastsum_plan *_fastsum_original;
+   fastsum_plan *_fastsum_derivative;
+} str_adj, *pstr_adj;
 
 /* ---- generic kernel parameter struct --------------------------------------------------------- */
 /* replaces SRC/linearalg/kernels.c:404-436 */

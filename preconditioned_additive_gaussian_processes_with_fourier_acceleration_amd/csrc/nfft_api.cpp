@@ -5,6 +5,7 @@
 // gathered window columns (host); _dwork = 3n host doubles as in the reference; _external = our
 // device plan.  Hyperparameters are read from _params / _noise_level at setup time and cached,
 // as the reference caches them in str_adj (nfft_interface.c:219-256).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <array>
@@ -70,8 +71,12 @@ struct PlanExt {
    std::vector<TimingRec> pool;
 };
 
-// single-component handle (the reference's str_adj): *Kp of the single-component setup points here
+// single-component handle (the reference's str_adj): *Kp of the single-component setup points here.  The
+// public str_adj comes first, so a caller that casts *Kp to str_adj* (INC/_external.h:28-51) reads the
+// reference's cached scalars.
 struct SingleAdj {
+   str_adj pub{};
+   double sigma_pub = 0.0;  // pub._sigma points here
    nfft4gp_kernel* owner = nullptr;
    int dim = 1;
    int max_n = 0;
@@ -356,13 +361,24 @@ PlanExt* additive_plan(void* str)
 }
 
 
-nfft4gp_kernel* kernel_struct_create(int max_n)
+// kernels.c:404-441: _ldwork = max_n, or max_n * omp_get_max_threads() for an OpenMP handle.  This library
+// has no OpenMP of its own, but when the reference's dense kernels share the process (its kernels.c calls
+// this function through the dynamic linker once libnfft4gp_amd precedes it) they index _dwork per thread:
+// ask the OpenMP runtime already in the process, if any.
+int omp_threads_in_process()
+{
+   using fn_t = int (*)();
+   static fn_t f = (fn_t)dlsym(RTLD_DEFAULT, "omp_get_max_threads");
+   return f ? std::max(1, f()) : 1;
+}
+
+nfft4gp_kernel* kernel_struct_create(int max_n, int omp = 0)
 {
    nfft4gp_kernel* k = (nfft4gp_kernel*)calloc(1, sizeof(nfft4gp_kernel));
    k->_max_n = max_n;
-   k->_omp = 0;
-   k->_ldwork = (size_t)max_n;
-   k->_dwork = (double*)malloc(sizeof(double) * (size_t)std::max(1, max_n));
+   k->_omp = omp;
+   k->_ldwork = (size_t)max_n * (size_t)(omp ? omp_threads_in_process() : 1);
+   k->_dwork = (double*)malloc(sizeof(double) * std::max<size_t>(1, k->_ldwork));
    return k;
 }
 
@@ -540,12 +556,7 @@ int Nfft4GPAmdDeviceAvailable(void) { return device_ok(); }
 void Nfft4GPAmdSetStream(void* s) { g_stream = (hipStream_t)s; }
 void* Nfft4GPAmdGetStream(void) { return (void*)g_stream; }
 
-void* Nfft4GPKernelParamCreate(int max_n, int omp)
-{
-   nfft4gp_kernel* k = kernel_struct_create(max_n);
-   k->_omp = omp;
-   return k;
-}
+void* Nfft4GPKernelParamCreate(int max_n, int omp) { return kernel_struct_create(max_n, omp); }
 
 void Nfft4GPKernelParamFree(void* str)
 {
@@ -900,6 +911,24 @@ static int single_setup(void* str, int kernel, double* data, int n, int ldim, in
    }
    AdditivePlan& P = adj->plan->P;
    if (plan_setup(P, adj->data.data(), kernel, kd->_params[0], kd->_params[1], kd->_noise_level)) return -1;
+   // the reference's str_adj scalars (nfft_interface.c:14-28, :150-231)
+   str_adj& A = adj->pub;
+   A._kernel = kernel;
+   A._d = d;
+   adj->sigma_pub = P.comp_sigma.empty() ? 0.0 : P.comp_sigma[0];
+   A._sigma = &adj->sigma_pub;
+   A._mu = kd->_noise_level;
+   A._N = kBand;
+   A._p = 1;
+   A._m = kM;
+   A._eps = 0.0;
+   A._n = n;
+   A._NN = kNos;
+   A._x = nullptr;
+   A._scale = P.comp_scale.empty() ? 1.0 : P.comp_scale[0];
+   A._kernel_scale = kd->_params[0];
+   A._fastsum_original = nullptr;
+   A._fastsum_derivative = nullptr;
    *Kp = (double*)adj;
    *dKp = (double*)adj;
    return 0;
