@@ -249,19 +249,17 @@ def run_pcg_nystrom(op, torch, n, k, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=
 def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1, schur="fsai",
                 order="random"):
     """PCG to 1e-6 with the AFN preconditioner (BASELINE configs[1-2]: "AFN rank=512") of the same dense
-    additive kernel, set up on the GPU (afn.c:161-489 with rank k: FPS order, K11 Cholesky, K12,
-    W = L11^-1 K12 on MFMA, FSAI of the Schur complement with lfil entries per row)."""
+    additive kernel, set up on the GPU the way the reference's Nfft4GPPrecondAFNSetup does it
+    (Nfft4GPAmdPrecondAFNSetup, afn.c:161-489): rank estimation with max_k = k, then the AFN when the
+    estimate reaches max_k, or the rank-k' Nystrom the reference switches to when it does not
+    (afn.c:294-304; reported as ..._kind "nystrom" with the estimated rank)."""
+    import ctypes
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
     assert op.setup(amd.GAUSSIAN, f=1.0, l=l_pcg, mu=0.01) == 0
+    ctypes.CDLL(None).srand(807)  # the rank estimation and random order draw libc rand() as the reference's
     torch.cuda.synchronize()
     t0 = time.time()
-    # the reference's perm_opt 0 (afn.c:210-218, random order: the Nystrom leg's permutation) or 1 (FPS)
-    if order == "random":
-        perm = np.random.default_rng(rng_seed + 2).permutation(n).astype(np.int32)
-        pre = amd.AfnPrecond.setup(X, k, 1.0, l_pcg, 0.01, perm_opt="perm", perm=perm, schur_lfil=lfil, op=op,
-                                   schur=schur)
-    else:
-        pre = amd.AfnPrecond.setup(X, k, 1.0, l_pcg, 0.01, perm_opt="fps", schur_lfil=lfil, op=op, schur=schur)
+    pre = amd.PrecondAFN(X, k, perm_opt=order, schur=schur, schur_lfil=lfil, op=op)
     torch.cuda.synchronize()
     t_setup = time.time() - t0
     b = torch.tensor(np.random.default_rng(rng_seed + 1).random(n) - 0.5, device="cuda")
@@ -279,11 +277,13 @@ def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000
         pre.solve(x, r)
     torch.cuda.synchronize()
     t_apply = (time.time() - t1) / 10
+    kind, rank = pre.kind, pre.k
     pre.free()
     key = "pcg_afn" if schur == "fsai" else "pcg_afn_" + schur
     if order != "random":
         key += "_" + order
-    return {key + "_rank": k, key + "_order": order, key + "_schur": schur, key + "_schur_lfil": lfil if schur == "fsai" else None,
+    return {key + "_max_k": k, key + "_kind": kind, key + "_rank": rank, key + "_order": order,
+            key + "_schur": schur, key + "_schur_lfil": lfil if schur == "fsai" else None,
             key + "_setup_s": t_setup, key + "_time_s": t, key + "_iters": iters, key + "_rel_res": relres,
             key + "_total_s": t_setup + t, key + "_apply_ms": 1e3 * t_apply}
 

@@ -393,6 +393,19 @@ int Nfft4GPAmdRankestDefault(const NFFT4GP_DOUBLE *data, int n, int ldim, int d,
  * reference builds a rank-k Nystrom instead (afn.c:287-296). */
 int Nfft4GPAmdAfnRankEstimate(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int max_k, int perm_opt,
                               int nsamples, int kernel, void *fkernel_params, int *perm);
+/* Nfft4GPPrecondAFNSetup (afn.c:161-489) in one call, its arguments as there (kernel: 0 Gaussian, 1
+ * Matern-1/2; fkernel_params an nfft4gp_kernel or this library's additive NFFT handle):
+ * Nfft4GPAmdAfnRankEstimate, then the AFN with that rank and order (k == max_k, k == 0, k == n), or
+ * the rank-k Nystrom on the estimated landmarks when 0 < k < max_k (afn.c:294-304, MATLAB afn_setup.m:80-83),
+ * or -- when the AFN's factors break down (K11 not positive definite, the Schur FSAI meets a non-positive
+ * pivot) -- MATLAB's RAN fallback, a Nystrom on the same order (afn_setup.m:93-98).  Nfft4GPAmdPrecondAFNSolve
+ * is the func_solve of whichever was built; Nfft4GPAmdPrecondAFNInfo reports kind (0 AFN, 1 Nystrom below
+ * max_k, 2 Nystrom after a breakdown), k and the underlying Nfft4GPAmdAfn* / Nfft4GPAmdNys* handle. */
+void *Nfft4GPAmdPrecondAFNSetup(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int max_k, int perm_opt,
+                                int schur_opt, int schur_lfil, int nsamples, int kernel, void *fkernel_params);
+int Nfft4GPAmdPrecondAFNSolve(void *pre, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
+int Nfft4GPAmdPrecondAFNInfo(void *pre, int *kind, int *k, void **afn, void **nys);
+void Nfft4GPAmdPrecondAFNFree(void *pre);
 
 /* ---- farthest point sampling (SRC/linearalg/ordering.c) -------------------------------------------
  * Nfft4GPSortFps with kFpsAlgorithmParallel1 (ordering.c:422-739): *k in: the number of points to select

@@ -147,6 +147,11 @@ _SIGS = {
     "Nfft4GPAmdShardSpread": (C.c_int, [vp, vp, vp]),
     "Nfft4GPAmdShardFinish": (C.c_int, [vp, vp, C.c_int, C.c_double, vp, C.c_double, vp]),
     "Nfft4GPAmdShardGridSize": (C.c_longlong, [vp]),
+    "Nfft4GPAmdPrecondAFNSetup": (vp, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_int, vp]),
+    "Nfft4GPAmdPrecondAFNSolve": (C.c_int, [vp, C.c_int, vp, vp]),
+    "Nfft4GPAmdPrecondAFNInfo": (C.c_int, [vp, ip, ip, C.POINTER(vp), C.POINTER(vp)]),
+    "Nfft4GPAmdPrecondAFNFree": (None, [vp]),
     "Nfft4GPAmdCommUniqueId": (C.c_int, [vp]),
     "Nfft4GPAmdCommCreateRccl": (vp, [C.c_int, C.c_int, vp]),
     "Nfft4GPAmdCommCreateCallback": (vp, [C.c_int, C.c_int, ALLREDUCE, vp, vp, C.c_longlong]),

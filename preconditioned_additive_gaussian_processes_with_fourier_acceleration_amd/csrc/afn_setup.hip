@@ -369,7 +369,10 @@ __global__ __launch_bounds__(1024) void k_sumsq_lower(const double* __restrict__
 std::vector<int> rand_perm(int n, int k)
 {
    std::vector<std::pair<double, int>> v(n);
-   for (int i = 0; i < n; i++) v[i] = {(double)rand(), i};
+   {
+      CallerRandBatch caller;
+      for (int i = 0; i < n; i++) v[i] = {(double)rand(), i};
+   }
    std::partial_sort(v.begin(), v.begin() + k, v.end());
    std::vector<int> out(k);
    for (int i = 0; i < k; i++) out[i] = v[i].second;
@@ -649,10 +652,16 @@ void* Nfft4GPAmdAfnSetup(const double* data, int n, int ldim, int d, int k, int 
    return Nfft4GPAmdAfnSetupSchur(data, n, ldim, d, k, perm_opt, perm, 3, schur_lfil, kernel, fkernel_params);
 }
 
-void* Nfft4GPAmdAfnSetupSchur(const double* data, int n, int ldim, int d, int k, int perm_opt, const int* perm,
-                              int schur_opt, int schur_lfil, int kernel, void* fkernel_params)
+}  // extern "C"
+
+namespace {
+// Nfft4GPAmdAfnSetupSchur's body; *breakdown = true when the factors cannot be formed (K11 not positive
+// definite, or a row of the Schur complement's FSAI with a non-positive pivot: non-finite values, MATLAB's
+// ~isreal(PRE.GS), afn_setup.m:93-98)
+void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm_opt, const int* perm, int schur_opt,
+                     int schur_lfil, int kernel, void* fkernel_params, bool* breakdown)
 {
-   if (!need_device("Nfft4GPAmdAfnSetup")) return nullptr;
+   *breakdown = false;
    if (!data || !fkernel_params || n <= 0 || ldim < n || d <= 0 || k < 0 || k > n || perm_opt < 0 || perm_opt > 2 ||
        (perm_opt == 2 && !perm) || (schur_opt != 0 && schur_opt != 3) || (schur_opt == 0 && k == 0)) {
       fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup needs data (ldim >= n), kernel parameters, 0 <= k <= n, "
@@ -720,6 +729,7 @@ void* Nfft4GPAmdAfnSetupSchur(const double* data, int n, int ldim, int d, int k,
       const int info = chol_inverse_dev(K11, k, 0.0, G, Gt, dinfo, s);
       if (info > 0) {
          fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: K11 is not positive definite (column %d)\n", info);
+         *breakdown = true;
          return fail(nullptr);
       }
       if (info < 0) return fail("Cholesky / triangular inverse of K11");
@@ -753,6 +763,12 @@ void* Nfft4GPAmdAfnSetupSchur(const double* data, int n, int ldim, int d, int k,
       (void)hipStreamSynchronize(s);
       (void)hipFree(X2);
       if (rc) return fail("Schur-complement FSAI");
+      if (!std::all_of(aa.begin(), aa.end(), [](double v) { return std::isfinite(v); })) {
+         fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: the Schur complement's FSAI broke down (non-positive "
+                         "pivot)\n");
+         *breakdown = true;
+         return fail(nullptr);
+      }
       S = Nfft4GPAmdFsaiCreate(n2, ia.data(), ja.data(), aa.data());
       if (!S) return fail("FSAI upload");
    }
@@ -768,11 +784,24 @@ void* Nfft4GPAmdAfnSetupSchur(const double* data, int n, int ldim, int d, int k,
    }
    return A;
 }
+}  // namespace
+
+extern "C" {
+
+void* Nfft4GPAmdAfnSetupSchur(const double* data, int n, int ldim, int d, int k, int perm_opt, const int* perm,
+                              int schur_opt, int schur_lfil, int kernel, void* fkernel_params)
+{
+   if (!need_device("Nfft4GPAmdAfnSetup")) return nullptr;
+   bool breakdown = false;
+   return afn_setup_impl(data, n, ldim, d, k, perm_opt, perm, schur_opt, schur_lfil, kernel, fkernel_params,
+                         &breakdown);
+}
 
 
 int Nfft4GPAmdRankestNysScaled(const double* data, int n, int ldim, int d, int kernel, void* fkernel_params,
                                int max_rank, int nsample, int nsample_r)
 {
+   RandScope rand_scope;  // libc rand() as the reference draws it (internal.h)
    if (!need_device("Nfft4GPAmdRankestNysScaled")) return -1;
    RankCtx C;
    double *owned = nullptr, *owned_k = nullptr;
@@ -786,6 +815,7 @@ int Nfft4GPAmdRankestNysScaled(const double* data, int n, int ldim, int d, int k
 int Nfft4GPAmdRankestDefault(const double* data, int n, int ldim, int d, int kernel, void* fkernel_params,
                              int max_rank, int nsample, int nsample_r, double full_tol, int* perm)
 {
+   RandScope rand_scope;  // libc rand() as the reference draws it (internal.h)
    if (!need_device("Nfft4GPAmdRankestDefault")) return -1;
    RankCtx C;
    double *owned = nullptr, *owned_k = nullptr;
@@ -801,6 +831,7 @@ int Nfft4GPAmdRankestDefault(const double* data, int n, int ldim, int d, int ker
 int Nfft4GPAmdAfnRankEstimate(const double* data, int n, int ldim, int d, int max_k, int perm_opt, int nsamples,
                               int kernel, void* fkernel_params, int* perm)
 {
+   RandScope rand_scope;  // libc rand() as the reference draws it (internal.h)
    if (!need_device("Nfft4GPAmdAfnRankEstimate")) return -1;
    if (!perm) return -1;
    max_k = std::min(max_k, n);  // afn.c:167
@@ -835,6 +866,107 @@ int Nfft4GPAmdAfnRankEstimate(const double* data, int n, int ldim, int d, int ma
    const std::vector<int> full = expand_perm(sel.data(), (int)sel.size(), n);
    std::copy(full.begin(), full.end(), perm);
    return k;
+}
+
+
+/* Nfft4GPPrecondAFNSetup (afn.c:161-489) as one call: the rank estimation and ordering
+ * (Nfft4GPAmdAfnRankEstimate), then
+ *   k == 0 or k == n, or k == max_k: the AFN (Nfft4GPAmdAfnSetupSchur with that k and order);
+ *   0 < k < max_k: the rank-k Nystrom on those landmarks instead (afn.c:294-304, afn_setup.m:80-83);
+ *   the AFN's factors break down (K11 not positive definite, or the Schur FSAI meets a non-positive pivot):
+ *   the rank-max_k Nystrom on the same order, MATLAB's RAN fallback (afn_setup.m:93-98). */
+struct AfnFlow {
+   int kind = 0;  // 0 AFN, 1 Nystrom (rank below max_k), 2 Nystrom after an AFN breakdown (RAN)
+   int k = 0;
+   int n = 0;
+   void* afn = nullptr;
+   NysDev* nys = nullptr;
+};
+
+static NysDev* flow_nystrom(const double* data, int n, int ldim, int d, int kernel, void* fkernel_params,
+                            const int* perm, int k)
+{
+   KernelSpec K;
+   double* owned = nullptr;
+   const int additive = kernel_spec_of(fkernel_params, nullptr, kernel, n, K, &owned);
+   (void)hipFree(owned);
+   if (additive < 0) return nullptr;
+   if (additive) return (NysDev*)Nfft4GPAmdNysSetupAdditive(fkernel_params, perm, k, 1);
+   // the plain kernel of all d features is the additive kernel of one d-feature window (weight 1)
+   std::vector<double> xw((size_t)n * d);
+   for (int c = 0; c < d; c++) {
+      const hipMemcpyKind kind = is_device_ptr(data) ? hipMemcpyDeviceToHost : hipMemcpyHostToHost;
+      if (hipMemcpy(xw.data() + (size_t)c * n, data + (size_t)c * ldim, sizeof(double) * n, kind) != hipSuccess)
+         return nullptr;
+   }
+   return nys_setup_additive(xw.data(), n, 1, d, 0, kernel, K.f, K.l, K.mu, perm, k, 1);
+}
+
+void* Nfft4GPAmdPrecondAFNSetup(const double* data, int n, int ldim, int d, int max_k, int perm_opt, int schur_opt,
+                                int schur_lfil, int nsamples, int kernel, void* fkernel_params)
+{
+   RandScope rand_scope;  // libc rand() as the reference draws it (internal.h)
+   if (!need_device("Nfft4GPAmdPrecondAFNSetup")) return nullptr;
+   if (!data || !fkernel_params || n <= 0 || ldim < n || (perm_opt != 0 && perm_opt != 1)) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondAFNSetup needs data (ldim >= n), kernel parameters and "
+                      "perm_opt 0 (random) or 1 (FPS)\n");
+      return nullptr;
+   }
+   std::vector<int> perm(n);
+   const int max_kk = std::min(max_k, n);
+   const int k = Nfft4GPAmdAfnRankEstimate(data, n, ldim, d, max_k, perm_opt, nsamples, kernel, fkernel_params,
+                                           perm.data());
+   if (k < 0) return nullptr;
+   AfnFlow* F = new AfnFlow();
+   F->n = n;
+   F->k = k;
+   if (max_kk > 0 && k > 0 && k < n && k < max_kk) {
+      printf("The estimated rank %d is below max_k = %d: rank-%d Nystrom (afn.c:294-304)\n", k, max_kk, k);
+      F->kind = 1;
+      F->nys = flow_nystrom(data, n, ldim, d, kernel, fkernel_params, perm.data(), k);
+   } else {
+      bool breakdown = false;
+      F->afn = afn_setup_impl(data, n, ldim, d, k, 2, perm.data(), schur_opt, schur_lfil, kernel, fkernel_params,
+                              &breakdown);
+      if (!F->afn && breakdown && k > 0 && k < n) {
+         printf("AFN factors broke down: rank-%d Nystrom on the same order (afn_setup.m:93-98)\n", k);
+         F->kind = 2;
+         F->nys = flow_nystrom(data, n, ldim, d, kernel, fkernel_params, perm.data(), k);
+      }
+   }
+   if (!F->afn && !F->nys) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondAFNSetup failed\n");
+      delete F;
+      return nullptr;
+   }
+   return F;
+}
+
+int Nfft4GPAmdPrecondAFNSolve(void* pre, int n, double* x, double* rhs)
+{
+   AfnFlow* F = (AfnFlow*)pre;
+   if (!F || n != F->n) return -1;
+   return F->afn ? Nfft4GPAmdAfnSolve(F->afn, n, x, rhs) : Nfft4GPAmdNysSolve(F->nys, n, x, rhs);
+}
+
+int Nfft4GPAmdPrecondAFNInfo(void* pre, int* kind, int* k, void** afn, void** nys)
+{
+   AfnFlow* F = (AfnFlow*)pre;
+   if (!F) return -1;
+   if (kind) *kind = F->kind;
+   if (k) *k = F->k;
+   if (afn) *afn = F->afn;
+   if (nys) *nys = F->nys;
+   return 0;
+}
+
+void Nfft4GPAmdPrecondAFNFree(void* pre)
+{
+   AfnFlow* F = (AfnFlow*)pre;
+   if (!F) return;
+   if (F->afn) Nfft4GPAmdAfnFree(F->afn);
+   if (F->nys) Nfft4GPAmdNysFree(F->nys);
+   delete F;
 }
 
 }  // extern "C"

@@ -255,6 +255,22 @@ hipStream_t current_stream();
 bool is_device_ptr(const void* p);
 int device_ok();
 
+// ---- libc rand() of the reference (nfft_api.cpp) --------------------------------------------------
+// The reference draws libc rand() (Nfft4GPRandPerm, Nfft4GPVecRand, rankest.c), so after the same srand()
+// both libraries see the same numbers -- unless something else in the call draws too: the ROCm libraries
+// do while they initialise.  An entry point that draws opens a RandScope: the process runs on a private
+// random() state for the duration of the call, and each batch of the reference's draws runs inside a
+// CallerRandBatch on the caller's state (glibc rand() is random(); initstate / setstate switch its state).
+struct RandScope {
+   RandScope();
+   ~RandScope();
+};
+struct CallerRandBatch {
+   char* prev = nullptr;
+   CallerRandBatch();
+   ~CallerRandBatch();
+};
+
 // ---- multi-GPU (dist.hip) -----------------------------------------------------------------------
 // a process group: in-place sum of count device doubles over the ranks, ordered on stream s
 struct Comm {

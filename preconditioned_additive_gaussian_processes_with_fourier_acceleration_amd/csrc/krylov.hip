@@ -705,7 +705,10 @@ int lanczos_dev(Callbacks& cb, double* x, const double* rhs, int wsize, int maxi
          z = Z + (size_t)iter * n;
          v = V + (size_t)iter * n;
          std::vector<double> rnd(n);
-         for (size_t i = 0; i < n; i++) rnd[i] = (double)rand() / (double)RAND_MAX;  // Nfft4GPVecRand
+         {
+            CallerRandBatch caller;
+            for (size_t i = 0; i < n; i++) rnd[i] = (double)rand() / (double)RAND_MAX;  // Nfft4GPVecRand
+         }
          NFFT4GP_HIP_CHECK(hipMemcpy(z, rnd.data(), sizeof(double) * n, hipMemcpyHostToDevice));
          double td, te;
          if (mgs2(c, z, V, Z, iter - 1, &td, &te, &t)) return -1;
@@ -880,6 +883,7 @@ int Nfft4GPSolverLanczos(void* mat_data, int n, func_symmatvec matvec, void* pre
                          double* x, double* rhs, int wsize, int maxits, int atol, double tol, double* prel_res,
                          double** prel_res_v, int* piter, int* tsize, double** TDp, double** TEp, int print_level)
 {
+   RandScope rand_scope;  // libc rand() as the reference draws it (internal.h)
    if (!need_device("Nfft4GPSolverLanczos")) return -1;
    Callbacks cb;
    if (!make_callbacks(cb, n, matvec, mat_data, precondfunc, prec_data)) return -1;
@@ -897,6 +901,7 @@ int Nfft4GPLanczosQuadratureLogdet(void* mat_data, void* dmat_data, int n, func_
                                    func_trace tracefunc, func_logdet logdetfunc, func_dvp dvpfunc, int maxits,
                                    int nvecs, double* radamacher, int print_level, double* logdet, double** dlogdetp)
 {
+   RandScope rand_scope;  // libc rand() as the reference draws it (internal.h)
    if (!need_device("Nfft4GPLanczosQuadratureLogdet")) return -1;
    Callbacks cb, dcb;
    if (!make_callbacks(cb, n, matvec, mat_data, precondfunc, prec_data) ||
@@ -967,6 +972,7 @@ int Nfft4GPGpLoss(double* x, double* data, double* label, int n, int ldim, int d
                   nfft4gp_transform_type transform,
                   int* mask, int print_level, double* dwork, double* loss, double* grad)
 {
+   RandScope rand_scope;  // libc rand() as the reference draws it (internal.h)
    (void)precond_vfkernel_data_free;
    (void)wsize;
    if (!need_device("Nfft4GPGpLoss")) return -1;

@@ -24,6 +24,35 @@ using namespace nfft4gp_amd;
 
 namespace nfft4gp_amd {
 
+namespace {
+int g_rand_depth = 0;
+char* g_caller_rand = nullptr;
+char g_private_rand[256];
+}  // namespace
+
+RandScope::RandScope()
+{
+   if (g_rand_depth++ == 0) g_caller_rand = initstate(20240807u, g_private_rand, sizeof(g_private_rand));
+}
+
+RandScope::~RandScope()
+{
+   if (--g_rand_depth == 0) {
+      setstate(g_caller_rand);
+      g_caller_rand = nullptr;
+   }
+}
+
+CallerRandBatch::CallerRandBatch()
+{
+   if (g_rand_depth > 0) prev = setstate(g_caller_rand);
+}
+
+CallerRandBatch::~CallerRandBatch()
+{
+   if (prev) g_caller_rand = setstate(prev);
+}
+
 static hipStream_t g_stream = nullptr;
 
 hipStream_t current_stream() { return g_stream; }

@@ -20,6 +20,7 @@
 // kernel matrix of buffer slices, not of the landmarks perm[:k] (checked against the compiled reference
 // to 1e-11).  k11_mode 0 reproduces that (parity); k11_mode 1 uses K(perm[:k], perm[:k]), the matrix the
 // method intends, which is what makes the preconditioner effective.
+#include <cstdlib>
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rocsolver/rocsolver.h>  // types and prototypes only: the library is dlopen'ed on first use
@@ -528,6 +529,16 @@ RocSolver& rocsolver()
                                               "/opt/rocm/lib/librocsolver.so.0", "/opt/rocm/lib/librocsolver.so",
                                               nullptr};
    std::string why;
+   // rocBLAS / rocSOLVER draw libc rand() while they initialise (measured: the first rank estimation after an
+   // srand() then picked other subsamples than the second).  The reference's draws (Nfft4GPRandPerm,
+   // rankest.c) must see the caller's sequence, so the loading, the handle and one warm-up call of each
+   // routine run on a private random() state (initstate / setstate: rand() is random() in glibc).
+   static char priv_state[256];
+   char* caller_state = initstate(20240807u, priv_state, sizeof(priv_state));
+   struct Restore {
+      char* s;
+      ~Restore() { setstate(s); }
+   } restore{caller_state};
    void* hb = dlopen_first(blas_names, why);
    void* hs = hb ? dlopen_first(solver_names, why) : nullptr;
    auto create = hb ? (decltype(&rocblas_create_handle))dlsym(hb, "rocblas_create_handle") : nullptr;
@@ -542,6 +553,22 @@ RocSolver& rocsolver()
          why += "\n  rocblas_create_handle failed";
       else
          R.ok = true;
+   }
+   if (R.ok) {
+      // first calls initialise the libraries' internals (inside the private random() state)
+      double* A = nullptr;
+      int* info = nullptr;
+      if (hipMalloc((void**)&A, sizeof(double) * 8) == hipSuccess && hipMalloc((void**)&info, sizeof(int)) == hipSuccess) {
+         const double one[4] = {1.0, 0.0, 0.0, 1.0};
+         (void)hipMemcpy(A, one, sizeof(one), hipMemcpyHostToDevice);
+         (void)R.potrf(R.h, rocblas_fill_lower, 2, A, 2, info);
+         (void)R.trtri(R.h, rocblas_fill_lower, rocblas_diagonal_non_unit, 2, A, 2, info);
+         (void)hipMemcpy(A, one, sizeof(one), hipMemcpyHostToDevice);
+         (void)R.syevd(R.h, rocblas_evect_none, rocblas_fill_lower, 2, A, 2, A + 4, A + 6, info);
+         (void)hipDeviceSynchronize();
+      }
+      (void)hipFree(A);
+      (void)hipFree(info);
    }
    if (!R.ok)
       fprintf(stderr, "nfft4gp_amd: rocSOLVER could not be loaded; k x k Cholesky / inverse / eigensolves run on "

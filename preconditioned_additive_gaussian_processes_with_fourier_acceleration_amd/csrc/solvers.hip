@@ -581,9 +581,12 @@ void Nfft4GPVecFill(double* x, size_t n, double val)
 static void vec_random(double* x, int n, bool rademacher)
 {
    std::vector<double> h(std::max(0, n));
-   for (int i = 0; i < n; i++) {
-      h[i] = (double)rand() / (double)RAND_MAX;
-      if (rademacher) h[i] = h[i] < 0.5 ? -1.0 : 1.0;
+   {
+      CallerRandBatch caller;
+      for (int i = 0; i < n; i++) {
+         h[i] = (double)rand() / (double)RAND_MAX;
+         if (rademacher) h[i] = h[i] < 0.5 ? -1.0 : 1.0;
+      }
    }
    if (n > 0 && is_device_ptr(x))
       (void)hipMemcpy(x, h.data(), sizeof(double) * n, hipMemcpyHostToDevice);
@@ -975,7 +978,8 @@ bool library_operator(const void* fn)
           fn == (const void*)&Nfft4GPAmdAfnSolve || fn == (const void*)&Nfft4GPAmdPrecondNysSolve ||
           fn == (const void*)&Nfft4GPAmdPrecondNysDvp || fn == (const void*)&Nfft4GPAmdPrecondFsaiSolve ||
           fn == (const void*)&Nfft4GPAmdPrecondFsaiDvp || fn == (const void*)&Nfft4GPAmdDistMatSymv ||
-          fn == (const void*)&Nfft4GPAmdDistGradMatSymv || fn == (const void*)&Nfft4GPAmdDistNysSolve;
+          fn == (const void*)&Nfft4GPAmdDistGradMatSymv || fn == (const void*)&Nfft4GPAmdDistNysSolve ||
+          fn == (const void*)&Nfft4GPAmdPrecondAFNSolve;
 }
 }  // namespace nfft4gp_amd
 

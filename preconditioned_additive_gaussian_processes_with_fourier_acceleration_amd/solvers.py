@@ -219,19 +219,65 @@ class AfnPrecond(_Apply):
         return self.k, perm, (ia, ja, aa)
 
 
-def afn_rank_estimate(X, max_k: int, f: float, l: float, mu: float, perm_opt: str = "fps", nsamples: int = 500,
-                      kernel: int = 0):
+class PrecondAFN(_Apply):
+    """Nfft4GPPrecondAFNSetup (afn.c:161-489) as the reference runs it (Nfft4GPAmdPrecondAFNSetup): rank
+    estimation and ordering, then the AFN when the estimate reaches max_k (or k is 0 or n), the rank-k
+    Nystrom on the estimated landmarks when 0 < k < max_k (afn.c:294-304), and MATLAB's RAN fallback -- a
+    Nystrom on the same order -- when the AFN's factors break down (afn_setup.m:93-98).
+
+    ``kind`` is "afn", "nystrom" or "ran"; ``k`` the rank.  The kernel is the plain Gaussian / Matern-1/2 of X
+    (f, l, mu), or with ``op`` (an NFFTAdditiveKernel after its setup) the dense additive kernel of op's
+    windows and hyperparameters.  perm_opt: "random" (0) or "fps" (1); schur: "fsai" (schur_opt 3) or
+    "noise" (0).  max_k <= 0: the predefined rank -max_k in natural order, no estimation (afn.c:245-256)."""
+
+    _solve, _free = "Nfft4GPAmdPrecondAFNSolve", "Nfft4GPAmdPrecondAFNFree"
+    KINDS = ("afn", "nystrom", "ran")
+
+    def __init__(self, X, max_k: int, f: float = 1.0, l: float = 1.0, mu: float = 0.01, perm_opt: str = "random",
+                 schur: str = "fsai", schur_lfil: int = 20, nsamples: int = 500, kernel: int = 0, op=None):
+        L = _lib.lib()
+        X = np.asfortranarray(np.asarray(X, dtype=np.float64))
+        n, d = X.shape
+        params = op.h if op is not None else _lib.kernel_params(f, l, mu, n)
+        self.n = n
+        self.h = L.Nfft4GPAmdPrecondAFNSetup(X.ctypes.data, n, n, d, int(max_k), {"random": 0, "fps": 1}[perm_opt],
+                                             {"fsai": 3, "noise": 0}[schur], int(schur_lfil), int(nsamples),
+                                             int(kernel), params)
+        if op is None:
+            L.Nfft4GPKernelParamFree(params)
+        if not self.h:
+            raise RuntimeError("Nfft4GPAmdPrecondAFNSetup failed (see stderr)")
+        kind, k = C.c_int(), C.c_int()
+        L.Nfft4GPAmdPrecondAFNInfo(self.h, C.byref(kind), C.byref(k), None, None)
+        self.kind, self.k = self.KINDS[kind.value], k.value
+
+    def free(self):
+        if getattr(self, "h", None):
+            _lib.lib().Nfft4GPAmdPrecondAFNFree(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def afn_rank_estimate(X, max_k: int, f: float = 1.0, l: float = 1.0, mu: float = 0.01, perm_opt: str = "fps",
+                      nsamples: int = 500, kernel: int = 0, op=None):
     """Nfft4GPAmdAfnRankEstimate -- the rank / ordering step of Nfft4GPPrecondAFNSetup (afn.c:165-256) on
     the GPU: (k, perm).  k == max_k: build ``AfnPrecond.setup(X, k, ..., perm_opt="perm", perm=perm)``;
-    0 < k < max_k: the reference switches to a rank-k Nystrom (afn.c:287-296).  Draws libc rand()."""
+    0 < k < max_k: the reference switches to a rank-k Nystrom (afn.c:287-296) -- ``PrecondAFN`` makes that
+    choice.  With ``op`` the kernel is op's dense additive kernel.  Draws libc rand()."""
     L = _lib.lib()
     X = np.asfortranarray(np.asarray(X, dtype=np.float64))
     n, d = X.shape
     perm = np.zeros(n, np.int32)
-    params = _lib.kernel_params(f, l, mu, n)
+    params = op.h if op is not None else _lib.kernel_params(f, l, mu, n)
     k = L.Nfft4GPAmdAfnRankEstimate(X.ctypes.data, n, n, d, int(max_k), {"random": 0, "fps": 1}[perm_opt],
                                     int(nsamples), int(kernel), params, perm.ctypes.data)
-    L.Nfft4GPKernelParamFree(params)
+    if op is None:
+        L.Nfft4GPKernelParamFree(params)
     if k < 0:
         raise RuntimeError("Nfft4GPAmdAfnRankEstimate failed (see stderr)")
     return k, perm
