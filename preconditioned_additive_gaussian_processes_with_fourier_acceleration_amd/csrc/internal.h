@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -66,6 +68,32 @@ __host__ __device__ inline size_t quad_index(long long t, int w, int lane, int n
    return (((size_t)t * (size_t)(nwords / 4) + (size_t)(w >> 2)) * kWave + (size_t)lane) * 4 + (size_t)(w & 3);
 }
 
+// std::allocator that leaves trivially constructible elements uninitialised (resize / construction without
+// a value): the layout arrays (3.6 GB at config E) are written in full by their builder, zero-filling them
+// first cost ~1 s
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+   template <class U>
+   struct rebind {
+      using other = DefaultInitAlloc<U>;
+   };
+   DefaultInitAlloc() = default;
+   template <class U>
+   DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+   template <class U>
+   void construct(U* p) noexcept
+   {
+      ::new ((void*)p) U;
+   }
+   template <class U, class... A>
+   void construct(U* p, A&&... a)
+   {
+      ::new ((void*)p) U(std::forward<A>(a)...);
+   }
+};
+template <class T>
+using RawVec = std::vector<T, DefaultInitAlloc<T>>;
+
 struct Layout {
    int n = 0;           // local points
    int nw = 0;          // components
@@ -74,13 +102,13 @@ struct Layout {
    int ngroups = 0;
    int nblocks = 0;
    long long ntiles = 0;
-   std::vector<uint16_t> meta;     // [ntiles*64]      comp<<6 | cell
-   std::vector<uint32_t> lo;       // [ntiles*R/4*64]  local index bits 0-5, one byte per point
-   std::vector<uint32_t> q;        // [ntiles*R*64]    offset in cell (26 bits) | index bits 6-11
+   RawVec<uint16_t> meta;          // [ntiles*64]      comp<<6 | cell
+   RawVec<uint32_t> lo;            // [ntiles*R/4*64]  local index bits 0-5, one byte per point
+   RawVec<uint32_t> q;             // [ntiles*R*64]    offset in cell (26 bits) | index bits 6-11
    std::vector<int> tile_off;      // [nblocks*ngroups+1]
 };
 // build from per-component quantized coordinates qc[c*n + j]
-void build_layout(const std::vector<uint32_t>& qc, int n, int nw, int B, int CG, Layout& L);
+void build_layout(const uint32_t* qc, int n, int nw, int B, int CG, Layout& L);
 
 // ---- device plan --------------------------------------------------------------------------------
 struct DevLayout {

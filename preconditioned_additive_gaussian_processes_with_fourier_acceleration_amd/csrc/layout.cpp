@@ -77,7 +77,7 @@ void balance_tile(uint32_t (*loc)[kR], uint32_t (*fr)[kR])
 // tiles.  With arrays, writes them into tiles [t0, t0 + T) where T = ntiles: chunk k goes to tile
 // t0 + k % T, lane k / T ("dealt" column-wise), so the 64 lanes of a tile hold chunks T apart in the
 // sorted order -- different cells -- and their LDS flushes do not collide on one address.
-long long emit_block_group(const std::vector<uint32_t>& qc, int n, int nw, int B, int CG, int b, int g,
+long long emit_block_group(const uint32_t* qc, int n, int nw, int B, int CG, int b, int g,
                            const ChunkSink* out, long long t0, long long T, std::vector<int>& cnt,
                            std::vector<int>& off, std::vector<uint16_t>& sorted)
 {
@@ -98,7 +98,7 @@ long long emit_block_group(const std::vector<uint32_t>& qc, int n, int nw, int B
    }
    long long nchunks = 0;
    for (int c = c0; c < c1; c++) {
-      const uint32_t* qq = qc.data() + (size_t)c * n + base;
+      const uint32_t* qq = qc + (size_t)c * n + base;
       std::fill(cnt.begin(), cnt.end(), 0);
       for (int j = 0; j < nloc; j++) cnt[qq[j] >> 26]++;
       off[0] = 0;
@@ -156,7 +156,7 @@ void parallel_for(int nitems, F&& f)
 
 }  // namespace
 
-void build_layout(const std::vector<uint32_t>& qc, int n, int nw, int B, int CG, Layout& L)
+void build_layout(const uint32_t* qc, int n, int nw, int B, int CG, Layout& L)
 {
    L.n = n;
    L.nw = nw;
@@ -180,9 +180,9 @@ void build_layout(const std::vector<uint32_t>& qc, int n, int nw, int B, int CG,
    }
    L.tile_off[nbg] = (int)acc;
    L.ntiles = acc;
-   L.meta.assign((size_t)acc * kWave, 0);
-   L.lo.assign((size_t)acc * (kR / 4) * kWave, 0);
-   L.q.assign((size_t)acc * kR * kWave, 0);
+   L.meta.resize((size_t)acc * kWave);  // every element is written below (emit_block_group)
+   L.lo.resize((size_t)acc * (kR / 4) * kWave);
+   L.q.resize((size_t)acc * kR * kWave);
    ChunkSink sink{L.meta.data(), L.lo.data(), L.q.data()};
    parallel_for(L.nblocks, [&](int b) {
       std::vector<int> cnt(kNos), off(kNos + 1);

@@ -10,6 +10,9 @@
 
 #include <array>
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -153,8 +156,8 @@ void free_plan(PlanExt* E)
    delete E;
 }
 
-template <class T>
-int upload(T** dptr, const std::vector<T>& h)
+template <class T, class A>
+int upload(T** dptr, const std::vector<T, A>& h)
 {
    if (*dptr) {
       (void)hipFree(*dptr);
@@ -206,7 +209,7 @@ uint32_t quantize(double x)
 int plan_build_points(AdditivePlan& P, const double* buffer)
 {
    const int ng = P.n_global;
-   std::vector<uint32_t> qc((size_t)P.nw * P.n);
+   RawVec<uint32_t> qc((size_t)P.nw * P.n);  // every entry is written below
    P.comp_scale.assign(P.nw, 1.0);
    std::vector<double> xs;
    if (std::any_of(P.comp_dims.begin(), P.comp_dims.end(), [](int d) { return d != 1; })) {
@@ -225,19 +228,36 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
       P.points_ready = true;
       return 0;
    }
-   for (int c = 0; c < P.nw; c++) {
-      const double* col = buffer + (size_t)c * ng * P.dw;  // nfft_interface.c:703 stride n*dwindows
-      P.comp_scale[c] = centre_and_scale(col, ng, 1, xs);
+   // windows are independent: one host thread per window at a time (centre, scale, quantize)
+   const auto t0 = std::chrono::steady_clock::now();
+   std::atomic<int> next{0};
+   auto work = [&]() {
+      std::vector<double> xw;
+      for (int c = next++; c < P.nw; c = next++) {
+         const double* col = buffer + (size_t)c * ng * P.dw;  // nfft_interface.c:703 stride n*dwindows
+         P.comp_scale[c] = centre_and_scale(col, ng, 1, xw);
+         if (P.comp_scale[c] < 0.0) continue;
+         for (int j = 0; j < P.n; j++) qc[(size_t)c * P.n + j] = quantize(xw[(size_t)P.row_begin + j]);
+      }
+   };
+   {
+      const int nt = std::max(1, std::min({16, P.nw, (int)std::thread::hardware_concurrency()}));
+      std::vector<std::thread> th;
+      for (int t = 1; t < nt; t++) th.emplace_back(work);
+      work();
+      for (auto& t : th) t.join();
+   }
+   for (int c = 0; c < P.nw; c++)
       if (P.comp_scale[c] < 0.0) {
          fprintf(stderr,
                  "nfft4gp_amd: all points of window %d coincide (radius 0); the reference's scaling "
                  "0.25/radius (nfft_interface.c:190) is undefined there.\n", c);
          return -1;
       }
-      for (int j = 0; j < P.n; j++) qc[(size_t)c * P.n + j] = quantize(xs[(size_t)P.row_begin + j]);
-   }
+   const auto t1 = std::chrono::steady_clock::now();
    Layout L;
-   build_layout(qc, P.n, P.nw, P.B, P.CG, L);
+   build_layout(qc.data(), P.n, P.nw, P.B, P.CG, L);
+   const auto t2 = std::chrono::steady_clock::now();
    P.ngroups = L.ngroups;
    P.nblocks = L.nblocks;
    free_layout(P);
@@ -246,6 +266,12 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
       return -1;
    P.dl.ntiles = L.ntiles;
    P.dl.bytes = L.meta.size() * 2 + L.lo.size() * 4 + L.q.size() * 4 + L.tile_off.size() * 4;
+   if (getenv("NFFT4GP_AMD_VERBOSE")) {
+      const auto t3 = std::chrono::steady_clock::now();
+      auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+      fprintf(stderr, "nfft4gp_amd: layout setup: centre/scale/quantize %.1f ms, layout %.1f ms, upload %.1f ms\n",
+              ms(t0, t1), ms(t1, t2), ms(t2, t3));
+   }
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part, sizeof(double) * (size_t)std::max(1, P.nblocks) * P.nw * kNos));
    dfree(P.d_dot_part);
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_dot_part, sizeof(double) * (size_t)std::max(1, P.nblocks)));
@@ -253,6 +279,7 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
       NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_dot_ticket, sizeof(unsigned int) * kTicketWords));
       NFFT4GP_HIP_CHECK(hipMemset(P.d_dot_ticket, 0, sizeof(unsigned int) * kTicketWords));
    }
+
    if (!P.d_H) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_H, sizeof(double) * (size_t)P.nw * kNos * kNC));
    if (!P.d_Hd) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_Hd, sizeof(double) * (size_t)P.nw * kNos * kNC));
    if (upload_tap_coeffs()) return -1;
@@ -859,9 +886,8 @@ int Nfft4GPAmdHostLayout(const unsigned int* qc, int n, int nw, int B, int CG, l
                          unsigned short* meta, unsigned int* lo, unsigned int* q, int* tile_off)
 {
    if (B <= 0 || B > kMaxBlock || CG <= 0 || n < 0 || nw <= 0 || nw > 1023) return -1;
-   std::vector<uint32_t> v(qc, qc + (size_t)n * nw);
    Layout L;
-   build_layout(v, n, nw, B, CG, L);
+   build_layout(qc, n, nw, B, CG, L);
    counts[0] = L.ntiles;
    counts[1] = L.ngroups;
    counts[2] = L.nblocks;
