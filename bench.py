@@ -323,6 +323,9 @@ def main():
     # one GPU (RCCL refuses duplicate devices); the driver's multi-GPU runs use the default, nccl (RCCL)
     dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
+    # one dedicated stream for torch and the library: launches on the legacy null stream carry its implicit
+    # synchronisation and cost ~8 us per matvec (tools/graph_probe.py: 93 -> 85 us at config C)
+    torch.cuda.set_stream(torch.cuda.Stream())
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group(os.environ.get("NFFT4GP_BENCH_BACKEND", "nccl"))
