@@ -402,10 +402,28 @@ int Nfft4GPAmdAfnRankEstimate(const NFFT4GP_DOUBLE *data, int n, int ldim, int d
  * is the func_solve of whichever was built; Nfft4GPAmdPrecondAFNInfo reports kind (0 AFN, 1 Nystrom below
  * max_k, 2 Nystrom after a breakdown), k and the underlying Nfft4GPAmdAfn* / Nfft4GPAmdNys* handle. */
 void *Nfft4GPAmdPrecondAFNSetup(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int max_k, int perm_opt,
-                                int schur_opt, int schur_lfil, int nsamples, int kernel, void *fkernel_params);
+                                int schur_opt, int schur_lfil, int nsamples, int kernel, void *fkernel_params,
+                                int require_grad);
 int Nfft4GPAmdPrecondAFNSolve(void *pre, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
 int Nfft4GPAmdPrecondAFNInfo(void *pre, int *kind, int *k, void **afn, void **nys);
 void Nfft4GPAmdPrecondAFNFree(void *pre);
+/* The same preconditioner behind the interface Nfft4GPGpLoss takes (gp_loss.c:96-307: precond_kernel_setup,
+ * func_solve, func_trace, func_logdet, func_dvp, reset): Create keeps the parameters, SetupWithKernel
+ * rebuilds on every loss call (fkernel Nfft4GPNFFTAdditiveKernelMatern12Kernel selects Matern-1/2, anything
+ * else the Gaussian).  With require_grad the AFN keeps its gradient pieces -- MATLAB afn_setup.m / afn_dvp.m /
+ * afn_trace.m / afn_logdet.m; the reference's C afn.c has none: dL11 = L Phi(L^{-1} dK11 L^{-T}), dK12, the
+ * Schur FSAI's dG from the Schur kernel's gradient (schurCombinedKernelMat.m) -- and the Nystrom branches
+ * are Nfft4GPAmdPrecondNys* with gradients (additive handle as kernel data).  Dvp returns
+ * M^{-1} (dM/dtheta_g) x like the reference's nys.c / fsai.c (afn_dvp.m returns (dM/dtheta_g) x: the
+ * result goes through the apply once more); Trace = tr(M^{-1} dM/dtheta_g), Logdet = log det M.
+ * AFN gradients need 0 < k < n and schur_opt 3. */
+void *Nfft4GPAmdPrecondAFNCreate(int max_k, int perm_opt, int schur_opt, int schur_lfil, int nsamples);
+int Nfft4GPAmdPrecondAFNSetupWithKernel(NFFT4GP_DOUBLE *data, int n, int ldim, int d, func_kernel fkernel,
+                                        void *fkernel_params, int require_grad, void *pre);
+int Nfft4GPAmdPrecondAFNDvp(void *pre, int n, int *mask, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE **yp);
+int Nfft4GPAmdPrecondAFNTrace(void *pre, NFFT4GP_DOUBLE **tracesp);
+NFFT4GP_DOUBLE Nfft4GPAmdPrecondAFNLogdet(void *pre);
+void Nfft4GPAmdPrecondAFNReset(void *pre);
 
 /* ---- farthest point sampling (SRC/linearalg/ordering.c) -------------------------------------------
  * Nfft4GPSortFps with kFpsAlgorithmParallel1 (ordering.c:422-739): *k in: the number of points to select

@@ -148,7 +148,13 @@ _SIGS = {
     "Nfft4GPAmdShardFinish": (C.c_int, [vp, vp, C.c_int, C.c_double, vp, C.c_double, vp]),
     "Nfft4GPAmdShardGridSize": (C.c_longlong, [vp]),
     "Nfft4GPAmdPrecondAFNSetup": (vp, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
-                                      C.c_int, vp]),
+                                      C.c_int, vp, C.c_int]),
+    "Nfft4GPAmdPrecondAFNCreate": (vp, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "Nfft4GPAmdPrecondAFNSetupWithKernel": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp]),
+    "Nfft4GPAmdPrecondAFNDvp": (C.c_int, [vp, C.c_int, vp, vp, vp]),
+    "Nfft4GPAmdPrecondAFNTrace": (C.c_int, [vp, vp]),
+    "Nfft4GPAmdPrecondAFNLogdet": (C.c_double, [vp]),
+    "Nfft4GPAmdPrecondAFNReset": (None, [vp]),
     "Nfft4GPAmdPrecondAFNSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdPrecondAFNInfo": (C.c_int, [vp, ip, ip, C.POINTER(vp), C.POINTER(vp)]),
     "Nfft4GPAmdPrecondAFNFree": (None, [vp]),

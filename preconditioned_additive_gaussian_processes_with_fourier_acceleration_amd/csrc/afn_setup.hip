@@ -249,6 +249,35 @@ __global__ __launch_bounds__(256) void k_kmat(const double* __restrict__ X, long
    out[(size_t)j * ldo + i] = K;
 }
 
+// out[i + j*ldo] = dK_g(x_{row0+i}, x_{col0+j}) (kernel_eval.hpp: g = 0 f, 1 l, 2 mu)
+__global__ __launch_bounds__(256) void k_kmat_grad(const double* __restrict__ X, long long ldx, int row0, int m,
+                                                   int col0, KernelParams P, int diag_noise, int g,
+                                                   double* __restrict__ out, long long ldo)
+{
+   const int i = blockIdx.x * 256 + threadIdx.x;
+   const int j = blockIdx.y;
+   if (i >= m) return;
+   double K, dK[3];
+   kern_pair(P, X, ldx, row0 + i, col0 + j, diag_noise && row0 + i == col0 + j, K, dK);
+   out[(size_t)j * ldo + i] = dK[g];
+}
+
+// Phi(M) of chol_setup.m: the lower triangle with the diagonal halved, in place
+__global__ void k_phi(double* M, int k)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
+   if (i >= k) return;
+   double& v = M[i + (size_t)j * k];
+   if (i < j) v = 0.0;
+   else if (i == j) v *= 0.5;
+}
+
+__global__ void k_diag_of(const double* __restrict__ A, int k, double* __restrict__ out)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < k) out[i] = A[i + (size_t)i * k];
+}
+
 __global__ void k_gather_points(const double* __restrict__ X, long long ldim, int n, int d, const int* __restrict__ perm,
                                 double* __restrict__ Xp)
 {
@@ -659,9 +688,14 @@ namespace {
 // definite, or a row of the Schur complement's FSAI with a non-positive pivot: non-finite values, MATLAB's
 // ~isreal(PRE.GS), afn_setup.m:93-98)
 void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm_opt, const int* perm, int schur_opt,
-                     int schur_lfil, int kernel, void* fkernel_params, bool* breakdown)
+                     int schur_lfil, int kernel, void* fkernel_params, bool* breakdown, AfnGrad** gout = nullptr)
 {
    *breakdown = false;
+   if (gout) *gout = nullptr;
+   if (gout && (k <= 0 || k >= n || schur_opt != 3)) {
+      fprintf(stderr, "nfft4gp_amd: AFN gradients need 0 < k < n and the Schur FSAI (schur_opt 3)\n");
+      return nullptr;
+   }
    if (!data || !fkernel_params || n <= 0 || ldim < n || d <= 0 || k < 0 || k > n || perm_opt < 0 || perm_opt > 2 ||
        (perm_opt == 2 && !perm) || (schur_opt != 0 && schur_opt != 3) || (schur_opt == 0 && k == 0)) {
       fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup needs data (ldim >= n), kernel parameters, 0 <= k <= n, "
@@ -678,15 +712,21 @@ void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm
    const int n2 = n - k;
    double *dX = nullptr, *Xp = nullptr, *Xkp = nullptr, *K11 = nullptr, *G = nullptr, *Gt = nullptr, *K12 = nullptr,
           *W = nullptr;
+   // gradients: L, dK11 / GdKG (3 k x k each), dL, dK12 (2 panels), B (2) and C (3) panels of the Schur FSAI
+   double *Lf = nullptr, *dK11 = nullptr, *GdKG = nullptr, *dLg = nullptr, *dK12 = nullptr, *PB = nullptr,
+          *PC = nullptr, *tmp = nullptr;
+   AfnGrad* AG = nullptr;
    int *dperm = nullptr, *dinfo = nullptr;
    void* S = nullptr;
    auto fail = [&](const char* what) -> void* {
       if (what) fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: %s failed\n", what);
       (void)hipStreamSynchronize(s);
       for (void* p : {(void*)dX, (void*)Xp, (void*)Xkp, (void*)dXk, (void*)K11, (void*)G, (void*)Gt, (void*)K12,
-                      (void*)W, (void*)dperm, (void*)dinfo})
+                      (void*)W, (void*)dperm, (void*)dinfo, (void*)Lf, (void*)dK11, (void*)GdKG, (void*)dLg,
+                      (void*)dK12, (void*)PB, (void*)PC, (void*)tmp})
          (void)hipFree(p);
       if (S) Nfft4GPAmdFsaiFree(S);
+      if (AG) afn_grad_free(AG);
       return nullptr;
    };
    if (dalloc(&dX, (size_t)ldim * d)) return fail("allocation");
@@ -726,6 +766,10 @@ void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm
       if (dalloc(&K11, kk) || dalloc(&G, kk) || dalloc(&Gt, kk) || dalloc(&dinfo, 1)) return fail("allocation");
       hipLaunchKernelGGL(k_kmat, dim3((k + 255) / 256, k), dim3(256), 0, s, Xk, (long long)n, 0, k, 0, P, 1, K11,
                          (long long)k);
+      if (gout) {  // L itself (afn_dvp.m multiplies by L and L'): a second potrf on a copy
+         if (dalloc(&Lf, kk) || hipMemcpyAsync(Lf, K11, sizeof(double) * kk, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return fail("allocation");
+      }
       const int info = chol_inverse_dev(K11, k, 0.0, G, Gt, dinfo, s);
       if (info > 0) {
          fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: K11 is not positive definite (column %d)\n", info);
@@ -733,6 +777,7 @@ void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm
          return fail(nullptr);
       }
       if (info < 0) return fail("Cholesky / triangular inverse of K11");
+      if (gout && chol_factor_dev(Lf, k, dinfo, s)) return fail("Cholesky of K11");
    }
    if (n2 > 0 && k > 0) {
       // K12 = K(X1, X2) (afn.c:436), W = L11^{-1} K12 (afn.c:443, dtrtrs; the Schur FSAI's kernel)
@@ -743,6 +788,35 @@ void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm
                             K12 + (size_t)j0 * k, (long long)k);
       }
       if (schur_opt == 3 && gemm_f64(false, k, n2, k, G, k, K12, k, W, k, s)) return fail("gemm");
+   }
+   if (gout) {
+      // chol_setup.m with require_grad: GdKG_g = L^{-1} dK11_g L^{-T}, dL_g = L Phi(GdKG_g); the Schur kernel's
+      // panels B_g = L^{-1} dK12_g and C_g = GdKG_g L^{-1} K12 (schurCombinedKernel.m); dK12_mu = 0
+      const size_t kn2 = (size_t)k * n2;
+      if (dalloc(&dK11, 3 * kk) || dalloc(&GdKG, 3 * kk) || dalloc(&dLg, 3 * kk) || dalloc(&tmp, kk) ||
+          dalloc(&dK12, 2 * kn2) || dalloc(&PB, 2 * kn2) || dalloc(&PC, 3 * kn2))
+         return fail("allocation (gradients)");
+      for (int g = 0; g < 3; g++) {
+         double* dKg = dK11 + g * kk;
+         double* GdKGg = GdKG + g * kk;
+         hipLaunchKernelGGL(k_kmat_grad, dim3((k + 255) / 256, k), dim3(256), 0, s, Xk, (long long)n, 0, k, 0, P, 1, g,
+                            dKg, (long long)k);
+         if (gemm_f64(false, k, k, k, G, k, dKg, k, tmp, k, s) || gemm_f64(false, k, k, k, tmp, k, Gt, k, GdKGg, k, s))
+            return fail("gemm (GdKG)");
+         if (hipMemcpyAsync(tmp, GdKGg, sizeof(double) * kk, hipMemcpyDeviceToDevice, s) != hipSuccess) return fail("copy");
+         hipLaunchKernelGGL(k_phi, dim3((k + 255) / 256, k), dim3(256), 0, s, tmp, k);
+         if (gemm_f64(false, k, k, k, Lf, k, tmp, k, dLg + g * kk, k, s)) return fail("gemm (dL)");
+         if (gemm_f64(false, k, n2, k, GdKGg, k, W, k, PC + g * kn2, k, s)) return fail("gemm (C)");
+      }
+      for (int g = 0; g < 2; g++) {
+         for (int j0 = 0; j0 < n2; j0 += 65535) {
+            const int nb = std::min(65535, n2 - j0);
+            hipLaunchKernelGGL(k_kmat_grad, dim3((k + 255) / 256, nb), dim3(256), 0, s, Xk, (long long)n, 0, k, k + j0, P,
+                               0, g, dK12 + g * kn2 + (size_t)j0 * k, (long long)k);
+         }
+         if (gemm_f64(false, k, n2, k, G, k, dK12 + g * kn2, k, PB + g * kn2, k, s)) return fail("gemm (B)");
+      }
+      if (hipGetLastError() != hipSuccess) return fail("gradient kernels");
    }
    if (n2 > 0 && schur_opt == 3) {
       // FSAI of the Schur complement on X2 (afn.c:445-473): KNN on the points' coordinates, values of the
@@ -759,10 +833,16 @@ void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm
          }
       KernelSpec K2 = Kp;
       K2.Xk = additive ? Xkp + k : nullptr;  // column c of the last n2 points: Xkp + c*n + k + i
-      const int rc = fsai_kernel_csr(X2, n2, n2, d, schur_lfil, K2, W, k > 0 ? k : 0, 0, ia, ja, aa, da, s);
+      const int rc = fsai_kernel_csr(X2, n2, n2, d, schur_lfil, K2, W, k > 0 ? k : 0, gout ? 1 : 0, ia, ja, aa, da, s,
+                                     PB, PC);
       (void)hipStreamSynchronize(s);
       (void)hipFree(X2);
       if (rc) return fail("Schur-complement FSAI");
+      if (gout && !std::all_of(da.begin(), da.end(), [](double v) { return std::isfinite(v); })) {
+         fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: the Schur FSAI's gradients are not finite\n");
+         *breakdown = true;
+         return fail(nullptr);
+      }
       if (!std::all_of(aa.begin(), aa.end(), [](double v) { return std::isfinite(v); })) {
          fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: the Schur complement's FSAI broke down (non-positive "
                          "pivot)\n");
@@ -771,16 +851,64 @@ void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm
       }
       S = Nfft4GPAmdFsaiCreate(n2, ia.data(), ja.data(), aa.data());
       if (!S) return fail("FSAI upload");
+      if (gout) {
+         AG = new AfnGrad();
+         AG->S = fsai_grad_create(n2, ia.data(), ja.data(), aa.data(), da.data());
+         if (!AG->S) return fail("FSAI (gradients) upload");
+      }
+   }
+   if (gout) {
+      // trace (afn_trace.m) and logdet (afn_logdet.m) from the diagonals; the factors the dvp keeps
+      std::vector<double> hL(k), hdL(3 * (size_t)k);
+      hipLaunchKernelGGL(k_diag_of, dim3((k + 255) / 256), dim3(256), 0, s, Lf, k, tmp);
+      for (int g = 0; g < 3; g++)
+         hipLaunchKernelGGL(k_diag_of, dim3((k + 255) / 256), dim3(256), 0, s, dLg + g * kk, k, tmp + (size_t)(g + 1) * k);
+      if (hipMemcpyAsync(hL.data(), tmp, sizeof(double) * k, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipMemcpyAsync(hdL.data(), tmp + k, sizeof(double) * 3 * k, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+         return fail("copy");
+      double ld = 0.0;
+      for (int i = 0; i < k; i++) ld += std::log(hL[i]);
+      AG->logdet = 2.0 * (ld + fsai_grad_diag(AG->S, -1, s));
+      for (int g = 0; g < 3; g++) {
+         double t = 0.0;
+         for (int i = 0; i < k; i++) t += hdL[(size_t)g * k + i] / hL[i];
+         // the Schur part: diagU = 1 / G_ii, diagdU = -dG_ii / G_ii^2, so sum diagdU / diagU = -sum dG_ii / G_ii
+         AG->trace[g] = 2.0 * (t - fsai_grad_diag(AG->S, g, s));
+      }
+      AG->n = n;
+      AG->k = k;
+      AG->n2 = n2;
+      if (dalloc(&AG->perm, n) ||
+          hipMemcpyAsync(AG->perm, dperm, sizeof(int) * n, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+          dalloc(&AG->Linv, kk) || hipMemcpyAsync(AG->Linv, G, sizeof(double) * kk, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+          dalloc(&AG->LinvT, kk) ||
+          hipMemcpyAsync(AG->LinvT, Gt, sizeof(double) * kk, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+          dalloc(&AG->work, 6 * (size_t)n + 8 * (size_t)k))
+         return fail("allocation (gradients)");
+      AG->L = Lf;
+      AG->dL = dLg;
+      AG->dK12 = dK12;
+      AG->K12 = K12;
+      Lf = dLg = dK12 = nullptr;
    }
    (void)hipStreamSynchronize(s);
-   for (void* p : {(void*)dX, (void*)Xp, (void*)Xkp, (void*)dXk, (void*)K11, (void*)W, (void*)dinfo}) (void)hipFree(p);
+   for (void* p : {(void*)dX, (void*)Xp, (void*)Xkp, (void*)dXk, (void*)K11, (void*)W, (void*)dinfo, (void*)dK11,
+                   (void*)GdKG, (void*)PB, (void*)PC, (void*)tmp})
+      (void)hipFree(p);
    dX = Xp = Xkp = dXk = K11 = W = nullptr;
+   dK11 = GdKG = PB = PC = tmp = nullptr;
    dinfo = nullptr;
    // schur_opt 0 (afn.c:451-459): S^{-1} = I / _noise_level
    void* A = afn_create_device(n, k, dperm, G, Gt, K12, S, schur_opt == 0 ? 1.0 / K.mu : 0.0);
    if (!A) {
       fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: allocation failed\n");
+      if (AG) afn_grad_free(AG);
       return nullptr;  // afn_create_device released the factors and S
+   }
+   if (gout) {
+      AG->afn = A;
+      *gout = AG;
    }
    return A;
 }
@@ -869,18 +997,36 @@ int Nfft4GPAmdAfnRankEstimate(const double* data, int n, int ldim, int d, int ma
 }
 
 
-/* Nfft4GPPrecondAFNSetup (afn.c:161-489) as one call: the rank estimation and ordering
- * (Nfft4GPAmdAfnRankEstimate), then
+/* Nfft4GPPrecondAFNSetup (afn.c:161-489): the rank estimation and ordering (Nfft4GPAmdAfnRankEstimate), then
  *   k == 0 or k == n, or k == max_k: the AFN (Nfft4GPAmdAfnSetupSchur with that k and order);
  *   0 < k < max_k: the rank-k Nystrom on those landmarks instead (afn.c:294-304, afn_setup.m:80-83);
  *   the AFN's factors break down (K11 not positive definite, or the Schur FSAI meets a non-positive pivot):
- *   the rank-max_k Nystrom on the same order, MATLAB's RAN fallback (afn_setup.m:93-98). */
+ *   the Nystrom on the same order, MATLAB's RAN fallback (afn_setup.m:93-98).
+ * With require_grad the AFN keeps its gradient pieces (afn_grad.hip) and the Nystrom branches are the
+ * Nystrom-with-gradients of nys_grad.hip (an additive handle of this library as kernel data). */
 struct AfnFlow {
+   // parameters (Nfft4GPAmdPrecondAFNCreate)
+   int max_k = 0, perm_opt = 0, schur_opt = 3, schur_lfil = 20, nsamples = 500;
+   // what the last setup built
    int kind = 0;  // 0 AFN, 1 Nystrom (rank below max_k), 2 Nystrom after an AFN breakdown (RAN)
    int k = 0;
    int n = 0;
    void* afn = nullptr;
-   NysDev* nys = nullptr;
+   NysDev* nys = nullptr;     // Nystrom branches without gradients
+   void* nysg = nullptr;      // Nystrom branches with gradients (Nfft4GPAmdPrecondNys* handle)
+   AfnGrad* grad = nullptr;   // the AFN's gradient pieces
+   void reset()
+   {
+      if (grad) afn_grad_free(grad);
+      if (afn) Nfft4GPAmdAfnFree(afn);
+      if (nys) Nfft4GPAmdNysFree(nys);
+      if (nysg) Nfft4GPAmdPrecondNysFree(nysg);
+      grad = nullptr;
+      afn = nullptr;
+      nys = nullptr;
+      nysg = nullptr;
+      kind = k = n = 0;
+   }
 };
 
 static NysDev* flow_nystrom(const double* data, int n, int ldim, int d, int kernel, void* fkernel_params,
@@ -902,40 +1048,109 @@ static NysDev* flow_nystrom(const double* data, int n, int ldim, int d, int kern
    return nys_setup_additive(xw.data(), n, 1, d, 0, kernel, K.f, K.l, K.mu, perm, k, 1);
 }
 
+// the Nystrom with gradients on the landmarks perm[:k] (nys.c:518-660 restated, K11 on the landmarks)
+static void* flow_nystrom_grad(double* data, int n, int ldim, int d, int kernel, void* fkernel_params, int* perm,
+                               int k)
+{
+   KernelSpec K;
+   double* owned = nullptr;
+   const int additive = kernel_spec_of(fkernel_params, nullptr, kernel, n, K, &owned);
+   (void)hipFree(owned);
+   if (additive != 1) {
+      fprintf(stderr, "nfft4gp_amd: the AFN's Nystrom branch with gradients needs this library's additive handle as "
+                      "kernel data\n");
+      return nullptr;
+   }
+   void* N = Nfft4GPAmdPrecondNysCreate();
+   Nfft4GPAmdPrecondNysSetRank(N, k);
+   Nfft4GPAmdPrecondNysSetPerm(N, perm, 0);
+   Nfft4GPAmdPrecondNysSetK11Mode(N, 1);
+   func_kernel fk = K.kernel ? &Nfft4GPNFFTAdditiveKernelMatern12Kernel : &Nfft4GPNFFTAdditiveKernelGaussianKernel;
+   if (Nfft4GPAmdPrecondNysSetupWithKernel(data, n, ldim, d, fk, fkernel_params, 1, N)) {
+      Nfft4GPAmdPrecondNysFree(N);
+      return nullptr;
+   }
+   return N;
+}
+
+static int flow_setup(AfnFlow* F, double* data, int n, int ldim, int d, int kernel, void* fkernel_params, int grad)
+{
+   F->reset();
+   std::vector<int> perm(n);
+   const int max_kk = std::min(F->max_k, n);
+   const int k = Nfft4GPAmdAfnRankEstimate(data, n, ldim, d, F->max_k, F->perm_opt, F->nsamples, kernel,
+                                           fkernel_params, perm.data());
+   if (k < 0) return -1;
+   F->n = n;
+   F->k = k;
+   auto nystrom = [&](int kind) {
+      F->kind = kind;
+      if (grad)
+         F->nysg = flow_nystrom_grad(data, n, ldim, d, kernel, fkernel_params, perm.data(), k);
+      else
+         F->nys = flow_nystrom(data, n, ldim, d, kernel, fkernel_params, perm.data(), k);
+   };
+   if (max_kk > 0 && k > 0 && k < n && k < max_kk) {
+      printf("The estimated rank %d is below max_k = %d: rank-%d Nystrom (afn.c:294-304)\n", k, max_kk, k);
+      nystrom(1);
+   } else {
+      bool breakdown = false;
+      F->afn = afn_setup_impl(data, n, ldim, d, k, 2, perm.data(), F->schur_opt, F->schur_lfil, kernel,
+                              fkernel_params, &breakdown, grad ? &F->grad : nullptr);
+      if (!F->afn && breakdown && k > 0 && k < n) {
+         printf("AFN factors broke down: rank-%d Nystrom on the same order (afn_setup.m:93-98)\n", k);
+         nystrom(2);
+      }
+   }
+   if (!F->afn && !F->nys && !F->nysg) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondAFNSetup failed\n");
+      return -1;
+   }
+   return 0;
+}
+
+void* Nfft4GPAmdPrecondAFNCreate(int max_k, int perm_opt, int schur_opt, int schur_lfil, int nsamples)
+{
+   if ((perm_opt != 0 && perm_opt != 1) || (schur_opt != 0 && schur_opt != 3)) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondAFNCreate: perm_opt 0 (random) or 1 (FPS), schur_opt 0 or 3\n");
+      return nullptr;
+   }
+   AfnFlow* F = new AfnFlow();
+   F->max_k = max_k;
+   F->perm_opt = perm_opt;
+   F->schur_opt = schur_opt;
+   F->schur_lfil = schur_lfil;
+   F->nsamples = nsamples;
+   return F;
+}
+
+int Nfft4GPAmdPrecondAFNSetupWithKernel(double* data, int n, int ldim, int d, func_kernel fkernel,
+                                        void* fkernel_params, int require_grad, void* pre)
+{
+   RandScope rand_scope;  // libc rand() as the reference draws it (internal.h)
+   if (!need_device("Nfft4GPAmdPrecondAFNSetupWithKernel")) return -1;
+   AfnFlow* F = (AfnFlow*)pre;
+   if (!F || !data || !fkernel_params || n <= 0 || ldim < n) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondAFNSetupWithKernel needs a handle, data (ldim >= n) and kernel "
+                      "parameters\n");
+      return -1;
+   }
+   const int kernel = fkernel == &Nfft4GPNFFTAdditiveKernelMatern12Kernel ? 1 : 0;
+   return flow_setup(F, data, n, ldim, d, kernel, fkernel_params, require_grad ? 1 : 0);
+}
+
 void* Nfft4GPAmdPrecondAFNSetup(const double* data, int n, int ldim, int d, int max_k, int perm_opt, int schur_opt,
-                                int schur_lfil, int nsamples, int kernel, void* fkernel_params)
+                                int schur_lfil, int nsamples, int kernel, void* fkernel_params, int require_grad)
 {
    RandScope rand_scope;  // libc rand() as the reference draws it (internal.h)
    if (!need_device("Nfft4GPAmdPrecondAFNSetup")) return nullptr;
-   if (!data || !fkernel_params || n <= 0 || ldim < n || (perm_opt != 0 && perm_opt != 1)) {
-      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondAFNSetup needs data (ldim >= n), kernel parameters and "
-                      "perm_opt 0 (random) or 1 (FPS)\n");
+   if (!data || !fkernel_params || n <= 0 || ldim < n) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondAFNSetup needs data (ldim >= n) and kernel parameters\n");
       return nullptr;
    }
-   std::vector<int> perm(n);
-   const int max_kk = std::min(max_k, n);
-   const int k = Nfft4GPAmdAfnRankEstimate(data, n, ldim, d, max_k, perm_opt, nsamples, kernel, fkernel_params,
-                                           perm.data());
-   if (k < 0) return nullptr;
-   AfnFlow* F = new AfnFlow();
-   F->n = n;
-   F->k = k;
-   if (max_kk > 0 && k > 0 && k < n && k < max_kk) {
-      printf("The estimated rank %d is below max_k = %d: rank-%d Nystrom (afn.c:294-304)\n", k, max_kk, k);
-      F->kind = 1;
-      F->nys = flow_nystrom(data, n, ldim, d, kernel, fkernel_params, perm.data(), k);
-   } else {
-      bool breakdown = false;
-      F->afn = afn_setup_impl(data, n, ldim, d, k, 2, perm.data(), schur_opt, schur_lfil, kernel, fkernel_params,
-                              &breakdown);
-      if (!F->afn && breakdown && k > 0 && k < n) {
-         printf("AFN factors broke down: rank-%d Nystrom on the same order (afn_setup.m:93-98)\n", k);
-         F->kind = 2;
-         F->nys = flow_nystrom(data, n, ldim, d, kernel, fkernel_params, perm.data(), k);
-      }
-   }
-   if (!F->afn && !F->nys) {
-      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondAFNSetup failed\n");
+   AfnFlow* F = (AfnFlow*)Nfft4GPAmdPrecondAFNCreate(max_k, perm_opt, schur_opt, schur_lfil, nsamples);
+   if (!F) return nullptr;
+   if (flow_setup(F, const_cast<double*>(data), n, ldim, d, kernel, fkernel_params, require_grad ? 1 : 0)) {
       delete F;
       return nullptr;
    }
@@ -946,7 +1161,74 @@ int Nfft4GPAmdPrecondAFNSolve(void* pre, int n, double* x, double* rhs)
 {
    AfnFlow* F = (AfnFlow*)pre;
    if (!F || n != F->n) return -1;
-   return F->afn ? Nfft4GPAmdAfnSolve(F->afn, n, x, rhs) : Nfft4GPAmdNysSolve(F->nys, n, x, rhs);
+   if (F->afn) return Nfft4GPAmdAfnSolve(F->afn, n, x, rhs);
+   if (F->nysg) return Nfft4GPAmdPrecondNysSolve(F->nysg, n, x, rhs);
+   return Nfft4GPAmdNysSolve(F->nys, n, x, rhs);
+}
+
+int Nfft4GPAmdPrecondAFNDvp(void* pre, int n, int* mask, double* x, double** yp)
+{
+   AfnFlow* F = (AfnFlow*)pre;
+   if (!F || n != F->n || !yp) return -1;
+   if (F->nysg) return Nfft4GPAmdPrecondNysDvp(F->nysg, n, mask, x, yp);
+   if (!F->grad) {
+      printf("Setup AFN without gradient, dvp not supported.\n");
+      return -1;
+   }
+   // host or device x; *yp allocated on x's side when NULL (the reference's convention)
+   hipStream_t s = current_stream();
+   const bool xd = is_device_ptr(x);
+   if (!*yp) {
+      if (xd)
+         NFFT4GP_HIP_CHECK(hipMalloc((void**)yp, sizeof(double) * 3 * (size_t)n));
+      else
+         *yp = (double*)calloc(3 * (size_t)n, sizeof(double));
+   }
+   const bool yd = is_device_ptr(*yp);
+   double *dx = x, *dy = *yp;
+   if (!xd) {
+      NFFT4GP_HIP_CHECK(hipMalloc((void**)&dx, sizeof(double) * n));
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(dx, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
+   }
+   if (!yd) NFFT4GP_HIP_CHECK(hipMalloc((void**)&dy, sizeof(double) * 3 * (size_t)n));
+   int rc = afn_grad_dvp(F->grad, mask, dx, dy, s);
+   if (!yd) {
+      if (!rc && hipMemcpyAsync(*yp, dy, sizeof(double) * 3 * (size_t)n, hipMemcpyDeviceToHost, s) != hipSuccess) rc = -1;
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(dy);
+   }
+   if (!xd) {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(dx);
+   }
+   return rc;
+}
+
+int Nfft4GPAmdPrecondAFNTrace(void* pre, double** tracesp)
+{
+   AfnFlow* F = (AfnFlow*)pre;
+   if (!F || !tracesp) return -1;
+   if (F->nysg) return Nfft4GPAmdPrecondNysTrace(F->nysg, tracesp);
+   if (!F->grad) {
+      printf("Setup AFN without gradient, trace not supported.\n");
+      return -1;
+   }
+   if (!*tracesp) *tracesp = (double*)calloc(3, sizeof(double));
+   for (int g = 0; g < 3; g++) (*tracesp)[g] = F->grad->trace[g];
+   return 0;
+}
+
+double Nfft4GPAmdPrecondAFNLogdet(void* pre)
+{
+   AfnFlow* F = (AfnFlow*)pre;
+   if (!F) return NAN;
+   if (F->nysg) return Nfft4GPAmdPrecondNysLogdet(F->nysg);
+   return F->grad ? F->grad->logdet : NAN;
+}
+
+void Nfft4GPAmdPrecondAFNReset(void* pre)
+{
+   if (pre) ((AfnFlow*)pre)->reset();
 }
 
 int Nfft4GPAmdPrecondAFNInfo(void* pre, int* kind, int* k, void** afn, void** nys)
@@ -956,7 +1238,7 @@ int Nfft4GPAmdPrecondAFNInfo(void* pre, int* kind, int* k, void** afn, void** ny
    if (kind) *kind = F->kind;
    if (k) *k = F->k;
    if (afn) *afn = F->afn;
-   if (nys) *nys = F->nys;
+   if (nys) *nys = F->nys ? (void*)F->nys : F->nysg;
    return 0;
 }
 
@@ -964,8 +1246,7 @@ void Nfft4GPAmdPrecondAFNFree(void* pre)
 {
    AfnFlow* F = (AfnFlow*)pre;
    if (!F) return;
-   if (F->afn) Nfft4GPAmdAfnFree(F->afn);
-   if (F->nys) Nfft4GPAmdNysFree(F->nys);
+   F->reset();
    delete F;
 }
 

@@ -419,11 +419,16 @@ __device__ void wave_trsv(double (*A)[kFsaiMaxK + 1], int k, double* b, int tran
 // W (kw x n column-major, optional): the Schur-complement kernel K(x_r, x_c) - W(:, r)' W(:, c) of the AFN
 // setup (Nfft4GPKernelSchurCombineKernel, kernels.c:3599-3760, with W = L11^{-1} K12), staged through LDS
 // kSchurChunk rows of W at a time so each row reads its lfil columns of W once.
+// Gradients of the Schur kernel (MATLAB schurCombinedKernelMat.m): with B_g = L11^{-1} dK12_g (GB, g = f, l;
+// zero for mu) and C_g = (L11^{-1} dK11_g L11^{-T}) W (GC, g = f, l, mu), both kw x n per g,
+//   dS_g(r, c) = dK_g(r, c) - W_r' B_g,c - B_g,r' W_c + W_r' C_g,c,
+// so (dS_g a)_r = (dK_g a)_r - W_r' (B_g a - C_g a) - B_g,r' (W a) with the kw-vectors W a = sum_c W_c a_c etc.
 constexpr int kSchurChunk = 32;
 __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, long long ldim,
                                                   const int* __restrict__ ia, const int* __restrict__ ja,
                                                   KernelParams P, const double* __restrict__ W, int kw, int grad,
-                                                  int nnz, double* __restrict__ aa, double* __restrict__ da)
+                                                  int nnz, double* __restrict__ aa, double* __restrict__ da,
+                                                  const double* __restrict__ GB, const double* __restrict__ GC)
 {
    __shared__ double A[kFsaiMaxK][kFsaiMaxK + 1];
    __shared__ double Ws[kFsaiMaxK][kSchurChunk + 1];
@@ -499,6 +504,37 @@ __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, 
          u[lane] = -acc;
       }
       __syncthreads();
+      if (W && GC) {
+         // the Schur terms, kSchurChunk entries of the kw-vectors at a time: Ws holds (W a, B_g a - C_g a)
+         const double* Bg = g < 2 ? GB + (size_t)g * kw * ((size_t)gridDim.x) : nullptr;
+         const double* Cg = GC + (size_t)g * kw * ((size_t)gridDim.x);
+         double acc = 0.0;
+         for (int t0 = 0; t0 < kw; t0 += kSchurChunk) {
+            const int tc = min(kSchurChunk, kw - t0);
+            if (lane < tc) {
+               double wa = 0.0, ba = 0.0, ca = 0.0;
+               for (int c = 0; c < k; c++) {
+                  const size_t o = (size_t)idx[c] * kw + t0 + lane;
+                  wa = fma(W[o], a[c], wa);
+                  if (Bg) ba = fma(Bg[o], a[c], ba);
+                  ca = fma(Cg[o], a[c], ca);
+               }
+               Ws[0][lane] = wa;
+               Ws[1][lane] = ba - ca;
+            }
+            __syncthreads();
+            if (lane < k) {
+               const size_t o = (size_t)idx[lane] * kw + t0;
+               for (int tt = 0; tt < tc; tt++) {
+                  acc = fma(W[o + tt], Ws[1][tt], acc);
+                  if (Bg) acc = fma(Bg[o + tt], Ws[0][tt], acc);
+               }
+            }
+            __syncthreads();
+         }
+         if (lane < k) u[lane] += acc;  // u = -(dS_g a)
+         __syncthreads();
+      }
       wave_trsv(A, k, u, 0);
       wave_trsv(A, k, u, 1);
       const double t = -0.5 * u[k - 1] * dd_scale;
@@ -792,15 +828,15 @@ int kernel_spec_of(void* fkernel_params, func_kernel fkernel, int kernel, int n,
 // gradients), copied to host CSR.  dW (kw x n, optional): the Schur-complement kernel of the AFN setup.
 int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const KernelSpec& Ks, const double* dW, int kw,
                     int require_grad, std::vector<int>& hia, std::vector<int>& hja, std::vector<double>& haa,
-                    std::vector<double>& hda, hipStream_t s)
+                    std::vector<double>& hda, hipStream_t s, const double* dGB, const double* dGC)
 {
    if (n <= 0 || ldim < n || d <= 0 || d > kMaxDims || lfil < 1 || lfil > kFsaiMaxK || (dW && kw <= 0)) {
       fprintf(stderr, "nfft4gp_amd: FSAI setup needs 1 <= lfil <= %d and at most %d features\n", kFsaiMaxK,
               kMaxDims);
       return -1;
    }
-   if (require_grad && dW) {
-      fprintf(stderr, "nfft4gp_amd: FSAI setup: gradients of the Schur-complement kernel are not supported\n");
+   if (require_grad && dW && !dGC) {
+      fprintf(stderr, "nfft4gp_amd: FSAI setup: gradients of the Schur-complement kernel need its B / C panels\n");
       return -1;
    }
    // pattern row pointers (kernels.c:133-168): dense rows below lfil, lfil entries after
@@ -855,7 +891,7 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const Ke
    const double* Xk = Ks.Xk ? Ks.Xk : dX;
    const long long ldk = Ks.Xk ? Ks.ldk : ldim;
    hipLaunchKernelGGL(k_fsai_rows, dim3(n), dim3(64), 0, s, Xk, ldk, dia, dja, P, dW, kw, require_grad ? 1 : 0, nnz,
-                      daa, dda);
+                      daa, dda, dGB, dGC);
    haa.assign((size_t)nnz, 0.0);
    hda.assign(require_grad ? 3 * (size_t)nnz : 0, 0.0);
    if (hipGetLastError() != hipSuccess ||
@@ -866,6 +902,50 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const Ke
        hipStreamSynchronize(s) != hipSuccess)
       return cleanup(-1);
    return cleanup(0);
+}
+
+// ---- the Schur FSAI's operators for the AFN gradients (afn_grad.hip) ----------------------------------
+void* fsai_grad_create(int n, const int* ia, const int* ja, const double* aa, const double* da)
+{
+   PrecondFsaiAmd* F = new PrecondFsaiAmd();
+   if (fsai_load(F, n, ia, ja, aa, da)) {
+      F->release();
+      delete F;
+      return nullptr;
+   }
+   return F;
+}
+
+void fsai_grad_free(void* F)
+{
+   if (!F) return;
+   ((PrecondFsaiAmd*)F)->release();
+   delete (PrecondFsaiAmd*)F;
+}
+
+// y = G x (op 0), G^T x (1), G^{-1} x (2), G^{-T} x (3), dG_g x (4), dG_g^T x (5); x != y
+int fsai_grad_op(void* vF, int op, int g, const double* x, double* y, hipStream_t s)
+{
+   PrecondFsaiAmd* F = (PrecondFsaiAmd*)vF;
+   const int n = F->n;
+   switch (op) {
+      case 0: csr_mv(F->ia, F->ja, F->aa, x, y, n, 0, s); break;
+      case 1: csr_mv(F->tia, F->tja, F->taa, x, y, n, 0, s); break;
+      case 2: return inv_l(F, y, x, s);
+      case 3: return inv_lt(F, y, x, s);
+      case 4: csr_mv(F->ia, F->ja, F->da + (size_t)g * F->nnz, x, y, n, 0, s); break;
+      case 5: csr_mv(F->tia, F->tja, F->tda + (size_t)g * F->nnz, x, y, n, 0, s); break;
+      default: return -1;
+   }
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+// sum_i dG_g(i,i) / G(i,i) (g = 0..2), or sum_i log(1 / G(i,i)) (g < 0)
+double fsai_grad_diag(void* vF, int g, hipStream_t s)
+{
+   PrecondFsaiAmd* F = (PrecondFsaiAmd*)vF;
+   return diag_sum(F, g < 0 ? nullptr : F->da + (size_t)g * F->nnz, s);
 }
 
 }  // namespace nfft4gp_amd

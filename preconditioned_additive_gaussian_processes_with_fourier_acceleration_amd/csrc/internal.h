@@ -268,12 +268,44 @@ struct KernelSpec {
 };
 // FSAI of a kernel matrix (fsai_setup.hip): KNN pattern on dX (n x d, ld ldim), values of the kernel
 // K; host CSR out; dW (kw x n): the Schur-complement kernel K - W'W
+// With require_grad and dW: dGB (2 kw x n panels L11^{-1} dK12_g) and dGC (3 panels GdK11G_g W) give the
+// Schur kernel's gradients (fsai_setup.hip k_fsai_rows)
 int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const KernelSpec& K, const double* dW, int kw,
                     int require_grad, std::vector<int>& ia, std::vector<int>& ja, std::vector<double>& aa,
-                    std::vector<double>& da, hipStream_t s);
+                    std::vector<double>& da, hipStream_t s, const double* dGB = nullptr,
+                    const double* dGC = nullptr);
+// the Schur FSAI with gradients as operators (fsai_setup.hip): create from host CSR (+ 3 nnz gradients)
+void* fsai_grad_create(int n, const int* ia, const int* ja, const double* aa, const double* da);
+void fsai_grad_free(void* F);
+// y = G x, G^T x, G^{-1} x, G^{-T} x, dG_g x, dG_g^T x for op = 0..5
+int fsai_grad_op(void* F, int op, int g, const double* x, double* y, hipStream_t s);
+// sum_i dG_g(i,i) / G(i,i) (g >= 0) or sum_i log(1 / G(i,i)) (g < 0)
+double fsai_grad_diag(void* F, int g, hipStream_t s);
+// lower Cholesky factor of A (k x k, in place, upper triangle zeroed; rocSOLVER potrf, host fallback);
+// returns 0, the failing column + 1, or -1 (nystrom.hip)
+int chol_factor_dev(double* A, int k, int* d_info, hipStream_t s);
 // the KernelSpec of fkernel_params (this library's additive handle: its window buffer, uploaded to
 // *owned; else the plain kernel); 1 additive, 0 plain, -1 error (fsai_setup.hip)
 int kernel_spec_of(void* fkernel_params, func_kernel fkernel, int kernel, int n, KernelSpec& K, double** owned);
+// The AFN's gradient pieces (MATLAB afn_setup.m with require_grad; afn_dvp.m, afn_trace.m, afn_logdet.m):
+// the factors of the apply plus dL_g = L Phi(L^{-1} dK11_g L^{-T}), dK12_g and the Schur FSAI's dG_g
+struct AfnGrad {
+   int n = 0, k = 0, n2 = 0;
+   int* perm = nullptr;                 // device, n
+   double *L = nullptr, *Linv = nullptr, *LinvT = nullptr;  // k x k
+   double* dL = nullptr;                // 3 k x k (g = f, l, mu)
+   const double* K12 = nullptr;         // k x n2, the apply object's
+   double* dK12 = nullptr;              // 2 k x n2 (g = f, l; dK12_mu = 0)
+   void* S = nullptr;                   // fsai_grad_create handle of the Schur FSAI (n2)
+   void* afn = nullptr;                 // the apply (M^{-1}), not owned
+   double trace[3] = {0.0, 0.0, 0.0};   // tr(M^{-1} dM/dtheta_g)
+   double logdet = 0.0;                 // log det M
+   double* work = nullptr;              // 6 n + 8 k scratch
+};
+void afn_grad_free(AfnGrad* G);
+// y_g = M^{-1} (dM/dtheta_g) x for the gradients in mask (all three when NULL), device vectors, y: 3n
+int afn_grad_dvp(AfnGrad* G, const int* mask, const double* x, double* y, hipStream_t s);
+
 // AFN apply object from device factors (fsai_afn.hip); owns all of them and S
 // S == NULL with n - k > 0: the Schur complement solve is schur_scale * I (schur_opt 0)
 void* afn_create_device(int n, int k, int* d_perm, double* d_Linv, double* d_LinvT, double* d_K12, void* S,

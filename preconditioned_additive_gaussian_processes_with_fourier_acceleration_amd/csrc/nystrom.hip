@@ -676,6 +676,36 @@ int chol_inverse_dev(double* A, int k, double shift, double* G, double* Gt, int*
    return 0;
 }
 
+__global__ void k_zero_upper(double* A, int k)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
+   if (i < j && i < k) A[i + (size_t)j * k] = 0.0;
+}
+
+int chol_factor_dev(double* A, int k, int* d_info, hipStream_t s)
+{
+   RocSolver& R = rocsolver();
+   if (R.ok) {
+      int info = 0;
+      R.set_stream(R.h, s);
+      if (R.potrf(R.h, rocblas_fill_lower, k, A, k, d_info) != rocblas_status_success ||
+          hipMemcpyAsync(&info, d_info, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+         return -1;
+      if (info) return info;
+      hipLaunchKernelGGL(k_zero_upper, dim3((k + 255) / 256, k), dim3(256), 0, s, A, k);
+      return hipGetLastError() == hipSuccess ? 0 : -1;
+   }
+   std::vector<double> h((size_t)k * k);
+   if (hipMemcpyAsync(h.data(), A, sizeof(double) * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess)
+      return -1;
+   if (int info = chol_lower(h, k)) return info;
+   for (int j = 0; j < k; j++)
+      for (int i = 0; i < j; i++) h[i + (size_t)j * k] = 0.0;
+   return hipMemcpy(A, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+
 // C (M x N, ld ldc) = A^T B with A K x M (lda) and B K x N (ldb), K split over row chunks (fixed-order sum,
 // deterministic); sym: C symmetric with A == B (only tiles on and below the diagonal are computed)
 int gram_tn(int M, int N, int K, const double* A, long long lda, const double* B, long long ldb, double* C, int sym,

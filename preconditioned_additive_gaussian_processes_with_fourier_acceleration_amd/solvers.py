@@ -228,13 +228,16 @@ class PrecondAFN(_Apply):
     ``kind`` is "afn", "nystrom" or "ran"; ``k`` the rank.  The kernel is the plain Gaussian / Matern-1/2 of X
     (f, l, mu), or with ``op`` (an NFFTAdditiveKernel after its setup) the dense additive kernel of op's
     windows and hyperparameters.  perm_opt: "random" (0) or "fps" (1); schur: "fsai" (schur_opt 3) or
-    "noise" (0).  max_k <= 0: the predefined rank -max_k in natural order, no estimation (afn.c:245-256)."""
+    "noise" (0).  max_k <= 0: the predefined rank -max_k in natural order, no estimation (afn.c:245-256).
+    require_grad: keep the gradient pieces (MATLAB afn_dvp.m / afn_trace.m / afn_logdet.m; the Nystrom
+    branches need ``op``) for ``dvp`` (M^{-1} dM/dtheta_g x, g = f, l, mu), ``trace`` and ``logdet``."""
 
     _solve, _free = "Nfft4GPAmdPrecondAFNSolve", "Nfft4GPAmdPrecondAFNFree"
     KINDS = ("afn", "nystrom", "ran")
 
     def __init__(self, X, max_k: int, f: float = 1.0, l: float = 1.0, mu: float = 0.01, perm_opt: str = "random",
-                 schur: str = "fsai", schur_lfil: int = 20, nsamples: int = 500, kernel: int = 0, op=None):
+                 schur: str = "fsai", schur_lfil: int = 20, nsamples: int = 500, kernel: int = 0, op=None,
+                 require_grad: bool = False):
         L = _lib.lib()
         X = np.asfortranarray(np.asarray(X, dtype=np.float64))
         n, d = X.shape
@@ -242,7 +245,7 @@ class PrecondAFN(_Apply):
         self.n = n
         self.h = L.Nfft4GPAmdPrecondAFNSetup(X.ctypes.data, n, n, d, int(max_k), {"random": 0, "fps": 1}[perm_opt],
                                              {"fsai": 3, "noise": 0}[schur], int(schur_lfil), int(nsamples),
-                                             int(kernel), params)
+                                             int(kernel), params, int(bool(require_grad)))
         if op is None:
             L.Nfft4GPKernelParamFree(params)
         if not self.h:
@@ -250,6 +253,28 @@ class PrecondAFN(_Apply):
         kind, k = C.c_int(), C.c_int()
         L.Nfft4GPAmdPrecondAFNInfo(self.h, C.byref(kind), C.byref(k), None, None)
         self.kind, self.k = self.KINDS[kind.value], k.value
+
+    def dvp(self, x, mask=None):
+        """[M^{-1} dM/df x, M^{-1} dM/dl x, M^{-1} dM/dmu x] (3 n, host numpy or a GPU tensor like x)."""
+        _check_len("x", x, self.n)
+        y = x.new_zeros(3 * self.n) if hasattr(x, "data_ptr") else np.zeros(3 * self.n)
+        yp = C.c_void_p(_ptr(y)[0])
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.int32)
+        if _lib.lib().Nfft4GPAmdPrecondAFNDvp(self.h, self.n, None if m is None else m.ctypes.data, _ptr(x)[0],
+                                              C.byref(yp)):
+            raise RuntimeError("Nfft4GPAmdPrecondAFNDvp failed (setup without require_grad?)")
+        return y
+
+    def trace(self):
+        """tr(M^{-1} dM/dtheta_g), g = f, l, mu."""
+        t = np.zeros(3)
+        tp = C.c_void_p(t.ctypes.data)
+        if _lib.lib().Nfft4GPAmdPrecondAFNTrace(self.h, C.byref(tp)):
+            raise RuntimeError("Nfft4GPAmdPrecondAFNTrace failed (setup without require_grad?)")
+        return t
+
+    def logdet(self):
+        return float(_lib.lib().Nfft4GPAmdPrecondAFNLogdet(self.h))
 
     def free(self):
         if getattr(self, "h", None):
