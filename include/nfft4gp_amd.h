@@ -161,6 +161,11 @@ int Nfft4GPAdditiveNFFTMatSymv(void *data, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_
 /* replaces SRC/external/nfft_interface.c:819-840 */
 int Nfft4GPAdditiveNFFTGradMatSymv(void *data, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE beta,
                                    NFFT4GP_DOUBLE *y);
+/* Nfft4GPAdditiveNFFTMatSymv on nrhs column-major device vectors X (ldx) -> Y (ldy): two vectors per pass
+ * over the HBM layout (the layout read and the per-point decode shared).  The reference calls its matvec
+ * once per vector (lanczos.c:490-574 probe by probe). */
+int Nfft4GPAmdAdditiveMatSymvMulti(void *data, int n, int nrhs, NFFT4GP_DOUBLE alpha, const NFFT4GP_DOUBLE *X,
+                                   long long ldx, NFFT4GP_DOUBLE beta, NFFT4GP_DOUBLE *Y, long long ldy);
 /* replaces SRC/external/nfft_interface.c:842-856 */
 void Nfft4GPAdditiveNFFTKernelFree(void *str);
 /* replaces SRC/external/nfft_interface.c:873-1068: posterior mean at the n_predict points of data_all

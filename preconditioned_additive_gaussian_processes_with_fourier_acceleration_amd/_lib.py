@@ -149,6 +149,8 @@ _SIGS = {
     "Nfft4GPAmdShardGridSize": (C.c_longlong, [vp]),
     "Nfft4GPAmdPrecondAFNSetup": (vp, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.c_int, vp, C.c_int]),
+    "Nfft4GPAmdAdditiveMatSymvMulti": (C.c_int, [vp, C.c_int, C.c_int, C.c_double, vp, C.c_longlong, C.c_double, vp,
+                                               C.c_longlong]),
     "Nfft4GPAmdPrecondAFNCreate": (vp, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
     "Nfft4GPAmdPrecondAFNSetupWithKernel": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp]),
     "Nfft4GPAmdPrecondAFNDvp": (C.c_int, [vp, C.c_int, vp, vp, vp]),

@@ -175,6 +175,8 @@ struct AdditivePlan {
    double* d_C = nullptr;     // [kTaps][kNC]
    double* d_dot_part = nullptr;         // [nblocks] fused matvec-dot partials
    unsigned int* d_dot_ticket = nullptr; // arrival counters (reduce.hpp)
+   double* d_part2 = nullptr; // two-vector matvec: the second vector's partial grids
+   double* d_H2 = nullptr;    // [2][nw][64][kNC]
    double* d_xs = nullptr;    // staging (host pointer calls)
    double* d_ys = nullptr;    // staging 3n
    MdPlan md;  // used instead of the 1-D layout when any window has more than one feature
@@ -197,6 +199,11 @@ int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_g
 // d_dot != nullptr (non-grad): also writes (y, x) to *d_dot (device), one grid-wide reduction in the launch
 int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, double beta, double* d_y,
                   hipStream_t stream, double* d_dot = nullptr);
+// y_v = beta y_v + alpha A x_v, v = 0, 1, in one pass over the layout (1-D layouts; -1 for multi-feature windows)
+int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double* x1, double beta, double* y0,
+                   double* y1, hipStream_t stream);
+// y_v = beta y_v + alpha A x_v for nv device vectors of this library's additive handle (pairs per layout pass)
+int additive_matvec_multi(void* str, int nv, double alpha, const double* const* X, double beta, double* const* Y);
 // y = A x (alpha = 1, beta = 0) and *d_dot = (y, x) on device pointers: the matvec + dot of a CG step in
 // the matvec's own three launches (used by Nfft4GPSolverPcg when its operator is this library's)
 int additive_matvec_dot(void* str, const double* d_x, double* d_y, double* d_dot);

@@ -129,8 +129,11 @@ void free_layout(AdditivePlan& P)
    dfree(P.dl.tile_off);
    P.dl = DevLayout();
    dfree(P.d_part);
+   dfree(P.d_part2);
+   dfree(P.d_H2);
    dfree(P.d_dot_part);
    dfree(P.d_dot_ticket);
+   P.d_part2 = P.d_H2 = nullptr;
    P.d_part = nullptr;
    P.d_dot_part = nullptr;
    P.d_dot_ticket = nullptr;
@@ -544,6 +547,24 @@ int additive_matvec_dot(void* str, const double* d_x, double* d_y, double* d_dot
 }  // namespace nfft4gp_amd
 
 namespace nfft4gp_amd {
+// y_v = beta y_v + alpha A x_v for nv device vectors: two per pass over the layout (launch_matvec2), an odd
+// last vector (and multi-feature-window handles) through the single-vector matvec
+int additive_matvec_multi(void* str, int nv, double alpha, const double* const* X, double beta, double* const* Y)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready) return -1;
+   AdditivePlan& P = E->P;
+   if (P.row_begin != 0 || P.row_end != P.n_global) return -1;
+   hipStream_t s = current_stream();
+   int v = 0;
+   if (!P.md.on && !P.timing)
+      for (; v + 1 < nv; v += 2)
+         if (launch_matvec2(P, alpha, X[v], X[v + 1], beta, Y[v], Y[v + 1], s)) return -1;
+   for (; v < nv; v++)
+      if (plan_apply_dev(E, 0, alpha, X[v], beta, Y[v])) return -1;
+   return 0;
+}
+
 // rows of an additive handle: local (this shard) and global; -1 when str is not an additive handle
 int additive_rows(void* str, int* n_local, int* n_global, int* row_begin)
 {
@@ -664,6 +685,28 @@ int Nfft4GPAdditiveNFFTMatSymv(void* data, int n, double alpha, double* x, doubl
    PlanExt* E = additive_plan(data);
    if (!E) return -1;
    return plan_apply(E, n, 0, alpha, x, beta, y);
+}
+
+int Nfft4GPAmdAdditiveMatSymvMulti(void* data, int n, int nrhs, double alpha, const double* X, long long ldx,
+                                   double beta, double* Y, long long ldy)
+{
+   PlanExt* E = additive_plan(data);
+   if (!E || !E->P.points_ready || n != E->P.n || nrhs < 0 || ldx < n || ldy < n) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAdditiveMatSymvMulti: handle not set up, or n / ld mismatch\n");
+      return -1;
+   }
+   if (nrhs == 0) return 0;
+   if (!is_device_ptr(X) || !is_device_ptr(Y)) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAdditiveMatSymvMulti takes device arrays\n");
+      return -1;
+   }
+   std::vector<const double*> xs(nrhs);
+   std::vector<double*> ys(nrhs);
+   for (int v = 0; v < nrhs; v++) {
+      xs[v] = X + (size_t)v * ldx;
+      ys[v] = Y + (size_t)v * ldy;
+   }
+   return additive_matvec_multi(data, nrhs, alpha, xs.data(), beta, ys.data());
 }
 
 int Nfft4GPAdditiveNFFTGradMatSymv(void* data, int n, double alpha, double* x, double beta, double* y)

@@ -278,16 +278,19 @@ __device__ void grid_tail(int comp, const double* __restrict__ s_g, const double
 }
 
 // part: [nw][nparts][64] (from_sum = 0) or the summed grids [nw][64] (from_sum = 1)
+// blockIdx.y: right-hand side (two-vector matvec): part and H advance by part_rs / h_rs elements per vector
 __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict__ part, int nparts,
                                                       const double* __restrict__ w, const double* __restrict__ wd,
                                                       double* __restrict__ H, double* __restrict__ Hd, int grad,
-                                                      int from_sum)
+                                                      int from_sum, long long part_rs = 0, long long h_rs = 0)
 {
    __shared__ double s_red[kGridThreads];
    __shared__ double s_g[kNos];
    __shared__ double s_h[kNos];
    __shared__ double s_w[kNos];
    const int comp = blockIdx.x;
+   part += blockIdx.y * part_rs;
+   H += blockIdx.y * h_rs;
    const int tid = threadIdx.x;
    if (from_sum) {
       if (tid < kNos) s_g[tid] = part[(size_t)comp * kNos + tid];
@@ -492,6 +495,84 @@ __global__ __launch_bounds__(THREADS) void k_interp(
 }
 
 // ------------------------------------------------------------------------------------------------
+// two right-hand sides per pass over the layout (SLQ probes in lockstep, krylov.hip)
+// ------------------------------------------------------------------------------------------------
+// The interpolation reads the layout (5 B per (point, window)) once for both vectors and shares the
+// per-point decode; each vector keeps its own H and LDS y-slice (planar, so the layout's bank balancing
+// for ds_add_f64 holds).  The spread stays one launch per vector: a two-vector spread needs 97 KB of LDS
+// per workgroup (two alpha slices and a 21-double moment row), one workgroup per CU, and measured 135 us
+// against 2 x 55 us at config C; the two-vector interpolation measured 51 us against
+// 2 x 34 us.
+
+// y_v = beta y_v + alpha f^2 (sum_windows interp_v + mu x_v), v = 0, 1; H of vector v at H + v * h_rs
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_interp2(const uint16_t* __restrict__ meta,
+                                                     const uint32_t* __restrict__ lo,
+                                                     const uint32_t* __restrict__ qarr,
+                                                     const int* __restrict__ tile_off, const double* __restrict__ H,
+                                                     size_t h_rs, const double* __restrict__ x0,
+                                                     const double* __restrict__ x1, double* __restrict__ y0,
+                                                     double* __restrict__ y1, int n, int B, int ngroups, double alpha,
+                                                     double beta, double f, double mu)
+{
+   extern __shared__ __attribute__((aligned(16))) double smem[];
+   const int Bp = B + kPad;
+   double* s_y0 = smem;
+   double* s_y1 = smem + Bp;
+   const int b = blockIdx.x;
+   const int tid = threadIdx.x;
+   const int base = b * B;
+   const int nloc = min(B, n - base);
+   const int lane = tid & 63;
+   const int wave = tid >> 6;
+   constexpr int nwaves = THREADS / 64;
+   const int t0 = tile_off[b * ngroups];
+   const int t1 = tile_off[(b + 1) * ngroups];
+   TileRegs cur;
+   int t = t0 + wave;
+   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
+   for (int i = tid; i < Bp; i += THREADS) s_y0[i] = s_y1[i] = 0.0;
+   __syncthreads();
+   const double* H1 = H + h_rs;
+   for (; t < t1; t += nwaves) {
+      const size_t hoff = (size_t)cur.mt * kNC;
+      double h0[kNC], h1[kNC];
+#pragma unroll
+      for (int d = 0; d < kNC; d += 2) {
+         const double2 v0 = *reinterpret_cast<const double2*>(H + hoff + d);
+         const double2 v1 = *reinterpret_cast<const double2*>(H1 + hoff + d);
+         h0[d] = v0.x;
+         h0[d + 1] = v0.y;
+         h1[d] = v1.x;
+         h1[d + 1] = v1.y;
+      }
+#pragma unroll
+      for (int r = 0; r < kR; r++) {
+         const uint32_t loc = slot_loc(cur, r);
+         const double u = q_to_u(cur.qq[r]);
+         double v0 = h0[kNC - 1], v1 = h1[kNC - 1];
+#pragma unroll
+         for (int d = kNC - 2; d >= 0; d--) {
+            v0 = fma(v0, u, h0[d]);
+            v1 = fma(v1, u, h1[d]);
+         }
+         atomicAdd(s_y0 + loc, v0);
+         atomicAdd(s_y1 + loc, v1);
+      }
+      if (t + nwaves < t1) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
+   }
+   __syncthreads();
+   const double ff = f * f;
+   for (int j = tid; j < nloc; j += THREADS) {
+      const size_t gj = (size_t)base + j;
+      const double v0 = ff * (s_y0[j] + mu * x0[gj]);
+      const double v1 = ff * (s_y1[j] + mu * x1[gj]);
+      y0[gj] = (beta == 0.0) ? alpha * v0 : fma(beta, y0[gj], alpha * v0);
+      y1[gj] = (beta == 0.0) ? alpha * v1 : fma(beta, y1[gj], alpha * v1);
+   }
+}
+
+// ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
 // plain launch, or (timing mode) a launch whose start / stop events are the dispatch's own timestamps
@@ -562,21 +643,23 @@ constexpr int kNumInterpVariants = sizeof(kInterpVariants) / sizeof(kInterpVaria
 
 static void raise_lds_limit_once()
 {
-   static bool raised = false;
-   if (raised) return;
-   for (int i = 0; i < kNumSpreadVariants; i++)
-      (void)hipFuncSetAttribute((const void*)kSpreadVariants[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-   for (int i = 0; i < kNumInterpVariants; i++) {
-      (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-      (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn_grad,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn_dot,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-   }
-   (void)hipGetLastError();
-   raised = true;
+   // a function-local static initialiser runs once (thread-safe)
+   static const bool raised = []() {
+      for (int i = 0; i < kNumSpreadVariants; i++)
+         (void)hipFuncSetAttribute((const void*)kSpreadVariants[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024);
+      for (int i = 0; i < kNumInterpVariants; i++) {
+         (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024);
+         (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn_grad,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+         (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn_dot,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      }
+      (void)hipGetLastError();
+      return true;
+   }();
+   (void)raised;
 }
 
 int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream)
@@ -596,7 +679,7 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream)
 {
    launch_ev(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, P.kev ? P.kev + 2 : nullptr, d_part, nparts,
-             (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 0);
+             (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 0, 0ll, 0ll);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -604,7 +687,7 @@ int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int gra
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream)
 {
    launch_ev(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, P.kev ? P.kev + 2 : nullptr, d_gridsum, 1,
-             (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 1);
+             (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 1, 0ll, 0ll);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -632,6 +715,38 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
    launch_ev(fn, dim3(P.nblocks), dim3(V.threads), interp_lds_bytes(P, grad), stream, P.kev ? P.kev + 4 : nullptr,
              P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H, (const double*)P.d_Hd, d_x, d_y, P.n,
              P.B, P.ngroups, alpha, beta, P.f, P.mu * P.diag, P.diag, P.d_dot_part, P.d_dot_ticket, d_dot);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+// y_v = beta y_v + alpha A x_v for two vectors: one spread per vector, both grids in one launch, one
+// two-vector interpolation (1-D layouts, whole-row handles)
+constexpr int kInterp2Threads = 1024;
+
+int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double* x1, double beta, double* y0,
+                   double* y1, hipStream_t stream)
+{
+   if (P.n == 0) return 0;
+   if (P.md.on) return -1;
+   static bool attr = false;
+   if (!attr) {
+      (void)hipFuncSetAttribute((const void*)k_interp2<kInterp2Threads>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      (void)hipGetLastError();
+      attr = true;
+   }
+   const size_t part_rs = (size_t)std::max(1, P.nblocks) * P.nw * kNos;
+   const size_t h_rs = (size_t)P.nw * kNos * kNC;
+   if (!P.d_part2) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part2, sizeof(double) * part_rs));
+   if (!P.d_H2) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_H2, sizeof(double) * 2 * h_rs));
+   if (launch_spread(P, x0, P.d_part, stream) || launch_spread(P, x1, P.d_part2, stream)) return -1;
+   hipLaunchKernelGGL(k_grid, dim3(P.nw, 2), dim3(kGridThreads), 0, stream, (const double*)P.d_part, P.nblocks,
+                      (const double*)P.d_w, (const double*)P.d_wd, P.d_H2, P.d_Hd, 0, 0,
+                      (long long)(P.d_part2 - P.d_part), (long long)h_rs);
+   const size_t lds_i = sizeof(double) * 2 * ((size_t)P.B + kPad);
+   hipLaunchKernelGGL(k_interp2<kInterp2Threads>, dim3(P.nblocks), dim3(kInterp2Threads), lds_i, stream, P.dl.meta,
+                      P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H2, h_rs, x0, x1, y0, y1, P.n, P.B,
+                      P.ngroups, alpha, beta, P.f, P.mu * P.diag);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
