@@ -581,12 +581,21 @@ int lanczos_dev(Callbacks& cb, double* x, const double* rhs, int wsize, int maxi
       fprintf(stderr, "nfft4gp_amd: Nfft4GPSolverLanczos: maxits %d above %d\n", maxits, KScratch::kScal - 2);
       return -1;
    }
+   // without a preconditioner v = z at every step (the same copy, scaled by the same factor), so the
+   // basis is stored once and is its own update basis
+   const bool alias = !cb.prec;
    double *V = nullptr, *Z = nullptr;
-   if (dmalloc(&V, n * (size_t)(maxits + 1)) || dmalloc(&Z, n * (size_t)(maxits + 1))) return -1;
+   if (dmalloc(&V, n * (size_t)(maxits + 1))) return -1;
+   if (alias) {
+      Z = V;
+   } else if (dmalloc(&Z, n * (size_t)(maxits + 1))) {
+      (void)hipFree(V);
+      return -1;
+   }
    auto cleanup = [&]() {
       (void)hipStreamSynchronize(c.s);
       (void)hipFree(V);
-      (void)hipFree(Z);
+      if (!alias) (void)hipFree(Z);
    };
    std::vector<double> TLD(maxits + 1, 0.0), TLE(maxits + 1, 0.0), y(maxits + 1, 0.0);
    double* TD = *TDp ? *TDp : (double*)calloc((size_t)maxits + 1, sizeof(double));
@@ -603,7 +612,7 @@ int lanczos_dev(Callbacks& cb, double* x, const double* rhs, int wsize, int maxi
          cleanup();
          return -1;
       }
-   } else {
+   } else if (!alias) {
       c.copy(v, z);
    }
    double normr = c.norm(z);
@@ -630,7 +639,7 @@ int lanczos_dev(Callbacks& cb, double* x, const double* rhs, int wsize, int maxi
       printf("Step    Residual norm  Relative res.  Convergence Rate\n");
       printf("%5d   %8e   %8e   N/A\n", 0, normr, rel[0]);
    }
-   c.scale(v, z, 1.0 / beta);
+   c.scale(v, alias ? nullptr : z, 1.0 / beta);
    auto step = [&](bool first_loop) -> int {
       iter++;
       z = Z + (size_t)iter * n;
@@ -643,8 +652,6 @@ int lanczos_dev(Callbacks& cb, double* x, const double* rhs, int wsize, int maxi
       if (t < EPS) return 1;
       if (cb.prec) {
          if (cb.solve(v, z)) return -1;
-      } else {
-         c.copy(v, z);
       }
       double* o = g_k.scal + KScratch::kScal - 2;
       hipLaunchKernelGGL(k_dot2, dim3(kgrid(n)), dim3(kKThreads), 0, c.s, v, z, n, g_k.part, g_k.ticket, g_k.part2,
@@ -653,7 +660,7 @@ int lanczos_dev(Callbacks& cb, double* x, const double* rhs, int wsize, int maxi
       if (c.read(o, 2, vz)) return -1;
       dotvz = std::sqrt(vz[0]);
       if (dotvz < EPS) return 1;
-      c.scale(v, z, 1.0 / dotvz);
+      c.scale(v, alias ? nullptr : z, 1.0 / dotvz);
       if (first_loop) {
          const double normz = std::sqrt(vz[1]) / dotvz;
          if (iter != 1) {
@@ -715,12 +722,10 @@ int lanczos_dev(Callbacks& cb, double* x, const double* rhs, int wsize, int maxi
          if (t < EPS) break;
          if (cb.prec) {
             if (cb.solve(v, z)) return -1;
-         } else {
-            c.copy(v, z);
          }
          dotvz = std::sqrt(c.dot(v, z));
          if (dotvz < EPS) break;
-         c.scale(v, z, 1.0 / dotvz);
+         c.scale(v, alias ? nullptr : z, 1.0 / dotvz);
       }
       while (iter < wsize) {
          const int r = step(false);
