@@ -547,6 +547,9 @@ NFFT4GP_DOUBLE Nfft4GPAmdHostPrepare(const NFFT4GP_DOUBLE *col, int n, unsigned 
  * in the cell in bits 0-25, local index bits 6-11 in bits 26-31), nblocks*ngroups+1 (tile_off) */
 int Nfft4GPAmdHostLayout(const unsigned int *qc, int n, int nw, int B, int CG, long long *counts,
                          unsigned short *meta, unsigned int *lo, unsigned int *q, int *tile_off);
+/* The same layout built on the GPU (layout_gpu.hip, what the operator's setup uses): identical arrays. */
+int Nfft4GPAmdDeviceLayout(const unsigned int *qc, int n, int nw, int B, int CG, long long *counts,
+                           unsigned short *meta, unsigned int *lo, unsigned int *q, int *tile_off);
 /* the Nystrom setup's host k x k steps: symmetric eigensolve (dsyev 'V' semantics: ascending w,
  * eigenvectors as the columns of V, column-major) and L^{-1} of the lower Cholesky factor of A + shift I
  * (returns 0, or the failing column + 1 if A + shift I is not positive definite) */

@@ -180,6 +180,8 @@ _SIGS = {
     "Nfft4GPAmdHostCholInverse": (C.c_int, [vp, C.c_int, C.c_double, vp]),
     "Nfft4GPAmdHostLayout": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_longlong), vp, vp,
                                        vp, vp]),
+    "Nfft4GPAmdDeviceLayout": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_longlong), vp, vp,
+                                         vp, vp]),
 }
 
 _lib = None

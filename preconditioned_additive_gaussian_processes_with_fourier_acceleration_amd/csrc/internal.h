@@ -109,6 +109,10 @@ struct Layout {
 };
 // build from per-component quantized coordinates qc[c*n + j]
 void build_layout(const uint32_t* qc, int n, int nw, int B, int CG, Layout& L);
+struct AdditivePlan;
+// the same layout from device-resident coordinates into P.dl / P.ngroups / P.nblocks (layout_gpu.hip); -1
+// when a (block, group) exceeds the emit kernel's LDS
+int build_layout_dev(const uint32_t* d_qc, int n, int nw, int B, int CG, AdditivePlan& P, hipStream_t s);
 
 // ---- device plan --------------------------------------------------------------------------------
 struct DevLayout {

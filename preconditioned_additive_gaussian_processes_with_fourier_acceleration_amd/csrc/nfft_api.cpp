@@ -258,22 +258,35 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
          return -1;
       }
    const auto t1 = std::chrono::steady_clock::now();
-   Layout L;
-   build_layout(qc.data(), P.n, P.nw, P.B, P.CG, L);
-   const auto t2 = std::chrono::steady_clock::now();
-   P.ngroups = L.ngroups;
-   P.nblocks = L.nblocks;
+   // the layout is built on the GPU from the quantised coordinates (layout_gpu.hip); layout.cpp builds the
+   // same arrays on the host when a (block, group) would not fit the GPU builder's LDS (B > 4064 or CG > 3
+   // would need it; neither is a setting the plan uses)
    free_layout(P);
-   if (upload(&P.dl.meta, L.meta) || upload(&P.dl.lo, L.lo) || upload(&P.dl.q, L.q) ||
-       upload(&P.dl.tile_off, L.tile_off))
-      return -1;
-   P.dl.ntiles = L.ntiles;
-   P.dl.bytes = L.meta.size() * 2 + L.lo.size() * 4 + L.q.size() * 4 + L.tile_off.size() * 4;
+   hipStream_t s = current_stream();
+   uint32_t* d_qc = nullptr;
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&d_qc, sizeof(uint32_t) * std::max<size_t>(1, qc.size())));
+   NFFT4GP_HIP_CHECK(hipMemcpyAsync(d_qc, qc.data(), sizeof(uint32_t) * qc.size(), hipMemcpyHostToDevice, s));
+   const auto t2 = std::chrono::steady_clock::now();
+   const int rc_dev = build_layout_dev(d_qc, P.n, P.nw, P.B, P.CG, P, s);
+   (void)hipStreamSynchronize(s);
+   (void)hipFree(d_qc);
+   if (rc_dev) {
+      Layout L;
+      build_layout(qc.data(), P.n, P.nw, P.B, P.CG, L);
+      P.ngroups = L.ngroups;
+      P.nblocks = L.nblocks;
+      free_layout(P);
+      if (upload(&P.dl.meta, L.meta) || upload(&P.dl.lo, L.lo) || upload(&P.dl.q, L.q) ||
+          upload(&P.dl.tile_off, L.tile_off))
+         return -1;
+      P.dl.ntiles = L.ntiles;
+      P.dl.bytes = L.meta.size() * 2 + L.lo.size() * 4 + L.q.size() * 4 + L.tile_off.size() * 4;
+   }
    if (getenv("NFFT4GP_AMD_VERBOSE")) {
       const auto t3 = std::chrono::steady_clock::now();
       auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-      fprintf(stderr, "nfft4gp_amd: layout setup: centre/scale/quantize %.1f ms, layout %.1f ms, upload %.1f ms\n",
-              ms(t0, t1), ms(t1, t2), ms(t2, t3));
+      fprintf(stderr, "nfft4gp_amd: layout setup: centre/scale/quantize %.1f ms, coordinate upload %.1f ms, "
+                      "layout (%s) %.1f ms\n", ms(t0, t1), ms(t1, t2), rc_dev ? "host" : "GPU", ms(t2, t3));
    }
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part, sizeof(double) * (size_t)std::max(1, P.nblocks) * P.nw * kNos));
    dfree(P.d_dot_part);
