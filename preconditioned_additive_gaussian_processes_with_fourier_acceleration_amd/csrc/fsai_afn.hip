@@ -16,6 +16,7 @@
 #include <cstring>
 #include <vector>
 
+#include "csr.hpp"
 #include "internal.h"
 
 namespace nfft4gp_amd {
@@ -45,15 +46,13 @@ struct AfnDev {
 };
 
 // y[i] = sum_j a[j] x[ja[j]] in the row's stored order, unfused (matops.c:239-248)
+// y = A x, a thread per CSR row (csr.hpp: column order, bitwise the reference's)
 __global__ void k_csr_rows(const int* __restrict__ ia, const int* __restrict__ ja, const double* __restrict__ a,
                            const double* __restrict__ x, double* __restrict__ y, int n)
 {
-#pragma clang fp contract(off)  // the reference's host build multiplies and adds separately (no FMA)
    const int i = blockIdx.x * blockDim.x + threadIdx.x;
    if (i >= n) return;
-   double r = 0.0;
-   for (int j = ia[i]; j < ia[i + 1]; j++) r += a[j] * x[ja[j]];
-   y[i] = r;
+   y[i] = csr_row_dot(ja, a, x, ia[i], ia[i + 1], 0.0);
 }
 
 __global__ void k_scale_into(const double* __restrict__ src, int n, double a, double* __restrict__ dst)

@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "callbacks.hpp"
+#include "csr.hpp"
 #include "internal.h"
 #include "kernel_eval.hpp"
 
@@ -592,12 +593,9 @@ __global__ __launch_bounds__(kTrsvThreads) void k_trsv_upper(const int* __restri
 __global__ void k_csr_mv(const int* __restrict__ ia, const int* __restrict__ ja, const double* __restrict__ a,
                          const double* __restrict__ x, double* __restrict__ y, int n, int beta_one)
 {
-#pragma clang fp contract(off)
    const int i = blockIdx.x * blockDim.x + threadIdx.x;
    if (i >= n) return;
-   double r = beta_one ? y[i] : 0.0;
-   for (int j = ia[i]; j < ia[i + 1]; j++) r += a[j] * x[ja[j]];
-   y[i] = r;
+   y[i] = csr_row_dot(ja, a, x, ia[i], ia[i + 1], beta_one ? y[i] : 0.0);
 }
 
 // out[blk] = sum over the block's rows of num[diag_i] / den[diag_i] (or log(1 / den[diag_i]) when num is
