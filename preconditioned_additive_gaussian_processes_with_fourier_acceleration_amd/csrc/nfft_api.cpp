@@ -471,9 +471,22 @@ int setup_common(void* str, int kernel, int n, int ldim, double** Kp, double** d
    return 0;
 }
 
+// Points per block B: the interpolation runs one workgroup per block and the spread one per (block, window
+// group), so a handle with few points (a small problem, or a row shard of several GPUs) needs smaller
+// blocks to fill the 256 CUs, at the price of more partial grids and per-workgroup folds.  Measured per
+// matvec (32 windows; n: B = 4064 / 2032 / 1016): 1e6: 85.6 / 104.4 / 146.9 us; 5e5: 59.7 / 57.0 / -;
+// 2.5e5: 45.6 / 39.7 / 41.5; 1.25e5: 39.1 / 29.9 / 29.1; 1e5 (8 windows): 21.6 / 17.1 / 16.9.
+int default_block(int n)
+{
+   if (n >= 200 * kMaxBlock) return kMaxBlock;
+   if (n >= 40 * 2032) return 2032;
+   return 1016;
+}
+
 // tuning overrides (layout only; results are independent of them up to rounding)
 void env_layout(AdditivePlan& P)
 {
+   P.B = default_block(P.n);
    if (const char* e = getenv("NFFT4GP_AMD_BLOCK")) {
       const int v = atoi(e);
       if (v >= 256) P.B = std::min(v, kMaxBlock) & ~1;  // even: the LDS slice is staged in 16-byte pairs
