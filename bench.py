@@ -368,10 +368,17 @@ def main():
         running GP loop sits in the busy state.  The timed region is unchanged: exactly K steps."""
         torch.cuda.synchronize()
         t_end = time.perf_counter() + seconds
-        while time.perf_counter() < t_end:
+        while True:
             for _ in range(50):
                 step()
             torch.cuda.synchronize()
+            more = time.perf_counter() < t_end
+            if world > 1:  # rank 0's clock decides, so every rank runs the same steps (collectives match)
+                flag = torch.tensor([1.0 if more else 0.0], dtype=torch.float64, device="cuda")
+                dist.broadcast(flag, src=0)
+                more = bool(flag.item())
+            if not more:
+                break
 
     # The PCG legs (the metric's second half) run first, after a pre-warm (the GPU's idle clock state costs
     # the first few hundred matvecs ~15 %, tools/warm_probe.py: 100 us per matvec cold, 85 us warm, back to
