@@ -327,17 +327,38 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
    if (grad) grid_tail(comp, s_g, wd, Hd, s_w, s_h);
 }
 
-// gsum[comp][cell] = sum_b part[comp][b][cell]   (row-sharded path: before the all-reduce)
-__global__ __launch_bounds__(256) void k_reduce_parts(const double* __restrict__ part, int nparts, int nw,
-                                                     double* __restrict__ gsum)
+// gsum[comp][cell] = sum_b part[comp][b][cell]   (row-sharded path: before the all-reduce).  One
+// workgroup per window, k_grid's 16 strands per cell with 16 loads in flight each (a thread per cell
+// summing the partials one after another took 16 us at an 8-GPU shard of config C)
+__global__ __launch_bounds__(kGridThreads) void k_reduce_parts(const double* __restrict__ part, int nparts, int nw,
+                                                              double* __restrict__ gsum)
 {
-   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-   if (idx >= nw * kNos) return;
-   const int comp = idx / kNos, cell = idx % kNos;
+   __shared__ double s_red[kGridThreads];
+   const int comp = blockIdx.x;
+   const int tid = threadIdx.x;
+   constexpr int kPer = 16;
+   const int cell = tid & 63;
+   const int strand = tid >> 6;
+   constexpr int nstr = kGridThreads / 64;
    const double* src = part + (size_t)comp * nparts * kNos + cell;
-   double s = 0.0;
-   for (int p = 0; p < nparts; p++) s += src[(size_t)p * kNos];
-   gsum[idx] = s;
+   double acc = 0.0;
+   for (int p0 = strand; p0 < nparts; p0 += kPer * nstr) {
+      double v[kPer];
+#pragma unroll
+      for (int k = 0; k < kPer; k++) {
+         const int p = p0 + k * nstr;
+         v[k] = p < nparts ? src[(size_t)p * kNos] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < kPer; k++) acc += v[k];
+   }
+   s_red[tid] = acc;
+   __syncthreads();
+   if (tid < kNos) {
+      double v = 0.0;
+      for (int k = 0; k < nstr; k++) v += s_red[k * 64 + tid];
+      gsum[(size_t)comp * kNos + tid] = v;
+   }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -694,8 +715,7 @@ int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int gra
 
 int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream)
 {
-   const int total = P.nw * kNos;
-   hipLaunchKernelGGL(k_reduce_parts, dim3((total + 255) / 256), dim3(256), 0, stream, d_part, P.nblocks, P.nw,
+   hipLaunchKernelGGL(k_reduce_parts, dim3(P.nw), dim3(kGridThreads), 0, stream, d_part, P.nblocks, P.nw,
                       d_gridsum);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;

@@ -1,0 +1,62 @@
+"""Row-shard matvec time on one GPU (the per-rank work of an N-GPU run without the all-reduce):
+Nfft4GPAmdShardSpread -> Nfft4GPAmdShardFinish for rows [0, n_global / N) of config C.
+
+    python tools/shard_probe.py [--ranks 8]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--d", type=int, default=32)
+    ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=2000)
+    args = ap.parse_args()
+    import torch
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    torch.cuda.set_device(0)
+    L = amd.lib()
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    L.Nfft4GPAmdSetStream(s.cuda_stream)
+    n, d = args.n, args.d
+    X = np.asfortranarray(np.random.default_rng(906).random((n, d)))
+    win = np.arange(d, dtype=np.int32)
+    re = n // args.ranks
+    op = amd.NFFTAdditiveKernel(X, win, d, 1, shard=(0, re))
+    assert op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) == 0
+    h = op.h
+    g = L.Nfft4GPAmdShardGridSize(h)
+    grid = torch.zeros(g, dtype=torch.float64, device="cuda")
+    x = torch.tensor(np.random.default_rng(1).random(re) - 0.5, device="cuda")
+    y = torch.zeros(re, dtype=torch.float64, device="cuda")
+
+    def step():
+        assert L.Nfft4GPAmdShardSpread(h, x.data_ptr(), grid.data_ptr()) == 0
+        assert L.Nfft4GPAmdShardFinish(h, grid.data_ptr(), 0, 1.0, x.data_ptr(), 0.0, y.data_ptr()) == 0
+
+    t_end = time.perf_counter() + 0.5
+    while time.perf_counter() < t_end:
+        for _ in range(50):
+            step()
+        torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.reps):
+        step()
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / args.reps * 1e6
+    print(json.dumps({"rows": re, "us_per_shard_matvec": us, "y_norm": float(y.norm())}))
+
+
+if __name__ == "__main__":
+    main()
