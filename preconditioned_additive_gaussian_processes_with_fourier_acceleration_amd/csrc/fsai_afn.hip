@@ -45,14 +45,15 @@ struct AfnDev {
    int nblk = 0, cols = 1;  // A12 y2: workgroups, columns per workgroup
 };
 
-// y[i] = sum_j a[j] x[ja[j]] in the row's stored order, unfused (matops.c:239-248)
-// y = A x, a thread per CSR row (csr.hpp: column order, bitwise the reference's)
-__global__ void k_csr_rows(const int* __restrict__ ia, const int* __restrict__ ja, const double* __restrict__ a,
-                           const double* __restrict__ x, double* __restrict__ y, int n)
+// y = A x, a thread per CSR row summing in the row's stored order, unfused (matops.c:239-248); the
+// entries and their gathers go through LDS a workgroup-wide chunk at a time (csr.hpp)
+constexpr int kCsrT = 256;
+constexpr int kCsrCH = 2048;
+__global__ __launch_bounds__(kCsrT) void k_csr_staged(const int* __restrict__ ia, const int* __restrict__ ja,
+                                                      const double* __restrict__ a, const double* __restrict__ x,
+                                                      double* __restrict__ y, int n)
 {
-   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-   if (i >= n) return;
-   y[i] = csr_row_dot(ja, a, x, ia[i], ia[i + 1], 0.0);
+   csr_rows_staged<kCsrT, kCsrCH>(ia, ja, a, x, y, n, false);
 }
 
 __global__ void k_scale_into(const double* __restrict__ src, int n, double a, double* __restrict__ dst)
@@ -88,18 +89,47 @@ __global__ __launch_bounds__(256) void k_trmv(const double* __restrict__ M, int 
    if (lane == 0) out[i] = r;
 }
 
-// rp2[j] -= sum_i K12[i + j*k] y[i]  (one wave per column)
+// rp2[j] -= sum_i K12[i + j*k] y[i]: one wave per kA12tCols consecutive columns (their loads in flight
+// together), y staged in LDS (k <= kA12tLdsMax; beyond, read from HBM through the caches).  Each column's
+// sum is the same lane-strided sum and shuffle tree as with a wave per column.
+constexpr int kA12tCols = 4;
+constexpr int kA12tLdsMax = 8192;
+template <bool LDS>
 __global__ __launch_bounds__(256) void k_a12t(const double* __restrict__ K12, int k, int n2, const double* __restrict__ y,
                                               double* __restrict__ rp2)
 {
+   extern __shared__ double s_y_[];
+   const double* s_y = LDS ? s_y_ : y;
+   if (LDS) {
+      for (int i = threadIdx.x; i < k; i += 256) s_y_[i] = y[i];
+      __syncthreads();
+   }
    const int lane = threadIdx.x & 63;
-   const long long j = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-   if (j >= n2) return;
-   const double* col = K12 + j * k;
-   double r = 0.0;
-   for (int i = lane; i < k; i += 64) r = fma(col[i], y[i], r);
-   for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off, 64);
-   if (lane == 0) rp2[j] -= r;
+   const long long j0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * kA12tCols;
+   if (j0 >= n2) return;
+   const int nc = (int)std::min<long long>(kA12tCols, n2 - j0);
+   const double* col = K12 + j0 * k;
+   double r[kA12tCols];
+#pragma unroll
+   for (int c = 0; c < kA12tCols; c++) r[c] = 0.0;
+   if (nc == kA12tCols) {
+      for (int i = lane; i < k; i += 64) {
+         const double yi = s_y[i];
+#pragma unroll
+         for (int c = 0; c < kA12tCols; c++) r[c] = fma(col[(size_t)c * k + i], yi, r[c]);
+      }
+   } else {
+      for (int i = lane; i < k; i += 64) {
+         const double yi = s_y[i];
+         for (int c = 0; c < nc; c++) r[c] = fma(col[(size_t)c * k + i], yi, r[c]);
+      }
+   }
+#pragma unroll
+   for (int c = 0; c < kA12tCols; c++) {
+      double v = r[c];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+      if (lane == 0 && c < nc) rp2[j0 + c] -= v;
+   }
 }
 
 // part[blk][i] = sum_{j in blk} K12[i + j*k] y2[j]; `cols` columns per workgroup, sized at create so
@@ -121,19 +151,27 @@ __global__ __launch_bounds__(256) void k_a12_part(const double* __restrict__ K12
    }
 }
 
-// rp[i] -= sum_blk part[blk][i]: 4 waves split the workgroups, fixed order
-__global__ __launch_bounds__(256) void k_a12_reduce(const double* __restrict__ part, int nblk, int k,
-                                                    double* __restrict__ rp)
+// rp[i] -= sum_blk part[blk][i]: a workgroup per 16 outputs, 64 strands over the partials (strand s takes
+// blk = s mod 64, four rotating accumulators, all its loads independent), strands added in order in LDS.
+// Fixed order, so the same bits every run.
+__global__ __launch_bounds__(1024) void k_a12_reduce(const double* __restrict__ part, int nblk, int k,
+                                                     double* __restrict__ rp)
 {
-   __shared__ double s[4][64];
-   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-   const int i = blockIdx.x * 64 + lane;
-   double r = 0.0;
-   if (i < k)
-      for (int b = w; b < nblk; b += 4) r += part[(size_t)b * k + i];
-   s[w][lane] = r;
+   __shared__ double s[64][17];
+   const int c = threadIdx.x & 15, strand = threadIdx.x >> 4;
+   const int i = blockIdx.x * 16 + c;
+   double z[4] = {0.0, 0.0, 0.0, 0.0};
+   if (i < k) {
+      int u = 0;
+      for (int b = strand; b < nblk; b += 64, u = (u + 1) & 3) z[u] += part[(size_t)b * k + i];
+   }
+   s[strand][c] = (z[0] + z[1]) + (z[2] + z[3]);
    __syncthreads();
-   if (w == 0 && i < k) rp[i] -= (s[0][lane] + s[1][lane]) + (s[2][lane] + s[3][lane]);
+   if (threadIdx.x < 16 && i < k) {
+      double t = 0.0;
+      for (int q = 0; q < 64; q++) t += s[q][threadIdx.x];
+      rp[i] -= t;
+   }
 }
 
 void a12_shape(int n2, int& cols, int& nblk)
@@ -188,9 +226,9 @@ FsaiDev* fsai_create(int n, const int* ia, const int* ja, const double* aa)
 
 int fsai_apply_dev(FsaiDev* F, double* dx, const double* drhs, hipStream_t s)
 {
-   const int g = (F->n + 255) / 256;
-   hipLaunchKernelGGL(k_csr_rows, dim3(g), dim3(256), 0, s, F->ia, F->ja, F->aa, drhs, F->work, F->n);
-   hipLaunchKernelGGL(k_csr_rows, dim3(g), dim3(256), 0, s, F->tia, F->tja, F->taa, F->work, dx, F->n);
+   const int g = (F->n + kCsrT - 1) / kCsrT;
+   hipLaunchKernelGGL(k_csr_staged, dim3(g), dim3(kCsrT), 0, s, F->ia, F->ja, F->aa, drhs, F->work, F->n);
+   hipLaunchKernelGGL(k_csr_staged, dim3(g), dim3(kCsrT), 0, s, F->tia, F->tja, F->taa, F->work, dx, F->n);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -244,7 +282,11 @@ int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->LinvT, k, A->rp, A->t);
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y);
    // rp2 -= A12^T y
-   hipLaunchKernelGGL(k_a12t, dim3((n2 + 3) / 4), dim3(256), 0, s, A->K12, k, n2, A->y, rp2);
+   const dim3 ga((n2 + 4 * kA12tCols - 1) / (4 * kA12tCols));
+   if (k <= kA12tLdsMax)
+      hipLaunchKernelGGL(k_a12t<true>, ga, dim3(256), sizeof(double) * k, s, A->K12, k, n2, A->y, rp2);
+   else
+      hipLaunchKernelGGL(k_a12t<false>, ga, dim3(256), 0, s, A->K12, k, n2, A->y, rp2);
    // y2 = FSAI(rp2), or rp2 / noise (schur_opt 0)
    if (A->S) {
       if (fsai_apply_dev(A->S, y2, rp2, s)) return -1;
@@ -253,7 +295,7 @@ int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
    }
    // rp -= A12 y2
    hipLaunchKernelGGL(k_a12_part, dim3(A->nblk), dim3(256), 0, s, A->K12, k, n2, A->cols, y2, A->part);
-   hipLaunchKernelGGL(k_a12_reduce, dim3((k + 63) / 64), dim3(256), 0, s, A->part, A->nblk, k, A->rp);
+   hipLaunchKernelGGL(k_a12_reduce, dim3((k + 15) / 16), dim3(1024), 0, s, A->part, A->nblk, k, A->rp);
    // y = A11 \ rp
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->LinvT, k, A->rp, A->t);
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y);

@@ -590,12 +590,11 @@ __global__ __launch_bounds__(kTrsvThreads) void k_trsv_upper(const int* __restri
 
 // y = beta y + A x for a CSR A (matops.c:139-272 with alpha = 1, beta in {0, 1}): the row accumulates
 // into y[i] itself (matops.c:247), in row order, unfused
-__global__ void k_csr_mv(const int* __restrict__ ia, const int* __restrict__ ja, const double* __restrict__ a,
-                         const double* __restrict__ x, double* __restrict__ y, int n, int beta_one)
+__global__ __launch_bounds__(256) void k_csr_mv(const int* __restrict__ ia, const int* __restrict__ ja,
+                                                const double* __restrict__ a, const double* __restrict__ x,
+                                                double* __restrict__ y, int n, int beta_one)
 {
-   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-   if (i >= n) return;
-   y[i] = csr_row_dot(ja, a, x, ia[i], ia[i + 1], beta_one ? y[i] : 0.0);
+   csr_rows_staged<256, 2048>(ia, ja, a, x, y, n, beta_one != 0);  // csr.hpp: the entries through LDS
 }
 
 // out[blk] = sum over the block's rows of num[diag_i] / den[diag_i] (or log(1 / den[diag_i]) when num is
