@@ -20,3 +20,11 @@ L.Nfft4GPAmdPrecondFsaiSetLfil(h, lfil)
 t0 = time.perf_counter()
 assert L.Nfft4GPAmdPrecondFsaiSetupWithKernel(X.ctypes.data, n, n, d, None, P, grad, h) == 0
 print(f"FSAI setup n={n} d={d} lfil={lfil} grad={grad}: {time.perf_counter() - t0:.3f} s")
+if len(sys.argv) > 5:  # dump the pattern and values (A/B of kernel variants: they must agree bitwise)
+    nnz = L.Nfft4GPAmdPrecondFsaiCsr(h, None, None, None, None)
+    ia = np.zeros(n + 1, np.int32)
+    ja = np.zeros(nnz, np.int32)
+    aa = np.zeros(nnz)
+    da = np.zeros(3 * nnz)
+    assert L.Nfft4GPAmdPrecondFsaiCsr(h, ia.ctypes.data, ja.ctypes.data, aa.ctypes.data, da.ctypes.data) == nnz
+    np.savez(sys.argv[5], ia=ia, ja=ja, aa=aa)
