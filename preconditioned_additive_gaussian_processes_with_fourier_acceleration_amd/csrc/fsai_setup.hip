@@ -407,7 +407,8 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn_bounded(const double* __res
 }
 
 // In place on the wave's LDS vector b: b = L^{-1} b (trans = 0) or L^{-T} b (trans = 1), L lower in A.
-__device__ void wave_trsv(double (*A)[kFsaiMaxK + 1], int k, double* b, int trans)
+template <int LD>
+__device__ void wave_trsv(double (*A)[LD], int k, double* b, int trans)
 {
    const int lane = threadIdx.x;
    if (!trans) {
@@ -436,17 +437,20 @@ __device__ void wave_trsv(double (*A)[kFsaiMaxK + 1], int k, double* b, int tran
 // zero for mu) and C_g = (L11^{-1} dK11_g L11^{-T}) W (GC, g = f, l, mu), both kw x n per g,
 //   dS_g(r, c) = dK_g(r, c) - W_r' B_g,c - B_g,r' W_c + W_r' C_g,c,
 // so (dS_g a)_r = (dK_g a)_r - W_r' (B_g a - C_g a) - B_g,r' (W a) with the kw-vectors W a = sum_c W_c a_c etc.
+// KM: the LDS arrays' row capacity (>= lfil); KM = 32 takes 17 KB per workgroup (9 per CU) where 64
+// takes 51 KB (3 per CU).
 constexpr int kSchurChunk = 32;
+template <int KM>
 __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, long long ldim,
                                                   const int* __restrict__ ia, const int* __restrict__ ja,
                                                   KernelParams P, const double* __restrict__ W, int kw, int grad,
                                                   int nnz, double* __restrict__ aa, double* __restrict__ da,
                                                   const double* __restrict__ GB, const double* __restrict__ GC)
 {
-   __shared__ double A[kFsaiMaxK][kFsaiMaxK + 1];
-   __shared__ double Ws[kFsaiMaxK][kSchurChunk + 1];
-   __shared__ double a[kFsaiMaxK], u[kFsaiMaxK];
-   __shared__ int idx[kFsaiMaxK];
+   __shared__ double A[KM][KM + 1];
+   __shared__ double Ws[KM][kSchurChunk + 1];
+   __shared__ double a[KM], u[KM];
+   __shared__ int idx[KM];
    const int i = blockIdx.x;
    const int lane = threadIdx.x;
    const int j1 = ia[i];
@@ -900,7 +904,8 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const Ke
    const KernelParams P = kernel_params_of(Ks, d);
    const double* Xk = Ks.Xk ? Ks.Xk : dX;
    const long long ldk = Ks.Xk ? Ks.ldk : ldim;
-   hipLaunchKernelGGL(k_fsai_rows, dim3(n), dim3(64), 0, s, Xk, ldk, dia, dja, P, dW, kw, require_grad ? 1 : 0, nnz,
+   auto rows_kernel = lfil <= 32 ? k_fsai_rows<32> : k_fsai_rows<kFsaiMaxK>;
+   hipLaunchKernelGGL(rows_kernel, dim3(n), dim3(64), 0, s, Xk, ldk, dia, dja, P, dW, kw, require_grad ? 1 : 0, nnz,
                       daa, dda, dGB, dGC);
    haa.assign((size_t)nnz, 0.0);
    hda.assign(require_grad ? 3 * (size_t)nnz : 0, 0.0);
