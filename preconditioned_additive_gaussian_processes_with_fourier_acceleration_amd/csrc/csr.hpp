@@ -15,23 +15,23 @@ namespace nfft4gp_amd {
 // contraction off, r += a * x is round(r + round(a * x)), so the sums are bitwise csr_row_dot's, and the
 // gathers of a long row (a column of a KNN pattern's transpose can hold thousands) are spread over the
 // whole workgroup instead of running 8 at a time on one thread.  beta_one: rows start from y.
+// Rows [r0, r1) (r1 - r0 <= T): a workgroup's rows, a fixed T of them or a span sized by entry count.
 template <int T, int CH>
 __device__ __forceinline__ void csr_rows_staged(const int* __restrict__ ia, const int* __restrict__ ja,
                                                 const double* __restrict__ a, const double* __restrict__ x,
-                                                double* __restrict__ y, int n, bool beta_one)
+                                                double* __restrict__ y, int r0, int r1, bool beta_one)
 {
 #pragma clang fp contract(off)
    static_assert(CH % T == 0, "chunk must be a multiple of the workgroup");
    constexpr int K = CH / T;
    __shared__ double s_p[CH];
    const int tid = threadIdx.x;
-   const int r0 = blockIdx.x * T;
    const int row = r0 + tid;
    const int e0 = ia[r0];
-   const int e1 = ia[min(r0 + T, n)];
+   const int e1 = ia[r1];
    int j0 = 0, j1 = 0;
    double r = 0.0;
-   if (row < n) {
+   if (row < r1) {
       j0 = ia[row];
       j1 = ia[row + 1];
       if (beta_one) r = y[row];
@@ -55,7 +55,7 @@ __device__ __forceinline__ void csr_rows_staged(const int* __restrict__ ia, cons
       const int je = min(j1, c + m) - c;
       for (int j = max(j0, c) - c; j < je; j++) r += s_p[j];
    }
-   if (row < n) y[row] = r;
+   if (row < r1) y[row] = r;
 }
 
 }  // namespace nfft4gp_amd

@@ -30,6 +30,8 @@ struct FsaiDev {
    int *tia = nullptr, *tja = nullptr;  // L^T
    double* taa = nullptr;
    double* work = nullptr;
+   int *part = nullptr, *tpart = nullptr;  // row spans of the workgroups of L and L^T (csr_partition)
+   int nparts = 0, ntparts = 0;
 };
 
 struct AfnDev {
@@ -49,11 +51,28 @@ struct AfnDev {
 // entries and their gathers go through LDS a workgroup-wide chunk at a time (csr.hpp)
 constexpr int kCsrT = 256;
 constexpr int kCsrCH = 2048;
+constexpr int kCsrBudget = 3 * kCsrCH;  // entries per workgroup span (a longer row gets a span of its own)
 __global__ __launch_bounds__(kCsrT) void k_csr_staged(const int* __restrict__ ia, const int* __restrict__ ja,
                                                       const double* __restrict__ a, const double* __restrict__ x,
-                                                      double* __restrict__ y, int n)
+                                                      double* __restrict__ y, const int* __restrict__ part)
 {
-   csr_rows_staged<kCsrT, kCsrCH>(ia, ja, a, x, y, n, false);
+   csr_rows_staged<kCsrT, kCsrCH>(ia, ja, a, x, y, part[blockIdx.x], part[blockIdx.x + 1], false);
+}
+
+// workgroup row spans: at most kCsrT rows and kCsrBudget entries each, so that the workgroups holding a
+// transposed KNN pattern's long rows do not run many more chunks than the rest
+std::vector<int> csr_partition(int n, const int* ia)
+{
+   std::vector<int> p{0};
+   int r0 = 0;
+   for (int i = 0; i < n; i++) {
+      if (i > r0 && (i - r0 == kCsrT || ia[i + 1] - ia[r0] > kCsrBudget)) {
+         p.push_back(i);
+         r0 = i;
+      }
+   }
+   p.push_back(n);
+   return p;
 }
 
 __global__ void k_scale_into(const double* __restrict__ src, int n, double a, double* __restrict__ dst)
@@ -192,7 +211,7 @@ void fsai_free(FsaiDev* F)
 {
    if (!F) return;
    for (void* p : {(void*)F->ia, (void*)F->ja, (void*)F->aa, (void*)F->tia, (void*)F->tja, (void*)F->taa,
-                   (void*)F->work})
+                   (void*)F->work, (void*)F->part, (void*)F->tpart})
       (void)hipFree(p);
    delete F;
 }
@@ -221,14 +240,22 @@ FsaiDev* fsai_create(int n, const int* ia, const int* ja, const double* aa)
       fsai_free(F);
       return nullptr;
    }
+   const std::vector<int> p = csr_partition(n, ia), tp = csr_partition(n, tia.data());
+   F->nparts = (int)p.size() - 1;
+   F->ntparts = (int)tp.size() - 1;
+   if (up(&F->part, p.data(), p.size()) || up(&F->tpart, tp.data(), tp.size())) {
+      fsai_free(F);
+      return nullptr;
+   }
    return F;
 }
 
 int fsai_apply_dev(FsaiDev* F, double* dx, const double* drhs, hipStream_t s)
 {
-   const int g = (F->n + kCsrT - 1) / kCsrT;
-   hipLaunchKernelGGL(k_csr_staged, dim3(g), dim3(kCsrT), 0, s, F->ia, F->ja, F->aa, drhs, F->work, F->n);
-   hipLaunchKernelGGL(k_csr_staged, dim3(g), dim3(kCsrT), 0, s, F->tia, F->tja, F->taa, F->work, dx, F->n);
+   hipLaunchKernelGGL(k_csr_staged, dim3(F->nparts), dim3(kCsrT), 0, s, F->ia, F->ja, F->aa, drhs, F->work,
+                      F->part);
+   hipLaunchKernelGGL(k_csr_staged, dim3(F->ntparts), dim3(kCsrT), 0, s, F->tia, F->tja, F->taa, F->work, dx,
+                      F->tpart);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

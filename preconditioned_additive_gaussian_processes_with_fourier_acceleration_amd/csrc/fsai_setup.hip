@@ -610,7 +610,8 @@ __global__ __launch_bounds__(256) void k_csr_mv(const int* __restrict__ ia, cons
                                                 const double* __restrict__ a, const double* __restrict__ x,
                                                 double* __restrict__ y, int n, int beta_one)
 {
-   csr_rows_staged<256, 2048>(ia, ja, a, x, y, n, beta_one != 0);  // csr.hpp: the entries through LDS
+   const int r0 = blockIdx.x * 256;
+   csr_rows_staged<256, 2048>(ia, ja, a, x, y, r0, min(r0 + 256, n), beta_one != 0);  // csr.hpp: entries via LDS
 }
 
 // out[blk] = sum over the block's rows of num[diag_i] / den[diag_i] (or log(1 / den[diag_i]) when num is
