@@ -202,7 +202,9 @@ def test_row_sharded_nystrom_apply_and_pcg(gloo2, single):
     assert rel(z, single["nys_z"]) < 1e-12
     its = [int(r["nys_it"]) for r in gloo2]
     assert len(set(its)) == 1 and its[0] > 0
-    assert abs(its[0] - int(single["nys_it"])) <= 2, (its, single["nys_it"])
+    it1 = int(single["nys_it"])
+    # the same run-to-run LDS-atomic order effect as in test_distributed_pcg_matches_single_gpu (58 vs 55 seen)
+    assert abs(its[0] - it1) <= max(3, it1 // 20), (its, it1)
     assert rel(np.concatenate([r["nys_x"] for r in gloo2]), single["nys_x"]) < 1e-4
 
 
