@@ -405,7 +405,8 @@ int Nfft4GPAmdAfnRankEstimate(const NFFT4GP_DOUBLE *data, int n, int ldim, int d
  * or -- when the AFN's factors break down (K11 not positive definite, the Schur FSAI meets a non-positive
  * pivot) -- MATLAB's RAN fallback, a Nystrom on the same order (afn_setup.m:93-98).  Nfft4GPAmdPrecondAFNSolve
  * is the func_solve of whichever was built; Nfft4GPAmdPrecondAFNInfo reports kind (0 AFN, 1 Nystrom below
- * max_k, 2 Nystrom after a breakdown), k and the underlying Nfft4GPAmdAfn* / Nfft4GPAmdNys* handle. */
+ * max_k, 2 Nystrom after a breakdown; with gradients 3 FSAI at k = 0, 4 Nystrom at k = n), k and the
+ * underlying Nfft4GPAmdAfn* / Nfft4GPAmdNys* handle. */
 void *Nfft4GPAmdPrecondAFNSetup(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int max_k, int perm_opt,
                                 int schur_opt, int schur_lfil, int nsamples, int kernel, void *fkernel_params,
                                 int require_grad);
@@ -421,7 +422,9 @@ void Nfft4GPAmdPrecondAFNFree(void *pre);
  * are Nfft4GPAmdPrecondNys* with gradients (additive handle as kernel data).  Dvp returns
  * M^{-1} (dM/dtheta_g) x like the reference's nys.c / fsai.c (afn_dvp.m returns (dM/dtheta_g) x: the
  * result goes through the apply once more); Trace = tr(M^{-1} dM/dtheta_g), Logdet = log det M.
- * AFN gradients need 0 < k < n and schur_opt 3. */
+ * AFN gradients need schur_opt 3.  With gradients the k = n and k = 0 branches (afn.c:263-284) are built as
+ * their exact equivalents that have gradients: kind 4, the rank-n Nystrom (= K + mu f^2 I), and kind 3, the
+ * FSAI of the whole kernel (Nfft4GPAmdPrecondFsai*, lfil schur_lfil); Info reports them. */
 void *Nfft4GPAmdPrecondAFNCreate(int max_k, int perm_opt, int schur_opt, int schur_lfil, int nsamples);
 int Nfft4GPAmdPrecondAFNSetupWithKernel(NFFT4GP_DOUBLE *data, int n, int ldim, int d, func_kernel fkernel,
                                         void *fkernel_params, int require_grad, void *pre);
@@ -521,6 +524,18 @@ int Nfft4GPAmdDistMatSymv(void *dop, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE
                           NFFT4GP_DOUBLE *y);
 int Nfft4GPAmdDistGradMatSymv(void *dop, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE beta,
                               NFFT4GP_DOUBLE *y);
+/* func_kernel (kernels.h:49) of a distributed operator, for Nfft4GPGpLoss (gp_loss.c:96-307): dop begins
+ * with an nfft4gp_kernel header, so the loss writes _params[0] (f), _params[1] (l) and _noise_level (mu)
+ * into it as it does into the reference's handle (gp_loss.c:143-150); the setup hands them to the local
+ * handle (Nfft4GPNFFTAdditiveKernelGaussianKernel / ...Matern12Kernel, nfft_interface.c:676-794) and
+ * returns *Kp = *dKp = dop.  With matvec = Nfft4GPAmdDistMatSymv and dmatvec = Nfft4GPAmdDistGradMatSymv
+ * the loss, Nfft4GPSolverFgmres and Nfft4GPSolverLanczos run on the split operator: for kind 0 (rows)
+ * n, label and the Rademacher probes are this rank's rows (probes column-major with stride n) and every
+ * dot product and norm is summed over the communicator; kind 1 (components) has whole vectors. */
+int Nfft4GPAmdDistGaussianKernel(void *dop, NFFT4GP_DOUBLE *data, int n, int ldim, int d, int *permr, int kr,
+                                 int *permc, int kc, NFFT4GP_DOUBLE **Kp, NFFT4GP_DOUBLE **dKp);
+int Nfft4GPAmdDistMatern12Kernel(void *dop, NFFT4GP_DOUBLE *data, int n, int ldim, int d, int *permr, int kr,
+                                 int *permc, int kc, NFFT4GP_DOUBLE **Kp, NFFT4GP_DOUBLE **dKp);
 /* Row-sharded Nystrom apply (nys.c:115-173 over row shards): keeps rows [row_begin, row_end) of a
  * Nystrom preconditioner's U (Nfft4GPAmdNysCreate / Nfft4GPAmdNysSetupAdditive; copied, the source may
  * be freed); the apply is a local U^T r, a k-vector all-reduce and a local U w + r/eta.  func_solve on

@@ -170,6 +170,10 @@ _SIGS = {
     "Nfft4GPAmdDistFree": (None, [vp]),
     "Nfft4GPAmdDistMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),
     "Nfft4GPAmdDistGradMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),
+    "Nfft4GPAmdDistGaussianKernel": (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, C.c_int, vp,
+                                              vp]),
+    "Nfft4GPAmdDistMatern12Kernel": (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, C.c_int, vp,
+                                              vp]),
     "Nfft4GPAmdNysShard": (vp, [vp, C.c_int, C.c_int, vp]),
     "Nfft4GPAmdDistNysSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdDistNysFree": (None, [vp]),

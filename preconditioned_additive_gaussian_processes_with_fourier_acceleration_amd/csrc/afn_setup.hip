@@ -1008,16 +1008,22 @@ struct AfnFlow {
    // parameters (Nfft4GPAmdPrecondAFNCreate)
    int max_k = 0, perm_opt = 0, schur_opt = 3, schur_lfil = 20, nsamples = 500;
    // what the last setup built
-   int kind = 0;  // 0 AFN, 1 Nystrom (rank below max_k), 2 Nystrom after an AFN breakdown (RAN)
+   // 0 AFN, 1 Nystrom (rank below max_k), 2 Nystrom after an AFN breakdown (RAN); with gradients the AFN's
+   // k = 0 / k = n branches (afn.c:263-284) as their exact equivalents: 3 the FSAI of the whole kernel
+   // (k = 0), 4 the rank-n Nystrom, which is K + mu f^2 I itself (k = n)
+   int kind = 0;
    int k = 0;
    int n = 0;
    void* afn = nullptr;
    NysDev* nys = nullptr;     // Nystrom branches without gradients
    void* nysg = nullptr;      // Nystrom branches with gradients (Nfft4GPAmdPrecondNys* handle)
    AfnGrad* grad = nullptr;   // the AFN's gradient pieces
+   void* fsaig = nullptr;     // kind 3 (Nfft4GPAmdPrecondFsai* handle with gradients)
    void reset()
    {
       if (grad) afn_grad_free(grad);
+      if (fsaig) Nfft4GPAmdPrecondFsaiFree(fsaig);
+      fsaig = nullptr;
       if (afn) Nfft4GPAmdAfnFree(afn);
       if (nys) Nfft4GPAmdNysFree(nys);
       if (nysg) Nfft4GPAmdPrecondNysFree(nysg);
@@ -1073,6 +1079,20 @@ static void* flow_nystrom_grad(double* data, int n, int ldim, int d, int kernel,
    return N;
 }
 
+// the FSAI with gradients of the whole kernel (the AFN at k = 0 with its Schur FSAI, schur_opt 3)
+static void* flow_fsai_grad(double* data, int n, int ldim, int d, int kernel, void* fkernel_params, int lfil)
+{
+   void* S = Nfft4GPAmdPrecondFsaiCreate();
+   Nfft4GPAmdPrecondFsaiSetLfil(S, lfil);
+   Nfft4GPAmdPrecondFsaiSetKernel(S, kernel);
+   func_kernel fk = kernel ? &Nfft4GPNFFTAdditiveKernelMatern12Kernel : &Nfft4GPNFFTAdditiveKernelGaussianKernel;
+   if (Nfft4GPAmdPrecondFsaiSetupWithKernel(data, n, ldim, d, fk, fkernel_params, 1, S)) {
+      Nfft4GPAmdPrecondFsaiFree(S);
+      return nullptr;
+   }
+   return S;
+}
+
 static int flow_setup(AfnFlow* F, double* data, int n, int ldim, int d, int kernel, void* fkernel_params, int grad)
 {
    F->reset();
@@ -1093,6 +1113,14 @@ static int flow_setup(AfnFlow* F, double* data, int n, int ldim, int d, int kern
    if (max_kk > 0 && k > 0 && k < n && k < max_kk) {
       printf("The estimated rank %d is below max_k = %d: rank-%d Nystrom (afn.c:294-304)\n", k, max_kk, k);
       nystrom(1);
+   } else if (grad && k >= n) {
+      // M = K11 + mu f^2 I = K + mu f^2 I (afn.c:263-272); the rank-n Nystrom is the same matrix and has
+      // gradients (nys_grad.hip)
+      nystrom(4);
+   } else if (grad && k == 0 && F->schur_opt == 3) {
+      // M^{-1} = G^T G, the FSAI of the whole kernel (afn.c:274-284); fsai_setup.hip has its gradients
+      F->kind = 3;
+      F->fsaig = flow_fsai_grad(data, n, ldim, d, kernel, fkernel_params, F->schur_lfil);
    } else {
       bool breakdown = false;
       F->afn = afn_setup_impl(data, n, ldim, d, k, 2, perm.data(), F->schur_opt, F->schur_lfil, kernel,
@@ -1102,7 +1130,7 @@ static int flow_setup(AfnFlow* F, double* data, int n, int ldim, int d, int kern
          nystrom(2);
       }
    }
-   if (!F->afn && !F->nys && !F->nysg) {
+   if (!F->afn && !F->nys && !F->nysg && !F->fsaig) {
       fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdPrecondAFNSetup failed\n");
       return -1;
    }
@@ -1163,6 +1191,7 @@ int Nfft4GPAmdPrecondAFNSolve(void* pre, int n, double* x, double* rhs)
    if (!F || n != F->n) return -1;
    if (F->afn) return Nfft4GPAmdAfnSolve(F->afn, n, x, rhs);
    if (F->nysg) return Nfft4GPAmdPrecondNysSolve(F->nysg, n, x, rhs);
+   if (F->fsaig) return Nfft4GPAmdPrecondFsaiSolve(F->fsaig, n, x, rhs);
    return Nfft4GPAmdNysSolve(F->nys, n, x, rhs);
 }
 
@@ -1171,6 +1200,7 @@ int Nfft4GPAmdPrecondAFNDvp(void* pre, int n, int* mask, double* x, double** yp)
    AfnFlow* F = (AfnFlow*)pre;
    if (!F || n != F->n || !yp) return -1;
    if (F->nysg) return Nfft4GPAmdPrecondNysDvp(F->nysg, n, mask, x, yp);
+   if (F->fsaig) return Nfft4GPAmdPrecondFsaiDvp(F->fsaig, n, mask, x, yp);
    if (!F->grad) {
       printf("Setup AFN without gradient, dvp not supported.\n");
       return -1;
@@ -1209,6 +1239,7 @@ int Nfft4GPAmdPrecondAFNTrace(void* pre, double** tracesp)
    AfnFlow* F = (AfnFlow*)pre;
    if (!F || !tracesp) return -1;
    if (F->nysg) return Nfft4GPAmdPrecondNysTrace(F->nysg, tracesp);
+   if (F->fsaig) return Nfft4GPAmdPrecondFsaiTrace(F->fsaig, tracesp);
    if (!F->grad) {
       printf("Setup AFN without gradient, trace not supported.\n");
       return -1;
@@ -1223,6 +1254,7 @@ double Nfft4GPAmdPrecondAFNLogdet(void* pre)
    AfnFlow* F = (AfnFlow*)pre;
    if (!F) return NAN;
    if (F->nysg) return Nfft4GPAmdPrecondNysLogdet(F->nysg);
+   if (F->fsaig) return Nfft4GPAmdPrecondFsaiLogdet(F->fsaig);
    return F->grad ? F->grad->logdet : NAN;
 }
 

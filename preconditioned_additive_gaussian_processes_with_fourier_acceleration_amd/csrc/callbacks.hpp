@@ -65,6 +65,10 @@ struct Callbacks {
    bool mv_dev, pc_dev;
    size_t n;
    size_t out_mult = 1;  // 3 for the gradient operators (y has 3n entries)
+   // a distributed operator (dist.hip): row shards sum every dot over `comm` and hold rows
+   // [row_begin, row_begin + n) of n_global; replicated vectors (component shards, one GPU) have comm == NULL
+   Comm* comm = nullptr;
+   size_t n_global = 0, row_begin = 0;
    double *h_in = nullptr, *h_out = nullptr;
    int ensure_host()
    {
@@ -106,6 +110,21 @@ struct Callbacks {
       return 0;
    }
 };
+
+// fills cb.comm / n_global / row_begin from the operator (after cb.matvec, cb.mat, cb.n, cb.mv_dev are set)
+inline int bind_dist(Callbacks& cb)
+{
+   cb.comm = nullptr;
+   cb.n_global = cb.n;
+   cb.row_begin = 0;
+   if (!cb.mv_dev || (cb.matvec != &Nfft4GPAmdDistMatSymv && cb.matvec != &Nfft4GPAmdDistGradMatSymv)) return 0;
+   DistPcgInfo info;
+   if (dist_pcg_info(cb.mat, info)) return -1;
+   cb.comm = info.dot_comm;
+   cb.n_global = (size_t)info.n_global;
+   cb.row_begin = (size_t)info.row_begin;
+   return 0;
+}
 
 // the library's own func_symmatvec / func_solve entry points (these take device pointers)
 bool library_operator(const void* fn);

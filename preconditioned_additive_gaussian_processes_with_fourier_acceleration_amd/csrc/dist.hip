@@ -95,6 +95,9 @@ struct CommCallback : Comm {
       for (size_t off = 0; off < count; off += cap) {
          const size_t m = std::min(cap, count - off);
          NFFT4GP_HIP_CHECK(hipMemcpyAsync(stage, d_buf + off, sizeof(double) * m, hipMemcpyDeviceToDevice, s));
+         // the callback may read the staging buffer on another stream (or from the host): the copy must
+         // have landed before it runs
+         NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
          if (fn(ctx, stage, (long long)m)) {
             fprintf(stderr, "nfft4gp_amd: the all-reduce callback failed\n");
             return -1;
@@ -113,10 +116,14 @@ __global__ void k_axpby_add(double beta, double* __restrict__ y, const double* _
 }
 
 struct DistOp {
+   // first member: a distributed operator is also the kernel data of the loss (gp_loss.c:143-150 writes
+   // _params[0] = f, _params[1] = l and _noise_level = mu into it before calling the kernel setup,
+   // Nfft4GPAmdDistGaussianKernel / ...Matern12Kernel, which hands them to the local handle)
+   nfft4gp_kernel hdr{};
    int kind = 0;  // 0 rows, 1 components
    void* h = nullptr;
    Comm* comm = nullptr;
-   int n_local = 0, n_global = 0;
+   int n_local = 0, n_global = 0, row_begin = 0;
    double* d_grid = nullptr;
    size_t grid_count = 0;
    double* d_tmp = nullptr;  // components, beta != 0: 3 n
@@ -196,6 +203,7 @@ int dist_pcg_info(void* dop, DistPcgInfo& info)
    DistOp* D = (DistOp*)dop;
    if (!D) return -1;
    info.n_global = D->n_global;
+   info.row_begin = D->kind == 0 ? D->row_begin : 0;
    info.dot_comm = D->kind == 0 ? D->comm : nullptr;
    info.fused_dot = D->kind == 0 && shard_fused_dot_ok(D->h);
    return 0;
@@ -299,6 +307,11 @@ void* Nfft4GPAmdDistCreate(void* handle, int kind, void* comm)
    D->comm = (Comm*)comm;
    D->n_local = nl;
    D->n_global = ng;
+   D->row_begin = rb;
+   const nfft4gp_kernel* kd = (const nfft4gp_kernel*)handle;
+   D->hdr._params[0] = kd->_params[0];
+   D->hdr._params[1] = kd->_params[1];
+   D->hdr._noise_level = kd->_noise_level;
    return D;
 }
 
@@ -310,6 +323,45 @@ void Nfft4GPAmdDistFree(void* dop)
    if (D->d_grid) (void)hipFree(D->d_grid);
    if (D->d_tmp) (void)hipFree(D->d_tmp);
    delete D;
+}
+
+// func_kernel of a distributed operator (kernels.h:49): the hyperparameters written into its header go to
+// the local handle, whose own setup runs (nfft_interface.c:676-794); *Kp = *dKp = the operator, so the
+// loss's matvec / grad-matvec calls reach Nfft4GPAmdDistMatSymv / ...GradMatSymv with it
+static int dist_kernel_setup(void* str, int kernel, double** Kp, double** dKp)
+{
+   DistOp* D = (DistOp*)str;
+   if (!D || !Kp || !dKp) {
+      printf("Error: NFFT kernel requires Kp and dKp to be not NULL.\n");
+      return -1;
+   }
+   nfft4gp_kernel* kd = (nfft4gp_kernel*)D->h;
+   kd->_params[0] = D->hdr._params[0];
+   kd->_params[1] = D->hdr._params[1];
+   kd->_noise_level = D->hdr._noise_level;
+   double *K = nullptr, *dK = nullptr;
+   const int rc = kernel == 0 ? Nfft4GPNFFTAdditiveKernelGaussianKernel(D->h, nullptr, D->n_local, D->n_local, 0,
+                                                                        nullptr, 0, nullptr, 0, &K, &dK)
+                              : Nfft4GPNFFTAdditiveKernelMatern12Kernel(D->h, nullptr, D->n_local, D->n_local, 0,
+                                                                        nullptr, 0, nullptr, 0, &K, &dK);
+   if (rc) return -1;
+   *Kp = (double*)D;
+   *dKp = (double*)D;
+   return 0;
+}
+
+int Nfft4GPAmdDistGaussianKernel(void* str, double* data, int n, int ldim, int d, int* permr, int kr, int* permc,
+                                 int kc, double** Kp, double** dKp)
+{
+   (void)data, (void)n, (void)ldim, (void)d, (void)permr, (void)kr, (void)permc, (void)kc;
+   return dist_kernel_setup(str, 0, Kp, dKp);
+}
+
+int Nfft4GPAmdDistMatern12Kernel(void* str, double* data, int n, int ldim, int d, int* permr, int kr, int* permc,
+                                 int kc, double** Kp, double** dKp)
+{
+   (void)data, (void)n, (void)ldim, (void)d, (void)permr, (void)kr, (void)permc, (void)kc;
+   return dist_kernel_setup(str, 1, Kp, dKp);
 }
 
 int Nfft4GPAmdDistMatSymv(void* dop, int n, double alpha, double* x, double beta, double* y)

@@ -179,7 +179,7 @@ struct AdditivePlan {
    double* d_C = nullptr;     // [kTaps][kNC]
    double* d_dot_part = nullptr;         // [nblocks] fused matvec-dot partials
    unsigned int* d_dot_ticket = nullptr; // arrival counters (reduce.hpp)
-   double* d_part2 = nullptr; // two-vector matvec: the second vector's partial grids
+   double* d_part2 = nullptr; // two-vector matvec: both vectors' partial grids [2][nblocks][nw][64]
    double* d_H2 = nullptr;    // [2][nw][64][kNC]
    double* d_xs = nullptr;    // staging (host pointer calls)
    double* d_ys = nullptr;    // staging 3n
@@ -360,6 +360,7 @@ int shard_finish_dot(void* str, const double* grid, const double* x_local, doubl
 struct DistPcgInfo {
    Comm* dot_comm = nullptr;
    int n_global = 0;
+   int row_begin = 0;  // this rank's first row (0 for replicated vectors)
    bool fused_dot = false;
 };
 int dist_pcg_info(void* dop, DistPcgInfo& info);

@@ -286,13 +286,20 @@ KScratch g_k;
 struct Ctx {
    hipStream_t s;
    size_t n;
+   // row-sharded vectors (a distributed operator's rows): every inner product is a local partial, summed
+   // in place over the ranks on the stream before anything reads it; NULL for whole vectors
+   Comm* comm = nullptr;
+   int red(double* d, int count)
+   {
+      return comm ? comm->allreduce(d, (size_t)count, s) : 0;
+   }
    // w -= h u (u optional), *out = (w, v) or ||w||^2
    int gs(double* w, const double* u, const double* hprev, const double* v, double* out)
    {
       hipLaunchKernelGGL(k_gs_step, dim3(kgrid(n)), dim3(kKThreads), 0, s, w, u, hprev, v, n, g_k.part, g_k.ticket,
                          out);
       NFFT4GP_HIP_CHECK(hipGetLastError());
-      return 0;
+      return red(out, 1);
    }
    int read(const double* d, int count, double* h)
    {
@@ -317,14 +324,18 @@ struct Ctx {
       if (g_k.ensure_bpart()) return -1;
       const int nb = bd_grid(n);
       const int mc = m + with_norm;
+      // h[m], h[m + 1] take part in the all-reduce below even when this pass does not write them
+      if (comm) NFFT4GP_HIP_CHECK(hipMemsetAsync(h + m, 0, sizeof(double) * 2, s));
       hipLaunchKernelGGL(k_block_dots, dim3(nb, (mc + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m, with_norm,
                          g_k.bpart, KScratch::kScal);
       hipLaunchKernelGGL(k_block_reduce, dim3((mc + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, mc, m,
                          h);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      if (red(h, m + 2)) return -1;  // the projections and the norm before them, summed over the row shards
       hipLaunchKernelGGL(k_block_update, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, Z, n, h, m,
                          g_k.part, g_k.ticket, h + m);
       NFFT4GP_HIP_CHECK(hipGetLastError());
-      return 0;
+      return red(h + m, 1);
    }
    void scale(double* a, double* b, double f)
    {
@@ -380,9 +391,9 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
                double* prel_res, double** prel_res_v, int* piter, int print_level)
 {
    const size_t n = cb.n;
-   Ctx c{current_stream(), n};
+   Ctx c{current_stream(), n, cb.comm};
    const double EPS = DBL_EPSILON;
-   if (n == 0) {
+   if (cb.n_global == 0) {  // (a row shard may hold no rows: it still takes part in every all-reduce)
       *prel_res = 0.0;
       *piter = 0;
       *prel_res_v = rel_hist(1);
@@ -576,7 +587,7 @@ struct LanczosRun {
 
    LanczosRun(Callbacks& cb_, double* x_, int wsize_, int maxits_, int atol_, double tol_, int print_level_,
               double** TDp_, double** TEp_)
-       : cb(cb_), c{current_stream(), cb_.n}, n(cb_.n), x(x_), wsize(wsize_), maxits(maxits_),
+       : cb(cb_), c{current_stream(), cb_.n, cb_.comm}, n(cb_.n), x(x_), wsize(wsize_), maxits(maxits_),
          print_level(print_level_), tol(tol_), atol(atol_), TDp(TDp_), TEp(TEp_)
    {
       if (wsize <= 0) wsize = maxits;
@@ -594,7 +605,7 @@ struct LanczosRun {
    // everything before the first step; returns -1 on error, 1 when the run is already complete
    int init(const double* rhs, double* prel_res, double** prel_res_v, int* piter)
    {
-      if (n == 0) {
+      if (cb.n_global == 0) {
          *prel_res = 0.0;
          *piter = 0;
          *prel_res_v = rel_hist(1);
@@ -681,7 +692,7 @@ struct LanczosRun {
       hipLaunchKernelGGL(k_dot2, dim3(kgrid(n)), dim3(kKThreads), 0, c.s, v, z, n, g_k.part, g_k.ticket, g_k.part2,
                          g_k.ticket2, o);
       double vz[2];
-      if (c.read(o, 2, vz)) return -1;
+      if (c.red(o, 2) || c.read(o, 2, vz)) return -1;
       dotvz = std::sqrt(vz[0]);
       if (dotvz < EPS) return 1;
       c.scale(v, alias ? nullptr : z, 1.0 / dotvz);
@@ -735,12 +746,14 @@ struct LanczosRun {
          if (t < EPS || dotvz < EPS) {
             z = Z + (size_t)iter * n;
             v = V + (size_t)iter * n;
-            std::vector<double> rnd(n);
+            // Nfft4GPVecRand of the whole vector (every rank draws the same n_global numbers; a row shard
+            // keeps its rows)
+            std::vector<double> rnd(cb.n_global);
             {
                CallerRandBatch caller;
-               for (size_t i = 0; i < n; i++) rnd[i] = (double)rand() / (double)RAND_MAX;  // Nfft4GPVecRand
+               for (size_t i = 0; i < cb.n_global; i++) rnd[i] = (double)rand() / (double)RAND_MAX;
             }
-            NFFT4GP_HIP_CHECK(hipMemcpy(z, rnd.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+            NFFT4GP_HIP_CHECK(hipMemcpy(z, rnd.data() + cb.row_begin, sizeof(double) * n, hipMemcpyHostToDevice));
             double td, te;
             if (mgs2(c, z, V, Z, iter - 1, &td, &te, &t)) return -1;
             if (t < EPS) break;
@@ -839,15 +852,16 @@ int lanczos_logdet_dev(Callbacks& cb, Callbacks& dcb, func_trace tracefunc, func
                        double* logdet, double** dlogdetp)
 {
    const size_t n = cb.n;
-   Ctx c{current_stream(), n};
+   const double nall = (double)cb.n_global;  // the 1/n normalisations use the whole problem's n
+   Ctx c{current_stream(), n, cb.comm};
    void* prec_data = cb.prec ? cb.pdata : nullptr;
    double* dval = *dlogdetp ? *dlogdetp : (double*)calloc(3, sizeof(double));
    double traces_precond[3] = {0.0, 0.0, 0.0}, logdet_precond = 0.0;
    if (prec_data) {
       double* tp = traces_precond;
       if (tracefunc(prec_data, &tp)) return -1;
-      for (int i = 0; i < 3; i++) traces_precond[i] /= (double)n;
-      logdet_precond = logdetfunc(prec_data) / (double)n;
+      for (int i = 0; i < 3; i++) traces_precond[i] /= nall;
+      logdet_precond = logdetfunc(prec_data) / nall;
    }
    const bool dvp_dev = g_cb_mode == 1 || (g_cb_mode == -1 && library_operator((const void*)dvpfunc));
    double *z = nullptr, *x = nullptr, *dAz = nullptr, *px = nullptr;
@@ -939,9 +953,10 @@ int lanczos_logdet_dev(Callbacks& cb, Callbacks& dcb, func_trace tracefunc, func
          NFFT4GP_HIP_CHECK(hipMemcpyAsync(z, radamacher + (size_t)i * n, sizeof(double) * n,
                                           rad_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c.s));
       } else {
-         hz.resize(n);
-         Nfft4GPVecRadamacher(hz.data(), (int)n);
-         NFFT4GP_HIP_CHECK(hipMemcpyAsync(z, hz.data(), sizeof(double) * n, hipMemcpyHostToDevice, c.s));
+         // every rank draws the whole probe (the same libc sequence); a row shard keeps its rows
+         hz.resize(cb.n_global);
+         Nfft4GPVecRadamacher(hz.data(), (int)cb.n_global);
+         NFFT4GP_HIP_CHECK(hipMemcpy(z, hz.data() + cb.row_begin, sizeof(double) * n, hipMemcpyHostToDevice));
       }
       NFFT4GP_HIP_CHECK(hipMemsetAsync(x, 0, sizeof(double) * n, c.s));
       double rel_res, *rel_res_v = nullptr, *TD = nullptr, *TE = nullptr;
@@ -961,7 +976,7 @@ int lanczos_logdet_dev(Callbacks& cb, Callbacks& dcb, func_trace tracefunc, func
    cleanup();
    double scale = 1.0 / (double)nvecs;
    val *= scale;
-   scale /= (double)n;
+   scale /= nall;
    for (int j = 0; j < 3; j++) dval[j] *= scale;
    val += logdet_precond;
    for (int j = 0; j < 3; j++) dval[j] += traces_precond[j];
@@ -986,6 +1001,7 @@ bool make_callbacks(Callbacks& cb, int n, func_symmatvec matvec, void* mat, func
    cb.n = (size_t)n;
    cb.mv_dev = g_cb_mode == 1 || (g_cb_mode == -1 && library_operator((const void*)matvec));
    cb.pc_dev = g_cb_mode == 1 || (g_cb_mode == -1 && library_operator((const void*)prec));
+   if (bind_dist(cb)) return false;
    return g_k.ensure() == 0;
 }
 
@@ -1137,13 +1153,18 @@ int Nfft4GPGpLoss(double* x, double* data, double* label, int n, int ldim, int d
        !make_callbacks(dcb, n, dmatvec, dkernel_mat, nullptr, nullptr))
       return -1;
    dcb.out_mult = 3;
+   if (cb.comm != dcb.comm || cb.n_global != dcb.n_global) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPGpLoss: matvec and dmatvec must be split the same way\n");
+      return -1;
+   }
+   const int nall = (int)cb.n_global;  // n of the whole problem (a row shard holds n of its rows)
    hipStream_t s = current_stream();
-   Ctx c{s, (size_t)n};
+   Ctx c{s, (size_t)n, cb.comm};
    double *iKY = nullptr, *dKiKY = nullptr;
    Vec vl;
    if (dmalloc(&iKY, (size_t)n) || dmalloc(&dKiKY, 3 * (size_t)n) || vl.open(label, n, true)) return -1;
    NFFT4GP_HIP_CHECK(hipMemsetAsync(iKY, 0, sizeof(double) * n, s));
-   const int solve_kdim = std::min(n, maxits * 2), solve_maxits = std::min(n, maxits * 2);
+   const int solve_kdim = std::min(nall, maxits * 2), solve_maxits = std::min(nall, maxits * 2);
    double rel_res, *rel_res_v = nullptr;
    int niter = 0;
    if (fgmres_dev(cb, iKY, vl.d, solve_kdim, solve_maxits, atol, tol, &rel_res, &rel_res_v, &niter, print_level))
@@ -1153,12 +1174,12 @@ int Nfft4GPGpLoss(double* x, double* data, double* label, int n, int ldim, int d
       printf("Current parameters (after transform): f = %f, l = %f, mu = %f\n", tvals[0], tvals[1], tvals[2]);
    }
    free(rel_res_v);
-   const double L1 = c.dot(vl.d, iKY) / (double)n;
+   const double L1 = c.dot(vl.d, iKY) / (double)nall;
    if (dcb.apply(1.0, iKY, 0.0, dKiKY)) return -1;
    double L1_grad[3];
-   for (int i = 0; i < 3; i++) L1_grad[i] = c.dot(dKiKY + (size_t)i * n, iKY) / (double)n * dtvals[i];
+   for (int i = 0; i < 3; i++) L1_grad[i] = c.dot(dKiKY + (size_t)i * n, iKY) / (double)nall * dtvals[i];
    double L2 = 0.0, *L2_grad = nullptr;
-   const int qits = std::min(n, maxits);
+   const int qits = std::min(nall, maxits);
    const int err = lanczos_logdet_dev(cb, dcb, precond_trace, precond_logdet, precond_dvp, qits, nvecs, radamacher,
                                       print_level, &L2, &L2_grad);
    (void)hipStreamSynchronize(s);
@@ -1217,6 +1238,10 @@ int Nfft4GPAdditiveNFFTGpPredict(double* x, double* data, double* label, int n, 
    if (!make_callbacks(cb11, n, matvec, K11, precond_solve, precond_data) ||
        !make_callbacks(cba, na, matvec, K, nullptr, nullptr))
       return -1;
+   if (cb11.n_global != cb11.n || cb11.comm) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAdditiveNFFTGpPredict takes a one-GPU operator\n");
+      return -1;
+   }
    hipStream_t s = current_stream();
    Ctx c{s, (size_t)n};
    double *iKY = nullptr, *helper = nullptr;

@@ -882,6 +882,9 @@ int Nfft4GPAmdAdditiveComponentShard(void* str, int nw_global, int own_diag)
    }
    E->P.weight = 1.0 / (double)nw_global;  // the whole operator's 1/nwindows (nfft_interface.c:806)
    E->P.diag = own_diag ? 1.0 : 0.0;
+   // after a kernel setup the weight is already folded into the circulants: rebuild them with the new one
+   AdditivePlan& P = E->P;
+   if (P.points_ready) return plan_setup(P, ((nfft4gp_kernel*)str)->_buffer, P.kernel, P.f, P.l, P.mu);
    return 0;
 }
 

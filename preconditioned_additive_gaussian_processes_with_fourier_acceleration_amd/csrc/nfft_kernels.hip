@@ -757,12 +757,13 @@ int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double
    }
    const size_t part_rs = (size_t)std::max(1, P.nblocks) * P.nw * kNos;
    const size_t h_rs = (size_t)P.nw * kNos * kNC;
-   if (!P.d_part2) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part2, sizeof(double) * part_rs));
+   // both vectors' partial grids in one allocation, so k_grid's per-vector stride stays inside it
+   if (!P.d_part2) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part2, sizeof(double) * 2 * part_rs));
    if (!P.d_H2) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_H2, sizeof(double) * 2 * h_rs));
-   if (launch_spread(P, x0, P.d_part, stream) || launch_spread(P, x1, P.d_part2, stream)) return -1;
-   hipLaunchKernelGGL(k_grid, dim3(P.nw, 2), dim3(kGridThreads), 0, stream, (const double*)P.d_part, P.nblocks,
-                      (const double*)P.d_w, (const double*)P.d_wd, P.d_H2, P.d_Hd, 0, 0,
-                      (long long)(P.d_part2 - P.d_part), (long long)h_rs);
+   if (launch_spread(P, x0, P.d_part2, stream) || launch_spread(P, x1, P.d_part2 + part_rs, stream)) return -1;
+   hipLaunchKernelGGL(k_grid, dim3(P.nw, 2), dim3(kGridThreads), 0, stream, (const double*)P.d_part2, P.nblocks,
+                      (const double*)P.d_w, (const double*)P.d_wd, P.d_H2, P.d_Hd, 0, 0, (long long)part_rs,
+                      (long long)h_rs);
    const size_t lds_i = sizeof(double) * 2 * ((size_t)P.B + kPad);
    hipLaunchKernelGGL(k_interp2<kInterp2Threads>, dim3(P.nblocks), dim3(kInterp2Threads), lds_i, stream, P.dl.meta,
                       P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H2, h_rs, x0, x1, y0, y1, P.n, P.B,

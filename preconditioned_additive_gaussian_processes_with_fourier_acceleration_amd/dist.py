@@ -125,7 +125,8 @@ class DistributedAdditiveKernel:
     rows:       x, y hold this rank's rows [row_begin, row_end); ``n`` is their count.
     components: this rank's windows [comp_begin, comp_end) for all n points, x and y whole (replicated).
     ``solvers.pcg(self, b, x)`` runs Nfft4GPSolverPcg on it (device-controlled, dots summed over the ranks
-    for rows)."""
+    for rows); ``solvers.fgmres``, ``solvers.logdet`` and ``gp.gp_loss(..., op=self)`` run the reference's
+    FGMRES, Lanczos quadrature and GP loss on it the same way (krylov.hip, every rank collectively)."""
 
     def __init__(self, data, windows, nwindows: int, dwindows: int, comm: Communicator, partition: str = "rows"):
         from . import _lib
@@ -181,6 +182,11 @@ class DistributedAdditiveKernel:
     def matvec_fnptr(self) -> int:
         from . import _lib
         return _lib.fnptr("Nfft4GPAmdDistMatSymv")
+
+    @property
+    def gradmatvec_fnptr(self) -> int:
+        from . import _lib
+        return _lib.fnptr("Nfft4GPAmdDistGradMatSymv")
 
     def free(self):
         from . import _lib

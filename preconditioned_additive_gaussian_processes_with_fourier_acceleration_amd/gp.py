@@ -2,7 +2,9 @@
 
 ``gp_loss``     Nfft4GPGpLoss (SRC/optimizer/gp_loss.c:96-307) with Nfft4GPNFFTAdditiveKernelGaussianKernel /
                 Nfft4GPAdditiveNFFTMatSymv / Nfft4GPAdditiveNFFTGradMatSymv as kernel, matvec and grad matvec,
-                no preconditioner (TEST1-style call of the north-star operator inside the loss).
+                no preconditioner (TEST1-style call of the north-star operator inside the loss); or, over
+                one process per GPU, a dist.DistributedAdditiveKernel with Nfft4GPAmdDistGaussianKernel /
+                Nfft4GPAmdDistMatSymv / Nfft4GPAmdDistGradMatSymv (BASELINE configs[4]).
 ``gp_predict``  Nfft4GPAdditiveNFFTGpPredict (SRC/external/nfft_interface.c:873-1068): posterior mean and,
                 optionally, standard deviation at new points (a second handle over [X; Xp], as TEST4 does).
 """
@@ -29,13 +31,26 @@ def gp_loss(X, windows, nwindows, dwindows, y, hyper, maxits=50, nvecs=10, radem
     """(loss, grad) of Nfft4GPGpLoss for the additive NFFT Gaussian kernel; ``hyper`` = (f, l, mu) before
     the transform (0 softplus, 1 sigmoid, 2 exp, 3 identity).  ``op``: an existing NFFTAdditiveKernel over
     the same X to reuse, as the reference's optimizer loop reuses its kernel handle across loss calls
-    (its points, centring and scale stay those of its first setup, nfft_interface.c:150)."""
+    (its points, centring and scale stay those of its first setup, nfft_interface.c:150); or a
+    dist.DistributedAdditiveKernel (every rank calls gp_loss collectively): with partition "rows", ``y``
+    and ``rademacher`` hold this rank's rows [op.row_begin, op.row_end) only; with "components" they are
+    whole.  Every rank returns the same loss and gradient."""
+    from .dist import DistributedAdditiveKernel
     X = np.asfortranarray(np.asarray(X, dtype=np.float64))
     n, d = X.shape
+    setup_fn, mv, dmv = ("Nfft4GPNFFTAdditiveKernelGaussianKernel", "Nfft4GPAdditiveNFFTMatSymv",
+                         "Nfft4GPAdditiveNFFTGradMatSymv")
     if op is None:
         op = NFFTAdditiveKernel(X, windows, nwindows, dwindows)
+    elif isinstance(op, DistributedAdditiveKernel):
+        if op.n_global != n:
+            raise ValueError("op was created over a different number of points")
+        n = op.n  # this rank's rows (the whole n for components)
+        setup_fn, mv, dmv = "Nfft4GPAmdDistGaussianKernel", "Nfft4GPAmdDistMatSymv", "Nfft4GPAmdDistGradMatSymv"
     elif op.n != n:
         raise ValueError("op was created over a different number of points")
+    if len(y) != n:
+        raise ValueError(f"{len(y)} labels for {n} rows")
     L = _lib.lib()
     fn = L.Nfft4GPGpLoss
     fn.argtypes = _GPLOSS_ARGS
@@ -53,7 +68,7 @@ def gp_loss(X, windows, nwindows, dwindows, y, hyper, maxits=50, nvecs=10, radem
     loss = np.zeros(1)
     grad = np.zeros(3)
     rc = fn(x.ctypes.data, X.ctypes.data, lab.ctypes.data, n, n, d,
-            _lib.fnptr("Nfft4GPNFFTAdditiveKernelGaussianKernel"), op.h, None, op.matvec_fnptr, op.gradmatvec_fnptr,
+            _lib.fnptr(setup_fn), op.h, None, _lib.fnptr(mv), _lib.fnptr(dmv),
             None, None, None, None, None, None, None, None, None, None, 0, float(tol), int(maxits), int(maxits),
             int(nvecs), r_ptr, int(transform),
             m.ctypes.data if m is not None else None, int(print_level), None, loss.ctypes.data_as(_lib.dp),

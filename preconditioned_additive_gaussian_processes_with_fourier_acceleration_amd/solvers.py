@@ -225,7 +225,8 @@ class PrecondAFN(_Apply):
     Nystrom on the estimated landmarks when 0 < k < max_k (afn.c:294-304), and MATLAB's RAN fallback -- a
     Nystrom on the same order -- when the AFN's factors break down (afn_setup.m:93-98).
 
-    ``kind`` is "afn", "nystrom" or "ran"; ``k`` the rank.  The kernel is the plain Gaussian / Matern-1/2 of X
+    ``kind`` is "afn", "nystrom" or "ran" (with require_grad also "fsai" at k = 0 and "nystrom_full" at k = n,
+    the gradient-capable equivalents of afn.c:263-284's branches); ``k`` the rank.  The kernel is the plain Gaussian / Matern-1/2 of X
     (f, l, mu), or with ``op`` (an NFFTAdditiveKernel after its setup) the dense additive kernel of op's
     windows and hyperparameters.  perm_opt: "random" (0) or "fps" (1); schur: "fsai" (schur_opt 3) or
     "noise" (0).  max_k <= 0: the predefined rank -max_k in natural order, no estimation (afn.c:245-256).
@@ -233,7 +234,7 @@ class PrecondAFN(_Apply):
     branches need ``op``) for ``dvp`` (M^{-1} dM/dtheta_g x, g = f, l, mu), ``trace`` and ``logdet``."""
 
     _solve, _free = "Nfft4GPAmdPrecondAFNSolve", "Nfft4GPAmdPrecondAFNFree"
-    KINDS = ("afn", "nystrom", "ran")
+    KINDS = ("afn", "nystrom", "ran", "fsai", "nystrom_full")
 
     def __init__(self, X, max_k: int, f: float = 1.0, l: float = 1.0, mu: float = 0.01, perm_opt: str = "random",
                  schur: str = "fsai", schur_lfil: int = 20, nsamples: int = 500, kernel: int = 0, op=None,

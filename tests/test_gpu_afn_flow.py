@@ -101,3 +101,76 @@ def test_breakdown_falls_back_to_nystrom(torch_cuda):
     direct.free()
     pre.free()
     op.free()
+
+
+def _dense_additive(X, f, l):
+    """f^2 (1/nw) sum_w exp(-(x_w - y_w)^2 / (2 l^2)) over 1-D windows and its l-derivative (kernels.c:3099-3494
+    with kernels.c:680-1289 per window)."""
+    n, d = X.shape
+    K = np.zeros((n, n))
+    dKl = np.zeros((n, n))
+    for w in range(d):
+        r2 = (X[:, w:w + 1] - X[:, w][None, :]) ** 2
+        e = np.exp(-r2 / (2 * l * l))
+        K += e
+        dKl += e * r2 / l ** 3
+    return f * f * K / d, f * f * dKl / d
+
+
+def test_gradients_at_k_equal_n_use_the_full_rank_nystrom(torch_cuda):
+    """with require_grad the k = n branch (afn.c:263-272, M = K + mu f^2 I) used to fail the whole
+    setup.  It is now the rank-n Nystrom with gradients (kind 4), which is that matrix: apply, logdet, trace
+    and dvp against the dense kernel."""
+    torch = torch_cuda
+    n, d, f, l, mu = 300, 6, 1.2, 0.05, 0.05
+    X = np.random.default_rng(31).random((n, d))
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    assert op.setup(amd.GAUSSIAN, f=f, l=l, mu=mu) == 0
+    pre = amd.PrecondAFN(X, -n, op=op, require_grad=True)
+    assert pre.kind == "nystrom_full" and pre.k == n
+    K, dKl = _dense_additive(X, f, l)
+    M = K + mu * f * f * np.eye(n)
+    r = np.random.default_rng(32).random(n)
+    z = pre.solve(torch.zeros(n, dtype=torch.float64, device="cuda"),
+                  torch.tensor(r, device="cuda")).cpu().numpy()
+    assert rel(z, np.linalg.solve(M, r)) < 1e-8
+    assert pre.logdet() == pytest.approx(np.linalg.slogdet(M)[1], rel=1e-8)
+    Mi = np.linalg.inv(M)
+    dM = [2.0 * M / f, dKl, f * f * np.eye(n)]
+    np.testing.assert_allclose(pre.trace(), [np.trace(Mi @ g) for g in dM], rtol=1e-6)
+    y = pre.dvp(r)
+    for g in range(3):
+        assert rel(y[g * n:(g + 1) * n], Mi @ (dM[g] @ r)) < 1e-6
+    pre.free()
+    op.free()
+
+
+def test_gradients_at_k_zero_use_the_whole_kernel_fsai(torch_cuda):
+    """the k = 0 branch with require_grad (afn.c:274-284: the Schur FSAI of the whole kernel) is
+    the FSAI preconditioner with gradients (kind 3), equal to Nfft4GPAmdPrecondFsai* built directly."""
+    from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd import _lib
+    torch = torch_cuda
+    n, d, lfil = 2000, 4, 12
+    X, op = additive_problem(n=n, d=d, l=0.2, mu=0.05)
+    pre = amd.PrecondAFN(X, 0, op=op, schur_lfil=lfil, require_grad=True)
+    assert pre.kind == "fsai" and pre.k == 0
+    L = _lib.lib()
+    h = L.Nfft4GPAmdPrecondFsaiCreate()
+    L.Nfft4GPAmdPrecondFsaiSetLfil(h, lfil)
+    Xf = np.asfortranarray(X)
+    assert L.Nfft4GPAmdPrecondFsaiSetupWithKernel(Xf.ctypes.data, n, n, d,
+                                                  _lib.fnptr("Nfft4GPNFFTAdditiveKernelGaussianKernel"), op.h, 1,
+                                                  h) == 0
+    r = np.random.default_rng(33).random(n)
+    z1 = pre.solve(torch.zeros(n, dtype=torch.float64, device="cuda"), torch.tensor(r, device="cuda")).cpu().numpy()
+    z2 = np.zeros(n)
+    assert L.Nfft4GPAmdPrecondFsaiSolve(h, n, z2.ctypes.data, np.ascontiguousarray(r).ctypes.data) == 0
+    np.testing.assert_array_equal(z1, z2)
+    assert pre.logdet() == L.Nfft4GPAmdPrecondFsaiLogdet(h)
+    t = np.zeros(3)
+    tp = ctypes.c_void_p(t.ctypes.data)
+    assert L.Nfft4GPAmdPrecondFsaiTrace(h, ctypes.byref(tp)) == 0
+    np.testing.assert_array_equal(pre.trace(), t)
+    L.Nfft4GPAmdPrecondFsaiFree(h)
+    pre.free()
+    op.free()

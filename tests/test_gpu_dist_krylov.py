@@ -1,0 +1,126 @@
+"""The GP loss, FGMRES and the Lanczos log-det quadrature on the split operator (BASELINE configs[4]:
+log-marginal-likelihood + gradient on 8 GPUs), rehearsed with two gloo ranks on one GPU through the
+library's callback communicator.
+
+Reference loops being split: gp_loss.c:96-307 (loss and gradient), fgmres.c:3-252, lanczos.c:421-610.
+With rows split (dist.hip kind 0) every inner product of krylov.hip is a local partial summed over the
+ranks on the stream; with components split (kind 1) the vectors are whole and y is all-reduced.  Both
+must reproduce the one-GPU loss (rounding-level differences: the sums are regrouped) and the reference's
+loss on the oracle's operator (tests/golden/config_e_reduced.npz, make_golden.py config_e).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(HERE, "golden"))
+
+
+def _inputs():
+    from make_golden import config_e_inputs
+    z = dict(np.load(os.path.join(HERE, "golden", "config_e_reduced.npz")))
+    n, d, nvecs, maxits, seed = (int(z[k]) for k in ("n", "d", "nvecs", "maxits", "seed"))
+    X, y, R = config_e_inputs(n, d, nvecs, seed)
+    return z, X, y, R, d, nvecs, maxits
+
+
+def _worker(rank, world, port, outdir):
+    for p in (ROOT, HERE, os.path.join(HERE, "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import (
+        Communicator, DistributedAdditiveKernel)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Communicator.callback()
+    z, X, y, R, d, nvecs, maxits = _inputs()
+    win = np.arange(d, dtype=np.int32)
+    out = {}
+    for part in ("rows", "components"):
+        op = DistributedAdditiveKernel(X, win, d, 1, comm, partition=part)
+        rb, re = op.row_begin, op.row_end
+        loss, grad = amd.gp_loss(X, win, d, 1, y[rb:re], np.asarray(z["hyper"]), maxits=maxits, nvecs=nvecs,
+                                 rademacher=np.asfortranarray(R[rb:re]), tol=1e-8, transform=0, op=op)
+        # the solvers on their own, after the loss's setup (f = 1, l = 0.1, mu = 0.01)
+        b = torch.tensor(y[rb:re], device="cuda")
+        xs = torch.zeros_like(b)
+        _, rr, hist, it = amd.fgmres(op, b, xs, kdim=25, maxits=120, tol=1e-10)
+        ld, dld = amd.logdet(op, 15, nvecs, rademacher=np.asfortranarray(R[rb:re]))
+        out.update({part + "_loss": loss, part + "_grad": grad, part + "_x": xs.cpu().numpy(), part + "_it": it,
+                    part + "_rr": rr, part + "_hist": hist, part + "_ld": ld, part + "_dld": dld,
+                    part + "_rb": rb, part + "_re": re})
+        op.free()
+    torch.cuda.synchronize()
+    comm.free()
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def gloo2(tmp_path_factory):
+    import torch.multiprocessing as mp
+    from test_gpu_dist import _free_port
+    out = tmp_path_factory.mktemp("dist_krylov")
+    mp.spawn(_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    return [dict(np.load(os.path.join(out, f"rank{r}.npz"))) for r in range(2)]
+
+
+@pytest.fixture(scope="module")
+def single(torch_cuda):
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    torch = torch_cuda
+    z, X, y, R, d, nvecs, maxits = _inputs()
+    win = np.arange(d, dtype=np.int32)
+    op = amd.NFFTAdditiveKernel(X, win, d, 1)
+    loss, grad = amd.gp_loss(X, win, d, 1, y, np.asarray(z["hyper"]), maxits=maxits, nvecs=nvecs, rademacher=R,
+                             tol=1e-8, transform=0, op=op)
+    b = torch.tensor(y, device="cuda")
+    xs = torch.zeros_like(b)
+    _, rr, hist, it = amd.fgmres(op, b, xs, kdim=25, maxits=120, tol=1e-10)
+    ld, dld = amd.logdet(op, 15, nvecs, rademacher=R)
+    op.free()
+    return {"loss": loss, "grad": grad, "x": xs.cpu().numpy(), "it": it, "hist": hist, "ld": ld, "dld": dld,
+            "z": z}
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / max(np.linalg.norm(b), 1e-300))
+
+
+@pytest.mark.parametrize("part", ["rows", "components"])
+def test_distributed_gp_loss_matches_single_gpu_and_reference(gloo2, single, part):
+    for r in gloo2[1:]:  # every rank reports the same loss and gradient
+        assert float(r[part + "_loss"]) == float(gloo2[0][part + "_loss"])
+        np.testing.assert_array_equal(r[part + "_grad"], gloo2[0][part + "_grad"])
+    loss, grad = float(gloo2[0][part + "_loss"]), np.asarray(gloo2[0][part + "_grad"])
+    print(f"{part}: loss {loss!r} (one GPU {single['loss']!r}), grad {grad} (one GPU {single['grad']})")
+    assert loss == pytest.approx(single["loss"], rel=1e-10)
+    np.testing.assert_allclose(grad, single["grad"], rtol=1e-8, atol=1e-12)
+    z = single["z"]
+    assert loss == pytest.approx(float(z["loss"]), rel=1e-8)
+    np.testing.assert_allclose(grad, z["grad"], rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("part", ["rows", "components"])
+def test_distributed_fgmres_and_logdet_match_single_gpu(gloo2, single, part):
+    its = [int(r[part + "_it"]) for r in gloo2]
+    assert len(set(its)) == 1 and its[0] == int(single["it"]), (its, single["it"])
+    if part == "rows":
+        x = np.concatenate([r[part + "_x"] for r in gloo2])
+    else:
+        np.testing.assert_array_equal(gloo2[1][part + "_x"], gloo2[0][part + "_x"])
+        x = gloo2[0][part + "_x"]
+    assert _rel(x, single["x"]) < 1e-9
+    np.testing.assert_allclose(gloo2[0][part + "_hist"][:its[0] + 1], single["hist"][:its[0] + 1], rtol=1e-6)
+    assert float(gloo2[0][part + "_ld"]) == pytest.approx(single["ld"], rel=1e-10)
+    np.testing.assert_allclose(gloo2[0][part + "_dld"], single["dld"], rtol=1e-8, atol=1e-12)
