@@ -541,6 +541,14 @@ int Nfft4GPAmdDistMatern12Kernel(void *dop, NFFT4GP_DOUBLE *data, int n, int ldi
  * be freed); the apply is a local U^T r, a k-vector all-reduce and a local U w + r/eta.  func_solve on
  * this rank's rows (device). */
 void *Nfft4GPAmdNysShard(void *nys, int row_begin, int row_end, void *comm);
+/* The Nystrom setup (Nfft4GPPrecondNysSetupWithKernel, nys.c:518-660, as Nfft4GPAmdNysSetupAdditive with
+ * k11_mode 0 / 1) split over the row shards of a distributed operator (kind 0, after its kernel setup):
+ * each rank forms the panel K(rows, perm[:k]) of its own rows, U1 = Kp L^{-T} and its partial Gram
+ * U1^T U1 on MFMA; one k x k all-reduce sums the Gram (matops.c:65-137), rank 0's k x k factors are
+ * broadcast, and each rank keeps U for its rows only (n/N x k).  perm: the global landmark order (the
+ * first k entries are read), the same on every rank.  Returns a handle for Nfft4GPAmdDistNysSolve /
+ * Nfft4GPAmdDistNysFree. */
+void *Nfft4GPAmdNysShardSetupAdditive(void *dop, const int *perm, int k, int k11_mode);
 int Nfft4GPAmdDistNysSolve(void *dnys, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
 void Nfft4GPAmdDistNysFree(void *dnys);
 

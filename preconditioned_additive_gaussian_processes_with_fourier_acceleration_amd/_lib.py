@@ -175,6 +175,7 @@ _SIGS = {
     "Nfft4GPAmdDistMatern12Kernel": (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, C.c_int, vp,
                                               vp]),
     "Nfft4GPAmdNysShard": (vp, [vp, C.c_int, C.c_int, vp]),
+    "Nfft4GPAmdNysShardSetupAdditive": (vp, [vp, vp, C.c_int, C.c_int]),
     "Nfft4GPAmdDistNysSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdDistNysFree": (None, [vp]),
     "Nfft4GPAmdHostTapPoly": (C.c_int, [vp]),

@@ -408,6 +408,27 @@ void* Nfft4GPAmdNysShard(void* nys, int row_begin, int row_end, void* comm)
    return D;
 }
 
+// Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660, K11 on the landmarks) split over the row shards of a
+// distributed operator: every rank forms the panel of its own rows, U1 = Kp L^{-T} and its partial Gram
+// U1^T U1; ONE k x k all-reduce sums the Gram (matops.c:65-137 is a sum over rows); rank 0's k x k factors
+// (L^{-T}, the eigenbasis) are broadcast so every rank scales its rows alike.  No rank holds more than its
+// n/N rows of the n x k panel.
+void* Nfft4GPAmdNysShardSetupAdditive(void* dop, const int* perm, int k, int k11_mode)
+{
+   DistOp* D = (DistOp*)dop;
+   if (!D || D->kind != 0 || !perm || (k11_mode != 0 && k11_mode != 1)) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdNysShardSetupAdditive needs a row-sharded operator (kind 0), the "
+                      "landmark order and k11_mode 0 or 1\n");
+      return nullptr;
+   }
+   NysDev* N = nys_setup_shard(D->h, perm, k, k11_mode, D->comm);
+   if (!N) return nullptr;
+   DistNys* R = new DistNys();
+   R->N = N;
+   R->comm = D->comm;
+   return R;
+}
+
 int Nfft4GPAmdDistNysSolve(void* dnys, int n, double* x, double* rhs)
 {
    DistNys* D = (DistNys*)dnys;

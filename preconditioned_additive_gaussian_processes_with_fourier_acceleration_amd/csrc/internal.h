@@ -245,8 +245,17 @@ int gemm_f64(bool transA, int M, int N, int K, const double* A, long long lda, c
              double* C, long long ldc, hipStream_t s);
 int sym_eig_host(const std::vector<double>& A, int n, std::vector<double>& w, std::vector<double>& V);
 int chol_inverse_host(std::vector<double>& A, int k);
+struct Comm;
+// a row shard of the Nystrom setup: this process holds rows [row_begin, row_begin + n) of n_global; the
+// Gram is all-reduced over comm and rank 0's k x k factors are broadcast (dist.hip)
+struct NysShard {
+   Comm* comm = nullptr;
+   int row_begin = 0, n_global = 0;
+};
+// xw_host: the gathered window buffer (n rows, or n_global with a shard); perm: at least k entries
 NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int skip_last, int kernel, double f,
-                           double l, double mu, const int* perm, int k, int k11_mode, bool with_grad = false);
+                           double l, double mu, const int* perm, int k, int k11_mode, bool with_grad = false,
+                           const NysShard* shard = nullptr);
 
 // multi-dimensional windows (nfft_md.hip).  xs[c] = component c's centred, scaled coordinates
 // (n_global x d column-major); the plan keeps rows [row_begin, row_end).
@@ -364,6 +373,7 @@ struct DistPcgInfo {
    bool fused_dot = false;
 };
 int dist_pcg_info(void* dop, DistPcgInfo& info);
+NysDev* nys_setup_shard(void* str, const int* perm, int k, int k11_mode, Comm* comm);  // nfft_api.cpp
 // q = A p with the local (q, p) in *d_dot (row shards; the caller all-reduces it)
 int dist_matvec_dot(void* dop, const double* d_p, double* d_q, double* d_dot);
 

@@ -872,6 +872,31 @@ void* Nfft4GPAmdNysSetupAdditive(void* str, const int* perm, int k, int k11_mode
                              kd->_params[1], kd->_noise_level, perm, k, k11_mode);
 }
 
+}  // extern "C"
+
+namespace nfft4gp_amd {
+// the row-sharded Nystrom setup of a row-shard handle (its gathered buffer holds all n_global rows): the
+// panel, U1 and U of its own rows, the Gram all-reduced over comm (dist.hip Nfft4GPAmdNysShardSetupAdditive)
+NysDev* nys_setup_shard(void* str, const int* perm, int k, int k11_mode, Comm* comm)
+{
+   nfft4gp_kernel* kd = (nfft4gp_kernel*)str;
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready || !perm || !comm) {
+      fprintf(stderr, "nfft4gp_amd: the sharded Nystrom setup needs a row-shard handle after its kernel setup\n");
+      return nullptr;
+   }
+   const AdditivePlan& P = E->P;
+   NysShard sh;
+   sh.comm = comm;
+   sh.row_begin = P.row_begin;
+   sh.n_global = P.n_global;
+   return nys_setup_additive(kd->_buffer, P.n, P.nw, P.dw, P.skip_last, P.kernel, kd->_params[0], kd->_params[1],
+                             kd->_noise_level, perm, k, k11_mode, false, &sh);
+}
+}  // namespace nfft4gp_amd
+
+extern "C" {
+
 int Nfft4GPAmdAdditiveComponentShard(void* str, int nw_global, int own_diag)
 {
    PlanExt* E = additive_plan(str);

@@ -41,10 +41,11 @@ namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// ---- panel: Kp[jj + ii*n] = (f^2/nw) sum_c kern(|x_c[rperm[jj]] - x_c[cperm[ii]]|), jj < n, ii < k -------
-// rperm = NULL: rows in natural order.  The reference's panel rows are perm-ordered (nys.c:566-567); a
-// natural-order panel gives the same U1^T U1 (a sum over rows) and lands U in natural row order
-// directly, so the final product needs no row scatter and the apply reads U as stored.
+// ---- panel: Kp[jj + ii*n] = (f^2/nw) sum_c kern(|xr_c[jj] - xc_c[ii]|), jj < n, ii < k ------------------
+// xr: the rows' window coordinates (n x D, column t of window w at t = w*dw + dd, ld n), xc: the landmarks'
+// (k x D, ld k).  The reference's panel rows are perm-ordered (nys.c:566-567); a natural-order panel gives
+// the same U1^T U1 (a sum over rows) and lands U in natural row order directly, so the final product needs
+// no row scatter and the apply reads U as stored.  A row shard passes its own rows as xr.
 constexpr int kPanelRows = 64, kPanelCols = 64, kPanelThreads = 256;
 constexpr int kPanelMaxDims = 128;  // window dimensions summed over all windows (nw * dw)
 
@@ -56,11 +57,10 @@ constexpr int kPanelMaxDims = 128;  // window dimensions summed over all windows
 // dK (kernels.c:3169 passes NULL for its dK), while its square no-permutation matrix (the K11 of
 // nys.c:569) keeps it (kernels.c:3398); grad_nw = nw - 1 reproduces the former.
 template <int KERNEL, bool GRAD>  // KERNEL 0 Gaussian exp(-r^2 / 2l^2), 1 Matern-1/2 exp(-r / l)
-__global__ __launch_bounds__(kPanelThreads) void k_nys_panel(const double* __restrict__ xw, int n, int nw, int dw,
-                                                             int last_dw, const int* __restrict__ rperm,
-                                                             const int* __restrict__ cperm, int k, double scale,
-                                                             double inv, double* __restrict__ Kp, int grad_nw,
-                                                             double df_scale, double dl_scale)
+__global__ __launch_bounds__(kPanelThreads) void k_nys_panel(const double* __restrict__ xr, int n, int nw, int dw,
+                                                             int last_dw, const double* __restrict__ xc, int k,
+                                                             double scale, double inv, double* __restrict__ Kp,
+                                                             int grad_nw, double df_scale, double dl_scale)
 {
    extern __shared__ double sm[];
    const int D = (nw - 1) * dw + last_dw;
@@ -71,8 +71,8 @@ __global__ __launch_bounds__(kPanelThreads) void k_nys_panel(const double* __res
       const int t = e / kPanelRows, i = e % kPanelRows;
       const int w = min(t / dw, nw - 1), dd = t - w * dw;  // window w, its dimension dd
       const size_t col = (size_t)w * dw + dd;               // windows packed at stride n*dw (kernels.c:3160)
-      s_r[e] = (r0 + i < n) ? xw[col * n + (rperm ? rperm[r0 + i] : r0 + i)] : 0.0;
-      s_c[e] = (c0 + i < k) ? xw[col * n + cperm[c0 + i]] : 0.0;
+      s_r[e] = (r0 + i < n) ? xr[col * n + r0 + i] : 0.0;
+      s_c[e] = (c0 + i < k) ? xc[col * k + c0 + i] : 0.0;
    }
    __syncthreads();
    // thread -> 4 rows x 4 columns, rows fastest so stores are coalesced per column
@@ -129,16 +129,16 @@ __global__ __launch_bounds__(kPanelThreads) void k_nys_panel(const double* __res
 }
 
 // launch the panel variant for (kernel, grad)
-void launch_panel(int kernel, bool grad, dim3 grid, size_t lds, hipStream_t s, const double* xw, int n, int nw, int dw,
-                  int last_dw, const int* rperm, const int* cperm, int k, double f, double l, double* Kp, int grad_nw)
+void launch_panel(int kernel, bool grad, dim3 grid, size_t lds, hipStream_t s, const double* xr, int n, int nw, int dw,
+                  int last_dw, const double* xc, int k, double f, double l, double* Kp, int grad_nw)
 {
    const double f2nw = f * f / nw;
    const double inv = (kernel == 0) ? 1.0 / (2.0 * l * l) : 1.0 / l;
    const double df_scale = 2.0 / f * f2nw;
    const double dl_scale = (kernel == 0) ? f2nw / (l * l * l) : f2nw / (l * l);
 #define NYS_PANEL(KK, GG)                                                                                        \
-   hipLaunchKernelGGL((k_nys_panel<KK, GG>), grid, dim3(kPanelThreads), lds, s, xw, n, nw, dw, last_dw, rperm, \
-                      cperm, k, f2nw, inv, Kp, grad_nw, df_scale, dl_scale)
+   hipLaunchKernelGGL((k_nys_panel<KK, GG>), grid, dim3(kPanelThreads), lds, s, xr, n, nw, dw, last_dw, xc, k, \
+                      f2nw, inv, Kp, grad_nw, df_scale, dl_scale)
    if (kernel == 0) {
       if (grad) NYS_PANEL(0, true); else NYS_PANEL(0, false);
    } else {
@@ -473,20 +473,6 @@ __global__ void k_nys_scale(const double* __restrict__ V, const double* __restri
    }
 }
 
-// K11[a + b k] = Kp[perm[a] + b n]
-__global__ void k_gather_rows(const double* __restrict__ Kp, long long n, const int* __restrict__ perm, int k,
-                              double* __restrict__ K11)
-{
-   const int a = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
-   if (a < k) K11[a + (size_t)b * k] = Kp[perm[a] + b * n];
-}
-
-__global__ void k_iota(int* p, int k)
-{
-   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-   if (i < k) p[i] = i;
-}
-
 // rocSOLVER (dpotrf / dtrtri / dsyevd) loaded on first use: with PyTorch in the process it binds to the
 // copy PyTorch already loaded (one ROCm runtime per process); without it, to /opt/rocm.  If it cannot be
 // loaded the k x k steps run on the host instead (NFFT4GP_AMD_NO_ROCSOLVER=1 forces that).
@@ -729,9 +715,21 @@ int gram_tn(int M, int N, int K, const double* A, long long lda, const double* B
 }
 
 // ------------------------------------------------------------------------------------------------
-NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int skip_last, int kernel, double f,
-                           double l, double mu, const int* perm, int k, int k11_mode, bool with_grad)
+// rank 0's count doubles at d on every rank (the others contribute zeros to the sum)
+static int bcast_root(Comm* comm, double* d, size_t count, hipStream_t s)
 {
+   if (comm->rank != 0) NFFT4GP_HIP_CHECK(hipMemsetAsync(d, 0, sizeof(double) * count, s));
+   return comm->allreduce(d, count, s);
+}
+
+NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int skip_last, int kernel, double f,
+                           double l, double mu, const int* perm, int k, int k11_mode, bool with_grad,
+                           const NysShard* shard)
+{
+   // the gathered buffer holds n_all rows per window column; this setup's rows are [rb, rb + n)
+   const int n_all = shard ? shard->n_global : n;
+   const int rb = shard ? shard->row_begin : 0;
+   Comm* comm = shard ? shard->comm : nullptr;
    const int last_dw = dw - skip_last;
    const int D = (nw - 1) * dw + last_dw;
    // NFFT4GP_AMD_VERBOSE=1: per-phase wall times on stderr
@@ -745,21 +743,22 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
               std::chrono::duration<double, std::milli>(now - tic).count());
       tic = now;
    };
-   if (k <= 0 || k > n || D > kPanelMaxDims || last_dw <= 0) {
-      fprintf(stderr, "nfft4gp_amd: Nystrom setup needs 0 < k <= n and <= %d window dimensions\n", kPanelMaxDims);
+   if (k <= 0 || k > n_all || D > kPanelMaxDims || last_dw <= 0 || (shard && (with_grad || !comm))) {
+      fprintf(stderr, "nfft4gp_amd: Nystrom setup needs 0 < k <= n, <= %d window dimensions (and no gradients on "
+                      "row shards)\n", kPanelMaxDims);
       return nullptr;
    }
    hipStream_t s = current_stream();
    const int nblk = with_grad ? 3 : 1;  // panel blocks: K (and dK/df, dK/dl)
-   double *d_xw = nullptr, *d_Kp = nullptr, *d_U1 = nullptr, *d_B = nullptr, *d_AA = nullptr;
+   double *d_xw = nullptr, *d_xk = nullptr, *d_x11 = nullptr, *d_Kp = nullptr, *d_U1 = nullptr, *d_B = nullptr, *d_AA = nullptr;
    double *d_K11 = nullptr, *d_w1 = nullptr, *d_e = nullptr, *d_s = nullptr, *d_T = nullptr;
-   int *d_perm = nullptr, *d_iota = nullptr, *d_info = nullptr;
+   int* d_info = nullptr;
    NysDev* N = new NysDev();
    N->n = n;
    N->k = k;
    auto release = [&]() {
-      for (double* p : {d_xw, d_Kp, d_U1, d_B, d_AA, d_K11, d_w1, d_e, d_s, d_T}) (void)hipFree(p);
-      for (int* p : {d_perm, d_iota, d_info}) (void)hipFree(p);
+      for (double* p : {d_xw, d_xk, d_x11, d_Kp, d_U1, d_B, d_AA, d_K11, d_w1, d_e, d_s, d_T}) (void)hipFree(p);
+      (void)hipFree(d_info);
    };
    auto fail = [&](const char* what) -> NysDev* {
       if (what) fprintf(stderr, "nfft4gp_amd: Nystrom setup: %s\n", what);
@@ -779,12 +778,28 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
       }
    } ev_guard{ev};
    const size_t nk = (size_t)n * k, kk = (size_t)k * k;
-   if (dalloc(&d_xw, (size_t)n * nw * dw) || dalloc(&d_perm, (size_t)n) || dalloc(&d_info, 1) ||
+   if (dalloc(&d_xw, (size_t)n * D) || dalloc(&d_xk, (size_t)k * D) || dalloc(&d_x11, (size_t)k * D) ||
+       dalloc(&d_info, 1) ||
        dalloc(&d_Kp, nk * nblk) || dalloc(&d_U1, nk) || dalloc(&d_B, kk) || dalloc(&d_AA, kk))
       return fail("allocation");
-   if (hipMemcpy(d_xw, xw_host, sizeof(double) * (size_t)n * ((nw - 1) * dw + last_dw), hipMemcpyHostToDevice) ||
-       hipMemcpy(d_perm, perm, sizeof(int) * (size_t)n, hipMemcpyHostToDevice))
-      return fail("upload");
+   // this setup's rows (n x D, ld n), the landmarks perm[:k] (k x D, ld k) and the K11 points: the
+   // landmarks (mode 1), or the reference's K11 rows (mode 0: nys.c:569 hands the k x d sub-data to
+   // Nfft4GPKernelAdditiveKernel, which ignores it and reads window i of its own gathered buffer at offset
+   // i*n*dwindows with n = k, kernels.c:3160 -- the columns of a buffer of k rows: column t of that buffer
+   // starts at t*k of ours)
+   {
+      std::vector<double> xk((size_t)k * D), x11((size_t)k * D);
+      for (int t = 0; t < D; t++)
+         for (int a = 0; a < k; a++) {
+            xk[(size_t)t * k + a] = xw_host[(size_t)t * n_all + perm[a]];
+            x11[(size_t)t * k + a] = k11_mode == 1 ? xk[(size_t)t * k + a] : xw_host[(size_t)t * k + a];
+         }
+      if ((n > 0 && hipMemcpy2D(d_xw, sizeof(double) * n, xw_host + rb, sizeof(double) * n_all, sizeof(double) * n, D,
+                                hipMemcpyHostToDevice)) ||
+          hipMemcpy(d_xk, xk.data(), sizeof(double) * xk.size(), hipMemcpyHostToDevice) ||
+          hipMemcpy(d_x11, x11.data(), sizeof(double) * x11.size(), hipMemcpyHostToDevice))
+         return fail("upload");
+   }
 
    // 1. panel K(perm, perm[:k]) (noise-free, nys.c:566-567 / kernels.c "when have permc"), rows in natural
    //    order; with gradients also dK/df and dK/dl (nys.c:597-601)
@@ -793,25 +808,20 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    const size_t lds = sizeof(double) * (size_t)D * (kPanelRows + kPanelCols);
    dim3 pgrid((n + kPanelRows - 1) / kPanelRows, (k + kPanelCols - 1) / kPanelCols);
    (void)hipEventRecord(ev[0], s);
-   launch_panel(kernel, with_grad, pgrid, lds, s, d_xw, n, nw, dw, last_dw, nullptr, d_perm, k, f, l, d_Kp,
-                nw_grad_panel);
+   if (n > 0)
+      launch_panel(kernel, with_grad, pgrid, lds, s, d_xw, n, nw, dw, last_dw, d_xk, k, f, l, d_Kp, nw_grad_panel);
    if (hipGetLastError() != hipSuccess) return fail("panel launch");
    (void)hipEventRecord(ev[1], s);
 
    phase("panel");
-   // 2. K11 (and dK11) on the device: the landmark rows of the panel (mode 1), or the reference's K11
-   //    (mode 0: nys.c:569 hands the k x d sub-data to Nfft4GPKernelAdditiveKernel, which ignores it and
-   //    reads window i of its own gathered buffer at offset i*n*dwindows with n = k, kernels.c:3160 --
-   //    the panel kernel over that buffer with n = k and the identity permutation)
-   if (dalloc(&d_K11, kk * nblk) || dalloc(&d_iota, (size_t)k)) return fail("allocation");
-   if (k11_mode == 1) {
-      for (int b = 0; b < nblk; b++)
-         hipLaunchKernelGGL(k_gather_rows, dim3((k + 255) / 256, k), dim3(256), 0, s, d_Kp + b * nk, (long long)n,
-                            d_perm, k, d_K11 + b * kk);
-   } else {
-      hipLaunchKernelGGL(k_iota, dim3((k + 255) / 256), dim3(256), 0, s, d_iota, k);
+   // 2. K11 (and dK11) on the device: the panel kernel on the K11 points against themselves (mode 1: the
+   //    landmark rows of the whole panel, entry for entry the same arithmetic; mode 0: the reference's
+   //    buffer rows, all windows in dK11, kernels.c:3398)
+   if (dalloc(&d_K11, kk * nblk)) return fail("allocation");
+   {
       dim3 kgrid((k + kPanelRows - 1) / kPanelRows, (k + kPanelCols - 1) / kPanelCols);
-      launch_panel(kernel, with_grad, kgrid, lds, s, d_xw, k, nw, dw, last_dw, nullptr, d_iota, k, f, l, d_K11, nw);
+      launch_panel(kernel, with_grad, kgrid, lds, s, d_x11, k, nw, dw, last_dw, d_x11, k, f, l, d_K11,
+                   k11_mode == 1 ? nw_grad_panel : nw);
    }
    // stable shift nu = sqrt(k) ulp(|K11|_F) (chol.c:449-465; dlansy 'F' 'L' = the full-matrix norm)
    std::vector<double> K11(kk);
@@ -834,6 +844,8 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
          return fail(nullptr);
       }
       if (info < 0) return fail("Cholesky / triangular inverse of K11");
+      // every row shard multiplies its rows by rank 0's factor (bitwise the same U1 rows as one GPU's)
+      if (comm && bcast_root(comm, d_B, kk, s)) return fail("broadcast of L^{-T}");
    }
    if (with_grad) {
       // GdKG_g = L^{-1} dK11_g L^{-T} for g = f, l (chol.c:512-523)
@@ -850,13 +862,16 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    phase("k11+chol");
    // 3. U1 = Kp G^T  (dtrmm 'R' 'L' 'T', matops.c Nfft4GPTrilNystromMm)
    (void)hipEventRecord(ev[2], s);
-   if (gemm(false, n, k, k, d_Kp, n, d_B, k, d_U1, n, s)) return fail("gemm");
+   if (n > 0 && gemm(false, n, k, k, d_Kp, n, d_B, k, d_U1, n, s)) return fail("gemm");
    (void)hipEventRecord(ev[3], s);
 
    phase("gemm1");
    // 4. AA = U1^T U1, split over rows (fixed-order sum, deterministic); with gradients D = AA is kept
    (void)hipEventRecord(ev[4], s);
-   if (gram_tn(k, k, n, d_U1, n, d_U1, n, d_AA, 1, s)) return fail("gram");
+   if (n > 0 && gram_tn(k, k, n, d_U1, n, d_U1, n, d_AA, 1, s)) return fail("gram");
+   if (n == 0 && hipMemsetAsync(d_AA, 0, sizeof(double) * kk, s) != hipSuccess) return fail("gram");
+   // the Gram is a sum over rows (matops.c:65-137): the row shards' partial Grams add up to the whole one
+   if (comm && comm->allreduce(d_AA, kk, s)) return fail("all-reduce of the Gram");
    (void)hipEventRecord(ev[5], s);
    if (with_grad) {
       if (dalloc(&N->D, kk) ||
@@ -890,6 +905,9 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
    }
    hipLaunchKernelGGL(k_nys_scale, dim3((k + 255) / 256, k), dim3(256), 0, s, d_AA, d_w1, k, eta, d_B, d_s,
                       k11_mode == 1 ? 1 : 0);
+   // one eigenbasis for all row shards: rank 0's (an eigensolver may differ in signs or rounding elsewhere)
+   if (comm && (bcast_root(comm, d_B, kk, s) || bcast_root(comm, d_s, (size_t)k, s)))
+      return fail("broadcast of the eigenbasis");
    phase("eig");
    // 6. U = U1 W.  Without gradients the panel's storage is reused for U; with them the panel (K, dK/df,
    //    dK/dl) and U1 (= dU, nys.c:611-615) stay, for Dvp and Trace.
@@ -900,7 +918,7 @@ NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int ski
       d_Kp = nullptr;
    }
    (void)hipEventRecord(ev[6], s);
-   if (gemm(false, n, k, k, d_U1, n, d_B, k, N->U, n, s)) return fail("gemm");
+   if (n > 0 && gemm(false, n, k, k, d_U1, n, d_B, k, N->U, n, s)) return fail("gemm");
    (void)hipEventRecord(ev[7], s);
    N->eta = eta;
    N->s = d_s;

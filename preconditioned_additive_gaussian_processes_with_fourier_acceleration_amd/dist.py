@@ -215,6 +215,24 @@ class RowShardedNystrom:
         if not self.h:
             raise RuntimeError("Nfft4GPAmdNysShard failed")
 
+    @classmethod
+    def setup(cls, op: "DistributedAdditiveKernel", perm, k: int, k11: str = "landmarks"):
+        """The setup itself split over the rows (Nfft4GPAmdNysShardSetupAdditive, nys.c:518-660): every rank
+        forms the panel of its own rows and its partial Gram, one k x k all-reduce sums the Gram, and no
+        rank holds more than its rows of U.  ``op``: a row-partitioned operator after its kernel setup;
+        ``perm``: the global landmark order (its first k entries), the same on every rank."""
+        from . import _lib
+        if op.partition != "rows":
+            raise ValueError("the sharded Nystrom setup splits rows: use a partition='rows' operator")
+        self = cls.__new__(cls)
+        self.n, self.k, self.comm = op.n, int(k), op.comm
+        p = np.ascontiguousarray(np.asarray(perm, dtype=np.int32))
+        self.h = _lib.lib().Nfft4GPAmdNysShardSetupAdditive(op.h, p.ctypes.data, int(k),
+                                                            {"reference": 0, "landmarks": 1}[k11])
+        if not self.h:
+            raise RuntimeError("Nfft4GPAmdNysShardSetupAdditive failed (see stderr)")
+        return self
+
     def solve(self, x, rhs):
         from . import _lib
         from .nfft import _check_len, _ptr

@@ -84,6 +84,14 @@ def _worker(rank, world, port, outdir, backend):
                 r = torch.tensor(np.random.default_rng(6).random(n)[rb:re], device="cuda")
                 z = torch.zeros_like(r)
                 dn.solve(z, r)
+                # the setup itself split over the rows (one k x k all-reduce of the Gram)
+                ds = RowShardedNystrom.setup(op, perm, 64, k11="landmarks")
+                zs = torch.zeros_like(r)
+                ds.solve(zs, r)
+                xs3 = torch.zeros_like(b)
+                _, _, _, it3 = amd.pcg(op, b, xs3, maxits=2000, tol=1e-6, precond=ds)
+                out.update({"nys_shard_z": zs.cpu().numpy(), "nys_shard_x": xs3.cpu().numpy(), "nys_shard_it": it3})
+                ds.free()
                 xs2 = torch.zeros_like(b)
                 _, rr2, _, it2 = amd.pcg(op, b, xs2, maxits=2000, tol=1e-6, precond=dn)
                 out.update({"nys_z": z.cpu().numpy(), "nys_x": xs2.cpu().numpy(), "nys_rr": rr2, "nys_it": it2})
@@ -195,6 +203,18 @@ def test_distributed_pcg_matches_single_gpu(gloo2, single, kind, part):
     # LDS-atomic accumulation order moves CG's count by a few iterations run to run
     assert abs(it - it1) <= max(3, it1 // 20), (it, it1)
     assert rel(gather(gloo2, key + "_x", part), single[kind + "_x"]) < 1e-4
+
+
+def test_row_sharded_nystrom_setup(gloo2, single):
+    """Nfft4GPAmdNysShardSetupAdditive: panel, U1 and U per row shard, the Gram summed
+    with one k x k all-reduce; the apply equals the one-GPU setup's (the Gram's sum is regrouped, so its
+    eigenbasis moves at rounding level) and PCG with it takes the one-GPU iteration count."""
+    z = np.concatenate([r["nys_shard_z"] for r in gloo2])
+    assert rel(z, single["nys_z"]) < 1e-9
+    its = [int(r["nys_shard_it"]) for r in gloo2]
+    assert len(set(its)) == 1 and its[0] > 0
+    assert abs(its[0] - int(single["nys_it"])) <= max(3, int(single["nys_it"]) // 20), (its, single["nys_it"])
+    assert rel(np.concatenate([r["nys_shard_x"] for r in gloo2]), single["nys_x"]) < 1e-4
 
 
 def test_row_sharded_nystrom_apply_and_pcg(gloo2, single):
