@@ -551,6 +551,15 @@ void *Nfft4GPAmdNysShard(void *nys, int row_begin, int row_end, void *comm);
 void *Nfft4GPAmdNysShardSetupAdditive(void *dop, const int *perm, int k, int k11_mode);
 int Nfft4GPAmdDistNysSolve(void *dnys, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
 void Nfft4GPAmdDistNysFree(void *dnys);
+/* Row-sharded AFN apply (afn.c:82-143 over row shards): from an AFN apply handle (Nfft4GPAmdAfnCreate /
+ * Nfft4GPAmdAfnSetup*, or the AFN of Nfft4GPAmdPrecondAFNInfo; 0 < k < n), this rank keeps the points of
+ * rows [row_begin, row_end): its landmarks, the K12 columns of its Schur-complement points (k x ~(n-k)/N)
+ * and their rows of the Schur FSAI G and of G^T.  An apply exchanges the rhs's landmark entries and the
+ * K12 y2 partial sums (two k all-reduces) and, with the Schur FSAI, the Schur vector before each sparse
+ * product (two (n-k) all-reduces of zero-padded vectors).  func_solve on this rank's rows (device). */
+void *Nfft4GPAmdAfnShard(void *afn, int row_begin, int row_end, void *comm);
+int Nfft4GPAmdDistAfnSolve(void *dafn, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
+void Nfft4GPAmdDistAfnFree(void *dafn);
 
 /* ---- host-only helpers (no GPU needed): the setup math of the device plan, exported so the CPU
  * test-suite can check it and emulate the kernels against the oracle ------------------------------- */

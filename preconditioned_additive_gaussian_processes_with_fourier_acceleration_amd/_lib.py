@@ -176,6 +176,9 @@ _SIGS = {
                                               vp]),
     "Nfft4GPAmdNysShard": (vp, [vp, C.c_int, C.c_int, vp]),
     "Nfft4GPAmdNysShardSetupAdditive": (vp, [vp, vp, C.c_int, C.c_int]),
+    "Nfft4GPAmdAfnShard": (vp, [vp, C.c_int, C.c_int, vp]),
+    "Nfft4GPAmdDistAfnSolve": (C.c_int, [vp, C.c_int, vp, vp]),
+    "Nfft4GPAmdDistAfnFree": (None, [vp]),
     "Nfft4GPAmdDistNysSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdDistNysFree": (None, [vp]),
     "Nfft4GPAmdHostTapPoly": (C.c_int, [vp]),

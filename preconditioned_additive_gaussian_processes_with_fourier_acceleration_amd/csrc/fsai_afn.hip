@@ -331,6 +331,236 @@ int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
    return 0;
 }
 
+// ---- the AFN apply split over row shards (afn.c:82-143 with the rows of the operator's shards) ----------
+// Each rank keeps, for the points of its own rows [rb, re): which of them are landmarks (their index in
+// perm[:k]) and which are Schur points (their position in perm[k:]), the K12 columns of its Schur points,
+// and the rows of the Schur FSAI G and of G^T that belong to its Schur points (sub-CSRs with global column
+// indices).  The k x k factors are replicated.  An apply exchanges: the landmark entries of the rhs (one
+// k all-reduce), the K12 y2 partial sums (one k all-reduce) and -- with the Schur FSAI -- the Schur vector
+// before each of the two sparse products (an all-gather, as an n2 all-reduce of a zero-padded vector).
+struct AfnShard {
+   int n = 0, k = 0, n2 = 0, m1 = 0, m2 = 0;
+   Comm* comm = nullptr;
+   int *lm_idx = nullptr, *lm_row = nullptr;  // m1: landmark index a in [0, k), local row
+   int *nl_pos = nullptr, *nl_row = nullptr;  // m2: Schur position p in [0, n2), local row
+   double *Linv = nullptr, *LinvT = nullptr, *K12 = nullptr;  // k x k, k x k, k x m2
+   FsaiDev G, GT;  // rows of G / G^T at this rank's Schur points (ia, ja, aa, part; ja global)
+   bool fsai = false;
+   double schur_scale = 0.0;
+   double *rp1 = nullptr, *y1 = nullptr, *t = nullptr, *w = nullptr;  // k
+   double *rp2 = nullptr, *y2 = nullptr, *v = nullptr;                 // m2
+   double *gbuf = nullptr;                                              // n2
+   double* part = nullptr;
+   int nblk = 0, cols = 1;
+};
+
+__global__ void k_take(const double* __restrict__ src, const int* __restrict__ idx, int m, double* __restrict__ dst)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < m) dst[i] = src[idx[i]];
+}
+
+__global__ void k_put(const double* __restrict__ src, const int* __restrict__ idx, int m, double* __restrict__ dst)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < m) dst[idx[i]] = src[i];
+}
+
+// dst[idx_dst[i]] = src[idx_src[i]]
+__global__ void k_move(const double* __restrict__ src, const int* __restrict__ idx_src, const int* __restrict__ idx_dst,
+                       int m, double* __restrict__ dst)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < m) dst[idx_dst[i]] = src[idx_src[i]];
+}
+
+__global__ void k_add_into(double* __restrict__ y, const double* __restrict__ w, int k)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < k) y[i] += w[i];
+}
+
+// out[:, i] = K12[:, cols[i]] (k x n2 column-major -> k x m)
+__global__ void k_take_cols(const double* __restrict__ K12, int k, const int* __restrict__ cols, int m,
+                            double* __restrict__ out)
+{
+   const int i = blockIdx.y;
+   const double* src = K12 + (size_t)cols[i] * k;
+   double* dst = out + (size_t)i * k;
+   for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < k; r += gridDim.x * blockDim.x) dst[r] = src[r];
+}
+
+void csr_free_parts(FsaiDev& F)
+{
+   for (void* p : {(void*)F.ia, (void*)F.ja, (void*)F.aa, (void*)F.part}) (void)hipFree(p);
+   F = FsaiDev();
+}
+
+// rows `rows` of a host CSR (ia, ja, aa) as a device CSR with its workgroup spans
+int csr_rows_upload(const std::vector<int>& ia, const std::vector<int>& ja, const std::vector<double>& aa,
+                    const std::vector<int>& rows, FsaiDev& F)
+{
+   std::vector<int> sia(rows.size() + 1, 0), sja;
+   std::vector<double> saa;
+   for (size_t i = 0; i < rows.size(); i++) {
+      for (int j = ia[rows[i]]; j < ia[rows[i] + 1]; j++) {
+         sja.push_back(ja[j]);
+         saa.push_back(aa[j]);
+      }
+      sia[i + 1] = (int)sja.size();
+   }
+   F.n = (int)rows.size();
+   const std::vector<int> p = csr_partition(F.n, sia.data());
+   F.nparts = (int)p.size() - 1;
+   if (up(&F.ia, sia.data(), sia.size()) || up(&F.ja, sja.data(), sja.size()) || up(&F.aa, saa.data(), saa.size()) ||
+       up(&F.part, p.data(), p.size()))
+      return -1;
+   return 0;
+}
+
+void afn_shard_free(AfnShard* S)
+{
+   if (!S) return;
+   (void)hipStreamSynchronize(current_stream());
+   for (void* p : {(void*)S->lm_idx, (void*)S->lm_row, (void*)S->nl_pos, (void*)S->nl_row, (void*)S->Linv,
+                   (void*)S->LinvT, (void*)S->K12, (void*)S->rp1, (void*)S->y1, (void*)S->t, (void*)S->w,
+                   (void*)S->rp2, (void*)S->y2, (void*)S->v, (void*)S->gbuf, (void*)S->part})
+      (void)hipFree(p);
+   csr_free_parts(S->G);
+   csr_free_parts(S->GT);
+   delete S;
+}
+
+template <class T>
+int dl(std::vector<T>& h, const T* d, size_t count)
+{
+   h.resize(count);
+   if (count) NFFT4GP_HIP_CHECK(hipMemcpy(h.data(), d, sizeof(T) * count, hipMemcpyDeviceToHost));
+   return 0;
+}
+
+AfnShard* afn_shard_create(const AfnDev* A, int rb, int re, Comm* comm)
+{
+   const int n = A->n, k = A->k, n2 = A->n2;
+   if (k <= 0 || n2 <= 0 || rb < 0 || re > n || rb > re) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShard needs 0 < k < n and rows within [0, %d)\n", n);
+      return nullptr;
+   }
+   std::vector<int> perm;
+   if (dl(perm, A->perm, (size_t)n)) return nullptr;
+   AfnShard* S = new AfnShard();
+   S->n = re - rb;
+   S->k = k;
+   S->n2 = n2;
+   S->comm = comm;
+   S->fsai = A->S != nullptr;
+   S->schur_scale = A->schur_scale;
+   std::vector<int> lm_idx, lm_row, nl_pos, nl_row;
+   for (int p = 0; p < n; p++) {
+      const int row = perm[p];
+      if (row < rb || row >= re) continue;
+      if (p < k) {
+         lm_idx.push_back(p);
+         lm_row.push_back(row - rb);
+      } else {
+         nl_pos.push_back(p - k);
+         nl_row.push_back(row - rb);
+      }
+   }
+   S->m1 = (int)lm_idx.size();
+   S->m2 = (int)nl_pos.size();
+   a12_shape(std::max(1, S->m2), S->cols, S->nblk);
+   hipStream_t s = current_stream();
+   const size_t kk = (size_t)k * k;
+   bool ok = !up(&S->lm_idx, lm_idx.data(), lm_idx.size()) && !up(&S->lm_row, lm_row.data(), lm_row.size()) &&
+             !up(&S->nl_pos, nl_pos.data(), nl_pos.size()) && !up(&S->nl_row, nl_row.data(), nl_row.size());
+   for (double** p : {&S->Linv, &S->LinvT})
+      ok = ok && hipMalloc((void**)p, sizeof(double) * kk) == hipSuccess;
+   ok = ok && hipMalloc((void**)&S->K12, sizeof(double) * std::max<size_t>(1, (size_t)k * S->m2)) == hipSuccess;
+   for (double** p : {&S->rp1, &S->y1, &S->t, &S->w})
+      ok = ok && hipMalloc((void**)p, sizeof(double) * k) == hipSuccess;
+   for (double** p : {&S->rp2, &S->y2, &S->v})
+      ok = ok && hipMalloc((void**)p, sizeof(double) * std::max(1, S->m2)) == hipSuccess;
+   ok = ok && hipMalloc((void**)&S->gbuf, sizeof(double) * n2) == hipSuccess &&
+        hipMalloc((void**)&S->part, sizeof(double) * (size_t)S->nblk * k) == hipSuccess;
+   ok = ok && hipMemcpyAsync(S->Linv, A->Linv, sizeof(double) * kk, hipMemcpyDeviceToDevice, s) == hipSuccess &&
+        hipMemcpyAsync(S->LinvT, A->LinvT, sizeof(double) * kk, hipMemcpyDeviceToDevice, s) == hipSuccess;
+   if (ok && S->m2 > 0) {
+      hipLaunchKernelGGL(k_take_cols, dim3((k + 255) / 256, S->m2), dim3(256), 0, s, (const double*)A->K12, k,
+                         (const int*)S->nl_pos, S->m2, S->K12);
+      ok = hipGetLastError() == hipSuccess;
+   }
+   if (ok && S->fsai) {
+      const FsaiDev* F = A->S;
+      std::vector<int> ia, ja, tia, tja;
+      std::vector<double> aa, taa;
+      ok = !dl(ia, F->ia, (size_t)n2 + 1) && !dl(tia, F->tia, (size_t)n2 + 1);
+      ok = ok && !dl(ja, F->ja, (size_t)ia[n2]) && !dl(aa, F->aa, (size_t)ia[n2]) && !dl(tja, F->tja, (size_t)tia[n2]) &&
+           !dl(taa, F->taa, (size_t)tia[n2]);
+      ok = ok && !csr_rows_upload(ia, ja, aa, nl_pos, S->G) && !csr_rows_upload(tia, tja, taa, nl_pos, S->GT);
+   }
+   if (!ok || hipStreamSynchronize(s) != hipSuccess) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShard: allocation or copy failed\n");
+      afn_shard_free(S);
+      return nullptr;
+   }
+   return S;
+}
+
+int afn_shard_apply(AfnShard* S, double* x, const double* r, hipStream_t s)
+{
+   const int k = S->k, m1 = S->m1, m2 = S->m2;
+   const int gk = (k + 3) / 4, g1 = (m1 + 255) / 256 + 1, g2 = (m2 + 255) / 256 + 1;
+   // [rp1; rp2] = r(perm): the landmark entries are spread over the ranks (one owner each)
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(S->rp1, 0, sizeof(double) * k, s));
+   hipLaunchKernelGGL(k_move, dim3(g1), dim3(256), 0, s, r, (const int*)S->lm_row, (const int*)S->lm_idx, m1, S->rp1);
+   if (S->comm->allreduce(S->rp1, (size_t)k, s)) return -1;
+   hipLaunchKernelGGL(k_take, dim3(g2), dim3(256), 0, s, r, (const int*)S->nl_row, m2, S->rp2);
+   // y1 = A11 \ rp1
+   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, S->LinvT, k, S->rp1, S->t);
+   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, S->Linv, k, S->t, S->y1);
+   // rp2 -= A12^T y1 on this rank's columns
+   if (m2 > 0) {
+      const dim3 ga((m2 + 4 * kA12tCols - 1) / (4 * kA12tCols));
+      if (k <= kA12tLdsMax)
+         hipLaunchKernelGGL(k_a12t<true>, ga, dim3(256), sizeof(double) * k, s, S->K12, k, m2, S->y1, S->rp2);
+      else
+         hipLaunchKernelGGL(k_a12t<false>, ga, dim3(256), 0, s, S->K12, k, m2, S->y1, S->rp2);
+   }
+   // y2 = G^T G rp2 (each product reads the whole Schur vector: all-gathered), or rp2 / noise
+   if (S->fsai) {
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(S->gbuf, 0, sizeof(double) * S->n2, s));
+      hipLaunchKernelGGL(k_put, dim3(g2), dim3(256), 0, s, S->rp2, (const int*)S->nl_pos, m2, S->gbuf);
+      if (S->comm->allreduce(S->gbuf, (size_t)S->n2, s)) return -1;
+      if (m2 > 0)
+         hipLaunchKernelGGL(k_csr_staged, dim3(S->G.nparts), dim3(kCsrT), 0, s, S->G.ia, S->G.ja, S->G.aa, S->gbuf,
+                            S->v, S->G.part);
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(S->gbuf, 0, sizeof(double) * S->n2, s));
+      hipLaunchKernelGGL(k_put, dim3(g2), dim3(256), 0, s, S->v, (const int*)S->nl_pos, m2, S->gbuf);
+      if (S->comm->allreduce(S->gbuf, (size_t)S->n2, s)) return -1;
+      if (m2 > 0)
+         hipLaunchKernelGGL(k_csr_staged, dim3(S->GT.nparts), dim3(kCsrT), 0, s, S->GT.ia, S->GT.ja, S->GT.aa,
+                            S->gbuf, S->y2, S->GT.part);
+   } else if (m2 > 0) {
+      hipLaunchKernelGGL(k_scale_into, dim3(g2), dim3(256), 0, s, S->rp2, m2, S->schur_scale, S->y2);
+   }
+   // rp1 -= A12 y2: this rank's columns' partial sum (negated by k_a12_reduce), summed over the ranks
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(S->w, 0, sizeof(double) * k, s));
+   if (m2 > 0) {
+      hipLaunchKernelGGL(k_a12_part, dim3(S->nblk), dim3(256), 0, s, S->K12, k, m2, S->cols, S->y2, S->part);
+      hipLaunchKernelGGL(k_a12_reduce, dim3((k + 15) / 16), dim3(1024), 0, s, S->part, S->nblk, k, S->w);
+   }
+   if (S->comm->allreduce(S->w, (size_t)k, s)) return -1;
+   hipLaunchKernelGGL(k_add_into, dim3((k + 255) / 256), dim3(256), 0, s, S->rp1, S->w, k);
+   // y1 = A11 \ rp1, then x(perm) = [y1; y2] on this rank's rows
+   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, S->LinvT, k, S->rp1, S->t);
+   hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, S->Linv, k, S->t, S->y1);
+   hipLaunchKernelGGL(k_move, dim3(g1), dim3(256), 0, s, S->y1, (const int*)S->lm_idx, (const int*)S->lm_row, m1, x);
+   hipLaunchKernelGGL(k_put, dim3(g2), dim3(256), 0, s, S->y2, (const int*)S->nl_row, m2, x);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
 }  // namespace
 
 // an AFN apply object from factors already in HBM (afn_setup.hip); takes ownership of d_perm, d_Linv,
@@ -450,6 +680,28 @@ void Nfft4GPAmdAfnFree(void* afn)
    if (A->own_S) fsai_free(A->S);
    delete A;
 }
+
+void* Nfft4GPAmdAfnShard(void* afn, int row_begin, int row_end, void* comm)
+{
+   if (!afn || !comm) return nullptr;
+   return afn_shard_create((const AfnDev*)afn, row_begin, row_end, (Comm*)comm);
+}
+
+int Nfft4GPAmdDistAfnSolve(void* dafn, int n, double* x, double* rhs)
+{
+   AfnShard* S = (AfnShard*)dafn;
+   if (!S || n != S->n) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdDistAfnSolve: size %d, this rank holds %d rows\n", n, S ? S->n : -1);
+      return -1;
+   }
+   if (n > 0 && (!is_device_ptr(x) || !is_device_ptr(rhs))) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdDistAfnSolve takes device vectors\n");
+      return -1;
+   }
+   return afn_shard_apply(S, x, rhs, current_stream());
+}
+
+void Nfft4GPAmdDistAfnFree(void* dafn) { afn_shard_free((AfnShard*)dafn); }
 
 int Nfft4GPAmdAfnInfo(void* afn, int* k, int* perm, int* ia, int* ja, double* aa)
 {

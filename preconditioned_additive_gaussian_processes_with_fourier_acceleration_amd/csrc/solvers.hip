@@ -979,6 +979,7 @@ bool library_operator(const void* fn)
           fn == (const void*)&Nfft4GPAmdPrecondNysDvp || fn == (const void*)&Nfft4GPAmdPrecondFsaiSolve ||
           fn == (const void*)&Nfft4GPAmdPrecondFsaiDvp || fn == (const void*)&Nfft4GPAmdDistMatSymv ||
           fn == (const void*)&Nfft4GPAmdDistGradMatSymv || fn == (const void*)&Nfft4GPAmdDistNysSolve ||
+          fn == (const void*)&Nfft4GPAmdDistAfnSolve ||
           fn == (const void*)&Nfft4GPAmdPrecondAFNSolve || fn == (const void*)&Nfft4GPAmdPrecondAFNDvp;
 }
 }  // namespace nfft4gp_amd

@@ -260,6 +260,55 @@ class RowShardedNystrom:
             pass
 
 
+class RowShardedAfn:
+    """Rows [row_begin, row_end) of an AFN apply (Nfft4GPAmdAfnShard, afn.c:82-143 over row shards): this rank's
+    landmarks, the K12 columns of its Schur points and their rows of the Schur FSAI; an apply exchanges two
+    k-vectors (and, with the Schur FSAI, the Schur vector before each sparse product).  ``afn``: an
+    AfnPrecond, or a PrecondAFN whose estimate built the AFN itself."""
+
+    def __init__(self, afn, row_begin: int, row_end: int, comm: Communicator):
+        import ctypes as C
+        from . import _lib
+        L = _lib.lib()
+        h = afn.h
+        if hasattr(afn, "KINDS"):  # a PrecondAFN: its AFN apply object, if that is what it built
+            a = C.c_void_p()
+            L.Nfft4GPAmdPrecondAFNInfo(afn.h, None, None, C.byref(a), None)
+            if not a.value:
+                raise ValueError(f"the PrecondAFN built a {afn.kind}, not an AFN")
+            h = a.value
+        self.n, self.comm = row_end - row_begin, comm
+        self.h = L.Nfft4GPAmdAfnShard(h, int(row_begin), int(row_end), comm.h)
+        if not self.h:
+            raise RuntimeError("Nfft4GPAmdAfnShard failed (see stderr)")
+
+    def solve(self, x, rhs):
+        from . import _lib
+        from .nfft import _check_len, _ptr
+        _check_len("x", x, self.n)
+        _check_len("rhs", rhs, self.n)
+        if _lib.lib().Nfft4GPAmdDistAfnSolve(self.h, self.n, _ptr(x)[0], _ptr(rhs)[0]) != 0:
+            raise RuntimeError("Nfft4GPAmdDistAfnSolve failed")
+        return x
+
+    @property
+    def solve_fnptr(self) -> int:
+        from . import _lib
+        return _lib.fnptr("Nfft4GPAmdDistAfnSolve")
+
+    def free(self):
+        from . import _lib
+        if getattr(self, "h", None):
+            _lib.lib().Nfft4GPAmdDistAfnFree(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class GpuVecOps:
     """BLAS-1 on device tensors through this library's HIP kernels (Nfft4GPVec*, vecops.c:3-155)."""
 

@@ -50,7 +50,7 @@ def _worker(rank, world, port, outdir, backend):
     import torch.distributed as dist
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
     from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import (
-        Communicator, DistributedAdditiveKernel, RowShardedNystrom)
+        Communicator, DistributedAdditiveKernel, RowShardedAfn, RowShardedNystrom)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = Communicator.rccl() if backend == "rccl" else Communicator.callback()
@@ -92,6 +92,19 @@ def _worker(rank, world, port, outdir, backend):
                 _, _, _, it3 = amd.pcg(op, b, xs3, maxits=2000, tol=1e-6, precond=ds)
                 out.update({"nys_shard_z": zs.cpu().numpy(), "nys_shard_x": xs3.cpu().numpy(), "nys_shard_it": it3})
                 ds.free()
+                # the AFN apply split over the rows (both Schur solves), from a full setup on every rank
+                for schur in ("fsai", "noise"):
+                    afn = amd.AfnPrecond.setup(X, 64, 0, 0, 0, perm_opt="perm", perm=perm, schur_lfil=10, op=full,
+                                               schur=schur)
+                    da = RowShardedAfn(afn, rb, re, comm)
+                    za = torch.zeros_like(r)
+                    da.solve(za, r)
+                    xs4 = torch.zeros_like(b)
+                    _, _, _, it4 = amd.pcg(op, b, xs4, maxits=2000, tol=1e-6, precond=da)
+                    out.update({f"afn_{schur}_z": za.cpu().numpy(), f"afn_{schur}_x": xs4.cpu().numpy(),
+                                f"afn_{schur}_it": it4})
+                    da.free()
+                    afn.free()
                 xs2 = torch.zeros_like(b)
                 _, rr2, _, it2 = amd.pcg(op, b, xs2, maxits=2000, tol=1e-6, precond=dn)
                 out.update({"nys_z": z.cpu().numpy(), "nys_x": xs2.cpu().numpy(), "nys_rr": rr2, "nys_it": it2})
@@ -149,6 +162,14 @@ def single(torch_cuda):
             _, _, _, res["nys_it"] = amd.pcg(op, xd.clone(), xs2, maxits=2000, tol=1e-6, precond=nys)
             res["nys_x"] = xs2.cpu().numpy()
             nys.free()
+            for schur in ("fsai", "noise"):
+                afn = amd.AfnPrecond.setup(X, 64, 0, 0, 0, perm_opt="perm", perm=perm, schur_lfil=10, op=op,
+                                           schur=schur)
+                res[f"afn_{schur}_z"] = afn.solve(torch.zeros_like(r), r).cpu().numpy()
+                xs4 = torch.zeros_like(xd)
+                _, _, _, res[f"afn_{schur}_it"] = amd.pcg(op, xd.clone(), xs4, maxits=2000, tol=1e-6, precond=afn)
+                res[f"afn_{schur}_x"] = xs4.cpu().numpy()
+                afn.free()
         op.free()
     return res
 
@@ -215,6 +236,20 @@ def test_row_sharded_nystrom_setup(gloo2, single):
     assert len(set(its)) == 1 and its[0] > 0
     assert abs(its[0] - int(single["nys_it"])) <= max(3, int(single["nys_it"]) // 20), (its, single["nys_it"])
     assert rel(np.concatenate([r["nys_shard_x"] for r in gloo2]), single["nys_x"]) < 1e-4
+
+
+@pytest.mark.parametrize("schur", ["fsai", "noise"])
+def test_row_sharded_afn_apply_and_pcg(gloo2, single, schur):
+    """Nfft4GPAmdAfnShard: each rank keeps its landmarks, the K12 columns of its Schur
+    points and their FSAI rows; the apply equals the one-GPU apply (the K12 y2 sum is regrouped over the
+    ranks) and PCG with it matches the one-GPU iteration count."""
+    z = np.concatenate([r[f"afn_{schur}_z"] for r in gloo2])
+    assert rel(z, single[f"afn_{schur}_z"]) < 1e-12
+    its = [int(r[f"afn_{schur}_it"]) for r in gloo2]
+    it1 = int(single[f"afn_{schur}_it"])
+    assert len(set(its)) == 1 and its[0] > 0
+    assert abs(its[0] - it1) <= max(3, it1 // 20), (its, it1)
+    assert rel(np.concatenate([r[f"afn_{schur}_x"] for r in gloo2]), single[f"afn_{schur}_x"]) < 1e-4
 
 
 def test_row_sharded_nystrom_apply_and_pcg(gloo2, single):
