@@ -57,8 +57,33 @@ def algorithmic_bytes(info, n, nw, beta_zero=True):
     return spread, interp
 
 
-def cpu_baseline(n, d, X, x, max_seconds=25.0):
-    """Oracle (C + OpenMP restatement of nfft_interface.c + NFFT3 fastsum) on this host."""
+def host_info():
+    """The CPU the baseline ran on: model name, logical CPUs this process may use, physical cores of the
+    machine (sockets x cores per socket, /proc/cpuinfo), and the OpenMP binding variables in effect."""
+    model, phys = None, set()
+    try:
+        cur = {}
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if ":" not in line:
+                    if cur.get("physical id") is not None:
+                        phys.add((cur.get("physical id"), cur.get("core id")))
+                    cur = {}
+                    continue
+                k, v = (t.strip() for t in line.split(":", 1))
+                cur[k] = v
+                if k == "model name" and model is None:
+                    model = v
+    except OSError:
+        pass
+    return {"cpu_model": model, "physical_cores_machine": len(phys) or None,
+            "cpus_allowed": len(os.sched_getaffinity(0)),
+            "omp_env": {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OMP_PROC_BIND", "OMP_PLACES")}}
+
+
+def cpu_baseline(n, d, X, x, max_seconds=25.0, min_samples=5, max_samples=15):
+    """Oracle (C + OpenMP restatement of nfft_interface.c + NFFT3 fastsum) on this host: the median of
+    5-15 timed full matvecs after one warm-up (min / max beside it), bounded by max_seconds of CPU work."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc_mod
     lib = None
@@ -81,22 +106,25 @@ def cpu_baseline(n, d, X, x, max_seconds=25.0):
     o.setup(0, 1.0, 1.0, 0.01)
     t_setup = time.time() - t0
     o.matsymv(x)  # warm
-    reps, t_total = 0, 0.0
-    while t_total < max_seconds and reps < 20:
-        t0 = time.time()
+    times = []
+    while len(times) < max_samples and (len(times) < min_samples or sum(times) < max_seconds):
+        t0 = time.perf_counter()
         o.matsymv(x)
-        t_total += time.time() - t0
-        reps += 1
-        if t_total > 0.5 * max_seconds:
-            break
+        times.append(time.perf_counter() - t0)
     threads = int(lib.orc_num_threads())
+    med = float(np.median(times))
     return {
-        "value": reps / t_total,
+        "value": 1.0 / med,
         "unit": "matvecs/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{reps} matvecs of the full workload (n={n}, {d} windows) after one warm-up; "
-                  f"setup (PRE_PSI taps, bhat) {t_setup:.1f}s untimed; -march=native={native}; "
+        "samples": len(times),
+        "median_s": med,
+        "min_s": float(min(times)),
+        "max_s": float(max(times)),
+        "host": host_info(),
+        "sample": f"median of {len(times)} timed matvecs of the full workload (n={n}, {d} windows) after one "
+                  f"warm-up; setup (PRE_PSI taps, bhat) {t_setup:.1f}s untimed; -march=native={native}; "
                   f"OMP threads={threads}",
     }
 
@@ -211,11 +239,16 @@ def run_pcg_nystrom(op, torch, n, k, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=
     pre = amd.NystromPrecond.from_additive(op, perm, k, k11="landmarks")
     torch.cuda.synchronize()
     t_setup_first = time.time() - t0
-    pre.free()
-    t0 = time.time()
-    pre = amd.NystromPrecond.from_additive(op, perm, k, k11="landmarks")
-    torch.cuda.synchronize()
-    t_setup = time.time() - t0
+    # the steady-state setup: the median of three (each rebuilds the factors from scratch)
+    setups = []
+    for _ in range(3):
+        pre.free()
+        torch.cuda.synchronize()
+        t0 = time.time()
+        pre = amd.NystromPrecond.from_additive(op, perm, k, k11="landmarks")
+        torch.cuda.synchronize()
+        setups.append(time.time() - t0)
+    t_setup = float(np.median(setups))
     ms = pre.setup_times()
     flops = 2.0 * n * k * k  # each of the three n x k x k products
     mfma = {"kernel": "k_gemm_f64 (v_mfma_f64_16x16x4)", "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
@@ -243,7 +276,31 @@ def run_pcg_nystrom(op, torch, n, k, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=
     return {"pcg_nys_f32u_time_s": t32, "pcg_nys_f32u_iters": iters32, "pcg_nys_f32u_rel_res": relres32,
             "pcg_nys_rank": k, "pcg_nys_setup_s": t_setup, "pcg_nys_time_s": t, "pcg_nys_iters": iters,
             "pcg_nys_rel_res": relres, "pcg_nys_total_s": t_setup + t, "pcg_nys_setup_first_s": t_setup_first,
-            "nys_setup_mfma": mfma}
+            "pcg_nys_setup_samples_s": setups, "nys_setup_mfma": mfma}
+
+
+def run_fgmres(op, torch, n, rng_seed=906, tol=1e-6, kdim=50, maxits=3000, l=1.0, rows=None, dist=None):
+    """FGMRES (the reference's solver for this system, gp_loss.c:199-213; fgmres.c:3-252) to 1e-6 at the
+    metric's own l = 1, where the NFFT-approximated kernel is indefinite and CG cannot run; restart
+    dimension kdim.  With a distributed operator every rank runs it on its rows (time: max over ranks)."""
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    assert op.setup(amd.GAUSSIAN, f=1.0, l=l, mu=0.01) == 0
+    rb, re = rows if rows is not None else (0, n)
+    b = torch.tensor((np.random.default_rng(rng_seed + 1).random(n) - 0.5)[rb:re], device="cuda")
+    x = torch.zeros(re - rb, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.time()
+    _, relres, hist, iters = amd.fgmres(op, b, x, kdim=kdim, maxits=maxits, tol=tol)
+    torch.cuda.synchronize()
+    t = time.time() - t0
+    if dist is not None:
+        tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    return {"fgmres_time_s": t, "fgmres_iters": iters, "fgmres_rel_res": relres, "fgmres_converged": relres <= tol,
+            "fgmres_tol": tol, "fgmres_l": l, "fgmres_kdim": kdim, "fgmres_ms_per_iter": 1e3 * t / max(iters, 1)}
 
 
 def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1, schur="fsai",
@@ -302,7 +359,7 @@ def main():
     ap.add_argument("--afn-rank", type=int, default=512, help="rank of the AFN-preconditioned PCG (0: off)")
     ap.add_argument("--afn-schur", default="both", choices=["fsai", "noise", "both"],
                     help="AFN Schur-complement solve: kernel FSAI (schur_opt 3), I/mu (0) or both")
-    ap.add_argument("--afn-order", default="random", choices=["random", "fps", "both"],
+    ap.add_argument("--afn-order", default="both", choices=["random", "fps", "both"],
                     help="AFN landmark order: random (perm_opt 0) or farthest points (1)")
     ap.add_argument("--partition", default="rows", choices=["rows", "components"],
                     help="N > 1: the headline split (the other one is timed too)")
@@ -398,6 +455,7 @@ def main():
             op.matsymv(xh, 1.0, 0.0, yh)
         pcie_rate = reps_h / (time.perf_counter() - t0)
     if world == 1 and not args.no_pcg:
+        pcg.update(run_fgmres(op, torch, n))
         pcg.update(run_pcg_single(op, torch, n))
         if args.nys_rank > 0:
             try:
@@ -469,6 +527,7 @@ def main():
                "all_reduce_bytes_per_matvec": 8 * (op2.n if other == "components" else d * 64)}
         if not args.no_pcg:
             alt.update(run_pcg_single(op2, torch, n, rows=(op2.row_begin, op2.row_end), dist=dist))
+            alt.update(run_fgmres(op2, torch, n, rows=(op2.row_begin, op2.row_end), dist=dist))
         op2.free()
         op, xd, yd = op_main, xd_main, yd_main
     headline = n == 1_000_000 and d == 32
@@ -552,6 +611,7 @@ def main():
         if not args.no_pcg:
             result.update(run_pcg_single(op, torch, n, rows=(rb, re), dist=dist))
             result["pcg_impl"] = f"Nfft4GPSolverPcg on Nfft4GPAmdDistMatSymv ({args.partition}), device-controlled"
+            result.update(run_fgmres(op, torch, n, rows=(rb, re), dist=dist))
         result["partition_" + alt["partition"]] = alt
     if rank == 0:
         print(json.dumps(result), flush=True)

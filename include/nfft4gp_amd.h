@@ -522,6 +522,12 @@ void Nfft4GPAmdDistFree(void *dop);
  * to the global n, so its iterations equal the single-GPU solver's up to rounding. */
 int Nfft4GPAmdDistMatSymv(void *dop, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE beta,
                           NFFT4GP_DOUBLE *y);
+/* kind 1 (components): y is all-reduced in `chunks` pieces (default 4) on a stream of the operator's own,
+ * each piece as soon as the interpolation launch that writes it is done, so the all-reduce of piece i
+ * overlaps the interpolation of piece i + 1 (1-D windows, plain matvec; the gradient matvec and
+ * multi-feature windows all-reduce y once).  chunks = 1: one all-reduce after the matvec.  The sums are
+ * the same element for element. */
+int Nfft4GPAmdDistSetChunks(void *dop, int chunks);
 int Nfft4GPAmdDistGradMatSymv(void *dop, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE beta,
                               NFFT4GP_DOUBLE *y);
 /* func_kernel (kernels.h:49) of a distributed operator, for Nfft4GPGpLoss (gp_loss.c:96-307): dop begins

@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "internal.h"
 
@@ -102,6 +103,9 @@ struct CommCallback : Comm {
             fprintf(stderr, "nfft4gp_amd: the all-reduce callback failed\n");
             return -1;
          }
+         // the callback may have written the sum on the library stream (torch's current stream); s may be
+         // another one (the component split's chunk stream)
+         if (s != current_stream()) NFFT4GP_HIP_CHECK(hipStreamSynchronize(current_stream()));
          NFFT4GP_HIP_CHECK(hipMemcpyAsync(d_buf + off, stage, sizeof(double) * m, hipMemcpyDeviceToDevice, s));
       }
       return 0;
@@ -127,7 +131,43 @@ struct DistOp {
    double* d_grid = nullptr;
    size_t grid_count = 0;
    double* d_tmp = nullptr;  // components, beta != 0: 3 n
+   // components: y is all-reduced in `chunks` pieces on a stream of its own, each piece as soon as the
+   // interpolation launch that writes it is done, so the all-reduce of piece i overlaps the interpolation
+   // of piece i + 1; chunks = 1: one all-reduce after the whole matvec
+   int chunks = 4;
+   hipStream_t cs = nullptr;
+   std::vector<hipEvent_t> ev;
 };
+
+struct ChunkCtx {
+   DistOp* D;
+   double* y;
+   hipStream_t s;
+   int i;
+};
+
+// after the interpolation of rows [r0, r1): the comm stream waits for it, then all-reduces those rows
+int chunk_done(void* vctx, size_t r0, size_t r1)
+{
+   ChunkCtx* C = (ChunkCtx*)vctx;
+   DistOp* D = C->D;
+   if ((size_t)C->i + 1 >= D->ev.size()) return -1;
+   hipEvent_t e = D->ev[C->i++];
+   NFFT4GP_HIP_CHECK(hipEventRecord(e, C->s));
+   NFFT4GP_HIP_CHECK(hipStreamWaitEvent(D->cs, e, 0));
+   return D->comm->allreduce(C->y + r0, r1 - r0, D->cs);
+}
+
+int ensure_chunk_stream(DistOp* D)
+{
+   if (!D->cs) NFFT4GP_HIP_CHECK(hipStreamCreateWithFlags(&D->cs, hipStreamNonBlocking));
+   while (D->ev.size() < (size_t)D->chunks + 1) {
+      hipEvent_t e;
+      NFFT4GP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      D->ev.push_back(e);
+   }
+   return 0;
+}
 
 int grid_ready(DistOp* D)
 {
@@ -169,9 +209,25 @@ int dist_apply(DistOp* D, int n, int grad, double alpha, double* x, double beta,
       if (!D->d_tmp) NFFT4GP_HIP_CHECK(hipMalloc((void**)&D->d_tmp, sizeof(double) * 3 * std::max<size_t>(1, n)));
       out = D->d_tmp;
    }
-   const int rc = grad ? Nfft4GPAdditiveNFFTGradMatSymv(D->h, n, alpha, x, 0.0, out)
-                       : Nfft4GPAdditiveNFFTMatSymv(D->h, n, alpha, x, 0.0, out);
-   if (rc || D->comm->allreduce(out, ny, s)) return -1;
+   bool chunked = false;
+   if (!grad && D->chunks > 1 && n > 0) {
+      if (ensure_chunk_stream(D)) return -1;
+      ChunkCtx C{D, out, s, 0};
+      const int rc = additive_matvec_chunked(D->h, alpha, x, out, D->chunks, &chunk_done, &C);
+      if (rc == 0) {
+         // the stream's later work (the caller's reads of y, the next matvec) waits for the last piece
+         NFFT4GP_HIP_CHECK(hipEventRecord(D->ev[C.i], D->cs));
+         NFFT4GP_HIP_CHECK(hipStreamWaitEvent(s, D->ev[C.i], 0));
+         chunked = true;
+      } else if (C.i > 0) {
+         return -1;  // failed after some pieces were enqueued
+      }
+   }
+   if (!chunked) {
+      const int rc = grad ? Nfft4GPAdditiveNFFTGradMatSymv(D->h, n, alpha, x, 0.0, out)
+                          : Nfft4GPAdditiveNFFTMatSymv(D->h, n, alpha, x, 0.0, out);
+      if (rc || D->comm->allreduce(out, ny, s)) return -1;
+   }
    if (beta != 0.0) {
       const int g = (int)std::min<size_t>(4096, (ny + 255) / 256);
       hipLaunchKernelGGL(k_axpby_add, dim3(std::max(g, 1)), dim3(256), 0, s, beta, y, (const double*)D->d_tmp, ny);
@@ -320,8 +376,11 @@ void Nfft4GPAmdDistFree(void* dop)
    DistOp* D = (DistOp*)dop;
    if (!D) return;
    (void)hipStreamSynchronize(current_stream());
+   if (D->cs) (void)hipStreamSynchronize(D->cs);
    if (D->d_grid) (void)hipFree(D->d_grid);
    if (D->d_tmp) (void)hipFree(D->d_tmp);
+   for (hipEvent_t e : D->ev) (void)hipEventDestroy(e);
+   if (D->cs) (void)hipStreamDestroy(D->cs);
    delete D;
 }
 
@@ -362,6 +421,15 @@ int Nfft4GPAmdDistMatern12Kernel(void* str, double* data, int n, int ldim, int d
 {
    (void)data, (void)n, (void)ldim, (void)d, (void)permr, (void)kr, (void)permc, (void)kc;
    return dist_kernel_setup(str, 1, Kp, dKp);
+}
+
+int Nfft4GPAmdDistSetChunks(void* dop, int chunks)
+{
+   DistOp* D = (DistOp*)dop;
+   if (!D || chunks < 1 || chunks > 256) return -1;
+   (void)hipStreamSynchronize(current_stream());
+   D->chunks = chunks;
+   return 0;
 }
 
 int Nfft4GPAmdDistMatSymv(void* dop, int n, double alpha, double* x, double beta, double* y)

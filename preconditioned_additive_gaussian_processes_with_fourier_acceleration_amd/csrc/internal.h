@@ -203,6 +203,9 @@ int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_g
 // d_dot != nullptr (non-grad): also writes (y, x) to *d_dot (device), one grid-wide reduction in the launch
 int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, double beta, double* d_y,
                   hipStream_t stream, double* d_dot = nullptr);
+// the interpolation of blocks [b0, b1) (plain matvec, no gradient / dot)
+int launch_interp_blocks(const AdditivePlan& P, double alpha, const double* d_x, double beta, double* d_y, int b0,
+                         int b1, hipStream_t stream);
 // y_v = beta y_v + alpha A x_v, v = 0, 1, in one pass over the layout (1-D layouts; -1 for multi-feature windows)
 int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double* x1, double beta, double* y0,
                    double* y1, hipStream_t stream);
@@ -374,6 +377,11 @@ struct DistPcgInfo {
 };
 int dist_pcg_info(void* dop, DistPcgInfo& info);
 NysDev* nys_setup_shard(void* str, const int* perm, int k, int k11_mode, Comm* comm);  // nfft_api.cpp
+// y = alpha A x (beta = 0) of a whole-row 1-D handle with its interpolation split into nchunks launches of
+// consecutive blocks; after each, done(r0, r1) is called with the rows that launch wrote (enqueued work
+// only, on the current stream).  -1: not a 1-D whole-row handle (the caller runs the plain matvec)
+int additive_matvec_chunked(void* str, double alpha, const double* d_x, double* d_y, int nchunks,
+                            int (*done)(void* ctx, size_t r0, size_t r1), void* ctx);
 // q = A p with the local (q, p) in *d_dot (row shards; the caller all-reduces it)
 int dist_matvec_dot(void* dop, const double* d_p, double* d_q, double* d_dot);
 

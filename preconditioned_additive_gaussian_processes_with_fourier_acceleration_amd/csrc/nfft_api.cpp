@@ -591,6 +591,24 @@ int additive_matvec_multi(void* str, int nv, double alpha, const double* const* 
    return 0;
 }
 
+int additive_matvec_chunked(void* str, double alpha, const double* d_x, double* d_y, int nchunks,
+                            int (*done)(void* ctx, size_t r0, size_t r1), void* ctx)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready) return -1;
+   AdditivePlan& P = E->P;
+   if (P.md.on || P.timing || P.row_begin != 0 || P.row_end != P.n_global || P.nblocks == 0) return -1;
+   hipStream_t s = current_stream();
+   if (launch_spread(P, d_x, P.d_part, s) || launch_grid(P, P.d_part, P.nblocks, 0, s)) return -1;
+   nchunks = std::max(1, std::min(nchunks, P.nblocks));
+   for (int c = 0; c < nchunks; c++) {
+      const int b0 = (int)((long long)P.nblocks * c / nchunks), b1 = (int)((long long)P.nblocks * (c + 1) / nchunks);
+      if (launch_interp_blocks(P, alpha, d_x, 0.0, d_y, b0, b1, s)) return -1;
+      if (done(ctx, (size_t)b0 * P.B, std::min((size_t)b1 * P.B, (size_t)P.n))) return -1;
+   }
+   return 0;
+}
+
 // rows of an additive handle: local (this shard) and global; -1 when str is not an additive handle
 int additive_rows(void* str, int* n_local, int* n_global, int* row_begin)
 {

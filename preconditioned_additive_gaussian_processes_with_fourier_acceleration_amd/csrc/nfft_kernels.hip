@@ -739,6 +739,24 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
    return 0;
 }
 
+// the plain interpolation (no gradient, no fused dot) of blocks [b0, b1) only: the kernel sees a layout
+// whose first block is b0 (tile_off, x and y offset by b0 blocks), so each launch writes rows
+// [b0 B, min(b1 B, n)) exactly as the whole launch would
+int launch_interp_blocks(const AdditivePlan& P, double alpha, const double* d_x, double beta, double* d_y, int b0,
+                         int b1, hipStream_t stream)
+{
+   if (P.n == 0 || b1 <= b0) return 0;
+   raise_lds_limit_once();
+   const InterpVariant& V = kInterpVariants[std::min(std::max(P.interp_variant, 0), kNumInterpVariants - 1)];
+   const size_t off = (size_t)b0 * P.B;
+   hipLaunchKernelGGL(V.fn, dim3(b1 - b0), dim3(V.threads), interp_lds_bytes(P, 0), stream, P.dl.meta, P.dl.lo,
+                      P.dl.q, P.dl.tile_off + (size_t)b0 * P.ngroups, (const double*)P.d_H, (const double*)P.d_Hd,
+                      d_x + off, d_y + off, P.n - (int)off, P.B, P.ngroups, alpha, beta, P.f, P.mu * P.diag, P.diag,
+                      (double*)nullptr, (unsigned int*)nullptr, (double*)nullptr);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
 // y_v = beta y_v + alpha A x_v for two vectors: one spread per vector, both grids in one launch, one
 // two-vector interpolation (1-D layouts, whole-row handles)
 constexpr int kInterp2Threads = 1024;

@@ -67,6 +67,15 @@ def _worker(rank, world, port, outdir, backend):
             y0 = torch.full_like(y, 0.25)
             yb = op.matsymv(xd, 0.7, -1.5, y0.clone())
             g = op.gradmatsymv(xd)
+            if part == "components":
+                # y all-reduced in one piece instead of 4 overlapped pieces: the same sums, bit for bit
+                L = amd.lib()
+                assert L.Nfft4GPAmdDistSetChunks(op.h, 1) == 0
+                out[f"{kind}_{part}_y1"] = op.matsymv(xd).cpu().numpy()
+                out[f"{kind}_{part}_yb1"] = op.matsymv(xd, 0.7, -1.5, y0.clone()).cpu().numpy()
+                assert L.Nfft4GPAmdDistSetChunks(op.h, 7) == 0
+                out[f"{kind}_{part}_y7"] = op.matsymv(xd).cpu().numpy()
+                assert L.Nfft4GPAmdDistSetChunks(op.h, 4) == 0
             b = torch.tensor(x[rb:re], device="cuda")
             xs = torch.zeros_like(b)
             _, rr, hist, it = amd.pcg(op, b, xs, maxits=2000, tol=1e-6)
@@ -224,6 +233,16 @@ def test_distributed_pcg_matches_single_gpu(gloo2, single, kind, part):
     # LDS-atomic accumulation order moves CG's count by a few iterations run to run
     assert abs(it - it1) <= max(3, it1 // 20), (it, it1)
     assert rel(gather(gloo2, key + "_x", part), single[kind + "_x"]) < 1e-4
+
+
+@pytest.mark.parametrize("kind", ["1d", "md"])
+def test_component_split_chunked_allreduce_is_bitwise(gloo2, kind):
+    """the component split all-reduces y in pieces on its own stream, each overlapping the
+    next piece's interpolation; 1, 4 (default) and 7 pieces give the same bits (elementwise sums)."""
+    for r in gloo2:
+        np.testing.assert_array_equal(r[f"{kind}_components_y"], r[f"{kind}_components_y1"])
+        np.testing.assert_array_equal(r[f"{kind}_components_y"], r[f"{kind}_components_y7"])
+        np.testing.assert_array_equal(r[f"{kind}_components_yb"], r[f"{kind}_components_yb1"])
 
 
 def test_row_sharded_nystrom_setup(gloo2, single):
