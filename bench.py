@@ -345,6 +345,35 @@ def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000
             key + "_total_s": t_setup + t, key + "_apply_ms": 1e3 * t_apply}
 
 
+def run_loss(op, torch, n, d, X, rng_seed=906, maxits=50, nvecs=10, rows=None, dist=None):
+    """One log-marginal-likelihood + gradient evaluation (Nfft4GPGpLoss, gp_loss.c:96-307: FGMRES for K^-1 y,
+    stochastic Lanczos quadrature with nvecs Rademacher probes of maxits steps, the gradient matvecs) on the
+    bench's operator at (f, l, mu) = (1, 1, 0.01), identity transform -- the loop BASELINE configs[4] runs
+    at n = 1e7 on 8 GPUs, here at the bench's size.  With a distributed operator every rank runs it on its
+    rows (krylov.hip sums every inner product over the ranks); time: max over ranks."""
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    rb, re = rows if rows is not None else (0, n)
+    rng = np.random.default_rng(rng_seed + 3)
+    y = rng.random(n) - 0.5
+    R = np.where(rng.random((n, nvecs)) < 0.5, -1.0, 1.0)
+    win = np.arange(d, dtype=np.int32)
+    Rl = torch.tensor(np.asfortranarray(R[rb:re]).T.copy(), device="cuda")  # probe-major = column-major n x nvecs
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.time()
+    loss, grad = amd.gp_loss(X, win, d, 1, y[rb:re], (1.0, 1.0, 0.01), maxits=maxits, nvecs=nvecs, rademacher=Rl,
+                             tol=1e-6, transform=3, op=op)
+    torch.cuda.synchronize()
+    t = time.time() - t0
+    if dist is not None:
+        tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    return {"loss_time_s": t, "loss_value": loss, "loss_grad": [float(g) for g in grad], "loss_maxits": maxits,
+            "loss_nvecs": nvecs}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -455,6 +484,7 @@ def main():
             op.matsymv(xh, 1.0, 0.0, yh)
         pcie_rate = reps_h / (time.perf_counter() - t0)
     if world == 1 and not args.no_pcg:
+        pcg.update(run_loss(op, torch, n, d, X))
         pcg.update(run_fgmres(op, torch, n))
         pcg.update(run_pcg_single(op, torch, n))
         if args.nys_rank > 0:
@@ -612,6 +642,7 @@ def main():
             result.update(run_pcg_single(op, torch, n, rows=(rb, re), dist=dist))
             result["pcg_impl"] = f"Nfft4GPSolverPcg on Nfft4GPAmdDistMatSymv ({args.partition}), device-controlled"
             result.update(run_fgmres(op, torch, n, rows=(rb, re), dist=dist))
+            result.update(run_loss(op, torch, n, d, X, rows=(rb, re), dist=dist))
         result["partition_" + alt["partition"]] = alt
     if rank == 0:
         print(json.dumps(result), flush=True)

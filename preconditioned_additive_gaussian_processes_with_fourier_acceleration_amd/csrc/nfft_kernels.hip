@@ -241,6 +241,137 @@ __global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__
    }
 }
 
+// ------------------------------------------------------------------------------------------------
+// persistent spread: one 1024-thread workgroup per CU walks a contiguous range of items (block b,
+// super-group of S layout groups = S*CG windows); the block's alpha slice is staged once per block and the
+// NEXT block's slice is loaded into registers (B/1024 doubles per thread) while the current item runs, so
+// no item waits for its alpha; the next item's first run is loaded while the current one folds.  Same
+// moments, fold order and partial grids as k_spread (results identical up to the ds_add_f64 order).
+// ------------------------------------------------------------------------------------------------
+constexpr int kPersThreads = 1024;
+constexpr int kPersAlpha = (kMaxBlock + kPad + kPersThreads - 1) / kPersThreads;  // alpha doubles per thread
+
+__device__ __forceinline__ void alpha_regs_load(double (&a)[kPersAlpha], const double* __restrict__ x, int base,
+                                                int nloc)
+{
+#pragma unroll
+   for (int k = 0; k < kPersAlpha; k++) {
+      const int e = threadIdx.x + k * kPersThreads;
+      a[k] = e < nloc ? x[(size_t)base + e] : 0.0;
+   }
+}
+
+__device__ __forceinline__ void alpha_regs_store(double* __restrict__ s, const double (&a)[kPersAlpha], int Bp)
+{
+#pragma unroll
+   for (int k = 0; k < kPersAlpha; k++) {
+      const int e = threadIdx.x + k * kPersThreads;
+      if (e < Bp) s[e] = a[k];  // entries >= nloc (pad and dummy slots) are zero
+   }
+}
+
+template <int S>
+__global__ __launch_bounds__(kPersThreads) void k_spread_pers(const uint16_t* __restrict__ meta,
+                                                               const uint32_t* __restrict__ lo,
+                                                               const uint32_t* __restrict__ qarr,
+                                                               const int* __restrict__ tile_off,
+                                                               const double* __restrict__ x, int n, int B, int nblocks,
+                                                               int ngroups, int CG, int nw,
+                                                               double* __restrict__ part)
+{
+   extern __shared__ __attribute__((aligned(16))) double smem[];
+   const int Bp = B + kPad;
+   double* s_alpha = smem;
+   double* s_mom = smem + Bp;  // S*CG*64*kMomStride
+   const int nsg = (ngroups + S - 1) / S;  // super-groups per block
+   const long long nitems = (long long)nblocks * nsg;
+   const int i_begin = (int)(nitems * blockIdx.x / gridDim.x);
+   const int i_end = (int)(nitems * (blockIdx.x + 1) / gridDim.x);
+   if (i_begin >= i_end) return;
+   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+   constexpr int nwaves = kPersThreads / 64;
+   const int mom_count = S * CG * kNos * kMomStride;
+
+   // the first item: its alpha slice and first run
+   int b = i_begin / nsg;
+   int sg = i_begin % nsg;
+   int t1 = tile_off[b * ngroups + min(ngroups, (sg + 1) * S)];
+   int t = tile_off[b * ngroups + sg * S] + wave;
+   TileRegs cur;
+   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
+   {
+      double a[kPersAlpha];
+      alpha_regs_load(a, x, b * B, min(B, n - b * B));
+      alpha_regs_store(s_alpha, a, Bp);
+   }
+   for (int i = tid; i < mom_count; i += kPersThreads) s_mom[i] = 0.0;
+   __syncthreads();
+
+   for (int item = i_begin; item < i_end; item++) {
+      const int c0 = sg * S * CG;
+      // the next item's alpha slice, if it starts a new block, travels while this item runs
+      const int nb = (item + 1 < i_end) ? (item + 1) / nsg : b;
+      double an[kPersAlpha];
+      if (nb != b) alpha_regs_load(an, x, nb * B, min(B, n - nb * B));
+      for (; t < t1; t += nwaves) {
+         TileRegs nxt;
+         const int tn = t + nwaves;
+         if (tn < t1) load_tile(nxt, meta, lo, qarr, tn, lane);
+         double acc[kNC];
+#pragma unroll
+         for (int d = 0; d < kNC; d++) acc[d] = 0.0;
+#pragma unroll
+         for (int r = 0; r < kR; r++) {
+            const uint32_t loc = slot_loc(cur, r);
+            const double u = q_to_u(cur.qq[r]);
+            double tpow = s_alpha[loc];
+            acc[0] += tpow;
+#pragma unroll
+            for (int d = 1; d < kNC; d++) {
+               tpow *= u;
+               acc[d] += tpow;
+            }
+         }
+         const int comp_local = (int)(cur.mt >> 6) - c0;
+         const int cell = (int)(cur.mt & 63u);
+         double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
+#pragma unroll
+         for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
+         if (tn < t1) cur = nxt;
+      }
+      __syncthreads();
+      // the next item's first run is loaded while this one folds
+      const int ob = b;
+      if (item + 1 < i_end) {
+         b = nb;
+         sg = (item + 1) % nsg;
+         t1 = tile_off[b * ngroups + min(ngroups, (sg + 1) * S)];
+         t = tile_off[b * ngroups + sg * S] + wave;
+         if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
+      }
+      // fold (as k_spread): g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
+      const int ncomp = min(S * CG, nw - c0);
+      for (int idx = tid; idx < ncomp * kNos; idx += kPersThreads) {
+         const int cl = idx / kNos;
+         const int gi = idx % kNos;
+         double v = 0.0;
+#pragma unroll 1
+         for (int tp = 0; tp < kTaps; tp++) {
+            const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
+#pragma unroll
+            for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
+         }
+         part[((size_t)(c0 + cl) * nblocks + ob) * kNos + gi] = v;  // [comp][block][cell]
+      }
+      if (item + 1 < i_end) {
+         __syncthreads();  // fold reads and the last run's alpha reads are done
+         for (int i = tid; i < mom_count; i += kPersThreads) s_mom[i] = 0.0;
+         if (nb != ob) alpha_regs_store(s_alpha, an, Bp);
+         __syncthreads();
+      }
+   }
+}
+
 // copy the diagnostic timeline out (tools/ only)
 extern "C" int Nfft4GPAmdDebugStamps(unsigned long long* out, int nwg)
 {
@@ -611,6 +742,13 @@ static size_t spread_lds_bytes(const AdditivePlan& P)
    return sizeof(double) * ((size_t)P.B + kPad + (size_t)P.CG * kNos * kMomStride);
 }
 
+// the persistent spread: super-groups of kPersS layout groups while they fit the LDS with the alpha slice
+constexpr int kPersS = 4;
+static size_t pers_lds_bytes(const AdditivePlan& P, int S)
+{
+   return sizeof(double) * ((size_t)P.B + kPad + (size_t)S * P.CG * kNos * kMomStride);
+}
+
 static size_t interp_lds_bytes(const AdditivePlan& P, int grad)
 {
    return sizeof(double) * ((size_t)P.B + kPad) * (grad ? 2 : 1);
@@ -687,6 +825,29 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
    raise_lds_limit_once();
+   if (P.spread_variant == 5 && pers_lds_bytes(P, kPersS) <= 160 * 1024) {
+      static bool attr = false;
+      if (!attr) {
+         (void)hipFuncSetAttribute((const void*)k_spread_pers<kPersS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024);
+         (void)hipGetLastError();
+         attr = true;
+      }
+      static int ncu = 0;
+      if (!ncu) {
+         int dev = 0;
+         (void)hipGetDevice(&dev);
+         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+      }
+      const long long nitems = (long long)P.nblocks * ((P.ngroups + kPersS - 1) / kPersS);
+      const int grid = (int)std::min<long long>(ncu, nitems);
+      launch_ev(k_spread_pers<kPersS>, dim3(grid), dim3(kPersThreads), pers_lds_bytes(P, kPersS), stream,
+                P.kev ? P.kev + 0 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks,
+                P.ngroups, P.CG, P.nw, d_part);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   }
    const SpreadVariant& V = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
    const int gpw = std::min(std::max(P.gpw, 1), P.ngroups);
    const int nslices = (P.ngroups + gpw - 1) / gpw;
