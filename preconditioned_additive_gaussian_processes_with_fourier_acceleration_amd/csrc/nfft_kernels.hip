@@ -248,30 +248,35 @@ __global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__
 // no item waits for its alpha; the next item's first run is loaded while the current one folds.  Same
 // moments, fold order and partial grids as k_spread (results identical up to the ds_add_f64 order).
 // ------------------------------------------------------------------------------------------------
-constexpr int kPersThreads = 1024;
-constexpr int kPersAlpha = (kMaxBlock + kPad + kPersThreads - 1) / kPersThreads;  // alpha doubles per thread
+template <int T>
+constexpr int pers_alpha() { return (kMaxBlock + kPad + T - 1) / T; }  // alpha doubles per thread
 
-__device__ __forceinline__ void alpha_regs_load(double (&a)[kPersAlpha], const double* __restrict__ x, int base,
+template <int T>
+__device__ __forceinline__ void alpha_regs_load(double (&a)[pers_alpha<T>()], const double* __restrict__ x, int base,
                                                 int nloc)
 {
 #pragma unroll
-   for (int k = 0; k < kPersAlpha; k++) {
-      const int e = threadIdx.x + k * kPersThreads;
+   for (int k = 0; k < pers_alpha<T>(); k++) {
+      const int e = threadIdx.x + k * T;
       a[k] = e < nloc ? x[(size_t)base + e] : 0.0;
    }
 }
 
-__device__ __forceinline__ void alpha_regs_store(double* __restrict__ s, const double (&a)[kPersAlpha], int Bp)
+template <int T>
+__device__ __forceinline__ void alpha_regs_store(double* __restrict__ s, const double (&a)[pers_alpha<T>()], int Bp)
 {
 #pragma unroll
-   for (int k = 0; k < kPersAlpha; k++) {
-      const int e = threadIdx.x + k * kPersThreads;
+   for (int k = 0; k < pers_alpha<T>(); k++) {
+      const int e = threadIdx.x + k * T;
       if (e < Bp) s[e] = a[k];  // entries >= nloc (pad and dummy slots) are zero
    }
 }
 
-template <int S>
-__global__ __launch_bounds__(kPersThreads) void k_spread_pers(const uint16_t* __restrict__ meta,
+// THREADS = 1024, PF = true: one workgroup per CU, the next block's alpha in registers during an item.
+// THREADS = 512, PF = false: three per CU (the k_spread footprint), the alpha slice staged after the fold
+// when the block changes; the persistence only removes the launch tail and re-staging within a block.
+template <int THREADS, int S, bool PF>
+__global__ __launch_bounds__(THREADS) void k_spread_pers(const uint16_t* __restrict__ meta,
                                                                const uint32_t* __restrict__ lo,
                                                                const uint32_t* __restrict__ qarr,
                                                                const int* __restrict__ tile_off,
@@ -289,7 +294,9 @@ __global__ __launch_bounds__(kPersThreads) void k_spread_pers(const uint16_t* __
    const int i_end = (int)(nitems * (blockIdx.x + 1) / gridDim.x);
    if (i_begin >= i_end) return;
    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-   constexpr int nwaves = kPersThreads / 64;
+   constexpr int nwaves = THREADS / 64;
+   constexpr int kPersThreads = THREADS;
+   constexpr int NA = pers_alpha<THREADS>();
    const int mom_count = S * CG * kNos * kMomStride;
 
    // the first item: its alpha slice and first run
@@ -299,11 +306,7 @@ __global__ __launch_bounds__(kPersThreads) void k_spread_pers(const uint16_t* __
    int t = tile_off[b * ngroups + sg * S] + wave;
    TileRegs cur;
    if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
-   {
-      double a[kPersAlpha];
-      alpha_regs_load(a, x, b * B, min(B, n - b * B));
-      alpha_regs_store(s_alpha, a, Bp);
-   }
+   stage_block<THREADS>(s_alpha, x, b * B, min(B, n - b * B), B);
    for (int i = tid; i < mom_count; i += kPersThreads) s_mom[i] = 0.0;
    __syncthreads();
 
@@ -311,12 +314,14 @@ __global__ __launch_bounds__(kPersThreads) void k_spread_pers(const uint16_t* __
       const int c0 = sg * S * CG;
       // the next item's alpha slice, if it starts a new block, travels while this item runs
       const int nb = (item + 1 < i_end) ? (item + 1) / nsg : b;
-      double an[kPersAlpha];
-      if (nb != b) alpha_regs_load(an, x, nb * B, min(B, n - nb * B));
+      double an[PF ? NA : 1];
+      if constexpr (PF) {
+         if (nb != b) alpha_regs_load<THREADS>(an, x, nb * B, min(B, n - nb * B));
+      }
       for (; t < t1; t += nwaves) {
          TileRegs nxt;
          const int tn = t + nwaves;
-         if (tn < t1) load_tile(nxt, meta, lo, qarr, tn, lane);
+         if (PF && tn < t1) load_tile(nxt, meta, lo, qarr, tn, lane);
          double acc[kNC];
 #pragma unroll
          for (int d = 0; d < kNC; d++) acc[d] = 0.0;
@@ -337,7 +342,11 @@ __global__ __launch_bounds__(kPersThreads) void k_spread_pers(const uint16_t* __
          double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
 #pragma unroll
          for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
-         if (tn < t1) cur = nxt;
+         if (PF) {
+            if (tn < t1) cur = nxt;
+         } else if (tn < t1) {
+            load_tile(cur, meta, lo, qarr, tn, lane);
+         }
       }
       __syncthreads();
       // the next item's first run is loaded while this one folds
@@ -366,7 +375,12 @@ __global__ __launch_bounds__(kPersThreads) void k_spread_pers(const uint16_t* __
       if (item + 1 < i_end) {
          __syncthreads();  // fold reads and the last run's alpha reads are done
          for (int i = tid; i < mom_count; i += kPersThreads) s_mom[i] = 0.0;
-         if (nb != ob) alpha_regs_store(s_alpha, an, Bp);
+         if (nb != ob) {
+            if constexpr (PF)
+               alpha_regs_store<THREADS>(s_alpha, an, Bp);
+            else
+               stage_block<THREADS>(s_alpha, x, nb * B, min(B, n - nb * B), B);
+         }
          __syncthreads();
       }
    }
@@ -825,11 +839,13 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
    raise_lds_limit_once();
-   if (P.spread_variant == 5 && pers_lds_bytes(P, kPersS) <= 160 * 1024) {
+   if ((P.spread_variant == 5 && pers_lds_bytes(P, kPersS) <= 160 * 1024) || P.spread_variant == 6) {
       static bool attr = false;
       if (!attr) {
-         (void)hipFuncSetAttribute((const void*)k_spread_pers<kPersS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   160 * 1024);
+         (void)hipFuncSetAttribute((const void*)k_spread_pers<1024, kPersS, true>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+         (void)hipFuncSetAttribute((const void*)k_spread_pers<512, 1, false>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
          (void)hipGetLastError();
          attr = true;
       }
@@ -840,11 +856,19 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
          if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
             ncu = 256;
       }
-      const long long nitems = (long long)P.nblocks * ((P.ngroups + kPersS - 1) / kPersS);
-      const int grid = (int)std::min<long long>(ncu, nitems);
-      launch_ev(k_spread_pers<kPersS>, dim3(grid), dim3(kPersThreads), pers_lds_bytes(P, kPersS), stream,
-                P.kev ? P.kev + 0 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks,
-                P.ngroups, P.CG, P.nw, d_part);
+      if (P.spread_variant == 5) {
+         const long long nitems = (long long)P.nblocks * ((P.ngroups + kPersS - 1) / kPersS);
+         const int grid = (int)std::min<long long>(ncu, nitems);
+         launch_ev(k_spread_pers<1024, kPersS, true>, dim3(grid), dim3(1024), pers_lds_bytes(P, kPersS), stream,
+                   P.kev ? P.kev + 0 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks,
+                   P.ngroups, P.CG, P.nw, d_part);
+      } else {
+         const long long nitems = (long long)P.nblocks * P.ngroups;
+         const int grid = (int)std::min<long long>(3LL * ncu, nitems);
+         launch_ev(k_spread_pers<512, 1, false>, dim3(grid), dim3(512), pers_lds_bytes(P, 1), stream,
+                   P.kev ? P.kev + 0 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks,
+                   P.ngroups, P.CG, P.nw, d_part);
+      }
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return 0;
    }

@@ -11,15 +11,21 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd  # noqa: E402
 
 n, d = 1000000, 32
+ranks = int(sys.argv[1]) if len(sys.argv) > 1 else 1  # > 1: the row shard [0, n / ranks) (tools/shard_probe.py)
 rng = np.random.default_rng(906)
 X = rng.random((n, d))
 x = rng.random(n) - 0.5
-op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+nl = n // ranks
+op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1, shard=(0, nl) if ranks > 1 else None)
 assert op.setup(amd.GAUSSIAN, 1.0, 1.0, 0.01) == 0
-xd = torch.tensor(x, device="cuda")
-yd = torch.zeros(n, dtype=torch.float64, device="cuda")
+xd = torch.tensor(x[:nl], device="cuda")
+yd = torch.zeros(nl, dtype=torch.float64, device="cuda")
+grid = torch.zeros(max(1, amd.lib().Nfft4GPAmdShardGridSize(op.h)), dtype=torch.float64, device="cuda")
 for _ in range(5):
-    op.matsymv(xd, 1.0, 0.0, yd)
+    if ranks > 1:
+        amd.lib().Nfft4GPAmdShardSpread(op.h, xd.data_ptr(), grid.data_ptr())
+    else:
+        op.matsymv(xd, 1.0, 0.0, yd)
 torch.cuda.synchronize()
 info = op.layout_info()
 ngroups, nblocks = info["ngroups"], info["nblocks"]
