@@ -37,3 +37,35 @@ def test_restatement_is_self_consistent():
         dM = (Ms[0] - Ms[1]) / (2 * h)
         np.testing.assert_allclose(y[g], dM @ x, rtol=1e-6, atol=1e-8 * np.abs(dM @ x).max())
         assert tr[g] == pytest.approx(np.trace(np.linalg.solve(M, dM)), rel=1e-6)
+
+
+def test_ran_restatement_is_self_consistent():
+    """oracle/ran_spec.py (MATLAB ran_*.m): Logdet is log det of its own M, Trace is tr(M^{-1} dM) with dM
+    from its own ran_dvp, and ran_dvp's dK_f / dK_l blocks are the central differences of the noise-free
+    Nystrom K1' K11^{-1} K1 (plus the f^2 I of mu)."""
+    import ran_spec as R
+    rng = np.random.default_rng(5)
+    n, d, k = 60, 3, 12
+    X = rng.random((n, d))
+    win = [[0], [1], [2]]
+    perm = rng.permutation(n)
+    theta = np.array([1.1, 0.2, 0.03])
+    P = R.ran_setup(X, win, *theta, perm, k)
+    Minv = np.column_stack([R.ran_solve(P, e) for e in np.eye(n)])
+    M = np.linalg.inv(Minv)
+    assert R.ran_logdet(P) == pytest.approx(np.linalg.slogdet(M)[1], rel=1e-9)
+    dM = [np.column_stack([R.ran_dvp(P, e)[g] for e in np.eye(n)]) for g in range(3)]
+    np.testing.assert_allclose(R.ran_trace(P), [np.trace(Minv @ g) for g in dM], rtol=1e-7)
+
+    def nys(t):
+        K1, _ = R.additive_noise_free(X, win, t[0], t[1], perm[:k], np.arange(n))
+        K11, _ = R.additive_noise_free(X, win, t[0], t[1], perm[:k], perm[:k])
+        return K1.T @ np.linalg.solve(K11, K1)
+
+    for g in range(2):
+        h = 1e-5 * theta[g]
+        tp, tm = theta.copy(), theta.copy()
+        tp[g] += h
+        tm[g] -= h
+        fd = (nys(tp) - nys(tm)) / (2 * h)
+        np.testing.assert_allclose(dM[g], fd, rtol=1e-5, atol=1e-7 * np.abs(fd).max())

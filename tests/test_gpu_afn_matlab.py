@@ -69,3 +69,29 @@ def test_afn_gradients_match_matlab_spec(torch_cuda, n, d, k, lfil, theta):
     for g in range(3):
         assert rel(y[g * n:(g + 1) * n], S.afn_solve(R, spec[g])) < 1e-8, g
     P.free()
+
+
+@pytest.mark.parametrize("n,d,k,theta", [(400, 6, 24, (1.2, 0.15, 0.04)), (300, 4, 40, (0.9, 0.1, 0.01))])
+def test_nystrom_gradients_match_matlab_ran_spec(torch_cuda, n, d, k, theta):
+    """The Nystrom with gradients on landmarks perm[:k] (Nfft4GPAmdPrecondNys*, k11 mode 1; the AFN flow's
+    Nystrom branches) against MATLAB's ran_setup.m / ran_solve.m / ran_logdet.m / ran_trace.m / ran_dvp.m
+    (oracle/ran_spec.py) on the additive kernel of 1-D windows: apply 1e-9, Logdet 1e-10, Trace and
+    M^{-1} ran_dvp 1e-7 (MATLAB shifts K11 by sqrt(n) eps(||K1||_2) and S by -nu, nys.c by sqrt(k) ulp(||K11||_F):
+    rounding-level differences in the factors, amplified by K11's conditioning)."""
+    import ran_spec as R
+    from test_gpu_nys_grad import AmdNys
+    rng = np.random.default_rng(n + k)
+    X = rng.random((n, d))
+    win = np.arange(d, dtype=np.int32)
+    perm = rng.permutation(n).astype(np.int32)
+    P = AmdNys(X, win, d, 1, 0, *theta, k, perm, grad=True, k11_mode=1)
+    Rs = R.ran_setup(X, [[c] for c in range(d)], *theta, perm, k)
+    r = rng.random(n) - 0.5
+    assert rel(P.solve(r), R.ran_solve(Rs, r)) < 1e-9
+    assert P.logdet() == pytest.approx(R.ran_logdet(Rs), rel=1e-10)
+    np.testing.assert_allclose(P.trace(), R.ran_trace(Rs), rtol=1e-7)
+    y = P.dvp(r)
+    spec = R.ran_dvp(Rs, r)
+    for g in range(3):
+        assert rel(y[g * n:(g + 1) * n], R.ran_solve(Rs, spec[g])) < 1e-7, g
+    P.free()
