@@ -238,11 +238,16 @@ def test_distributed_pcg_matches_single_gpu(gloo2, single, kind, part):
 @pytest.mark.parametrize("kind", ["1d", "md"])
 def test_component_split_chunked_allreduce_is_bitwise(gloo2, kind):
     """the component split all-reduces y in pieces on its own stream, each overlapping the
-    next piece's interpolation; 1, 4 (default) and 7 pieces give the same bits (elementwise sums)."""
+    next piece's interpolation.  The pieces are disjoint slices summed element for element, so 1, 4 (default)
+    and 7 pieces compute the same sums; the interpolation's ds_add_f64 order follows the wave schedule, so
+    two matvecs of the same x differ at rounding level anyway: compared to 1e-14, and every
+    rank holds the same bits (multi-feature windows keep the single all-reduce)."""
     for r in gloo2:
-        np.testing.assert_array_equal(r[f"{kind}_components_y"], r[f"{kind}_components_y1"])
-        np.testing.assert_array_equal(r[f"{kind}_components_y"], r[f"{kind}_components_y7"])
-        np.testing.assert_array_equal(r[f"{kind}_components_yb"], r[f"{kind}_components_yb1"])
+        assert rel(r[f"{kind}_components_y1"], r[f"{kind}_components_y"]) < 1e-14
+        assert rel(r[f"{kind}_components_y7"], r[f"{kind}_components_y"]) < 1e-14
+        assert rel(r[f"{kind}_components_yb1"], r[f"{kind}_components_yb"]) < 1e-14
+    for key in ("y", "y1", "y7", "yb", "yb1"):
+        np.testing.assert_array_equal(gloo2[0][f"{kind}_components_{key}"], gloo2[1][f"{kind}_components_{key}"])
 
 
 def test_row_sharded_nystrom_setup(gloo2, single):
