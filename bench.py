@@ -345,6 +345,26 @@ def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000
             key + "_total_s": t_setup + t, key + "_apply_ms": 1e3 * t_apply}
 
 
+class _StdoutToStderr:
+    """The reference's loss prints progress with printf (gp_loss.c 'Transform ...'); the bench's stdout must
+    carry only the JSON line, so C-level stdout goes to stderr inside this block."""
+
+    def __enter__(self):
+        import ctypes
+        self.libc = ctypes.CDLL(None)
+        sys.stdout.flush()
+        self.libc.fflush(None)
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        self.libc.fflush(None)
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def run_loss(op, torch, n, d, X, rng_seed=906, maxits=50, nvecs=10, rows=None, dist=None):
     """One log-marginal-likelihood + gradient evaluation (Nfft4GPGpLoss, gp_loss.c:96-307: FGMRES for K^-1 y,
     stochastic Lanczos quadrature with nvecs Rademacher probes of maxits steps, the gradient matvecs) on the
@@ -362,9 +382,10 @@ def run_loss(op, torch, n, d, X, rng_seed=906, maxits=50, nvecs=10, rows=None, d
     if dist is not None:
         dist.barrier()
     t0 = time.time()
-    loss, grad = amd.gp_loss(X, win, d, 1, y[rb:re], (1.0, 1.0, 0.01), maxits=maxits, nvecs=nvecs, rademacher=Rl,
-                             tol=1e-6, transform=3, op=op)
-    torch.cuda.synchronize()
+    with _StdoutToStderr():
+        loss, grad = amd.gp_loss(X, win, d, 1, y[rb:re], (1.0, 1.0, 0.01), maxits=maxits, nvecs=nvecs,
+                                 rademacher=Rl, tol=1e-6, transform=3, op=op)
+        torch.cuda.synchronize()
     t = time.time() - t0
     if dist is not None:
         tt = torch.tensor([t], dtype=torch.float64, device="cuda")
