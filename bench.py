@@ -279,12 +279,17 @@ def run_pcg_nystrom(op, torch, n, k, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=
             "pcg_nys_setup_samples_s": setups, "nys_setup_mfma": mfma}
 
 
-def run_fgmres(op, torch, n, rng_seed=906, tol=1e-6, kdim=50, maxits=3000, l=1.0, rows=None, dist=None):
+def run_fgmres(op, torch, n, rng_seed=906, tol=1e-6, kdim=1000, maxits=1000, l=1.0, rows=None, dist=None, ortho=0):
     """FGMRES (the reference's solver for this system, gp_loss.c:199-213; fgmres.c:3-252) to 1e-6 at the
-    metric's own l = 1, where the NFFT-approximated kernel is indefinite and CG cannot run; restart
-    dimension kdim.  With a distributed operator every rank runs it on its rows (time: max over ranks)."""
+    metric's own l = 1, where the NFFT-approximated kernel is indefinite and CG cannot run.  The spectrum
+    has ~1000 outlying Fourier modes around mu = 0.01, so a restarted FGMRES stagnates (restart 50: 2.7e-2
+    after 3000 iterations; tools/fgmres_probe.py) and it runs unrestarted (kdim = maxits = 1000; converges
+    in ~330).  ortho 0: the reference's modified Gram-Schmidt; 1: two block classical passes
+    (Nfft4GPAmdSetFgmresOrtho).  With a distributed operator every rank runs it on its rows (time: max over
+    ranks)."""
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
     assert op.setup(amd.GAUSSIAN, f=1.0, l=l, mu=0.01) == 0
+    amd.lib().Nfft4GPAmdSetFgmresOrtho(ortho)
     rb, re = rows if rows is not None else (0, n)
     b = torch.tensor((np.random.default_rng(rng_seed + 1).random(n) - 0.5)[rb:re], device="cuda")
     x = torch.zeros(re - rb, dtype=torch.float64, device="cuda")
@@ -295,12 +300,15 @@ def run_fgmres(op, torch, n, rng_seed=906, tol=1e-6, kdim=50, maxits=3000, l=1.0
     _, relres, hist, iters = amd.fgmres(op, b, x, kdim=kdim, maxits=maxits, tol=tol)
     torch.cuda.synchronize()
     t = time.time() - t0
+    amd.lib().Nfft4GPAmdSetFgmresOrtho(0)
     if dist is not None:
         tt = torch.tensor([t], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
-    return {"fgmres_time_s": t, "fgmres_iters": iters, "fgmres_rel_res": relres, "fgmres_converged": relres <= tol,
-            "fgmres_tol": tol, "fgmres_l": l, "fgmres_kdim": kdim, "fgmres_ms_per_iter": 1e3 * t / max(iters, 1)}
+    p = "fgmres_" if ortho == 0 else "fgmres_cgs2_"
+    return {p + "time_s": t, p + "iters": iters, p + "rel_res": relres, p + "converged": relres <= tol,
+            p + "tol": tol, p + "l": l, p + "kdim": kdim, p + "ms_per_iter": 1e3 * t / max(iters, 1),
+            p + "ortho": "modified Gram-Schmidt (fgmres.c)" if ortho == 0 else "block classical Gram-Schmidt x2"}
 
 
 def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1, schur="fsai",
@@ -507,6 +515,7 @@ def main():
     if world == 1 and not args.no_pcg:
         pcg.update(run_loss(op, torch, n, d, X))
         pcg.update(run_fgmres(op, torch, n))
+        pcg.update(run_fgmres(op, torch, n, ortho=1))
         pcg.update(run_pcg_single(op, torch, n))
         if args.nys_rank > 0:
             try:
@@ -578,7 +587,7 @@ def main():
                "all_reduce_bytes_per_matvec": 8 * (op2.n if other == "components" else d * 64)}
         if not args.no_pcg:
             alt.update(run_pcg_single(op2, torch, n, rows=(op2.row_begin, op2.row_end), dist=dist))
-            alt.update(run_fgmres(op2, torch, n, rows=(op2.row_begin, op2.row_end), dist=dist))
+            alt.update(run_fgmres(op2, torch, n, rows=(op2.row_begin, op2.row_end), dist=dist, ortho=1))
         op2.free()
         op, xd, yd = op_main, xd_main, yd_main
     headline = n == 1_000_000 and d == 32
@@ -663,6 +672,7 @@ def main():
             result.update(run_pcg_single(op, torch, n, rows=(rb, re), dist=dist))
             result["pcg_impl"] = f"Nfft4GPSolverPcg on Nfft4GPAmdDistMatSymv ({args.partition}), device-controlled"
             result.update(run_fgmres(op, torch, n, rows=(rb, re), dist=dist))
+            result.update(run_fgmres(op, torch, n, rows=(rb, re), dist=dist, ortho=1))
             result.update(run_loss(op, torch, n, d, X, rows=(rb, re), dist=dist))
         result["partition_" + alt["partition"]] = alt
     if rank == 0:

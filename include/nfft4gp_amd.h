@@ -209,6 +209,10 @@ int Nfft4GPAmdPcgHistoryLength(void);
  * Same signatures and results as the reference; every n-vector lives in HBM, callbacks follow the PCG
  * rules above (this library's operators/preconditioners get device pointers, others host vectors).
  * prel_res_v / TDp / TEp are malloc'ed (free with free()). */
+/* FGMRES's orthogonalisation: 0 (default) the reference's modified Gram-Schmidt (Nfft4GPModifiedGS,
+ * matops.c:274-346: one launch per basis vector), 1 two block classical Gram-Schmidt passes (a fixed four
+ * launches per step; the same projections up to rounding; kdim <= 2046).  Env NFFT4GP_AMD_FGMRES_ORTHO. */
+void Nfft4GPAmdSetFgmresOrtho(int ortho);
 /* SRC/solvers/fgmres.c:3-252 (MGS without re-orthogonalisation; kdim <= 4094) */
 int Nfft4GPSolverFgmres(void *mat_data, int n, func_symmatvec matvec, void *prec_data, func_solve precondfunc,
                         NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs, int kdim, int maxits, int atol, NFFT4GP_DOUBLE tol,

@@ -170,6 +170,7 @@ _SIGS = {
     "Nfft4GPAmdDistFree": (None, [vp]),
     "Nfft4GPAmdDistMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),
     "Nfft4GPAmdDistSetChunks": (C.c_int, [vp, C.c_int]),
+    "Nfft4GPAmdSetFgmresOrtho": (None, [C.c_int]),
     "Nfft4GPAmdDistGradMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),
     "Nfft4GPAmdDistGaussianKernel": (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, C.c_int, vp,
                                               vp]),

@@ -386,6 +386,19 @@ int tridiag_eig(int m, const double* d, const double* e, std::vector<double>& w,
 
 namespace nfft4gp_amd {
 
+// FGMRES orthogonalisation: 0 = the reference's modified Gram-Schmidt (Nfft4GPModifiedGS, one launch per
+// basis vector), 1 = two block classical Gram-Schmidt passes (the Lanczos re-orthogonalisation's kernels:
+// four launches per step whatever its length, the basis read four times) -- Nfft4GPAmdSetFgmresOrtho
+int g_fgmres_ortho = -1;
+int fgmres_ortho()
+{
+   if (g_fgmres_ortho < 0) {
+      const char* e = getenv("NFFT4GP_AMD_FGMRES_ORTHO");
+      g_fgmres_ortho = (e && atoi(e) == 1) ? 1 : 0;
+   }
+   return g_fgmres_ortho;
+}
+
 // ---- FGMRES (fgmres.c:3-252) on device vectors ----------------------------------------------------
 int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits, int atol, double tol,
                double* prel_res, double** prel_res_v, int* piter, int print_level)
@@ -407,8 +420,10 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
       *prel_res_v = rel_hist(1);
       return 0;
    }
-   if (kdim + 2 > KScratch::kScal) {
-      fprintf(stderr, "nfft4gp_amd: Nfft4GPSolverFgmres: restart dimension %d above %d\n", kdim, KScratch::kScal - 2);
+   const int ortho = fgmres_ortho();
+   const int kmax = ortho ? KScratch::kScal / 2 - 2 : KScratch::kScal - 2;
+   if (kdim > kmax) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPSolverFgmres: restart dimension %d above %d\n", kdim, kmax);
       return -1;
    }
    double *V = nullptr, *Z = nullptr;
@@ -471,14 +486,24 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
                return -1;
             }
          }
-         // Nfft4GPModifiedGS (matops.c:274-346) with k = i-1, no re-orthogonalisation
          double* hd = g_k.scal;
-         for (int j = 0; j < i; j++)
-            if (c.gs(w, j ? V + (size_t)(j - 1) * n : nullptr, j ? hd + j - 1 : nullptr, V + (size_t)j * n, hd + j))
-               return -1;
-         if (c.gs(w, V + (size_t)(i - 1) * n, hd + i - 1, nullptr, hd + i)) return -1;
          std::vector<double> hcol(i + 1);
-         if (c.read(hd, i + 1, hcol.data())) return -1;
+         if (ortho == 0) {
+            // Nfft4GPModifiedGS (matops.c:274-346) with k = i-1, no re-orthogonalisation
+            for (int j = 0; j < i; j++)
+               if (c.gs(w, j ? V + (size_t)(j - 1) * n : nullptr, j ? hd + j - 1 : nullptr, V + (size_t)j * n, hd + j))
+                  return -1;
+            if (c.gs(w, V + (size_t)(i - 1) * n, hd + i - 1, nullptr, hd + i)) return -1;
+            if (c.read(hd, i + 1, hcol.data())) return -1;
+         } else {
+            // two classical passes: h = V^T w, w -= V h, twice; H(:, i) = h1 + h2, ||w|| after the second
+            double* hd2 = hd + i + 2;
+            if (c.block_gs(w, V, V, i, hd) || c.block_gs(w, V, V, i, hd2)) return -1;
+            std::vector<double> hh(2 * i + 3);
+            if (c.read(hd, 2 * i + 3, hh.data())) return -1;
+            for (int j = 0; j < i; j++) hcol[j] = hh[j] + hh[i + 2 + j];
+            hcol[i] = hh[2 * i + 2];
+         }
          const double t = std::sqrt(hcol[i]);
          double* Hc = H.data() + (size_t)(i - 1) * (kdim + 1);
          for (int j = 0; j < i; j++) Hc[j] = hcol[j];
@@ -1008,6 +1033,8 @@ bool make_callbacks(Callbacks& cb, int n, func_symmatvec matvec, void* mat, func
 }  // namespace
 
 extern "C" {
+
+void Nfft4GPAmdSetFgmresOrtho(int ortho) { g_fgmres_ortho = (ortho == 1) ? 1 : 0; }
 
 int Nfft4GPSolverFgmres(void* mat_data, int n, func_symmatvec matvec, void* prec_data, func_solve precondfunc,
                         double* x, double* rhs, int kdim, int maxits, int atol, double tol, double* prel_res,

@@ -957,6 +957,12 @@ int Nfft4GPAmdShardFinish(void* str, const double* grid, int grad, double alpha,
       if (md_grid(P, grid, grad, s)) return -1;
       return md_interp(P, grad, alpha, x_local, beta, y_local, s);
    }
+   // few blocks (a row shard of a few GPUs): S interpolation workgroups per block so the launch fills the
+   // CUs (NFFT4GP_AMD_SHARD_SPLIT overrides S; 1 = one workgroup per block)
+   int S = std::max(1, std::min(4, 256 / std::max(1, P.nblocks)));
+   if (const char* e = getenv("NFFT4GP_AMD_SHARD_SPLIT")) S = std::max(1, std::min(16, atoi(e)));
+   S = std::min(S, std::max(1, P.ngroups));
+   if (!grad && S > 1 && !P.timing) return launch_shard_finish_split(P, grid, alpha, x_local, beta, y_local, S, s);
    if (launch_grid_from_sum(P, grid, grad, s)) return -1;
    return launch_interp(P, grad, alpha, x_local, beta, y_local, s);
 }

@@ -472,6 +472,75 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
    if (grad) grid_tail(comp, s_g, wd, Hd, s_w, s_h);
 }
 
+// Row shards with few blocks, split interpolation (launch_shard_finish_split): the grid kernel from the summed
+// grids also initialises y = beta y + alpha f^2 mu diag x (a grid-stride loop over all its threads), and the
+// interpolation runs S workgroups per block, each over a contiguous range of window groups, adding alpha f^2
+// times its LDS y-slice into y with global atomics.  A shard of config C on 8 GPUs has 62 blocks: the
+// one-workgroup-per-block interpolation runs on 62 of the 256 CUs.
+__global__ __launch_bounds__(kGridThreads) void k_grid_sum_yinit(const double* __restrict__ gsum,
+                                                                const double* __restrict__ w, double* __restrict__ H,
+                                                                double* __restrict__ y, const double* __restrict__ x,
+                                                                int n, double beta, double amu)
+{
+   __shared__ double s_g[kNos];
+   __shared__ double s_h[kNos];
+   __shared__ double s_w[kNos];
+   const int comp = blockIdx.x;
+   const int tid = threadIdx.x;
+   for (size_t j = (size_t)blockIdx.x * kGridThreads + tid; j < (size_t)n; j += (size_t)gridDim.x * kGridThreads)
+      y[j] = (beta == 0.0 ? 0.0 : beta * y[j]) + amu * x[j];
+   if (tid < kNos) s_g[tid] = gsum[(size_t)comp * kNos + tid];
+   __syncthreads();
+   grid_tail(comp, s_g, w, H, s_w, s_h);
+}
+
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_interp_part(const uint16_t* __restrict__ meta,
+                                                        const uint32_t* __restrict__ lo,
+                                                        const uint32_t* __restrict__ qarr,
+                                                        const int* __restrict__ tile_off, const double* __restrict__ H,
+                                                        double* __restrict__ y, int n, int B, int ngroups, int S,
+                                                        double scale)
+{
+   extern __shared__ __attribute__((aligned(16))) double smem[];
+   double* s_y = smem;
+   const int b = blockIdx.x / S, part = blockIdx.x % S;
+   const int g0 = part * ngroups / S, g1 = (part + 1) * ngroups / S;
+   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+   constexpr int nwaves = THREADS / 64;
+   const int base = b * B;
+   const int nloc = min(B, n - base);
+   const int t1 = tile_off[b * ngroups + g1];
+   int t = tile_off[b * ngroups + g0] + wave;
+   TileRegs cur;
+   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
+   for (int i = tid; i < B + kPad; i += THREADS) s_y[i] = 0.0;
+   __syncthreads();
+   for (; t < t1; t += nwaves) {
+      const size_t hoff = (size_t)cur.mt * kNC;
+      double hc[kNC];
+#pragma unroll
+      for (int d = 0; d < kNC; d += 2) {
+         const double2 v = *reinterpret_cast<const double2*>(H + hoff + d);
+         hc[d] = v.x;
+         hc[d + 1] = v.y;
+      }
+#pragma unroll
+      for (int r = 0; r < kR; r++) {
+         const uint32_t loc = slot_loc(cur, r);
+         const double u = q_to_u(cur.qq[r]);
+         double v = hc[kNC - 1];
+#pragma unroll
+         for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
+         atomicAdd(s_y + loc, v);
+      }
+      const int tn = t + nwaves;
+      if (tn < t1) load_tile(cur, meta, lo, qarr, tn, lane);
+   }
+   __syncthreads();
+   for (int j = tid; j < nloc; j += THREADS) atomicAdd(y + (size_t)base + j, scale * s_y[j]);
+}
+
 // gsum[comp][cell] = sum_b part[comp][b][cell]   (row-sharded path: before the all-reduce).  One
 // workgroup per window, k_grid's 16 strands per cell with 16 loads in flight each (a thread per cell
 // summing the partials one after another took 16 us at an 8-GPU shard of config C)
@@ -894,6 +963,27 @@ int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int gra
 {
    launch_ev(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, P.kev ? P.kev + 2 : nullptr, d_gridsum, 1,
              (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 1, 0ll, 0ll);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, double alpha, const double* d_x,
+                              double beta, double* d_y, int S, hipStream_t stream)
+{
+   constexpr int T = 512;
+   static bool attr = false;
+   if (!attr) {
+      (void)hipFuncSetAttribute((const void*)k_interp_part<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipGetLastError();
+      attr = true;
+   }
+   const double ff = P.f * P.f;
+   hipLaunchKernelGGL(k_grid_sum_yinit, dim3(P.nw), dim3(kGridThreads), 0, stream, d_gridsum, (const double*)P.d_w,
+                      P.d_H, d_y, d_x, P.n, beta, alpha * ff * P.mu * P.diag);
+   if (P.n > 0)
+      hipLaunchKernelGGL(k_interp_part<T>, dim3(P.nblocks * S), dim3(T), sizeof(double) * (size_t)(P.B + kPad), stream,
+                         P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H, d_y, P.n, P.B, P.ngroups, S,
+                         alpha * ff);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

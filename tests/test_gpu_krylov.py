@@ -198,3 +198,27 @@ def test_gp_loss_wrapper(torch_cuda, case):
                              maxits=int(k["maxits"]), nvecs=int(k["nvecs"]), rademacher=k["rademacher"], tol=1e-8)
     assert loss == pytest.approx(float(k["loss_nfft"]), rel=1e-8)
     np.testing.assert_allclose(grad, k["grad_nfft"], rtol=1e-6, atol=1e-9)
+
+
+def test_fgmres_block_cgs2_matches_mgs(torch_cuda):
+    """Nfft4GPAmdSetFgmresOrtho(1): two block classical Gram-Schmidt passes instead of the reference's MGS
+    (matops.c:274-346) give the same iterations, history (1e-8) and solution (1e-9) on the NFFT operator."""
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    torch = torch_cuda
+    n, d = 30000, 8
+    rng = np.random.default_rng(17)
+    X = rng.random((n, d))
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    assert op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) == 0
+    b = torch.tensor(rng.random(n) - 0.5, device="cuda")
+    res = []
+    for ortho in (0, 1):
+        amd.lib().Nfft4GPAmdSetFgmresOrtho(ortho)
+        x = torch.zeros_like(b)
+        _, rr, hist, it = amd.fgmres(op, b, x, kdim=400, maxits=400, tol=1e-8)
+        res.append((x.cpu().numpy(), rr, hist[:it + 1], it))
+    amd.lib().Nfft4GPAmdSetFgmresOrtho(0)
+    assert res[0][3] == res[1][3] > 0 and res[1][1] <= 1e-8
+    np.testing.assert_allclose(res[1][2], res[0][2], rtol=1e-8)
+    assert np.linalg.norm(res[1][0] - res[0][0]) <= 1e-9 * np.linalg.norm(res[0][0])
+    op.free()

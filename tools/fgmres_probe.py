@@ -14,3 +14,10 @@ for kdim in [int(a) for a in sys.argv[1:]]:
     torch.cuda.synchronize()
     h = hist[:it+1]
     print(kdim, "iters", it, "rel", rr, "time", round(time.time()-t0, 3), "hist@", [float("%.2e" % h[i]) for i in range(0, len(h), max(1, len(h)//10))], flush=True)
+# block CGS2 orthogonalisation (Nfft4GPAmdSetFgmresOrtho(1)) at the largest restart dimension given
+amd.lib().Nfft4GPAmdSetFgmresOrtho(1)
+kdim = int(sys.argv[-1])
+xs = torch.zeros_like(b); torch.cuda.synchronize(); t0 = time.time()
+_, rr, hist, it = amd.fgmres(op, b, xs, kdim=kdim, maxits=kdim, tol=1e-6)
+torch.cuda.synchronize()
+print("cgs2", kdim, "iters", it, "rel", rr, "time", round(time.time()-t0, 3), flush=True)
