@@ -342,6 +342,21 @@ def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000
         pre.solve(x, r)
     torch.cuda.synchronize()
     t_apply = (time.time() - t1) / 10
+    # the same solve with the apply's K12 (or the Nystrom branch's U) read as an fp32 copy, fp64 accumulation
+    pre.set_storage(32)
+    x32 = torch.zeros(n, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    t1 = time.time()
+    _, relres32, _, iters32 = amd.pcg(op, b, x32, maxits=maxits, tol=tol, precond=pre)
+    torch.cuda.synchronize()
+    t32 = time.time() - t1
+    pre.solve(x, r)
+    torch.cuda.synchronize()
+    t1 = time.time()
+    for _ in range(10):
+        pre.solve(x, r)
+    torch.cuda.synchronize()
+    t_apply32 = (time.time() - t1) / 10
     kind, rank = pre.kind, pre.k
     pre.free()
     key = "pcg_afn" if schur == "fsai" else "pcg_afn_" + schur
@@ -350,7 +365,8 @@ def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000
     return {key + "_max_k": k, key + "_kind": kind, key + "_rank": rank, key + "_order": order,
             key + "_schur": schur, key + "_schur_lfil": lfil if schur == "fsai" else None,
             key + "_setup_s": t_setup, key + "_time_s": t, key + "_iters": iters, key + "_rel_res": relres,
-            key + "_total_s": t_setup + t, key + "_apply_ms": 1e3 * t_apply}
+            key + "_total_s": t_setup + t, key + "_apply_ms": 1e3 * t_apply, key + "_f32_time_s": t32,
+            key + "_f32_iters": iters32, key + "_f32_rel_res": relres32, key + "_f32_apply_ms": 1e3 * t_apply32}
 
 
 class _StdoutToStderr:

@@ -567,6 +567,13 @@ void Nfft4GPAmdDistNysFree(void *dnys);
  * and their rows of the Schur FSAI G and of G^T.  An apply exchanges the rhs's landmark entries and the
  * K12 y2 partial sums (two k all-reduces) and, with the Schur FSAI, the Schur vector before each sparse
  * product (two (n-k) all-reduces of zero-padded vectors).  func_solve on this rank's rows (device). */
+/* The AFN apply's two K12 passes (2 x 8 k (n - k) bytes, most of an apply) read an fp32 copy of K12 with
+ * fp64 accumulation (bits 32), or the fp64 K12 (64, the default) -- Nfft4GPAmdNysSetStorage's analogue;
+ * the preconditioner stays a fixed symmetric operator either way. */
+int Nfft4GPAmdAfnSetStorage(void *afn, int bits);
+/* The same choice for the setup flow's preconditioner: the AFN's K12 or the Nystrom branch's U (the
+ * gradient-capable branches keep fp64). */
+int Nfft4GPAmdPrecondAFNSetStorage(void *pre, int bits);
 void *Nfft4GPAmdAfnShard(void *afn, int row_begin, int row_end, void *comm);
 int Nfft4GPAmdDistAfnSolve(void *dafn, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
 void Nfft4GPAmdDistAfnFree(void *dafn);

@@ -179,6 +179,8 @@ _SIGS = {
     "Nfft4GPAmdNysShard": (vp, [vp, C.c_int, C.c_int, vp]),
     "Nfft4GPAmdNysShardSetupAdditive": (vp, [vp, vp, C.c_int, C.c_int]),
     "Nfft4GPAmdAfnShard": (vp, [vp, C.c_int, C.c_int, vp]),
+    "Nfft4GPAmdAfnSetStorage": (C.c_int, [vp, C.c_int]),
+    "Nfft4GPAmdPrecondAFNSetStorage": (C.c_int, [vp, C.c_int]),
     "Nfft4GPAmdDistAfnSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdDistAfnFree": (None, [vp]),
     "Nfft4GPAmdDistNysSolve": (C.c_int, [vp, C.c_int, vp, vp]),

@@ -1195,6 +1195,15 @@ int Nfft4GPAmdPrecondAFNSolve(void* pre, int n, double* x, double* rhs)
    return Nfft4GPAmdNysSolve(F->nys, n, x, rhs);
 }
 
+int Nfft4GPAmdPrecondAFNSetStorage(void* pre, int bits)
+{
+   AfnFlow* F = (AfnFlow*)pre;
+   if (!F || (bits != 32 && bits != 64)) return -1;
+   if (F->afn) return Nfft4GPAmdAfnSetStorage(F->afn, bits);
+   if (F->nys) return Nfft4GPAmdNysSetStorage(F->nys, bits);
+   return 0;  // the gradient-capable branches keep their fp64 factors
+}
+
 int Nfft4GPAmdPrecondAFNDvp(void* pre, int n, int* mask, double* x, double** yp)
 {
    AfnFlow* F = (AfnFlow*)pre;

@@ -40,6 +40,7 @@ struct AfnDev {
    double* Linv = nullptr;   // k x k, inverse of the lower Cholesky factor of A11 (column j: rows >= j)
    double* LinvT = nullptr;  // its transpose (column i = row i of Linv)
    double* K12 = nullptr;   // k x n2 column-major
+   float* K12f = nullptr;   // optional fp32 copy the two K12 passes read instead (Nfft4GPAmdAfnSetStorage)
    FsaiDev* S = nullptr;    // FSAI of the Schur complement (n2)
    double schur_scale = 0.0;  // S == NULL, n2 > 0: S^{-1} = schur_scale I (schur_opt 0, afn.c:451-459)
    bool own_S = false;
@@ -113,8 +114,8 @@ __global__ __launch_bounds__(256) void k_trmv(const double* __restrict__ M, int 
 // sum is the same lane-strided sum and shuffle tree as with a wave per column.
 constexpr int kA12tCols = 4;
 constexpr int kA12tLdsMax = 8192;
-template <bool LDS>
-__global__ __launch_bounds__(256) void k_a12t(const double* __restrict__ K12, int k, int n2, const double* __restrict__ y,
+template <bool LDS, typename TK = double>
+__global__ __launch_bounds__(256) void k_a12t(const TK* __restrict__ K12, int k, int n2, const double* __restrict__ y,
                                               double* __restrict__ rp2)
 {
    extern __shared__ double s_y_[];
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(256) void k_a12t(const double* __restrict__ K12, in
    const long long j0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * kA12tCols;
    if (j0 >= n2) return;
    const int nc = (int)std::min<long long>(kA12tCols, n2 - j0);
-   const double* col = K12 + j0 * k;
+   const TK* col = K12 + j0 * k;
    double r[kA12tCols];
 #pragma unroll
    for (int c = 0; c < kA12tCols; c++) r[c] = 0.0;
@@ -135,12 +136,12 @@ __global__ __launch_bounds__(256) void k_a12t(const double* __restrict__ K12, in
       for (int i = lane; i < k; i += 64) {
          const double yi = s_y[i];
 #pragma unroll
-         for (int c = 0; c < kA12tCols; c++) r[c] = fma(col[(size_t)c * k + i], yi, r[c]);
+         for (int c = 0; c < kA12tCols; c++) r[c] = fma((double)col[(size_t)c * k + i], yi, r[c]);
       }
    } else {
       for (int i = lane; i < k; i += 64) {
          const double yi = s_y[i];
-         for (int c = 0; c < nc; c++) r[c] = fma(col[(size_t)c * k + i], yi, r[c]);
+         for (int c = 0; c < nc; c++) r[c] = fma((double)col[(size_t)c * k + i], yi, r[c]);
       }
    }
 #pragma unroll
@@ -154,7 +155,8 @@ __global__ __launch_bounds__(256) void k_a12t(const double* __restrict__ K12, in
 // part[blk][i] = sum_{j in blk} K12[i + j*k] y2[j]; `cols` columns per workgroup, sized at create so
 // that ~2048 workgroups stream K12 (one HBM pass over k x n2)
 constexpr int kA12Blocks = 2048;
-__global__ __launch_bounds__(256) void k_a12_part(const double* __restrict__ K12, int k, int n2, int cols,
+template <typename TK = double>
+__global__ __launch_bounds__(256) void k_a12_part(const TK* __restrict__ K12, int k, int n2, int cols,
                                                   const double* __restrict__ y2, double* __restrict__ part)
 {
    const int j0 = blockIdx.x * cols, j1 = min(n2, j0 + cols);
@@ -162,10 +164,10 @@ __global__ __launch_bounds__(256) void k_a12_part(const double* __restrict__ K12
       double r0 = 0.0, r1 = 0.0;
       int j = j0;
       for (; j + 1 < j1; j += 2) {
-         r0 = fma(K12[i + (size_t)j * k], y2[j], r0);
-         r1 = fma(K12[i + (size_t)(j + 1) * k], y2[j + 1], r1);
+         r0 = fma((double)K12[i + (size_t)j * k], y2[j], r0);
+         r1 = fma((double)K12[i + (size_t)(j + 1) * k], y2[j + 1], r1);
       }
-      if (j < j1) r0 = fma(K12[i + (size_t)j * k], y2[j], r0);
+      if (j < j1) r0 = fma((double)K12[i + (size_t)j * k], y2[j], r0);
       part[(size_t)blockIdx.x * k + i] = r0 + r1;
    }
 }
@@ -310,10 +312,17 @@ int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y);
    // rp2 -= A12^T y
    const dim3 ga((n2 + 4 * kA12tCols - 1) / (4 * kA12tCols));
-   if (k <= kA12tLdsMax)
-      hipLaunchKernelGGL(k_a12t<true>, ga, dim3(256), sizeof(double) * k, s, A->K12, k, n2, A->y, rp2);
-   else
-      hipLaunchKernelGGL(k_a12t<false>, ga, dim3(256), 0, s, A->K12, k, n2, A->y, rp2);
+   if (A->K12f) {
+      if (k <= kA12tLdsMax)
+         hipLaunchKernelGGL((k_a12t<true, float>), ga, dim3(256), sizeof(double) * k, s, (const float*)A->K12f, k, n2,
+                            A->y, rp2);
+      else
+         hipLaunchKernelGGL((k_a12t<false, float>), ga, dim3(256), 0, s, (const float*)A->K12f, k, n2, A->y, rp2);
+   } else if (k <= kA12tLdsMax) {
+      hipLaunchKernelGGL(k_a12t<true>, ga, dim3(256), sizeof(double) * k, s, (const double*)A->K12, k, n2, A->y, rp2);
+   } else {
+      hipLaunchKernelGGL(k_a12t<false>, ga, dim3(256), 0, s, (const double*)A->K12, k, n2, A->y, rp2);
+   }
    // y2 = FSAI(rp2), or rp2 / noise (schur_opt 0)
    if (A->S) {
       if (fsai_apply_dev(A->S, y2, rp2, s)) return -1;
@@ -321,7 +330,12 @@ int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
       hipLaunchKernelGGL(k_scale_into, dim3((n2 + 255) / 256), dim3(256), 0, s, rp2, n2, A->schur_scale, y2);
    }
    // rp -= A12 y2
-   hipLaunchKernelGGL(k_a12_part, dim3(A->nblk), dim3(256), 0, s, A->K12, k, n2, A->cols, y2, A->part);
+   if (A->K12f)
+      hipLaunchKernelGGL(k_a12_part<float>, dim3(A->nblk), dim3(256), 0, s, (const float*)A->K12f, k, n2, A->cols, y2,
+                         A->part);
+   else
+      hipLaunchKernelGGL(k_a12_part<double>, dim3(A->nblk), dim3(256), 0, s, (const double*)A->K12, k, n2, A->cols,
+                         y2, A->part);
    hipLaunchKernelGGL(k_a12_reduce, dim3((k + 15) / 16), dim3(1024), 0, s, A->part, A->nblk, k, A->rp);
    // y = A11 \ rp
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->LinvT, k, A->rp, A->t);
@@ -523,9 +537,10 @@ int afn_shard_apply(AfnShard* S, double* x, const double* r, hipStream_t s)
    if (m2 > 0) {
       const dim3 ga((m2 + 4 * kA12tCols - 1) / (4 * kA12tCols));
       if (k <= kA12tLdsMax)
-         hipLaunchKernelGGL(k_a12t<true>, ga, dim3(256), sizeof(double) * k, s, S->K12, k, m2, S->y1, S->rp2);
+         hipLaunchKernelGGL(k_a12t<true>, ga, dim3(256), sizeof(double) * k, s, (const double*)S->K12, k, m2, S->y1,
+                            S->rp2);
       else
-         hipLaunchKernelGGL(k_a12t<false>, ga, dim3(256), 0, s, S->K12, k, m2, S->y1, S->rp2);
+         hipLaunchKernelGGL(k_a12t<false>, ga, dim3(256), 0, s, (const double*)S->K12, k, m2, S->y1, S->rp2);
    }
    // y2 = G^T G rp2 (each product reads the whole Schur vector: all-gathered), or rp2 / noise
    if (S->fsai) {
@@ -547,7 +562,8 @@ int afn_shard_apply(AfnShard* S, double* x, const double* r, hipStream_t s)
    // rp1 -= A12 y2: this rank's columns' partial sum (negated by k_a12_reduce), summed over the ranks
    NFFT4GP_HIP_CHECK(hipMemsetAsync(S->w, 0, sizeof(double) * k, s));
    if (m2 > 0) {
-      hipLaunchKernelGGL(k_a12_part, dim3(S->nblk), dim3(256), 0, s, S->K12, k, m2, S->cols, S->y2, S->part);
+      hipLaunchKernelGGL(k_a12_part<double>, dim3(S->nblk), dim3(256), 0, s, (const double*)S->K12, k, m2, S->cols,
+                         S->y2, S->part);
       hipLaunchKernelGGL(k_a12_reduce, dim3((k + 15) / 16), dim3(1024), 0, s, S->part, S->nblk, k, S->w);
    }
    if (S->comm->allreduce(S->w, (size_t)k, s)) return -1;
@@ -672,13 +688,40 @@ void Nfft4GPAmdAfnFree(void* afn)
 {
    AfnDev* A = (AfnDev*)afn;
    if (!A) return;
-   for (void* p : {(void*)A->perm, (void*)A->Linv, (void*)A->LinvT, (void*)A->K12, (void*)A->rp, (void*)A->y,
-                   (void*)A->t, (void*)A->part})
+   for (void* p : {(void*)A->perm, (void*)A->Linv, (void*)A->LinvT, (void*)A->K12, (void*)A->K12f, (void*)A->rp,
+                   (void*)A->y, (void*)A->t, (void*)A->part})
       (void)hipFree(p);
    // the Schur complement's FSAI handle stays with its creator (Nfft4GPAmdFsaiFree) unless the AFN was
    // set up on the device (Nfft4GPAmdAfnSetup), which owns it
    if (A->own_S) fsai_free(A->S);
    delete A;
+}
+
+__global__ void k_afn_to_f32(const double* __restrict__ a, size_t count, float* __restrict__ b)
+{
+   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x)
+      b[i] = (float)a[i];
+}
+
+int Nfft4GPAmdAfnSetStorage(void* afn, int bits)
+{
+   AfnDev* A = (AfnDev*)afn;
+   if (!A || (bits != 32 && bits != 64)) return -1;
+   hipStream_t s = current_stream();
+   if (bits == 64) {
+      if (A->K12f) {
+         NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
+         NFFT4GP_HIP_CHECK(hipFree(A->K12f));
+         A->K12f = nullptr;
+      }
+      return 0;
+   }
+   if (A->K12f || !A->K12) return 0;
+   const size_t count = (size_t)A->k * A->n2;
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&A->K12f, sizeof(float) * std::max<size_t>(1, count)));
+   hipLaunchKernelGGL(k_afn_to_f32, dim3(4096), dim3(256), 0, s, (const double*)A->K12, count, A->K12f);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
 }
 
 void* Nfft4GPAmdAfnShard(void* afn, int row_begin, int row_end, void* comm)

@@ -957,9 +957,11 @@ int Nfft4GPAmdShardFinish(void* str, const double* grid, int grad, double alpha,
       if (md_grid(P, grid, grad, s)) return -1;
       return md_interp(P, grad, alpha, x_local, beta, y_local, s);
    }
-   // few blocks (a row shard of a few GPUs): S interpolation workgroups per block so the launch fills the
-   // CUs (NFFT4GP_AMD_SHARD_SPLIT overrides S; 1 = one workgroup per block)
-   int S = std::max(1, std::min(4, 256 / std::max(1, P.nblocks)));
+   // few blocks (a row shard of many GPUs): S interpolation workgroups per block so the launch fills more
+   // CUs.  Measured per-rank matvec at config C (tools/shard_probe.py, S = 1 / 2 / 4 / 8): 8 GPUs (62 blocks)
+   // 31.1 / 31.3 / 29.3 / 32.1 us; 4 GPUs (123 blocks) 41.0 / 43.0 / 45.2 / 50.5; 2 GPUs 59.7 / 66.8 / ...
+   // so S = 4 at <= 64 blocks, else 1 (NFFT4GP_AMD_SHARD_SPLIT overrides S)
+   int S = P.nblocks <= 64 ? 4 : 1;
    if (const char* e = getenv("NFFT4GP_AMD_SHARD_SPLIT")) S = std::max(1, std::min(16, atoi(e)));
    S = std::min(S, std::max(1, P.ngroups));
    if (!grad && S > 1 && !P.timing) return launch_shard_finish_split(P, grid, alpha, x_local, beta, y_local, S, s);

@@ -205,6 +205,13 @@ class AfnPrecond(_Apply):
         self.k = kk.value
         return self
 
+    def set_storage(self, bits: int):
+        """K12 read by the apply's two passes in fp64 (64, the reference's) or as an fp32 copy (32; fp64
+        accumulation), Nfft4GPAmdAfnSetStorage."""
+        if _lib.lib().Nfft4GPAmdAfnSetStorage(self.h, int(bits)):
+            raise ValueError("storage bits must be 32 or 64")
+        return self
+
     def info(self):
         """(k, perm, (ia, ja, aa) of the Schur complement's FSAI or None)"""
         L = _lib.lib()
@@ -254,6 +261,13 @@ class PrecondAFN(_Apply):
         kind, k = C.c_int(), C.c_int()
         L.Nfft4GPAmdPrecondAFNInfo(self.h, C.byref(kind), C.byref(k), None, None)
         self.kind, self.k = self.KINDS[kind.value], k.value
+
+    def set_storage(self, bits: int):
+        """The AFN's K12 / the Nystrom branch's U read in fp64 (64) or as an fp32 copy (32; fp64 accumulation),
+        Nfft4GPAmdPrecondAFNSetStorage; the gradient-capable branches keep fp64."""
+        if _lib.lib().Nfft4GPAmdPrecondAFNSetStorage(self.h, int(bits)):
+            raise ValueError("storage bits must be 32 or 64")
+        return self
 
     def dvp(self, x, mask=None):
         """[M^{-1} dM/df x, M^{-1} dM/dl x, M^{-1} dM/dmu x] (3 n, host numpy or a GPU tensor like x)."""

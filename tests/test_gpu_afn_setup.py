@@ -320,3 +320,38 @@ def test_afn_setup_schur_noise_matches_restatement(torch_cuda):
     x = np.zeros_like(r)
     pre.solve(x, r.copy())
     assert rel(x, O.afn_apply(perm, L11, K12, lambda v: v / mu, r.copy())) <= 1e-9
+
+
+def test_afn_fp32_k12_storage_pcg(torch_cuda):
+    """Nfft4GPAmdAfnSetStorage(32) / Nfft4GPAmdPrecondAFNSetStorage(32): the apply's two K12 passes read an
+    fp32 copy (fp64 accumulation).  The apply moves by ~1e-7 relative; PCG stops on its fp64 true residual
+    (pcg.c:181-193), so it reaches the same tolerance in about as many iterations; back to 64 is bitwise the
+    fp64 apply."""
+    torch = torch_cuda
+    rng = np.random.default_rng(29)
+    n, d, f, l, mu, k = 20000, 8, 1.0, 0.2, 0.01, 256
+    X = np.asfortranarray(rng.random((n, d)))
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    op.setup(amd.GAUSSIAN, f, l, mu)
+    for pre in (amd.AfnPrecond.setup(X, k, f, l, mu, perm_opt="fps", schur_lfil=20, op=op),
+                amd.PrecondAFN(X, -k, schur_lfil=20, op=op)):
+        r = torch.tensor(rng.random(n) - 0.5, device="cuda")
+        z64 = torch.zeros(n, dtype=torch.float64, device="cuda")
+        pre.solve(z64, r.clone())
+        b = torch.tensor(rng.random(n) - 0.5, device="cuda")
+        _, rr64, _, it64 = amd.pcg(op, b, torch.zeros_like(b), maxits=3000, tol=1e-6, precond=pre)
+        pre.set_storage(32)
+        z32 = torch.zeros(n, dtype=torch.float64, device="cuda")
+        pre.solve(z32, r.clone())
+        assert rel(z32.cpu().numpy(), z64.cpu().numpy()) < 1e-5
+        assert not torch.equal(z32, z64)  # the fp32 copy is what the apply read
+        _, rr32, _, it32 = amd.pcg(op, b, torch.zeros_like(b), maxits=3000, tol=1e-6, precond=pre)
+        assert it64 > 0 and it32 > 0 and rr32 <= 1e-6
+        assert abs(it32 - it64) <= max(2, it64 // 10), (it32, it64)
+        pre.set_storage(64)
+        z = torch.zeros(n, dtype=torch.float64, device="cuda")
+        pre.solve(z, r.clone())
+        assert torch.equal(z, z64)
+        with pytest.raises(ValueError):
+            pre.set_storage(16)
+        pre.free()
