@@ -247,7 +247,8 @@ template <int P>
 __global__ __launch_bounds__(kKnnThreads) void k_knn_bounded(const double* __restrict__ X, int ldim, int n, int d,
                                                              int lfil, const int* __restrict__ ia,
                                                              int* __restrict__ ja, int* __restrict__ fail,
-                                                             int* __restrict__ nfail)
+                                                             int* __restrict__ nfail, const int* __restrict__ rows,
+                                                             int nrows)
 {
    constexpr int R = kKnnRows;
    __shared__ double q[kKnnMaxDims2][R];
@@ -257,16 +258,20 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn_bounded(const double* __res
    __shared__ int s_idx[R][kKnnGather2 + kFsaiMaxK];
    __shared__ unsigned long long s_tau[R];
    __shared__ int s_base[R], s_bstar[R], s_ok[R];
-   __shared__ int s_nsel[R], s_ngat[R];
+   __shared__ int s_nsel[R], s_ngat[R], s_row[R];
    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
    const int K = lfil - 1;
-   const int ngroups = (n - lfil + R - 1) / R;
+   // rows: ascending row indices (nrows of them) instead of lfil..n-1
+   const int nall = rows ? nrows : n - lfil;
+   const int ngroups = (nall + R - 1) / R;
    for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
-      const int i0 = lfil + g * R;
-      const int nr = min(R, n - i0);
+      const int nr = min(R, nall - g * R);
+      const int i0 = rows ? rows[g * R] : lfil + g * R;
+      if (tid < R) s_row[tid] = tid < nr ? (rows ? rows[g * R + tid] : i0 + tid) : n;
+      __syncthreads();
       for (int e = tid; e < R * d; e += kKnnThreads) {
          const int r = e / d, c = e % d;
-         q[c][r] = (r < nr) ? X[(size_t)c * ldim + i0 + r] : 0.0;
+         q[c][r] = (r < nr) ? X[(size_t)c * ldim + s_row[r]] : 0.0;
       }
       for (int e = tid; e < R * 256; e += kKnnThreads) {
          h0[e / 256][e % 256] = 0u;
@@ -313,12 +318,12 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn_bounded(const double* __res
       }
       __syncthreads();
       // count: keys below tau by (exponent, 4 mantissa bits)
-      const int jmax = i0 + nr - 1;
+      const int jmax = s_row[nr - 1];
       knn_scan<P, R>(X, ldim, d, q, jmax, [&](int j, const double* acc) {
 #pragma unroll
          for (int r = 0; r < R; r++) {
             const unsigned long long u = (unsigned long long)__double_as_longlong(acc[r]);
-            if (r < nr && j < i0 + r && u < s_tau[r]) atomicAdd(&h1[r][knn_bin(u, s_base[r])], 1u);
+            if (r < nr && j < s_row[r] && u < s_tau[r]) atomicAdd(&h1[r][knn_bin(u, s_base[r])], 1u);
          }
       });
       __syncthreads();
@@ -349,7 +354,7 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn_bounded(const double* __res
 #pragma unroll
          for (int r = 0; r < R; r++) {
             const unsigned long long u = (unsigned long long)__double_as_longlong(acc[r]);
-            if (r < nr && s_ok[r] && j < i0 + r && u < s_tau[r]) {
+            if (r < nr && s_ok[r] && j < s_row[r] && u < s_tau[r]) {
                const int b = knn_bin(u, s_base[r]);
                if (b < s_bstar[r]) {
                   const int p = atomicAdd(&s_nsel[r], 1);
@@ -384,7 +389,7 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn_bounded(const double* __res
       }
       __syncthreads();
       for (int r = wave; r < nr; r += kKnnThreads / 64) {
-         const int i = i0 + r;
+         const int i = s_row[r];
          if (!s_ok[r]) {
             if (lane == 0) fail[atomicAdd(nfail, 1)] = i;
             continue;
@@ -404,6 +409,396 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn_bounded(const double* __res
       }
       __syncthreads();
    }
+}
+
+// The same pattern rows from fp32 screening keys: the scans of k_knn_bounded run on an fp32 copy of the
+// points with the key of point j to row r kept as acc = -(|x_j|^2 + |q_r|^2) / 2 + x_j.q_r, so key~ =
+// max(0, -2 acc) and "key~ < T" is the single compare acc > -T/2 against a workgroup-uniform value (one
+// packed fp32 FMA per two (point, row) pairs per feature, half the bytes per point, 32 rows per workgroup;
+// the fp64 scan spends a subtract and an FMA per pair per feature).  Only the few candidates left are
+// ranked by the exact fp64 key sqdist() computes:
+//   sample  two passes over points 0..S-1 (S = min(i0, 4096)): exponent histogram, then 16 bins per
+//           octave below it; T1 = the upper end of the bin of the sample's (lfil-1)-th smallest key~;
+//   count   key~ < T1 over all earlier points by (exponent, 4 mantissa bits), 16 octaves below T1: U = the
+//           upper end of the bin b* holding the (lfil-1)-th smallest, so lfil-1 points have key~ < U;
+//   collect every earlier point with key~ <= U + 2 m, where m bounds |key~ - key| (below);
+//   exact   one wave per row: key = sqdist's sum, rank the candidates by (key, index), the first lfil-1
+//           are the row.
+// |key~ - key| <= m: rounding the coordinates to fp32 moves sqrt(key) by at most u (|x_j| + |q|) (u =
+// 2^-24); the fp32 norms, the start value and the d-term sum add at most (6 d + 6) u M^2, with M^2 =
+// max_j |x_j|^2, so |key~ - key| <= (6 d + 15) u M^2; m = (8 d + 64) u M^2.  The lfil-1 points with key~ <
+// U have key < U + m, so every true neighbour (key <= the (lfil-1)-th smallest) has key~ < U + 2 m in any
+// scan and is collected; ranking the collected set by the exact key is therefore the exact selection, ties
+// by index included.  A row with more than kScrCap candidates (duplicates, coordinates far from the origin
+// against their spread) goes to `fail` for k_knn, as does every row when M^2 is not finite.
+constexpr int kScrRows = 32;
+constexpr int kScrThreads = 512;
+constexpr int kScrCap = 160;
+constexpr int kScrSample = 4096;
+
+// Xf = fp32 copy of X (column-major, leading dimension n, zero features d..dp-1), nx = fl32 squared norms,
+// *m2 = bits of max nx
+__global__ __launch_bounds__(256) void k_knn_prep(const double* __restrict__ X, int ldim, int n, int d, int dp,
+                                                  float* __restrict__ Xf, float* __restrict__ nx,
+                                                  unsigned int* __restrict__ m2)
+{
+   unsigned int mx = 0u;
+   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+      float a = 0.f;
+      for (int c = 0; c < d; c++) {
+         const float v = (float)X[(size_t)c * ldim + j];
+         Xf[(size_t)c * n + j] = v;
+         a = fmaf(v, v, a);
+      }
+      for (int c = d; c < dp; c++) Xf[(size_t)c * n + j] = 0.f;
+      nx[j] = a;
+      mx = max(mx, __float_as_uint(a));  // non-negative floats order like their bits (NaN above inf)
+   }
+   for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned int)__shfl_xor((int)mx, off, 64));
+   if ((threadIdx.x & 63) == 0) atomicMax(m2, mx);
+}
+
+__device__ __forceinline__ int knn_bin32(unsigned int u, int base)
+{
+   const int e = (int)(u >> 23);
+   return (e < base) ? 0 : (((e - base) << 4) | (int)((u >> 19) & 15u));
+}
+
+struct ScrShared {
+   float q[kKnnMaxDims2][kScrRows];  // the rows' fp32 coordinates
+   float nqh[kScrRows];              // -|q_r|^2 / 2
+   union {
+      unsigned int h[kScrRows][256];
+      double key[kScrRows][kScrCap];
+   } u;
+   int idx[kScrRows][kScrCap];
+   float thr[kScrRows];  // -T_r / 2 of the current scan (rows beyond nr: +inf, never pass)
+   int base[kScrRows], cnt[kScrRows];
+};
+
+// One scan of points j in [j0, j1) against the workgroup's R = 32 rows on v_mfma_f32_32x32x2_f32: each
+// wave takes tiles of 32 points; the rows' coordinates are the A operand, held in registers for the whole
+// scan (lane l: row l & 31, features 2s + (l >> 5)), the points' the B operand (one coalesced fp32 load per
+// step), and the 32 x 32 accumulator starts at -(|x_j|^2 + |q_r|^2) / 2 (lane l: point l & 31, rows
+// (v & 3) + 8 (v >> 2) + 4 (l >> 5) of its 16 values).  MODE 0: exponent histogram of every key~; 1 / 2:
+// keys below the row's threshold binned 16 per octave from base; 3: append keys <= the threshold to the
+// row's candidates.  CHECK: only points before the row (j < i0 + r) count.  STEPS = ceil(d / 2) bound.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+template <int MODE, bool CHECK, int STEPS>
+__device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restrict__ Xf,
+                                              const float* __restrict__ nx, int n, int d, int i0, int j0, int j1)
+{
+   constexpr int W = kScrThreads / 64;
+   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, col = lane & 31;
+   float a[STEPS];
+#pragma unroll
+   for (int st = 0; st < STEPS; st++) a[st] = S.q[2 * st + h][col];  // zero beyond d
+   float nqh[16], thr[16];
+#pragma unroll
+   for (int v = 0; v < 16; v++) {
+      const int r = (v & 3) + 8 * (v >> 2) + 4 * h;
+      nqh[v] = S.nqh[r];
+      thr[v] = S.thr[r];
+   }
+   // the next tile's loads are issued before the current tile's MFMAs (software pipelining)
+   float b[STEPS], a0;
+   auto load = [&](int jb) {
+      const int jl = min(jb + col, j1 - 1);  // a valid point for the lanes past the end (their keys are dropped)
+      a0 = nx[jl];
+#pragma unroll
+      for (int st = 0; st < STEPS; st++) b[st] = Xf[(size_t)(2 * st + h) * n + jl];  // Xf zero-padded to 2 STEPS
+   };
+   if (j0 + wave * 32 < j1) load(j0 + wave * 32);
+   for (int jb = j0 + wave * 32; jb < j1; jb += W * 32) {
+      const int j = jb + col;
+      const bool ok = j < j1;
+      f32x16 c;
+      float bc[STEPS];
+#pragma unroll
+      for (int v = 0; v < 16; v++) c[v] = fmaf(a0, -0.5f, nqh[v]);
+#pragma unroll
+      for (int st = 0; st < STEPS; st++) bc[st] = b[st];
+      if (jb + W * 32 < j1) load(jb + W * 32);
+#pragma unroll
+      for (int st = 0; st < STEPS; st++) c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], bc[st], c, 0, 0, 0);
+      if (!ok) continue;
+      if (MODE == 0) {
+#pragma unroll
+         for (int v = 0; v < 16; v++) {
+            if (c[v] < thr[v]) continue;  // rows beyond nr (thr +inf)
+            const int r = (v & 3) + 8 * (v >> 2) + 4 * h;
+            atomicAdd(&S.u.h[r][__float_as_uint(fmaxf(0.f, -2.f * c[v])) >> 23], 1u);
+         }
+         continue;
+      }
+      bool any = false;
+#pragma unroll
+      for (int v = 0; v < 16; v++) any |= (MODE == 3 ? c[v] >= thr[v] : c[v] > thr[v]);
+      if (!any) continue;
+#pragma unroll
+      for (int v = 0; v < 16; v++) {
+         const int r = (v & 3) + 8 * (v >> 2) + 4 * h;
+         const bool pass = MODE == 3 ? c[v] >= thr[v] : c[v] > thr[v];
+         if (!pass || (CHECK && j >= i0 + r)) continue;
+         if (MODE == 3) {
+            const int slot = atomicAdd(&S.cnt[r], 1);
+            if (slot < kScrCap) S.idx[r][slot] = j;
+         } else {
+            const float key = fmaxf(0.f, -2.f * c[v]);
+            atomicAdd(&S.u.h[r][knn_bin32(__float_as_uint(key), S.base[r])], 1u);
+         }
+      }
+   }
+}
+
+template <int STEPS>
+__global__ __launch_bounds__(kScrThreads, 2) void k_knn_screen(const double* __restrict__ X, int ldim,
+                                                               const float* __restrict__ Xf,
+                                                               const float* __restrict__ nx, int n, int d, int lfil,
+                                                               float margin2, const int* __restrict__ ia,
+                                                               int* __restrict__ ja, int* __restrict__ fail,
+                                                               int* __restrict__ nfail)
+{
+   constexpr int R = kScrRows, CAP = kScrCap, W = kScrThreads / 64;
+   __shared__ ScrShared S;
+   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+   const int K = lfil - 1;
+   const int ngroups = (n - lfil + R - 1) / R;
+   const float inf = __int_as_float(0x7f800000);
+   // the first bin where the cumulative count of h[r] reaches K (one wave per row; every lane returns it),
+   // -1 when the histogram holds fewer than K keys (the scans' roundings may differ; such a row goes to k_knn)
+   auto kth_bin = [&](int r) {
+      unsigned int loc = 0;
+      for (int b = 0; b < 4; b++) loc += S.u.h[r][lane * 4 + b];
+      unsigned int incl = loc;
+      for (int off = 1; off < 64; off <<= 1) {
+         const unsigned int o = __shfl_up(incl, off, 64);
+         if (lane >= off) incl += o;
+      }
+      const unsigned long long hit = __ballot(incl >= (unsigned)K);
+      if (!hit) return -1;
+      const int first = __ffsll((long long)hit) - 1;
+      int b = lane * 4;
+      if (lane == first) {
+         unsigned int cum = incl - loc;
+         for (; b < lane * 4 + 3; b++) {
+            if (cum + S.u.h[r][b] >= (unsigned)K) break;
+            cum += S.u.h[r][b];
+         }
+      }
+      return __shfl(b, first, 64);
+   };
+   auto give_up = [&](int r) {  // lane 0 of the row's wave
+      S.thr[r] = inf;
+      S.cnt[r] = CAP + 1;
+   };
+   // upper end of bin b of the 16-per-octave bins from base (bin 0 also holds every exponent below base)
+   auto bin_top = [](int base, int b) {
+      const int e = base + (b >> 4);
+      return (e < 0) ? 0.f : __uint_as_float(((unsigned)e << 23) + ((unsigned)((b & 15) + 1) << 19));
+   };
+   auto clear_h = [&]() {
+      for (int e = tid; e < R * 256; e += kScrThreads) S.u.h[e / 256][e % 256] = 0u;
+   };
+   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+      const int i0 = lfil + g * R;
+      const int nr = min(R, n - i0);
+      for (int e = tid; e < R * 2 * STEPS; e += kScrThreads) {
+         const int r = e % R, c = e / R;
+         S.q[c][r] = (r < nr) ? Xf[(size_t)c * n + i0 + r] : 0.f;
+      }
+      clear_h();
+      if (tid < R) S.nqh[tid] = (tid < nr) ? -0.5f * nx[i0 + tid] : 0.f;
+      if (tid < R) {
+         S.thr[tid] = (tid < nr) ? -inf : inf;
+         S.cnt[tid] = 0;
+      }
+      __syncthreads();
+      const int Sn = min(i0, kScrSample);
+      knn_scan_mfma<0, false, STEPS>(S, Xf, nx, n, d, i0, 0, Sn);
+      __syncthreads();
+      for (int r = wave; r < nr; r += W) {
+         const int b = kth_bin(r);  // exponent bin: keys there are below 2^(b - 126)
+         if (lane == 0 && b < 0) give_up(r);
+         if (lane == 0 && b >= 0) {
+            S.thr[r] = (b == 255) ? -inf : -0.5f * __uint_as_float((unsigned)(b + 1) << 23);
+            S.base[r] = ((b == 255) ? 255 : b + 1) - 16;
+         }
+      }
+      __syncthreads();
+      clear_h();
+      __syncthreads();
+      knn_scan_mfma<1, false, STEPS>(S, Xf, nx, n, d, i0, 0, Sn);
+      __syncthreads();
+      for (int r = wave; r < nr; r += W) {
+         const int b = kth_bin(r);
+         if (lane == 0 && b < 0 && S.thr[r] != inf) give_up(r);
+         if (lane == 0 && b >= 0) {
+            const float T1 = (S.thr[r] == -inf) ? inf : bin_top(S.base[r], b);
+            S.thr[r] = -0.5f * T1;
+            S.base[r] = (T1 == inf) ? 255 - 16 : (int)(__float_as_uint(T1) >> 23) + ((__float_as_uint(T1) & 0x7fffffu) ? 1 : 0) - 16;
+         }
+      }
+      __syncthreads();
+      clear_h();
+      __syncthreads();
+      // count over every earlier point: [0, i0) before all rows, [i0, i0 + nr - 1) before some
+      knn_scan_mfma<2, false, STEPS>(S, Xf, nx, n, d, i0, 0, i0);
+      knn_scan_mfma<2, true, STEPS>(S, Xf, nx, n, d, i0, i0, i0 + nr - 1);
+      __syncthreads();
+      for (int r = wave; r < nr; r += W) {
+         const int b = kth_bin(r);
+         if (lane == 0 && b < 0 && S.thr[r] != inf) give_up(r);
+         if (lane == 0 && b >= 0) S.thr[r] = -0.5f * ((bin_top(S.base[r], b) + margin2) * 1.000001f);
+      }
+      __syncthreads();
+      knn_scan_mfma<3, false, STEPS>(S, Xf, nx, n, d, i0, 0, i0);
+      knn_scan_mfma<3, true, STEPS>(S, Xf, nx, n, d, i0, i0, i0 + nr - 1);
+      __syncthreads();
+      // exact keys of the candidates (the histogram space is free now)
+      for (int r = wave; r < nr; r += W) {
+         const int i = i0 + r, cnt = S.cnt[r];
+         if (cnt > CAP || cnt < K) continue;
+         for (int e = lane; e < cnt; e += 64) {
+            const int j = S.idx[r][e];
+            double a = 0.0;
+            for (int c = 0; c < d; c++) {
+               const double t = X[(size_t)c * ldim + j] - X[(size_t)c * ldim + i];
+               a = fma(t, t, a);
+            }
+            S.u.key[r][e] = a;
+         }
+      }
+      __syncthreads();
+      for (int r = wave; r < nr; r += W) {
+         const int i = i0 + r, cnt = S.cnt[r];
+         if (cnt > CAP || cnt < K) {
+            if (lane == 0) fail[atomicAdd(nfail, 1)] = i;
+            continue;
+         }
+         const int row = ia[i];
+         for (int e = lane; e < cnt; e += 64) {
+            const double ke = S.u.key[r][e];
+            const int ie = S.idx[r][e];
+            int rank = 0;
+            for (int o = 0; o < cnt; o++) {
+               const double ko = S.u.key[r][o];
+               rank += (ko < ke || (ko == ke && S.idx[r][o] < ie)) ? 1 : 0;
+            }
+            if (rank < K) ja[row + rank] = ie;
+         }
+         if (lane == 0) ja[row + K] = i;
+      }
+      __syncthreads();
+   }
+}
+
+template <class T>
+int upload(T** d, const T* h, size_t count);
+
+// KNN pattern rows [lfil, n) into dja (CSR row pointers dia): variant 1 (default) the fp32-screened scans,
+// 0 the fp64 k_knn_bounded, 2 the radix-select k_knn for every row; the rows the bounded variants leave go
+// to k_knn.  Returns the number of such rows, or -1.
+int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* dia, int* dja, hipStream_t s,
+                int variant)
+{
+   if (n <= lfil) return 0;
+   if (variant < 0) {
+      const char* e = getenv("NFFT4GP_AMD_KNN");
+      variant = e ? atoi(e) : 1;
+   }
+   if (d > kKnnMaxDims2) variant = 2;
+   const int nrows = n - lfil;
+   if (variant == 2) {
+      hipLaunchKernelGGL(k_knn, dim3(std::min(nrows, 4096)), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia, dja,
+                         nullptr, 0);
+      return hipGetLastError() == hipSuccess ? nrows : -1;
+   }
+   int* dfail = nullptr;
+   float *Xf = nullptr, *nx = nullptr;
+   int nfail = -1;
+   unsigned int m2bits = 0u;
+   auto done = [&](int rc) {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(dfail);
+      (void)hipFree(Xf);
+      (void)hipFree(nx);
+      return rc;
+   };
+   if (upload(&dfail, (const int*)nullptr, (size_t)nrows + 2) ||
+       hipMemsetAsync(dfail + nrows, 0, 2 * sizeof(int), s) != hipSuccess)
+      return done(-1);
+   if (variant == 1) {
+      const int steps = d <= 4 ? 2 : d <= 8 ? 4 : d <= 16 ? 8 : d <= 32 ? 16 : 32;
+      if (hipMalloc((void**)&Xf, sizeof(float) * (size_t)n * 2 * steps) != hipSuccess ||
+          hipMalloc((void**)&nx, sizeof(float) * (size_t)n) != hipSuccess)
+         return done(-1);
+      hipLaunchKernelGGL(k_knn_prep, dim3(std::min((n + 255) / 256, 4096)), dim3(256), 0, s, dX, ldim, n, d, 2 * steps, Xf, nx,
+                         (unsigned int*)(dfail + nrows + 1));
+      if (hipMemcpyAsync(&m2bits, dfail + nrows + 1, sizeof(unsigned int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+         return done(-1);
+      float m2;
+      memcpy(&m2, &m2bits, sizeof(float));
+      const double margin = (8.0 * d + 64.0) * std::ldexp(1.0, -24) * (double)m2;
+      if (!std::isfinite(m2) || !std::isfinite((float)(2.0 * margin))) {
+         variant = 2;  // every row to k_knn
+      } else {
+         const int ngroups = (nrows + kScrRows - 1) / kScrRows;
+         auto screen = steps == 2 ? k_knn_screen<2> : steps == 4 ? k_knn_screen<4> : steps == 8 ? k_knn_screen<8>
+                       : steps == 16 ? k_knn_screen<16> : k_knn_screen<32>;
+         hipLaunchKernelGGL(screen, dim3(std::min(ngroups, 4096)),
+                            dim3(kScrThreads), 0, s, dX, ldim,
+                            (const float*)Xf, (const float*)nx, n, d, lfil, (float)(2.0 * margin) * 1.0001f, dia, dja,
+                            dfail, dfail + nrows);
+      }
+   } else {
+      const int ngroups = (nrows + kKnnRows - 1) / kKnnRows;
+      // 2 points per thread: 5.6 -> 4.0 s for the n = 1e6, d = 32, lfil = 20 setup; 4 drop to 1 wave per SIMD
+      hipLaunchKernelGGL(k_knn_bounded<kKnnPoints>, dim3(std::min(ngroups, 8192)), dim3(kKnnThreads), 0, s, dX, ldim,
+                         n, d, lfil, dia, dja, dfail, dfail + nrows, nullptr, 0);
+   }
+   if (variant == 2) {
+      hipLaunchKernelGGL(k_knn, dim3(std::min(nrows, 4096)), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia, dja,
+                         nullptr, 0);
+      return done(hipGetLastError() == hipSuccess ? nrows : -1);
+   }
+   if (hipGetLastError() != hipSuccess ||
+       hipMemcpyAsync(&nfail, dfail + nrows, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess)
+      return done(-1);
+   if (variant == 1 && nfail > 64) {
+      // many rows the fp32 screen could not settle (clustered data far from the origin against its spread):
+      // the fp64 two-pass scan on them, in ascending order, before the radix select on what it leaves
+      std::vector<int> hrows(nfail);
+      if (hipMemcpy(hrows.data(), dfail, sizeof(int) * nfail, hipMemcpyDeviceToHost) != hipSuccess) return done(-1);
+      std::sort(hrows.begin(), hrows.end());
+      int* drows = nullptr;
+      if (upload(&drows, hrows.data(), hrows.size()) ||
+          hipMemsetAsync(dfail + nrows, 0, sizeof(int), s) != hipSuccess) {
+         (void)hipFree(drows);
+         return done(-1);
+      }
+      const int ngroups = (nfail + kKnnRows - 1) / kKnnRows;
+      hipLaunchKernelGGL(k_knn_bounded<kKnnPoints>, dim3(std::min(ngroups, 8192)), dim3(kKnnThreads), 0, s, dX, ldim,
+                         n, d, lfil, dia, dja, dfail, dfail + nrows, (const int*)drows, nfail);
+      const int nscreen = nfail;
+      if (hipGetLastError() != hipSuccess ||
+          hipMemcpyAsync(&nfail, dfail + nrows, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess) {
+         (void)hipFree(drows);
+         return done(-1);
+      }
+      (void)hipFree(drows);
+      if (nfail > 0)
+         hipLaunchKernelGGL(k_knn, dim3(std::min(nfail, 4096)), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia,
+                            dja, dfail, nfail);
+      return done(hipGetLastError() == hipSuccess ? nscreen : -1);
+   }
+   if (nfail > 0)
+      hipLaunchKernelGGL(k_knn, dim3(std::min(nfail, 4096)), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia, dja,
+                         dfail, nfail);
+   return done(hipGetLastError() == hipSuccess ? nfail : -1);
 }
 
 // In place on the wave's LDS vector b: b = L^{-1} b (trans = 0) or L^{-T} b (trans = 1), L lower in A.
@@ -873,33 +1268,8 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const Ke
        (require_grad && upload(&dda, (const double*)nullptr, 3 * (size_t)nnz)))
       return cleanup(-1);
    if (n > lfil) {
-      // bounded two-pass KNN, then the radix-select kernel on the rows it could not settle
-      int* dfail = nullptr;
-      if (upload(&dfail, (const int*)nullptr, (size_t)(n - lfil) + 1) ||
-          hipMemsetAsync(dfail + (n - lfil), 0, sizeof(int), s) != hipSuccess) {
-         (void)hipFree(dfail);
-         return cleanup(-1);
-      }
-      const int ngroups = (n - lfil + kKnnRows - 1) / kKnnRows;
-      int nfail = 0;
-      if (d <= kKnnMaxDims2) {
-         // 2 points per thread: 5.6 -> 4.0 s for the n = 1e6, d = 32, lfil = 20 setup; 4 drop to 1 wave per SIMD
-         hipLaunchKernelGGL(k_knn_bounded<kKnnPoints>, dim3(std::min(ngroups, 8192)), dim3(kKnnThreads), 0, s, dX, ldim,
-                            n, d, lfil, dia, dja, dfail, dfail + (n - lfil));
-         if (hipMemcpyAsync(&nfail, dfail + (n - lfil), sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
-             hipStreamSynchronize(s) != hipSuccess) {
-            (void)hipFree(dfail);
-            return cleanup(-1);
-         }
-         if (nfail > 0)
-            hipLaunchKernelGGL(k_knn, dim3(std::min(nfail, 4096)), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia,
-                               dja, dfail, nfail);
-      } else {
-         hipLaunchKernelGGL(k_knn, dim3(std::min(n - lfil, 4096)), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia,
-                            dja, nullptr, 0);
-      }
-      (void)hipStreamSynchronize(s);
-      (void)hipFree(dfail);
+      const int nfail = knn_pattern(dX, n, ldim, d, lfil, dia, dja, s, -1);
+      if (nfail < 0) return cleanup(-1);
       knn_fallback_rows = nfail;
    }
    const KernelParams P = kernel_params_of(Ks, d);
@@ -1138,6 +1508,34 @@ double Nfft4GPAmdPrecondFsaiLogdet(void* vfsai_mat)
    PrecondFsaiAmd* F = (PrecondFsaiAmd*)vfsai_mat;
    if (!F || !F->ia) return NAN;
    return 2.0 * diag_sum(F, nullptr, current_stream());
+}
+
+// Test hook: the KNN pattern (column indices of rows lfil..n-1, lfil each) of the host points X (n x d,
+// leading dimension ldim) with the given variant (knn_pattern); *nfail = rows handed to k_knn.
+int Nfft4GPAmdDebugKnn(const double* X, int n, int ldim, int d, int lfil, int variant, int* ja_out, int* nfail)
+{
+   if (n <= lfil || lfil < 1 || lfil > kFsaiMaxK || d <= 0 || d > kMaxDims || ldim < n) return -1;
+   hipStream_t s = current_stream();
+   std::vector<int> hia(n + 1, 0);
+   for (int i = 0; i < n; i++) hia[i + 1] = hia[i] + (i < lfil ? i + 1 : lfil);
+   double* dX = nullptr;
+   int *dia = nullptr, *dja = nullptr;
+   int rc = -1;
+   if (upload(&dX, X, (size_t)ldim * d) == 0 && upload(&dia, hia.data(), hia.size()) == 0 &&
+       upload(&dja, (const int*)nullptr, (size_t)hia[n]) == 0) {
+      const int nf = knn_pattern(dX, n, ldim, d, lfil, dia, dja, s, variant);
+      if (nf >= 0 && hipMemcpyAsync(ja_out, dja + hia[lfil], sizeof(int) * (size_t)(n - lfil) * lfil,
+                                    hipMemcpyDeviceToHost, s) == hipSuccess &&
+          hipStreamSynchronize(s) == hipSuccess) {
+         if (nfail) *nfail = nf;
+         rc = 0;
+      }
+   }
+   (void)hipStreamSynchronize(s);
+   (void)hipFree(dX);
+   (void)hipFree(dia);
+   (void)hipFree(dja);
+   return rc;
 }
 
 }  // extern "C"

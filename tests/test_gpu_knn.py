@@ -1,0 +1,96 @@
+"""The FSAI pattern's KNN (Nfft4GPDistanceEuclidKnn, kernels.c:121-278: row i >= lfil holds the lfil-1
+nearest earlier points by (squared distance, index), then i) on the GPU: the fp32-screened scans
+(k_knn_screen, the default) must give exactly the rows of the fp64 two-pass scan (k_knn_bounded) and of the
+radix select over every point (k_knn), on random, clustered, tied and badly centred data; rows the screen
+cannot settle fall back to k_knn (counted)."""
+import ctypes as C
+import time
+
+import numpy as np
+import pytest
+
+import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+
+pytestmark = pytest.mark.gpu
+
+
+def knn(X, lfil, variant):
+    X = np.asfortranarray(X, dtype=np.float64)
+    n, d = X.shape
+    f = amd.lib().Nfft4GPAmdDebugKnn
+    f.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    f.restype = C.c_int
+    ja = np.full((n - lfil) * lfil, -1, np.int32)
+    nfail = C.c_int(-1)
+    assert f(X.ctypes.data, n, n, d, lfil, variant, ja.ctypes.data, C.byref(nfail)) == 0
+    return ja.reshape(n - lfil, lfil), nfail.value
+
+
+def brute(X, lfil, rows):
+    out = {}
+    for i in rows:
+        t = X[:i] - X[i]
+        d2 = np.zeros(i)
+        for c in range(X.shape[1]):  # the fma chain's order; ties by index
+            d2 = d2 + t[:, c] * t[:, c]
+        out[i] = np.lexsort((np.arange(i), d2))[: lfil - 1]
+    return out
+
+
+def check_same(X, lfil, expect_few_fallbacks=True):
+    a, nf = knn(X, lfil, 1)
+    b, _ = knn(X, lfil, 0)
+    c, _ = knn(X, lfil, 2)
+    n = X.shape[0]
+    assert np.array_equal(a, c) and np.array_equal(b, c)
+    assert np.array_equal(a[:, -1], np.arange(lfil, n))
+    if expect_few_fallbacks:
+        assert nf <= max(2, (n - lfil) // 100), nf
+    return a, nf
+
+
+@pytest.mark.parametrize("n,d,lfil", [(20000, 32, 20), (6000, 3, 20), (5000, 64, 32), (3000, 8, 2), (300, 5, 64)])
+def test_knn_screen_matches_exact_random(torch_cuda, n, d, lfil):
+    X = np.random.default_rng(n + d).random((n, d))
+    a, _ = check_same(X, lfil)
+    rows = [lfil, lfil + 1, n // 2, n - 1]
+    ref = brute(X, lfil, rows)
+    for i in rows:
+        assert np.array_equal(a[i - lfil, :-1], ref[i]), i
+
+
+def test_knn_screen_clustered_and_ties(torch_cuda):
+    rng = np.random.default_rng(3)
+    centres = rng.random((20, 16)) * 10
+    X = centres[rng.integers(0, 20, 15000)] + 0.01 * rng.standard_normal((15000, 16))
+    # clusters 1e-2 wide at |x| ~ 20: the fp32 margin exceeds the neighbour distances, so most rows go on to
+    # the fp64 scan (and what that leaves to the radix select) -- still the exact rows
+    _, nf = check_same(X, 20, expect_few_fallbacks=False)
+    assert nf > 64
+    # coordinates on a coarse grid: many exactly equal distances, ties broken by index
+    G = np.round(rng.random((8000, 6)) * 4) / 4
+    check_same(G, 20, expect_few_fallbacks=False)
+
+
+def test_knn_screen_far_from_origin_falls_back_exactly(torch_cuda):
+    """Coordinates far from the origin against their spread: the fp32 margin swamps the bins, every row
+    goes to the exact radix select, and the rows are still exact."""
+    X = 1e4 + np.random.default_rng(5).random((4000, 8))
+    a, nf = check_same(X, 20, expect_few_fallbacks=False)
+    assert nf > 0
+
+
+def test_knn_screen_speed_config_c_slice(torch_cuda):
+    """Timing at n = 2e5, d = 32 (config C's features): the screened scans against the fp64 scans."""
+    X = np.random.default_rng(906).random((200000, 32))
+    t = {}
+    for v in (1, 0):
+        knn(X[:30000], 20, v)
+        t0 = time.time()
+        r, nf = knn(X, 20, v)
+        t[v] = time.time() - t0
+        if v == 1:
+            r1, nf1 = r, nf
+    assert np.array_equal(r1, r)
+    print(f"KNN n=2e5 d=32: screen {t[1]:.3f} s (fallback rows {nf1}), fp64 {t[0]:.3f} s")
+    assert nf1 <= 2000
