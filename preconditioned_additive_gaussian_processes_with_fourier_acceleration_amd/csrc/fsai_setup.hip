@@ -435,6 +435,9 @@ constexpr int kScrRows = 32;
 constexpr int kScrThreads = 512;
 constexpr int kScrCap = 160;
 constexpr int kScrSample = 4096;
+#ifndef KNN_SCR_WAVES
+#define KNN_SCR_WAVES 2  // waves per SIMD the screen kernels are compiled for
+#endif
 
 // Xf = fp32 copy of X (column-major, leading dimension n, zero features d..dp-1), nx = fl32 squared norms,
 // *m2 = bits of max nx
@@ -500,25 +503,30 @@ __device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restr
       nqh[v] = S.nqh[r];
       thr[v] = S.thr[r];
    }
-   // the next tile's loads are issued before the current tile's MFMAs (software pipelining)
-   float b[STEPS], a0;
-   auto load = [&](int jb) {
+   // the loads run two tiles ahead of the MFMAs (software pipelining over the memory latency)
+   float b0[STEPS], b1[STEPS], a00 = 0.f, a01 = 0.f;
+   auto load = [&](int jb, float (&b)[STEPS], float& a0) {
       const int jl = min(jb + col, j1 - 1);  // a valid point for the lanes past the end (their keys are dropped)
       a0 = nx[jl];
 #pragma unroll
       for (int st = 0; st < STEPS; st++) b[st] = Xf[(size_t)(2 * st + h) * n + jl];  // Xf zero-padded to 2 STEPS
    };
-   if (j0 + wave * 32 < j1) load(j0 + wave * 32);
+   if (j0 + wave * 32 < j1) load(j0 + wave * 32, b0, a00);
+   if (j0 + wave * 32 + W * 32 < j1) load(j0 + wave * 32 + W * 32, b1, a01);
    for (int jb = j0 + wave * 32; jb < j1; jb += W * 32) {
       const int j = jb + col;
       const bool ok = j < j1;
       f32x16 c;
       float bc[STEPS];
 #pragma unroll
-      for (int v = 0; v < 16; v++) c[v] = fmaf(a0, -0.5f, nqh[v]);
+      for (int v = 0; v < 16; v++) c[v] = fmaf(a00, -0.5f, nqh[v]);
 #pragma unroll
-      for (int st = 0; st < STEPS; st++) bc[st] = b[st];
-      if (jb + W * 32 < j1) load(jb + W * 32);
+      for (int st = 0; st < STEPS; st++) {
+         bc[st] = b0[st];
+         b0[st] = b1[st];
+      }
+      a00 = a01;
+      if (jb + 2 * W * 32 < j1) load(jb + 2 * W * 32, b1, a01);
 #pragma unroll
       for (int st = 0; st < STEPS; st++) c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], bc[st], c, 0, 0, 0);
       if (!ok) continue;
@@ -551,11 +559,14 @@ __device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restr
    }
 }
 
-template <int STEPS>
-__global__ __launch_bounds__(kScrThreads, 2) void k_knn_screen(const double* __restrict__ X, int ldim,
+// Two launches, so that each holds only its own scans' registers: PHASE 0 = sample and count, leaving each
+// row's collect limit U + 2m in lim (NaN: the row goes to the fallback); PHASE 1 = collect, exact keys, rank.
+template <int STEPS, int PHASE>
+__global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const double* __restrict__ X, int ldim,
                                                                const float* __restrict__ Xf,
                                                                const float* __restrict__ nx, int n, int d, int lfil,
-                                                               float margin2, const int* __restrict__ ia,
+                                                               float margin2, float* __restrict__ lim,
+                                                               const int* __restrict__ ia,
                                                                int* __restrict__ ja, int* __restrict__ fail,
                                                                int* __restrict__ nfail)
 {
@@ -610,10 +621,17 @@ __global__ __launch_bounds__(kScrThreads, 2) void k_knn_screen(const double* __r
       clear_h();
       if (tid < R) S.nqh[tid] = (tid < nr) ? -0.5f * nx[i0 + tid] : 0.f;
       if (tid < R) {
-         S.thr[tid] = (tid < nr) ? -inf : inf;
          S.cnt[tid] = 0;
+         if (PHASE == 0) {
+            S.thr[tid] = (tid < nr) ? -inf : inf;
+         } else {
+            const float L = (tid < nr) ? lim[i0 - lfil + tid] : inf;
+            S.thr[tid] = (L != L || tid >= nr) ? inf : -0.5f * L;
+            if (tid < nr && L != L) S.cnt[tid] = CAP + 1;
+         }
       }
       __syncthreads();
+      if constexpr (PHASE == 0) {
       const int Sn = min(i0, kScrSample);
       knn_scan_mfma<0, false, STEPS>(S, Xf, nx, n, d, i0, 0, Sn);
       __syncthreads();
@@ -648,10 +666,14 @@ __global__ __launch_bounds__(kScrThreads, 2) void k_knn_screen(const double* __r
       __syncthreads();
       for (int r = wave; r < nr; r += W) {
          const int b = kth_bin(r);
-         if (lane == 0 && b < 0 && S.thr[r] != inf) give_up(r);
-         if (lane == 0 && b >= 0) S.thr[r] = -0.5f * ((bin_top(S.base[r], b) + margin2) * 1.000001f);
+         if (lane == 0) {
+            const bool gave_up = S.thr[r] == inf;
+            lim[i0 - lfil + r] = (gave_up || b < 0) ? __int_as_float(0x7fc00000)
+                                                    : (bin_top(S.base[r], b) + margin2) * 1.000001f;
+         }
       }
       __syncthreads();
+      } else {
       knn_scan_mfma<3, false, STEPS>(S, Xf, nx, n, d, i0, 0, i0);
       knn_scan_mfma<3, true, STEPS>(S, Xf, nx, n, d, i0, i0, i0 + nr - 1);
       __syncthreads();
@@ -690,6 +712,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void k_knn_screen(const double* __r
          if (lane == 0) ja[row + K] = i;
       }
       __syncthreads();
+      }
    }
 }
 
@@ -745,12 +768,25 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
          variant = 2;  // every row to k_knn
       } else {
          const int ngroups = (nrows + kScrRows - 1) / kScrRows;
-         auto screen = steps == 2 ? k_knn_screen<2> : steps == 4 ? k_knn_screen<4> : steps == 8 ? k_knn_screen<8>
-                       : steps == 16 ? k_knn_screen<16> : k_knn_screen<32>;
-         hipLaunchKernelGGL(screen, dim3(std::min(ngroups, 4096)),
-                            dim3(kScrThreads), 0, s, dX, ldim,
-                            (const float*)Xf, (const float*)nx, n, d, lfil, (float)(2.0 * margin) * 1.0001f, dia, dja,
-                            dfail, dfail + nrows);
+         float* lim = nullptr;
+         if (hipMalloc((void**)&lim, sizeof(float) * (size_t)nrows) != hipSuccess) return done(-1);
+         for (int phase = 0; phase < 2; phase++) {
+            auto screen = phase == 0 ? (steps == 2    ? k_knn_screen<2, 0>
+                                        : steps == 4  ? k_knn_screen<4, 0>
+                                        : steps == 8  ? k_knn_screen<8, 0>
+                                        : steps == 16 ? k_knn_screen<16, 0>
+                                                      : k_knn_screen<32, 0>)
+                                     : (steps == 2    ? k_knn_screen<2, 1>
+                                        : steps == 4  ? k_knn_screen<4, 1>
+                                        : steps == 8  ? k_knn_screen<8, 1>
+                                        : steps == 16 ? k_knn_screen<16, 1>
+                                                      : k_knn_screen<32, 1>);
+            hipLaunchKernelGGL(screen, dim3(std::min(ngroups, 4096)), dim3(kScrThreads), 0, s, dX, ldim,
+                               (const float*)Xf, (const float*)nx, n, d, lfil, (float)(2.0 * margin) * 1.0001f, lim,
+                               dia, dja, dfail, dfail + nrows);
+         }
+         (void)hipStreamSynchronize(s);
+         (void)hipFree(lim);
       }
    } else {
       const int ngroups = (nrows + kKnnRows - 1) / kKnnRows;

@@ -127,13 +127,17 @@ __device__ __forceinline__ void stage_block(double* __restrict__ s, const double
 // ------------------------------------------------------------------------------------------------
 // spread
 // ------------------------------------------------------------------------------------------------
+// gsum (row shards): the partial grids are stored memory-side and the last block to finish a slice of
+// window groups sums them over the blocks in block order into gsum[comp][cell] (reduce.hpp's handoff;
+// tickets: one counter per slice, kTicketStride apart, left at zero) -- k_reduce_parts inside the spread.
 template <int THREADS, bool PREFETCH, bool TIMELINE = false>
 __global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__ meta,
                                                     const uint32_t* __restrict__ lo,
                                                     const uint32_t* __restrict__ qarr,
                                                     const int* __restrict__ tile_off, const double* __restrict__ x,
                                                     int n, int B, int nblocks, int ngroups, int CG, int nw, int gpw,
-                                                    double* __restrict__ part)
+                                                    double* __restrict__ part, double* __restrict__ gsum,
+                                                    unsigned int* __restrict__ ticket)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = B + kPad;
@@ -227,7 +231,11 @@ __global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__
 #pragma unroll
             for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
          }
-         part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
+         double* dst = part + ((size_t)(c0 + cl) * nblocks + b) * kNos + gi;  // [comp][block][cell]
+         if (gsum)
+            __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+         else
+            *dst = v;
       }
       if (g + 1 < g_end) {
          __syncthreads();  // every fold read done before the table is cleared
@@ -238,6 +246,37 @@ __global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__
    if (TIMELINE) {
       __syncthreads();
       stamp(3);
+   }
+   if (gsum) {
+      __shared__ int s_last;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+         const unsigned old = __hip_atomic_fetch_add(ticket + slice * kTicketStride, 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+         s_last = (old == (unsigned)nblocks - 1);
+      }
+      __syncthreads();
+      if (!s_last) return;
+      // the slice's windows: sum the blocks' grids in block order, 8 loads in flight per thread
+      const int c_begin = g_begin * CG, c_end = min(nw, g_end * CG);
+      for (int idx = tid; idx < (c_end - c_begin) * kNos; idx += THREADS) {
+         const int comp = c_begin + idx / kNos, cell = idx % kNos;
+         const double* src = part + (size_t)comp * nblocks * kNos + cell;
+         double acc = 0.0;
+         for (int p0 = 0; p0 < nblocks; p0 += 8) {
+            double v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+               v[k] = p0 + k < nblocks
+                          ? __hip_atomic_load(src + (size_t)(p0 + k) * kNos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) acc += v[k];
+         }
+         gsum[(size_t)comp * kNos + cell] = acc;
+      }
+      if (tid == 0) __hip_atomic_store(ticket + slice * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
    }
 }
 
@@ -539,6 +578,107 @@ __global__ __launch_bounds__(THREADS) void k_interp_part(const uint16_t* __restr
    }
    __syncthreads();
    for (int j = tid; j < nloc; j += THREADS) atomicAdd(y + (size_t)base + j, scale * s_y[j]);
+}
+
+// Row shards with few blocks, one launch (launch_shard_finish_fused): workgroup (block b, part s) builds the
+// interpolation polynomials H of its own window groups in LDS from the summed grids (k_grid's circulant
+// and tap products, same operation order), interpolates its tiles into an LDS y-slice, stores the slice
+// memory-side, and the last of the block's S workgroups forms y = beta y + amu x + scale sum_s slice_s in
+// part order (deterministic, no global atomics, no separate grid or y-initialisation launch).
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_shard_finish(const uint16_t* __restrict__ meta,
+                                                         const uint32_t* __restrict__ lo,
+                                                         const uint32_t* __restrict__ qarr,
+                                                         const int* __restrict__ tile_off,
+                                                         const double* __restrict__ gsum, const double* __restrict__ w,
+                                                         const double* __restrict__ x, double* __restrict__ y, int n,
+                                                         int B, int ngroups, int CG, int nw, int S, double scale,
+                                                         double beta, double amu, double* __restrict__ ypart,
+                                                         unsigned int* __restrict__ ticket)
+{
+   extern __shared__ __attribute__((aligned(16))) double smem[];
+   const int b = blockIdx.x / S, part = blockIdx.x % S;
+   const int g0 = part * ngroups / S, g1 = (part + 1) * ngroups / S;
+   const int c_begin = min(nw, g0 * CG), c_end = min(nw, g1 * CG), nc = c_end - c_begin;
+   double* s_y = smem;                            // B + kPad
+   double* s_H = smem + B + kPad;                 // [nc][64][kNC]
+   double* s_g = s_H + (size_t)nc * kNos * kNC;   // [nc][64]
+   double* s_h = s_g + (size_t)nc * kNos;         // [nc][64]
+   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+   constexpr int nwaves = THREADS / 64;
+   const int base = b * B;
+   const int nloc = min(B, n - base);
+   const int t1 = tile_off[b * ngroups + g1];
+   int t = tile_off[b * ngroups + g0] + wave;
+   TileRegs cur;
+   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
+   for (int i = tid; i < B + kPad; i += THREADS) s_y[i] = 0.0;
+   for (int i = tid; i < nc * kNos; i += THREADS) s_g[i] = gsum[(size_t)c_begin * kNos + i];
+   __syncthreads();
+   for (int i = tid; i < nc * kNos; i += THREADS) {
+      const int c = i / kNos, tt = i % kNos;
+      const double* wc = w + (size_t)(c_begin + c) * kNos;
+      const double* gc = s_g + c * kNos;
+      double h = 0.0;
+#pragma unroll 8
+      for (int l2 = 0; l2 < kNos; l2++) h = fma(wc[(tt - l2) & (kNos - 1)], gc[l2], h);
+      s_h[i] = h;
+   }
+   __syncthreads();
+   for (int i = tid; i < nc * kNos * kNC; i += THREADS) {
+      const int c = i / (kNos * kNC), rem = i % (kNos * kNC);
+      const int cell = rem / kNC, d = rem % kNC;
+      const double* hc = s_h + c * kNos;
+      double v = 0.0;
+#pragma unroll
+      for (int tp = 0; tp < kTaps; tp++) v = fma(hc[(cell - kM + tp) & (kNos - 1)], c_taps[tp * kNC + d], v);
+      s_H[i] = v;
+   }
+   __syncthreads();
+   const int hbase = c_begin * kNos;
+   for (; t < t1; t += nwaves) {
+      const double* hp = s_H + (size_t)((int)cur.mt - hbase) * kNC;
+      double hc[kNC];
+#pragma unroll
+      for (int d = 0; d < kNC; d += 2) {
+         const double2 v = *reinterpret_cast<const double2*>(hp + d);
+         hc[d] = v.x;
+         hc[d + 1] = v.y;
+      }
+#pragma unroll
+      for (int r = 0; r < kR; r++) {
+         const uint32_t loc = slot_loc(cur, r);
+         const double u = q_to_u(cur.qq[r]);
+         double v = hc[kNC - 1];
+#pragma unroll
+         for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
+         atomicAdd(s_y + loc, v);
+      }
+      const int tn = t + nwaves;
+      if (tn < t1) load_tile(cur, meta, lo, qarr, tn, lane);
+   }
+   __syncthreads();
+   double* mine = ypart + ((size_t)b * S + part) * B;
+   for (int j = tid; j < nloc; j += THREADS) __hip_atomic_store(mine + j, s_y[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+   __syncthreads();
+   __shared__ int s_last;
+   if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(ticket + b * kTicketStride, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      s_last = (old == (unsigned)S - 1);
+   }
+   __syncthreads();
+   if (!s_last) return;
+   const double* slices = ypart + (size_t)b * S * B;
+   for (int j = tid; j < nloc; j += THREADS) {
+      double acc = 0.0;
+      for (int p = 0; p < S; p++)
+         acc += __hip_atomic_load(slices + (size_t)p * B + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const size_t jj = (size_t)base + j;
+      y[jj] = (beta == 0.0 ? 0.0 : beta * y[jj]) + amu * x[jj] + scale * acc;
+   }
+   if (tid == 0) __hip_atomic_store(ticket + b * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // gsum[comp][cell] = sum_b part[comp][b][cell]   (row-sharded path: before the all-reduce).  One
@@ -853,7 +993,7 @@ int upload_tap_coeffs()
 }
 
 typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, int, int, int,
-                         int, int, int, int, double*);
+                         int, int, int, int, double*, double*, unsigned int*);
 struct SpreadVariant {
    SpreadFn fn;
    int threads;
@@ -904,7 +1044,7 @@ static void raise_lds_limit_once()
    (void)raised;
 }
 
-int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream)
+int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream, double* d_gsum)
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
    raise_lds_limit_once();
@@ -945,8 +1085,10 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
    const int gpw = std::min(std::max(P.gpw, 1), P.ngroups);
    const int nslices = (P.ngroups + gpw - 1) / gpw;
    const int gridx = ((P.nblocks + 7) / 8) * 8 * nslices;
+   if (d_gsum && (!P.d_sum_ticket || nslices > kMaxSumSlices)) return -1;
    launch_ev(V.fn, dim3(gridx), dim3(V.threads), spread_lds_bytes(P), stream, P.kev ? P.kev + 0 : nullptr, P.dl.meta,
-             P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, gpw, d_part);
+             P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, gpw, d_part, d_gsum,
+             d_gsum ? P.d_sum_ticket : nullptr);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -984,6 +1126,33 @@ int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, do
       hipLaunchKernelGGL(k_interp_part<T>, dim3(P.nblocks * S), dim3(T), sizeof(double) * (size_t)(P.B + kPad), stream,
                          P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H, d_y, P.n, P.B, P.ngroups, S,
                          alpha * ff);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+size_t shard_finish_lds_bytes(const AdditivePlan& P, int S)
+{
+   const int ncmax = ((P.ngroups + S - 1) / S) * P.CG;
+   return sizeof(double) * ((size_t)P.B + kPad + (size_t)ncmax * kNos * (kNC + 2));
+}
+
+int launch_shard_finish_fused(const AdditivePlan& P, const double* d_gridsum, double alpha, const double* d_x,
+                              double beta, double* d_y, int S, double* d_ypart, hipStream_t stream)
+{
+   constexpr int T = 512;
+   static bool attr = false;
+   if (!attr) {
+      (void)hipFuncSetAttribute((const void*)k_shard_finish<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      (void)hipGetLastError();
+      attr = true;
+   }
+   if (P.n == 0) return 0;
+   const double ff = P.f * P.f;
+   hipLaunchKernelGGL(k_shard_finish<T>, dim3(P.nblocks * S), dim3(T), shard_finish_lds_bytes(P, S), stream, P.dl.meta,
+                      P.dl.lo, P.dl.q, P.dl.tile_off, d_gridsum, (const double*)P.d_w, d_x, d_y, P.n, P.B, P.ngroups,
+                      P.CG, P.nw, S, alpha * ff, beta, alpha * ff * P.mu * P.diag, d_ypart,
+                      P.d_sum_ticket + (size_t)kMaxSumSlices * kTicketStride);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
