@@ -431,7 +431,8 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn_bounded(const double* __res
 // scan and is collected; ranking the collected set by the exact key is therefore the exact selection, ties
 // by index included.  A row with more than kScrCap candidates (duplicates, coordinates far from the origin
 // against their spread) goes to `fail` for k_knn, as does every row when M^2 is not finite.
-constexpr int kScrRows = 32;
+constexpr int kScrRowBlocks = 1;  // 32-row MFMA tiles per workgroup; each point tile is read by that many waves (2: same time)
+constexpr int kScrRows = 32 * kScrRowBlocks;
 constexpr int kScrThreads = 512;
 constexpr int kScrCap = 160;
 constexpr int kScrSample = 4096;
@@ -491,15 +492,18 @@ template <int MODE, bool CHECK, int STEPS>
 __device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restrict__ Xf,
                                               const float* __restrict__ nx, int n, int d, int i0, int j0, int j1)
 {
-   constexpr int W = kScrThreads / 64;
-   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, col = lane & 31;
+   // wave w: row tile w % kScrRowBlocks (rows rt .. rt + 31), point stream w / kScrRowBlocks of W; the waves
+   // of one point stream read the same points at the same time (one fetch beyond L2 serves all of them)
+   constexpr int W = kScrThreads / 64 / kScrRowBlocks;
+   const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+   const int rt = 32 * ((threadIdx.x >> 6) % kScrRowBlocks), wave = (threadIdx.x >> 6) / kScrRowBlocks;
    float a[STEPS];
 #pragma unroll
-   for (int st = 0; st < STEPS; st++) a[st] = S.q[2 * st + h][col];  // zero beyond d
+   for (int st = 0; st < STEPS; st++) a[st] = S.q[2 * st + h][rt + col];  // zero beyond d
    float nqh[16], thr[16];
 #pragma unroll
    for (int v = 0; v < 16; v++) {
-      const int r = (v & 3) + 8 * (v >> 2) + 4 * h;
+      const int r = rt + (v & 3) + 8 * (v >> 2) + 4 * h;
       nqh[v] = S.nqh[r];
       thr[v] = S.thr[r];
    }
@@ -534,7 +538,7 @@ __device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restr
 #pragma unroll
          for (int v = 0; v < 16; v++) {
             if (c[v] < thr[v]) continue;  // rows beyond nr (thr +inf)
-            const int r = (v & 3) + 8 * (v >> 2) + 4 * h;
+            const int r = rt + (v & 3) + 8 * (v >> 2) + 4 * h;
             atomicAdd(&S.u.h[r][__float_as_uint(fmaxf(0.f, -2.f * c[v])) >> 23], 1u);
          }
          continue;
@@ -545,7 +549,7 @@ __device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restr
       if (!any) continue;
 #pragma unroll
       for (int v = 0; v < 16; v++) {
-         const int r = (v & 3) + 8 * (v >> 2) + 4 * h;
+         const int r = rt + (v & 3) + 8 * (v >> 2) + 4 * h;
          const bool pass = MODE == 3 ? c[v] >= thr[v] : c[v] > thr[v];
          if (!pass || (CHECK && j >= i0 + r)) continue;
          if (MODE == 3) {

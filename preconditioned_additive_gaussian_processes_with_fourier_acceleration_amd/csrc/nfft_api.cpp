@@ -940,6 +940,16 @@ int Nfft4GPAmdAdditiveComponentShard(void* str, int nw_global, int own_diag)
    return 0;
 }
 
+// the two-launch shard path: NFFT4GP_AMD_SHARD_FUSE, or the test hook below; off by default
+static int g_shard_fuse = -1;
+static int shard_fuse()
+{
+   if (g_shard_fuse < 0) g_shard_fuse = getenv("NFFT4GP_AMD_SHARD_FUSE") ? atoi(getenv("NFFT4GP_AMD_SHARD_FUSE")) : 0;
+   return g_shard_fuse;
+}
+
+extern "C" void Nfft4GPAmdDebugSetShardFuse(int on) { g_shard_fuse = on ? 1 : 0; }
+
 int Nfft4GPAmdShardSpread(void* str, const double* x_local, double* grid)
 {
    PlanExt* E = additive_plan(str);
@@ -953,9 +963,8 @@ int Nfft4GPAmdShardSpread(void* str, const double* x_local, double* grid)
    }
    // the blocks' partial grids summed inside the spread (its last block per slice of window groups), or by
    // k_reduce_parts after it (NFFT4GP_AMD_SHARD_FUSE=0; the persistent spread variants)
-   static const int fuse = getenv("NFFT4GP_AMD_SHARD_FUSE") ? atoi(getenv("NFFT4GP_AMD_SHARD_FUSE")) : 0;
    const int gpw = std::min(std::max(P.gpw, 1), P.ngroups);
-   if (fuse && P.spread_variant < 5 && P.dl.ntiles > 0 && (P.ngroups + gpw - 1) / gpw <= kMaxSumSlices)
+   if (shard_fuse() && P.spread_variant < 5 && P.dl.ntiles > 0 && (P.ngroups + gpw - 1) / gpw <= kMaxSumSlices)
       return launch_spread(P, x_local, P.d_part, s, grid);
    if (launch_spread(P, x_local, P.d_part, s)) return -1;
    return launch_reduce_parts(P, P.d_part, grid, s);
@@ -979,8 +988,7 @@ int Nfft4GPAmdShardFinish(void* str, const double* grid, int grad, double alpha,
    int S = P.nblocks <= 64 ? 4 : 1;
    if (const char* e = getenv("NFFT4GP_AMD_SHARD_SPLIT")) S = std::max(1, std::min(16, atoi(e)));
    S = std::min(S, std::max(1, P.ngroups));
-   static const int fuse = getenv("NFFT4GP_AMD_SHARD_FUSE") ? atoi(getenv("NFFT4GP_AMD_SHARD_FUSE")) : 0;
-   if (!grad && S > 1 && !P.timing && fuse && P.nblocks <= kMaxSumSlices &&
+   if (!grad && S > 1 && !P.timing && shard_fuse() && P.nblocks <= kMaxSumSlices &&
        shard_finish_lds_bytes(P, S) <= 160 * 1024) {
       const size_t need = (size_t)S * P.nblocks * P.B;
       if (P.ypart_count < need) {
