@@ -150,6 +150,12 @@ struct MdPlan {
    double* d_bhd = nullptr;  // [nw][M]  the same for the derivative kernel, times dscale
    double* d_dot_part = nullptr;
    unsigned int* d_dot_ticket = nullptr;
+   // tiled spread: each component's points sorted by the 8^d tile of their first tap cell; work items
+   // (component, tile, first, end) of at most a few thousand points, each summed in LDS then added to the grid
+   int* d_perm = nullptr;    // [comp][n] local point indices in tile order
+   int4* d_items = nullptr;  // {comp, tile, first, end} (first/end index the component's d_perm)
+   int nitems = 0;
+   double* d_part = nullptr; // tiled interpolation: [2][comp][n] per-component values (K, then K')
 };
 
 struct AdditivePlan {

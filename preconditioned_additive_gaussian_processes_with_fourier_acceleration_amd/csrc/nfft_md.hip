@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "internal.h"
@@ -76,6 +77,215 @@ __global__ __launch_bounds__(kMdThreads) void k_md_spread(const MdComp* __restri
    const int u0 = uj[0];
 #pragma unroll
    for (int lt = 0; lt < kTaps; lt++) atomicAdd(g + ((u0 + lt) & (kNos - 1)), w * pj[lt]);
+}
+
+// Tiled spread: work item (component, tile, first, end) = the points of one 8^d tile of first-tap cells (a
+// chunk of them); their 10^d taps are summed into the tile's (8 + 9)^d footprint in LDS (ds_add_f64), and
+// the footprint's non-zero cells are then added to the grid (one global atomic per cell and item instead
+// of one per tap: 1000 per point in 3-D).  Thread = (point, tap row over axes 1..d-1) as k_md_spread.
+constexpr int kMdTile = 8;
+constexpr int kMdFoot = kMdTile + kTaps - 1;  // 17
+constexpr int kMdSpreadThreads = 512;
+__global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdComp* __restrict__ comps,
+                                                                      const int4* __restrict__ items,
+                                                                      const int* __restrict__ perm,
+                                                                      const int* __restrict__ u,
+                                                                      const double* __restrict__ psi,
+                                                                      const double* __restrict__ x, int n,
+                                                                      double* __restrict__ grid, long long G)
+{
+   extern __shared__ double s_acc[];  // kMdFoot^d
+   const int4 it = items[blockIdx.x];
+   const MdComp cp = comps[it.x];
+   const int d = cp.d;
+   int foot = 1, ntile = 1;
+   for (int t = 0; t < d; t++) {
+      foot *= kMdFoot;
+      ntile *= kNos / kMdTile;
+   }
+   (void)ntile;
+   int lo[kMdMaxDim];
+   {
+      int rem = it.y;
+      for (int t = 0; t < d; t++) {
+         lo[t] = (rem % (kNos / kMdTile)) * kMdTile;
+         rem /= kNos / kMdTile;
+      }
+   }
+   for (int e = threadIdx.x; e < foot; e += kMdSpreadThreads) s_acc[e] = 0.0;
+   __syncthreads();
+   const int* pp = perm + (long long)it.x * n;
+   const int npts = it.w - it.z;
+   const long long work = (long long)npts * cp.hicount;
+   for (long long w = threadIdx.x; w < work; w += kMdSpreadThreads) {
+      const int k = (int)(w / cp.hicount), hi = (int)(w % cp.hicount);
+      const int j = pp[it.z + k];
+      const int* uj = u + cp.u_off + (long long)j * d;
+      const double* pj = psi + (cp.u_off + (long long)j * d) * kTaps;
+      // local footprint index of the row's first cell and the row's tap product
+      double wt = x[j];
+      int e = 0, stride = kMdFoot;
+      int rem = hi;
+      for (int t = 1; t < d; t++) {
+         const int lt = rem % kTaps;
+         rem /= kTaps;
+         e += (((uj[t] & (kNos - 1)) - lo[t]) + lt) * stride;
+         stride *= kMdFoot;
+         wt *= pj[t * kTaps + lt];
+      }
+      e += (uj[0] & (kNos - 1)) - lo[0];
+#pragma unroll
+      for (int lt = 0; lt < kTaps; lt++) atomicAdd(s_acc + e + lt, wt * pj[lt]);
+   }
+   __syncthreads();
+   double* g = grid + (long long)it.x * G;
+   for (int e = threadIdx.x; e < foot; e += kMdSpreadThreads) {
+      const double v = s_acc[e];
+      if (v == 0.0) continue;
+      long long idx = 0, stride = 1;
+      int rem = e;
+      for (int t = 0; t < d; t++) {
+         idx += (long long)((lo[t] + rem % kMdFoot) & (kNos - 1)) * stride;
+         rem /= kMdFoot;
+         stride *= kNos;
+      }
+      atomicAdd(g + idx, v);
+   }
+}
+
+// Tiled interpolation, the spread's work items: the tile's footprint of h (and h' for the gradient) is
+// staged in LDS, each point's 10^d taps are read from there by a group of L lanes (L = 64 / 16 / 1 for
+// 3 / 2 / 1 features: the point's tap rows strided over the group, a fixed-order butterfly sum), and the
+// component's value of the point goes to part[comp][j]; k_md_combine sums the components in order and
+// applies the epilogue.
+template <int GRAD>
+__global__ __launch_bounds__(kMdSpreadThreads) void k_md_interp_tiled(const MdComp* __restrict__ comps,
+                                                                      const int4* __restrict__ items,
+                                                                      const int* __restrict__ perm,
+                                                                      const int* __restrict__ u,
+                                                                      const double* __restrict__ psi,
+                                                                      const double* __restrict__ h0,
+                                                                      const double* __restrict__ h1, long long G,
+                                                                      int n, int nw, double* __restrict__ part)
+{
+   extern __shared__ double s_h[];  // [GRAD + 1][kMdFoot^d]
+   const int4 it = items[blockIdx.x];
+   const MdComp cp = comps[it.x];
+   const int d = cp.d;
+   int foot = 1;
+   for (int t = 0; t < d; t++) foot *= kMdFoot;
+   int lo[kMdMaxDim];
+   {
+      int rem = it.y;
+      for (int t = 0; t < d; t++) {
+         lo[t] = (rem % (kNos / kMdTile)) * kMdTile;
+         rem /= kNos / kMdTile;
+      }
+   }
+   const double* g0 = h0 + (long long)it.x * G;
+   const double* g1 = h1 + (long long)it.x * G;
+   for (int e = threadIdx.x; e < foot; e += kMdSpreadThreads) {
+      long long idx = 0, stride = 1;
+      int rem = e;
+      for (int t = 0; t < d; t++) {
+         idx += (long long)((lo[t] + rem % kMdFoot) & (kNos - 1)) * stride;
+         rem /= kMdFoot;
+         stride *= kNos;
+      }
+      s_h[e] = g0[idx];
+      if (GRAD) s_h[foot + e] = g1[idx];
+   }
+   __syncthreads();
+   const int L = d >= 3 ? 64 : d == 2 ? 16 : 1;  // lanes per point
+   const int lane = threadIdx.x & (L - 1);
+   const int groups = kMdSpreadThreads / L;
+   const int* pp = perm + (long long)it.x * n;
+   const int npts = it.w - it.z;
+   // every group runs the same number of passes (the butterfly needs whole waves)
+   for (int k0 = 0; k0 < npts; k0 += groups) {
+      const int k = k0 + (int)threadIdx.x / L;
+      const bool ok = k < npts;
+      double a0 = 0.0, a1 = 0.0;
+      int j = 0;
+      if (ok) {
+         j = pp[it.z + k];
+         const int* uj = u + cp.u_off + (long long)j * d;
+         const double* pj = psi + (cp.u_off + (long long)j * d) * kTaps;
+         const int o0 = (uj[0] & (kNos - 1)) - lo[0];
+         for (int hi = lane; hi < cp.hicount; hi += L) {
+            double wt = 1.0;
+            int e = o0, stride = kMdFoot, rem = hi;
+            for (int t = 1; t < d; t++) {
+               const int lt = rem % kTaps;
+               rem /= kTaps;
+               e += (((uj[t] & (kNos - 1)) - lo[t]) + lt) * stride;
+               stride *= kMdFoot;
+               wt *= pj[t * kTaps + lt];
+            }
+            double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+            for (int lt = 0; lt < kTaps; lt++) {
+               v0 = fma(s_h[e + lt], pj[lt], v0);
+               if (GRAD) v1 = fma(s_h[foot + e + lt], pj[lt], v1);
+            }
+            a0 = fma(wt, v0, a0);
+            if (GRAD) a1 = fma(wt, v1, a1);
+         }
+      }
+      for (int off = L / 2; off > 0; off >>= 1) {
+         a0 += __shfl_xor(a0, off, 64);
+         if (GRAD) a1 += __shfl_xor(a1, off, 64);
+      }
+      if (ok && lane == 0) {
+         part[(long long)it.x * n + j] = a0;
+         if (GRAD) part[((long long)nw + it.x) * n + j] = a1;
+      }
+   }
+}
+
+// y from the components' values in component order, with the 1-D path's epilogue (k_md_interp's)
+template <int GRAD, int DOT>
+__global__ __launch_bounds__(kMdThreads) void k_md_combine(int nw, const double* __restrict__ part,
+                                                           const double* __restrict__ x, double* __restrict__ y,
+                                                           int n, double alpha, double beta, double f, double mu,
+                                                           double dg, double* __restrict__ dot_part,
+                                                           unsigned int* __restrict__ dot_ticket,
+                                                           double* __restrict__ dot_out)
+{
+   const double ff = f * f;
+   double dacc = 0.0;
+   for (int j = blockIdx.x * kMdThreads + threadIdx.x; j < n; j += gridDim.x * kMdThreads) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int c = 0; c < nw; c++) {
+         s0 += part[(long long)c * n + j];
+         if (GRAD) s1 += part[((long long)nw + c) * n + j];
+      }
+      const double xj = x[j];
+      if (!GRAD) {
+         const double v = ff * (s0 + mu * xj);
+         const double yo = (beta == 0.0) ? alpha * v : fma(beta, y[j], alpha * v);
+         y[j] = yo;
+         if (DOT) dacc = fma(yo, xj, dacc);
+      } else {
+         const double v0 = 2.0 * f * (s0 + mu * xj), v1 = ff * s1, v2 = dg * ff * xj;
+         double* y1 = y + n;
+         double* y2 = y + 2 * (size_t)n;
+         if (beta == 0.0) {
+            y[j] = alpha * v0;
+            y1[j] = alpha * v1;
+            y2[j] = alpha * v2;
+         } else {
+            y[j] = fma(beta, y[j], alpha * v0);
+            y1[j] = fma(beta, y1[j], alpha * v1);
+            y2[j] = fma(beta, y2[j], alpha * v2);
+         }
+      }
+   }
+   if (DOT) {
+      dacc = block_sum0<kMdThreads>(dacc);
+      double tot;
+      if (grid_total<kMdThreads>(dacc, dot_part, dot_ticket, &tot) && threadIdx.x == 0) *dot_out = tot;
+   }
 }
 
 // forward pass along axis t: in [32^t][64][64^(d-t-1)] (real grid when t == 0) -> out [32^t][32][...]
@@ -303,6 +513,10 @@ void md_free(AdditivePlan& P)
    dfree_md(D.d_bhd);
    dfree_md(D.d_dot_part);
    dfree_md(D.d_dot_ticket);
+   dfree_md(D.d_perm);
+   dfree_md(D.d_items);
+   dfree_md(D.d_part);
+   D.nitems = 0;
 }
 
 // first setup: PRE_PSI taps of the kept rows (nfft_interface.c:150-213 then fastsum's PRE_PSI), buffers
@@ -368,6 +582,47 @@ int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
       NFFT4GP_HIP_CHECK(hipMemcpy(D.d_psi, psi.data(), sizeof(double) * psi.size(), hipMemcpyHostToDevice));
    }
    NFFT4GP_HIP_CHECK(hipMemset(D.d_dot_ticket, 0, sizeof(unsigned int) * kTicketWords));
+   // tiled spread: per component, a counting sort of the points by the tile of their first tap cell, then
+   // items of at most ~2e6 / 10^d points
+   {
+      std::vector<int> perm((size_t)P.nw * n);
+      std::vector<int4> items;
+      for (int c = 0; c < P.nw; c++) {
+         const MdComp& cp = D.comps[c];
+         const int d = cp.d;
+         const int tiles_per_axis = kNos / kMdTile;
+         int ntiles = 1, taps = 1;
+         for (int t = 0; t < d; t++) {
+            ntiles *= tiles_per_axis;
+            taps *= kTaps;
+         }
+         std::vector<int> tile(n), cnt(ntiles + 1, 0);
+         for (int j = 0; j < n; j++) {
+            int tl = 0, mul = 1;
+            for (int t = 0; t < d; t++) {
+               tl += ((u[cp.u_off + (size_t)j * d + t] & (kNos - 1)) / kMdTile) * mul;
+               mul *= tiles_per_axis;
+            }
+            tile[j] = tl;
+            cnt[tl + 1]++;
+         }
+         for (int t = 0; t < ntiles; t++) cnt[t + 1] += cnt[t];
+         std::vector<int> pos(cnt.begin(), cnt.end() - 1);
+         int* pc = perm.data() + (size_t)c * n;
+         for (int j = 0; j < n; j++) pc[pos[tile[j]]++] = j;
+         const int chunk = std::max(256, 2000000 / taps);
+         for (int t = 0; t < ntiles; t++)
+            for (int b = cnt[t]; b < cnt[t + 1]; b += chunk) items.push_back(make_int4(c, t, b, std::min(cnt[t + 1], b + chunk)));
+      }
+      D.nitems = (int)items.size();
+      if (dalloc(&D.d_perm, perm.size()) || dalloc(&D.d_items, items.size()) ||
+          dalloc(&D.d_part, 2 * (size_t)P.nw * n))
+         return -1;
+      if (!perm.empty())
+         NFFT4GP_HIP_CHECK(hipMemcpy(D.d_perm, perm.data(), sizeof(int) * perm.size(), hipMemcpyHostToDevice));
+      if (!items.empty())
+         NFFT4GP_HIP_CHECK(hipMemcpy(D.d_items, items.data(), sizeof(int4) * items.size(), hipMemcpyHostToDevice));
+   }
    return upload_md_constants();
 }
 
@@ -405,6 +660,22 @@ int md_spread(const AdditivePlan& P, const double* d_x, double* d_grid, hipStrea
    const MdPlan& D = P.md;
    NFFT4GP_HIP_CHECK(hipMemsetAsync(d_grid, 0, sizeof(double) * (size_t)P.nw * D.G, s));
    if (P.n == 0) return 0;
+   static const int tiled = getenv("NFFT4GP_AMD_MD_SPREAD") ? atoi(getenv("NFFT4GP_AMD_MD_SPREAD")) : 1;
+   if (tiled && D.nitems > 0) {
+      size_t foot = 1;
+      for (int t = 0; t < D.maxd; t++) foot *= kMdFoot;
+      static bool attr = false;
+      if (!attr) {
+         (void)hipFuncSetAttribute((const void*)k_md_spread_tiled, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024);
+         (void)hipGetLastError();
+         attr = true;
+      }
+      hipLaunchKernelGGL(k_md_spread_tiled, dim3(D.nitems), dim3(kMdSpreadThreads), sizeof(double) * foot, s,
+                         D.d_comps, D.d_items, D.d_perm, D.d_u, D.d_psi, d_x, P.n, d_grid, D.G);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   }
    int hi_max = 1;
    for (int t = 1; t < D.maxd; t++) hi_max *= kTaps;
    const long long work = (long long)P.n * hi_max;
@@ -445,6 +716,45 @@ int md_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, 
    const MdPlan& D = P.md;
    if (P.n == 0) {
       if (d_dot) NFFT4GP_HIP_CHECK(hipMemsetAsync(d_dot, 0, sizeof(double), s));
+      return 0;
+   }
+   static const int tiled = getenv("NFFT4GP_AMD_MD_INTERP") ? atoi(getenv("NFFT4GP_AMD_MD_INTERP")) : 1;
+   // small handles (TEST1's bike: ~34 points per 3-D tile) stage more footprint than they read: one wave per
+   // point over the L2-resident grid instead
+   long long tiles = 1;
+   for (int t = 0; t < D.maxd; t++) tiles *= kNos / kMdTile;
+   if (tiled && D.nitems > 0 && D.d_part && (long long)P.n >= 100 * tiles) {
+      size_t foot = 1;
+      for (int t = 0; t < D.maxd; t++) foot *= kMdFoot;
+      static bool attr = false;
+      if (!attr) {
+         (void)hipFuncSetAttribute((const void*)k_md_interp_tiled<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024);
+         (void)hipFuncSetAttribute((const void*)k_md_interp_tiled<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024);
+         (void)hipGetLastError();
+         attr = true;
+      }
+      if (grad)
+         hipLaunchKernelGGL(k_md_interp_tiled<1>, dim3(D.nitems), dim3(kMdSpreadThreads), 2 * sizeof(double) * foot, s,
+                            D.d_comps, D.d_items, D.d_perm, D.d_u, D.d_psi, D.d_h[0], D.d_h[1], D.G, P.n, P.nw,
+                            D.d_part);
+      else
+         hipLaunchKernelGGL(k_md_interp_tiled<0>, dim3(D.nitems), dim3(kMdSpreadThreads), sizeof(double) * foot, s,
+                            D.d_comps, D.d_items, D.d_perm, D.d_u, D.d_psi, D.d_h[0], D.d_h[1], D.G, P.n, P.nw,
+                            D.d_part);
+      const int cb = std::min(kMdInterpBlocks, (P.n + kMdThreads - 1) / kMdThreads);
+#define NFFT4GP_MD_COMBINE(G_, D_)                                                                               \
+   hipLaunchKernelGGL((k_md_combine<G_, D_>), dim3(cb), dim3(kMdThreads), 0, s, P.nw, (const double*)D.d_part, d_x, \
+                      d_y, P.n, alpha, beta, P.f, P.mu * P.diag, P.diag, D.d_dot_part, D.d_dot_ticket, d_dot)
+      if (grad)
+         NFFT4GP_MD_COMBINE(1, 0);
+      else if (d_dot)
+         NFFT4GP_MD_COMBINE(0, 1);
+      else
+         NFFT4GP_MD_COMBINE(0, 0);
+#undef NFFT4GP_MD_COMBINE
+      NFFT4GP_HIP_CHECK(hipGetLastError());
       return 0;
    }
    const int blocks = std::min(kMdInterpBlocks, (P.n + kMdThreads / 64 - 1) / (kMdThreads / 64));
