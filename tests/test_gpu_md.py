@@ -148,3 +148,30 @@ def test_row_shards_sum_to_full(torch_cuda):
     ys = [s.shard_finish(total, torch.tensor(x[s.row_begin:s.row_end], device="cuda")).cpu().numpy()
           for s in shards]
     assert rel(np.concatenate(ys), y_full) < 1e-12
+
+
+@pytest.mark.parametrize("n,nw,dw", [(60000, 2, 3), (20000, 3, 2)])
+def test_tiled_paths_match_oracle(torch_cuda, n, nw, dw):
+    """Handles with >= 100 points per 8^d tile take the tiled interpolation (footprint of h in LDS, ordered
+    component combine) as well as the tiled spread: matvec with alpha / beta, all 3n gradient outputs and
+    host vectors against the oracle."""
+    rng = np.random.default_rng(n + dw)
+    X = rng.random((n, nw * dw))
+    check_operator(torch_cuda, X, np.arange(nw * dw, dtype=np.int32), nw, dw, 0, 1.0, 0.5, 0.01)
+
+
+def test_pcg_tiled_3d(torch_cuda):
+    """PCG's fused (q, p) dot through k_md_combine: converged, true residual at the tolerance."""
+    torch = torch_cuda
+    rng = np.random.default_rng(61)
+    n = 60000
+    X = rng.random((n, 6))
+    win = np.arange(6, dtype=np.int32)
+    op = amd.NFFTAdditiveKernel(X, win, 2, 3)
+    assert op.setup(0, 1.0, 0.3, 0.01) == 0
+    b = rng.random(n) - 0.5
+    x = torch.zeros(n, dtype=torch.float64, device="cuda")
+    x, rr, hist, it = amd.pcg(op, torch.tensor(b, device="cuda"), x, maxits=2000, tol=1e-8)
+    assert it > 0 and rr <= 1e-8
+    y = op.matsymv(x, 1.0, 0.0, torch.zeros(n, dtype=torch.float64, device="cuda")).cpu().numpy()
+    assert np.linalg.norm(b - y) / np.linalg.norm(b) < 1e-7
