@@ -125,7 +125,8 @@ struct DevLayout {
 };
 
 // multi-dimensional windows (nfft_md.hip): per-component 64^d grids, dims <= kMdMaxDim
-constexpr int kMdMaxDim = 3;
+constexpr int kMdMaxDim = 4;     // 4-feature windows: 64^4 grids (134 MB each), the untiled spread / interp
+constexpr int kMdTiledMaxDim = 3;  // the tiled kernels' LDS footprint (17^d doubles) fits up to 3 features
 struct MdComp {
    int d = 0;
    int hicount = 1;          // kTaps^(d-1): tap rows per point

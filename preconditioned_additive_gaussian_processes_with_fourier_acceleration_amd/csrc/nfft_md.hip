@@ -16,9 +16,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <thread>
 #include <vector>
 
 #include "internal.h"
@@ -552,20 +554,37 @@ int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
       off += (long long)P.n * cp.d;
    }
    const int n = P.n, ng = P.n_global;
-   std::vector<int> u;
-   std::vector<double> psi;
-   for (int c = 0; c < P.nw; c++) {
+   // PRE_PSI taps of every (component, point, axis), filled by up to 16 host threads over point ranges
+   std::vector<int> u((size_t)off);
+   std::vector<double> psi((size_t)off * kTaps);
+   auto fill = [&](int c, int j0, int j1) {
       const int d = P.comp_dims[c];
-      for (int j = 0; j < n; j++)
+      for (int j = j0; j < j1; j++)
          for (int t = 0; t < d; t++) {
             const double xj = xs[c][(size_t)t * ng + P.row_begin + j];
             const int uj = (int)std::floor(xj * (double)kNos) - kM;
-            u.push_back(uj);
+            const size_t e = (size_t)D.comps[c].u_off + (size_t)j * d + t;
+            u[e] = uj;
             for (int lt = 0; lt < kTaps; lt++) {
                const double tx = xj - (double)(uj + lt) / (double)kNos;
-               psi.push_back(kb_phi(tx * (double)kNos));
+               psi[e * kTaps + lt] = kb_phi(tx * (double)kNos);
             }
          }
+   };
+   const int nth = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+   const int per = std::max(4096, (n + nth - 1) / nth);
+   {
+      std::vector<std::thread> th;
+      std::vector<std::pair<int, int>> work;
+      for (int c = 0; c < P.nw; c++)
+         for (int j0 = 0; j0 < n; j0 += per) work.push_back({c, j0});
+      std::atomic<size_t> next{0};
+      for (int t = 0; t < nth; t++)
+         th.emplace_back([&]() {
+            for (size_t w; (w = next.fetch_add(1)) < work.size();)
+               fill(work[w].first, work[w].second, std::min(n, work[w].second + per));
+         });
+      for (auto& t : th) t.join();
    }
    const size_t nw = (size_t)P.nw;
    if (dalloc(&D.d_comps, nw) || dalloc(&D.d_u, u.size()) || dalloc(&D.d_psi, psi.size()) ||
@@ -583,11 +602,12 @@ int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
    }
    NFFT4GP_HIP_CHECK(hipMemset(D.d_dot_ticket, 0, sizeof(unsigned int) * kTicketWords));
    // tiled spread: per component, a counting sort of the points by the tile of their first tap cell, then
-   // items of at most ~2e6 / 10^d points
-   {
+   // items of at most ~2e6 / 10^d points (up to 3 features; 4-feature handles use the untiled kernels)
+   if (D.maxd <= kMdTiledMaxDim) {
       std::vector<int> perm((size_t)P.nw * n);
-      std::vector<int4> items;
-      for (int c = 0; c < P.nw; c++) {
+      std::vector<std::vector<int4>> citems(P.nw);
+      auto sort_comp = [&](int c) {
+         std::vector<int4>& items = citems[c];
          const MdComp& cp = D.comps[c];
          const int d = cp.d;
          const int tiles_per_axis = kNos / kMdTile;
@@ -613,7 +633,18 @@ int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
          const int chunk = std::max(256, 2000000 / taps);
          for (int t = 0; t < ntiles; t++)
             for (int b = cnt[t]; b < cnt[t + 1]; b += chunk) items.push_back(make_int4(c, t, b, std::min(cnt[t + 1], b + chunk)));
+      };
+      {
+         std::vector<std::thread> th;
+         std::atomic<int> next{0};
+         for (int t = 0; t < std::min(nth, P.nw); t++)
+            th.emplace_back([&]() {
+               for (int c; (c = next.fetch_add(1)) < P.nw;) sort_comp(c);
+            });
+         for (auto& t : th) t.join();
       }
+      std::vector<int4> items;
+      for (auto& ci : citems) items.insert(items.end(), ci.begin(), ci.end());
       D.nitems = (int)items.size();
       if (dalloc(&D.d_perm, perm.size()) || dalloc(&D.d_items, items.size()) ||
           dalloc(&D.d_part, 2 * (size_t)P.nw * n))
@@ -661,7 +692,7 @@ int md_spread(const AdditivePlan& P, const double* d_x, double* d_grid, hipStrea
    NFFT4GP_HIP_CHECK(hipMemsetAsync(d_grid, 0, sizeof(double) * (size_t)P.nw * D.G, s));
    if (P.n == 0) return 0;
    static const int tiled = getenv("NFFT4GP_AMD_MD_SPREAD") ? atoi(getenv("NFFT4GP_AMD_MD_SPREAD")) : 1;
-   if (tiled && D.nitems > 0) {
+   if (tiled && D.nitems > 0 && D.maxd <= kMdTiledMaxDim) {
       size_t foot = 1;
       for (int t = 0; t < D.maxd; t++) foot *= kMdFoot;
       static bool attr = false;
@@ -723,7 +754,7 @@ int md_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, 
    // point over the L2-resident grid instead
    long long tiles = 1;
    for (int t = 0; t < D.maxd; t++) tiles *= kNos / kMdTile;
-   if (tiled && D.nitems > 0 && D.d_part && (long long)P.n >= 100 * tiles) {
+   if (tiled && D.nitems > 0 && D.d_part && D.maxd <= kMdTiledMaxDim && (long long)P.n >= 100 * tiles) {
       size_t foot = 1;
       for (int t = 0; t < D.maxd; t++) foot *= kMdFoot;
       static bool attr = false;

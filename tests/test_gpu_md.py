@@ -175,3 +175,24 @@ def test_pcg_tiled_3d(torch_cuda):
     assert it > 0 and rr <= 1e-8
     y = op.matsymv(x, 1.0, 0.0, torch.zeros(n, dtype=torch.float64, device="cuda")).cpu().numpy()
     assert np.linalg.norm(b - y) / np.linalg.norm(b) < 1e-7
+
+
+def test_window_of_four_features_matches_fixture(torch_cuda):
+    """A window of 4 features (64^4 grids, the untiled spread / interpolation) against the oracle's NFFT
+    values committed in tests/golden/md4d.npz (tests/golden/make_md4d.py: ~80 s per oracle matvec on the
+    host, too slow to run here): matvec and all 3n gradient outputs to 1e-10; the oracle itself sits
+    within the N = 32 truncation of the reference's dense operator (y_dense)."""
+    import os
+    torch = torch_cuda
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "md4d.npz"))
+    X, x = z["X"], z["x"]
+    n = x.size
+    op = amd.NFFTAdditiveKernel(X, np.arange(4, dtype=np.int32), 1, 4)
+    assert op.setup(0, float(z["f"]), float(z["l"]), float(z["mu"])) == 0
+    xd = torch.tensor(x, device="cuda")
+    y = op.matsymv(xd, 1.0, 0.0, torch.zeros(n, dtype=torch.float64, device="cuda")).cpu().numpy()
+    assert rel(y, z["y_nfft"]) < TOL
+    g = op.gradmatsymv(xd, 1.0, 0.0, torch.zeros(3 * n, dtype=torch.float64, device="cuda")).cpu().numpy()
+    for i in range(3):
+        assert rel(g[i * n:(i + 1) * n], z["g_nfft"][i * n:(i + 1) * n]) < TOL, i
+    assert rel(z["y_nfft"], z["y_dense"]) < 1e-2
