@@ -264,15 +264,15 @@ __global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__
          const int comp = c_begin + idx / kNos, cell = idx % kNos;
          const double* src = part + (size_t)comp * nblocks * kNos + cell;
          double acc = 0.0;
-         for (int p0 = 0; p0 < nblocks; p0 += 8) {
-            double v[8];
+         for (int p0 = 0; p0 < nblocks; p0 += 16) {
+            double v[16];
 #pragma unroll
-            for (int k = 0; k < 8; k++)
+            for (int k = 0; k < 16; k++)
                v[k] = p0 + k < nblocks
                           ? __hip_atomic_load(src + (size_t)(p0 + k) * kNos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                           : 0.0;
 #pragma unroll
-            for (int k = 0; k < 8; k++) acc += v[k];
+            for (int k = 0; k < 16; k++) acc += v[k];
          }
          gsum[(size_t)comp * kNos + cell] = acc;
       }
@@ -604,6 +604,7 @@ __global__ __launch_bounds__(THREADS) void k_shard_finish(const uint16_t* __rest
    double* s_H = smem + B + kPad;                 // [nc][64][kNC]
    double* s_g = s_H + (size_t)nc * kNos * kNC;   // [nc][64]
    double* s_h = s_g + (size_t)nc * kNos;         // [nc][64]
+   double* s_w = s_h + (size_t)nc * kNos;         // [nc][64] circulants
    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
    constexpr int nwaves = THREADS / 64;
    const int base = b * B;
@@ -613,11 +614,14 @@ __global__ __launch_bounds__(THREADS) void k_shard_finish(const uint16_t* __rest
    TileRegs cur;
    if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
    for (int i = tid; i < B + kPad; i += THREADS) s_y[i] = 0.0;
-   for (int i = tid; i < nc * kNos; i += THREADS) s_g[i] = gsum[(size_t)c_begin * kNos + i];
+   for (int i = tid; i < nc * kNos; i += THREADS) {
+      s_g[i] = gsum[(size_t)c_begin * kNos + i];
+      s_w[i] = w[(size_t)c_begin * kNos + i];
+   }
    __syncthreads();
    for (int i = tid; i < nc * kNos; i += THREADS) {
       const int c = i / kNos, tt = i % kNos;
-      const double* wc = w + (size_t)(c_begin + c) * kNos;
+      const double* wc = s_w + c * kNos;
       const double* gc = s_g + c * kNos;
       double h = 0.0;
 #pragma unroll 8
@@ -1133,7 +1137,7 @@ int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, do
 size_t shard_finish_lds_bytes(const AdditivePlan& P, int S)
 {
    const int ncmax = ((P.ngroups + S - 1) / S) * P.CG;
-   return sizeof(double) * ((size_t)P.B + kPad + (size_t)ncmax * kNos * (kNC + 2));
+   return sizeof(double) * ((size_t)P.B + kPad + (size_t)ncmax * kNos * (kNC + 3));
 }
 
 int launch_shard_finish_fused(const AdditivePlan& P, const double* d_gridsum, double alpha, const double* d_x,
