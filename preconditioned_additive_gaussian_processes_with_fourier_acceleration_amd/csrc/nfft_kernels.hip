@@ -437,17 +437,27 @@ extern "C" int Nfft4GPAmdDebugStamps(unsigned long long* out, int nwg)
 // ------------------------------------------------------------------------------------------------
 // grid: sum partial grids, circulant, interpolation polynomials
 // ------------------------------------------------------------------------------------------------
+// circulant h = w (*) g, then H[cell][d] = sum_t h[cell - m + t] C[t][d].  The circulant runs as 16
+// strands of 4 terms per output summed in a fixed butterfly inside the wave (blockDim >= 1024: 4 outputs
+// x 16 strands per wave); one 64-term chain per output was bound by its dependent LDS reads.
 __device__ void grid_tail(int comp, const double* __restrict__ s_g, const double* __restrict__ w,
                           double* __restrict__ H, double* s_w, double* s_h)
 {
    const int tid = threadIdx.x;
    if (tid < kNos) s_w[tid] = w[(size_t)comp * kNos + tid];
    __syncthreads();
-   if (tid < kNos) {
+   {
+      const int o = tid >> 4, st = tid & 15;
       double h = 0.0;
-#pragma unroll 8
-      for (int l2 = 0; l2 < kNos; l2++) h = fma(s_w[(tid - l2) & (kNos - 1)], s_g[l2], h);
-      s_h[tid] = h;
+      if (o < kNos) {
+#pragma unroll
+         for (int k = 0; k < 4; k++) {
+            const int l2 = st * 4 + k;
+            h = fma(s_w[(o - l2) & (kNos - 1)], s_g[l2], h);
+         }
+      }
+      for (int off = 8; off > 0; off >>= 1) h += __shfl_xor(h, off, 64);
+      if (o < kNos && st == 0) s_h[o] = h;
    }
    __syncthreads();
    for (int idx = tid; idx < kNos * kNC; idx += blockDim.x) {
@@ -526,37 +536,11 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_sum_yinit(const double* _
    __shared__ double s_w[kNos];
    const int comp = blockIdx.x;
    const int tid = threadIdx.x;
-   if (tid < kNos) {
-      s_g[tid] = gsum[(size_t)comp * kNos + tid];
-      s_w[tid] = w[(size_t)comp * kNos + tid];
-   }
+   if (tid < kNos) s_g[tid] = gsum[(size_t)comp * kNos + tid];
    for (size_t j = (size_t)blockIdx.x * kGridThreads + tid; j < (size_t)n; j += (size_t)gridDim.x * kGridThreads)
       y[j] = (beta == 0.0 ? 0.0 : beta * y[j]) + amu * x[j];
    __syncthreads();
-   // circulant h = w (*) g: 16 strands of 4 terms per output (the single 64-term chain of grid_tail is LDS-
-   // latency bound), summed in a fixed butterfly inside the wave (4 outputs x 16 strands per wave)
-   {
-      const int o = tid >> 4, st = tid & 15;  // o < 64 for the first 1024 threads
-      double h = 0.0;
-      if (o < kNos) {
-#pragma unroll
-         for (int k = 0; k < 4; k++) {
-            const int l2 = st * 4 + k;
-            h = fma(s_w[(o - l2) & (kNos - 1)], s_g[l2], h);
-         }
-      }
-      for (int off = 8; off > 0; off >>= 1) h += __shfl_xor(h, off, 64);
-      if (o < kNos && st == 0) s_h[o] = h;
-   }
-   __syncthreads();
-   for (int idx = tid; idx < kNos * kNC; idx += blockDim.x) {
-      const int cell = idx / kNC;
-      const int d = idx % kNC;
-      double v = 0.0;
-#pragma unroll
-      for (int tp = 0; tp < kTaps; tp++) v = fma(s_h[(cell - kM + tp) & (kNos - 1)], c_taps[tp * kNC + d], v);
-      H[((size_t)comp * kNos + cell) * kNC + d] = v;
-   }
+   grid_tail(comp, s_g, w, H, s_w, s_h);
 }
 
 template <int THREADS>
