@@ -31,11 +31,21 @@ namespace {
 int g_rand_depth = 0;
 char* g_caller_rand = nullptr;
 char g_private_rand[256];
+bool g_private_ready = false;
 }  // namespace
 
+// the private state is seeded once and then switched in with setstate (O(1)), so every entry point can
+// open a scope
 RandScope::RandScope()
 {
-   if (g_rand_depth++ == 0) g_caller_rand = initstate(20240807u, g_private_rand, sizeof(g_private_rand));
+   if (g_rand_depth++ == 0) {
+      if (!g_private_ready) {
+         g_caller_rand = initstate(20240807u, g_private_rand, sizeof(g_private_rand));
+         g_private_ready = true;
+      } else {
+         g_caller_rand = setstate(g_private_rand);
+      }
+   }
 }
 
 RandScope::~RandScope()
@@ -705,6 +715,7 @@ void* Nfft4GPNFFTAdditiveKernelParamCreate(double* data, int n, int ldim, int d,
                                            int dwindows)
 {
    (void)d;
+   RandScope rand_scope;  // HIP's first use may draw rand(); the reference's NFFT entry points draw none
    return additive_create(data, n, ldim, windows, nwindows, dwindows, 0, n);
 }
 
@@ -723,6 +734,7 @@ int Nfft4GPNFFTAdditiveKernelGaussianKernel(void* str, double* data, int n, int 
                                             int* permc, int kc, double** Kp, double** dKp)
 {
    (void)data, (void)d, (void)permr, (void)kr, (void)permc, (void)kc;
+   RandScope rand_scope;
    return setup_common(str, 0, n, ldim, Kp, dKp);
 }
 
@@ -730,6 +742,7 @@ int Nfft4GPNFFTAdditiveKernelMatern12Kernel(void* str, double* data, int n, int 
                                             int* permc, int kc, double** Kp, double** dKp)
 {
    (void)data, (void)d, (void)permr, (void)kr, (void)permc, (void)kc;
+   RandScope rand_scope;
    return setup_common(str, 1, n, ldim, Kp, dKp);
 }
 
@@ -737,6 +750,7 @@ int Nfft4GPAdditiveNFFTMatSymv(void* data, int n, double alpha, double* x, doubl
 {
    PlanExt* E = additive_plan(data);
    if (!E) return -1;
+   RandScope rand_scope;
    return plan_apply(E, n, 0, alpha, x, beta, y);
 }
 
@@ -766,6 +780,7 @@ int Nfft4GPAdditiveNFFTGradMatSymv(void* data, int n, double alpha, double* x, d
 {
    PlanExt* E = additive_plan(data);
    if (!E) return -1;
+   RandScope rand_scope;
    return plan_apply(E, n, 1, alpha, x, beta, y);
 }
 
@@ -1152,6 +1167,7 @@ int Nfft4GPNFFTKernelGaussianKernel(void* str, double* data, int n, int ldim, in
                                     int kc, double** Kp, double** dKp)
 {
    (void)permr, (void)kr, (void)permc, (void)kc;
+   RandScope rand_scope;
    return single_setup(str, 0, data, n, ldim, d, Kp, dKp);
 }
 
@@ -1159,6 +1175,7 @@ int Nfft4GPNFFTKernelMatern12Kernel(void* str, double* data, int n, int ldim, in
                                     int kc, double** Kp, double** dKp)
 {
    (void)permr, (void)kr, (void)permc, (void)kc;
+   RandScope rand_scope;
    return single_setup(str, 1, data, n, ldim, d, Kp, dKp);
 }
 
@@ -1166,6 +1183,7 @@ int Nfft4GPNFFTMatSymv(void* data, int n, double alpha, double* x, double beta, 
 {
    SingleAdj* adj = (SingleAdj*)data;
    if (!adj || !adj->plan) return -1;
+   RandScope rand_scope;
    return plan_apply(adj->plan, n, 0, alpha, x, beta, y);
 }
 
@@ -1173,6 +1191,7 @@ int Nfft4GPNFFTGradMatSymv(void* data, int n, double alpha, double* x, double be
 {
    SingleAdj* adj = (SingleAdj*)data;
    if (!adj || !adj->plan) return -1;
+   RandScope rand_scope;
    return plan_apply(adj->plan, n, 1, alpha, x, beta, y);
 }
 
