@@ -219,6 +219,7 @@ def test_fgmres_block_cgs2_matches_mgs(torch_cuda):
         res.append((x.cpu().numpy(), rr, hist[:it + 1], it))
     amd.lib().Nfft4GPAmdSetFgmresOrtho(0)
     assert res[0][3] == res[1][3] > 0 and res[1][1] <= 1e-8
-    np.testing.assert_allclose(res[1][2], res[0][2], rtol=1e-8)
+    # the history's tail sits at 1e-8 relative residual, where a 1e-16 rounding difference is 1e-8 relative
+    np.testing.assert_allclose(res[1][2], res[0][2], rtol=1e-8, atol=1e-14)
     assert np.linalg.norm(res[1][0] - res[0][0]) <= 1e-9 * np.linalg.norm(res[0][0])
     op.free()
