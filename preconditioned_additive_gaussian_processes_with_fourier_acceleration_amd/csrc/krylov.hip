@@ -44,28 +44,30 @@ int kgrid(size_t n)
    return (int)(g == 0 ? 1 : g);
 }
 
-// w -= (*hprev) * u (when u != nullptr); then *out = (w, v) (v != nullptr) or ||w||^2 (v == nullptr)
-__global__ __launch_bounds__(kKThreads) void k_gs_step(double* __restrict__ w, const double* __restrict__ u,
-                                                       const double* __restrict__ hprev,
-                                                       const double* __restrict__ v, size_t n,
-                                                       double* __restrict__ part, unsigned int* __restrict__ ticket,
-                                                       double* __restrict__ out)
+// w -= (*hprev) * u (when u != nullptr); then *out = (w, v) (v != nullptr) or ||w||^2 (v == nullptr).
+// T threads per block: 1024 gives a quarter of the partials for the last block to add (the MGS loop of
+// FGMRES runs one of these per projection, so its serial tail is most of a step at n = 1e6).
+template <int T, int EPT = kKEPT>
+__global__ __launch_bounds__(T) void k_gs_step(double* __restrict__ w, const double* __restrict__ u,
+                                               const double* __restrict__ hprev, const double* __restrict__ v,
+                                               size_t n, double* __restrict__ part, unsigned int* __restrict__ ticket,
+                                               double* __restrict__ out)
 {
    const double h = u ? *hprev : 0.0;
    double acc = 0.0;
-   const size_t stride = (size_t)gridDim.x * kKThreads * kKEPT;
-   for (size_t i0 = (size_t)blockIdx.x * kKThreads * kKEPT + threadIdx.x; i0 < n; i0 += stride) {
-      double wv[kKEPT], uv[kKEPT], vv[kKEPT];
+   const size_t stride = (size_t)gridDim.x * T * EPT;
+   for (size_t i0 = (size_t)blockIdx.x * T * EPT + threadIdx.x; i0 < n; i0 += stride) {
+      double wv[EPT], uv[EPT], vv[EPT];
 #pragma unroll
-      for (int e = 0; e < kKEPT; e++) {
-         const size_t i = i0 + (size_t)e * kKThreads;
+      for (int e = 0; e < EPT; e++) {
+         const size_t i = i0 + (size_t)e * T;
          wv[e] = i < n ? w[i] : 0.0;
          uv[e] = (u && i < n) ? u[i] : 0.0;
          vv[e] = (v && i < n) ? v[i] : 0.0;
       }
 #pragma unroll
-      for (int e = 0; e < kKEPT; e++) {
-         const size_t i = i0 + (size_t)e * kKThreads;
+      for (int e = 0; e < EPT; e++) {
+         const size_t i = i0 + (size_t)e * T;
          if (u) {
             wv[e] = fma(-h, uv[e], wv[e]);
             if (i < n) w[i] = wv[e];
@@ -73,9 +75,9 @@ __global__ __launch_bounds__(kKThreads) void k_gs_step(double* __restrict__ w, c
          acc = v ? fma(wv[e], vv[e], acc) : fma(wv[e], wv[e], acc);
       }
    }
-   acc = block_sum0<kKThreads>(acc);
+   acc = block_sum0<T>(acc);
    double tot;
-   if (grid_total<kKThreads>(acc, part, ticket, &tot) && threadIdx.x == 0) *out = tot;
+   if (grid_total<T>(acc, part, ticket, &tot) && threadIdx.x == 0) *out = tot;
 }
 
 // out[0] = (a, b), out[1] = (b, b): the Lanczos (v, z) and ||z||^2 in one pass
@@ -296,8 +298,23 @@ struct Ctx {
    // w -= h u (u optional), *out = (w, v) or ||w||^2
    int gs(double* w, const double* u, const double* hprev, const double* v, double* out)
    {
-      hipLaunchKernelGGL(k_gs_step, dim3(kgrid(n)), dim3(kKThreads), 0, s, w, u, hprev, v, n, g_k.part, g_k.ticket,
-                         out);
+      static const int variant = getenv("NFFT4GP_AMD_GS_VARIANT") ? atoi(getenv("NFFT4GP_AMD_GS_VARIANT")) : 1;
+      auto grid_for = [&](int T, int E) {
+         return (unsigned)std::max<size_t>(1, std::min<size_t>((n + (size_t)T * E - 1) / ((size_t)T * E), kKMaxBlocks));
+      };
+      if (variant == 1) {
+         hipLaunchKernelGGL((k_gs_step<1024, 4>), dim3(grid_for(1024, 4)), dim3(1024), 0, s, w, u, hprev, v, n,
+                            g_k.part, g_k.ticket, out);
+      } else if (variant == 2) {
+         hipLaunchKernelGGL((k_gs_step<1024, 8>), dim3(grid_for(1024, 8)), dim3(1024), 0, s, w, u, hprev, v, n,
+                            g_k.part, g_k.ticket, out);
+      } else if (variant == 3) {
+         hipLaunchKernelGGL((k_gs_step<512, 4>), dim3(grid_for(512, 4)), dim3(512), 0, s, w, u, hprev, v, n,
+                            g_k.part, g_k.ticket, out);
+      } else {
+         hipLaunchKernelGGL(k_gs_step<kKThreads>, dim3(kgrid(n)), dim3(kKThreads), 0, s, w, u, hprev, v, n, g_k.part,
+                            g_k.ticket, out);
+      }
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return red(out, 1);
    }
