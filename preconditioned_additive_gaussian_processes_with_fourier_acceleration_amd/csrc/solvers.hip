@@ -234,8 +234,10 @@ __device__ void pcg_xr_tail(double tot, PcgState* st, double* __restrict__ rhos,
    pcg_slot_write(st, slot, normr, ii);
 }
 
-// x += alpha p ; r -= alpha q ; ||r|| ; convergence test ; status slot  (pcg.c:168-182)
-__global__ __launch_bounds__(kVecThreads) void k_pcg_xr(double* __restrict__ x, double* __restrict__ r,
+// x += alpha p ; r -= alpha q ; ||r|| ; convergence test ; status slot  (pcg.c:168-182).  T = 1024: a
+// quarter of the block partials for the last block (the MGS step's measurement, krylov.hip)
+template <int T>
+__global__ __launch_bounds__(T) void k_pcg_xr(double* __restrict__ x, double* __restrict__ r,
                                                         const double* __restrict__ p, const double* __restrict__ q,
                                                         size_t n, double* __restrict__ part,
                                                         unsigned int* __restrict__ ticket, PcgState* st,
@@ -259,12 +261,12 @@ __global__ __launch_bounds__(kVecThreads) void k_pcg_xr(double* __restrict__ x, 
    }
    const double a = rhos[ii] / st->pq;
    double acc = 0.0;
-   const size_t stride = (size_t)gridDim.x * kVecThreads * kEPT;
-   for (size_t i0 = (size_t)blockIdx.x * kVecThreads * kEPT + threadIdx.x; i0 < n; i0 += stride) {
+   const size_t stride = (size_t)gridDim.x * T * kEPT;
+   for (size_t i0 = (size_t)blockIdx.x * T * kEPT + threadIdx.x; i0 < n; i0 += stride) {
       double xv[kEPT], rv[kEPT], pv[kEPT], qv[kEPT];
 #pragma unroll
       for (int u = 0; u < kEPT; u++) {
-         const size_t i = i0 + (size_t)u * kVecThreads;
+         const size_t i = i0 + (size_t)u * T;
          const bool ok = i < n;
          xv[u] = ok ? x[i] : 0.0;
          rv[u] = ok ? r[i] : 0.0;
@@ -273,7 +275,7 @@ __global__ __launch_bounds__(kVecThreads) void k_pcg_xr(double* __restrict__ x, 
       }
 #pragma unroll
       for (int u = 0; u < kEPT; u++) {
-         const size_t i = i0 + (size_t)u * kVecThreads;
+         const size_t i = i0 + (size_t)u * T;
          const double xi = xv[u] + a * pv[u];
          const double ri = rv[u] + (-a) * qv[u];
          acc = fma(ri, ri, acc);
@@ -283,9 +285,9 @@ __global__ __launch_bounds__(kVecThreads) void k_pcg_xr(double* __restrict__ x, 
          }
       }
    }
-   acc = block_sum0<kVecThreads>(acc);
+   acc = block_sum0<T>(acc);
    double tot;
-   if (!grid_total<kVecThreads>(acc, part, ticket, &tot) || threadIdx.x != 0) return;
+   if (!grid_total<T>(acc, part, ticket, &tot) || threadIdx.x != 0) return;
    if (loc) {
       *loc = tot;
       return;
@@ -740,6 +742,7 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
 
    const int g = pcg_grid(N);
    const int ge = g;
+   const int g_xr = (int)std::max<size_t>(1, std::min<size_t>((N + 1024 * kEPT - 1) / (1024 * kEPT), kPcgMaxBlocks));
    // this library's additive operator forms (q, p) in its own interpolation launch
    const bool fused_dot = cb.mv_dev && ((matvec == &Nfft4GPAdditiveNFFTMatSymv && additive_fused_dot_ok(mat_data)) ||
                                         (is_dist && dinfo.fused_dot));
@@ -788,7 +791,7 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
             }
          }
          PcgSlot* slot = slots_d + (ii % PcgScratch::kSlots);
-         hipLaunchKernelGGL(k_pcg_xr, dim3(g), dim3(kVecThreads), 0, s, vx.d, r, p, q, N, g_pcg.part, g_pcg.ticket,
+         hipLaunchKernelGGL(k_pcg_xr<1024>, dim3(g_xr), dim3(1024), 0, s, vx.d, r, p, q, N, g_pcg.part, g_pcg.ticket,
                             st, rhos, hist_d, ii, prec_data ? 0 : 1, fused_dot ? 1 : 0, slot, loc1);
          if (red) {
             if (red->allreduce(loc1, 1, s)) { rc = -1; break; }
