@@ -79,8 +79,9 @@ def case():
 # (key, kdim, maxits, Nystrom, history rtol, solution rtol).  The restarted case (kdim 10) stagnates at
 # |r| ~ 0.86 |b| on this ill-conditioned operator (l = 0.1) and its restart vector is not re-normalised
 # (fgmres.c:236-243 scales by the Givens estimate): measured, 1e-16 operator rounding grows to ~5e-5 in
-# the history within two cycles, so that case is held to 1e-3.
-FG_CASES = [("fg", 100, 400, False, 1e-5, 1e-6), ("fgr", 10, 60, False, 1e-3, 1e-3),
+# the history within two cycles, so that case's history is held to 1e-3 and its solution to 3e-3 (the
+# projections' summation order alone -- 256- or 1024-thread blocks in k_gs_step -- moves it 0.9e-3 / 1.06e-3).
+FG_CASES = [("fg", 100, 400, False, 1e-5, 1e-6), ("fgr", 10, 60, False, 1e-3, 3e-3),
             ("fgn", 100, 400, True, 1e-5, 1e-6)]
 
 
