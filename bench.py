@@ -389,12 +389,14 @@ class _StdoutToStderr:
         return False
 
 
-def run_loss(op, torch, n, d, X, rng_seed=906, maxits=50, nvecs=10, rows=None, dist=None):
+def run_loss(op, torch, n, d, X, rng_seed=906, maxits=50, nvecs=10, rows=None, dist=None, l=0.1):
     """One log-marginal-likelihood + gradient evaluation (Nfft4GPGpLoss, gp_loss.c:96-307: FGMRES for K^-1 y,
     stochastic Lanczos quadrature with nvecs Rademacher probes of maxits steps, the gradient matvecs) on the
-    bench's operator at (f, l, mu) = (1, 1, 0.01), identity transform -- the loop BASELINE configs[4] runs
-    at n = 1e7 on 8 GPUs, here at the bench's size.  With a distributed operator every rank runs it on its
-    rows (krylov.hip sums every inner product over the ranks); time: max over ranks."""
+    bench's operator at (f, l, mu) = (1, 0.1, 0.01), identity transform -- the loop BASELINE configs[4] runs
+    at n = 1e7 on 8 GPUs, here at the bench's size.  l = 0.1 as for PCG: at l = 1 the NFFT operator is
+    indefinite and the quadrature's Lanczos solve (lanczos.c, an LDL^T recursion of T) breaks
+    down, so the gradient comes out NaN there, as the reference's would.  With a distributed operator every
+    rank runs it on its rows (krylov.hip sums every inner product over the ranks); time: max over ranks."""
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
     rb, re = rows if rows is not None else (0, n)
     rng = np.random.default_rng(rng_seed + 3)
@@ -407,7 +409,7 @@ def run_loss(op, torch, n, d, X, rng_seed=906, maxits=50, nvecs=10, rows=None, d
         dist.barrier()
     t0 = time.time()
     with _StdoutToStderr():
-        loss, grad = amd.gp_loss(X, win, d, 1, y[rb:re], (1.0, 1.0, 0.01), maxits=maxits, nvecs=nvecs,
+        loss, grad = amd.gp_loss(X, win, d, 1, y[rb:re], (1.0, l, 0.01), maxits=maxits, nvecs=nvecs,
                                  rademacher=Rl, tol=1e-6, transform=3, op=op)
         torch.cuda.synchronize()
     t = time.time() - t0
@@ -416,7 +418,7 @@ def run_loss(op, torch, n, d, X, rng_seed=906, maxits=50, nvecs=10, rows=None, d
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
     return {"loss_time_s": t, "loss_value": loss, "loss_grad": [float(g) for g in grad], "loss_maxits": maxits,
-            "loss_nvecs": nvecs}
+            "loss_nvecs": nvecs, "loss_l": l}
 
 
 def main():

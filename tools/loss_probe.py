@@ -27,10 +27,11 @@ def main():
     for rep in range(2):
         torch.cuda.synchronize()
         t0 = time.time()
-        loss, grad = amd.gp_loss(X, win, d, 1, y, (1.0, 1.0, 0.01), maxits=50, nvecs=10, rademacher=Rl, tol=1e-6,
+        lval = float(os.environ.get("LOSS_L", "0.1"))
+        loss, grad = amd.gp_loss(X, win, d, 1, y, (1.0, lval, 0.01), maxits=50, nvecs=10, rademacher=Rl, tol=1e-6,
                                  transform=3, op=op)
         torch.cuda.synchronize()
-        print(f"loss {loss:.12e} time {time.time() - t0:.3f} s", file=sys.stderr, flush=True)
+        print(f"loss {loss:.12e} grad {list(grad)} time {time.time() - t0:.3f} s", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":
