@@ -478,7 +478,15 @@ def main():
         # RCCL; the gloo rehearsal of several ranks on one GPU (RCCL refuses that) uses the group's own
         # all-reduce through a staging buffer instead
         gloo = os.environ.get("NFFT4GP_BENCH_BACKEND", "nccl") == "gloo"
-        comm = Communicator.callback() if gloo else Communicator.rccl()
+        comm_kind = "rccl"
+        if gloo:
+            comm, comm_kind = Communicator.callback(), "gloo"
+        else:
+            try:
+                comm = Communicator.rccl()
+            except RuntimeError as e:  # the library's own RCCL communicator failed on every rank alike
+                print(f"bench: {e}; using torch's RCCL through Communicator.callback() instead", file=sys.stderr)
+                comm, comm_kind = Communicator.callback(), "callback"
         op = DistributedAdditiveKernel(X, win, d, 1, comm, partition=args.partition)
         rb, re = op.row_begin, op.row_end
     t0 = time.time()
@@ -685,7 +693,9 @@ def main():
     if world > 1:
         result["config"]["all_reduce_bytes_per_matvec"] = 8 * (op.n if args.partition == "components" else d * 64)
         result["config"]["communicator"] = ("gloo rehearsal (host all-reduce)" if gloo else
-                                            "RCCL (library-owned ncclComm, all-reduce enqueued by dist.hip)")
+                                            "RCCL (library-owned ncclComm, all-reduce enqueued by dist.hip)"
+                                            if comm_kind == "rccl" else
+                                            "RCCL through torch.distributed (callback fallback, synchronising)")
         if not args.no_pcg:
             result.update(run_pcg_single(op, torch, n, rows=(rb, re), dist=dist))
             result["pcg_impl"] = f"Nfft4GPSolverPcg on Nfft4GPAmdDistMatSymv ({args.partition}), device-controlled"

@@ -41,9 +41,10 @@ class Communicator:
 
     ``Communicator.rccl()``: RCCL over xGMI, one communicator per process created from an id that rank 0
     makes and torch.distributed broadcasts; all-reduces are enqueued on the library stream.
-    ``Communicator.callback()``: the all-reduce of a torch.distributed group (e.g. gloo, for several
-    ranks on one GPU, which RCCL refuses), through a device staging buffer; the sum goes through host
-    memory, so it synchronises -- a test path, not a fast one."""
+    ``Communicator.callback()``: the all-reduce of a torch.distributed group through a device staging
+    buffer -- gloo (several ranks on one GPU, which RCCL refuses) sums a host copy, nccl sums the staging
+    buffer itself with torch's own RCCL communicator; it synchronises -- a test and fallback path, not a
+    fast one."""
 
     def __init__(self, h, rank, world, keep=()):
         self.h, self.rank, self.world, self._keep = h, rank, world, keep
@@ -82,9 +83,14 @@ class Communicator:
         from . import _lib
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         stage = torch.zeros(capacity, dtype=torch.float64, device="cuda")
+        on_device = dist.get_backend(group) == "nccl"
 
         def _allreduce(ctx, ptr, count):
             try:
+                if on_device:  # torch's RCCL communicator, in place, on torch's current stream
+                    dist.all_reduce(stage[:count], group=group)
+                    torch.cuda.current_stream().synchronize()
+                    return 0
                 host = stage[:count].cpu()  # on torch's current stream = the library stream
                 dist.all_reduce(host, group=group)
                 stage[:count].copy_(host)

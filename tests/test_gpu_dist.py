@@ -52,7 +52,8 @@ def _worker(rank, world, port, outdir, backend):
     from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import (
         Communicator, DistributedAdditiveKernel, RowShardedAfn, RowShardedNystrom)
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # "nccl_callback": torch's own RCCL process group behind the callback communicator (bench.py's fallback)
+    dist.init_process_group("nccl" if backend == "nccl_callback" else "gloo", rank=rank, world_size=world)
     comm = Communicator.rccl() if backend == "rccl" else Communicator.callback()
     out = {}
     for kind in ("1d", "md"):
@@ -143,6 +144,11 @@ def gloo2(tmp_path_factory):
 @pytest.fixture(scope="module")
 def rccl1(tmp_path_factory):
     return _run(tmp_path_factory, "rccl", 1)
+
+
+@pytest.fixture(scope="module")
+def nccl_cb1(tmp_path_factory):
+    return _run(tmp_path_factory, "nccl_callback", 1)
 
 
 @pytest.fixture(scope="module")
@@ -295,3 +301,13 @@ def test_rccl_communicator_one_rank(rccl1, single, kind):
         assert rel(rccl1[0][key + "_y"], single[kind + "_y"]) < 1e-12
         assert rel(rccl1[0][key + "_g"], single[kind + "_g"]) < 1e-12
         assert int(rccl1[0][key + "_it"]) > 0
+
+
+@pytest.mark.parametrize("kind", ["1d", "md"])
+def test_callback_communicator_over_torch_nccl(nccl_cb1, single, kind):
+    """The callback communicator on a torch "nccl" (RCCL) group: device buffers all-reduced in place."""
+    for part in ("rows", "components"):
+        key = f"{kind}_{part}"
+        assert rel(nccl_cb1[0][key + "_y"], single[kind + "_y"]) < 1e-12
+        assert rel(nccl_cb1[0][key + "_g"], single[kind + "_g"]) < 1e-12
+        assert int(nccl_cb1[0][key + "_it"]) > 0
