@@ -62,18 +62,28 @@ class Communicator:
         from . import _lib
         L = _lib.lib()
         rank, world = dist.get_rank(group), dist.get_world_size(group)
-        buf = np.zeros(128, dtype=np.uint8)
-        if rank == 0 and L.Nfft4GPAmdCommUniqueId(buf.ctypes.data) != 0:
-            raise RuntimeError("Nfft4GPAmdCommUniqueId failed (RCCL not loadable, see stderr)")
+        on_device = dist.get_backend(group) == "nccl"
+        # the 128-byte id plus a status byte, so that a failure on rank 0 reaches every rank through the same
+        # broadcast (no rank is left waiting in a collective the others never enter)
+        buf = np.zeros(129, dtype=np.uint8)
+        if rank == 0:
+            buf[128] = 1 if L.Nfft4GPAmdCommUniqueId(buf.ctypes.data) == 0 else 0
         t = torch.from_numpy(buf)
-        if dist.get_backend(group) == "nccl":
+        if on_device:
             t = t.cuda()
         dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         buf = np.ascontiguousarray(t.cpu().numpy())
+        if buf[128] != 1:
+            raise RuntimeError("Nfft4GPAmdCommUniqueId failed on rank 0 (RCCL not loadable, see its stderr)")
         cls._bind_stream()
         h = L.Nfft4GPAmdCommCreateRccl(rank, world, buf.ctypes.data)
-        if not h:
-            raise RuntimeError("Nfft4GPAmdCommCreateRccl failed (see stderr)")
+        # every rank learns whether every rank has a communicator before any of them uses one
+        ok = torch.tensor([0.0 if h else 1.0], dtype=torch.float64, device="cuda" if on_device else "cpu")
+        dist.all_reduce(ok, group=group)
+        if float(ok.item()) != 0.0:
+            if h:
+                L.Nfft4GPAmdCommFree(h)
+            raise RuntimeError("Nfft4GPAmdCommCreateRccl failed on %d rank(s) (see stderr)" % int(ok.item()))
         return cls(h, rank, world)
 
     @classmethod
