@@ -2,7 +2,8 @@
 //
 // Per matvec three launches on one stream (see internal.h for the algebra):
 //   k_spread  one workgroup per (block of B points, group of CG windows).  The workgroup stages the
-//             block's alpha slice (B doubles) in LDS once for its windows; each lane walks one R-point
+//             block's alpha slice (B doubles) in LDS once for its windows (by LDS-DMA,
+//             global_load_lds_dwordx4: no VGPR round trip, 46.7 -> 43.1 us at config C); each lane walks one R-point
 //             run of a single (window, cell), accumulates the kNC = 10 moments alpha*u^d in registers and
 //             flushes them with ds_add_f64 into an LDS moment table; the workgroup finally folds the
 //             moments into 64-cell partial grids (taps = C * M) and writes them to part[comp][block].
@@ -124,13 +125,29 @@ __device__ __forceinline__ void stage_block(double* __restrict__ s, const double
    if (tid < kPad) s[B + tid] = 0.0;
 }
 
+// The same slice by LDS-DMA (global_load_lds_dwordx4): each wave moves 1 KB pieces straight into LDS (lane l
+// lands at the wave-uniform base + 16 l), no VGPR round trip and no ds_write; the ragged tail and the pad go
+// through plain stores.  The caller waits vmcnt(0) before the barrier that publishes the slice.
+template <int THREADS>
+__device__ __forceinline__ void stage_block_glds(double* __restrict__ s, const double* __restrict__ x, int base,
+                                                 int nloc, int B)
+{
+   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+   const double* src = x + base;
+   const int nfull = ((reinterpret_cast<uintptr_t>(src) & 15) == 0) ? nloc / 128 : 0;  // whole 1 KB pieces
+   for (int p = wave; p < nfull; p += THREADS / 64)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 128 * p + 2 * lane),
+                                       (__attribute__((address_space(3))) void*)(s + 128 * p), 16, 0, 0);
+   for (int e = 128 * nfull + tid; e < B + kPad; e += THREADS) s[e] = e < nloc ? src[e] : 0.0;
+}
+
 // ------------------------------------------------------------------------------------------------
 // spread
 // ------------------------------------------------------------------------------------------------
 // gsum (row shards): the partial grids are stored memory-side and the last block to finish a slice of
 // window groups sums them over the blocks in block order into gsum[comp][cell] (reduce.hpp's handoff;
 // tickets: one counter per slice, kTicketStride apart, left at zero) -- k_reduce_parts inside the spread.
-template <int THREADS, bool PREFETCH, bool TIMELINE = false>
+template <int THREADS, bool PREFETCH, bool TIMELINE = false, bool GLDS = false>
 __global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__ meta,
                                                     const uint32_t* __restrict__ lo,
                                                     const uint32_t* __restrict__ qarr,
@@ -170,8 +187,12 @@ __global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__
    int t = t0 + wave;
    if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
    const int base = b * B;
-   stage_block<THREADS>(s_alpha, x, base, min(B, n - base), B);
+   if (GLDS)
+      stage_block_glds<THREADS>(s_alpha, x, base, min(B, n - base), B);
+   else
+      stage_block<THREADS>(s_alpha, x, base, min(B, n - base), B);
    for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
+   if (GLDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces have landed
    __syncthreads();
    if (TIMELINE) stamp(1);
 
@@ -1014,10 +1035,13 @@ struct SpreadVariant {
 };
 static const SpreadVariant kSpreadVariants[] = {
     {k_spread<512, true>, 512},         // 0: 8 waves, next-run prefetch
-    {k_spread<512, false>, 512},        // 1: 8 waves (default)
-    {k_spread<256, true>, 256},         // 2: 4 waves, prefetch
-    {k_spread<1024, false>, 1024},      // 3: 16 waves
-    {k_spread<512, false, true>, 512},  // 4: variant 1 + per-workgroup s_memrealtime timeline (tools/)
+    {k_spread<512, false, false, true>, 512},  // 1: 8 waves, alpha slice by LDS-DMA (default)
+    {k_spread<256, true>, 256},                // 2: 4 waves, prefetch
+    {k_spread<1024, false>, 1024},             // 3: 16 waves
+    {k_spread<512, false, true, true>, 512},   // 4: variant 1 + per-workgroup s_memrealtime timeline (tools/)
+    {k_spread<512, false>, 512},               // 5, 6: the persistent kernels (launch_spread), never read here
+    {k_spread<512, false>, 512},
+    {k_spread<512, false>, 512},  // 7: variant 1 with the alpha slice staged through registers (rounds 1-3)
 };
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
