@@ -1,0 +1,12 @@
+# Round evidence at the current head: the driver's three commands (tools/driver_check.sh), then a rocprofv3
+# kernel trace of the bench (tools/prof_summary.py over its timed loops) and the SQ / LDS counter passes
+# (tools/pmc_sq.py).  Outputs under gpurun_out/; copy the ones to keep into profiles/rNN_*.
+set -o pipefail
+bash tools/driver_check.sh || exit 1
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+rm -rf gpurun_out/prof
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-traffic > gpurun_out/prof_bench.log 2>&1 || { echo PROF_FAIL; tail -20 gpurun_out/prof_bench.log; exit 1; }
+python tools/prof_summary.py $(find gpurun_out/prof -name "*kernel_trace.csv" | head -1) --steps 200 --out gpurun_out/prof_summary.json
+cp $(find gpurun_out/prof -name "*kernel_stats.csv" | head -1) gpurun_out/prof_kernel_stats.csv
+timeout -k 10 600 python tools/pmc_sq.py --out gpurun_out/pmc_sq.csv > gpurun_out/pmc_sq.log 2>&1 || { echo PMC_SQ_FAIL; tail -20 gpurun_out/pmc_sq.log; exit 1; }
+tail -2 gpurun_out/pmc_sq.log
