@@ -461,11 +461,13 @@ extern "C" int Nfft4GPAmdDebugStamps(unsigned long long* out, int nwg)
 // circulant h = w (*) g, then H[cell][d] = sum_t h[cell - m + t] C[t][d].  The circulant runs as 16
 // strands of 4 terms per output summed in a fixed butterfly inside the wave (blockDim >= 1024: 4 outputs
 // x 16 strands per wave); one 64-term chain per output was bound by its dependent LDS reads.
-__device__ void grid_tail(int comp, const double* __restrict__ s_g, const double* __restrict__ w,
-                          double* __restrict__ H, double* s_w, double* s_h)
+// wreg: this thread's circulant entry w[comp][tid] (tid < 64), loaded by the caller at kernel entry so its
+// latency overlaps the grid loads instead of following them
+__device__ void grid_tail(int comp, const double* __restrict__ s_g, double wreg, double* __restrict__ H, double* s_w,
+                          double* s_h)
 {
    const int tid = threadIdx.x;
-   if (tid < kNos) s_w[tid] = w[(size_t)comp * kNos + tid];
+   if (tid < kNos) s_w[tid] = wreg;
    __syncthreads();
    {
       const int o = tid >> 4, st = tid & 15;
@@ -507,6 +509,8 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
    part += blockIdx.y * part_rs;
    H += blockIdx.y * h_rs;
    const int tid = threadIdx.x;
+   const double wv = tid < kNos ? w[(size_t)comp * kNos + tid] : 0.0;
+   const double wdv = (grad && tid < kNos) ? wd[(size_t)comp * kNos + tid] : 0.0;
    if (from_sum) {
       if (tid < kNos) s_g[tid] = part[(size_t)comp * kNos + tid];
    } else {
@@ -538,8 +542,8 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
       }
    }
    __syncthreads();
-   grid_tail(comp, s_g, w, H, s_w, s_h);
-   if (grad) grid_tail(comp, s_g, wd, Hd, s_w, s_h);
+   grid_tail(comp, s_g, wv, H, s_w, s_h);
+   if (grad) grid_tail(comp, s_g, wdv, Hd, s_w, s_h);
 }
 
 // Row shards with few blocks, split interpolation (launch_shard_finish_split): the grid kernel from the summed
@@ -557,11 +561,12 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_sum_yinit(const double* _
    __shared__ double s_w[kNos];
    const int comp = blockIdx.x;
    const int tid = threadIdx.x;
+   const double wv = tid < kNos ? w[(size_t)comp * kNos + tid] : 0.0;
    if (tid < kNos) s_g[tid] = gsum[(size_t)comp * kNos + tid];
    for (size_t j = (size_t)blockIdx.x * kGridThreads + tid; j < (size_t)n; j += (size_t)gridDim.x * kGridThreads)
       y[j] = (beta == 0.0 ? 0.0 : beta * y[j]) + amu * x[j];
    __syncthreads();
-   grid_tail(comp, s_g, w, H, s_w, s_h);
+   grid_tail(comp, s_g, wv, H, s_w, s_h);
 }
 
 template <int THREADS>

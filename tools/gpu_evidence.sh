@@ -8,5 +8,6 @@ rm -rf gpurun_out/prof
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-traffic > gpurun_out/prof_bench.log 2>&1 || { echo PROF_FAIL; tail -20 gpurun_out/prof_bench.log; exit 1; }
 python tools/prof_summary.py $(find gpurun_out/prof -name "*kernel_trace.csv" | head -1) --steps 200 --out gpurun_out/prof_summary.json
 cp $(find gpurun_out/prof -name "*kernel_stats.csv" | head -1) gpurun_out/prof_kernel_stats.csv
+rm -rf gpurun_out/prof  # the full trace is > 64 MiB: gpurun would not copy gpurun_out/ back
 timeout -k 10 600 python tools/pmc_sq.py --out gpurun_out/pmc_sq.csv > gpurun_out/pmc_sq.log 2>&1 || { echo PMC_SQ_FAIL; tail -20 gpurun_out/pmc_sq.log; exit 1; }
 tail -2 gpurun_out/pmc_sq.log

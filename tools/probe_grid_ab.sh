@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_nfft.py tests/test_gpu_dist.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pt.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/pt.log; exit 1; }
+tail -2 gpurun_out/pt.log
+for r in 1 2; do timeout -k 10 300 python bench.py --no-cpu-baseline --no-traffic --no-pcg --steps 500 > gpurun_out/b$r.json 2>/dev/null || { echo BENCH_FAIL; exit 1; }; python -c "import json;d=json.load(open('gpurun_out/b$r.json'));print(round(d['ms_per_step']*1e3,2), {k:round(x*1e3,2) for k,x in d['kernels_ms'].items()})"; done
+for N in 8 4 2; do timeout -k 10 300 python tools/shard_probe.py --ranks $N 2>/dev/null | tail -1 || exit 1; done
