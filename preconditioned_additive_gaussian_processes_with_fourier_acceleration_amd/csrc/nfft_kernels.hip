@@ -147,8 +147,9 @@ __device__ __forceinline__ void stage_block_glds(double* __restrict__ s, const d
 // gsum (row shards): the partial grids are stored memory-side and the last block to finish a slice of
 // window groups sums them over the blocks in block order into gsum[comp][cell] (reduce.hpp's handoff;
 // tickets: one counter per slice, kTicketStride apart, left at zero) -- k_reduce_parts inside the spread.
-template <int THREADS, bool PREFETCH, bool TIMELINE = false, bool GLDS = false>
-__global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__ meta,
+// no-prefetch variants: at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
+template <int THREADS, bool PREFETCH, bool TIMELINE = false, bool GLDS = false, bool FOLD2 = false>
+__global__ __launch_bounds__(THREADS, PREFETCH ? 1 : 6) void k_spread(const uint16_t* __restrict__ meta,
                                                     const uint32_t* __restrict__ lo,
                                                     const uint32_t* __restrict__ qarr,
                                                     const int* __restrict__ tile_off, const double* __restrict__ x,
@@ -245,13 +246,29 @@ __global__ __launch_bounds__(THREADS) void k_spread(const uint16_t* __restrict__
       for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
          const int cl = idx / kNos;
          const int gi = idx % kNos;
-         double v = 0.0;
+         // FOLD2 (variant 8): two chains (even and odd taps) instead of one dependent 100-term chain; measured
+         // neutral at config C (44.3 vs 44.4 us) and 1 % slower at config E, so one chain stays the default
+         double v0 = 0.0, v1 = 0.0;
+         if (FOLD2) {
 #pragma unroll 1
-         for (int tp = 0; tp < kTaps; tp++) {
-            const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
+            for (int tp = 0; tp < kTaps; tp += 2) {
+               const double* m0 = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
+               const double* m1 = s_mom + (cl * kNos + ((gi + kM - tp - 1) & (kNos - 1))) * kMomStride;
 #pragma unroll
-            for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
+               for (int d = 0; d < kNC; d++) {
+                  v0 = fma(c_taps[tp * kNC + d], m0[d], v0);
+                  v1 = fma(c_taps[(tp + 1) * kNC + d], m1[d], v1);
+               }
+            }
+         } else {  // one 100-term chain
+#pragma unroll 1
+            for (int tp = 0; tp < kTaps; tp++) {
+               const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
+#pragma unroll
+               for (int d = 0; d < kNC; d++) v0 = fma(c_taps[tp * kNC + d], mrow[d], v0);
+            }
          }
+         const double v = v0 + v1;
          double* dst = part + ((size_t)(c0 + cl) * nblocks + b) * kNos + gi;  // [comp][block][cell]
          if (gsum)
             __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1047,6 +1064,7 @@ static const SpreadVariant kSpreadVariants[] = {
     {k_spread<512, false>, 512},               // 5, 6: the persistent kernels (launch_spread), never read here
     {k_spread<512, false>, 512},
     {k_spread<512, false>, 512},  // 7: variant 1 with the alpha slice staged through registers (rounds 1-3)
+    {k_spread<512, false, false, true, true>, 512},  // 8: variant 1 with the fold in two chains (neutral)
 };
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
