@@ -478,11 +478,22 @@ extern "C" int Nfft4GPAmdDebugStamps(unsigned long long* out, int nwg)
 // circulant h = w (*) g, then H[cell][d] = sum_t h[cell - m + t] C[t][d].  The circulant runs as 16
 // strands of 4 terms per output summed in a fixed butterfly inside the wave (blockDim >= 1024: 4 outputs
 // x 16 strands per wave); one 64-term chain per output was bound by its dependent LDS reads.
-// wreg: this thread's circulant entry w[comp][tid] (tid < 64), loaded by the caller at kernel entry so its
-// latency overlaps the grid loads instead of following them
-__device__ void grid_tail(int comp, const double* __restrict__ s_g, double wreg, double* __restrict__ H, double* s_w,
-                          double* s_h)
+// wreg: this thread's circulant entry w[comp][tid] (tid < 64); ct: the tap coefficients C[t][tid % kNC] of this
+// thread's output H[tid / kNC][tid % kNC] (tid < 64 kNC; blockDim == kGridThreads >= 64 kNC).  Both are
+// loaded by the caller at kernel entry, so their latency overlaps the grid loads instead of following the
+// last barrier.
+__device__ __forceinline__ void grid_tail_coeffs(double (&ct)[kTaps])
 {
+   const int tid = threadIdx.x;
+   const int d = tid % kNC;
+#pragma unroll
+   for (int tp = 0; tp < kTaps; tp++) ct[tp] = tid < kNos * kNC ? c_taps[tp * kNC + d] : 0.0;
+}
+
+__device__ void grid_tail(int comp, const double* __restrict__ s_g, double wreg, const double (&ct)[kTaps],
+                          double* __restrict__ H, double* s_w, double* s_h)
+{
+   static_assert(kGridThreads >= kNos * kNC, "one H entry per thread");
    const int tid = threadIdx.x;
    if (tid < kNos) s_w[tid] = wreg;
    __syncthreads();
@@ -500,12 +511,12 @@ __device__ void grid_tail(int comp, const double* __restrict__ s_g, double wreg,
       if (o < kNos && st == 0) s_h[o] = h;
    }
    __syncthreads();
-   for (int idx = tid; idx < kNos * kNC; idx += blockDim.x) {
-      const int cell = idx / kNC;
-      const int d = idx % kNC;
+   if (tid < kNos * kNC) {
+      const int cell = tid / kNC;
+      const int d = tid % kNC;
       double v = 0.0;
 #pragma unroll
-      for (int tp = 0; tp < kTaps; tp++) v = fma(s_h[(cell - kM + tp) & (kNos - 1)], c_taps[tp * kNC + d], v);
+      for (int tp = 0; tp < kTaps; tp++) v = fma(s_h[(cell - kM + tp) & (kNos - 1)], ct[tp], v);
       H[((size_t)comp * kNos + cell) * kNC + d] = v;
    }
    __syncthreads();
@@ -528,6 +539,8 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
    const int tid = threadIdx.x;
    const double wv = tid < kNos ? w[(size_t)comp * kNos + tid] : 0.0;
    const double wdv = (grad && tid < kNos) ? wd[(size_t)comp * kNos + tid] : 0.0;
+   double ct[kTaps];
+   grid_tail_coeffs(ct);
    if (from_sum) {
       if (tid < kNos) s_g[tid] = part[(size_t)comp * kNos + tid];
    } else {
@@ -559,8 +572,8 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
       }
    }
    __syncthreads();
-   grid_tail(comp, s_g, wv, H, s_w, s_h);
-   if (grad) grid_tail(comp, s_g, wdv, Hd, s_w, s_h);
+   grid_tail(comp, s_g, wv, ct, H, s_w, s_h);
+   if (grad) grid_tail(comp, s_g, wdv, ct, Hd, s_w, s_h);
 }
 
 // Row shards with few blocks, split interpolation (launch_shard_finish_split): the grid kernel from the summed
@@ -579,11 +592,29 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_sum_yinit(const double* _
    const int comp = blockIdx.x;
    const int tid = threadIdx.x;
    const double wv = tid < kNos ? w[(size_t)comp * kNos + tid] : 0.0;
+   double ct[kTaps];
+   grid_tail_coeffs(ct);
    if (tid < kNos) s_g[tid] = gsum[(size_t)comp * kNos + tid];
-   for (size_t j = (size_t)blockIdx.x * kGridThreads + tid; j < (size_t)n; j += (size_t)gridDim.x * kGridThreads)
-      y[j] = (beta == 0.0 ? 0.0 : beta * y[j]) + amu * x[j];
+   // y init: 4 elements per thread per pass, all loads issued before the first store (one latency per
+   // pass instead of one per element)
+   constexpr int kU = 4;
+   const size_t stride = (size_t)gridDim.x * kGridThreads;
+   for (size_t j0 = (size_t)blockIdx.x * kGridThreads + tid; j0 < (size_t)n; j0 += kU * stride) {
+      double xv[kU], yv[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+         const size_t j = j0 + u * stride;
+         xv[u] = j < (size_t)n ? x[j] : 0.0;
+         yv[u] = (beta != 0.0 && j < (size_t)n) ? y[j] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+         const size_t j = j0 + u * stride;
+         if (j < (size_t)n) y[j] = (beta == 0.0 ? 0.0 : beta * yv[u]) + amu * xv[u];
+      }
+   }
    __syncthreads();
-   grid_tail(comp, s_g, wv, H, s_w, s_h);
+   grid_tail(comp, s_g, wv, ct, H, s_w, s_h);
 }
 
 template <int THREADS>
