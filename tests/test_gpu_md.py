@@ -171,7 +171,9 @@ def test_pcg_tiled_3d(torch_cuda):
     assert op.setup(0, 1.0, 0.3, 0.01) == 0
     b = rng.random(n) - 0.5
     x = torch.zeros(n, dtype=torch.float64, device="cuda")
-    x, rr, hist, it = amd.pcg(op, torch.tensor(b, device="cuda"), x, maxits=2000, tol=1e-8)
+    # 1971-2015 iterations over four runs (tools/md_pcg_diag.py): the tiled spread's fp64 atomics add in a
+    # varying order, so the count moves by a few percent; maxits 2000 failed one run in round 3
+    x, rr, hist, it = amd.pcg(op, torch.tensor(b, device="cuda"), x, maxits=4000, tol=1e-8)
     assert it > 0 and rr <= 1e-8
     y = op.matsymv(x, 1.0, 0.0, torch.zeros(n, dtype=torch.float64, device="cuda")).cpu().numpy()
     assert np.linalg.norm(b - y) / np.linalg.norm(b) < 1e-7
