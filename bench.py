@@ -81,13 +81,8 @@ def host_info():
             "omp_env": {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OMP_PROC_BIND", "OMP_PLACES")}}
 
 
-def cpu_baseline(n, d, X, x, max_seconds=25.0, min_samples=5, max_samples=15):
-    """Oracle (C + OpenMP restatement of nfft_interface.c + NFFT3 fastsum) on this host: the median of
-    5-15 timed full matvecs after one warm-up (min / max beside it), bounded by max_seconds of CPU work."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as orc_mod
-    lib = None
-    # prefer a -march=native build of the oracle for this host (built into a scratch dir)
+def _native_oracle():
+    """A -march=native build of the oracle for this host (built into a scratch dir), or None."""
     try:
         out_dir = os.path.join(ROOT, "gpurun_out", "oracle_native")
         os.makedirs(out_dir, exist_ok=True)
@@ -95,37 +90,70 @@ def cpu_baseline(n, d, X, x, max_seconds=25.0, min_samples=5, max_samples=15):
         subprocess.run(["gcc", "-O3", "-march=native", "-fPIC", "-fopenmp", "-std=gnu11", "-shared",
                         os.path.join(ROOT, "oracle", "nfft4gp_oracle.c"), "-o", so, "-lm"],
                        check=True, capture_output=True, timeout=120)
-        lib = orc_mod.oracle_lib(so)
-        native = True
+        return so
     except Exception:
-        lib = orc_mod.oracle_lib()
-        native = False
-    win = np.arange(d, dtype=np.int32)
-    o = orc_mod.OracleAdditiveNFFT(X, win, d, 1, lib=lib)
+        return None
+
+
+def cpu_baseline_child(n, d, so, threads_list, max_seconds=12.0, min_samples=5, max_samples=15):
+    """Child of cpu_baseline (its OpenMP binding fixed by the parent's environment before libgomp starts): one
+    setup, then for each thread count the median of 5-15 timed full matvecs after one warm-up, bounded by
+    max_seconds of timed work per count.  Prints one JSON line."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc_mod
+    lib = orc_mod.oracle_lib(so) if so else orc_mod.oracle_lib()
+    X, x = make_problem(n, d)
+    o = orc_mod.OracleAdditiveNFFT(X, np.arange(d, dtype=np.int32), d, 1, lib=lib)
     t0 = time.time()
     o.setup(0, 1.0, 1.0, 0.01)
-    t_setup = time.time() - t0
-    o.matsymv(x)  # warm
-    times = []
-    while len(times) < max_samples and (len(times) < min_samples or sum(times) < max_seconds):
-        t0 = time.perf_counter()
-        o.matsymv(x)
-        times.append(time.perf_counter() - t0)
-    threads = int(lib.orc_num_threads())
-    med = float(np.median(times))
+    out = {"setup_s": time.time() - t0, "runs": []}
+    for th in threads_list:
+        lib.orc_set_num_threads(th)
+        o.matsymv(x)  # warm (and the team of this size started)
+        times = []
+        while len(times) < max_samples and (len(times) < min_samples or sum(times) < max_seconds):
+            t0 = time.perf_counter()
+            o.matsymv(x)
+            times.append(time.perf_counter() - t0)
+        out["runs"].append({"threads": int(lib.orc_num_threads()), "samples": len(times),
+                            "median_s": float(np.median(times)), "min_s": float(min(times)),
+                            "max_s": float(max(times))})
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline(n, d, threads=16, timeout=400):
+    """Oracle (C + OpenMP restatement of nfft_interface.c + NFFT3 fastsum, oracle/nfft4gp_oracle.c, with
+    NFFT3's PRE_PSI taps and a 1-D fast path) on this host's cores, in a child process whose OpenMP threads
+    are bound one per physical core (OMP_PROC_BIND=close, OMP_PLACES=cores) -- the value at `threads` (16:
+    the GPU box's CPU share, which its OMP_NUM_THREADS also names), with a one-thread run of the same setup
+    beside it."""
+    so = _native_oracle()
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores")
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--n", str(n), "--d", str(d),
+           "--cpu-threads", f"{threads},1"] + (["--cpu-oracle-so", so] if so else [])
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu baseline child failed ({r.returncode}): {r.stderr[-400:]}")
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    main_run, single = res["runs"][0], res["runs"][1]
+    host = host_info()
+    host["omp_env"] = {k: env.get(k) for k in ("OMP_NUM_THREADS", "OMP_PROC_BIND", "OMP_PLACES")}
     return {
-        "value": 1.0 / med,
+        "value": 1.0 / main_run["median_s"],
         "unit": "matvecs/s",
-        "cores": threads,
+        "cores": main_run["threads"],
         "kind": "port",
-        "samples": len(times),
-        "median_s": med,
-        "min_s": float(min(times)),
-        "max_s": float(max(times)),
-        "host": host_info(),
-        "sample": f"median of {len(times)} timed matvecs of the full workload (n={n}, {d} windows) after one "
-                  f"warm-up; setup (PRE_PSI taps, bhat) {t_setup:.1f}s untimed; -march=native={native}; "
-                  f"OMP threads={threads}",
+        "samples": main_run["samples"],
+        "median_s": main_run["median_s"],
+        "min_s": main_run["min_s"],
+        "max_s": main_run["max_s"],
+        "one_thread": {"value": 1.0 / single["median_s"], "cores": 1, "samples": single["samples"],
+                       "median_s": single["median_s"], "min_s": single["min_s"], "max_s": single["max_s"]},
+        "host": host,
+        "sample": f"median of {main_run['samples']} timed matvecs of the full workload (n={n}, {d} windows) after "
+                  f"one warm-up, {main_run['threads']} OpenMP threads bound one per physical core (close, cores) "
+                  f"in a child process; one_thread: the same setup on 1 thread; setup (PRE_PSI taps, bhat) "
+                  f"{res['setup_s']:.1f}s untimed; -march=native={so is not None}",
     }
 
 
@@ -439,8 +467,18 @@ def main():
                     help="AFN landmark order: random (perm_opt 0) or farthest points (1)")
     ap.add_argument("--partition", default="rows", choices=["rows", "components"],
                     help="N > 1: the headline split (the other one is timed too)")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="OpenMP threads of the CPU baseline")
     ap.add_argument("--kernel-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-oracle-so", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--kernel-only-nys", type=int, default=0, help=argparse.SUPPRESS)
+    if "--cpu-baseline-child" in sys.argv:  # the child's --cpu-threads is a list "16,1"
+        i = sys.argv.index("--cpu-threads")
+        threads_list = [int(t) for t in sys.argv[i + 1].split(",")]
+        del sys.argv[i:i + 2]
+        args = ap.parse_args()
+        cpu_baseline_child(args.n, args.d, args.cpu_oracle_so, threads_list)
+        return
     args = ap.parse_args()
     if args.kernel_only:
         kernel_only(args.n, args.d, args.kernel_only_nys)
@@ -543,18 +581,14 @@ def main():
         pcg.update(run_fgmres(op, torch, n))
         pcg.update(run_fgmres(op, torch, n, ortho=1))
         pcg.update(run_pcg_single(op, torch, n))
+        # the preconditioned legs are the metric's "PCG time with AFN rank=512": an exception here ends the
+        # bench (no silent *_error key)
         if args.nys_rank > 0:
-            try:
-                pcg.update(run_pcg_nystrom(op, torch, n, args.nys_rank))
-            except Exception as e:  # report, do not fail the GPU measurement
-                pcg["pcg_nys_error"] = repr(e)
+            pcg.update(run_pcg_nystrom(op, torch, n, args.nys_rank))
         if args.afn_rank > 0:
             for schur in (["noise", "fsai"] if args.afn_schur == "both" else [args.afn_schur]):
                 for order in (["random", "fps"] if args.afn_order == "both" else [args.afn_order]):
-                    try:
-                        pcg.update(run_pcg_afn(op, X, torch, n, args.afn_rank, schur=schur, order=order))
-                    except Exception as e:  # report, do not fail the GPU measurement
-                        pcg["pcg_afn_" + schur + "_" + order + "_error"] = repr(e)
+                    pcg.update(run_pcg_afn(op, X, torch, n, args.afn_rank, schur=schur, order=order))
         if op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) != 0:
             raise SystemExit("setup failed")
 
@@ -687,7 +721,7 @@ def main():
         result["pcie_inclusive_matvecs_per_s"] = pcie_rate
         if not args.no_cpu_baseline:
             try:
-                result["cpu_baseline"] = cpu_baseline(n, d, X, x_host)
+                result["cpu_baseline"] = cpu_baseline(n, d, threads=args.cpu_threads)
             except Exception as e:  # report, do not fail the GPU measurement
                 result["cpu_baseline"] = {"value": None, "error": repr(e)}
     if world > 1:

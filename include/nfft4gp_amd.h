@@ -502,6 +502,7 @@ long long Nfft4GPAmdShardGridSize(void *str);
  * process group), called with a device staging buffer of `capacity` doubles it owns; it must leave the
  * elementwise sum over the ranks in place.  Both return NULL on failure. */
 typedef int (*Nfft4GPAmdAllreduceFn)(void *ctx, NFFT4GP_DOUBLE *d_buf, long long count);
+int Nfft4GPAmdCommRcclAvailable(void);  /* 1: this process can create an RCCL communicator */
 int Nfft4GPAmdCommUniqueId(void *id128);
 void *Nfft4GPAmdCommCreateRccl(int rank, int world, const void *id128);
 void *Nfft4GPAmdCommCreateCallback(int rank, int world, Nfft4GPAmdAllreduceFn fn, void *ctx,

@@ -57,6 +57,24 @@
 #include <omp.h>
 #endif
 
+static int orc_max_threads(void)
+{
+#ifdef _OPENMP
+   return omp_get_max_threads();
+#else
+   return 1;
+#endif
+}
+
+static int orc_thread_num(void)
+{
+#ifdef _OPENMP
+   return omp_get_thread_num();
+#else
+   return 0;
+#endif
+}
+
 #define ORC_N 32    /* bandwidth, nfft_interface.c:18 */
 #define ORC_M 4     /* window cutoff, nfft_interface.c:20 */
 #define ORC_NOS 64  /* oversampled grid, nfft_interface.c:25-27 */
@@ -154,6 +172,7 @@ typedef struct
    double *buffer;         /* gathered window columns, n x (sum dims) col-major */
    orc_comp *comps;
    double *work;           /* 3n accumulator (_dwork) */
+   cplx *al, *fo, *fd;     /* n-long scratch of one component's apply (alpha_c, f, f'), kept between calls */
 } orc_additive;
 
 /* bhat for a kernel (fastsum_precompute, kernel part) */
@@ -217,6 +236,33 @@ static void orc_comp_fastsum(const orc_comp *cp, const double *bh, const cplx *a
 
    /* ---- adjoint B^T: spread onto the oversampled grid (per-thread private grids) ---- */
    cplx *g = (cplx *)calloc((size_t)ng, sizeof(cplx));
+   if (d == 1)
+   {
+      /* 1-D windows (configs B-E): the cell index of each tap is (u + lt) mod 64 with no integer division,
+       * each thread keeps its 64-cell grid on the stack, and the thread grids are added in thread order
+       * after the loop (deterministic for a fixed thread count).  Same sums as the generic path below. */
+      const int nth = orc_max_threads();
+      cplx *tg = (cplx *)calloc((size_t)nth * ORC_NOS, sizeof(cplx));
+#pragma omp parallel
+      {
+         cplx gl[ORC_NOS];
+         for (int i = 0; i < ORC_NOS; i++) gl[i] = 0.0;
+#pragma omp for schedule(static)
+         for (int j = 0; j < n; j++)
+         {
+            const int u0 = cp->u[j];
+            const double *ps = cp->psi + (size_t)j * T;
+            const cplx aj = alpha[j];
+            for (int lt = 0; lt < T; lt++) gl[(u0 + lt) & (ORC_NOS - 1)] += aj * ps[lt];
+         }
+         memcpy(tg + (size_t)orc_thread_num() * ORC_NOS, gl, sizeof(gl));
+      }
+      for (int th = 0; th < nth; th++)
+         for (int i = 0; i < ORC_NOS; i++) g[i] += tg[(size_t)th * ORC_NOS + i];
+      free(tg);
+   }
+   else
+   {
 #pragma omp parallel
    {
       cplx *gl = (cplx *)calloc((size_t)ng, sizeof(cplx));
@@ -243,6 +289,7 @@ static void orc_comp_fastsum(const orc_comp *cp, const double *bh, const cplx *a
 #pragma omp critical
       for (int i = 0; i < ng; i++) g[i] += gl[i];
       free(gl);
+   }
    }
 
    /* ---- F^H + D: fhat_k = phihut_inv(k) * sum_l g_l e^{+2 pi i k l / n_os} (separable) ---- */
@@ -315,6 +362,20 @@ static void orc_comp_fastsum(const orc_comp *cp, const double *bh, const cplx *a
    free(g);
 
    /* ---- B: interpolate ---- */
+   if (d == 1)
+   {
+#pragma omp parallel for schedule(static)
+      for (int j = 0; j < n; j++)
+      {
+         const int u0 = cp->u[j];
+         const double *ps = cp->psi + (size_t)j * T;
+         cplx acc = 0.0;
+         for (int lt = 0; lt < T; lt++) acc += a[(u0 + lt) & (ORC_NOS - 1)] * ps[lt];
+         fout[j] = acc;
+      }
+      free(a);
+      return;
+   }
 #pragma omp parallel for schedule(static)
    for (int j = 0; j < n; j++)
    {
@@ -470,6 +531,9 @@ void *orc_additive_create(const double *data, int n, int ldim, int d, const int 
    h->buffer = (double *)malloc(sizeof(double) * (size_t)n * nwindows * dwindows);
    h->comps = (orc_comp *)calloc((size_t)nwindows, sizeof(orc_comp));
    h->work = (double *)malloc(sizeof(double) * 3 * (size_t)n);
+   h->al = (cplx *)malloc(sizeof(cplx) * (size_t)(n > 0 ? n : 1));
+   h->fo = (cplx *)malloc(sizeof(cplx) * (size_t)(n > 0 ? n : 1));
+   h->fd = (cplx *)malloc(sizeof(cplx) * (size_t)(n > 0 ? n : 1));
    /* gather (nfft_interface.c:648-670) */
    double *dst = h->buffer;
    const int *fw = windows;
@@ -535,43 +599,38 @@ static void orc_comp_apply(orc_comp *cp, int exact, int which, const cplx *alpha
       orc_comp_fastsum(cp, bh, alpha, fout);
 }
 
-/* Nfft4GPNFFTMatSymv (:400-497) for one component, accumulating with beta = 1 */
-static void orc_comp_matsymv_acc(orc_comp *cp, int exact, double a, const double *x, double *y)
+/* Nfft4GPNFFTMatSymv (:400-497) for one component, accumulating with beta = 1; al / fo: n-long scratch */
+static void orc_comp_matsymv_acc(orc_comp *cp, int exact, double a, const double *x, double *y, cplx *al, cplx *fo)
 {
    const int n = cp->n;
    const double ff = cp->kscale * cp->kscale;
-   cplx *al = (cplx *)malloc(sizeof(cplx) * n);
-   cplx *fo = (cplx *)malloc(sizeof(cplx) * n);
+#pragma omp parallel for schedule(static)
    for (int i = 0; i < n; i++) al[i] = a * x[i];
    orc_comp_apply(cp, exact, 0, al, fo);
+#pragma omp parallel for schedule(static)
    for (int i = 0; i < n; i++) y[i] += ff * (creal(fo[i]) + cp->mu * creal(al[i]));
-   free(al);
-   free(fo);
 }
 
 /* Nfft4GPNFFTGradMatSymv (:499-620), beta = 1 branch */
-static void orc_comp_gradmatsymv_acc(orc_comp *cp, int exact, double a, const double *x, double *y)
+static void orc_comp_gradmatsymv_acc(orc_comp *cp, int exact, double a, const double *x, double *y, cplx *al,
+                                     cplx *fo, cplx *fd)
 {
    const int n = cp->n;
    const double ff = cp->kscale * cp->kscale;
    const double f2 = cp->kscale * 2.0;
-   cplx *al = (cplx *)malloc(sizeof(cplx) * n);
-   cplx *fo = (cplx *)malloc(sizeof(cplx) * n);
-   cplx *fd = (cplx *)malloc(sizeof(cplx) * n);
+#pragma omp parallel for schedule(static)
    for (int i = 0; i < n; i++) al[i] = a * x[i];
    orc_comp_apply(cp, exact, 0, al, fo);
    orc_comp_apply(cp, exact, 1, al, fd);
    double scale = cp->kernel == 0 ? 2.0 * cp->scale * sqrt(2.0) / cp->sigma0 : cp->scale / cp->sigma0;
    scale *= ff;
+#pragma omp parallel for schedule(static)
    for (int i = 0; i < n; i++)
    {
       y[i] += f2 * (creal(fo[i]) + cp->mu * creal(al[i]));
       y[n + i] += scale * creal(fd[i]);
       y[2 * n + i] += ff * creal(al[i]);
    }
-   free(al);
-   free(fo);
-   free(fd);
 }
 
 static void orc_scale_vec(double *y, size_t n, double beta)
@@ -589,7 +648,7 @@ int orc_additive_matsymv(void *vh, int n, double alpha, const double *x, double 
    orc_additive *h = (orc_additive *)vh;
    memset(h->work, 0, sizeof(double) * n);
    const double scale = 1.0 / (double)h->nw * alpha;
-   for (int i = 0; i < h->nw; i++) orc_comp_matsymv_acc(&h->comps[i], exact, scale, x, h->work);
+   for (int i = 0; i < h->nw; i++) orc_comp_matsymv_acc(&h->comps[i], exact, scale, x, h->work, h->al, h->fo);
    orc_scale_vec(y, n, beta);
    for (int i = 0; i < n; i++) y[i] += h->work[i];
    return 0;
@@ -601,7 +660,8 @@ int orc_additive_gradmatsymv(void *vh, int n, double alpha, const double *x, dou
    orc_additive *h = (orc_additive *)vh;
    memset(h->work, 0, sizeof(double) * 3 * n);
    const double scale = 1.0 / (double)h->nw * alpha;
-   for (int i = 0; i < h->nw; i++) orc_comp_gradmatsymv_acc(&h->comps[i], exact, scale, x, h->work);
+   for (int i = 0; i < h->nw; i++)
+      orc_comp_gradmatsymv_acc(&h->comps[i], exact, scale, x, h->work, h->al, h->fo, h->fd);
    orc_scale_vec(y, 3 * (size_t)n, beta);
    for (int i = 0; i < 3 * n; i++) y[i] += h->work[i];
    return 0;
@@ -651,14 +711,20 @@ void orc_additive_free(void *vh)
    free(h->comps);
    free(h->buffer);
    free(h->work);
+   free(h->al);
+   free(h->fo);
+   free(h->fd);
    free(h);
 }
 
-int orc_num_threads(void)
+int orc_num_threads(void) { return orc_max_threads(); }
+
+/* the OpenMP team size of later calls (bench.py's CPU baseline times 16 threads and then 1 on one setup) */
+void orc_set_num_threads(int t)
 {
 #ifdef _OPENMP
-   return omp_get_max_threads();
+   if (t > 0) omp_set_num_threads(t);
 #else
-   return 1;
+   (void)t;
 #endif
 }

@@ -53,6 +53,7 @@ def oracle_lib(path: str | None = None):
         lib.orc_window_phi_hut.restype = C.c_double
         lib.orc_window_phi_hut.argtypes = [C.c_int]
         lib.orc_num_threads.restype = C.c_int
+        lib.orc_set_num_threads.argtypes = [C.c_int]
         if path is not None:
             return lib
         _olib = lib

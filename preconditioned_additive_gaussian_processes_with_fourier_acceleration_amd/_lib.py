@@ -160,6 +160,7 @@ _SIGS = {
     "Nfft4GPAmdPrecondAFNSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdPrecondAFNInfo": (C.c_int, [vp, ip, ip, C.POINTER(vp), C.POINTER(vp)]),
     "Nfft4GPAmdPrecondAFNFree": (None, [vp]),
+    "Nfft4GPAmdCommRcclAvailable": (C.c_int, []),
     "Nfft4GPAmdCommUniqueId": (C.c_int, [vp]),
     "Nfft4GPAmdCommCreateRccl": (vp, [C.c_int, C.c_int, vp]),
     "Nfft4GPAmdCommCreateCallback": (vp, [C.c_int, C.c_int, ALLREDUCE, vp, vp, C.c_longlong]),

@@ -1199,6 +1199,9 @@ int Nfft4GPAmdPrecondAFNSetStorage(void* pre, int bits)
 {
    AfnFlow* F = (AfnFlow*)pre;
    if (!F || (bits != 32 && bits != 64)) return -1;
+   // with gradients the fp64 factors serve Dvp, Trace and Logdet: an fp32 solve would no longer be the
+   // preconditioner those terms describe, so the storage stays fp64
+   if (F->grad) return 0;
    if (F->afn) return Nfft4GPAmdAfnSetStorage(F->afn, bits);
    if (F->nys) return Nfft4GPAmdNysSetStorage(F->nys, bits);
    return 0;  // the gradient-capable branches keep their fp64 factors

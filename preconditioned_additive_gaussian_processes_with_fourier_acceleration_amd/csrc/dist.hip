@@ -295,6 +295,14 @@ int Nfft4GPAmdCommUniqueId(void* id128)
    return 0;
 }
 
+// every rank asks this before any rank enters ncclCommInitRank (dist.py all-reduces the answers): a rank
+// that would return before the collective init (no device, RCCL not loadable) must not leave the others
+// blocked inside it
+int Nfft4GPAmdCommRcclAvailable(void)
+{
+   return (device_ok() && rccl().ok) ? 1 : 0;
+}
+
 void* Nfft4GPAmdCommCreateRccl(int rank, int world, const void* id128)
 {
    if (!device_ok() || !id128 || world < 1 || rank < 0 || rank >= world) return nullptr;

@@ -367,6 +367,10 @@ int device_ok();
 // do while they initialise.  An entry point that draws opens a RandScope: the process runs on a private
 // random() state for the duration of the call, and each batch of the reference's draws runs inside a
 // CallerRandBatch on the caller's state (glibc rand() is random(); initstate / setstate switch its state).
+// A scope holds a process-wide recursive lock, so scopes of several host threads do not interleave; a thread
+// that calls libc rand() while another thread's library call holds a scope draws from the private state
+// (do not call rand() concurrently with this library's setup entry points).  The apply paths (MatSymv,
+// GradMatSymv) open no scope.
 struct RandScope {
    RandScope();
    ~RandScope();

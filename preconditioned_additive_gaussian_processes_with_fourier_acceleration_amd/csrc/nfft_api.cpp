@@ -28,6 +28,10 @@ using namespace nfft4gp_amd;
 namespace nfft4gp_amd {
 
 namespace {
+// the scope holds this lock for its lifetime: the depth, the saved caller state and the process-wide
+// glibc random() state are switched by one host thread at a time (other threads' library calls that
+// open a scope wait; libc rand() itself stays unsafe to call concurrently with a scope, see internal.h)
+std::recursive_mutex g_rand_mu;
 int g_rand_depth = 0;
 char* g_caller_rand = nullptr;
 char g_private_rand[256];
@@ -38,6 +42,7 @@ bool g_private_ready = false;
 // open a scope
 RandScope::RandScope()
 {
+   g_rand_mu.lock();
    if (g_rand_depth++ == 0) {
       if (!g_private_ready) {
          g_caller_rand = initstate(20240807u, g_private_rand, sizeof(g_private_rand));
@@ -54,6 +59,7 @@ RandScope::~RandScope()
       setstate(g_caller_rand);
       g_caller_rand = nullptr;
    }
+   g_rand_mu.unlock();
 }
 
 CallerRandBatch::CallerRandBatch()
@@ -750,7 +756,7 @@ int Nfft4GPAdditiveNFFTMatSymv(void* data, int n, double alpha, double* x, doubl
 {
    PlanExt* E = additive_plan(data);
    if (!E) return -1;
-   RandScope rand_scope;
+   // no RandScope on the apply path: HIP was initialised by the handle's create / setup
    return plan_apply(E, n, 0, alpha, x, beta, y);
 }
 
@@ -780,7 +786,6 @@ int Nfft4GPAdditiveNFFTGradMatSymv(void* data, int n, double alpha, double* x, d
 {
    PlanExt* E = additive_plan(data);
    if (!E) return -1;
-   RandScope rand_scope;
    return plan_apply(E, n, 1, alpha, x, beta, y);
 }
 
@@ -1183,7 +1188,6 @@ int Nfft4GPNFFTMatSymv(void* data, int n, double alpha, double* x, double beta, 
 {
    SingleAdj* adj = (SingleAdj*)data;
    if (!adj || !adj->plan) return -1;
-   RandScope rand_scope;
    return plan_apply(adj->plan, n, 0, alpha, x, beta, y);
 }
 
@@ -1191,7 +1195,6 @@ int Nfft4GPNFFTGradMatSymv(void* data, int n, double alpha, double* x, double be
 {
    SingleAdj* adj = (SingleAdj*)data;
    if (!adj || !adj->plan) return -1;
-   RandScope rand_scope;
    return plan_apply(adj->plan, n, 1, alpha, x, beta, y);
 }
 

@@ -722,6 +722,12 @@ static int bcast_root(Comm* comm, double* d, size_t count, hipStream_t s)
    return comm->allreduce(d, count, s);
 }
 
+// Row shards (shard != nullptr): the collectives below (the L^{-T} broadcast, the Gram all-reduce, the
+// eigenbasis broadcast) are entered by every rank in the same order.  A rank-local failure between them
+// (an allocation, an upload, a rocSOLVER error) returns on that rank only, and the other ranks then wait in
+// their next collective: under a communicator any setup error is fatal to the whole group, and the caller
+// must tear the group down (the replicated steps -- K11, its Cholesky -- fail on every rank
+// alike).
 NysDev* nys_setup_additive(const double* xw_host, int n, int nw, int dw, int skip_last, int kernel, double f,
                            double l, double mu, const int* perm, int k, int k11_mode, bool with_grad,
                            const NysShard* shard)

@@ -63,6 +63,15 @@ class Communicator:
         L = _lib.lib()
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         on_device = dist.get_backend(group) == "nccl"
+        dev = "cuda" if on_device else "cpu"
+        # every rank learns whether every rank can create a communicator BEFORE any of them enters
+        # ncclCommInitRank: a rank that cannot (no device, RCCL not loadable) would otherwise return early
+        # while the others wait inside the collective init for it
+        notready = torch.tensor([0.0 if L.Nfft4GPAmdCommRcclAvailable() == 1 else 1.0], dtype=torch.float64,
+                                device=dev)
+        dist.all_reduce(notready, group=group)
+        if float(notready.item()) != 0.0:
+            raise RuntimeError("RCCL is not available on %d rank(s) (see stderr)" % int(notready.item()))
         # the 128-byte id plus a status byte, so that a failure on rank 0 reaches every rank through the same
         # broadcast (no rank is left waiting in a collective the others never enter)
         buf = np.zeros(129, dtype=np.uint8)
@@ -78,7 +87,7 @@ class Communicator:
         cls._bind_stream()
         h = L.Nfft4GPAmdCommCreateRccl(rank, world, buf.ctypes.data)
         # every rank learns whether every rank has a communicator before any of them uses one
-        ok = torch.tensor([0.0 if h else 1.0], dtype=torch.float64, device="cuda" if on_device else "cpu")
+        ok = torch.tensor([0.0 if h else 1.0], dtype=torch.float64, device=dev)
         dist.all_reduce(ok, group=group)
         if float(ok.item()) != 0.0:
             if h:

@@ -7,9 +7,14 @@
   there.  l in {0.01, 0.03} on the committed fixtures' points (foo1d: TEST2's data, synth1d, bike3d:
   TEST1's bike windows) against the oracle.  Contract 1e-6 (north star); the CPU emulation of the same
   layout measured <= 7e-9, so the tests also assert 5e-8 for 1-D windows.
-* config D (configs[3]: config C over 8 GPUs) on one GPU: 8 HIP row shards through
-  Nfft4GPAmdShardSpread / ShardFinish, their grids summed, equal to the whole operator and the oracle;
-  plus a zero-row shard.
+* config D (configs[3]: config C, "components sharded 4-per-GPU across 8 GPUs") on one GPU: the 8
+  component shards of 4 windows each (Nfft4GPAmdAdditiveComponentShard, the mu x term on shard 0), their y
+  summed (what the RCCL all-reduce does), equal to the whole operator and the oracle for the matvec and all
+  3n gradient outputs; and the 8 row shards (Nfft4GPAmdShardSpread / ShardFinish, grids summed), plus a
+  zero-row shard.
+* configs[1] (B: n = 1e5, 8 windows, rank 256) and configs[2] (C: n = 1e6, 32 windows, rank 512): PCG to
+  1e-6 (pcg.c:3-206) with the Nystrom (nys.c:518-660) and the AFN (afn.c:161-489) preconditioners, checked
+  by their true residual.
 * config E (configs[4]: n = 1e7, 64 windows, loss + gradient): the reference's Nfft4GPGpLoss on the
   oracle's operator at n = 2e4, d = 64 (tests/golden/config_e_reduced.npz, make_golden.py config_e),
   and the full size through size-independent properties.
@@ -133,6 +138,137 @@ def test_config_d_eight_row_shards_on_one_gpu(torch_cuda, config_c):
     e = rel(y8, orc.matsymv(x))
     print(f"config D (8 row shards, one GPU): rel err vs oracle {e:.2e}")
     assert e <= 1e-8
+
+
+def _component_shards(X, win, nw, world, l):
+    """The component split of dist.component_range: shard r holds windows [r nw / world, (r+1) nw / world) for
+    all points, weighted 1 / nw_global, the mu x (and f^2 x) term on shard 0 only (nfft_interface.c:796-817
+    sums the components one after another; the split sums the shards' partial y instead)."""
+    from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import component_range
+    L = amd.lib()
+    shards = []
+    for r in range(world):
+        c0, c1 = component_range(nw, r, world)
+        s = amd.NFFTAdditiveKernel(X, win[c0:c1], c1 - c0, 1)
+        assert L.Nfft4GPAmdAdditiveComponentShard(s.h, nw, int(r == 0)) == 0
+        assert s.setup(amd.GAUSSIAN, 1.0, l, 0.01) == 0
+        shards.append(s)
+    return shards
+
+
+@pytest.mark.parametrize("l", [1.0, 0.1])
+def test_config_d_component_shards_on_one_gpu(torch_cuda, config_c, l):
+    """configs[3] as BASELINE writes it: config C's 32 windows sharded 4 per GPU over 8 GPUs.  The 8 component
+    shards run on one GPU; their y summed (the all-reduce) equals the whole operator to 1e-12 and the oracle to
+    1e-8, for the matvec (beta = 0 and beta != 0) and all 3n gradient outputs."""
+    from oracle import OracleAdditiveNFFT
+    torch = torch_cuda
+    X, x = config_c
+    n, d = X.shape
+    win = np.arange(d, dtype=np.int32)
+    shards = _component_shards(X, win, d, 8, l)
+    assert [s.nwindows for s in shards] == [4] * 8
+    xd = torch.tensor(x, device="cuda")
+    y0 = torch.tensor(np.random.default_rng(2).random(n) - 0.5, device="cuda")
+    ysum = torch.zeros(n, dtype=torch.float64, device="cuda")
+    ybsum = torch.zeros(n, dtype=torch.float64, device="cuda")
+    gsum = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
+    for r, s in enumerate(shards):
+        ysum += s.matsymv(xd)
+        # beta y on one shard only, as dist.hip's component matvec does before its all-reduce
+        ybsum += s.matsymv(xd, 0.7, -1.5 if r == 0 else 0.0, y0.clone() if r == 0 else None)
+        gsum += s.gradmatsymv(xd)
+        s.free()
+    full = amd.NFFTAdditiveKernel(X, win, d, 1)
+    assert full.setup(amd.GAUSSIAN, 1.0, l, 0.01) == 0
+    y1 = full.matsymv(xd).cpu().numpy()
+    yb1 = full.matsymv(xd, 0.7, -1.5, y0.clone()).cpu().numpy()
+    g1 = full.gradmatsymv(xd).cpu().numpy()
+    full.free()
+    y8, yb8, g8 = ysum.cpu().numpy(), ybsum.cpu().numpy(), gsum.cpu().numpy()
+    assert rel(y8, y1) <= 1e-12 and rel(yb8, yb1) <= 1e-12
+    assert max(rel(g8[i * n:(i + 1) * n], g1[i * n:(i + 1) * n]) for i in range(3)) <= 1e-12
+    orc = OracleAdditiveNFFT(X, win, d, 1)
+    orc.setup(0, 1.0, l, 0.01)
+    e = rel(y8, orc.matsymv(x))
+    g_ref = orc.gradmatsymv(x)
+    eg = [rel(g8[i * n:(i + 1) * n], g_ref[i * n:(i + 1) * n]) for i in range(3)]
+    print(f"config D (8 component shards of 4 windows, one GPU) l={l}: matvec rel err {e:.2e}, "
+          f"grad {', '.join(f'{v:.2e}' for v in eg)}")
+    assert e <= 1e-8 and max(eg) <= 1e-8, (e, eg)
+
+
+def _true_relres(torch, op, b, x):
+    r = b - op.matsymv(x)
+    return float(torch.linalg.norm(r) / torch.linalg.norm(b))
+
+
+def _pcg_checked(torch, op, b, precond, maxits, tol=1e-6):
+    x = torch.zeros_like(b)
+    _, relres, hist, it = amd.pcg(op, b, x, maxits=maxits, tol=tol, precond=precond)
+    tr = _true_relres(torch, op, b, x)
+    return it, relres, tr
+
+
+def test_config_b_pcg_nystrom_and_afn(torch_cuda):
+    """configs[1]: n = 1e5, 8 additive 1-D windows, rank 256, fp64, PCG to 1e-6 (l = 0.1, where the NFFT
+    operator is SPD).  Unpreconditioned, with the rank-256 Nystrom (landmark K11) and with the
+    reference's AFN flow (Nfft4GPAmdPrecondAFNSetup, afn.c:161-489) for both Schur solves: each converges,
+    its true residual is <= 1.01e-6, and the preconditioners take fewer iterations than none."""
+    import ctypes
+    torch = torch_cuda
+    rng = np.random.default_rng(906)
+    n, d, k = 100_000, 8, 256
+    X = rng.random((n, d))
+    win = np.arange(d, dtype=np.int32)
+    op = amd.NFFTAdditiveKernel(X, win, d, 1)
+    assert op.setup(amd.GAUSSIAN, 1.0, 0.1, 0.01) == 0
+    b = torch.tensor(np.random.default_rng(907).random(n) - 0.5, device="cuda")
+    it0, rr0, tr0 = _pcg_checked(torch, op, b, None, 3000)
+    assert it0 > 0 and tr0 <= 1.01e-6, (it0, rr0, tr0)
+    perm = np.random.default_rng(908).permutation(n).astype(np.int32)
+    nys = amd.NystromPrecond.from_additive(op, perm, k, k11="landmarks")
+    it1, rr1, tr1 = _pcg_checked(torch, op, b, nys, 3000)
+    nys.free()
+    print(f"config B: PCG none {it0} its (true rel res {tr0:.2e}), Nystrom-{k} {it1} its ({tr1:.2e})")
+    assert it1 > 0 and tr1 <= 1.01e-6 and it1 < it0, (it1, rr1, tr1)
+    for schur in ("noise", "fsai"):
+        ctypes.CDLL(None).srand(807)
+        afn = amd.PrecondAFN(X, k, perm_opt="random", schur=schur, schur_lfil=20, op=op)
+        it2, rr2, tr2 = _pcg_checked(torch, op, b, afn, 3000)
+        print(f"config B: PCG AFN ({afn.kind}, rank {afn.k}, schur {schur}) {it2} its ({tr2:.2e})")
+        assert afn.k > 0
+        afn.free()
+        assert it2 > 0 and tr2 <= 1.01e-6 and it2 < it0, (schur, it2, rr2, tr2)
+
+
+def test_config_c_pcg_nystrom_and_afn(torch_cuda, config_c):
+    """configs[2]: n = 1e6, 32 windows, rank 512, PCG to 1e-6 (l = 0.1) with the rank-512 Nystrom and the
+    rank-512 AFN with S^-1 = I/mu (schur_opt 0; the kernel-FSAI Schur leg is the bench's, 5-7 s): both converge
+    with a true residual <= 1.01e-6."""
+    import ctypes
+    torch = torch_cuda
+    X, _ = config_c
+    n, d = X.shape
+    k = 512
+    win = np.arange(d, dtype=np.int32)
+    op = amd.NFFTAdditiveKernel(X, win, d, 1)
+    assert op.setup(amd.GAUSSIAN, 1.0, 0.1, 0.01) == 0
+    b = torch.tensor(np.random.default_rng(907).random(n) - 0.5, device="cuda")
+    perm = np.random.default_rng(908).permutation(n).astype(np.int32)
+    nys = amd.NystromPrecond.from_additive(op, perm, k, k11="landmarks")
+    it1, rr1, tr1 = _pcg_checked(torch, op, b, nys, 3000)
+    nys.free()
+    ctypes.CDLL(None).srand(807)
+    afn = amd.PrecondAFN(X, k, perm_opt="random", schur="noise", op=op)
+    it2, rr2, tr2 = _pcg_checked(torch, op, b, afn, 3000)
+    kind, rank = afn.kind, afn.k
+    afn.free()
+    op.free()
+    print(f"config C: PCG Nystrom-{k} {it1} its (true rel res {tr1:.2e}); AFN ({kind}, rank {rank}, I/mu) "
+          f"{it2} its ({tr2:.2e})")
+    assert it1 > 0 and tr1 <= 1.01e-6, (it1, rr1, tr1)
+    assert it2 > 0 and tr2 <= 1.01e-6, (it2, rr2, tr2)
 
 
 def test_config_d_row_shards_two_launch_path(torch_cuda, config_c):

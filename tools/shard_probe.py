@@ -1,7 +1,11 @@
-"""Row-shard matvec time on one GPU (the per-rank work of an N-GPU run without the all-reduce):
-Nfft4GPAmdShardSpread -> Nfft4GPAmdShardFinish for rows [0, n_global / N) of config C.
+"""Per-rank matvec time of an N-GPU run on one GPU, without the all-reduce:
 
-    python tools/shard_probe.py [--ranks 8]
+* rows (default): Nfft4GPAmdShardSpread -> Nfft4GPAmdShardFinish for rows [0, n_global / N) of config C;
+* components: rank 0 of the component split (BASELINE configs[3]: 4 of config C's 32 windows per GPU at
+  N = 8) -- Nfft4GPAdditiveNFFTMatSymv on a handle of windows [0, nw / N) for all n points
+  (Nfft4GPAmdAdditiveComponentShard, the mu x term on this rank).
+
+    python tools/shard_probe.py [--ranks 8] [--partition components]
 """
 import argparse
 import json
@@ -20,6 +24,7 @@ def main():
     ap.add_argument("--d", type=int, default=32)
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2000)
+    ap.add_argument("--partition", default="rows", choices=["rows", "components"])
     args = ap.parse_args()
     import torch
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
@@ -31,18 +36,29 @@ def main():
     n, d = args.n, args.d
     X = np.asfortranarray(np.random.default_rng(906).random((n, d)))
     win = np.arange(d, dtype=np.int32)
-    re = n // args.ranks
-    op = amd.NFFTAdditiveKernel(X, win, d, 1, shard=(0, re))
-    assert op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) == 0
-    h = op.h
-    g = L.Nfft4GPAmdShardGridSize(h)
-    grid = torch.zeros(g, dtype=torch.float64, device="cuda")
+    if args.partition == "rows":
+        re = n // args.ranks
+        op = amd.NFFTAdditiveKernel(X, win, d, 1, shard=(0, re))
+        assert op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) == 0
+        h = op.h
+        g = L.Nfft4GPAmdShardGridSize(h)
+        grid = torch.zeros(g, dtype=torch.float64, device="cuda")
+    else:
+        re = n
+        nwl = d // args.ranks
+        op = amd.NFFTAdditiveKernel(X, win[:nwl], nwl, 1)
+        assert L.Nfft4GPAmdAdditiveComponentShard(op.h, d, 1) == 0
+        assert op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) == 0
+        h = op.h
     x = torch.tensor(np.random.default_rng(1).random(re) - 0.5, device="cuda")
     y = torch.zeros(re, dtype=torch.float64, device="cuda")
 
     def step():
-        assert L.Nfft4GPAmdShardSpread(h, x.data_ptr(), grid.data_ptr()) == 0
-        assert L.Nfft4GPAmdShardFinish(h, grid.data_ptr(), 0, 1.0, x.data_ptr(), 0.0, y.data_ptr()) == 0
+        if args.partition == "rows":
+            assert L.Nfft4GPAmdShardSpread(h, x.data_ptr(), grid.data_ptr()) == 0
+            assert L.Nfft4GPAmdShardFinish(h, grid.data_ptr(), 0, 1.0, x.data_ptr(), 0.0, y.data_ptr()) == 0
+        else:
+            op.matsymv(x, 1.0, 0.0, y)
 
     t_end = time.perf_counter() + 0.5
     while time.perf_counter() < t_end:
@@ -55,7 +71,9 @@ def main():
         step()
     torch.cuda.synchronize()
     us = (time.perf_counter() - t0) / args.reps * 1e6
-    print(json.dumps({"rows": re, "us_per_shard_matvec": us, "y_norm": float(y.norm())}))
+    print(json.dumps({"partition": args.partition, "ranks": args.ranks, "rows": re,
+                      "windows": d if args.partition == "rows" else d // args.ranks, "us_per_shard_matvec": us,
+                      "y_norm": float(y.norm())}))
 
 
 if __name__ == "__main__":
