@@ -174,8 +174,7 @@ struct AdditivePlan {
    double diag = 1.0;    // 1: this handle adds the mu x (and grad f^2 x) terms; 0: a component shard without them
    // layout
    int B = kMaxBlock, CG = 3, ngroups = 0, nblocks = 0;  // CG = 3: 3 spread workgroups fit a CU's LDS
-   int spread_variant = 1, interp_variant = 1;  // kernel shape variants (nfft_kernels.hip)
-   int gpw = 1;                                  // window groups per spread workgroup (alpha staged once)
+   int spread_variant = 0;  // 0: the spread; 1: the same with timeline stamps (NFFT4GP_AMD_SPREAD_VARIANT, tools/)
    DevLayout dl;
    // device buffers
    double* d_part = nullptr;  // [nblocks][nw][64]
@@ -186,10 +185,6 @@ struct AdditivePlan {
    double* d_C = nullptr;     // [kTaps][kNC]
    double* d_dot_part = nullptr;         // [nblocks] fused matvec-dot partials
    unsigned int* d_dot_ticket = nullptr; // arrival counters (reduce.hpp)
-   unsigned int* d_sum_ticket = nullptr; // row shards: arrival counters, [slice] of the fused spread sum then
-                                         // [block] of the fused finish (2 x kMaxSumSlices, kTicketStride apart)
-   double* d_ypart = nullptr;            // row shards: the fused finish's y-slices
-   size_t ypart_count = 0;
    double* d_part2 = nullptr; // two-vector matvec: both vectors' partial grids [2][nblocks][nw][64]
    double* d_H2 = nullptr;    // [2][nw][64][kNC]
    double* d_xs = nullptr;    // staging (host pointer calls)
@@ -207,20 +202,12 @@ struct AdditivePlan {
 // copy the tap polynomial table into constant memory of the current device
 int upload_tap_coeffs();
 // launchers (nfft_kernels.hip); all enqueue on `stream`
-// d_gsum (row shards): the spread also sums the blocks' partial grids into d_gsum[nw][64]
-constexpr int kMaxSumSlices = 256;
-int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream,
-                  double* d_gsum = nullptr);
+int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream);
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream);
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream);
 int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream);
 // row shards with few blocks: grid from the summed grids + y = beta y + alpha f^2 mu x, then the interpolation
 // with S workgroups per block adding into y atomically (plain matvec)
-// the same in one launch: H of each part's windows built in LDS, deterministic sum of the S slices
-// (d_ypart: S * nblocks * B doubles; P.nblocks <= kMaxSumSlices)
-size_t shard_finish_lds_bytes(const AdditivePlan& P, int S);
-int launch_shard_finish_fused(const AdditivePlan& P, const double* d_gridsum, double alpha, const double* d_x,
-                              double beta, double* d_y, int S, double* d_ypart, hipStream_t stream);
 int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, double alpha, const double* d_x,
                               double beta, double* d_y, int S, hipStream_t stream);
 // d_dot != nullptr (non-grad): also writes (y, x) to *d_dot (device), one grid-wide reduction in the launch

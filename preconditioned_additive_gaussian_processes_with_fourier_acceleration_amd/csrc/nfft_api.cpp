@@ -149,11 +149,6 @@ void free_layout(AdditivePlan& P)
    dfree(P.d_H2);
    dfree(P.d_dot_part);
    dfree(P.d_dot_ticket);
-   dfree(P.d_sum_ticket);
-   P.d_sum_ticket = nullptr;
-   dfree(P.d_ypart);
-   P.d_ypart = nullptr;
-   P.ypart_count = 0;
    P.d_part2 = P.d_H2 = nullptr;
    P.d_part = nullptr;
    P.d_dot_part = nullptr;
@@ -315,10 +310,6 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
    if (!P.d_dot_ticket) {
       NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_dot_ticket, sizeof(unsigned int) * kTicketWords));
       NFFT4GP_HIP_CHECK(hipMemset(P.d_dot_ticket, 0, sizeof(unsigned int) * kTicketWords));
-   }
-   if (!P.d_sum_ticket) {
-      NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_sum_ticket, sizeof(unsigned int) * 2 * kMaxSumSlices * kTicketStride));
-      NFFT4GP_HIP_CHECK(hipMemset(P.d_sum_ticket, 0, sizeof(unsigned int) * 2 * kMaxSumSlices * kTicketStride));
    }
 
    if (!P.d_H) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_H, sizeof(double) * (size_t)P.nw * kNos * kNC));
@@ -521,8 +512,6 @@ void env_layout(AdditivePlan& P)
       if (v >= 1 && v <= 64) P.CG = v;
    }
    if (const char* e = getenv("NFFT4GP_AMD_SPREAD_VARIANT")) P.spread_variant = atoi(e);
-   if (const char* e = getenv("NFFT4GP_AMD_GPW")) P.gpw = std::max(1, atoi(e));
-   if (const char* e = getenv("NFFT4GP_AMD_INTERP_VARIANT")) P.interp_variant = atoi(e);
 }
 
 void* additive_create(double* data, int n_global, int ldim, int* windows, int nwindows, int dwindows, int rb, int re)
@@ -960,16 +949,6 @@ int Nfft4GPAmdAdditiveComponentShard(void* str, int nw_global, int own_diag)
    return 0;
 }
 
-// the two-launch shard path: NFFT4GP_AMD_SHARD_FUSE, or the test hook below; off by default
-static int g_shard_fuse = -1;
-static int shard_fuse()
-{
-   if (g_shard_fuse < 0) g_shard_fuse = getenv("NFFT4GP_AMD_SHARD_FUSE") ? atoi(getenv("NFFT4GP_AMD_SHARD_FUSE")) : 0;
-   return g_shard_fuse;
-}
-
-extern "C" void Nfft4GPAmdDebugSetShardFuse(int on) { g_shard_fuse = on ? 1 : 0; }
-
 int Nfft4GPAmdShardSpread(void* str, const double* x_local, double* grid)
 {
    PlanExt* E = additive_plan(str);
@@ -981,11 +960,7 @@ int Nfft4GPAmdShardSpread(void* str, const double* x_local, double* grid)
       NFFT4GP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * P.nw * kNos, s));
       return 0;
    }
-   // the blocks' partial grids summed inside the spread (its last block per slice of window groups), or by
-   // k_reduce_parts after it (NFFT4GP_AMD_SHARD_FUSE=0; the persistent spread variants)
-   const int gpw = std::min(std::max(P.gpw, 1), P.ngroups);
-   if (shard_fuse() && P.spread_variant < 5 && P.dl.ntiles > 0 && (P.ngroups + gpw - 1) / gpw <= kMaxSumSlices)
-      return launch_spread(P, x_local, P.d_part, s, grid);
+   // the blocks' partial grids summed by k_reduce_parts into the grid the caller all-reduces
    if (launch_spread(P, x_local, P.d_part, s)) return -1;
    return launch_reduce_parts(P, P.d_part, grid, s);
 }
@@ -1008,18 +983,6 @@ int Nfft4GPAmdShardFinish(void* str, const double* grid, int grad, double alpha,
    int S = P.nblocks <= 64 ? 4 : 1;
    if (const char* e = getenv("NFFT4GP_AMD_SHARD_SPLIT")) S = std::max(1, std::min(16, atoi(e)));
    S = std::min(S, std::max(1, P.ngroups));
-   if (!grad && S > 1 && !P.timing && shard_fuse() && P.nblocks <= kMaxSumSlices &&
-       shard_finish_lds_bytes(P, S) <= 160 * 1024) {
-      const size_t need = (size_t)S * P.nblocks * P.B;
-      if (P.ypart_count < need) {
-         dfree(P.d_ypart);
-         P.d_ypart = nullptr;
-         P.ypart_count = 0;
-         NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_ypart, sizeof(double) * need));
-         P.ypart_count = need;
-      }
-      return launch_shard_finish_fused(P, grid, alpha, x_local, beta, y_local, S, P.d_ypart, s);
-   }
    if (!grad && S > 1 && !P.timing) return launch_shard_finish_split(P, grid, alpha, x_local, beta, y_local, S, s);
    if (launch_grid_from_sum(P, grid, grad, s)) return -1;
    return launch_interp(P, grad, alpha, x_local, beta, y_local, s);

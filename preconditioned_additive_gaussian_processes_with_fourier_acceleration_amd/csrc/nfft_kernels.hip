@@ -15,10 +15,8 @@
 //             Horner per point, ds_add_f64 into an LDS y-block; the epilogue applies
 //             y = beta*y + alpha*ff*(sum + mu*x) (grad: the three outputs of nfft_interface.c:547-549)
 //             in one coalesced pass.
-// Kernel shapes (threads per workgroup, occupancy hint, next-run prefetch) are template parameters;
-// the launchers pick a variant from AdditivePlan (env NFFT4GP_AMD_SPREAD_VARIANT / _INTERP_VARIANT).
-// Rejected experiments (persistent workgroups, three-deep run rings, mixed-precision moments, the grid
-// step fused into the spread tail via global atomics) are in the git history; DESIGN.md has numbers.
+// Rejected experiments (persistent workgroups, prefetching runs, three-deep run rings, mixed-precision moments,
+// the grid step fused into the spread tail) are in the git history; DESIGN.md 3.5 has their numbers.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -92,40 +90,8 @@ __device__ __forceinline__ uint32_t slot_loc(const TileRegs& T, int r)
    return ((T.qq[r] >> 26) << 6) | ((T.lo[r >> 2] >> (8 * (r & 3))) & 63u);
 }
 
-// Stage x[base, base + nloc) of a block into LDS (zero beyond nloc, up to B), plus two zero pad
-// entries s[B .. B+kPad) that the layout's dummy slots point at.  Every thread issues ALL its 16-byte
-// loads before its first LDS write, so the slice costs one memory latency instead of B/THREADS.
-template <int THREADS>
-__device__ __forceinline__ void stage_block(double* __restrict__ s, const double* __restrict__ x, int base, int nloc,
-                                            int B)
-{
-   constexpr int U = 4;  // 16-byte loads in flight per thread
-   const int tid = threadIdx.x;
-   const double* src = x + base;
-   const bool vec = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
-   const int npair = B >> 1;
-   for (int i0 = tid; i0 < npair; i0 += U * THREADS) {
-      double2 v[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-         const int e = 2 * (i0 + u * THREADS);
-         if (vec && e + 1 < nloc) {
-            v[u] = *reinterpret_cast<const double2*>(src + e);
-         } else {
-            v[u].x = e < nloc ? src[e] : 0.0;
-            v[u].y = e + 1 < nloc ? src[e + 1] : 0.0;
-         }
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-         const int i = i0 + u * THREADS;
-         if (i < npair) reinterpret_cast<double2*>(s)[i] = v[u];
-      }
-   }
-   if (tid < kPad) s[B + tid] = 0.0;
-}
-
-// The same slice by LDS-DMA (global_load_lds_dwordx4): each wave moves 1 KB pieces straight into LDS (lane l
+// Stage x[base, base + nloc) of a block into LDS (zero beyond nloc, up to B, plus kPad zero entries that the
+// layout's dummy slots point at) by LDS-DMA (global_load_lds_dwordx4): each wave moves 1 KB pieces straight into LDS (lane l
 // lands at the wave-uniform base + 16 l), no VGPR round trip and no ds_write; the ragged tail and the pad go
 // through plain stores.  The caller waits vmcnt(0) before the barrier that publishes the slice.
 template <int THREADS>
@@ -144,36 +110,27 @@ __device__ __forceinline__ void stage_block_glds(double* __restrict__ s, const d
 // ------------------------------------------------------------------------------------------------
 // spread
 // ------------------------------------------------------------------------------------------------
-// gsum (row shards): the partial grids are stored memory-side and the last block to finish a slice of
-// window groups sums them over the blocks in block order into gsum[comp][cell] (reduce.hpp's handoff;
-// tickets: one counter per slice, kTicketStride apart, left at zero) -- k_reduce_parts inside the spread.
-// no-prefetch variants: at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
-template <int THREADS, bool PREFETCH, bool TIMELINE = false, bool GLDS = false, bool FOLD2 = false>
-__global__ __launch_bounds__(THREADS, PREFETCH ? 1 : 6) void k_spread(const uint16_t* __restrict__ meta,
-                                                    const uint32_t* __restrict__ lo,
-                                                    const uint32_t* __restrict__ qarr,
-                                                    const int* __restrict__ tile_off, const double* __restrict__ x,
-                                                    int n, int B, int nblocks, int ngroups, int CG, int nw, int gpw,
-                                                    double* __restrict__ part, double* __restrict__ gsum,
-                                                    unsigned int* __restrict__ ticket)
+// at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
+template <int THREADS, bool TIMELINE = false>
+__global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restrict__ meta,
+                                                      const uint32_t* __restrict__ lo,
+                                                      const uint32_t* __restrict__ qarr,
+                                                      const int* __restrict__ tile_off, const double* __restrict__ x,
+                                                      int n, int B, int nblocks, int ngroups, int CG, int nw,
+                                                      double* __restrict__ part)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = B + kPad;
    double* s_alpha = smem;     // Bp
    double* s_mom = smem + Bp;  // CG*64*kMomStride per-cell moments
 
-   // One workgroup = one block of points x a slice of gpw consecutive window groups: the block's
-   // alpha slice is staged ONCE and reused for every group of the slice, and the next group's first
-   // run is fetched while the current group folds.  XCD-aware decode: the slices of one block land
-   // on one XCD (blockIdx % 8), so its alpha slice is read into one L2.  Placement is speed only.
-   const int nslices = (ngroups + gpw - 1) / gpw;
+   // One workgroup = one block of points x one group of CG windows.  XCD-aware decode: the groups of one
+   // block land on one XCD (blockIdx % 8), so its alpha slice is read into one L2.  Placement is speed only.
    const int xcd = blockIdx.x & 7;
    const int rest = blockIdx.x >> 3;
-   const int slice = rest % nslices;
-   const int b = (rest / nslices) * 8 + xcd;
+   const int g = rest % ngroups;
+   const int b = (rest / ngroups) * 8 + xcd;
    if (b >= nblocks) return;
-   const int g_begin = slice * gpw;
-   const int g_end = min(ngroups, g_begin + gpw);
    if (TIMELINE) stamp(0);
 
    const int tid = threadIdx.x;
@@ -183,283 +140,61 @@ __global__ __launch_bounds__(THREADS, PREFETCH ? 1 : 6) void k_spread(const uint
 
    // the first run's loads and the alpha slice are in flight together
    TileRegs cur;
-   int t0 = tile_off[b * ngroups + g_begin];
-   int t1 = tile_off[b * ngroups + g_begin + 1];
-   int t = t0 + wave;
+   const int t1 = tile_off[b * ngroups + g + 1];
+   int t = tile_off[b * ngroups + g] + wave;
    if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
    const int base = b * B;
-   if (GLDS)
-      stage_block_glds<THREADS>(s_alpha, x, base, min(B, n - base), B);
-   else
-      stage_block<THREADS>(s_alpha, x, base, min(B, n - base), B);
+   stage_block_glds<THREADS>(s_alpha, x, base, min(B, n - base), B);
    for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
-   if (GLDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces have landed
+   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces have landed
    __syncthreads();
    if (TIMELINE) stamp(1);
 
-   for (int g = g_begin; g < g_end; g++) {
-      const int c0 = g * CG;
-      for (; t < t1; t += nwaves) {
-         TileRegs nxt;
-         const int tn = t + nwaves;
-         if (PREFETCH && tn < t1) load_tile(nxt, meta, lo, qarr, tn, lane);  // prefetch the next run
-         double acc[kNC];
+   const int c0 = g * CG;
+   for (; t < t1; t += nwaves) {
+      double acc[kNC];
 #pragma unroll
-         for (int d = 0; d < kNC; d++) acc[d] = 0.0;
+      for (int d = 0; d < kNC; d++) acc[d] = 0.0;
 #pragma unroll
-         for (int r = 0; r < kR; r++) {
-            const uint32_t loc = slot_loc(cur, r);
-            const double u = q_to_u(cur.qq[r]);
-            double tpow = s_alpha[loc];
-            acc[0] += tpow;
+      for (int r = 0; r < kR; r++) {
+         const uint32_t loc = slot_loc(cur, r);
+         const double u = q_to_u(cur.qq[r]);
+         double tpow = s_alpha[loc];
+         acc[0] += tpow;
 #pragma unroll
-            for (int d = 1; d < kNC; d++) {
-               tpow *= u;
-               acc[d] += tpow;
-            }
-         }
-         const int comp_local = (int)(cur.mt >> 6) - c0;
-         const int cell = (int)(cur.mt & 63u);
-         double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
-#pragma unroll
-         for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
-         if (PREFETCH) {
-            if (tn < t1) cur = nxt;
-         } else if (tn < t1) {
-            load_tile(cur, meta, lo, qarr, tn, lane);
+         for (int d = 1; d < kNC; d++) {
+            tpow *= u;
+            acc[d] += tpow;
          }
       }
-      __syncthreads();
-      if (TIMELINE && g == g_begin) stamp(2);
+      const int comp_local = (int)(cur.mt >> 6) - c0;
+      const int cell = (int)(cur.mt & 63u);
+      double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
+#pragma unroll
+      for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
+      if (t + nwaves < t1) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
+   }
+   __syncthreads();
+   if (TIMELINE) stamp(2);
 
-      // the next group's first run is loaded while this group folds
-      if (g + 1 < g_end) {
-         t0 = t1;
-         t1 = tile_off[b * ngroups + g + 2];
-         t = t0 + wave;
-         if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
-      }
-
-      // fold moments into the 64-cell partial grid of every window of this group:
-      //   g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
-      const int ncomp = min(CG, nw - c0);
-      for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
-         const int cl = idx / kNos;
-         const int gi = idx % kNos;
-         // FOLD2 (variant 8): two chains (even and odd taps) instead of one dependent 100-term chain; measured
-         // neutral at config C (44.3 vs 44.4 us) and 1 % slower at config E, so one chain stays the default
-         double v0 = 0.0, v1 = 0.0;
-         if (FOLD2) {
+   // fold moments into the 64-cell partial grid of every window of this group:
+   //   g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
+   const int ncomp = min(CG, nw - c0);
+   for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
+      const int cl = idx / kNos;
+      const int gi = idx % kNos;
+      double v = 0.0;
 #pragma unroll 1
-            for (int tp = 0; tp < kTaps; tp += 2) {
-               const double* m0 = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
-               const double* m1 = s_mom + (cl * kNos + ((gi + kM - tp - 1) & (kNos - 1))) * kMomStride;
+      for (int tp = 0; tp < kTaps; tp++) {
+         const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
 #pragma unroll
-               for (int d = 0; d < kNC; d++) {
-                  v0 = fma(c_taps[tp * kNC + d], m0[d], v0);
-                  v1 = fma(c_taps[(tp + 1) * kNC + d], m1[d], v1);
-               }
-            }
-         } else {  // one 100-term chain
-#pragma unroll 1
-            for (int tp = 0; tp < kTaps; tp++) {
-               const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
-#pragma unroll
-               for (int d = 0; d < kNC; d++) v0 = fma(c_taps[tp * kNC + d], mrow[d], v0);
-            }
-         }
-         const double v = v0 + v1;
-         double* dst = part + ((size_t)(c0 + cl) * nblocks + b) * kNos + gi;  // [comp][block][cell]
-         if (gsum)
-            __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-         else
-            *dst = v;
+         for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
       }
-      if (g + 1 < g_end) {
-         __syncthreads();  // every fold read done before the table is cleared
-         for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
-         __syncthreads();
-      }
+      part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
    }
    if (TIMELINE) {
       __syncthreads();
       stamp(3);
-   }
-   if (gsum) {
-      __shared__ int s_last;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-         const unsigned old = __hip_atomic_fetch_add(ticket + slice * kTicketStride, 1u, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-         s_last = (old == (unsigned)nblocks - 1);
-      }
-      __syncthreads();
-      if (!s_last) return;
-      // the slice's windows: sum the blocks' grids in block order, 8 loads in flight per thread
-      const int c_begin = g_begin * CG, c_end = min(nw, g_end * CG);
-      for (int idx = tid; idx < (c_end - c_begin) * kNos; idx += THREADS) {
-         const int comp = c_begin + idx / kNos, cell = idx % kNos;
-         const double* src = part + (size_t)comp * nblocks * kNos + cell;
-         double acc = 0.0;
-         for (int p0 = 0; p0 < nblocks; p0 += 16) {
-            double v[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-               v[k] = p0 + k < nblocks
-                          ? __hip_atomic_load(src + (size_t)(p0 + k) * kNos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                          : 0.0;
-#pragma unroll
-            for (int k = 0; k < 16; k++) acc += v[k];
-         }
-         gsum[(size_t)comp * kNos + cell] = acc;
-      }
-      if (tid == 0) __hip_atomic_store(ticket + slice * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-   }
-}
-
-// ------------------------------------------------------------------------------------------------
-// persistent spread: one 1024-thread workgroup per CU walks a contiguous range of items (block b,
-// super-group of S layout groups = S*CG windows); the block's alpha slice is staged once per block and the
-// NEXT block's slice is loaded into registers (B/1024 doubles per thread) while the current item runs, so
-// no item waits for its alpha; the next item's first run is loaded while the current one folds.  Same
-// moments, fold order and partial grids as k_spread (results identical up to the ds_add_f64 order).
-// ------------------------------------------------------------------------------------------------
-template <int T>
-constexpr int pers_alpha() { return (kMaxBlock + kPad + T - 1) / T; }  // alpha doubles per thread
-
-template <int T>
-__device__ __forceinline__ void alpha_regs_load(double (&a)[pers_alpha<T>()], const double* __restrict__ x, int base,
-                                                int nloc)
-{
-#pragma unroll
-   for (int k = 0; k < pers_alpha<T>(); k++) {
-      const int e = threadIdx.x + k * T;
-      a[k] = e < nloc ? x[(size_t)base + e] : 0.0;
-   }
-}
-
-template <int T>
-__device__ __forceinline__ void alpha_regs_store(double* __restrict__ s, const double (&a)[pers_alpha<T>()], int Bp)
-{
-#pragma unroll
-   for (int k = 0; k < pers_alpha<T>(); k++) {
-      const int e = threadIdx.x + k * T;
-      if (e < Bp) s[e] = a[k];  // entries >= nloc (pad and dummy slots) are zero
-   }
-}
-
-// THREADS = 1024, PF = true: one workgroup per CU, the next block's alpha in registers during an item.
-// THREADS = 512, PF = false: three per CU (the k_spread footprint), the alpha slice staged after the fold
-// when the block changes; the persistence only removes the launch tail and re-staging within a block.
-template <int THREADS, int S, bool PF>
-__global__ __launch_bounds__(THREADS) void k_spread_pers(const uint16_t* __restrict__ meta,
-                                                               const uint32_t* __restrict__ lo,
-                                                               const uint32_t* __restrict__ qarr,
-                                                               const int* __restrict__ tile_off,
-                                                               const double* __restrict__ x, int n, int B, int nblocks,
-                                                               int ngroups, int CG, int nw,
-                                                               double* __restrict__ part)
-{
-   extern __shared__ __attribute__((aligned(16))) double smem[];
-   const int Bp = B + kPad;
-   double* s_alpha = smem;
-   double* s_mom = smem + Bp;  // S*CG*64*kMomStride
-   const int nsg = (ngroups + S - 1) / S;  // super-groups per block
-   const long long nitems = (long long)nblocks * nsg;
-   const int i_begin = (int)(nitems * blockIdx.x / gridDim.x);
-   const int i_end = (int)(nitems * (blockIdx.x + 1) / gridDim.x);
-   if (i_begin >= i_end) return;
-   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-   constexpr int nwaves = THREADS / 64;
-   constexpr int kPersThreads = THREADS;
-   constexpr int NA = pers_alpha<THREADS>();
-   const int mom_count = S * CG * kNos * kMomStride;
-
-   // the first item: its alpha slice and first run
-   int b = i_begin / nsg;
-   int sg = i_begin % nsg;
-   int t1 = tile_off[b * ngroups + min(ngroups, (sg + 1) * S)];
-   int t = tile_off[b * ngroups + sg * S] + wave;
-   TileRegs cur;
-   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
-   stage_block<THREADS>(s_alpha, x, b * B, min(B, n - b * B), B);
-   for (int i = tid; i < mom_count; i += kPersThreads) s_mom[i] = 0.0;
-   __syncthreads();
-
-   for (int item = i_begin; item < i_end; item++) {
-      const int c0 = sg * S * CG;
-      // the next item's alpha slice, if it starts a new block, travels while this item runs
-      const int nb = (item + 1 < i_end) ? (item + 1) / nsg : b;
-      double an[PF ? NA : 1];
-      if constexpr (PF) {
-         if (nb != b) alpha_regs_load<THREADS>(an, x, nb * B, min(B, n - nb * B));
-      }
-      for (; t < t1; t += nwaves) {
-         TileRegs nxt;
-         const int tn = t + nwaves;
-         if (PF && tn < t1) load_tile(nxt, meta, lo, qarr, tn, lane);
-         double acc[kNC];
-#pragma unroll
-         for (int d = 0; d < kNC; d++) acc[d] = 0.0;
-#pragma unroll
-         for (int r = 0; r < kR; r++) {
-            const uint32_t loc = slot_loc(cur, r);
-            const double u = q_to_u(cur.qq[r]);
-            double tpow = s_alpha[loc];
-            acc[0] += tpow;
-#pragma unroll
-            for (int d = 1; d < kNC; d++) {
-               tpow *= u;
-               acc[d] += tpow;
-            }
-         }
-         const int comp_local = (int)(cur.mt >> 6) - c0;
-         const int cell = (int)(cur.mt & 63u);
-         double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
-#pragma unroll
-         for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
-         if (PF) {
-            if (tn < t1) cur = nxt;
-         } else if (tn < t1) {
-            load_tile(cur, meta, lo, qarr, tn, lane);
-         }
-      }
-      __syncthreads();
-      // the next item's first run is loaded while this one folds
-      const int ob = b;
-      if (item + 1 < i_end) {
-         b = nb;
-         sg = (item + 1) % nsg;
-         t1 = tile_off[b * ngroups + min(ngroups, (sg + 1) * S)];
-         t = tile_off[b * ngroups + sg * S] + wave;
-         if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
-      }
-      // fold (as k_spread): g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
-      const int ncomp = min(S * CG, nw - c0);
-      for (int idx = tid; idx < ncomp * kNos; idx += kPersThreads) {
-         const int cl = idx / kNos;
-         const int gi = idx % kNos;
-         double v = 0.0;
-#pragma unroll 1
-         for (int tp = 0; tp < kTaps; tp++) {
-            const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
-#pragma unroll
-            for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
-         }
-         part[((size_t)(c0 + cl) * nblocks + ob) * kNos + gi] = v;  // [comp][block][cell]
-      }
-      if (item + 1 < i_end) {
-         __syncthreads();  // fold reads and the last run's alpha reads are done
-         for (int i = tid; i < mom_count; i += kPersThreads) s_mom[i] = 0.0;
-         if (nb != ob) {
-            if constexpr (PF)
-               alpha_regs_store<THREADS>(s_alpha, an, Bp);
-            else
-               stage_block<THREADS>(s_alpha, x, nb * B, min(B, n - nb * B), B);
-         }
-         __syncthreads();
-      }
    }
 }
 
@@ -664,111 +399,6 @@ __global__ __launch_bounds__(THREADS) void k_interp_part(const uint16_t* __restr
    for (int j = tid; j < nloc; j += THREADS) atomicAdd(y + (size_t)base + j, scale * s_y[j]);
 }
 
-// Row shards with few blocks, one launch (launch_shard_finish_fused): workgroup (block b, part s) builds the
-// interpolation polynomials H of its own window groups in LDS from the summed grids (k_grid's circulant
-// and tap products, same operation order), interpolates its tiles into an LDS y-slice, stores the slice
-// memory-side, and the last of the block's S workgroups forms y = beta y + amu x + scale sum_s slice_s in
-// part order (deterministic, no global atomics, no separate grid or y-initialisation launch).
-template <int THREADS>
-__global__ __launch_bounds__(THREADS) void k_shard_finish(const uint16_t* __restrict__ meta,
-                                                         const uint32_t* __restrict__ lo,
-                                                         const uint32_t* __restrict__ qarr,
-                                                         const int* __restrict__ tile_off,
-                                                         const double* __restrict__ gsum, const double* __restrict__ w,
-                                                         const double* __restrict__ x, double* __restrict__ y, int n,
-                                                         int B, int ngroups, int CG, int nw, int S, double scale,
-                                                         double beta, double amu, double* __restrict__ ypart,
-                                                         unsigned int* __restrict__ ticket)
-{
-   extern __shared__ __attribute__((aligned(16))) double smem[];
-   const int b = blockIdx.x / S, part = blockIdx.x % S;
-   const int g0 = part * ngroups / S, g1 = (part + 1) * ngroups / S;
-   const int c_begin = min(nw, g0 * CG), c_end = min(nw, g1 * CG), nc = c_end - c_begin;
-   double* s_y = smem;                            // B + kPad
-   double* s_H = smem + B + kPad;                 // [nc][64][kNC]
-   double* s_g = s_H + (size_t)nc * kNos * kNC;   // [nc][64]
-   double* s_h = s_g + (size_t)nc * kNos;         // [nc][64]
-   double* s_w = s_h + (size_t)nc * kNos;         // [nc][64] circulants
-   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-   constexpr int nwaves = THREADS / 64;
-   const int base = b * B;
-   const int nloc = min(B, n - base);
-   const int t1 = tile_off[b * ngroups + g1];
-   int t = tile_off[b * ngroups + g0] + wave;
-   TileRegs cur;
-   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
-   for (int i = tid; i < B + kPad; i += THREADS) s_y[i] = 0.0;
-   for (int i = tid; i < nc * kNos; i += THREADS) {
-      s_g[i] = gsum[(size_t)c_begin * kNos + i];
-      s_w[i] = w[(size_t)c_begin * kNos + i];
-   }
-   __syncthreads();
-   for (int i = tid; i < nc * kNos; i += THREADS) {
-      const int c = i / kNos, tt = i % kNos;
-      const double* wc = s_w + c * kNos;
-      const double* gc = s_g + c * kNos;
-      double h = 0.0;
-#pragma unroll 8
-      for (int l2 = 0; l2 < kNos; l2++) h = fma(wc[(tt - l2) & (kNos - 1)], gc[l2], h);
-      s_h[i] = h;
-   }
-   __syncthreads();
-   for (int i = tid; i < nc * kNos * kNC; i += THREADS) {
-      const int c = i / (kNos * kNC), rem = i % (kNos * kNC);
-      const int cell = rem / kNC, d = rem % kNC;
-      const double* hc = s_h + c * kNos;
-      double v = 0.0;
-#pragma unroll
-      for (int tp = 0; tp < kTaps; tp++) v = fma(hc[(cell - kM + tp) & (kNos - 1)], c_taps[tp * kNC + d], v);
-      s_H[i] = v;
-   }
-   __syncthreads();
-   const int hbase = c_begin * kNos;
-   for (; t < t1; t += nwaves) {
-      const double* hp = s_H + (size_t)((int)cur.mt - hbase) * kNC;
-      double hc[kNC];
-#pragma unroll
-      for (int d = 0; d < kNC; d += 2) {
-         const double2 v = *reinterpret_cast<const double2*>(hp + d);
-         hc[d] = v.x;
-         hc[d + 1] = v.y;
-      }
-#pragma unroll
-      for (int r = 0; r < kR; r++) {
-         const uint32_t loc = slot_loc(cur, r);
-         const double u = q_to_u(cur.qq[r]);
-         double v = hc[kNC - 1];
-#pragma unroll
-         for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
-         atomicAdd(s_y + loc, v);
-      }
-      const int tn = t + nwaves;
-      if (tn < t1) load_tile(cur, meta, lo, qarr, tn, lane);
-   }
-   __syncthreads();
-   double* mine = ypart + ((size_t)b * S + part) * B;
-   for (int j = tid; j < nloc; j += THREADS) __hip_atomic_store(mine + j, s_y[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-   __syncthreads();
-   __shared__ int s_last;
-   if (tid == 0) {
-      const unsigned old = __hip_atomic_fetch_add(ticket + b * kTicketStride, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-      s_last = (old == (unsigned)S - 1);
-   }
-   __syncthreads();
-   if (!s_last) return;
-   const double* slices = ypart + (size_t)b * S * B;
-   for (int j = tid; j < nloc; j += THREADS) {
-      double acc = 0.0;
-      for (int p = 0; p < S; p++)
-         acc += __hip_atomic_load(slices + (size_t)p * B + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const size_t jj = (size_t)base + j;
-      y[jj] = (beta == 0.0 ? 0.0 : beta * y[jj]) + amu * x[jj] + scale * acc;
-   }
-   if (tid == 0) __hip_atomic_store(ticket + b * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // gsum[comp][cell] = sum_b part[comp][b][cell]   (row-sharded path: before the all-reduce).  One
 // workgroup per window, k_grid's 16 strands per cell with 16 loads in flight each (a thread per cell
 // summing the partials one after another took 16 us at an 8-GPU shard of config C)
@@ -810,7 +440,7 @@ constexpr int kEpMax = 8;  // epilogue values per thread held in registers (B <=
 
 // DOT (non-GRAD only): also forms (y_out, x) -- the (q, p) of a CG step when y = A p -- with a
 // deterministic grid-wide sum written to *dot_out by the last block (reduce.hpp)
-template <bool GRAD, int THREADS, bool PREFETCH, bool DOT = false>
+template <bool GRAD, int THREADS, bool DOT = false>
 __global__ __launch_bounds__(THREADS) void k_interp(
     const uint16_t* __restrict__ meta, const uint32_t* __restrict__ lo, const uint32_t* __restrict__ qarr,
     const int* __restrict__ tile_off, const double* __restrict__ H, const double* __restrict__ Hd,
@@ -852,9 +482,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
    __syncthreads();
 
    for (; t < t1; t += nwaves) {
-      TileRegs nxt;
       const int tn = t + nwaves;
-      if (PREFETCH && tn < t1) load_tile(nxt, meta, lo, qarr, tn, lane);  // prefetch the next run
       const size_t hoff = (size_t)cur.mt * kNC;  // (comp*64 + cell) * kNC: meta is comp<<6|cell
       double hc[kNC], hdc[GRAD ? kNC : 1];
 #pragma unroll
@@ -883,11 +511,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
             atomicAdd(s_yd + loc, vd);
          }
       }
-      if (PREFETCH) {
-         if (tn < t1) cur = nxt;
-      } else if (tn < t1) {
-         load_tile(cur, meta, lo, qarr, tn, lane);
-      }
+      if (tn < t1) load_tile(cur, meta, lo, qarr, tn, lane);
    }
    __syncthreads();
 
@@ -1053,13 +677,6 @@ static size_t spread_lds_bytes(const AdditivePlan& P)
    return sizeof(double) * ((size_t)P.B + kPad + (size_t)P.CG * kNos * kMomStride);
 }
 
-// the persistent spread: super-groups of kPersS layout groups while they fit the LDS with the alpha slice
-constexpr int kPersS = 4;
-static size_t pers_lds_bytes(const AdditivePlan& P, int S)
-{
-   return sizeof(double) * ((size_t)P.B + kPad + (size_t)S * P.CG * kNos * kMomStride);
-}
-
 static size_t interp_lds_bytes(const AdditivePlan& P, int grad)
 {
    return sizeof(double) * ((size_t)P.B + kPad) * (grad ? 2 : 1);
@@ -1081,106 +698,44 @@ int upload_tap_coeffs()
 }
 
 typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, int, int, int,
-                         int, int, int, int, double*, double*, unsigned int*);
-struct SpreadVariant {
-   SpreadFn fn;
-   int threads;
-};
-static const SpreadVariant kSpreadVariants[] = {
-    {k_spread<512, true>, 512},         // 0: 8 waves, next-run prefetch
-    {k_spread<512, false, false, true>, 512},  // 1: 8 waves, alpha slice by LDS-DMA (default)
-    {k_spread<256, true>, 256},                // 2: 4 waves, prefetch
-    {k_spread<1024, false>, 1024},             // 3: 16 waves
-    {k_spread<512, false, true, true>, 512},   // 4: variant 1 + per-workgroup s_memrealtime timeline (tools/)
-    {k_spread<512, false>, 512},               // 5, 6: the persistent kernels (launch_spread), never read here
-    {k_spread<512, false>, 512},
-    {k_spread<512, false>, 512},  // 7: variant 1 with the alpha slice staged through registers (rounds 1-3)
-    {k_spread<512, false, false, true, true>, 512},  // 8: variant 1 with the fold in two chains (neutral)
-};
+                         int, int, int, double*);
+// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py).  Variants that
+// measured slower or neutral (prefetching runs, persistent workgroups, several groups per workgroup, the fold in
+// two chains, register-staged alpha, the row shards' block sum in the spread's tail) were removed in round 4;
+// DESIGN.md 3.5 keeps their numbers.
+constexpr int kSpreadThreads = 512;
+static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>};
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
+constexpr int kInterpThreads = 1024;
 typedef void (*InterpFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*,
                          const double*, const double*, double*, int, int, int, double, double, double, double,
                          double, double*, unsigned int*, double*);
-struct InterpVariant {
-   InterpFn fn, fn_grad, fn_dot;
-   int threads;
-};
-static const InterpVariant kInterpVariants[] = {
-    {k_interp<false, 1024, true>, k_interp<true, 1024, true>, k_interp<false, 1024, true, true>, 1024},  // 0
-    {k_interp<false, 1024, false>, k_interp<true, 1024, false>, k_interp<false, 1024, false, true>,
-     1024},                                                                                            // 1 (default)
-    {k_interp<false, 512, true>, k_interp<true, 512, true>, k_interp<false, 512, true, true>, 512},      // 2
-    {k_interp<false, 512, false>, k_interp<true, 512, false>, k_interp<false, 512, false, true>, 512},   // 3
-};
-constexpr int kNumInterpVariants = sizeof(kInterpVariants) / sizeof(kInterpVariants[0]);
 
 static void raise_lds_limit_once()
 {
    // a function-local static initialiser runs once (thread-safe)
    static const bool raised = []() {
       for (int i = 0; i < kNumSpreadVariants; i++)
-         (void)hipFuncSetAttribute((const void*)kSpreadVariants[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+         (void)hipFuncSetAttribute((const void*)kSpreadVariants[i], hipFuncAttributeMaxDynamicSharedMemorySize,
                                    160 * 1024);
-      for (int i = 0; i < kNumInterpVariants; i++) {
-         (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   160 * 1024);
-         (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn_grad,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-         (void)hipFuncSetAttribute((const void*)kInterpVariants[i].fn_dot,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      }
+      for (const void* f : {(const void*)k_interp<false, kInterpThreads>, (const void*)k_interp<true, kInterpThreads>,
+                            (const void*)k_interp<false, kInterpThreads, true>})
+         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipGetLastError();
       return true;
    }();
    (void)raised;
 }
 
-int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream, double* d_gsum)
+int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream)
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
    raise_lds_limit_once();
-   if ((P.spread_variant == 5 && pers_lds_bytes(P, kPersS) <= 160 * 1024) || P.spread_variant == 6) {
-      static bool attr = false;
-      if (!attr) {
-         (void)hipFuncSetAttribute((const void*)k_spread_pers<1024, kPersS, true>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-         (void)hipFuncSetAttribute((const void*)k_spread_pers<512, 1, false>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-         (void)hipGetLastError();
-         attr = true;
-      }
-      static int ncu = 0;
-      if (!ncu) {
-         int dev = 0;
-         (void)hipGetDevice(&dev);
-         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-            ncu = 256;
-      }
-      if (P.spread_variant == 5) {
-         const long long nitems = (long long)P.nblocks * ((P.ngroups + kPersS - 1) / kPersS);
-         const int grid = (int)std::min<long long>(ncu, nitems);
-         launch_ev(k_spread_pers<1024, kPersS, true>, dim3(grid), dim3(1024), pers_lds_bytes(P, kPersS), stream,
-                   P.kev ? P.kev + 0 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks,
-                   P.ngroups, P.CG, P.nw, d_part);
-      } else {
-         const long long nitems = (long long)P.nblocks * P.ngroups;
-         const int grid = (int)std::min<long long>(3LL * ncu, nitems);
-         launch_ev(k_spread_pers<512, 1, false>, dim3(grid), dim3(512), pers_lds_bytes(P, 1), stream,
-                   P.kev ? P.kev + 0 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks,
-                   P.ngroups, P.CG, P.nw, d_part);
-      }
-      NFFT4GP_HIP_CHECK(hipGetLastError());
-      return 0;
-   }
-   const SpreadVariant& V = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
-   const int gpw = std::min(std::max(P.gpw, 1), P.ngroups);
-   const int nslices = (P.ngroups + gpw - 1) / gpw;
-   const int gridx = ((P.nblocks + 7) / 8) * 8 * nslices;
-   if (d_gsum && (!P.d_sum_ticket || nslices > kMaxSumSlices)) return -1;
-   launch_ev(V.fn, dim3(gridx), dim3(V.threads), spread_lds_bytes(P), stream, P.kev ? P.kev + 0 : nullptr, P.dl.meta,
-             P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, gpw, d_part, d_gsum,
-             d_gsum ? P.d_sum_ticket : nullptr);
+   const SpreadFn fn = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
+   const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
+   launch_ev(fn, dim3(gridx), dim3(kSpreadThreads), spread_lds_bytes(P), stream, P.kev ? P.kev + 0 : nullptr,
+             P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -1222,33 +777,6 @@ int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, do
    return 0;
 }
 
-size_t shard_finish_lds_bytes(const AdditivePlan& P, int S)
-{
-   const int ncmax = ((P.ngroups + S - 1) / S) * P.CG;
-   return sizeof(double) * ((size_t)P.B + kPad + (size_t)ncmax * kNos * (kNC + 3));
-}
-
-int launch_shard_finish_fused(const AdditivePlan& P, const double* d_gridsum, double alpha, const double* d_x,
-                              double beta, double* d_y, int S, double* d_ypart, hipStream_t stream)
-{
-   constexpr int T = 512;
-   static bool attr = false;
-   if (!attr) {
-      (void)hipFuncSetAttribute((const void*)k_shard_finish<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-      (void)hipGetLastError();
-      attr = true;
-   }
-   if (P.n == 0) return 0;
-   const double ff = P.f * P.f;
-   hipLaunchKernelGGL(k_shard_finish<T>, dim3(P.nblocks * S), dim3(T), shard_finish_lds_bytes(P, S), stream, P.dl.meta,
-                      P.dl.lo, P.dl.q, P.dl.tile_off, d_gridsum, (const double*)P.d_w, d_x, d_y, P.n, P.B, P.ngroups,
-                      P.CG, P.nw, S, alpha * ff, beta, alpha * ff * P.mu * P.diag, d_ypart,
-                      P.d_sum_ticket + (size_t)kMaxSumSlices * kTicketStride);
-   NFFT4GP_HIP_CHECK(hipGetLastError());
-   return 0;
-}
-
 int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream)
 {
    hipLaunchKernelGGL(k_reduce_parts, dim3(P.nw), dim3(kGridThreads), 0, stream, d_part, P.nblocks, P.nw,
@@ -1262,15 +790,16 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
 {
    if (P.n == 0) return 0;
    raise_lds_limit_once();
-   const InterpVariant& V = kInterpVariants[std::min(std::max(P.interp_variant, 0), kNumInterpVariants - 1)];
    if (d_dot && (grad || P.nblocks > kRedMaxBlocks)) {
       fprintf(stderr, "nfft4gp_amd: fused matvec-dot needs a plain matvec and <= %d blocks\n", kRedMaxBlocks);
       return -1;
    }
-   const InterpFn fn = grad ? V.fn_grad : (d_dot ? V.fn_dot : V.fn);
-   launch_ev(fn, dim3(P.nblocks), dim3(V.threads), interp_lds_bytes(P, grad), stream, P.kev ? P.kev + 4 : nullptr,
-             P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H, (const double*)P.d_Hd, d_x, d_y, P.n,
-             P.B, P.ngroups, alpha, beta, P.f, P.mu * P.diag, P.diag, P.d_dot_part, P.d_dot_ticket, d_dot);
+   const InterpFn fn = grad ? k_interp<true, kInterpThreads>
+                            : (d_dot ? k_interp<false, kInterpThreads, true> : k_interp<false, kInterpThreads>);
+   launch_ev(fn, dim3(P.nblocks), dim3(kInterpThreads), interp_lds_bytes(P, grad), stream,
+             P.kev ? P.kev + 4 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H,
+             (const double*)P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups, alpha, beta, P.f, P.mu * P.diag, P.diag,
+             P.d_dot_part, P.d_dot_ticket, d_dot);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -1283,12 +812,11 @@ int launch_interp_blocks(const AdditivePlan& P, double alpha, const double* d_x,
 {
    if (P.n == 0 || b1 <= b0) return 0;
    raise_lds_limit_once();
-   const InterpVariant& V = kInterpVariants[std::min(std::max(P.interp_variant, 0), kNumInterpVariants - 1)];
    const size_t off = (size_t)b0 * P.B;
-   hipLaunchKernelGGL(V.fn, dim3(b1 - b0), dim3(V.threads), interp_lds_bytes(P, 0), stream, P.dl.meta, P.dl.lo,
-                      P.dl.q, P.dl.tile_off + (size_t)b0 * P.ngroups, (const double*)P.d_H, (const double*)P.d_Hd,
-                      d_x + off, d_y + off, P.n - (int)off, P.B, P.ngroups, alpha, beta, P.f, P.mu * P.diag, P.diag,
-                      (double*)nullptr, (unsigned int*)nullptr, (double*)nullptr);
+   hipLaunchKernelGGL((k_interp<false, kInterpThreads>), dim3(b1 - b0), dim3(kInterpThreads), interp_lds_bytes(P, 0),
+                      stream, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off + (size_t)b0 * P.ngroups, (const double*)P.d_H,
+                      (const double*)P.d_Hd, d_x + off, d_y + off, P.n - (int)off, P.B, P.ngroups, alpha, beta, P.f,
+                      P.mu * P.diag, P.diag, (double*)nullptr, (unsigned int*)nullptr, (double*)nullptr);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

@@ -271,29 +271,6 @@ def test_config_c_pcg_nystrom_and_afn(torch_cuda, config_c):
     assert it2 > 0 and tr2 <= 1.01e-6, (it2, rr2, tr2)
 
 
-def test_config_d_row_shards_two_launch_path(torch_cuda, config_c):
-    """The opt-in two-launch shard path (spread with the block-grid sum in its tail, one-launch finish with a
-    deterministic slice sum; Nfft4GPAmdDebugSetShardFuse): the 8 shards of config D equal the whole operator,
-    and the four-launch default is restored afterwards."""
-    torch = torch_cuda
-    X, x = config_c
-    n, d = X.shape
-    win = np.arange(d, dtype=np.int32)
-    ranges = [row_range(n, r, 8) for r in range(8)]
-    full = amd.NFFTAdditiveKernel(X, win, d, 1)
-    assert full.setup(amd.GAUSSIAN, 1.0, 1.0, 0.01) == 0
-    y1 = full.matsymv(torch.tensor(x, device="cuda")).cpu().numpy()
-    L = amd.lib()
-    try:
-        L.Nfft4GPAmdDebugSetShardFuse(1)
-        ya = _shard_sum(torch, X, win, d, 1, x, ranges, 1.0)
-    finally:
-        L.Nfft4GPAmdDebugSetShardFuse(0)
-    assert rel(ya, y1) <= 1e-12
-    yc = _shard_sum(torch, X, win, d, 1, x, ranges, 1.0)
-    assert rel(yc, y1) <= 1e-12 and rel(ya, yc) <= 1e-13
-
-
 def test_row_shards_1d_with_empty_shard_and_grad(torch_cuda):
     """1-D windows: two shards and a zero-row shard; matvec and all 3n gradient outputs."""
     torch = torch_cuda

@@ -6,7 +6,7 @@ import sys
 import numpy as np
 import torch
 
-os.environ["NFFT4GP_AMD_SPREAD_VARIANT"] = "4"
+os.environ["NFFT4GP_AMD_SPREAD_VARIANT"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd  # noqa: E402
 
