@@ -318,6 +318,7 @@ def run_fgmres(op, torch, n, rng_seed=906, tol=1e-6, kdim=1000, maxits=1000, l=1
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
     assert op.setup(amd.GAUSSIAN, f=1.0, l=l, mu=0.01) == 0
     amd.lib().Nfft4GPAmdSetFgmresOrtho(ortho)
+    amd.lib().Nfft4GPAmdFgmresSecondPasses()  # reset the DGKS counter
     rb, re = rows if rows is not None else (0, n)
     b = torch.tensor((np.random.default_rng(rng_seed + 1).random(n) - 0.5)[rb:re], device="cuda")
     x = torch.zeros(re - rb, dtype=torch.float64, device="cuda")
@@ -334,9 +335,11 @@ def run_fgmres(op, torch, n, rng_seed=906, tol=1e-6, kdim=1000, maxits=1000, l=1
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
     p = "fgmres_" if ortho == 0 else "fgmres_cgs2_"
-    return {p + "time_s": t, p + "iters": iters, p + "rel_res": relres, p + "converged": relres <= tol,
+    extra = {} if ortho == 0 else {p + "second_passes": int(amd.lib().Nfft4GPAmdFgmresSecondPasses())}
+    return {**extra, p + "time_s": t, p + "iters": iters, p + "rel_res": relres, p + "converged": relres <= tol,
             p + "tol": tol, p + "l": l, p + "kdim": kdim, p + "ms_per_iter": 1e3 * t / max(iters, 1),
-            p + "ortho": "modified Gram-Schmidt (fgmres.c)" if ortho == 0 else "block classical Gram-Schmidt x2"}
+            p + "ortho": "modified Gram-Schmidt (fgmres.c)" if ortho == 0 else
+            "block classical Gram-Schmidt, second pass by the DGKS test"}
 
 
 def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1, schur="fsai",

@@ -210,9 +210,12 @@ int Nfft4GPAmdPcgHistoryLength(void);
  * rules above (this library's operators/preconditioners get device pointers, others host vectors).
  * prel_res_v / TDp / TEp are malloc'ed (free with free()). */
 /* FGMRES's orthogonalisation: 0 (default) the reference's modified Gram-Schmidt (Nfft4GPModifiedGS,
- * matops.c:274-346: one launch per basis vector), 1 two block classical Gram-Schmidt passes (a fixed four
- * launches per step; the same projections up to rounding; kdim <= 2046).  Env NFFT4GP_AMD_FGMRES_ORTHO. */
+ * matops.c:274-346: one launch per basis vector), 1 block classical Gram-Schmidt (two launches per pass
+ * whatever the step; a second pass when the first drops ||w|| below 0.7071 of its value, the DGKS test of
+ * matops.c:348-440; the same projections up to rounding; kdim <= 2046).  Env NFFT4GP_AMD_FGMRES_ORTHO.
+ * Nfft4GPAmdFgmresSecondPasses: second passes taken since the last call (then reset). */
 void Nfft4GPAmdSetFgmresOrtho(int ortho);
+long long Nfft4GPAmdFgmresSecondPasses(void);
 /* SRC/solvers/fgmres.c:3-252 (MGS without re-orthogonalisation; kdim <= 4094) */
 int Nfft4GPSolverFgmres(void *mat_data, int n, func_symmatvec matvec, void *prec_data, func_solve precondfunc,
                         NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs, int kdim, int maxits, int atol, NFFT4GP_DOUBLE tol,
@@ -576,6 +579,19 @@ int Nfft4GPAmdAfnSetStorage(void *afn, int bits);
  * gradient-capable branches keep fp64). */
 int Nfft4GPAmdPrecondAFNSetStorage(void *pre, int bits);
 void *Nfft4GPAmdAfnShard(void *afn, int row_begin, int row_end, void *comm);
+/* The same row shard set up on its own rank, with no full AFN anywhere (afn.c:161-489 split by rows, every
+ * rank collectively): the ordering (perm_opt 0 identity, 1 FPS, 2 perm given; afn.c:196-256) and the k x k
+ * factor of A11 are replicated (rank 0's L11^{-1} broadcast); each rank forms only the K12 columns of its own
+ * Schur points (k x m2, afn.c:430-443), the KNN pattern of its own rows of the Schur FSAI (kernels.c:121-278:
+ * scans over the earlier points of those rows only) and their values (fsai.c:302-670), with
+ * W = L11^{-1} K12 formed chunk by chunk for the columns each chunk of rows touches.  G^T products sum each
+ * rank's rows' contributions with one (n-k) all-reduce.  schur_opt 0 (S^-1 = I / mu) or 3 (kernel FSAI);
+ * no gradients.  Apply / free with Nfft4GPAmdDistAfnSolve / Nfft4GPAmdDistAfnFree. */
+void *Nfft4GPAmdAfnShardSetup(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int k, int perm_opt,
+                              const int *perm, int schur_opt, int schur_lfil, int kernel, void *fkernel_params,
+                              int row_begin, int row_end, void *comm);
+/* what a row shard holds: its landmarks m1, its Schur points m2, K12 doubles (k m2), G entries */
+int Nfft4GPAmdAfnShardInfo(void *dafn, int *m1, int *m2, long long *k12_doubles, long long *g_nnz);
 int Nfft4GPAmdDistAfnSolve(void *dafn, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
 void Nfft4GPAmdDistAfnFree(void *dafn);
 

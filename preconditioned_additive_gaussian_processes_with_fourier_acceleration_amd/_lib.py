@@ -172,6 +172,7 @@ _SIGS = {
     "Nfft4GPAmdDistMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),
     "Nfft4GPAmdDistSetChunks": (C.c_int, [vp, C.c_int]),
     "Nfft4GPAmdSetFgmresOrtho": (None, [C.c_int]),
+    "Nfft4GPAmdFgmresSecondPasses": (C.c_longlong, []),
     "Nfft4GPAmdDistGradMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),
     "Nfft4GPAmdDistGaussianKernel": (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, C.c_int, vp,
                                               vp]),
@@ -180,6 +181,9 @@ _SIGS = {
     "Nfft4GPAmdNysShard": (vp, [vp, C.c_int, C.c_int, vp]),
     "Nfft4GPAmdNysShardSetupAdditive": (vp, [vp, vp, C.c_int, C.c_int]),
     "Nfft4GPAmdAfnShard": (vp, [vp, C.c_int, C.c_int, vp]),
+    "Nfft4GPAmdAfnShardSetup": (vp, [dp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.c_int, C.c_int, C.c_int,
+                                    vp, C.c_int, C.c_int, vp]),
+    "Nfft4GPAmdAfnShardInfo": (C.c_int, [vp, ip, ip, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
     "Nfft4GPAmdAfnSetStorage": (C.c_int, [vp, C.c_int]),
     "Nfft4GPAmdPrecondAFNSetStorage": (C.c_int, [vp, C.c_int]),
     "Nfft4GPAmdDistAfnSolve": (C.c_int, [vp, C.c_int, vp, vp]),

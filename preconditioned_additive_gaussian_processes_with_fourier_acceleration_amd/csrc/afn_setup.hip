@@ -914,6 +914,194 @@ void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm
 }
 }  // namespace
 
+namespace {
+// the sharded AFN setup (Nfft4GPAmdAfnShardSetup): afn.c:161-489 with the column work split by rows
+void* afn_shard_setup_impl(const double* data, int n, int ldim, int d, int k, int perm_opt, const int* perm,
+                           int schur_opt, int schur_lfil, int kernel, void* fkernel_params, int rb, int re, Comm* comm)
+{
+   if (!data || !fkernel_params || !comm || n <= 0 || ldim < n || d <= 0 || k <= 0 || k >= n || perm_opt < 0 ||
+       perm_opt > 2 || (perm_opt == 2 && !perm) || (schur_opt != 0 && schur_opt != 3) || rb < 0 || re > n || rb > re) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup needs data (ldim >= n), kernel parameters, a communicator, "
+                      "0 < k < n, perm_opt 0 / 1 / 2 (perm given), schur_opt 0 or 3 and rows within [0, n)\n");
+      return nullptr;
+   }
+   KernelSpec K;
+   double* dXk = nullptr;
+   const int additive = kernel_spec_of(fkernel_params, nullptr, kernel, n, K, &dXk);
+   if (additive < 0) return nullptr;
+   const int D = additive ? (K.nw - 1) * K.dw + K.last_dw : d;
+   hipStream_t s = current_stream();
+   const int n2 = n - k;
+   const size_t kk = (size_t)k * k;
+   double *dX = nullptr, *Xp = nullptr, *Xkp = nullptr, *K11 = nullptr, *G = nullptr, *Gt = nullptr, *K12 = nullptr;
+   double *X2 = nullptr, *Xc = nullptr, *Ku = nullptr, *Wu = nullptr, *daa = nullptr;
+   int *dperm = nullptr, *dinfo = nullptr, *didx = nullptr, *dia = nullptr, *dja = nullptr, *dwcol = nullptr;
+   auto release = [&]() {
+      (void)hipStreamSynchronize(s);
+      for (void* p : {(void*)dX, (void*)Xp, (void*)Xkp, (void*)dXk, (void*)K11, (void*)X2, (void*)Xc, (void*)Ku,
+                      (void*)Wu, (void*)daa, (void*)dperm, (void*)dinfo, (void*)didx, (void*)dia, (void*)dja,
+                      (void*)dwcol})
+         (void)hipFree(p);
+   };
+   auto fail = [&](const char* what) -> void* {
+      if (what) fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup: %s failed\n", what);
+      release();
+      for (void* p : {(void*)G, (void*)Gt, (void*)K12}) (void)hipFree(p);
+      return nullptr;
+   };
+   if (dalloc(&dX, (size_t)ldim * d)) return fail("allocation");
+   const hipMemcpyKind kind = is_device_ptr(data) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+   if (hipMemcpy(dX, data, sizeof(double) * (size_t)ldim * d, kind) != hipSuccess) return fail("upload");
+   // the ordering is computed by every rank alike (afn.c:196-256): FPS is deterministic, a given perm is shared
+   std::vector<int> hperm(n);
+   for (int i = 0; i < n; i++) hperm[i] = i;
+   if (perm_opt == 1) {
+      std::vector<int> sel(k);
+      const int cnt = fps_device(dX, ldim, n, d, k, 0.0, sel.data(), nullptr, s);
+      if (cnt < 0) return fail("FPS");
+      hperm = expand_perm(sel.data(), cnt, n);
+   } else if (perm_opt == 2) {
+      hperm.assign(perm, perm + n);
+   }
+   if (dalloc(&dperm, n) || hipMemcpy(dperm, hperm.data(), sizeof(int) * n, hipMemcpyHostToDevice) != hipSuccess ||
+       dalloc(&Xp, (size_t)n * d))
+      return fail("allocation");
+   hipLaunchKernelGGL(k_gather_points, dim3((n + 255) / 256, d), dim3(256), 0, s, dX, (long long)ldim, n, d, dperm, Xp);
+   if (additive) {
+      if (dalloc(&Xkp, (size_t)n * D)) return fail("allocation");
+      hipLaunchKernelGGL(k_gather_points, dim3((n + 255) / 256, D), dim3(256), 0, s, dXk, (long long)n, n, D, dperm,
+                         Xkp);
+   }
+   const double* Xk = additive ? Xkp : Xp;  // kernel coordinates in the permuted order, ld n
+   KernelSpec Kp = K;
+   Kp.Xk = additive ? Xkp : nullptr;
+   Kp.ldk = n;
+   const KernelParams P = kernel_params_of(Kp, d);
+   // A11 = K(X1) + noise, L11^{-1}: replicated; every rank keeps rank 0's factors (afn.c:425-428)
+   if (dalloc(&K11, kk) || dalloc(&G, kk) || dalloc(&Gt, kk) || dalloc(&dinfo, 1)) return fail("allocation");
+   hipLaunchKernelGGL(k_kmat, dim3((k + 255) / 256, k), dim3(256), 0, s, Xk, (long long)n, 0, k, 0, P, 1, K11,
+                      (long long)k);
+   const int info = chol_inverse_dev(K11, k, 0.0, G, Gt, dinfo, s);
+   if (info > 0) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup: K11 is not positive definite (column %d)\n", info);
+      return fail(nullptr);
+   }
+   if (info < 0) return fail("Cholesky / triangular inverse of K11");
+   if (comm->rank != 0 &&
+       (hipMemsetAsync(G, 0, sizeof(double) * kk, s) != hipSuccess || hipMemsetAsync(Gt, 0, sizeof(double) * kk, s) != hipSuccess))
+      return fail("broadcast");
+   if (comm->allreduce(G, kk, s) || comm->allreduce(Gt, kk, s)) return fail("broadcast of L11^{-1}");
+   // this rank's landmarks and Schur points (the rows it holds, in the permuted order)
+   std::vector<int> lm_idx, lm_row, nl_pos, nl_row;
+   for (int p = 0; p < n; p++) {
+      const int row = hperm[p];
+      if (row < rb || row >= re) continue;
+      if (p < k) {
+         lm_idx.push_back(p);
+         lm_row.push_back(row - rb);
+      } else {
+         nl_pos.push_back(p - k);
+         nl_row.push_back(row - rb);
+      }
+   }
+   const int m2 = (int)nl_pos.size();
+   // kernel coordinates of [X1; the listed X2 points] (ld k + m), then K(X1, those points): k x m
+   auto panel = [&](const std::vector<int>& pos, double* out) -> int {
+      const int m = (int)pos.size();
+      std::vector<int> idx(k + m);
+      for (int a = 0; a < k; a++) idx[a] = a;
+      for (int j = 0; j < m; j++) idx[k + j] = k + pos[j];
+      (void)hipFree(Xc);
+      (void)hipFree(didx);
+      Xc = nullptr;
+      didx = nullptr;
+      if (dalloc(&Xc, (size_t)(k + m) * D) || dalloc(&didx, idx.size()) ||
+          hipMemcpy(didx, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice) != hipSuccess)
+         return -1;
+      hipLaunchKernelGGL(k_gather_points, dim3((k + m + 255) / 256, D), dim3(256), 0, s, Xk, (long long)n, k + m, D,
+                         (const int*)didx, Xc);
+      for (int j0 = 0; j0 < m; j0 += 65535) {
+         const int nb = std::min(65535, m - j0);
+         hipLaunchKernelGGL(k_kmat, dim3((k + 255) / 256, nb), dim3(256), 0, s, (const double*)Xc, (long long)(k + m), 0,
+                            k, k + j0, P, 0, out + (size_t)j0 * k, (long long)k);
+      }
+      return hipGetLastError() == hipSuccess ? 0 : -1;
+   };
+   // K12 at this rank's Schur points only (afn.c:436): k x m2 instead of k x (n - k)
+   if (dalloc(&K12, (size_t)k * std::max(1, m2)) || (m2 > 0 && panel(nl_pos, K12))) return fail("K12 panel");
+   std::vector<int> gia, gja;
+   std::vector<double> gaa;
+   if (schur_opt == 3) {
+      // FSAI of the Schur complement (afn.c:445-473) at this rank's rows: the KNN over their earlier points,
+      // then the values in chunks of rows, each with W = L11^{-1} K12 formed for the columns it touches only
+      if (dalloc(&X2, (size_t)n2 * d)) return fail("allocation");
+      for (int c = 0; c < d; c++)
+         if (hipMemcpyAsync(X2 + (size_t)c * n2, Xp + (size_t)c * n + k, sizeof(double) * n2, hipMemcpyDeviceToDevice,
+                            s) != hipSuccess)
+            return fail("copy");
+      if (fsai_pattern_rows(X2, n2, n2, d, schur_lfil, nl_pos, gia, gja, s)) return fail("Schur FSAI pattern");
+      const size_t nnz = gja.size();
+      gaa.assign(nnz, 0.0);
+      if (nnz > 0) {
+         if (dalloc(&dia, gia.size()) || dalloc(&dja, nnz) || dalloc(&daa, nnz) || dalloc(&dwcol, nnz) ||
+             hipMemcpy(dia, gia.data(), sizeof(int) * gia.size(), hipMemcpyHostToDevice) != hipSuccess ||
+             hipMemcpy(dja, gja.data(), sizeof(int) * nnz, hipMemcpyHostToDevice) != hipSuccess)
+            return fail("allocation");
+         KernelSpec K2 = Kp;
+         K2.Xk = additive ? Xkp + k : nullptr;  // column c of the Schur points: Xkp + c n + k + i
+         constexpr int kMaxCols = 65536;        // W columns per chunk (k x 64 Ki doubles: 256 MB at k = 512)
+         std::vector<int> U, wcol;
+         std::vector<int> mark(n2, -1);
+         int r0 = 0;
+         while (r0 < m2) {
+            // the chunk: rows while the union of their columns stays below kMaxCols
+            U.clear();
+            int r1 = r0;
+            while (r1 < m2) {
+               int add = 0;
+               for (int e = gia[r1]; e < gia[r1 + 1]; e++) add += mark[gja[e]] < 0 ? 1 : 0;
+               if (r1 > r0 && (int)U.size() + add > kMaxCols) break;
+               for (int e = gia[r1]; e < gia[r1 + 1]; e++)
+                  if (mark[gja[e]] < 0) {
+                     mark[gja[e]] = (int)U.size();
+                     U.push_back(gja[e]);
+                  }
+               r1++;
+            }
+            wcol.resize(gia[r1] - gia[r0]);
+            for (int e = gia[r0]; e < gia[r1]; e++) wcol[e - gia[r0]] = mark[gja[e]];
+            for (int j : U) mark[j] = -1;
+            const size_t ku = (size_t)k * U.size();
+            (void)hipFree(Ku);
+            (void)hipFree(Wu);
+            Ku = Wu = nullptr;
+            if (dalloc(&Ku, ku) || dalloc(&Wu, ku) ||
+                hipMemcpy(dwcol + gia[r0], wcol.data(), sizeof(int) * wcol.size(), hipMemcpyHostToDevice) != hipSuccess ||
+                panel(U, Ku) || gemm_f64(false, k, (int)U.size(), k, G, k, Ku, k, Wu, k, s) ||
+                fsai_values_rows(K2, X2, n2, d, schur_lfil, dia + r0, dja, r1 - r0, Wu, k, dwcol, daa, s))
+               return fail("Schur FSAI values");
+            r0 = r1;
+         }
+         if (hipMemcpyAsync(gaa.data(), daa, sizeof(double) * nnz, hipMemcpyDeviceToHost, s) != hipSuccess ||
+             hipStreamSynchronize(s) != hipSuccess)
+            return fail("copy");
+         if (!std::all_of(gaa.begin(), gaa.end(), [](double v) { return std::isfinite(v); })) {
+            fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup: the Schur complement's FSAI broke down (non-positive "
+                            "pivot)\n");
+            return fail(nullptr);
+         }
+      }
+   } else {
+      gia.assign(m2 + 1, 0);
+   }
+   release();
+   // the apply object takes G, Gt and K12
+   void* S = afn_shard_from_parts(re - rb, k, n2, comm, lm_idx, lm_row, nl_pos, nl_row, G, Gt, K12, schur_opt == 3,
+                                  schur_opt == 0 ? 1.0 / K.mu : 0.0, gia, gja, gaa);
+   return S;
+}
+}  // namespace
+
 extern "C" {
 
 void* Nfft4GPAmdAfnSetupSchur(const double* data, int n, int ldim, int d, int k, int perm_opt, const int* perm,
@@ -925,6 +1113,16 @@ void* Nfft4GPAmdAfnSetupSchur(const double* data, int n, int ldim, int d, int k,
                          &breakdown);
 }
 
+
+// afn.c:161-489 split over row shards (the AFN apply of Nfft4GPAmdAfnShard, set up without a full AFN on any rank)
+void* Nfft4GPAmdAfnShardSetup(const double* data, int n, int ldim, int d, int k, int perm_opt, const int* perm,
+                              int schur_opt, int schur_lfil, int kernel, void* fkernel_params, int row_begin,
+                              int row_end, void* comm)
+{
+   if (!need_device("Nfft4GPAmdAfnShardSetup")) return nullptr;
+   return afn_shard_setup_impl(data, n, ldim, d, k, perm_opt, perm, schur_opt, schur_lfil, kernel, fkernel_params,
+                               row_begin, row_end, (Comm*)comm);
+}
 
 int Nfft4GPAmdRankestNysScaled(const double* data, int n, int ldim, int d, int kernel, void* fkernel_params,
                                int max_rank, int nsample, int nsample_r)

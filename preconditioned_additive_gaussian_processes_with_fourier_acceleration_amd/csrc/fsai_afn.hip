@@ -359,6 +359,14 @@ struct AfnShard {
    int *nl_pos = nullptr, *nl_row = nullptr;  // m2: Schur position p in [0, n2), local row
    double *Linv = nullptr, *LinvT = nullptr, *K12 = nullptr;  // k x k, k x k, k x m2
    FsaiDev G, GT;  // rows of G / G^T at this rank's Schur points (ia, ja, aa, part; ja global)
+   // a shard set up by its own rank (afn_shard_from_parts): G's own rows only, so G^T w is formed as this rank's
+   // partial sums over its rows -- GTp, one CSR row per Schur column its rows touch (tcols), entries in
+   // ascending row order, x = this rank's w -- scattered into the Schur vector and summed over the ranks
+   bool gt_scatter = false;
+   long long g_nnz = 0;  // entries of G's rows this rank holds
+   FsaiDev GTp;
+   int* tcols = nullptr;
+   double* tbuf = nullptr;
    bool fsai = false;
    double schur_scale = 0.0;
    double *rp1 = nullptr, *y1 = nullptr, *t = nullptr, *w = nullptr;  // k
@@ -442,6 +450,9 @@ void afn_shard_free(AfnShard* S)
       (void)hipFree(p);
    csr_free_parts(S->G);
    csr_free_parts(S->GT);
+   csr_free_parts(S->GTp);
+   (void)hipFree(S->tcols);
+   (void)hipFree(S->tbuf);
    delete S;
 }
 
@@ -512,6 +523,7 @@ AfnShard* afn_shard_create(const AfnDev* A, int rb, int re, Comm* comm)
       ok = ok && !dl(ja, F->ja, (size_t)ia[n2]) && !dl(aa, F->aa, (size_t)ia[n2]) && !dl(tja, F->tja, (size_t)tia[n2]) &&
            !dl(taa, F->taa, (size_t)tia[n2]);
       ok = ok && !csr_rows_upload(ia, ja, aa, nl_pos, S->G) && !csr_rows_upload(tia, tja, taa, nl_pos, S->GT);
+      for (int p : nl_pos) S->g_nnz += ia[p + 1] - ia[p];
    }
    if (!ok || hipStreamSynchronize(s) != hipSuccess) {
       fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShard: allocation or copy failed\n");
@@ -551,11 +563,25 @@ int afn_shard_apply(AfnShard* S, double* x, const double* r, hipStream_t s)
          hipLaunchKernelGGL(k_csr_staged, dim3(S->G.nparts), dim3(kCsrT), 0, s, S->G.ia, S->G.ja, S->G.aa, S->gbuf,
                             S->v, S->G.part);
       NFFT4GP_HIP_CHECK(hipMemsetAsync(S->gbuf, 0, sizeof(double) * S->n2, s));
-      hipLaunchKernelGGL(k_put, dim3(g2), dim3(256), 0, s, S->v, (const int*)S->nl_pos, m2, S->gbuf);
-      if (S->comm->allreduce(S->gbuf, (size_t)S->n2, s)) return -1;
-      if (m2 > 0)
-         hipLaunchKernelGGL(k_csr_staged, dim3(S->GT.nparts), dim3(kCsrT), 0, s, S->GT.ia, S->GT.ja, S->GT.aa,
-                            S->gbuf, S->y2, S->GT.part);
+      if (S->gt_scatter) {
+         // (G^T v)_j = sum over every rank's rows i of G_ij v_i: this rank's partial sums at the columns its rows
+         // touch, scattered into the Schur vector, summed over the ranks, own entries taken
+         const int nt = S->GTp.n;
+         if (nt > 0) {
+            hipLaunchKernelGGL(k_csr_staged, dim3(S->GTp.nparts), dim3(kCsrT), 0, s, S->GTp.ia, S->GTp.ja, S->GTp.aa,
+                               S->v, S->tbuf, S->GTp.part);
+            hipLaunchKernelGGL(k_put, dim3((nt + 255) / 256 + 1), dim3(256), 0, s, S->tbuf, (const int*)S->tcols, nt,
+                               S->gbuf);
+         }
+         if (S->comm->allreduce(S->gbuf, (size_t)S->n2, s)) return -1;
+         if (m2 > 0) hipLaunchKernelGGL(k_take, dim3(g2), dim3(256), 0, s, S->gbuf, (const int*)S->nl_pos, m2, S->y2);
+      } else {
+         hipLaunchKernelGGL(k_put, dim3(g2), dim3(256), 0, s, S->v, (const int*)S->nl_pos, m2, S->gbuf);
+         if (S->comm->allreduce(S->gbuf, (size_t)S->n2, s)) return -1;
+         if (m2 > 0)
+            hipLaunchKernelGGL(k_csr_staged, dim3(S->GT.nparts), dim3(kCsrT), 0, s, S->GT.ia, S->GT.ja, S->GT.aa,
+                               S->gbuf, S->y2, S->GT.part);
+      }
    } else if (m2 > 0) {
       hipLaunchKernelGGL(k_scale_into, dim3(g2), dim3(256), 0, s, S->rp2, m2, S->schur_scale, S->y2);
    }
@@ -578,6 +604,76 @@ int afn_shard_apply(AfnShard* S, double* x, const double* r, hipStream_t s)
 }
 
 }  // namespace
+
+// A row shard of the AFN apply from the pieces one rank's sharded setup computed (afn_setup.hip,
+// Nfft4GPAmdAfnShardSetup): its landmarks (lm_idx: index in perm[:k], lm_row: local row), its Schur points
+// (nl_pos: Schur position, ascending; nl_row: local row), the replicated L11^{-1} and its transpose, K12's
+// columns at its Schur points (k x m2), and G's rows at its Schur points as host CSR (gia over the m2 rows,
+// gja global Schur positions).  Takes ownership of d_Linv, d_LinvT and d_K12.
+void* afn_shard_from_parts(int n_local, int k, int n2, Comm* comm, const std::vector<int>& lm_idx,
+                           const std::vector<int>& lm_row, const std::vector<int>& nl_pos,
+                           const std::vector<int>& nl_row, double* d_Linv, double* d_LinvT, double* d_K12, bool fsai,
+                           double schur_scale, const std::vector<int>& gia, const std::vector<int>& gja,
+                           const std::vector<double>& gaa)
+{
+   AfnShard* S = new AfnShard();
+   S->n = n_local;
+   S->k = k;
+   S->n2 = n2;
+   S->comm = comm;
+   S->fsai = fsai;
+   S->schur_scale = schur_scale;
+   S->m1 = (int)lm_idx.size();
+   S->m2 = (int)nl_pos.size();
+   S->Linv = d_Linv;
+   S->LinvT = d_LinvT;
+   S->K12 = d_K12;
+   a12_shape(std::max(1, S->m2), S->cols, S->nblk);
+   bool ok = !up(&S->lm_idx, lm_idx.data(), lm_idx.size()) && !up(&S->lm_row, lm_row.data(), lm_row.size()) &&
+             !up(&S->nl_pos, nl_pos.data(), nl_pos.size()) && !up(&S->nl_row, nl_row.data(), nl_row.size());
+   for (double** p : {&S->rp1, &S->y1, &S->t, &S->w})
+      ok = ok && hipMalloc((void**)p, sizeof(double) * k) == hipSuccess;
+   for (double** p : {&S->rp2, &S->y2, &S->v})
+      ok = ok && hipMalloc((void**)p, sizeof(double) * std::max(1, S->m2)) == hipSuccess;
+   ok = ok && hipMalloc((void**)&S->gbuf, sizeof(double) * n2) == hipSuccess &&
+        hipMalloc((void**)&S->part, sizeof(double) * (size_t)S->nblk * k) == hipSuccess;
+   if (ok && fsai) {
+      std::vector<int> rows(S->m2);
+      for (int i = 0; i < S->m2; i++) rows[i] = i;
+      ok = !csr_rows_upload(gia, gja, gaa, rows, S->G);
+      S->g_nnz = (long long)gja.size();
+      // the transpose of the own rows, grouped by column: counting sort over the columns touched, rows ascending
+      std::vector<int> cnt(n2 + 1, 0);
+      for (int j : gja) cnt[j + 1]++;
+      std::vector<int> tcols, tia(1, 0);
+      std::vector<int> where(n2, -1);
+      for (int c = 0; c < n2; c++)
+         if (cnt[c + 1]) {
+            where[c] = (int)tcols.size();
+            tcols.push_back(c);
+            tia.push_back(tia.back() + cnt[c + 1]);
+         }
+      std::vector<int> tja(gja.size()), fill(tia.begin(), tia.end() - 1);
+      std::vector<double> taa(gja.size());
+      for (int i = 0; i < S->m2; i++)
+         for (int e = gia[i]; e < gia[i + 1]; e++) {
+            const int slot = fill[where[gja[e]]]++;
+            tja[slot] = i;
+            taa[slot] = gaa[e];
+         }
+      std::vector<int> trows(tcols.size());
+      for (size_t t = 0; t < tcols.size(); t++) trows[t] = (int)t;
+      ok = ok && !csr_rows_upload(tia, tja, taa, trows, S->GTp) && !up(&S->tcols, tcols.data(), tcols.size()) &&
+           hipMalloc((void**)&S->tbuf, sizeof(double) * std::max<size_t>(1, tcols.size())) == hipSuccess;
+      S->gt_scatter = true;
+   }
+   if (!ok || hipStreamSynchronize(current_stream()) != hipSuccess) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup: allocation or copy failed\n");
+      afn_shard_free(S);
+      return nullptr;
+   }
+   return S;
+}
 
 // an AFN apply object from factors already in HBM (afn_setup.hip); takes ownership of d_perm, d_Linv,
 // d_K12 (hipMalloc'ed) and of the Schur FSAI handle S (an Nfft4GPAmdFsaiCreate handle of size n - k)
@@ -745,6 +841,17 @@ int Nfft4GPAmdDistAfnSolve(void* dafn, int n, double* x, double* rhs)
 }
 
 void Nfft4GPAmdDistAfnFree(void* dafn) { afn_shard_free((AfnShard*)dafn); }
+
+int Nfft4GPAmdAfnShardInfo(void* dafn, int* m1, int* m2, long long* k12_doubles, long long* g_nnz)
+{
+   const AfnShard* S = (const AfnShard*)dafn;
+   if (!S) return -1;
+   if (m1) *m1 = S->m1;
+   if (m2) *m2 = S->m2;
+   if (k12_doubles) *k12_doubles = (long long)S->k * S->m2;
+   if (g_nnz) *g_nnz = S->g_nnz;
+   return 0;
+}
 
 int Nfft4GPAmdAfnInfo(void* afn, int* k, int* perm, int* ia, int* ja, double* aa)
 {

@@ -478,6 +478,7 @@ struct ScrShared {
    int idx[kScrRows][kScrCap];
    float thr[kScrRows];  // -T_r / 2 of the current scan (rows beyond nr: +inf, never pass)
    int base[kScrRows], cnt[kScrRows];
+   int row[kScrRows];    // the rows' indices (a row counts only points before it)
 };
 
 // One scan of points j in [j0, j1) against the workgroup's R = 32 rows on v_mfma_f32_32x32x2_f32: each
@@ -486,7 +487,7 @@ struct ScrShared {
 // step), and the 32 x 32 accumulator starts at -(|x_j|^2 + |q_r|^2) / 2 (lane l: point l & 31, rows
 // (v & 3) + 8 (v >> 2) + 4 (l >> 5) of its 16 values).  MODE 0: exponent histogram of every key~; 1 / 2:
 // keys below the row's threshold binned 16 per octave from base; 3: append keys <= the threshold to the
-// row's candidates.  CHECK: only points before the row (j < i0 + r) count.  STEPS = ceil(d / 2) bound.
+// row's candidates.  CHECK: only points before the row (j < S.row[r]) count.  STEPS = ceil(d / 2) bound.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 template <int MODE, bool CHECK, int STEPS>
 __device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restrict__ Xf,
@@ -501,11 +502,13 @@ __device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restr
 #pragma unroll
    for (int st = 0; st < STEPS; st++) a[st] = S.q[2 * st + h][rt + col];  // zero beyond d
    float nqh[16], thr[16];
+   int rlim[16];
 #pragma unroll
    for (int v = 0; v < 16; v++) {
       const int r = rt + (v & 3) + 8 * (v >> 2) + 4 * h;
       nqh[v] = S.nqh[r];
       thr[v] = S.thr[r];
+      rlim[v] = CHECK ? S.row[r] : 0;
    }
    // the loads run two tiles ahead of the MFMAs (software pipelining over the memory latency)
    float b0[STEPS], b1[STEPS], a00 = 0.f, a01 = 0.f;
@@ -551,7 +554,7 @@ __device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restr
       for (int v = 0; v < 16; v++) {
          const int r = rt + (v & 3) + 8 * (v >> 2) + 4 * h;
          const bool pass = MODE == 3 ? c[v] >= thr[v] : c[v] > thr[v];
-         if (!pass || (CHECK && j >= i0 + r)) continue;
+         if (!pass || (CHECK && j >= rlim[v])) continue;
          if (MODE == 3) {
             const int slot = atomicAdd(&S.cnt[r], 1);
             if (slot < kScrCap) S.idx[r][slot] = j;
@@ -572,13 +575,16 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
                                                                float margin2, float* __restrict__ lim,
                                                                const int* __restrict__ ia,
                                                                int* __restrict__ ja, int* __restrict__ fail,
-                                                               int* __restrict__ nfail)
+                                                               int* __restrict__ nfail, const int* __restrict__ rows,
+                                                               int nrows_list)
 {
    constexpr int R = kScrRows, CAP = kScrCap, W = kScrThreads / 64;
    __shared__ ScrShared S;
    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
    const int K = lfil - 1;
-   const int ngroups = (n - lfil + R - 1) / R;
+   // rows (ascending, all >= lfil; nrows_list of them) instead of lfil .. n-1: a row shard's own rows
+   const int nall = rows ? nrows_list : n - lfil;
+   const int ngroups = (nall + R - 1) / R;
    const float inf = __int_as_float(0x7f800000);
    // the first bin where the cumulative count of h[r] reaches K (one wave per row; every lane returns it),
    // -1 when the histogram holds fewer than K keys (the scans' roundings may differ; such a row goes to k_knn)
@@ -616,20 +622,26 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
       for (int e = tid; e < R * 256; e += kScrThreads) S.u.h[e / 256][e % 256] = 0u;
    };
    for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
-      const int i0 = lfil + g * R;
-      const int nr = min(R, n - i0);
+      const int lp0 = g * R;  // list position of the group's first row
+      const int nr = min(R, nall - lp0);
+      const int i0 = rows ? rows[lp0] : lfil + lp0;
+      const int ilast = rows ? rows[lp0 + nr - 1] : i0 + nr - 1;
+      auto row_of = [&](int r) { return rows ? rows[lp0 + r] : i0 + r; };
       for (int e = tid; e < R * 2 * STEPS; e += kScrThreads) {
          const int r = e % R, c = e / R;
-         S.q[c][r] = (r < nr) ? Xf[(size_t)c * n + i0 + r] : 0.f;
+         S.q[c][r] = (r < nr) ? Xf[(size_t)c * n + row_of(r)] : 0.f;
       }
       clear_h();
-      if (tid < R) S.nqh[tid] = (tid < nr) ? -0.5f * nx[i0 + tid] : 0.f;
+      if (tid < R) {
+         S.row[tid] = tid < nr ? row_of(tid) : 0;
+         S.nqh[tid] = (tid < nr) ? -0.5f * nx[row_of(tid)] : 0.f;
+      }
       if (tid < R) {
          S.cnt[tid] = 0;
          if (PHASE == 0) {
             S.thr[tid] = (tid < nr) ? -inf : inf;
          } else {
-            const float L = (tid < nr) ? lim[i0 - lfil + tid] : inf;
+            const float L = (tid < nr) ? lim[lp0 + tid] : inf;
             S.thr[tid] = (L != L || tid >= nr) ? inf : -0.5f * L;
             if (tid < nr && L != L) S.cnt[tid] = CAP + 1;
          }
@@ -666,24 +678,24 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
       __syncthreads();
       // count over every earlier point: [0, i0) before all rows, [i0, i0 + nr - 1) before some
       knn_scan_mfma<2, false, STEPS>(S, Xf, nx, n, d, i0, 0, i0);
-      knn_scan_mfma<2, true, STEPS>(S, Xf, nx, n, d, i0, i0, i0 + nr - 1);
+      knn_scan_mfma<2, true, STEPS>(S, Xf, nx, n, d, i0, i0, ilast);
       __syncthreads();
       for (int r = wave; r < nr; r += W) {
          const int b = kth_bin(r);
          if (lane == 0) {
             const bool gave_up = S.thr[r] == inf;
-            lim[i0 - lfil + r] = (gave_up || b < 0) ? __int_as_float(0x7fc00000)
-                                                    : (bin_top(S.base[r], b) + margin2) * 1.000001f;
+            lim[lp0 + r] = (gave_up || b < 0) ? __int_as_float(0x7fc00000)
+                                              : (bin_top(S.base[r], b) + margin2) * 1.000001f;
          }
       }
       __syncthreads();
       } else {
       knn_scan_mfma<3, false, STEPS>(S, Xf, nx, n, d, i0, 0, i0);
-      knn_scan_mfma<3, true, STEPS>(S, Xf, nx, n, d, i0, i0, i0 + nr - 1);
+      knn_scan_mfma<3, true, STEPS>(S, Xf, nx, n, d, i0, i0, ilast);
       __syncthreads();
       // exact keys of the candidates (the histogram space is free now)
       for (int r = wave; r < nr; r += W) {
-         const int i = i0 + r, cnt = S.cnt[r];
+         const int i = S.row[r], cnt = S.cnt[r];
          if (cnt > CAP || cnt < K) continue;
          for (int e = lane; e < cnt; e += 64) {
             const int j = S.idx[r][e];
@@ -697,7 +709,7 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
       }
       __syncthreads();
       for (int r = wave; r < nr; r += W) {
-         const int i = i0 + r, cnt = S.cnt[r];
+         const int i = S.row[r], cnt = S.cnt[r];
          if (cnt > CAP || cnt < K) {
             if (lane == 0) fail[atomicAdd(nfail, 1)] = i;
             continue;
@@ -727,18 +739,18 @@ int upload(T** d, const T* h, size_t count);
 // 0 the fp64 k_knn_bounded, 2 the radix-select k_knn for every row; the rows the bounded variants leave go
 // to k_knn.  Returns the number of such rows, or -1.
 int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* dia, int* dja, hipStream_t s,
-                int variant)
+                int variant, const int* d_rows = nullptr, int nrows_list = 0)
 {
-   if (n <= lfil) return 0;
+   if (n <= lfil || (d_rows && nrows_list <= 0)) return 0;
    if (variant < 0) {
       const char* e = getenv("NFFT4GP_AMD_KNN");
       variant = e ? atoi(e) : 1;
    }
    if (d > kKnnMaxDims2) variant = 2;
-   const int nrows = n - lfil;
+   const int nrows = d_rows ? nrows_list : n - lfil;
    if (variant == 2) {
       hipLaunchKernelGGL(k_knn, dim3(std::min(nrows, 4096)), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia, dja,
-                         nullptr, 0);
+                         d_rows, d_rows ? nrows : 0);
       return hipGetLastError() == hipSuccess ? nrows : -1;
    }
    int* dfail = nullptr;
@@ -787,7 +799,7 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
                                                       : k_knn_screen<32, 1>);
             hipLaunchKernelGGL(screen, dim3(std::min(ngroups, 4096)), dim3(kScrThreads), 0, s, dX, ldim,
                                (const float*)Xf, (const float*)nx, n, d, lfil, (float)(2.0 * margin) * 1.0001f, lim,
-                               dia, dja, dfail, dfail + nrows);
+                               dia, dja, dfail, dfail + nrows, d_rows, nrows);
          }
          (void)hipStreamSynchronize(s);
          (void)hipFree(lim);
@@ -796,11 +808,11 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
       const int ngroups = (nrows + kKnnRows - 1) / kKnnRows;
       // 2 points per thread: 5.6 -> 4.0 s for the n = 1e6, d = 32, lfil = 20 setup; 4 drop to 1 wave per SIMD
       hipLaunchKernelGGL(k_knn_bounded<kKnnPoints>, dim3(std::min(ngroups, 8192)), dim3(kKnnThreads), 0, s, dX, ldim,
-                         n, d, lfil, dia, dja, dfail, dfail + nrows, nullptr, 0);
+                         n, d, lfil, dia, dja, dfail, dfail + nrows, d_rows, d_rows ? nrows : 0);
    }
    if (variant == 2) {
       hipLaunchKernelGGL(k_knn, dim3(std::min(nrows, 4096)), dim3(kKnnThreads), 0, s, dX, ldim, n, d, lfil, dia, dja,
-                         nullptr, 0);
+                         d_rows, d_rows ? nrows : 0);
       return done(hipGetLastError() == hipSuccess ? nrows : -1);
    }
    if (hipGetLastError() != hipSuccess ||
@@ -880,17 +892,22 @@ __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, 
                                                   const int* __restrict__ ia, const int* __restrict__ ja,
                                                   KernelParams P, const double* __restrict__ W, int kw, int grad,
                                                   int nnz, double* __restrict__ aa, double* __restrict__ da,
-                                                  const double* __restrict__ GB, const double* __restrict__ GC)
+                                                  const double* __restrict__ GB, const double* __restrict__ GC,
+                                                  const int* __restrict__ wcol)
 {
    __shared__ double A[KM][KM + 1];
    __shared__ double Ws[KM][kSchurChunk + 1];
    __shared__ double a[KM], u[KM];
-   __shared__ int idx[KM];
+   __shared__ int idx[KM], widx[KM];
    const int i = blockIdx.x;
    const int lane = threadIdx.x;
    const int j1 = ia[i];
    const int k = ia[i + 1] - j1;
-   if (lane < k) idx[lane] = ja[j1 + lane];
+   if (lane < k) {
+      idx[lane] = ja[j1 + lane];
+      // W's column of the entry: the point itself, or (a row shard's chunk of W) its position in the chunk
+      widx[lane] = wcol ? wcol[j1 + lane] : idx[lane];
+   }
    __syncthreads();
    // K_a (lower triangle is all the factorisation reads)
    for (int e = lane; e < k * k; e += 64) {
@@ -906,7 +923,7 @@ __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, 
          const int tc = min(kSchurChunk, kw - t0);
          for (int e = lane; e < k * tc; e += 64) {
             const int r = e / tc, tt = e % tc;
-            Ws[r][tt] = W[(size_t)idx[r] * kw + t0 + tt];
+            Ws[r][tt] = W[(size_t)widx[r] * kw + t0 + tt];
          }
          __syncthreads();
          for (int e = lane; e < k * k; e += 64) {
@@ -966,7 +983,7 @@ __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, 
             if (lane < tc) {
                double wa = 0.0, ba = 0.0, ca = 0.0;
                for (int c = 0; c < k; c++) {
-                  const size_t o = (size_t)idx[c] * kw + t0 + lane;
+                  const size_t o = (size_t)widx[c] * kw + t0 + lane;
                   wa = fma(W[o], a[c], wa);
                   if (Bg) ba = fma(Bg[o], a[c], ba);
                   ca = fma(Cg[o], a[c], ca);
@@ -976,7 +993,7 @@ __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, 
             }
             __syncthreads();
             if (lane < k) {
-               const size_t o = (size_t)idx[lane] * kw + t0;
+               const size_t o = (size_t)widx[lane] * kw + t0;
                for (int tt = 0; tt < tc; tt++) {
                   acc = fma(W[o + tt], Ws[1][tt], acc);
                   if (Bg) acc = fma(Bg[o + tt], Ws[0][tt], acc);
@@ -1317,7 +1334,7 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const Ke
    const long long ldk = Ks.Xk ? Ks.ldk : ldim;
    auto rows_kernel = lfil <= 32 ? k_fsai_rows<32> : k_fsai_rows<kFsaiMaxK>;
    hipLaunchKernelGGL(rows_kernel, dim3(n), dim3(64), 0, s, Xk, ldk, dia, dja, P, dW, kw, require_grad ? 1 : 0, nnz,
-                      daa, dda, dGB, dGC);
+                      daa, dda, dGB, dGC, (const int*)nullptr);
    haa.assign((size_t)nnz, 0.0);
    hda.assign(require_grad ? 3 * (size_t)nnz : 0, 0.0);
    if (hipGetLastError() != hipSuccess ||
@@ -1328,6 +1345,60 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const Ke
        hipStreamSynchronize(s) != hipSuccess)
       return cleanup(-1);
    return cleanup(0);
+}
+
+// A row shard's rows of the FSAI pattern (kernels.c:121-278): `rows` (ascending) of the n points; rows below
+// lfil hold every earlier point, the others the lfil - 1 nearest earlier points and themselves (the
+// screened scans over this rank's rows only).  hia: m + 1 pointers over the listed rows, hja: point indices.
+int fsai_pattern_rows(const double* dX, int n, int ldim, int d, int lfil, const std::vector<int>& rows,
+                      std::vector<int>& hia, std::vector<int>& hja, hipStream_t s)
+{
+   if (n <= 0 || ldim < n || d <= 0 || d > kMaxDims || lfil < 1 || lfil > kFsaiMaxK) return -1;
+   const int m = (int)rows.size();
+   hia.assign(m + 1, 0);
+   std::vector<int> iav((size_t)n + 1, 0), knn_rows;
+   for (int r = 0; r < m; r++) {
+      const int i = rows[r];
+      const int len = (n <= lfil || i < lfil) ? i + 1 : lfil;
+      iav[i] = hia[r];
+      hia[r + 1] = hia[r] + len;
+      if (!(n <= lfil || i < lfil)) knn_rows.push_back(i);
+   }
+   hja.assign((size_t)hia[m], 0);
+   for (int r = 0; r < m; r++)
+      if (n <= lfil || rows[r] < lfil)
+         for (int j = 0; j <= rows[r]; j++) hja[hia[r] + j] = j;
+   if (knn_rows.empty()) return 0;
+   int *dia = nullptr, *dja = nullptr, *drows = nullptr;
+   auto cleanup = [&](int rc) {
+      (void)hipStreamSynchronize(s);
+      for (int* p : {dia, dja, drows}) (void)hipFree(p);
+      return rc;
+   };
+   if (upload(&dia, iav.data(), iav.size()) || upload(&dja, hja.data(), hja.size()) ||
+       upload(&drows, knn_rows.data(), knn_rows.size()))
+      return cleanup(-1);
+   const int nf = knn_pattern(dX, n, ldim, d, lfil, dia, dja, s, -1, drows, (int)knn_rows.size());
+   if (nf < 0 || hipMemcpyAsync(hja.data(), dja, sizeof(int) * hja.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess)
+      return cleanup(-1);
+   knn_fallback_rows = nf;
+   return cleanup(0);
+}
+
+// Values of `nrows` pattern rows (device ia over those rows, absolute offsets into ja / aa) of the kernel (or,
+// with W, the Schur-complement kernel): k_fsai_rows, W's column of each entry from wcol (nullptr: the point).
+int fsai_values_rows(const KernelSpec& Ks, const double* dX, long long ldim, int d, int lfil, const int* dia,
+                     const int* dja, int nrows, const double* dW, int kw, const int* dwcol, double* daa, hipStream_t s)
+{
+   if (nrows <= 0) return 0;
+   const KernelParams P = kernel_params_of(Ks, d);
+   const double* Xk = Ks.Xk ? Ks.Xk : dX;
+   const long long ldk = Ks.Xk ? Ks.ldk : ldim;
+   auto rows_kernel = lfil <= 32 ? k_fsai_rows<32> : k_fsai_rows<kFsaiMaxK>;
+   hipLaunchKernelGGL(rows_kernel, dim3(nrows), dim3(64), 0, s, Xk, ldk, dia, dja, P, dW, kw, 0, 0, daa,
+                      (double*)nullptr, (const double*)nullptr, (const double*)nullptr, dwcol);
+   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // ---- the Schur FSAI's operators for the AFN gradients (afn_grad.hip) ----------------------------------

@@ -310,6 +310,18 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const Ke
                     int require_grad, std::vector<int>& ia, std::vector<int>& ja, std::vector<double>& aa,
                     std::vector<double>& da, hipStream_t s, const double* dGB = nullptr,
                     const double* dGC = nullptr);
+// a row shard's rows of the FSAI (fsai_setup.hip): the pattern of the listed rows (ascending) -- KNN over their
+// earlier points only -- and the values of a range of pattern rows, W's column of each entry from dwcol
+int fsai_pattern_rows(const double* dX, int n, int ldim, int d, int lfil, const std::vector<int>& rows,
+                      std::vector<int>& hia, std::vector<int>& hja, hipStream_t s);
+int fsai_values_rows(const KernelSpec& Ks, const double* dX, long long ldim, int d, int lfil, const int* dia,
+                     const int* dja, int nrows, const double* dW, int kw, const int* dwcol, double* daa, hipStream_t s);
+// a row shard of the AFN apply from one rank's sharded setup (fsai_afn.hip; takes d_Linv, d_LinvT, d_K12)
+void* afn_shard_from_parts(int n_local, int k, int n2, Comm* comm, const std::vector<int>& lm_idx,
+                           const std::vector<int>& lm_row, const std::vector<int>& nl_pos,
+                           const std::vector<int>& nl_row, double* d_Linv, double* d_LinvT, double* d_K12, bool fsai,
+                           double schur_scale, const std::vector<int>& gia, const std::vector<int>& gja,
+                           const std::vector<double>& gaa);
 // the Schur FSAI with gradients as operators (fsai_setup.hip): create from host CSR (+ 3 nnz gradients)
 void* fsai_grad_create(int n, const int* ia, const int* ja, const double* aa, const double* da);
 void fsai_grad_free(void* F);

@@ -404,9 +404,10 @@ int tridiag_eig(int m, const double* d, const double* e, std::vector<double>& w,
 namespace nfft4gp_amd {
 
 // FGMRES orthogonalisation: 0 = the reference's modified Gram-Schmidt (Nfft4GPModifiedGS, one launch per
-// basis vector), 1 = two block classical Gram-Schmidt passes (the Lanczos re-orthogonalisation's kernels:
-// four launches per step whatever its length, the basis read four times) -- Nfft4GPAmdSetFgmresOrtho
+// basis vector), 1 = block classical Gram-Schmidt passes (the Lanczos re-orthogonalisation's kernels: two
+// launches per pass whatever its length), a second pass when the DGKS test asks for it -- Nfft4GPAmdSetFgmresOrtho
 int g_fgmres_ortho = -1;
+long long g_fgmres_second_passes = 0;  // DGKS re-orthogonalisations taken (ortho 1), Nfft4GPAmdFgmresStats
 int fgmres_ortho()
 {
    if (g_fgmres_ortho < 0) {
@@ -513,13 +514,20 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
             if (c.gs(w, V + (size_t)(i - 1) * n, hd + i - 1, nullptr, hd + i)) return -1;
             if (c.read(hd, i + 1, hcol.data())) return -1;
          } else {
-            // two classical passes: h = V^T w, w -= V h, twice; H(:, i) = h1 + h2, ||w|| after the second
+            // classical passes h = V^T w, w -= V h; a second one only when the first dropped ||w|| below 0.7071
+            // of its value before it (the DGKS test of the reference's MGS2, matops.c:348-440); H(:, i) = the
+            // sum of the passes' projections, ||w|| after the last
             double* hd2 = hd + i + 2;
-            if (c.block_gs(w, V, V, i, hd) || c.block_gs(w, V, V, i, hd2)) return -1;
             std::vector<double> hh(2 * i + 3);
-            if (c.read(hd, 2 * i + 3, hh.data())) return -1;
-            for (int j = 0; j < i; j++) hcol[j] = hh[j] + hh[i + 2 + j];
-            hcol[i] = hh[2 * i + 2];
+            if (c.block_gs(w, V, V, i, hd, 1) || c.read(hd, i + 2, hh.data())) return -1;
+            for (int j = 0; j < i; j++) hcol[j] = hh[j];
+            hcol[i] = hh[i];
+            if (std::sqrt(hh[i]) < 0.7071 * std::sqrt(hh[i + 1])) {
+               if (c.block_gs(w, V, V, i, hd2) || c.read(hd2, i + 1, hh.data() + i + 2)) return -1;
+               for (int j = 0; j < i; j++) hcol[j] += hh[i + 2 + j];
+               hcol[i] = hh[2 * i + 2];
+               g_fgmres_second_passes++;
+            }
          }
          const double t = std::sqrt(hcol[i]);
          double* Hc = H.data() + (size_t)(i - 1) * (kdim + 1);
@@ -577,29 +585,37 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
 }
 
 // ---- Lanczos (lanczos.c:3-419) on device vectors ----------------------------------------------------
-// Re-orthogonalisation of w against V[0..k] (dots) / Z[0..k] (updates), repeated while ||w|| < 0.7071 *
-// its previous norm and >= eps, adding the last two projections to td / te (Nfft4GPModifiedGS2,
-// matops.c:348-440).  Each pass is a block classical Gram-Schmidt step (Ctx::block_gs) rather than the
-// reference's vector-by-vector MGS: the repeat-while-the-norm-drops rule is the "twice is enough"
-// criterion that makes the classical form as orthogonal as MGS, and a pass then moves the basis twice
-// instead of four vectors per basis vector.  Projections differ from MGS's only by rounding.
+// Re-orthogonalisation of w against V[0..k] (dots) / Z[0..k] (updates), adding the projections on v_{k-1}
+// and v_k to te / td (Nfft4GPModifiedGS2, matops.c:348-440: MGS over the whole basis, repeated while ||w||
+// drops below 0.7071 of its previous value).  Here:
+//   1. a local classical pass against the last one or two basis vectors (v_{k-1}, v_k: the three-term
+//      recurrence, where the large projections of a Lanczos step are), with ||w|| before it;
+//   2. classical passes over the whole basis (Ctx::block_gs: one launch for all the dots, one for the update),
+//      repeated while ||w|| drops below 0.7071 of its value before the pass (the DGKS / "twice is enough"
+//      test the reference applies), at least one.
+// After the local pass the whole-basis projections are at rounding level, so one whole pass normally ends the
+// step: the basis is read twice per step instead of four times (two whole passes, the round-3 scheme).  In
+// exact arithmetic the projections equal MGS's; in floating point they differ by rounding.
 static int mgs2(Ctx& c, double* w, const double* V, const double* Z, int k, double* td, double* te, double* t)
 {
-   double normw = 0.0;
    double* hd = g_k.scal;
-   for (int pass = 0;; pass++) {
-      // the first pass also returns ||w|| before the projections (hd[k + 2])
-      if (c.block_gs(w, V, Z, k + 1, hd, pass == 0)) return -1;
-      std::vector<double> h(k + 3);
-      if (c.read(hd, pass == 0 ? k + 3 : k + 2, h.data())) return -1;
-      if (pass == 0) normw = std::sqrt(h[k + 2]);
-      if (pass == 0) {
-         if (k >= 1 && te) *te = h[k - 1];
-         if (td) *td = h[k];
-      } else {
-         if (k >= 1 && te) *te += h[k - 1];
-         if (td) *td += h[k];
-      }
+   const size_t n = c.n;
+   const int j0 = k >= 1 ? k - 1 : 0;
+   const int ml = k + 1 - j0;  // 1 or 2 basis vectors in the local pass
+   if (c.block_gs(w, V + (size_t)j0 * n, Z + (size_t)j0 * n, ml, hd, 1)) return -1;
+   double hl[4];
+   if (c.read(hd, ml + 2, hl)) return -1;
+   if (k >= 1 && te) *te = hl[0];
+   if (td) *td = hl[ml - 1];
+   double normw = std::sqrt(hl[ml]);  // ||w|| after the local pass
+   *t = normw;
+   if (normw < DBL_EPSILON) return 0;  // w lies in span(v_{k-1}, v_k): the reference's loop stops here too
+   std::vector<double> h(k + 2);
+   for (;;) {
+      if (c.block_gs(w, V, Z, k + 1, hd, 0)) return -1;
+      if (c.read(hd, k + 2, h.data())) return -1;
+      if (k >= 1 && te) *te += h[k - 1];
+      if (td) *td += h[k];
       *t = std::sqrt(h[k + 1]);
       if (!(*t < normw * 0.7071 && *t >= DBL_EPSILON)) break;
       normw = *t;
@@ -1052,6 +1068,14 @@ bool make_callbacks(Callbacks& cb, int n, func_symmatvec matvec, void* mat, func
 extern "C" {
 
 void Nfft4GPAmdSetFgmresOrtho(int ortho) { g_fgmres_ortho = (ortho == 1) ? 1 : 0; }
+
+// the second classical passes FGMRES (ortho 1) has taken since the last call (its DGKS test), then reset
+long long Nfft4GPAmdFgmresSecondPasses(void)
+{
+   const long long v = g_fgmres_second_passes;
+   g_fgmres_second_passes = 0;
+   return v;
+}
 
 int Nfft4GPSolverFgmres(void* mat_data, int n, func_symmatvec matvec, void* prec_data, func_solve precondfunc,
                         double* x, double* rhs, int kdim, int maxits, int atol, double tol, double* prel_res,

@@ -307,6 +307,44 @@ class RowShardedAfn:
         if not self.h:
             raise RuntimeError("Nfft4GPAmdAfnShard failed (see stderr)")
 
+    @classmethod
+    def setup(cls, X, k: int, comm: Communicator, row_begin: int, row_end: int, perm_opt: str = "fps", perm=None,
+              schur: str = "fsai", schur_lfil: int = 20, kernel: int = 0, op=None, f: float = 1.0, l: float = 1.0,
+              mu: float = 0.01):
+        """Nfft4GPAmdAfnShardSetup: the same row shard set up on this rank alone, every rank collectively, with
+        no full AFN on any rank (afn.c:161-489 split by rows): the ordering and L11^{-1} replicated, K12 only at
+        this rank's Schur points, the Schur FSAI's KNN and values only for this rank's rows.  X (n x d) and
+        ``op`` (an NFFTAdditiveKernel of all n points after its setup: the dense additive kernel) are the same
+        on every rank; perm_opt "identity" / "fps" / "perm" (``perm`` given); schur "fsai" / "noise"."""
+        from . import _lib
+        L = _lib.lib()
+        X = np.asfortranarray(np.asarray(X, dtype=np.float64))
+        n, d = X.shape
+        opt = {"identity": 0, "fps": 1, "perm": 2}[perm_opt]
+        p = None if perm is None else np.ascontiguousarray(np.asarray(perm, dtype=np.int32))
+        if opt == 2 and (p is None or p.size != n):
+            raise ValueError("perm_opt 'perm' needs a permutation of the n points")
+        params = op.h if op is not None else _lib.kernel_params(f, l, mu, n)
+        self = cls.__new__(cls)
+        self.n, self.comm = row_end - row_begin, comm
+        self.h = L.Nfft4GPAmdAfnShardSetup(X.ctypes.data, n, n, d, int(k), opt, None if p is None else p.ctypes.data,
+                                           {"fsai": 3, "noise": 0}[schur], int(schur_lfil), int(kernel), params,
+                                           int(row_begin), int(row_end), comm.h)
+        if op is None:
+            L.Nfft4GPKernelParamFree(params)
+        if not self.h:
+            raise RuntimeError("Nfft4GPAmdAfnShardSetup failed (see stderr)")
+        return self
+
+    def info(self) -> dict:
+        """Landmarks m1 and Schur points m2 of this rank, the K12 doubles it holds (k m2) and its G entries."""
+        import ctypes as C
+        from . import _lib
+        m1, m2 = C.c_int(), C.c_int()
+        k12, nnz = C.c_longlong(), C.c_longlong()
+        _lib.lib().Nfft4GPAmdAfnShardInfo(self.h, C.byref(m1), C.byref(m2), C.byref(k12), C.byref(nnz))
+        return {"m1": m1.value, "m2": m2.value, "k12_doubles": k12.value, "g_nnz": nnz.value}
+
     def solve(self, x, rhs):
         from . import _lib
         from .nfft import _check_len, _ptr

@@ -115,6 +115,19 @@ def _worker(rank, world, port, outdir, backend):
                                 f"afn_{schur}_it": it4})
                     da.free()
                     afn.free()
+                    # the same shard set up on this rank alone (no full AFN anywhere): K12 at its Schur points
+                    # only, the Schur FSAI's KNN and values for its rows only
+                    ds_a = RowShardedAfn.setup(X, 64, comm, rb, re, perm_opt="perm", perm=perm, schur=schur,
+                                               schur_lfil=10, op=full)
+                    zs_a = torch.zeros_like(r)
+                    ds_a.solve(zs_a, r)
+                    xs5 = torch.zeros_like(b)
+                    _, _, _, it5 = amd.pcg(op, b, xs5, maxits=2000, tol=1e-6, precond=ds_a)
+                    inf = ds_a.info()
+                    out.update({f"afn_{schur}_sz": zs_a.cpu().numpy(), f"afn_{schur}_sx": xs5.cpu().numpy(),
+                                f"afn_{schur}_sit": it5, f"afn_{schur}_m2": inf["m2"],
+                                f"afn_{schur}_k12": inf["k12_doubles"], f"afn_{schur}_gnnz": inf["g_nnz"]})
+                    ds_a.free()
                 xs2 = torch.zeros_like(b)
                 _, rr2, _, it2 = amd.pcg(op, b, xs2, maxits=2000, tol=1e-6, precond=dn)
                 out.update({"nys_z": z.cpu().numpy(), "nys_x": xs2.cpu().numpy(), "nys_rr": rr2, "nys_it": it2})
@@ -280,6 +293,31 @@ def test_row_sharded_afn_apply_and_pcg(gloo2, single, schur):
     assert len(set(its)) == 1 and its[0] > 0
     assert abs(its[0] - it1) <= max(3, it1 // 20), (its, it1)
     assert rel(np.concatenate([r[f"afn_{schur}_x"] for r in gloo2]), single[f"afn_{schur}_x"]) < 1e-4
+
+
+@pytest.mark.parametrize("schur", ["fsai", "noise"])
+def test_row_sharded_afn_setup(gloo2, single, schur):
+    """Nfft4GPAmdAfnShardSetup: each rank sets up its own shard -- the K12 columns of its
+    Schur points only (k x m2 with m2 ~ (n - k) / N), the Schur FSAI's KNN and values for its rows only -- and
+    the apply equals the one-GPU AFN apply (afn.c:82-143 on the full setup) to 1e-12; PCG with it takes the
+    one-GPU iteration count."""
+    X, _, _, _, _ = problem("1d")
+    n, k = X.shape[0], 64
+    z = np.concatenate([r[f"afn_{schur}_sz"] for r in gloo2])
+    assert rel(z, single[f"afn_{schur}_z"]) < 1e-12
+    m2 = [int(r[f"afn_{schur}_m2"]) for r in gloo2]
+    assert sum(m2) == n - k  # every Schur point is held by exactly one rank
+    for r, m in zip(gloo2, m2):
+        assert int(r[f"afn_{schur}_k12"]) == k * m  # K12 memory per rank: k (n - k) / N, not k (n - k)
+        assert m <= (n - k) // 2 + 200
+    if schur == "fsai":
+        # the G rows of the ranks together: the full pattern's n - k rows of up to lfil = 10 entries
+        assert sum(int(r["afn_fsai_gnnz"]) for r in gloo2) <= 10 * (n - k)
+    its = [int(r[f"afn_{schur}_sit"]) for r in gloo2]
+    it1 = int(single[f"afn_{schur}_it"])
+    assert len(set(its)) == 1 and its[0] > 0
+    assert abs(its[0] - it1) <= max(3, it1 // 20), (its, it1)
+    assert rel(np.concatenate([r[f"afn_{schur}_sx"] for r in gloo2]), single[f"afn_{schur}_x"]) < 1e-4
 
 
 def test_row_sharded_nystrom_apply_and_pcg(gloo2, single):
