@@ -181,7 +181,7 @@ _SIGS = {
     "Nfft4GPAmdNysShard": (vp, [vp, C.c_int, C.c_int, vp]),
     "Nfft4GPAmdNysShardSetupAdditive": (vp, [vp, vp, C.c_int, C.c_int]),
     "Nfft4GPAmdAfnShard": (vp, [vp, C.c_int, C.c_int, vp]),
-    "Nfft4GPAmdAfnShardSetup": (vp, [dp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.c_int, C.c_int, C.c_int,
+    "Nfft4GPAmdAfnShardSetup": (vp, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int,
                                     vp, C.c_int, C.c_int, vp]),
     "Nfft4GPAmdAfnShardInfo": (C.c_int, [vp, ip, ip, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
     "Nfft4GPAmdAfnSetStorage": (C.c_int, [vp, C.c_int]),

@@ -60,11 +60,46 @@ __device__ __forceinline__ double tap_row(const int* uj, const double* pj, int d
    return w;
 }
 
-// thread = (point, tap row); the row's 10 cells along axis 0 get fp64 atomic adds
+// ---- fixed-point accumulation of the spread -----------------------------------------------------------
+// Every tap contribution a = x_j * prod psi is added as round(a * 2^s) to 64-bit integer accumulators (LDS
+// ds_add_u64, global atomic add u64): integer adds are exact, so the grid is the same whatever order the
+// atomics run in -- the spread, hence the matvec, is bitwise reproducible.  s is set per launch from the
+// bound B = n max|x| psi_max^maxd >= every partial sum: s = 60 - ilogb(B), so |sums| < 2^61 and one
+// contribution's rounding is 2^-61 B.  k_md_fix2f turns the accumulators back into doubles.
+__global__ void k_md_absmax(const double* __restrict__ x, int n, unsigned long long* __restrict__ out)
+{
+   unsigned long long m = 0ull;
+   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
+      m = max(m, (unsigned long long)__double_as_longlong(fabs(x[j])));  // |x| >= 0 orders like its bits
+   for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned long long)__shfl_xor((long long)m, off, 64));
+   if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+__device__ __forceinline__ double fix_scale(const unsigned long long* xmax, double n_bound)
+{
+   const double B = __longlong_as_double((long long)*xmax) * n_bound;
+   return (B > 0.0 && B < 1e300) ? ldexp(1.0, 60 - ilogb(B)) : 1.0;
+}
+
+__device__ __forceinline__ unsigned long long to_fix(double a, double scale)
+{
+   return (unsigned long long)__double2ll_rn(a * scale);
+}
+
+__global__ void k_md_fix2f(const unsigned long long* __restrict__ fx, long long count,
+                           const unsigned long long* __restrict__ xmax, double n_bound, double* __restrict__ grid)
+{
+   const double inv = 1.0 / fix_scale(xmax, n_bound);
+   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (long long)gridDim.x * blockDim.x)
+      grid[i] = (double)(long long)fx[i] * inv;
+}
+
+// thread = (point, tap row); the row's 10 cells along axis 0 get fixed-point atomic adds
 __global__ __launch_bounds__(kMdThreads) void k_md_spread(const MdComp* __restrict__ comps,
                                                           const int* __restrict__ u, const double* __restrict__ psi,
                                                           const double* __restrict__ x, int n, int hi_max,
-                                                          double* __restrict__ grid, long long G)
+                                                          unsigned long long* __restrict__ grid, long long G,
+                                                          const unsigned long long* __restrict__ xmax, double n_bound)
 {
    const MdComp cp = comps[blockIdx.y];
    const long long idx = (long long)blockIdx.x * kMdThreads + threadIdx.x;
@@ -75,10 +110,11 @@ __global__ __launch_bounds__(kMdThreads) void k_md_spread(const MdComp* __restri
    const double* pj = psi + (cp.u_off + (long long)j * cp.d) * kTaps;
    long long base;
    const double w = x[j] * tap_row(uj, pj, cp.d, hi, &base);
-   double* g = grid + (long long)blockIdx.y * G + base;
+   unsigned long long* g = grid + (long long)blockIdx.y * G + base;
+   const double scale = fix_scale(xmax, n_bound);
    const int u0 = uj[0];
 #pragma unroll
-   for (int lt = 0; lt < kTaps; lt++) atomicAdd(g + ((u0 + lt) & (kNos - 1)), w * pj[lt]);
+   for (int lt = 0; lt < kTaps; lt++) atomicAdd(g + ((u0 + lt) & (kNos - 1)), to_fix(w * pj[lt], scale));
 }
 
 // Tiled spread: work item (component, tile, first, end) = the points of one 8^d tile of first-tap cells (a
@@ -94,9 +130,11 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
                                                                       const int* __restrict__ u,
                                                                       const double* __restrict__ psi,
                                                                       const double* __restrict__ x, int n,
-                                                                      double* __restrict__ grid, long long G)
+                                                                      unsigned long long* __restrict__ grid, long long G,
+                                                                      const unsigned long long* __restrict__ xmax,
+                                                                      double n_bound)
 {
-   extern __shared__ double s_acc[];  // kMdFoot^d
+   extern __shared__ unsigned long long s_acc[];  // kMdFoot^d fixed-point accumulators
    const int4 it = items[blockIdx.x];
    const MdComp cp = comps[it.x];
    const int d = cp.d;
@@ -114,8 +152,9 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
          rem /= kNos / kMdTile;
       }
    }
-   for (int e = threadIdx.x; e < foot; e += kMdSpreadThreads) s_acc[e] = 0.0;
+   for (int e = threadIdx.x; e < foot; e += kMdSpreadThreads) s_acc[e] = 0ull;
    __syncthreads();
+   const double scale = fix_scale(xmax, n_bound);
    const int* pp = perm + (long long)it.x * n;
    const int npts = it.w - it.z;
    const long long work = (long long)npts * cp.hicount;
@@ -137,13 +176,13 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
       }
       e += (uj[0] & (kNos - 1)) - lo[0];
 #pragma unroll
-      for (int lt = 0; lt < kTaps; lt++) atomicAdd(s_acc + e + lt, wt * pj[lt]);
+      for (int lt = 0; lt < kTaps; lt++) atomicAdd(s_acc + e + lt, to_fix(wt * pj[lt], scale));  // ds_add_u64
    }
    __syncthreads();
-   double* g = grid + (long long)it.x * G;
+   unsigned long long* g = grid + (long long)it.x * G;
    for (int e = threadIdx.x; e < foot; e += kMdSpreadThreads) {
-      const double v = s_acc[e];
-      if (v == 0.0) continue;
+      const unsigned long long v = s_acc[e];
+      if (v == 0ull) continue;
       long long idx = 0, stride = 1;
       int rem = e;
       for (int t = 0; t < d; t++) {
@@ -515,6 +554,8 @@ void md_free(AdditivePlan& P)
    dfree_md(D.d_bhd);
    dfree_md(D.d_dot_part);
    dfree_md(D.d_dot_ticket);
+   dfree_md(D.d_gfix);
+   dfree_md(D.d_xmax);
    dfree_md(D.d_perm);
    dfree_md(D.d_items);
    dfree_md(D.d_part);
@@ -593,8 +634,10 @@ int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
        dalloc(&D.d_B[1], nw * D.Cmax) || dalloc(&D.d_B[2], nw * D.Cmax) || dalloc(&D.d_B[3], nw * D.Cmax) ||
        dalloc(&D.d_h[0], nw * D.G) || dalloc(&D.d_h[1], nw * D.G) || dalloc(&D.d_bh, nw * D.M) ||
        dalloc(&D.d_bhd, nw * D.M) || dalloc(&D.d_dot_part, (size_t)kMdInterpBlocks) ||
-       dalloc(&D.d_dot_ticket, (size_t)kTicketWords))
+       dalloc(&D.d_dot_ticket, (size_t)kTicketWords) || dalloc(&D.d_gfix, nw * D.G) || dalloc(&D.d_xmax, 1))
       return -1;
+   D.psi_max = 0.0;
+   for (double v : psi) D.psi_max = std::max(D.psi_max, std::fabs(v));
    NFFT4GP_HIP_CHECK(hipMemcpy(D.d_comps, D.comps.data(), sizeof(MdComp) * nw, hipMemcpyHostToDevice));
    if (!u.empty()) {
       NFFT4GP_HIP_CHECK(hipMemcpy(D.d_u, u.data(), sizeof(int) * u.size(), hipMemcpyHostToDevice));
@@ -686,11 +729,32 @@ int md_setup(AdditivePlan& P)
    return 0;
 }
 
+static int md_spread_fix(const AdditivePlan& P, const double* d_x, double n_bound, hipStream_t s);
+
 int md_spread(const AdditivePlan& P, const double* d_x, double* d_grid, hipStream_t s)
 {
    const MdPlan& D = P.md;
-   NFFT4GP_HIP_CHECK(hipMemsetAsync(d_grid, 0, sizeof(double) * (size_t)P.nw * D.G, s));
-   if (P.n == 0) return 0;
+   const size_t count = (size_t)P.nw * D.G;
+   if (P.n == 0) {
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(d_grid, 0, sizeof(double) * count, s));
+      return 0;
+   }
+   // fixed-point bound: n max|x| psi_max^maxd (max|x| on the device)
+   const double n_bound = (double)P.n * std::pow(std::max(D.psi_max, 1e-300), D.maxd);
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(D.d_gfix, 0, sizeof(unsigned long long) * count, s));
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(D.d_xmax, 0, sizeof(unsigned long long), s));
+   hipLaunchKernelGGL(k_md_absmax, dim3(std::min(1024, (P.n + 255) / 256)), dim3(256), 0, s, d_x, P.n, D.d_xmax);
+   if (md_spread_fix(P, d_x, n_bound, s)) return -1;
+   hipLaunchKernelGGL(k_md_fix2f, dim3((unsigned)std::min<size_t>(16384, (count + 255) / 256)), dim3(256), 0, s,
+                      (const unsigned long long*)D.d_gfix, (long long)count, (const unsigned long long*)D.d_xmax,
+                      n_bound, d_grid);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+static int md_spread_fix(const AdditivePlan& P, const double* d_x, double n_bound, hipStream_t s)
+{
+   const MdPlan& D = P.md;
    static const int tiled = getenv("NFFT4GP_AMD_MD_SPREAD") ? atoi(getenv("NFFT4GP_AMD_MD_SPREAD")) : 1;
    if (tiled && D.nitems > 0 && D.maxd <= kMdTiledMaxDim) {
       size_t foot = 1;
@@ -702,8 +766,9 @@ int md_spread(const AdditivePlan& P, const double* d_x, double* d_grid, hipStrea
          (void)hipGetLastError();
          attr = true;
       }
-      hipLaunchKernelGGL(k_md_spread_tiled, dim3(D.nitems), dim3(kMdSpreadThreads), sizeof(double) * foot, s,
-                         D.d_comps, D.d_items, D.d_perm, D.d_u, D.d_psi, d_x, P.n, d_grid, D.G);
+      hipLaunchKernelGGL(k_md_spread_tiled, dim3(D.nitems), dim3(kMdSpreadThreads), sizeof(unsigned long long) * foot,
+                         s, D.d_comps, D.d_items, D.d_perm, D.d_u, D.d_psi, d_x, P.n, D.d_gfix, D.G,
+                         (const unsigned long long*)D.d_xmax, n_bound);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return 0;
    }
@@ -711,7 +776,8 @@ int md_spread(const AdditivePlan& P, const double* d_x, double* d_grid, hipStrea
    for (int t = 1; t < D.maxd; t++) hi_max *= kTaps;
    const long long work = (long long)P.n * hi_max;
    hipLaunchKernelGGL(k_md_spread, dim3((unsigned)((work + kMdThreads - 1) / kMdThreads), P.nw), dim3(kMdThreads), 0,
-                      s, D.d_comps, D.d_u, D.d_psi, d_x, P.n, hi_max, d_grid, D.G);
+                      s, D.d_comps, D.d_u, D.d_psi, d_x, P.n, hi_max, D.d_gfix, D.G,
+                      (const unsigned long long*)D.d_xmax, n_bound);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

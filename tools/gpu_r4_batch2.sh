@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out/r4
-timeout -k 10 900 python -u -m pytest tests/test_gpu_multi.py tests/test_gpu_krylov.py tests/test_gpu_slq_pairs.py tests/test_gpu_dist.py tests/test_gpu_dist_krylov.py -m gpu -x -q --timeout 600 --timeout-method thread > gpurun_out/r4/pt_b2.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/r4/pt_b2.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_multi.py tests/test_gpu_krylov.py tests/test_gpu_slq_pairs.py tests/test_gpu_md.py tests/test_gpu_dist.py tests/test_gpu_dist_krylov.py -m gpu -q --timeout 600 --timeout-method thread > gpurun_out/r4/pt_b2.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/r4/pt_b2.log; exit 1; }
 tail -2 gpurun_out/r4/pt_b2.log
 timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -q --timeout 600 --timeout-method thread -k "config_e" > gpurun_out/r4/pt_e.log 2>&1 || { echo PYTEST_E_FAIL; tail -40 gpurun_out/r4/pt_e.log; exit 1; }
 tail -2 gpurun_out/r4/pt_e.log
