@@ -64,8 +64,8 @@ __device__ __forceinline__ double tap_row(const int* uj, const double* pj, int d
 // Every tap contribution a = x_j * prod psi is added as round(a * 2^s) to 64-bit integer accumulators (LDS
 // ds_add_u64, global atomic add u64): integer adds are exact, so the grid is the same whatever order the
 // atomics run in -- the spread, hence the matvec, is bitwise reproducible.  s is set per launch from the
-// bound B = n max|x| psi_max^maxd >= every partial sum: s = 60 - ilogb(B), so |sums| < 2^61 and one
-// contribution's rounding is 2^-61 B.  k_md_fix2f turns the accumulators back into doubles.
+// bound B_c = n max|x| psi_max^d_c >= every partial sum of component c (d_c features): s_c = 60 - ilogb(B_c),
+// so |sums| < 2^61 and one contribution's rounding is 2^-61 B_c.  k_md_fix2f turns the accumulators back into doubles.
 __global__ void k_md_absmax(const double* __restrict__ x, int n, unsigned long long* __restrict__ out)
 {
    unsigned long long m = 0ull;
@@ -75,9 +75,11 @@ __global__ void k_md_absmax(const double* __restrict__ x, int n, unsigned long l
    if ((threadIdx.x & 63) == 0) atomicMax(out, m);
 }
 
-__device__ __forceinline__ double fix_scale(const unsigned long long* xmax, double n_bound)
+// component c's scale: B = n max|x| psi_max^d_c (each of its d_c taps is at most psi_max)
+__device__ __forceinline__ double fix_scale(const unsigned long long* xmax, double n, double psi_max, int dc)
 {
-   const double B = __longlong_as_double((long long)*xmax) * n_bound;
+   double B = __longlong_as_double((long long)*xmax) * n;
+   for (int t = 0; t < dc; t++) B *= psi_max;
    return (B > 0.0 && B < 1e300) ? ldexp(1.0, 60 - ilogb(B)) : 1.0;
 }
 
@@ -86,11 +88,16 @@ __device__ __forceinline__ unsigned long long to_fix(double a, double scale)
    return (unsigned long long)__double2ll_rn(a * scale);
 }
 
-__global__ void k_md_fix2f(const unsigned long long* __restrict__ fx, long long count,
-                           const unsigned long long* __restrict__ xmax, double n_bound, double* __restrict__ grid)
+// grid[c][i] = fx[c][i] / scale_c; blockIdx.y = component c
+__global__ void k_md_fix2f(const MdComp* __restrict__ comps, const unsigned long long* __restrict__ fx, long long G,
+                           const unsigned long long* __restrict__ xmax, double n, double psi_max,
+                           double* __restrict__ grid)
 {
-   const double inv = 1.0 / fix_scale(xmax, n_bound);
-   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (long long)gridDim.x * blockDim.x)
+   const int c = blockIdx.y;
+   const double inv = 1.0 / fix_scale(xmax, n, psi_max, comps[c].d);
+   fx += (long long)c * G;
+   grid += (long long)c * G;
+   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (long long)gridDim.x * blockDim.x)
       grid[i] = (double)(long long)fx[i] * inv;
 }
 
@@ -99,7 +106,7 @@ __global__ __launch_bounds__(kMdThreads) void k_md_spread(const MdComp* __restri
                                                           const int* __restrict__ u, const double* __restrict__ psi,
                                                           const double* __restrict__ x, int n, int hi_max,
                                                           unsigned long long* __restrict__ grid, long long G,
-                                                          const unsigned long long* __restrict__ xmax, double n_bound)
+                                                          const unsigned long long* __restrict__ xmax, double psi_max)
 {
    const MdComp cp = comps[blockIdx.y];
    const long long idx = (long long)blockIdx.x * kMdThreads + threadIdx.x;
@@ -111,7 +118,7 @@ __global__ __launch_bounds__(kMdThreads) void k_md_spread(const MdComp* __restri
    long long base;
    const double w = x[j] * tap_row(uj, pj, cp.d, hi, &base);
    unsigned long long* g = grid + (long long)blockIdx.y * G + base;
-   const double scale = fix_scale(xmax, n_bound);
+   const double scale = fix_scale(xmax, (double)n, psi_max, cp.d);
    const int u0 = uj[0];
 #pragma unroll
    for (int lt = 0; lt < kTaps; lt++) atomicAdd(g + ((u0 + lt) & (kNos - 1)), to_fix(w * pj[lt], scale));
@@ -132,7 +139,7 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
                                                                       const double* __restrict__ x, int n,
                                                                       unsigned long long* __restrict__ grid, long long G,
                                                                       const unsigned long long* __restrict__ xmax,
-                                                                      double n_bound)
+                                                                      double psi_max)
 {
    extern __shared__ unsigned long long s_acc[];  // kMdFoot^d fixed-point accumulators
    const int4 it = items[blockIdx.x];
@@ -154,7 +161,7 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
    }
    for (int e = threadIdx.x; e < foot; e += kMdSpreadThreads) s_acc[e] = 0ull;
    __syncthreads();
-   const double scale = fix_scale(xmax, n_bound);
+   const double scale = fix_scale(xmax, (double)n, psi_max, d);
    const int* pp = perm + (long long)it.x * n;
    const int npts = it.w - it.z;
    const long long work = (long long)npts * cp.hicount;
@@ -729,7 +736,7 @@ int md_setup(AdditivePlan& P)
    return 0;
 }
 
-static int md_spread_fix(const AdditivePlan& P, const double* d_x, double n_bound, hipStream_t s);
+static int md_spread_fix(const AdditivePlan& P, const double* d_x, double psi_max, hipStream_t s);
 
 int md_spread(const AdditivePlan& P, const double* d_x, double* d_grid, hipStream_t s)
 {
@@ -739,20 +746,19 @@ int md_spread(const AdditivePlan& P, const double* d_x, double* d_grid, hipStrea
       NFFT4GP_HIP_CHECK(hipMemsetAsync(d_grid, 0, sizeof(double) * count, s));
       return 0;
    }
-   // fixed-point bound: n max|x| psi_max^maxd (max|x| on the device)
-   const double n_bound = (double)P.n * std::pow(std::max(D.psi_max, 1e-300), D.maxd);
+   // fixed-point bounds n max|x| psi_max^d_c (max|x| on the device)
    NFFT4GP_HIP_CHECK(hipMemsetAsync(D.d_gfix, 0, sizeof(unsigned long long) * count, s));
    NFFT4GP_HIP_CHECK(hipMemsetAsync(D.d_xmax, 0, sizeof(unsigned long long), s));
    hipLaunchKernelGGL(k_md_absmax, dim3(std::min(1024, (P.n + 255) / 256)), dim3(256), 0, s, d_x, P.n, D.d_xmax);
-   if (md_spread_fix(P, d_x, n_bound, s)) return -1;
-   hipLaunchKernelGGL(k_md_fix2f, dim3((unsigned)std::min<size_t>(16384, (count + 255) / 256)), dim3(256), 0, s,
-                      (const unsigned long long*)D.d_gfix, (long long)count, (const unsigned long long*)D.d_xmax,
-                      n_bound, d_grid);
+   if (md_spread_fix(P, d_x, D.psi_max, s)) return -1;
+   hipLaunchKernelGGL(k_md_fix2f, dim3((unsigned)std::min<long long>(4096, (D.G + 255) / 256), P.nw), dim3(256), 0, s,
+                      (const MdComp*)D.d_comps, (const unsigned long long*)D.d_gfix, D.G,
+                      (const unsigned long long*)D.d_xmax, (double)P.n, D.psi_max, d_grid);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
 
-static int md_spread_fix(const AdditivePlan& P, const double* d_x, double n_bound, hipStream_t s)
+static int md_spread_fix(const AdditivePlan& P, const double* d_x, double psi_max, hipStream_t s)
 {
    const MdPlan& D = P.md;
    static const int tiled = getenv("NFFT4GP_AMD_MD_SPREAD") ? atoi(getenv("NFFT4GP_AMD_MD_SPREAD")) : 1;
@@ -768,7 +774,7 @@ static int md_spread_fix(const AdditivePlan& P, const double* d_x, double n_boun
       }
       hipLaunchKernelGGL(k_md_spread_tiled, dim3(D.nitems), dim3(kMdSpreadThreads), sizeof(unsigned long long) * foot,
                          s, D.d_comps, D.d_items, D.d_perm, D.d_u, D.d_psi, d_x, P.n, D.d_gfix, D.G,
-                         (const unsigned long long*)D.d_xmax, n_bound);
+                         (const unsigned long long*)D.d_xmax, psi_max);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return 0;
    }
@@ -777,7 +783,7 @@ static int md_spread_fix(const AdditivePlan& P, const double* d_x, double n_boun
    const long long work = (long long)P.n * hi_max;
    hipLaunchKernelGGL(k_md_spread, dim3((unsigned)((work + kMdThreads - 1) / kMdThreads), P.nw), dim3(kMdThreads), 0,
                       s, D.d_comps, D.d_u, D.d_psi, d_x, P.n, hi_max, D.d_gfix, D.G,
-                      (const unsigned long long*)D.d_xmax, n_bound);
+                      (const unsigned long long*)D.d_xmax, psi_max);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

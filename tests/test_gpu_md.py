@@ -176,7 +176,8 @@ def test_pcg_tiled_3d(torch_cuda):
     # count.  Since round 4 the spread adds in 64-bit fixed point (exact integer adds: the grid, hence the
     # matvec, is bitwise reproducible, test_md_matvec_is_bitwise_reproducible), so the count is fixed.
     x, rr, hist, it = amd.pcg(op, torch.tensor(b, device="cuda"), x, maxits=2000, tol=1e-8)
-    assert it > 0 and rr <= 1e-8
+    print(f"tiled 3-D PCG: {it} iterations, rel res {rr:.3e}")
+    assert it > 0 and rr <= 1e-8, (it, rr)
     y = op.matsymv(x, 1.0, 0.0, torch.zeros(n, dtype=torch.float64, device="cuda")).cpu().numpy()
     assert np.linalg.norm(b - y) / np.linalg.norm(b) < 1e-7
 
