@@ -157,8 +157,8 @@ struct MdPlan {
    int4* d_items = nullptr;  // {comp, tile, first, end} (first/end index the component's d_perm)
    int nitems = 0;
    double* d_part = nullptr; // tiled interpolation: [2][comp][n] per-component values (K, then K')
-   // the spread adds in 64-bit fixed point (exact, so the grid does not depend on the order of the atomics):
-   // d_gfix [nw][G] int64 accumulators, d_xmax the bits of max |x| of the launch, psi_max the largest tap
+   // the spread adds in 128-bit fixed point (exact, so the grid does not depend on the order of the atomics):
+   // d_gfix [nw][G][lo, hi] 64-bit pairs, d_xmax the bits of max |x| of the launch, psi_max the largest tap
    unsigned long long* d_gfix = nullptr;
    unsigned long long* d_xmax = nullptr;
    double psi_max = 0.0;

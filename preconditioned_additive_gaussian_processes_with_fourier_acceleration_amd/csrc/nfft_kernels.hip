@@ -846,9 +846,16 @@ static void raise_lds_limit_once()
    (void)raised;
 }
 
+int launch_spread_multi(const AdditivePlan& P, int V, const double* const* xs, double* d_part, size_t part_rs,
+                        hipStream_t stream);
+
 int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream)
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
+   if (P.spread_variant == 2) {  // A/B only: k_spread_multi with one vector (gpw groups per workgroup)
+      const double* xs[1] = {d_x};
+      return launch_spread_multi(P, 1, xs, d_part, 0, stream);
+   }
    raise_lds_limit_once();
    const SpreadFn fn = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
    const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
@@ -953,7 +960,7 @@ int launch_spread_multi(const AdditivePlan& P, int V, const double* const* xs, d
                         hipStream_t stream)
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
-   const int threads = P.spread2 == 2 ? 1024 : 512;
+   const int threads = (V > 1 && P.spread2 == 2) ? 1024 : 512;
    const int gpw = std::min(std::max(P.spread2_gpw, 1), P.ngroups);
    const int nslices = (P.ngroups + gpw - 1) / gpw;
    const int gridx = ((P.nblocks + 7) / 8) * 8 * nslices;
@@ -962,6 +969,7 @@ int launch_spread_multi(const AdditivePlan& P, int V, const double* const* xs, d
    typedef void (*Fn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, const double*,
                       const double*, const double*, int, int, int, int, int, int, int, double*, long long);
    Fn fn = nullptr;
+   if (V == 1) fn = threads == 1024 ? k_spread_multi<1024, 1> : k_spread_multi<512, 1>;
    if (V == 2) fn = threads == 1024 ? k_spread_multi<1024, 2> : k_spread_multi<512, 2>;
    if (V == 4) fn = threads == 1024 ? k_spread_multi<1024, 4> : k_spread_multi<512, 4>;
    if (!fn) return -1;

@@ -61,11 +61,13 @@ __device__ __forceinline__ double tap_row(const int* uj, const double* pj, int d
 }
 
 // ---- fixed-point accumulation of the spread -----------------------------------------------------------
-// Every tap contribution a = x_j * prod psi is added as round(a * 2^s) to 64-bit integer accumulators (LDS
-// ds_add_u64, global atomic add u64): integer adds are exact, so the grid is the same whatever order the
-// atomics run in -- the spread, hence the matvec, is bitwise reproducible.  s is set per launch from the
-// bound B_c = n max|x| psi_max^d_c >= every partial sum of component c (d_c features): s_c = 60 - ilogb(B_c),
-// so |sums| < 2^61 and one contribution's rounding is 2^-61 B_c.  k_md_fix2f turns the accumulators back into doubles.
+// Every tap contribution a = x_j * prod psi is added as the 128-bit integer round(a * 2^s) to (lo, hi) pairs of
+// 64-bit accumulators (LDS ds_add_rtn_u64 / ds_add_u64, global atomic adds): the lo add returns the old value,
+// its wrap-around is the exact carry into hi, so the pair ends as the exact 128-bit sum whatever order the
+// atomics run in -- the spread, hence the matvec, is bitwise reproducible.  s_c = 124 - ilogb(B_c) with the
+// bound B_c = n max|x| psi_max^d_c >= every partial sum of component c (d_c features), so |sums| < 2^125
+// and one contribution is rounded at 2^-124 B_c (B_c can exceed a cell's value by ~2^22: still ~2^-100).
+// k_md_fix2f turns the pairs back into doubles.
 __global__ void k_md_absmax(const double* __restrict__ x, int n, unsigned long long* __restrict__ out)
 {
    unsigned long long m = 0ull;
@@ -75,30 +77,55 @@ __global__ void k_md_absmax(const double* __restrict__ x, int n, unsigned long l
    if ((threadIdx.x & 63) == 0) atomicMax(out, m);
 }
 
-// component c's scale: B = n max|x| psi_max^d_c (each of its d_c taps is at most psi_max)
-__device__ __forceinline__ double fix_scale(const unsigned long long* xmax, double n, double psi_max, int dc)
+// exponent s_c of component c (d_c features): B = n max|x| psi_max^d_c
+__device__ __forceinline__ int fix_exp(const unsigned long long* xmax, double n, double psi_max, int dc)
 {
    double B = __longlong_as_double((long long)*xmax) * n;
    for (int t = 0; t < dc; t++) B *= psi_max;
-   return (B > 0.0 && B < 1e300) ? ldexp(1.0, 60 - ilogb(B)) : 1.0;
+   return (B > 0.0 && B < 1e300) ? 124 - ilogb(B) : 0;
 }
 
-__device__ __forceinline__ unsigned long long to_fix(double a, double scale)
+// round(a 2^s) as a two's-complement 128-bit (lo, hi): a 2^(s-64) = hi + f with hi = floor, f in [0, 1),
+// lo = f 2^64 truncated (the bits below 2^0 of a 2^s)
+__device__ __forceinline__ void to_fix(double a, int s, unsigned long long& lo, long long& hi)
 {
-   return (unsigned long long)__double2ll_rn(a * scale);
+   const double t = ldexp(a, s - 64);
+   const double h = floor(t);
+   const double f = t - h;  // exact; 1.0 only when t is a tiny negative number (then the value rounds to 0)
+   hi = (long long)h + (f >= 1.0 ? 1 : 0);
+   lo = f >= 1.0 ? 0ull : (unsigned long long)ldexp(f, 64);
 }
 
-// grid[c][i] = fx[c][i] / scale_c; blockIdx.y = component c
+// acc[0] = lo, acc[1] = hi (LDS or global): exact 128-bit add
+__device__ __forceinline__ void fix_add(unsigned long long* acc, unsigned long long lo, long long hi)
+{
+   const unsigned long long old = atomicAdd(acc, lo);
+   const unsigned long long carry = (old + lo < old) ? 1ull : 0ull;
+   const unsigned long long h = (unsigned long long)hi + carry;
+   if (h) atomicAdd(acc + 1, h);
+}
+
+// grid[c][i] = (hi 2^64 + lo) 2^-s_c; blockIdx.y = component c; fx: [c][i][lo, hi]
 __global__ void k_md_fix2f(const MdComp* __restrict__ comps, const unsigned long long* __restrict__ fx, long long G,
                            const unsigned long long* __restrict__ xmax, double n, double psi_max,
                            double* __restrict__ grid)
 {
    const int c = blockIdx.y;
-   const double inv = 1.0 / fix_scale(xmax, n, psi_max, comps[c].d);
-   fx += (long long)c * G;
+   const int e = fix_exp(xmax, n, psi_max, comps[c].d);
+   fx += 2 * (long long)c * G;
    grid += (long long)c * G;
-   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (long long)gridDim.x * blockDim.x)
-      grid[i] = (double)(long long)fx[i] * inv;
+   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (long long)gridDim.x * blockDim.x) {
+      const unsigned long long lo = fx[2 * i];
+      const long long hi = (long long)fx[2 * i + 1];
+      double v;
+      if (hi == 0)
+         v = (double)lo;
+      else if (hi == -1)
+         v = -(double)(0ull - lo);  // lo - 2^64
+      else
+         v = ldexp((double)hi, 64) + (double)lo;
+      grid[i] = ldexp(v, -e);
+   }
 }
 
 // thread = (point, tap row); the row's 10 cells along axis 0 get fixed-point atomic adds
@@ -117,11 +144,16 @@ __global__ __launch_bounds__(kMdThreads) void k_md_spread(const MdComp* __restri
    const double* pj = psi + (cp.u_off + (long long)j * cp.d) * kTaps;
    long long base;
    const double w = x[j] * tap_row(uj, pj, cp.d, hi, &base);
-   unsigned long long* g = grid + (long long)blockIdx.y * G + base;
-   const double scale = fix_scale(xmax, (double)n, psi_max, cp.d);
+   unsigned long long* g = grid + 2 * ((long long)blockIdx.y * G + base);
+   const int ex = fix_exp(xmax, (double)n, psi_max, cp.d);
    const int u0 = uj[0];
 #pragma unroll
-   for (int lt = 0; lt < kTaps; lt++) atomicAdd(g + ((u0 + lt) & (kNos - 1)), to_fix(w * pj[lt], scale));
+   for (int lt = 0; lt < kTaps; lt++) {
+      unsigned long long lo;
+      long long hi;
+      to_fix(w * pj[lt], ex, lo, hi);
+      fix_add(g + 2 * ((u0 + lt) & (kNos - 1)), lo, hi);
+   }
 }
 
 // Tiled spread: work item (component, tile, first, end) = the points of one 8^d tile of first-tap cells (a
@@ -141,7 +173,7 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
                                                                       const unsigned long long* __restrict__ xmax,
                                                                       double psi_max)
 {
-   extern __shared__ unsigned long long s_acc[];  // kMdFoot^d fixed-point accumulators
+   extern __shared__ unsigned long long s_acc[];  // kMdFoot^d fixed-point (lo, hi) pairs
    const int4 it = items[blockIdx.x];
    const MdComp cp = comps[it.x];
    const int d = cp.d;
@@ -159,9 +191,9 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
          rem /= kNos / kMdTile;
       }
    }
-   for (int e = threadIdx.x; e < foot; e += kMdSpreadThreads) s_acc[e] = 0ull;
+   for (int e = threadIdx.x; e < 2 * foot; e += kMdSpreadThreads) s_acc[e] = 0ull;
    __syncthreads();
-   const double scale = fix_scale(xmax, (double)n, psi_max, d);
+   const int ex = fix_exp(xmax, (double)n, psi_max, d);
    const int* pp = perm + (long long)it.x * n;
    const int npts = it.w - it.z;
    const long long work = (long long)npts * cp.hicount;
@@ -183,13 +215,19 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
       }
       e += (uj[0] & (kNos - 1)) - lo[0];
 #pragma unroll
-      for (int lt = 0; lt < kTaps; lt++) atomicAdd(s_acc + e + lt, to_fix(wt * pj[lt], scale));  // ds_add_u64
+      for (int lt = 0; lt < kTaps; lt++) {
+         unsigned long long lo;
+         long long hi;
+         to_fix(wt * pj[lt], ex, lo, hi);
+         fix_add(s_acc + 2 * (e + lt), lo, hi);
+      }
    }
    __syncthreads();
-   unsigned long long* g = grid + (long long)it.x * G;
+   unsigned long long* g = grid + 2 * (long long)it.x * G;
    for (int e = threadIdx.x; e < foot; e += kMdSpreadThreads) {
-      const unsigned long long v = s_acc[e];
-      if (v == 0ull) continue;
+      const unsigned long long vlo = s_acc[2 * e];
+      const long long vhi = (long long)s_acc[2 * e + 1];
+      if (vlo == 0ull && vhi == 0) continue;
       long long idx = 0, stride = 1;
       int rem = e;
       for (int t = 0; t < d; t++) {
@@ -197,7 +235,7 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
          rem /= kMdFoot;
          stride *= kNos;
       }
-      atomicAdd(g + idx, v);
+      fix_add(g + 2 * idx, vlo, vhi);
    }
 }
 
@@ -641,7 +679,7 @@ int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
        dalloc(&D.d_B[1], nw * D.Cmax) || dalloc(&D.d_B[2], nw * D.Cmax) || dalloc(&D.d_B[3], nw * D.Cmax) ||
        dalloc(&D.d_h[0], nw * D.G) || dalloc(&D.d_h[1], nw * D.G) || dalloc(&D.d_bh, nw * D.M) ||
        dalloc(&D.d_bhd, nw * D.M) || dalloc(&D.d_dot_part, (size_t)kMdInterpBlocks) ||
-       dalloc(&D.d_dot_ticket, (size_t)kTicketWords) || dalloc(&D.d_gfix, nw * D.G) || dalloc(&D.d_xmax, 1))
+       dalloc(&D.d_dot_ticket, (size_t)kTicketWords) || dalloc(&D.d_gfix, 2 * nw * D.G) || dalloc(&D.d_xmax, 1))
       return -1;
    D.psi_max = 0.0;
    for (double v : psi) D.psi_max = std::max(D.psi_max, std::fabs(v));
@@ -747,7 +785,7 @@ int md_spread(const AdditivePlan& P, const double* d_x, double* d_grid, hipStrea
       return 0;
    }
    // fixed-point bounds n max|x| psi_max^d_c (max|x| on the device)
-   NFFT4GP_HIP_CHECK(hipMemsetAsync(D.d_gfix, 0, sizeof(unsigned long long) * count, s));
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(D.d_gfix, 0, 2 * sizeof(unsigned long long) * count, s));
    NFFT4GP_HIP_CHECK(hipMemsetAsync(D.d_xmax, 0, sizeof(unsigned long long), s));
    hipLaunchKernelGGL(k_md_absmax, dim3(std::min(1024, (P.n + 255) / 256)), dim3(256), 0, s, d_x, P.n, D.d_xmax);
    if (md_spread_fix(P, d_x, D.psi_max, s)) return -1;
@@ -772,7 +810,7 @@ static int md_spread_fix(const AdditivePlan& P, const double* d_x, double psi_ma
          (void)hipGetLastError();
          attr = true;
       }
-      hipLaunchKernelGGL(k_md_spread_tiled, dim3(D.nitems), dim3(kMdSpreadThreads), sizeof(unsigned long long) * foot,
+      hipLaunchKernelGGL(k_md_spread_tiled, dim3(D.nitems), dim3(kMdSpreadThreads), 2 * sizeof(unsigned long long) * foot,
                          s, D.d_comps, D.d_items, D.d_perm, D.d_u, D.d_psi, d_x, P.n, D.d_gfix, D.G,
                          (const unsigned long long*)D.d_xmax, psi_max);
       NFFT4GP_HIP_CHECK(hipGetLastError());

@@ -173,7 +173,7 @@ def test_pcg_tiled_3d(torch_cuda):
     x = torch.zeros(n, dtype=torch.float64, device="cuda")
     # round 3 measured 1971-2015 iterations over four runs: the tiled spread's fp64 atomics added in a varying
     # order, and CG at 1e-8 on this operator amplifies those rounding differences into a few percent of the
-    # count.  Since round 4 the spread adds in 64-bit fixed point (exact integer adds: the grid, hence the
+    # count.  Since round 4 the spread adds in 128-bit fixed point (exact integer adds: the grid, hence the
     # matvec, is bitwise reproducible, test_md_matvec_is_bitwise_reproducible), so the count is fixed.
     x, rr, hist, it = amd.pcg(op, torch.tensor(b, device="cuda"), x, maxits=2000, tol=1e-8)
     print(f"tiled 3-D PCG: {it} iterations, rel res {rr:.3e}")
@@ -184,7 +184,7 @@ def test_pcg_tiled_3d(torch_cuda):
 
 @pytest.mark.parametrize("n,nw,dw", [(60000, 2, 3), (3000, 2, 3), (20000, 3, 2), (2000, 1, 4)])
 def test_md_matvec_is_bitwise_reproducible(torch_cuda, n, nw, dw):
-    """The multi-feature spread accumulates in 64-bit fixed point (nfft_md.hip: exact integer atomics in LDS and
+    """The multi-feature spread accumulates in 128-bit fixed point (nfft_md.hip: exact integer atomics in LDS and
     in the grid), so two matvecs and two gradient matvecs of the same vector are bitwise equal, for the tiled
     (60000 points: >= 100 per tile) and untiled (3000 points, and 4-feature windows) spreads."""
     torch = torch_cuda

@@ -1,4 +1,6 @@
-# A/B of environment settings on the bench workload: bash tools/ab_env.sh "NFFT4GP_AMD_FUSE_GRID=0 NFFT4GP_AMD_FUSE_GRID=1" [bench args]
+# A/B of environment settings on the bench workload (the library reads its knobs at handle creation):
+#   bash tools/ab_env.sh "NFFT4GP_AMD_SPREAD_VARIANT=0 NFFT4GP_AMD_SPREAD_VARIANT=2,NFFT4GP_AMD_SPREAD2_GPW=2" [bench args]
+# one setting per word, several variables of one setting joined by commas
 set -o pipefail
 mkdir -p gpurun_out
 SETS="$1"; shift
@@ -6,7 +8,7 @@ for rep in 1 2; do
   i=0
   for kv in $SETS; do
     i=$((i+1))
-    env $kv timeout -k 10 300 python bench.py --no-cpu-baseline --no-traffic --no-pcg "$@" > gpurun_out/ab_$i.json 2> gpurun_out/ab_$i.err || { echo BENCH_FAIL $kv; tail -20 gpurun_out/ab_$i.err; exit 1; }
+    env $(echo "$kv" | tr ',' ' ') timeout -k 10 300 python bench.py --no-cpu-baseline --no-traffic --no-pcg "$@" > gpurun_out/ab_$i.json 2> gpurun_out/ab_$i.err || { echo BENCH_FAIL $kv; tail -20 gpurun_out/ab_$i.err; exit 1; }
     python -c "import json;d=json.load(open('gpurun_out/ab_$i.json'));print('$kv rep $rep', round(d['ms_per_step']*1e3,1), {k:round(x*1e3,2) for k,x in d['kernels_ms'].items()})"
   done
 done
