@@ -151,15 +151,19 @@ void launch_panel(int kernel, bool grad, dim3 grid, size_t lds, hipStream_t s, c
 // op(A) is M x K: A column-major (lda) or, with TRANSA, A^T of a column-major K x M array.  B is K x N
 // column-major (ldb).  128 x 128 output tile per workgroup: 4 waves in 2 x 2, each 64 x 64 = 4 x 4
 // blocks of v_mfma_f64_16x16x4_f64 (64 doubles of accumulator per lane).  K advances in steps of 16
-// through LDS; the next step's global loads are issued before the current step's 64 MFMAs per wave,
-// so their latency hides behind ~4k MFMA cycles.  The MFMA operands are swapped (B feeds the
-// A-operand slot) so a lane's accumulators hold 16 consecutive ROWS of C: every store instruction
-// writes 4 full 128-B column segments of the column-major C instead of 16 scattered 32-B pieces.
-// gridDim.z > 1 splits K into chunks of ksplit; chunk z writes its partial product at
-// C + z * split_stride (summed by k_sum_splits).  sym: C is symmetric (the Gram U^T U), only tiles
-// with tile_n <= tile_m are computed (k_sum_splits mirrors the rest).
+// through a double-buffered LDS tile: step i's MFMAs read buffer i & 1 while step i + 1's global loads
+// (issued before them) are in flight; their registers then go to the other buffer, one barrier per step.
+// The MFMA operands are swapped (B feeds the A-operand slot) so a lane's accumulators hold 16 consecutive
+// ROWS of C: every store instruction writes 4 full 128-B column segments of the column-major C instead of
+// 16 scattered 32-B pieces.  Tile order: the N tiles of one M tile are consecutive and run on one XCD
+// (workgroup id % 8), so the A rows they share are read from HBM once and then from that XCD's L2.
+// ksplit < K splits K into chunks (tile order z-major); chunk z writes its partial product at
+// C + z * split_stride (summed by k_sum_splits).  sym: C is symmetric (the Gram U^T U), only tiles with
+// tile_n <= tile_m are computed (k_sum_splits mirrors the rest).  The accumulation order over K is the
+// same as a single-buffered step loop: results do not depend on the tile order.
 constexpr int kGemmTile = 128, kGemmK = 16, kGemmThreads = 256, kGemmPad = 1;
 constexpr int kGemmLd = kGemmTile + kGemmPad;
+constexpr size_t kGemmLds = sizeof(double) * 2 * 2 * kGemmK * kGemmLd;  // [buffer][A | B][kk][row]
 
 template <bool TRANSA>
 __global__ __launch_bounds__(kGemmThreads) void k_gemm_f64(int M, int N, int K, const double* __restrict__ A,
@@ -167,14 +171,23 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm_f64(int M, int N, int K, 
                                                            long long ldb, double* __restrict__ C, long long ldc,
                                                            long long split_stride, int ksplit, int sym)
 {
-   if (sym && blockIdx.y > blockIdx.x) return;
-   __shared__ double As[kGemmK * kGemmLd];  // As[kk][row]
-   __shared__ double Bs[kGemmK * kGemmLd];  // Bs[kk][col]
-   const int m0 = blockIdx.x * kGemmTile, n0 = blockIdx.y * kGemmTile;
-   const int kbeg = blockIdx.z * ksplit, kend = min(K, kbeg + ksplit);
+   extern __shared__ double g_smem[];
+   const int mt = (M + kGemmTile - 1) / kGemmTile, nt = (N + kGemmTile - 1) / kGemmTile;
+   const int nz = (K + ksplit - 1) / ksplit;
+   const long long total = (long long)mt * nt * nz;
+   const long long per = (total + 7) / 8;
+   const long long tpos = (long long)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+   if (tpos >= total) return;
+   const int zi = (int)(tpos / ((long long)mt * nt));
+   const int rem = (int)(tpos % ((long long)mt * nt));
+   const int tm = rem / nt, tn = rem % nt;
+   if (sym && tn > tm) return;
+   const int m0 = tm * kGemmTile, n0 = tn * kGemmTile;
+   const int kbeg = zi * ksplit, kend = min(K, kbeg + ksplit);
    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
    const int wm = (wave & 1) * 64, wn = (wave >> 1) * 64;
    constexpr int kPer = kGemmK * kGemmTile / kGemmThreads;  // 8 elements of each operand per thread
+   constexpr int kBuf = 2 * kGemmK * kGemmLd;                // doubles per buffer (A then B)
    d4 acc[4][4];
 #pragma unroll
    for (int i = 0; i < 4; i++)
@@ -200,9 +213,9 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm_f64(int M, int N, int K, 
          bv[u] = (gbk < kend && gbc < N) ? B[gbk + (long long)gbc * ldb] : 0.0;
       }
    };
-   fetch(kbeg);
-   for (int k0 = kbeg; k0 < kend; k0 += kGemmK) {
-      __syncthreads();  // the previous step's LDS reads are done
+   auto store = [&](double* buf) {
+      double* As = buf;
+      double* Bs = buf + kGemmK * kGemmLd;
 #pragma unroll
       for (int u = 0; u < kPer; u++) {
          const int e = tid + u * kGemmThreads;
@@ -212,8 +225,16 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm_f64(int M, int N, int K, 
             As[(e & (kGemmK - 1)) * kGemmLd + (e >> 4)] = av[u];
          Bs[(e & (kGemmK - 1)) * kGemmLd + (e >> 4)] = bv[u];
       }
-      __syncthreads();
-      if (k0 + kGemmK < kend) fetch(k0 + kGemmK);  // in flight during this step's MFMAs
+   };
+   fetch(kbeg);
+   store(g_smem);
+   __syncthreads();
+   int cur = 0;
+   for (int k0 = kbeg; k0 < kend; k0 += kGemmK) {
+      const bool more = k0 + kGemmK < kend;
+      if (more) fetch(k0 + kGemmK);  // in flight during this step's MFMAs
+      const double* As = g_smem + cur * kBuf;
+      const double* Bs = As + kGemmK * kGemmLd;
 #pragma unroll
       for (int k4 = 0; k4 < kGemmK / 4; k4++) {
          const int kk = 4 * k4 + (lane >> 4);
@@ -227,10 +248,13 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm_f64(int M, int N, int K, 
 #pragma unroll
             for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(b[j], a[i], acc[i][j], 0, 0, 0);
       }
+      if (more) store(g_smem + (cur ^ 1) * kBuf);  // the other buffer: nobody reads it during this step
+      __syncthreads();
+      cur ^= 1;
    }
    // D map of v_mfma_f64_16x16x4_f64: D col = lane & 15 (B-operand index = row of C here),
    // D row = (lane >> 4) + 4 * reg (A-operand index = column of C here)
-   double* Cz = C + (size_t)blockIdx.z * split_stride;
+   double* Cz = C + (size_t)zi * split_stride;
 #pragma unroll
    for (int i = 0; i < 4; i++)
 #pragma unroll
@@ -241,6 +265,25 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm_f64(int M, int N, int K, 
             const int gc = n0 + wn + 16 * j + (lane >> 4) + 4 * rg;
             if (gr < M && gc < N) Cz[gr + (long long)gc * ldc] = acc[i][j][rg];
          }
+}
+
+// the launch grid of k_gemm_f64: one workgroup per (M tile, N tile, K chunk), rounded up to a multiple of 8
+static unsigned gemm_blocks(int M, int N, int K, int ksplit)
+{
+   const long long total = (long long)((M + kGemmTile - 1) / kGemmTile) * ((N + kGemmTile - 1) / kGemmTile) *
+                           ((K + ksplit - 1) / ksplit);
+   return (unsigned)(((total + 7) / 8) * 8);
+}
+
+static void gemm_attr_once()
+{
+   static const bool done = []() {
+      (void)hipFuncSetAttribute((const void*)k_gemm_f64<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmLds);
+      (void)hipFuncSetAttribute((const void*)k_gemm_f64<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmLds);
+      (void)hipGetLastError();
+      return true;
+   }();
+   (void)done;
 }
 
 // C[i] = sum_z part[z * stride + i] in z order.  sym (square C of order ld): elements of tiles above the
@@ -263,11 +306,16 @@ __global__ void k_sum_splits(const double* __restrict__ part, int nsplit, long l
 int gemm(bool transA, int M, int N, int K, const double* A, long long lda, const double* B, long long ldb, double* C,
          long long ldc, hipStream_t s)
 {
-   dim3 grid((M + kGemmTile - 1) / kGemmTile, (N + kGemmTile - 1) / kGemmTile, 1);
+   if (M <= 0 || N <= 0) return 0;
+   gemm_attr_once();
+   const int ks = std::max(K, 1);
+   const dim3 grid(gemm_blocks(M, N, ks, ks));
    if (transA)
-      hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(kGemmThreads), 0, s, M, N, K, A, lda, B, ldb, C, ldc, 0LL, K, 0);
+      hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(kGemmThreads), kGemmLds, s, M, N, K, A, lda, B, ldb, C, ldc, 0LL,
+                         ks, 0);
    else
-      hipLaunchKernelGGL(k_gemm_f64<false>, grid, dim3(kGemmThreads), 0, s, M, N, K, A, lda, B, ldb, C, ldc, 0LL, K, 0);
+      hipLaunchKernelGGL(k_gemm_f64<false>, grid, dim3(kGemmThreads), kGemmLds, s, M, N, K, A, lda, B, ldb, C, ldc, 0LL,
+                         ks, 0);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -702,9 +750,10 @@ int gram_tn(int M, int N, int K, const double* A, long long lda, const double* B
    const int nsplit_used = (K + ksplit - 1) / ksplit;
    double* part = nullptr;
    if (dalloc(&part, (size_t)nsplit_used * M * N)) return -1;
-   dim3 grid((M + kGemmTile - 1) / kGemmTile, (N + kGemmTile - 1) / kGemmTile, nsplit_used);
-   hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(kGemmThreads), 0, s, M, N, K, A, lda, B, ldb, part, (long long)M,
-                      (long long)M * N, ksplit, sym);
+   gemm_attr_once();
+   const dim3 grid(gemm_blocks(M, N, K, ksplit));
+   hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(kGemmThreads), kGemmLds, s, M, N, K, A, lda, B, ldb, part,
+                      (long long)M, (long long)M * N, ksplit, sym);
    const long long cnt = (long long)M * N;
    hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, part, nsplit_used, cnt, cnt,
                       C, sym, M);
