@@ -121,10 +121,13 @@ def test_distributed_fgmres_and_logdet_match_single_gpu(gloo2, single, part):
         np.testing.assert_array_equal(gloo2[1][part + "_x"], gloo2[0][part + "_x"])
         x = gloo2[0][part + "_x"]
     assert _rel(x, single["x"]) < 1e-9
-    # the first restart cycle to 1e-8; later cycles to 1e-2: the reference's restart scales the new residual
-    # by the Givens estimate, not its norm (fgmres.c:236-243), which amplifies rounding
+    # the first restart cycle to 1e-8; later cycles to 4e-2: this FGMRES(25) stagnates at 0.24 and the
+    # reference's restart scales the new residual by the Givens estimate, not its norm (fgmres.c:236-243),
+    # which amplifies rounding -- the REFERENCE ITSELF under one-ulp operator noise moves its later-cycle
+    # history by up to 1.2e-2 (tools/fgmres_restart_sensitivity.py, profiles/r04_fgmres_restart_sensitivity.txt;
+    # a split operator sums in another order, the same kind of perturbation): 3x that
     h0, h1 = gloo2[0][part + "_hist"][:its[0] + 1], single["hist"][:its[0] + 1]
     np.testing.assert_allclose(h0[:26], h1[:26], rtol=1e-8)
-    np.testing.assert_allclose(h0, h1, rtol=1e-2)
+    np.testing.assert_allclose(h0, h1, rtol=4e-2)
     assert float(gloo2[0][part + "_ld"]) == pytest.approx(single["ld"], rel=1e-10)
     np.testing.assert_allclose(gloo2[0][part + "_dld"], single["dld"], rtol=1e-8, atol=1e-12)
