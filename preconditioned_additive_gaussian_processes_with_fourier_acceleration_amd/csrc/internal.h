@@ -180,9 +180,6 @@ struct AdditivePlan {
    // layout
    int B = kMaxBlock, CG = 3, ngroups = 0, nblocks = 0;  // CG = 3: 3 spread workgroups fit a CU's LDS
    int spread_variant = 0;  // 0: the spread; 1: the same with timeline stamps (NFFT4GP_AMD_SPREAD_VARIANT, tools/)
-   // two-vector matvec: 0 one spread per vector, 1 / 2 k_spread_multi with 512 / 1024 threads
-   // (NFFT4GP_AMD_SPREAD2), gpw window groups per workgroup (NFFT4GP_AMD_SPREAD2_GPW)
-   int spread2 = 1, spread2_gpw = 1;
    DevLayout dl;
    // device buffers
    double* d_part = nullptr;  // [nblocks][nw][64]

@@ -512,8 +512,6 @@ void env_layout(AdditivePlan& P)
       if (v >= 1 && v <= 64) P.CG = v;
    }
    if (const char* e = getenv("NFFT4GP_AMD_SPREAD_VARIANT")) P.spread_variant = atoi(e);
-   if (const char* e = getenv("NFFT4GP_AMD_SPREAD2")) P.spread2 = atoi(e);
-   if (const char* e = getenv("NFFT4GP_AMD_SPREAD2_GPW")) P.spread2_gpw = std::max(1, atoi(e));
 }
 
 void* additive_create(double* data, int n_global, int ldim, int* windows, int nwindows, int dwindows, int rb, int re)

@@ -198,124 +198,6 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    }
 }
 
-// ------------------------------------------------------------------------------------------------
-// several vectors per pass over the layout (the SLQ probes in lockstep, krylov.hip)
-// ------------------------------------------------------------------------------------------------
-// V vectors share each run's layout loads, its slot decode and its powers u^d; every vector keeps its own
-// alpha slice in LDS (planar: the layout's bank balancing of the alpha gather holds per vector) and its own
-// 10 moments per (window, cell) (moment rows of V*kNC + 1 doubles).  One workgroup = one block x a slice of
-// gpw consecutive window groups: the V alpha slices are staged once for the slice, the next group's first
-// run is loaded while the current group folds.  part: V planes of [comp][block][cell], part_rs apart.
-template <int V>
-constexpr int mom_stride_v() { return V * kNC + 1; }
-
-template <int THREADS, int V>
-__global__ __launch_bounds__(THREADS) void k_spread_multi(const uint16_t* __restrict__ meta,
-                                                          const uint32_t* __restrict__ lo,
-                                                          const uint32_t* __restrict__ qarr,
-                                                          const int* __restrict__ tile_off, const double* __restrict__ x0,
-                                                          const double* __restrict__ x1, const double* __restrict__ x2,
-                                                          const double* __restrict__ x3, int n, int B, int nblocks,
-                                                          int ngroups, int CG, int nw, int gpw, double* __restrict__ part,
-                                                          long long part_rs)
-{
-   static_assert(V >= 1 && V <= 4, "1 to 4 vectors");
-   constexpr int MS = mom_stride_v<V>();
-   extern __shared__ __attribute__((aligned(16))) double smem[];
-   const int Bp = B + kPad;
-   double* s_alpha = smem;          // [V][Bp]
-   double* s_mom = smem + V * Bp;   // [CG][64][MS]
-   const int nslices = (ngroups + gpw - 1) / gpw;
-   const int xcd = blockIdx.x & 7;
-   const int rest = blockIdx.x >> 3;
-   const int slice = rest % nslices;
-   const int b = (rest / nslices) * 8 + xcd;
-   if (b >= nblocks) return;
-   const int g_begin = slice * gpw;
-   const int g_end = min(ngroups, g_begin + gpw);
-   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-   constexpr int nwaves = THREADS / 64;
-
-   TileRegs cur;
-   int t1 = tile_off[b * ngroups + g_begin + 1];
-   int t = tile_off[b * ngroups + g_begin] + wave;
-   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
-   const int base = b * B;
-   const int nloc = min(B, n - base);
-   const double* xs[4] = {x0, x1, x2, x3};
-#pragma unroll
-   for (int v = 0; v < V; v++) stage_block_glds<THREADS>(s_alpha + v * Bp, xs[v], base, nloc, B);
-   const int mom_count = CG * kNos * MS;
-   for (int i = tid; i < mom_count; i += THREADS) s_mom[i] = 0.0;
-   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-   __syncthreads();
-
-   for (int g = g_begin; g < g_end; g++) {
-      const int c0 = g * CG;
-      for (; t < t1; t += nwaves) {
-         double acc[V][kNC];
-#pragma unroll
-         for (int v = 0; v < V; v++)
-#pragma unroll
-            for (int d = 0; d < kNC; d++) acc[v][d] = 0.0;
-#pragma unroll
-         for (int r = 0; r < kR; r++) {
-            const uint32_t loc = slot_loc(cur, r);
-            const double u = q_to_u(cur.qq[r]);
-            double a[V];
-#pragma unroll
-            for (int v = 0; v < V; v++) {
-               a[v] = s_alpha[v * Bp + loc];
-               acc[v][0] += a[v];
-            }
-            double up = u;
-#pragma unroll
-            for (int d = 1; d < kNC; d++) {
-#pragma unroll
-               for (int v = 0; v < V; v++) acc[v][d] = fma(a[v], up, acc[v][d]);
-               if (d + 1 < kNC) up *= u;
-            }
-         }
-         const int comp_local = (int)(cur.mt >> 6) - c0;
-         const int cell = (int)(cur.mt & 63u);
-         double* dst = s_mom + (comp_local * kNos + cell) * MS;
-#pragma unroll
-         for (int v = 0; v < V; v++)
-#pragma unroll
-            for (int d = 0; d < kNC; d++) atomicAdd(dst + v * kNC + d, acc[v][d]);  // ds_add_f64
-         if (t + nwaves < t1) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
-      }
-      __syncthreads();
-      // the next group's first run is loaded while this group folds
-      if (g + 1 < g_end) {
-         const int t0n = t1;
-         t1 = tile_off[b * ngroups + g + 2];
-         t = t0n + wave;
-         if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
-      }
-      const int ncomp = min(CG, nw - c0);
-      for (int idx = tid; idx < V * ncomp * kNos; idx += THREADS) {
-         const int v = idx / (ncomp * kNos);
-         const int rem = idx % (ncomp * kNos);
-         const int cl = rem / kNos;
-         const int gi = rem % kNos;
-         double acc = 0.0;
-#pragma unroll 1
-         for (int tp = 0; tp < kTaps; tp++) {
-            const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * MS + v * kNC;
-#pragma unroll
-            for (int d = 0; d < kNC; d++) acc = fma(c_taps[tp * kNC + d], mrow[d], acc);
-         }
-         part[v * part_rs + ((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = acc;
-      }
-      if (g + 1 < g_end) {
-         __syncthreads();  // every fold read done before the table is cleared
-         for (int i = tid; i < mom_count; i += THREADS) s_mom[i] = 0.0;
-         __syncthreads();
-      }
-   }
-}
-
 // copy the diagnostic timeline out (tools/ only)
 extern "C" int Nfft4GPAmdDebugStamps(unsigned long long* out, int nwg)
 {
@@ -704,10 +586,10 @@ __global__ __launch_bounds__(THREADS) void k_interp(
 // ------------------------------------------------------------------------------------------------
 // The interpolation reads the layout (5 B per (point, window)) once for both vectors and shares the
 // per-point decode; each vector keeps its own H and LDS y-slice (planar, so the layout's bank balancing
-// for ds_add_f64 holds).  The spread stays one launch per vector: a two-vector spread needs 97 KB of LDS
-// per workgroup (two alpha slices and a 21-double moment row), one workgroup per CU, and measured 135 us
-// against 2 x 55 us at config C; the two-vector interpolation measured 51 us against
-// 2 x 34 us.
+// for ds_add_f64 holds).  The spread stays one launch per vector: a two-vector spread needs 98 KB of LDS
+// per workgroup at B = 4064 (two alpha slices and 21-double moment rows), one workgroup per CU, and
+// measured slower than two single-vector spreads; the two-vector interpolation measured
+// 51 us against 2 x 34 us.
 
 // y_v = beta y_v + alpha f^2 (sum_windows interp_v + mu x_v), v = 0, 1; H of vector v at H + v * h_rs
 template <int THREADS>
@@ -846,16 +728,9 @@ static void raise_lds_limit_once()
    (void)raised;
 }
 
-int launch_spread_multi(const AdditivePlan& P, int V, const double* const* xs, double* d_part, size_t part_rs,
-                        hipStream_t stream);
-
 int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream)
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
-   if (P.spread_variant == 2) {  // A/B only: k_spread_multi with one vector (gpw groups per workgroup)
-      const double* xs[1] = {d_x};
-      return launch_spread_multi(P, 1, xs, d_part, 0, stream);
-   }
    raise_lds_limit_once();
    const SpreadFn fn = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
    const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
@@ -946,46 +821,10 @@ int launch_interp_blocks(const AdditivePlan& P, double alpha, const double* d_x,
    return 0;
 }
 
-// y_v = beta y_v + alpha A x_v for two vectors: both spread in one pass over the layout (k_spread_multi; or one
-// single-vector spread each, P.spread2 = 0), both grids in one launch, one two-vector interpolation (1-D layouts,
-// whole-row handles)
+// y_v = beta y_v + alpha A x_v for two vectors: one spread per vector, both grids in one launch, one two-vector
+// interpolation (1-D layouts, whole-row handles).  A two-vector spread (both alpha slices and 21-double moment
+// rows in LDS, the layout and u^d shared) measured slower at every shape tried in round 4
 constexpr int kInterp2Threads = 1024;
-
-static size_t spread_multi_lds_bytes(const AdditivePlan& P, int V)
-{
-   return sizeof(double) * ((size_t)V * (P.B + kPad) + (size_t)P.CG * kNos * (V * kNC + 1));
-}
-
-int launch_spread_multi(const AdditivePlan& P, int V, const double* const* xs, double* d_part, size_t part_rs,
-                        hipStream_t stream)
-{
-   if (P.dl.ntiles == 0 || P.n == 0) return 0;
-   const int threads = (V > 1 && P.spread2 == 2) ? 1024 : 512;
-   const int gpw = std::min(std::max(P.spread2_gpw, 1), P.ngroups);
-   const int nslices = (P.ngroups + gpw - 1) / gpw;
-   const int gridx = ((P.nblocks + 7) / 8) * 8 * nslices;
-   const size_t lds = spread_multi_lds_bytes(P, V);
-   if (lds > 160 * 1024) return -1;
-   typedef void (*Fn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, const double*,
-                      const double*, const double*, int, int, int, int, int, int, int, double*, long long);
-   Fn fn = nullptr;
-   if (V == 1) fn = threads == 1024 ? k_spread_multi<1024, 1> : k_spread_multi<512, 1>;
-   if (V == 2) fn = threads == 1024 ? k_spread_multi<1024, 2> : k_spread_multi<512, 2>;
-   if (V == 4) fn = threads == 1024 ? k_spread_multi<1024, 4> : k_spread_multi<512, 4>;
-   if (!fn) return -1;
-   static bool attr[2][5] = {};
-   bool& a = attr[threads == 1024][V];
-   if (!a) {
-      (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipGetLastError();
-      a = true;
-   }
-   const double* x[4] = {xs[0], xs[1 % V], xs[2 % V], xs[3 % V]};
-   hipLaunchKernelGGL(fn, dim3(gridx), dim3(threads), lds, stream, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, x[0],
-                      x[1], x[2], x[3], P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, gpw, d_part, (long long)part_rs);
-   NFFT4GP_HIP_CHECK(hipGetLastError());
-   return 0;
-}
 
 int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double* x1, double beta, double* y0,
                    double* y1, hipStream_t stream)
@@ -1004,12 +843,7 @@ int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double
    // both vectors' partial grids in one allocation, so k_grid's per-vector stride stays inside it
    if (!P.d_part2) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part2, sizeof(double) * 2 * part_rs));
    if (!P.d_H2) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_H2, sizeof(double) * 2 * h_rs));
-   const double* xs[2] = {x0, x1};
-   if (P.spread2 > 0 && spread_multi_lds_bytes(P, 2) <= 160 * 1024) {
-      if (launch_spread_multi(P, 2, xs, P.d_part2, part_rs, stream)) return -1;
-   } else if (launch_spread(P, x0, P.d_part2, stream) || launch_spread(P, x1, P.d_part2 + part_rs, stream)) {
-      return -1;
-   }
+   if (launch_spread(P, x0, P.d_part2, stream) || launch_spread(P, x1, P.d_part2 + part_rs, stream)) return -1;
    hipLaunchKernelGGL(k_grid, dim3(P.nw, 2), dim3(kGridThreads), 0, stream, (const double*)P.d_part2, P.nblocks,
                       (const double*)P.d_w, (const double*)P.d_wd, P.d_H2, P.d_Hd, 0, 0, (long long)part_rs,
                       (long long)h_rs);

@@ -1,8 +1,7 @@
 """Nfft4GPAmdAdditiveMatSymvMulti: the additive matvec on several device vectors, two per pass of the
 interpolation over the layout (nfft_kernels.hip k_interp2).  Each column equals the single-vector
 Nfft4GPAdditiveNFFTMatSymv to the matvec's run-to-run rounding (LDS atomics: 1e-13 relative), for an even
-and an odd count, beta != 0, and multi-feature windows (served one vector at a time); the spread of the two
-vectors is one pass too (k_spread_multi, NFFT4GP_AMD_SPREAD2 = 1 / 2; 0: one spread per vector)."""
+and an odd count, beta != 0, and multi-feature windows (served one vector at a time)."""
 import ctypes as C
 
 import numpy as np
@@ -14,17 +13,14 @@ from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd im
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("spread2", ["0", "1", "2"])
 @pytest.mark.parametrize("nv,nw,dw,beta,n", [(4, 16, 1, 0.0, 30000), (5, 16, 1, 0.7, 30000), (3, 2, 3, 0.0, 30000),
                                              (2, 9, 1, 0.0, 100000)],
                          ids=["even", "odd_beta", "md", "b2032"])
-def test_multi_matches_single(torch_cuda, monkeypatch, spread2, nv, nw, dw, beta, n):
-    """Each column equals the single-vector matvec to 1e-15 (relative): the two-vector spread (k_spread_multi,
-    512 / 1024 threads) computes the same moments up to rounding (u^d formed once for both vectors), the
-    interpolation adds in LDS with ds_add_f64 in the wave order."""
+def test_multi_matches_single(torch_cuda, nv, nw, dw, beta, n):
+    """Each column equals the single-vector matvec to 1e-15 (relative): the same spread per vector, and the
+    two-vector interpolation adds in LDS with ds_add_f64 in the wave order."""
     import torch
 
-    monkeypatch.setenv("NFFT4GP_AMD_SPREAD2", spread2)
     d = nw * dw
     rng = np.random.default_rng(nv)
     X = np.asfortranarray(rng.random((n, d)))
