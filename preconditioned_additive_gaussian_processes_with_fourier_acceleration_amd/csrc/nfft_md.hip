@@ -61,13 +61,14 @@ __device__ __forceinline__ double tap_row(const int* uj, const double* pj, int d
 }
 
 // ---- fixed-point accumulation of the spread -----------------------------------------------------------
-// Every tap contribution a = x_j * prod psi is added as the 128-bit integer round(a * 2^s) to (lo, hi) pairs of
-// 64-bit accumulators (LDS ds_add_rtn_u64 / ds_add_u64, global atomic adds): the lo add returns the old value,
-// its wrap-around is the exact carry into hi, so the pair ends as the exact 128-bit sum whatever order the
-// atomics run in -- the spread, hence the matvec, is bitwise reproducible.  s_c = 124 - ilogb(B_c) with the
-// bound B_c = n max|x| psi_max^d_c >= every partial sum of component c (d_c features), so |sums| < 2^125
-// and one contribution is rounded at 2^-124 B_c (B_c can exceed a cell's value by ~2^22: still ~2^-100).
-// k_md_fix2f turns the pairs back into doubles.
+// Every tap contribution a = x_j * prod psi is scaled to the integer A = a 2^s_c (rounded at 2^0) and split as
+// A = H 2^32 + L with H = floor(A / 2^32) (signed) and L in [0, 2^32); the H's and the L's of a cell are summed
+// in two separate 64-bit integer accumulators (LDS ds_add_u64, then global atomic adds, no return values).
+// Integer adds are exact, so each cell's pair (sum H, sum L) -- and its value (sum H) 2^32 + sum L -- is the
+// same whatever order the atomics run in: the spread, hence the matvec, is bitwise reproducible.
+// s_c = 94 - ilogb(B_c) with the bound B_c = n max|x| psi_max^d_c >= every |partial sum| of component c (d_c
+// features), so |sum H| < 2^62 and sum L < n 2^32 <= 2^63 never overflow, and one contribution is rounded at
+// 2^-94 B_c (B_c can exceed a cell's value by ~2^22: still ~2^-72 of it).  k_md_fix2f forms the doubles.
 __global__ void k_md_absmax(const double* __restrict__ x, int n, unsigned long long* __restrict__ out)
 {
    unsigned long long m = 0ull;
@@ -82,30 +83,27 @@ __device__ __forceinline__ int fix_exp(const unsigned long long* xmax, double n,
 {
    double B = __longlong_as_double((long long)*xmax) * n;
    for (int t = 0; t < dc; t++) B *= psi_max;
-   return (B > 0.0 && B < 1e300) ? 124 - ilogb(B) : 0;
+   return (B > 0.0 && B < 1e300) ? 94 - ilogb(B) : 0;
 }
 
-// round(a 2^s) as a two's-complement 128-bit (lo, hi): a 2^(s-64) = hi + f with hi = floor, f in [0, 1),
-// lo = f 2^64 truncated (the bits below 2^0 of a 2^s)
-__device__ __forceinline__ void to_fix(double a, int s, unsigned long long& lo, long long& hi)
+// a 2^s = H 2^32 + L (truncated below 2^0): t = a 2^(s-32), H = floor(t), L = (t - H) 2^32
+__device__ __forceinline__ void to_fix(double a, int s, unsigned long long& L, long long& H)
 {
-   const double t = ldexp(a, s - 64);
+   const double t = ldexp(a, s - 32);
    const double h = floor(t);
    const double f = t - h;  // exact; 1.0 only when t is a tiny negative number (then the value rounds to 0)
-   hi = (long long)h + (f >= 1.0 ? 1 : 0);
-   lo = f >= 1.0 ? 0ull : (unsigned long long)ldexp(f, 64);
+   H = (long long)h + (f >= 1.0 ? 1 : 0);
+   L = f >= 1.0 ? 0ull : (unsigned long long)(unsigned int)ldexp(f, 32);
 }
 
-// acc[0] = lo, acc[1] = hi (LDS or global): exact 128-bit add
-__device__ __forceinline__ void fix_add(unsigned long long* acc, unsigned long long lo, long long hi)
+// acc[0] += L, acc[1] += H (LDS or global; exact integer adds, no carries needed)
+__device__ __forceinline__ void fix_add(unsigned long long* acc, unsigned long long L, long long H)
 {
-   const unsigned long long old = atomicAdd(acc, lo);
-   const unsigned long long carry = (old + lo < old) ? 1ull : 0ull;
-   const unsigned long long h = (unsigned long long)hi + carry;
-   if (h) atomicAdd(acc + 1, h);
+   if (L) atomicAdd(acc, L);
+   if (H) atomicAdd(acc + 1, (unsigned long long)H);
 }
 
-// grid[c][i] = (hi 2^64 + lo) 2^-s_c; blockIdx.y = component c; fx: [c][i][lo, hi]
+// grid[c][i] = ((sum H) 2^32 + sum L) 2^-s_c; blockIdx.y = component c; fx: [c][i][sum L, sum H]
 __global__ void k_md_fix2f(const MdComp* __restrict__ comps, const unsigned long long* __restrict__ fx, long long G,
                            const unsigned long long* __restrict__ xmax, double n, double psi_max,
                            double* __restrict__ grid)
@@ -115,16 +113,9 @@ __global__ void k_md_fix2f(const MdComp* __restrict__ comps, const unsigned long
    fx += 2 * (long long)c * G;
    grid += (long long)c * G;
    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (long long)gridDim.x * blockDim.x) {
-      const unsigned long long lo = fx[2 * i];
-      const long long hi = (long long)fx[2 * i + 1];
-      double v;
-      if (hi == 0)
-         v = (double)lo;
-      else if (hi == -1)
-         v = -(double)(0ull - lo);  // lo - 2^64
-      else
-         v = ldexp((double)hi, 64) + (double)lo;
-      grid[i] = ldexp(v, -e);
+      const double lo = (double)fx[2 * i];
+      const double hi = (double)(long long)fx[2 * i + 1];
+      grid[i] = ldexp(fma(hi, 4294967296.0, lo), -e);
    }
 }
 
