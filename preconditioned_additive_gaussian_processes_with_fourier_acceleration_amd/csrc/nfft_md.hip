@@ -149,8 +149,14 @@ __global__ __launch_bounds__(kMdThreads) void k_md_spread(const MdComp* __restri
 
 // Tiled spread: work item (component, tile, first, end) = the points of one 8^d tile of first-tap cells (a
 // chunk of them); their 10^d taps are summed into the tile's (8 + 9)^d footprint in LDS (ds_add_f64), and
-// the footprint's non-zero cells are then added to the grid (one global atomic per cell and item instead
-// of one per tap: 1000 per point in 3-D).  Thread = (point, tap row over axes 1..d-1) as k_md_spread.
+// the footprint's non-zero cells are then added to the grid (one global add per cell and item instead of
+// one per tap: 1000 per point in 3-D).
+// Deterministic: the footprint's lines along axis 0 (one per coordinate of axes 1..d-1: 17^(d-1) of them)
+// are dealt to the workgroup's waves (line % 8), and each wave walks every point of the item, 64 at a time
+// (lane = point), adding only the tap rows that fall on its own lines -- so every LDS cell is updated by one
+// wave, in program order (point chunks, then the point's rows), and the item's sums do not depend on the
+// wave schedule.  The items overlap at their halos, so the grid takes their sums in exact fixed point
+// (to_fix / fix_add above).
 constexpr int kMdTile = 8;
 constexpr int kMdFoot = kMdTile + kTaps - 1;  // 17
 constexpr int kMdSpreadThreads = 512;
@@ -164,16 +170,13 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
                                                                       const unsigned long long* __restrict__ xmax,
                                                                       double psi_max)
 {
-   extern __shared__ unsigned long long s_acc[];  // kMdFoot^d fixed-point (lo, hi) pairs
+   extern __shared__ double s_acc[];  // kMdFoot^d
+   constexpr int NW = kMdSpreadThreads / 64;
    const int4 it = items[blockIdx.x];
    const MdComp cp = comps[it.x];
    const int d = cp.d;
-   int foot = 1, ntile = 1;
-   for (int t = 0; t < d; t++) {
-      foot *= kMdFoot;
-      ntile *= kNos / kMdTile;
-   }
-   (void)ntile;
+   int foot = 1;
+   for (int t = 0; t < d; t++) foot *= kMdFoot;
    int lo[kMdMaxDim];
    {
       int rem = it.y;
@@ -182,43 +185,46 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
          rem /= kNos / kMdTile;
       }
    }
-   for (int e = threadIdx.x; e < 2 * foot; e += kMdSpreadThreads) s_acc[e] = 0ull;
+   for (int e = threadIdx.x; e < foot; e += kMdSpreadThreads) s_acc[e] = 0.0;
    __syncthreads();
-   const int ex = fix_exp(xmax, (double)n, psi_max, d);
+   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
    const int* pp = perm + (long long)it.x * n;
    const int npts = it.w - it.z;
-   const long long work = (long long)npts * cp.hicount;
-   for (long long w = threadIdx.x; w < work; w += kMdSpreadThreads) {
-      const int k = (int)(w / cp.hicount), hi = (int)(w % cp.hicount);
+   for (int k = lane; k < npts; k += 64) {
       const int j = pp[it.z + k];
       const int* uj = u + cp.u_off + (long long)j * d;
       const double* pj = psi + (cp.u_off + (long long)j * d) * kTaps;
-      // local footprint index of the row's first cell and the row's tap product
-      double wt = x[j];
-      int e = 0, stride = kMdFoot;
-      int rem = hi;
-      for (int t = 1; t < d; t++) {
-         const int lt = rem % kTaps;
-         rem /= kTaps;
-         e += (((uj[t] & (kNos - 1)) - lo[t]) + lt) * stride;
-         stride *= kMdFoot;
-         wt *= pj[t * kTaps + lt];
-      }
-      e += (uj[0] & (kNos - 1)) - lo[0];
+      const double xj = x[j];
+      const int x0 = (uj[0] & (kNos - 1)) - lo[0];
+      if (d == 1) {
+         if (wv == 0) {
 #pragma unroll
-      for (int lt = 0; lt < kTaps; lt++) {
-         unsigned long long lo;
-         long long hi;
-         to_fix(wt * pj[lt], ex, lo, hi);
-         fix_add(s_acc + 2 * (e + lt), lo, hi);
+            for (int lt = 0; lt < kTaps; lt++) atomicAdd(s_acc + x0 + lt, xj * pj[lt]);
+         }
+         continue;
+      }
+      const int y0 = (uj[1] & (kNos - 1)) - lo[1];
+      const int nz = d == 3 ? kTaps : 1;
+      const int z0 = d == 3 ? (uj[2] & (kNos - 1)) - lo[2] : 0;
+      for (int lz = 0; lz < nz; lz++) {
+         const int z = z0 + lz;
+         const double wz = d == 3 ? xj * pj[2 * kTaps + lz] : xj;
+         // this wave's lines y + 17 z (line % NW == wv): y = y0 + ly with ly in [0, kTaps)
+         int ly = ((wv - kMdFoot * z - y0) % NW + NW) % NW;
+         for (; ly < kTaps; ly += NW) {
+            const double wt = wz * pj[kTaps + ly];
+            double* row = s_acc + ((size_t)(y0 + ly) + (size_t)kMdFoot * z) * kMdFoot + x0;
+#pragma unroll
+            for (int lt = 0; lt < kTaps; lt++) atomicAdd(row + lt, wt * pj[lt]);
+         }
       }
    }
    __syncthreads();
+   const int ex = fix_exp(xmax, (double)n, psi_max, d);
    unsigned long long* g = grid + 2 * (long long)it.x * G;
    for (int e = threadIdx.x; e < foot; e += kMdSpreadThreads) {
-      const unsigned long long vlo = s_acc[2 * e];
-      const long long vhi = (long long)s_acc[2 * e + 1];
-      if (vlo == 0ull && vhi == 0) continue;
+      const double v = s_acc[e];
+      if (v == 0.0) continue;
       long long idx = 0, stride = 1;
       int rem = e;
       for (int t = 0; t < d; t++) {
@@ -226,7 +232,10 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
          rem /= kMdFoot;
          stride *= kNos;
       }
-      fix_add(g + 2 * idx, vlo, vhi);
+      unsigned long long L;
+      long long H;
+      to_fix(v, ex, L, H);
+      fix_add(g + 2 * idx, L, H);
    }
 }
 
@@ -801,7 +810,7 @@ static int md_spread_fix(const AdditivePlan& P, const double* d_x, double psi_ma
          (void)hipGetLastError();
          attr = true;
       }
-      hipLaunchKernelGGL(k_md_spread_tiled, dim3(D.nitems), dim3(kMdSpreadThreads), 2 * sizeof(unsigned long long) * foot,
+      hipLaunchKernelGGL(k_md_spread_tiled, dim3(D.nitems), dim3(kMdSpreadThreads), sizeof(double) * foot,
                          s, D.d_comps, D.d_items, D.d_perm, D.d_u, D.d_psi, d_x, P.n, D.d_gfix, D.G,
                          (const unsigned long long*)D.d_xmax, psi_max);
       NFFT4GP_HIP_CHECK(hipGetLastError());
