@@ -304,7 +304,8 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
       fprintf(stderr, "nfft4gp_amd: layout setup: centre/scale/quantize %.1f ms, coordinate upload %.1f ms, "
                       "layout (%s) %.1f ms\n", ms(t0, t1), ms(t1, t2), rc_dev ? "host" : "GPU", ms(t2, t3));
    }
-   NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part, sizeof(double) * (size_t)std::max(1, P.nblocks) * P.nw * kNos));
+   P.nparts = P.spread_variant == 2 ? (P.nblocks + std::max(1, P.spread_bpr) - 1) / std::max(1, P.spread_bpr) : P.nblocks;
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part, sizeof(double) * (size_t)std::max(1, P.nparts) * P.nw * kNos));
    dfree(P.d_dot_part);
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_dot_part, sizeof(double) * (size_t)std::max(1, P.nblocks)));
    if (!P.d_dot_ticket) {
@@ -383,7 +384,7 @@ int plan_apply_dev(PlanExt* E, int grad, double alpha, const double* d_x, double
       (void)hipEventRecord(rec.ev[1], s);
       (void)hipEventRecord(rec.ev[2], s);
    }
-   if (!rc) rc = P.md.on ? md_grid(P, P.md.d_grid, grad, s) : launch_grid(P, P.d_part, P.nblocks, grad, s);
+   if (!rc) rc = P.md.on ? md_grid(P, P.md.d_grid, grad, s) : launch_grid(P, P.d_part, P.nparts, grad, s);
    if (mdt) {
       (void)hipEventRecord(rec.ev[3], s);
       (void)hipEventRecord(rec.ev[4], s);
@@ -512,6 +513,7 @@ void env_layout(AdditivePlan& P)
       if (v >= 1 && v <= 64) P.CG = v;
    }
    if (const char* e = getenv("NFFT4GP_AMD_SPREAD_VARIANT")) P.spread_variant = atoi(e);
+   if (const char* e = getenv("NFFT4GP_AMD_SPREAD_BPR")) P.spread_bpr = std::max(1, atoi(e));
 }
 
 void* additive_create(double* data, int n_global, int ldim, int* windows, int nwindows, int dwindows, int rb, int re)
@@ -581,7 +583,7 @@ int additive_matvec_dot(void* str, const double* d_x, double* d_y, double* d_dot
       return md_interp(P, 0, 1.0, d_x, 0.0, d_y, s, d_dot);
    }
    if (launch_spread(P, d_x, P.d_part, s)) return -1;
-   if (launch_grid(P, P.d_part, P.nblocks, 0, s)) return -1;
+   if (launch_grid(P, P.d_part, P.nparts, 0, s)) return -1;
    return launch_interp(P, 0, 1.0, d_x, 0.0, d_y, s, d_dot);
 }
 }  // namespace nfft4gp_amd
@@ -613,7 +615,7 @@ int additive_matvec_chunked(void* str, double alpha, const double* d_x, double* 
    AdditivePlan& P = E->P;
    if (P.md.on || P.timing || P.row_begin != 0 || P.row_end != P.n_global || P.nblocks == 0) return -1;
    hipStream_t s = current_stream();
-   if (launch_spread(P, d_x, P.d_part, s) || launch_grid(P, P.d_part, P.nblocks, 0, s)) return -1;
+   if (launch_spread(P, d_x, P.d_part, s) || launch_grid(P, P.d_part, P.nparts, 0, s)) return -1;
    nchunks = std::max(1, std::min(nchunks, P.nblocks));
    for (int c = 0; c < nchunks; c++) {
       const int b0 = (int)((long long)P.nblocks * c / nchunks), b1 = (int)((long long)P.nblocks * (c + 1) / nchunks);
@@ -871,7 +873,7 @@ int Nfft4GPAmdKernelBench(void* str, int which, int grad, int reps, const double
       else if (which == 0)
          rc = launch_spread(P, x, P.d_part, s);
       else if (which == 1)
-         rc = launch_grid(P, P.d_part, P.nblocks, grad, s);
+         rc = launch_grid(P, P.d_part, P.nparts, grad, s);
       else
          rc = launch_interp(P, grad, 1.0, x, 0.0, y, s);
       if (rc) return -1;
