@@ -179,10 +179,8 @@ struct AdditivePlan {
    double diag = 1.0;    // 1: this handle adds the mu x (and grad f^2 x) terms; 0: a component shard without them
    // layout
    int B = kMaxBlock, CG = 3, ngroups = 0, nblocks = 0;  // CG = 3: 3 spread workgroups fit a CU's LDS
-   int spread_variant = 0;  // 0: the spread; 1: the same with timeline stamps (NFFT4GP_AMD_SPREAD_VARIANT, tools/);
-                            // 2: workgroups over ranges of spread_bpr blocks (NFFT4GP_AMD_SPREAD_BPR)
-   int spread_bpr = 4;
-   int nparts = 0;          // partial grids per window the spread writes: nblocks, or the block ranges (variant 2)
+   int spread_variant = 0;  // 0: the spread; 1: the same with timeline stamps (NFFT4GP_AMD_SPREAD_VARIANT, tools/)
+   int nparts = 0;          // partial grids per window the spread writes (one per block)
    DevLayout dl;
    // device buffers
    double* d_part = nullptr;  // [nblocks][nw][64]

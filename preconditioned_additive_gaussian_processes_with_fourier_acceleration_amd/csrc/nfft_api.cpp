@@ -304,7 +304,7 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
       fprintf(stderr, "nfft4gp_amd: layout setup: centre/scale/quantize %.1f ms, coordinate upload %.1f ms, "
                       "layout (%s) %.1f ms\n", ms(t0, t1), ms(t1, t2), rc_dev ? "host" : "GPU", ms(t2, t3));
    }
-   P.nparts = P.spread_variant == 2 ? (P.nblocks + std::max(1, P.spread_bpr) - 1) / std::max(1, P.spread_bpr) : P.nblocks;
+   P.nparts = P.nblocks;
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part, sizeof(double) * (size_t)std::max(1, P.nparts) * P.nw * kNos));
    dfree(P.d_dot_part);
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_dot_part, sizeof(double) * (size_t)std::max(1, P.nblocks)));
@@ -513,7 +513,6 @@ void env_layout(AdditivePlan& P)
       if (v >= 1 && v <= 64) P.CG = v;
    }
    if (const char* e = getenv("NFFT4GP_AMD_SPREAD_VARIANT")) P.spread_variant = atoi(e);
-   if (const char* e = getenv("NFFT4GP_AMD_SPREAD_BPR")) P.spread_bpr = std::max(1, atoi(e));
 }
 
 void* additive_create(double* data, int n_global, int ldim, int* windows, int nwindows, int dwindows, int rb, int re)

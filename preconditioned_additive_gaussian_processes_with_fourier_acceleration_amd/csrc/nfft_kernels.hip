@@ -198,83 +198,6 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    }
 }
 
-// Block ranges (spread variant 2): one workgroup = one group of CG windows x a range of `bpr` consecutive
-// blocks.  The moment table accumulates over the whole range (moments are sums over points, whatever their
-// block), so the fold, the table clear and the partial-grid store happen once per range instead of once per
-// block; each block's alpha slice is staged in turn (a barrier before it is overwritten).  part: [comp][range]
-// [cell] (nranges partial grids per window for k_grid).  XCD-aware: the groups of one range share an XCD.
-template <int THREADS>
-__global__ __launch_bounds__(THREADS, 6) void k_spread_range(const uint16_t* __restrict__ meta,
-                                                            const uint32_t* __restrict__ lo,
-                                                            const uint32_t* __restrict__ qarr,
-                                                            const int* __restrict__ tile_off,
-                                                            const double* __restrict__ x, int n, int B, int nblocks,
-                                                            int ngroups, int CG, int nw, int bpr, int nranges,
-                                                            double* __restrict__ part)
-{
-   extern __shared__ __attribute__((aligned(16))) double smem[];
-   const int Bp = B + kPad;
-   double* s_alpha = smem;
-   double* s_mom = smem + Bp;
-   const int xcd = blockIdx.x & 7;
-   const int rest = blockIdx.x >> 3;
-   const int g = rest % ngroups;
-   const int range = (rest / ngroups) * 8 + xcd;
-   if (range >= nranges) return;
-   const int b0 = range * bpr, b1 = min(nblocks, b0 + bpr);
-   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-   constexpr int nwaves = THREADS / 64;
-   const int c0 = g * CG;
-   for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
-   for (int b = b0; b < b1; b++) {
-      TileRegs cur;
-      const int t1 = tile_off[b * ngroups + g + 1];
-      int t = tile_off[b * ngroups + g] + wave;
-      if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
-      const int base = b * B;
-      stage_block_glds<THREADS>(s_alpha, x, base, min(B, n - base), B);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      for (; t < t1; t += nwaves) {
-         double acc[kNC];
-#pragma unroll
-         for (int d = 0; d < kNC; d++) acc[d] = 0.0;
-#pragma unroll
-         for (int r = 0; r < kR; r++) {
-            const uint32_t loc = slot_loc(cur, r);
-            const double u = q_to_u(cur.qq[r]);
-            double tpow = s_alpha[loc];
-            acc[0] += tpow;
-#pragma unroll
-            for (int d = 1; d < kNC; d++) {
-               tpow *= u;
-               acc[d] += tpow;
-            }
-         }
-         const int comp_local = (int)(cur.mt >> 6) - c0;
-         const int cell = (int)(cur.mt & 63u);
-         double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
-#pragma unroll
-         for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
-         if (t + nwaves < t1) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
-      }
-      __syncthreads();  // every read of this block's alpha slice (and every moment flush) is done
-   }
-   const int ncomp = min(CG, nw - c0);
-   for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
-      const int cl = idx / kNos;
-      const int gi = idx % kNos;
-      double v = 0.0;
-#pragma unroll 1
-      for (int tp = 0; tp < kTaps; tp++) {
-         const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
-#pragma unroll
-         for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
-      }
-      part[((size_t)(c0 + cl) * nranges + range) * kNos + gi] = v;  // [comp][range][cell]
-   }
-}
-
 // copy the diagnostic timeline out (tools/ only)
 extern "C" int Nfft4GPAmdDebugStamps(unsigned long long* out, int nwg)
 {
@@ -809,23 +732,6 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
    raise_lds_limit_once();
-   if (P.spread_variant == 2) {
-      static bool attr = false;
-      if (!attr) {
-         (void)hipFuncSetAttribute((const void*)k_spread_range<kSpreadThreads>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-         (void)hipGetLastError();
-         attr = true;
-      }
-      const int bpr = std::max(1, P.spread_bpr);
-      const int nranges = P.nparts;
-      const int gridx = ((nranges + 7) / 8) * 8 * P.ngroups;
-      launch_ev(k_spread_range<kSpreadThreads>, dim3(gridx), dim3(kSpreadThreads), spread_lds_bytes(P), stream,
-                P.kev ? P.kev + 0 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks,
-                P.ngroups, P.CG, P.nw, bpr, nranges, d_part);
-      NFFT4GP_HIP_CHECK(hipGetLastError());
-      return 0;
-   }
    const SpreadFn fn = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
    const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
    launch_ev(fn, dim3(gridx), dim3(kSpreadThreads), spread_lds_bytes(P), stream, P.kev ? P.kev + 0 : nullptr,
