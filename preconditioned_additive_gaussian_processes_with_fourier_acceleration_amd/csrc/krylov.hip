@@ -189,6 +189,49 @@ __global__ __launch_bounds__(kBDThreads) void k_block_dots(const double* __restr
    }
 }
 
+// The same partials with 16-byte loads (two rows per lane, n even) and KB = 16 basis vectors per workgroup:
+// 16 loads in flight per lane and half the re-reads of w (once per KB columns)
+constexpr int kBD2 = 16;
+__global__ __launch_bounds__(kBDThreads) void k_block_dots_x2(const double* __restrict__ w,
+                                                              const double* __restrict__ V, size_t n, int m,
+                                                              int with_norm, double* __restrict__ part, int ldp)
+{
+   __shared__ double s[kBDThreads / 64][kBD2];
+   const int g0 = blockIdx.y * kBD2;
+   const int cnt = min(kBD2, m + with_norm - g0);
+   const int nv = m - g0;
+   double acc[kBD2];
+#pragma unroll
+   for (int j = 0; j < kBD2; j++) acc[j] = 0.0;
+   const size_t n2 = n / 2;
+   const double2* w2 = reinterpret_cast<const double2*>(w);
+   const size_t stride = (size_t)gridDim.x * kBDThreads;
+   for (size_t r = (size_t)blockIdx.x * kBDThreads + threadIdx.x; r < n2; r += stride) {
+      const double2 wr = w2[r];
+      double2 v[kBD2];
+#pragma unroll
+      for (int j = 0; j < kBD2; j++)
+         v[j] = j < nv && j < cnt ? reinterpret_cast<const double2*>(V + (size_t)(g0 + j) * n)[r]
+                                  : (j < cnt ? wr : make_double2(0.0, 0.0));
+#pragma unroll
+      for (int j = 0; j < kBD2; j++) acc[j] = fma(v[j].y, wr.y, fma(v[j].x, wr.x, acc[j]));
+   }
+   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+   for (int j = 0; j < kBD2; j++) {
+      double a = acc[j];
+      for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off, 64);
+      if (lane == 0) s[wave][j] = a;
+   }
+   __syncthreads();
+   if (threadIdx.x < cnt) {
+      double t = 0.0;
+#pragma unroll
+      for (int q = 0; q < kBDThreads / 64; q++) t += s[q][threadIdx.x];
+      part[(size_t)blockIdx.x * ldp + g0 + threadIdx.x] = t;
+   }
+}
+
 // h[i] = sum_b part[b ldp + i] (fixed order: 16 strands over blocks b = g mod 16, then the strands) for
 // i < m; column i = m (the norm column of k_block_dots, when mc = m + 1) lands in h[m + 1]
 __global__ __launch_bounds__(1024) void k_block_reduce(const double* __restrict__ part, int nblk, int ldp, int mc,
@@ -238,6 +281,60 @@ __global__ __launch_bounds__(kKThreads) void k_block_update(double* __restrict__
             const size_t i = i0 + (size_t)e * kKThreads;
             wv[e] = fma(-hj, i < n ? zj[i] : 0.0, wv[e]);
          }
+      }
+#pragma unroll
+      for (int e = 0; e < kKEPT; e++) {
+         const size_t i = i0 + (size_t)e * kKThreads;
+         if (i < n) w[i] = wv[e];
+         acc = fma(wv[e], wv[e], acc);
+      }
+   }
+   acc = block_sum0<kKThreads>(acc);
+   double tot;
+   if (grid_total<kKThreads>(acc, part, ticket, &tot) && threadIdx.x == 0) *out = tot;
+}
+
+// k_block_update with four columns' loads in flight per step (16 per lane): the same operations in the same
+// order (w -= h_j z_j for j = 0, 1, ...), so the result is bitwise k_block_update's
+__global__ __launch_bounds__(kKThreads) void k_block_update_x4(double* __restrict__ w, const double* __restrict__ Z,
+                                                               size_t n, const double* __restrict__ h, int m,
+                                                               double* __restrict__ part,
+                                                               unsigned int* __restrict__ ticket,
+                                                               double* __restrict__ out)
+{
+   extern __shared__ double s_h[];
+   for (int j = threadIdx.x; j < m; j += kKThreads) s_h[j] = h[j];
+   __syncthreads();
+   double acc = 0.0;
+   const size_t stride = (size_t)gridDim.x * kKThreads * kKEPT;
+   for (size_t i0 = (size_t)blockIdx.x * kKThreads * kKEPT + threadIdx.x; i0 < n; i0 += stride) {
+      double wv[kKEPT];
+      bool in[kKEPT];
+#pragma unroll
+      for (int e = 0; e < kKEPT; e++) {
+         const size_t i = i0 + (size_t)e * kKThreads;
+         in[e] = i < n;
+         wv[e] = in[e] ? w[i] : 0.0;
+      }
+      int j = 0;
+      for (; j + 4 <= m; j += 4) {
+         double z[4][kKEPT];
+#pragma unroll
+         for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int e = 0; e < kKEPT; e++) z[q][e] = in[e] ? Z[(size_t)(j + q) * n + i0 + (size_t)e * kKThreads] : 0.0;
+#pragma unroll
+         for (int q = 0; q < 4; q++) {
+            const double hj = s_h[j + q];
+#pragma unroll
+            for (int e = 0; e < kKEPT; e++) wv[e] = fma(-hj, z[q][e], wv[e]);
+         }
+      }
+      for (; j < m; j++) {
+         const double hj = s_h[j];
+#pragma unroll
+         for (int e = 0; e < kKEPT; e++)
+            wv[e] = fma(-hj, in[e] ? Z[(size_t)j * n + i0 + (size_t)e * kKThreads] : 0.0, wv[e]);
       }
 #pragma unroll
       for (int e = 0; e < kKEPT; e++) {
@@ -343,14 +440,24 @@ struct Ctx {
       const int mc = m + with_norm;
       // h[m], h[m + 1] take part in the all-reduce below even when this pass does not write them
       if (comm) NFFT4GP_HIP_CHECK(hipMemsetAsync(h + m, 0, sizeof(double) * 2, s));
-      hipLaunchKernelGGL(k_block_dots, dim3(nb, (mc + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m, with_norm,
-                         g_k.bpart, KScratch::kScal);
+      static const int bv = getenv("NFFT4GP_AMD_BGS_VARIANT") ? atoi(getenv("NFFT4GP_AMD_BGS_VARIANT")) : 1;
+      const bool x2 = bv == 1 && n % 2 == 0;
+      if (x2)
+         hipLaunchKernelGGL(k_block_dots_x2, dim3(nb, (mc + kBD2 - 1) / kBD2), dim3(kBDThreads), 0, s, w, V, n, m,
+                            with_norm, g_k.bpart, KScratch::kScal);
+      else
+         hipLaunchKernelGGL(k_block_dots, dim3(nb, (mc + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m,
+                            with_norm, g_k.bpart, KScratch::kScal);
       hipLaunchKernelGGL(k_block_reduce, dim3((mc + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, mc, m,
                          h);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       if (red(h, m + 2)) return -1;  // the projections and the norm before them, summed over the row shards
-      hipLaunchKernelGGL(k_block_update, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, Z, n, h, m,
-                         g_k.part, g_k.ticket, h + m);
+      if (bv == 1)
+         hipLaunchKernelGGL(k_block_update_x4, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, Z, n, h, m,
+                            g_k.part, g_k.ticket, h + m);
+      else
+         hipLaunchKernelGGL(k_block_update, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, Z, n, h, m,
+                            g_k.part, g_k.ticket, h + m);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return red(h + m, 1);
    }
@@ -445,7 +552,8 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
       return -1;
    }
    double *V = nullptr, *Z = nullptr;
-   if (dmalloc(&V, n * (size_t)(kdim + 1)) || dmalloc(&Z, n * (size_t)(kdim + 1))) return -1;
+   // without a preconditioner z_i = v_i: the combination reads V and no Z is kept
+   if (dmalloc(&V, n * (size_t)(kdim + 1)) || (cb.prec && dmalloc(&Z, n * (size_t)(kdim + 1)))) return -1;
    auto cleanup = [&]() {
       (void)hipStreamSynchronize(c.s);
       (void)hipFree(V);
@@ -488,16 +596,15 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
          i++;
          iter++;
          v = V + (size_t)(i - 1) * n;
-         double* z = Z + (size_t)(i - 1) * n;
          w = V + (size_t)i * n;
          if (cb.prec) {
+            double* z = Z + (size_t)(i - 1) * n;
             if (cb.solve(z, v) || cb.apply(1.0, z, 0.0, w)) {
                free(rel);
                cleanup();
                return -1;
             }
          } else {
-            c.copy(z, v);
             if (cb.apply(1.0, v, 0.0, w)) {
                free(rel);
                cleanup();
@@ -565,7 +672,7 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
          for (int j = k + 1; j < i; j++) rs[k] -= H[(size_t)j * (kdim + 1) + k] * rs[j];
          rs[k] /= H[(size_t)k * (kdim + 1) + k];
       }
-      if (c.combine(x, Z, i, rs.data())) return -1;
+      if (c.combine(x, cb.prec ? Z : V, i, rs.data())) return -1;
       if (normr <= tolr) break;
       // restart (fgmres.c:236-243): v = rhs - A x through w; normr keeps the Givens estimate
       v = V;

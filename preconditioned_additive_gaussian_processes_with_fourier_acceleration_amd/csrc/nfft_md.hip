@@ -692,6 +692,10 @@ int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
    // tiled spread: per component, a counting sort of the points by the tile of their first tap cell, then
    // items of at most ~2e6 / 10^d points (up to 3 features; 4-feature handles use the untiled kernels)
    if (D.maxd <= kMdTiledMaxDim) {
+      // taps per work item (A/B knob NFFT4GP_AMD_MD_CHUNK; the results do not depend on it beyond the spread's
+      // fixed-point rounding, which is exact)
+      long long chunk_taps = 2000000;
+      if (const char* e = getenv("NFFT4GP_AMD_MD_CHUNK")) chunk_taps = std::max(1000LL, atoll(e));
       std::vector<int> perm((size_t)P.nw * n);
       std::vector<std::vector<int4>> citems(P.nw);
       auto sort_comp = [&](int c) {
@@ -718,7 +722,7 @@ int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
          std::vector<int> pos(cnt.begin(), cnt.end() - 1);
          int* pc = perm.data() + (size_t)c * n;
          for (int j = 0; j < n; j++) pc[pos[tile[j]]++] = j;
-         const int chunk = std::max(256, 2000000 / taps);
+         const int chunk = (int)std::max<long long>(256, chunk_taps / taps);
          for (int t = 0; t < ntiles; t++)
             for (int b = cnt[t]; b < cnt[t + 1]; b += chunk) items.push_back(make_int4(c, t, b, std::min(cnt[t + 1], b + chunk)));
       };
