@@ -312,8 +312,8 @@ def run_fgmres(op, torch, n, rng_seed=906, tol=1e-6, kdim=1000, maxits=1000, l=1
     metric's own l = 1, where the NFFT-approximated kernel is indefinite and CG cannot run.  The spectrum
     has ~1000 outlying Fourier modes around mu = 0.01, so a restarted FGMRES stagnates (restart 50: 2.7e-2
     after 3000 iterations; tools/fgmres_probe.py) and it runs unrestarted (kdim = maxits = 1000; converges
-    in ~330).  ortho 0: the reference's modified Gram-Schmidt; 1: two block classical passes
-    (Nfft4GPAmdSetFgmresOrtho).  With a distributed operator every rank runs it on its rows (time: max over
+    in ~330).  ortho 0: the reference's modified Gram-Schmidt; 1: block classical Gram-Schmidt with the DGKS
+    second pass; 2: delayed CGS2, two basis sweeps per step (Nfft4GPAmdSetFgmresOrtho).  With a distributed operator every rank runs it on its rows (time: max over
     ranks)."""
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
     assert op.setup(amd.GAUSSIAN, f=1.0, l=l, mu=0.01) == 0
@@ -334,12 +334,13 @@ def run_fgmres(op, torch, n, rng_seed=906, tol=1e-6, kdim=1000, maxits=1000, l=1
         tt = torch.tensor([t], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
-    p = "fgmres_" if ortho == 0 else "fgmres_cgs2_"
-    extra = {} if ortho == 0 else {p + "second_passes": int(amd.lib().Nfft4GPAmdFgmresSecondPasses())}
+    p = ["fgmres_", "fgmres_cgs2_", "fgmres_dcgs2_"][ortho]
+    extra = {p + "second_passes": int(amd.lib().Nfft4GPAmdFgmresSecondPasses())} if ortho == 1 else {}
     return {**extra, p + "time_s": t, p + "iters": iters, p + "rel_res": relres, p + "converged": relres <= tol,
             p + "tol": tol, p + "l": l, p + "kdim": kdim, p + "ms_per_iter": 1e3 * t / max(iters, 1),
-            p + "ortho": "modified Gram-Schmidt (fgmres.c)" if ortho == 0 else
-            "block classical Gram-Schmidt, second pass by the DGKS test"}
+            p + "ortho": ["modified Gram-Schmidt (fgmres.c)",
+                          "block classical Gram-Schmidt, second pass by the DGKS test",
+                          "delayed CGS2 (second pass lagged one step, two basis sweeps per step)"][ortho]}
 
 
 def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000, l_pcg=0.1, schur="fsai",
@@ -583,6 +584,7 @@ def main():
         pcg.update(run_loss(op, torch, n, d, X))
         pcg.update(run_fgmres(op, torch, n))
         pcg.update(run_fgmres(op, torch, n, ortho=1))
+        pcg.update(run_fgmres(op, torch, n, ortho=2))
         pcg.update(run_pcg_single(op, torch, n))
         # the preconditioned legs are the metric's "PCG time with AFN rank=512": an exception here ends the
         # bench (no silent *_error key)
@@ -738,6 +740,7 @@ def main():
             result["pcg_impl"] = f"Nfft4GPSolverPcg on Nfft4GPAmdDistMatSymv ({args.partition}), device-controlled"
             result.update(run_fgmres(op, torch, n, rows=(rb, re), dist=dist))
             result.update(run_fgmres(op, torch, n, rows=(rb, re), dist=dist, ortho=1))
+            result.update(run_fgmres(op, torch, n, rows=(rb, re), dist=dist, ortho=2))
             result.update(run_loss(op, torch, n, d, X, rows=(rb, re), dist=dist))
         result["partition_" + alt["partition"]] = alt
     if rank == 0:

@@ -153,10 +153,13 @@ int bd_grid(size_t n)
 
 // part[blockIdx.x * ldp + i] = sum over this block's rows r of w[r] V[i n + r], i in [g0, g0 + kBD) & < m;
 // with_norm: column m is w itself (part[.. + m] sums ||w||^2)
+// c_after / c_before (optional): a second pass that runs only when the DGKS test of k_block_update holds
 __global__ __launch_bounds__(kBDThreads) void k_block_dots(const double* __restrict__ w, const double* __restrict__ V,
                                                            size_t n, int m, int with_norm, double* __restrict__ part,
-                                                           int ldp)
+                                                           int ldp, const double* __restrict__ c_after = nullptr,
+                                                           const double* __restrict__ c_before = nullptr)
 {
+   if (c_after && !(sqrt(*c_after) < 0.7071 * sqrt(*c_before))) return;
    __shared__ double s[kBDThreads / 64][kBD];
    const int g0 = blockIdx.y * kBD;
    const int cnt = min(kBD, m + with_norm - g0);
@@ -176,49 +179,6 @@ __global__ __launch_bounds__(kBDThreads) void k_block_dots(const double* __restr
    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
    for (int j = 0; j < kBD; j++) {
-      double a = acc[j];
-      for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off, 64);
-      if (lane == 0) s[wave][j] = a;
-   }
-   __syncthreads();
-   if (threadIdx.x < cnt) {
-      double t = 0.0;
-#pragma unroll
-      for (int q = 0; q < kBDThreads / 64; q++) t += s[q][threadIdx.x];
-      part[(size_t)blockIdx.x * ldp + g0 + threadIdx.x] = t;
-   }
-}
-
-// The same partials with 16-byte loads (two rows per lane, n even) and KB = 16 basis vectors per workgroup:
-// 16 loads in flight per lane and half the re-reads of w (once per KB columns)
-constexpr int kBD2 = 16;
-__global__ __launch_bounds__(kBDThreads) void k_block_dots_x2(const double* __restrict__ w,
-                                                              const double* __restrict__ V, size_t n, int m,
-                                                              int with_norm, double* __restrict__ part, int ldp)
-{
-   __shared__ double s[kBDThreads / 64][kBD2];
-   const int g0 = blockIdx.y * kBD2;
-   const int cnt = min(kBD2, m + with_norm - g0);
-   const int nv = m - g0;
-   double acc[kBD2];
-#pragma unroll
-   for (int j = 0; j < kBD2; j++) acc[j] = 0.0;
-   const size_t n2 = n / 2;
-   const double2* w2 = reinterpret_cast<const double2*>(w);
-   const size_t stride = (size_t)gridDim.x * kBDThreads;
-   for (size_t r = (size_t)blockIdx.x * kBDThreads + threadIdx.x; r < n2; r += stride) {
-      const double2 wr = w2[r];
-      double2 v[kBD2];
-#pragma unroll
-      for (int j = 0; j < kBD2; j++)
-         v[j] = j < nv && j < cnt ? reinterpret_cast<const double2*>(V + (size_t)(g0 + j) * n)[r]
-                                  : (j < cnt ? wr : make_double2(0.0, 0.0));
-#pragma unroll
-      for (int j = 0; j < kBD2; j++) acc[j] = fma(v[j].y, wr.y, fma(v[j].x, wr.x, acc[j]));
-   }
-   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-   for (int j = 0; j < kBD2; j++) {
       double a = acc[j];
       for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off, 64);
       if (lane == 0) s[wave][j] = a;
@@ -254,54 +214,24 @@ __global__ __launch_bounds__(1024) void k_block_reduce(const double* __restrict_
    }
 }
 
-// w -= sum_{j < m} h[j] Z[j n + .] (j in order), then *out = ||w||^2 (fixed-order grid reduction)
+// w -= sum_{j < m} h[j] Z[j n + .] (j in order, four columns' loads in flight per step), then *out = ||w||^2
+// (fixed-order grid reduction).  c_after / c_before (optional device scalars, the squared norms after and
+// before the previous pass): the pass runs only when the DGKS test sqrt(after) < 0.7071 sqrt(before) holds --
+// the same in every workgroup -- and *c_flag records the decision (1 / 0) for the host
 __global__ __launch_bounds__(kKThreads) void k_block_update(double* __restrict__ w, const double* __restrict__ Z,
                                                             size_t n, const double* __restrict__ h, int m,
                                                             double* __restrict__ part,
                                                             unsigned int* __restrict__ ticket,
-                                                            double* __restrict__ out)
+                                                            double* __restrict__ out,
+                                                            const double* __restrict__ c_after = nullptr,
+                                                            const double* __restrict__ c_before = nullptr,
+                                                            double* __restrict__ c_flag = nullptr)
 {
-   extern __shared__ double s_h[];
-   for (int j = threadIdx.x; j < m; j += kKThreads) s_h[j] = h[j];
-   __syncthreads();
-   double acc = 0.0;
-   const size_t stride = (size_t)gridDim.x * kKThreads * kKEPT;
-   for (size_t i0 = (size_t)blockIdx.x * kKThreads * kKEPT + threadIdx.x; i0 < n; i0 += stride) {
-      double wv[kKEPT];
-#pragma unroll
-      for (int e = 0; e < kKEPT; e++) {
-         const size_t i = i0 + (size_t)e * kKThreads;
-         wv[e] = i < n ? w[i] : 0.0;
-      }
-      for (int j = 0; j < m; j++) {
-         const double hj = s_h[j];
-         const double* zj = Z + (size_t)j * n;
-#pragma unroll
-         for (int e = 0; e < kKEPT; e++) {
-            const size_t i = i0 + (size_t)e * kKThreads;
-            wv[e] = fma(-hj, i < n ? zj[i] : 0.0, wv[e]);
-         }
-      }
-#pragma unroll
-      for (int e = 0; e < kKEPT; e++) {
-         const size_t i = i0 + (size_t)e * kKThreads;
-         if (i < n) w[i] = wv[e];
-         acc = fma(wv[e], wv[e], acc);
-      }
+   if (c_after) {
+      const bool again = sqrt(*c_after) < 0.7071 * sqrt(*c_before);
+      if (blockIdx.x == 0 && threadIdx.x == 0) *c_flag = again ? 1.0 : 0.0;
+      if (!again) return;
    }
-   acc = block_sum0<kKThreads>(acc);
-   double tot;
-   if (grid_total<kKThreads>(acc, part, ticket, &tot) && threadIdx.x == 0) *out = tot;
-}
-
-// k_block_update with four columns' loads in flight per step (16 per lane): the same operations in the same
-// order (w -= h_j z_j for j = 0, 1, ...), so the result is bitwise k_block_update's
-__global__ __launch_bounds__(kKThreads) void k_block_update_x4(double* __restrict__ w, const double* __restrict__ Z,
-                                                               size_t n, const double* __restrict__ h, int m,
-                                                               double* __restrict__ part,
-                                                               unsigned int* __restrict__ ticket,
-                                                               double* __restrict__ out)
-{
    extern __shared__ double s_h[];
    for (int j = threadIdx.x; j < m; j += kKThreads) s_h[j] = h[j];
    __syncthreads();
@@ -348,6 +278,138 @@ __global__ __launch_bounds__(kKThreads) void k_block_update_x4(double* __restric
    if (grid_total<kKThreads>(acc, part, ticket, &tot) && threadIdx.x == 0) *out = tot;
 }
 
+// ---- DCGS2 (delayed classical Gram-Schmidt with re-orthogonalisation; FGMRES ortho 2) ----------------------
+// Sweep 1 of a step: S[k] = (v_k, a) and T[k] = (v_k, b) for the m basis columns (the last of them is a itself,
+// the step's provisional column) -- the previous column's second pass and this column's first pass read the
+// basis once together.  Partials: part[blk ldp + k] (S), part[blk ldp + m + k] (T); b may be null.
+constexpr int kBD2 = 16;
+__global__ __launch_bounds__(kBDThreads) void k_block_dots_ab(const double* __restrict__ a, const double* __restrict__ b,
+                                                              const double* __restrict__ V, size_t n, int m,
+                                                              double* __restrict__ part, int ldp)
+{
+   __shared__ double s[kBDThreads / 64][2 * kBD2];
+   const int g0 = blockIdx.y * kBD2;
+   const int cnt = min(kBD2, m - g0);
+   double sa[kBD2], sb[kBD2];
+#pragma unroll
+   for (int j = 0; j < kBD2; j++) sa[j] = sb[j] = 0.0;
+   const size_t stride = (size_t)gridDim.x * kBDThreads;
+   for (size_t r = (size_t)blockIdx.x * kBDThreads + threadIdx.x; r < n; r += stride) {
+      const double ar = a[r];
+      const double br = b ? b[r] : 0.0;
+      double v[kBD2];
+#pragma unroll
+      for (int j = 0; j < kBD2; j++) v[j] = j < cnt ? V[(size_t)(g0 + j) * n + r] : 0.0;
+#pragma unroll
+      for (int j = 0; j < kBD2; j++) {
+         sa[j] = fma(v[j], ar, sa[j]);
+         sb[j] = fma(v[j], br, sb[j]);
+      }
+   }
+   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+   for (int j = 0; j < kBD2; j++) {
+      double x = sa[j], y = sb[j];
+      for (int off = 32; off > 0; off >>= 1) {
+         x += __shfl_down(x, off, 64);
+         y += __shfl_down(y, off, 64);
+      }
+      if (lane == 0) {
+         s[wave][j] = x;
+         s[wave][kBD2 + j] = y;
+      }
+   }
+   __syncthreads();
+   if (threadIdx.x < 2 * kBD2) {
+      const int j = threadIdx.x % kBD2, which = threadIdx.x / kBD2;
+      if (j < cnt && (which == 0 || b)) {
+         double t = 0.0;
+#pragma unroll
+         for (int q = 0; q < kBDThreads / 64; q++) t += s[q][threadIdx.x];
+         part[(size_t)blockIdx.x * ldp + which * m + g0 + j] = t;
+      }
+   }
+}
+
+// Update of a step (row-parallel, basis columns read once): column j is finalised in place,
+// v_j = (V[:, j] - sum_{k<j} s_k v_k) / alpha, and w becomes the next provisional column's numerator
+// u = w / alpha - sum_{k<j} g_k v_k - g_j v_j; *out = ||u||^2.  coef = [s (j) | g (j + 1) | 1 / alpha].
+__global__ __launch_bounds__(kKThreads) void k_dcgs2_update(double* __restrict__ V, double* __restrict__ w, size_t n,
+                                                            int j, const double* __restrict__ coef,
+                                                            double* __restrict__ part,
+                                                            unsigned int* __restrict__ ticket,
+                                                            double* __restrict__ out)
+{
+   extern __shared__ double s_c[];
+   for (int k = threadIdx.x; k < 2 * j + 2; k += kKThreads) s_c[k] = coef[k];
+   __syncthreads();
+   const double* s_s = s_c;
+   const double* s_g = s_c + j;
+   const double ia = s_c[2 * j + 1];
+   double acc = 0.0;
+   const size_t stride = (size_t)gridDim.x * kKThreads * kKEPT;
+   double* vjcol = V + (size_t)j * n;
+   for (size_t i0 = (size_t)blockIdx.x * kKThreads * kKEPT + threadIdx.x; i0 < n; i0 += stride) {
+      double v0[kKEPT], u[kKEPT];
+      bool in[kKEPT];
+#pragma unroll
+      for (int e = 0; e < kKEPT; e++) {
+         const size_t i = i0 + (size_t)e * kKThreads;
+         in[e] = i < n;
+         v0[e] = in[e] ? vjcol[i] : 0.0;
+         u[e] = in[e] ? w[i] * ia : 0.0;
+      }
+      int k = 0;
+      for (; k + 4 <= j; k += 4) {
+         double z[4][kKEPT];
+#pragma unroll
+         for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int e = 0; e < kKEPT; e++) z[q][e] = in[e] ? V[(size_t)(k + q) * n + i0 + (size_t)e * kKThreads] : 0.0;
+#pragma unroll
+         for (int q = 0; q < 4; q++) {
+            const double sk = s_s[k + q], gk = s_g[k + q];
+#pragma unroll
+            for (int e = 0; e < kKEPT; e++) {
+               v0[e] = fma(-sk, z[q][e], v0[e]);
+               u[e] = fma(-gk, z[q][e], u[e]);
+            }
+         }
+      }
+      for (; k < j; k++) {
+         const double sk = s_s[k], gk = s_g[k];
+#pragma unroll
+         for (int e = 0; e < kKEPT; e++) {
+            const double z = in[e] ? V[(size_t)k * n + i0 + (size_t)e * kKThreads] : 0.0;
+            v0[e] = fma(-sk, z, v0[e]);
+            u[e] = fma(-gk, z, u[e]);
+         }
+      }
+      const double gj = s_g[j];
+#pragma unroll
+      for (int e = 0; e < kKEPT; e++) {
+         const size_t i = i0 + (size_t)e * kKThreads;
+         const double vj = v0[e] * ia;
+         u[e] = fma(-gj, vj, u[e]);
+         if (in[e]) {
+            vjcol[i] = vj;
+            w[i] = u[e];
+         }
+         acc = fma(u[e], u[e], acc);
+      }
+   }
+   acc = block_sum0<kKThreads>(acc);
+   double tot;
+   if (grid_total<kKThreads>(acc, part, ticket, &tot) && threadIdx.x == 0) *out = tot;
+}
+
+// a *= 1 / sqrt(*nrm2) (the provisional column's normalisation, without a host round trip)
+__global__ void k_scale_rnorm(double* __restrict__ a, size_t n, const double* __restrict__ nrm2)
+{
+   const double f = 1.0 / sqrt(*nrm2);
+   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) a[i] *= f;
+}
+
 int egrid(size_t n)
 {
    size_t g = (n + 255) / 256;
@@ -358,6 +420,7 @@ int egrid(size_t n)
 struct KScratch {
    static constexpr int kScal = 4096;
    double *part = nullptr, *part2 = nullptr, *scal = nullptr, *hscal = nullptr, *coef = nullptr;
+   double* hcoef = nullptr;  // pinned staging of per-step coefficients (DCGS2)
    double* bpart = nullptr;  // block Gram-Schmidt partials [kBDMaxBlocks][kScal]
    unsigned int *ticket = nullptr, *ticket2 = nullptr;
    int ensure_bpart()
@@ -377,6 +440,7 @@ struct KScratch {
       NFFT4GP_HIP_CHECK(hipMemset(ticket, 0, sizeof(unsigned int) * kTicketWords));
       NFFT4GP_HIP_CHECK(hipMemset(ticket2, 0, sizeof(unsigned int) * kTicketWords));
       NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&hscal, sizeof(double) * kScal));
+      NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&hcoef, sizeof(double) * kScal));
       return 0;
    }
 };
@@ -440,26 +504,69 @@ struct Ctx {
       const int mc = m + with_norm;
       // h[m], h[m + 1] take part in the all-reduce below even when this pass does not write them
       if (comm) NFFT4GP_HIP_CHECK(hipMemsetAsync(h + m, 0, sizeof(double) * 2, s));
-      static const int bv = getenv("NFFT4GP_AMD_BGS_VARIANT") ? atoi(getenv("NFFT4GP_AMD_BGS_VARIANT")) : 1;
-      const bool x2 = bv == 1 && n % 2 == 0;
-      if (x2)
-         hipLaunchKernelGGL(k_block_dots_x2, dim3(nb, (mc + kBD2 - 1) / kBD2), dim3(kBDThreads), 0, s, w, V, n, m,
-                            with_norm, g_k.bpart, KScratch::kScal);
-      else
-         hipLaunchKernelGGL(k_block_dots, dim3(nb, (mc + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m,
-                            with_norm, g_k.bpart, KScratch::kScal);
+      hipLaunchKernelGGL(k_block_dots, dim3(nb, (mc + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m, with_norm,
+                         g_k.bpart, KScratch::kScal);
       hipLaunchKernelGGL(k_block_reduce, dim3((mc + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, mc, m,
                          h);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       if (red(h, m + 2)) return -1;  // the projections and the norm before them, summed over the row shards
-      if (bv == 1)
-         hipLaunchKernelGGL(k_block_update_x4, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, Z, n, h, m,
-                            g_k.part, g_k.ticket, h + m);
-      else
-         hipLaunchKernelGGL(k_block_update, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, Z, n, h, m,
-                            g_k.part, g_k.ticket, h + m);
+      hipLaunchKernelGGL(k_block_update, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, Z, n, h, m,
+                         g_k.part, g_k.ticket, h + m, nullptr, nullptr, nullptr);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return red(h + m, 1);
+   }
+   // CGS2 against the basis V (m columns) with one host read: pass 1 (dots with the norm before, update with
+   // the norm after), then pass 2 with every launch gated on the device by the DGKS test on pass 1's norms, so
+   // the host does not wait between the passes.  h: [0, m) pass-1 projections, h[m] ||w||^2 after pass 1,
+   // h[m + 1] before it, [m + 2, 2m + 2) pass-2 projections, h[2m + 2] ||w||^2 after pass 2, h[2m + 3] the
+   // decision (1 / 0); pass-2 entries are meaningful only when the decision is 1
+   int block_cgs2(double* w, const double* V, int m, double* h)
+   {
+      if (m <= 0 || 2 * m + 4 > KScratch::kScal) return -1;
+      if (block_gs(w, V, V, m, h, 1)) return -1;
+      const int nb = bd_grid(n);
+      const double* after = h + m;
+      const double* before = h + m + 1;
+      hipLaunchKernelGGL(k_block_dots, dim3(nb, (m + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m, 0, g_k.bpart,
+                         KScratch::kScal, after, before);
+      hipLaunchKernelGGL(k_block_reduce, dim3((m + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, m, m,
+                         h + m + 2);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      if (red(h + m + 2, m)) return -1;
+      hipLaunchKernelGGL(k_block_update, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, V, n, h + m + 2,
+                         m, g_k.part, g_k.ticket, h + 2 * m + 2, after, before, h + 2 * m + 3);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return red(h + 2 * m + 2, 1);
+   }
+   // DCGS2 sweep 1: out[0, m) = V(:, 0..m)^T a, out[m, 2m) = V(:, 0..m)^T b (b optional; column m - 1 is a)
+   int dots_ab(const double* a, const double* b, const double* V, int m, double* out)
+   {
+      if (m <= 0 || 2 * m > KScratch::kScal) return -1;
+      if (g_k.ensure_bpart()) return -1;
+      const int nb = bd_grid(n);
+      hipLaunchKernelGGL(k_block_dots_ab, dim3(nb, (m + kBD2 - 1) / kBD2), dim3(kBDThreads), 0, s, a, b, V, n, m,
+                         g_k.bpart, KScratch::kScal);
+      const int mc = b ? 2 * m : m;
+      hipLaunchKernelGGL(k_block_reduce, dim3((mc + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, mc,
+                         mc, out);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return red(out, mc);
+   }
+   // DCGS2 update (k_dcgs2_update) with the host's coefficients [s | g | 1/alpha], then w /= ||w|| on the
+   // device; *nrm2 = ||w||^2 before that scaling
+   int dcgs2_update(double* V, double* w, int j, const std::vector<double>& coef, double* nrm2)
+   {
+      if (coef.size() > (size_t)KScratch::kScal) return -1;
+      // pinned staging: the previous step's copy has run (the host read this step's sweep after it)
+      memcpy(g_k.hcoef, coef.data(), sizeof(double) * coef.size());
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(g_k.coef, g_k.hcoef, sizeof(double) * coef.size(), hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(k_dcgs2_update, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * (2 * j + 2), s, V, w, n, j,
+                         g_k.coef, g_k.part, g_k.ticket, nrm2);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      if (red(nrm2, 1)) return -1;
+      hipLaunchKernelGGL(k_scale_rnorm, dim3(egrid(n)), dim3(256), 0, s, w, n, (const double*)nrm2);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
    }
    void scale(double* a, double* b, double f)
    {
@@ -519,9 +626,202 @@ int fgmres_ortho()
 {
    if (g_fgmres_ortho < 0) {
       const char* e = getenv("NFFT4GP_AMD_FGMRES_ORTHO");
-      g_fgmres_ortho = (e && atoi(e) == 1) ? 1 : 0;
+      g_fgmres_ortho = (e && (atoi(e) == 1 || atoi(e) == 2)) ? atoi(e) : 0;
    }
    return g_fgmres_ortho;
+}
+
+// ---- FGMRES with DCGS2 (ortho 2, no preconditioner) ----------------------------------------------------------
+// The reference's FGMRES (fgmres.c:3-252: the same Givens recurrence, breakdown exit, restart and reporting)
+// with the Arnoldi basis orthogonalised by delayed CGS2 (Swirydowicz, Langou, Ananthan, Yang, Thomas 2020):
+// step j multiplies the provisional column v_j^0 = u_j / beta_j (once orthogonalised), then ONE sweep forms
+// s = V^T v_j^0 (v_j's second pass, delayed) and t = V^T w (w = A v_j^0), and ONE update sweep finalises
+// v_j = (v_j^0 - V s) / alpha, alpha^2 = (v_j^0, v_j^0) - |s|^2, and forms the next provisional column
+// u = A v_j - V c through the Arnoldi relation A v_j = (w - V H s) / alpha, which gives
+// u = (w - V_{<j} t) / alpha - ((v_j^0, w) - s.t) / alpha^2 v_j.  Column j - 1 of H becomes final at step j:
+// H(<j, j-1) += beta_j s, H(j, j-1) = beta_j alpha, so the Givens rotation and the residual of iteration j are
+// applied one step late (one extra operator application per cycle).  Mathematically CGS2 with a second pass at
+// every step; the basis is read twice per step instead of up to four times.
+int fgmres_dcgs2_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits, int atol, double tol,
+                     double* prel_res, double** prel_res_v, int* piter, int print_level)
+{
+   const size_t n = cb.n;
+   Ctx c{current_stream(), n, cb.comm};
+   const double EPS = DBL_EPSILON;
+   if (cb.n_global == 0) {
+      *prel_res = 0.0;
+      *piter = 0;
+      *prel_res_v = rel_hist(1);
+      return 0;
+   }
+   const double normb = c.norm(rhs);
+   if (normb < EPS) {
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(x, 0, sizeof(double) * n, c.s));
+      *prel_res = 0.0;
+      *piter = 0;
+      *prel_res_v = rel_hist(1);
+      return 0;
+   }
+   const int kmax = KScratch::kScal / 2 - 2;
+   if (kdim > kmax) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPSolverFgmres: restart dimension %d above %d\n", kdim, kmax);
+      return -1;
+   }
+   double* V = nullptr;
+   if (dmalloc(&V, n * (size_t)(kdim + 1))) return -1;
+   auto cleanup = [&]() {
+      (void)hipStreamSynchronize(c.s);
+      (void)hipFree(V);
+   };
+   // Hr: the unrotated Hessenberg (the Arnoldi relation), H: the rotated one (fgmres.c's H)
+   std::vector<double> Hr((size_t)kdim * (kdim + 1), 0.0), H((size_t)kdim * (kdim + 1), 0.0), cs(kdim), sn(kdim),
+       rs(kdim + 1);
+   double* v = V;
+   c.copy(v, rhs);
+   if (cb.apply(-1.0, x, 1.0, v)) {
+      cleanup();
+      return -1;
+   }
+   double normr = c.norm(v);
+   if (normr < EPS) {
+      *prel_res = 0.0;
+      *piter = 0;
+      *prel_res_v = rel_hist(1);
+      cleanup();
+      return 0;
+   }
+   const double tolr = atol ? tol : tol * normb;
+   double* rel = rel_hist(maxits + 1);
+   rel[0] = normr / normb;
+   int iter = 0, i = 0;
+   if (print_level > 0) {
+      printf("--------------------------------------------------------------------------------\n");
+      printf("Start FlexGMRES(%d)\n", kdim);
+      printf("Residual Tol: %e\nMax number of inner iterations: %d\n", tolr, maxits);
+      printf("--------------------------------------------------------------------------------\n");
+      printf("Step    Residual norm  Relative res.  Convergence Rate\n");
+      printf("%5d   %8e   %8e   N/A\n", 0, normr, rel[0]);
+   }
+   double* dsc = g_k.scal;  // device scalars of step j (m = j + 1): [0, 2m) the sweep, [2m] ||u_j||^2
+   std::vector<double> hh, coef;
+   bool broke = false, converged = false;
+   if (2 * (kdim + 1) + 1 > KScratch::kScal) {
+      cleanup();
+      free(rel);
+      return -1;
+   }
+   while (iter < maxits) {
+      rs[0] = normr;
+      c.scale(V, nullptr, 1.0 / normr);
+      i = 0;                 // final columns of H in this cycle
+      double beta = 0.0;     // ||u_j|| of the provisional column j (j >= 1)
+      for (int j = 0;; j++) {
+         // step j: column j of V is provisional (j >= 1); column j - 1 of H is completed here
+         const bool more = j < kdim && iter + (j > 0 ? 1 : 0) < maxits;  // will column j get a first pass?
+         double* vj = V + (size_t)j * n;
+         double* w = V + (size_t)(j + 1) * n;
+         if (more && cb.apply(1.0, vj, 0.0, w)) {
+            free(rel);
+            cleanup();
+            return -1;
+         }
+         const int m = j + 1;
+         hh.assign(2 * m + 1, 0.0);
+         if (c.dots_ab(vj, more ? w : nullptr, V, m, dsc)) return -1;
+         if (c.read(dsc, 2 * m + 1, hh.data())) return -1;  // (T is stale when !more)
+         if (j > 0) beta = std::sqrt(hh[2 * m]);
+         // the delayed second pass of column j: s = hh[0, j), omega = hh[j]
+         double alpha = 1.0, ss = 0.0;
+         if (j > 0) {
+            for (int k = 0; k < j; k++) ss += hh[k] * hh[k];
+            const double a2 = hh[j] - ss;
+            alpha = a2 > 0.0 ? std::sqrt(a2) : std::sqrt(hh[j]);
+            // column j - 1 of H is final: H(<j, j-1) += beta s, H(j, j-1) = beta alpha
+            double* Hrc = Hr.data() + (size_t)(j - 1) * (kdim + 1);
+            for (int k = 0; k < j; k++) Hrc[k] += beta * hh[k];
+            Hrc[j] = beta * alpha;
+            // fgmres.c:160-200 on that column: the previous rotations, a new one, the residual estimate
+            i = j;
+            iter++;
+            double* Hc = H.data() + (size_t)(i - 1) * (kdim + 1);
+            for (int k = 0; k <= i; k++) Hc[k] = Hrc[k];
+            for (int k = 1; k < i; k++) {
+               const double hii = Hc[k - 1];
+               Hc[k - 1] = cs[k - 1] * hii + sn[k - 1] * Hc[k];
+               Hc[k] = -sn[k - 1] * hii + cs[k - 1] * Hc[k];
+            }
+            const double hii = Hc[i - 1], hii1 = Hc[i];
+            const double gam = std::sqrt(hii * hii + hii1 * hii1);
+            if (std::fabs(gam) < EPS) {
+               broke = true;
+               break;
+            }
+            cs[i - 1] = hii / gam;
+            sn[i - 1] = hii1 / gam;
+            rs[i] = -sn[i - 1] * rs[i - 1];
+            rs[i - 1] = cs[i - 1] * rs[i - 1];
+            Hc[i - 1] = cs[i - 1] * hii + sn[i - 1] * hii1;
+            normr = std::fabs(rs[i]);
+            rel[iter] = normr / normb;
+            if (print_level > 0)
+               printf("%5d   %8e   %8e   %8.6f\n", iter, normr, rel[iter], rel[iter] / rel[iter - 1]);
+            if (normr <= tolr) {
+               converged = true;
+               break;
+            }
+         }
+         if (!more) break;
+         // first pass of A v_j: H(<j, j) = (t - (H s))/alpha, H(j, j) = ((v_j^0, w) - s.t)/alpha - (H s)_j)/alpha
+         const double* t = hh.data() + m;
+         double st = 0.0;
+         for (int k = 0; k < j; k++) st += hh[k] * t[k];
+         const double vjw = (t[j] - st) / alpha;
+         std::vector<double> Hs(m, 0.0);
+         for (int q = 0; q < j; q++) {
+            const double* Hrq = Hr.data() + (size_t)q * (kdim + 1);
+            for (int k = 0; k <= q + 1 && k < m; k++) Hs[k] += Hrq[k] * hh[q];
+         }
+         double* Hrj = Hr.data() + (size_t)j * (kdim + 1);
+         for (int k = 0; k < j; k++) Hrj[k] = (t[k] - Hs[k]) / alpha;
+         Hrj[j] = (vjw - Hs[j]) / alpha;
+         // update: v_j final, u = w / alpha - sum_{k<j} (t_k / alpha) v_k - (vjw / alpha) v_j
+         coef.assign(2 * j + 2, 0.0);
+         for (int k = 0; k < j; k++) {
+            coef[k] = j > 0 ? hh[k] : 0.0;
+            coef[j + k] = t[k] / alpha;
+         }
+         coef[2 * j] = vjw / alpha;
+         coef[2 * j + 1] = 1.0 / alpha;
+         if (c.dcgs2_update(V, w, j, coef, dsc + 2 * (m + 1))) return -1;  // ||u_{j+1}||^2 where step j + 1 reads it
+      }
+      if (broke) break;
+      if (print_level == 0)
+         printf("Rel. residual at the end of current cycle (# of steps per cycle/total its: %d/%d): %e \n", kdim,
+                iter, rel[iter]);
+      if (i > 0) {
+         rs[i - 1] /= H[(size_t)(i - 1) * (kdim + 1) + i - 1];
+         for (int k = i - 2; k >= 0; k--) {
+            for (int q = k + 1; q < i; q++) rs[k] -= H[(size_t)q * (kdim + 1) + k] * rs[q];
+            rs[k] /= H[(size_t)k * (kdim + 1) + k];
+         }
+         if (c.combine(x, V, i, rs.data())) return -1;
+      }
+      if (converged || normr <= tolr) break;
+      // restart (fgmres.c:236-243): v = rhs - A x through w; normr keeps the Givens estimate
+      double* w = V + n;
+      c.copy(V, rhs);
+      if (cb.apply(1.0, x, 0.0, w)) {
+         free(rel);
+         cleanup();
+         return -1;
+      }
+      hipLaunchKernelGGL(k_sub, dim3(egrid(n)), dim3(256), 0, c.s, V, V, w, n);
+   }
+   *prel_res = normr / normb;
+   *piter = iter;
+   *prel_res_v = rel;
+   cleanup();
+   return 0;
 }
 
 // ---- FGMRES (fgmres.c:3-252) on device vectors ----------------------------------------------------
@@ -546,6 +846,8 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
       return 0;
    }
    const int ortho = fgmres_ortho();
+   if (ortho == 2 && !cb.prec)
+      return fgmres_dcgs2_dev(cb, x, rhs, kdim, maxits, atol, tol, prel_res, prel_res_v, piter, print_level);
    const int kmax = ortho ? KScratch::kScal / 2 - 2 : KScratch::kScal - 2;
    if (kdim > kmax) {
       fprintf(stderr, "nfft4gp_amd: Nfft4GPSolverFgmres: restart dimension %d above %d\n", kdim, kmax);
@@ -624,13 +926,11 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
             // classical passes h = V^T w, w -= V h; a second one only when the first dropped ||w|| below 0.7071
             // of its value before it (the DGKS test of the reference's MGS2, matops.c:348-440); H(:, i) = the
             // sum of the passes' projections, ||w|| after the last
-            double* hd2 = hd + i + 2;
-            std::vector<double> hh(2 * i + 3);
-            if (c.block_gs(w, V, V, i, hd, 1) || c.read(hd, i + 2, hh.data())) return -1;
+            std::vector<double> hh(2 * i + 4);
+            if (c.block_cgs2(w, V, i, hd) || c.read(hd, 2 * i + 4, hh.data())) return -1;
             for (int j = 0; j < i; j++) hcol[j] = hh[j];
             hcol[i] = hh[i];
-            if (std::sqrt(hh[i]) < 0.7071 * std::sqrt(hh[i + 1])) {
-               if (c.block_gs(w, V, V, i, hd2) || c.read(hd2, i + 1, hh.data() + i + 2)) return -1;
+            if (hh[2 * i + 3] != 0.0) {
                for (int j = 0; j < i; j++) hcol[j] += hh[i + 2 + j];
                hcol[i] = hh[2 * i + 2];
                g_fgmres_second_passes++;
@@ -1174,7 +1474,7 @@ bool make_callbacks(Callbacks& cb, int n, func_symmatvec matvec, void* mat, func
 
 extern "C" {
 
-void Nfft4GPAmdSetFgmresOrtho(int ortho) { g_fgmres_ortho = (ortho == 1) ? 1 : 0; }
+void Nfft4GPAmdSetFgmresOrtho(int ortho) { g_fgmres_ortho = (ortho == 1 || ortho == 2) ? ortho : 0; }
 
 // the second classical passes FGMRES (ortho 1) has taken since the last call (its DGKS test), then reset
 long long Nfft4GPAmdFgmresSecondPasses(void)

@@ -694,7 +694,7 @@ int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
    if (D.maxd <= kMdTiledMaxDim) {
       // taps per work item (A/B knob NFFT4GP_AMD_MD_CHUNK; the results do not depend on it beyond the spread's
       // fixed-point rounding, which is exact)
-      long long chunk_taps = 2000000;
+      long long chunk_taps = 50000;  // 256 points (3-D) / 500 (2-D): tools/md_chunk_sweep.sh, profiles/r04_md_chunk_sweep.txt
       if (const char* e = getenv("NFFT4GP_AMD_MD_CHUNK")) chunk_taps = std::max(1000LL, atoll(e));
       std::vector<int> perm((size_t)P.nw * n);
       std::vector<std::vector<int4>> citems(P.nw);

@@ -1,4 +1,4 @@
-"""FGMRES with the block CGS2 orthogonalisation (Nfft4GPAmdSetFgmresOrtho(1)) at the bench's FGMRES
+"""FGMRES with the block CGS2 (Nfft4GPAmdSetFgmresOrtho(1)) and delayed CGS2 (2) orthogonalisations at the bench's FGMRES
 configuration (config C, l = 1, kdim = maxits = 1000, tol 1e-6): time, iterations, second passes.
     python tools/fgmres_cgs2_probe.py [reps]"""
 import json
@@ -25,18 +25,19 @@ def main():
     op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
     assert op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) == 0
     b = torch.tensor(np.random.default_rng(907).random(n) - 0.5, device="cuda")
-    L.Nfft4GPAmdSetFgmresOrtho(1)
     for rep in range(int(sys.argv[1]) if len(sys.argv) > 1 else 2):
-        xs = torch.zeros_like(b)
-        L.Nfft4GPAmdFgmresSecondPasses()
-        torch.cuda.synchronize()
-        t0 = time.time()
-        _, rr, hist, it = amd.fgmres(op, b, xs, kdim=1000, maxits=1000, tol=1e-6)
-        torch.cuda.synchronize()
-        dt = time.time() - t0
-        print(json.dumps({"rep": rep, "iters": it, "rel_res": rr, "time_s": round(dt, 4),
-                          "second_passes": int(L.Nfft4GPAmdFgmresSecondPasses()),
-                          "hist_10": float(hist[10]), "hist_100": float(hist[100])}), flush=True)
+        for ortho in (1, 2):
+            L.Nfft4GPAmdSetFgmresOrtho(ortho)
+            xs = torch.zeros_like(b)
+            L.Nfft4GPAmdFgmresSecondPasses()
+            torch.cuda.synchronize()
+            t0 = time.time()
+            _, rr, hist, it = amd.fgmres(op, b, xs, kdim=1000, maxits=1000, tol=1e-6)
+            torch.cuda.synchronize()
+            dt = time.time() - t0
+            print(json.dumps({"ortho": ortho, "rep": rep, "iters": it, "rel_res": rr, "time_s": round(dt, 4),
+                              "second_passes": int(L.Nfft4GPAmdFgmresSecondPasses()),
+                              "hist_10": float(hist[10]), "hist_100": float(hist[100])}), flush=True)
 
 
 if __name__ == "__main__":
