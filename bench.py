@@ -421,16 +421,18 @@ class _StdoutToStderr:
         return False
 
 
-def run_loss(op, torch, n, d, X, rng_seed=906, maxits=50, nvecs=10, rows=None, dist=None, l=0.1):
+def run_loss(op, torch, n, d, X, rng_seed=906, maxits=50, nvecs=10, rows=None, dist=None, l=0.1, ortho=0):
     """One log-marginal-likelihood + gradient evaluation (Nfft4GPGpLoss, gp_loss.c:96-307: FGMRES for K^-1 y,
     stochastic Lanczos quadrature with nvecs Rademacher probes of maxits steps, the gradient matvecs) on the
     bench's operator at (f, l, mu) = (1, 0.1, 0.01), identity transform -- the loop BASELINE configs[4] runs
     at n = 1e7 on 8 GPUs, here at the bench's size.  l = 0.1 as for PCG: at l = 1 the NFFT operator is
     indefinite and the quadrature's Lanczos solve (lanczos.c, an LDL^T recursion of T) breaks
     down, so the gradient comes out NaN there, as the reference's would.  With a distributed operator every
-    rank runs it on its rows (krylov.hip sums every inner product over the ranks); time: max over ranks."""
+    rank runs it on its rows (krylov.hip sums every inner product over the ranks); time: max over ranks.
+    ortho 2: the loss's FGMRES solve with delayed CGS2 instead of the reference's MGS (loss_dcgs2_*)."""
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
     rb, re = rows if rows is not None else (0, n)
+    amd.lib().Nfft4GPAmdSetFgmresOrtho(ortho)
     rng = np.random.default_rng(rng_seed + 3)
     y = rng.random(n) - 0.5
     R = np.where(rng.random((n, nvecs)) < 0.5, -1.0, 1.0)
@@ -445,10 +447,13 @@ def run_loss(op, torch, n, d, X, rng_seed=906, maxits=50, nvecs=10, rows=None, d
                                  rademacher=Rl, tol=1e-6, transform=3, op=op)
         torch.cuda.synchronize()
     t = time.time() - t0
+    amd.lib().Nfft4GPAmdSetFgmresOrtho(0)
     if dist is not None:
         tt = torch.tensor([t], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
+    if ortho == 2:
+        return {"loss_dcgs2_time_s": t, "loss_dcgs2_value": loss, "loss_dcgs2_grad": [float(g) for g in grad]}
     return {"loss_time_s": t, "loss_value": loss, "loss_grad": [float(g) for g in grad], "loss_maxits": maxits,
             "loss_nvecs": nvecs, "loss_l": l}
 
@@ -582,6 +587,7 @@ def main():
         pcie_rate = reps_h / (time.perf_counter() - t0)
     if world == 1 and not args.no_pcg:
         pcg.update(run_loss(op, torch, n, d, X))
+        pcg.update(run_loss(op, torch, n, d, X, ortho=2))
         pcg.update(run_fgmres(op, torch, n))
         pcg.update(run_fgmres(op, torch, n, ortho=1))
         pcg.update(run_fgmres(op, torch, n, ortho=2))

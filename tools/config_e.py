@@ -81,6 +81,18 @@ def main():
     out["loss_s"] = time.time() - t0
     out["loss"] = loss
     out["grad"] = [float(g) for g in grad]
+    # the same loss with the loss's FGMRES solve orthogonalised by delayed CGS2 (Nfft4GPAmdSetFgmresOrtho(2))
+    # instead of the reference's MGS; the Lanczos quadrature is unchanged
+    L.Nfft4GPAmdSetFgmresOrtho(2)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    loss2, grad2 = amd.gp_loss(X, win, d, 1, y, (1.0, args.l, 0.01), maxits=args.maxits, nvecs=args.nvecs,
+                               rademacher=Rd, transform=3, op=op)
+    torch.cuda.synchronize()
+    out["loss_dcgs2_s"] = time.time() - t0
+    L.Nfft4GPAmdSetFgmresOrtho(0)
+    out["loss_dcgs2_rel_diff"] = abs(loss2 - loss) / abs(loss)
+    out["grad_dcgs2_rel_diff"] = float(np.max(np.abs(np.asarray(grad2) - np.asarray(grad)) / np.abs(np.asarray(grad))))
     out["nvecs"] = args.nvecs
     out["maxits"] = args.maxits
     print(json.dumps(out), flush=True)
