@@ -807,7 +807,9 @@ int fgmres_dcgs2_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int 
          if (c.combine(x, V, i, rs.data())) return -1;
       }
       if (converged || normr <= tolr) break;
-      // restart (fgmres.c:236-243): v = rhs - A x through w; normr keeps the Givens estimate
+      // restart (fgmres.c:236-243): v = rhs - A x through w.  The reference keeps the Givens estimate as the
+      // new cycle's norm, so its first basis vector is not of unit length; MGS tolerates that, but the block
+      // orthogonalisations assume an orthonormal basis, so they restart from the true norm (one dot)
       double* w = V + n;
       c.copy(V, rhs);
       if (cb.apply(1.0, x, 0.0, w)) {
@@ -816,6 +818,7 @@ int fgmres_dcgs2_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int 
          return -1;
       }
       hipLaunchKernelGGL(k_sub, dim3(egrid(n)), dim3(256), 0, c.s, V, V, w, n);
+      normr = c.norm(V);
    }
    *prel_res = normr / normb;
    *piter = iter;
@@ -983,6 +986,7 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
          return -1;
       }
       hipLaunchKernelGGL(k_sub, dim3(egrid(n)), dim3(256), 0, c.s, v, v, w, n);
+      if (ortho) normr = c.norm(v);  // block CGS2: restart from the true norm (see fgmres_dcgs2_dev)
    }
    *prel_res = normr / normb;
    *piter = iter;
