@@ -111,9 +111,8 @@ __device__ __forceinline__ void stage_block_glds(double* __restrict__ s, const d
 // spread
 // ------------------------------------------------------------------------------------------------
 // at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
-// FOLD 1: the fold in two steps over all the workgroup's threads (Q = C M per cell and tap into the dead alpha
-// slice, then 10-term sums per output); FOLD 0: one 100-term chain per output on 64 ncomp threads
-template <int THREADS, bool TIMELINE = false, int FOLD = 1>
+// PREFETCH: the next run's tile is loaded before this run is processed (A/B variant)
+template <int THREADS, bool TIMELINE = false, bool PREFETCH = false>
 __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restrict__ meta,
                                                       const uint32_t* __restrict__ lo,
                                                       const uint32_t* __restrict__ qarr,
@@ -122,7 +121,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
                                                       double* __restrict__ part)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
-   const int Bp = max(B + kPad, CG * kNos * kTaps);  // the alpha slice, then the fold's Q (spread_lds_bytes)
+   const int Bp = B + kPad;
    double* s_alpha = smem;     // Bp
    double* s_mom = smem + Bp;  // CG*64*kMomStride per-cell moments
 
@@ -154,6 +153,8 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
 
    const int c0 = g * CG;
    for (; t < t1; t += nwaves) {
+      TileRegs nxt;
+      if (PREFETCH && t + nwaves < t1) load_tile(nxt, meta, lo, qarr, t + nwaves, lane);  // in flight during this run
       double acc[kNC];
 #pragma unroll
       for (int d = 0; d < kNC; d++) acc[d] = 0.0;
@@ -174,7 +175,10 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
       double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
 #pragma unroll
       for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
-      if (t + nwaves < t1) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
+      if (PREFETCH)
+         cur = nxt;
+      else if (t + nwaves < t1)
+         load_tile(cur, meta, lo, qarr, t + nwaves, lane);
    }
    __syncthreads();
    if (TIMELINE) stamp(2);
@@ -182,43 +186,17 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    // fold moments into the 64-cell partial grid of every window of this group:
    //   g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
    const int ncomp = min(CG, nw - c0);
-   if (FOLD == 1) {
-      // Q[tp][cl][cell] = sum_d C[tp][d] M[cl][cell][d] (tp wave-uniform: the taps are scalar loads), into
-      // the alpha slice, which no thread reads after the barrier above
-      double* s_q = s_alpha;
-      const int nq = ncomp * kNos;
-      for (int idx = tid; idx < kTaps * nq; idx += THREADS) {
-         const int tp = idx / nq;
-         const int cc = idx - tp * nq;  // cl * 64 + cell
-         const double* mrow = s_mom + cc * kMomStride;
-         double q = 0.0;
-#pragma unroll
-         for (int d = 0; d < kNC; d++) q = fma(c_taps[tp * kNC + d], mrow[d], q);
-         s_q[idx] = q;
-      }
-      __syncthreads();
-      // g[cl][gi] = sum_tp Q[tp][cl][(gi + m - tp) mod 64]
-      for (int idx = tid; idx < nq; idx += THREADS) {
-         const int cl = idx / kNos;
-         const int gi = idx % kNos;
-         double v = 0.0;
-#pragma unroll
-         for (int tp = 0; tp < kTaps; tp++) v += s_q[tp * nq + cl * kNos + ((gi + kM - tp) & (kNos - 1))];
-         part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
-      }
-   } else {
-      for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
-         const int cl = idx / kNos;
-         const int gi = idx % kNos;
-         double v = 0.0;
+   for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
+      const int cl = idx / kNos;
+      const int gi = idx % kNos;
+      double v = 0.0;
 #pragma unroll 1
-         for (int tp = 0; tp < kTaps; tp++) {
-            const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
+      for (int tp = 0; tp < kTaps; tp++) {
+         const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
 #pragma unroll
-            for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
-         }
-         part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
+         for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
       }
+      part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
    }
    if (TIMELINE) {
       __syncthreads();
@@ -702,8 +680,7 @@ static void launch_ev(F fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, co
 
 static size_t spread_lds_bytes(const AdditivePlan& P)
 {
-   const size_t slice = std::max<size_t>((size_t)P.B + kPad, (size_t)P.CG * kNos * kTaps);  // alpha, then the fold's Q
-   return sizeof(double) * (slice + (size_t)P.CG * kNos * kMomStride);
+   return sizeof(double) * ((size_t)P.B + kPad + (size_t)P.CG * kNos * kMomStride);
 }
 
 static size_t interp_lds_bytes(const AdditivePlan& P, int grad)
@@ -728,14 +705,14 @@ int upload_tap_coeffs()
 
 typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, int, int, int,
                          int, int, int, double*);
-// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py); 2: the
-// one-chain fold (A/B).  Variants that
+// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py); 2: the next
+// run's tile loaded before this run is processed (A/B).  Variants that
 // measured slower or neutral (prefetching runs, persistent workgroups, several groups per workgroup, the fold in
 // two chains, register-staged alpha, the row shards' block sum in the spread's tail) were removed in round 4;
 // DESIGN.md 3.5 keeps their numbers.
 constexpr int kSpreadThreads = 512;
 static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>,
-                                           k_spread<kSpreadThreads, false, 0>};
+                                           k_spread<kSpreadThreads, false, true>};
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
 constexpr int kInterpThreads = 1024;

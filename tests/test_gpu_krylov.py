@@ -231,8 +231,21 @@ def test_fgmres_block_orthogonalisation_matches_mgs(torch_cuda, ortho, kdim, max
     assert res[0][3] == res[1][3] > 0
     if kdim == maxits == 400:
         assert res[1][1] <= 1e-8
-    # the history's tail sits at 1e-8 relative residual, where a 1e-16 rounding difference is 1e-8 relative
-    htol, xtol = 1e-8, 1e-9
-    np.testing.assert_allclose(res[1][2], res[0][2], rtol=htol, atol=1e-14)
-    assert np.linalg.norm(res[1][0] - res[0][0]) <= xtol * np.linalg.norm(res[0][0])
+    assert np.linalg.norm(res[1][0] - res[0][0]) <= 1e-9 * np.linalg.norm(res[0][0])
+    if kdim < maxits:
+        # restarted: the first cycle to 1e-8; after the first restart the residual estimates of this stagnating
+        # solve move by several percent under a one-ulp change of b in CGS2 itself (tools/diag_dcgs2.py: 4.5e-2
+        # while x moves 7e-13), so the later history is held to three times that spread, measured here
+        np.testing.assert_allclose(res[1][2][:kdim + 1], res[0][2][:kdim + 1], rtol=1e-8, atol=1e-14)
+        bp = b.cpu().numpy().copy()
+        bp[::7] = np.nextafter(bp[::7], 2.0)
+        amd.lib().Nfft4GPAmdSetFgmresOrtho(1)
+        _, _, hp, itp = amd.fgmres(op, torch.tensor(bp, device="cuda"), torch.zeros_like(b), kdim=kdim,
+                                   maxits=maxits, tol=1e-8)
+        amd.lib().Nfft4GPAmdSetFgmresOrtho(0)
+        spread = np.max(np.abs(hp[:itp + 1] - res[0][2]) / res[0][2])
+        assert np.max(np.abs(res[1][2] - res[0][2]) / res[0][2]) <= 3 * spread + 1e-8
+    else:
+        # the history's tail sits at 1e-8 relative residual, where a 1e-16 rounding difference is 1e-8 relative
+        np.testing.assert_allclose(res[1][2], res[0][2], rtol=1e-8, atol=1e-14)
     op.free()
