@@ -212,7 +212,10 @@ int Nfft4GPAmdPcgHistoryLength(void);
 /* FGMRES's orthogonalisation: 0 (default) the reference's modified Gram-Schmidt (Nfft4GPModifiedGS,
  * matops.c:274-346: one launch per basis vector), 1 block classical Gram-Schmidt (two launches per pass
  * whatever the step; a second pass when the first drops ||w|| below 0.7071 of its value, the DGKS test of
- * matops.c:348-440; the same projections up to rounding; kdim <= 2046).  Env NFFT4GP_AMD_FGMRES_ORTHO.
+ * matops.c:348-440; the same projections up to rounding; kdim <= 2046), 2 delayed CGS2 (the second pass
+ * of column j run with step j + 1's first pass: two basis sweeps and one host read per step; no
+ * preconditioner -- with one, mode 1).  The block modes restart from the true residual norm (fgmres.c:236-243
+ * keeps the Givens estimate).  Env NFFT4GP_AMD_FGMRES_ORTHO.
  * Nfft4GPAmdFgmresSecondPasses: second passes taken since the last call (then reset). */
 void Nfft4GPAmdSetFgmresOrtho(int ortho);
 long long Nfft4GPAmdFgmresSecondPasses(void);

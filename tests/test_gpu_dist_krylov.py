@@ -58,6 +58,12 @@ def _worker(rank, world, port, outdir):
         out.update({part + "_loss": loss, part + "_grad": grad, part + "_x": xs.cpu().numpy(), part + "_it": it,
                     part + "_rr": rr, part + "_hist": hist, part + "_ld": ld, part + "_dld": dld,
                     part + "_rb": rb, part + "_re": re})
+        # delayed CGS2 (Nfft4GPAmdSetFgmresOrtho(2)), unrestarted: its sweeps' dots are summed over the ranks
+        amd.lib().Nfft4GPAmdSetFgmresOrtho(2)
+        xs = torch.zeros_like(b)
+        _, rr, hist, it = amd.fgmres(op, b, xs, kdim=120, maxits=120, tol=1e-10)
+        amd.lib().Nfft4GPAmdSetFgmresOrtho(0)
+        out.update({part + "_dx": xs.cpu().numpy(), part + "_dit": it, part + "_dhist": hist})
         op.free()
     torch.cuda.synchronize()
     comm.free()
@@ -88,9 +94,13 @@ def single(torch_cuda):
     xs = torch.zeros_like(b)
     _, rr, hist, it = amd.fgmres(op, b, xs, kdim=25, maxits=120, tol=1e-10)
     ld, dld = amd.logdet(op, 15, nvecs, rademacher=R)
+    amd.lib().Nfft4GPAmdSetFgmresOrtho(2)
+    dx = torch.zeros_like(b)
+    _, _, dhist, dit = amd.fgmres(op, b, dx, kdim=120, maxits=120, tol=1e-10)
+    amd.lib().Nfft4GPAmdSetFgmresOrtho(0)
     op.free()
     return {"loss": loss, "grad": grad, "x": xs.cpu().numpy(), "it": it, "hist": hist, "ld": ld, "dld": dld,
-            "z": z}
+            "z": z, "dx": dx.cpu().numpy(), "dit": dit, "dhist": dhist}
 
 
 def _rel(a, b):
@@ -131,3 +141,14 @@ def test_distributed_fgmres_and_logdet_match_single_gpu(gloo2, single, part):
     np.testing.assert_allclose(h0, h1, rtol=4e-2)
     assert float(gloo2[0][part + "_ld"]) == pytest.approx(single["ld"], rel=1e-10)
     np.testing.assert_allclose(gloo2[0][part + "_dld"], single["dld"], rtol=1e-8, atol=1e-12)
+
+
+@pytest.mark.parametrize("part", ["rows", "components"])
+def test_distributed_fgmres_dcgs2_matches_single_gpu(gloo2, single, part):
+    """Delayed CGS2 on the split operator: every rank takes the one-GPU iteration count, the history to 1e-8
+    and the solution to 1e-9 (unrestarted, so no restart amplification)."""
+    its = [int(r[part + "_dit"]) for r in gloo2]
+    assert len(set(its)) == 1 and its[0] == int(single["dit"]) > 0, (its, single["dit"])
+    x = np.concatenate([r[part + "_dx"] for r in gloo2]) if part == "rows" else gloo2[0][part + "_dx"]
+    assert _rel(x, single["dx"]) < 1e-9
+    np.testing.assert_allclose(gloo2[0][part + "_dhist"][:its[0] + 1], single["dhist"][:its[0] + 1], rtol=1e-8)
