@@ -111,14 +111,18 @@ __device__ __forceinline__ void stage_block_glds(double* __restrict__ s, const d
 // spread
 // ------------------------------------------------------------------------------------------------
 // at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
-// PREFETCH: the next run's tile is loaded before this run is processed (A/B variant)
-template <int THREADS, bool TIMELINE = false, bool PREFETCH = false>
+// PREFETCH: the next run's tile is loaded before this run is processed (A/B variant).
+// TAIL (row shards): instead of one partial grid per block for k_reduce_parts, every workgroup adds its folded
+// grid into gacc with fp64 atomics, and the last workgroup of each window group (an arrival ticket) moves the
+// group's sums to part = the shard's grid [comp][cell] and clears gacc and the ticket for the next call.
+template <int THREADS, bool TIMELINE = false, bool PREFETCH = false, bool TAIL = false>
 __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restrict__ meta,
                                                       const uint32_t* __restrict__ lo,
                                                       const uint32_t* __restrict__ qarr,
                                                       const int* __restrict__ tile_off, const double* __restrict__ x,
                                                       int n, int B, int nblocks, int ngroups, int CG, int nw,
-                                                      double* __restrict__ part)
+                                                      double* __restrict__ part, double* __restrict__ gacc,
+                                                      unsigned int* __restrict__ ticket)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = B + kPad;
@@ -196,7 +200,27 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
 #pragma unroll
          for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
       }
-      part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
+      if (TAIL)
+         unsafeAtomicAdd(gacc + (size_t)(c0 + cl) * kNos + gi, v);  // global_atomic_add_f64, no return
+      else
+         part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
+   }
+   if (TAIL) {
+      __shared__ int s_last;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's atomics have been performed
+      __syncthreads();
+      if (tid == 0)
+         s_last = __hip_atomic_fetch_add(ticket + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                  (unsigned)(nblocks - 1);
+      __syncthreads();
+      if (s_last) {
+         for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
+            double* a = gacc + (size_t)c0 * kNos + idx;
+            part[(size_t)c0 * kNos + idx] = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+         }
+         if (tid == 0) __hip_atomic_store(ticket + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
    }
    if (TIMELINE) {
       __syncthreads();
@@ -704,7 +728,7 @@ int upload_tap_coeffs()
 }
 
 typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, int, int, int,
-                         int, int, int, double*);
+                         int, int, int, double*, double*, unsigned int*);
 // 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py); 2: the next
 // run's tile loaded before this run is processed (A/B).  Variants that
 // measured slower or neutral (prefetching runs, persistent workgroups, several groups per workgroup, the fold in
@@ -743,7 +767,27 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
    const SpreadFn fn = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
    const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
    launch_ev(fn, dim3(gridx), dim3(kSpreadThreads), spread_lds_bytes(P), stream, P.kev ? P.kev + 0 : nullptr,
-             P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part);
+             P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part,
+             (double*)nullptr, (unsigned int*)nullptr);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+// a row shard's spread straight into its grid (the TAIL variant: no partial grids, no k_reduce_parts)
+int launch_spread_tail(const AdditivePlan& P, const double* d_x, double* d_grid, hipStream_t stream)
+{
+   if (P.dl.ntiles == 0 || P.n == 0 || !P.d_gacc || !P.d_gticket) return -1;
+   static const bool attr = [] {
+      (void)hipFuncSetAttribute((const void*)k_spread<kSpreadThreads, false, false, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipGetLastError();
+      return true;
+   }();
+   (void)attr;
+   const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
+   launch_ev(k_spread<kSpreadThreads, false, false, true>, dim3(gridx), dim3(kSpreadThreads), spread_lds_bytes(P),
+             stream, P.kev ? P.kev + 0 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks,
+             P.ngroups, P.CG, P.nw, d_grid, P.d_gacc, P.d_gticket);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
