@@ -10,4 +10,4 @@ for rep in 1 2; do
   done
 done
 bash tools/ab_env.sh "NFFT4GP_AMD_SPREAD_VARIANT=0 NFFT4GP_AMD_SPREAD_VARIANT=2 NFFT4GP_AMD_BLOCK=2032 NFFT4GP_AMD_CG=4,NFFT4GP_AMD_BLOCK=3840" --steps 300 || exit 1
-bash tools/ab_env.sh "NFFT4GP_AMD_SPREAD_VARIANT=0 NFFT4GP_AMD_SPREAD_VARIANT=2" --n 10000000 --d 64 --steps 30 --warmup 5
+bash tools/ab_env.sh "NFFT4GP_AMD_SPREAD_VARIANT=0 NFFT4GP_AMD_SPREAD_VARIANT=2 NFFT4GP_AMD_BLOCK=2032" --n 10000000 --d 64 --steps 30 --warmup 5
