@@ -459,23 +459,11 @@ struct Ctx {
    // w -= h u (u optional), *out = (w, v) or ||w||^2
    int gs(double* w, const double* u, const double* hprev, const double* v, double* out)
    {
-      static const int variant = getenv("NFFT4GP_AMD_GS_VARIANT") ? atoi(getenv("NFFT4GP_AMD_GS_VARIANT")) : 1;
-      auto grid_for = [&](int T, int E) {
-         return (unsigned)std::max<size_t>(1, std::min<size_t>((n + (size_t)T * E - 1) / ((size_t)T * E), kKMaxBlocks));
-      };
-      if (variant == 1) {
-         hipLaunchKernelGGL((k_gs_step<1024, 4>), dim3(grid_for(1024, 4)), dim3(1024), 0, s, w, u, hprev, v, n,
-                            g_k.part, g_k.ticket, out);
-      } else if (variant == 2) {
-         hipLaunchKernelGGL((k_gs_step<1024, 8>), dim3(grid_for(1024, 8)), dim3(1024), 0, s, w, u, hprev, v, n,
-                            g_k.part, g_k.ticket, out);
-      } else if (variant == 3) {
-         hipLaunchKernelGGL((k_gs_step<512, 4>), dim3(grid_for(512, 4)), dim3(512), 0, s, w, u, hprev, v, n,
-                            g_k.part, g_k.ticket, out);
-      } else {
-         hipLaunchKernelGGL(k_gs_step<kKThreads>, dim3(kgrid(n)), dim3(kKThreads), 0, s, w, u, hprev, v, n, g_k.part,
-                            g_k.ticket, out);
-      }
+      // 1024 threads x 4 elements: a quarter of the 256-thread partials for the last block to add (8.35 us per
+      // projection at n = 1e6 against 9.16; 1024 x 8: 10.7, 512 x 4: 8.49 -- round 3, tools/ab_gs.sh, removed)
+      const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((n + 4095) / 4096, kKMaxBlocks));
+      hipLaunchKernelGGL((k_gs_step<1024, 4>), dim3(grid), dim3(1024), 0, s, w, u, hprev, v, n, g_k.part, g_k.ticket,
+                         out);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return red(out, 1);
    }

@@ -1,5 +1,5 @@
 # A/B of environment settings on the bench workload (the library reads its knobs at handle creation):
-#   bash tools/ab_env.sh "NFFT4GP_AMD_SPREAD_VARIANT=0 NFFT4GP_AMD_SPREAD_VARIANT=2,NFFT4GP_AMD_SPREAD2_GPW=2" [bench args]
+#   bash tools/ab_env.sh "NFFT4GP_AMD_SPREAD_VARIANT=0 NFFT4GP_AMD_BLOCK=2032,NFFT4GP_AMD_CG=2" [bench args]
 # one setting per word, several variables of one setting joined by commas
 set -o pipefail
 mkdir -p gpurun_out
