@@ -971,9 +971,9 @@ int Nfft4GPAmdShardSpread(void* str, const double* x_local, double* grid)
       NFFT4GP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * P.nw * kNos, s));
       return 0;
    }
-   // the spread's atomic tail writes the grid the caller all-reduces (NFFT4GP_AMD_SHARD_TAIL=0: the blocks'
-   // partial grids summed by k_reduce_parts, for A/B)
-   static const int tail = getenv("NFFT4GP_AMD_SHARD_TAIL") ? atoi(getenv("NFFT4GP_AMD_SHARD_TAIL")) : 1;
+   // the blocks' partial grids summed by k_reduce_parts into the grid the caller all-reduces, or (A/B,
+   // NFFT4GP_AMD_SHARD_TAIL=1) the spread's atomic tail writing that grid directly
+   static const int tail = getenv("NFFT4GP_AMD_SHARD_TAIL") ? atoi(getenv("NFFT4GP_AMD_SHARD_TAIL")) : 0;
    if (tail && P.d_gacc && !P.timing) return launch_spread_tail(P, x_local, grid, s);
    if (launch_spread(P, x_local, P.d_part, s)) return -1;
    return launch_reduce_parts(P, P.d_part, grid, s);
