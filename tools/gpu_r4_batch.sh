@@ -4,6 +4,8 @@ set -o pipefail
 mkdir -p gpurun_out/r4
 timeout -k 10 500 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_gpu_dist_krylov.py tests/test_gpu_dist.py tests/test_gpu_configs.py > gpurun_out/r4/pt_batch.log 2>&1 || { echo PYTEST_FAIL; tail -30 gpurun_out/r4/pt_batch.log; exit 1; }
 tail -2 gpurun_out/r4/pt_batch.log
+NFFT4GP_AMD_SHARD_TAIL=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_gpu_dist.py tests/test_gpu_configs.py > gpurun_out/r4/pt_tail.log 2>&1 || { echo PYTEST_TAIL_FAIL; tail -30 gpurun_out/r4/pt_tail.log; exit 1; }
+tail -2 gpurun_out/r4/pt_tail.log
 NFFT4GP_AMD_SPREAD_VARIANT=3 NFFT4GP_AMD_BLOCK=2032 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_nfft.py tests/test_gpu_golden.py > gpurun_out/r4/pt_v3.log 2>&1 || { echo PYTEST_V3_FAIL; tail -30 gpurun_out/r4/pt_v3.log; exit 1; }
 tail -2 gpurun_out/r4/pt_v3.log
 for rep in 1 2; do
