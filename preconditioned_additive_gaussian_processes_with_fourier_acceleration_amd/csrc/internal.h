@@ -184,8 +184,6 @@ struct AdditivePlan {
    DevLayout dl;
    // device buffers
    double* d_part = nullptr;  // [nblocks][nw][64]
-   double* d_gacc = nullptr;          // row shards: [nw][64] fp64 sums of the spread's atomic tail (kept zero)
-   unsigned int* d_gticket = nullptr; // row shards: per window group arrival tickets (kept zero)
    double* d_w = nullptr;     // [nw][64] circulant, kernel
    double* d_wd = nullptr;    // [nw][64] circulant, derivative kernel
    double* d_H = nullptr;     // [nw][64][kNC]
@@ -214,7 +212,6 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream);
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream);
 int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream);
-int launch_spread_tail(const AdditivePlan& P, const double* d_x, double* d_grid, hipStream_t stream);
 // row shards with few blocks: grid from the summed grids + y = beta y + alpha f^2 mu x, then the interpolation
 // with S workgroups per block adding into y atomically (plain matvec)
 int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, double alpha, const double* d_x,

@@ -146,10 +146,6 @@ void free_layout(AdditivePlan& P)
    P.dl = DevLayout();
    dfree(P.d_part);
    dfree(P.d_part2);
-   dfree(P.d_gacc);
-   dfree(P.d_gticket);
-   P.d_gacc = nullptr;
-   P.d_gticket = nullptr;
    dfree(P.d_H2);
    dfree(P.d_dot_part);
    dfree(P.d_dot_ticket);
@@ -310,12 +306,7 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
    }
    P.nparts = P.nblocks;
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part, sizeof(double) * (size_t)std::max(1, P.nparts) * P.nw * kNos));
-   if (P.row_begin != 0 || P.row_end != P.n_global) {  // a row shard: the spread's atomic tail
-      NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_gacc, sizeof(double) * (size_t)P.nw * kNos));
-      NFFT4GP_HIP_CHECK(hipMemset(P.d_gacc, 0, sizeof(double) * (size_t)P.nw * kNos));
-      NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_gticket, sizeof(unsigned int) * (size_t)std::max(1, P.ngroups)));
-      NFFT4GP_HIP_CHECK(hipMemset(P.d_gticket, 0, sizeof(unsigned int) * (size_t)std::max(1, P.ngroups)));
-   }
+
    dfree(P.d_dot_part);
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_dot_part, sizeof(double) * (size_t)std::max(1, P.nblocks)));
    if (!P.d_dot_ticket) {
@@ -971,10 +962,7 @@ int Nfft4GPAmdShardSpread(void* str, const double* x_local, double* grid)
       NFFT4GP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * P.nw * kNos, s));
       return 0;
    }
-   // the blocks' partial grids summed by k_reduce_parts into the grid the caller all-reduces, or (A/B,
-   // NFFT4GP_AMD_SHARD_TAIL=1) the spread's atomic tail writing that grid directly
-   static const int tail = getenv("NFFT4GP_AMD_SHARD_TAIL") ? atoi(getenv("NFFT4GP_AMD_SHARD_TAIL")) : 0;
-   if (tail && P.d_gacc && !P.timing) return launch_spread_tail(P, x_local, grid, s);
+   // the blocks' partial grids summed by k_reduce_parts into the grid the caller all-reduces
    if (launch_spread(P, x_local, P.d_part, s)) return -1;
    return launch_reduce_parts(P, P.d_part, grid, s);
 }

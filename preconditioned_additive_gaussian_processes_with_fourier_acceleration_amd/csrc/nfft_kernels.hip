@@ -111,18 +111,13 @@ __device__ __forceinline__ void stage_block_glds(double* __restrict__ s, const d
 // spread
 // ------------------------------------------------------------------------------------------------
 // at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
-// PREFETCH: the next run's tile is loaded before this run is processed (A/B variant).
-// TAIL (row shards): instead of one partial grid per block for k_reduce_parts, every workgroup adds its folded
-// grid into gacc with fp64 atomics, and the last workgroup of each window group (an arrival ticket) moves the
-// group's sums to part = the shard's grid [comp][cell] and clears gacc and the ticket for the next call.
-template <int THREADS, bool TIMELINE = false, bool PREFETCH = false, bool TAIL = false>
+template <int THREADS, bool TIMELINE = false>
 __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restrict__ meta,
                                                       const uint32_t* __restrict__ lo,
                                                       const uint32_t* __restrict__ qarr,
                                                       const int* __restrict__ tile_off, const double* __restrict__ x,
                                                       int n, int B, int nblocks, int ngroups, int CG, int nw,
-                                                      double* __restrict__ part, double* __restrict__ gacc,
-                                                      unsigned int* __restrict__ ticket)
+                                                      double* __restrict__ part)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = B + kPad;
@@ -157,8 +152,6 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
 
    const int c0 = g * CG;
    for (; t < t1; t += nwaves) {
-      TileRegs nxt;
-      if (PREFETCH && t + nwaves < t1) load_tile(nxt, meta, lo, qarr, t + nwaves, lane);  // in flight during this run
       double acc[kNC];
 #pragma unroll
       for (int d = 0; d < kNC; d++) acc[d] = 0.0;
@@ -179,10 +172,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
       double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
 #pragma unroll
       for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
-      if (PREFETCH)
-         cur = nxt;
-      else if (t + nwaves < t1)
-         load_tile(cur, meta, lo, qarr, t + nwaves, lane);
+      if (t + nwaves < t1) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
    }
    __syncthreads();
    if (TIMELINE) stamp(2);
@@ -200,123 +190,11 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
 #pragma unroll
          for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
       }
-      if (TAIL)
-         unsafeAtomicAdd(gacc + (size_t)(c0 + cl) * kNos + gi, v);  // global_atomic_add_f64, no return
-      else
-         part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
-   }
-   if (TAIL) {
-      __shared__ int s_last;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's atomics have been performed
-      __syncthreads();
-      if (tid == 0)
-         s_last = __hip_atomic_fetch_add(ticket + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                  (unsigned)(nblocks - 1);
-      __syncthreads();
-      if (s_last) {
-         for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
-            double* a = gacc + (size_t)c0 * kNos + idx;
-            part[(size_t)c0 * kNos + idx] = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-         }
-         if (tid == 0) __hip_atomic_store(ticket + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
    }
    if (TIMELINE) {
       __syncthreads();
       stamp(3);
-   }
-}
-
-// Persistent spread (A/B variant 3): a grid of co-resident workgroups, each taking a contiguous range of
-// (block, group) items in block-major order, so consecutive items mostly share their block's alpha slice, which
-// is staged once.  Two alpha buffers: when the next item starts a new block, every wave issues its LDS-DMA
-// pieces of that block as soon as it has issued its last tile load of the current item, so the staging overlaps
-// the last run, the fold and the next item's moment-table clear instead of opening the item.
-template <int THREADS>
-__global__ __launch_bounds__(THREADS, 6) void k_spread_persist(const uint16_t* __restrict__ meta,
-                                                              const uint32_t* __restrict__ lo,
-                                                              const uint32_t* __restrict__ qarr,
-                                                              const int* __restrict__ tile_off,
-                                                              const double* __restrict__ x, int n, int B, int nblocks,
-                                                              int ngroups, int CG, int nw, double* __restrict__ part,
-                                                              double* __restrict__ /*gacc*/,
-                                                              unsigned int* __restrict__ /*ticket*/)
-{
-   extern __shared__ __attribute__((aligned(16))) double smem[];
-   const int Bp = B + kPad;
-   double* s_mom = smem + 2 * Bp;
-   const int nitems = nblocks * ngroups;
-   const int per = (nitems + (int)gridDim.x - 1) / (int)gridDim.x;
-   const int i0 = (int)blockIdx.x * per, i1 = min(nitems, i0 + per);
-   if (i0 >= i1) return;
-   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-   constexpr int nwaves = THREADS / 64;
-   int buf = 0;
-   int bcur = i0 / ngroups;
-   stage_block_glds<THREADS>(smem, x, bcur * B, min(B, n - bcur * B), B);
-   for (int it = i0; it < i1; it++) {
-      const int b = it / ngroups, g = it - b * ngroups;
-      if (b != bcur) {  // prefetched during the previous item
-         buf ^= 1;
-         bcur = b;
-      }
-      const double* sa = smem + buf * Bp;
-      TileRegs cur;
-      const int t1 = tile_off[it + 1];
-      int t = tile_off[it] + wave;
-      if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
-      for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of the block have landed
-      __syncthreads();
-      const int bn = it + 1 < i1 ? (it + 1) / ngroups : -1;
-      const bool pf = bn >= 0 && bn != b;
-      bool issued = false;
-      const int c0 = g * CG;
-      for (; t < t1; t += nwaves) {
-         const bool last = t + nwaves >= t1;
-         if (last && pf) {  // no tile load follows in this item: start the next block's alpha
-            stage_block_glds<THREADS>(smem + (buf ^ 1) * Bp, x, bn * B, min(B, n - bn * B), B);
-            issued = true;
-         }
-         double acc[kNC];
-#pragma unroll
-         for (int d = 0; d < kNC; d++) acc[d] = 0.0;
-#pragma unroll
-         for (int r = 0; r < kR; r++) {
-            const uint32_t loc = slot_loc(cur, r);
-            const double u = q_to_u(cur.qq[r]);
-            double tpow = sa[loc];
-            acc[0] += tpow;
-#pragma unroll
-            for (int d = 1; d < kNC; d++) {
-               tpow *= u;
-               acc[d] += tpow;
-            }
-         }
-         const int comp_local = (int)(cur.mt >> 6) - c0;
-         const int cell = (int)(cur.mt & 63u);
-         double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
-#pragma unroll
-         for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);
-         if (!last) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
-      }
-      if (pf && !issued) stage_block_glds<THREADS>(smem + (buf ^ 1) * Bp, x, bn * B, min(B, n - bn * B), B);
-      __syncthreads();
-      const int ncomp = min(CG, nw - c0);
-      for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
-         const int cl = idx / kNos;
-         const int gi = idx % kNos;
-         double v = 0.0;
-#pragma unroll 1
-         for (int tp = 0; tp < kTaps; tp++) {
-            const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
-#pragma unroll
-            for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
-         }
-         part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;
-      }
-      __syncthreads();  // the fold's reads of the moment table precede the next item's clear
    }
 }
 
@@ -820,16 +698,13 @@ int upload_tap_coeffs()
 }
 
 typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, int, int, int,
-                         int, int, int, double*, double*, unsigned int*);
-// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py); 2: the next
-// run's tile loaded before this run is processed (A/B); 3: persistent workgroups with a prefetched second
-// alpha buffer (A/B).  Variants that
+                         int, int, int, double*);
+// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py).  Variants that
 // measured slower or neutral (prefetching runs, persistent workgroups, several groups per workgroup, the fold in
 // two chains, register-staged alpha, the row shards' block sum in the spread's tail) were removed in round 4;
 // DESIGN.md 3.5 keeps their numbers.
 constexpr int kSpreadThreads = 512;
-static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>,
-                                           k_spread<kSpreadThreads, false, true>, k_spread_persist<kSpreadThreads>};
+static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>};
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
 constexpr int kInterpThreads = 1024;
@@ -857,37 +732,10 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
    raise_lds_limit_once();
-   const int variant = std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1);
-   const SpreadFn fn = kSpreadVariants[variant];
-   int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
-   size_t lds = spread_lds_bytes(P);
-   if (variant == 3) {  // persistent: two alpha buffers, as many workgroups as fit the CUs at once
-      lds += sizeof(double) * ((size_t)P.B + kPad);
-      const int per_cu = std::max(1, std::min(3, (int)((160 * 1024) / lds)));
-      gridx = std::min(P.nblocks * P.ngroups, 256 * per_cu);
-   }
-   launch_ev(fn, dim3(gridx), dim3(kSpreadThreads), lds, stream, P.kev ? P.kev + 0 : nullptr,
-             P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part,
-             (double*)nullptr, (unsigned int*)nullptr);
-   NFFT4GP_HIP_CHECK(hipGetLastError());
-   return 0;
-}
-
-// a row shard's spread straight into its grid (the TAIL variant: no partial grids, no k_reduce_parts)
-int launch_spread_tail(const AdditivePlan& P, const double* d_x, double* d_grid, hipStream_t stream)
-{
-   if (P.dl.ntiles == 0 || P.n == 0 || !P.d_gacc || !P.d_gticket) return -1;
-   static const bool attr = [] {
-      (void)hipFuncSetAttribute((const void*)k_spread<kSpreadThreads, false, false, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipGetLastError();
-      return true;
-   }();
-   (void)attr;
+   const SpreadFn fn = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
    const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
-   launch_ev(k_spread<kSpreadThreads, false, false, true>, dim3(gridx), dim3(kSpreadThreads), spread_lds_bytes(P),
-             stream, P.kev ? P.kev + 0 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks,
-             P.ngroups, P.CG, P.nw, d_grid, P.d_gacc, P.d_gticket);
+   launch_ev(fn, dim3(gridx), dim3(kSpreadThreads), spread_lds_bytes(P), stream, P.kev ? P.kev + 0 : nullptr,
+             P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

@@ -11,7 +11,7 @@ tail -2 gpurun_out/r4/pt_v3.log
 for rep in 1 2; do
   for t in 0 1; do
     r=$(NFFT4GP_AMD_SHARD_TAIL=$t timeout -k 10 120 python tools/shard_probe.py --ranks 8 2>/dev/null) || { echo PROBE_FAIL; exit 1; }
-    echo "tail=$t rep=$rep $r"
+    echo " rep=$rep $r"
   done
 done
 bash tools/ab_env.sh "NFFT4GP_AMD_SPREAD_VARIANT=0 NFFT4GP_AMD_SPREAD_VARIANT=2 NFFT4GP_AMD_BLOCK=2032 NFFT4GP_AMD_BLOCK=2032,NFFT4GP_AMD_SPREAD_VARIANT=3 NFFT4GP_AMD_SPREAD_VARIANT=3 NFFT4GP_AMD_CG=4,NFFT4GP_AMD_BLOCK=3840" --steps 300 || exit 1
