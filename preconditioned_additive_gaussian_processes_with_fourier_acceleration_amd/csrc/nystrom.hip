@@ -278,8 +278,8 @@ static unsigned gemm_blocks(int M, int N, int K, int ksplit)
 static void gemm_attr_once()
 {
    static const bool done = []() {
-      (void)hipFuncSetAttribute((const void*)k_gemm_f64<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmLds);
-      (void)hipFuncSetAttribute((const void*)k_gemm_f64<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmLds);
+      for (const void* f : {(const void*)k_gemm_f64<false>, (const void*)k_gemm_f64<true>})
+         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmLds);
       (void)hipGetLastError();
       return true;
    }();
