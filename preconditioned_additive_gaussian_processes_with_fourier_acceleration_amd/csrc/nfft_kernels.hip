@@ -111,11 +111,7 @@ __device__ __forceinline__ void stage_block_glds(double* __restrict__ s, const d
 // spread
 // ------------------------------------------------------------------------------------------------
 // at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
-// GATHER (A/B variant 2): no alpha slice in LDS -- every run gathers its 16 alpha values from the block's
-// slice of x in global memory (L2-resident: the block's 11 window groups read the same 32 KB), so a workgroup
-// starts on its first run after one tile-load latency instead of staging the slice first (a row shard's waves
-// run at most one run each); the LDS holds the moment table only
-template <int THREADS, bool TIMELINE = false, bool GATHER = false>
+template <int THREADS, bool TIMELINE = false>
 __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restrict__ meta,
                                                       const uint32_t* __restrict__ lo,
                                                       const uint32_t* __restrict__ qarr,
@@ -124,7 +120,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
                                                       double* __restrict__ part)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
-   const int Bp = GATHER ? 0 : B + kPad;
+   const int Bp = B + kPad;
    double* s_alpha = smem;     // Bp
    double* s_mom = smem + Bp;  // CG*64*kMomStride per-cell moments
 
@@ -148,11 +144,9 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    int t = tile_off[b * ngroups + g] + wave;
    if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
    const int base = b * B;
-   const int nloc = min(B, n - base);
-   const double* xb = x + base;
-   if (!GATHER) stage_block_glds<THREADS>(s_alpha, x, base, nloc, B);
+   stage_block_glds<THREADS>(s_alpha, x, base, min(B, n - base), B);
    for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
-   if (!GATHER) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces have landed
+   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces have landed
    __syncthreads();
    if (TIMELINE) stamp(1);
 
@@ -161,19 +155,11 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
       double acc[kNC];
 #pragma unroll
       for (int d = 0; d < kNC; d++) acc[d] = 0.0;
-      double av[kR];
-      if (GATHER) {  // all 16 gathers in flight before the first use (dummy slots point past the block: 0)
-#pragma unroll
-         for (int r = 0; r < kR; r++) {
-            const uint32_t loc = slot_loc(cur, r);
-            av[r] = loc < (uint32_t)nloc ? xb[loc] : 0.0;
-         }
-      }
 #pragma unroll
       for (int r = 0; r < kR; r++) {
          const uint32_t loc = slot_loc(cur, r);
          const double u = q_to_u(cur.qq[r]);
-         double tpow = GATHER ? av[r] : s_alpha[loc];
+         double tpow = s_alpha[loc];
          acc[0] += tpow;
 #pragma unroll
          for (int d = 1; d < kNC; d++) {
@@ -713,14 +699,12 @@ int upload_tap_coeffs()
 
 typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, int, int, int,
                          int, int, int, double*);
-// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py); 2: alpha
-// gathered from global memory instead of staged in LDS (A/B).  Variants that
+// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py).  Variants that
 // measured slower or neutral (prefetching runs, persistent workgroups, several groups per workgroup, the fold in
 // two chains, register-staged alpha, the row shards' block sum in the spread's tail) were removed in round 4;
 // DESIGN.md 3.5 keeps their numbers.
 constexpr int kSpreadThreads = 512;
-static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>,
-                                           k_spread<kSpreadThreads, false, true>};
+static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>};
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
 constexpr int kInterpThreads = 1024;
@@ -748,11 +732,9 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
    raise_lds_limit_once();
-   const int variant = std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1);
-   const SpreadFn fn = kSpreadVariants[variant];
+   const SpreadFn fn = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
    const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
-   const size_t lds = variant == 2 ? sizeof(double) * (size_t)P.CG * kNos * kMomStride : spread_lds_bytes(P);
-   launch_ev(fn, dim3(gridx), dim3(kSpreadThreads), lds, stream, P.kev ? P.kev + 0 : nullptr,
+   launch_ev(fn, dim3(gridx), dim3(kSpreadThreads), spread_lds_bytes(P), stream, P.kev ? P.kev + 0 : nullptr,
              P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
