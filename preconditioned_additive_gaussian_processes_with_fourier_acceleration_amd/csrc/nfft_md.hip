@@ -239,6 +239,127 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
    }
 }
 
+// Line-owned spread (NFFT4GP_AMD_MD_SPREAD=2, A/B): the tiled spread's work items, but a thread owns one line
+// of the tile's footprint along axis 0 (17^(d-1) lines: 289 in 3-D) and keeps its 17 cells in registers; the
+// item's points are staged 64 at a time in LDS (x_j folded into the axis-0 taps, padded by 8 zeros on each
+// side so a point's taps land on the line's cells by an offset read), and every line walks them in order,
+// adding the point's row when it covers the line.  No LDS atomics: each cell is summed by one thread in
+// point order.  With fewer than 3 features, `groups` copies of the lines walk interleaved points and are
+// added in group order in LDS.  The item's cells go to the grid in exact fixed point (to_fix / fix_add).
+constexpr int kMdLinesThreads = 320;  // the 289 lines of a 3-D footprint
+constexpr int kMdStage = 64;          // points per staging round
+constexpr int kMdPadX = 26;           // 8 zeros, 10 taps, 8 zeros
+constexpr size_t kMdLinesStageLds = sizeof(double) * kMdStage * (kMdPadX + 2 * kTaps);
+constexpr size_t kMdLinesRedLds = sizeof(double) * kMdLinesThreads * kMdFoot;
+__global__ __launch_bounds__(kMdLinesThreads) void k_md_spread_lines(const MdComp* __restrict__ comps,
+                                                                     const int4* __restrict__ items,
+                                                                     const int* __restrict__ perm,
+                                                                     const int* __restrict__ u,
+                                                                     const double* __restrict__ psi,
+                                                                     const double* __restrict__ x, int n,
+                                                                     unsigned long long* __restrict__ grid, long long G,
+                                                                     const unsigned long long* __restrict__ xmax,
+                                                                     double psi_max)
+{
+   extern __shared__ double sm[];
+   double* s_px = sm;                         // [kMdStage][kMdPadX]
+   double* s_py = s_px + kMdStage * kMdPadX;  // [kMdStage][kTaps]
+   double* s_pz = s_py + kMdStage * kTaps;    // [kMdStage][kTaps]
+   double* s_red = s_pz + kMdStage * kTaps;   // [groups][lines][17] (d < 3 only)
+   __shared__ int4 s_o[kMdStage];             // the point's first tap cell relative to the tile, per axis
+   const int4 it = items[blockIdx.x];
+   const MdComp cp = comps[it.x];
+   const int d = cp.d;
+   int lines = 1;
+   for (int t = 1; t < d; t++) lines *= kMdFoot;
+   const int groups = kMdLinesThreads / lines;
+   const int tid = threadIdx.x;
+   const int grp = tid / lines, line = tid - grp * lines;
+   const bool active = grp < groups;
+   const int yl = line % kMdFoot, zl = line / kMdFoot;
+   int lo[kMdMaxDim];
+   {
+      int rem = it.y;
+      for (int t = 0; t < d; t++) {
+         lo[t] = (rem % (kNos / kMdTile)) * kMdTile;
+         rem /= kNos / kMdTile;
+      }
+   }
+   double acc[kMdFoot];
+#pragma unroll
+   for (int c = 0; c < kMdFoot; c++) acc[c] = 0.0;
+   const int* pp = perm + (long long)it.x * n;
+   for (int c0 = it.z; c0 < it.w; c0 += kMdStage) {
+      const int cnt = min(kMdStage, it.w - c0);
+      for (int e = tid; e < cnt * 32; e += kMdLinesThreads) {
+         const int p = e >> 5, q = e & 31;
+         const int j = pp[c0 + p];
+         const int* uj = u + cp.u_off + (long long)j * d;
+         const double* pj = psi + (cp.u_off + (long long)j * d) * kTaps;
+         if (q < kTaps) {
+            s_px[p * kMdPadX + 8 + q] = x[j] * pj[q];
+         } else if (q < 2 * kTaps) {
+            s_py[p * kTaps + q - kTaps] = d > 1 ? pj[q] : (q == kTaps ? 1.0 : 0.0);
+         } else if (q < 3 * kTaps) {
+            s_pz[p * kTaps + q - 2 * kTaps] = d > 2 ? pj[q] : (q == 2 * kTaps ? 1.0 : 0.0);
+         } else if (q == 30) {
+            s_o[p] = make_int4((uj[0] & (kNos - 1)) - lo[0], d > 1 ? (uj[1] & (kNos - 1)) - lo[1] : 0,
+                               d > 2 ? (uj[2] & (kNos - 1)) - lo[2] : 0, 0);
+         } else {
+#pragma unroll
+            for (int z = 0; z < 8; z++) {
+               s_px[p * kMdPadX + z] = 0.0;
+               s_px[p * kMdPadX + 18 + z] = 0.0;
+            }
+         }
+      }
+      __syncthreads();
+      if (active) {
+         for (int p = grp; p < cnt; p += groups) {
+            const int4 o = s_o[p];
+            const int ly = yl - o.y, lz = zl - o.z;
+            if ((unsigned)ly < (unsigned)kTaps && (unsigned)lz < (unsigned)kTaps) {
+               const double wyz = s_py[p * kTaps + ly] * s_pz[p * kTaps + lz];
+               const double* px = s_px + p * kMdPadX + 8 - o.x;  // px[c] = x_j psi_x[c - o.x], zero outside
+#pragma unroll
+               for (int c = 0; c < kMdFoot; c++) acc[c] = fma(wyz, px[c], acc[c]);
+            }
+         }
+      }
+      __syncthreads();  // the stage is rewritten next round
+   }
+   const int ex = fix_exp(xmax, (double)n, psi_max, d);
+   unsigned long long* g = grid + 2 * (long long)it.x * G;
+   auto flush = [&](int c, int yy, int zz, double v) {
+      if (v == 0.0) return;
+      long long idx = (lo[0] + c) & (kNos - 1);
+      if (d > 1) idx += (long long)((lo[1] + yy) & (kNos - 1)) * kNos;
+      if (d > 2) idx += (long long)((lo[2] + zz) & (kNos - 1)) * kNos * kNos;
+      unsigned long long L;
+      long long H;
+      to_fix(v, ex, L, H);
+      fix_add(g + 2 * idx, L, H);
+   };
+   if (groups == 1) {
+      if (active) {
+#pragma unroll
+         for (int c = 0; c < kMdFoot; c++) flush(c, yl, zl, acc[c]);
+      }
+   } else {
+      if (active) {
+#pragma unroll
+         for (int c = 0; c < kMdFoot; c++) s_red[(grp * lines + line) * kMdFoot + c] = acc[c];
+      }
+      __syncthreads();
+      for (int e = tid; e < lines * kMdFoot; e += kMdLinesThreads) {
+         double v = 0.0;
+         for (int gr = 0; gr < groups; gr++) v += s_red[gr * lines * kMdFoot + e];
+         const int ln = e / kMdFoot;
+         flush(e - ln * kMdFoot, ln % kMdFoot, ln / kMdFoot, v);
+      }
+   }
+}
+
 // Tiled interpolation, the spread's work items: the tile's footprint of h (and h' for the gradient) is
 // staged in LDS, each point's 10^d taps are read from there by a group of L lanes (L = 64 / 16 / 1 for
 // 3 / 2 / 1 features: the point's tap rows strided over the group, a fixed-order butterfly sum), and the
@@ -804,6 +925,23 @@ static int md_spread_fix(const AdditivePlan& P, const double* d_x, double psi_ma
 {
    const MdPlan& D = P.md;
    static const int tiled = getenv("NFFT4GP_AMD_MD_SPREAD") ? atoi(getenv("NFFT4GP_AMD_MD_SPREAD")) : 1;
+   if (tiled == 2 && D.nitems > 0 && D.maxd <= kMdTiledMaxDim) {
+      int mind = kMdMaxDim;
+      for (const MdComp& c : D.comps) mind = std::min(mind, c.d);
+      const size_t lds = kMdLinesStageLds + (mind < 3 ? kMdLinesRedLds : 0);
+      static const bool attr = [] {
+         (void)hipFuncSetAttribute((const void*)k_md_spread_lines, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024);
+         (void)hipGetLastError();
+         return true;
+      }();
+      (void)attr;
+      hipLaunchKernelGGL(k_md_spread_lines, dim3(D.nitems), dim3(kMdLinesThreads), lds, s, D.d_comps, D.d_items,
+                         D.d_perm, D.d_u, D.d_psi, d_x, P.n, D.d_gfix, D.G, (const unsigned long long*)D.d_xmax,
+                         psi_max);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   }
    if (tiled && D.nitems > 0 && D.maxd <= kMdTiledMaxDim) {
       size_t foot = 1;
       for (int t = 0; t < D.maxd; t++) foot *= kMdFoot;
