@@ -156,6 +156,7 @@ struct MdPlan {
    int* d_perm = nullptr;    // [comp][n] local point indices in tile order
    int4* d_items = nullptr;  // {comp, tile, first, end} (first/end index the component's d_perm)
    int nitems = 0;
+   bool lines = false;       // spread by k_md_spread_lines (all windows 3-D, n >= 4e5; NFFT4GP_AMD_MD_SPREAD overrides)
    double* d_part = nullptr; // tiled interpolation: [2][comp][n] per-component values (K, then K')
    // the spread adds in 128-bit fixed point (exact, so the grid does not depend on the order of the atomics):
    // d_gfix [nw][G][lo, hi] 64-bit pairs, d_xmax the bits of max |x| of the launch, psi_max the largest tap

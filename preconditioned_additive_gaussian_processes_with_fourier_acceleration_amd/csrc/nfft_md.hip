@@ -815,7 +815,16 @@ int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
    if (D.maxd <= kMdTiledMaxDim) {
       // taps per work item (A/B knob NFFT4GP_AMD_MD_CHUNK; the results do not depend on it beyond the spread's
       // fixed-point rounding, which is exact)
-      long long chunk_taps = 50000;  // 256 points (3-D) / 500 (2-D): tools/md_chunk_sweep.sh, profiles/r04_md_chunk_sweep.txt
+      // The spread kernel: line-owned (k_md_spread_lines) when every window has 3 features and the tiles hold
+      // ~1000 points or more (n >= 4e5 over 512 tiles), on 1000-point items; otherwise the wave-owned tiled
+      // kernel on items of 256 (3-D) / 500 (2-D) points (profiles/r04_md_chunk_sweep.txt, r04_md_lines_ab.txt,
+      // r04_md_lines_chunks.txt).  NFFT4GP_AMD_MD_SPREAD (0 untiled, 1 tiled, 2 lines) and
+      // NFFT4GP_AMD_MD_CHUNK (taps per item) override.
+      int mind = kMdMaxDim;
+      for (const MdComp& c : D.comps) mind = std::min(mind, c.d);
+      D.lines = mind == 3 && D.maxd == 3 && n >= 400000;
+      if (const char* e = getenv("NFFT4GP_AMD_MD_SPREAD")) D.lines = atoi(e) == 2;
+      long long chunk_taps = D.lines ? 1000000 : 50000;
       if (const char* e = getenv("NFFT4GP_AMD_MD_CHUNK")) chunk_taps = std::max(1000LL, atoll(e));
       std::vector<int> perm((size_t)P.nw * n);
       std::vector<std::vector<int4>> citems(P.nw);
@@ -925,7 +934,7 @@ static int md_spread_fix(const AdditivePlan& P, const double* d_x, double psi_ma
 {
    const MdPlan& D = P.md;
    static const int tiled = getenv("NFFT4GP_AMD_MD_SPREAD") ? atoi(getenv("NFFT4GP_AMD_MD_SPREAD")) : 1;
-   if (tiled == 2 && D.nitems > 0 && D.maxd <= kMdTiledMaxDim) {
+   if (D.lines && D.nitems > 0 && D.maxd <= kMdTiledMaxDim) {
       int mind = kMdMaxDim;
       for (const MdComp& c : D.comps) mind = std::min(mind, c.d);
       const size_t lds = kMdLinesStageLds + (mind < 3 ? kMdLinesRedLds : 0);

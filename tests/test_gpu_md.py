@@ -207,6 +207,31 @@ def test_md_matvec_is_bitwise_reproducible(torch_cuda, n, nw, dw):
     np.testing.assert_array_equal(gs[0], gs[1])
 
 
+def test_line_spread_matches_tiled_and_is_reproducible(torch_cuda, monkeypatch):
+    """Handles whose windows all have 3 features and n >= 4e5 spread with k_md_spread_lines (a thread per
+    footprint line, 1000-point items): the matvec and the 3n gradient outputs equal the wave-owned tiled spread's
+    (oracle-pinned above) to 1e-12, and two calls are bitwise equal."""
+    torch = torch_cuda
+    n, nw, dw = 400000, 2, 3
+    rng = np.random.default_rng(n)
+    X = rng.random((n, nw * dw))
+    win = np.arange(nw * dw, dtype=np.int32)
+    xd = torch.tensor(rng.random(n) - 0.5, device="cuda")
+    op = amd.NFFTAdditiveKernel(X, win, nw, dw)
+    assert op.setup(0, 1.0, 0.3, 0.01) == 0
+    y1, y2 = op.matsymv(xd).cpu().numpy(), op.matsymv(xd).cpu().numpy()
+    g1 = op.gradmatsymv(xd).cpu().numpy()
+    np.testing.assert_array_equal(y1, y2)
+    monkeypatch.setenv("NFFT4GP_AMD_MD_SPREAD", "1")
+    monkeypatch.setenv("NFFT4GP_AMD_MD_CHUNK", "50000")
+    ref = amd.NFFTAdditiveKernel(X, win, nw, dw)
+    assert ref.setup(0, 1.0, 0.3, 0.01) == 0
+    assert rel(y1, ref.matsymv(xd).cpu().numpy()) < 1e-12
+    assert rel(g1, ref.gradmatsymv(xd).cpu().numpy()) < 1e-12
+    op.free()
+    ref.free()
+
+
 def test_window_of_four_features_matches_fixture(torch_cuda):
     """A window of 4 features (64^4 grids, the untiled spread / interpolation) against the oracle's NFFT
     values committed in tests/golden/md4d.npz (tests/golden/make_md4d.py: ~80 s per oracle matvec on the
