@@ -505,6 +505,14 @@ int default_block(int n)
 void env_layout(AdditivePlan& P)
 {
    P.B = default_block(P.n);
+   // windows per spread workgroup: at most 3 (three workgroups per CU fit the LDS), spread evenly over the
+   // fewest groups -- 4 windows as 2 + 2 instead of 3 + 1 (a one-window workgroup pays the whole alpha staging
+   // and fold): 22.3 against 24.2 us per rank of BASELINE configs[3]'s component split
+   // (profiles/r04_component_cg_sweep.txt)
+   {
+      const int ngroups = (std::max(P.nw, 1) + 2) / 3;
+      P.CG = (std::max(P.nw, 1) + ngroups - 1) / ngroups;
+   }
    if (const char* e = getenv("NFFT4GP_AMD_BLOCK")) {
       const int v = atoi(e);
       if (v >= 256) P.B = std::min(v, kMaxBlock) & ~1;  // even: the LDS slice is staged in 16-byte pairs
