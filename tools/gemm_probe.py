@@ -1,7 +1,7 @@
 """The Nystrom setup's three MFMA products at config C (n = 1e6, k = 512; nystrom.hip k_gemm_f64): per-product
 hipEvent times over several setups, the same way bench.py's nys_setup_mfma reports them, plus a checksum of U
 (the products' accumulation order does not depend on the GEMM variant, so U is bitwise the same).
-    NFFT4GP_AMD_GEMM_AHEAD=2 python tools/gemm_probe.py"""
+    python tools/gemm_probe.py   (profiles/r04_gemm_ahead_ab.txt compared a removed two-step-lookahead variant)"""
 import json
 import os
 import sys
@@ -29,7 +29,7 @@ def main():
         pre.free()
     med = {key: float(np.median([r[key] for r in rows])) for key in rows[0]}
     flops = 2.0 * n * k * k
-    print(json.dumps({"ahead": os.environ.get("NFFT4GP_AMD_GEMM_AHEAD", "1"), "ms": med,
+    print(json.dumps({"ms": med,
                       "tflops": {key: flops / (v * 1e-3) / 1e12 for key, v in med.items()},
                       "frac": {key: flops / (v * 1e-3) / 1e12 / 78.6 for key, v in med.items()}}), flush=True)
 
