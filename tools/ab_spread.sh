@@ -1,5 +1,5 @@
 # A/B of spread kernel variants / block sizes on the bench workload:
-#   bash tools/ab_spread.sh "1:4064 5:4064 6:2032" [extra bench args]
+#   bash tools/ab_spread.sh "0:4064 0:2032" [extra bench args]   (variant:block)
 set -o pipefail
 mkdir -p gpurun_out
 VARS="$1"; shift
