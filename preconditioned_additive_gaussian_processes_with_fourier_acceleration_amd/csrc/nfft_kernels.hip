@@ -111,9 +111,7 @@ __device__ __forceinline__ void stage_block_glds(double* __restrict__ s, const d
 // spread
 // ------------------------------------------------------------------------------------------------
 // at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
-// SKEW (A/B variant 2): window c of the group stores cell i's moments in row (i + 11 c) mod 64 of its table,
-// so lanes whose cells differ by 32 in different windows of the group hit different LDS banks on the flush
-template <int THREADS, bool TIMELINE = false, bool SKEW = false>
+template <int THREADS, bool TIMELINE = false>
 __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restrict__ meta,
                                                       const uint32_t* __restrict__ lo,
                                                       const uint32_t* __restrict__ qarr,
@@ -170,7 +168,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
          }
       }
       const int comp_local = (int)(cur.mt >> 6) - c0;
-      const int cell = SKEW ? (int)((cur.mt + 11u * (uint32_t)comp_local) & 63u) : (int)(cur.mt & 63u);
+      const int cell = (int)(cur.mt & 63u);
       double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
 #pragma unroll
       for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
@@ -188,8 +186,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
       double v = 0.0;
 #pragma unroll 1
       for (int tp = 0; tp < kTaps; tp++) {
-         const int row = SKEW ? (gi + kM - tp + 11 * cl) & (kNos - 1) : (gi + kM - tp) & (kNos - 1);
-         const double* mrow = s_mom + (cl * kNos + row) * kMomStride;
+         const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
 #pragma unroll
          for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
       }
@@ -702,14 +699,12 @@ int upload_tap_coeffs()
 
 typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, int, int, int,
                          int, int, int, double*);
-// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py); 2: skewed
-// moment-table rows (A/B).  Variants that
+// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py).  Variants that
 // measured slower or neutral (prefetching runs, persistent workgroups, several groups per workgroup, the fold in
 // two chains, register-staged alpha, the row shards' block sum in the spread's tail) were removed in round 4;
 // DESIGN.md 3.5 keeps their numbers.
 constexpr int kSpreadThreads = 512;
-static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>,
-                                           k_spread<kSpreadThreads, false, true>};
+static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>};
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
 constexpr int kInterpThreads = 1024;
