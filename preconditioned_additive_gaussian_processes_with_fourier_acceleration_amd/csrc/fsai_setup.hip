@@ -887,6 +887,8 @@ __device__ void wave_trsv(double (*A)[LD], int k, double* b, int trans)
 // KM: the LDS arrays' row capacity (>= lfil); KM = 32 takes 17 KB per workgroup (9 per CU) where 64
 // takes 51 KB (3 per CU).
 constexpr int kSchurChunk = 32;
+// KM = 20 (the reference's default lfil) takes 8.8 KB, so 18 row-waves share a CU instead of 9 at KM = 32: the
+// Schur rows are bound by the latency of their W-chunk loads, and twice the rows in flight hide twice as much
 template <int KM>
 __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, long long ldim,
                                                   const int* __restrict__ ia, const int* __restrict__ ja,
@@ -1011,6 +1013,17 @@ __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, 
       if (lane < k) da[(size_t)g * nnz + j1 + lane] = fma(t, a[lane], u[lane]);
       __syncthreads();
    }
+}
+
+// the row kernel with the smallest LDS rows for the pattern (NFFT4GP_AMD_FSAI_KM=32 forces the 32-row one, A/B)
+typedef void (*FsaiRowsFn)(const double*, long long, const int*, const int*, KernelParams, const double*, int, int,
+                           int, double*, double*, const double*, const double*, const int*);
+static FsaiRowsFn fsai_rows_kernel(int lfil)
+{
+   static const int force = getenv("NFFT4GP_AMD_FSAI_KM") ? atoi(getenv("NFFT4GP_AMD_FSAI_KM")) : 0;
+   if (lfil <= 20 && force != 32) return k_fsai_rows<20>;
+   if (lfil <= 32) return k_fsai_rows<32>;
+   return k_fsai_rows<kFsaiMaxK>;
 }
 
 // ---- level-scheduled CSR triangular solves: one workgroup, a barrier between levels ----------------
@@ -1332,7 +1345,7 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const Ke
    const KernelParams P = kernel_params_of(Ks, d);
    const double* Xk = Ks.Xk ? Ks.Xk : dX;
    const long long ldk = Ks.Xk ? Ks.ldk : ldim;
-   auto rows_kernel = lfil <= 32 ? k_fsai_rows<32> : k_fsai_rows<kFsaiMaxK>;
+   auto rows_kernel = fsai_rows_kernel(lfil);
    hipLaunchKernelGGL(rows_kernel, dim3(n), dim3(64), 0, s, Xk, ldk, dia, dja, P, dW, kw, require_grad ? 1 : 0, nnz,
                       daa, dda, dGB, dGC, (const int*)nullptr);
    haa.assign((size_t)nnz, 0.0);
@@ -1395,7 +1408,7 @@ int fsai_values_rows(const KernelSpec& Ks, const double* dX, long long ldim, int
    const KernelParams P = kernel_params_of(Ks, d);
    const double* Xk = Ks.Xk ? Ks.Xk : dX;
    const long long ldk = Ks.Xk ? Ks.ldk : ldim;
-   auto rows_kernel = lfil <= 32 ? k_fsai_rows<32> : k_fsai_rows<kFsaiMaxK>;
+   auto rows_kernel = fsai_rows_kernel(lfil);
    hipLaunchKernelGGL(rows_kernel, dim3(nrows), dim3(64), 0, s, Xk, ldk, dia, dja, P, dW, kw, 0, 0, daa,
                       (double*)nullptr, (const double*)nullptr, (const double*)nullptr, dwcol);
    return hipGetLastError() == hipSuccess ? 0 : -1;
