@@ -921,13 +921,27 @@ __global__ __launch_bounds__(64) void k_fsai_rows(const double* __restrict__ X, 
    }
    __syncthreads();
    if (W) {
+      // the next chunk's W entries are loaded into registers while this chunk's products run
+      constexpr int kPerLane = (KM * kSchurChunk + 63) / 64;
+      double wr[kPerLane];
+      auto fetch_chunk = [&](int t0) {
+         const int tc = min(kSchurChunk, kw - t0);
+#pragma unroll
+         for (int q = 0; q < kPerLane; q++) {
+            const int e = lane + 64 * q;
+            wr[q] = e < k * tc ? W[(size_t)widx[e / tc] * kw + t0 + e % tc] : 0.0;
+         }
+      };
+      fetch_chunk(0);
       for (int t0 = 0; t0 < kw; t0 += kSchurChunk) {
          const int tc = min(kSchurChunk, kw - t0);
-         for (int e = lane; e < k * tc; e += 64) {
-            const int r = e / tc, tt = e % tc;
-            Ws[r][tt] = W[(size_t)widx[r] * kw + t0 + tt];
+#pragma unroll
+         for (int q = 0; q < kPerLane; q++) {
+            const int e = lane + 64 * q;
+            if (e < k * tc) Ws[e / tc][e % tc] = wr[q];
          }
          __syncthreads();
+         if (t0 + kSchurChunk < kw) fetch_chunk(t0 + kSchurChunk);
          for (int e = lane; e < k * k; e += 64) {
             const int r = e % k, c = e / k;
             if (c > r) continue;
