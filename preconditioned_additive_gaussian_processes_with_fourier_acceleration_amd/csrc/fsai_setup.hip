@@ -436,6 +436,9 @@ constexpr int kScrRows = 32 * kScrRowBlocks;
 constexpr int kScrThreads = 512;
 constexpr int kScrCap = 160;
 constexpr int kScrSample = 4096;
+// the count scan over a 1/kScrSub subset of the points before the group once there are kScrSubFrom of them
+// (NFFT4GP_AMD_KNN_SUB overrides kScrSub at launch: 1 = every point)
+constexpr int kScrSubFrom = 65536;
 #ifndef KNN_SCR_WAVES
 #define KNN_SCR_WAVES 2  // waves per SIMD the screen kernels are compiled for
 #endif
@@ -489,9 +492,11 @@ struct ScrShared {
 // keys below the row's threshold binned 16 per octave from base; 3: append keys <= the threshold to the
 // row's candidates.  CHECK: only points before the row (j < S.row[r]) count.  STEPS = ceil(d / 2) bound.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+// sub > 1: only every sub-th round of W tiles (a systematic 1/sub subset of [j0, j1))
 template <int MODE, bool CHECK, int STEPS>
 __device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restrict__ Xf,
-                                              const float* __restrict__ nx, int n, int d, int i0, int j0, int j1)
+                                              const float* __restrict__ nx, int n, int d, int i0, int j0, int j1,
+                                              int sub = 1)
 {
    // wave w: row tile w % kScrRowBlocks (rows rt .. rt + 31), point stream w / kScrRowBlocks of W; the waves
    // of one point stream read the same points at the same time (one fetch beyond L2 serves all of them)
@@ -518,9 +523,10 @@ __device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restr
 #pragma unroll
       for (int st = 0; st < STEPS; st++) b[st] = Xf[(size_t)(2 * st + h) * n + jl];  // Xf zero-padded to 2 STEPS
    };
+   const int step = W * 32 * sub;
    if (j0 + wave * 32 < j1) load(j0 + wave * 32, b0, a00);
-   if (j0 + wave * 32 + W * 32 < j1) load(j0 + wave * 32 + W * 32, b1, a01);
-   for (int jb = j0 + wave * 32; jb < j1; jb += W * 32) {
+   if (j0 + wave * 32 + step < j1) load(j0 + wave * 32 + step, b1, a01);
+   for (int jb = j0 + wave * 32; jb < j1; jb += step) {
       const int j = jb + col;
       const bool ok = j < j1;
       f32x16 c;
@@ -533,7 +539,7 @@ __device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restr
          b0[st] = b1[st];
       }
       a00 = a01;
-      if (jb + 2 * W * 32 < j1) load(jb + 2 * W * 32, b1, a01);
+      if (jb + 2 * step < j1) load(jb + 2 * step, b1, a01);
 #pragma unroll
       for (int st = 0; st < STEPS; st++) c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], bc[st], c, 0, 0, 0);
       if (!ok) continue;
@@ -576,7 +582,7 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
                                                                const int* __restrict__ ia,
                                                                int* __restrict__ ja, int* __restrict__ fail,
                                                                int* __restrict__ nfail, const int* __restrict__ rows,
-                                                               int nrows_list)
+                                                               int nrows_list, int kScrSub)
 {
    constexpr int R = kScrRows, CAP = kScrCap, W = kScrThreads / 64;
    __shared__ ScrShared S;
@@ -676,8 +682,10 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
       __syncthreads();
       clear_h();
       __syncthreads();
-      // count over every earlier point: [0, i0) before all rows, [i0, i0 + nr - 1) before some
-      knn_scan_mfma<2, false, STEPS>(S, Xf, nx, n, d, i0, 0, i0);
+      // count over the earlier points: [0, i0) before all rows (a systematic quarter of it once i0 is large:
+      // the (lfil-1)-th smallest key of any subset bounds the row's from above, so U + 2m still collects every
+      // neighbour, with about 4 (lfil - 1) candidates), [i0, i0 + nr - 1) before some
+      knn_scan_mfma<2, false, STEPS>(S, Xf, nx, n, d, i0, 0, i0, i0 >= kScrSubFrom ? kScrSub : 1);
       knn_scan_mfma<2, true, STEPS>(S, Xf, nx, n, d, i0, i0, ilast);
       __syncthreads();
       for (int r = wave; r < nr; r += W) {
@@ -784,6 +792,7 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
          variant = 2;  // every row to k_knn
       } else {
          const int ngroups = (nrows + kScrRows - 1) / kScrRows;
+         static const int sub = getenv("NFFT4GP_AMD_KNN_SUB") ? std::max(1, atoi(getenv("NFFT4GP_AMD_KNN_SUB"))) : 4;
          float* lim = nullptr;
          if (hipMalloc((void**)&lim, sizeof(float) * (size_t)nrows) != hipSuccess) return done(-1);
          for (int phase = 0; phase < 2; phase++) {
@@ -799,7 +808,7 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
                                                       : k_knn_screen<32, 1>);
             hipLaunchKernelGGL(screen, dim3(std::min(ngroups, 4096)), dim3(kScrThreads), 0, s, dX, ldim,
                                (const float*)Xf, (const float*)nx, n, d, lfil, (float)(2.0 * margin) * 1.0001f, lim,
-                               dia, dja, dfail, dfail + nrows, d_rows, nrows);
+                               dia, dja, dfail, dfail + nrows, d_rows, nrows, sub);
          }
          (void)hipStreamSynchronize(s);
          (void)hipFree(lim);

@@ -94,3 +94,22 @@ def test_knn_screen_speed_config_c_slice(torch_cuda):
     assert np.array_equal(r1, r)
     print(f"KNN n=2e5 d=32: screen {t[1]:.3f} s (fallback rows {nf1}), fp64 {t[0]:.3f} s")
     assert nf1 <= 2000
+
+
+@pytest.mark.parametrize("kind", ["random", "clustered"])
+def test_knn_screen_subsampled_count(torch_cuda, kind):
+    """Row groups with >= 65536 earlier points count on a systematic quarter of them (the subset's
+    (lfil-1)-th smallest key bounds the row's, so the collect limit still holds every neighbour): the rows
+    equal the fp64 scan's on random and clustered data at n = 9e4."""
+    rng = np.random.default_rng(11)
+    n, d = 90000, 8
+    if kind == "random":
+        X = rng.random((n, d))
+    else:
+        centres = rng.random((50, d))
+        X = centres[rng.integers(0, 50, n)] + 0.02 * rng.standard_normal((n, d))
+    a, nf = knn(X, 20, 1)
+    b, _ = knn(X, 20, 0)
+    assert np.array_equal(a, b)
+    if kind == "random":
+        assert nf <= (n - 20) // 100, nf
