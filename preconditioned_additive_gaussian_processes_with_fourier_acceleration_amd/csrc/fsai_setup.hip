@@ -436,8 +436,10 @@ constexpr int kScrRows = 32 * kScrRowBlocks;
 constexpr int kScrThreads = 512;
 constexpr int kScrCap = 160;
 constexpr int kScrSample = 4096;
-// the count scan over a 1/kScrSub subset of the points before the group once there are kScrSubFrom of them
-// (NFFT4GP_AMD_KNN_SUB overrides kScrSub at launch: 1 = every point)
+// the count scan over a 1/sub subset of the points before the group once there are kScrSubFrom of them (sub = 2;
+// NFFT4GP_AMD_KNN_SUB overrides, 1 = every point).  Config-C AFN setup (profiles/r04_knn_sub_ab.txt): sub 1 / 2
+// / 3 / 4: 1.37-1.43 / 1.18-1.22 / 1.19-1.21 / 1.27-1.28 s -- at 4 the collect overflows its 160 candidates in
+// ~3 % of the rows (d = 32) and those rows take the fp64 fallback
 constexpr int kScrSubFrom = 65536;
 #ifndef KNN_SCR_WAVES
 #define KNN_SCR_WAVES 2  // waves per SIMD the screen kernels are compiled for
@@ -682,9 +684,9 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
       __syncthreads();
       clear_h();
       __syncthreads();
-      // count over the earlier points: [0, i0) before all rows (a systematic quarter of it once i0 is large:
-      // the (lfil-1)-th smallest key of any subset bounds the row's from above, so U + 2m still collects every
-      // neighbour, with about 4 (lfil - 1) candidates), [i0, i0 + nr - 1) before some
+      // count over the earlier points: [0, i0) before all rows (a systematic half of it once i0 is large: the
+      // (lfil-1)-th smallest key of any subset bounds the row's from above, so U + 2m still collects every
+      // neighbour, with about 2 (lfil - 1) candidates), [i0, i0 + nr - 1) before some
       knn_scan_mfma<2, false, STEPS>(S, Xf, nx, n, d, i0, 0, i0, i0 >= kScrSubFrom ? kScrSub : 1);
       knn_scan_mfma<2, true, STEPS>(S, Xf, nx, n, d, i0, i0, ilast);
       __syncthreads();
@@ -792,7 +794,7 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
          variant = 2;  // every row to k_knn
       } else {
          const int ngroups = (nrows + kScrRows - 1) / kScrRows;
-         static const int sub = getenv("NFFT4GP_AMD_KNN_SUB") ? std::max(1, atoi(getenv("NFFT4GP_AMD_KNN_SUB"))) : 4;
+         static const int sub = getenv("NFFT4GP_AMD_KNN_SUB") ? std::max(1, atoi(getenv("NFFT4GP_AMD_KNN_SUB"))) : 2;
          float* lim = nullptr;
          if (hipMalloc((void**)&lim, sizeof(float) * (size_t)nrows) != hipSuccess) return done(-1);
          for (int phase = 0; phase < 2; phase++) {

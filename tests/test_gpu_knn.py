@@ -98,7 +98,7 @@ def test_knn_screen_speed_config_c_slice(torch_cuda):
 
 @pytest.mark.parametrize("kind", ["random", "clustered"])
 def test_knn_screen_subsampled_count(torch_cuda, kind):
-    """Row groups with >= 65536 earlier points count on a systematic quarter of them (the subset's
+    """Row groups with >= 65536 earlier points count on a systematic half of them (the subset's
     (lfil-1)-th smallest key bounds the row's, so the collect limit still holds every neighbour): the rows
     equal the fp64 scan's on random and clustered data at n = 9e4."""
     rng = np.random.default_rng(11)
