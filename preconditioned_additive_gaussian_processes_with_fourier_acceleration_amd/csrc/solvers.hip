@@ -742,10 +742,7 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
 
    const int g = pcg_grid(N);
    const int ge = g;
-   static const int xr_t = getenv("NFFT4GP_AMD_PCG_XR_THREADS") ? atoi(getenv("NFFT4GP_AMD_PCG_XR_THREADS")) : 1024;
-   const int xr_threads = (xr_t == 256 || xr_t == 512) ? xr_t : 1024;
-   const int g_xr = (int)std::max<size_t>(
-       1, std::min<size_t>((N + (size_t)xr_threads * kEPT - 1) / ((size_t)xr_threads * kEPT), kPcgMaxBlocks));
+   const int g_xr = (int)std::max<size_t>(1, std::min<size_t>((N + 1024 * kEPT - 1) / (1024 * kEPT), kPcgMaxBlocks));
    // this library's additive operator forms (q, p) in its own interpolation launch
    const bool fused_dot = cb.mv_dev && ((matvec == &Nfft4GPAdditiveNFFTMatSymv && additive_fused_dot_ok(mat_data)) ||
                                         (is_dist && dinfo.fused_dot));
@@ -794,15 +791,8 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
             }
          }
          PcgSlot* slot = slots_d + (ii % PcgScratch::kSlots);
-         if (xr_threads == 256)
-            hipLaunchKernelGGL(k_pcg_xr<256>, dim3(g_xr), dim3(256), 0, s, vx.d, r, p, q, N, g_pcg.part, g_pcg.ticket,
-                               st, rhos, hist_d, ii, prec_data ? 0 : 1, fused_dot ? 1 : 0, slot, loc1);
-         else if (xr_threads == 512)
-            hipLaunchKernelGGL(k_pcg_xr<512>, dim3(g_xr), dim3(512), 0, s, vx.d, r, p, q, N, g_pcg.part, g_pcg.ticket,
-                               st, rhos, hist_d, ii, prec_data ? 0 : 1, fused_dot ? 1 : 0, slot, loc1);
-         else
-            hipLaunchKernelGGL(k_pcg_xr<1024>, dim3(g_xr), dim3(1024), 0, s, vx.d, r, p, q, N, g_pcg.part,
-                               g_pcg.ticket, st, rhos, hist_d, ii, prec_data ? 0 : 1, fused_dot ? 1 : 0, slot, loc1);
+         hipLaunchKernelGGL(k_pcg_xr<1024>, dim3(g_xr), dim3(1024), 0, s, vx.d, r, p, q, N, g_pcg.part, g_pcg.ticket,
+                            st, rhos, hist_d, ii, prec_data ? 0 : 1, fused_dot ? 1 : 0, slot, loc1);
          if (red) {
             if (red->allreduce(loc1, 1, s)) { rc = -1; break; }
             hipLaunchKernelGGL(k_pcg_xr_fin, dim3(1), dim3(64), 0, s, st, rhos, hist_d, ii, prec_data ? 0 : 1, slot,
