@@ -111,9 +111,7 @@ __device__ __forceinline__ void stage_block_glds(double* __restrict__ s, const d
 // spread
 // ------------------------------------------------------------------------------------------------
 // at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
-// FOLD2 (A/B variant 2): each output's 10 taps split over two threads (5 each), so 384 threads fold instead of
-// 192 and each chain is half as long
-template <int THREADS, bool TIMELINE = false, bool FOLD2 = false>
+template <int THREADS, bool TIMELINE = false>
 __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restrict__ meta,
                                                       const uint32_t* __restrict__ lo,
                                                       const uint32_t* __restrict__ qarr,
@@ -182,28 +180,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    // fold moments into the 64-cell partial grid of every window of this group:
    //   g[gi] = sum_t sum_d C[t][d] M[(gi + m - t) mod 64][d]
    const int ncomp = min(CG, nw - c0);
-   if (FOLD2) {
-      // threads [0, 192) fold taps 0-4 and [192, 384) taps 5-9 of output t mod 192 (the half is wave-uniform, so
-      // the tap coefficients stay scalar loads); the second halves meet the first through the dead alpha slice
-      const int half = tid >= 3 * kNos, o = tid - half * 3 * kNos;
-      double v = 0.0;
-      if (tid < 6 * kNos && o < ncomp * kNos) {
-         const int cl = o / kNos, gi = o % kNos;
-#pragma unroll 1
-         for (int tp = half * (kTaps / 2); tp < (half + 1) * (kTaps / 2); tp++) {
-            const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
-#pragma unroll
-            for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
-         }
-         if (half) s_alpha[o] = v;
-      }
-      __syncthreads();
-      if (!half && o < ncomp * kNos) {
-         const int cl = o / kNos, gi = o % kNos;
-         part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v + s_alpha[o];
-      }
-   }
-   for (int idx = FOLD2 ? ncomp * kNos : tid; idx < ncomp * kNos; idx += THREADS) {
+   for (int idx = tid; idx < ncomp * kNos; idx += THREADS) {
       const int cl = idx / kNos;
       const int gi = idx % kNos;
       double v = 0.0;
@@ -722,14 +699,12 @@ int upload_tap_coeffs()
 
 typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, int, int, int,
                          int, int, int, double*);
-// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py); 2: the fold on
-// lane pairs (A/B).  Variants that
+// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py).  Variants that
 // measured slower or neutral (prefetching runs, persistent workgroups, several groups per workgroup, the fold in
 // two chains, register-staged alpha, the row shards' block sum in the spread's tail) were removed in round 4;
 // DESIGN.md 3.5 keeps their numbers.
 constexpr int kSpreadThreads = 512;
-static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>,
-                                           k_spread<kSpreadThreads, false, true>};
+static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>};
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
 constexpr int kInterpThreads = 1024;
