@@ -794,18 +794,22 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
       fprintf(stderr, "nfft4gp_amd: fused matvec-dot needs a plain matvec and <= %d blocks\n", kRedMaxBlocks);
       return -1;
    }
-   // A/B: NFFT4GP_AMD_INTERP_THREADS=512 runs the plain matvec's interpolation on 512-thread workgroups
-   static const int it512 = getenv("NFFT4GP_AMD_INTERP_THREADS") && atoi(getenv("NFFT4GP_AMD_INTERP_THREADS")) == 512;
+   // 512-thread workgroups once there are >= 512 blocks (two workgroups per CU overlap one another's prologue
+   // and epilogue: 787 -> 734 us at config E; with fewer blocks half the CU would idle, 30.8 -> 34.3 us at
+   // config C; profiles/r04_interp_threads_ab.txt).  NFFT4GP_AMD_INTERP_THREADS=512 / 1024 forces either.
+   static const int forced = getenv("NFFT4GP_AMD_INTERP_THREADS") ? atoi(getenv("NFFT4GP_AMD_INTERP_THREADS")) : 0;
    static const bool attr512 = [] {
-      (void)hipFuncSetAttribute((const void*)k_interp<false, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      for (const void* f : {(const void*)k_interp<false, 512>, (const void*)k_interp<true, 512>,
+                            (const void*)k_interp<false, 512, true>})
+         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipGetLastError();
       return true;
    }();
    (void)attr512;
-   const bool small = it512 && !grad && !d_dot;
-   const InterpFn fn = small ? k_interp<false, 512>
-                             : grad ? k_interp<true, kInterpThreads>
-                                    : (d_dot ? k_interp<false, kInterpThreads, true> : k_interp<false, kInterpThreads>);
+   const bool small = forced == 512 || (forced != 1024 && P.nblocks >= 512);
+   const InterpFn fn = small ? (grad ? k_interp<true, 512> : (d_dot ? k_interp<false, 512, true> : k_interp<false, 512>))
+                             : (grad ? k_interp<true, kInterpThreads>
+                                     : (d_dot ? k_interp<false, kInterpThreads, true> : k_interp<false, kInterpThreads>));
    launch_ev(fn, dim3(P.nblocks), dim3(small ? 512 : kInterpThreads), interp_lds_bytes(P, grad), stream,
              P.kev ? P.kev + 4 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H,
              (const double*)P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups, alpha, beta, P.f, P.mu * P.diag, P.diag,
