@@ -847,14 +847,11 @@ int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double
    if (P.md.on) return -1;
    static bool attr = false;
    if (!attr) {
-      for (const void* f : {(const void*)k_interp2<kInterp2Threads>, (const void*)k_interp2<512>})
-         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_interp2<kInterp2Threads>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
       (void)hipGetLastError();
       attr = true;
    }
-   // as launch_interp: 512-thread workgroups at >= 512 blocks (A/B: NFFT4GP_AMD_INTERP_THREADS)
-   static const int forced = getenv("NFFT4GP_AMD_INTERP_THREADS") ? atoi(getenv("NFFT4GP_AMD_INTERP_THREADS")) : 0;
-   const bool small = forced == 512 || (forced != 1024 && P.nblocks >= 512);
    const size_t part_rs = (size_t)std::max(1, P.nparts) * P.nw * kNos;
    const size_t h_rs = (size_t)P.nw * kNos * kNC;
    // both vectors' partial grids in one allocation, so k_grid's per-vector stride stays inside it
@@ -865,14 +862,9 @@ int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double
                       (const double*)P.d_w, (const double*)P.d_wd, P.d_H2, P.d_Hd, 0, 0, (long long)part_rs,
                       (long long)h_rs);
    const size_t lds_i = sizeof(double) * 2 * ((size_t)P.B + kPad);
-   if (small)
-      hipLaunchKernelGGL(k_interp2<512>, dim3(P.nblocks), dim3(512), lds_i, stream, P.dl.meta, P.dl.lo, P.dl.q,
-                         P.dl.tile_off, (const double*)P.d_H2, h_rs, x0, x1, y0, y1, P.n, P.B, P.ngroups, alpha, beta,
-                         P.f, P.mu * P.diag);
-   else
-      hipLaunchKernelGGL(k_interp2<kInterp2Threads>, dim3(P.nblocks), dim3(kInterp2Threads), lds_i, stream,
-                         P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H2, h_rs, x0, x1, y0, y1, P.n,
-                         P.B, P.ngroups, alpha, beta, P.f, P.mu * P.diag);
+   hipLaunchKernelGGL(k_interp2<kInterp2Threads>, dim3(P.nblocks), dim3(kInterp2Threads), lds_i, stream, P.dl.meta,
+                      P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H2, h_rs, x0, x1, y0, y1, P.n, P.B,
+                      P.ngroups, alpha, beta, P.f, P.mu * P.diag);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
