@@ -7,8 +7,12 @@ vector x ~ U(-0.5, 0.5) (TESTS/TEST1/foo.cpp:243-247), numpy PCG64 seed 906 (syn
 One "step" = one Nfft4GPAdditiveNFFTMatSymv(y = K x) with x and y resident in HBM.
 
 N = 1:  the matvec on one GPU.
-N > 1:  one process per GPU (torch.distributed launches the ranks; the library's own RCCL communicator
-        does the all-reduces over xGMI, enqueued on the stream by dist.hip).  The headline splits ROWS:
+N > 1:  one process per GPU: under torch.distributed.run (WORLD_SIZE set, which must equal --gpus) or, when
+        no launcher set WORLD_SIZE, spawned by this script itself before anything touches the GPU (each child
+        gets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT; the parent exits non-zero if
+        any rank fails, or with RCCL if fewer than N devices are visible).  The library's own RCCL communicator
+        does the all-reduces over xGMI, enqueued on the stream by dist.hip; the line reports the ranks RCCL
+        itself counts (ncclCommCount) and each rank's kernel and all-reduce time.  The headline splits ROWS:
         each rank spreads its own n/N points for all 32 windows, the 32x64 oversampled grids (16 KB) are
         all-reduced, each rank interpolates its own rows.  The line also carries the split BASELINE
         configs[3] names, 4 COMPONENTS per GPU (y, 8 MB, all-reduced), timed the same way
@@ -155,6 +159,93 @@ def cpu_baseline(n, d, threads=16, timeout=400):
                   f"in a child process; one_thread: the same setup on 1 thread; setup (PRE_PSI taps, bhat) "
                   f"{res['setup_s']:.1f}s untimed; -march=native={so is not None}",
     }
+
+
+def resolve_world(gpus, env=None):
+    """How this process runs: ("single", 1), ("rank", WORLD_SIZE) under a launcher, or ("spawn", N) when --gpus N > 1
+    and no launcher set WORLD_SIZE.  A launcher's WORLD_SIZE must equal --gpus when both are given."""
+    env = os.environ if env is None else env
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        ws = int(ws)
+        if gpus is not None and gpus != ws:
+            raise SystemExit(f"bench: the launcher set WORLD_SIZE={ws} but --gpus {gpus}; they must agree")
+        return ("rank" if ws > 1 else "single"), ws
+    n = 1 if gpus is None else int(gpus)
+    if n < 1:
+        raise SystemExit(f"bench: --gpus {n}: need at least one GPU")
+    return ("spawn" if n > 1 else "single"), n
+
+
+def rank_envs(n, port, base=None):
+    """The environment of each spawned rank (what torch.distributed.run would set on one node)."""
+    base = dict(os.environ if base is None else base)
+    return [dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port)) for r in range(n)]
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def visible_devices():
+    """GPUs this process may use; torch.cuda.device_count() does not initialise the GPU on this image."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def spawn_ranks(n, argv, backend=None, poll_s=0.2):
+    """Start n ranks of this script (one process per GPU) and wait for them.  Nothing here touches the GPU: the
+    children are new processes, not a fork of an initialised one.  Rank 0's stdout is this process's (it prints
+    the line); the other ranks' stdout is discarded.  Returns the exit code: 0 only if every rank succeeded; when
+    one fails the others are terminated (their own PIDs) so that none waits in a collective forever."""
+    backend = backend or os.environ.get("NFFT4GP_BENCH_BACKEND", "nccl")
+    if backend != "gloo" and "--launcher-selftest" not in argv:
+        ndev = visible_devices()
+        if ndev < n:
+            print(f"bench: --gpus {n} with RCCL needs {n} visible GPUs, this box has {ndev}; not running "
+                  f"(NFFT4GP_BENCH_BACKEND=gloo rehearses the ranks on fewer GPUs)", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r, env in enumerate(rank_envs(n, port)):
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench: rank {procs.index(p)} exited with {code}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(poll_s)
+    return rc
+
+
+def launcher_selftest(fail_rank):
+    """--launcher-selftest (CPU test of the plumbing): each rank writes what it received, one rank may fail."""
+    rank = int(os.environ.get("RANK", "-1"))
+    out = os.environ.get("NFFT4GP_BENCH_SELFTEST_DIR")
+    rec = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+                                          "MASTER_PORT")}
+    rec["argv"] = sys.argv[1:]
+    if out:
+        with open(os.path.join(out, f"rank{rank}.json"), "w") as fh:
+            json.dump(rec, fh)
+    if rank == fail_rank:
+        raise SystemExit(3)
+    if rank == 0:
+        print(json.dumps({"selftest": True, "world": int(rec["WORLD_SIZE"])}), flush=True)
 
 
 def kernel_only(n, d, nys_rank=0):
@@ -460,7 +551,8 @@ def run_loss(op, torch, n, d, X, rng_seed=906, maxits=50, nvecs=10, rows=None, d
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one process each); without a launcher N > 1 ranks are spawned here (default 1)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=1_000_000)
@@ -481,6 +573,8 @@ def main():
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-oracle-so", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--kernel-only-nys", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--launcher-selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     if "--cpu-baseline-child" in sys.argv:  # the child's --cpu-threads is a list "16,1"
         i = sys.argv.index("--cpu-threads")
         threads_list = [int(t) for t in sys.argv[i + 1].split(",")]
@@ -492,6 +586,12 @@ def main():
     if args.kernel_only:
         kernel_only(args.n, args.d, args.kernel_only_nys)
         return
+    mode, nranks = resolve_world(args.gpus)
+    if mode == "spawn":
+        raise SystemExit(spawn_ranks(nranks, sys.argv[1:]))
+    if args.launcher_selftest:
+        launcher_selftest(args.launcher_selftest_fail_rank)
+        return
 
     import torch
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
@@ -501,6 +601,9 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; NFFT4GP_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on
     # one GPU (RCCL refuses duplicate devices); the driver's multi-GPU runs use the default, nccl (RCCL)
+    if world > 1 and os.environ.get("NFFT4GP_BENCH_BACKEND", "nccl") != "gloo" and torch.cuda.device_count() < world:
+        raise SystemExit(f"bench: {world} ranks with RCCL need {world} visible GPUs, this box has "
+                         f"{torch.cuda.device_count()}")
     dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
     # one dedicated stream for torch and the library: launches on the legacy null stream carry its implicit
@@ -607,6 +710,26 @@ def main():
     for _ in range(args.warmup):
         step()
 
+    def gather_ranks(rec):
+        """{key: value} of this rank -> {key: [value of rank 0, 1, ...]} on every rank (one all-reduce of a
+        zero-padded world x keys table, which gloo and RCCL both take)."""
+        keys = sorted(rec)
+        tab = torch.zeros(world, len(keys), dtype=torch.float64, device="cuda")
+        tab[rank] = torch.tensor([float(rec[k]) for k in keys], dtype=torch.float64)
+        dist.all_reduce(tab)
+        tab = tab.cpu().numpy()
+        return {k: [float(v) for v in tab[:, i]] for i, k in enumerate(keys)}
+
+    def rank_times(per, el_inst):
+        """The per-rank instrumented timing of one partition, in microseconds per matvec."""
+        return {"kernels_before_exchange_us": [1e3 * v for v in per["local_before_ms"]],
+                "allreduce_us": [1e3 * v for v in per["allreduce_ms"]],
+                "kernels_after_exchange_us": [1e3 * v for v in per["local_after_ms"]],
+                "matvecs_timed": [int(v) for v in per["matvecs"]],
+                "ms_per_step_instrumented": 1e3 * el_inst / args.steps,
+                "source": "hipEvents on the library stream around each rank's kernels and its enqueued all-reduce "
+                          "(components: each chunk's all-reduce on the comm stream), over a repeat of the timed steps"}
+
     def timed(instrumented):
         """K steps bracketed by barrier + synchronize; with `instrumented` every spread / grid / interp
         dispatch of the loop carries start / stop hipEvents (Nfft4GPAmdTimingEnable), so the per-kernel
@@ -626,7 +749,10 @@ def main():
         el = time.perf_counter() - t0
         per = None
         if instrumented:
-            per = {k: ms / max(c, 1) for k, (ms, c) in op.timing_query().items()}
+            if world == 1:
+                per = {k: ms / max(c, 1) for k, (ms, c) in op.timing_query().items()}
+            else:
+                per = gather_ranks(op.timing_query())
             op.timing(False)
         if world > 1:
             tt = torch.tensor([el], dtype=torch.float64, device="cuda")
@@ -638,7 +764,8 @@ def main():
     # every kernel (about 13 us per matvec of event overhead, reported as ms_per_step_instrumented) for the
     # per-kernel durations of the roofline
     elapsed, _ = timed(False)
-    elapsed_inst, kern_avg = timed(True) if world == 1 else (None, None)
+    elapsed_inst, kern_avg = timed(True)
+    per_rank = rank_times(kern_avg, elapsed_inst) if world > 1 else None
     alt = None
     if world > 1:
         # the other split, timed the same way (W warmup + K steps between barriers, max over ranks)
@@ -654,8 +781,10 @@ def main():
         for _ in range(args.warmup):
             step()
         el2, _ = timed(False)
+        el2_inst, per2 = timed(True)
         alt = {"partition": other, "value": args.steps / el2, "ms_per_step": 1e3 * el2 / args.steps,
-               "all_reduce_bytes_per_matvec": 8 * (op2.n if other == "components" else d * 64)}
+               "all_reduce_bytes_per_matvec": 8 * (op2.n if other == "components" else d * 64),
+               "per_rank": rank_times(per2, el2_inst)}
         if not args.no_pcg:
             alt.update(run_pcg_single(op2, torch, n, rows=(op2.row_begin, op2.row_end), dist=dist))
             alt.update(run_fgmres(op2, torch, n, rows=(op2.row_begin, op2.row_end), dist=dist, ortho=1))
@@ -737,6 +866,10 @@ def main():
                 result["cpu_baseline"] = {"value": None, "error": repr(e)}
     if world > 1:
         result["config"]["all_reduce_bytes_per_matvec"] = 8 * (op.n if args.partition == "components" else d * 64)
+        result["rccl_ranks"] = comm.ranks() if comm_kind == "rccl" else None
+        result["comm_ranks"] = comm.ranks()
+        result["config"]["devices_visible"] = torch.cuda.device_count()
+        result["per_rank"] = per_rank
         result["config"]["communicator"] = ("gloo rehearsal (host all-reduce)" if gloo else
                                             "RCCL (library-owned ncclComm, all-reduce enqueued by dist.hip)"
                                             if comm_kind == "rccl" else

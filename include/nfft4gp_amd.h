@@ -516,6 +516,8 @@ void *Nfft4GPAmdCommCreateCallback(int rank, int world, Nfft4GPAmdAllreduceFn fn
 /* sum of count doubles at d_buf (device) over the ranks, in place, on the library stream */
 int Nfft4GPAmdCommAllreduce(void *comm, NFFT4GP_DOUBLE *d_buf, long long count);
 void Nfft4GPAmdCommFree(void *comm);
+/* ranks the communicator's backend itself reports: ncclCommCount for RCCL, the group size for a callback */
+int Nfft4GPAmdCommRanks(void *comm);
 
 /* Component shard: a whole-row additive handle over a subset of the windows, weighted 1/nw_global (the
  * whole operator's 1/nwindows, nfft_interface.c:806); own_diag = 1 on exactly one rank, which adds the
@@ -539,6 +541,12 @@ int Nfft4GPAmdDistMatSymv(void *dop, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE
  * multi-feature windows all-reduce y once).  chunks = 1: one all-reduce after the matvec.  The sums are
  * the same element for element. */
 int Nfft4GPAmdDistSetChunks(void *dop, int chunks);
+/* per-rank timing of a distributed operator (0 disables; enabling resets): every matvec records hipEvents
+ * on the library stream around this rank's kernels before the exchange, the all-reduce and the kernels
+ * after it (kind 1: the local matvec, and each chunk's all-reduce on the operator's comm stream).
+ * Query: ms[0..2] = total milliseconds of the three, *cnt = matvecs timed. */
+int Nfft4GPAmdDistTimingEnable(void *dop, int enable);
+int Nfft4GPAmdDistTimingQuery(void *dop, double *ms, long long *cnt);
 int Nfft4GPAmdDistGradMatSymv(void *dop, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE beta,
                               NFFT4GP_DOUBLE *y);
 /* func_kernel (kernels.h:49) of a distributed operator, for Nfft4GPGpLoss (gp_loss.c:96-307): dop begins

@@ -36,6 +36,7 @@ struct RcclApi {
    decltype(&ncclAllReduce) all_reduce = nullptr;
    decltype(&ncclCommDestroy) destroy = nullptr;
    decltype(&ncclGetErrorString) err = nullptr;
+   decltype(&ncclCommCount) count = nullptr;
 };
 
 RcclApi& rccl()
@@ -61,7 +62,8 @@ RcclApi& rccl()
       R.all_reduce = (decltype(&ncclAllReduce))dlsym(h, "ncclAllReduce");
       R.destroy = (decltype(&ncclCommDestroy))dlsym(h, "ncclCommDestroy");
       R.err = (decltype(&ncclGetErrorString))dlsym(h, "ncclGetErrorString");
-      R.ok = R.get_id && R.init_rank && R.all_reduce && R.destroy && R.err;
+      R.count = (decltype(&ncclCommCount))dlsym(h, "ncclCommCount");
+      R.ok = R.get_id && R.init_rank && R.all_reduce && R.destroy && R.err && R.count;
       if (!R.ok) why += "\n  an RCCL entry point is missing";
    }
    if (!R.ok) fprintf(stderr, "nfft4gp_amd: RCCL could not be loaded:%s\n", why.c_str());
@@ -70,6 +72,12 @@ RcclApi& rccl()
 
 struct CommRccl : Comm {
    ncclComm_t c = nullptr;
+   int ranks() override
+   {
+      int k = -1;
+      if (!c || rccl().count(c, &k) != ncclSuccess) return -1;
+      return k;
+   }
    int allreduce(double* d_buf, size_t count, hipStream_t s) override
    {
       if (count == 0) return 0;
@@ -87,6 +95,7 @@ struct CommRccl : Comm {
 };
 
 struct CommCallback : Comm {
+   int ranks() override { return world; }
    Nfft4GPAmdAllreduceFn fn = nullptr;
    void* ctx = nullptr;
    double* stage = nullptr;  // the caller's device buffer
@@ -137,7 +146,37 @@ struct DistOp {
    int chunks = 4;
    hipStream_t cs = nullptr;
    std::vector<hipEvent_t> ev;
+   // timing (Nfft4GPAmdDistTimingEnable): per matvec, event pairs around this rank's kernels before the
+   // exchange, the all-reduce(s) and the kernels after it; summed by Nfft4GPAmdDistTimingQuery
+   bool timing = false;
+   std::vector<hipEvent_t> tpool;        // every timed event, released at the query
+   std::vector<std::pair<int, int>> tpairs[3];  // indices into tpool: [0] local before, [1] all-reduce, [2] after
+   long long tcount = 0;
 };
+
+hipEvent_t timing_event(DistOp* D, int* idx)
+{
+   hipEvent_t e = nullptr;
+   if (hipEventCreate(&e) != hipSuccess) return nullptr;
+   *idx = (int)D->tpool.size();
+   D->tpool.push_back(e);
+   return e;
+}
+
+// record an event on stream s (timing on); returns its pool index, or -1
+int timing_mark(DistOp* D, hipStream_t s)
+{
+   if (!D->timing) return -1;
+   int i = -1;
+   hipEvent_t e = timing_event(D, &i);
+   if (!e || hipEventRecord(e, s) != hipSuccess) return -1;
+   return i;
+}
+
+void timing_pair(DistOp* D, int which, int a, int b)
+{
+   if (a >= 0 && b >= 0) D->tpairs[which].push_back({a, b});
+}
 
 struct ChunkCtx {
    DistOp* D;
@@ -155,7 +194,10 @@ int chunk_done(void* vctx, size_t r0, size_t r1)
    hipEvent_t e = D->ev[C->i++];
    NFFT4GP_HIP_CHECK(hipEventRecord(e, C->s));
    NFFT4GP_HIP_CHECK(hipStreamWaitEvent(D->cs, e, 0));
-   return D->comm->allreduce(C->y + r0, r1 - r0, D->cs);
+   const int a = timing_mark(D, D->cs);
+   if (D->comm->allreduce(C->y + r0, r1 - r0, D->cs)) return -1;
+   timing_pair(D, 1, a, timing_mark(D, D->cs));
+   return 0;
 }
 
 int ensure_chunk_stream(DistOp* D)
@@ -197,12 +239,22 @@ int dist_apply(DistOp* D, int n, int grad, double alpha, double* x, double beta,
       return -1;
    }
    hipStream_t s = current_stream();
+   if (D->timing) D->tcount++;
    if (D->kind == 0) {
       if (grid_ready(D)) return -1;
+      const int e0 = timing_mark(D, s);
       if (Nfft4GPAmdShardSpread(D->h, x, D->d_grid)) return -1;
+      const int e1 = timing_mark(D, s);
       if (D->comm->allreduce(D->d_grid, D->grid_count, s)) return -1;
-      return Nfft4GPAmdShardFinish(D->h, D->d_grid, grad, alpha, x, beta, y);
+      const int e2 = timing_mark(D, s);
+      if (Nfft4GPAmdShardFinish(D->h, D->d_grid, grad, alpha, x, beta, y)) return -1;
+      const int e3 = timing_mark(D, s);
+      timing_pair(D, 0, e0, e1);
+      timing_pair(D, 1, e1, e2);
+      timing_pair(D, 2, e2, e3);
+      return 0;
    }
+   const int c0 = timing_mark(D, s);
    const size_t ny = (size_t)n * (grad ? 3 : 1);
    double* out = y;
    if (beta != 0.0) {
@@ -215,6 +267,7 @@ int dist_apply(DistOp* D, int n, int grad, double alpha, double* x, double beta,
       ChunkCtx C{D, out, s, 0};
       const int rc = additive_matvec_chunked(D->h, alpha, x, out, D->chunks, &chunk_done, &C);
       if (rc == 0) {
+         timing_pair(D, 0, c0, timing_mark(D, s));
          // the stream's later work (the caller's reads of y, the next matvec) waits for the last piece
          NFFT4GP_HIP_CHECK(hipEventRecord(D->ev[C.i], D->cs));
          NFFT4GP_HIP_CHECK(hipStreamWaitEvent(s, D->ev[C.i], 0));
@@ -226,7 +279,11 @@ int dist_apply(DistOp* D, int n, int grad, double alpha, double* x, double beta,
    if (!chunked) {
       const int rc = grad ? Nfft4GPAdditiveNFFTGradMatSymv(D->h, n, alpha, x, 0.0, out)
                           : Nfft4GPAdditiveNFFTMatSymv(D->h, n, alpha, x, 0.0, out);
-      if (rc || D->comm->allreduce(out, ny, s)) return -1;
+      if (rc) return -1;
+      const int e1 = timing_mark(D, s);
+      timing_pair(D, 0, c0, e1);
+      if (D->comm->allreduce(out, ny, s)) return -1;
+      timing_pair(D, 1, e1, timing_mark(D, s));
    }
    if (beta != 0.0) {
       const int g = (int)std::min<size_t>(4096, (ny + 255) / 256);
@@ -388,6 +445,7 @@ void Nfft4GPAmdDistFree(void* dop)
    if (D->d_grid) (void)hipFree(D->d_grid);
    if (D->d_tmp) (void)hipFree(D->d_tmp);
    for (hipEvent_t e : D->ev) (void)hipEventDestroy(e);
+   for (hipEvent_t e : D->tpool) (void)hipEventDestroy(e);
    if (D->cs) (void)hipStreamDestroy(D->cs);
    delete D;
 }
@@ -429,6 +487,50 @@ int Nfft4GPAmdDistMatern12Kernel(void* str, double* data, int n, int ldim, int d
 {
    (void)data, (void)n, (void)ldim, (void)d, (void)permr, (void)kr, (void)permc, (void)kc;
    return dist_kernel_setup(str, 1, Kp, dKp);
+}
+
+int Nfft4GPAmdCommRanks(void* comm)
+{
+   if (!comm) return -1;
+   return ((Comm*)comm)->ranks();
+}
+
+static void dist_timing_reset(DistOp* D)
+{
+   for (hipEvent_t e : D->tpool) (void)hipEventDestroy(e);
+   D->tpool.clear();
+   for (auto& v : D->tpairs) v.clear();
+   D->tcount = 0;
+}
+
+int Nfft4GPAmdDistTimingEnable(void* dop, int enable)
+{
+   DistOp* D = (DistOp*)dop;
+   if (!D) return -1;
+   NFFT4GP_HIP_CHECK(hipStreamSynchronize(current_stream()));
+   if (D->cs) NFFT4GP_HIP_CHECK(hipStreamSynchronize(D->cs));
+   if (enable) dist_timing_reset(D);
+   D->timing = enable != 0;
+   return 0;
+}
+
+int Nfft4GPAmdDistTimingQuery(void* dop, double* ms, long long* cnt)
+{
+   DistOp* D = (DistOp*)dop;
+   if (!D || !ms) return -1;
+   NFFT4GP_HIP_CHECK(hipStreamSynchronize(current_stream()));
+   if (D->cs) NFFT4GP_HIP_CHECK(hipStreamSynchronize(D->cs));
+   for (int w = 0; w < 3; w++) {
+      double t = 0.0;
+      for (const auto& p : D->tpairs[w]) {
+         float f = 0.0f;
+         NFFT4GP_HIP_CHECK(hipEventElapsedTime(&f, D->tpool[p.first], D->tpool[p.second]));
+         t += f;
+      }
+      ms[w] = t;
+   }
+   if (cnt) *cnt = D->tcount;
+   return 0;
 }
 
 int Nfft4GPAmdDistSetChunks(void* dop, int chunks)

@@ -393,6 +393,8 @@ struct Comm {
    int rank = 0, world = 1;
    virtual ~Comm() {}
    virtual int allreduce(double* d_buf, size_t count, hipStream_t s) = 0;
+   // the number of ranks the backend itself reports (RCCL: ncclCommCount)
+   virtual int ranks() { return world; }
 };
 // additive handle rows (nfft_api.cpp): local, global, first row; -1 if not an additive handle
 int additive_rows(void* str, int* n_local, int* n_global, int* row_begin);

@@ -131,6 +131,11 @@ class Communicator:
             raise RuntimeError("Nfft4GPAmdCommAllreduce failed")
         return t
 
+    def ranks(self) -> int:
+        """The ranks the backend itself reports (ncclCommCount for RCCL; the group size for a callback)."""
+        from . import _lib
+        return int(_lib.lib().Nfft4GPAmdCommRanks(self.h))
+
     def free(self):
         if getattr(self, "h", None):
             from . import _lib
@@ -202,6 +207,25 @@ class DistributedAdditiveKernel:
 
     def gradmatsymv(self, x, alpha=1.0, beta=0.0, y=None):
         return self._apply("Nfft4GPAmdDistGradMatSymv", x, alpha, beta, y, 3)
+
+    def timing(self, on: bool = True):
+        """Per-rank hipEvent timing of every matvec (Nfft4GPAmdDistTimingEnable; enabling resets)."""
+        from . import _lib
+        if _lib.lib().Nfft4GPAmdDistTimingEnable(self.h, int(bool(on))) != 0:
+            raise RuntimeError("Nfft4GPAmdDistTimingEnable failed")
+
+    def timing_query(self) -> dict:
+        """Milliseconds per timed matvec of this rank's kernels before the exchange, the all-reduce(s) and the
+        kernels after it, and the number of matvecs timed."""
+        import ctypes as C
+        from . import _lib
+        ms = (C.c_double * 3)()
+        cnt = C.c_longlong()
+        if _lib.lib().Nfft4GPAmdDistTimingQuery(self.h, ms, C.byref(cnt)) != 0:
+            raise RuntimeError("Nfft4GPAmdDistTimingQuery failed")
+        k = max(cnt.value, 1)
+        return {"local_before_ms": ms[0] / k, "allreduce_ms": ms[1] / k, "local_after_ms": ms[2] / k,
+                "matvecs": cnt.value}
 
     @property
     def matvec_fnptr(self) -> int:
