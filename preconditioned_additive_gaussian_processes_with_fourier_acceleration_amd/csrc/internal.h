@@ -94,6 +94,17 @@ struct DefaultInitAlloc : std::allocator<T> {
 template <class T>
 using RawVec = std::vector<T, DefaultInitAlloc<T>>;
 
+// the q word of a (point, window) slot (layout.cpp): the offset in the cell in 2^-32 units of a cell, e = 64 frac,
+// moved to the nearest value congruent to the low 4 bits of the local index mod 16 (so |move| <= 8, an eighth of
+// the 2^-26 quantum), bit 31 flipped so that (int32)q = 2^32 (u = offset - 1/2).  The other 8 index bits are the
+// slot's lo byte (lo_byte).
+__host__ __device__ inline uint32_t slot_word(uint32_t loc, uint32_t frac)
+{
+   const uint32_t lo4 = loc & 15u, e = (frac & 0x3FFFFFFu) << 6;
+   return ((lo4 >= 8u && e != 0u) ? e - 16u + lo4 : e + lo4) ^ 0x80000000u;
+}
+__host__ __device__ inline uint32_t lo_byte(uint32_t loc) { return (loc >> 4) & 255u; }
+
 struct Layout {
    int n = 0;           // local points
    int nw = 0;          // components
@@ -103,8 +114,8 @@ struct Layout {
    int nblocks = 0;
    long long ntiles = 0;
    RawVec<uint16_t> meta;          // [ntiles*64]      comp<<6 | cell
-   RawVec<uint32_t> lo;            // [ntiles*R/4*64]  local index bits 0-5, one byte per point
-   RawVec<uint32_t> q;             // [ntiles*R*64]    offset in cell (26 bits) | index bits 6-11
+   RawVec<uint32_t> lo;            // [ntiles*R/4*64]  local index bits 4-11, one byte per point
+   RawVec<uint32_t> q;             // [ntiles*R*64]    slot_word: offset in the cell, index bits 0-3 below it
    std::vector<int> tile_off;      // [nblocks*ngroups+1]
 };
 // build from per-component quantized coordinates qc[c*n + j]

@@ -14,11 +14,13 @@
 //             grouped in 16-byte quads, quads lane-fastest, so each lane loads 16 B per instruction
 //             and a wave instruction reads 1 KiB contiguous (quad_index in internal.h):
 //               meta [tile][lane]            u16  comp << 6 | cell
-//               q    [tile][r/4][lane][r%4]  u32  bits 0-25: offset in the cell (2^-26 units),
-//                                                 bits 26-31: local index bits 6-11
-//               lo   [tile][0][lane][r/4]    u32  byte r%4 = local index bits 0-5
-//             5 bytes per (point, window): the chunk's cell lives in meta, so the coordinate word's
-//             top 6 bits carry half of the 12-bit local index instead.
+//               q    [tile][r/4][lane][r%4]  u32  slot_word (internal.h): the offset in the cell in 2^-32 cell
+//                                                  units, its low 4 bits = local index bits 0-3, bit 31 flipped
+//               lo   [tile][0][lane][r/4]    u32  byte r%4 = local index bits 4-11
+//             5 bytes per (point, window): the chunk's cell lives in meta.  The kernels read the q word as a
+//             signed int32: s = (int)q = 2^32 (offset - 1/2), one conversion for the centred offset scaled by 2^32
+//             (the 2^-32d are folded into the tap polynomial coefficients); carrying 4 index bits moves a point by
+//             at most an eighth of the coordinates' 2^-26-of-a-cell quantum.
 //   tile_off[b*ngroups + g] = first tile of (b, g); the spread kernel gets one workgroup per (b, g),
 //   the interpolation kernel one workgroup per b (all groups).
 #include <algorithm>
@@ -37,10 +39,9 @@ struct ChunkSink {
    uint32_t* q;
 };
 
-inline uint32_t slot_word(uint32_t loc, uint32_t frac) { return ((loc >> 6) << 26) | (frac & 0x3FFFFFFu); }
 inline uint32_t lo_word(const uint32_t* loc4)
 {
-   return (loc4[0] & 63u) | ((loc4[1] & 63u) << 8) | ((loc4[2] & 63u) << 16) | ((loc4[3] & 63u) << 24);
+   return lo_byte(loc4[0]) | (lo_byte(loc4[1]) << 8) | (lo_byte(loc4[2]) << 16) | (lo_byte(loc4[3]) << 24);
 }
 
 // Order the 16 points of every lane's run so that, at each point slot r, the 64 lanes of a tile hit

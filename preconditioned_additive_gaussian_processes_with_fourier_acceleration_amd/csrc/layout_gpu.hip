@@ -66,11 +66,14 @@ struct EmitLds {
       off = take(sizeof(int) * CG * (kNos + 1));
       run = take(sizeof(int) * CG * kNos);
       cbase = take(sizeof(int) * (CG * kNos + 1));
-      sorted = take(sizeof(uint16_t) * CG * B);
+      // the sorted indices are dead once the chunks are dealt (step 3), before the balance counters are used
+      // (step 4): one region serves both, so four windows per group fit at B = 4064
+      const size_t sorted_bytes = sizeof(uint16_t) * CG * B, cnt_bytes = sizeof(int) * Tmax * (2 * 32 + 4 * 16);
+      sorted = take(sorted_bytes > cnt_bytes ? sorted_bytes : cnt_bytes);
+      cnt = sorted;
       sloc = take(sizeof(uint16_t) * Tmax * kWave * kR);
       sfr = take(sizeof(uint32_t) * Tmax * kWave * kR);
       smeta = take(sizeof(uint16_t) * Tmax * kWave);
-      cnt = take(sizeof(int) * Tmax * (2 * 32 + 4 * 16));
       total = p;
    }
 };
@@ -89,7 +92,7 @@ __global__ __launch_bounds__(kLT) void k_lay_emit(const uint32_t* __restrict__ q
    uint16_t* s_loc = reinterpret_cast<uint16_t*>(lds + E.sloc);       // [T][64][16]
    uint32_t* s_fr = reinterpret_cast<uint32_t*>(lds + E.sfr);         // [T][64][16]
    uint16_t* s_meta = reinterpret_cast<uint16_t*>(lds + E.smeta);     // [T][64]
-   int* s_cnt = reinterpret_cast<int*>(lds + E.cnt);                  // [T][128] balance counters
+   int* s_cnt = reinterpret_cast<int*>(lds + E.cnt);                  // [T][128] balance counters (step 4; aliases s_sorted)
 
    const int bg = blockIdx.x, b = bg / ngroups, g = bg % ngroups;
    const int base = b * B, nloc = min(B, n - base);
@@ -224,13 +227,13 @@ __global__ __launch_bounds__(kLT) void k_lay_emit(const uint32_t* __restrict__ q
    for (int i = tid; i < T * kWave * kR; i += kLT) {
       const int tile = i / (kWave * kR), ln = (i / kR) % kWave, r = i % kR;
       const uint32_t loc = s_loc[i];
-      q[quad_index(t0 + tile, r, ln, kR)] = ((loc >> 6) << 26) | (s_fr[i] & 0x3FFFFFFu);
+      q[quad_index(t0 + tile, r, ln, kR)] = slot_word(loc, s_fr[i]);
    }
    for (int i = tid; i < T * kWave * (kR / 4); i += kLT) {
       const int tile = i / (kWave * (kR / 4)), ln = (i / (kR / 4)) % kWave, r4 = i % (kR / 4);
       const uint16_t* l4 = s_loc + ((size_t)tile * kWave + ln) * kR + 4 * r4;
       lo[quad_index(t0 + tile, r4, ln, kR / 4)] =
-          (l4[0] & 63u) | ((l4[1] & 63u) << 8) | ((l4[2] & 63u) << 16) | ((l4[3] & 63u) << 24);
+          lo_byte(l4[0]) | (lo_byte(l4[1]) << 8) | (lo_byte(l4[2]) << 16) | (lo_byte(l4[3]) << 24);
    }
 }
 
@@ -243,7 +246,9 @@ int build_layout_dev(const uint32_t* d_qc, int n, int nw, int B, int CG, Additiv
 {
    const int ngroups = (nw + CG - 1) / CG, nblocks = (n + B - 1) / B, nbg = ngroups * nblocks;
    const int Tmax_bound = (CG * (B / kR + kNos) + kWave - 1) / kWave + 1;
-   if (EmitLds(CG, B, Tmax_bound).total > 160 * 1024) return -1;
+   // the emit kernel's LDS is sized by the largest (block, group) actually counted (checked below); a group too
+   // large even at its smallest possible tile count goes to the host builder at once
+   if (EmitLds(CG, B, (CG * ((B + kR - 1) / kR) + kWave - 1) / kWave).total > 160 * 1024) return -1;
    int* d_tiles = nullptr;
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&d_tiles, sizeof(int) * (nbg + 1)));
    hipLaunchKernelGGL(k_lay_count, dim3(std::max(1, nbg)), dim3(kLT), 0, s, d_qc, n, nw, B, CG, ngroups, d_tiles);
@@ -260,7 +265,7 @@ int build_layout_dev(const uint32_t* d_qc, int n, int nw, int B, int CG, Additiv
       Tmax = std::max(Tmax, tiles[i]);
    }
    toff[nbg] = (int)acc;
-   if (Tmax > Tmax_bound) {
+   if (Tmax > Tmax_bound || EmitLds(CG, B, Tmax).total > 160 * 1024) {
       (void)hipFree(d_tiles);
       return -1;
    }

@@ -275,7 +275,7 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
       }
    const auto t1 = std::chrono::steady_clock::now();
    // the layout is built on the GPU from the quantised coordinates (layout_gpu.hip); layout.cpp builds the
-   // same arrays on the host when a (block, group) would not fit the GPU builder's LDS (B > 4064 or CG > 3
+   // same arrays on the host when a (block, group) would not fit the GPU builder's LDS (B > 4064, or CG > 4
    // would need it; neither is a setting the plan uses)
    free_layout(P);
    hipStream_t s = current_stream();

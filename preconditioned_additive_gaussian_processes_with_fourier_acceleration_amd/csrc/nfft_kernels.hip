@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 
 #include "internal.h"
@@ -29,17 +30,31 @@
 namespace nfft4gp_amd {
 
 constexpr int kGridThreads = 1024;
-// LDS row stride of the moment table: 13 doubles (26 banks) so rows of different cells spread over
-// the 64 banks instead of repeating every 8 cells (stride 12 -> 24 banks)
+// The spread's LDS moment table of a window group.  MOMT 1 (the default): [window][degree][cell], kMomWin
+// doubles per window (kNC x 64 plus 4: the windows' tables start 4 banks apart), so a run's 10 flushes are
+// one address each 64 doubles apart and the fold's lanes (consecutive cells) read consecutive doubles; 20.6 KB
+// for 4 windows, which with a 4064-point alpha slice still fits three workgroups per CU.  MOMT 0 (round 4):
+// [window][cell][degree] rows of kMomStride = 11 doubles (3 windows: 16.9 KB; 4 would not fit three per CU).
 constexpr int kMomStride = kNC + 1;
-
-__device__ __forceinline__ double q_to_u(uint32_t q)
+constexpr int kMomWin = kNC * kNos + 4;
+template <int MOMT>
+__host__ __device__ constexpr int mom_doubles_per_window()
 {
-   // offset inside the cell minus one half: exact in fp64
-   return (double)(q & 0x3FFFFFFu) * 0x1p-26 - 0.5;
+   return MOMT ? kMomWin : kNos * kMomStride;
+}
+template <int MOMT>
+__device__ __forceinline__ int mom_index(int cl, int cell, int d)
+{
+   return MOMT ? cl * kMomWin + d * kNos + cell : (cl * kNos + cell) * kMomStride + d;
 }
 
-// tap polynomial coefficients C[t][d] in constant memory: wave-uniform reads become scalar loads
+// the point's centred offset in its cell scaled by 2^32, s = 2^32 u: the q word read as int32 (slot_word,
+// internal.h) -- one conversion, no mask, no scale (the tap coefficients below carry the 2^-32d; scaling by
+// powers of two is exact, so the moments, H and Horner are those of u, bit for bit)
+__device__ __forceinline__ double q_to_s(uint32_t q) { return (double)(int)q; }
+
+// tap polynomial coefficients C[t][d] 2^-32d (monomials in s = 2^32 u) in constant memory: wave-uniform reads
+// become scalar loads
 __constant__ double c_taps[kTaps * kNC];
 
 // diagnostic timeline (TIMELINE builds only): per workgroup 4 s_memrealtime stamps (100 MHz)
@@ -54,8 +69,8 @@ __device__ __forceinline__ void stamp(int slot)
 
 struct TileRegs {
    uint32_t mt;
-   uint32_t lo[kR / 4];  // local index bits 0-5, one byte per point
-   uint32_t qq[kR];      // offset in the cell (bits 0-25) | local index bits 6-11 (bits 26-31)
+   uint32_t lo[kR / 4];  // local index bits 4-11, one byte per point
+   uint32_t qq[kR];      // slot_word (internal.h): offset in the cell, bit 31 flipped; bits 0-3 = local index bits 0-3
 };
 
 __device__ __forceinline__ void load_tile(TileRegs& T, const uint16_t* __restrict__ meta,
@@ -84,10 +99,34 @@ __device__ __forceinline__ void load_tile(TileRegs& T, const uint16_t* __restric
    }
 }
 
-// local index of point r of the run (0..B-1, or B for a dummy slot)
-__device__ __forceinline__ uint32_t slot_loc(const TileRegs& T, int r)
+// byte offset of point r's entry in a block's LDS slice of doubles: 8 x the local index (0..B-1, or B + lane % 32
+// for a dummy slot), whose bits 4-11 are the lo byte and bits 0-3 the low bits of the q word
+__device__ __forceinline__ uint32_t slot_off(const TileRegs& T, int r)
 {
-   return ((T.qq[r] >> 26) << 6) | ((T.lo[r >> 2] >> (8 * (r & 3))) & 63u);
+   // v_lshlrev_b32_sdwa (the byte, shifted) + v_lshlrev_b32 + v_and_or_b32: left to itself the compiler adds the
+   // two fields and the slice's LDS base 0 with an extra v_and + v_add3
+   const uint32_t hi = ((T.lo[r >> 2] >> (8 * (r & 3))) & 255u) << 7;
+   uint32_t off;
+   asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(off) : "v"(T.qq[r] << 3), "s"(0x78u), "v"(hi));
+   return off;
+}
+
+template <class V>
+__device__ __forceinline__ V* at_off(V* base, uint32_t byte_off)
+{
+   return reinterpret_cast<V*>(reinterpret_cast<char*>(base) + byte_off);
+}
+
+// the double at LDS byte address `byte_off`: the first dynamic slice of a kernel WITHOUT static LDS starts at LDS
+// address 0 (the launchers check that the kernel's static LDS is 0 bytes: static_lds_zero).  Through the extern
+// __shared__ pointer the compiler adds the slice base (a link-time constant) to every per-point offset, one VALU
+// add per point
+typedef __attribute__((address_space(3))) double lds_f64;
+__device__ __forceinline__ lds_f64* lds_at(uint32_t byte_off) { return (lds_f64*)(size_t)byte_off; }
+// ds_add_f64 at LDS byte address byte_off (the same convention)
+__device__ __forceinline__ void lds_add(uint32_t byte_off, double v)
+{
+   (void)__hip_atomic_fetch_add(lds_at(byte_off), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Stage x[base, base + nloc) of a block into LDS (zero beyond nloc, up to B, plus kPad zero entries that the
@@ -111,7 +150,7 @@ __device__ __forceinline__ void stage_block_glds(double* __restrict__ s, const d
 // spread
 // ------------------------------------------------------------------------------------------------
 // at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
-template <int THREADS, bool TIMELINE = false>
+template <int THREADS, bool TIMELINE = false, int MOMT = 1>
 __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restrict__ meta,
                                                       const uint32_t* __restrict__ lo,
                                                       const uint32_t* __restrict__ qarr,
@@ -122,7 +161,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = B + kPad;
    double* s_alpha = smem;     // Bp
-   double* s_mom = smem + Bp;  // CG*64*kMomStride per-cell moments
+   double* s_mom = smem + Bp;  // CG windows' moment tables (mom_index)
 
    // One workgroup = one block of points x one group of CG windows.  XCD-aware decode: the groups of one
    // block land on one XCD (blockIdx % 8), so its alpha slice is read into one L2.  Placement is speed only.
@@ -145,7 +184,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
    const int base = b * B;
    stage_block_glds<THREADS>(s_alpha, x, base, min(B, n - base), B);
-   for (int i = tid; i < CG * kNos * kMomStride; i += THREADS) s_mom[i] = 0.0;
+   for (int i = tid; i < CG * mom_doubles_per_window<MOMT>(); i += THREADS) s_mom[i] = 0.0;
    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces have landed
    __syncthreads();
    if (TIMELINE) stamp(1);
@@ -157,9 +196,8 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
       for (int d = 0; d < kNC; d++) acc[d] = 0.0;
 #pragma unroll
       for (int r = 0; r < kR; r++) {
-         const uint32_t loc = slot_loc(cur, r);
-         const double u = q_to_u(cur.qq[r]);
-         double tpow = s_alpha[loc];
+         const double u = q_to_s(cur.qq[r]);
+         double tpow = *lds_at(slot_off(cur, r));  // s_alpha is the first dynamic slice
          acc[0] += tpow;
 #pragma unroll
          for (int d = 1; d < kNC; d++) {
@@ -169,9 +207,9 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
       }
       const int comp_local = (int)(cur.mt >> 6) - c0;
       const int cell = (int)(cur.mt & 63u);
-      double* dst = s_mom + (comp_local * kNos + cell) * kMomStride;
+      double* dst = s_mom + mom_index<MOMT>(comp_local, cell, 0);
 #pragma unroll
-      for (int d = 0; d < kNC; d++) atomicAdd(dst + d, acc[d]);  // ds_add_f64
+      for (int d = 0; d < kNC; d++) atomicAdd(dst + mom_index<MOMT>(0, 0, d), acc[d]);  // ds_add_f64
       if (t + nwaves < t1) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
    }
    __syncthreads();
@@ -186,9 +224,9 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
       double v = 0.0;
 #pragma unroll 1
       for (int tp = 0; tp < kTaps; tp++) {
-         const double* mrow = s_mom + (cl * kNos + ((gi + kM - tp) & (kNos - 1))) * kMomStride;
+         const double* mrow = s_mom + mom_index<MOMT>(cl, (gi + kM - tp) & (kNos - 1), 0);
 #pragma unroll
-         for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[d], v);
+         for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[mom_index<MOMT>(0, 0, d)], v);
       }
       part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
    }
@@ -385,12 +423,12 @@ __global__ __launch_bounds__(THREADS) void k_interp_part(const uint16_t* __restr
       }
 #pragma unroll
       for (int r = 0; r < kR; r++) {
-         const uint32_t loc = slot_loc(cur, r);
-         const double u = q_to_u(cur.qq[r]);
+         const uint32_t off = slot_off(cur, r);
+         const double u = q_to_s(cur.qq[r]);
          double v = hc[kNC - 1];
 #pragma unroll
          for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
-         atomicAdd(s_y + loc, v);
+         lds_add(off, v);  // s_y is the first dynamic slice
       }
       const int tn = t + nwaves;
       if (tn < t1) load_tile(cur, meta, lo, qarr, tn, lane);
@@ -498,17 +536,17 @@ __global__ __launch_bounds__(THREADS) void k_interp(
       }
 #pragma unroll
       for (int r = 0; r < kR; r++) {
-         const uint32_t loc = slot_loc(cur, r);
-         const double u = q_to_u(cur.qq[r]);
+         const uint32_t off = slot_off(cur, r);
+         const double u = q_to_s(cur.qq[r]);
          double v = hc[kNC - 1];
 #pragma unroll
          for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
-         atomicAdd(s_y + loc, v);
+         lds_add(off, v);  // s_y is the first dynamic slice
          if (GRAD) {
             double vd = hdc[kNC - 1];
 #pragma unroll
             for (int d = kNC - 2; d >= 0; d--) vd = fma(vd, u, hdc[d]);
-            atomicAdd(s_yd + loc, vd);
+            lds_add(off + 8u * (uint32_t)Bp, vd);  // s_yd follows it
          }
       }
       if (tn < t1) load_tile(cur, meta, lo, qarr, tn, lane);
@@ -635,16 +673,16 @@ __global__ __launch_bounds__(THREADS) void k_interp2(const uint16_t* __restrict_
       }
 #pragma unroll
       for (int r = 0; r < kR; r++) {
-         const uint32_t loc = slot_loc(cur, r);
-         const double u = q_to_u(cur.qq[r]);
+         const uint32_t off = slot_off(cur, r);
+         const double u = q_to_s(cur.qq[r]);
          double v0 = h0[kNC - 1], v1 = h1[kNC - 1];
 #pragma unroll
          for (int d = kNC - 2; d >= 0; d--) {
             v0 = fma(v0, u, h0[d]);
             v1 = fma(v1, u, h1[d]);
          }
-         atomicAdd(s_y0 + loc, v0);
-         atomicAdd(s_y1 + loc, v1);
+         lds_add(off, v0);                      // s_y0: the first dynamic slice
+         lds_add(off + 8u * (uint32_t)Bp, v1);  // s_y1 follows it
       }
       if (t + nwaves < t1) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
    }
@@ -672,9 +710,12 @@ static void launch_ev(F fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, co
       hipLaunchKernelGGL(fn, grid, block, lds, s, args...);
 }
 
+static int spread_momt(const AdditivePlan& P) { return P.spread_variant == 2 ? 0 : 1; }
+
 static size_t spread_lds_bytes(const AdditivePlan& P)
 {
-   return sizeof(double) * ((size_t)P.B + kPad + (size_t)P.CG * kNos * kMomStride);
+   const size_t per = spread_momt(P) ? mom_doubles_per_window<1>() : mom_doubles_per_window<0>();
+   return sizeof(double) * ((size_t)P.B + kPad + (size_t)P.CG * per);
 }
 
 static size_t interp_lds_bytes(const AdditivePlan& P, int grad)
@@ -690,7 +731,10 @@ int upload_tap_coeffs()
    NFFT4GP_HIP_CHECK(hipGetDevice(&dev));
    if (dev < 0 || dev >= 64) return -1;
    if (!done[dev]) {
-      const std::vector<double>& C = tap_poly_coeffs();
+      // C[t][d] 2^-32d: the kernels evaluate the polynomials in s = 2^32 u (q_to_s)
+      std::vector<double> C = tap_poly_coeffs();
+      for (int t = 0; t < kTaps; t++)
+         for (int d = 0; d < kNC; d++) C[t * kNC + d] = std::ldexp(C[t * kNC + d], -32 * d);
       NFFT4GP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_taps), C.data(), sizeof(double) * kTaps * kNC));
       done[dev] = true;
    }
@@ -699,18 +743,27 @@ int upload_tap_coeffs()
 
 typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, int, int, int,
                          int, int, int, double*);
-// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py).  Variants that
-// measured slower or neutral (prefetching runs, persistent workgroups, several groups per workgroup, the fold in
-// two chains, register-staged alpha, the row shards' block sum in the spread's tail) were removed in round 4;
-// DESIGN.md 3.5 keeps their numbers.
+// 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py); 2: the round-4
+// moment table (MOMT 0, A/B).  Variants that measured slower or neutral (prefetching runs, persistent workgroups,
+// several groups per workgroup, the fold in two chains, register-staged alpha, the row shards' block sum in the
+// spread's tail) were removed in round 4; DESIGN.md 3.5 keeps their numbers.
 constexpr int kSpreadThreads = 512;
-static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>};
+static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>,
+                                           k_spread<kSpreadThreads, false, 0>};
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
 constexpr int kInterpThreads = 1024;
 typedef void (*InterpFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*,
                          const double*, const double*, double*, int, int, int, double, double, double, double,
                          double, double*, unsigned int*, double*);
+
+// a kernel whose dynamic slice is addressed absolutely (lds_at) must have no static LDS
+static bool static_lds_zero(const void* fn)
+{
+   hipFuncAttributes a;
+   if (hipFuncGetAttributes(&a, fn) != hipSuccess) return false;
+   return a.sharedSizeBytes == 0;
+}
 
 static void raise_lds_limit_once()
 {
@@ -728,10 +781,35 @@ static void raise_lds_limit_once()
    (void)raised;
 }
 
+// every kernel that addresses its dynamic LDS absolutely (lds_at / lds_add) has no static LDS
+static bool abs_lds_ok()
+{
+   static const bool ok = [] {
+      for (const void* f :
+           {(const void*)k_interp<false, 512>, (const void*)k_interp<true, 512>, (const void*)k_interp<false, 512, true>,
+            (const void*)k_interp<false, kInterpThreads>, (const void*)k_interp<true, kInterpThreads>,
+            (const void*)k_interp<false, kInterpThreads, true>, (const void*)k_interp_part<512>,
+            (const void*)k_interp2<1024>})
+         if (!static_lds_zero(f)) return false;
+      return true;
+   }();
+   if (!ok) fprintf(stderr, "nfft4gp_amd: an interpolation kernel has static LDS; its absolute LDS addressing is wrong\n");
+   return ok;
+}
+
 int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream)
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
    raise_lds_limit_once();
+   static const bool abs_ok = [] {
+      for (int i = 0; i < kNumSpreadVariants; i++)
+         if (!static_lds_zero((const void*)kSpreadVariants[i])) return false;
+      return true;
+   }();
+   if (!abs_ok) {
+      fprintf(stderr, "nfft4gp_amd: k_spread has static LDS; its absolute LDS addressing (lds_at) would be wrong\n");
+      return -1;
+   }
    const SpreadFn fn = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
    const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
    launch_ev(fn, dim3(gridx), dim3(kSpreadThreads), spread_lds_bytes(P), stream, P.kev ? P.kev + 0 : nullptr,
@@ -766,6 +844,7 @@ int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, do
       (void)hipGetLastError();
       attr = true;
    }
+   if (!abs_lds_ok()) return -1;
    const double ff = P.f * P.f;
    hipLaunchKernelGGL(k_grid_sum_yinit, dim3(P.nw), dim3(kGridThreads), 0, stream, d_gridsum, (const double*)P.d_w,
                       P.d_H, d_y, d_x, P.n, beta, alpha * ff * P.mu * P.diag);
@@ -790,6 +869,7 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
 {
    if (P.n == 0) return 0;
    raise_lds_limit_once();
+   if (!abs_lds_ok()) return -1;
    if (d_dot && (grad || P.nblocks > kRedMaxBlocks)) {
       fprintf(stderr, "nfft4gp_amd: fused matvec-dot needs a plain matvec and <= %d blocks\n", kRedMaxBlocks);
       return -1;
@@ -826,6 +906,7 @@ int launch_interp_blocks(const AdditivePlan& P, double alpha, const double* d_x,
 {
    if (P.n == 0 || b1 <= b0) return 0;
    raise_lds_limit_once();
+   if (!abs_lds_ok()) return -1;
    const size_t off = (size_t)b0 * P.B;
    hipLaunchKernelGGL((k_interp<false, kInterpThreads>), dim3(b1 - b0), dim3(kInterpThreads), interp_lds_bytes(P, 0),
                       stream, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off + (size_t)b0 * P.ngroups, (const double*)P.d_H,
@@ -844,7 +925,7 @@ int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double
                    double* y1, hipStream_t stream)
 {
    if (P.n == 0) return 0;
-   if (P.md.on) return -1;
+   if (P.md.on || !abs_lds_ok()) return -1;
    static bool attr = false;
    if (!attr) {
       (void)hipFuncSetAttribute((const void*)k_interp2<kInterp2Threads>, hipFuncAttributeMaxDynamicSharedMemorySize,

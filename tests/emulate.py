@@ -57,16 +57,18 @@ def layout(qc, n, nw, B=4064, CG=8):
     def quads(a, words):  # the 16-byte-quad layout [tile][w/4][lane][w%4] (layout.cpp) -> [tile][lane][w]
         return a.reshape(ntiles, words // 4, 64, 4).transpose(0, 2, 1, 3).reshape(ntiles, 64, words)
 
-    # 12-bit local index split over q (bits 26-31) and lo (a byte per point)
+    # 12-bit local index split over lo (bits 4-11, a byte per point) and q (bits 0-3); q read as int32 is the
+    # centred offset in the cell scaled by 2^32 (slot_word, internal.h)
     lw = quads(lo, R // 4).astype(np.int64)
-    qq = quads(q, R).astype(np.int64)
+    qw = quads(q, R)
     lob = np.empty((ntiles, 64, R), np.int64)
     for k in range(4):
-        lob[:, :, k::4] = (lw >> (8 * k)) & 63
-    loc = ((qq >> 26) << 6) | lob                      # local index (B + lane % 32 for dummies)
-    frac = qq & 0x3FFFFFF                              # offset in the cell, 2^-26 units
+        lob[:, :, k::4] = (lw >> (8 * k)) & 255
+    loc = (lob << 4) | (qw.astype(np.int64) & 15)      # local index (B + lane % 32 for dummies)
+    u = qw.view(np.int32).astype(np.float64) * 2.0 ** -32   # offset in the cell - 1/2
+    frac = (((qw ^ np.uint32(0x80000000)).astype(np.int64) + 32) >> 6)  # the nearest 26-bit offset, 2^-26 units
     return dict(ntiles=ntiles, ngroups=ngroups, nblocks=nblocks, meta=meta.reshape(ntiles, 64).astype(np.int64),
-                loc=loc, q=frac, tile_off=toff, B=B, CG=CG)
+                loc=loc, q=frac, u=u, tile_off=toff, B=B, CG=CG)
 
 
 class EmulatedPlan:
@@ -105,7 +107,7 @@ class EmulatedPlan:
         L = self.L
         B = L["B"]
         grid = np.zeros((self.nw, NOS))
-        u = (L["q"] & 0x3FFFFFF) * 2.0 ** -26 - 0.5          # [tile][lane][r]
+        u = L["u"]                                           # [tile][lane][r]
         comp = L["meta"] >> 6
         cell = L["meta"] & 63
         ng = L["ngroups"]
@@ -138,7 +140,7 @@ class EmulatedPlan:
         for tp in range(NTAP):
             Hm += h[:, (cells - M + tp) % NOS, None] * self.C[tp][None, None, :]
             Hdm += hd[:, (cells - M + tp) % NOS, None] * self.C[tp][None, None, :]
-        u = (L["q"] & 0x3FFFFFF) * 2.0 ** -26 - 0.5
+        u = L["u"]
         comp = L["meta"] >> 6
         cell = L["meta"] & 63
         acc = np.zeros(self.n)

@@ -38,7 +38,8 @@ def quantised(X):
 
 @pytest.mark.parametrize("n,nw,B,CG,kind", [(20000, 7, 4064, 3, "uniform"), (9000, 4, 512, 3, "clustered"),
                                             (5000, 3, 4064, 3, "duplicates"), (4064 * 3, 6, 4064, 3, "uniform"),
-                                            (777, 2, 100, 1, "uniform")])
+                                            (777, 2, 100, 1, "uniform"), (4064 * 10 + 17, 8, 4064, 4, "uniform"),
+                                            (9000, 5, 512, 4, "clustered")])
 def test_device_layout_equals_host(torch_cuda, n, nw, B, CG, kind):
     rng = np.random.default_rng(n + nw)
     if kind == "uniform":
