@@ -473,6 +473,11 @@ int Nfft4GPAmdAdditiveLayoutInfo(void *str, long long *out, int nout);
  * Nfft4GPAmdTimingQuery writes total milliseconds and launch counts for the three kernels:
  * ms[0..2] = spread, grid, interp;  cnt[0..2] likewise.  Returns 0. */
 int Nfft4GPAmdTimingEnable(void *str, int enable);
+/* deterministic 1-D matvec (on by default): the spread's moment-table flushes and the interpolation's y adds are
+ * rounded, before their LDS atomics, to a grid on which every partial sum is exact, so the result does not
+ * depend on the order the waves add in -- two matvecs of one vector are bitwise equal, and so are two PCG runs.
+ * Costs ~2^-45 relative rounding of each cell's moments and y value.  0 restores plain fp64 atomics. */
+int Nfft4GPAmdSetDeterministic(void *str, int on);
 int Nfft4GPAmdTimingQuery(void *str, double *ms, long long *cnt);
 /* average duration of ONE kernel of the additive matvec (which: 0 spread, 1 grid, 2 interp), measured
  * with a single hipEvent pair around `reps` back-to-back launches on the library stream (per-launch

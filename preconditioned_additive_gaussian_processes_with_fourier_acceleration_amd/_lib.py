@@ -167,6 +167,7 @@ _SIGS = {
     "Nfft4GPAmdCommAllreduce": (C.c_int, [vp, vp, C.c_longlong]),
     "Nfft4GPAmdCommFree": (None, [vp]),
     "Nfft4GPAmdCommRanks": (C.c_int, [vp]),
+    "Nfft4GPAmdSetDeterministic": (C.c_int, [vp, C.c_int]),
     "Nfft4GPAmdDistTimingEnable": (C.c_int, [vp, C.c_int]),
     "Nfft4GPAmdDistTimingQuery": (C.c_int, [vp, dp, C.POINTER(C.c_longlong)]),
     "Nfft4GPAmdAdditiveComponentShard": (C.c_int, [vp, C.c_int, C.c_int]),

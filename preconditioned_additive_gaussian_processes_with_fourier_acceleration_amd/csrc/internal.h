@@ -117,6 +117,7 @@ struct Layout {
    RawVec<uint32_t> lo;            // [ntiles*R/4*64]  local index bits 4-11, one byte per point
    RawVec<uint32_t> q;             // [ntiles*R*64]    slot_word: offset in the cell, index bits 0-3 below it
    std::vector<int> tile_off;      // [nblocks*ngroups+1]
+   std::vector<int> cmax;          // [nblocks*ngroups] the most points any one (window, cell) of (b, g) holds
 };
 // build from per-component quantized coordinates qc[c*n + j]
 void build_layout(const uint32_t* qc, int n, int nw, int B, int CG, Layout& L);
@@ -131,6 +132,7 @@ struct DevLayout {
    uint32_t* lo = nullptr;
    uint32_t* q = nullptr;
    int* tile_off = nullptr;
+   int* cmax = nullptr;  // [nblocks*ngroups] the most points of one (window, cell) of each (block, group)
    long long ntiles = 0;
    size_t bytes = 0;
 };
@@ -191,7 +193,11 @@ struct AdditivePlan {
    double diag = 1.0;    // 1: this handle adds the mu x (and grad f^2 x) terms; 0: a component shard without them
    // layout
    int B = kMaxBlock, CG = 3, ngroups = 0, nblocks = 0;  // CG = 3: 3 spread workgroups fit a CU's LDS
-   int spread_variant = 0;  // 0: the spread; 1: the same with timeline stamps (NFFT4GP_AMD_SPREAD_VARIANT, tools/)
+   int spread_variant = 0;  // 0: the spread; 1: the same with timeline stamps; 2: round-4 moment table (A/B)
+   // deterministic 1-D matvec: the spread's moment flushes and the interpolation's y adds are rounded to a grid on
+   // which every sum is exact, so results do not depend on the order of the LDS atomics (Nfft4GPAmdSetDeterministic)
+   bool det = true;
+   double* d_hb = nullptr;  // [vector 0, 1][H, Hd][nw] bounds of the interpolation polynomials (k_grid, det)
    int nparts = 0;          // partial grids per window the spread writes (one per block)
    DevLayout dl;
    // device buffers

@@ -80,7 +80,7 @@ void balance_tile(uint32_t (*loc)[kR], uint32_t (*fr)[kR])
 // sorted order -- different cells -- and their LDS flushes do not collide on one address.
 long long emit_block_group(const uint32_t* qc, int n, int nw, int B, int CG, int b, int g,
                            const ChunkSink* out, long long t0, long long T, std::vector<int>& cnt,
-                           std::vector<int>& off, std::vector<uint16_t>& sorted)
+                           std::vector<int>& off, std::vector<uint16_t>& sorted, int* cmax = nullptr)
 {
    const int base = b * B;
    const int nloc = std::min(B, n - base);
@@ -102,6 +102,8 @@ long long emit_block_group(const uint32_t* qc, int n, int nw, int B, int CG, int
       const uint32_t* qq = qc + (size_t)c * n + base;
       std::fill(cnt.begin(), cnt.end(), 0);
       for (int j = 0; j < nloc; j++) cnt[qq[j] >> 26]++;
+      if (cmax)
+         for (int cell = 0; cell < kNos; cell++) *cmax = std::max(*cmax, cnt[cell]);
       off[0] = 0;
       for (int cell = 0; cell < kNos; cell++) off[cell + 1] = off[cell] + cnt[cell];
       if (out) {
@@ -167,11 +169,13 @@ void build_layout(const uint32_t* qc, int n, int nw, int B, int CG, Layout& L)
    L.nblocks = (n + B - 1) / B;
    const int nbg = L.nblocks * L.ngroups;
    std::vector<long long> tiles(nbg, 0);
+   L.cmax.assign(nbg, 0);
    parallel_for(L.nblocks, [&](int b) {
       std::vector<int> cnt(kNos), off(kNos + 1);
       std::vector<uint16_t> sorted(B);
       for (int g = 0; g < L.ngroups; g++)
-         tiles[b * L.ngroups + g] = emit_block_group(qc, n, nw, B, CG, b, g, nullptr, 0, 0, cnt, off, sorted);
+         tiles[b * L.ngroups + g] = emit_block_group(qc, n, nw, B, CG, b, g, nullptr, 0, 0, cnt, off, sorted,
+                                                     &L.cmax[b * L.ngroups + g]);
    });
    L.tile_off.assign(nbg + 1, 0);
    long long acc = 0;

@@ -27,15 +27,15 @@ constexpr int kLT = 256;
 constexpr int kLWaves = kLT / 64;
 
 __global__ __launch_bounds__(kLT) void k_lay_count(const uint32_t* __restrict__ qc, int n, int nw, int B, int CG,
-                                                   int ngroups, int* __restrict__ tiles)
+                                                   int ngroups, int* __restrict__ tiles, int* __restrict__ cmax)
 {
    __shared__ int hist[kNos];
-   __shared__ int nch;
+   __shared__ int nch, mx;
    const int bg = blockIdx.x, b = bg / ngroups, g = bg % ngroups;
    const int base = b * B, nloc = min(B, n - base);
    const int c0 = g * CG, c1 = min(nw, c0 + CG);
    const int tid = threadIdx.x;
-   if (tid == 0) nch = 0;
+   if (tid == 0) nch = mx = 0;
    for (int c = c0; c < c1; c++) {
       const uint32_t* qq = qc + (size_t)c * n + base;
       if (tid < kNos) hist[tid] = 0;
@@ -43,13 +43,22 @@ __global__ __launch_bounds__(kLT) void k_lay_count(const uint32_t* __restrict__ 
       for (int j = tid; j < nloc; j += kLT) atomicAdd(&hist[qq[j] >> 26], 1);
       __syncthreads();
       if (tid < 64) {
-         int v = (hist[tid] + kR - 1) / kR;
-         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-         if (tid == 0) nch += v;
+         int v = (hist[tid] + kR - 1) / kR, m = hist[tid];
+         for (int off = 32; off > 0; off >>= 1) {
+            v += __shfl_xor(v, off, 64);
+            m = max(m, __shfl_xor(m, off, 64));
+         }
+         if (tid == 0) {
+            nch += v;
+            mx = max(mx, m);
+         }
       }
       __syncthreads();
    }
-   if (tid == 0) tiles[bg] = (nch + kWave - 1) / kWave;
+   if (tid == 0) {
+      tiles[bg] = (nch + kWave - 1) / kWave;
+      cmax[bg] = mx;
+   }
 }
 
 struct EmitLds {
@@ -250,8 +259,11 @@ int build_layout_dev(const uint32_t* d_qc, int n, int nw, int B, int CG, Additiv
    // large even at its smallest possible tile count goes to the host builder at once
    if (EmitLds(CG, B, (CG * ((B + kR - 1) / kR) + kWave - 1) / kWave).total > 160 * 1024) return -1;
    int* d_tiles = nullptr;
+   int* d_cmax = nullptr;
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&d_tiles, sizeof(int) * (nbg + 1)));
-   hipLaunchKernelGGL(k_lay_count, dim3(std::max(1, nbg)), dim3(kLT), 0, s, d_qc, n, nw, B, CG, ngroups, d_tiles);
+   NFFT4GP_HIP_CHECK(hipMalloc((void**)&d_cmax, sizeof(int) * std::max(1, nbg)));
+   hipLaunchKernelGGL(k_lay_count, dim3(std::max(1, nbg)), dim3(kLT), 0, s, d_qc, n, nw, B, CG, ngroups, d_tiles,
+                      d_cmax);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    std::vector<int> tiles(nbg);
    NFFT4GP_HIP_CHECK(hipMemcpyAsync(tiles.data(), d_tiles, sizeof(int) * nbg, hipMemcpyDeviceToHost, s));
@@ -267,11 +279,13 @@ int build_layout_dev(const uint32_t* d_qc, int n, int nw, int B, int CG, Additiv
    toff[nbg] = (int)acc;
    if (Tmax > Tmax_bound || EmitLds(CG, B, Tmax).total > 160 * 1024) {
       (void)hipFree(d_tiles);
+      (void)hipFree(d_cmax);
       return -1;
    }
    P.ngroups = ngroups;
    P.nblocks = nblocks;
    P.dl = DevLayout();
+   P.dl.cmax = d_cmax;
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.dl.tile_off, sizeof(int) * (nbg + 1)));
    NFFT4GP_HIP_CHECK(hipMemcpyAsync(P.dl.tile_off, toff.data(), sizeof(int) * (nbg + 1), hipMemcpyHostToDevice, s));
    const size_t nt = (size_t)std::max<long long>(acc, 1);
@@ -324,6 +338,7 @@ extern "C" int Nfft4GPAmdDeviceLayout(const unsigned int* qc, int n, int nw, int
    if (q && hipMemcpy(q, P.dl.q, sizeof(uint32_t) * nt * kR * kWave, hipMemcpyDeviceToHost) != hipSuccess) err = 1;
    if (tile_off && hipMemcpy(tile_off, P.dl.tile_off, sizeof(int) * (nbg + 1), hipMemcpyDeviceToHost) != hipSuccess)
       err = 1;
-   for (void* p : {(void*)P.dl.meta, (void*)P.dl.lo, (void*)P.dl.q, (void*)P.dl.tile_off}) (void)hipFree(p);
+   for (void* p : {(void*)P.dl.meta, (void*)P.dl.lo, (void*)P.dl.q, (void*)P.dl.tile_off, (void*)P.dl.cmax})
+      (void)hipFree(p);
    return err ? -1 : 0;
 }

@@ -143,6 +143,7 @@ void free_layout(AdditivePlan& P)
    dfree(P.dl.lo);
    dfree(P.dl.q);
    dfree(P.dl.tile_off);
+   dfree(P.dl.cmax);
    P.dl = DevLayout();
    dfree(P.d_part);
    dfree(P.d_part2);
@@ -165,6 +166,7 @@ void free_plan(PlanExt* E)
    dfree(P.d_wd);
    dfree(P.d_H);
    dfree(P.d_Hd);
+   dfree(P.d_hb);
    dfree(P.d_C);
    dfree(P.d_xs);
    dfree(P.d_ys);
@@ -293,7 +295,7 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
       P.nblocks = L.nblocks;
       free_layout(P);
       if (upload(&P.dl.meta, L.meta) || upload(&P.dl.lo, L.lo) || upload(&P.dl.q, L.q) ||
-          upload(&P.dl.tile_off, L.tile_off))
+          upload(&P.dl.tile_off, L.tile_off) || upload(&P.dl.cmax, L.cmax))
          return -1;
       P.dl.ntiles = L.ntiles;
       P.dl.bytes = L.meta.size() * 2 + L.lo.size() * 4 + L.q.size() * 4 + L.tile_off.size() * 4;
@@ -316,6 +318,7 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
 
    if (!P.d_H) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_H, sizeof(double) * (size_t)P.nw * kNos * kNC));
    if (!P.d_Hd) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_Hd, sizeof(double) * (size_t)P.nw * kNos * kNC));
+   if (!P.d_hb) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_hb, sizeof(double) * 4 * (size_t)std::max(1, P.nw)));
    if (upload_tap_coeffs()) return -1;
    P.points_ready = true;
    return 0;
@@ -494,11 +497,14 @@ int setup_common(void* str, int kernel, int n, int ldim, double** Kp, double** d
 // blocks to fill the 256 CUs, at the price of more partial grids and per-workgroup folds.  Measured per
 // matvec (32 windows; n: B = 4064 / 2032 / 1016): 1e6: 85.6 / 104.4 / 146.9 us; 5e5: 59.7 / 57.0 / -;
 // 2.5e5: 45.6 / 39.7 / 41.5; 1.25e5: 39.1 / 29.9 / 29.1; 1e5 (8 windows): 21.6 / 17.1 / 16.9.
+// Every block size is a multiple of 16 (so are the row shards' first rows, dist.row_range): a point's local index
+// is then its global index mod 16 in its low 4 bits whatever the layout, and so is the sub-quantum offset those
+// bits set in its q word (slot_word) -- the operator does not depend on the block size or the row split.
 int default_block(int n)
 {
    if (n >= 200 * kMaxBlock) return kMaxBlock;
    if (n >= 40 * 2032) return 2032;
-   return 1016;
+   return 1024;
 }
 
 // tuning overrides (layout only; results are independent of them up to rounding)
@@ -515,13 +521,14 @@ void env_layout(AdditivePlan& P)
    }
    if (const char* e = getenv("NFFT4GP_AMD_BLOCK")) {
       const int v = atoi(e);
-      if (v >= 256) P.B = std::min(v, kMaxBlock) & ~1;  // even: the LDS slice is staged in 16-byte pairs
+      if (v >= 256) P.B = std::min(v, kMaxBlock) & ~15;  // a multiple of 16 (default_block)
    }
    if (const char* e = getenv("NFFT4GP_AMD_CG")) {
       const int v = atoi(e);
       if (v >= 1 && v <= 64) P.CG = v;
    }
    if (const char* e = getenv("NFFT4GP_AMD_SPREAD_VARIANT")) P.spread_variant = atoi(e);
+   if (const char* e = getenv("NFFT4GP_AMD_DET")) P.det = atoi(e) != 0;
 }
 
 void* additive_create(double* data, int n_global, int ldim, int* windows, int nwindows, int dwindows, int rb, int re)
@@ -814,6 +821,15 @@ int Nfft4GPAmdAdditiveLayoutInfo(void* str, long long* out, int nout)
    long long v[10] = {P.n, P.nw, P.B, P.nblocks, P.dl.ntiles, P.dl.ntiles * kWave * kR, kR, P.CG, P.ngroups,
                       (long long)P.dl.bytes};
    for (int i = 0; i < nout && i < 10; i++) out[i] = v[i];
+   return 0;
+}
+
+int Nfft4GPAmdSetDeterministic(void* str, int on)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E) return -1;
+   (void)hipStreamSynchronize(current_stream());
+   E->P.det = on != 0;
    return 0;
 }
 

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <vector>
 
 #include "internal.h"
 #include "reduce.hpp"
@@ -149,19 +150,71 @@ __device__ __forceinline__ void stage_block_glds(double* __restrict__ s, const d
 // ------------------------------------------------------------------------------------------------
 // spread
 // ------------------------------------------------------------------------------------------------
+// DET (deterministic spread): every run's moment is rounded, before its ds_add_f64 into the moment
+// table, to a multiple of ulp(C_d), C_d = 1.5 2^E_d, with E_d chosen so that every partial sum of a table entry is
+// a multiple of that ulp below 2^(E_d + 1): the additions are then exact, so the table -- and the whole spread --
+// does not depend on the order the waves flush in.  The bound: |M_d| <= cm max|alpha| 2^31d (cm = the most
+// points of one (window, cell) in the workgroup, from the layout; |s| <= 2^31), a run's |moment| <= 16 max|alpha|
+// 2^31d, so E_d = e(max|alpha|) + max(log2 cm, 6) + 1 + 31 d.  Rounding costs ~2^-45 of a cell's moment.
+__device__ __forceinline__ double det_grid(uint32_t bexp)  // 1.5 x 2^(bexp - 1023) (bexp: a biased exponent)
+{
+   return __hiloint2double((int)((bexp << 20) | 0x80000u), 0);
+}
+__device__ __forceinline__ double det_round(double v, double C) { return (v + C) - C; }
+
+// the biased exponent field of max |x[base .. base + nloc)| (hi words; exact in any order), the same in every
+// thread of the workgroup; s_red: nwaves words of LDS.  Published by the caller's barrier (det_max_finish after it)
+template <int THREADS>
+__device__ __forceinline__ void det_max_start(const double* __restrict__ x, int base, int nloc, uint32_t* s_red)
+{
+   const uint32_t* xw = reinterpret_cast<const uint32_t*>(x + base);
+   uint32_t m = 0;
+   constexpr int kMaxPer = (kMaxBlock + THREADS - 1) / THREADS;
+   uint32_t v[kMaxPer];
+#pragma unroll
+   for (int k = 0; k < kMaxPer; k++) {
+      const int e = threadIdx.x + k * THREADS;
+      v[k] = e < nloc ? xw[2 * e + 1] & 0x7FFFFFFFu : 0u;
+   }
+#pragma unroll
+   for (int k = 0; k < kMaxPer; k++) m = max(m, v[k]);
+   for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+   if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = m;
+}
+template <int THREADS>
+__device__ __forceinline__ uint32_t det_max_finish(const uint32_t* s_red)
+{
+   uint32_t m = 0;
+#pragma unroll
+   for (int w = 0; w < THREADS / 64; w++) m = max(m, s_red[w]);
+   return (uint32_t)__builtin_amdgcn_readfirstlane((int)m) >> 20;
+}
+
+// DET interpolation: y_j sums one value per window, |f_c| <= hb[c] (k_grid), so with Y = sum_c hb[c] every partial
+// sum is below Y: each value is rounded to a multiple of ulp(C), C = 1.5 2^(e(Y) + 2), and the ds_add_f64 sums are
+// exact (order-independent).  Returns the biased exponent of C.
+__device__ __forceinline__ uint32_t det_interp_exp(const double* __restrict__ hb, int nw)
+{
+   double Y = 0.0;
+   for (int c = 0; c < nw; c++) Y += hb[c];
+   const uint32_t bY = ((uint32_t)__double2hiint(Y) >> 20) & 0x7FFu;
+   return min(bY + 2u, 2046u);
+}
+
 // at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
-template <int THREADS, bool TIMELINE = false, int MOMT = 1>
+template <int THREADS, bool TIMELINE = false, int MOMT = 1, bool DET = false>
 __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restrict__ meta,
                                                       const uint32_t* __restrict__ lo,
                                                       const uint32_t* __restrict__ qarr,
-                                                      const int* __restrict__ tile_off, const double* __restrict__ x,
-                                                      int n, int B, int nblocks, int ngroups, int CG, int nw,
-                                                      double* __restrict__ part)
+                                                      const int* __restrict__ tile_off, const int* __restrict__ cmax,
+                                                      const double* __restrict__ x, int n, int B, int nblocks,
+                                                      int ngroups, int CG, int nw, double* __restrict__ part)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = B + kPad;
    double* s_alpha = smem;     // Bp
    double* s_mom = smem + Bp;  // CG windows' moment tables (mom_index)
+   uint32_t* s_red = reinterpret_cast<uint32_t*>(s_mom + CG * mom_doubles_per_window<MOMT>());  // DET: nwaves
 
    // One workgroup = one block of points x one group of CG windows.  XCD-aware decode: the groups of one
    // block land on one XCD (blockIdx % 8), so its alpha slice is read into one L2.  Placement is speed only.
@@ -184,10 +237,17 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
    const int base = b * B;
    stage_block_glds<THREADS>(s_alpha, x, base, min(B, n - base), B);
+   if (DET) det_max_start<THREADS>(x, base, min(B, n - base), s_red);
    for (int i = tid; i < CG * mom_doubles_per_window<MOMT>(); i += THREADS) s_mom[i] = 0.0;
    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces have landed
    __syncthreads();
    if (TIMELINE) stamp(1);
+   uint32_t bC0 = 0;  // DET: biased exponent of C_0 (C_d: + 31 d)
+   if (DET) {
+      const int cm = cmax[b * ngroups + g];
+      const uint32_t lc = cm > 1 ? 32u - (uint32_t)__clz(cm - 1) : 0u;
+      bC0 = det_max_finish<THREADS>(s_red) + max(lc, 6u) + 1u;
+   }
 
    const int c0 = g * CG;
    for (; t < t1; t += nwaves) {
@@ -209,7 +269,10 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
       const int cell = (int)(cur.mt & 63u);
       double* dst = s_mom + mom_index<MOMT>(comp_local, cell, 0);
 #pragma unroll
-      for (int d = 0; d < kNC; d++) atomicAdd(dst + mom_index<MOMT>(0, 0, d), acc[d]);  // ds_add_f64
+      for (int d = 0; d < kNC; d++) {
+         const double a = DET ? det_round(acc[d], det_grid(bC0 + 31u * d)) : acc[d];
+         atomicAdd(dst + mom_index<MOMT>(0, 0, d), a);  // ds_add_f64
+      }
       if (t + nwaves < t1) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
    }
    __syncthreads();
@@ -263,8 +326,11 @@ __device__ __forceinline__ void grid_tail_coeffs(double (&ct)[kTaps])
    for (int tp = 0; tp < kTaps; tp++) ct[tp] = tid < kNos * kNC ? c_taps[tp * kNC + d] : 0.0;
 }
 
+// hb (det, may be NULL): hb[comp] = max over cells of sum_d |H[cell][d]| 2^31d, a bound on |f(s)| for |s| <= 2^31
+// (the interpolation's rounding grid); s_scr: kNos * kNC doubles of LDS scratch when hb is given
 __device__ void grid_tail(int comp, const double* __restrict__ s_g, double wreg, const double (&ct)[kTaps],
-                          double* __restrict__ H, double* s_w, double* s_h)
+                          double* __restrict__ H, double* s_w, double* s_h, double* __restrict__ hb = nullptr,
+                          double* s_scr = nullptr)
 {
    static_assert(kGridThreads >= kNos * kNC, "one H entry per thread");
    const int tid = threadIdx.x;
@@ -291,16 +357,29 @@ __device__ void grid_tail(int comp, const double* __restrict__ s_g, double wreg,
 #pragma unroll
       for (int tp = 0; tp < kTaps; tp++) v = fma(s_h[(cell - kM + tp) & (kNos - 1)], ct[tp], v);
       H[((size_t)comp * kNos + cell) * kNC + d] = v;
+      if (hb) s_scr[tid] = ldexp(fabs(v), 31 * d);
+   }
+   if (hb) {
+      __syncthreads();
+      if (tid < kNos) {  // one wave: a cell per lane, summed in degree order, then the max over the cells
+         double m = 0.0;
+#pragma unroll
+         for (int d = 0; d < kNC; d++) m += s_scr[tid * kNC + d];
+         for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
+         if (tid == 0) hb[comp] = m;
+      }
    }
    __syncthreads();
 }
 
 // part: [nw][nparts][64] (from_sum = 0) or the summed grids [nw][64] (from_sum = 1)
 // blockIdx.y: right-hand side (two-vector matvec): part and H advance by part_rs / h_rs elements per vector
+// hb (det, may be NULL): the bounds of H at hb[comp] and of Hd at hb[nw + comp], per vector at hb + 2 nw y
 __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict__ part, int nparts,
                                                       const double* __restrict__ w, const double* __restrict__ wd,
                                                       double* __restrict__ H, double* __restrict__ Hd, int grad,
-                                                      int from_sum, long long part_rs = 0, long long h_rs = 0)
+                                                      int from_sum, long long part_rs = 0, long long h_rs = 0,
+                                                      double* __restrict__ hb = nullptr)
 {
    __shared__ double s_red[kGridThreads];
    __shared__ double s_g[kNos];
@@ -345,8 +424,9 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
       }
    }
    __syncthreads();
-   grid_tail(comp, s_g, wv, ct, H, s_w, s_h);
-   if (grad) grid_tail(comp, s_g, wdv, ct, Hd, s_w, s_h);
+   if (hb) hb += 2 * (size_t)gridDim.x * blockIdx.y;
+   grid_tail(comp, s_g, wv, ct, H, s_w, s_h, hb, s_red);
+   if (grad) grid_tail(comp, s_g, wdv, ct, Hd, s_w, s_h, hb ? hb + gridDim.x : nullptr, s_red);
 }
 
 // Row shards with few blocks, split interpolation (launch_shard_finish_split): the grid kernel from the summed
@@ -478,13 +558,14 @@ constexpr int kEpMax = 8;  // epilogue values per thread held in registers (B <=
 
 // DOT (non-GRAD only): also forms (y_out, x) -- the (q, p) of a CG step when y = A p -- with a
 // deterministic grid-wide sum written to *dot_out by the last block (reduce.hpp)
-template <bool GRAD, int THREADS, bool DOT = false>
+// DET: the y adds rounded on the grid of det_interp_exp (hb: the bounds of H, and of Hd at hb + nw)
+template <bool GRAD, int THREADS, bool DOT = false, bool DET = false>
 __global__ __launch_bounds__(THREADS) void k_interp(
     const uint16_t* __restrict__ meta, const uint32_t* __restrict__ lo, const uint32_t* __restrict__ qarr,
     const int* __restrict__ tile_off, const double* __restrict__ H, const double* __restrict__ Hd,
     const double* __restrict__ x, double* __restrict__ y, int n, int B, int ngroups, double alpha, double beta,
     double f, double mu, double dg, double* __restrict__ dot_part, unsigned int* __restrict__ dot_ticket,
-    double* __restrict__ dot_out)
+    double* __restrict__ dot_out, const double* __restrict__ hb, int nw)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = B + kPad;
@@ -517,6 +598,11 @@ __global__ __launch_bounds__(THREADS) void k_interp(
       s_y[i] = 0.0;
       if (GRAD) s_yd[i] = 0.0;
    }
+   double Cy = 0.0, Cyd = 0.0;
+   if (DET) {
+      Cy = det_grid(det_interp_exp(hb, nw));
+      if (GRAD) Cyd = det_grid(det_interp_exp(hb + nw, nw));
+   }
    __syncthreads();
 
    for (; t < t1; t += nwaves) {
@@ -541,12 +627,12 @@ __global__ __launch_bounds__(THREADS) void k_interp(
          double v = hc[kNC - 1];
 #pragma unroll
          for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
-         lds_add(off, v);  // s_y is the first dynamic slice
+         lds_add(off, DET ? det_round(v, Cy) : v);  // s_y is the first dynamic slice
          if (GRAD) {
             double vd = hdc[kNC - 1];
 #pragma unroll
             for (int d = kNC - 2; d >= 0; d--) vd = fma(vd, u, hdc[d]);
-            lds_add(off + 8u * (uint32_t)Bp, vd);  // s_yd follows it
+            lds_add(off + 8u * (uint32_t)Bp, DET ? det_round(vd, Cyd) : vd);  // s_yd follows it
          }
       }
       if (tn < t1) load_tile(cur, meta, lo, qarr, tn, lane);
@@ -613,9 +699,15 @@ __global__ __launch_bounds__(THREADS) void k_interp(
       }
    }
    if (DOT && !GRAD) {
-      dacc = block_sum0<THREADS>(dacc);
+      // LDS scratch after the y slices (kRedScratch bytes): the kernel keeps no static LDS (lds_add addresses its
+      // first dynamic slice absolutely)
+      double* s_scr = smem + (GRAD ? 2 : 1) * Bp;
+      dacc = block_sum0_s<THREADS>(dacc, s_scr);
       double tot;
-      if (grid_total<THREADS>(dacc, dot_part, dot_ticket, &tot) && threadIdx.x == 0) *dot_out = tot;
+      if (grid_total_s<THREADS>(dacc, dot_part, dot_ticket, &tot, reinterpret_cast<int*>(s_scr + 2 * (THREADS / 64)),
+                                s_scr + THREADS / 64) &&
+          threadIdx.x == 0)
+         *dot_out = tot;
    }
 }
 
@@ -630,7 +722,9 @@ __global__ __launch_bounds__(THREADS) void k_interp(
 // 51 us against 2 x 34 us.
 
 // y_v = beta y_v + alpha f^2 (sum_windows interp_v + mu x_v), v = 0, 1; H of vector v at H + v * h_rs
-template <int THREADS>
+// DET: as k_interp's, each vector on the grid of its own bounds (hb, hb + 2 nw: k_grid's per-vector layout), so
+// each column equals the single-vector matvec bit for bit
+template <int THREADS, bool DET = false>
 __global__ __launch_bounds__(THREADS) void k_interp2(const uint16_t* __restrict__ meta,
                                                      const uint32_t* __restrict__ lo,
                                                      const uint32_t* __restrict__ qarr,
@@ -638,7 +732,8 @@ __global__ __launch_bounds__(THREADS) void k_interp2(const uint16_t* __restrict_
                                                      size_t h_rs, const double* __restrict__ x0,
                                                      const double* __restrict__ x1, double* __restrict__ y0,
                                                      double* __restrict__ y1, int n, int B, int ngroups, double alpha,
-                                                     double beta, double f, double mu)
+                                                     double beta, double f, double mu, const double* __restrict__ hb,
+                                                     int nw)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = B + kPad;
@@ -657,6 +752,11 @@ __global__ __launch_bounds__(THREADS) void k_interp2(const uint16_t* __restrict_
    int t = t0 + wave;
    if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
    for (int i = tid; i < Bp; i += THREADS) s_y0[i] = s_y1[i] = 0.0;
+   double C0 = 0.0, C1 = 0.0;
+   if (DET) {
+      C0 = det_grid(det_interp_exp(hb, nw));
+      C1 = det_grid(det_interp_exp(hb + 2 * nw, nw));
+   }
    __syncthreads();
    const double* H1 = H + h_rs;
    for (; t < t1; t += nwaves) {
@@ -681,8 +781,8 @@ __global__ __launch_bounds__(THREADS) void k_interp2(const uint16_t* __restrict_
             v0 = fma(v0, u, h0[d]);
             v1 = fma(v1, u, h1[d]);
          }
-         lds_add(off, v0);                      // s_y0: the first dynamic slice
-         lds_add(off + 8u * (uint32_t)Bp, v1);  // s_y1 follows it
+         lds_add(off, DET ? det_round(v0, C0) : v0);                      // s_y0: the first dynamic slice
+         lds_add(off + 8u * (uint32_t)Bp, DET ? det_round(v1, C1) : v1);  // s_y1 follows it
       }
       if (t + nwaves < t1) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
    }
@@ -715,12 +815,15 @@ static int spread_momt(const AdditivePlan& P) { return P.spread_variant == 2 ? 0
 static size_t spread_lds_bytes(const AdditivePlan& P)
 {
    const size_t per = spread_momt(P) ? mom_doubles_per_window<1>() : mom_doubles_per_window<0>();
-   return sizeof(double) * ((size_t)P.B + kPad + (size_t)P.CG * per);
+   return sizeof(double) * ((size_t)P.B + kPad + (size_t)P.CG * per) + (P.det ? 4 * (512 / 64) : 0);  // DET: a word per wave (kSpreadThreads)
 }
+
+// the fused dot's reduction scratch after the y slices: 2 x (1024 / 64) doubles and an int
+constexpr size_t kRedScratch = sizeof(double) * (2 * (1024 / 64) + 1);
 
 static size_t interp_lds_bytes(const AdditivePlan& P, int grad)
 {
-   return sizeof(double) * ((size_t)P.B + kPad) * (grad ? 2 : 1);
+   return sizeof(double) * ((size_t)P.B + kPad) * (grad ? 2 : 1) + kRedScratch;
 }
 
 int upload_tap_coeffs()
@@ -741,8 +844,8 @@ int upload_tap_coeffs()
    return 0;
 }
 
-typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, int, int, int,
-                         int, int, int, double*);
+typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const int*, const double*, int,
+                         int, int, int, int, int, double*);
 // 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py); 2: the round-4
 // moment table (MOMT 0, A/B).  Variants that measured slower or neutral (prefetching runs, persistent workgroups,
 // several groups per workgroup, the fold in two chains, register-staged alpha, the row shards' block sum in the
@@ -750,12 +853,34 @@ typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, cons
 constexpr int kSpreadThreads = 512;
 static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>,
                                            k_spread<kSpreadThreads, false, 0>};
+// the deterministic spread (AdditivePlan::det) of each variant
+static const SpreadFn kSpreadVariantsDet[] = {k_spread<kSpreadThreads, false, 1, true>,
+                                              k_spread<kSpreadThreads, true, 1, true>,
+                                              k_spread<kSpreadThreads, false, 0, true>};
 constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
 
 constexpr int kInterpThreads = 1024;
 typedef void (*InterpFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*,
                          const double*, const double*, double*, int, int, int, double, double, double, double,
-                         double, double*, unsigned int*, double*);
+                         double, double*, unsigned int*, double*, const double*, int);
+
+// the interpolation kernel of a launch: gradient or not, fused (q, p) or not, 512 or 1024 threads, deterministic
+template <int T>
+static InterpFn interp_fn_t(bool grad, bool dot, bool det)
+{
+   if (grad) return det ? k_interp<true, T, false, true> : k_interp<true, T, false, false>;
+   if (dot) return det ? k_interp<false, T, true, true> : k_interp<false, T, true, false>;
+   return det ? k_interp<false, T, false, true> : k_interp<false, T, false, false>;
+}
+static InterpFn interp_fn(bool grad, bool dot, bool small, bool det)
+{
+   return small ? interp_fn_t<512>(grad, dot, det) : interp_fn_t<kInterpThreads>(grad, dot, det);
+}
+constexpr int kInterp2Threads = 1024;
+typedef void (*Interp2Fn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, size_t,
+                          const double*, const double*, double*, double*, int, int, int, double, double, double, double,
+                          const double*, int);
+static Interp2Fn interp2_fn(bool det) { return det ? k_interp2<kInterp2Threads, true> : k_interp2<kInterp2Threads, false>; }
 
 // a kernel whose dynamic slice is addressed absolutely (lds_at) must have no static LDS
 static bool static_lds_zero(const void* fn)
@@ -765,16 +890,29 @@ static bool static_lds_zero(const void* fn)
    return a.sharedSizeBytes == 0;
 }
 
+// every interpolation kernel the launchers pick
+static std::vector<const void*> interp_kernels()
+{
+   std::vector<const void*> v;
+   for (int g = 0; g < 2; g++)
+      for (int d = 0; d < 2; d++)
+         for (int sm = 0; sm < 2; sm++)
+            for (int det = 0; det < 2; det++) v.push_back((const void*)interp_fn(g, d && !g, sm, det));
+   v.push_back((const void*)interp2_fn(false));
+   v.push_back((const void*)interp2_fn(true));
+   return v;
+}
+
 static void raise_lds_limit_once()
 {
    // a function-local static initialiser runs once (thread-safe)
    static const bool raised = []() {
       for (int i = 0; i < kNumSpreadVariants; i++)
-         (void)hipFuncSetAttribute((const void*)kSpreadVariants[i], hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   160 * 1024);
-      for (const void* f : {(const void*)k_interp<false, kInterpThreads>, (const void*)k_interp<true, kInterpThreads>,
-                            (const void*)k_interp<false, kInterpThreads, true>})
+         for (const SpreadFn f : {kSpreadVariants[i], kSpreadVariantsDet[i]})
+            (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      for (const void* f : interp_kernels())
          (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_interp_part<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipGetLastError();
       return true;
    }();
@@ -785,15 +923,17 @@ static void raise_lds_limit_once()
 static bool abs_lds_ok()
 {
    static const bool ok = [] {
-      for (const void* f :
-           {(const void*)k_interp<false, 512>, (const void*)k_interp<true, 512>, (const void*)k_interp<false, 512, true>,
-            (const void*)k_interp<false, kInterpThreads>, (const void*)k_interp<true, kInterpThreads>,
-            (const void*)k_interp<false, kInterpThreads, true>, (const void*)k_interp_part<512>,
-            (const void*)k_interp2<1024>})
+      std::vector<const void*> v = interp_kernels();
+      v.push_back((const void*)k_interp_part<512>);
+      for (int i = 0; i < kNumSpreadVariants; i++) {
+         v.push_back((const void*)kSpreadVariants[i]);
+         v.push_back((const void*)kSpreadVariantsDet[i]);
+      }
+      for (const void* f : v)
          if (!static_lds_zero(f)) return false;
       return true;
    }();
-   if (!ok) fprintf(stderr, "nfft4gp_amd: an interpolation kernel has static LDS; its absolute LDS addressing is wrong\n");
+   if (!ok) fprintf(stderr, "nfft4gp_amd: a matvec kernel has static LDS; its absolute LDS addressing would be wrong\n");
    return ok;
 }
 
@@ -801,19 +941,13 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
    raise_lds_limit_once();
-   static const bool abs_ok = [] {
-      for (int i = 0; i < kNumSpreadVariants; i++)
-         if (!static_lds_zero((const void*)kSpreadVariants[i])) return false;
-      return true;
-   }();
-   if (!abs_ok) {
-      fprintf(stderr, "nfft4gp_amd: k_spread has static LDS; its absolute LDS addressing (lds_at) would be wrong\n");
-      return -1;
-   }
-   const SpreadFn fn = kSpreadVariants[std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1)];
+   if (!abs_lds_ok()) return -1;
+   const int v = std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1);
+   const SpreadFn fn = P.det ? kSpreadVariantsDet[v] : kSpreadVariants[v];
    const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
    launch_ev(fn, dim3(gridx), dim3(kSpreadThreads), spread_lds_bytes(P), stream, P.kev ? P.kev + 0 : nullptr,
-             P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, d_x, P.n, P.B, P.nblocks, P.ngroups, P.CG, P.nw, d_part);
+             P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const int*)P.dl.cmax, d_x, P.n, P.B, P.nblocks, P.ngroups,
+             P.CG, P.nw, d_part);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -821,7 +955,8 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream)
 {
    launch_ev(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, P.kev ? P.kev + 2 : nullptr, d_part, nparts,
-             (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 0, 0ll, 0ll);
+             (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 0, 0ll, 0ll,
+             P.det ? P.d_hb : (double*)nullptr);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -829,7 +964,8 @@ int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int gra
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream)
 {
    launch_ev(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, P.kev ? P.kev + 2 : nullptr, d_gridsum, 1,
-             (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 1, 0ll, 0ll);
+             (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 1, 0ll, 0ll,
+             P.det ? P.d_hb : (double*)nullptr);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -838,12 +974,7 @@ int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, do
                               double beta, double* d_y, int S, hipStream_t stream)
 {
    constexpr int T = 512;
-   static bool attr = false;
-   if (!attr) {
-      (void)hipFuncSetAttribute((const void*)k_interp_part<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipGetLastError();
-      attr = true;
-   }
+   raise_lds_limit_once();
    if (!abs_lds_ok()) return -1;
    const double ff = P.f * P.f;
    hipLaunchKernelGGL(k_grid_sum_yinit, dim3(P.nw), dim3(kGridThreads), 0, stream, d_gridsum, (const double*)P.d_w,
@@ -878,22 +1009,12 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
    // and epilogue: 787 -> 734 us at config E; with fewer blocks half the CU would idle, 30.8 -> 34.3 us at
    // config C; profiles/r04_interp_threads_ab.txt).  NFFT4GP_AMD_INTERP_THREADS=512 / 1024 forces either.
    static const int forced = getenv("NFFT4GP_AMD_INTERP_THREADS") ? atoi(getenv("NFFT4GP_AMD_INTERP_THREADS")) : 0;
-   static const bool attr512 = [] {
-      for (const void* f : {(const void*)k_interp<false, 512>, (const void*)k_interp<true, 512>,
-                            (const void*)k_interp<false, 512, true>})
-         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipGetLastError();
-      return true;
-   }();
-   (void)attr512;
    const bool small = forced == 512 || (forced != 1024 && P.nblocks >= 512);
-   const InterpFn fn = small ? (grad ? k_interp<true, 512> : (d_dot ? k_interp<false, 512, true> : k_interp<false, 512>))
-                             : (grad ? k_interp<true, kInterpThreads>
-                                     : (d_dot ? k_interp<false, kInterpThreads, true> : k_interp<false, kInterpThreads>));
+   const InterpFn fn = interp_fn(grad, d_dot != nullptr, small, P.det);
    launch_ev(fn, dim3(P.nblocks), dim3(small ? 512 : kInterpThreads), interp_lds_bytes(P, grad), stream,
              P.kev ? P.kev + 4 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H,
              (const double*)P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups, alpha, beta, P.f, P.mu * P.diag, P.diag,
-             P.d_dot_part, P.d_dot_ticket, d_dot);
+             P.d_dot_part, P.d_dot_ticket, d_dot, (const double*)P.d_hb, P.nw);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -908,10 +1029,11 @@ int launch_interp_blocks(const AdditivePlan& P, double alpha, const double* d_x,
    raise_lds_limit_once();
    if (!abs_lds_ok()) return -1;
    const size_t off = (size_t)b0 * P.B;
-   hipLaunchKernelGGL((k_interp<false, kInterpThreads>), dim3(b1 - b0), dim3(kInterpThreads), interp_lds_bytes(P, 0),
-                      stream, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off + (size_t)b0 * P.ngroups, (const double*)P.d_H,
-                      (const double*)P.d_Hd, d_x + off, d_y + off, P.n - (int)off, P.B, P.ngroups, alpha, beta, P.f,
-                      P.mu * P.diag, P.diag, (double*)nullptr, (unsigned int*)nullptr, (double*)nullptr);
+   hipLaunchKernelGGL(interp_fn(false, false, false, P.det), dim3(b1 - b0), dim3(kInterpThreads),
+                      interp_lds_bytes(P, 0), stream, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off + (size_t)b0 * P.ngroups,
+                      (const double*)P.d_H, (const double*)P.d_Hd, d_x + off, d_y + off, P.n - (int)off, P.B, P.ngroups,
+                      alpha, beta, P.f, P.mu * P.diag, P.diag, (double*)nullptr, (unsigned int*)nullptr,
+                      (double*)nullptr, (const double*)P.d_hb, P.nw);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -919,33 +1041,27 @@ int launch_interp_blocks(const AdditivePlan& P, double alpha, const double* d_x,
 // y_v = beta y_v + alpha A x_v for two vectors: one spread per vector, both grids in one launch, one two-vector
 // interpolation (1-D layouts, whole-row handles).  A two-vector spread (both alpha slices and 21-double moment
 // rows in LDS, the layout and u^d shared) measured slower at every shape tried in round 4
-constexpr int kInterp2Threads = 1024;
-
 int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double* x1, double beta, double* y0,
                    double* y1, hipStream_t stream)
 {
    if (P.n == 0) return 0;
-   if (P.md.on || !abs_lds_ok()) return -1;
-   static bool attr = false;
-   if (!attr) {
-      (void)hipFuncSetAttribute((const void*)k_interp2<kInterp2Threads>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-      (void)hipGetLastError();
-      attr = true;
-   }
+   if (P.md.on) return -1;
+   raise_lds_limit_once();
+   if (!abs_lds_ok()) return -1;
    const size_t part_rs = (size_t)std::max(1, P.nparts) * P.nw * kNos;
    const size_t h_rs = (size_t)P.nw * kNos * kNC;
    // both vectors' partial grids in one allocation, so k_grid's per-vector stride stays inside it
    if (!P.d_part2) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_part2, sizeof(double) * 2 * part_rs));
    if (!P.d_H2) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_H2, sizeof(double) * 2 * h_rs));
    if (launch_spread(P, x0, P.d_part2, stream) || launch_spread(P, x1, P.d_part2 + part_rs, stream)) return -1;
+   // P.d_hb holds [vector][H, Hd][nw]: the grid writes each vector's H bound at hb + 2 nw y
    hipLaunchKernelGGL(k_grid, dim3(P.nw, 2), dim3(kGridThreads), 0, stream, (const double*)P.d_part2, P.nparts,
                       (const double*)P.d_w, (const double*)P.d_wd, P.d_H2, P.d_Hd, 0, 0, (long long)part_rs,
-                      (long long)h_rs);
+                      (long long)h_rs, P.det ? P.d_hb : (double*)nullptr);
    const size_t lds_i = sizeof(double) * 2 * ((size_t)P.B + kPad);
-   hipLaunchKernelGGL(k_interp2<kInterp2Threads>, dim3(P.nblocks), dim3(kInterp2Threads), lds_i, stream, P.dl.meta,
-                      P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H2, h_rs, x0, x1, y0, y1, P.n, P.B,
-                      P.ngroups, alpha, beta, P.f, P.mu * P.diag);
+   hipLaunchKernelGGL(interp2_fn(P.det), dim3(P.nblocks), dim3(kInterp2Threads), lds_i, stream, P.dl.meta, P.dl.lo,
+                      P.dl.q, P.dl.tile_off, (const double*)P.d_H2, h_rs, x0, x1, y0, y1, P.n, P.B, P.ngroups, alpha,
+                      beta, P.f, P.mu * P.diag, (const double*)P.d_hb, P.nw);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

@@ -18,11 +18,10 @@ constexpr int kTicketStride = 64;                              // unsigned ints:
 constexpr int kTicketWords = (kRedXcds + 1) * kTicketStride;   // size of a ticket array
 constexpr int kRedMaxBlocks = 4096;                            // partials a last arriver can sum
 
-// block-wide sum of `acc`; the result is valid in thread 0
+// block-wide sum of `acc`; the result is valid in thread 0.  s: THREADS / 64 doubles of LDS scratch
 template <int THREADS>
-__device__ __forceinline__ double block_sum0(double acc)
+__device__ __forceinline__ double block_sum0_s(double acc, double* s)
 {
-   __shared__ double s[THREADS / 64];
    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
    __syncthreads();
@@ -31,14 +30,21 @@ __device__ __forceinline__ double block_sum0(double acc)
       for (int w = 0; w < THREADS / 64; w++) v += s[w];
    return v;
 }
+template <int THREADS>
+__device__ __forceinline__ double block_sum0(double acc)
+{
+   __shared__ double s[THREADS / 64];
+   return block_sum0_s<THREADS>(acc, s);
+}
 
 // thread 0 holds the block's partial `v`; returns true in every thread of the last arriving block,
 // with the fixed-order total in *total.  gridDim.x <= kRedMaxBlocks.  Leaves the tickets at zero.
+// s_last, s_red (THREADS / 64 doubles): LDS scratch
 template <int THREADS>
-__device__ bool grid_total(double v, double* __restrict__ part, unsigned int* __restrict__ ticket, double* total)
+__device__ bool grid_total_s(double v, double* __restrict__ part, unsigned int* __restrict__ ticket, double* total,
+                             int* s_last_p, double* s_red)
 {
-   __shared__ int s_last;
-   __shared__ double s_red[THREADS / 64];
+   int& s_last = *s_last_p;
    if (threadIdx.x == 0) {
       __hip_atomic_store(part + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -76,6 +82,13 @@ __device__ bool grid_total(double v, double* __restrict__ part, unsigned int* __
    if (threadIdx.x <= (unsigned)kRedXcds)
       __hip_atomic_store(ticket + threadIdx.x * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
    return true;
+}
+template <int THREADS>
+__device__ bool grid_total(double v, double* __restrict__ part, unsigned int* __restrict__ ticket, double* total)
+{
+   __shared__ int s_last;
+   __shared__ double s_red[THREADS / 64];
+   return grid_total_s<THREADS>(v, part, ticket, total, &s_last, s_red);
 }
 
 }  // namespace nfft4gp_amd

@@ -25,8 +25,11 @@ import numpy as np
 
 
 def row_range(n: int, rank: int, world: int) -> tuple[int, int]:
-    """Contiguous row block of `rank` (ceil-divided, the last ranks may get fewer or zero rows)."""
+    """Contiguous row block of `rank` (ceil-divided and rounded up to a multiple of 16, so every shard starts
+    at a multiple of 16 and its points keep their low 4 local-index bits -- and the sub-quantum offsets the layout
+    derives from them -- exactly as in the whole handle; the last ranks may get fewer or zero rows)."""
     per = (n + world - 1) // world
+    per = (per + 15) // 16 * 16
     return min(n, rank * per), min(n, (rank + 1) * per)
 
 

@@ -197,6 +197,11 @@ class NFFTAdditiveKernel:
                 "layout_bytes"]
         return dict(zip(keys, [int(v) for v in out]))
 
+    def set_deterministic(self, on: bool = True):
+        """Nfft4GPAmdSetDeterministic: bitwise reproducible 1-D matvecs (the default) or plain fp64 LDS atomics."""
+        if _lib.lib().Nfft4GPAmdSetDeterministic(self.h, int(bool(on))) != 0:
+            raise RuntimeError("Nfft4GPAmdSetDeterministic failed")
+
     def timing(self, enable: bool):
         _lib.lib().Nfft4GPAmdTimingEnable(self.h, int(enable))
 

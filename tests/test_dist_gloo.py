@@ -127,3 +127,4 @@ def test_row_range_covers_rows():
         rs = [row_range(n, r, w) for r in range(w)]
         assert rs[0][0] == 0 and rs[-1][1] == n
         assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+        assert all(a % 16 == 0 or a == n for a, _ in rs)  # shards start at multiples of 16 (slot_word)

@@ -37,6 +37,8 @@ def test_multi_matches_single(torch_cuda, nv, nw, dw, beta, n):
     torch.cuda.synchronize()
     rel = ((Y1 - Y2).norm(dim=1) / Y1.norm(dim=1)).max().item()
     assert rel < 1e-15, rel
+    if dw == 1:  # deterministic 1-D matvec (the default): the columns are the single-vector matvecs bit for bit
+        assert torch.equal(Y1, Y2)
     # host arrays and a short leading dimension are refused
     h = np.zeros(n)
     assert L.Nfft4GPAmdAdditiveMatSymvMulti(op.h, n, 1, 1.0, h.ctypes.data, n, 0.0, h.ctypes.data, n) != 0

@@ -1,5 +1,5 @@
 # Round 5: the GPU suite on the in-tree build, then tools/ab_lib.sh (in-tree build A against gpurun_ab/ build B)
-# and the spread's moment-table / window-group settings on the in-tree build.
+# and the spread's moment table, window groups and the deterministic mode on the in-tree build.
 #   bash tools/gpu_r5_ab.sh [skip-tests]
 set -o pipefail
 mkdir -p gpurun_out
@@ -8,4 +8,4 @@ if [ "$1" != "skip-tests" ]; then
   tail -2 gpurun_out/r5_pytest.log
 fi
 bash tools/ab_lib.sh 2>&1 | tee gpurun_out/r5_ab.txt || exit 1
-bash tools/ab_env.sh "NFFT4GP_AMD_SPREAD_VARIANT=0 NFFT4GP_AMD_SPREAD_VARIANT=2 NFFT4GP_AMD_CG=4" --steps 500 2>&1 | tee gpurun_out/r5_ab_env.txt
+bash tools/ab_env.sh "NFFT4GP_AMD_DET=1 NFFT4GP_AMD_DET=0 NFFT4GP_AMD_SPREAD_VARIANT=2,NFFT4GP_AMD_DET=0 NFFT4GP_AMD_CG=4,NFFT4GP_AMD_DET=0 NFFT4GP_AMD_CG=4" --steps 500 2>&1 | tee gpurun_out/r5_ab_env.txt
