@@ -919,16 +919,40 @@ namespace {
 void* afn_shard_setup_impl(const double* data, int n, int ldim, int d, int k, int perm_opt, const int* perm,
                            int schur_opt, int schur_lfil, int kernel, void* fkernel_params, int rb, int re, Comm* comm)
 {
-   if (!data || !fkernel_params || !comm || n <= 0 || ldim < n || d <= 0 || k <= 0 || k >= n || perm_opt < 0 ||
-       perm_opt > 2 || (perm_opt == 2 && !perm) || (schur_opt != 0 && schur_opt != 3) || rb < 0 || re > n || rb > re) {
-      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup needs data (ldim >= n), kernel parameters, a communicator, "
-                      "0 < k < n, perm_opt 0 / 1 / 2 (perm given), schur_opt 0 or 3 and rows within [0, n)\n");
+   if (!comm) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup needs a communicator\n");
       return nullptr;
    }
+   // Every rank reaches the same collectives: a failure on one rank (bad arguments, an allocation, a non-positive
+   // pivot of ITS Schur rows, ...) is agreed over the communicator at three points -- before the L11^{-1}
+   // broadcast, before the apply object is built, after it is built -- and then every rank returns NULL.
+   auto agree = [&](bool ok_here) -> bool {
+      double* d_flag = nullptr;
+      double flag = ok_here ? 0.0 : 1.0;
+      hipStream_t st = current_stream();
+      if (hipMalloc((void**)&d_flag, sizeof(double)) != hipSuccess) return false;  // cannot even vote: HIP is gone
+      bool ok = hipMemcpyAsync(d_flag, &flag, sizeof(double), hipMemcpyHostToDevice, st) == hipSuccess &&
+                comm->allreduce(d_flag, 1, st) == 0 &&
+                hipMemcpyAsync(&flag, d_flag, sizeof(double), hipMemcpyDeviceToHost, st) == hipSuccess &&
+                hipStreamSynchronize(st) == hipSuccess;
+      (void)hipFree(d_flag);
+      if (ok && flag != 0.0 && ok_here)
+         fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup: %d rank(s) failed; every rank returns NULL\n", (int)flag);
+      return ok && flag == 0.0;
+   };
+   const bool args_ok = data && fkernel_params && n > 0 && ldim >= n && d > 0 && k > 0 && k < n && perm_opt >= 0 &&
+                        perm_opt <= 2 && (perm_opt != 2 || perm) && (schur_opt == 0 || schur_opt == 3) && rb >= 0 &&
+                        re <= n && rb <= re;
+   if (!args_ok)
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup needs data (ldim >= n), kernel parameters, 0 < k < n, "
+                      "perm_opt 0 / 1 / 2 (perm given), schur_opt 0 or 3 and rows within [0, n)\n");
    KernelSpec K;
    double* dXk = nullptr;
-   const int additive = kernel_spec_of(fkernel_params, nullptr, kernel, n, K, &dXk);
-   if (additive < 0) return nullptr;
+   const int additive = args_ok ? kernel_spec_of(fkernel_params, nullptr, kernel, n, K, &dXk) : -1;
+   if (!agree(additive >= 0)) {
+      (void)hipFree(dXk);
+      return nullptr;
+   }
    const int D = additive ? (K.nw - 1) * K.dw + K.last_dw : d;
    hipStream_t s = current_stream();
    const int n2 = n - k;
@@ -949,50 +973,68 @@ void* afn_shard_setup_impl(const double* data, int n, int ldim, int d, int k, in
       for (void* p : {(void*)G, (void*)Gt, (void*)K12}) (void)hipFree(p);
       return nullptr;
    };
-   if (dalloc(&dX, (size_t)ldim * d)) return fail("allocation");
+   // phase A (replicated): the ordering, K11 + noise and its Cholesky / inverse
+   std::vector<int> hperm;
+   auto phase_a = [&]() -> const char* {
+   if (dalloc(&dX, (size_t)ldim * d)) return "allocation";
    const hipMemcpyKind kind = is_device_ptr(data) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-   if (hipMemcpy(dX, data, sizeof(double) * (size_t)ldim * d, kind) != hipSuccess) return fail("upload");
+   if (hipMemcpy(dX, data, sizeof(double) * (size_t)ldim * d, kind) != hipSuccess) return "upload";
    // the ordering is computed by every rank alike (afn.c:196-256): FPS is deterministic, a given perm is shared
-   std::vector<int> hperm(n);
+   hperm.resize(n);
    for (int i = 0; i < n; i++) hperm[i] = i;
    if (perm_opt == 1) {
       std::vector<int> sel(k);
       const int cnt = fps_device(dX, ldim, n, d, k, 0.0, sel.data(), nullptr, s);
-      if (cnt < 0) return fail("FPS");
+      if (cnt < 0) return "FPS";
       hperm = expand_perm(sel.data(), cnt, n);
    } else if (perm_opt == 2) {
       hperm.assign(perm, perm + n);
    }
    if (dalloc(&dperm, n) || hipMemcpy(dperm, hperm.data(), sizeof(int) * n, hipMemcpyHostToDevice) != hipSuccess ||
        dalloc(&Xp, (size_t)n * d))
-      return fail("allocation");
+      return "allocation";
    hipLaunchKernelGGL(k_gather_points, dim3((n + 255) / 256, d), dim3(256), 0, s, dX, (long long)ldim, n, d, dperm, Xp);
    if (additive) {
-      if (dalloc(&Xkp, (size_t)n * D)) return fail("allocation");
+      if (dalloc(&Xkp, (size_t)n * D)) return "allocation";
       hipLaunchKernelGGL(k_gather_points, dim3((n + 255) / 256, D), dim3(256), 0, s, dXk, (long long)n, n, D, dperm,
                          Xkp);
    }
+   return (const char*)nullptr;
+   };
+   const char* err = phase_a();
    const double* Xk = additive ? Xkp : Xp;  // kernel coordinates in the permuted order, ld n
    KernelSpec Kp = K;
    Kp.Xk = additive ? Xkp : nullptr;
    Kp.ldk = n;
    const KernelParams P = kernel_params_of(Kp, d);
    // A11 = K(X1) + noise, L11^{-1}: replicated; every rank keeps rank 0's factors (afn.c:425-428)
-   if (dalloc(&K11, kk) || dalloc(&G, kk) || dalloc(&Gt, kk) || dalloc(&dinfo, 1)) return fail("allocation");
-   hipLaunchKernelGGL(k_kmat, dim3((k + 255) / 256, k), dim3(256), 0, s, Xk, (long long)n, 0, k, 0, P, 1, K11,
-                      (long long)k);
-   const int info = chol_inverse_dev(K11, k, 0.0, G, Gt, dinfo, s);
-   if (info > 0) {
-      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup: K11 is not positive definite (column %d)\n", info);
-      return fail(nullptr);
+   if (!err && (dalloc(&K11, kk) || dalloc(&G, kk) || dalloc(&Gt, kk) || dalloc(&dinfo, 1))) err = "allocation";
+   int info = 0;
+   if (!err) {
+      hipLaunchKernelGGL(k_kmat, dim3((k + 255) / 256, k), dim3(256), 0, s, Xk, (long long)n, 0, k, 0, P, 1, K11,
+                         (long long)k);
+      info = chol_inverse_dev(K11, k, 0.0, G, Gt, dinfo, s);
+      if (info > 0) {
+         fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup: K11 is not positive definite (column %d)\n", info);
+         err = "";
+      } else if (info < 0) {
+         err = "Cholesky / triangular inverse of K11";
+      }
    }
-   if (info < 0) return fail("Cholesky / triangular inverse of K11");
+   if (err && *err) fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup: %s failed\n", err);
+   if (!agree(err == nullptr)) return fail(nullptr);
    if (comm->rank != 0 &&
        (hipMemsetAsync(G, 0, sizeof(double) * kk, s) != hipSuccess || hipMemsetAsync(Gt, 0, sizeof(double) * kk, s) != hipSuccess))
       return fail("broadcast");
    if (comm->allreduce(G, kk, s) || comm->allreduce(Gt, kk, s)) return fail("broadcast of L11^{-1}");
-   // this rank's landmarks and Schur points (the rows it holds, in the permuted order)
+   // phase B (this rank's rows): its landmarks and Schur points, K12 at those points, the Schur FSAI's rows
    std::vector<int> lm_idx, lm_row, nl_pos, nl_row;
+   std::vector<int> gia, gja;
+   std::vector<double> gaa;
+   auto phase_b = [&]() -> const char* {
+   // fault injection for the tests (tests/test_gpu_dist.py): this rank's rows fail as a local breakdown would
+   if (const char* e = getenv("NFFT4GP_AMD_FAULT_AFN_SHARD"))
+      if (atoi(e) != 0) return "the fault injected by NFFT4GP_AMD_FAULT_AFN_SHARD";
    for (int p = 0; p < n; p++) {
       const int row = hperm[p];
       if (row < rb || row >= re) continue;
@@ -1028,25 +1070,23 @@ void* afn_shard_setup_impl(const double* data, int n, int ldim, int d, int k, in
       return hipGetLastError() == hipSuccess ? 0 : -1;
    };
    // K12 at this rank's Schur points only (afn.c:436): k x m2 instead of k x (n - k)
-   if (dalloc(&K12, (size_t)k * std::max(1, m2)) || (m2 > 0 && panel(nl_pos, K12))) return fail("K12 panel");
-   std::vector<int> gia, gja;
-   std::vector<double> gaa;
+   if (dalloc(&K12, (size_t)k * std::max(1, m2)) || (m2 > 0 && panel(nl_pos, K12))) return "K12 panel";
    if (schur_opt == 3) {
       // FSAI of the Schur complement (afn.c:445-473) at this rank's rows: the KNN over their earlier points,
       // then the values in chunks of rows, each with W = L11^{-1} K12 formed for the columns it touches only
-      if (dalloc(&X2, (size_t)n2 * d)) return fail("allocation");
+      if (dalloc(&X2, (size_t)n2 * d)) return "allocation";
       for (int c = 0; c < d; c++)
          if (hipMemcpyAsync(X2 + (size_t)c * n2, Xp + (size_t)c * n + k, sizeof(double) * n2, hipMemcpyDeviceToDevice,
                             s) != hipSuccess)
-            return fail("copy");
-      if (fsai_pattern_rows(X2, n2, n2, d, schur_lfil, nl_pos, gia, gja, s)) return fail("Schur FSAI pattern");
+            return "copy";
+      if (fsai_pattern_rows(X2, n2, n2, d, schur_lfil, nl_pos, gia, gja, s)) return "Schur FSAI pattern";
       const size_t nnz = gja.size();
       gaa.assign(nnz, 0.0);
       if (nnz > 0) {
          if (dalloc(&dia, gia.size()) || dalloc(&dja, nnz) || dalloc(&daa, nnz) || dalloc(&dwcol, nnz) ||
              hipMemcpy(dia, gia.data(), sizeof(int) * gia.size(), hipMemcpyHostToDevice) != hipSuccess ||
              hipMemcpy(dja, gja.data(), sizeof(int) * nnz, hipMemcpyHostToDevice) != hipSuccess)
-            return fail("allocation");
+            return "allocation";
          KernelSpec K2 = Kp;
          K2.Xk = additive ? Xkp + k : nullptr;  // column c of the Schur points: Xkp + c n + k + i
          constexpr int kMaxCols = 65536;        // W columns per chunk (k x 64 Ki doubles: 256 MB at k = 512)
@@ -1079,25 +1119,32 @@ void* afn_shard_setup_impl(const double* data, int n, int ldim, int d, int k, in
                 hipMemcpy(dwcol + gia[r0], wcol.data(), sizeof(int) * wcol.size(), hipMemcpyHostToDevice) != hipSuccess ||
                 panel(U, Ku) || gemm_f64(false, k, (int)U.size(), k, G, k, Ku, k, Wu, k, s) ||
                 fsai_values_rows(K2, X2, n2, d, schur_lfil, dia + r0, dja, r1 - r0, Wu, k, dwcol, daa, s))
-               return fail("Schur FSAI values");
+               return "Schur FSAI values";
             r0 = r1;
          }
          if (hipMemcpyAsync(gaa.data(), daa, sizeof(double) * nnz, hipMemcpyDeviceToHost, s) != hipSuccess ||
              hipStreamSynchronize(s) != hipSuccess)
-            return fail("copy");
+            return "copy";
          if (!std::all_of(gaa.begin(), gaa.end(), [](double v) { return std::isfinite(v); })) {
-            fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup: the Schur complement's FSAI broke down (non-positive "
-                            "pivot)\n");
-            return fail(nullptr);
+            return "the Schur complement's FSAI (a non-positive pivot)";
          }
       }
    } else {
       gia.assign(m2 + 1, 0);
    }
+   return (const char*)nullptr;
+   };
+   err = phase_b();
+   if (err) fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnShardSetup: %s failed\n", err);
+   if (!agree(err == nullptr)) return fail(nullptr);
    release();
-   // the apply object takes G, Gt and K12
+   // the apply object takes G, Gt and K12 (and frees them if it fails)
    void* S = afn_shard_from_parts(re - rb, k, n2, comm, lm_idx, lm_row, nl_pos, nl_row, G, Gt, K12, schur_opt == 3,
                                   schur_opt == 0 ? 1.0 / K.mu : 0.0, gia, gja, gaa);
+   if (!agree(S != nullptr)) {
+      if (S) Nfft4GPAmdDistAfnFree(S);
+      return nullptr;
+   }
    return S;
 }
 }  // namespace

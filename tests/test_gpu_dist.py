@@ -128,6 +128,17 @@ def _worker(rank, world, port, outdir, backend):
                                 f"afn_{schur}_sit": it5, f"afn_{schur}_m2": inf["m2"],
                                 f"afn_{schur}_k12": inf["k12_doubles"], f"afn_{schur}_gnnz": inf["g_nnz"]})
                     ds_a.free()
+                # a failure on ONE rank's rows (a local Schur FSAI breakdown left the other rank in
+                # PCG's collectives): every rank must return NULL and none may wait forever
+                if rank == 1:
+                    os.environ["NFFT4GP_AMD_FAULT_AFN_SHARD"] = "1"
+                try:
+                    RowShardedAfn.setup(X, 64, comm, rb, re, perm_opt="perm", perm=perm, schur="fsai", schur_lfil=10,
+                                        op=full)
+                    out["afn_fault_raised"] = 0
+                except RuntimeError:
+                    out["afn_fault_raised"] = 1
+                os.environ.pop("NFFT4GP_AMD_FAULT_AFN_SHARD", None)
                 xs2 = torch.zeros_like(b)
                 _, rr2, _, it2 = amd.pcg(op, b, xs2, maxits=2000, tol=1e-6, precond=dn)
                 out.update({"nys_z": z.cpu().numpy(), "nys_x": xs2.cpu().numpy(), "nys_rr": rr2, "nys_it": it2})
@@ -318,6 +329,12 @@ def test_row_sharded_afn_setup(gloo2, single, schur):
     assert len(set(its)) == 1 and its[0] > 0
     assert abs(its[0] - it1) <= max(3, it1 // 20), (its, it1)
     assert rel(np.concatenate([r[f"afn_{schur}_sx"] for r in gloo2]), single[f"afn_{schur}_x"]) < 1e-4
+
+
+def test_row_sharded_afn_setup_failure_on_one_rank(gloo2):
+    """A breakdown on one rank's rows only (fault-injected on rank 1): the sharded setup agrees the failure over
+    the communicator, so BOTH ranks return NULL (and the worker went on to its next collectives)."""
+    assert [int(r["afn_fault_raised"]) for r in gloo2] == [1, 1]
 
 
 def test_row_sharded_nystrom_apply_and_pcg(gloo2, single):
