@@ -213,8 +213,9 @@ int Nfft4GPAmdPcgHistoryLength(void);
  * matops.c:274-346: one launch per basis vector), 1 block classical Gram-Schmidt (two launches per pass
  * whatever the step; a second pass when the first drops ||w|| below 0.7071 of its value, the DGKS test of
  * matops.c:348-440; the same projections up to rounding; kdim <= 2046), 2 delayed CGS2 (the second pass
- * of column j run with step j + 1's first pass: two basis sweeps and one host read per step; no
- * preconditioner -- with one, mode 1).  The block modes restart from the true residual norm (fgmres.c:236-243
+ * of column j run with step j + 1's first pass: two basis sweeps and one host read per step; with a
+ * preconditioner the provisional directions z_j^0 = M^-1 v_j^0 are kept and x is updated through the delayed
+ * pass's triangular recurrence).  The block modes restart from the true residual norm (fgmres.c:236-243
  * keeps the Givens estimate).  Env NFFT4GP_AMD_FGMRES_ORTHO.
  * Nfft4GPAmdFgmresSecondPasses: second passes taken since the last call (then reset). */
 void Nfft4GPAmdSetFgmresOrtho(int ortho);
@@ -473,10 +474,11 @@ int Nfft4GPAmdAdditiveLayoutInfo(void *str, long long *out, int nout);
  * Nfft4GPAmdTimingQuery writes total milliseconds and launch counts for the three kernels:
  * ms[0..2] = spread, grid, interp;  cnt[0..2] likewise.  Returns 0. */
 int Nfft4GPAmdTimingEnable(void *str, int enable);
-/* deterministic 1-D matvec (on by default): the spread's moment-table flushes and the interpolation's y adds are
- * rounded, before their LDS atomics, to a grid on which every partial sum is exact, so the result does not
- * depend on the order the waves add in -- two matvecs of one vector are bitwise equal, and so are two PCG runs.
- * Costs ~2^-45 relative rounding of each cell's moments and y value.  0 restores plain fp64 atomics. */
+/* deterministic 1-D matvec (off by default; env NFFT4GP_AMD_DET=1): the spread's moment-table flushes and the
+ * interpolation's y adds are rounded, before their LDS atomics, to a grid on which every partial sum is exact, so
+ * the result does not depend on the order the waves add in -- two matvecs of one vector are bitwise equal, and so
+ * are two PCG runs.  Costs ~2^-45 relative rounding of each cell's moments and y value, and ~11 % of the matvec
+ * at config C.  0: plain fp64 LDS atomics, reproducible to rounding. */
 int Nfft4GPAmdSetDeterministic(void *str, int on);
 int Nfft4GPAmdTimingQuery(void *str, double *ms, long long *cnt);
 /* average duration of ONE kernel of the additive matvec (which: 0 spread, 1 grid, 2 interp), measured

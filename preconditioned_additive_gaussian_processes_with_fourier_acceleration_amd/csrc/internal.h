@@ -196,7 +196,7 @@ struct AdditivePlan {
    int spread_variant = 0;  // 0: the spread; 1: the same with timeline stamps; 2: round-4 moment table (A/B)
    // deterministic 1-D matvec: the spread's moment flushes and the interpolation's y adds are rounded to a grid on
    // which every sum is exact, so results do not depend on the order of the LDS atomics (Nfft4GPAmdSetDeterministic)
-   bool det = true;
+   bool det = false;
    double* d_hb = nullptr;  // [vector 0, 1][H, Hd][nw] bounds of the interpolation polynomials (k_grid, det)
    int nparts = 0;          // partial grids per window the spread writes (one per block)
    DevLayout dl;

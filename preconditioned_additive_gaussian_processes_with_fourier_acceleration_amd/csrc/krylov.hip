@@ -403,10 +403,12 @@ __global__ __launch_bounds__(kKThreads) void k_dcgs2_update(double* __restrict__
    if (grid_total<kKThreads>(acc, part, ticket, &tot) && threadIdx.x == 0) *out = tot;
 }
 
-// a *= 1 / sqrt(*nrm2) (the provisional column's normalisation, without a host round trip)
+// a *= 1 / sqrt(*nrm2) (the provisional column's normalisation, without a host round trip).  A lucky breakdown
+// (u = 0 exactly, e.g. A = I) leaves the zero column as it is: 1 / sqrt(0) would fill it with NaN, and the host
+// finishes the Hessenberg column with H(j, j-1) = 0 (convergence)
 __global__ void k_scale_rnorm(double* __restrict__ a, size_t n, const double* __restrict__ nrm2)
 {
-   const double f = 1.0 / sqrt(*nrm2);
+   const double f = *nrm2 > 0.0 ? 1.0 / sqrt(*nrm2) : 0.0;
    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) a[i] *= f;
 }
 
@@ -619,7 +621,7 @@ int fgmres_ortho()
    return g_fgmres_ortho;
 }
 
-// ---- FGMRES with DCGS2 (ortho 2, no preconditioner) ----------------------------------------------------------
+// ---- FGMRES with DCGS2 (ortho 2) ------------------------------------------------------------------------------
 // The reference's FGMRES (fgmres.c:3-252: the same Givens recurrence, breakdown exit, restart and reporting)
 // with the Arnoldi basis orthogonalised by delayed CGS2 (Swirydowicz, Langou, Ananthan, Yang, Thomas 2020):
 // step j multiplies the provisional column v_j^0 = u_j / beta_j (once orthogonalised), then ONE sweep forms
@@ -630,6 +632,10 @@ int fgmres_ortho()
 // H(<j, j-1) += beta_j s, H(j, j-1) = beta_j alpha, so the Givens rotation and the residual of iteration j are
 // applied one step late (one extra operator application per cycle).  Mathematically CGS2 with a second pass at
 // every step; the basis is read twice per step instead of up to four times.
+// With a (flexible, right) preconditioner M (fgmres.c:140-146: z = M^-1 v, w = A z) the provisional column's
+// z_j^0 = M^-1 v_j^0 is kept, w = A z_j^0, and the finalised direction z_j = (z_j^0 - sum_{k<j} s_k z_k) / alpha
+// satisfies A z_j = (w - V H s) / alpha: the same Arnoldi relation, so V, H and the sweeps are unchanged.  z_j is
+// never formed: x += Z y is applied as Z^0 c, c from y by the triangular recurrence of the s and alpha (combine).
 int fgmres_dcgs2_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits, int atol, double tol,
                      double* prel_res, double** prel_res_v, int* piter, int print_level)
 {
@@ -655,21 +661,30 @@ int fgmres_dcgs2_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int 
       fprintf(stderr, "nfft4gp_amd: Nfft4GPSolverFgmres: restart dimension %d above %d\n", kdim, kmax);
       return -1;
    }
-   double* V = nullptr;
-   if (dmalloc(&V, n * (size_t)(kdim + 1))) return -1;
+   double *V = nullptr, *Z = nullptr;  // Z: the provisional directions z_j^0 = M^-1 v_j^0 (preconditioned only)
+   double* rel = nullptr;
    auto cleanup = [&]() {
       (void)hipStreamSynchronize(c.s);
       (void)hipFree(V);
+      (void)hipFree(Z);
    };
+   // every error exit: the basis, Z and the history are released
+   auto fail = [&]() -> int {
+      free(rel);
+      rel = nullptr;
+      cleanup();
+      return -1;
+   };
+   if (dmalloc(&V, n * (size_t)(kdim + 1)) || (cb.prec && dmalloc(&Z, n * (size_t)(kdim + 1)))) return fail();
    // Hr: the unrotated Hessenberg (the Arnoldi relation), H: the rotated one (fgmres.c's H)
    std::vector<double> Hr((size_t)kdim * (kdim + 1), 0.0), H((size_t)kdim * (kdim + 1), 0.0), cs(kdim), sn(kdim),
        rs(kdim + 1);
+   // the delayed second pass of each column (s_j, alpha_j): the recurrence from y to Z^0's coefficients
+   std::vector<std::vector<double>> spass(kdim + 1);
+   std::vector<double> alph(kdim + 1, 1.0), ccoef;
    double* v = V;
    c.copy(v, rhs);
-   if (cb.apply(-1.0, x, 1.0, v)) {
-      cleanup();
-      return -1;
-   }
+   if (cb.apply(-1.0, x, 1.0, v)) return fail();
    double normr = c.norm(v);
    if (normr < EPS) {
       *prel_res = 0.0;
@@ -679,7 +694,7 @@ int fgmres_dcgs2_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int 
       return 0;
    }
    const double tolr = atol ? tol : tol * normb;
-   double* rel = rel_hist(maxits + 1);
+   rel = rel_hist(maxits + 1);
    rel[0] = normr / normb;
    int iter = 0, i = 0;
    if (print_level > 0) {
@@ -693,11 +708,7 @@ int fgmres_dcgs2_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int 
    double* dsc = g_k.scal;  // device scalars of step j (m = j + 1): [0, 2m) the sweep, [2m] ||u_j||^2
    std::vector<double> hh, coef;
    bool broke = false, converged = false;
-   if (2 * (kdim + 1) + 1 > KScratch::kScal) {
-      cleanup();
-      free(rel);
-      return -1;
-   }
+   if (2 * (kdim + 1) + 1 > KScratch::kScal) return fail();
    while (iter < maxits) {
       rs[0] = normr;
       c.scale(V, nullptr, 1.0 / normr);
@@ -708,15 +719,18 @@ int fgmres_dcgs2_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int 
          const bool more = j < kdim && iter + (j > 0 ? 1 : 0) < maxits;  // will column j get a first pass?
          double* vj = V + (size_t)j * n;
          double* w = V + (size_t)(j + 1) * n;
-         if (more && cb.apply(1.0, vj, 0.0, w)) {
-            free(rel);
-            cleanup();
-            return -1;
+         if (more) {
+            if (cb.prec) {
+               double* zj = Z + (size_t)j * n;  // z_j^0 = M^-1 v_j^0, w = A z_j^0
+               if (cb.solve(zj, vj) || cb.apply(1.0, zj, 0.0, w)) return fail();
+            } else if (cb.apply(1.0, vj, 0.0, w)) {
+               return fail();
+            }
          }
          const int m = j + 1;
          hh.assign(2 * m + 1, 0.0);
-         if (c.dots_ab(vj, more ? w : nullptr, V, m, dsc)) return -1;
-         if (c.read(dsc, 2 * m + 1, hh.data())) return -1;  // (T is stale when !more)
+         if (c.dots_ab(vj, more ? w : nullptr, V, m, dsc)) return fail();
+         if (c.read(dsc, 2 * m + 1, hh.data())) return fail();  // (T is stale when !more)
          if (j > 0) beta = std::sqrt(hh[2 * m]);
          // the delayed second pass of column j: s = hh[0, j), omega = hh[j]
          double alpha = 1.0, ss = 0.0;
@@ -724,6 +738,8 @@ int fgmres_dcgs2_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int 
             for (int k = 0; k < j; k++) ss += hh[k] * hh[k];
             const double a2 = hh[j] - ss;
             alpha = a2 > 0.0 ? std::sqrt(a2) : std::sqrt(hh[j]);
+            spass[j].assign(hh.begin(), hh.begin() + j);
+            alph[j] = alpha;
             // column j - 1 of H is final: H(<j, j-1) += beta s, H(j, j-1) = beta alpha
             double* Hrc = Hr.data() + (size_t)(j - 1) * (kdim + 1);
             for (int k = 0; k < j; k++) Hrc[k] += beta * hh[k];
@@ -780,7 +796,7 @@ int fgmres_dcgs2_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int 
          }
          coef[2 * j] = vjw / alpha;
          coef[2 * j + 1] = 1.0 / alpha;
-         if (c.dcgs2_update(V, w, j, coef, dsc + 2 * (m + 1))) return -1;  // ||u_{j+1}||^2 where step j + 1 reads it
+         if (c.dcgs2_update(V, w, j, coef, dsc + 2 * (m + 1))) return fail();  // ||u_{j+1}||^2 where step j + 1 reads it
       }
       if (broke) break;
       if (print_level == 0)
@@ -792,7 +808,18 @@ int fgmres_dcgs2_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int 
             for (int q = k + 1; q < i; q++) rs[k] -= H[(size_t)q * (kdim + 1) + k] * rs[q];
             rs[k] /= H[(size_t)k * (kdim + 1) + k];
          }
-         if (c.combine(x, V, i, rs.data())) return -1;
+         if (!cb.prec) {
+            if (c.combine(x, V, i, rs.data())) return fail();
+         } else {
+            // x += sum_j y_j z_j with z_j = (z_j^0 - sum_{k<j} s_jk z_k) / alpha_j: from the last column down,
+            // c_j = y_j / alpha_j moves -c_j s_jk onto z_k's coefficient
+            ccoef.assign(rs.begin(), rs.begin() + i);
+            for (int q = i - 1; q >= 0; q--) {
+               ccoef[q] /= alph[q];
+               for (int k = 0; k < q && k < (int)spass[q].size(); k++) ccoef[k] -= ccoef[q] * spass[q][k];
+            }
+            if (c.combine(x, Z, i, ccoef.data())) return fail();
+         }
       }
       if (converged || normr <= tolr) break;
       // restart (fgmres.c:236-243): v = rhs - A x through w.  The reference keeps the Givens estimate as the
@@ -800,11 +827,7 @@ int fgmres_dcgs2_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int 
       // orthogonalisations assume an orthonormal basis, so they restart from the true norm (one dot)
       double* w = V + n;
       c.copy(V, rhs);
-      if (cb.apply(1.0, x, 0.0, w)) {
-         free(rel);
-         cleanup();
-         return -1;
-      }
+      if (cb.apply(1.0, x, 0.0, w)) return fail();
       hipLaunchKernelGGL(k_sub, dim3(egrid(n)), dim3(256), 0, c.s, V, V, w, n);
       normr = c.norm(V);
    }
@@ -837,7 +860,7 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
       return 0;
    }
    const int ortho = fgmres_ortho();
-   if (ortho == 2 && !cb.prec)
+   if (ortho == 2)
       return fgmres_dcgs2_dev(cb, x, rhs, kdim, maxits, atol, tol, prel_res, prel_res_v, piter, print_level);
    const int kmax = ortho ? KScratch::kScal / 2 - 2 : KScratch::kScal - 2;
    if (kdim > kmax) {
@@ -852,13 +875,18 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
       (void)hipFree(V);
       (void)hipFree(Z);
    };
+   double* rel = nullptr;
+   // every error exit: the bases and the history are released
+   auto fail = [&]() -> int {
+      free(rel);
+      rel = nullptr;
+      cleanup();
+      return -1;
+   };
    std::vector<double> H((size_t)kdim * (kdim + 1), 0.0), cs(kdim), sn(kdim), rs(kdim + 1);
    double* v = V;
    c.copy(v, rhs);
-   if (cb.apply(-1.0, x, 1.0, v)) {
-      cleanup();
-      return -1;
-   }
+   if (cb.apply(-1.0, x, 1.0, v)) return fail();
    double normr = c.norm(v);
    if (normr < EPS) {
       *prel_res = 0.0;
@@ -868,7 +896,7 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
       return 0;
    }
    const double tolr = atol ? tol : tol * normb;
-   double* rel = rel_hist(maxits + 1);
+   rel = rel_hist(maxits + 1);
    rel[0] = normr / normb;
    int iter = 0, i = 0;
    double* w = V;
@@ -892,17 +920,9 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
          w = V + (size_t)i * n;
          if (cb.prec) {
             double* z = Z + (size_t)(i - 1) * n;
-            if (cb.solve(z, v) || cb.apply(1.0, z, 0.0, w)) {
-               free(rel);
-               cleanup();
-               return -1;
-            }
+            if (cb.solve(z, v) || cb.apply(1.0, z, 0.0, w)) return fail();
          } else {
-            if (cb.apply(1.0, v, 0.0, w)) {
-               free(rel);
-               cleanup();
-               return -1;
-            }
+            if (cb.apply(1.0, v, 0.0, w)) return fail();
          }
          double* hd = g_k.scal;
          std::vector<double> hcol(i + 1);
@@ -910,15 +930,15 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
             // Nfft4GPModifiedGS (matops.c:274-346) with k = i-1, no re-orthogonalisation
             for (int j = 0; j < i; j++)
                if (c.gs(w, j ? V + (size_t)(j - 1) * n : nullptr, j ? hd + j - 1 : nullptr, V + (size_t)j * n, hd + j))
-                  return -1;
-            if (c.gs(w, V + (size_t)(i - 1) * n, hd + i - 1, nullptr, hd + i)) return -1;
-            if (c.read(hd, i + 1, hcol.data())) return -1;
+                  return fail();
+            if (c.gs(w, V + (size_t)(i - 1) * n, hd + i - 1, nullptr, hd + i)) return fail();
+            if (c.read(hd, i + 1, hcol.data())) return fail();
          } else {
             // classical passes h = V^T w, w -= V h; a second one only when the first dropped ||w|| below 0.7071
             // of its value before it (the DGKS test of the reference's MGS2, matops.c:348-440); H(:, i) = the
             // sum of the passes' projections, ||w|| after the last
             std::vector<double> hh(2 * i + 4);
-            if (c.block_cgs2(w, V, i, hd) || c.read(hd, 2 * i + 4, hh.data())) return -1;
+            if (c.block_cgs2(w, V, i, hd) || c.read(hd, 2 * i + 4, hh.data())) return fail();
             for (int j = 0; j < i; j++) hcol[j] = hh[j];
             hcol[i] = hh[i];
             if (hh[2 * i + 3] != 0.0) {
@@ -963,16 +983,12 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
          for (int j = k + 1; j < i; j++) rs[k] -= H[(size_t)j * (kdim + 1) + k] * rs[j];
          rs[k] /= H[(size_t)k * (kdim + 1) + k];
       }
-      if (c.combine(x, cb.prec ? Z : V, i, rs.data())) return -1;
+      if (c.combine(x, cb.prec ? Z : V, i, rs.data())) return fail();
       if (normr <= tolr) break;
       // restart (fgmres.c:236-243): v = rhs - A x through w; normr keeps the Givens estimate
       v = V;
       c.copy(v, rhs);
-      if (cb.apply(1.0, x, 0.0, w)) {
-         free(rel);
-         cleanup();
-         return -1;
-      }
+      if (cb.apply(1.0, x, 0.0, w)) return fail();
       hipLaunchKernelGGL(k_sub, dim3(egrid(n)), dim3(256), 0, c.s, v, v, w, n);
       if (ortho) normr = c.norm(v);  // block CGS2: restart from the true norm (see fgmres_dcgs2_dev)
    }

@@ -511,12 +511,13 @@ int default_block(int n)
 void env_layout(AdditivePlan& P)
 {
    P.B = default_block(P.n);
-   // windows per spread workgroup: at most 3 (three workgroups per CU fit the LDS), spread evenly over the
-   // fewest groups -- 4 windows as 2 + 2 instead of 3 + 1 (a one-window workgroup pays the whole alpha staging
-   // and fold): 22.3 against 24.2 us per rank of BASELINE configs[3]'s component split
-   // (profiles/r04_component_cg_sweep.txt)
+   // windows per spread workgroup: at most 4 (with the [window][degree][cell] moment table three 4-window
+   // workgroups of a 4064-point block fit a CU's LDS: config C's spread 40.8 -> 38.7 us, the matvec 78.9 -> 78.4,
+   // profiles/r05_spread_ab.txt), spread evenly over the fewest groups -- a one-window workgroup pays the whole
+   // alpha staging and fold (round 4: 4 windows as 2 + 2 took 22.3 against 24.2 us as 3 + 1 per rank of
+   // BASELINE configs[3]'s component split, profiles/r04_component_cg_sweep.txt)
    {
-      const int ngroups = (std::max(P.nw, 1) + 2) / 3;
+      const int ngroups = (std::max(P.nw, 1) + 3) / 4;
       P.CG = (std::max(P.nw, 1) + ngroups - 1) / ngroups;
    }
    if (const char* e = getenv("NFFT4GP_AMD_BLOCK")) {

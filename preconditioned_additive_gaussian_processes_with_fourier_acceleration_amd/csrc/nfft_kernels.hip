@@ -162,31 +162,34 @@ __device__ __forceinline__ double det_grid(uint32_t bexp)  // 1.5 x 2^(bexp - 10
 }
 __device__ __forceinline__ double det_round(double v, double C) { return (v + C) - C; }
 
-// the biased exponent field of max |x[base .. base + nloc)| (hi words; exact in any order), the same in every
-// thread of the workgroup; s_red: nwaves words of LDS.  Published by the caller's barrier (det_max_finish after it)
+// The biased exponent field of max |alpha| over the block's staged slice (hi words: exact in any order), without a
+// second barrier: after the staging barrier each wave takes the max of its eighth of the LDS slice, publishes it in
+// s_red[wave] and counts itself in s_red[nwaves] (release); a wave reads the total only before its first flush
+// (det_max_wait: acquire-spin, normally satisfied at once -- every wave published before it computed a run).
 template <int THREADS>
-__device__ __forceinline__ void det_max_start(const double* __restrict__ x, int base, int nloc, uint32_t* s_red)
+__device__ __forceinline__ void det_max_publish(const double* s_alpha, int nloc, uint32_t* s_red)
 {
-   const uint32_t* xw = reinterpret_cast<const uint32_t*>(x + base);
+   constexpr int nwaves = THREADS / 64;
+   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+   const int per = (nloc + nwaves - 1) / nwaves;
+   const uint32_t* hw = reinterpret_cast<const uint32_t*>(s_alpha);
    uint32_t m = 0;
-   constexpr int kMaxPer = (kMaxBlock + THREADS - 1) / THREADS;
-   uint32_t v[kMaxPer];
-#pragma unroll
-   for (int k = 0; k < kMaxPer; k++) {
-      const int e = threadIdx.x + k * THREADS;
-      v[k] = e < nloc ? xw[2 * e + 1] & 0x7FFFFFFFu : 0u;
-   }
-#pragma unroll
-   for (int k = 0; k < kMaxPer; k++) m = max(m, v[k]);
+   for (int e = wave * per + lane; e < min(nloc, (wave + 1) * per); e += 64) m = max(m, hw[2 * e + 1] & 0x7FFFFFFFu);
    for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
-   if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = m;
+   if (lane == 0) {
+      s_red[wave] = m;
+      __hip_atomic_fetch_add(s_red + nwaves, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+   }
 }
 template <int THREADS>
-__device__ __forceinline__ uint32_t det_max_finish(const uint32_t* s_red)
+__device__ __forceinline__ uint32_t det_max_wait(uint32_t* s_red)
 {
+   constexpr int nwaves = THREADS / 64;
+   while (__hip_atomic_load(s_red + nwaves, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)nwaves)
+      __builtin_amdgcn_s_sleep(1);
    uint32_t m = 0;
 #pragma unroll
-   for (int w = 0; w < THREADS / 64; w++) m = max(m, s_red[w]);
+   for (int w = 0; w < nwaves; w++) m = max(m, s_red[w]);
    return (uint32_t)__builtin_amdgcn_readfirstlane((int)m) >> 20;
 }
 
@@ -237,16 +240,17 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
    const int base = b * B;
    stage_block_glds<THREADS>(s_alpha, x, base, min(B, n - base), B);
-   if (DET) det_max_start<THREADS>(x, base, min(B, n - base), s_red);
    for (int i = tid; i < CG * mom_doubles_per_window<MOMT>(); i += THREADS) s_mom[i] = 0.0;
+   if (DET && tid == 0) s_red[nwaves] = 0u;
    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces have landed
    __syncthreads();
    if (TIMELINE) stamp(1);
-   uint32_t bC0 = 0;  // DET: biased exponent of C_0 (C_d: + 31 d)
+   // DET: biased exponent of C_0 (C_d: + 31 d), known before the wave's first flush
+   uint32_t bC0 = 0, lcm = 0;
    if (DET) {
+      det_max_publish<THREADS>(s_alpha, min(B, n - base), s_red);
       const int cm = cmax[b * ngroups + g];
-      const uint32_t lc = cm > 1 ? 32u - (uint32_t)__clz(cm - 1) : 0u;
-      bC0 = det_max_finish<THREADS>(s_red) + max(lc, 6u) + 1u;
+      lcm = max(cm > 1 ? 32u - (uint32_t)__clz(cm - 1) : 0u, 6u) + 1u;
    }
 
    const int c0 = g * CG;
@@ -268,6 +272,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
       const int comp_local = (int)(cur.mt >> 6) - c0;
       const int cell = (int)(cur.mt & 63u);
       double* dst = s_mom + mom_index<MOMT>(comp_local, cell, 0);
+      if (DET && bC0 == 0) bC0 = det_max_wait<THREADS>(s_red) + lcm;
 #pragma unroll
       for (int d = 0; d < kNC; d++) {
          const double a = DET ? det_round(acc[d], det_grid(bC0 + 31u * d)) : acc[d];
@@ -815,7 +820,7 @@ static int spread_momt(const AdditivePlan& P) { return P.spread_variant == 2 ? 0
 static size_t spread_lds_bytes(const AdditivePlan& P)
 {
    const size_t per = spread_momt(P) ? mom_doubles_per_window<1>() : mom_doubles_per_window<0>();
-   return sizeof(double) * ((size_t)P.B + kPad + (size_t)P.CG * per) + (P.det ? 4 * (512 / 64) : 0);  // DET: a word per wave (kSpreadThreads)
+   return sizeof(double) * ((size_t)P.B + kPad + (size_t)P.CG * per) + (P.det ? 64 : 0);  // DET: a word per wave (kSpreadThreads / 64) and a counter
 }
 
 // the fused dot's reduction scratch after the y slices: 2 x (1024 / 64) doubles and an int

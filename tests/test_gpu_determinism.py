@@ -1,4 +1,4 @@
-"""The deterministic 1-D matvec (Nfft4GPAmdSetDeterministic, nfft_kernels.hip DET): at
+"""The deterministic 1-D matvec (opt-in Nfft4GPAmdSetDeterministic, nfft_kernels.hip DET): at
 BASELINE configs[2] (config C: n = 1e6, 32 additive 1-D windows) two matvecs, two gradient matvecs and two PCG
 solves of the same input are bitwise equal, so the PCG iteration count is one number, not a range.  The reference
 adds its components in a fixed order (SRC/external/nfft_interface.c:807-811); here the spread's moment-table
@@ -21,6 +21,7 @@ def config_c_op(torch_cuda):
     x = rng.random(n) - 0.5
     op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
     assert op.setup(amd.GAUSSIAN, f=1.0, l=0.1, mu=0.01) == 0
+    op.set_deterministic(True)
     yield op, torch_cuda.tensor(x, device="cuda")
     op.free()
 

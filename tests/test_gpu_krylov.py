@@ -249,3 +249,58 @@ def test_fgmres_block_orthogonalisation_matches_mgs(torch_cuda, ortho, kdim, max
         # the history's tail sits at 1e-8 relative residual, where a 1e-16 rounding difference is 1e-8 relative
         np.testing.assert_allclose(res[1][2], res[0][2], rtol=1e-8, atol=1e-14)
     op.free()
+
+
+def test_fgmres_dcgs2_preconditioned_matches_mgs(torch_cuda, case):
+    """Delayed CGS2 with a preconditioner (flexible, the provisional directions
+    z_j^0 = M^-1 v_j^0 kept and x updated through the delayed pass's recurrence) against the reference's MGS
+    with the same Nystrom preconditioner on the "fgn" case: the same iterations, history to 1e-8, x to 1e-9."""
+    torch = torch_cuda
+    z, k, op = case
+    pre = amd.NystromPrecond(z["nys_U"], z["nys_s"], float(z["nys_eta"]), z["nys_perm"])
+    b = torch.tensor(np.asarray(z["b"]), device="cuda")
+    res = []
+    for o in (0, 2):
+        amd.lib().Nfft4GPAmdSetFgmresOrtho(o)
+        x = torch.zeros(op.n, dtype=torch.float64, device="cuda")
+        x, rr, hist, it = amd.fgmres(op, b, x, kdim=100, maxits=400, tol=1e-8, precond=pre)
+        res.append((x.cpu().numpy(), rr, hist[:it + 1], it))
+    amd.lib().Nfft4GPAmdSetFgmresOrtho(0)
+    pre.free()
+    assert res[0][3] == res[1][3] > 0, (res[0][3], res[1][3])
+    np.testing.assert_allclose(res[1][2], res[0][2], rtol=1e-8, atol=1e-14)
+    assert np.linalg.norm(res[1][0] - res[0][0]) <= 1e-9 * np.linalg.norm(res[0][0])
+
+
+class HostScaledIdentity:
+    """y = alpha c x + beta y on host vectors: A = c I, whose first Arnoldi step is a lucky breakdown."""
+
+    def __init__(self, n, c):
+        self.n, self.h = n, None
+
+        def mv(_m, nn, alpha, xp, beta, yp):
+            xv = np.ctypeslib.as_array(C.cast(xp, _lib.dp), shape=(nn,))
+            yv = np.ctypeslib.as_array(C.cast(yp, _lib.dp), shape=(nn,))
+            yv[:] = alpha * c * xv + (beta * yv if beta != 0.0 else 0.0)
+            return 0
+
+        self._cb = _lib.SYMMATVEC(mv)
+        self.matvec_fnptr = C.cast(self._cb, C.c_void_p).value
+
+
+@pytest.mark.parametrize("ortho", [0, 1, 2])
+def test_fgmres_lucky_breakdown(torch_cuda, ortho):
+    """A = I: after one step the new Arnoldi vector is exactly zero.  Every orthogonalisation
+    finishes with H(1, 0) = 0 -- converged in one iteration with x = b -- and none divides by that zero norm."""
+    torch = torch_cuda
+    n = 5000
+    op = HostScaledIdentity(n, 1.0)
+    b = torch.tensor(np.random.default_rng(3).random(n) - 0.5, device="cuda")
+    amd.lib().Nfft4GPAmdSetFgmresOrtho(ortho)
+    x = torch.zeros(n, dtype=torch.float64, device="cuda")
+    x, rr, hist, it = amd.fgmres(op, b, x, kdim=10, maxits=10, tol=1e-10)
+    amd.lib().Nfft4GPAmdSetFgmresOrtho(0)
+    xv = x.cpu().numpy()
+    assert np.all(np.isfinite(xv)) and np.isfinite(rr)
+    assert it == 1 and rr <= 1e-10, (it, rr)
+    assert rel(xv, b.cpu().numpy()) <= 1e-14

@@ -26,6 +26,8 @@ def test_multi_matches_single(torch_cuda, nv, nw, dw, beta, n):
     X = np.asfortranarray(rng.random((n, d)))
     op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), nw, dw)
     assert op.setup(amd.GAUSSIAN, f=1.1, l=0.3, mu=0.02) == 0
+    if dw == 1:
+        op.set_deterministic(True)  # the columns are then compared bit for bit below
     V = torch.tensor(rng.random((nv, n)) - 0.5, device="cuda")
     Y0 = torch.tensor(rng.random((nv, n)), device="cuda")
     Y1 = Y0.clone()
@@ -37,7 +39,7 @@ def test_multi_matches_single(torch_cuda, nv, nw, dw, beta, n):
     torch.cuda.synchronize()
     rel = ((Y1 - Y2).norm(dim=1) / Y1.norm(dim=1)).max().item()
     assert rel < 1e-15, rel
-    if dw == 1:  # deterministic 1-D matvec (the default): the columns are the single-vector matvecs bit for bit
+    if dw == 1:  # the deterministic 1-D matvec: the columns are the single-vector matvecs bit for bit
         assert torch.equal(Y1, Y2)
     # host arrays and a short leading dimension are refused
     h = np.zeros(n)
