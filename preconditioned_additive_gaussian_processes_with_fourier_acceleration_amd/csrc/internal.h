@@ -6,8 +6,9 @@
 //   with B the 2m+2 = 10-tap Kaiser-Bessel spreading matrix onto a 64-cell periodic grid and F the
 //   32-mode DFT.  For one component the middle factor is a real 64x64 circulant W (only Re f is used,
 //   nfft_interface.c:436) and each tap is an entire function of the point's offset u in its cell.
-//   We write the 10 taps as degree-9 polynomials in u (max error 2.5e-10 of the window peak, below
-//   the KB window's own 5e-8 truncation; degree 11 would give 8e-13 at 20 % more VALU work), so
+//   We write the 10 taps as degree-7 polynomials in u (max error 3.8e-8 of the window peak, the KB window's own
+//   truncation level; the band-limited circulant filters the error's high-frequency content, so against the
+//   oracle the matvec moves by at most 1.4x the coordinate quantisation's error: DESIGN 3.1), so
 //     spread : M[cell][d] = sum_{j in cell} alpha_j u_j^d        (per-cell moments)
 //              g[(cell-4+t) mod 64] += sum_d C[t][d] M[cell][d]
 //     grid   : h = W g,   H[cell][d] = sum_t h[(cell-4+t) mod 64] C[t][d]
@@ -33,7 +34,7 @@ constexpr int kNos = 64;            // oversampled grid n_os (nfft_interface.c:2
 constexpr int kBand = 32;           // bandwidth N (nfft_interface.c:18)
 constexpr int kM = 4;               // window cutoff m (nfft_interface.c:20)
 constexpr int kTaps = 2 * kM + 2;   // PRE_PSI taps per dim
-constexpr int kDeg = 9;             // tap polynomial degree
+constexpr int kDeg = 7;             // tap polynomial degree (round 5: 9 -> 7)
 constexpr int kNC = kDeg + 1;       // coefficients per cell
 constexpr int kR = 16;              // points per lane-run (chunk)
 constexpr int kWave = 64;

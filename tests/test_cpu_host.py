@@ -68,7 +68,7 @@ def test_tap_polynomials_match_window():
         approx = np.polynomial.polynomial.polyval(u, Cm[t])
         err = max(err, np.max(np.abs(exact - approx)) / peak)
     # Chebyshev-node interpolation error of the degree-(NC-1) tap polynomials (window.cpp)
-    bound = {12: 1e-12, 10: 5e-10}[Cm.shape[1]]
+    bound = {12: 1e-12, 10: 5e-10, 8: 5e-8}[Cm.shape[1]]
     assert err < bound, err
 
 

@@ -88,7 +88,8 @@ def test_emulated_kernels_match_golden(name, pre, kernel, l):
     E.setup(kernel, float(z["f"]), l, float(z["mu"]))
     x = z["x"]
     n = x.size
-    # design error of the product path: degree-9 tap polynomials (2.5e-10 of the window peak) and
+    # design error of the product path: degree-7 tap polynomials (3.8e-8 of the window peak, mostly filtered by the
+    # band-limited circulant) and
     # 2^-26-cell fixed-point coordinates, amplified by the high modes of a short length scale
     # (9e-10 at l = 0.1); the north-star bar is 1e-6
     assert rel(E.matsymv(x), z[pre + "_nfft_y"]) < 1e-8

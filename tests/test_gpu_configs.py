@@ -3,7 +3,7 @@
 * config C (BASELINE configs[2]: n = 1e6, 32 additive 1-D windows) against the oracle at full size,
   l in {1, 0.1}.  The oracle's C/OpenMP restatement takes about a second per matvec on the box's host.
 * TEST1's length-scale sweep goes down to l = 0.01 (TESTS/TEST1/foo.ipynb: logspace(-2, 2, 20)); the
-  product's degree-9 tap polynomials and 2^-26-cell fixed-point offsets are amplified by the high modes
+  product's degree-7 tap polynomials and 2^-26-cell fixed-point offsets are amplified by the high modes
   there.  l in {0.01, 0.03} on the committed fixtures' points (foo1d: TEST2's data, synth1d, bike3d:
   TEST1's bike windows) against the oracle.  Contract 1e-6 (north star); the CPU emulation of the same
   layout measured <= 7e-9, so the tests also assert 5e-8 for 1-D windows.

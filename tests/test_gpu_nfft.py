@@ -2,7 +2,7 @@
 
 Tolerance (north star, BASELINE.json): the matvec matches the reference to <= 1e-6 relative.
 The HIP path stores node coordinates as 32-bit fixed point (error <= 2^-33 after the reference's
-scaling) and the window taps as degree-9 polynomials (2.5e-10 of the window peak); measured
+scaling) and the window taps as degree-7 polynomials (3.8e-8 of the window peak); measured
 deviations are ~1e-10, so the tests also assert a tighter 1e-8 where the length scale is not tiny.
 """
 import numpy as np
