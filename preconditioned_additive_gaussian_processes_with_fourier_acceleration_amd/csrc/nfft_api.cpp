@@ -516,9 +516,17 @@ void env_layout(AdditivePlan& P)
    // profiles/r05_spread_ab.txt), spread evenly over the fewest groups -- a one-window workgroup pays the whole
    // alpha staging and fold (round 4: 4 windows as 2 + 2 took 22.3 against 24.2 us as 3 + 1 per rank of
    // BASELINE configs[3]'s component split, profiles/r04_component_cg_sweep.txt)
+   // ... unless that leaves fewer than 384 spread workgroups (1.5 per CU): then at most 3 per group, as in round 4
+   // (BASELINE configs[3]'s component shard, 4 windows x 247 blocks: one 4-window group is 247 workgroups, 23.3 us
+   // per rank against 22.3 us as 2 + 2, profiles/r05_mid_shard_components8.json)
    {
-      const int ngroups = (std::max(P.nw, 1) + 3) / 4;
-      P.CG = (std::max(P.nw, 1) + ngroups - 1) / ngroups;
+      const int nw = std::max(P.nw, 1), nblocks = std::max(1, (P.n + P.B - 1) / P.B);
+      auto pick = [&](int cgmax) {
+         const int ngroups = (nw + cgmax - 1) / cgmax;
+         P.CG = (nw + ngroups - 1) / ngroups;
+         return ngroups;
+      };
+      if ((long long)pick(4) * nblocks < 384) pick(3);
    }
    if (const char* e = getenv("NFFT4GP_AMD_BLOCK")) {
       const int v = atoi(e);

@@ -885,7 +885,12 @@ constexpr int kInterp2Threads = 1024;
 typedef void (*Interp2Fn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, size_t,
                           const double*, const double*, double*, double*, int, int, int, double, double, double, double,
                           const double*, int);
-static Interp2Fn interp2_fn(bool det) { return det ? k_interp2<kInterp2Threads, true> : k_interp2<kInterp2Threads, false>; }
+// 512-thread workgroups at >= 512 blocks, as the single-vector interpolation (launch_interp)
+static Interp2Fn interp2_fn(bool det, bool small)
+{
+   if (small) return det ? k_interp2<512, true> : k_interp2<512, false>;
+   return det ? k_interp2<kInterp2Threads, true> : k_interp2<kInterp2Threads, false>;
+}
 
 // a kernel whose dynamic slice is addressed absolutely (lds_at) must have no static LDS
 static bool static_lds_zero(const void* fn)
@@ -903,8 +908,8 @@ static std::vector<const void*> interp_kernels()
       for (int d = 0; d < 2; d++)
          for (int sm = 0; sm < 2; sm++)
             for (int det = 0; det < 2; det++) v.push_back((const void*)interp_fn(g, d && !g, sm, det));
-   v.push_back((const void*)interp2_fn(false));
-   v.push_back((const void*)interp2_fn(true));
+   for (int det = 0; det < 2; det++)
+      for (int sm = 0; sm < 2; sm++) v.push_back((const void*)interp2_fn(det, sm));
    return v;
 }
 
@@ -1064,7 +1069,12 @@ int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double
                       (const double*)P.d_w, (const double*)P.d_wd, P.d_H2, P.d_Hd, 0, 0, (long long)part_rs,
                       (long long)h_rs, P.det ? P.d_hb : (double*)nullptr);
    const size_t lds_i = sizeof(double) * 2 * ((size_t)P.B + kPad);
-   hipLaunchKernelGGL(interp2_fn(P.det), dim3(P.nblocks), dim3(kInterp2Threads), lds_i, stream, P.dl.meta, P.dl.lo,
+   // 1024 threads: 512-thread workgroups at config E's 2461 blocks measured the same loss (1.700 s either way,
+   // profiles/r05_interp2_ab.txt); NFFT4GP_AMD_INTERP2_THREADS=512 selects them
+   static const int forced = getenv("NFFT4GP_AMD_INTERP2_THREADS") ? atoi(getenv("NFFT4GP_AMD_INTERP2_THREADS")) : 0;
+   const bool small = forced == 512;
+   hipLaunchKernelGGL(interp2_fn(P.det, small), dim3(P.nblocks), dim3(small ? 512 : kInterp2Threads), lds_i, stream,
+                      P.dl.meta, P.dl.lo,
                       P.dl.q, P.dl.tile_off, (const double*)P.d_H2, h_rs, x0, x1, y0, y1, P.n, P.B, P.ngroups, alpha,
                       beta, P.f, P.mu * P.diag, (const double*)P.d_hb, P.nw);
    NFFT4GP_HIP_CHECK(hipGetLastError());
