@@ -480,6 +480,14 @@ int Nfft4GPAmdTimingEnable(void *str, int enable);
  * are two PCG runs.  Costs ~2^-45 relative rounding of each cell's moments and y value, and ~11 % of the matvec
  * at config C.  0: plain fp64 LDS atomics, reproducible to rounding. */
 int Nfft4GPAmdSetDeterministic(void *str, int on);
+/* 32-bit precision mode of a 1-D additive handle (bits 32; 64 = the default), the analogue of the reference's
+ * NFFT4GP_USING_FLOAT32 (SRC/utils/utils.h:28-31) for BASELINE configs[4]: each (point, window) is ONE 32-bit
+ * record -- the offset in the cell to 2^-21 of a cell (2^-27 of the period, finer than an fp32 coordinate) with the
+ * 12-bit local index in its low bits -- instead of 5 bytes, a fifth fewer bytes per pass; the arithmetic stays fp64.
+ * Matches the reference to ~1e-7 (tests/test_gpu_precision.py; the fp64 default to ~1e-9).  The layout is rebuilt
+ * (and the kernel re-set up) when called after the first setup; env NFFT4GP_AMD_PRECISION=32.  Multi-feature
+ * windows are unaffected. */
+int Nfft4GPAmdSetPrecision(void *str, int bits);
 int Nfft4GPAmdTimingQuery(void *str, double *ms, long long *cnt);
 /* average duration of ONE kernel of the additive matvec (which: 0 spread, 1 grid, 2 interp), measured
  * with a single hipEvent pair around `reps` back-to-back launches on the library stream (per-launch
@@ -631,9 +639,15 @@ NFFT4GP_DOUBLE Nfft4GPAmdHostPrepare(const NFFT4GP_DOUBLE *col, int n, unsigned 
  * in the cell in bits 0-25, local index bits 6-11 in bits 26-31), nblocks*ngroups+1 (tile_off) */
 int Nfft4GPAmdHostLayout(const unsigned int *qc, int n, int nw, int B, int CG, long long *counts,
                          unsigned short *meta, unsigned int *lo, unsigned int *q, int *tile_off);
+/* the same for either record (rec 5: the default, as above; rec 4: Nfft4GPAmdSetPrecision 32 -- no lo array,
+ * q = the in-cell offset with the 12-bit local index in its low bits) */
+int Nfft4GPAmdHostLayoutRec(const unsigned int *qc, int n, int nw, int B, int CG, int rec, long long *counts,
+                            unsigned short *meta, unsigned int *lo, unsigned int *q, int *tile_off);
 /* The same layout built on the GPU (layout_gpu.hip, what the operator's setup uses): identical arrays. */
 int Nfft4GPAmdDeviceLayout(const unsigned int *qc, int n, int nw, int B, int CG, long long *counts,
                            unsigned short *meta, unsigned int *lo, unsigned int *q, int *tile_off);
+int Nfft4GPAmdDeviceLayoutRec(const unsigned int *qc, int n, int nw, int B, int CG, int rec, long long *counts,
+                              unsigned short *meta, unsigned int *lo, unsigned int *q, int *tile_off);
 /* the Nystrom setup's host k x k steps: symmetric eigensolve (dsyev 'V' semantics: ascending w,
  * eigenvectors as the columns of V, column-major) and L^{-1} of the lower Cholesky factor of A + shift I
  * (returns 0, or the failing column + 1 if A + shift I is not positive definite) */

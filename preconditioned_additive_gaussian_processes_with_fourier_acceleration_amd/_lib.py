@@ -168,6 +168,7 @@ _SIGS = {
     "Nfft4GPAmdCommFree": (None, [vp]),
     "Nfft4GPAmdCommRanks": (C.c_int, [vp]),
     "Nfft4GPAmdSetDeterministic": (C.c_int, [vp, C.c_int]),
+    "Nfft4GPAmdSetPrecision": (C.c_int, [vp, C.c_int]),
     "Nfft4GPAmdDistTimingEnable": (C.c_int, [vp, C.c_int]),
     "Nfft4GPAmdDistTimingQuery": (C.c_int, [vp, dp, C.POINTER(C.c_longlong)]),
     "Nfft4GPAmdAdditiveComponentShard": (C.c_int, [vp, C.c_int, C.c_int]),
@@ -203,6 +204,10 @@ _SIGS = {
                                        vp, vp]),
     "Nfft4GPAmdDeviceLayout": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_longlong), vp, vp,
                                          vp, vp]),
+    "Nfft4GPAmdHostLayoutRec": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_longlong),
+                                          vp, vp, vp, vp]),
+    "Nfft4GPAmdDeviceLayoutRec": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                            C.POINTER(C.c_longlong), vp, vp, vp, vp]),
 }
 
 _lib = None

@@ -105,12 +105,26 @@ __host__ __device__ inline uint32_t slot_word(uint32_t loc, uint32_t frac)
    return ((lo4 >= 8u && e != 0u) ? e - 16u + lo4 : e + lo4) ^ 0x80000000u;
 }
 __host__ __device__ inline uint32_t lo_byte(uint32_t loc) { return (loc >> 4) & 255u; }
+// The 4-byte record of the 32-bit precision mode (Nfft4GPAmdSetPrecision(h, 32), the analogue of the reference's
+// NFFT4GP_USING_FLOAT32, SRC/utils/utils.h:28-31): ONE word per (point, window) holding the whole 12-bit local
+// index in its low bits -- the offset in the cell is e moved to the nearest value congruent to loc mod 4096, so
+// |move| <= 2048 units of 2^-32 of a cell (2^-21 of a cell, 2^-27 of the period: finer than an fp32 coordinate)
+__host__ __device__ inline uint32_t slot_word4(uint32_t loc, uint32_t frac)
+{
+   const uint32_t e = (frac & 0x3FFFFFFu) << 6, L = loc & 4095u;
+   const uint32_t v = (e & ~4095u) | L;  // the candidate in e's 4096-unit window; e's low 6 bits are zero
+   const int32_t dv = (int32_t)(v - e);  // in (-4096, 4096)
+   const uint32_t down = (dv > 2048 && v >= 4096u) ? 4096u : 0u;
+   const uint32_t up = (dv < -2048 && v <= 0xFFFFEFFFu) ? 4096u : 0u;
+   return (v - down + up) ^ 0x80000000u;
+}
 
 struct Layout {
    int n = 0;           // local points
    int nw = 0;          // components
    int B = kMaxBlock;   // block size (points)
    int CG = 8;          // components per spread group
+   int rec = 5;         // bytes per (point, window): 5 (slot_word + lo byte) or 4 (slot_word4, no lo array)
    int ngroups = 0;
    int nblocks = 0;
    long long ntiles = 0;
@@ -121,11 +135,11 @@ struct Layout {
    std::vector<int> cmax;          // [nblocks*ngroups] the most points any one (window, cell) of (b, g) holds
 };
 // build from per-component quantized coordinates qc[c*n + j]
-void build_layout(const uint32_t* qc, int n, int nw, int B, int CG, Layout& L);
+void build_layout(const uint32_t* qc, int n, int nw, int B, int CG, Layout& L, int rec = 5);
 struct AdditivePlan;
 // the same layout from device-resident coordinates into P.dl / P.ngroups / P.nblocks (layout_gpu.hip); -1
 // when a (block, group) exceeds the emit kernel's LDS
-int build_layout_dev(const uint32_t* d_qc, int n, int nw, int B, int CG, AdditivePlan& P, hipStream_t s);
+int build_layout_dev(const uint32_t* d_qc, int n, int nw, int B, int CG, AdditivePlan& P, hipStream_t s, int rec = 5);
 
 // ---- device plan --------------------------------------------------------------------------------
 struct DevLayout {
@@ -194,6 +208,7 @@ struct AdditivePlan {
    double diag = 1.0;    // 1: this handle adds the mu x (and grad f^2 x) terms; 0: a component shard without them
    // layout
    int B = kMaxBlock, CG = 3, ngroups = 0, nblocks = 0;  // CG = 3: 3 spread workgroups fit a CU's LDS
+   int rec = 5;  // layout record: 5 bytes per (point, window) (fp64 default) or 4 (Nfft4GPAmdSetPrecision 32)
    int spread_variant = 0;  // 0: the spread; 1: the same with timeline stamps; 2: round-4 moment table (A/B)
    // deterministic 1-D matvec: the spread's moment flushes and the interpolation's y adds are rounded to a grid on
    // which every sum is exact, so results do not depend on the order of the LDS atomics (Nfft4GPAmdSetDeterministic)

@@ -21,6 +21,7 @@
 //             signed int32: s = (int)q = 2^32 (offset - 1/2), one conversion for the centred offset scaled by 2^32
 //             (the 2^-32d are folded into the tap polynomial coefficients); carrying 4 index bits moves a point by
 //             at most an eighth of the coordinates' 2^-26-of-a-cell quantum.
+//   rec 4 (32-bit precision mode): no lo array; q = slot_word4 (internal.h), the 12-bit index in the low bits.
 //   tile_off[b*ngroups + g] = first tile of (b, g); the spread kernel gets one workgroup per (b, g),
 //   the interpolation kernel one workgroup per b (all groups).
 #include <algorithm>
@@ -80,7 +81,7 @@ void balance_tile(uint32_t (*loc)[kR], uint32_t (*fr)[kR])
 // sorted order -- different cells -- and their LDS flushes do not collide on one address.
 long long emit_block_group(const uint32_t* qc, int n, int nw, int B, int CG, int b, int g,
                            const ChunkSink* out, long long t0, long long T, std::vector<int>& cnt,
-                           std::vector<int>& off, std::vector<uint16_t>& sorted, int* cmax = nullptr)
+                           std::vector<int>& off, std::vector<uint16_t>& sorted, int* cmax = nullptr, int rec = 5)
 {
    const int base = b * B;
    const int nloc = std::min(B, n - base);
@@ -136,8 +137,12 @@ long long emit_block_group(const uint32_t* qc, int n, int nw, int B, int CG, int
          auto* F = reinterpret_cast<uint32_t(*)[kR]>(sfr.data() + (size_t)tile * kWave * kR);
          balance_tile(L, F);
          for (int lane = 0; lane < kWave; lane++) {
-            for (int r4 = 0; r4 < kR / 4; r4++) out->lo[quad_index(t0 + tile, r4, lane, kR / 4)] = lo_word(L[lane] + 4 * r4);
-            for (int r = 0; r < kR; r++) out->q[quad_index(t0 + tile, r, lane, kR)] = slot_word(L[lane][r], F[lane][r]);
+            if (rec == 5)
+               for (int r4 = 0; r4 < kR / 4; r4++)
+                  out->lo[quad_index(t0 + tile, r4, lane, kR / 4)] = lo_word(L[lane] + 4 * r4);
+            for (int r = 0; r < kR; r++)
+               out->q[quad_index(t0 + tile, r, lane, kR)] =
+                   rec == 5 ? slot_word(L[lane][r], F[lane][r]) : slot_word4(L[lane][r], F[lane][r]);
          }
       }
    }
@@ -159,7 +164,7 @@ void parallel_for(int nitems, F&& f)
 
 }  // namespace
 
-void build_layout(const uint32_t* qc, int n, int nw, int B, int CG, Layout& L)
+void build_layout(const uint32_t* qc, int n, int nw, int B, int CG, Layout& L, int rec)
 {
    L.n = n;
    L.nw = nw;
@@ -186,7 +191,7 @@ void build_layout(const uint32_t* qc, int n, int nw, int B, int CG, Layout& L)
    L.tile_off[nbg] = (int)acc;
    L.ntiles = acc;
    L.meta.resize((size_t)acc * kWave);  // every element is written below (emit_block_group)
-   L.lo.resize((size_t)acc * (kR / 4) * kWave);
+   L.lo.resize(rec == 5 ? (size_t)acc * (kR / 4) * kWave : 0);
    L.q.resize((size_t)acc * kR * kWave);
    ChunkSink sink{L.meta.data(), L.lo.data(), L.q.data()};
    parallel_for(L.nblocks, [&](int b) {
@@ -194,7 +199,8 @@ void build_layout(const uint32_t* qc, int n, int nw, int B, int CG, Layout& L)
       std::vector<uint16_t> sorted(B);
       for (int g = 0; g < L.ngroups; g++)
          emit_block_group(qc, n, nw, B, CG, b, g, &sink, L.tile_off[b * L.ngroups + g],
-                          L.tile_off[b * L.ngroups + g + 1] - L.tile_off[b * L.ngroups + g], cnt, off, sorted);
+                          L.tile_off[b * L.ngroups + g + 1] - L.tile_off[b * L.ngroups + g], cnt, off, sorted,
+                          nullptr, rec);
    });
 }
 

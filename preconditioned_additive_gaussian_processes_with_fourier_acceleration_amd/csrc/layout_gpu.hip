@@ -87,6 +87,7 @@ struct EmitLds {
    }
 };
 
+template <int REC>
 __global__ __launch_bounds__(kLT) void k_lay_emit(const uint32_t* __restrict__ qc, int n, int nw, int B, int CG,
                                                   int ngroups, int Tmax, const int* __restrict__ tile_off,
                                                   uint16_t* __restrict__ meta, uint32_t* __restrict__ lo,
@@ -236,8 +237,9 @@ __global__ __launch_bounds__(kLT) void k_lay_emit(const uint32_t* __restrict__ q
    for (int i = tid; i < T * kWave * kR; i += kLT) {
       const int tile = i / (kWave * kR), ln = (i / kR) % kWave, r = i % kR;
       const uint32_t loc = s_loc[i];
-      q[quad_index(t0 + tile, r, ln, kR)] = slot_word(loc, s_fr[i]);
+      q[quad_index(t0 + tile, r, ln, kR)] = REC == 5 ? slot_word(loc, s_fr[i]) : slot_word4(loc, s_fr[i]);
    }
+   if (REC != 5) return;
    for (int i = tid; i < T * kWave * (kR / 4); i += kLT) {
       const int tile = i / (kWave * (kR / 4)), ln = (i / (kR / 4)) % kWave, r4 = i % (kR / 4);
       const uint16_t* l4 = s_loc + ((size_t)tile * kWave + ln) * kR + 4 * r4;
@@ -251,7 +253,7 @@ __global__ __launch_bounds__(kLT) void k_lay_emit(const uint32_t* __restrict__ q
 // the layout of the device-resident quantised coordinates d_qc ([window][point] u32) into P.dl and
 // P.ngroups / P.nblocks; -1 when a (block, group) would not fit the emit kernel's LDS (the caller then
 // builds on the host)
-int build_layout_dev(const uint32_t* d_qc, int n, int nw, int B, int CG, AdditivePlan& P, hipStream_t s)
+int build_layout_dev(const uint32_t* d_qc, int n, int nw, int B, int CG, AdditivePlan& P, hipStream_t s, int rec)
 {
    const int ngroups = (nw + CG - 1) / CG, nblocks = (n + B - 1) / B, nbg = ngroups * nblocks;
    const int Tmax_bound = (CG * (B / kR + kNos) + kWave - 1) / kWave + 1;
@@ -290,40 +292,52 @@ int build_layout_dev(const uint32_t* d_qc, int n, int nw, int B, int CG, Additiv
    NFFT4GP_HIP_CHECK(hipMemcpyAsync(P.dl.tile_off, toff.data(), sizeof(int) * (nbg + 1), hipMemcpyHostToDevice, s));
    const size_t nt = (size_t)std::max<long long>(acc, 1);
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.dl.meta, sizeof(uint16_t) * nt * kWave));
-   NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.dl.lo, sizeof(uint32_t) * nt * (kR / 4) * kWave));
+   if (rec == 5) NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.dl.lo, sizeof(uint32_t) * nt * (kR / 4) * kWave));
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.dl.q, sizeof(uint32_t) * nt * kR * kWave));
    const size_t lds = EmitLds(CG, B, Tmax).total;
    static const bool attr = []() {
-      (void)hipFuncSetAttribute((const void*)k_lay_emit, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_lay_emit<5>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_lay_emit<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipGetLastError();
       return true;
    }();
    (void)attr;
    if (nbg > 0)
-      hipLaunchKernelGGL(k_lay_emit, dim3(nbg), dim3(kLT), lds, s, d_qc, n, nw, B, CG, ngroups, Tmax, P.dl.tile_off,
-                         P.dl.meta, P.dl.lo, P.dl.q);
+      hipLaunchKernelGGL(rec == 5 ? k_lay_emit<5> : k_lay_emit<4>, dim3(nbg), dim3(kLT), lds, s, d_qc, n, nw, B, CG,
+                         ngroups, Tmax, P.dl.tile_off, P.dl.meta, P.dl.lo, P.dl.q);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
    (void)hipFree(d_tiles);
    P.dl.ntiles = acc;
-   P.dl.bytes = (size_t)acc * kWave * (2 + 4 * (kR / 4) + 4 * kR) + sizeof(int) * (nbg + 1);
+   P.dl.bytes = (size_t)acc * kWave * (2 + (rec == 5 ? 4 * (kR / 4) : 0) + 4 * kR) + sizeof(int) * (nbg + 1);
    return 0;
 }
 
 }  // namespace nfft4gp_amd
 
+extern "C" int Nfft4GPAmdDeviceLayoutRec(const unsigned int* qc, int n, int nw, int B, int CG, int rec,
+                                         long long* counts, unsigned short* meta, unsigned int* lo, unsigned int* q,
+                                         int* tile_off);
 extern "C" int Nfft4GPAmdDeviceLayout(const unsigned int* qc, int n, int nw, int B, int CG, long long* counts,
                                       unsigned short* meta, unsigned int* lo, unsigned int* q, int* tile_off)
 {
+   return Nfft4GPAmdDeviceLayoutRec(qc, n, nw, B, CG, 5, counts, meta, lo, q, tile_off);
+}
+
+extern "C" int Nfft4GPAmdDeviceLayoutRec(const unsigned int* qc, int n, int nw, int B, int CG, int rec,
+                                         long long* counts, unsigned short* meta, unsigned int* lo, unsigned int* q,
+                                         int* tile_off)
+{
    using namespace nfft4gp_amd;
-   if (B <= 0 || B > kMaxBlock || CG <= 0 || n < 0 || nw <= 0 || nw > 1023 || !counts) return -1;
+   if (B <= 0 || B > kMaxBlock || CG <= 0 || n < 0 || nw <= 0 || nw > 1023 || !counts || (rec != 4 && rec != 5))
+      return -1;
    if (!need_device("Nfft4GPAmdDeviceLayout")) return -1;
    hipStream_t s = current_stream();
    uint32_t* d_qc = nullptr;
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&d_qc, sizeof(uint32_t) * std::max<size_t>(1, (size_t)n * nw)));
    NFFT4GP_HIP_CHECK(hipMemcpy(d_qc, qc, sizeof(uint32_t) * (size_t)n * nw, hipMemcpyHostToDevice));
    AdditivePlan P;
-   const int rc = build_layout_dev(d_qc, n, nw, B, CG, P, s);
+   const int rc = build_layout_dev(d_qc, n, nw, B, CG, P, s, rec);
    (void)hipFree(d_qc);
    if (rc) return -1;
    const int nbg = P.ngroups * P.nblocks;
@@ -333,7 +347,8 @@ extern "C" int Nfft4GPAmdDeviceLayout(const unsigned int* qc, int n, int nw, int
    const size_t nt = (size_t)P.dl.ntiles;
    int err = 0;
    if (meta && hipMemcpy(meta, P.dl.meta, sizeof(uint16_t) * nt * kWave, hipMemcpyDeviceToHost) != hipSuccess) err = 1;
-   if (lo && hipMemcpy(lo, P.dl.lo, sizeof(uint32_t) * nt * (kR / 4) * kWave, hipMemcpyDeviceToHost) != hipSuccess)
+   if (lo && rec == 5 &&
+       hipMemcpy(lo, P.dl.lo, sizeof(uint32_t) * nt * (kR / 4) * kWave, hipMemcpyDeviceToHost) != hipSuccess)
       err = 1;
    if (q && hipMemcpy(q, P.dl.q, sizeof(uint32_t) * nt * kR * kWave, hipMemcpyDeviceToHost) != hipSuccess) err = 1;
    if (tile_off && hipMemcpy(tile_off, P.dl.tile_off, sizeof(int) * (nbg + 1), hipMemcpyDeviceToHost) != hipSuccess)

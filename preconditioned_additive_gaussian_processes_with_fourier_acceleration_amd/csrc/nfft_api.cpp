@@ -285,12 +285,12 @@ int plan_build_points(AdditivePlan& P, const double* buffer)
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&d_qc, sizeof(uint32_t) * std::max<size_t>(1, qc.size())));
    NFFT4GP_HIP_CHECK(hipMemcpyAsync(d_qc, qc.data(), sizeof(uint32_t) * qc.size(), hipMemcpyHostToDevice, s));
    const auto t2 = std::chrono::steady_clock::now();
-   const int rc_dev = build_layout_dev(d_qc, P.n, P.nw, P.B, P.CG, P, s);
+   const int rc_dev = build_layout_dev(d_qc, P.n, P.nw, P.B, P.CG, P, s, P.rec);
    (void)hipStreamSynchronize(s);
    (void)hipFree(d_qc);
    if (rc_dev) {
       Layout L;
-      build_layout(qc.data(), P.n, P.nw, P.B, P.CG, L);
+      build_layout(qc.data(), P.n, P.nw, P.B, P.CG, L, P.rec);
       P.ngroups = L.ngroups;
       P.nblocks = L.nblocks;
       free_layout(P);
@@ -538,6 +538,7 @@ void env_layout(AdditivePlan& P)
    }
    if (const char* e = getenv("NFFT4GP_AMD_SPREAD_VARIANT")) P.spread_variant = atoi(e);
    if (const char* e = getenv("NFFT4GP_AMD_DET")) P.det = atoi(e) != 0;
+   if (const char* e = getenv("NFFT4GP_AMD_PRECISION")) P.rec = atoi(e) == 32 ? 4 : 5;
 }
 
 void* additive_create(double* data, int n_global, int ldim, int* windows, int nwindows, int dwindows, int rb, int re)
@@ -833,6 +834,26 @@ int Nfft4GPAmdAdditiveLayoutInfo(void* str, long long* out, int nout)
    return 0;
 }
 
+int Nfft4GPAmdSetPrecision(void* str, int bits)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || (bits != 32 && bits != 64)) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdSetPrecision needs an additive handle and bits 32 or 64\n");
+      return -1;
+   }
+   AdditivePlan& P = E->P;
+   const int rec = bits == 32 ? 4 : 5;
+   if (rec == P.rec) return 0;
+   (void)hipStreamSynchronize(current_stream());
+   P.rec = rec;
+   if (!P.points_ready || P.md.on) return 0;  // multi-feature windows keep their fp64 coordinates
+   // the layout is rebuilt from the handle's points, and the kernel's coefficients with it
+   const double* buffer = ((nfft4gp_kernel*)str)->_buffer;
+   P.points_ready = false;
+   if (plan_build_points(P, buffer)) return -1;
+   return plan_setup(P, buffer, P.kernel, P.f, P.l, P.mu);
+}
+
 int Nfft4GPAmdSetDeterministic(void* str, int on)
 {
    PlanExt* E = additive_plan(str);
@@ -1062,14 +1083,20 @@ double Nfft4GPAmdHostPrepare(const double* col, int n, unsigned int* q)
 int Nfft4GPAmdHostLayout(const unsigned int* qc, int n, int nw, int B, int CG, long long* counts,
                          unsigned short* meta, unsigned int* lo, unsigned int* q, int* tile_off)
 {
-   if (B <= 0 || B > kMaxBlock || CG <= 0 || n < 0 || nw <= 0 || nw > 1023) return -1;
+   return Nfft4GPAmdHostLayoutRec(qc, n, nw, B, CG, 5, counts, meta, lo, q, tile_off);
+}
+
+int Nfft4GPAmdHostLayoutRec(const unsigned int* qc, int n, int nw, int B, int CG, int rec, long long* counts,
+                            unsigned short* meta, unsigned int* lo, unsigned int* q, int* tile_off)
+{
+   if (B <= 0 || B > kMaxBlock || CG <= 0 || n < 0 || nw <= 0 || nw > 1023 || (rec != 4 && rec != 5)) return -1;
    Layout L;
-   build_layout(qc, n, nw, B, CG, L);
+   build_layout(qc, n, nw, B, CG, L, rec);
    counts[0] = L.ntiles;
    counts[1] = L.ngroups;
    counts[2] = L.nblocks;
    if (meta) memcpy(meta, L.meta.data(), L.meta.size() * sizeof(uint16_t));
-   if (lo) memcpy(lo, L.lo.data(), L.lo.size() * sizeof(uint32_t));
+   if (lo && !L.lo.empty()) memcpy(lo, L.lo.data(), L.lo.size() * sizeof(uint32_t));
    if (q) memcpy(q, L.q.data(), L.q.size() * sizeof(uint32_t));
    if (tile_off) memcpy(tile_off, L.tile_off.data(), L.tile_off.size() * sizeof(int));
    return 0;

@@ -74,6 +74,8 @@ struct TileRegs {
    uint32_t qq[kR];      // slot_word (internal.h): offset in the cell, bit 31 flipped; bits 0-3 = local index bits 0-3
 };
 
+// REC: the layout's record (AdditivePlan::rec): 5 bytes (q word + lo byte) or 4 (slot_word4: no lo array)
+template <int REC = 5>
 __device__ __forceinline__ void load_tile(TileRegs& T, const uint16_t* __restrict__ meta,
                                           const uint32_t* __restrict__ lo, const uint32_t* __restrict__ qarr,
                                           int t, int lane)
@@ -83,7 +85,7 @@ __device__ __forceinline__ void load_tile(TileRegs& T, const uint16_t* __restric
    const uint4* l4 = reinterpret_cast<const uint4*>(lo) + (size_t)t * (kR / 16) * 64 + lane;
    const uint4* q4 = reinterpret_cast<const uint4*>(qarr) + (size_t)t * (kR / 4) * 64 + lane;
 #pragma unroll
-   for (int k = 0; k < kR / 16; k++) {
+   for (int k = 0; k < (REC == 5 ? kR / 16 : 0); k++) {
       const uint4 v = l4[k * 64];
       T.lo[4 * k + 0] = v.x;
       T.lo[4 * k + 1] = v.y;
@@ -102,8 +104,10 @@ __device__ __forceinline__ void load_tile(TileRegs& T, const uint16_t* __restric
 
 // byte offset of point r's entry in a block's LDS slice of doubles: 8 x the local index (0..B-1, or B + lane % 32
 // for a dummy slot), whose bits 4-11 are the lo byte and bits 0-3 the low bits of the q word
+template <int REC = 5>
 __device__ __forceinline__ uint32_t slot_off(const TileRegs& T, int r)
 {
+   if (REC == 4) return (T.qq[r] << 3) & 0x7FF8u;  // slot_word4: the whole index in bits 0-11
    // v_lshlrev_b32_sdwa (the byte, shifted) + v_lshlrev_b32 + v_and_or_b32: left to itself the compiler adds the
    // two fields and the slice's LDS base 0 with an extra v_and + v_add3
    const uint32_t hi = ((T.lo[r >> 2] >> (8 * (r & 3))) & 255u) << 7;
@@ -205,7 +209,7 @@ __device__ __forceinline__ uint32_t det_interp_exp(const double* __restrict__ hb
 }
 
 // at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
-template <int THREADS, bool TIMELINE = false, int MOMT = 1, bool DET = false>
+template <int THREADS, bool TIMELINE = false, int MOMT = 1, bool DET = false, int REC = 5>
 __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restrict__ meta,
                                                       const uint32_t* __restrict__ lo,
                                                       const uint32_t* __restrict__ qarr,
@@ -237,7 +241,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    TileRegs cur;
    const int t1 = tile_off[b * ngroups + g + 1];
    int t = tile_off[b * ngroups + g] + wave;
-   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
+   if (t < t1) load_tile<REC>(cur, meta, lo, qarr, t, lane);
    const int base = b * B;
    stage_block_glds<THREADS>(s_alpha, x, base, min(B, n - base), B);
    for (int i = tid; i < CG * mom_doubles_per_window<MOMT>(); i += THREADS) s_mom[i] = 0.0;
@@ -261,7 +265,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
 #pragma unroll
       for (int r = 0; r < kR; r++) {
          const double u = q_to_s(cur.qq[r]);
-         double tpow = *lds_at(slot_off(cur, r));  // s_alpha is the first dynamic slice
+         double tpow = *lds_at(slot_off<REC>(cur, r));  // s_alpha is the first dynamic slice
          acc[0] += tpow;
 #pragma unroll
          for (int d = 1; d < kNC; d++) {
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
          const double a = DET ? det_round(acc[d], det_grid(bC0 + 31u * d)) : acc[d];
          atomicAdd(dst + mom_index<MOMT>(0, 0, d), a);  // ds_add_f64
       }
-      if (t + nwaves < t1) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
+      if (t + nwaves < t1) load_tile<REC>(cur, meta, lo, qarr, t + nwaves, lane);
    }
    __syncthreads();
    if (TIMELINE) stamp(2);
@@ -475,7 +479,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_sum_yinit(const double* _
    grid_tail(comp, s_g, wv, ct, H, s_w, s_h);
 }
 
-template <int THREADS>
+template <int THREADS, int REC = 5>
 __global__ __launch_bounds__(THREADS) void k_interp_part(const uint16_t* __restrict__ meta,
                                                         const uint32_t* __restrict__ lo,
                                                         const uint32_t* __restrict__ qarr,
@@ -494,7 +498,7 @@ __global__ __launch_bounds__(THREADS) void k_interp_part(const uint16_t* __restr
    const int t1 = tile_off[b * ngroups + g1];
    int t = tile_off[b * ngroups + g0] + wave;
    TileRegs cur;
-   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
+   if (t < t1) load_tile<REC>(cur, meta, lo, qarr, t, lane);
    for (int i = tid; i < B + kPad; i += THREADS) s_y[i] = 0.0;
    __syncthreads();
    for (; t < t1; t += nwaves) {
@@ -508,7 +512,7 @@ __global__ __launch_bounds__(THREADS) void k_interp_part(const uint16_t* __restr
       }
 #pragma unroll
       for (int r = 0; r < kR; r++) {
-         const uint32_t off = slot_off(cur, r);
+         const uint32_t off = slot_off<REC>(cur, r);
          const double u = q_to_s(cur.qq[r]);
          double v = hc[kNC - 1];
 #pragma unroll
@@ -516,7 +520,7 @@ __global__ __launch_bounds__(THREADS) void k_interp_part(const uint16_t* __restr
          lds_add(off, v);  // s_y is the first dynamic slice
       }
       const int tn = t + nwaves;
-      if (tn < t1) load_tile(cur, meta, lo, qarr, tn, lane);
+      if (tn < t1) load_tile<REC>(cur, meta, lo, qarr, tn, lane);
    }
    __syncthreads();
    for (int j = tid; j < nloc; j += THREADS) atomicAdd(y + (size_t)base + j, scale * s_y[j]);
@@ -564,7 +568,7 @@ constexpr int kEpMax = 8;  // epilogue values per thread held in registers (B <=
 // DOT (non-GRAD only): also forms (y_out, x) -- the (q, p) of a CG step when y = A p -- with a
 // deterministic grid-wide sum written to *dot_out by the last block (reduce.hpp)
 // DET: the y adds rounded on the grid of det_interp_exp (hb: the bounds of H, and of Hd at hb + nw)
-template <bool GRAD, int THREADS, bool DOT = false, bool DET = false>
+template <bool GRAD, int THREADS, bool DOT = false, bool DET = false, int REC = 5>
 __global__ __launch_bounds__(THREADS) void k_interp(
     const uint16_t* __restrict__ meta, const uint32_t* __restrict__ lo, const uint32_t* __restrict__ qarr,
     const int* __restrict__ tile_off, const double* __restrict__ H, const double* __restrict__ Hd,
@@ -587,7 +591,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
    const int t1 = tile_off[(b + 1) * ngroups];
    TileRegs cur;
    int t = t0 + wave;
-   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
+   if (t < t1) load_tile<REC>(cur, meta, lo, qarr, t, lane);
    // the epilogue's x (mu term) and, when beta != 0, y are fetched now, behind the first run
    const bool ep_regs = B <= kEpMax * THREADS;
    double xe[kEpMax], ye[kEpMax];
@@ -627,7 +631,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
       }
 #pragma unroll
       for (int r = 0; r < kR; r++) {
-         const uint32_t off = slot_off(cur, r);
+         const uint32_t off = slot_off<REC>(cur, r);
          const double u = q_to_s(cur.qq[r]);
          double v = hc[kNC - 1];
 #pragma unroll
@@ -640,7 +644,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
             lds_add(off + 8u * (uint32_t)Bp, DET ? det_round(vd, Cyd) : vd);  // s_yd follows it
          }
       }
-      if (tn < t1) load_tile(cur, meta, lo, qarr, tn, lane);
+      if (tn < t1) load_tile<REC>(cur, meta, lo, qarr, tn, lane);
    }
    __syncthreads();
 
@@ -729,7 +733,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
 // y_v = beta y_v + alpha f^2 (sum_windows interp_v + mu x_v), v = 0, 1; H of vector v at H + v * h_rs
 // DET: as k_interp's, each vector on the grid of its own bounds (hb, hb + 2 nw: k_grid's per-vector layout), so
 // each column equals the single-vector matvec bit for bit
-template <int THREADS, bool DET = false>
+template <int THREADS, bool DET = false, int REC = 5>
 __global__ __launch_bounds__(THREADS) void k_interp2(const uint16_t* __restrict__ meta,
                                                      const uint32_t* __restrict__ lo,
                                                      const uint32_t* __restrict__ qarr,
@@ -755,7 +759,7 @@ __global__ __launch_bounds__(THREADS) void k_interp2(const uint16_t* __restrict_
    const int t1 = tile_off[(b + 1) * ngroups];
    TileRegs cur;
    int t = t0 + wave;
-   if (t < t1) load_tile(cur, meta, lo, qarr, t, lane);
+   if (t < t1) load_tile<REC>(cur, meta, lo, qarr, t, lane);
    for (int i = tid; i < Bp; i += THREADS) s_y0[i] = s_y1[i] = 0.0;
    double C0 = 0.0, C1 = 0.0;
    if (DET) {
@@ -778,7 +782,7 @@ __global__ __launch_bounds__(THREADS) void k_interp2(const uint16_t* __restrict_
       }
 #pragma unroll
       for (int r = 0; r < kR; r++) {
-         const uint32_t off = slot_off(cur, r);
+         const uint32_t off = slot_off<REC>(cur, r);
          const double u = q_to_s(cur.qq[r]);
          double v0 = h0[kNC - 1], v1 = h1[kNC - 1];
 #pragma unroll
@@ -789,7 +793,7 @@ __global__ __launch_bounds__(THREADS) void k_interp2(const uint16_t* __restrict_
          lds_add(off, DET ? det_round(v0, C0) : v0);                      // s_y0: the first dynamic slice
          lds_add(off + 8u * (uint32_t)Bp, DET ? det_round(v1, C1) : v1);  // s_y1 follows it
       }
-      if (t + nwaves < t1) load_tile(cur, meta, lo, qarr, t + nwaves, lane);
+      if (t + nwaves < t1) load_tile<REC>(cur, meta, lo, qarr, t + nwaves, lane);
    }
    __syncthreads();
    const double ff = f * f;
@@ -856,13 +860,21 @@ typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, cons
 // several groups per workgroup, the fold in two chains, register-staged alpha, the row shards' block sum in the
 // spread's tail) were removed in round 4; DESIGN.md 3.5 keeps their numbers.
 constexpr int kSpreadThreads = 512;
-static const SpreadFn kSpreadVariants[] = {k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>,
-                                           k_spread<kSpreadThreads, false, 0>};
-// the deterministic spread (AdditivePlan::det) of each variant
-static const SpreadFn kSpreadVariantsDet[] = {k_spread<kSpreadThreads, false, 1, true>,
-                                              k_spread<kSpreadThreads, true, 1, true>,
-                                              k_spread<kSpreadThreads, false, 0, true>};
-constexpr int kNumSpreadVariants = sizeof(kSpreadVariants) / sizeof(kSpreadVariants[0]);
+// [record 5 / 4][plain / deterministic][variant]
+static const SpreadFn kSpreadFns[2][2][3] = {
+    {{k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>, k_spread<kSpreadThreads, false, 0>},
+     {k_spread<kSpreadThreads, false, 1, true>, k_spread<kSpreadThreads, true, 1, true>,
+      k_spread<kSpreadThreads, false, 0, true>}},
+    {{k_spread<kSpreadThreads, false, 1, false, 4>, k_spread<kSpreadThreads, true, 1, false, 4>,
+      k_spread<kSpreadThreads, false, 0, false, 4>},
+     {k_spread<kSpreadThreads, false, 1, true, 4>, k_spread<kSpreadThreads, true, 1, true, 4>,
+      k_spread<kSpreadThreads, false, 0, true, 4>}}};
+constexpr int kNumSpreadVariants = 3;
+static SpreadFn spread_fn(const AdditivePlan& P)
+{
+   const int v = std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1);
+   return kSpreadFns[P.rec == 4 ? 1 : 0][P.det ? 1 : 0][v];
+}
 
 constexpr int kInterpThreads = 1024;
 typedef void (*InterpFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*,
@@ -870,27 +882,36 @@ typedef void (*InterpFn)(const uint16_t*, const uint32_t*, const uint32_t*, cons
                          double, double*, unsigned int*, double*, const double*, int);
 
 // the interpolation kernel of a launch: gradient or not, fused (q, p) or not, 512 or 1024 threads, deterministic
-template <int T>
+template <int T, int REC>
 static InterpFn interp_fn_t(bool grad, bool dot, bool det)
 {
-   if (grad) return det ? k_interp<true, T, false, true> : k_interp<true, T, false, false>;
-   if (dot) return det ? k_interp<false, T, true, true> : k_interp<false, T, true, false>;
-   return det ? k_interp<false, T, false, true> : k_interp<false, T, false, false>;
+   if (grad) return det ? k_interp<true, T, false, true, REC> : k_interp<true, T, false, false, REC>;
+   if (dot) return det ? k_interp<false, T, true, true, REC> : k_interp<false, T, true, false, REC>;
+   return det ? k_interp<false, T, false, true, REC> : k_interp<false, T, false, false, REC>;
 }
-static InterpFn interp_fn(bool grad, bool dot, bool small, bool det)
+static InterpFn interp_fn(bool grad, bool dot, bool small, bool det, int rec)
 {
-   return small ? interp_fn_t<512>(grad, dot, det) : interp_fn_t<kInterpThreads>(grad, dot, det);
+   if (rec == 4) return small ? interp_fn_t<512, 4>(grad, dot, det) : interp_fn_t<kInterpThreads, 4>(grad, dot, det);
+   return small ? interp_fn_t<512, 5>(grad, dot, det) : interp_fn_t<kInterpThreads, 5>(grad, dot, det);
 }
 constexpr int kInterp2Threads = 1024;
 typedef void (*Interp2Fn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, size_t,
                           const double*, const double*, double*, double*, int, int, int, double, double, double, double,
                           const double*, int);
 // 512-thread workgroups at >= 512 blocks, as the single-vector interpolation (launch_interp)
-static Interp2Fn interp2_fn(bool det, bool small)
+template <int REC>
+static Interp2Fn interp2_fn_t(bool det, bool small)
 {
-   if (small) return det ? k_interp2<512, true> : k_interp2<512, false>;
-   return det ? k_interp2<kInterp2Threads, true> : k_interp2<kInterp2Threads, false>;
+   if (small) return det ? k_interp2<512, true, REC> : k_interp2<512, false, REC>;
+   return det ? k_interp2<kInterp2Threads, true, REC> : k_interp2<kInterp2Threads, false, REC>;
 }
+static Interp2Fn interp2_fn(bool det, bool small, int rec)
+{
+   return rec == 4 ? interp2_fn_t<4>(det, small) : interp2_fn_t<5>(det, small);
+}
+typedef void (*InterpPartFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, double*, int,
+                             int, int, int, double);
+static InterpPartFn interp_part_fn(int rec) { return rec == 4 ? k_interp_part<512, 4> : k_interp_part<512, 5>; }
 
 // a kernel whose dynamic slice is addressed absolutely (lds_at) must have no static LDS
 static bool static_lds_zero(const void* fn)
@@ -907,9 +928,12 @@ static std::vector<const void*> interp_kernels()
    for (int g = 0; g < 2; g++)
       for (int d = 0; d < 2; d++)
          for (int sm = 0; sm < 2; sm++)
-            for (int det = 0; det < 2; det++) v.push_back((const void*)interp_fn(g, d && !g, sm, det));
+            for (int det = 0; det < 2; det++)
+               for (int rec = 4; rec <= 5; rec++) v.push_back((const void*)interp_fn(g, d && !g, sm, det, rec));
    for (int det = 0; det < 2; det++)
-      for (int sm = 0; sm < 2; sm++) v.push_back((const void*)interp2_fn(det, sm));
+      for (int sm = 0; sm < 2; sm++)
+         for (int rec = 4; rec <= 5; rec++) v.push_back((const void*)interp2_fn(det, sm, rec));
+   for (int rec = 4; rec <= 5; rec++) v.push_back((const void*)interp_part_fn(rec));
    return v;
 }
 
@@ -917,12 +941,12 @@ static void raise_lds_limit_once()
 {
    // a function-local static initialiser runs once (thread-safe)
    static const bool raised = []() {
-      for (int i = 0; i < kNumSpreadVariants; i++)
-         for (const SpreadFn f : {kSpreadVariants[i], kSpreadVariantsDet[i]})
-            (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      for (const auto& byrec : kSpreadFns)
+         for (const auto& bydet : byrec)
+            for (const SpreadFn f : bydet)
+               (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       for (const void* f : interp_kernels())
          (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)k_interp_part<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipGetLastError();
       return true;
    }();
@@ -934,11 +958,9 @@ static bool abs_lds_ok()
 {
    static const bool ok = [] {
       std::vector<const void*> v = interp_kernels();
-      v.push_back((const void*)k_interp_part<512>);
-      for (int i = 0; i < kNumSpreadVariants; i++) {
-         v.push_back((const void*)kSpreadVariants[i]);
-         v.push_back((const void*)kSpreadVariantsDet[i]);
-      }
+      for (const auto& byrec : kSpreadFns)
+         for (const auto& bydet : byrec)
+            for (const SpreadFn f : bydet) v.push_back((const void*)f);
       for (const void* f : v)
          if (!static_lds_zero(f)) return false;
       return true;
@@ -952,8 +974,7 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
    raise_lds_limit_once();
    if (!abs_lds_ok()) return -1;
-   const int v = std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1);
-   const SpreadFn fn = P.det ? kSpreadVariantsDet[v] : kSpreadVariants[v];
+   const SpreadFn fn = spread_fn(P);
    const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
    launch_ev(fn, dim3(gridx), dim3(kSpreadThreads), spread_lds_bytes(P), stream, P.kev ? P.kev + 0 : nullptr,
              P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const int*)P.dl.cmax, d_x, P.n, P.B, P.nblocks, P.ngroups,
@@ -990,7 +1011,7 @@ int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, do
    hipLaunchKernelGGL(k_grid_sum_yinit, dim3(P.nw), dim3(kGridThreads), 0, stream, d_gridsum, (const double*)P.d_w,
                       P.d_H, d_y, d_x, P.n, beta, alpha * ff * P.mu * P.diag);
    if (P.n > 0)
-      hipLaunchKernelGGL(k_interp_part<T>, dim3(P.nblocks * S), dim3(T), sizeof(double) * (size_t)(P.B + kPad), stream,
+      hipLaunchKernelGGL(interp_part_fn(P.rec), dim3(P.nblocks * S), dim3(T), sizeof(double) * (size_t)(P.B + kPad), stream,
                          P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H, d_y, P.n, P.B, P.ngroups, S,
                          alpha * ff);
    NFFT4GP_HIP_CHECK(hipGetLastError());
@@ -1020,7 +1041,7 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
    // config C; profiles/r04_interp_threads_ab.txt).  NFFT4GP_AMD_INTERP_THREADS=512 / 1024 forces either.
    static const int forced = getenv("NFFT4GP_AMD_INTERP_THREADS") ? atoi(getenv("NFFT4GP_AMD_INTERP_THREADS")) : 0;
    const bool small = forced == 512 || (forced != 1024 && P.nblocks >= 512);
-   const InterpFn fn = interp_fn(grad, d_dot != nullptr, small, P.det);
+   const InterpFn fn = interp_fn(grad, d_dot != nullptr, small, P.det, P.rec);
    launch_ev(fn, dim3(P.nblocks), dim3(small ? 512 : kInterpThreads), interp_lds_bytes(P, grad), stream,
              P.kev ? P.kev + 4 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H,
              (const double*)P.d_Hd, d_x, d_y, P.n, P.B, P.ngroups, alpha, beta, P.f, P.mu * P.diag, P.diag,
@@ -1039,7 +1060,7 @@ int launch_interp_blocks(const AdditivePlan& P, double alpha, const double* d_x,
    raise_lds_limit_once();
    if (!abs_lds_ok()) return -1;
    const size_t off = (size_t)b0 * P.B;
-   hipLaunchKernelGGL(interp_fn(false, false, false, P.det), dim3(b1 - b0), dim3(kInterpThreads),
+   hipLaunchKernelGGL(interp_fn(false, false, false, P.det, P.rec), dim3(b1 - b0), dim3(kInterpThreads),
                       interp_lds_bytes(P, 0), stream, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off + (size_t)b0 * P.ngroups,
                       (const double*)P.d_H, (const double*)P.d_Hd, d_x + off, d_y + off, P.n - (int)off, P.B, P.ngroups,
                       alpha, beta, P.f, P.mu * P.diag, P.diag, (double*)nullptr, (unsigned int*)nullptr,
@@ -1073,7 +1094,7 @@ int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double
    // profiles/r05_interp2_ab.txt); NFFT4GP_AMD_INTERP2_THREADS=512 selects them
    static const int forced = getenv("NFFT4GP_AMD_INTERP2_THREADS") ? atoi(getenv("NFFT4GP_AMD_INTERP2_THREADS")) : 0;
    const bool small = forced == 512;
-   hipLaunchKernelGGL(interp2_fn(P.det, small), dim3(P.nblocks), dim3(small ? 512 : kInterp2Threads), lds_i, stream,
+   hipLaunchKernelGGL(interp2_fn(P.det, small, P.rec), dim3(P.nblocks), dim3(small ? 512 : kInterp2Threads), lds_i, stream,
                       P.dl.meta, P.dl.lo,
                       P.dl.q, P.dl.tile_off, (const double*)P.d_H2, h_rs, x0, x1, y0, y1, P.n, P.B, P.ngroups, alpha,
                       beta, P.f, P.mu * P.diag, (const double*)P.d_hb, P.nw);

@@ -198,9 +198,15 @@ class NFFTAdditiveKernel:
         return dict(zip(keys, [int(v) for v in out]))
 
     def set_deterministic(self, on: bool = True):
-        """Nfft4GPAmdSetDeterministic: bitwise reproducible 1-D matvecs (the default) or plain fp64 LDS atomics."""
+        """Nfft4GPAmdSetDeterministic: bitwise reproducible 1-D matvecs, or plain fp64 LDS atomics (the default)."""
         if _lib.lib().Nfft4GPAmdSetDeterministic(self.h, int(bool(on))) != 0:
             raise RuntimeError("Nfft4GPAmdSetDeterministic failed")
+
+    def set_precision(self, bits: int):
+        """Nfft4GPAmdSetPrecision: 32 (one 32-bit record per (point, window), BASELINE configs[4]'s fp32 matvec) or
+        64 (the default 5-byte records); after the first setup the layout is rebuilt."""
+        if _lib.lib().Nfft4GPAmdSetPrecision(self.h, int(bits)) != 0:
+            raise RuntimeError("Nfft4GPAmdSetPrecision failed")
 
     def timing(self, enable: bool):
         _lib.lib().Nfft4GPAmdTimingEnable(self.h, int(enable))

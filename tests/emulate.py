@@ -41,18 +41,19 @@ def prepare(col):
     return sc, q
 
 
-def layout(qc, n, nw, B=4064, CG=8):
+def layout(qc, n, nw, B=4064, CG=8, rec=5):
+    """The product's host layout (rec 5: the fp64 default's 5-byte records; rec 4: the 32-bit mode's one word)."""
     qc = np.ascontiguousarray(qc, dtype=np.uint32)
     cnt = (C.c_longlong * 3)()
     L = amd.lib()
-    assert L.Nfft4GPAmdHostLayout(qc.ctypes.data, n, nw, B, CG, cnt, None, None, None, None) == 0
+    assert L.Nfft4GPAmdHostLayoutRec(qc.ctypes.data, n, nw, B, CG, rec, cnt, None, None, None, None) == 0
     ntiles, ngroups, nblocks = cnt[0], cnt[1], cnt[2]
     meta = np.zeros(ntiles * 64, np.uint16)
     lo = np.zeros(ntiles * (R // 4) * 64, np.uint32)
     q = np.zeros(ntiles * R * 64, np.uint32)
     toff = np.zeros(nblocks * ngroups + 1, np.int32)
-    assert L.Nfft4GPAmdHostLayout(qc.ctypes.data, n, nw, B, CG, cnt, meta.ctypes.data, lo.ctypes.data,
-                                  q.ctypes.data, toff.ctypes.data) == 0
+    assert L.Nfft4GPAmdHostLayoutRec(qc.ctypes.data, n, nw, B, CG, rec, cnt, meta.ctypes.data, lo.ctypes.data,
+                                     q.ctypes.data, toff.ctypes.data) == 0
 
     def quads(a, words):  # the 16-byte-quad layout [tile][w/4][lane][w%4] (layout.cpp) -> [tile][lane][w]
         return a.reshape(ntiles, words // 4, 64, 4).transpose(0, 2, 1, 3).reshape(ntiles, 64, words)
@@ -65,6 +66,8 @@ def layout(qc, n, nw, B=4064, CG=8):
     for k in range(4):
         lob[:, :, k::4] = (lw >> (8 * k)) & 255
     loc = (lob << 4) | (qw.astype(np.int64) & 15)      # local index (B + lane % 32 for dummies)
+    if rec == 4:                                       # slot_word4: the whole index in the low 12 bits
+        loc = qw.astype(np.int64) & 4095
     u = qw.view(np.int32).astype(np.float64) * 2.0 ** -32   # offset in the cell - 1/2
     frac = (((qw ^ np.uint32(0x80000000)).astype(np.int64) + 32) >> 6)  # the nearest 26-bit offset, 2^-26 units
     return dict(ntiles=ntiles, ngroups=ngroups, nblocks=nblocks, meta=meta.reshape(ntiles, 64).astype(np.int64),
@@ -74,7 +77,7 @@ def layout(qc, n, nw, B=4064, CG=8):
 class EmulatedPlan:
     """Host setup + numpy replay of the device plan for 1-D windows (rows [rb, re) of n_global)."""
 
-    def __init__(self, X, windows, B=4064, CG=8, shard=None):
+    def __init__(self, X, windows, B=4064, CG=8, shard=None, rec=5):
         X = np.asarray(X, dtype=np.float64)
         self.n_global = X.shape[0]
         self.windows = list(windows)
@@ -88,7 +91,7 @@ class EmulatedPlan:
             assert sc > 0
             self.scales.append(sc)
             qc[c] = q[self.rb:self.re]
-        self.L = layout(qc.ravel(), self.n, self.nw, B, CG)
+        self.L = layout(qc.ravel(), self.n, self.nw, B, CG, rec)
         self.C = tap_poly()
 
     def setup(self, kernel, f, l, mu):

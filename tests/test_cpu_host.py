@@ -102,15 +102,18 @@ def test_prepare_matches_reference_scaling():
     assert prepare(np.full(10, 3.0))[0] == -1.0
 
 
-@pytest.mark.parametrize("n,B,CG", [(10000, 4064, 8), (5000, 1000, 3), (777, 4064, 2), (9000, 256, 3)])
-def test_layout_invariants(n, B, CG):
+@pytest.mark.parametrize("n,B,CG,rec", [(10000, 4064, 8, 5), (5000, 1000, 3, 5), (777, 4064, 2, 5), (9000, 256, 3, 5),
+                                        (10000, 4064, 4, 4), (5000, 1024, 3, 4)])
+def test_layout_invariants(n, B, CG, rec):
+    """The chunk layout of both records (rec 4: the 32-bit precision mode's one word per slot, whose offset may move
+    by up to 2^-21 of a cell to carry the 12-bit local index in its low bits)."""
     nw = 5
     rng = np.random.default_rng(n)
     qc = np.zeros((nw, n), np.uint32)
     for c in range(nw):
         x = rng.beta(0.5, 2.0, n) if c == 0 else rng.random(n)
         _, qc[c] = prepare(x)
-    L = layout(qc.ravel(), n, nw, B, CG)
+    L = layout(qc.ravel(), n, nw, B, CG, rec)
     meta, loc, q = L["meta"], L["loc"], L["q"]
     comp, cell = meta >> 6, meta & 63
     seen = np.zeros((nw, n), np.int64)
@@ -127,7 +130,15 @@ def test_layout_invariants(n, B, CG):
             tt, ll, rr = np.nonzero(real)
             j = b * B + loc[t0:t1][tt, ll, rr]
             c = cc[tt, ll]
-            assert np.all(q[t0:t1][tt, ll, rr] == (qc[c, j] & 0x3FFFFFF))   # offset in the cell
+            if rec == 5:
+                assert np.all(q[t0:t1][tt, ll, rr] == (qc[c, j] & 0x3FFFFFF))   # offset in the cell
+            else:  # the offset in 2^-32 of a cell, moved by at most 2048 units to carry the index (4095 within
+                # 2048 units of the cell's ends, where the nearest congruent value would leave the cell)
+                ueff = L["u"][t0:t1][tt, ll, rr]
+                utrue = (qc[c, j] & 0x3FFFFFF) * 2.0 ** -26 - 0.5
+                dv = np.abs(ueff - utrue) * 2.0 ** 32
+                edge = np.minimum(utrue + 0.5, 0.5 - utrue) * 2.0 ** 32 < 4096
+                assert np.all(dv[~edge] <= 2048) and np.all(dv <= 4095)
             assert np.all((qc[c, j] >> 26) == cell[t0:t1][tt, ll])          # the chunk's cell
             lanes = np.broadcast_to(np.arange(64)[None, :, None], loc[t0:t1].shape)
             assert np.all(loc[t0:t1][~real] == B + lanes[~real] % 32)         # dummies -> pad slots
@@ -142,6 +153,23 @@ def test_layout_invariants(n, B, CG):
             assert conflicts <= 0.22 * (t1 - t0) * 16 * 64
             np.add.at(seen, (c, j), 1)
     assert np.all(seen == 1)  # every (window, point) exactly once
+
+
+@pytest.mark.parametrize("l,bound", [(1.0, 1e-8), (0.1, 1e-7), (0.01, 1e-6)])
+def test_emulated_32bit_records_match_oracle(l, bound):
+    """The 32-bit precision mode (Nfft4GPAmdSetPrecision 32: one word per (point, window), offsets to 2^-21 of a
+    cell) replayed on the CPU against the oracle: within the north star's 1e-6 at TEST1's shortest length scale
+    (the fp64 default's 5-byte records: ~4e-9 there)."""
+    rng = np.random.default_rng(11)
+    n, d = 8000, 4
+    X = rng.random((n, d))
+    x = rng.random(n) - 0.5
+    orc = OracleAdditiveNFFT(X, np.arange(d, dtype=np.int32), d, 1)
+    orc.setup(0, 1.0, l, 0.01)
+    em = EmulatedPlan(X, [[c] for c in range(d)], B=4064, CG=4, rec=4)
+    em.setup(0, 1.0, l, 0.01)
+    e = rel(em.matsymv(x), orc.matsymv(x))
+    assert e < bound, e
 
 
 @pytest.mark.parametrize("kernel", [0, 1])

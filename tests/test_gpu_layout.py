@@ -12,18 +12,18 @@ import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd 
 pytestmark = pytest.mark.gpu
 
 
-def build(fn, qc, n, nw, B, CG):
+def build(fn, qc, n, nw, B, CG, rec=5):
     L = amd.lib()
     cnt = (C.c_longlong * 3)()
-    assert getattr(L, fn)(qc.ctypes.data, n, nw, B, CG, cnt, None, None, None, None) == 0
+    assert getattr(L, fn)(qc.ctypes.data, n, nw, B, CG, rec, cnt, None, None, None, None) == 0
     ntiles, ngroups, nblocks = cnt[0], cnt[1], cnt[2]
     meta = np.zeros(max(ntiles, 1) * 64, np.uint16)
     lo = np.zeros(max(ntiles, 1) * 4 * 64, np.uint32)
     q = np.zeros(max(ntiles, 1) * 16 * 64, np.uint32)
     toff = np.zeros(nblocks * ngroups + 1, np.int32)
-    assert getattr(L, fn)(qc.ctypes.data, n, nw, B, CG, cnt, meta.ctypes.data, lo.ctypes.data, q.ctypes.data,
+    assert getattr(L, fn)(qc.ctypes.data, n, nw, B, CG, rec, cnt, meta.ctypes.data, lo.ctypes.data, q.ctypes.data,
                           toff.ctypes.data) == 0
-    return ntiles, toff, meta[:ntiles * 64], lo[:ntiles * 256], q[:ntiles * 1024]
+    return ntiles, toff, meta[:ntiles * 64], lo[:ntiles * 256] if rec == 5 else lo[:0], q[:ntiles * 1024]
 
 
 def quantised(X):
@@ -36,11 +36,12 @@ def quantised(X):
     return np.ascontiguousarray(qc)
 
 
-@pytest.mark.parametrize("n,nw,B,CG,kind", [(20000, 7, 4064, 3, "uniform"), (9000, 4, 512, 3, "clustered"),
-                                            (5000, 3, 4064, 3, "duplicates"), (4064 * 3, 6, 4064, 3, "uniform"),
-                                            (777, 2, 100, 1, "uniform"), (4064 * 10 + 17, 8, 4064, 4, "uniform"),
-                                            (9000, 5, 512, 4, "clustered")])
-def test_device_layout_equals_host(torch_cuda, n, nw, B, CG, kind):
+@pytest.mark.parametrize("n,nw,B,CG,kind,rec", [(20000, 7, 4064, 3, "uniform", 5), (9000, 4, 512, 3, "clustered", 5),
+                                                (5000, 3, 4064, 3, "duplicates", 5), (4064 * 3, 6, 4064, 3, "uniform", 5),
+                                                (777, 2, 100, 1, "uniform", 5), (4064 * 10 + 17, 8, 4064, 4, "uniform", 5),
+                                                (9000, 5, 512, 4, "clustered", 5), (4064 * 10 + 17, 8, 4064, 4, "uniform", 4),
+                                                (9000, 5, 512, 3, "duplicates", 4)])
+def test_device_layout_equals_host(torch_cuda, n, nw, B, CG, kind, rec):
     rng = np.random.default_rng(n + nw)
     if kind == "uniform":
         X = rng.random((n, nw))
@@ -49,8 +50,8 @@ def test_device_layout_equals_host(torch_cuda, n, nw, B, CG, kind):
     else:
         X = rng.integers(0, 9, (n, nw)) / 8.0
     qc = quantised(X)
-    h = build("Nfft4GPAmdHostLayout", qc, n, nw, B, CG)
-    d = build("Nfft4GPAmdDeviceLayout", qc, n, nw, B, CG)
+    h = build("Nfft4GPAmdHostLayoutRec", qc, n, nw, B, CG, rec)
+    d = build("Nfft4GPAmdDeviceLayoutRec", qc, n, nw, B, CG, rec)
     assert h[0] == d[0]
     for a, b, name in zip(h[1:], d[1:], ("tile_off", "meta", "lo", "q")):
         np.testing.assert_array_equal(a, b, err_msg=name)

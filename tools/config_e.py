@@ -28,6 +28,8 @@ def main():
     # l = 0.1: the NFFT-approximated Gaussian is SPD on U[0,1) data (at l >= 0.3 some bhat_k < 0, the
     # Lanczos Cholesky of T fails and the reference's gradient is NaN; DESIGN.md 'SPD')
     ap.add_argument("--l", type=float, default=0.1)
+    ap.add_argument("--precision", type=int, default=64, choices=[32, 64],
+                    help="Nfft4GPAmdSetPrecision: 64 (default records) or 32 (BASELINE configs[4]'s fp32 matvec)")
     args = ap.parse_args()
     import torch
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
@@ -45,12 +47,23 @@ def main():
                        f"l={args.l} mu=0.01", "data_gen_s": t_gen}
     t0 = time.time()
     op = amd.NFFTAdditiveKernel(X, win, d, 1)
+    if args.precision == 32:
+        op.set_precision(32)
+    out["precision"] = args.precision
     out["create_s"] = time.time() - t0
     t0 = time.time()
     assert op.setup(amd.GAUSSIAN, f=1.0, l=args.l, mu=0.01) == 0
     torch.cuda.synchronize()
     out["setup_s"] = time.time() - t0
     out["layout"] = op.layout_info()
+    # bytes a matvec's kernels move: the layout in both passes, alpha, x and y, the partial grids written and read;
+    # against SURVEY 8(d)'s figure for configs[4] (fp32 coordinates in both passes, 2 x 4 n d, plus the fp64 vector
+    # read and y written, 16 n)
+    lay = out["layout"]
+    moved = 2 * lay["layout_bytes"] + 24 * n + 2 * 8 * lay["nblocks"] * d * 64
+    out["bytes_moved_per_matvec"] = moved
+    out["bytes_survey_fp32_per_matvec"] = 8 * n * d + 16 * n
+    out["bytes_ratio"] = moved / out["bytes_survey_fp32_per_matvec"]
     xd = torch.tensor(y, device="cuda")
     yd = torch.zeros(n, dtype=torch.float64, device="cuda")
     gd = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
