@@ -55,8 +55,10 @@ __device__ __forceinline__ int mom_index(int cl, int cell, int d)
 __device__ __forceinline__ double q_to_s(uint32_t q) { return (double)(int)q; }
 
 // tap polynomial coefficients C[t][d] 2^-32d (monomials in s = 2^32 u) in constant memory: wave-uniform reads
-// become scalar loads
+// become scalar loads; c_taps_u: C[t][d] itself (monomials in u: the 32-bit mode's fp32 moments)
 __constant__ double c_taps[kTaps * kNC];
+__constant__ double c_taps_u[kTaps * kNC];
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // diagnostic timeline (TIMELINE builds only): per workgroup 4 s_memrealtime stamps (100 MHz)
 constexpr int kMaxStampWG = 16384;
@@ -260,17 +262,41 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    const int c0 = g * CG;
    for (; t < t1; t += nwaves) {
       double acc[kNC];
+      if constexpr (REC == 4) {
+         // the 32-bit mode (BASELINE configs[4]: fp32 matvec, fp64 accumulation): a run's moments in fp32, two
+         // degrees per packed instruction (v_pk_mul_f32 / v_pk_add_f32), u = the offset in the cell - 1/2 (not
+         // scaled by 2^32: fp32 would overflow; the fold uses the unscaled taps), flushed into the fp64 table
+         static_assert(kNC == 8, "the packed moment chain is written for degree 7");
+         f32x2 m01 = {0.f, 0.f}, m23 = {0.f, 0.f}, m45 = {0.f, 0.f}, m67 = {0.f, 0.f};
 #pragma unroll
-      for (int d = 0; d < kNC; d++) acc[d] = 0.0;
+         for (int r = 0; r < kR; r++) {
+            const float u = (float)(int)cur.qq[r] * 0x1p-32f;
+            const float al = (float)*lds_at(slot_off<REC>(cur, r));  // s_alpha is the first dynamic slice
+            const float u2 = u * u;
+            f32x2 p = {al, al * u};
+            m01 += p;
+            p *= u2;
+            m23 += p;
+            p *= u2;
+            m45 += p;
+            p *= u2;
+            m67 += p;
+         }
+         acc[0] = m01.x, acc[1] = m01.y, acc[2] = m23.x, acc[3] = m23.y;
+         acc[4] = m45.x, acc[5] = m45.y, acc[6] = m67.x, acc[7] = m67.y;
+      } else {
 #pragma unroll
-      for (int r = 0; r < kR; r++) {
-         const double u = q_to_s(cur.qq[r]);
-         double tpow = *lds_at(slot_off<REC>(cur, r));  // s_alpha is the first dynamic slice
-         acc[0] += tpow;
+         for (int d = 0; d < kNC; d++) acc[d] = 0.0;
 #pragma unroll
-         for (int d = 1; d < kNC; d++) {
-            tpow *= u;
-            acc[d] += tpow;
+         for (int r = 0; r < kR; r++) {
+            const double u = q_to_s(cur.qq[r]);
+            double tpow = *lds_at(slot_off<REC>(cur, r));  // s_alpha is the first dynamic slice
+            acc[0] += tpow;
+#pragma unroll
+            for (int d = 1; d < kNC; d++) {
+               tpow *= u;
+               acc[d] += tpow;
+            }
          }
       }
       const int comp_local = (int)(cur.mt >> 6) - c0;
@@ -279,7 +305,8 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
       if (DET && bC0 == 0) bC0 = det_max_wait<THREADS>(s_red) + lcm;
 #pragma unroll
       for (int d = 0; d < kNC; d++) {
-         const double a = DET ? det_round(acc[d], det_grid(bC0 + 31u * d)) : acc[d];
+         // (32-bit mode: moments in u, |u| <= 1/2, so one grid for every degree)
+         const double a = DET ? det_round(acc[d], det_grid(REC == 4 ? bC0 : bC0 + 31u * d)) : acc[d];
          atomicAdd(dst + mom_index<MOMT>(0, 0, d), a);  // ds_add_f64
       }
       if (t + nwaves < t1) load_tile<REC>(cur, meta, lo, qarr, t + nwaves, lane);
@@ -298,7 +325,8 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
       for (int tp = 0; tp < kTaps; tp++) {
          const double* mrow = s_mom + mom_index<MOMT>(cl, (gi + kM - tp) & (kNos - 1), 0);
 #pragma unroll
-         for (int d = 0; d < kNC; d++) v = fma(c_taps[tp * kNC + d], mrow[mom_index<MOMT>(0, 0, d)], v);
+         for (int d = 0; d < kNC; d++)
+            v = fma((REC == 4 ? c_taps_u : c_taps)[tp * kNC + d], mrow[mom_index<MOMT>(0, 0, d)], v);
       }
       part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
    }
@@ -843,6 +871,7 @@ int upload_tap_coeffs()
    NFFT4GP_HIP_CHECK(hipGetDevice(&dev));
    if (dev < 0 || dev >= 64) return -1;
    if (!done[dev]) {
+      NFFT4GP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_taps_u), tap_poly_coeffs().data(), sizeof(double) * kTaps * kNC));
       // C[t][d] 2^-32d: the kernels evaluate the polynomials in s = 2^32 u (q_to_s)
       std::vector<double> C = tap_poly_coeffs();
       for (int t = 0; t < kTaps; t++)
