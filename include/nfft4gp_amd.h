@@ -556,6 +556,19 @@ int Nfft4GPAmdDistMatSymv(void *dop, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE
  * multi-feature windows all-reduce y once).  chunks = 1: one all-reduce after the matvec.  The sums are
  * the same element for element. */
 int Nfft4GPAmdDistSetChunks(void *dop, int chunks);
+/* kind 0 (rows), 1-D windows: replace the all-reduce of the grids by a peer-memory exchange (collective; call
+ * on every rank after the kernel setup).  Each rank exports one device buffer (hipIpcGetMemHandle: two slots
+ * of the nw x 64 grids and an arrival flag per window) and opens the others'; a matvec then writes its grids
+ * into its own slot and publishes the flags (k_reduce_parts), and the grid kernel waits for every rank's
+ * flags and sums the slots in rank order -- every rank holds the same bits, and there is no separate
+ * all-reduce launch.  A wait gives up after NFFT4GP_AMD_PEER_SPIN polls (default 2^20, ~2 s): the call after
+ * it returns -1.  Returns 0 (on), 1 (not applicable: kind 1 or multi-feature windows, on every rank alike)
+ * or -1 (some rank could not allocate, export or open a buffer: every rank keeps the all-reduce).  With the
+ * exchange on, Nfft4GPAmdDistFree is collective.  Replaces the grid all-reduce of the reference's sequential
+ * component sum (nfft_interface.c:796-817) split over row shards; no reference counterpart. */
+int Nfft4GPAmdDistPeerEnable(void *dop);
+/* 1 if the peer exchange is on, 0 if not, -1 for a NULL operator */
+int Nfft4GPAmdDistPeerActive(void *dop);
 /* per-rank timing of a distributed operator (0 disables; enabling resets): every matvec records hipEvents
  * on the library stream around this rank's kernels before the exchange, the all-reduce and the kernels
  * after it (kind 1: the local matvec, and each chunk's all-reduce on the operator's comm stream).

@@ -128,6 +128,18 @@ __global__ void k_axpby_add(double beta, double* __restrict__ y, const double* _
       y[i] = (beta == 0.0 ? 0.0 : beta * y[i]) + t[i];
 }
 
+// the peer-memory exchange of a row-sharded operator (Nfft4GPAmdDistPeerEnable): this rank's exported buffer,
+// the peers' opened ones, the device pointer table and the host-mapped error word the waits set
+constexpr int kPeerMaxWorld = 256;  // the grid kernels' threads: one polls each rank's flag
+
+struct PeerState {
+   PeerArgs a;
+   char* local = nullptr;
+   std::vector<char*> opened;  // peers' buffers from hipIpcOpenMemHandle (closed at free)
+   char** d_bufs = nullptr;
+   unsigned int* h_err = nullptr;
+};
+
 struct DistOp {
    // first member: a distributed operator is also the kernel data of the loss (gp_loss.c:143-150 writes
    // _params[0] = f, _params[1] = l and _noise_level = mu into it before calling the kernel setup,
@@ -152,7 +164,30 @@ struct DistOp {
    std::vector<hipEvent_t> tpool;        // every timed event, released at the query
    std::vector<std::pair<int, int>> tpairs[3];  // indices into tpool: [0] local before, [1] all-reduce, [2] after
    long long tcount = 0;
+   PeerState* peer = nullptr;  // row split: the peer exchange instead of comm->allreduce of the grids
 };
+
+void peer_free(PeerState* P)
+{
+   if (!P) return;
+   for (char* b : P->opened)
+      if (b) (void)hipIpcCloseMemHandle(b);
+   if (P->local) (void)hipFree(P->local);
+   if (P->d_bufs) (void)hipFree(P->d_bufs);
+   if (P->h_err) (void)hipHostFree(P->h_err);
+   delete P;
+}
+
+// a wait of an earlier exchange gave up (a peer never published): every later call fails
+int peer_check(DistOp* D)
+{
+   if (D->peer && __atomic_load_n(D->peer->h_err, __ATOMIC_ACQUIRE)) {
+      fprintf(stderr, "nfft4gp_amd: a peer exchange timed out (a rank did not publish its grids); the distributed "
+                      "operator is unusable\n");
+      return -1;
+   }
+   return 0;
+}
 
 hipEvent_t timing_event(DistOp* D, int* idx)
 {
@@ -240,6 +275,19 @@ int dist_apply(DistOp* D, int n, int grad, double alpha, double* x, double beta,
    }
    hipStream_t s = current_stream();
    if (D->timing) D->tcount++;
+   if (D->kind == 0 && D->peer) {
+      if (grid_ready(D) || peer_check(D)) return -1;
+      PeerArgs& A = D->peer->a;
+      A.epoch++;
+      const int e0 = timing_mark(D, s);
+      if (shard_spread_peer(D->h, x, A)) return -1;
+      const int e1 = timing_mark(D, s);
+      if (shard_finish_peer(D->h, A, D->d_grid, grad, alpha, x, beta, y)) return -1;
+      const int e3 = timing_mark(D, s);
+      timing_pair(D, 0, e0, e1);
+      timing_pair(D, 2, e1, e3);  // the exchange is inside the grid kernel: the all-reduce slot stays empty
+      return 0;
+   }
    if (D->kind == 0) {
       if (grid_ready(D)) return -1;
       const int e0 = timing_mark(D, s);
@@ -326,6 +374,13 @@ int dist_matvec_dot(void* dop, const double* d_p, double* d_q, double* d_dot)
 {
    DistOp* D = (DistOp*)dop;
    if (!D || D->kind != 0 || grid_ready(D)) return -1;
+   if (D->peer) {
+      if (peer_check(D)) return -1;
+      PeerArgs& A = D->peer->a;
+      A.epoch++;
+      if (shard_spread_peer(D->h, d_p, A) || shard_peer_sum(D->h, A, D->d_grid)) return -1;
+      return shard_finish_dot(D->h, D->d_grid, d_p, d_q, d_dot);
+   }
    if (Nfft4GPAmdShardSpread(D->h, d_p, D->d_grid)) return -1;
    if (D->comm->allreduce(D->d_grid, D->grid_count, current_stream())) return -1;
    return shard_finish_dot(D->h, D->d_grid, d_p, d_q, d_dot);
@@ -442,6 +497,16 @@ void Nfft4GPAmdDistFree(void* dop)
    if (!D) return;
    (void)hipStreamSynchronize(current_stream());
    if (D->cs) (void)hipStreamSynchronize(D->cs);
+   if (D->peer) {
+      // collective: no rank unmaps or frees its buffer while another's last exchange may still read it
+      double one = 1.0, *d_one = nullptr;
+      if (hipMalloc((void**)&d_one, sizeof(double)) == hipSuccess &&
+          hipMemcpy(d_one, &one, sizeof(double), hipMemcpyHostToDevice) == hipSuccess)
+         (void)D->comm->allreduce(d_one, 1, current_stream());
+      (void)hipStreamSynchronize(current_stream());
+      (void)hipFree(d_one);
+      peer_free(D->peer);
+   }
    if (D->d_grid) (void)hipFree(D->d_grid);
    if (D->d_tmp) (void)hipFree(D->d_tmp);
    for (hipEvent_t e : D->ev) (void)hipEventDestroy(e);
@@ -531,6 +596,118 @@ int Nfft4GPAmdDistTimingQuery(void* dop, double* ms, long long* cnt)
    }
    if (cnt) *cnt = D->tcount;
    return 0;
+}
+
+// The peer-memory exchange for a row-sharded operator (collective): each rank exports one
+// buffer (two grid slots + a flag per window) with hipIpcGetMemHandle, the handles travel over the
+// communicator (one byte per double, so the sum is exact), every rank opens the others'.  From then on a
+// matvec publishes its grids into its own slot and the grid kernel sums all ranks' slots in rank order (every
+// rank holds the same bits) -- no all-reduce.  Returns 0 (on), 1 (not applicable: component split or
+// multi-feature windows -- the same answer on every rank) or -1 (a rank could not allocate, export or open:
+// every rank keeps the communicator's all-reduce).
+int Nfft4GPAmdDistPeerEnable(void* dop)
+{
+   DistOp* D = (DistOp*)dop;
+   if (!D) return -1;
+   if (D->peer) return 0;
+   if (D->kind != 0 || !shard_peer_ok(D->h)) return 1;
+   if (grid_ready(D)) return -1;
+   Comm* C = D->comm;
+   const int world = C->world, rank = C->rank;
+   if (world < 1 || world > kPeerMaxWorld) return 1;
+   hipStream_t s = current_stream();
+   PeerState* P = new PeerState();
+   const size_t gcount = D->grid_count, nw = gcount / kNos;
+   const size_t bytes = 2 * gcount * sizeof(double) + (nw * sizeof(unsigned int) + 255) / 256 * 256;
+   constexpr size_t HB = sizeof(hipIpcMemHandle_t);
+   bool ok = hipMalloc((void**)&P->local, bytes) == hipSuccess && hipMemsetAsync(P->local, 0, bytes, s) == hipSuccess &&
+             hipStreamSynchronize(s) == hipSuccess;
+   hipIpcMemHandle_t mine;
+   memset(&mine, 0, sizeof(mine));
+   if (ok && world > 1 && hipIpcGetMemHandle(&mine, P->local) != hipSuccess) {
+      fprintf(stderr, "nfft4gp_amd: hipIpcGetMemHandle refused the exchange buffer\n");
+      ok = false;
+   }
+   ok = ok && hipHostMalloc((void**)&P->h_err, sizeof(unsigned int), hipHostMallocMapped) == hipSuccess;
+   if (ok) *P->h_err = 0u;
+   ok = ok && hipMalloc((void**)&P->d_bufs, sizeof(char*) * world) == hipSuccess;
+   // round 1: the handles and whether every rank got this far
+   std::vector<double> hx((size_t)world * HB + 1, 0.0);
+   for (size_t b = 0; b < HB; b++) hx[(size_t)rank * HB + b] = (double)((const unsigned char*)&mine)[b];
+   hx.back() = ok ? 0.0 : 1.0;
+   double* dx = nullptr;
+   auto agree = [&](std::vector<double>& v) {
+      if (!dx && hipMalloc((void**)&dx, sizeof(double) * hx.size()) != hipSuccess) return false;
+      if (hipMemcpy(dx, v.data(), sizeof(double) * v.size(), hipMemcpyHostToDevice) != hipSuccess) return false;
+      if (C->allreduce(dx, v.size(), s)) return false;
+      return hipMemcpyAsync(v.data(), dx, sizeof(double) * v.size(), hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipStreamSynchronize(s) == hipSuccess;
+   };
+   bool all = agree(hx) && hx.back() == 0.0;
+   std::vector<char*> bufs(world, nullptr);
+   P->opened.assign(world, nullptr);
+   bool mine_ok = all;
+   for (int r = 0; r < world && mine_ok; r++) {
+      if (r == rank) {
+         bufs[r] = P->local;
+         continue;
+      }
+      hipIpcMemHandle_t h;
+      for (size_t b = 0; b < HB; b++) ((unsigned char*)&h)[b] = (unsigned char)hx[(size_t)r * HB + b];
+      void* ptr = nullptr;
+      if (hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+         fprintf(stderr, "nfft4gp_amd: hipIpcOpenMemHandle refused rank %d's exchange buffer\n", r);
+         mine_ok = false;
+         break;
+      }
+      P->opened[r] = (char*)ptr;
+      bufs[r] = (char*)ptr;
+   }
+   // timing probe only (one process): the exchange kernels read this rank's own slot `k` times, as k ranks would
+   int fake = 0;
+   if (world == 1 && mine_ok)
+      if (const char* e = getenv("NFFT4GP_AMD_PEER_FAKE_WORLD")) fake = std::max(0, std::min(kPeerMaxWorld, atoi(e)));
+   if (fake > 1) {
+      fprintf(stderr, "nfft4gp_amd: NFFT4GP_AMD_PEER_FAKE_WORLD=%d: the exchange sums this rank's slot %d times "
+                      "(timing only; the results are wrong)\n", fake, fake);
+      bufs.assign(fake, P->local);
+   }
+   mine_ok = mine_ok && hipMemcpy(P->d_bufs, bufs.data(), sizeof(char*) * std::min<size_t>(bufs.size(), world),
+                                  hipMemcpyHostToDevice) == hipSuccess;
+   if (fake > 1) {
+      (void)hipFree(P->d_bufs);
+      P->d_bufs = nullptr;
+      mine_ok = hipMalloc((void**)&P->d_bufs, sizeof(char*) * fake) == hipSuccess &&
+                hipMemcpy(P->d_bufs, bufs.data(), sizeof(char*) * fake, hipMemcpyHostToDevice) == hipSuccess;
+   }
+   // round 2: every rank opened every buffer
+   std::vector<double> ok2(hx.size(), 0.0);
+   ok2.back() = mine_ok ? 0.0 : 1.0;
+   all = agree(ok2) && ok2.back() == 0.0;
+   (void)hipFree(dx);
+   if (!all) {
+      peer_free(P);
+      return -1;
+   }
+   unsigned int* d_err = nullptr;
+   if (hipHostGetDevicePointer((void**)&d_err, P->h_err, 0) != hipSuccess) d_err = P->h_err;
+   long long spin = 1ll << 20;  // ~2 s of polls (each a system-scope load and an s_sleep)
+   if (const char* e = getenv("NFFT4GP_AMD_PEER_SPIN")) spin = std::max(1ll, atoll(e));
+   P->a.bufs = P->d_bufs;
+   P->a.own = P->local;
+   P->a.world = fake > 1 ? fake : world;
+   P->a.epoch = 0u;
+   P->a.err = d_err;
+   P->a.slot_doubles = (long long)gcount;
+   P->a.spin = spin;
+   D->peer = P;
+   return 0;
+}
+
+int Nfft4GPAmdDistPeerActive(void* dop)
+{
+   DistOp* D = (DistOp*)dop;
+   return D ? (D->peer ? 1 : 0) : -1;
 }
 
 int Nfft4GPAmdDistSetChunks(void* dop, int chunks)

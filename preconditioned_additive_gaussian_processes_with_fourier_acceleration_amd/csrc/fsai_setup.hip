@@ -479,6 +479,7 @@ struct ScrShared {
    union {
       unsigned int h[kScrRows][256];
       double key[kScrRows][kScrCap];
+      float ck[kScrRows][kScrCap];  // the one-pass collect's candidate accumulators
    } u;
    int idx[kScrRows][kScrCap];
    float thr[kScrRows];  // -T_r / 2 of the current scan (rows beyond nr: +inf, never pass)
@@ -574,8 +575,128 @@ __device__ __forceinline__ void knn_scan_mfma(ScrShared& S, const float* __restr
    }
 }
 
+// The one-pass collect (PHASE 2): every point j in [j0, j1) with key~ <= the row's limit L (acc >= S.thr = -L/2)
+// appends (j, acc) to the row's candidates, and at round boundaries the workgroup stops and each row holding
+// more than `trigger` candidates tightens L to V + 2m, V = the (lfil-1)-th smallest key~ it holds, and drops
+// the candidates above it.  Invariant: the candidates are every scanned point with key~ <= L, and L >= the
+// true (lfil-1)-th smallest key + m (the lfil-1 candidates with key~ <= V have key <= V + m), so every true
+// neighbour is still a candidate when the scan ends.  The boundaries fall every 16 rounds of 256 points up to
+// 16384 points, then every quarter of the points seen, so the appends between two boundaries stay near
+// (lfil - 1) / 4; a row that overflows kScrCap anyway goes to the fallback (cnt > kScrCap).
+template <bool CHECK, int STEPS>
+__device__ __forceinline__ void knn_stream_mfma(ScrShared& S, const float* __restrict__ Xf,
+                                                const float* __restrict__ nx, int n, int j0, int j1, int nr, int K,
+                                                float margin2)
+{
+   static_assert(kScrRowBlocks == 1, "the stream keeps one row tile per workgroup");
+   constexpr int W = kScrThreads / 64, CAP = kScrCap;
+   const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, wave = threadIdx.x >> 6;
+   const int trigger = min(CAP - 48, max(64, 2 * K));
+   float a[STEPS];
+#pragma unroll
+   for (int st = 0; st < STEPS; st++) a[st] = S.q[2 * st + h][col];
+   float nqh[16], thr[16];
+   int rlim[16];
+#pragma unroll
+   for (int v = 0; v < 16; v++) {
+      const int r = (v & 3) + 8 * (v >> 2) + 4 * h;
+      nqh[v] = S.nqh[r];
+      thr[v] = S.thr[r];
+      rlim[v] = CHECK ? S.row[r] : 0;
+   }
+   float b0[STEPS], b1[STEPS], a00 = 0.f, a01 = 0.f;
+   auto load = [&](int jb, float (&b)[STEPS], float& a0) {
+      const int jl = min(jb + col, j1 - 1);
+      a0 = nx[jl];
+#pragma unroll
+      for (int st = 0; st < STEPS; st++) b[st] = Xf[(size_t)(2 * st + h) * n + jl];
+   };
+   constexpr int step = W * 32;
+   const int nrounds = (j1 - j0 + step - 1) / step;  // workgroup-uniform: every wave meets every boundary
+   if (j0 + wave * 32 < j1) load(j0 + wave * 32, b0, a00);
+   if (j0 + wave * 32 + step < j1) load(j0 + wave * 32 + step, b1, a01);
+   int next = 16;  // the round after which the next boundary falls
+   for (int k = 0; k < nrounds; k++) {
+      const int jb = j0 + wave * 32 + k * step;
+      if (jb < j1) {
+         const int j = jb + col;
+         const bool ok = j < j1;
+         f32x16 c;
+         float bc[STEPS];
+#pragma unroll
+         for (int v = 0; v < 16; v++) c[v] = fmaf(a00, -0.5f, nqh[v]);
+#pragma unroll
+         for (int st = 0; st < STEPS; st++) {
+            bc[st] = b0[st];
+            b0[st] = b1[st];
+         }
+         a00 = a01;
+         if (jb + 2 * step < j1) load(jb + 2 * step, b1, a01);
+#pragma unroll
+         for (int st = 0; st < STEPS; st++) c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], bc[st], c, 0, 0, 0);
+         bool any = false;
+#pragma unroll
+         for (int v = 0; v < 16; v++) any |= c[v] >= thr[v];
+         if (ok && any) {
+#pragma unroll
+            for (int v = 0; v < 16; v++) {
+               const int r = (v & 3) + 8 * (v >> 2) + 4 * h;
+               if (!(c[v] >= thr[v]) || (CHECK && j >= rlim[v])) continue;
+               const int slot = atomicAdd(&S.cnt[r], 1);
+               if (slot < CAP) {
+                  S.idx[r][slot] = j;
+                  S.u.ck[r][slot] = c[v];
+               }
+            }
+         }
+      }
+      if (k + 1 != next || k + 1 == nrounds) continue;
+      next = (k + 1 < 64) ? k + 17 : k + 1 + (k + 1) / 4;
+      __syncthreads();
+      for (int r = wave; r < nr; r += W) {
+         const int cnt = S.cnt[r];
+         if (cnt <= trigger || cnt > CAP) continue;
+         // V = the K-th smallest key~ held: the largest key~ of rank < K (rank = the number strictly below)
+         float vmax = 0.f;
+         for (int e = lane; e < cnt; e += 64) {
+            const float ke = fmaxf(0.f, -2.f * S.u.ck[r][e]);
+            int rank = 0;
+            for (int o = 0; o < cnt; o++) rank += (fmaxf(0.f, -2.f * S.u.ck[r][o]) < ke) ? 1 : 0;
+            if (rank < K) vmax = fmaxf(vmax, ke);
+         }
+         for (int off = 32; off > 0; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off, 64));
+         const float tnew = -0.5f * ((vmax + margin2) * 1.000001f);
+         if (!(tnew > S.thr[r])) continue;  // wave-uniform
+         // keep acc >= tnew, in order (the writes of a 64-chunk land at or below its reads)
+         int kept = 0;
+         for (int e0 = 0; e0 < cnt; e0 += 64) {
+            const int e = e0 + lane;
+            const float ce = e < cnt ? S.u.ck[r][e] : 0.f;
+            const int je = e < cnt ? S.idx[r][e] : 0;
+            const bool keep = e < cnt && ce >= tnew;
+            const unsigned long long m = __ballot(keep);
+            const int pos = kept + __popcll(m & ((1ull << lane) - 1ull));
+            if (keep) {
+               S.u.ck[r][pos] = ce;
+               S.idx[r][pos] = je;
+            }
+            kept += __popcll(m);
+         }
+         if (lane == 0) {
+            S.cnt[r] = kept;
+            S.thr[r] = tnew;
+         }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int v = 0; v < 16; v++) thr[v] = S.thr[(v & 3) + 8 * (v >> 2) + 4 * h];
+   }
+}
+
 // Two launches, so that each holds only its own scans' registers: PHASE 0 = sample and count, leaving each
 // row's collect limit U + 2m in lim (NaN: the row goes to the fallback); PHASE 1 = collect, exact keys, rank.
+// PHASE 2 = the one-launch screen: the sample, then the one-pass collect above from the sample's limit
+// T1 + 2m, exact keys, rank.
 template <int STEPS, int PHASE>
 __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const double* __restrict__ X, int ldim,
                                                                const float* __restrict__ Xf,
@@ -646,7 +767,7 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
       }
       if (tid < R) {
          S.cnt[tid] = 0;
-         if (PHASE == 0) {
+         if (PHASE != 1) {
             S.thr[tid] = (tid < nr) ? -inf : inf;
          } else {
             const float L = (tid < nr) ? lim[lp0 + tid] : inf;
@@ -655,7 +776,7 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
          }
       }
       __syncthreads();
-      if constexpr (PHASE == 0) {
+      if constexpr (PHASE != 1) {
       const int Sn = min(i0, kScrSample);
       knn_scan_mfma<0, false, STEPS>(S, Xf, nx, n, d, i0, 0, Sn);
       __syncthreads();
@@ -682,6 +803,8 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
          }
       }
       __syncthreads();
+      }
+      if constexpr (PHASE == 0) {
       clear_h();
       __syncthreads();
       // count over the earlier points: [0, i0) before all rows (a systematic half of it once i0 is large: the
@@ -700,8 +823,19 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
       }
       __syncthreads();
       } else {
-      knn_scan_mfma<3, false, STEPS>(S, Xf, nx, n, d, i0, 0, i0);
-      knn_scan_mfma<3, true, STEPS>(S, Xf, nx, n, d, i0, i0, ilast);
+      if constexpr (PHASE == 1) {
+         knn_scan_mfma<3, false, STEPS>(S, Xf, nx, n, d, i0, 0, i0);
+         knn_scan_mfma<3, true, STEPS>(S, Xf, nx, n, d, i0, i0, ilast);
+      } else {
+         // the sample's limit T1 + 2m (thr = -T1 / 2 here; inf: gave up, -inf: T1 = inf)
+         if (tid < nr) {
+            const float t = S.thr[tid];
+            if (t != inf && t != -inf) S.thr[tid] = -0.5f * ((-2.f * t + margin2) * 1.000001f);
+         }
+         __syncthreads();
+         knn_stream_mfma<false, STEPS>(S, Xf, nx, n, 0, i0, nr, K, margin2);
+         knn_stream_mfma<true, STEPS>(S, Xf, nx, n, i0, ilast, nr, K, margin2);
+      }
       __syncthreads();
       // exact keys of the candidates (the histogram space is free now)
       for (int r = wave; r < nr; r += W) {
@@ -742,6 +876,298 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
    }
 }
 
+// ---- the one-launch tiled screen (variant 4, the default for d <= 32 and lfil <= 25) ----
+// 256 rows per workgroup, 32 per wave; the earlier points stream once through LDS in stages of 64, each
+// stage read by all eight waves, so the HBM / L2 traffic per (point, row) pair is an eighth of the
+// 32-row screens'.  key~ comes from v_mfma_f32_32x32x16_bf16 on a three-term bf16 split of the
+// coordinates: x = xh + xl + ex with xh = bf16(x), xl = bf16(x - xh), |ex| <= 2^-18 |x|, and
+// x.q ~ xh.qh + xh.ql + xl.qh (bf16 products are exact in fp32).  Error of key~ = |x|^2 + |q|^2 - 2 x.q
+// (fp32 norms of the fp32-rounded coordinates, as the 32-row screens):
+//   split       2 * 3.02 * 2^-18 |x||q|                     <= 387 * 2^-24 M^2
+//   MFMA sums   2 * 3d additions of partial sums <= 2.02 M^2 <= 12.2 d * 2^-24 M^2 (one fp32 rounding each)
+//   norms       2 (d + 2) * 2^-24 M^2, start value 4 * 2^-24 M^2
+// so |key~ - key| <= (14.2 d + 395) 2^-24 M^2 and m = (16 d + 448) 2^-24 M^2 (M^2 = max |x_j|^2 >= 2^-60, so
+// bf16 subnormal flushes stay far below it).  Each row keeps its candidates (index, acc) in LDS, at most
+// kTileCap: it starts accepting every earlier point; whenever a row holds more than kTileCap - 32 after a
+// 32-point tile, its wave tightens the row's limit to V + 2m (V = the (lfil-1)-th smallest key~ held) and
+// drops the candidates above it (the invariant of knn_stream_mfma), so a tile can never overflow a row that
+// the limit has settled; rows that overflow anyway (many equal keys) go to the fallback.  The rows are the
+// wave's own, so the selections need no barrier; the exact fp64 keys and the (key, index) ranking run on
+// one candidate per lane.
+constexpr int kTileRows = 256;
+constexpr int kTileCap = 64;
+constexpr int kTileStep = 64;  // points per LDS stage: two 32-point blocks
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <int KCH>
+struct TileShared {
+   int idx[kTileRows][kTileCap];
+   float ck[kTileRows][kTileCap];
+   uint4 pts[2][2 * KCH * 2 * 2 * 32];  // [stage][block][chunk][hi/lo][half][point] of 8 bf16
+   float nx[2][kTileStep];
+   float thr[kTileRows];
+   int cnt[kTileRows];
+   int row[kTileRows];
+};
+
+__device__ __forceinline__ unsigned int bf16_rn(float f)  // bits of the nearest bf16 (finite f)
+{
+   const unsigned int u = __float_as_uint(f);
+   return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// Xb: per 32-point block, [chunk KCH][hi, lo][half][point 32] x 16 B (features 16 ch + 8 half + 0..7),
+// zero past d and past n; nx = fp32 squared norms (+inf past n, so padded points never pass); *m2 = bits
+// of max nx over the n points.  npad = n rounded up to kTileStep.
+template <int KCH>
+__global__ __launch_bounds__(256) void k_knn_prep_bf(const double* __restrict__ X, int ldim, int n, int npad, int d,
+                                                     uint4* __restrict__ Xb, float* __restrict__ nx,
+                                                     unsigned int* __restrict__ m2)
+{
+   constexpr int BLK = KCH * 2 * 2 * 32;
+   unsigned int mx = 0u;
+   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < npad; j += gridDim.x * blockDim.x) {
+      float a = 0.f;
+      uint4* blk = Xb + (size_t)(j >> 5) * BLK + (j & 31);
+#pragma unroll
+      for (int ch = 0; ch < KCH; ch++) {
+#pragma unroll
+         for (int half = 0; half < 2; half++) {
+            unsigned int hw[4] = {0u, 0u, 0u, 0u}, lw[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+               const int c = 16 * ch + 8 * half + e;
+               const double x = (j < n && c < d) ? X[(size_t)c * ldim + j] : 0.0;
+               const float f = (float)x;
+               a = fmaf(f, f, a);
+               const unsigned int hb = bf16_rn(f);
+               const unsigned int lb = bf16_rn((float)(x - (double)__uint_as_float(hb << 16)));
+               hw[e >> 1] |= hb << (16 * (e & 1));
+               lw[e >> 1] |= lb << (16 * (e & 1));
+            }
+            blk[((ch * 2 + 0) * 2 + half) * 32] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+            blk[((ch * 2 + 1) * 2 + half) * 32] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+         }
+      }
+      nx[j] = j < n ? a : __int_as_float(0x7f800000);
+      if (j < n) mx = max(mx, __float_as_uint(a));
+   }
+   for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned int)__shfl_xor((int)mx, off, 64));
+   if ((threadIdx.x & 63) == 0) atomicMax(m2, mx);
+}
+
+template <int KCH>
+__global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ X, int ldim,
+                                                     const uint4* __restrict__ Xb, const float* __restrict__ nx,
+                                                     int n, int d, int lfil, float margin2,
+                                                     const int* __restrict__ ia, int* __restrict__ ja,
+                                                     int* __restrict__ fail, int* __restrict__ nfail,
+                                                     const int* __restrict__ rows, int nrows_list, int probe)
+{
+   constexpr int R = kTileRows, CAP = kTileCap, BLK = KCH * 2 * 2 * 32;
+   __shared__ TileShared<KCH> S;
+   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, col = lane & 31;
+   const int K = lfil - 1;
+   const int nall = rows ? nrows_list : n - lfil;
+   const int ngroups = (nall + R - 1) / R;
+   const float inf = __int_as_float(0x7f800000);
+   for (int gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+      const int g = ngroups - 1 - gi;  // the longest scans first
+      const int lp0 = g * R, nr = min(R, nall - lp0);
+      auto row_of = [&](int r) { return rows ? rows[lp0 + r] : lfil + lp0 + r; };
+      const int ilast = row_of(nr - 1);  // the rows see points [0, ilast) at most
+      if (tid < R) {
+         S.row[tid] = tid < nr ? row_of(tid) : 0;
+         S.cnt[tid] = 0;
+         S.thr[tid] = (tid < nr && !probe) ? -__FLT_MAX__ : inf;  // probe: the scan alone (timing)
+      }
+      // the wave's 32 rows as the A operand (lane: row 32 wave + col, features 8 h + 0..7 of each chunk)
+      const int iA = (32 * wave + col < nr) ? row_of(32 * wave + col) : row_of(0);
+      bf16x8 ah[KCH], al[KCH];
+      {
+         const uint4* blk = Xb + (size_t)(iA >> 5) * BLK + (iA & 31);
+#pragma unroll
+         for (int ch = 0; ch < KCH; ch++) {
+            const uint4 hv = blk[((ch * 2 + 0) * 2 + h) * 32], lv = blk[((ch * 2 + 1) * 2 + h) * 32];
+            ah[ch] = __builtin_bit_cast(bf16x8, hv);
+            al[ch] = __builtin_bit_cast(bf16x8, lv);
+         }
+      }
+      float nqh[16], thr[16];
+      int rlim[16];
+#pragma unroll
+      for (int v = 0; v < 16; v++) {
+         const int r = 32 * wave + (v & 3) + 8 * (v >> 2) + 4 * h;
+         nqh[v] = r < nr ? -0.5f * nx[row_of(r)] : 0.f;
+         rlim[v] = r < nr ? row_of(r) : 0;
+      }
+      const int nsteps = (ilast + kTileStep - 1) / kTileStep;
+      const int rowmin = row_of(0);
+      const unsigned long long below = (1ull << lane) - 1ull;
+      int cntv = 0;  // lane l < 32: candidates of the wave's row l
+      for (int t = tid; t < 2 * BLK; t += kScrThreads) S.pts[0][t] = Xb[t];
+      if (tid < kTileStep) S.nx[0][tid] = nx[tid];
+      __syncthreads();
+#pragma unroll
+      for (int v = 0; v < 16; v++) thr[v] = S.thr[32 * wave + (v & 3) + 8 * (v >> 2) + 4 * h];
+      // the stages' global loads run four stages ahead in registers p0..p3 (p_k holds a stage = k mod 4; one
+      // stage of MFMAs is ~0.4 us, an HBM / MALL miss several times that).  The loads are unconditional (a
+      // stage index clamped to the last stage, lanes past the stage's data re-read it), so no branch joins a
+      // loaded register and its wait stays at the LDS store.
+      const int tq = tid % (2 * BLK), tn = tid % kTileStep;
+      uint4 p0, p1, p2, p3;
+      float n0, n1, n2, n3;
+      auto fetch = [&](int t, uint4& pr, float& pn) {
+         t = min(t, nsteps - 1);
+         pr = Xb[(size_t)t * 2 * BLK + tq];
+         pn = nx[(size_t)t * kTileStep + tn];
+      };
+      fetch(1, p1, n1);
+      fetch(2, p2, n2);
+      fetch(3, p3, n3);
+      fetch(4, p0, n0);
+      // a 32-point tile's keys: B fragments from the stage, six MFMAs on the three-term split
+      auto mfma_tile = [&](int buf, int sub) {
+         const float nxj = S.nx[buf][32 * sub + col];
+         f32x16 c;
+#pragma unroll
+         for (int v = 0; v < 16; v++) c[v] = fmaf(nxj, -0.5f, nqh[v]);
+#pragma unroll
+         for (int ch = 0; ch < KCH; ch++) {
+            const bf16x8 bh = __builtin_bit_cast(bf16x8, S.pts[buf][sub * BLK + ((ch * 2 + 0) * 2 + h) * 32 + col]);
+            const bf16x8 bl = __builtin_bit_cast(bf16x8, S.pts[buf][sub * BLK + ((ch * 2 + 1) * 2 + h) * 32 + col]);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ch], bl, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ch], bh, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ch], bh, c, 0, 0, 0);
+         }
+         return c;
+      };
+      // test a tile's keys against the rows' limits (points j0 + col), append, tighten
+      auto test_tile = [&](const f32x16& c, int j0) {
+         const int j = j0 + col;
+         float mx = -inf;
+#pragma unroll
+         for (int v = 0; v < 16; v++) mx = fmaxf(mx, c[v] - thr[v]);  // NaN keys drop out
+         if (!__ballot(mx >= 0.f)) return;
+         // append: the wave owns its rows, so each (v, lane half) pair's slots come from one ballot
+         // (lanes 0-31: row rl = (v & 3) + 8 (v >> 2), lanes 32-63: rl + 4) and the counts live in cntv
+         // a point at or after a row never counts for it (rlim: the lane's 16 rows' indices; jj = -1 while
+         // every point of the tile precedes every row)
+         const int jj = (j0 + 31 < rowmin) ? -1 : j;
+#pragma unroll
+         for (int v = 0; v < 16; v++) {
+            const int rl = (v & 3) + 8 * (v >> 2);
+            const bool pass = c[v] >= thr[v] && jj < rlim[v];
+            const unsigned long long m = __ballot(pass);
+            if (!m) continue;
+            const unsigned int mlo = (unsigned int)m, mhi = (unsigned int)(m >> 32);
+            const int blo = __builtin_amdgcn_readlane(cntv, rl), bhi = __builtin_amdgcn_readlane(cntv, rl + 4);
+            if (pass) {
+               const int base = h ? bhi : blo;
+               const int pos = base + __popcll(m & below) - (h ? __popc(mlo) : 0);
+               if (pos < CAP) {
+                  S.idx[32 * wave + rl + 4 * h][pos] = j;
+                  S.ck[32 * wave + rl + 4 * h][pos] = c[v];
+               }
+            }
+            cntv += (lane == rl) ? __popc(mlo) : (lane == rl + 4) ? __popc(mhi) : 0;
+         }
+         // the wave's rows that another tile could overflow: tighten them (wave-uniform loop)
+         unsigned long long todo = __ballot(lane < 32 && cntv > CAP - 32);
+         if (!todo) return;
+         while (todo) {
+            const int rl = __ffsll((long long)todo) - 1;
+            todo &= todo - 1;
+            const int r = 32 * wave + rl;
+            const int cnt = __builtin_amdgcn_readlane(cntv, rl);
+            if (cnt > CAP) {  // overflowed: the fallback takes the row
+               if (lane == 0) S.thr[r] = inf;
+               continue;
+            }
+            const float ce = lane < cnt ? S.ck[r][lane] : -inf;
+            const int je = lane < cnt ? S.idx[r][lane] : 0;
+            const float ke = lane < cnt ? fmaxf(0.f, -2.f * ce) : inf;
+            int rank = 0;
+            for (int o = 0; o < cnt; o++)
+               rank += (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(ke), o)) < ke) ? 1 : 0;
+            float vk = (lane < cnt && rank < K) ? ke : 0.f;
+            for (int off = 32; off > 0; off >>= 1) vk = fmaxf(vk, __shfl_xor(vk, off, 64));
+            const float tnew = -0.5f * ((vk + margin2) * 1.000001f);
+            if (!(tnew > S.thr[r])) continue;
+            const bool keep = lane < cnt && ce >= tnew;
+            const unsigned long long m = __ballot(keep);
+            if (keep) {
+               const int pos = __popcll(m & ((1ull << lane) - 1ull));
+               S.ck[r][pos] = ce;
+               S.idx[r][pos] = je;
+            }
+            if (lane == rl) cntv = __popcll(m);
+            if (lane == 0) S.thr[r] = tnew;
+         }
+#pragma unroll
+         for (int v = 0; v < 16; v++) thr[v] = S.thr[32 * wave + (v & 3) + 8 * (v >> 2) + 4 * h];
+      };
+      // software pipeline: a tile's tests run under the next tile's MFMAs (c1 carries the previous
+      // stage's second tile)
+      f32x16 c0, c1;
+      // stage s: its two tiles, then stage s + 1 from pr (= p_{(s+1) mod 4}) into the other buffer, and pr
+      // refilled with stage s + 5
+      auto stage = [&](int s, uint4& pr, float& pn) {
+         const int buf = s & 1;
+         c0 = mfma_tile(buf, 0);
+         if (s > 0) test_tile(c1, s * kTileStep - 32);
+         c1 = mfma_tile(buf, 1);
+         test_tile(c0, s * kTileStep);
+         if (s + 1 < nsteps) {
+            if (tid < 2 * BLK) S.pts[buf ^ 1][tid] = pr;
+            if (tid < kTileStep) S.nx[buf ^ 1][tid] = pn;
+         }
+         fetch(s + 5, pr, pn);
+         __syncthreads();
+      };
+      for (int s0 = 0; s0 < nsteps; s0 += 4) {
+         stage(s0, p1, n1);
+         if (s0 + 1 >= nsteps) break;
+         stage(s0 + 1, p2, n2);
+         if (s0 + 2 >= nsteps) break;
+         stage(s0 + 2, p3, n3);
+         if (s0 + 3 >= nsteps) break;
+         stage(s0 + 3, p0, n0);
+      }
+      if (nsteps > 0) test_tile(c1, nsteps * kTileStep - 32);
+      if (lane < 32) S.cnt[32 * wave + lane] = cntv;
+      // exact fp64 keys of the candidates (one per lane) and the (key, index) ranking; the wave's rows
+      for (int rl = 0; rl < 32; rl++) {
+         const int r = 32 * wave + rl;
+         if (r >= nr) break;
+         const int i = S.row[r], cnt = S.cnt[r];
+         if (cnt > CAP || cnt < K) {
+            if (lane == 0) fail[atomicAdd(nfail, 1)] = i;
+            continue;
+         }
+         double ke = 0.0;
+         int ie = 0x7fffffff;
+         if (lane < cnt) {
+            ie = S.idx[r][lane];
+            for (int c = 0; c < d; c++) {
+               const double t = X[(size_t)c * ldim + ie] - X[(size_t)c * ldim + i];
+               ke = fma(t, t, ke);
+            }
+         }
+         int rank = 0;
+         for (int o = 0; o < cnt; o++) {
+            const double ko = __shfl(ke, o, 64);
+            const int io = __builtin_amdgcn_readlane(ie, o);
+            rank += (ko < ke || (ko == ke && io < ie)) ? 1 : 0;
+         }
+         const int rp = ia[i];
+         if (lane < cnt && rank < K) ja[rp + rank] = ie;
+         if (lane == 0) ja[rp + K] = i;
+      }
+      __syncthreads();
+   }
+}
+
 template <class T>
 int upload(T** d, const T* h, size_t count);
 
@@ -777,7 +1203,40 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
    if (upload(&dfail, (const int*)nullptr, (size_t)nrows + 2) ||
        hipMemsetAsync(dfail + nrows, 0, 2 * sizeof(int), s) != hipSuccess)
       return done(-1);
-   if (variant == 1) {
+   if (variant == 4 && (d > 32 || lfil - 1 > 24)) variant = 3;
+   if (variant == 4) {
+      const int kch = d <= 16 ? 1 : 2;
+      const int npad = (n + kTileStep - 1) / kTileStep * kTileStep;
+      if (hipMalloc((void**)&Xf, (size_t)npad * kch * 64) != hipSuccess ||
+          hipMalloc((void**)&nx, sizeof(float) * (size_t)npad) != hipSuccess)
+         return done(-1);
+      if (kch == 1)
+         hipLaunchKernelGGL(k_knn_prep_bf<1>, dim3(std::min((npad + 255) / 256, 4096)), dim3(256), 0, s, dX, ldim, n,
+                            npad, d, (uint4*)Xf, nx, (unsigned int*)(dfail + nrows + 1));
+      else
+         hipLaunchKernelGGL(k_knn_prep_bf<2>, dim3(std::min((npad + 255) / 256, 4096)), dim3(256), 0, s, dX, ldim, n,
+                            npad, d, (uint4*)Xf, nx, (unsigned int*)(dfail + nrows + 1));
+      if (hipMemcpyAsync(&m2bits, dfail + nrows + 1, sizeof(unsigned int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+         return done(-1);
+      float m2;
+      memcpy(&m2, &m2bits, sizeof(float));
+      const double margin = (16.0 * d + 448.0) * std::ldexp(1.0, -24) * (double)m2;
+      if (std::isfinite(m2) && m2 >= std::ldexp(1.0f, -60) && std::isfinite((float)(2.0 * margin))) {
+         const int ngroups = (nrows + kTileRows - 1) / kTileRows;
+         auto tile = kch == 1 ? k_knn_tile<1> : k_knn_tile<2>;
+         hipLaunchKernelGGL(tile, dim3(std::min(ngroups, 65535)), dim3(kScrThreads), 0, s, dX, ldim, (const uint4*)Xf,
+                            (const float*)nx, n, d, lfil, (float)(2.0 * margin) * 1.0001f, dia, dja, dfail,
+                            dfail + nrows, d_rows, nrows, getenv("NFFT4GP_AMD_KNN_TILE_PROBE") ? 1 : 0);
+      } else {
+         variant = 3;  // the fp32 screens decide (and route non-finite data to k_knn)
+         (void)hipFree(Xf);
+         (void)hipFree(nx);
+         Xf = nx = nullptr;
+         if (hipMemsetAsync(dfail + nrows, 0, 2 * sizeof(int), s) != hipSuccess) return done(-1);
+      }
+   }
+   if (variant == 1 || variant == 3) {
       const int steps = d <= 4 ? 2 : d <= 8 ? 4 : d <= 16 ? 8 : d <= 32 ? 16 : 32;
       if (hipMalloc((void**)&Xf, sizeof(float) * (size_t)n * 2 * steps) != hipSuccess ||
           hipMalloc((void**)&nx, sizeof(float) * (size_t)n) != hipSuccess)
@@ -797,7 +1256,17 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
          static const int sub = getenv("NFFT4GP_AMD_KNN_SUB") ? std::max(1, atoi(getenv("NFFT4GP_AMD_KNN_SUB"))) : 2;
          float* lim = nullptr;
          if (hipMalloc((void**)&lim, sizeof(float) * (size_t)nrows) != hipSuccess) return done(-1);
-         for (int phase = 0; phase < 2; phase++) {
+         if (variant == 3) {
+            auto screen = steps == 2    ? k_knn_screen<2, 2>
+                          : steps == 4  ? k_knn_screen<4, 2>
+                          : steps == 8  ? k_knn_screen<8, 2>
+                          : steps == 16 ? k_knn_screen<16, 2>
+                                        : k_knn_screen<32, 2>;
+            hipLaunchKernelGGL(screen, dim3(std::min(ngroups, 4096)), dim3(kScrThreads), 0, s, dX, ldim,
+                               (const float*)Xf, (const float*)nx, n, d, lfil, (float)(2.0 * margin) * 1.0001f, lim,
+                               dia, dja, dfail, dfail + nrows, d_rows, nrows, sub);
+         }
+         for (int phase = 0; phase < (variant == 3 ? 0 : 2); phase++) {
             auto screen = phase == 0 ? (steps == 2    ? k_knn_screen<2, 0>
                                         : steps == 4  ? k_knn_screen<4, 0>
                                         : steps == 8  ? k_knn_screen<8, 0>
@@ -815,7 +1284,7 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
          (void)hipStreamSynchronize(s);
          (void)hipFree(lim);
       }
-   } else {
+   } else if (variant == 0) {
       const int ngroups = (nrows + kKnnRows - 1) / kKnnRows;
       // 2 points per thread: 5.6 -> 4.0 s for the n = 1e6, d = 32, lfil = 20 setup; 4 drop to 1 wave per SIMD
       hipLaunchKernelGGL(k_knn_bounded<kKnnPoints>, dim3(std::min(ngroups, 8192)), dim3(kKnnThreads), 0, s, dX, ldim,
@@ -830,7 +1299,7 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
        hipMemcpyAsync(&nfail, dfail + nrows, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
        hipStreamSynchronize(s) != hipSuccess)
       return done(-1);
-   if (variant == 1 && nfail > 64) {
+   if ((variant == 1 || variant == 3 || variant == 4) && nfail > 64) {
       // many rows the fp32 screen could not settle (clustered data far from the origin against its spread):
       // the fp64 two-pass scan on them, in ascending order, before the radix select on what it leaves
       std::vector<int> hrows(nfail);

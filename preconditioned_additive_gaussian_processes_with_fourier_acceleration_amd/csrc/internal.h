@@ -245,11 +245,30 @@ int upload_tap_coeffs();
 int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream);
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream);
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream);
-int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream);
+// the peer-memory exchange of the row split (dist.hip, Nfft4GPAmdDistPeerEnable): every rank's buffer holds
+// two grid slots (epoch parity) of slot_doubles doubles, then one arrival flag (u32 epoch) per window.  A rank
+// writes its grids into its own slot and publishes the window's flag; every rank waits for all ranks' flags
+// (bounded: `spin` polls, then *err = 1 and the wait gives up) and sums the slots in rank order, so every rank
+// holds the same bits.
+struct PeerArgs {
+   char* const* bufs = nullptr;  // device array: the ranks' exchange buffers, rank order (own included)
+   char* own = nullptr;          // this rank's buffer
+   int world = 0;
+   unsigned int epoch = 0;
+   unsigned int* err = nullptr;  // device view of the host-mapped error word
+   long long slot_doubles = 0;
+   long long spin = 0;
+};
+// gsum = the grids of this shard; with A: into this rank's slot of A.epoch, then the windows' flags published
+int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream,
+                        const PeerArgs* A = nullptr);
 // row shards with few blocks: grid from the summed grids + y = beta y + alpha f^2 mu x, then the interpolation
-// with S workgroups per block adding into y atomically (plain matvec)
+// with S workgroups per block adding into y atomically (plain matvec); with A the summed grids come from the
+// ranks' slots (the wait overlaps the y initialisation)
 int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, double alpha, const double* d_x,
-                              double beta, double* d_y, int S, hipStream_t stream);
+                              double beta, double* d_y, int S, hipStream_t stream, const PeerArgs* A = nullptr);
+// d_grid = the rank-order sum of the ranks' slots of A.epoch (after waiting for their flags)
+int launch_peer_sum(const AdditivePlan& P, const PeerArgs& A, double* d_grid, hipStream_t stream);
 // d_dot != nullptr (non-grad): also writes (y, x) to *d_dot (device), one grid-wide reduction in the launch
 int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, double beta, double* d_y,
                   hipStream_t stream, double* d_dot = nullptr);
@@ -434,6 +453,13 @@ int additive_rows(void* str, int* n_local, int* n_global, int* row_begin);
 bool shard_fused_dot_ok(void* str);
 // row shard: grid (summed over the shards) -> y_local = A x_local and *d_dot = (y_local, x_local) locally
 int shard_finish_dot(void* str, const double* grid, const double* x_local, double* y_local, double* d_dot);
+// the row split over the peer exchange (1-D windows only: shard_peer_ok): spread into this rank's slot and
+// publish; then the exchange folded into the grid kernel (or summed into d_grid first: gradient, dot, many blocks)
+bool shard_peer_ok(void* str);
+int shard_spread_peer(void* str, const double* x_local, const PeerArgs& A);
+int shard_peer_sum(void* str, const PeerArgs& A, double* d_grid);
+int shard_finish_peer(void* str, const PeerArgs& A, double* d_grid, int grad, double alpha, const double* x_local,
+                      double beta, double* y_local);
 // what Nfft4GPSolverPcg needs to know about a distributed operator (matvec == Nfft4GPAmdDistMatSymv):
 // the communicator its dot products are summed over (NULL when the vectors are replicated), the global
 // n, and whether q = A p can also form the local (q, p) in its interpolation launch

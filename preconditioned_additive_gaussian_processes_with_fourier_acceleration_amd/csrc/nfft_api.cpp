@@ -661,6 +661,16 @@ int additive_rows(void* str, int* n_local, int* n_global, int* row_begin)
    return 0;
 }
 
+// interpolation workgroups per block of a row shard's split finish (Nfft4GPAmdShardFinish)
+// (deterministic mode: 1 unless NFFT4GP_AMD_SHARD_SPLIT asks -- the split interpolation's y-slices add with
+// unrounded atomics)
+static int shard_split(const AdditivePlan& P)
+{
+   int S = (P.nblocks <= 64 && !P.det) ? 4 : 1;
+   if (const char* e = getenv("NFFT4GP_AMD_SHARD_SPLIT")) S = std::max(1, std::min(16, atoi(e)));
+   return std::min(S, std::max(1, P.ngroups));
+}
+
 // the row-sharded matvec's local interpolation with the fused (y, x) partial dot of these rows
 // (not yet summed over the shards): the q = A p, (q, p) step of a distributed CG
 bool shard_fused_dot_ok(void* str)
@@ -668,6 +678,42 @@ bool shard_fused_dot_ok(void* str)
    PlanExt* E = additive_plan(str);
    if (!E || !E->P.points_ready) return false;
    return E->P.md.on || E->P.nblocks <= kRedMaxBlocks;
+}
+
+bool shard_peer_ok(void* str)
+{
+   PlanExt* E = additive_plan(str);
+   return E && E->P.points_ready && !E->P.md.on;
+}
+
+int shard_spread_peer(void* str, const double* x_local, const PeerArgs& A)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready || E->P.md.on) return -1;
+   AdditivePlan& P = E->P;
+   hipStream_t s = current_stream();
+   if (P.nblocks > 0 && launch_spread(P, x_local, P.d_part, s)) return -1;
+   return launch_reduce_parts(P, P.d_part, nullptr, s, &A);
+}
+
+int shard_peer_sum(void* str, const PeerArgs& A, double* d_grid)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready || E->P.md.on) return -1;
+   return launch_peer_sum(E->P, A, d_grid, current_stream());
+}
+
+int shard_finish_peer(void* str, const PeerArgs& A, double* d_grid, int grad, double alpha, const double* x_local,
+                      double beta, double* y_local)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready || E->P.md.on) return -1;
+   AdditivePlan& P = E->P;
+   hipStream_t s = current_stream();
+   const int S = shard_split(P);
+   if (!grad && S > 1 && !P.timing) return launch_shard_finish_split(P, nullptr, alpha, x_local, beta, y_local, S, s, &A);
+   if (launch_peer_sum(P, A, d_grid, s) || launch_grid_from_sum(P, d_grid, grad, s)) return -1;
+   return launch_interp(P, grad, alpha, x_local, beta, y_local, s);
 }
 
 int shard_finish_dot(void* str, const double* grid, const double* x_local, double* y_local, double* d_dot)
@@ -1036,12 +1082,23 @@ int Nfft4GPAmdShardFinish(void* str, const double* grid, int grad, double alpha,
    // CUs.  Measured per-rank matvec at config C (tools/shard_probe.py, S = 1 / 2 / 4 / 8): 8 GPUs (62 blocks)
    // 31.1 / 31.3 / 29.3 / 32.1 us; 4 GPUs (123 blocks) 41.0 / 43.0 / 45.2 / 50.5; 2 GPUs 59.7 / 66.8 / ...
    // so S = 4 at <= 64 blocks, else 1 (NFFT4GP_AMD_SHARD_SPLIT overrides S)
-   int S = P.nblocks <= 64 ? 4 : 1;
-   if (const char* e = getenv("NFFT4GP_AMD_SHARD_SPLIT")) S = std::max(1, std::min(16, atoi(e)));
-   S = std::min(S, std::max(1, P.ngroups));
+   const int S = shard_split(P);
    if (!grad && S > 1 && !P.timing) return launch_shard_finish_split(P, grid, alpha, x_local, beta, y_local, S, s);
    if (launch_grid_from_sum(P, grid, grad, s)) return -1;
    return launch_interp(P, grad, alpha, x_local, beta, y_local, s);
+}
+
+// debugging: the circulant coefficients H ([nw][64][kNC]) of the last grid pass into out (count doubles at
+// most); returns the number copied, or -1
+long long Nfft4GPAmdDebugShardH(void* str, double* out, long long count)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready || E->P.md.on || !out || !E->P.d_H) return -1;
+   const long long m = std::min(count, (long long)E->P.nw * kNos * kNC);
+   if (hipStreamSynchronize(current_stream()) != hipSuccess ||
+       hipMemcpy(out, E->P.d_H, sizeof(double) * (size_t)m, hipMemcpyDeviceToHost) != hipSuccess)
+      return -1;
+   return m;
 }
 
 long long Nfft4GPAmdShardGridSize(void* str)

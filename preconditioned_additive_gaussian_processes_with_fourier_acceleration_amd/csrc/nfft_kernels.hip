@@ -471,10 +471,69 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
 // interpolation runs S workgroups per block, each over a contiguous range of window groups, adding alpha f^2
 // times its LDS y-slice into y with global atomics.  A shard of config C on 8 GPUs has 62 blocks: the
 // one-workgroup-per-block interpolation runs on 62 of the 256 CUs.
+// ---- the peer exchange (PeerArgs, dist.hip) ----
+// flags after the two slots; slot of the epoch's parity.  A rank two epochs ahead would need this rank's flag
+// of the epoch between, so a slot is never rewritten while a reader still needs it.
+__device__ __forceinline__ unsigned int* peer_flags(char* buf, const PeerArgs& A)
+{
+   return (unsigned int*)(buf + 2 * A.slot_doubles * sizeof(double));
+}
+__device__ __forceinline__ double* peer_slot(char* buf, const PeerArgs& A)
+{
+   return (double*)(buf + (A.epoch & 1u) * A.slot_doubles * sizeof(double));
+}
+
+// after this workgroup's threads wrote window comp of this rank's slot: make the stores visible beyond the
+// device, then release the window's flag (system scope)
+__device__ __forceinline__ void peer_publish(const PeerArgs& A, int comp)
+{
+   __threadfence_system();
+   __syncthreads();
+   if (threadIdx.x == 0)
+      __hip_atomic_store(peer_flags(A.own, A) + comp, A.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// s_g[cell] = sum over ranks r = 0, 1, ... of rank r's slot (window comp), after waiting for the ranks' flags:
+// thread r < world polls rank r's flag (acquire, system scope) at most A.spin times, then sets *A.err and
+// stops waiting (the host fails the next call); the slot values load at system scope (no stale cache line)
+__device__ __forceinline__ void peer_gather(const PeerArgs& A, int comp, double* s_g)
+{
+   const int tid = threadIdx.x;
+   if (tid < A.world) {
+      const unsigned int* f = peer_flags(A.bufs[tid], A) + comp;
+      for (long long it = 0;; it++) {
+         const unsigned int e = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+         if ((int)(e - A.epoch) >= 0) break;
+         if (it >= A.spin) {
+            __hip_atomic_store(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+         }
+         __builtin_amdgcn_s_sleep(8);
+      }
+   }
+   __syncthreads();
+   if (tid < kNos) {
+      double v = 0.0;
+      for (int r = 0; r < A.world; r++) {
+         const double t = __hip_atomic_load(peer_slot(A.bufs[r], A) + (size_t)comp * kNos + tid, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_SYSTEM);
+         v = r == 0 ? t : v + t;  // the first term as is (no 0 + t: -0 stays -0, as in a two-rank all-reduce)
+      }
+      s_g[tid] = v;
+   }
+}
+
+__global__ __launch_bounds__(kGridThreads) void k_peer_sum(PeerArgs A, double* __restrict__ grid)
+{
+   __shared__ double s_g[kNos];
+   peer_gather(A, blockIdx.x, s_g);
+   if (threadIdx.x < kNos) grid[(size_t)blockIdx.x * kNos + threadIdx.x] = s_g[threadIdx.x];
+}
+
 __global__ __launch_bounds__(kGridThreads) void k_grid_sum_yinit(const double* __restrict__ gsum,
                                                                 const double* __restrict__ w, double* __restrict__ H,
                                                                 double* __restrict__ y, const double* __restrict__ x,
-                                                                int n, double beta, double amu)
+                                                                int n, double beta, double amu, PeerArgs A)
 {
    __shared__ double s_g[kNos];
    __shared__ double s_h[kNos];
@@ -484,7 +543,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_sum_yinit(const double* _
    const double wv = tid < kNos ? w[(size_t)comp * kNos + tid] : 0.0;
    double ct[kTaps];
    grid_tail_coeffs(ct);
-   if (tid < kNos) s_g[tid] = gsum[(size_t)comp * kNos + tid];
+   if (!A.bufs && tid < kNos) s_g[tid] = gsum[(size_t)comp * kNos + tid];
    // y init: 4 elements per thread per pass, all loads issued before the first store (one latency per
    // pass instead of one per element)
    constexpr int kU = 4;
@@ -503,6 +562,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_sum_yinit(const double* _
          if (j < (size_t)n) y[j] = (beta == 0.0 ? 0.0 : beta * yv[u]) + amu * xv[u];
       }
    }
+   if (A.bufs) peer_gather(A, comp, s_g);  // after the y initialisation: the peers' spreads overlap it
    __syncthreads();
    grid_tail(comp, s_g, wv, ct, H, s_w, s_h);
 }
@@ -557,8 +617,9 @@ __global__ __launch_bounds__(THREADS) void k_interp_part(const uint16_t* __restr
 // gsum[comp][cell] = sum_b part[comp][b][cell]   (row-sharded path: before the all-reduce).  One
 // workgroup per window, k_grid's 16 strands per cell with 16 loads in flight each (a thread per cell
 // summing the partials one after another took 16 us at an 8-GPU shard of config C)
+// A.bufs: gsum is this rank's slot of A.epoch and the window's flag is published after it
 __global__ __launch_bounds__(kGridThreads) void k_reduce_parts(const double* __restrict__ part, int nparts, int nw,
-                                                              double* __restrict__ gsum)
+                                                              double* __restrict__ gsum, PeerArgs A)
 {
    __shared__ double s_red[kGridThreads];
    const int comp = blockIdx.x;
@@ -586,6 +647,7 @@ __global__ __launch_bounds__(kGridThreads) void k_reduce_parts(const double* __r
       for (int k = 0; k < nstr; k++) v += s_red[k * 64 + tid];
       gsum[(size_t)comp * kNos + tid] = v;
    }
+   if (A.bufs) peer_publish(A, comp);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1031,14 +1093,14 @@ int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int gra
 }
 
 int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, double alpha, const double* d_x,
-                              double beta, double* d_y, int S, hipStream_t stream)
+                              double beta, double* d_y, int S, hipStream_t stream, const PeerArgs* A)
 {
    constexpr int T = 512;
    raise_lds_limit_once();
    if (!abs_lds_ok()) return -1;
    const double ff = P.f * P.f;
    hipLaunchKernelGGL(k_grid_sum_yinit, dim3(P.nw), dim3(kGridThreads), 0, stream, d_gridsum, (const double*)P.d_w,
-                      P.d_H, d_y, d_x, P.n, beta, alpha * ff * P.mu * P.diag);
+                      P.d_H, d_y, d_x, P.n, beta, alpha * ff * P.mu * P.diag, A ? *A : PeerArgs{});
    if (P.n > 0)
       hipLaunchKernelGGL(interp_part_fn(P.rec), dim3(P.nblocks * S), dim3(T), sizeof(double) * (size_t)(P.B + kPad), stream,
                          P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H, d_y, P.n, P.B, P.ngroups, S,
@@ -1047,10 +1109,26 @@ int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, do
    return 0;
 }
 
-int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream)
+int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream,
+                        const PeerArgs* A)
 {
-   hipLaunchKernelGGL(k_reduce_parts, dim3(P.nw), dim3(kGridThreads), 0, stream, d_part, P.nparts, P.nw,
-                      d_gridsum);
+   PeerArgs a = A ? *A : PeerArgs{};
+   if (A) {
+      // this rank's slot of the epoch (the caller's d_gridsum is not used)
+      d_gridsum = (double*)(A->own + (A->epoch & 1u) * A->slot_doubles * sizeof(double));
+      if (A->slot_doubles != (long long)P.nw * kNos) return -1;
+   }
+   // no blocks (a shard without rows): nparts = 0 writes zeros (and publishes them)
+   hipLaunchKernelGGL(k_reduce_parts, dim3(P.nw), dim3(kGridThreads), 0, stream, d_part, P.nblocks ? P.nparts : 0,
+                      P.nw, d_gridsum, a);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int launch_peer_sum(const AdditivePlan& P, const PeerArgs& A, double* d_grid, hipStream_t stream)
+{
+   if (A.slot_doubles != (long long)P.nw * kNos) return -1;
+   hipLaunchKernelGGL(k_peer_sum, dim3(P.nw), dim3(kGridThreads), 0, stream, A, d_grid);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

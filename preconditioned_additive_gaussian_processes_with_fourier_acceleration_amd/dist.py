@@ -211,6 +211,19 @@ class DistributedAdditiveKernel:
     def gradmatsymv(self, x, alpha=1.0, beta=0.0, y=None):
         return self._apply("Nfft4GPAmdDistGradMatSymv", x, alpha, beta, y, 3)
 
+    def enable_peer(self) -> bool:
+        """Row split, 1-D windows: exchange the grids through peer memory instead of the communicator's
+        all-reduce (Nfft4GPAmdDistPeerEnable; collective, after setup).  False when it does not apply or some
+        rank could not export / open its buffer (then every rank keeps the all-reduce).  With it on, free() is
+        collective."""
+        from . import _lib
+        return _lib.lib().Nfft4GPAmdDistPeerEnable(self.h) == 0
+
+    @property
+    def peer_active(self) -> bool:
+        from . import _lib
+        return bool(self.h) and _lib.lib().Nfft4GPAmdDistPeerActive(self.h) == 1
+
     def timing(self, on: bool = True):
         """Per-rank hipEvent timing of every matvec (Nfft4GPAmdDistTimingEnable; enabling resets)."""
         from . import _lib
@@ -251,7 +264,9 @@ class DistributedAdditiveKernel:
 
     def __del__(self):
         try:
-            self.free()
+            # with the peer exchange on, the free is collective: never from the collector of one rank alone
+            if not self.peer_active:
+                self.free()
         except Exception:
             pass
 

@@ -41,8 +41,13 @@ def check_same(X, lfil, expect_few_fallbacks=True):
     a, nf = knn(X, lfil, 1)
     b, _ = knn(X, lfil, 0)
     c, _ = knn(X, lfil, 2)
+    e, nf3 = knn(X, lfil, 3)  # the one-launch 32-row screen
+    f, nf4 = knn(X, lfil, 4)  # the one-launch 256-row bf16-split screen
     n = X.shape[0]
-    assert np.array_equal(a, c) and np.array_equal(b, c)
+    assert np.array_equal(a, c) and np.array_equal(b, c) and np.array_equal(e, c) and np.array_equal(f, c)
+    if expect_few_fallbacks:
+        assert nf3 <= max(2, (n - lfil) // 100), nf3
+        assert nf4 <= max(2, (n - lfil) // 100), nf4
     assert np.array_equal(a[:, -1], np.arange(lfil, n))
     if expect_few_fallbacks:
         assert nf <= max(2, (n - lfil) // 100), nf
@@ -83,17 +88,16 @@ def test_knn_screen_far_from_origin_falls_back_exactly(torch_cuda):
 def test_knn_screen_speed_config_c_slice(torch_cuda):
     """Timing at n = 2e5, d = 32 (config C's features): the screened scans against the fp64 scans."""
     X = np.random.default_rng(906).random((200000, 32))
-    t = {}
-    for v in (1, 0):
+    t, r, nf = {}, {}, {}
+    for v in (4, 3, 1, 0):
         knn(X[:30000], 20, v)
         t0 = time.time()
-        r, nf = knn(X, 20, v)
+        r[v], nf[v] = knn(X, 20, v)
         t[v] = time.time() - t0
-        if v == 1:
-            r1, nf1 = r, nf
-    assert np.array_equal(r1, r)
-    print(f"KNN n=2e5 d=32: screen {t[1]:.3f} s (fallback rows {nf1}), fp64 {t[0]:.3f} s")
-    assert nf1 <= 2000
+    assert np.array_equal(r[1], r[0]) and np.array_equal(r[3], r[0]) and np.array_equal(r[4], r[0])
+    print(f"KNN n=2e5 d=32: tiled screen {t[4]:.3f} s (fallback rows {nf[4]}), one-launch screen {t[3]:.3f} s "
+          f"(fallback rows {nf[3]}), two-launch screen {t[1]:.3f} s (fallback rows {nf[1]}), fp64 {t[0]:.3f} s")
+    assert nf[1] <= 2000 and nf[3] <= 2000 and nf[4] <= 2000
 
 
 @pytest.mark.parametrize("kind", ["random", "clustered"])
@@ -110,6 +114,10 @@ def test_knn_screen_subsampled_count(torch_cuda, kind):
         X = centres[rng.integers(0, 50, n)] + 0.02 * rng.standard_normal((n, d))
     a, nf = knn(X, 20, 1)
     b, _ = knn(X, 20, 0)
-    assert np.array_equal(a, b)
+    e, nf3 = knn(X, 20, 3)
+    f, nf4 = knn(X, 20, 4)
+    assert np.array_equal(a, b) and np.array_equal(e, b) and np.array_equal(f, b)
     if kind == "random":
         assert nf <= (n - 20) // 100, nf
+        assert nf3 <= (n - 20) // 100, nf3
+        assert nf4 <= (n - 20) // 100, nf4

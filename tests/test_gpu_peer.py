@@ -1,0 +1,159 @@
+"""The row split's peer-memory exchange (Nfft4GPAmdDistPeerEnable, dist.hip): two processes
+on one GPU export their grid buffers with hipIpcGetMemHandle and open each other's; a matvec publishes its
+grids into its own slot and the grid kernel sums both ranks' slots in rank order instead of an all-reduce.
+
+In deterministic mode (bitwise reproducible spreads) the matvec, the gradient matvec and a PCG
+over the exchange must equal the callback communicator's (gloo all-reduce) results bit for bit: with two
+ranks a + b is the same sum either way.  The grid kernel that folds the exchange in (k_grid_sum_yinit,
+few-block shards) is checked through its output H, bitwise, and its y to rounding (the split interpolation
+adds with atomics).  A rank that never publishes makes the other rank's wait give up and its next call fail.
+
+Reference behaviour being split: nfft_interface.c:796-817 (components summed one after another).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _worker(rank, world, port, outdir):
+    for p in (ROOT, HERE):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import ctypes as C
+    import torch
+    import torch.distributed as dist
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import (
+        Communicator, DistributedAdditiveKernel)
+    from test_gpu_dist import problem
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Communicator.callback()
+    L = amd.lib()
+    L.Nfft4GPAmdDebugShardH.restype = C.c_longlong
+    L.Nfft4GPAmdDebugShardH.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong]
+    X, win, nw, dw, x = problem("1d")
+    out = {}
+
+    def run(tag, op, xd, b):
+        y = op.matsymv(xd)
+        y0 = torch.full_like(y, 0.25)
+        yb = op.matsymv(xd, 0.7, -1.5, y0)
+        g = op.gradmatsymv(xd)
+        xs = torch.zeros_like(b)
+        _, rr, _, it = amd.pcg(op, b, xs, maxits=2000, tol=1e-6)
+        out.update({f"{tag}_y": y.cpu().numpy(), f"{tag}_yb": yb.cpu().numpy(), f"{tag}_g": g.cpu().numpy(),
+                    f"{tag}_x": xs.cpu().numpy(), f"{tag}_it": it, f"{tag}_rr": rr})
+        # epochs beyond the two slots' parity: every repeat the same bits
+        reps = [op.matsymv(xd).cpu().numpy() for _ in range(5)]
+        out[f"{tag}_reps_same"] = int(all(np.array_equal(r, reps[0]) for r in reps))
+
+    # deterministic mode: the default finish (no split interpolation), every output bitwise
+    op = DistributedAdditiveKernel(X, win, nw, dw, comm, partition="rows")
+    op.local.set_deterministic(True)
+    assert op.setup(amd.GAUSSIAN, f=1.3, l=0.1, mu=0.1) == 0
+    rb, re = op.row_begin, op.row_end
+    xd = torch.tensor(x[rb:re], device="cuda")
+    b = torch.tensor(x[rb:re], device="cuda")
+    run("cb", op, xd, b)
+    on = op.enable_peer()
+    out["peer_on"] = int(on)
+    if on:
+        assert op.peer_active
+        run("peer", op, xd, b)
+    op.free()
+
+    # the fused exchange + grid + y-init kernel (the split finish of few-block shards, forced in det mode)
+    os.environ["NFFT4GP_AMD_SHARD_SPLIT"] = "4"
+    op = DistributedAdditiveKernel(X, win, nw, dw, comm, partition="rows")
+    op.local.set_deterministic(True)
+    assert op.setup(amd.GAUSSIAN, f=1.3, l=0.1, mu=0.1) == 0
+    nh = nw * 64 * 8
+    H = np.zeros(nh)
+    y = op.matsymv(xd)
+    assert L.Nfft4GPAmdDebugShardH(op.local.h, H.ctypes.data, nh) == nh
+    out["split_cb_y"], out["split_cb_H"] = y.cpu().numpy(), H.copy()
+    if op.enable_peer():
+        y = op.matsymv(xd)
+        assert L.Nfft4GPAmdDebugShardH(op.local.h, H.ctypes.data, nh) == nh
+        out["split_peer_y"], out["split_peer_H"] = y.cpu().numpy(), H.copy()
+    op.free()
+    os.environ.pop("NFFT4GP_AMD_SHARD_SPLIT")
+
+    # a rank that never publishes: rank 0's wait gives up (short spin) and its next call fails
+    os.environ["NFFT4GP_AMD_PEER_SPIN"] = "2000"
+    op = DistributedAdditiveKernel(X, win, nw, dw, comm, partition="rows")
+    assert op.setup(amd.GAUSSIAN, f=1.3, l=0.1, mu=0.1) == 0
+    os.environ.pop("NFFT4GP_AMD_PEER_SPIN")
+    if op.enable_peer():
+        if rank == 0:
+            op.matsymv(xd)  # rank 1 is in the barrier below: this exchange times out
+            torch.cuda.synchronize()
+        dist.barrier()
+        if rank == 1:
+            op.matsymv(xd)  # rank 0 published this epoch: completes
+            torch.cuda.synchronize()
+        dist.barrier()
+        try:
+            if rank == 0:
+                op.matsymv(xd)
+            out["fault_raised"] = 0
+        except RuntimeError:
+            out["fault_raised"] = 1
+        torch.cuda.synchronize()
+        dist.barrier()
+    op.free()
+    out["rb"], out["re"] = rb, re
+    torch.cuda.synchronize()
+    comm.free()
+    np.savez(os.path.join(outdir, f"peer_rank{rank}.npz"), **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def peer2(tmp_path_factory):
+    import torch.multiprocessing as mp
+    from test_gpu_dist import _free_port
+    out = tmp_path_factory.mktemp("peer")
+    mp.spawn(_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    return [dict(np.load(os.path.join(out, f"peer_rank{r}.npz"))) for r in range(2)]
+
+
+def test_peer_exchange_enabled_on_one_gpu(peer2):
+    # hipIpcOpenMemHandle of another process's buffer on the same device (DESIGN 6 records a refusal)
+    assert all(int(r["peer_on"]) == 1 for r in peer2)
+
+
+@pytest.mark.parametrize("key", ["y", "yb", "g", "x"])
+def test_peer_exchange_bitwise_equals_callback_allreduce(peer2, key):
+    for r in peer2:
+        np.testing.assert_array_equal(r[f"peer_{key}"], r[f"cb_{key}"])
+
+
+def test_peer_exchange_pcg_iterations_and_repeats(peer2):
+    for r in peer2:
+        assert int(r["peer_it"]) == int(r["cb_it"]) and float(r["peer_rr"]) <= 1e-6
+        assert int(r["peer_reps_same"]) == 1 and int(r["cb_reps_same"]) == 1
+
+
+def test_peer_exchange_fused_grid_kernel(peer2):
+    for r in peer2:
+        np.testing.assert_array_equal(r["split_peer_H"], r["split_cb_H"])
+        y, y0 = r["split_peer_y"], r["split_cb_y"]
+        assert np.linalg.norm(y - y0) <= 1e-14 * np.linalg.norm(y0)
+    # both ranks hold the same circulants (the same summed grids)
+    np.testing.assert_array_equal(peer2[0]["split_peer_H"], peer2[1]["split_peer_H"])
+
+
+def test_peer_exchange_timeout_fails_the_next_call(peer2):
+    assert int(peer2[0]["fault_raised"]) == 1
+    assert int(peer2[1]["fault_raised"]) == 0

@@ -1,0 +1,8 @@
+#!/bin/bash
+# tiled KNN screen at n = 1e6, d = 32: parity tests, full kernel vs the scan alone (NFFT4GP_AMD_KNN_TILE_PROBE)
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_knn.py -s > gpurun_out/knn_tests.log 2>&1 &&
+timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_knn4a -o run -- python3 tools/knn_probe.py --variants 4 > gpurun_out/knn_probe_a.log 2>&1 &&
+NFFT4GP_AMD_KNN_TILE_PROBE=1 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_knn4b -o run -- python3 tools/knn_probe.py --variants 4 > gpurun_out/knn_probe_b.log 2>&1

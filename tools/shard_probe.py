@@ -5,7 +5,12 @@
   N = 8) -- Nfft4GPAdditiveNFFTMatSymv on a handle of windows [0, nw / N) for all n points
   (Nfft4GPAmdAdditiveComponentShard, the mu x term on this rank).
 
-    python tools/shard_probe.py [--ranks 8] [--partition components]
+* rows --peer: the same shard as a distributed operator over the peer-memory exchange (Nfft4GPAmdDistPeerEnable)
+  on a one-process communicator with NFFT4GP_AMD_PEER_FAKE_WORLD = N: the exchange kernels wait for N flags and
+  sum N slots (all this rank's own -- local reads where N GPUs would read N - 1 slots over xGMI), so the time
+  includes the exchange's kernels but not the peers' link latency (timing only; y is not the operator's).
+
+    python tools/shard_probe.py [--ranks 8] [--partition components] [--peer]
 """
 import argparse
 import json
@@ -25,6 +30,7 @@ def main():
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2000)
     ap.add_argument("--partition", default="rows", choices=["rows", "components"])
+    ap.add_argument("--peer", action="store_true")
     args = ap.parse_args()
     import torch
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
@@ -43,6 +49,19 @@ def main():
         h = op.h
         g = L.Nfft4GPAmdShardGridSize(h)
         grid = torch.zeros(g, dtype=torch.float64, device="cuda")
+        if args.peer:
+            import ctypes as C
+            import torch.distributed as dist
+            from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import Communicator
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group("gloo", rank=0, world_size=1)
+            comm = Communicator.callback()
+            L.Nfft4GPAmdDistCreate.restype = C.c_void_p
+            L.Nfft4GPAmdDistCreate.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+            dop = L.Nfft4GPAmdDistCreate(h, 0, comm.h)
+            os.environ["NFFT4GP_AMD_PEER_FAKE_WORLD"] = str(args.ranks)
+            assert L.Nfft4GPAmdDistPeerEnable(C.c_void_p(dop)) == 0
     else:
         re = n
         nwl = d // args.ranks
@@ -54,7 +73,9 @@ def main():
     y = torch.zeros(re, dtype=torch.float64, device="cuda")
 
     def step():
-        if args.partition == "rows":
+        if args.peer:
+            assert L.Nfft4GPAmdDistMatSymv(dop, re, 1.0, x.data_ptr(), 0.0, y.data_ptr()) == 0
+        elif args.partition == "rows":
             assert L.Nfft4GPAmdShardSpread(h, x.data_ptr(), grid.data_ptr()) == 0
             assert L.Nfft4GPAmdShardFinish(h, grid.data_ptr(), 0, 1.0, x.data_ptr(), 0.0, y.data_ptr()) == 0
         else:
@@ -71,7 +92,7 @@ def main():
         step()
     torch.cuda.synchronize()
     us = (time.perf_counter() - t0) / args.reps * 1e6
-    print(json.dumps({"partition": args.partition, "ranks": args.ranks, "rows": re,
+    print(json.dumps({"partition": args.partition + ("+peer" if args.peer else ""), "ranks": args.ranks, "rows": re,
                       "windows": d if args.partition == "rows" else d // args.ranks, "us_per_shard_matvec": us,
                       "y_norm": float(y.norm())}))
 
