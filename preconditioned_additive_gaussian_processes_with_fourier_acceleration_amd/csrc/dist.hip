@@ -617,8 +617,8 @@ int Nfft4GPAmdDistPeerEnable(void* dop)
    if (world < 1 || world > kPeerMaxWorld) return 1;
    hipStream_t s = current_stream();
    PeerState* P = new PeerState();
-   const size_t gcount = D->grid_count, nw = gcount / kNos;
-   const size_t bytes = 2 * gcount * sizeof(double) + (nw * sizeof(unsigned int) + 255) / 256 * 256;
+   const size_t gcount = D->grid_count;
+   const size_t bytes = 2 * gcount * 16;  // two slots of (low, high) words with the epoch (nfft_kernels.hip)
    constexpr size_t HB = sizeof(hipIpcMemHandle_t);
    bool ok = hipMalloc((void**)&P->local, bytes) == hipSuccess && hipMemsetAsync(P->local, 0, bytes, s) == hipSuccess &&
              hipStreamSynchronize(s) == hipSuccess;
@@ -694,6 +694,7 @@ int Nfft4GPAmdDistPeerEnable(void* dop)
    long long spin = 1ll << 20;  // ~2 s of polls (each a system-scope load and an s_sleep)
    if (const char* e = getenv("NFFT4GP_AMD_PEER_SPIN")) spin = std::max(1ll, atoll(e));
    P->a.bufs = P->d_bufs;
+   for (int r = 0; r < kPeerInline && r < (int)bufs.size(); r++) P->a.inl[r] = bufs[r];
    P->a.own = P->local;
    P->a.world = fake > 1 ? fake : world;
    P->a.epoch = 0u;

@@ -162,6 +162,7 @@ struct MdComp {
 };
 struct MdPlan {
    bool on = false;
+   bool gfix_per_window = false;  // d_gfix holds one window's fixed-point grid (nfft_md.hip md_spread)
    int maxd = 1;
    long long G = 0;          // 64^maxd: real grid stride per component
    long long Cmax = 0;       // 32 * 64^(maxd-1): complex pass buffer stride per component
@@ -246,12 +247,14 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream);
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream);
 // the peer-memory exchange of the row split (dist.hip, Nfft4GPAmdDistPeerEnable): every rank's buffer holds
-// two grid slots (epoch parity) of slot_doubles doubles, then one arrival flag (u32 epoch) per window.  A rank
-// writes its grids into its own slot and publishes the window's flag; every rank waits for all ranks' flags
-// (bounded: `spin` polls, then *err = 1 and the wait gives up) and sums the slots in rank order, so every rank
-// holds the same bits.
+// two grid slots (epoch parity) of slot_doubles entries, each entry two 64-bit words carrying the epoch
+// (nfft_kernels.hip).  A rank writes its grids into its own slot; every rank waits until all ranks' entries
+// carry the epoch (bounded: `spin` polls, then *err = 1 and the wait gives up) and sums them in rank order, so
+// every rank holds the same bits.
+constexpr int kPeerInline = 8;  // ranks whose buffer pointers travel in the kernel arguments
 struct PeerArgs {
    char* const* bufs = nullptr;  // device array: the ranks' exchange buffers, rank order (own included)
+   char* inl[kPeerInline] = {};  // the first kPeerInline of them (scalar loads, no dependent global load)
    char* own = nullptr;          // this rank's buffer
    int world = 0;
    unsigned int epoch = 0;

@@ -472,55 +472,73 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
 // times its LDS y-slice into y with global atomics.  A shard of config C on 8 GPUs has 62 blocks: the
 // one-workgroup-per-block interpolation runs on 62 of the 256 CUs.
 // ---- the peer exchange (PeerArgs, dist.hip) ----
-// flags after the two slots; slot of the epoch's parity.  A rank two epochs ahead would need this rank's flag
-// of the epoch between, so a slot is never rewritten while a reader still needs it.
-__device__ __forceinline__ unsigned int* peer_flags(char* buf, const PeerArgs& A)
+// A rank's buffer holds two slots (the epoch's parity) of nw x 64 entries; an entry is two 64-bit words, the
+// low and the high half of the double's bits, each with the epoch in its upper 32 bits.  A 64-bit store is
+// single-copy atomic, so a reader that sees the epoch in both words has the value -- one round trip, no
+// separate flag and no fence (a release here would write back the whole L2, an acquire invalidate it: 9 us
+// per matvec at N = 8 in the first version).  Every word is stored and loaded at system scope (written
+// through to memory, never served stale from a cache).  A rank two epochs ahead would need this rank's
+// entries of the epoch in between, so a slot is never rewritten while a reader still needs it.
+constexpr int kPeerLanes = kGridThreads / 64;  // ranks gathered per pass (a wave per rank, a lane per cell)
+
+__device__ __forceinline__ unsigned long long* peer_slot(char* buf, const PeerArgs& A)
 {
-   return (unsigned int*)(buf + 2 * A.slot_doubles * sizeof(double));
-}
-__device__ __forceinline__ double* peer_slot(char* buf, const PeerArgs& A)
-{
-   return (double*)(buf + (A.epoch & 1u) * A.slot_doubles * sizeof(double));
+   return (unsigned long long*)(buf + (A.epoch & 1u) * A.slot_doubles * 16);
 }
 
-// after this workgroup's threads wrote window comp of this rank's slot: make the stores visible beyond the
-// device, then release the window's flag (system scope)
-__device__ __forceinline__ void peer_publish(const PeerArgs& A, int comp)
+// rank r's buffer: the first kPeerInline from the kernel arguments (no dependent global load), then the table
+__device__ __forceinline__ char* peer_buf(const PeerArgs& A, int r)
 {
-   __threadfence_system();
-   __syncthreads();
-   if (threadIdx.x == 0)
-      __hip_atomic_store(peer_flags(A.own, A) + comp, A.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+   char* b = A.inl[0];
+#pragma unroll
+   for (int k = 1; k < kPeerInline; k++)
+      if (r == k) b = A.inl[k];
+   return r < kPeerInline ? b : A.bufs[r];
 }
 
-// s_g[cell] = sum over ranks r = 0, 1, ... of rank r's slot (window comp), after waiting for the ranks' flags:
-// thread r < world polls rank r's flag (acquire, system scope) at most A.spin times, then sets *A.err and
-// stops waiting (the host fails the next call); the slot values load at system scope (no stale cache line)
+// this rank's value of (window comp, cell) into its slot of the epoch
+__device__ __forceinline__ void peer_put(const PeerArgs& A, int comp, int cell, double v)
+{
+   unsigned long long* p = peer_slot(A.own, A) + 2 * ((size_t)comp * kNos + cell);
+   const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+   const unsigned long long e = (unsigned long long)A.epoch << 32;
+   __hip_atomic_store(p, (bits & 0xffffffffull) | e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+   __hip_atomic_store(p + 1, (bits >> 32) | e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// s_g[cell] = sum over ranks r = 0, 1, ... (in that order) of rank r's value of (comp, cell).  Wave w of the
+// workgroup polls rank r0 + w's entries (lane = cell) until both words carry the epoch -- at most A.spin
+// polls, then it sets *A.err and gives up (the host fails the next call) -- so up to kPeerLanes ranks' loads
+// are in flight at once; the sum runs over LDS in rank order, the first term as is (no 0 + t: -0 stays -0,
+// as in a two-rank all-reduce).  Every thread of the workgroup calls it.
 __device__ __forceinline__ void peer_gather(const PeerArgs& A, int comp, double* s_g)
 {
-   const int tid = threadIdx.x;
-   if (tid < A.world) {
-      const unsigned int* f = peer_flags(A.bufs[tid], A) + comp;
-      for (long long it = 0;; it++) {
-         const unsigned int e = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-         if ((int)(e - A.epoch) >= 0) break;
-         if (it >= A.spin) {
-            __hip_atomic_store(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
+   __shared__ double s_v[kPeerLanes][kNos];
+   const int tid = threadIdx.x, cell = tid & (kNos - 1), lr = tid / kNos;
+   double v = 0.0;
+   for (int r0 = 0; r0 < A.world; r0 += kPeerLanes) {
+      const int r = r0 + lr;
+      if (r < A.world) {
+         const unsigned long long* p = peer_slot(peer_buf(A, r), A) + 2 * ((size_t)comp * kNos + cell);
+         unsigned long long w0, w1;
+         for (long long it = 0;; it++) {
+            w0 = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            w1 = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((unsigned int)(w0 >> 32) == A.epoch && (unsigned int)(w1 >> 32) == A.epoch) break;
+            if (it >= A.spin) {
+               __hip_atomic_store(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+               break;
+            }
+            __builtin_amdgcn_s_sleep(2);
          }
-         __builtin_amdgcn_s_sleep(8);
+         s_v[lr][cell] = __longlong_as_double((long long)((w0 & 0xffffffffull) | (w1 << 32)));
       }
+      __syncthreads();
+      if (tid < kNos)
+         for (int k = 0; k < kPeerLanes && r0 + k < A.world; k++) v = (r0 + k == 0) ? s_v[k][tid] : v + s_v[k][tid];
+      __syncthreads();
    }
-   __syncthreads();
-   if (tid < kNos) {
-      double v = 0.0;
-      for (int r = 0; r < A.world; r++) {
-         const double t = __hip_atomic_load(peer_slot(A.bufs[r], A) + (size_t)comp * kNos + tid, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_SYSTEM);
-         v = r == 0 ? t : v + t;  // the first term as is (no 0 + t: -0 stays -0, as in a two-rank all-reduce)
-      }
-      s_g[tid] = v;
-   }
+   if (tid < kNos) s_g[tid] = v;
 }
 
 __global__ __launch_bounds__(kGridThreads) void k_peer_sum(PeerArgs A, double* __restrict__ grid)
@@ -617,7 +635,7 @@ __global__ __launch_bounds__(THREADS) void k_interp_part(const uint16_t* __restr
 // gsum[comp][cell] = sum_b part[comp][b][cell]   (row-sharded path: before the all-reduce).  One
 // workgroup per window, k_grid's 16 strands per cell with 16 loads in flight each (a thread per cell
 // summing the partials one after another took 16 us at an 8-GPU shard of config C)
-// A.bufs: gsum is this rank's slot of A.epoch and the window's flag is published after it
+// A.bufs: the sums go to this rank's slot of A.epoch (peer_put) instead of gsum
 __global__ __launch_bounds__(kGridThreads) void k_reduce_parts(const double* __restrict__ part, int nparts, int nw,
                                                               double* __restrict__ gsum, PeerArgs A)
 {
@@ -645,9 +663,11 @@ __global__ __launch_bounds__(kGridThreads) void k_reduce_parts(const double* __r
    if (tid < kNos) {
       double v = 0.0;
       for (int k = 0; k < nstr; k++) v += s_red[k * 64 + tid];
-      gsum[(size_t)comp * kNos + tid] = v;
+      if (A.bufs)
+         peer_put(A, comp, tid, v);
+      else
+         gsum[(size_t)comp * kNos + tid] = v;
    }
-   if (A.bufs) peer_publish(A, comp);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1113,11 +1133,7 @@ int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_g
                         const PeerArgs* A)
 {
    PeerArgs a = A ? *A : PeerArgs{};
-   if (A) {
-      // this rank's slot of the epoch (the caller's d_gridsum is not used)
-      d_gridsum = (double*)(A->own + (A->epoch & 1u) * A->slot_doubles * sizeof(double));
-      if (A->slot_doubles != (long long)P.nw * kNos) return -1;
-   }
+   if (A && A->slot_doubles != (long long)P.nw * kNos) return -1;  // with A: this rank's slot (peer_put)
    // no blocks (a shard without rows): nparts = 0 writes zeros (and publishes them)
    hipLaunchKernelGGL(k_reduce_parts, dim3(P.nw), dim3(kGridThreads), 0, stream, d_part, P.nblocks ? P.nparts : 0,
                       P.nw, d_gridsum, a);

@@ -66,9 +66,11 @@ __device__ __forceinline__ double tap_row(const int* uj, const double* pj, int d
 // in two separate 64-bit integer accumulators (LDS ds_add_u64, then global atomic adds, no return values).
 // Integer adds are exact, so each cell's pair (sum H, sum L) -- and its value (sum H) 2^32 + sum L -- is the
 // same whatever order the atomics run in: the spread, hence the matvec, is bitwise reproducible.
-// s_c = 94 - ilogb(B_c) with the bound B_c = n max|x| psi_max^d_c >= every |partial sum| of component c (d_c
-// features), so |sum H| < 2^62 and sum L < n 2^32 <= 2^63 never overflow, and one contribution is rounded at
-// 2^-94 B_c (B_c can exceed a cell's value by ~2^22: still ~2^-72 of it).  k_md_fix2f forms the doubles.
+// s_c = 93 - ilogb(B_c) with the bound B_c = n max|x| psi_max^d_c >= every |partial sum| of component c (d_c
+// features): B_c < 2^(ilogb(B_c) + 1), so |sum A| < 2^94, |sum H| < 2^62 and sum L < n 2^32 <= 2^63 never
+// overflow, and one contribution is rounded at 2^-93 B_c (B_c can exceed a cell's value by ~2^22: still ~2^-71
+// of it).  k_md_fix2f forms the doubles.  x with a NaN or an infinity (or B_c >= 1e300, beyond the fixed
+// point's range) makes every grid value NaN, so the matvec returns NaN as the fp64 sums would.
 __global__ void k_md_absmax(const double* __restrict__ x, int n, unsigned long long* __restrict__ out)
 {
    unsigned long long m = 0ull;
@@ -83,7 +85,16 @@ __device__ __forceinline__ int fix_exp(const unsigned long long* xmax, double n,
 {
    double B = __longlong_as_double((long long)*xmax) * n;
    for (int t = 0; t < dc; t++) B *= psi_max;
-   return (B > 0.0 && B < 1e300) ? 94 - ilogb(B) : 0;
+   return (B > 0.0 && B < 1e300) ? 93 - ilogb(B) : 0;
+}
+
+// B_c out of the fixed point's range: x holds a NaN or an infinity (their bits order above every finite
+// |x|), or n max|x| psi_max^d_c >= 1e300
+__device__ __forceinline__ bool fix_out_of_range(const unsigned long long* xmax, double n, double psi_max, int dc)
+{
+   double B = __longlong_as_double((long long)*xmax) * n;
+   for (int t = 0; t < dc; t++) B *= psi_max;
+   return !(B < 1e300);
 }
 
 // a 2^s = H 2^32 + L (truncated below 2^0): t = a 2^(s-32), H = floor(t), L = (t - H) 2^32
@@ -103,19 +114,21 @@ __device__ __forceinline__ void fix_add(unsigned long long* acc, unsigned long l
    if (H) atomicAdd(acc + 1, (unsigned long long)H);
 }
 
-// grid[c][i] = ((sum H) 2^32 + sum L) 2^-s_c; blockIdx.y = component c; fx: [c][i][sum L, sum H]
+// grid[c][i] = ((sum H) 2^32 + sum L) 2^-s_c; component c = c0 + blockIdx.y; fx: [blockIdx.y][i][sum L, sum H]
+// (the launch's components only: all of them, or one at a time for large grids, MdPlan::gfix_per_window)
 __global__ void k_md_fix2f(const MdComp* __restrict__ comps, const unsigned long long* __restrict__ fx, long long G,
                            const unsigned long long* __restrict__ xmax, double n, double psi_max,
-                           double* __restrict__ grid)
+                           double* __restrict__ grid, int c0)
 {
-   const int c = blockIdx.y;
+   const int c = c0 + blockIdx.y;
    const int e = fix_exp(xmax, n, psi_max, comps[c].d);
-   fx += 2 * (long long)c * G;
+   const bool nan = fix_out_of_range(xmax, n, psi_max, comps[c].d);
+   fx += 2 * (long long)blockIdx.y * G;
    grid += (long long)c * G;
    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (long long)gridDim.x * blockDim.x) {
       const double lo = (double)fx[2 * i];
       const double hi = (double)(long long)fx[2 * i + 1];
-      grid[i] = ldexp(fma(hi, 4294967296.0, lo), -e);
+      grid[i] = nan ? __longlong_as_double(0x7ff8000000000000ll) : ldexp(fma(hi, 4294967296.0, lo), -e);
    }
 }
 
@@ -124,9 +137,10 @@ __global__ __launch_bounds__(kMdThreads) void k_md_spread(const MdComp* __restri
                                                           const int* __restrict__ u, const double* __restrict__ psi,
                                                           const double* __restrict__ x, int n, int hi_max,
                                                           unsigned long long* __restrict__ grid, long long G,
-                                                          const unsigned long long* __restrict__ xmax, double psi_max)
+                                                          const unsigned long long* __restrict__ xmax, double psi_max,
+                                                          int c0)
 {
-   const MdComp cp = comps[blockIdx.y];
+   const MdComp cp = comps[c0 + blockIdx.y];  // grid: the launch's components (blockIdx.y) only
    const long long idx = (long long)blockIdx.x * kMdThreads + threadIdx.x;
    if (idx >= (long long)n * hi_max) return;
    const int j = (int)(idx / hi_max), hi = (int)(idx % hi_max);
@@ -800,8 +814,12 @@ int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
        dalloc(&D.d_B[1], nw * D.Cmax) || dalloc(&D.d_B[2], nw * D.Cmax) || dalloc(&D.d_B[3], nw * D.Cmax) ||
        dalloc(&D.d_h[0], nw * D.G) || dalloc(&D.d_h[1], nw * D.G) || dalloc(&D.d_bh, nw * D.M) ||
        dalloc(&D.d_bhd, nw * D.M) || dalloc(&D.d_dot_part, (size_t)kMdInterpBlocks) ||
-       dalloc(&D.d_dot_ticket, (size_t)kTicketWords) || dalloc(&D.d_gfix, 2 * nw * D.G) || dalloc(&D.d_xmax, 1))
+       dalloc(&D.d_dot_ticket, (size_t)kTicketWords) || dalloc(&D.d_xmax, 1))
       return -1;
+   // the spread's fixed-point grids (16 B per cell): every window's at once, or -- windows beyond the tiled
+   // kernels (4 features: 64^4 cells) whose set would pass 256 MB -- one window's, reused window by window
+   D.gfix_per_window = D.maxd > kMdTiledMaxDim && nw > 1 && 16.0 * (double)nw * (double)D.G > 256.0 * (1 << 20);
+   if (dalloc(&D.d_gfix, 2 * (D.gfix_per_window ? 1 : nw) * D.G)) return -1;
    D.psi_max = 0.0;
    for (double v : psi) D.psi_max = std::max(D.psi_max, std::fabs(v));
    NFFT4GP_HIP_CHECK(hipMemcpy(D.d_comps, D.comps.data(), sizeof(MdComp) * nw, hipMemcpyHostToDevice));
@@ -909,6 +927,7 @@ int md_setup(AdditivePlan& P)
 }
 
 static int md_spread_fix(const AdditivePlan& P, const double* d_x, double psi_max, hipStream_t s);
+static int md_spread_untiled(const AdditivePlan& P, const double* d_x, double psi_max, int c0, int nc, hipStream_t s);
 
 int md_spread(const AdditivePlan& P, const double* d_x, double* d_grid, hipStream_t s)
 {
@@ -919,13 +938,26 @@ int md_spread(const AdditivePlan& P, const double* d_x, double* d_grid, hipStrea
       return 0;
    }
    // fixed-point bounds n max|x| psi_max^d_c (max|x| on the device)
-   NFFT4GP_HIP_CHECK(hipMemsetAsync(D.d_gfix, 0, 2 * sizeof(unsigned long long) * count, s));
    NFFT4GP_HIP_CHECK(hipMemsetAsync(D.d_xmax, 0, sizeof(unsigned long long), s));
    hipLaunchKernelGGL(k_md_absmax, dim3(std::min(1024, (P.n + 255) / 256)), dim3(256), 0, s, d_x, P.n, D.d_xmax);
+   const unsigned gx = (unsigned)std::min<long long>(4096, (D.G + 255) / 256);
+   if (D.gfix_per_window) {
+      // one window's fixed-point grid at a time (4-feature windows: 64^4 cells, 268 MB each), untiled spread
+      for (int c = 0; c < P.nw; c++) {
+         NFFT4GP_HIP_CHECK(hipMemsetAsync(D.d_gfix, 0, 2 * sizeof(unsigned long long) * D.G, s));
+         if (md_spread_untiled(P, d_x, D.psi_max, c, 1, s)) return -1;
+         hipLaunchKernelGGL(k_md_fix2f, dim3(gx, 1), dim3(256), 0, s, (const MdComp*)D.d_comps,
+                            (const unsigned long long*)D.d_gfix, D.G, (const unsigned long long*)D.d_xmax, (double)P.n,
+                            D.psi_max, d_grid, c);
+      }
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   }
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(D.d_gfix, 0, 2 * sizeof(unsigned long long) * count, s));
    if (md_spread_fix(P, d_x, D.psi_max, s)) return -1;
-   hipLaunchKernelGGL(k_md_fix2f, dim3((unsigned)std::min<long long>(4096, (D.G + 255) / 256), P.nw), dim3(256), 0, s,
-                      (const MdComp*)D.d_comps, (const unsigned long long*)D.d_gfix, D.G,
-                      (const unsigned long long*)D.d_xmax, (double)P.n, D.psi_max, d_grid);
+   hipLaunchKernelGGL(k_md_fix2f, dim3(gx, P.nw), dim3(256), 0, s, (const MdComp*)D.d_comps,
+                      (const unsigned long long*)D.d_gfix, D.G, (const unsigned long long*)D.d_xmax, (double)P.n,
+                      D.psi_max, d_grid, 0);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -967,12 +999,19 @@ static int md_spread_fix(const AdditivePlan& P, const double* d_x, double psi_ma
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return 0;
    }
+   return md_spread_untiled(P, d_x, psi_max, 0, P.nw, s);
+}
+
+// the untiled spread of components [c0, c0 + nc) into D.d_gfix's first nc windows
+static int md_spread_untiled(const AdditivePlan& P, const double* d_x, double psi_max, int c0, int nc, hipStream_t s)
+{
+   const MdPlan& D = P.md;
    int hi_max = 1;
    for (int t = 1; t < D.maxd; t++) hi_max *= kTaps;
    const long long work = (long long)P.n * hi_max;
-   hipLaunchKernelGGL(k_md_spread, dim3((unsigned)((work + kMdThreads - 1) / kMdThreads), P.nw), dim3(kMdThreads), 0,
+   hipLaunchKernelGGL(k_md_spread, dim3((unsigned)((work + kMdThreads - 1) / kMdThreads), nc), dim3(kMdThreads), 0,
                       s, D.d_comps, D.d_u, D.d_psi, d_x, P.n, hi_max, D.d_gfix, D.G,
-                      (const unsigned long long*)D.d_xmax, psi_max);
+                      (const unsigned long long*)D.d_xmax, psi_max, c0);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }

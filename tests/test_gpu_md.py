@@ -251,3 +251,45 @@ def test_window_of_four_features_matches_fixture(torch_cuda):
     for i in range(3):
         assert rel(g[i * n:(i + 1) * n], z["g_nfft"][i * n:(i + 1) * n]) < TOL, i
     assert rel(z["y_nfft"], z["y_dense"]) < 1e-2
+
+
+def test_nan_in_x_gives_nan(torch_cuda):
+    """the fixed-point spread must not turn a NaN in x into finite values (the fp64 sums of the
+    reference propagate it): every output is NaN, for 3-D windows (tiled / line spread) and 2-D ones."""
+    torch = torch_cuda
+    rng = np.random.default_rng(3)
+    X = rng.random((3000, 6))
+    for win, nw, dw in ((np.arange(6, dtype=np.int32), 2, 3), (np.arange(6, dtype=np.int32), 3, 2)):
+        op = amd.NFFTAdditiveKernel(X, win, nw, dw)
+        assert op.setup(0, 1.0, 0.5, 0.1) == 0
+        x = rng.random(3000) - 0.5
+        x[17] = np.nan
+        y = op.matsymv(torch.tensor(x, device="cuda")).cpu().numpy()
+        assert np.isnan(y).all()
+        x[17] = np.inf
+        y = op.matsymv(torch.tensor(x, device="cuda")).cpu().numpy()
+        assert np.isnan(y).all()
+        op.free()
+
+
+def test_two_windows_of_four_features_one_fixed_point_grid_at_a_time(torch_cuda):
+    """two 4-feature windows (2 x 64^4 cells) spread one window at a time through one window's
+    fixed-point buffer (MdPlan::gfix_per_window): the operator is half the sum of the two one-window
+    operators (weight 1/nw, mu once), and bitwise reproducible."""
+    torch = torch_cuda
+    rng = np.random.default_rng(4)
+    n = 2000
+    X = rng.random((n, 8))
+    x = torch.tensor(rng.random(n) - 0.5, device="cuda")
+    op = amd.NFFTAdditiveKernel(X, np.arange(8, dtype=np.int32), 2, 4)
+    assert op.setup(0, 1.2, 0.4, 0.05) == 0
+    y = op.matsymv(x).cpu().numpy()
+    assert np.array_equal(y, op.matsymv(x).cpu().numpy())
+    parts = []
+    for c in range(2):
+        o1 = amd.NFFTAdditiveKernel(X, np.arange(4 * c, 4 * c + 4, dtype=np.int32), 1, 4)
+        assert o1.setup(0, 1.2, 0.4, 0.05) == 0
+        parts.append(o1.matsymv(x).cpu().numpy())
+        o1.free()
+    assert rel(y, 0.5 * (parts[0] + parts[1])) < 1e-12
+    op.free()
