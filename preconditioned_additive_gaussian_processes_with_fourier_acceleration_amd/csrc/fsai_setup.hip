@@ -956,7 +956,9 @@ __global__ __launch_bounds__(256) void k_knn_prep_bf(const double* __restrict__ 
    if ((threadIdx.x & 63) == 0) atomicMax(m2, mx);
 }
 
-template <int KCH>
+// DIRECT: every wave loads its B fragments from global memory itself (the eight waves read the same lines close
+// together: L1 / L2 hits), two tiles ahead in registers -- no LDS stages and no barriers in the scan
+template <int KCH, bool DIRECT>
 __global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ X, int ldim,
                                                      const uint4* __restrict__ Xb, const float* __restrict__ nx,
                                                      int n, int d, int lfil, float margin2,
@@ -1005,8 +1007,10 @@ __global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ 
       const int rowmin = row_of(0);
       const unsigned long long below = (1ull << lane) - 1ull;
       int cntv = 0;  // lane l < 32: candidates of the wave's row l
-      for (int t = tid; t < 2 * BLK; t += kScrThreads) S.pts[0][t] = Xb[t];
-      if (tid < kTileStep) S.nx[0][tid] = nx[tid];
+      if (!DIRECT) {
+         for (int t = tid; t < 2 * BLK; t += kScrThreads) S.pts[0][t] = Xb[t];
+         if (tid < kTileStep) S.nx[0][tid] = nx[tid];
+      }
       __syncthreads();
 #pragma unroll
       for (int v = 0; v < 16; v++) thr[v] = S.thr[32 * wave + (v & 3) + 8 * (v >> 2) + 4 * h];
@@ -1022,10 +1026,6 @@ __global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ 
          pr = Xb[(size_t)t * 2 * BLK + tq];
          pn = nx[(size_t)t * kTileStep + tn];
       };
-      fetch(1, p1, n1);
-      fetch(2, p2, n2);
-      fetch(3, p3, n3);
-      fetch(4, p0, n0);
       // a 32-point tile's keys: B fragments from the stage, six MFMAs on the three-term split
       auto mfma_tile = [&](int buf, int sub) {
          const float nxj = S.nx[buf][32 * sub + col];
@@ -1125,16 +1125,62 @@ __global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ 
          fetch(s + 5, pr, pn);
          __syncthreads();
       };
-      for (int s0 = 0; s0 < nsteps; s0 += 4) {
-         stage(s0, p1, n1);
-         if (s0 + 1 >= nsteps) break;
-         stage(s0 + 1, p2, n2);
-         if (s0 + 2 >= nsteps) break;
-         stage(s0 + 2, p3, n3);
-         if (s0 + 3 >= nsteps) break;
-         stage(s0 + 3, p0, n0);
+      if constexpr (!DIRECT) {
+         fetch(1, p1, n1);
+         fetch(2, p2, n2);
+         fetch(3, p3, n3);
+         fetch(4, p0, n0);
+         for (int s0 = 0; s0 < nsteps; s0 += 4) {
+            stage(s0, p1, n1);
+            if (s0 + 1 >= nsteps) break;
+            stage(s0 + 1, p2, n2);
+            if (s0 + 2 >= nsteps) break;
+            stage(s0 + 2, p3, n3);
+            if (s0 + 3 >= nsteps) break;
+            stage(s0 + 3, p0, n0);
+         }
+         if (nsteps > 0) test_tile(c1, nsteps * kTileStep - 32);
+      } else {
+         const int ntl = (ilast + 31) / 32;  // 32-point tiles
+         uint4 ah0[KCH], al0[KCH], ah1[KCH], al1[KCH];
+         float nx0, nx1;
+         auto fetchf = [&](int t, uint4 (&fh)[KCH], uint4 (&fl)[KCH], float& fn) {
+            t = min(t, ntl - 1);
+            const uint4* blk = Xb + (size_t)t * BLK + col;
+#pragma unroll
+            for (int ch = 0; ch < KCH; ch++) {
+               fh[ch] = blk[((ch * 2 + 0) * 2 + h) * 32];
+               fl[ch] = blk[((ch * 2 + 1) * 2 + h) * 32];
+            }
+            fn = nx[(size_t)t * 32 + col];
+         };
+         auto mfma_frag = [&](const uint4 (&fh)[KCH], const uint4 (&fl)[KCH], float fn) {
+            f32x16 c;
+#pragma unroll
+            for (int v = 0; v < 16; v++) c[v] = fmaf(fn, -0.5f, nqh[v]);
+#pragma unroll
+            for (int ch = 0; ch < KCH; ch++) {
+               const bf16x8 bh = __builtin_bit_cast(bf16x8, fh[ch]), bl = __builtin_bit_cast(bf16x8, fl[ch]);
+               c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ch], bl, c, 0, 0, 0);
+               c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ch], bh, c, 0, 0, 0);
+               c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ch], bh, c, 0, 0, 0);
+            }
+            return c;
+         };
+         fetchf(0, ah0, al0, nx0);
+         fetchf(1, ah1, al1, nx1);
+         for (int t0 = 0; t0 < ntl; t0 += 2) {
+            c0 = mfma_frag(ah0, al0, nx0);
+            fetchf(t0 + 2, ah0, al0, nx0);
+            if (t0 > 0) test_tile(c1, t0 * 32 - 32);
+            if (t0 + 1 < ntl) {
+               c1 = mfma_frag(ah1, al1, nx1);
+               fetchf(t0 + 3, ah1, al1, nx1);
+            }
+            test_tile(c0, t0 * 32);
+         }
+         if (ntl % 2 == 0) test_tile(c1, (ntl - 1) * 32);
       }
-      if (nsteps > 0) test_tile(c1, nsteps * kTileStep - 32);
       if (lane < 32) S.cnt[32 * wave + lane] = cntv;
       // exact fp64 keys of the candidates (one per lane) and the (key, index) ranking; the wave's rows
       for (int rl = 0; rl < 32; rl++) {
@@ -1171,7 +1217,9 @@ __global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ 
 template <class T>
 int upload(T** d, const T* h, size_t count);
 
-// KNN pattern rows [lfil, n) into dja (CSR row pointers dia): variant 1 (default) the fp32-screened scans,
+// KNN pattern rows [lfil, n) into dja (CSR row pointers dia): variant 4 (default) the tiled one-launch screen
+// (k_knn_tile; d <= 32 and lfil <= 25, else variant 3), 3 the one-launch 32-row screen (k_knn_screen PHASE 2),
+// 1 the two-launch count + collect screens,
 // 0 the fp64 k_knn_bounded, 2 the radix-select k_knn for every row; the rows the bounded variants leave go
 // to k_knn.  Returns the number of such rows, or -1.
 int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* dia, int* dja, hipStream_t s,
@@ -1180,7 +1228,7 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
    if (n <= lfil || (d_rows && nrows_list <= 0)) return 0;
    if (variant < 0) {
       const char* e = getenv("NFFT4GP_AMD_KNN");
-      variant = e ? atoi(e) : 1;
+      variant = e ? atoi(e) : 4;
    }
    if (d > kKnnMaxDims2) variant = 2;
    const int nrows = d_rows ? nrows_list : n - lfil;
@@ -1224,7 +1272,9 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
       const double margin = (16.0 * d + 448.0) * std::ldexp(1.0, -24) * (double)m2;
       if (std::isfinite(m2) && m2 >= std::ldexp(1.0f, -60) && std::isfinite((float)(2.0 * margin))) {
          const int ngroups = (nrows + kTileRows - 1) / kTileRows;
-         auto tile = kch == 1 ? k_knn_tile<1> : k_knn_tile<2>;
+         static const bool direct = getenv("NFFT4GP_AMD_KNN_TILE_DIRECT") && atoi(getenv("NFFT4GP_AMD_KNN_TILE_DIRECT"));
+         auto tile = kch == 1 ? (direct ? k_knn_tile<1, true> : k_knn_tile<1, false>)
+                              : (direct ? k_knn_tile<2, true> : k_knn_tile<2, false>);
          hipLaunchKernelGGL(tile, dim3(std::min(ngroups, 65535)), dim3(kScrThreads), 0, s, dX, ldim, (const uint4*)Xf,
                             (const float*)nx, n, d, lfil, (float)(2.0 * margin) * 1.0001f, dia, dja, dfail,
                             dfail + nrows, d_rows, nrows, getenv("NFFT4GP_AMD_KNN_TILE_PROBE") ? 1 : 0);

@@ -1,0 +1,10 @@
+# round-5 final evidence, part 3: SQ / LDS counter passes, and the N > 1 bench rehearsed with 2 gloo ranks
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 600 python tools/pmc_sq.py --out gpurun_out/pmc_sq.csv > gpurun_out/pmc_sq.log 2>&1 || { echo PMC_SQ_FAIL; tail -20 gpurun_out/pmc_sq.log; exit 1; }
+tail -2 gpurun_out/pmc_sq.log
+rm -rf gpurun_out/pmc_sq
+NFFT4GP_BENCH_BACKEND=gloo timeout -k 10 540 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > gpurun_out/bench_gloo2.json 2> gpurun_out/bench_gloo2.err || { echo GLOO2_FAIL; tail -30 gpurun_out/bench_gloo2.err; exit 1; }
+head -c 600 gpurun_out/bench_gloo2.json
+NFFT4GP_BENCH_BACKEND=gloo timeout -k 10 540 python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline --no-traffic --no-pcg > gpurun_out/bench_gloo2_self.json 2> gpurun_out/bench_gloo2_self.err || { echo GLOO2_SELF_FAIL; tail -30 gpurun_out/bench_gloo2_self.err; exit 1; }
+head -c 600 gpurun_out/bench_gloo2_self.json
