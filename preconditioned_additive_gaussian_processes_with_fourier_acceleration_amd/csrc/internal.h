@@ -268,8 +268,10 @@ int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_g
 // row shards with few blocks: grid from the summed grids + y = beta y + alpha f^2 mu x, then the interpolation
 // with S workgroups per block adding into y atomically (plain matvec); with A the summed grids come from the
 // ranks' slots (the wait overlaps the y initialisation)
+// (A and d_part: this rank's partial grids are summed and put into its slot in the same kernel)
 int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, double alpha, const double* d_x,
-                              double beta, double* d_y, int S, hipStream_t stream, const PeerArgs* A = nullptr);
+                              double beta, double* d_y, int S, hipStream_t stream, const PeerArgs* A = nullptr,
+                              const double* d_part = nullptr);
 // d_grid = the rank-order sum of the ranks' slots of A.epoch (after waiting for their flags)
 int launch_peer_sum(const AdditivePlan& P, const PeerArgs& A, double* d_grid, hipStream_t stream);
 // d_dot != nullptr (non-grad): also writes (y, x) to *d_dot (device), one grid-wide reduction in the launch
@@ -456,8 +458,9 @@ int additive_rows(void* str, int* n_local, int* n_global, int* row_begin);
 bool shard_fused_dot_ok(void* str);
 // row shard: grid (summed over the shards) -> y_local = A x_local and *d_dot = (y_local, x_local) locally
 int shard_finish_dot(void* str, const double* grid, const double* x_local, double* y_local, double* d_dot);
-// the row split over the peer exchange (1-D windows only: shard_peer_ok): spread into this rank's slot and
-// publish; then the exchange folded into the grid kernel (or summed into d_grid first: gradient, dot, many blocks)
+// the row split over the peer exchange (1-D windows only: shard_peer_ok): the spread into the partial grids;
+// then their sum, the put into this rank's slot, the exchange, the grid and y-init in one kernel (few-block
+// shards), or k_reduce_parts + k_peer_sum into d_grid before the usual finish (gradient, dot, many blocks)
 bool shard_peer_ok(void* str);
 int shard_spread_peer(void* str, const double* x_local, const PeerArgs& A);
 int shard_peer_sum(void* str, const PeerArgs& A, double* d_grid);

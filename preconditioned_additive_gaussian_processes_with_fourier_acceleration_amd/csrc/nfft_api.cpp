@@ -688,19 +688,21 @@ bool shard_peer_ok(void* str)
 
 int shard_spread_peer(void* str, const double* x_local, const PeerArgs& A)
 {
+   (void)A;  // the put into this rank's slot happens in the finish (or shard_peer_sum)
    PlanExt* E = additive_plan(str);
    if (!E || !E->P.points_ready || E->P.md.on) return -1;
    AdditivePlan& P = E->P;
    hipStream_t s = current_stream();
-   if (P.nblocks > 0 && launch_spread(P, x_local, P.d_part, s)) return -1;
-   return launch_reduce_parts(P, P.d_part, nullptr, s, &A);
+   return (P.nblocks > 0 && launch_spread(P, x_local, P.d_part, s)) ? -1 : 0;
 }
 
 int shard_peer_sum(void* str, const PeerArgs& A, double* d_grid)
 {
    PlanExt* E = additive_plan(str);
    if (!E || !E->P.points_ready || E->P.md.on) return -1;
-   return launch_peer_sum(E->P, A, d_grid, current_stream());
+   hipStream_t s = current_stream();
+   if (launch_reduce_parts(E->P, E->P.d_part, nullptr, s, &A)) return -1;
+   return launch_peer_sum(E->P, A, d_grid, s);
 }
 
 int shard_finish_peer(void* str, const PeerArgs& A, double* d_grid, int grad, double alpha, const double* x_local,
@@ -711,8 +713,9 @@ int shard_finish_peer(void* str, const PeerArgs& A, double* d_grid, int grad, do
    AdditivePlan& P = E->P;
    hipStream_t s = current_stream();
    const int S = shard_split(P);
-   if (!grad && S > 1 && !P.timing) return launch_shard_finish_split(P, nullptr, alpha, x_local, beta, y_local, S, s, &A);
-   if (launch_peer_sum(P, A, d_grid, s) || launch_grid_from_sum(P, d_grid, grad, s)) return -1;
+   if (!grad && S > 1 && !P.timing)
+      return launch_shard_finish_split(P, nullptr, alpha, x_local, beta, y_local, S, s, &A, P.d_part);
+   if (shard_peer_sum(str, A, d_grid) || launch_grid_from_sum(P, d_grid, grad, s)) return -1;
    return launch_interp(P, grad, alpha, x_local, beta, y_local, s);
 }
 

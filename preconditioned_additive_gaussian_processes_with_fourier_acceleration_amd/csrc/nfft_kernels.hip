@@ -541,6 +541,35 @@ __device__ __forceinline__ void peer_gather(const PeerArgs& A, int comp, double*
    if (tid < kNos) s_g[tid] = v;
 }
 
+// window comp's sum over the shard's nparts partial grids, for threads tid < 64 (cell tid; every thread of the
+// workgroup calls it): k_grid's 16 strands per cell with 16 loads in flight each, then the strands in order
+__device__ __forceinline__ double parts_sum(const double* __restrict__ part, int nparts, int comp, double* s_red)
+{
+   const int tid = threadIdx.x;
+   constexpr int kPer = 16;
+   const int cell = tid & 63;
+   const int strand = tid >> 6;
+   constexpr int nstr = kGridThreads / 64;
+   const double* src = part + (size_t)comp * nparts * kNos + cell;
+   double acc = 0.0;
+   for (int p0 = strand; p0 < nparts; p0 += kPer * nstr) {
+      double v[kPer];
+#pragma unroll
+      for (int k = 0; k < kPer; k++) {
+         const int p = p0 + k * nstr;
+         v[k] = p < nparts ? src[(size_t)p * kNos] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < kPer; k++) acc += v[k];
+   }
+   s_red[tid] = acc;
+   __syncthreads();
+   double v = 0.0;
+   if (tid < kNos)
+      for (int k = 0; k < nstr; k++) v += s_red[k * 64 + tid];
+   return v;
+}
+
 __global__ __launch_bounds__(kGridThreads) void k_peer_sum(PeerArgs A, double* __restrict__ grid)
 {
    __shared__ double s_g[kNos];
@@ -548,10 +577,14 @@ __global__ __launch_bounds__(kGridThreads) void k_peer_sum(PeerArgs A, double* _
    if (threadIdx.x < kNos) grid[(size_t)blockIdx.x * kNos + threadIdx.x] = s_g[threadIdx.x];
 }
 
+// With A (the peer exchange) and part: this rank's window comp summed from its nparts partial grids and put
+// into its slot first (k_reduce_parts folded in: the shard's matvec is three launches), then the y
+// initialisation, then the gather of every rank's window comp.
 __global__ __launch_bounds__(kGridThreads) void k_grid_sum_yinit(const double* __restrict__ gsum,
                                                                 const double* __restrict__ w, double* __restrict__ H,
                                                                 double* __restrict__ y, const double* __restrict__ x,
-                                                                int n, double beta, double amu, PeerArgs A)
+                                                                int n, double beta, double amu, PeerArgs A,
+                                                                const double* __restrict__ part, int nparts)
 {
    __shared__ double s_g[kNos];
    __shared__ double s_h[kNos];
@@ -562,6 +595,11 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_sum_yinit(const double* _
    double ct[kTaps];
    grid_tail_coeffs(ct);
    if (!A.bufs && tid < kNos) s_g[tid] = gsum[(size_t)comp * kNos + tid];
+   if (A.bufs && part) {
+      __shared__ double s_red[kGridThreads];
+      const double v = parts_sum(part, nparts, comp, s_red);
+      if (tid < kNos) peer_put(A, comp, tid, v);
+   }
    // y init: 4 elements per thread per pass, all loads issued before the first store (one latency per
    // pass instead of one per element)
    constexpr int kU = 4;
@@ -642,27 +680,8 @@ __global__ __launch_bounds__(kGridThreads) void k_reduce_parts(const double* __r
    __shared__ double s_red[kGridThreads];
    const int comp = blockIdx.x;
    const int tid = threadIdx.x;
-   constexpr int kPer = 16;
-   const int cell = tid & 63;
-   const int strand = tid >> 6;
-   constexpr int nstr = kGridThreads / 64;
-   const double* src = part + (size_t)comp * nparts * kNos + cell;
-   double acc = 0.0;
-   for (int p0 = strand; p0 < nparts; p0 += kPer * nstr) {
-      double v[kPer];
-#pragma unroll
-      for (int k = 0; k < kPer; k++) {
-         const int p = p0 + k * nstr;
-         v[k] = p < nparts ? src[(size_t)p * kNos] : 0.0;
-      }
-#pragma unroll
-      for (int k = 0; k < kPer; k++) acc += v[k];
-   }
-   s_red[tid] = acc;
-   __syncthreads();
+   const double v = parts_sum(part, nparts, comp, s_red);
    if (tid < kNos) {
-      double v = 0.0;
-      for (int k = 0; k < nstr; k++) v += s_red[k * 64 + tid];
       if (A.bufs)
          peer_put(A, comp, tid, v);
       else
@@ -1113,14 +1132,19 @@ int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int gra
 }
 
 int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, double alpha, const double* d_x,
-                              double beta, double* d_y, int S, hipStream_t stream, const PeerArgs* A)
+                              double beta, double* d_y, int S, hipStream_t stream, const PeerArgs* A,
+                              const double* d_part)
 {
    constexpr int T = 512;
    raise_lds_limit_once();
    if (!abs_lds_ok()) return -1;
+   if (A && A->slot_doubles != (long long)P.nw * kNos) return -1;
    const double ff = P.f * P.f;
    hipLaunchKernelGGL(k_grid_sum_yinit, dim3(P.nw), dim3(kGridThreads), 0, stream, d_gridsum, (const double*)P.d_w,
-                      P.d_H, d_y, d_x, P.n, beta, alpha * ff * P.mu * P.diag, A ? *A : PeerArgs{});
+                      P.d_H, d_y, d_x, P.n, beta, alpha * ff * P.mu * P.diag, A ? *A : PeerArgs{},
+                      // a shard without blocks puts zeros (nparts 0: the pointer is not read, but must be non-null)
+                      A ? (P.nblocks ? d_part : (const double*)P.d_w) : (const double*)nullptr,
+                      P.nblocks ? P.nparts : 0);
    if (P.n > 0)
       hipLaunchKernelGGL(interp_part_fn(P.rec), dim3(P.nblocks * S), dim3(T), sizeof(double) * (size_t)(P.B + kPad), stream,
                          P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H, d_y, P.n, P.B, P.ngroups, S,
