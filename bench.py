@@ -583,6 +583,52 @@ def run_loss(op, torch, n, d, X, rng_seed=906, maxits=50, nvecs=10, rows=None, d
             "loss_nvecs": nvecs, "loss_l": l}
 
 
+def peer_leg(op, xd, yd, step, prewarm, timed, rank_times, dist, world, args):
+    """N > 1, rows: the same timed steps over the peer-memory exchange (Nfft4GPAmdDistPeerEnable) instead of the
+    communicator's all-reduce, after a check that its matvec equals the all-reduce's (relative difference, max
+    over the ranks).  Every step that can fail on one rank only is followed by an all-reduced failure flag, so
+    every rank leaves together; the headline stays the all-reduce line."""
+    import torch
+
+    def agree(ok):
+        t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)
+        return float(t.item()) == 0.0
+
+    y_ref = op.matsymv(xd).clone()
+    if not op.enable_peer():
+        return {"enabled": False, "reason": "Nfft4GPAmdDistPeerEnable refused (a rank could not export or open)"}
+    ok, rel = True, None
+    try:
+        y_p = op.matsymv(xd)
+        rel = float(torch.linalg.norm(y_p - y_ref) / torch.linalg.norm(y_ref))
+    except RuntimeError:
+        ok = False
+    t = torch.tensor([rel if rel is not None else float("inf")], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    rel = float(t.item())
+    if not agree(ok) or not rel <= 1e-12:
+        op.disable_peer()
+        return {"enabled": True, "verified": False, "max_rel_diff_vs_allreduce": rel}
+    try:
+        prewarm()
+        for _ in range(args.warmup):
+            step()
+        el, _ = timed(False)
+        el_i, per = timed(True)
+        ok = True
+    except RuntimeError:
+        ok = False
+    if not agree(ok):
+        op.disable_peer()
+        return {"enabled": True, "verified": True, "max_rel_diff_vs_allreduce": rel, "timed": False}
+    op.disable_peer()
+    return {"enabled": True, "verified": True, "max_rel_diff_vs_allreduce": rel,
+            "value": args.steps / el, "ms_per_step": 1e3 * el / args.steps, "per_rank": rank_times(per, el_i),
+            "how": "rank-order sum of every rank's IPC-shared grid slots inside the grid kernel (dist.hip), "
+                   "no all-reduce; 16 KB of epoch-stamped words read per rank"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -603,6 +649,7 @@ def main():
     ap.add_argument("--partition", default="rows", choices=["rows", "components"],
                     help="N > 1: the headline split (the other one is timed too)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="OpenMP threads of the CPU baseline")
+    ap.add_argument("--no-peer", action="store_true", help="N > 1, rows: skip the peer-memory exchange leg")
     ap.add_argument("--kernel-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-oracle-so", default=None, help=argparse.SUPPRESS)
@@ -918,6 +965,8 @@ def main():
             result.update(run_fgmres(op, torch, n, rows=(rb, re), dist=dist, ortho=2))
             result.update(run_loss(op, torch, n, d, X, rows=(rb, re), dist=dist))
         result["partition_" + alt["partition"]] = alt
+        if args.partition == "rows" and not args.no_peer:
+            result["rows_peer_exchange"] = peer_leg(op, xd, yd, step, prewarm, timed, rank_times, dist, world, args)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -567,6 +567,8 @@ int Nfft4GPAmdDistSetChunks(void *dop, int chunks);
  * exchange on, Nfft4GPAmdDistFree is collective.  Replaces the grid all-reduce of the reference's sequential
  * component sum (nfft_interface.c:796-817) split over row shards; no reference counterpart. */
 int Nfft4GPAmdDistPeerEnable(void *dop);
+/* back to the communicator's all-reduce (collective; also after a wait gave up) */
+int Nfft4GPAmdDistPeerDisable(void *dop);
 /* 1 if the peer exchange is on, 0 if not, -1 for a NULL operator */
 int Nfft4GPAmdDistPeerActive(void *dop);
 /* per-rank timing of a distributed operator (0 disables; enabling resets): every matvec records hipEvents

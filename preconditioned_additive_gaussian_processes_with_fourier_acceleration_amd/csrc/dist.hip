@@ -178,6 +178,21 @@ void peer_free(PeerState* P)
    delete P;
 }
 
+// collective: no rank unmaps or frees its buffer while another's last exchange may still read it
+void peer_release(DistOp* D)
+{
+   if (!D->peer) return;
+   (void)hipStreamSynchronize(current_stream());
+   double one = 1.0, *d_one = nullptr;
+   if (hipMalloc((void**)&d_one, sizeof(double)) == hipSuccess &&
+       hipMemcpy(d_one, &one, sizeof(double), hipMemcpyHostToDevice) == hipSuccess)
+      (void)D->comm->allreduce(d_one, 1, current_stream());
+   (void)hipStreamSynchronize(current_stream());
+   (void)hipFree(d_one);
+   peer_free(D->peer);
+   D->peer = nullptr;
+}
+
 // a wait of an earlier exchange gave up (a peer never published): every later call fails
 int peer_check(DistOp* D)
 {
@@ -497,16 +512,7 @@ void Nfft4GPAmdDistFree(void* dop)
    if (!D) return;
    (void)hipStreamSynchronize(current_stream());
    if (D->cs) (void)hipStreamSynchronize(D->cs);
-   if (D->peer) {
-      // collective: no rank unmaps or frees its buffer while another's last exchange may still read it
-      double one = 1.0, *d_one = nullptr;
-      if (hipMalloc((void**)&d_one, sizeof(double)) == hipSuccess &&
-          hipMemcpy(d_one, &one, sizeof(double), hipMemcpyHostToDevice) == hipSuccess)
-         (void)D->comm->allreduce(d_one, 1, current_stream());
-      (void)hipStreamSynchronize(current_stream());
-      (void)hipFree(d_one);
-      peer_free(D->peer);
-   }
+   peer_release(D);
    if (D->d_grid) (void)hipFree(D->d_grid);
    if (D->d_tmp) (void)hipFree(D->d_tmp);
    for (hipEvent_t e : D->ev) (void)hipEventDestroy(e);
@@ -702,6 +708,15 @@ int Nfft4GPAmdDistPeerEnable(void* dop)
    P->a.slot_doubles = (long long)gcount;
    P->a.spin = spin;
    D->peer = P;
+   return 0;
+}
+
+// back to the communicator's all-reduce (collective); the operator is usable again after a timed-out wait
+int Nfft4GPAmdDistPeerDisable(void* dop)
+{
+   DistOp* D = (DistOp*)dop;
+   if (!D) return -1;
+   peer_release(D);
    return 0;
 }
 

@@ -219,6 +219,12 @@ class DistributedAdditiveKernel:
         from . import _lib
         return _lib.lib().Nfft4GPAmdDistPeerEnable(self.h) == 0
 
+    def disable_peer(self):
+        """Back to the communicator's all-reduce (collective)."""
+        from . import _lib
+        if _lib.lib().Nfft4GPAmdDistPeerDisable(self.h) != 0:
+            raise RuntimeError("Nfft4GPAmdDistPeerDisable failed")
+
     @property
     def peer_active(self) -> bool:
         from . import _lib
