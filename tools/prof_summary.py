@@ -26,7 +26,7 @@ def main():
         for r in csv.DictReader(fh):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    kinds = {"spread": "k_spread<", "grid": "k_grid(", "interp": "k_interp<false, 1024, false>"}
+    kinds = {"spread": "k_spread<", "grid": "k_grid(", "interp": "k_interp<false, 1024, false"}
     out = {"trace": args.trace, "steps": args.steps, "kernels": {}}
     for key, pat in kinds.items():
         durs = [(e - s) * 1e-6 for s, e, name in rows if pat in name]
