@@ -157,3 +157,85 @@ def test_peer_exchange_fused_grid_kernel(peer2):
 def test_peer_exchange_timeout_fails_the_next_call(peer2):
     assert int(peer2[0]["fault_raised"]) == 1
     assert int(peer2[1]["fault_raised"]) == 0
+
+
+def _worker3(rank, world, port, outdir):
+    """Three ranks: the rank-order sum is not the all-reduce's order, so the results agree to rounding, and
+    every rank must hold bitwise the same circulants (the same summed grids)."""
+    for p in (ROOT, HERE):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import ctypes as C
+    import torch
+    import torch.distributed as dist
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import (
+        Communicator, DistributedAdditiveKernel)
+    from test_gpu_dist import problem
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Communicator.callback()
+    L = amd.lib()
+    L.Nfft4GPAmdDebugShardH.restype = C.c_longlong
+    L.Nfft4GPAmdDebugShardH.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong]
+    X, win, nw, dw, x = problem("1d")
+    op = DistributedAdditiveKernel(X, win, nw, dw, comm, partition="rows")
+    op.local.set_deterministic(True)
+    assert op.setup(amd.GAUSSIAN, f=1.3, l=0.1, mu=0.1) == 0
+    rb, re = op.row_begin, op.row_end
+    xd = torch.tensor(x[rb:re], device="cuda")
+    out = {"rb": rb, "re": re}
+    nh = nw * 64 * 8
+    H = np.zeros(nh)
+    out["cb_y"] = op.matsymv(xd).cpu().numpy()
+    out["cb_g"] = op.gradmatsymv(xd).cpu().numpy()
+    xs = torch.zeros_like(xd)
+    _, _, _, out["cb_it"] = amd.pcg(op, xd.clone(), xs, maxits=2000, tol=1e-6)
+    out["cb_x"] = xs.cpu().numpy()
+    out["peer_on"] = int(op.enable_peer())
+    if out["peer_on"]:
+        out["peer_y"] = op.matsymv(xd).cpu().numpy()
+        assert L.Nfft4GPAmdDebugShardH(op.local.h, H.ctypes.data, nh) == nh
+        out["peer_H"] = H.copy()
+        out["peer_g"] = op.gradmatsymv(xd).cpu().numpy()
+        xs = torch.zeros_like(xd)
+        _, _, _, out["peer_it"] = amd.pcg(op, xd.clone(), xs, maxits=2000, tol=1e-6)
+        out["peer_x"] = xs.cpu().numpy()
+        op.disable_peer()  # back to the all-reduce, still usable
+        out["after_y"] = op.matsymv(xd).cpu().numpy()
+    op.free()
+    torch.cuda.synchronize()
+    comm.free()
+    np.savez(os.path.join(outdir, f"peer3_rank{rank}.npz"), **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def peer3(tmp_path_factory):
+    import torch.multiprocessing as mp
+    from test_gpu_dist import _free_port
+    out = tmp_path_factory.mktemp("peer3")
+    mp.spawn(_worker3, args=(3, _free_port(), str(out)), nprocs=3, join=True)
+    return [dict(np.load(os.path.join(out, f"peer3_rank{r}.npz"))) for r in range(3)]
+
+
+def test_peer_exchange_three_ranks(peer3):
+    assert all(int(r["peer_on"]) == 1 for r in peer3)
+    for r in peer3[1:]:
+        np.testing.assert_array_equal(r["peer_H"], peer3[0]["peer_H"])
+    y = np.concatenate([r["peer_y"] for r in peer3])
+    y0 = np.concatenate([r["cb_y"] for r in peer3])
+    assert np.linalg.norm(y - y0) <= 1e-14 * np.linalg.norm(y0)
+    for r in peer3:
+        n = int(r["re"]) - int(r["rb"])
+        for k in range(3):
+            a, b = r["peer_g"][k * n:(k + 1) * n], r["cb_g"][k * n:(k + 1) * n]
+            assert np.linalg.norm(a - b) <= 1e-13 * max(np.linalg.norm(b), 1e-300)
+        assert abs(int(r["peer_it"]) - int(r["cb_it"])) <= 2
+        np.testing.assert_array_equal(r["after_y"], r["cb_y"])  # disable: the all-reduce path again
+    x = np.concatenate([r["peer_x"] for r in peer3])
+    x0 = np.concatenate([r["cb_x"] for r in peer3])
+    assert np.linalg.norm(x - x0) <= 1e-8 * np.linalg.norm(x0)
