@@ -642,12 +642,21 @@ int Nfft4GPAmdDistPeerEnable(void* dop)
    for (size_t b = 0; b < HB; b++) hx[(size_t)rank * HB + b] = (double)((const unsigned char*)&mine)[b];
    hx.back() = ok ? 0.0 : 1.0;
    double* dx = nullptr;
+   // every rank enters both all-reduces whatever failed locally (a rank that skipped one would leave the
+   // others waiting in it); only a rank that cannot even hold the few-KB exchange buffer returns early
+   if (hipMalloc((void**)&dx, sizeof(double) * hx.size()) != hipSuccess) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdDistPeerEnable: no device memory for the handle exchange\n");
+      peer_free(P);
+      return -1;
+   }
    auto agree = [&](std::vector<double>& v) {
-      if (!dx && hipMalloc((void**)&dx, sizeof(double) * hx.size()) != hipSuccess) return false;
-      if (hipMemcpy(dx, v.data(), sizeof(double) * v.size(), hipMemcpyHostToDevice) != hipSuccess) return false;
-      if (C->allreduce(dx, v.size(), s)) return false;
-      return hipMemcpyAsync(v.data(), dx, sizeof(double) * v.size(), hipMemcpyDeviceToHost, s) == hipSuccess &&
-             hipStreamSynchronize(s) == hipSuccess;
+      bool ok = hipMemcpy(dx, v.data(), sizeof(double) * v.size(), hipMemcpyHostToDevice) == hipSuccess;
+      if (!ok) (void)hipMemset(dx + v.size() - 1, 0, sizeof(double));  // still the same collective
+      ok = C->allreduce(dx, v.size(), s) == 0 && ok;
+      ok = hipMemcpyAsync(v.data(), dx, sizeof(double) * v.size(), hipMemcpyDeviceToHost, s) == hipSuccess &&
+           hipStreamSynchronize(s) == hipSuccess && ok;
+      if (!ok) v.back() = 1.0;  // this rank's copy of the answer is unusable: report a failure
+      return true;
    };
    bool all = agree(hx) && hx.back() == 0.0;
    std::vector<char*> bufs(world, nullptr);
