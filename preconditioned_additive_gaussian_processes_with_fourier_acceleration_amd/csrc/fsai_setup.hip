@@ -1045,9 +1045,13 @@ __global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ 
       // test a tile's keys against the rows' limits (points j0 + col), append, tighten
       auto test_tile = [&](const f32x16& c, int j0) {
          const int j = j0 + col;
-         float mx = -inf;
+         // per group of 4 rows of the lane (v = 4 g .. 4 g + 3) the largest margin; NaN keys drop out
+         float mg[4];
 #pragma unroll
-         for (int v = 0; v < 16; v++) mx = fmaxf(mx, c[v] - thr[v]);  // NaN keys drop out
+         for (int g = 0; g < 4; g++)
+            mg[g] = fmaxf(fmaxf(c[4 * g] - thr[4 * g], c[4 * g + 1] - thr[4 * g + 1]),
+                          fmaxf(c[4 * g + 2] - thr[4 * g + 2], c[4 * g + 3] - thr[4 * g + 3]));
+         const float mx = fmaxf(fmaxf(mg[0], mg[1]), fmaxf(mg[2], mg[3]));
          if (!__ballot(mx >= 0.f)) return;
          // append: the wave owns its rows, so each (v, lane half) pair's slots come from one ballot
          // (lanes 0-31: row rl = (v & 3) + 8 (v >> 2), lanes 32-63: rl + 4) and the counts live in cntv
@@ -1055,22 +1059,27 @@ __global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ 
          // every point of the tile precedes every row)
          const int jj = (j0 + 31 < rowmin) ? -1 : j;
 #pragma unroll
-         for (int v = 0; v < 16; v++) {
-            const int rl = (v & 3) + 8 * (v >> 2);
-            const bool pass = c[v] >= thr[v] && jj < rlim[v];
-            const unsigned long long m = __ballot(pass);
-            if (!m) continue;
-            const unsigned int mlo = (unsigned int)m, mhi = (unsigned int)(m >> 32);
-            const int blo = __builtin_amdgcn_readlane(cntv, rl), bhi = __builtin_amdgcn_readlane(cntv, rl + 4);
-            if (pass) {
-               const int base = h ? bhi : blo;
-               const int pos = base + __popcll(m & below) - (h ? __popc(mlo) : 0);
-               if (pos < CAP) {
-                  S.idx[32 * wave + rl + 4 * h][pos] = j;
-                  S.ck[32 * wave + rl + 4 * h][pos] = c[v];
+         for (int g = 0; g < 4; g++) {
+            if (!__ballot(mg[g] >= 0.f)) continue;  // no lane passes in this group of 4 rows
+#pragma unroll
+            for (int vv = 0; vv < 4; vv++) {
+               const int v = 4 * g + vv;
+               const int rl = (v & 3) + 8 * (v >> 2);
+               const bool pass = c[v] >= thr[v] && jj < rlim[v];
+               const unsigned long long m = __ballot(pass);
+               if (!m) continue;
+               const unsigned int mlo = (unsigned int)m, mhi = (unsigned int)(m >> 32);
+               const int blo = __builtin_amdgcn_readlane(cntv, rl), bhi = __builtin_amdgcn_readlane(cntv, rl + 4);
+               if (pass) {
+                  const int base = h ? bhi : blo;
+                  const int pos = base + __popcll(m & below) - (h ? __popc(mlo) : 0);
+                  if (pos < CAP) {
+                     S.idx[32 * wave + rl + 4 * h][pos] = j;
+                     S.ck[32 * wave + rl + 4 * h][pos] = c[v];
+                  }
                }
+               cntv += (lane == rl) ? __popc(mlo) : (lane == rl + 4) ? __popc(mhi) : 0;
             }
-            cntv += (lane == rl) ? __popc(mlo) : (lane == rl + 4) ? __popc(mhi) : 0;
          }
          // the wave's rows that another tile could overflow: tighten them (wave-uniform loop)
          unsigned long long todo = __ballot(lane < 32 && cntv > CAP - 32);
