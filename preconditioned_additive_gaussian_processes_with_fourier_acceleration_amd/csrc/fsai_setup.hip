@@ -896,15 +896,12 @@ __global__ __launch_bounds__(kScrThreads, KNN_SCR_WAVES) void k_knn_screen(const
 // one candidate per lane.
 constexpr int kTileRows = 256;
 constexpr int kTileCap = 64;
-constexpr int kTileStep = 64;  // points per LDS stage: two 32-point blocks
+constexpr int kTileStep = 64;  // Xb's padding: n rounded up to 64 points
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-template <int KCH>
 struct TileShared {
    int idx[kTileRows][kTileCap];
    float ck[kTileRows][kTileCap];
-   uint4 pts[2][2 * KCH * 2 * 2 * 32];  // [stage][block][chunk][hi/lo][half][point] of 8 bf16
-   float nx[2][kTileStep];
    float thr[kTileRows];
    int cnt[kTileRows];
    int row[kTileRows];
@@ -956,9 +953,11 @@ __global__ __launch_bounds__(256) void k_knn_prep_bf(const double* __restrict__ 
    if ((threadIdx.x & 63) == 0) atomicMax(m2, mx);
 }
 
-// DIRECT: every wave loads its B fragments from global memory itself (the eight waves read the same lines close
-// together: L1 / L2 hits), two tiles ahead in registers -- no LDS stages and no barriers in the scan
-template <int KCH, bool DIRECT>
+// Every wave loads its B fragments from global memory itself (the eight waves read the same lines close
+// together: L1 / L2 hits), two tiles ahead in registers -- no LDS stages and no barriers in the scan (an
+// LDS-staged scan with a barrier per 64 points, loads four stages ahead, measured 0.221 s against 0.174 s at
+// n = 1e6, d = 32, and was removed)
+template <int KCH>
 __global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ X, int ldim,
                                                      const uint4* __restrict__ Xb, const float* __restrict__ nx,
                                                      int n, int d, int lfil, float margin2,
@@ -967,7 +966,7 @@ __global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ 
                                                      const int* __restrict__ rows, int nrows_list, int probe)
 {
    constexpr int R = kTileRows, CAP = kTileCap, BLK = KCH * 2 * 2 * 32;
-   __shared__ TileShared<KCH> S;
+   __shared__ TileShared S;
    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, col = lane & 31;
    const int K = lfil - 1;
    const int nall = rows ? nrows_list : n - lfil;
@@ -1003,45 +1002,12 @@ __global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ 
          nqh[v] = r < nr ? -0.5f * nx[row_of(r)] : 0.f;
          rlim[v] = r < nr ? row_of(r) : 0;
       }
-      const int nsteps = (ilast + kTileStep - 1) / kTileStep;
       const int rowmin = row_of(0);
       const unsigned long long below = (1ull << lane) - 1ull;
       int cntv = 0;  // lane l < 32: candidates of the wave's row l
-      if (!DIRECT) {
-         for (int t = tid; t < 2 * BLK; t += kScrThreads) S.pts[0][t] = Xb[t];
-         if (tid < kTileStep) S.nx[0][tid] = nx[tid];
-      }
       __syncthreads();
 #pragma unroll
       for (int v = 0; v < 16; v++) thr[v] = S.thr[32 * wave + (v & 3) + 8 * (v >> 2) + 4 * h];
-      // the stages' global loads run four stages ahead in registers p0..p3 (p_k holds a stage = k mod 4; one
-      // stage of MFMAs is ~0.4 us, an HBM / MALL miss several times that).  The loads are unconditional (a
-      // stage index clamped to the last stage, lanes past the stage's data re-read it), so no branch joins a
-      // loaded register and its wait stays at the LDS store.
-      const int tq = tid % (2 * BLK), tn = tid % kTileStep;
-      uint4 p0, p1, p2, p3;
-      float n0, n1, n2, n3;
-      auto fetch = [&](int t, uint4& pr, float& pn) {
-         t = min(t, nsteps - 1);
-         pr = Xb[(size_t)t * 2 * BLK + tq];
-         pn = nx[(size_t)t * kTileStep + tn];
-      };
-      // a 32-point tile's keys: B fragments from the stage, six MFMAs on the three-term split
-      auto mfma_tile = [&](int buf, int sub) {
-         const float nxj = S.nx[buf][32 * sub + col];
-         f32x16 c;
-#pragma unroll
-         for (int v = 0; v < 16; v++) c[v] = fmaf(nxj, -0.5f, nqh[v]);
-#pragma unroll
-         for (int ch = 0; ch < KCH; ch++) {
-            const bf16x8 bh = __builtin_bit_cast(bf16x8, S.pts[buf][sub * BLK + ((ch * 2 + 0) * 2 + h) * 32 + col]);
-            const bf16x8 bl = __builtin_bit_cast(bf16x8, S.pts[buf][sub * BLK + ((ch * 2 + 1) * 2 + h) * 32 + col]);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ch], bl, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ch], bh, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ch], bh, c, 0, 0, 0);
-         }
-         return c;
-      };
       // test a tile's keys against the rows' limits (points j0 + col), append, tighten
       auto test_tile = [&](const f32x16& c, int j0) {
          const int j = j0 + col;
@@ -1116,42 +1082,11 @@ __global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ 
 #pragma unroll
          for (int v = 0; v < 16; v++) thr[v] = S.thr[32 * wave + (v & 3) + 8 * (v >> 2) + 4 * h];
       };
-      // software pipeline: a tile's tests run under the next tile's MFMAs (c1 carries the previous
-      // stage's second tile)
+      // software pipeline: a tile's tests run under the next tile's MFMAs (c1 carries the previous tile)
       f32x16 c0, c1;
-      // stage s: its two tiles, then stage s + 1 from pr (= p_{(s+1) mod 4}) into the other buffer, and pr
-      // refilled with stage s + 5
-      auto stage = [&](int s, uint4& pr, float& pn) {
-         const int buf = s & 1;
-         c0 = mfma_tile(buf, 0);
-         if (s > 0) test_tile(c1, s * kTileStep - 32);
-         c1 = mfma_tile(buf, 1);
-         test_tile(c0, s * kTileStep);
-         if (s + 1 < nsteps) {
-            if (tid < 2 * BLK) S.pts[buf ^ 1][tid] = pr;
-            if (tid < kTileStep) S.nx[buf ^ 1][tid] = pn;
-         }
-         fetch(s + 5, pr, pn);
-         __syncthreads();
-      };
-      if constexpr (!DIRECT) {
-         fetch(1, p1, n1);
-         fetch(2, p2, n2);
-         fetch(3, p3, n3);
-         fetch(4, p0, n0);
-         for (int s0 = 0; s0 < nsteps; s0 += 4) {
-            stage(s0, p1, n1);
-            if (s0 + 1 >= nsteps) break;
-            stage(s0 + 1, p2, n2);
-            if (s0 + 2 >= nsteps) break;
-            stage(s0 + 2, p3, n3);
-            if (s0 + 3 >= nsteps) break;
-            stage(s0 + 3, p0, n0);
-         }
-         if (nsteps > 0) test_tile(c1, nsteps * kTileStep - 32);
-      } else {
+      {
          const int ntl = (ilast + 31) / 32;  // 32-point tiles
-         uint4 ah0[KCH], al0[KCH], ah1[KCH], al1[KCH];
+         uint4 bh0[KCH], bl0[KCH], bh1[KCH], bl1[KCH];
          float nx0, nx1;
          auto fetchf = [&](int t, uint4 (&fh)[KCH], uint4 (&fl)[KCH], float& fn) {
             t = min(t, ntl - 1);
@@ -1176,15 +1111,15 @@ __global__ __launch_bounds__(512, 2) void k_knn_tile(const double* __restrict__ 
             }
             return c;
          };
-         fetchf(0, ah0, al0, nx0);
-         fetchf(1, ah1, al1, nx1);
+         fetchf(0, bh0, bl0, nx0);
+         fetchf(1, bh1, bl1, nx1);
          for (int t0 = 0; t0 < ntl; t0 += 2) {
-            c0 = mfma_frag(ah0, al0, nx0);
-            fetchf(t0 + 2, ah0, al0, nx0);
+            c0 = mfma_frag(bh0, bl0, nx0);
+            fetchf(t0 + 2, bh0, bl0, nx0);
             if (t0 > 0) test_tile(c1, t0 * 32 - 32);
             if (t0 + 1 < ntl) {
-               c1 = mfma_frag(ah1, al1, nx1);
-               fetchf(t0 + 3, ah1, al1, nx1);
+               c1 = mfma_frag(bh1, bl1, nx1);
+               fetchf(t0 + 3, bh1, bl1, nx1);
             }
             test_tile(c0, t0 * 32);
          }
@@ -1281,10 +1216,7 @@ int knn_pattern(const double* dX, int n, int ldim, int d, int lfil, const int* d
       const double margin = (16.0 * d + 448.0) * std::ldexp(1.0, -24) * (double)m2;
       if (std::isfinite(m2) && m2 >= std::ldexp(1.0f, -60) && std::isfinite((float)(2.0 * margin))) {
          const int ngroups = (nrows + kTileRows - 1) / kTileRows;
-         // direct loads (default): 0.174 s against 0.221 s for the LDS-staged scan at n = 1e6, d = 32
-         static const bool direct = !getenv("NFFT4GP_AMD_KNN_TILE_DIRECT") || atoi(getenv("NFFT4GP_AMD_KNN_TILE_DIRECT"));
-         auto tile = kch == 1 ? (direct ? k_knn_tile<1, true> : k_knn_tile<1, false>)
-                              : (direct ? k_knn_tile<2, true> : k_knn_tile<2, false>);
+         auto tile = kch == 1 ? k_knn_tile<1> : k_knn_tile<2>;
          hipLaunchKernelGGL(tile, dim3(std::min(ngroups, 65535)), dim3(kScrThreads), 0, s, dX, ldim, (const uint4*)Xf,
                             (const float*)nx, n, d, lfil, (float)(2.0 * margin) * 1.0001f, dia, dja, dfail,
                             dfail + nrows, d_rows, nrows, getenv("NFFT4GP_AMD_KNN_TILE_PROBE") ? 1 : 0);
