@@ -513,7 +513,8 @@ void env_layout(AdditivePlan& P)
    P.B = default_block(P.n);
    // windows per spread workgroup: at most 4 (with the [window][degree][cell] moment table three 4-window
    // workgroups of a 4064-point block fit a CU's LDS: config C's spread 40.8 -> 38.7 us, the matvec 78.9 -> 78.4,
-   // profiles/r05_spread_ab.txt), spread evenly over the fewest groups -- a one-window workgroup pays the whole
+   // profiles/r05_spread_ab.txt; 5 / 6 / 8 windows: spread 34.0 -> 36.4 / 40.8 / 37.9 us,
+   // profiles/r05_spread_cg_ab.txt), spread evenly over the fewest groups -- a one-window workgroup pays the whole
    // alpha staging and fold (round 4: 4 windows as 2 + 2 took 22.3 against 24.2 us as 3 + 1 per rank of
    // BASELINE configs[3]'s component split, profiles/r04_component_cg_sweep.txt)
    // ... unless that leaves fewer than 384 spread workgroups (1.5 per CU): then at most 3 per group, as in round 4
