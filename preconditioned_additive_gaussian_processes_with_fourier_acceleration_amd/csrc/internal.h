@@ -273,6 +273,7 @@ int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, do
                               double beta, double* d_y, int S, hipStream_t stream, const PeerArgs* A = nullptr,
                               const double* d_part = nullptr);
 // d_grid = the rank-order sum of the ranks' slots of A.epoch (after waiting for their flags)
+int launch_peer_grid(const AdditivePlan& P, const PeerArgs& A, const double* d_part, hipStream_t stream);
 int launch_peer_sum(const AdditivePlan& P, const PeerArgs& A, double* d_grid, hipStream_t stream);
 // d_dot != nullptr (non-grad): also writes (y, x) to *d_dot (device), one grid-wide reduction in the launch
 int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d_x, double beta, double* d_y,

@@ -716,6 +716,10 @@ int shard_finish_peer(void* str, const PeerArgs& A, double* d_grid, int grad, do
    const int S = shard_split(P);
    if (!grad && S > 1 && !P.timing)
       return launch_shard_finish_split(P, nullptr, alpha, x_local, beta, y_local, S, s, &A, P.d_part);
+   // unsplit, not deterministic (k_grid's blocked H sum): the partial-grid sum, put, gather and H in one
+   // launch, then k_interp as on the all-reduce path (same grid_tail arithmetic: bitwise equal results)
+   if (!grad && !P.timing && !P.det)
+      return (launch_peer_grid(P, A, P.d_part, s) || launch_interp(P, 0, alpha, x_local, beta, y_local, s)) ? -1 : 0;
    if (shard_peer_sum(str, A, d_grid) || launch_grid_from_sum(P, d_grid, grad, s)) return -1;
    return launch_interp(P, grad, alpha, x_local, beta, y_local, s);
 }

@@ -1153,6 +1153,18 @@ int launch_shard_finish_split(const AdditivePlan& P, const double* d_gridsum, do
    return 0;
 }
 
+// the peer exchange's grid step on its own (one launch: partial-grid sum + put + gather + H), for a
+// shard whose interpolation runs unsplit (k_interp's epilogue, no y initialisation here)
+int launch_peer_grid(const AdditivePlan& P, const PeerArgs& A, const double* d_part, hipStream_t stream)
+{
+   if (A.slot_doubles != (long long)P.nw * kNos) return -1;
+   hipLaunchKernelGGL(k_grid_sum_yinit, dim3(P.nw), dim3(kGridThreads), 0, stream, (const double*)nullptr,
+                      (const double*)P.d_w, P.d_H, (double*)nullptr, (const double*)nullptr, 0, 0.0, 0.0, A,
+                      P.nblocks ? d_part : (const double*)P.d_w, P.nblocks ? P.nparts : 0);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
 int launch_reduce_parts(const AdditivePlan& P, const double* d_part, double* d_gridsum, hipStream_t stream,
                         const PeerArgs* A)
 {

@@ -88,6 +88,22 @@ def _worker(rank, world, port, outdir):
     op.free()
     os.environ.pop("NFFT4GP_AMD_SHARD_SPLIT")
 
+    # unsplit shards (more than 64 blocks at n / N >= 250k): the one-launch sum + exchange + H kernel, then
+    # k_interp as on the all-reduce path
+    os.environ["NFFT4GP_AMD_SHARD_SPLIT"] = "1"
+    op = DistributedAdditiveKernel(X, win, nw, dw, comm, partition="rows")
+    assert op.setup(amd.GAUSSIAN, f=1.3, l=0.1, mu=0.1) == 0
+    y = op.matsymv(xd, 0.7, -1.5, torch.full_like(xd, 0.25))
+    assert L.Nfft4GPAmdDebugShardH(op.local.h, H.ctypes.data, nh) == nh
+    out["unsplit_cb_y"], out["unsplit_cb_H"] = y.cpu().numpy(), H.copy()
+    if op.enable_peer():
+        for _ in range(3):
+            y = op.matsymv(xd, 0.7, -1.5, torch.full_like(xd, 0.25))
+        assert L.Nfft4GPAmdDebugShardH(op.local.h, H.ctypes.data, nh) == nh
+        out["unsplit_peer_y"], out["unsplit_peer_H"] = y.cpu().numpy(), H.copy()
+    op.free()
+    os.environ.pop("NFFT4GP_AMD_SHARD_SPLIT")
+
     # a rank that never publishes: rank 0's wait gives up (short spin) and its next call fails
     os.environ["NFFT4GP_AMD_PEER_SPIN"] = "2000"
     op = DistributedAdditiveKernel(X, win, nw, dw, comm, partition="rows")
@@ -152,6 +168,17 @@ def test_peer_exchange_fused_grid_kernel(peer2):
         assert np.linalg.norm(y - y0) <= 1e-14 * np.linalg.norm(y0)
     # both ranks hold the same circulants (the same summed grids)
     np.testing.assert_array_equal(peer2[0]["split_peer_H"], peer2[1]["split_peer_H"])
+
+
+def test_peer_exchange_unsplit_grid_kernel(peer2):
+    # default (not deterministic) mode: the spread's LDS atomics round in arrival order, so the two runs
+    # agree to rounding, not bitwise
+    for r in peer2:
+        H, H0 = r["unsplit_peer_H"], r["unsplit_cb_H"]
+        assert np.abs(H - H0).max() <= 1e-13 * np.abs(H0).max()
+        y, y0 = r["unsplit_peer_y"], r["unsplit_cb_y"]
+        assert np.linalg.norm(y - y0) <= 1e-13 * np.linalg.norm(y0)
+    np.testing.assert_array_equal(peer2[0]["unsplit_peer_H"], peer2[1]["unsplit_peer_H"])
 
 
 def test_peer_exchange_timeout_fails_the_next_call(peer2):
