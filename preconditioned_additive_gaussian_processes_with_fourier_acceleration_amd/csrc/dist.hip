@@ -393,8 +393,8 @@ int dist_matvec_dot(void* dop, const double* d_p, double* d_q, double* d_dot)
       if (peer_check(D)) return -1;
       PeerArgs& A = D->peer->a;
       A.epoch++;
-      if (shard_spread_peer(D->h, d_p, A) || shard_peer_sum(D->h, A, D->d_grid)) return -1;
-      return shard_finish_dot(D->h, D->d_grid, d_p, d_q, d_dot);
+      if (shard_spread_peer(D->h, d_p, A)) return -1;
+      return shard_finish_dot_peer(D->h, A, D->d_grid, d_p, d_q, d_dot);
    }
    if (Nfft4GPAmdShardSpread(D->h, d_p, D->d_grid)) return -1;
    if (D->comm->allreduce(D->d_grid, D->grid_count, current_stream())) return -1;

@@ -465,6 +465,8 @@ int shard_finish_dot(void* str, const double* grid, const double* x_local, doubl
 bool shard_peer_ok(void* str);
 int shard_spread_peer(void* str, const double* x_local, const PeerArgs& A);
 int shard_peer_sum(void* str, const PeerArgs& A, double* d_grid);
+int shard_finish_dot_peer(void* str, const PeerArgs& A, double* d_grid, const double* x_local, double* y_local,
+                          double* d_dot);
 int shard_finish_peer(void* str, const PeerArgs& A, double* d_grid, int grad, double alpha, const double* x_local,
                       double beta, double* y_local);
 // what Nfft4GPSolverPcg needs to know about a distributed operator (matvec == Nfft4GPAmdDistMatSymv):

@@ -741,6 +741,22 @@ int shard_finish_dot(void* str, const double* grid, const double* x_local, doubl
    if (launch_grid_from_sum(P, grid, 0, s)) return -1;
    return launch_interp(P, 0, 1.0, x_local, 0.0, y_local, s, d_dot);
 }
+
+// shard_finish_dot over the peer exchange: the one-launch grid step (sum, put, gather, H) where the plan allows
+// it (as shard_finish_peer), else the gather into d_grid and shard_finish_dot
+int shard_finish_dot_peer(void* str, const PeerArgs& A, double* d_grid, const double* x_local, double* y_local,
+                          double* d_dot)
+{
+   PlanExt* E = additive_plan(str);
+   if (!E || !E->P.points_ready || E->P.md.on) return -1;
+   AdditivePlan& P = E->P;
+   hipStream_t s = current_stream();
+   if (P.n > 0 && !P.det && !P.timing)
+      return (launch_peer_grid(P, A, P.d_part, s) || launch_interp(P, 0, 1.0, x_local, 0.0, y_local, s, d_dot)) ? -1
+                                                                                                            : 0;
+   if (shard_peer_sum(str, A, d_grid)) return -1;
+   return shard_finish_dot(str, d_grid, x_local, y_local, d_dot);
+}
 }  // namespace nfft4gp_amd
 
 namespace nfft4gp_amd {

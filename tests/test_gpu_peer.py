@@ -96,11 +96,19 @@ def _worker(rank, world, port, outdir):
     y = op.matsymv(xd, 0.7, -1.5, torch.full_like(xd, 0.25))
     assert L.Nfft4GPAmdDebugShardH(op.local.h, H.ctypes.data, nh) == nh
     out["unsplit_cb_y"], out["unsplit_cb_H"] = y.cpu().numpy(), H.copy()
+
+    def pcg_run(tag):  # the PCG's fused (q, p) finish: the one-launch grid step, then k_interp's dot epilogue
+        xs = torch.zeros_like(b)
+        _, rr, _, it = amd.pcg(op, b, xs, maxits=2000, tol=1e-6)
+        out[f"unsplit_{tag}_pcg_x"], out[f"unsplit_{tag}_pcg_it"], out[f"unsplit_{tag}_pcg_rr"] = xs.cpu().numpy(), it, rr
+
+    pcg_run("cb")
     if op.enable_peer():
         for _ in range(3):
             y = op.matsymv(xd, 0.7, -1.5, torch.full_like(xd, 0.25))
         assert L.Nfft4GPAmdDebugShardH(op.local.h, H.ctypes.data, nh) == nh
         out["unsplit_peer_y"], out["unsplit_peer_H"] = y.cpu().numpy(), H.copy()
+        pcg_run("peer")
     op.free()
     os.environ.pop("NFFT4GP_AMD_SHARD_SPLIT")
 
@@ -179,6 +187,11 @@ def test_peer_exchange_unsplit_grid_kernel(peer2):
         y, y0 = r["unsplit_peer_y"], r["unsplit_cb_y"]
         assert np.linalg.norm(y - y0) <= 1e-13 * np.linalg.norm(y0)
     np.testing.assert_array_equal(peer2[0]["unsplit_peer_H"], peer2[1]["unsplit_peer_H"])
+    for r in peer2:
+        assert abs(int(r["unsplit_peer_pcg_it"]) - int(r["unsplit_cb_pcg_it"])) <= 2
+        assert float(r["unsplit_peer_pcg_rr"]) <= 1e-6
+        xs, x0 = r["unsplit_peer_pcg_x"], r["unsplit_cb_pcg_x"]
+        assert np.linalg.norm(xs - x0) <= 1e-5 * np.linalg.norm(x0)
 
 
 def test_peer_exchange_timeout_fails_the_next_call(peer2):
