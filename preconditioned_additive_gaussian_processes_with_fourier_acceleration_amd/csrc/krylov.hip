@@ -47,13 +47,11 @@ int kgrid(size_t n)
 // w -= (*hprev) * u (when u != nullptr); then *out = (w, v) (v != nullptr) or ||w||^2 (v == nullptr).
 // T threads per block: 1024 gives a quarter of the partials for the last block to add (the MGS loop of
 // FGMRES runs one of these per projection, so its serial tail is most of a step at n = 1e6).
-template <int T, int EPT = kKEPT>
-__global__ __launch_bounds__(T) void k_gs_step(double* __restrict__ w, const double* __restrict__ u,
-                                               const double* __restrict__ hprev, const double* __restrict__ v,
-                                               size_t n, double* __restrict__ part, unsigned int* __restrict__ ticket,
-                                               double* __restrict__ out)
+template <int T, int EPT>
+__device__ __forceinline__ void gs_body(double* __restrict__ w, const double* __restrict__ u, double h,
+                                        const double* __restrict__ v, size_t n, double* __restrict__ part,
+                                        unsigned int* __restrict__ ticket, double* __restrict__ out)
 {
-   const double h = u ? *hprev : 0.0;
    double acc = 0.0;
    const size_t stride = (size_t)gridDim.x * T * EPT;
    for (size_t i0 = (size_t)blockIdx.x * T * EPT + threadIdx.x; i0 < n; i0 += stride) {
@@ -78,6 +76,66 @@ __global__ __launch_bounds__(T) void k_gs_step(double* __restrict__ w, const dou
    acc = block_sum0<T>(acc);
    double tot;
    if (grid_total<T>(acc, part, ticket, &tot) && threadIdx.x == 0) *out = tot;
+}
+
+template <int T, int EPT = kKEPT>
+__global__ __launch_bounds__(T) void k_gs_step(double* __restrict__ w, const double* __restrict__ u,
+                                               const double* __restrict__ hprev, const double* __restrict__ v,
+                                               size_t n, double* __restrict__ part, unsigned int* __restrict__ ticket,
+                                               double* __restrict__ out)
+{
+   gs_body<T, EPT>(w, u, u ? *hprev : 0.0, v, n, part, ticket, out);
+}
+
+// k_gs_step for several systems of one batch at once (the predict's std solves, fgmres_batch_dev): blockIdx.y
+// runs system s = act[y], whose operands sit ld* doubles apart (w + s ldw, ...), its scalars at hprev[s] and
+// out[s]; one partials / ticket pair per y.  Per system the arithmetic is k_gs_step's (same grid): bitwise.
+template <int T, int EPT>
+__global__ __launch_bounds__(T) void k_gs_batch(double* __restrict__ w, size_t ldw, const double* __restrict__ u,
+                                                size_t ldu, const double* __restrict__ hprev,
+                                                const double* __restrict__ v, size_t ldv, size_t n,
+                                                const int* __restrict__ act, double* __restrict__ part,
+                                                unsigned int* __restrict__ ticket, double* __restrict__ out)
+{
+   const int s = act[blockIdx.y];
+   gs_body<T, EPT>(w + (size_t)s * ldw, u ? u + (size_t)s * ldu : nullptr, u ? hprev[s] : 0.0,
+                   v ? v + (size_t)s * ldv : nullptr, n, part + (size_t)blockIdx.y * kKMaxBlocks,
+                   ticket + (size_t)blockIdx.y * kTicketWords, out + s);
+}
+
+// a[s] *= fac[s] for the systems act[y] (k_scale2's arithmetic)
+__global__ void k_scale_batch(double* __restrict__ a, size_t lda, size_t n, const int* __restrict__ act,
+                              const double* __restrict__ fac)
+{
+   const int s = act[blockIdx.y];
+   const double f = fac[s];
+   double* p = a + (size_t)s * lda;
+   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] *= f;
+}
+
+// x += sum_j c[j] cols[j] (columns in order: k_combine's arithmetic over columns that need not be contiguous)
+__global__ void k_combine_cols(double* __restrict__ x, const double* const* __restrict__ cols, size_t n,
+                               const double* __restrict__ c, int m)
+{
+   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+      double v = x[i];
+      for (int j = 0; j < m; j++) v = fma(c[j], cols[j][i], v);
+      x[i] = v;
+   }
+}
+
+// E[s ld + r0 + s] = 1 (unit columns of the predict's K12 / K22 probes; E zeroed before)
+__global__ void k_set_units(double* __restrict__ E, size_t ld, size_t r0, int m)
+{
+   const int s = blockIdx.x * blockDim.x + threadIdx.x;
+   if (s < m) E[(size_t)s * ld + r0 + s] = 1.0;
+}
+
+// out[s] = Y[s ld + r0 + s]
+__global__ void k_pick_diag(double* __restrict__ out, const double* __restrict__ Y, size_t ld, size_t r0, int m)
+{
+   const int s = blockIdx.x * blockDim.x + threadIdx.x;
+   if (s < m) out[s] = Y[(size_t)s * ld + r0 + s];
 }
 
 // out[0] = (a, b), out[1] = (b, b): the Lanczos (v, z) and ||z||^2 in one pass
@@ -999,6 +1057,354 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
    return 0;
 }
 
+// ---- FGMRES on a batch of right-hand sides (the predict's std solves) ---------------------------------------
+// fgmres_dev's MGS iteration (fgmres.c:3-252, ortho 0) for m systems A x_s = b_s at once, in lockstep: every
+// running system is at the same step, so each projection is ONE launch over all of them (k_gs_batch, grid.y =
+// running systems), the step's Hessenberg entries of every system come back in ONE read, and the operator
+// applications go out together (two vectors per pass on this library's additive operator,
+// additive_matvec_multi).  Per system the Givens recurrence, breakdown exit, restart and tolerance are
+// fgmres_dev's, and so is the arithmetic of every vector kernel (the same bodies and grids): with one system
+// the results are fgmres_dev's.  A system leaves the batch when it converges or breaks down, the others go on.
+// x0 = 0 (the predict's initial guess, nfft_interface.c:1030-1036), so v_0 = b without an operator application.
+// The basis grows in groups of columns as the steps need them (nfft_interface.c:1044 asks for a restart
+// dimension of n: no n x n basis is reserved).  x_s = X + s ldx, b_s = B + s ldb.  Lines that fgmres_dev
+// would print are kept per system and printed in system order at the end.
+struct BatchOut {
+   std::vector<int> iters;
+   std::vector<double> rel_res;
+};
+
+int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* B, size_t ldb, int kdim, int maxits,
+                     int atol, double tol, int print_level, BatchOut& res)
+{
+   const size_t n = cb.n;
+   hipStream_t st = current_stream();
+   const double EPS = DBL_EPSILON;
+   res.iters.assign(m, 0);
+   res.rel_res.assign(m, 0.0);
+   if (m <= 0) return 0;
+   if (cb.comm || cb.n_global != cb.n) return -1;
+   const bool multi = cb.mv_dev && cb.matvec == (func_symmatvec)&Nfft4GPAdditiveNFFTMatSymv;
+   const unsigned ggrid = (unsigned)std::max<size_t>(1, std::min<size_t>((n + 4095) / 4096, kKMaxBlocks));
+   // device scratch: partials / tickets per slot, the step's scalars [j][s], factors, the running list
+   double *part = nullptr, *hd = nullptr, *dfac = nullptr, *dcoef = nullptr;
+   const double** dcols = nullptr;
+   unsigned int* ticket = nullptr;
+   int* dact = nullptr;
+   double* pin = nullptr;  // pinned: [0, m) factors, then the combine's coefficients and column pointers
+   int* pact = nullptr;    // pinned: the running list
+   hipEvent_t pin_ev = nullptr;  // the last copy out of pin / pact
+   std::vector<double*> groups;  // basis column groups (V, then Z when preconditioned)
+   std::vector<double*> Vc, Zc;  // column j of every system: Vc[j] + s n
+   int hcap = 0;                 // columns of hd
+   auto cleanup = [&]() {
+      (void)hipStreamSynchronize(st);
+      for (double* g : groups) (void)hipFree(g);
+      (void)hipFree(part);
+      (void)hipFree(hd);
+      (void)hipFree(dfac);
+      (void)hipFree(dcoef);
+      (void)hipFree(dcols);
+      (void)hipFree(ticket);
+      (void)hipFree(dact);
+      if (pin) (void)hipHostFree(pin);
+      if (pact) (void)hipHostFree(pact);
+      if (pin_ev) (void)hipEventDestroy(pin_ev);
+   };
+   auto fail = [&]() -> int {
+      cleanup();
+      return -1;
+   };
+   const int kpin = 4 * m + 2 * (kdim + 1) + 16;
+   if (dmalloc(&part, (size_t)m * kKMaxBlocks) || dmalloc(&ticket, (size_t)m * kTicketWords) || dmalloc(&dfac, m) ||
+       dmalloc(&dact, m) || dmalloc(&dcoef, (size_t)kdim + 1) || dmalloc(&dcols, (size_t)kdim + 1))
+      return fail();
+   if (hipHostMalloc((void**)&pin, sizeof(double) * kpin) != hipSuccess) {
+      pin = nullptr;
+      return fail();
+   }
+   if (hipHostMalloc((void**)&pact, sizeof(int) * m) != hipSuccess) {
+      pact = nullptr;
+      return fail();
+   }
+   NFFT4GP_HIP_CHECK(hipEventCreateWithFlags(&pin_ev, hipEventDisableTiming));
+   NFFT4GP_HIP_CHECK(hipEventRecord(pin_ev, st));
+   // the staging buffers are rewritten only after the copies out of them have run
+   auto pin_wait = [&]() -> int {
+      NFFT4GP_HIP_CHECK(hipEventSynchronize(pin_ev));
+      return 0;
+   };
+   auto pin_done = [&]() -> int {
+      NFFT4GP_HIP_CHECK(hipEventRecord(pin_ev, st));
+      return 0;
+   };
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(ticket, 0, sizeof(unsigned int) * (size_t)m * kTicketWords, st));
+   // columns [0, need) of the basis (and of Z) allocated, in groups of 16 columns
+   auto ensure_cols = [&](int need) -> int {
+      constexpr int kG = 16;
+      while ((int)Vc.size() < need) {
+         const int g = std::min(kG, std::max(1, need + kG - 1 - (int)Vc.size()));
+         for (int pass = 0; pass < (cb.prec ? 2 : 1); pass++) {
+            double* base = nullptr;
+            if (hipMalloc((void**)&base, sizeof(double) * n * m * g) != hipSuccess) {
+               fprintf(stderr, "nfft4gp_amd: FGMRES batch of %d: no memory for %zu basis columns of %zu\n", m,
+                       Vc.size() + g, n);
+               return -1;
+            }
+            groups.push_back(base);
+            for (int k = 0; k < g; k++) (pass ? Zc : Vc).push_back(base + (size_t)k * n * m);
+         }
+      }
+      return 0;
+   };
+   auto ensure_h = [&](int cols) -> int {
+      if (cols <= hcap) return 0;
+      const int nc = std::max(cols, 2 * hcap);
+      double* nh = nullptr;
+      if (dmalloc(&nh, (size_t)nc * m)) return -1;
+      NFFT4GP_HIP_CHECK(hipStreamSynchronize(st));
+      (void)hipFree(hd);
+      hd = nh;
+      hcap = nc;
+      return 0;
+   };
+   std::vector<int> act;
+   auto upload_act = [&]() -> int {  // stream-ordered: launches already queued still read the old list
+      if (pin_wait()) return -1;
+      memcpy(pact, act.data(), sizeof(int) * act.size());
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(dact, pact, sizeof(int) * act.size(), hipMemcpyHostToDevice, st));
+      return pin_done();
+   };
+   auto read = [&](const double* d, size_t count, std::vector<double>& h) -> int {
+      h.resize(count);
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(h.data(), d, sizeof(double) * count, hipMemcpyDeviceToHost, st));
+      NFFT4GP_HIP_CHECK(hipStreamSynchronize(st));
+      return 0;
+   };
+   // w_s -= hprev[s] u_s (u optional), out[s] = (w_s, v_s) or ||w_s||^2, for the running systems
+   auto gs = [&](double* w, size_t ldw, const double* u, size_t ldu, const double* hprev, const double* v, size_t ldv,
+                 double* out) -> int {
+      hipLaunchKernelGGL((k_gs_batch<1024, 4>), dim3(ggrid, (unsigned)act.size()), dim3(1024), 0, st, w, ldw, u, ldu,
+                         hprev, v, ldv, n, (const int*)dact, part, ticket, out);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   };
+   auto scale = [&](double* a, const std::vector<double>& fac) -> int {
+      if (pin_wait()) return -1;
+      memcpy(pin, fac.data(), sizeof(double) * m);
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(dfac, pin, sizeof(double) * m, hipMemcpyHostToDevice, st));
+      if (pin_done()) return -1;
+      hipLaunchKernelGGL(k_scale_batch, dim3(std::max(1, egrid(n) / std::max(1, (int)act.size())), (unsigned)act.size()),
+                         dim3(256), 0, st, a, n, n, (const int*)dact, (const double*)dfac);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   };
+   // y_s = A x_s for the running systems
+   auto apply = [&](const std::vector<const double*>& xs, const std::vector<double*>& ys) -> int {
+      if (multi) return additive_matvec_multi(cb.mat, (int)xs.size(), 1.0, xs.data(), 0.0, ys.data());
+      for (size_t k = 0; k < xs.size(); k++)
+         if (cb.apply(1.0, const_cast<double*>(xs[k]), 0.0, ys[k])) return -1;
+      return 0;
+   };
+   // x_s += sum_j c[j] cols[j] + s n
+   auto combine = [&](int s, const std::vector<double*>& cols, int cnt, const double* c) -> int {
+      if (cnt <= 0) return 0;
+      if (pin_wait()) return -1;
+      double* pc = pin + m;
+      const double** pp = (const double**)(pin + m + cnt);
+      for (int j = 0; j < cnt; j++) {
+         pc[j] = c[j];
+         pp[j] = cols[j] + (size_t)s * n;
+      }
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(dcoef, pc, sizeof(double) * cnt, hipMemcpyHostToDevice, st));
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(dcols, pp, sizeof(double*) * cnt, hipMemcpyHostToDevice, st));
+      if (pin_done()) return -1;
+      hipLaunchKernelGGL(k_combine_cols, dim3(egrid(n)), dim3(256), 0, st, X + (size_t)s * ldx, (const double* const*)dcols,
+                         n, (const double*)dcoef, cnt);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   };
+   if (2 * (kdim + 1) + 2 * m > kpin) return fail();
+
+   struct Sys {
+      double normb = 0, normr = 0, tolr = 0, rel_prev = 0;
+      std::vector<std::vector<double>> H;  // H[i - 1]: column i - 1 (i + 1 entries)
+      std::vector<double> cs, sn, rs;
+      std::string log;
+      bool done = false;
+   };
+   std::vector<Sys> S(m);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wformat-security"
+   auto logf = [&](int s, const char* fmt, auto... a) {  // (fmt: the literals below)
+      char buf[256];
+      snprintf(buf, sizeof(buf), fmt, a...);
+      S[s].log += buf;
+   };
+#pragma clang diagnostic pop
+   for (int s = 0; s < m; s++) NFFT4GP_HIP_CHECK(hipMemsetAsync(X + (size_t)s * ldx, 0, sizeof(double) * n, st));
+   if (ensure_cols(2) || ensure_h(2)) return fail();
+   act.resize(m);
+   for (int s = 0; s < m; s++) act[s] = s;
+   if (upload_act()) return fail();
+   // ||b_s|| (c.norm: the dot of b with itself), then v_0 = b - A 0 = b
+   std::vector<double> hh;
+   if (gs(const_cast<double*>(B), ldb, nullptr, 0, nullptr, B, ldb, hd) || read(hd, m, hh)) return fail();
+   for (int s = 0; s < m; s++) {
+      S[s].normb = std::sqrt(hh[s]);
+      S[s].normr = S[s].normb;  // ||v_0|| = ||b||: the same vector
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(Vc[0] + (size_t)s * n, B + (size_t)s * ldb, sizeof(double) * n,
+                                       hipMemcpyDeviceToDevice, st));
+   }
+   act.clear();
+   for (int s = 0; s < m; s++) {
+      Sys& y = S[s];
+      if (y.normb < EPS) {  // x = 0 (set above), rel_res 0, 0 iterations
+         y.done = true;
+         continue;
+      }
+      y.tolr = atol ? tol : tol * y.normb;
+      y.rel_prev = y.normr / y.normb;
+      if (print_level > 0) {
+         logf(s, "--------------------------------------------------------------------------------\n");
+         logf(s, "Start FlexGMRES(%d)\n", kdim);
+         logf(s, "Residual Tol: %e\nMax number of inner iterations: %d\n", y.tolr, maxits);
+         logf(s, "--------------------------------------------------------------------------------\n");
+         logf(s, "Step    Residual norm  Relative res.  Convergence Rate\n");
+         logf(s, "%5d   %8e   %8e   N/A\n", 0, y.normr, y.rel_prev);
+      }
+      act.push_back(s);
+   }
+   if (upload_act()) return fail();
+   // the end of a cycle of system s after i steps (fgmres.c:221-235): back substitution, x += Z y
+   auto finish_cycle = [&](int s, int i) -> int {
+      Sys& y = S[s];
+      if (i <= 0) return 0;
+      std::vector<double>& rs = y.rs;
+      rs[i - 1] /= y.H[i - 1][i - 1];
+      for (int k = i - 2; k >= 0; k--) {
+         for (int j = k + 1; j < i; j++) rs[k] -= y.H[j][k] * rs[j];
+         rs[k] /= y.H[k][k];
+      }
+      return combine(s, cb.prec ? Zc : Vc, i, rs.data());
+   };
+   int iter = 0;
+   std::vector<double> fac(m, 0.0);
+   while (!act.empty() && iter < maxits) {
+      for (int s : act) {
+         S[s].rs.assign(1, S[s].normr);
+         S[s].H.clear();
+         S[s].cs.clear();
+         S[s].sn.clear();
+         fac[s] = 1.0 / S[s].normr;
+      }
+      if (scale(Vc[0], fac)) return fail();
+      int i = 0;
+      while (!act.empty() && i < kdim && iter < maxits) {
+         i++;
+         iter++;
+         if (ensure_cols(i + 1) || ensure_h(i + 1)) return fail();
+         std::vector<const double*> xs;
+         std::vector<double*> ys;
+         for (int s : act) {
+            double* v = Vc[i - 1] + (size_t)s * n;
+            if (cb.prec) {
+               double* z = Zc[i - 1] + (size_t)s * n;
+               if (cb.solve(z, v)) return fail();
+               xs.push_back(z);
+            } else {
+               xs.push_back(v);
+            }
+            ys.push_back(Vc[i] + (size_t)s * n);
+         }
+         if (apply(xs, ys)) return fail();
+         // Nfft4GPModifiedGS (matops.c:274-346) with k = i - 1, every running system per launch
+         for (int j = 0; j < i; j++)
+            if (gs(Vc[i], n, j ? Vc[j - 1] : nullptr, n, j ? hd + (size_t)(j - 1) * m : nullptr, Vc[j], n,
+                   hd + (size_t)j * m))
+               return fail();
+         if (gs(Vc[i], n, Vc[i - 1], n, hd + (size_t)(i - 1) * m, nullptr, 0, hd + (size_t)i * m)) return fail();
+         if (read(hd, (size_t)(i + 1) * m, hh)) return fail();
+         std::vector<int> keep, conv;
+         for (int s : act) {
+            Sys& y = S[s];
+            const double t = std::sqrt(hh[(size_t)i * m + s]);
+            std::vector<double> Hc(i + 1);
+            for (int j = 0; j < i; j++) Hc[j] = hh[(size_t)j * m + s];
+            Hc[i] = t;
+            fac[s] = 1.0 / t;
+            for (int j = 1; j < i; j++) {
+               const double hii = Hc[j - 1];
+               Hc[j - 1] = y.cs[j - 1] * hii + y.sn[j - 1] * Hc[j];
+               Hc[j] = -y.sn[j - 1] * hii + y.cs[j - 1] * Hc[j];
+            }
+            const double hii = Hc[i - 1], hii1 = Hc[i];
+            const double gam = std::sqrt(hii * hii + hii1 * hii1);
+            if (std::fabs(gam) < EPS) {  // fgmres.c:179-182: leave without updating x
+               y.done = true;
+               res.iters[s] = iter;
+               res.rel_res[s] = y.normr / y.normb;
+               continue;
+            }
+            y.cs.push_back(hii / gam);
+            y.sn.push_back(hii1 / gam);
+            y.rs.push_back(-y.sn[i - 1] * y.rs[i - 1]);
+            y.rs[i - 1] = y.cs[i - 1] * y.rs[i - 1];
+            Hc[i - 1] = y.cs[i - 1] * hii + y.sn[i - 1] * hii1;
+            y.H.push_back(std::move(Hc));
+            y.normr = std::fabs(y.rs[i]);
+            const double rel = y.normr / y.normb;
+            if (print_level > 0) logf(s, "%5d   %8e   %8e   %8.6f\n", iter, y.normr, rel, rel / y.rel_prev);
+            y.rel_prev = rel;
+            (y.normr <= y.tolr ? conv : keep).push_back(s);
+         }
+         if (scale(Vc[i], fac)) return fail();
+         for (int s : conv) {  // converged in this cycle: its end (fgmres.c:212-235)
+            if (print_level == 0)
+               logf(s, "Rel. residual at the end of current cycle (# of steps per cycle/total its: %d/%d): %e \n", kdim,
+                    iter, S[s].rel_prev);
+            if (finish_cycle(s, i)) return fail();
+            S[s].done = true;
+            res.iters[s] = iter;
+            res.rel_res[s] = S[s].normr / S[s].normb;
+         }
+         if (keep.size() != act.size()) {
+            act = keep;
+            if (!act.empty() && upload_act()) return fail();
+         }
+      }
+      if (act.empty()) break;
+      // the cycle ends for every running system together (restart dimension or maxits reached)
+      for (int s : act) {
+         if (print_level == 0)
+            logf(s, "Rel. residual at the end of current cycle (# of steps per cycle/total its: %d/%d): %e \n", kdim,
+                 iter, S[s].rel_prev);
+         if (finish_cycle(s, i)) return fail();
+      }
+      if (iter >= maxits) break;
+      // restart (fgmres.c:236-243): v = b - A x; normr keeps the Givens estimate
+      std::vector<const double*> xs;
+      std::vector<double*> ys;
+      for (int s : act) {
+         xs.push_back(X + (size_t)s * ldx);
+         ys.push_back(Vc[1] + (size_t)s * n);
+      }
+      if (apply(xs, ys)) return fail();
+      for (int s : act)
+         hipLaunchKernelGGL(k_sub, dim3(egrid(n)), dim3(256), 0, st, Vc[0] + (size_t)s * n, B + (size_t)s * ldb,
+                            (const double*)(Vc[1] + (size_t)s * n), n);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+   }
+   for (int s : act) {
+      res.iters[s] = iter;
+      res.rel_res[s] = S[s].normr / S[s].normb;
+   }
+   for (int s = 0; s < m; s++)
+      if (!S[s].log.empty()) fputs(S[s].log.c_str(), stdout);
+   cleanup();
+   return 0;
+}
+
 // ---- Lanczos (lanczos.c:3-419) on device vectors ----------------------------------------------------
 // Re-orthogonalisation of w against V[0..k] (dots) / Z[0..k] (updates), adding the projections on v_{k-1}
 // and v_k to te / td (Nfft4GPModifiedGS2, matops.c:348-440: MGS over the whole basis, repeated while ||w||
@@ -1756,26 +2162,85 @@ int Nfft4GPAdditiveNFFTGpPredict(double* x, double* data, double* label, int n, 
    NFFT4GP_HIP_CHECK(hipStreamSynchronize(s));
    if (!*label_predictp) *label_predictp = lp;
    if (std_predictp) {
-      // diag of K22 - K21 K11^{-1} K12, one column at a time (nfft_interface.c:993-1060)
+      // diag of K22 - K21 K11^{-1} K12 (nfft_interface.c:993-1060), a batch of prediction points at a time:
+      // the K12 columns and K22 diagonal entries of the batch by one operator application to its unit vectors
+      // (two per pass on this library's operator), then its solves K11 x = K12(:, i) in lockstep
+      // (fgmres_batch_dev: restart dimension and iteration limit n as the reference), then the dots
       double* sp = *std_predictp ? *std_predictp : (double*)malloc(sizeof(double) * std::max(1, n_predict));
       std::vector<double> hs(n_predict);
-      const double one = 1.0;
-      for (int i = 0; i < n_predict; i++) {
-         NFFT4GP_HIP_CHECK(hipMemsetAsync(iKY, 0, sizeof(double) * na, s));
-         NFFT4GP_HIP_CHECK(hipMemcpyAsync(iKY + n + i, &one, sizeof(double), hipMemcpyHostToDevice, s));
-         if (cba.apply(1.0, iKY, 0.0, helper)) {
-            cleanup();
-            return -1;
+      int bm = 16;
+      if (const char* e = getenv("NFFT4GP_AMD_PREDICT_BATCH")) bm = std::max(1, std::min(256, atoi(e)));
+      bm = std::max(1, std::min(bm, n_predict));
+      double *E = nullptr, *Y = nullptr, *Xs = nullptr, *dsc = nullptr;
+      int* dall = nullptr;
+      auto bfree = [&]() {
+         (void)hipStreamSynchronize(s);
+         (void)hipFree(E);
+         (void)hipFree(Y);
+         (void)hipFree(Xs);
+         (void)hipFree(dsc);
+         (void)hipFree(dall);
+      };
+      if (dmalloc(&E, (size_t)na * bm) || dmalloc(&Y, (size_t)na * bm) || dmalloc(&Xs, (size_t)n * bm) ||
+          dmalloc(&dsc, 2 * (size_t)bm) || dmalloc(&dall, bm)) {
+         bfree();
+         cleanup();
+         return -1;
+      }
+      const bool multi = cba.mv_dev && cba.matvec == (func_symmatvec)&Nfft4GPAdditiveNFFTMatSymv;
+      {
+         std::vector<int> ids(bm);
+         for (int k = 0; k < bm; k++) ids[k] = k;
+         NFFT4GP_HIP_CHECK(hipMemcpy(dall, ids.data(), sizeof(int) * bm, hipMemcpyHostToDevice));
+      }
+      double* gpart = nullptr;
+      unsigned int* gtick = nullptr;
+      if (dmalloc(&gpart, (size_t)bm * kKMaxBlocks) || dmalloc(&gtick, (size_t)bm * kTicketWords)) {
+         (void)hipFree(gpart);
+         bfree();
+         cleanup();
+         return -1;
+      }
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(gtick, 0, sizeof(unsigned int) * (size_t)bm * kTicketWords, s));
+      int rc = 0;
+      for (int i0 = 0; i0 < n_predict && !rc; i0 += bm) {
+         const int mb = std::min(bm, n_predict - i0);
+         NFFT4GP_HIP_CHECK(hipMemsetAsync(E, 0, sizeof(double) * (size_t)na * mb, s));
+         hipLaunchKernelGGL(k_set_units, dim3((mb + 255) / 256), dim3(256), 0, s, E, (size_t)na, (size_t)(n + i0), mb);
+         std::vector<const double*> xs(mb);
+         std::vector<double*> ys(mb);
+         for (int k = 0; k < mb; k++) {
+            xs[k] = E + (size_t)k * na;
+            ys[k] = Y + (size_t)k * na;
          }
-         double K22i;
-         if (c.read(helper + n + i, 1, &K22i)) return -1;
-         NFFT4GP_HIP_CHECK(hipMemsetAsync(iKY + n + i, 0, sizeof(double), s));
-         if (fgmres_dev(cb11, iKY, helper, n, n, atol, tol, &rel_res, &rel_res_v, &niter, print_level)) {
-            cleanup();
-            return -1;
+         if (multi) {
+            rc = additive_matvec_multi(cba.mat, mb, 1.0, xs.data(), 0.0, ys.data());
+         } else {
+            for (int k = 0; k < mb && !rc; k++) rc = cba.apply(1.0, const_cast<double*>(xs[k]), 0.0, ys[k]);
          }
-         free(rel_res_v);
-         hs[i] = std::sqrt(std::fabs(K22i - c.dot(helper, iKY)));
+         if (rc) break;
+         hipLaunchKernelGGL(k_pick_diag, dim3((mb + 255) / 256), dim3(256), 0, s, dsc, (const double*)Y, (size_t)na,
+                            (size_t)(n + i0), mb);
+         BatchOut bo;
+         if ((rc = fgmres_batch_dev(cb11, mb, Xs, (size_t)n, Y, (size_t)na, n, n, atol, tol, print_level, bo))) break;
+         // (K12(:, i), x_i) per point: k_gs_step's dot, batched
+         const unsigned gg = (unsigned)std::max<size_t>(1, std::min<size_t>(((size_t)n + 4095) / 4096, kKMaxBlocks));
+         hipLaunchKernelGGL((k_gs_batch<1024, 4>), dim3(gg, (unsigned)mb), dim3(1024), 0, s, Y, (size_t)na,
+                            (const double*)nullptr, (size_t)0, (const double*)nullptr, (const double*)Xs, (size_t)n,
+                            (size_t)n, (const int*)dall, gpart, gtick, dsc + bm);
+         NFFT4GP_HIP_CHECK(hipGetLastError());
+         std::vector<double> h2(2 * (size_t)bm);
+         if ((rc = c.read(dsc, 2 * bm, h2.data()))) break;
+         for (int k = 0; k < mb; k++) hs[i0 + k] = std::sqrt(std::fabs(h2[k] - h2[bm + k]));
+      }
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(gpart);
+      (void)hipFree(gtick);
+      bfree();
+      if (rc) {
+         if (!*std_predictp) free(sp);
+         cleanup();
+         return -1;
       }
       if (is_device_ptr(sp))
          NFFT4GP_HIP_CHECK(hipMemcpy(sp, hs.data(), sizeof(double) * n_predict, hipMemcpyHostToDevice));

@@ -195,6 +195,41 @@ def test_gp_predict_matches_restated_reference(torch_cuda):
     assert s2 is None and rel(m2, mean) < 1e-12  # LDS atomics in the spread: not bitwise run to run
 
 
+def test_gp_predict_std_batches(torch_cuda, monkeypatch):
+    """The std solves in lockstep batches (fgmres_batch_dev, NFFT4GP_AMD_PREDICT_BATCH): one point per batch,
+    the default 16 and a batch larger than the points give the same std (the two-vector matvec sums in a
+    different order than the one-vector one: rounding-level differences, amplified by the solve)."""
+    z = load("predict_synth")
+    out = {}
+    for bm in ("1", "16", "64"):
+        monkeypatch.setenv("NFFT4GP_AMD_PREDICT_BATCH", bm)
+        out[bm] = amd.gp_predict(z["X"], z["Xp"], z["windows"], 4, 1, z["y"], z["hyper"], maxits=int(z["maxits"]),
+                                 tol=float(z["tol"]), with_std=True)[1]
+    for bm in ("16", "64"):
+        np.testing.assert_allclose(out[bm], out["1"], rtol=1e-8)
+    np.testing.assert_allclose(out["16"], z["std"], rtol=1e-6)
+
+
+def test_gp_predict_std_beyond_the_scalar_limit(torch_cuda):
+    """n = 5000 training points: the std solves ask for restart dimension n (nfft_interface.c:1044); the batch
+    solver grows its basis as the steps need it (the one-system FGMRES caps the restart at 4094).  Against the
+    reference's own FGMRES over the oracle operator (oracle/_ref)."""
+    from oracle import ref_available, ref_nfft_gp_predict
+    if not ref_available():
+        pytest.skip("oracle/_ref not built")
+    rng = np.random.default_rng(77)
+    n, npred = 5000, 5
+    X = rng.random((n, 4))
+    Xp = rng.random((npred, 4))
+    y = np.sin(3 * X[:, 0]) + X[:, 1] ** 2 + 0.05 * rng.standard_normal(n)
+    win = np.arange(4, dtype=np.int32)
+    hyper = np.array([0.3, -0.5, -2.0])
+    mean, std = amd.gp_predict(X, Xp, win, 4, 1, y, hyper, maxits=300, tol=1e-10, with_std=True)
+    m0, s0 = ref_nfft_gp_predict(X, Xp, win, 4, 1, y, hyper, 300, 1e-10)
+    assert rel(mean, m0) < 1e-7
+    np.testing.assert_allclose(std, s0, rtol=1e-6)
+
+
 def test_gp_loss_wrapper(torch_cuda, case):
     z, k, op = case
     loss, grad = amd.gp_loss(z["X"], z["windows"], int(z["nw"]), int(z["dw"]), z["b"], k["hyper"],
