@@ -107,9 +107,13 @@ __global__ void k_axpy(double a, const double* __restrict__ x, size_t n, double*
 // ---------------------------------------------------------------------------------------------
 struct PcgState {
    double normb, tolb, pq, normr2;
-   int status;     // 0 running, 1 converged candidate, 2 rho == 0, 3 beta == 0, 4 pq <= 0
+   int status;     // 0 running, 1 converged candidate, 2 rho == 0, 3 beta == 0, 4 pq <= 0, 5 k_pcg_xr's
+                   // in-kernel wait gave up (an error)
    int flag_iter;  // iteration that set status
    double loc[2];  // distributed PCG: this rank's partial dot (0) / ||r||^2 (1), all-reduced in place
+   double beta_next;  // FUSEP k_pcg_xr: the next iteration's beta, handed from the last workgroup to the others
+   int bar;           // FUSEP k_pcg_xr: +ii (apply beta) / -ii (no update) once beta_next is stored
+   int pad;
 };
 
 struct PcgSlot {   // pinned host memory, written by the last kernel of each iteration
@@ -236,14 +240,18 @@ __device__ void pcg_xr_tail(double tot, PcgState* st, double* __restrict__ rhos,
 
 // x += alpha p ; r -= alpha q ; ||r|| ; convergence test ; status slot  (pcg.c:168-182).  T = 1024: a
 // quarter of the block partials for the last block (the MGS step's measurement, krylov.hip)
-template <int T>
+// FUSEP (no preconditioner, one GPU, every element in the first pass of a grid that is resident at once): also
+// the next iteration's direction update p = beta p + r (k_pcg_pupdate of ii + 1, with its rho == 0 / beta == 0
+// tests) from the p and r values still in registers.  The last workgroup, which has ||r||^2, hands beta to
+// the others through st (agent-scope stores and loads, as reduce.hpp's partials); they wait for it, boundedly.
+template <int T, bool FUSEP = false>
 __global__ __launch_bounds__(T) void k_pcg_xr(double* __restrict__ x, double* __restrict__ r,
-                                                        const double* __restrict__ p, const double* __restrict__ q,
+                                                        double* __restrict__ p, const double* __restrict__ q,
                                                         size_t n, double* __restrict__ part,
                                                         unsigned int* __restrict__ ticket, PcgState* st,
                                                         double* __restrict__ rhos, double* __restrict__ hist, int ii,
                                                         int rho_from_norm, int check_pq, PcgSlot* slot,
-                                                        double* __restrict__ loc)
+                                                        double* __restrict__ loc, int do_p = 0)
 {
    // loc != NULL (distributed PCG): the local ||r||^2 goes to *loc and k_pcg_xr_fin, after the all-reduce,
    // makes the convergence test and writes the status slot
@@ -261,6 +269,7 @@ __global__ __launch_bounds__(T) void k_pcg_xr(double* __restrict__ x, double* __
    }
    const double a = rhos[ii] / st->pq;
    double acc = 0.0;
+   double p_keep[kEPT], r_keep[kEPT];  // FUSEP: this thread's (single pass) p and new r
    const size_t stride = (size_t)gridDim.x * T * kEPT;
    for (size_t i0 = (size_t)blockIdx.x * T * kEPT + threadIdx.x; i0 < n; i0 += stride) {
       double xv[kEPT], rv[kEPT], pv[kEPT], qv[kEPT];
@@ -279,6 +288,10 @@ __global__ __launch_bounds__(T) void k_pcg_xr(double* __restrict__ x, double* __
          const double xi = xv[u] + a * pv[u];
          const double ri = rv[u] + (-a) * qv[u];
          acc = fma(ri, ri, acc);
+         if (FUSEP) {
+            p_keep[u] = pv[u];
+            r_keep[u] = ri;
+         }
          if (i < n) {
             x[i] = xi;
             r[i] = ri;
@@ -287,12 +300,84 @@ __global__ __launch_bounds__(T) void k_pcg_xr(double* __restrict__ x, double* __
    }
    acc = block_sum0<T>(acc);
    double tot;
-   if (!grid_total<T>(acc, part, ticket, &tot) || threadIdx.x != 0) return;
-   if (loc) {
-      *loc = tot;
-      return;
+   if constexpr (!FUSEP) {
+      if (!grid_total<T>(acc, part, ticket, &tot) || threadIdx.x != 0) return;
+      if (loc) {
+         *loc = tot;
+         return;
+      }
+      pcg_xr_tail(tot, st, rhos, hist, ii, rho_from_norm, slot);
+   } else {
+      __shared__ double s_beta;
+      __shared__ int s_go;
+      if (grid_total<T>(acc, part, ticket, &tot)) {
+         if (threadIdx.x == 0) {
+            // pcg_xr_tail's bookkeeping, with the status slot (a system-scope release: an L2 write-back) written
+            // after the others are released, and the next iteration's tests (k_pcg_pupdate's) in between
+            const double normr = sqrt(tot);
+            st->normr2 = normr;
+            hist[ii] = normr / st->normb;
+            rhos[ii + 1] = tot;  // z = r next iteration: rho = (r, r)
+            const int stat_ii = normr <= st->tolb ? 1 : 0;
+            if (stat_ii) {
+               st->status = 1;
+               st->flag_iter = ii;
+            }
+            int go = 0;
+            double beta = 0.0;
+            if (do_p && !stat_ii) {
+               const double rho = tot;
+               beta = rho / rhos[ii];
+               if (rho == 0.0) {
+                  st->status = 2;
+                  st->flag_iter = ii + 1;
+               } else if (beta == 0.0) {
+                  st->status = 3;
+                  st->flag_iter = ii + 1;
+               } else {
+                  go = 1;
+               }
+            }
+            __hip_atomic_store(&st->beta_next, beta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&st->bar, go ? ii : -ii, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_beta = beta;
+            s_go = go;
+            // slot ii as pcg_slot_write leaves it (status of iteration ii; 2 / 3 belong to ii + 1's slot)
+            slot->normr = normr;
+            slot->status = stat_ii;
+            slot->flag_iter = ii;
+            __hip_atomic_store(&slot->seq, ii, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+         }
+      } else if (threadIdx.x == 0) {
+         int b = 0;
+         for (long spin = 0; spin < (1l << 22); spin++) {
+            b = __hip_atomic_load(&st->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (b == ii || b == -ii) break;
+            __builtin_amdgcn_s_sleep(2);
+         }
+         if (b == ii) {
+            s_beta = __hip_atomic_load(&st->beta_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_go = 1;
+         } else {
+            s_go = 0;
+            if (b != -ii) {  // the last workgroup never arrived: fail loudly (host: status 5)
+               __hip_atomic_store(&st->status, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+               __hip_atomic_store(&st->flag_iter, ii, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+         }
+      }
+      __syncthreads();
+      if (!s_go) return;
+      const double beta = s_beta;
+      // k_pcg_pupdate's update for this thread's elements (the grid covers n in one pass: i0 < T kEPT gridDim.x)
+      const size_t i0 = (size_t)blockIdx.x * T * kEPT + threadIdx.x;
+#pragma unroll
+      for (int u = 0; u < kEPT; u++) {
+         const size_t i = i0 + (size_t)u * T;
+         if (i < n) p[i] = beta * p_keep[u] + r_keep[u];
+      }
    }
-   pcg_xr_tail(tot, st, rhos, hist, ii, rho_from_norm, slot);
 }
 
 __global__ void k_pcg_xr_fin(PcgState* st, double* __restrict__ rhos, double* __restrict__ hist, int ii,
@@ -748,6 +833,24 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
                                         (is_dist && dinfo.fused_dot));
    double* loc0 = red ? &st->loc[0] : nullptr;  // device addresses inside st
    double* loc1 = red ? &st->loc[1] : nullptr;
+   // the direction update folded into k_pcg_xr (FUSEP): no preconditioner, one GPU, n covered by one pass of a
+   // grid that fits the chip at once (its workgroups wait for the last one); NFFT4GP_AMD_PCG_FUSEP=0 disables
+   bool fusep = !prec_data && !red && (size_t)g_xr * 1024 * kEPT >= N;
+   if (fusep) {
+      static int occ = -1, ncu = 0;
+      if (occ < 0) {
+         int dev = 0;
+         hipDeviceProp_t prop;
+         if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+             hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_pcg_xr<1024, true>, 1024, 0) != hipSuccess)
+            occ = 0;
+         else
+            ncu = prop.multiProcessorCount;
+      }
+      const char* e = getenv("NFFT4GP_AMD_PCG_FUSEP");
+      fusep = occ > 0 && g_xr <= occ * ncu && !(e && atoi(e) == 0);
+   }
+   bool need_p = true;  // the next iteration's p update is not done yet (first iteration, after a resume)
    // iterations in flight ahead of the host's status check (1 when printing every step)
    const int lag = print_level > 0 ? 1 : PcgScratch::kSlots;
    double prev_rel = rel_res_v[0];
@@ -769,7 +872,8 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
             }
             zz = z;
          }
-         hipLaunchKernelGGL(k_pcg_pupdate, dim3(ge), dim3(kVecThreads), 0, s, p, zz, N, st, rhos, ii);
+         if (need_p || !fusep)
+            hipLaunchKernelGGL(k_pcg_pupdate, dim3(ge), dim3(kVecThreads), 0, s, p, zz, N, st, rhos, ii);
          if (fused_dot) {
             // q = A p with (q, p) formed inside the interpolation kernel's epilogue
             if (is_dist) {
@@ -791,8 +895,15 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
             }
          }
          PcgSlot* slot = slots_d + (ii % PcgScratch::kSlots);
-         hipLaunchKernelGGL(k_pcg_xr<1024>, dim3(g_xr), dim3(1024), 0, s, vx.d, r, p, q, N, g_pcg.part, g_pcg.ticket,
-                            st, rhos, hist_d, ii, prec_data ? 0 : 1, fused_dot ? 1 : 0, slot, loc1);
+         if (fusep) {
+            hipLaunchKernelGGL((k_pcg_xr<1024, true>), dim3(g_xr), dim3(1024), 0, s, vx.d, r, p, q, N, g_pcg.part,
+                               g_pcg.ticket, st, rhos, hist_d, ii, 1, fused_dot ? 1 : 0, slot, (double*)nullptr,
+                               ii < maxits ? 1 : 0);
+            need_p = false;
+         } else {
+            hipLaunchKernelGGL(k_pcg_xr<1024>, dim3(g_xr), dim3(1024), 0, s, vx.d, r, p, q, N, g_pcg.part,
+                               g_pcg.ticket, st, rhos, hist_d, ii, prec_data ? 0 : 1, fused_dot ? 1 : 0, slot, loc1);
+         }
          if (red) {
             if (red->allreduce(loc1, 1, s)) { rc = -1; break; }
             hipLaunchKernelGGL(k_pcg_xr_fin, dim3(1), dim3(64), 0, s, st, rhos, hist_d, ii, prec_data ? 0 : 1, slot,
@@ -839,6 +950,11 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
       NFFT4GP_HIP_CHECK(hipMemcpy(&h, st, sizeof(h), hipMemcpyDeviceToHost));
       NFFT4GP_HIP_CHECK(hipMemcpy(rel_res_v + 1, hist_d + 1, sizeof(double) * (size_t)fi, hipMemcpyDeviceToHost));
       normr2 = h.normr2;
+      if (status == 5) {
+         fprintf(stderr, "nfft4gp_amd: PCG iteration %d: the fused update's wait for its last workgroup gave up\n", fi);
+         rc = -1;
+         break;
+      }
       if (status != 1) {
          if (print_level > 1) {
             if (status == 2) printf("rho = %.16e\n", 0.0);
@@ -869,6 +985,7 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
       prev_rel = rel_res_v[fi];
       ii = fi + 1;
       next_check = fi + 1;
+      need_p = true;  // iteration fi's fused update saw its status and skipped p
    }
    if (!rc && iter == 0) {
       // not converged (maxits or breakdown): the history of the completed iterations

@@ -48,14 +48,18 @@ def test_matvec_and_grad_bitwise_reproducible(torch_cuda, config_c_op):
     assert e < 1e-12 and eg < 1e-12, (e, eg)
 
 
-def test_pcg_bitwise_reproducible(torch_cuda, config_c_op):
-    """Two PCG solves to 1e-6 at config C, l = 0.1 (the bench's PCG leg): the same iterations, history and x."""
+@pytest.mark.parametrize("fusep", ["1", "0"], ids=["fused_update", "separate_update"])
+def test_pcg_bitwise_reproducible(torch_cuda, config_c_op, monkeypatch, fusep):
+    """Two PCG solves to 1e-6 at config C, l = 0.1 (the bench's PCG leg): the same iterations, history and x.
+    The second solve of the fused_update case runs with the direction update as its own launch
+    (NFFT4GP_AMD_PCG_FUSEP=0, k_pcg_pupdate): the fused k_pcg_xr does the same arithmetic, so the same bits."""
     torch = torch_cuda
     op, _ = config_c_op
     n = op.n
     b = torch.tensor(np.random.default_rng(907).random(n) - 0.5, device="cuda")
     runs = []
-    for _ in range(2):
+    for k in range(2):
+        monkeypatch.setenv("NFFT4GP_AMD_PCG_FUSEP", "0" if (fusep == "0" or k == 1) else "1")
         x = torch.zeros(n, dtype=torch.float64, device="cuda")
         _, relres, hist, it = amd.pcg(op, b, x, maxits=3000, tol=1e-6)
         torch.cuda.synchronize()
