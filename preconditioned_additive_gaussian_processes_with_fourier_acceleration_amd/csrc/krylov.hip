@@ -1558,9 +1558,87 @@ struct LanczosRun {
       v = V + (size_t)iter * n;
    }
    // the rest of the step; 1 ends the loop (breakdown, or convergence in the first loop)
+   // the fast step (one host read): k of this step, and whether its scalars fit a region of kRegion doubles
+   static constexpr int kB0 = 8;
+   static constexpr int kRegion = KScratch::kScal / 2;
+   int step_k(bool first_loop) const { return first_loop ? std::min(iter - 1, wsize) : iter - 1; }
+   bool fast_ok(bool first_loop) const { return kB0 + step_k(first_loop) + 1 + 4 <= kRegion; }
+   int region_len(bool first_loop) const { return kB0 + step_k(first_loop) + 1 + 4; }
+   // mgs2's local pass and first whole-basis pass, then (speculatively) the preconditioner and k_dot2 of the
+   // step, scalars into hd[0, region_len): the host needs mgs2's scalars only to decide whether a further pass
+   // is due (rare after the local pass) or w broke down, and in both cases the speculative results are
+   // dropped (a further pass recomputes them; a breakdown restarts v and z).  Same kernels, same order, same
+   // values as mgs2 followed by the solve and the dot.
+   int step_enqueue(bool first_loop, double* hd)
+   {
+      const int k = step_k(first_loop);
+      const int m = k + 1;
+      const int j0 = k >= 1 ? k - 1 : 0;
+      const int ml = k + 1 - j0;
+      double* o = hd + kB0 + m + 2;
+      if (c.block_gs(z, V + (size_t)j0 * n, Z + (size_t)j0 * n, ml, hd, 1)) return -1;
+      if (c.block_gs(z, V, Z, m, hd + kB0, 0)) return -1;
+      if (cb.prec && cb.solve(v, z)) return -1;
+      hipLaunchKernelGGL(k_dot2, dim3(kgrid(n)), dim3(kKThreads), 0, c.s, v, z, n, g_k.part, g_k.ticket, g_k.part2,
+                         g_k.ticket2, o);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return c.red(o, 2);
+   }
+   // the host side of step_enqueue's scalars hh (read back): mgs2's bookkeeping and repeat rule, then the step's
+   // tail; 1 ends the loop
+   int step_after(bool first_loop, const double* hh)
+   {
+      const int k = step_k(first_loop);
+      const int m = k + 1;
+      const int j0 = k >= 1 ? k - 1 : 0;
+      const int ml = k + 1 - j0;
+      double te_dummy;
+      double* tdp = TD + iter - 1;
+      double* tep = iter >= 2 ? TE + iter - 2 : &te_dummy;
+      if (k >= 1) *tep = hh[0];
+      *tdp = hh[ml - 1];
+      double normw = std::sqrt(hh[ml]);  // ||w|| after the local pass
+      if (normw < DBL_EPSILON) {          // mgs2 stops after the local pass
+         t = normw;
+         return 1;
+      }
+      const double* h = hh + kB0;
+      if (k >= 1) *tep += h[k - 1];
+      *tdp += h[k];
+      t = std::sqrt(h[k + 1]);
+      bool again = t < normw * 0.7071 && t >= DBL_EPSILON;
+      double vz[2] = {hh[kB0 + m + 2], hh[kB0 + m + 3]};
+      if (again) {
+         double* hd = g_k.scal;
+         std::vector<double> h2(k + 2);
+         while (again) {  // mgs2's repeat rule, then the solve and the dot of the final w
+            normw = t;
+            if (c.block_gs(z, V, Z, m, hd, 0) || c.read(hd, k + 2, h2.data())) return -1;
+            if (k >= 1) *tep += h2[k - 1];
+            *tdp += h2[k];
+            t = std::sqrt(h2[k + 1]);
+            again = t < normw * 0.7071 && t >= DBL_EPSILON;
+         }
+         if (t < EPS) return 1;
+         if (cb.prec && cb.solve(v, z)) return -1;
+         double* o2 = g_k.scal + KScratch::kScal - 2;
+         hipLaunchKernelGGL(k_dot2, dim3(kgrid(n)), dim3(kKThreads), 0, c.s, v, z, n, g_k.part, g_k.ticket,
+                            g_k.part2, g_k.ticket2, o2);
+         if (c.red(o2, 2) || c.read(o2, 2, vz)) return -1;
+      } else if (t < EPS) {
+         return 1;
+      }
+      return step_tail(first_loop, vz);
+   }
    int step_end(bool first_loop)
    {
-      const int k = first_loop ? std::min(iter - 1, wsize) : iter - 1;
+      if (fast_ok(first_loop)) {
+         const int len = region_len(first_loop);
+         std::vector<double> hh(len);
+         if (step_enqueue(first_loop, g_k.scal) || c.read(g_k.scal, len, hh.data())) return -1;
+         return step_after(first_loop, hh.data());
+      }
+      const int k = step_k(first_loop);
       double te_dummy;
       if (mgs2(c, z, V, Z, k, TD + iter - 1, iter >= 2 ? TE + iter - 2 : &te_dummy, &t)) return -1;
       if (t < EPS) return 1;
@@ -1572,6 +1650,11 @@ struct LanczosRun {
                          g_k.ticket2, o);
       double vz[2];
       if (c.red(o, 2) || c.read(o, 2, vz)) return -1;
+      return step_tail(first_loop, vz);
+   }
+   // the rest of a step from (v, z) and ||z||^2 (the scaling, the Cholesky of T, the residual estimate)
+   int step_tail(bool first_loop, const double* vz)
+   {
       dotvz = std::sqrt(vz[0]);
       if (dotvz < EPS) return 1;
       c.scale(v, alias ? nullptr : z, 1.0 / dotvz);
@@ -1707,11 +1790,24 @@ int lanczos_pair_dev(Callbacks& cb, double* const* x, const double* const* rhs, 
          LanczosRun* Q = run[0] ? R[0] : R[1];
          if (cb.apply(1.0, Q->wv, 0.0, Q->z)) return -1;
       }
-      for (int k = 0; k < 2; k++) {
-         if (!run[k]) continue;
-         const int r = R[k]->step_end(true);
-         if (r < 0) return -1;
-         if (r) st[k] = 1;
+      if (run[0] && run[1] && R[0]->fast_ok(true) && R[1]->fast_ok(true)) {
+         // both runs' scalars behind one read (each in its half of the scalar buffer)
+         constexpr int kR = LanczosRun::kRegion;
+         if (R[0]->step_enqueue(true, g_k.scal) || R[1]->step_enqueue(true, g_k.scal + kR)) return -1;
+         std::vector<double> hh(kR + R[1]->region_len(true));
+         if (R[0]->c.read(g_k.scal, (int)hh.size(), hh.data())) return -1;
+         for (int k = 0; k < 2; k++) {
+            const int r = R[k]->step_after(true, hh.data() + k * kR);
+            if (r < 0) return -1;
+            if (r) st[k] = 1;
+         }
+      } else {
+         for (int k = 0; k < 2; k++) {
+            if (!run[k]) continue;
+            const int r = R[k]->step_end(true);
+            if (r < 0) return -1;
+            if (r) st[k] = 1;
+         }
       }
    }
    for (int k = 0; k < 2; k++) {

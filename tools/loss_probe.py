@@ -1,5 +1,10 @@
-"""One GP loss + gradient (Nfft4GPGpLoss) at config C (n = 1e6, 32 windows) as bench.py's loss leg runs it,
-for a kernel-trace profile:  rocprofv3 --kernel-trace --stats -- python3 tools/loss_probe.py"""
+"""Config-C loss + gradient (bench.py's run_loss leg: Nfft4GPGpLoss, 10 probes x 50 Lanczos steps, FGMRES 50) timed
+several times on one operator, to split its wall time from its kernel time under rocprofv3.
+
+    python tools/loss_probe.py [--reps 3] [--ortho 0]
+"""
+import argparse
+import json
 import os
 import sys
 import time
@@ -10,28 +15,23 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--ortho", type=int, default=0)
+    args = ap.parse_args()
     import torch
+    import bench
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
-    n, d = int(os.environ.get("LOSS_N", "1000000")), 32
-    s = torch.cuda.Stream()
-    torch.cuda.set_stream(s)
-    amd.lib().Nfft4GPAmdSetStream(s.cuda_stream)
-    X = np.asfortranarray(np.random.default_rng(906).random((n, d)))
-    win = np.arange(d, dtype=np.int32)
-    op = amd.NFFTAdditiveKernel(X, win, d, 1)
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(906)
+    n, d = 1_000_000, 32
+    X = rng.random((n, d))
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
     assert op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) == 0
-    rng = np.random.default_rng(909)
-    y = rng.random(n) - 0.5
-    R = np.where(rng.random((n, 10)) < 0.5, -1.0, 1.0)
-    Rl = torch.tensor(np.asfortranarray(R).T.copy(), device="cuda")
-    for rep in range(2):
-        torch.cuda.synchronize()
-        t0 = time.time()
-        lval = float(os.environ.get("LOSS_L", "0.1"))
-        loss, grad = amd.gp_loss(X, win, d, 1, y, (1.0, lval, 0.01), maxits=50, nvecs=10, rademacher=Rl, tol=1e-6,
-                                 transform=3, op=op)
-        torch.cuda.synchronize()
-        print(f"loss {loss:.12e} grad {list(grad)} time {time.time() - t0:.3f} s", file=sys.stderr, flush=True)
+    for rep in range(args.reps):
+        t0 = time.perf_counter()
+        r = bench.run_loss(op, torch, n, d, X, ortho=args.ortho)
+        print(json.dumps({"rep": rep, "wall_s": time.perf_counter() - t0, **r}), flush=True)
 
 
 if __name__ == "__main__":
