@@ -103,6 +103,94 @@ __global__ __launch_bounds__(T) void k_gs_batch(double* __restrict__ w, size_t l
                    ticket + (size_t)blockIdx.y * kTicketWords, out + s);
 }
 
+// The whole MGS sweep of one FGMRES step in ONE launch (Nfft4GPModifiedGS, matops.c:274-346, as the chain of
+// k_gs_step launches Ctx::gs makes): w stays in registers across the i projections and the norm, each step
+// reads only v_j (v_{j-1}, the previous step's u, is still in registers), and the grid-wide sum of step j
+// reaches every workgroup through hd[j] and the epoch word `bar` (agent-scope stores and loads, as
+// reduce.hpp's partials; the last arriver publishes).  Needs a grid that is resident at once and covers n in
+// one pass (the host checks the occupancy).  Per element and per reduction the arithmetic is k_gs_step's on
+// the same grid, so hd[0..i] and w are bitwise the chain's.  A wait that gives up sets *err (host: an error).
+template <int T, int EPT>
+__global__ __launch_bounds__(T) void k_mgs_chain(double* __restrict__ w, const double* __restrict__ V, size_t n,
+                                                 int i, double* __restrict__ hd, double* __restrict__ part,
+                                                 unsigned int* __restrict__ ticket, int* __restrict__ bar, int epoch0,
+                                                 int* __restrict__ err)
+{
+   __shared__ double s_h;
+   __shared__ int s_fail;
+   const size_t i0 = (size_t)blockIdx.x * T * EPT + threadIdx.x;
+   double wv[EPT], pv[EPT], vn[EPT];
+#pragma unroll
+   for (int e = 0; e < EPT; e++) {
+      const size_t k = i0 + (size_t)e * T;
+      wv[e] = k < n ? w[k] : 0.0;
+      pv[e] = 0.0;
+      vn[e] = (i > 0 && k < n) ? V[k] : 0.0;  // v_0
+   }
+   if (threadIdx.x == 0) s_fail = 0;
+   for (int j = 0; j <= i; j++) {
+      if (j > 0) {
+         const double h = s_h;
+#pragma unroll
+         for (int e = 0; e < EPT; e++) wv[e] = fma(-h, pv[e], wv[e]);
+      }
+      double acc = 0.0;
+      if (j < i) {
+         double vv[EPT];
+#pragma unroll
+         for (int e = 0; e < EPT; e++) vv[e] = vn[e];
+         // v_{j+1}'s loads go out now: they do not depend on this step's sum, so they overlap its grid-wide wait
+         if (j + 1 < i) {
+            const double* v1 = V + (size_t)(j + 1) * n;
+#pragma unroll
+            for (int e = 0; e < EPT; e++) {
+               const size_t k = i0 + (size_t)e * T;
+               vn[e] = k < n ? v1[k] : 0.0;
+            }
+         }
+#pragma unroll
+         for (int e = 0; e < EPT; e++) {
+            acc = fma(wv[e], vv[e], acc);
+            pv[e] = vv[e];
+         }
+      } else {
+#pragma unroll
+         for (int e = 0; e < EPT; e++) acc = fma(wv[e], wv[e], acc);
+      }
+      acc = block_sum0<T>(acc);
+      double tot;
+      const int target = epoch0 + j + 1;
+      if (grid_total<T>(acc, part, ticket, &tot)) {
+         if (threadIdx.x == 0) {
+            __hip_atomic_store(hd + j, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // hd[j] and the ticket resets before the epoch
+            __hip_atomic_store(bar, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_h = tot;
+         }
+      } else if (threadIdx.x == 0) {
+         int b = 0;
+         for (long spin = 0; spin < (1l << 22); spin++) {
+            b = __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (b == target) break;
+            __builtin_amdgcn_s_sleep(1);
+         }
+         if (b == target) {
+            s_h = __hip_atomic_load(hd + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+         } else {
+            s_fail = 1;
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+         }
+      }
+      __syncthreads();
+      if (s_fail) return;  // the others time out at the next step in turn
+   }
+#pragma unroll
+   for (int e = 0; e < EPT; e++) {
+      const size_t k = i0 + (size_t)e * T;
+      if (k < n) w[k] = wv[e];
+   }
+}
+
 // a[s] *= fac[s] for the systems act[y] (k_scale2's arithmetic)
 __global__ void k_scale_batch(double* __restrict__ a, size_t lda, size_t n, const int* __restrict__ act,
                               const double* __restrict__ fac)
@@ -483,6 +571,10 @@ struct KScratch {
    double* hcoef = nullptr;  // pinned staging of per-step coefficients (DCGS2)
    double* bpart = nullptr;  // block Gram-Schmidt partials [kBDMaxBlocks][kScal]
    unsigned int *ticket = nullptr, *ticket2 = nullptr;
+   int* chain = nullptr;      // k_mgs_chain: [0] epoch word, [1] error word
+   int* hchain_err = nullptr; // pinned read-back of the error word
+   int chain_epoch = 0;
+   int chain_occ = -1;        // resident workgroups of k_mgs_chain per CU x CUs (0: unusable)
    int ensure_bpart()
    {
       if (!bpart) NFFT4GP_HIP_CHECK(hipMalloc((void**)&bpart, sizeof(double) * kBDMaxBlocks * kScal));
@@ -501,6 +593,25 @@ struct KScratch {
       NFFT4GP_HIP_CHECK(hipMemset(ticket2, 0, sizeof(unsigned int) * kTicketWords));
       NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&hscal, sizeof(double) * kScal));
       NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&hcoef, sizeof(double) * kScal));
+      return 0;
+   }
+   int ensure_chain()
+   {
+      if (ensure()) return -1;
+      if (!chain) {
+         NFFT4GP_HIP_CHECK(hipMalloc((void**)&chain, sizeof(int) * 2));
+         NFFT4GP_HIP_CHECK(hipMemset(chain, 0, sizeof(int) * 2));
+         NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&hchain_err, sizeof(int)));
+         chain_epoch = 0;
+      }
+      if (chain_occ < 0) {
+         int dev = 0, occ = 0;
+         hipDeviceProp_t prop;
+         chain_occ = 0;
+         if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+             hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_mgs_chain<1024, 4>, 1024, 0) == hipSuccess)
+            chain_occ = occ * prop.multiProcessorCount;
+      }
       return 0;
    }
 };
@@ -526,6 +637,38 @@ struct Ctx {
                          out);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return red(out, 1);
+   }
+   // the MGS sweep of an FGMRES step (w against V[0..i), then ||w||^2) into hd[0..i] in one launch when the grid
+   // fits (k_mgs_chain); returns 1 when it does not (the caller runs the k_gs_step chain)
+   int mgs_chain(double* w, const double* V, int i, double* hd)
+   {
+      if (comm || g_k.ensure_chain()) return comm ? 1 : -1;
+      const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((n + 4095) / 4096, kKMaxBlocks));
+      const char* e = getenv("NFFT4GP_AMD_MGS_CHAIN");
+      const bool off = e && atoi(e) == 0;
+      if (off || (size_t)grid * 4096 < n || (int)grid > g_k.chain_occ) return 1;
+      if (g_k.chain_epoch > (1 << 30)) {
+         NFFT4GP_HIP_CHECK(hipMemsetAsync(g_k.chain, 0, sizeof(int), s));
+         g_k.chain_epoch = 0;
+      }
+      hipLaunchKernelGGL((k_mgs_chain<1024, 4>), dim3(grid), dim3(1024), 0, s, w, V, n, i, hd, g_k.part, g_k.ticket,
+                         g_k.chain, g_k.chain_epoch, g_k.chain + 1);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      // the error word comes back with the step's scalars (the caller's read synchronises)
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(g_k.hchain_err, g_k.chain + 1, sizeof(int), hipMemcpyDeviceToHost, s));
+      g_k.chain_epoch += i + 1;
+      return 0;
+   }
+   // after the read that follows mgs_chain: did a wait give up?  (then the reductions' tickets are reset, so
+   // later solves in this process sum correctly; the error word stays set and every later sweep fails)
+   int chain_failed()
+   {
+      if (*g_k.hchain_err) {
+         fprintf(stderr, "nfft4gp_amd: FGMRES: the one-launch MGS sweep's wait gave up\n");
+         (void)hipMemset(g_k.ticket, 0, sizeof(unsigned int) * kTicketWords);
+         return 1;
+      }
+      return 0;
    }
    int read(const double* d, int count, double* h)
    {
@@ -985,12 +1128,19 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
          double* hd = g_k.scal;
          std::vector<double> hcol(i + 1);
          if (ortho == 0) {
-            // Nfft4GPModifiedGS (matops.c:274-346) with k = i-1, no re-orthogonalisation
-            for (int j = 0; j < i; j++)
-               if (c.gs(w, j ? V + (size_t)(j - 1) * n : nullptr, j ? hd + j - 1 : nullptr, V + (size_t)j * n, hd + j))
-                  return fail();
-            if (c.gs(w, V + (size_t)(i - 1) * n, hd + i - 1, nullptr, hd + i)) return fail();
+            // Nfft4GPModifiedGS (matops.c:274-346) with k = i-1, no re-orthogonalisation: one launch for the
+            // sweep where the grid fits (k_mgs_chain), else one per projection
+            const int rc = c.mgs_chain(w, V, i, hd);
+            if (rc < 0) return fail();
+            if (rc > 0) {
+               for (int j = 0; j < i; j++)
+                  if (c.gs(w, j ? V + (size_t)(j - 1) * n : nullptr, j ? hd + j - 1 : nullptr, V + (size_t)j * n,
+                           hd + j))
+                     return fail();
+               if (c.gs(w, V + (size_t)(i - 1) * n, hd + i - 1, nullptr, hd + i)) return fail();
+            }
             if (c.read(hd, i + 1, hcol.data())) return fail();
+            if (rc == 0 && c.chain_failed()) return fail();
          } else {
             // classical passes h = V^T w, w -= V h; a second one only when the first dropped ||w|| below 0.7071
             // of its value before it (the DGKS test of the reference's MGS2, matops.c:348-440); H(:, i) = the

@@ -70,3 +70,27 @@ def test_pcg_bitwise_reproducible(torch_cuda, config_c_op, monkeypatch, fusep):
     assert r1 == r2
     np.testing.assert_array_equal(h1, h2)
     assert torch.equal(x1, x2)
+
+
+def test_fgmres_mgs_sweep_in_one_launch_is_bitwise(torch_cuda, config_c_op, monkeypatch):
+    """FGMRES with the reference's MGS (fgmres.c, matops.c:274-346): the sweep of each step in one launch
+    (k_mgs_chain, the default where the grid fits) against one k_gs_step launch per projection
+    (NFFT4GP_AMD_MGS_CHAIN=0): the same per-element and per-reduction arithmetic, so the same bits."""
+    torch = torch_cuda
+    op, _ = config_c_op
+    n = op.n
+    amd.lib().Nfft4GPAmdSetFgmresOrtho(0)
+    b = torch.tensor(np.random.default_rng(908).random(n) - 0.5, device="cuda")
+    runs = []
+    for chain in ("1", "0"):
+        monkeypatch.setenv("NFFT4GP_AMD_MGS_CHAIN", chain)
+        x = torch.zeros(n, dtype=torch.float64, device="cuda")
+        _, relres, hist, it = amd.fgmres(op, b, x, kdim=60, maxits=100, tol=1e-12)
+        torch.cuda.synchronize()
+        runs.append((x, relres, np.asarray(hist), it))
+    (x1, r1, h1, i1), (x2, r2, h2, i2) = runs
+    print(f"FGMRES(60) 100 steps: rel res {r1:.6e} / {r2:.6e}")
+    assert i1 == i2 == 100
+    assert r1 == r2
+    np.testing.assert_array_equal(h1, h2)
+    assert torch.equal(x1, x2)
