@@ -110,22 +110,40 @@ __global__ __launch_bounds__(T) void k_gs_batch(double* __restrict__ w, size_t l
 // reduce.hpp's partials; the last arriver publishes).  Needs a grid that is resident at once and covers n in
 // one pass (the host checks the occupancy).  Per element and per reduction the arithmetic is k_gs_step's on
 // the same grid, so hd[0..i] and w are bitwise the chain's.  A wait that gives up sets *err (host: an error).
-template <int T, int EPT>
+// BATCH (fgmres_batch_dev, the predict's std solves): blockIdx.y runs system s = act[y] of a batch of m, whose
+// column j is cols[j] + s n (w: column i), its scalars at hd[j m + s], one partials / ticket pair per y and one
+// epoch word per system (bar[s])
+template <int T, int EPT, bool BATCH = false>
 __global__ __launch_bounds__(T) void k_mgs_chain(double* __restrict__ w, const double* __restrict__ V, size_t n,
                                                  int i, double* __restrict__ hd, double* __restrict__ part,
                                                  unsigned int* __restrict__ ticket, int* __restrict__ bar, int epoch0,
-                                                 int* __restrict__ err)
+                                                 int* __restrict__ err, const double* const* __restrict__ cols = nullptr,
+                                                 const int* __restrict__ act = nullptr, int m = 1)
 {
    __shared__ double s_h;
    __shared__ int s_fail;
+   int hs = 1;  // hd stride between steps
+   if (BATCH) {
+      const int sy = act[blockIdx.y];
+      w = const_cast<double*>(cols[i]) + (size_t)sy * n;
+      hd += sy;
+      hs = m;
+      part += (size_t)blockIdx.y * kKMaxBlocks;
+      ticket += (size_t)blockIdx.y * kTicketWords;
+      bar += sy;
+   }
+   auto col = [&](int j) -> const double* {
+      return BATCH ? cols[j] + (size_t)act[blockIdx.y] * n : V + (size_t)j * n;
+   };
    const size_t i0 = (size_t)blockIdx.x * T * EPT + threadIdx.x;
    double wv[EPT], pv[EPT], vn[EPT];
+   const double* v0 = i > 0 ? col(0) : nullptr;
 #pragma unroll
    for (int e = 0; e < EPT; e++) {
       const size_t k = i0 + (size_t)e * T;
       wv[e] = k < n ? w[k] : 0.0;
       pv[e] = 0.0;
-      vn[e] = (i > 0 && k < n) ? V[k] : 0.0;  // v_0
+      vn[e] = (v0 && k < n) ? v0[k] : 0.0;  // v_0
    }
    if (threadIdx.x == 0) s_fail = 0;
    for (int j = 0; j <= i; j++) {
@@ -141,7 +159,7 @@ __global__ __launch_bounds__(T) void k_mgs_chain(double* __restrict__ w, const d
          for (int e = 0; e < EPT; e++) vv[e] = vn[e];
          // v_{j+1}'s loads go out now: they do not depend on this step's sum, so they overlap its grid-wide wait
          if (j + 1 < i) {
-            const double* v1 = V + (size_t)(j + 1) * n;
+            const double* v1 = col(j + 1);
 #pragma unroll
             for (int e = 0; e < EPT; e++) {
                const size_t k = i0 + (size_t)e * T;
@@ -162,7 +180,7 @@ __global__ __launch_bounds__(T) void k_mgs_chain(double* __restrict__ w, const d
       const int target = epoch0 + j + 1;
       if (grid_total<T>(acc, part, ticket, &tot)) {
          if (threadIdx.x == 0) {
-            __hip_atomic_store(hd + j, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(hd + (size_t)j * hs, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // hd[j] and the ticket resets before the epoch
             __hip_atomic_store(bar, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_h = tot;
@@ -175,7 +193,7 @@ __global__ __launch_bounds__(T) void k_mgs_chain(double* __restrict__ w, const d
             __builtin_amdgcn_s_sleep(1);
          }
          if (b == target) {
-            s_h = __hip_atomic_load(hd + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_h = __hip_atomic_load(hd + (size_t)j * hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
          } else {
             s_fail = 1;
             __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1243,6 +1261,11 @@ int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* 
    int* dact = nullptr;
    double* pin = nullptr;  // pinned: [0, m) factors, then the combine's coefficients and column pointers
    int* pact = nullptr;    // pinned: the running list
+   // the one-launch MGS sweep (k_mgs_chain<.., true>): device column table, epoch words, error word
+   const double** dvcols = nullptr;
+   const double** pvcols = nullptr;  // pinned staging of new column pointers
+   int *dbar = nullptr, *derr = nullptr, *herr = nullptr;
+   int vcols_up = 0, epoch = 0;
    hipEvent_t pin_ev = nullptr;  // the last copy out of pin / pact
    std::vector<double*> groups;  // basis column groups (V, then Z when preconditioned)
    std::vector<double*> Vc, Zc;  // column j of every system: Vc[j] + s n
@@ -1259,6 +1282,11 @@ int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* 
       (void)hipFree(dact);
       if (pin) (void)hipHostFree(pin);
       if (pact) (void)hipHostFree(pact);
+      (void)hipFree(dvcols);
+      (void)hipFree(dbar);
+      (void)hipFree(derr);
+      if (pvcols) (void)hipHostFree(pvcols);
+      if (herr) (void)hipHostFree(herr);
       if (pin_ev) (void)hipEventDestroy(pin_ev);
    };
    auto fail = [&]() -> int {
@@ -1276,6 +1304,26 @@ int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* 
    if (hipHostMalloc((void**)&pact, sizeof(int) * m) != hipSuccess) {
       pact = nullptr;
       return fail();
+   }
+   const int colcap = std::min(kdim, maxits) + 2;
+   if (dmalloc(&dvcols, (size_t)colcap) || dmalloc(&dbar, m) || dmalloc(&derr, 1)) return fail();
+   if (hipHostMalloc((void**)&pvcols, sizeof(double*) * 64) != hipSuccess ||
+       hipHostMalloc((void**)&herr, sizeof(int)) != hipSuccess) {
+      pvcols = nullptr;
+      herr = nullptr;
+      return fail();
+   }
+   *herr = 0;
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(dbar, 0, sizeof(int) * m, st));
+   NFFT4GP_HIP_CHECK(hipMemsetAsync(derr, 0, sizeof(int), st));
+   static int occ_batch = -1;  // resident k_mgs_chain<1024, 4, true> workgroups on the device
+   if (occ_batch < 0) {
+      int dev = 0, occ = 0;
+      hipDeviceProp_t prop;
+      occ_batch = 0;
+      if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_mgs_chain<1024, 4, true>, 1024, 0) == hipSuccess)
+         occ_batch = occ * prop.multiProcessorCount;
    }
    NFFT4GP_HIP_CHECK(hipEventCreateWithFlags(&pin_ev, hipEventDisableTiming));
    NFFT4GP_HIP_CHECK(hipEventRecord(pin_ev, st));
@@ -1468,13 +1516,39 @@ int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* 
             ys.push_back(Vc[i] + (size_t)s * n);
          }
          if (apply(xs, ys)) return fail();
-         // Nfft4GPModifiedGS (matops.c:274-346) with k = i - 1, every running system per launch
-         for (int j = 0; j < i; j++)
-            if (gs(Vc[i], n, j ? Vc[j - 1] : nullptr, n, j ? hd + (size_t)(j - 1) * m : nullptr, Vc[j], n,
-                   hd + (size_t)j * m))
-               return fail();
-         if (gs(Vc[i], n, Vc[i - 1], n, hd + (size_t)(i - 1) * m, nullptr, 0, hd + (size_t)i * m)) return fail();
+         // Nfft4GPModifiedGS (matops.c:274-346) with k = i - 1: the whole sweep of every running system in one
+         // launch where the grid fits (k_mgs_chain), else one launch per projection for all of them
+         const char* ce = getenv("NFFT4GP_AMD_MGS_CHAIN");
+         const bool chain = !(ce && atoi(ce) == 0) && (size_t)ggrid * 4096 >= n &&
+                            (long)ggrid * (long)act.size() <= (long)occ_batch && i + 1 <= colcap && !*herr;
+         if (chain) {
+            while (vcols_up <= i) {  // the column table: pointers of columns not uploaded yet
+               if (pin_wait()) return fail();
+               const int cnt = std::min(64, i + 1 - vcols_up);
+               for (int k = 0; k < cnt; k++) pvcols[k] = Vc[vcols_up + k];
+               NFFT4GP_HIP_CHECK(hipMemcpyAsync(dvcols + vcols_up, pvcols, sizeof(double*) * cnt,
+                                                hipMemcpyHostToDevice, st));
+               if (pin_done()) return fail();
+               vcols_up += cnt;
+            }
+            hipLaunchKernelGGL((k_mgs_chain<1024, 4, true>), dim3(ggrid, (unsigned)act.size()), dim3(1024), 0, st,
+                               (double*)nullptr, (const double*)nullptr, n, i, hd, part, ticket, dbar, epoch, derr,
+                               (const double* const*)dvcols, (const int*)dact, m);
+            NFFT4GP_HIP_CHECK(hipGetLastError());
+            epoch += i + 1;
+            NFFT4GP_HIP_CHECK(hipMemcpyAsync(herr, derr, sizeof(int), hipMemcpyDeviceToHost, st));
+         } else {
+            for (int j = 0; j < i; j++)
+               if (gs(Vc[i], n, j ? Vc[j - 1] : nullptr, n, j ? hd + (size_t)(j - 1) * m : nullptr, Vc[j], n,
+                      hd + (size_t)j * m))
+                  return fail();
+            if (gs(Vc[i], n, Vc[i - 1], n, hd + (size_t)(i - 1) * m, nullptr, 0, hd + (size_t)i * m)) return fail();
+         }
          if (read(hd, (size_t)(i + 1) * m, hh)) return fail();
+         if (chain && *herr) {
+            fprintf(stderr, "nfft4gp_amd: FGMRES batch: the one-launch MGS sweep's wait gave up\n");
+            return fail();
+         }
          std::vector<int> keep, conv;
          for (int s : act) {
             Sys& y = S[s];
@@ -2414,7 +2488,9 @@ int Nfft4GPAdditiveNFFTGpPredict(double* x, double* data, double* label, int n, 
       // (fgmres_batch_dev: restart dimension and iteration limit n as the reference), then the dots
       double* sp = *std_predictp ? *std_predictp : (double*)malloc(sizeof(double) * std::max(1, n_predict));
       std::vector<double> hs(n_predict);
-      int bm = 16;
+      // 32 points per batch up to n = 2^18 (0.077 against 0.108 s for 16 at n = 20 000, 0.366 against 0.417 s at
+      // n = 200 000: profiles/r05_predict_std_batch.txt), 16 above (each basis column holds batch x n doubles)
+      int bm = n <= (1 << 18) ? 32 : 16;
       if (const char* e = getenv("NFFT4GP_AMD_PREDICT_BATCH")) bm = std::max(1, std::min(256, atoi(e)));
       bm = std::max(1, std::min(bm, n_predict));
       double *E = nullptr, *Y = nullptr, *Xs = nullptr, *dsc = nullptr;

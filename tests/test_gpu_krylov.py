@@ -205,7 +205,12 @@ def test_gp_predict_std_batches(torch_cuda, monkeypatch):
         monkeypatch.setenv("NFFT4GP_AMD_PREDICT_BATCH", bm)
         out[bm] = amd.gp_predict(z["X"], z["Xp"], z["windows"], 4, 1, z["y"], z["hyper"], maxits=int(z["maxits"]),
                                  tol=float(z["tol"]), with_std=True)[1]
-    for bm in ("16", "64"):
+    # the sweeps one projection per launch (NFFT4GP_AMD_MGS_CHAIN=0) instead of one launch per sweep
+    monkeypatch.setenv("NFFT4GP_AMD_PREDICT_BATCH", "16")
+    monkeypatch.setenv("NFFT4GP_AMD_MGS_CHAIN", "0")
+    out["16_nochain"] = amd.gp_predict(z["X"], z["Xp"], z["windows"], 4, 1, z["y"], z["hyper"],
+                                       maxits=int(z["maxits"]), tol=float(z["tol"]), with_std=True)[1]
+    for bm in ("16", "64", "16_nochain"):
         np.testing.assert_allclose(out[bm], out["1"], rtol=1e-8)
     np.testing.assert_allclose(out["16"], z["std"], rtol=1e-6)
 
