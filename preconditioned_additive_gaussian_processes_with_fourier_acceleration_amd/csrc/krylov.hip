@@ -105,18 +105,21 @@ __global__ __launch_bounds__(T) void k_gs_batch(double* __restrict__ w, size_t l
 
 // The whole MGS sweep of one FGMRES step in ONE launch (Nfft4GPModifiedGS, matops.c:274-346, as the chain of
 // k_gs_step launches Ctx::gs makes): w stays in registers across the i projections and the norm, each step
-// reads only v_j (v_{j-1}, the previous step's u, is still in registers), and the grid-wide sum of step j
-// reaches every workgroup through hd[j] and the epoch word `bar` (agent-scope stores and loads, as
-// reduce.hpp's partials; the last arriver publishes).  Needs a grid that is resident at once and covers n in
-// one pass (the host checks the occupancy).  Per element and per reduction the arithmetic is k_gs_step's on
+// reads only v_j (v_{j-1}, the previous step's u, is still in registers; v_{j+1}'s loads go out before the
+// step's wait), and the grid-wide sum of step j (reduce.hpp's last arriver) reaches every workgroup through
+// hd[j] itself: the host presets hd[0..i] to an all-ones NaN pattern (kChainUnset) that no sum of finite data
+// produces, the last arriver stores the sum there (agent scope, after its ticket resets have landed) and the
+// others poll it until it changes -- no fences, as reduce.hpp.  Needs a grid that is resident at once and covers
+// n in one pass (the host checks the occupancy).  Per element and per reduction the arithmetic is k_gs_step's on
 // the same grid, so hd[0..i] and w are bitwise the chain's.  A wait that gives up sets *err (host: an error).
 // BATCH (fgmres_batch_dev, the predict's std solves): blockIdx.y runs system s = act[y] of a batch of m, whose
-// column j is cols[j] + s n (w: column i), its scalars at hd[j m + s], one partials / ticket pair per y and one
-// epoch word per system (bar[s])
+// column j is cols[j] + s n (w: column i), its scalars at hd[j m + s], one partials / ticket pair per y
+constexpr unsigned long long kChainUnset = ~0ull;  // hd[j] before step j's sum is published
+
 template <int T, int EPT, bool BATCH = false>
 __global__ __launch_bounds__(T) void k_mgs_chain(double* __restrict__ w, const double* __restrict__ V, size_t n,
                                                  int i, double* __restrict__ hd, double* __restrict__ part,
-                                                 unsigned int* __restrict__ ticket, int* __restrict__ bar, int epoch0,
+                                                 unsigned int* __restrict__ ticket,
                                                  int* __restrict__ err, const double* const* __restrict__ cols = nullptr,
                                                  const int* __restrict__ act = nullptr, int m = 1)
 {
@@ -130,7 +133,6 @@ __global__ __launch_bounds__(T) void k_mgs_chain(double* __restrict__ w, const d
       hs = m;
       part += (size_t)blockIdx.y * kKMaxBlocks;
       ticket += (size_t)blockIdx.y * kTicketWords;
-      bar += sy;
    }
    auto col = [&](int j) -> const double* {
       return BATCH ? cols[j] + (size_t)act[blockIdx.y] * n : V + (size_t)j * n;
@@ -177,23 +179,23 @@ __global__ __launch_bounds__(T) void k_mgs_chain(double* __restrict__ w, const d
       }
       acc = block_sum0<T>(acc);
       double tot;
-      const int target = epoch0 + j + 1;
+      unsigned long long* slot = reinterpret_cast<unsigned long long*>(hd + (size_t)j * hs);
       if (grid_total<T>(acc, part, ticket, &tot)) {
          if (threadIdx.x == 0) {
-            __hip_atomic_store(hd + (size_t)j * hs, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // hd[j] and the ticket resets before the epoch
-            __hip_atomic_store(bar, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ticket resets land before the publish
+            __hip_atomic_store(slot, (unsigned long long)__double_as_longlong(tot), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
             s_h = tot;
          }
       } else if (threadIdx.x == 0) {
-         int b = 0;
+         unsigned long long b = kChainUnset;
          for (long spin = 0; spin < (1l << 22); spin++) {
-            b = __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (b == target) break;
+            b = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (b != kChainUnset) break;
             __builtin_amdgcn_s_sleep(1);
          }
-         if (b == target) {
-            s_h = __hip_atomic_load(hd + (size_t)j * hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+         if (b != kChainUnset) {
+            s_h = __longlong_as_double((long long)b);
          } else {
             s_fail = 1;
             __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -589,9 +591,8 @@ struct KScratch {
    double* hcoef = nullptr;  // pinned staging of per-step coefficients (DCGS2)
    double* bpart = nullptr;  // block Gram-Schmidt partials [kBDMaxBlocks][kScal]
    unsigned int *ticket = nullptr, *ticket2 = nullptr;
-   int* chain = nullptr;      // k_mgs_chain: [0] epoch word, [1] error word
+   int* chain = nullptr;      // k_mgs_chain: [1] error word
    int* hchain_err = nullptr; // pinned read-back of the error word
-   int chain_epoch = 0;
    int chain_occ = -1;        // resident workgroups of k_mgs_chain per CU x CUs (0: unusable)
    int ensure_bpart()
    {
@@ -620,7 +621,7 @@ struct KScratch {
          NFFT4GP_HIP_CHECK(hipMalloc((void**)&chain, sizeof(int) * 2));
          NFFT4GP_HIP_CHECK(hipMemset(chain, 0, sizeof(int) * 2));
          NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&hchain_err, sizeof(int)));
-         chain_epoch = 0;
+         *hchain_err = 0;
       }
       if (chain_occ < 0) {
          int dev = 0, occ = 0;
@@ -665,16 +666,12 @@ struct Ctx {
       const char* e = getenv("NFFT4GP_AMD_MGS_CHAIN");
       const bool off = e && atoi(e) == 0;
       if (off || (size_t)grid * 4096 < n || (int)grid > g_k.chain_occ) return 1;
-      if (g_k.chain_epoch > (1 << 30)) {
-         NFFT4GP_HIP_CHECK(hipMemsetAsync(g_k.chain, 0, sizeof(int), s));
-         g_k.chain_epoch = 0;
-      }
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(hd, 0xFF, sizeof(double) * (i + 1), s));  // kChainUnset
       hipLaunchKernelGGL((k_mgs_chain<1024, 4>), dim3(grid), dim3(1024), 0, s, w, V, n, i, hd, g_k.part, g_k.ticket,
-                         g_k.chain, g_k.chain_epoch, g_k.chain + 1);
+                         g_k.chain + 1);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       // the error word comes back with the step's scalars (the caller's read synchronises)
       NFFT4GP_HIP_CHECK(hipMemcpyAsync(g_k.hchain_err, g_k.chain + 1, sizeof(int), hipMemcpyDeviceToHost, s));
-      g_k.chain_epoch += i + 1;
       return 0;
    }
    // after the read that follows mgs_chain: did a wait give up?  (then the reductions' tickets are reset, so
@@ -1261,11 +1258,11 @@ int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* 
    int* dact = nullptr;
    double* pin = nullptr;  // pinned: [0, m) factors, then the combine's coefficients and column pointers
    int* pact = nullptr;    // pinned: the running list
-   // the one-launch MGS sweep (k_mgs_chain<.., true>): device column table, epoch words, error word
+   // the one-launch MGS sweep (k_mgs_chain<.., true>): device column table, error word
    const double** dvcols = nullptr;
    const double** pvcols = nullptr;  // pinned staging of new column pointers
-   int *dbar = nullptr, *derr = nullptr, *herr = nullptr;
-   int vcols_up = 0, epoch = 0;
+   int *derr = nullptr, *herr = nullptr;
+   int vcols_up = 0;
    hipEvent_t pin_ev = nullptr;  // the last copy out of pin / pact
    std::vector<double*> groups;  // basis column groups (V, then Z when preconditioned)
    std::vector<double*> Vc, Zc;  // column j of every system: Vc[j] + s n
@@ -1283,7 +1280,6 @@ int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* 
       if (pin) (void)hipHostFree(pin);
       if (pact) (void)hipHostFree(pact);
       (void)hipFree(dvcols);
-      (void)hipFree(dbar);
       (void)hipFree(derr);
       if (pvcols) (void)hipHostFree(pvcols);
       if (herr) (void)hipHostFree(herr);
@@ -1306,7 +1302,7 @@ int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* 
       return fail();
    }
    const int colcap = std::min(kdim, maxits) + 2;
-   if (dmalloc(&dvcols, (size_t)colcap) || dmalloc(&dbar, m) || dmalloc(&derr, 1)) return fail();
+   if (dmalloc(&dvcols, (size_t)colcap) || dmalloc(&derr, 1)) return fail();
    if (hipHostMalloc((void**)&pvcols, sizeof(double*) * 64) != hipSuccess ||
        hipHostMalloc((void**)&herr, sizeof(int)) != hipSuccess) {
       pvcols = nullptr;
@@ -1314,7 +1310,6 @@ int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* 
       return fail();
    }
    *herr = 0;
-   NFFT4GP_HIP_CHECK(hipMemsetAsync(dbar, 0, sizeof(int) * m, st));
    NFFT4GP_HIP_CHECK(hipMemsetAsync(derr, 0, sizeof(int), st));
    static int occ_batch = -1;  // resident k_mgs_chain<1024, 4, true> workgroups on the device
    if (occ_batch < 0) {
@@ -1531,11 +1526,11 @@ int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* 
                if (pin_done()) return fail();
                vcols_up += cnt;
             }
+            NFFT4GP_HIP_CHECK(hipMemsetAsync(hd, 0xFF, sizeof(double) * (size_t)(i + 1) * m, st));  // kChainUnset
             hipLaunchKernelGGL((k_mgs_chain<1024, 4, true>), dim3(ggrid, (unsigned)act.size()), dim3(1024), 0, st,
-                               (double*)nullptr, (const double*)nullptr, n, i, hd, part, ticket, dbar, epoch, derr,
+                               (double*)nullptr, (const double*)nullptr, n, i, hd, part, ticket, derr,
                                (const double* const*)dvcols, (const int*)dact, m);
             NFFT4GP_HIP_CHECK(hipGetLastError());
-            epoch += i + 1;
             NFFT4GP_HIP_CHECK(hipMemcpyAsync(herr, derr, sizeof(int), hipMemcpyDeviceToHost, st));
          } else {
             for (int j = 0; j < i; j++)
