@@ -1618,8 +1618,13 @@ int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* 
       res.iters[s] = iter;
       res.rel_res[s] = S[s].normr / S[s].normb;
    }
+   bool printed = false;
    for (int s = 0; s < m; s++)
-      if (!S[s].log.empty()) fputs(S[s].log.c_str(), stdout);
+      if (!S[s].log.empty()) {
+         fputs(S[s].log.c_str(), stdout);
+         printed = true;
+      }
+   if (printed) fflush(stdout);
    cleanup();
    return 0;
 }

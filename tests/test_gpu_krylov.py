@@ -215,6 +215,23 @@ def test_gp_predict_std_batches(torch_cuda, monkeypatch):
     np.testing.assert_allclose(out["16"], z["std"], rtol=1e-6)
 
 
+def test_gp_predict_std_batch_prints_per_point(torch_cuda, capfd, monkeypatch):
+    """print_level 0: the batch keeps each point's lines and prints them in point order, as the reference's
+    one-FGMRES-per-point loop does (one end-of-cycle line per solve, nfft_interface.c:1037-1051)."""
+    z = load("predict_synth")
+    monkeypatch.setenv("NFFT4GP_AMD_PREDICT_BATCH", "2")
+    Xp = z["Xp"][:3]
+    _, std = amd.gp_predict(z["X"], Xp, z["windows"], 4, 1, z["y"], z["hyper"], maxits=int(z["maxits"]),
+                            tol=float(z["tol"]), with_std=True, print_level=0)
+    out = capfd.readouterr().out
+    lines = [ln for ln in out.splitlines() if ln.startswith("Rel. residual at the end of current cycle")]
+    assert len(lines) == 1 + 3  # the mean's solve, then one per point
+    # (the 3-point [X; Xp] handle is centred and scaled on its own points, so the golden std does not apply)
+    _, std2 = amd.gp_predict(z["X"], Xp, z["windows"], 4, 1, z["y"], z["hyper"], maxits=int(z["maxits"]),
+                             tol=float(z["tol"]), with_std=True)
+    np.testing.assert_allclose(std, std2, rtol=1e-8)
+
+
 def test_gp_predict_std_beyond_the_scalar_limit(torch_cuda):
     """n = 5000 training points: the std solves ask for restart dimension n (nfft_interface.c:1044); the batch
     solver grows its basis as the steps need it (the one-system FGMRES caps the restart at 4094).  Against the
