@@ -211,6 +211,96 @@ __global__ __launch_bounds__(T) void k_mgs_chain(double* __restrict__ w, const d
    }
 }
 
+// mgs2's local pass in ONE launch (what Ctx::block_gs(w, V + j0 n, Z + j0 n, ml, h, 1) does in three: h[0..ml) =
+// [v_j0, v_j0+1]^T w, h[ml + 1] = ||w||^2 before, w -= Z_loc h, h[ml] = ||w||^2 after).  The ml + 1 grid-wide sums
+// of the first half are reduce.hpp's last-arriver sums (one partials / ticket pair each), published into hd
+// slots the host preset to kChainUnset; every workgroup waits for the projections (bounded), updates its w
+// and forms the norm after, whose last arriver writes hd[ml].  alias: Z_loc == V_loc (no preconditioner), so
+// the update reuses the loaded columns.  The same sums as block_gs's up to their order (rounding level).
+template <int T, int EPT>
+__global__ __launch_bounds__(T) void k_lanczos_local(double* __restrict__ w, const double* __restrict__ V0,
+                                                     const double* __restrict__ Z0, int alias, size_t n, int ml,
+                                                     double* __restrict__ hd, double* __restrict__ part,
+                                                     unsigned int* __restrict__ ticket, int* __restrict__ err)
+{
+   __shared__ double s_sc[3][T / 64];
+   __shared__ int s_last[3];
+   __shared__ double s_h[2];
+   __shared__ int s_fail;
+   const size_t i0 = (size_t)blockIdx.x * T * EPT + threadIdx.x;
+   double wv[EPT], v0[EPT], v1[EPT];
+#pragma unroll
+   for (int e = 0; e < EPT; e++) {
+      const size_t k = i0 + (size_t)e * T;
+      const bool in = k < n;
+      wv[e] = in ? w[k] : 0.0;
+      v0[e] = in ? V0[k] : 0.0;
+      v1[e] = (in && ml == 2) ? V0[n + k] : 0.0;
+   }
+   double a0 = 0.0, a1 = 0.0, an = 0.0;
+#pragma unroll
+   for (int e = 0; e < EPT; e++) {
+      a0 = fma(wv[e], v0[e], a0);
+      a1 = fma(wv[e], v1[e], a1);
+      an = fma(wv[e], wv[e], an);
+   }
+   if (threadIdx.x == 0) s_fail = 0;
+   const double sums[3] = {a0, a1, an};
+   // hd slots: [0] (w, v_j0), [1] (w, v_j0+1) when ml == 2, [ml + 1] ||w||^2 before
+   const int slot_of[3] = {0, 1, ml + 1};
+#pragma unroll
+   for (int q = 0; q < 3; q++) {
+      if (q == 1 && ml != 2) continue;
+      double b = block_sum0_s<T>(sums[q], s_sc[q]);
+      double tot;
+      if (grid_total_s<T>(b, part + (size_t)q * kKMaxBlocks, ticket + (size_t)q * kTicketWords, &tot, &s_last[q],
+                          s_sc[q]) &&
+          threadIdx.x == 0) {
+         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ticket resets land before the publish
+         __hip_atomic_store(reinterpret_cast<unsigned long long*>(hd + slot_of[q]),
+                            (unsigned long long)__double_as_longlong(tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+   }
+   if (threadIdx.x == 0) {
+      for (int j = 0; j < ml; j++) {
+         unsigned long long* sl = reinterpret_cast<unsigned long long*>(hd + j);
+         unsigned long long b = kChainUnset;
+         for (long spin = 0; spin < (1l << 22); spin++) {
+            b = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (b != kChainUnset) break;
+            __builtin_amdgcn_s_sleep(1);
+         }
+         if (b == kChainUnset) {
+            s_fail = 1;
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+         }
+         s_h[j] = __longlong_as_double((long long)b);
+      }
+   }
+   __syncthreads();
+   if (s_fail) return;
+   const double h0 = s_h[0], h1 = ml == 2 ? s_h[1] : 0.0;
+   double acc = 0.0;
+#pragma unroll
+   for (int e = 0; e < EPT; e++) {
+      const size_t k = i0 + (size_t)e * T;
+      const bool in = k < n;
+      const double z0 = alias ? v0[e] : (in ? Z0[k] : 0.0);
+      const double z1 = ml == 2 ? (alias ? v1[e] : (in ? Z0[n + k] : 0.0)) : 0.0;
+      wv[e] = fma(-h0, z0, wv[e]);
+      if (ml == 2) wv[e] = fma(-h1, z1, wv[e]);
+      if (in) w[k] = wv[e];
+      acc = fma(wv[e], wv[e], acc);
+   }
+   // the norm after: tickets of pair 0 again (every workgroup is past that pair's publish, so its reset landed)
+   const double b = block_sum0_s<T>(acc, s_sc[0]);
+   double tot;
+   if (grid_total_s<T>(b, part + 3 * (size_t)kKMaxBlocks, ticket, &tot, &s_last[0], s_sc[0]) && threadIdx.x == 0)
+      hd[ml] = tot;
+}
+
 // a[s] *= fac[s] for the systems act[y] (k_scale2's arithmetic)
 __global__ void k_scale_batch(double* __restrict__ a, size_t lda, size_t n, const int* __restrict__ act,
                               const double* __restrict__ fac)
@@ -591,6 +681,9 @@ struct KScratch {
    double* hcoef = nullptr;  // pinned staging of per-step coefficients (DCGS2)
    double* bpart = nullptr;  // block Gram-Schmidt partials [kBDMaxBlocks][kScal]
    unsigned int *ticket = nullptr, *ticket2 = nullptr;
+   double* lz_part = nullptr;          // k_lanczos_local: 4 partial arrays
+   unsigned int* lz_ticket = nullptr;  // k_lanczos_local: 3 ticket arrays
+   int lz_occ = -1;                    // resident k_lanczos_local workgroups
    int* chain = nullptr;      // k_mgs_chain: [1] error word
    int* hchain_err = nullptr; // pinned read-back of the error word
    int chain_occ = -1;        // resident workgroups of k_mgs_chain per CU x CUs (0: unusable)
@@ -622,6 +715,19 @@ struct KScratch {
          NFFT4GP_HIP_CHECK(hipMemset(chain, 0, sizeof(int) * 2));
          NFFT4GP_HIP_CHECK(hipHostMalloc((void**)&hchain_err, sizeof(int)));
          *hchain_err = 0;
+      }
+      if (!lz_part) {
+         NFFT4GP_HIP_CHECK(hipMalloc((void**)&lz_part, sizeof(double) * 4 * kKMaxBlocks));
+         NFFT4GP_HIP_CHECK(hipMalloc((void**)&lz_ticket, sizeof(unsigned int) * 3 * kTicketWords));
+         NFFT4GP_HIP_CHECK(hipMemset(lz_ticket, 0, sizeof(unsigned int) * 3 * kTicketWords));
+      }
+      if (lz_occ < 0) {
+         int dev = 0, occ = 0;
+         hipDeviceProp_t prop;
+         lz_occ = 0;
+         if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+             hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lanczos_local<1024, 4>, 1024, 0) == hipSuccess)
+            lz_occ = occ * prop.multiProcessorCount;
       }
       if (chain_occ < 0) {
          int dev = 0, occ = 0;
@@ -671,6 +777,22 @@ struct Ctx {
                          g_k.chain + 1);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       // the error word comes back with the step's scalars (the caller's read synchronises)
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(g_k.hchain_err, g_k.chain + 1, sizeof(int), hipMemcpyDeviceToHost, s));
+      return 0;
+   }
+   // mgs2's local pass (block_gs(w, Vl, Zl, ml, h, 1)) in one launch where the grid fits (k_lanczos_local);
+   // otherwise block_gs.  NFFT4GP_AMD_LANCZOS_LOCAL=0 keeps block_gs.
+   int lanczos_local(double* w, const double* Vl, const double* Zl, int ml, double* h)
+   {
+      const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((n + 4095) / 4096, kKMaxBlocks));
+      const char* e = getenv("NFFT4GP_AMD_LANCZOS_LOCAL");
+      if (comm || (e && atoi(e) == 0) || ml < 1 || ml > 2 || g_k.ensure_chain() || (size_t)grid * 4096 < n ||
+          (int)grid > g_k.lz_occ || *g_k.hchain_err)
+         return block_gs(w, Vl, Zl, ml, h, 1);
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(h, 0xFF, sizeof(double) * (ml + 2), s));  // kChainUnset
+      hipLaunchKernelGGL((k_lanczos_local<1024, 4>), dim3(grid), dim3(1024), 0, s, w, Vl, Zl, Zl == Vl ? 1 : 0, n,
+                         ml, h, g_k.lz_part, g_k.lz_ticket, g_k.chain + 1);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
       NFFT4GP_HIP_CHECK(hipMemcpyAsync(g_k.hchain_err, g_k.chain + 1, sizeof(int), hipMemcpyDeviceToHost, s));
       return 0;
    }
@@ -1800,7 +1922,7 @@ struct LanczosRun {
       const int j0 = k >= 1 ? k - 1 : 0;
       const int ml = k + 1 - j0;
       double* o = hd + kB0 + m + 2;
-      if (c.block_gs(z, V + (size_t)j0 * n, Z + (size_t)j0 * n, ml, hd, 1)) return -1;
+      if (c.lanczos_local(z, V + (size_t)j0 * n, Z + (size_t)j0 * n, ml, hd)) return -1;
       if (c.block_gs(z, V, Z, m, hd + kB0, 0)) return -1;
       if (cb.prec && cb.solve(v, z)) return -1;
       hipLaunchKernelGGL(k_dot2, dim3(kgrid(n)), dim3(kKThreads), 0, c.s, v, z, n, g_k.part, g_k.ticket, g_k.part2,
@@ -1812,6 +1934,10 @@ struct LanczosRun {
    // tail; 1 ends the loop
    int step_after(bool first_loop, const double* hh)
    {
+      if (g_k.hchain_err && *g_k.hchain_err) {  // k_lanczos_local's wait gave up
+         fprintf(stderr, "nfft4gp_amd: Lanczos: the one-launch local pass's wait gave up\n");
+         return -1;
+      }
       const int k = step_k(first_loop);
       const int m = k + 1;
       const int j0 = k >= 1 ? k - 1 : 0;
