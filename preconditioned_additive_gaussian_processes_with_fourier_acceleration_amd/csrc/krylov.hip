@@ -1411,9 +1411,10 @@ int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* 
       cleanup();
       return -1;
    };
-   const int kpin = 4 * m + 2 * (kdim + 1) + 16;
+   const int kcyc = std::min(kdim, maxits) + 1;  // columns a cycle can combine
+   const int kpin = 4 * m + 2 * kcyc + 16;
    if (dmalloc(&part, (size_t)m * kKMaxBlocks) || dmalloc(&ticket, (size_t)m * kTicketWords) || dmalloc(&dfac, m) ||
-       dmalloc(&dact, m) || dmalloc(&dcoef, (size_t)kdim + 1) || dmalloc(&dcols, (size_t)kdim + 1))
+       dmalloc(&dact, m) || dmalloc(&dcoef, (size_t)kcyc) || dmalloc(&dcols, (size_t)kcyc))
       return fail();
    if (hipHostMalloc((void**)&pin, sizeof(double) * kpin) != hipSuccess) {
       pin = nullptr;
@@ -1539,7 +1540,7 @@ int fgmres_batch_dev(Callbacks& cb, int m, double* X, size_t ldx, const double* 
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return 0;
    };
-   if (2 * (kdim + 1) + 2 * m > kpin) return fail();
+   if (2 * kcyc + 2 * m > kpin) return fail();
 
    struct Sys {
       double normb = 0, normr = 0, tolr = 0, rel_prev = 0;
