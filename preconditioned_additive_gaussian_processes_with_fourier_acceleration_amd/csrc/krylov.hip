@@ -410,10 +410,16 @@ int bd_grid(size_t n)
 // part[blockIdx.x * ldp + i] = sum over this block's rows r of w[r] V[i n + r], i in [g0, g0 + kBD) & < m;
 // with_norm: column m is w itself (part[.. + m] sums ||w||^2)
 // c_after / c_before (optional): a second pass that runs only when the DGKS test of k_block_update holds
+// FOLD: k_block_reduce folded in -- the partials are stored at agent scope, the last arriving workgroup of each
+// column group (reduce.hpp's per-XCD tickets, one ticket array per group) sums them in k_block_reduce's order
+// and writes h[0..m) (h[m + 1] for the norm column): one launch instead of two, the same bits
+template <bool FOLD = false>
 __global__ __launch_bounds__(kBDThreads) void k_block_dots(const double* __restrict__ w, const double* __restrict__ V,
                                                            size_t n, int m, int with_norm, double* __restrict__ part,
                                                            int ldp, const double* __restrict__ c_after = nullptr,
-                                                           const double* __restrict__ c_before = nullptr)
+                                                           const double* __restrict__ c_before = nullptr,
+                                                           double* __restrict__ h = nullptr,
+                                                           unsigned int* __restrict__ tickets = nullptr)
 {
    if (c_after && !(sqrt(*c_after) < 0.7071 * sqrt(*c_before))) return;
    __shared__ double s[kBDThreads / 64][kBD];
@@ -444,7 +450,54 @@ __global__ __launch_bounds__(kBDThreads) void k_block_dots(const double* __restr
       double t = 0.0;
 #pragma unroll
       for (int q = 0; q < kBDThreads / 64; q++) t += s[q][threadIdx.x];
-      part[(size_t)blockIdx.x * ldp + g0 + threadIdx.x] = t;
+      if (FOLD)
+         __hip_atomic_store(part + (size_t)blockIdx.x * ldp + g0 + threadIdx.x, t, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+      else
+         part[(size_t)blockIdx.x * ldp + g0 + threadIdx.x] = t;
+   }
+   if constexpr (FOLD) {
+      __shared__ int s_last;
+      __shared__ double s_sum[16][kBD];
+      unsigned int* ticket = tickets + (size_t)blockIdx.y * kTicketWords;
+      if (threadIdx.x == 0) {  // the partial stores are wave 0's (cnt <= kBD lanes)
+         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+         const unsigned G = gridDim.x;
+         const unsigned xcd = blockIdx.x % kRedXcds;
+         const unsigned members = (G - xcd + kRedXcds - 1) / kRedXcds;
+         const unsigned groups = G < kRedXcds ? G : kRedXcds;
+         int last = 0;
+         const unsigned old = __hip_atomic_fetch_add(ticket + (1 + xcd) * kTicketStride, 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+         if (old == members - 1) {
+            const unsigned top = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = (top == groups - 1);
+         }
+         s_last = last;
+      }
+      __syncthreads();
+      if (!s_last) return;
+      // k_block_reduce's sum: 16 strands per column, four accumulators cycled, then the strands in order
+      const int col = threadIdx.x % kBD, g = threadIdx.x / kBD;
+      if (g < 16) {
+         double z[4] = {0.0, 0.0, 0.0, 0.0};
+         int u = 0;
+         const int nblk = (int)gridDim.x;
+         const int ii = col < cnt ? g0 + col : g0 + cnt - 1;
+         for (int b = g; b < nblk; b += 16, u = (u + 1) & 3)
+            z[u] += __hip_atomic_load(part + (size_t)b * ldp + ii, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+         s_sum[g][col] = (z[0] + z[1]) + (z[2] + z[3]);
+      }
+      __syncthreads();
+      if (threadIdx.x < cnt) {
+         double t = 0.0;
+#pragma unroll
+         for (int q = 0; q < 16; q++) t += s_sum[q][threadIdx.x];
+         const int i = g0 + threadIdx.x;
+         h[i < m ? i : m + 1] = t;
+      }
+      if (threadIdx.x <= (unsigned)kRedXcds)
+         __hip_atomic_store(ticket + threadIdx.x * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
    }
 }
 
@@ -687,9 +740,15 @@ struct KScratch {
    int* chain = nullptr;      // k_mgs_chain: [1] error word
    int* hchain_err = nullptr; // pinned read-back of the error word
    int chain_occ = -1;        // resident workgroups of k_mgs_chain per CU x CUs (0: unusable)
+   unsigned int* bd_tickets = nullptr;  // k_block_dots<true>: one ticket array per column group
    int ensure_bpart()
    {
       if (!bpart) NFFT4GP_HIP_CHECK(hipMalloc((void**)&bpart, sizeof(double) * kBDMaxBlocks * kScal));
+      if (!bd_tickets) {
+         const size_t words = (size_t)(kScal / kBD + 1) * kTicketWords;
+         NFFT4GP_HIP_CHECK(hipMalloc((void**)&bd_tickets, sizeof(unsigned int) * words));
+         NFFT4GP_HIP_CHECK(hipMemset(bd_tickets, 0, sizeof(unsigned int) * words));
+      }
       return 0;
    }
    int ensure()
@@ -822,6 +881,12 @@ struct Ctx {
       return v;
    }
    double norm(const double* a) { return std::sqrt(dot(a, a)); }
+   // k_block_reduce folded into k_block_dots (NFFT4GP_AMD_BD_FOLD=0: two launches)
+   static bool fold_reduce()
+   {
+      const char* e = getenv("NFFT4GP_AMD_BD_FOLD");
+      return !(e && atoi(e) == 0);
+   }
    // one classical Gram-Schmidt pass: h[0..m) = V^T w, w -= Z h, h[m] = ||w||^2 afterwards (device
    // scalars); with_norm: also h[m + 1] = ||w||^2 before the update (from the dot pass)
    int block_gs(double* w, const double* V, const double* Z, int m, double* h, int with_norm = 0)
@@ -832,10 +897,17 @@ struct Ctx {
       const int mc = m + with_norm;
       // h[m], h[m + 1] take part in the all-reduce below even when this pass does not write them
       if (comm) NFFT4GP_HIP_CHECK(hipMemsetAsync(h + m, 0, sizeof(double) * 2, s));
-      hipLaunchKernelGGL(k_block_dots, dim3(nb, (mc + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m, with_norm,
-                         g_k.bpart, KScratch::kScal);
-      hipLaunchKernelGGL(k_block_reduce, dim3((mc + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, mc, m,
-                         h);
+      if (fold_reduce()) {
+         hipLaunchKernelGGL(k_block_dots<true>, dim3(nb, (mc + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m,
+                            with_norm, g_k.bpart, KScratch::kScal, (const double*)nullptr, (const double*)nullptr, h,
+                            g_k.bd_tickets);
+      } else {
+         hipLaunchKernelGGL(k_block_dots<false>, dim3(nb, (mc + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m,
+                            with_norm, g_k.bpart, KScratch::kScal, (const double*)nullptr, (const double*)nullptr,
+                            (double*)nullptr, (unsigned int*)nullptr);
+         hipLaunchKernelGGL(k_block_reduce, dim3((mc + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, mc,
+                            m, h);
+      }
       NFFT4GP_HIP_CHECK(hipGetLastError());
       if (red(h, m + 2)) return -1;  // the projections and the norm before them, summed over the row shards
       hipLaunchKernelGGL(k_block_update, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, Z, n, h, m,
@@ -855,10 +927,15 @@ struct Ctx {
       const int nb = bd_grid(n);
       const double* after = h + m;
       const double* before = h + m + 1;
-      hipLaunchKernelGGL(k_block_dots, dim3(nb, (m + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m, 0, g_k.bpart,
-                         KScratch::kScal, after, before);
-      hipLaunchKernelGGL(k_block_reduce, dim3((m + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, m, m,
-                         h + m + 2);
+      if (fold_reduce()) {
+         hipLaunchKernelGGL(k_block_dots<true>, dim3(nb, (m + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m, 0,
+                            g_k.bpart, KScratch::kScal, after, before, h + m + 2, g_k.bd_tickets);
+      } else {
+         hipLaunchKernelGGL(k_block_dots<false>, dim3(nb, (m + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m, 0,
+                            g_k.bpart, KScratch::kScal, after, before, (double*)nullptr, (unsigned int*)nullptr);
+         hipLaunchKernelGGL(k_block_reduce, dim3((m + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, m, m,
+                            h + m + 2);
+      }
       NFFT4GP_HIP_CHECK(hipGetLastError());
       if (red(h + m + 2, m)) return -1;
       hipLaunchKernelGGL(k_block_update, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, V, n, h + m + 2,
