@@ -855,6 +855,9 @@ def main():
         el_ai, per_a = timed(True)
         rows_allreduce = {"value": args.steps / el_a, "ms_per_step": 1e3 * el_a / args.steps,
                           "per_rank": rank_times(per_a, el_ai)}
+        # the solver legs below run over the exchange again: their grids and their small all-reduces (dots,
+        # norms, Hessenberg columns: PeerComm, dist.hip) go through the peer buffers
+        peer["solvers"] = bool(peer_enable_verified(op, xd, dist).get("verified"))
     alt = None
     if world > 1:
         # the other split, timed the same way (W warmup + K steps between barriers, max over ranks)

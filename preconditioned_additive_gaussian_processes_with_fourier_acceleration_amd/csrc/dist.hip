@@ -132,13 +132,96 @@ __global__ void k_axpby_add(double beta, double* __restrict__ y, const double* _
 // the peers' opened ones, the device pointer table and the host-mapped error word the waits set
 constexpr int kPeerMaxWorld = 256;  // the grid kernels' threads: one polls each rank's flag
 
+constexpr int kPeerScal = 4096;  // scalars per peer all-reduce (larger ones go to the communicator)
+
+// rank r's buffer (nfft_kernels.hip's peer_buf: the first kPeerInline from the kernel arguments)
+__device__ __forceinline__ char* peer_rank_buf(const PeerArgs& A, int r)
+{
+   char* b = A.inl[0];
+#pragma unroll
+   for (int k = 1; k < kPeerInline; k++)
+      if (r == k) b = A.inl[k];
+   return r < kPeerInline ? b : A.bufs[r];
+}
+
+// The solvers' small all-reduces (dots, norms, Hessenberg columns) over the same IPC buffers as the grid exchange:
+// each rank puts its `count` values into its scalar slot of exchange e (two epoch-stamped 64-bit words per value,
+// system scope, as the grid entries), then a thread per (rank, value) polls that rank's entry until it carries e,
+// and the values are summed in rank order -- the same bits on every rank, and for two ranks the same as any
+// all-reduce.  Slot parity e & 1: a rank writes exchange e + 2's slot only after it has read every rank's e + 1,
+// which every rank published after reading e.  A wait that gives up sets *A.err (the next operator call fails).
+__global__ __launch_bounds__(1024) void k_peer_scalars(PeerArgs A, long long off, unsigned int e,
+                                                       double* __restrict__ v, int count)
+{
+   __shared__ double s_v[1024];
+   const unsigned long long stamp = (unsigned long long)e << 32;
+   const size_t slot = (size_t)off + (size_t)(e & 1u) * kPeerScal * 16;
+   for (int i = threadIdx.x; i < count; i += 1024) {
+      unsigned long long* p = (unsigned long long*)(A.own + slot) + 2 * i;
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(v[i]);
+      __hip_atomic_store(p, (bits & 0xffffffffull) | stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(p + 1, (bits >> 32) | stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+   }
+   __syncthreads();  // every thread's reads of v are done before any sum overwrites it
+   const int W = A.world;
+   const int per = 1024 / W;
+   for (int i0 = 0; i0 < count; i0 += per) {
+      const int r = threadIdx.x % W, k = threadIdx.x / W, i = i0 + k;
+      if (k < per && i < count) {
+         const unsigned long long* p = (const unsigned long long*)(peer_rank_buf(A, r) + slot) + 2 * i;
+         unsigned long long w0 = 0, w1 = 0;
+         for (long long it = 0;; it++) {
+            w0 = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            w1 = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((unsigned int)(w0 >> 32) == e && (unsigned int)(w1 >> 32) == e) break;
+            if (it >= A.spin) {
+               __hip_atomic_store(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+               break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+         }
+         s_v[k * W + r] = __longlong_as_double((long long)((w0 & 0xffffffffull) | (w1 << 32)));
+      }
+      __syncthreads();
+      if (threadIdx.x < per && i0 + (int)threadIdx.x < count) {
+         double sum = 0.0;
+         for (int q = 0; q < W; q++) sum = q == 0 ? s_v[threadIdx.x * W] : sum + s_v[threadIdx.x * W + q];
+         v[i0 + threadIdx.x] = sum;
+      }
+      __syncthreads();
+   }
+}
+
+struct PeerState;
+// the communicator the solvers see while the peer exchange is on: small all-reduces through the IPC buffers,
+// larger ones through the operator's own communicator
+struct PeerComm : Comm {
+   PeerState* P = nullptr;
+   Comm* base = nullptr;
+   int ranks() override { return base->ranks(); }
+   int allreduce(double* d_buf, size_t count, hipStream_t s) override;
+};
+
 struct PeerState {
    PeerArgs a;
    char* local = nullptr;
    std::vector<char*> opened;  // peers' buffers from hipIpcOpenMemHandle (closed at free)
    char** d_bufs = nullptr;
    unsigned int* h_err = nullptr;
+   long long scal_off = 0;     // bytes: the scalar slots after the two grid slots
+   unsigned int sepoch = 0;    // scalar exchanges so far (the stamp of the next is sepoch + 1)
+   PeerComm pcomm;
 };
+
+int PeerComm::allreduce(double* d_buf, size_t count, hipStream_t s)
+{
+   if (count == 0) return 0;
+   if (count > (size_t)kPeerScal) return base->allreduce(d_buf, count, s);
+   if (++P->sepoch == 0u) P->sepoch = 1u;  // 0 is the zeroed buffer's stamp
+   hipLaunchKernelGGL(k_peer_scalars, dim3(1), dim3(1024), 0, s, P->a, P->scal_off, P->sepoch, d_buf, (int)count);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
 
 struct DistOp {
    // first member: a distributed operator is also the kernel data of the loss (gp_loss.c:143-150 writes
@@ -380,7 +463,10 @@ int dist_pcg_info(void* dop, DistPcgInfo& info)
    if (!D) return -1;
    info.n_global = D->n_global;
    info.row_begin = D->kind == 0 ? D->row_begin : 0;
-   info.dot_comm = D->kind == 0 ? D->comm : nullptr;
+   // with the peer exchange on, the solvers' small all-reduces go through it too (PeerComm)
+   // (not under NFFT4GP_AMD_PEER_FAKE_WORLD, whose sums are wrong by design)
+   const bool peer_dots = D->peer && D->peer->a.world == D->comm->world;
+   info.dot_comm = D->kind == 0 ? (peer_dots ? (Comm*)&D->peer->pcomm : D->comm) : nullptr;
    info.fused_dot = D->kind == 0 && shard_fused_dot_ok(D->h);
    return 0;
 }
@@ -624,7 +710,8 @@ int Nfft4GPAmdDistPeerEnable(void* dop)
    hipStream_t s = current_stream();
    PeerState* P = new PeerState();
    const size_t gcount = D->grid_count;
-   const size_t bytes = 2 * gcount * 16;  // two slots of (low, high) words with the epoch (nfft_kernels.hip)
+   // two grid slots of (low, high) words with the epoch (nfft_kernels.hip), then two scalar slots (k_peer_scalars)
+   const size_t bytes = 2 * gcount * 16 + 2 * (size_t)kPeerScal * 16;
    constexpr size_t HB = sizeof(hipIpcMemHandle_t);
    bool ok = hipMalloc((void**)&P->local, bytes) == hipSuccess && hipMemsetAsync(P->local, 0, bytes, s) == hipSuccess &&
              hipStreamSynchronize(s) == hipSuccess;
@@ -716,6 +803,11 @@ int Nfft4GPAmdDistPeerEnable(void* dop)
    P->a.err = d_err;
    P->a.slot_doubles = (long long)gcount;
    P->a.spin = spin;
+   P->scal_off = (long long)(2 * gcount * 16);
+   P->pcomm.P = P;
+   P->pcomm.base = C;
+   P->pcomm.rank = C->rank;
+   P->pcomm.world = C->world;
    D->peer = P;
    return 0;
 }
