@@ -315,6 +315,50 @@ int Nfft4GPAmdPrecondNysDvp(void *vnys_mat, int n, int *mask, NFFT4GP_DOUBLE *x,
 int Nfft4GPAmdPrecondNysTrace(void *vnys_mat, NFFT4GP_DOUBLE **tracesp);
 NFFT4GP_DOUBLE Nfft4GPAmdPrecondNysLogdet(void *vnys_mat);
 
+/* ---- the reference's own Nystrom struct and apply, under the reference's name --------------------------
+ * precond_nys: field layout identical to SRC/preconds/nys.h:24-55 (INC/_preconds.h:320-351; offsets tested in
+ * tests/test_dropin.py).  The Cholesky factor stays opaque (SRC/preconds/chol.h:18).
+ * Nfft4GPPrecondNysSolve replaces the reference's (INC/_preconds.h:400, nys.c:115-173): x = M^{-1} rhs,
+ * M^{-1} = U S U^T + (I - U U^T) / eta in the permuted order of _perm, a func_solve.  vnys_mat is either
+ * a precond_nys built by the reference's own Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660; host _U, _s,
+ * _perm, _eta, _n, _k are read at the offsets above), or a handle of Nfft4GPAmdPrecondNysCreate (then it is
+ * Nfft4GPAmdPrecondNysSolve).  A reference struct's factors are mirrored into HBM on first use (U stored
+ * un-permuted, as Nfft4GPAmdNysCreate does) and the mirror is reused while _U, _s, _perm, _n, _k, _eta,
+ * _tset and a fingerprint of s and of sampled U and perm entries are unchanged (a re-setup rebuilds it);
+ * at most two mirrors are kept (least recently used first out).  x and rhs may be host or device
+ * arrays; n is ignored like the reference (it reads _n).  _titt / _tits are updated as nys.c:166-170 does.
+ * The reference's setup, Dvp, Trace and Logdet keep their host implementation (they run on the dense
+ * kernel callbacks of the caller and on its host-side _K / _dU / _chol_K11); the Dvp's own applies
+ * (nys.c:289, :312) reach this Solve through the dynamic linker when this library is linked first. */
+typedef struct NFFT4GP_PRECOND_CHOL_STRUCT *pprecond_chol;
+typedef struct NFFT4GP_PRECOND_NYS_STRUCT
+{
+   int _k_setup;
+   int _own_perm;
+   int *_perm;
+   int _n;
+   int _tits;
+   NFFT4GP_DOUBLE _titt;
+   NFFT4GP_DOUBLE _tset;
+   NFFT4GP_DOUBLE _tlogdet;
+   NFFT4GP_DOUBLE _tdvp;
+   int _nys_opt;
+   int _k;
+   NFFT4GP_DOUBLE _eta;
+   NFFT4GP_DOUBLE _f2;
+   NFFT4GP_DOUBLE *_U;
+   NFFT4GP_DOUBLE *_s;
+   NFFT4GP_DOUBLE *_work;
+   NFFT4GP_DOUBLE *_K;
+   NFFT4GP_DOUBLE *_dU;
+   NFFT4GP_DOUBLE *_dK;
+   pprecond_chol _chol_K11;
+   int _dvp_nosolve;
+} precond_nys, *pprecond_nys;
+int Nfft4GPPrecondNysSolve(void *vnys_mat, int n, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE *rhs);
+/* drop the HBM mirror kept for a reference precond_nys (e.g. before the caller frees it); 0 if none */
+int Nfft4GPAmdPrecondNysMirrorRelease(void *vnys_mat);
+
 /* ---- FSAI preconditioner built on the GPU, with gradients (SRC/preconds/fsai.h:46-207) ----------------
  * Drop-ins for Nfft4GPPrecondFsaiCreate / Free / Reset / SetLfil (fsai.c:3-104),
  * Nfft4GPPrecondFsaiSetupWithKernel (fsai.c:302-673: KNN pattern kernels.c:121-278, per-row Cholesky
@@ -550,6 +594,10 @@ void Nfft4GPAmdDistFree(void *dop);
  * to the global n, so its iterations equal the single-GPU solver's up to rounding. */
 int Nfft4GPAmdDistMatSymv(void *dop, int n, NFFT4GP_DOUBLE alpha, NFFT4GP_DOUBLE *x, NFFT4GP_DOUBLE beta,
                           NFFT4GP_DOUBLE *y);
+/* synchronise the library stream, then 0, or -1 (message on stderr) if a peer exchange of this operator timed
+ * out in the work enqueued so far: its y are then not to be used.  The solvers (PCG, FGMRES, Lanczos, the
+ * quadrature, the loss) make this check before they report success. */
+int Nfft4GPAmdDistCheck(void *dop);
 /* kind 1 (components): y is all-reduced in `chunks` pieces (default 4) on a stream of the operator's own,
  * each piece as soon as the interpolation launch that writes it is done, so the all-reduce of piece i
  * overlaps the interpolation of piece i + 1 (1-D windows, plain matvec; the gradient matvec and

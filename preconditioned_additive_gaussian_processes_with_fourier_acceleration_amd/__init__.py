@@ -8,7 +8,7 @@ from ._lib import ExtensionMissing, header_symbols, lib  # noqa: F401
 from .data import read_features, read_labels, read_windows  # noqa: F401
 from .gp import gp_loss, gp_predict  # noqa: F401
 from .nfft import GAUSSIAN, MATERN12, NFFTAdditiveKernel, NFFTKernel  # noqa: F401
-from .solvers import (AfnPrecond, FsaiPrecond, NystromPrecond, PrecondAFN, afn_rank_estimate, fgmres,  # noqa: F401
+from .solvers import (AfnPrecond, FsaiPrecond, NystromPrecond, PrecondAFN, ReferenceNystrom, afn_rank_estimate, fgmres,  # noqa: F401
                       logdet, pcg, sort_fps)
 
 __version__ = "0.1.0"

@@ -119,6 +119,8 @@ _SIGS = {
     "Nfft4GPAmdPrecondNysDvp": (C.c_int, [vp, C.c_int, vp, vp, vp]),
     "Nfft4GPAmdPrecondNysTrace": (C.c_int, [vp, vp]),
     "Nfft4GPAmdPrecondNysLogdet": (C.c_double, [vp]),
+    "Nfft4GPPrecondNysSolve": (C.c_int, [vp, C.c_int, vp, vp]),
+    "Nfft4GPAmdPrecondNysMirrorRelease": (C.c_int, [vp]),
     "Nfft4GPAmdFsaiCreate": (vp, [C.c_int, vp, vp, vp]),
     "Nfft4GPAmdFsaiSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdFsaiFree": (None, [vp]),

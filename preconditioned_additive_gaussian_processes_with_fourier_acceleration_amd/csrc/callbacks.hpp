@@ -126,6 +126,19 @@ inline int bind_dist(Callbacks& cb)
    return 0;
 }
 
+// a solver's last host sync before it reports success: a peer exchange of its distributed operator whose wait
+// gave up during the solve (dist.hip) fails the solve instead of returning numbers summed from stale words
+inline int dist_final_check(const Callbacks& cb)
+{
+   if (!cb.mv_dev || (cb.matvec != &Nfft4GPAmdDistMatSymv && cb.matvec != &Nfft4GPAmdDistGradMatSymv)) return 0;
+   NFFT4GP_HIP_CHECK(hipStreamSynchronize(current_stream()));
+   if (dist_failed(cb.mat)) {
+      fprintf(stderr, "nfft4gp_amd: a peer exchange timed out during the solve; its result is discarded\n");
+      return -1;
+   }
+   return 0;
+}
+
 // the library's own func_symmatvec / func_solve entry points (these take device pointers)
 bool library_operator(const void* fn);
 extern int g_cb_mode;  // Nfft4GPAmdSetCallbackPointerMode

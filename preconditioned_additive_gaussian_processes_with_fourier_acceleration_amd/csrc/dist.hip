@@ -217,7 +217,8 @@ int PeerComm::allreduce(double* d_buf, size_t count, hipStream_t s)
 {
    if (count == 0) return 0;
    if (count > (size_t)kPeerScal) return base->allreduce(d_buf, count, s);
-   if (++P->sepoch == 0u) P->sepoch = 1u;  // 0 is the zeroed buffer's stamp
+   // 0 is the zeroed buffer's stamp; on wrap skip to 2, which keeps the slot parity alternating (e / e + 2 reuse)
+   if (++P->sepoch == 0u) P->sepoch = 2u;
    hipLaunchKernelGGL(k_peer_scalars, dim3(1), dim3(1024), 0, s, P->a, P->scal_off, P->sepoch, d_buf, (int)count);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
@@ -457,6 +458,14 @@ struct DistNys {
 }  // namespace
 
 namespace nfft4gp_amd {
+// a peer exchange's wait gave up during the work enqueued so far (read after a host sync): the operator's
+// results, and a solver's that used it, are not to be trusted
+int dist_failed(void* dop)
+{
+   DistOp* D = (DistOp*)dop;
+   return D && peer_check(D) ? 1 : 0;
+}
+
 int dist_pcg_info(void* dop, DistPcgInfo& info)
 {
    DistOp* D = (DistOp*)dop;
@@ -585,6 +594,10 @@ void* Nfft4GPAmdDistCreate(void* handle, int kind, void* comm)
    D->n_local = nl;
    D->n_global = ng;
    D->row_begin = rb;
+   if (kind == 0 && rb % 16 != 0)
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdDistCreate: row shard starts at %d, not a multiple of 16: the 1-D layout's "
+                      "offset words then differ from the whole handle's, so the operator depends on the split by "
+                      "rounding (dist.row_range's shards start at multiples of 16)\n", rb);
    const nfft4gp_kernel* kd = (const nfft4gp_kernel*)handle;
    D->hdr._params[0] = kd->_params[0];
    D->hdr._params[1] = kd->_params[1];
@@ -793,7 +806,9 @@ int Nfft4GPAmdDistPeerEnable(void* dop)
    }
    unsigned int* d_err = nullptr;
    if (hipHostGetDevicePointer((void**)&d_err, P->h_err, 0) != hipSuccess) d_err = P->h_err;
-   long long spin = 1ll << 20;  // ~2 s of polls (each a system-scope load and an s_sleep)
+   // ~16 s of polls (each a system-scope load and an s_sleep): far above the host-side skew of ranks that
+   // enqueue the same solve, short enough that a dead peer ends the call
+   long long spin = 1ll << 23;
    if (const char* e = getenv("NFFT4GP_AMD_PEER_SPIN")) spin = std::max(1ll, atoll(e));
    P->a.bufs = P->d_bufs;
    for (int r = 0; r < kPeerInline && r < (int)bufs.size(); r++) P->a.inl[r] = bufs[r];
@@ -834,6 +849,13 @@ int Nfft4GPAmdDistSetChunks(void* dop, int chunks)
    (void)hipStreamSynchronize(current_stream());
    D->chunks = chunks;
    return 0;
+}
+
+int Nfft4GPAmdDistCheck(void* dop)
+{
+   if (!dop) return -1;
+   NFFT4GP_HIP_CHECK(hipStreamSynchronize(current_stream()));
+   return peer_check((DistOp*)dop);
 }
 
 int Nfft4GPAmdDistMatSymv(void* dop, int n, double alpha, double* x, double beta, double* y)

@@ -456,6 +456,8 @@ struct Comm {
 };
 // additive handle rows (nfft_api.cpp): local, global, first row; -1 if not an additive handle
 int additive_rows(void* str, int* n_local, int* n_global, int* row_begin);
+// 1 when a peer exchange of the distributed operator dop timed out (dist.hip; read after a host sync)
+int dist_failed(void* dop);
 bool shard_fused_dot_ok(void* str);
 // row shard: grid (summed over the shards) -> y_local = A x_local and *d_dot = (y_local, x_local) locally
 int shard_finish_dot(void* str, const double* grid, const double* x_local, double* y_local, double* d_dot);

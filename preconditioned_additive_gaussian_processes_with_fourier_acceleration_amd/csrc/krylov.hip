@@ -740,6 +740,20 @@ struct KScratch {
    int* chain = nullptr;      // k_mgs_chain: [1] error word
    int* hchain_err = nullptr; // pinned read-back of the error word
    int chain_occ = -1;        // resident workgroups of k_mgs_chain per CU x CUs (0: unusable)
+   // set once a one-launch sweep's wait has given up in this process: the sweeps then run as launch chains
+   // (k_gs_step / block_gs), which cannot wait on other workgroups
+   bool chain_off = false;
+   // after a wait gave up: clear the error word and every ticket array the one-launch kernels count on, so
+   // later reductions start from zero, and stop using those kernels (chain_off)
+   void chain_reset()
+   {
+      (void)hipDeviceSynchronize();
+      if (chain) (void)hipMemset(chain, 0, sizeof(int) * 2);
+      if (ticket) (void)hipMemset(ticket, 0, sizeof(unsigned int) * kTicketWords);
+      if (lz_ticket) (void)hipMemset(lz_ticket, 0, sizeof(unsigned int) * 3 * kTicketWords);
+      if (hchain_err) *hchain_err = 0;
+      chain_off = true;
+   }
    unsigned int* bd_tickets = nullptr;  // k_block_dots<true>: one ticket array per column group
    int ensure_bpart()
    {
@@ -807,6 +821,7 @@ struct Ctx {
    // row-sharded vectors (a distributed operator's rows): every inner product is a local partial, summed
    // in place over the ranks on the stream before anything reads it; NULL for whole vectors
    Comm* comm = nullptr;
+   bool lz_launched = false;  // the last lanczos_local call launched k_lanczos_local
    int red(double* d, int count)
    {
       return comm ? comm->allreduce(d, (size_t)count, s) : 0;
@@ -830,7 +845,7 @@ struct Ctx {
       const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((n + 4095) / 4096, kKMaxBlocks));
       const char* e = getenv("NFFT4GP_AMD_MGS_CHAIN");
       const bool off = e && atoi(e) == 0;
-      if (off || (size_t)grid * 4096 < n || (int)grid > g_k.chain_occ) return 1;
+      if (off || g_k.chain_off || (size_t)grid * 4096 < n || (int)grid > g_k.chain_occ) return 1;
       NFFT4GP_HIP_CHECK(hipMemsetAsync(hd, 0xFF, sizeof(double) * (i + 1), s));  // kChainUnset
       hipLaunchKernelGGL((k_mgs_chain<1024, 4>), dim3(grid), dim3(1024), 0, s, w, V, n, i, hd, g_k.part, g_k.ticket,
                          g_k.chain + 1);
@@ -845,9 +860,11 @@ struct Ctx {
    {
       const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((n + 4095) / 4096, kKMaxBlocks));
       const char* e = getenv("NFFT4GP_AMD_LANCZOS_LOCAL");
+      lz_launched = false;
       if (comm || (e && atoi(e) == 0) || ml < 1 || ml > 2 || g_k.ensure_chain() || (size_t)grid * 4096 < n ||
-          (int)grid > g_k.lz_occ || *g_k.hchain_err)
+          (int)grid > g_k.lz_occ || g_k.chain_off)
          return block_gs(w, Vl, Zl, ml, h, 1);
+      lz_launched = true;
       NFFT4GP_HIP_CHECK(hipMemsetAsync(h, 0xFF, sizeof(double) * (ml + 2), s));  // kChainUnset
       hipLaunchKernelGGL((k_lanczos_local<1024, 4>), dim3(grid), dim3(1024), 0, s, w, Vl, Zl, Zl == Vl ? 1 : 0, n,
                          ml, h, g_k.lz_part, g_k.lz_ticket, g_k.chain + 1);
@@ -855,13 +872,23 @@ struct Ctx {
       NFFT4GP_HIP_CHECK(hipMemcpyAsync(g_k.hchain_err, g_k.chain + 1, sizeof(int), hipMemcpyDeviceToHost, s));
       return 0;
    }
-   // after the read that follows mgs_chain: did a wait give up?  (then the reductions' tickets are reset, so
-   // later solves in this process sum correctly; the error word stays set and every later sweep fails)
+   // after the read that follows mgs_chain: did a wait give up?  Then this solve fails, the error word and the
+   // tickets are reset and later sweeps in this process run as k_gs_step chains (KScratch::chain_reset)
    int chain_failed()
    {
       if (*g_k.hchain_err) {
          fprintf(stderr, "nfft4gp_amd: FGMRES: the one-launch MGS sweep's wait gave up\n");
-         (void)hipMemset(g_k.ticket, 0, sizeof(unsigned int) * kTicketWords);
+         g_k.chain_reset();
+         return 1;
+      }
+      return 0;
+   }
+   // after the read that follows lanczos_local: did this step's launch give up waiting?  (same reset)
+   int lanczos_local_failed()
+   {
+      if (lz_launched && *g_k.hchain_err) {
+         fprintf(stderr, "nfft4gp_amd: Lanczos: the one-launch local pass's wait gave up\n");
+         g_k.chain_reset();
          return 1;
       }
       return 0;
@@ -2012,10 +2039,7 @@ struct LanczosRun {
    // tail; 1 ends the loop
    int step_after(bool first_loop, const double* hh)
    {
-      if (g_k.hchain_err && *g_k.hchain_err) {  // k_lanczos_local's wait gave up
-         fprintf(stderr, "nfft4gp_amd: Lanczos: the one-launch local pass's wait gave up\n");
-         return -1;
-      }
+      if (c.lanczos_local_failed()) return -1;
       const int k = step_k(first_loop);
       const int m = k + 1;
       const int j0 = k >= 1 ? k - 1 : 0;
@@ -2410,6 +2434,21 @@ bool make_callbacks(Callbacks& cb, int n, func_symmatvec matvec, void* mat, func
 
 }  // namespace
 
+// Fault injection for tests/test_gpu_krylov.py: mode 1 sets the one-launch kernels' error word (the state a
+// wait that gave up leaves) and re-enables them; mode 0 clears it and re-enables them.  Returns whether the
+// one-launch sweeps were off (a wait had given up) before the call.
+extern "C" int Nfft4GPAmdDebugChainFault(int mode)
+{
+   if (g_k.ensure_chain()) return -1;
+   const int was_off = g_k.chain_off ? 1 : 0;
+   (void)hipDeviceSynchronize();
+   const int v = mode ? 1 : 0;
+   NFFT4GP_HIP_CHECK(hipMemcpy(g_k.chain + 1, &v, sizeof(int), hipMemcpyHostToDevice));
+   *g_k.hchain_err = 0;
+   g_k.chain_off = false;
+   return was_off;
+}
+
 extern "C" {
 
 void Nfft4GPAmdSetFgmresOrtho(int ortho) { g_fgmres_ortho = (ortho == 1 || ortho == 2) ? ortho : 0; }
@@ -2431,7 +2470,8 @@ int Nfft4GPSolverFgmres(void* mat_data, int n, func_symmatvec matvec, void* prec
    if (!make_callbacks(cb, n, matvec, mat_data, precondfunc, prec_data)) return -1;
    Vec vx, vb;
    if (vx.open(x, n, true) || vb.open(rhs, n, true)) return -1;
-   const int rc = fgmres_dev(cb, vx.d, vb.d, kdim, maxits, atol, tol, prel_res, prel_res_v, piter, print_level);
+   int rc = fgmres_dev(cb, vx.d, vb.d, kdim, maxits, atol, tol, prel_res, prel_res_v, piter, print_level);
+   if (rc == 0 && dist_final_check(cb)) rc = -1;
    vb.close(false);
    vx.close(rc == 0);
    return rc;
@@ -2447,8 +2487,9 @@ int Nfft4GPSolverLanczos(void* mat_data, int n, func_symmatvec matvec, void* pre
    if (!make_callbacks(cb, n, matvec, mat_data, precondfunc, prec_data)) return -1;
    Vec vx, vb;
    if (vx.open(x, n, true) || vb.open(rhs, n, true)) return -1;
-   const int rc = lanczos_dev(cb, vx.d, vb.d, wsize, maxits, atol, tol, prel_res, prel_res_v, piter, tsize, TDp, TEp,
-                              print_level);
+   int rc = lanczos_dev(cb, vx.d, vb.d, wsize, maxits, atol, tol, prel_res, prel_res_v, piter, tsize, TDp, TEp,
+                        print_level);
+   if (rc == 0 && dist_final_check(cb)) rc = -1;
    vb.close(false);
    vx.close(rc == 0);
    return rc;
@@ -2466,8 +2507,9 @@ int Nfft4GPLanczosQuadratureLogdet(void* mat_data, void* dmat_data, int n, func_
        !make_callbacks(dcb, n, dmatvec, dmat_data, nullptr, nullptr))
       return -1;
    dcb.out_mult = 3;
-   return lanczos_logdet_dev(cb, dcb, tracefunc, logdetfunc, dvpfunc, maxits, nvecs, radamacher, print_level, logdet,
-                             dlogdetp);
+   const int rc = lanczos_logdet_dev(cb, dcb, tracefunc, logdetfunc, dvpfunc, maxits, nvecs, radamacher, print_level,
+                                     logdet, dlogdetp);
+   return rc == 0 && dist_final_check(cb) ? -1 : rc;
 }
 
 int Nfft4GPTransform(nfft4gp_transform_type type, double val, int inverse, double* tvalp, double* dtvalp)
@@ -2602,6 +2644,10 @@ int Nfft4GPGpLoss(double* x, double* data, double* label, int n, int ldim, int d
    if (err != 0) {
       printf("Error in Nfft4GPLanczosQuadratureLogdet\n");
       return err;
+   }
+   if (dist_final_check(cb)) {
+      free(L2_grad);
+      return -1;
    }
    loss[0] = 0.5 * (L1 + L2 + log(2.0 * 3.1415926535897932384626));
    for (int i = 0; i < 3; i++) {

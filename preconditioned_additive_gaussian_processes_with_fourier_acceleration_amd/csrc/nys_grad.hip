@@ -32,6 +32,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <set>
+#include <sys/time.h>
 #include <vector>
 
 #include "callbacks.hpp"
@@ -155,6 +158,97 @@ struct PrecondNysAmd {
    NysDev* dev = nullptr;
 };
 
+// handles of Nfft4GPAmdPrecondNysCreate, so Nfft4GPPrecondNysSolve can tell them from a reference precond_nys
+std::mutex g_amd_nys_mu;
+std::set<const void*> g_amd_nys;
+
+bool amd_nys_handle(const void* p)
+{
+   std::lock_guard<std::mutex> g(g_amd_nys_mu);
+   return g_amd_nys.count(p) != 0;
+}
+
+// HBM mirrors of reference precond_nys structs (nys.h:24-55) for Nfft4GPPrecondNysSolve.  The key is every
+// field the apply reads plus _tset (written by each setup, nys.c:657) and a fingerprint of the factors' values
+// (all of s, a strided sample of U and perm), so a re-setup into the same allocations is seen.
+struct NysMirror {
+   const void* owner = nullptr;
+   const double *U = nullptr, *s = nullptr;
+   const int* perm = nullptr;
+   int n = 0, k = 0;
+   double eta = 0.0, tset = 0.0;
+   uint64_t print = 0;
+   NysDev* dev = nullptr;
+   uint64_t used = 0;
+};
+std::mutex g_mirror_mu;
+NysMirror g_mirror[2];
+uint64_t g_mirror_clock = 0;
+
+uint64_t fnv(uint64_t h, const void* p, size_t bytes)
+{
+   const unsigned char* c = (const unsigned char*)p;
+   for (size_t i = 0; i < bytes; i++) h = (h ^ c[i]) * 1099511628211ull;
+   return h;
+}
+
+uint64_t nys_fingerprint(const precond_nys* R)
+{
+   uint64_t h = 14695981039346656037ull;
+   h = fnv(h, R->_s, sizeof(double) * (size_t)R->_k);
+   const size_t nk = (size_t)R->_n * R->_k;
+   const size_t stride = std::max<size_t>(1, nk / 257);
+   for (size_t i = 0; i < nk; i += stride) h = fnv(h, R->_U + i, sizeof(double));
+   h = fnv(h, R->_U + nk - 1, sizeof(double));
+   if (R->_perm) {
+      const size_t ps = std::max<size_t>(1, (size_t)R->_n / 64);
+      for (size_t i = 0; i < (size_t)R->_n; i += ps) h = fnv(h, R->_perm + i, sizeof(int));
+   }
+   return h;
+}
+
+// the mirror of R (built or rebuilt as needed); nullptr with a message on failure.  Caller holds g_mirror_mu.
+NysDev* nys_mirror(const precond_nys* R)
+{
+   const uint64_t print = nys_fingerprint(R);
+   NysMirror* hit = nullptr;
+   for (NysMirror& m : g_mirror)
+      if (m.owner == R) hit = &m;
+   if (hit && hit->dev && hit->U == R->_U && hit->s == R->_s && hit->perm == R->_perm && hit->n == R->_n &&
+       hit->k == R->_k && hit->eta == R->_eta && hit->tset == R->_tset && hit->print == print) {
+      hit->used = ++g_mirror_clock;
+      return hit->dev;
+   }
+   if (!hit) {  // least recently used slot
+      hit = &g_mirror[0];
+      for (NysMirror& m : g_mirror)
+         if (m.used < hit->used) hit = &m;
+   }
+   nys_free(hit->dev);
+   *hit = NysMirror();
+   NysDev* D = (NysDev*)Nfft4GPAmdNysCreate(R->_n, R->_k, R->_U, R->_s, R->_eta, R->_perm);
+   if (!D) return nullptr;
+   hit->owner = R;
+   hit->U = R->_U;
+   hit->s = R->_s;
+   hit->perm = R->_perm;
+   hit->n = R->_n;
+   hit->k = R->_k;
+   hit->eta = R->_eta;
+   hit->tset = R->_tset;
+   hit->print = print;
+   hit->dev = D;
+   hit->used = ++g_mirror_clock;
+   return D;
+}
+
+double wtime()
+{
+   struct timeval t;
+   gettimeofday(&t, nullptr);
+   return (double)t.tv_sec + 1e-6 * (double)t.tv_usec;
+}
+
 int dvp_dev(NysDev* N, const int* mask, const double* x, double* y, bool nosolve, hipStream_t s)
 {
    const int n = N->n, k = N->k;
@@ -270,7 +364,13 @@ int trace_dev(NysDev* N, double* traces, hipStream_t s)
 
 extern "C" {
 
-void* Nfft4GPAmdPrecondNysCreate(void) { return new PrecondNysAmd(); }
+void* Nfft4GPAmdPrecondNysCreate(void)
+{
+   PrecondNysAmd* P = new PrecondNysAmd();
+   std::lock_guard<std::mutex> g(g_amd_nys_mu);
+   g_amd_nys.insert(P);
+   return P;
+}
 
 void Nfft4GPAmdPrecondNysSetRank(void* str, int k)
 {
@@ -304,6 +404,10 @@ void Nfft4GPAmdPrecondNysFree(void* str)
    if (!P) return;
    nys_free(P->dev);
    if (P->own_perm) free(P->perm);
+   {
+      std::lock_guard<std::mutex> g(g_amd_nys_mu);
+      g_amd_nys.erase(P);
+   }
    delete P;
 }
 
@@ -343,6 +447,50 @@ int Nfft4GPAmdPrecondNysSolve(void* vnys_mat, int n, double* x, double* rhs)
    PrecondNysAmd* P = (PrecondNysAmd*)vnys_mat;
    if (!P || !P->dev) return -1;
    return Nfft4GPAmdNysSolve(P->dev, n, x, rhs);
+}
+
+int Nfft4GPPrecondNysSolve(void* vnys_mat, int n, double* x, double* rhs)
+{
+   if (amd_nys_handle(vnys_mat)) return Nfft4GPAmdPrecondNysSolve(vnys_mat, n, x, rhs);
+   precond_nys* R = (precond_nys*)vnys_mat;
+   if (!R || !need_device("Nfft4GPPrecondNysSolve")) return -1;
+   if (R->_n <= 0 || R->_k < 0 || R->_k > R->_n || (R->_k > 0 && (!R->_U || !R->_s)) || !(R->_eta != 0.0)) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPPrecondNysSolve: the precond_nys is not set up (n = %d, k = %d)\n",
+              R->_n, R->_k);
+      return -1;
+   }
+   const double ts = wtime();
+   int rc;
+   if (R->_k == 0) {  // nys.c:137-150 with no columns: x = rhs / eta (in place of the permuted copy)
+      Vec vx, vr;
+      if (vx.open(x, R->_n, false) || vr.open(rhs, R->_n, true)) return -1;
+      hipStream_t s = current_stream();
+      NFFT4GP_HIP_CHECK(hipMemcpyAsync(vx.d, vr.d, sizeof(double) * R->_n, hipMemcpyDeviceToDevice, s));
+      Nfft4GPVecScale(vx.d, (size_t)R->_n, 1.0 / R->_eta);
+      vr.close(false);
+      vx.close(true);
+      rc = 0;
+   } else {
+      std::lock_guard<std::mutex> g(g_mirror_mu);
+      NysDev* D = nys_mirror(R);
+      rc = D ? Nfft4GPAmdNysSolve(D, R->_n, x, rhs) : -1;
+   }
+   (void)n;
+   R->_titt += wtime() - ts;  // nys.c:166-170
+   R->_tits++;
+   return rc;
+}
+
+int Nfft4GPAmdPrecondNysMirrorRelease(void* vnys_mat)
+{
+   std::lock_guard<std::mutex> g(g_mirror_mu);
+   for (NysMirror& m : g_mirror)
+      if (m.owner == vnys_mat && m.dev) {
+         nys_free(m.dev);
+         m = NysMirror();
+         return 0;
+      }
+   return 0;
 }
 
 int Nfft4GPAmdPrecondNysDvp(void* vnys_mat, int n, int* mask, double* x, double** yp)

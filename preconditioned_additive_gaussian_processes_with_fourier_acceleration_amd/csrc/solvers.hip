@@ -1004,6 +1004,11 @@ int Nfft4GPSolverPcg(void* mat_data, int n, func_symmatvec matvec, void* prec_da
       cleanup(false);
       return -1;
    }
+   if (dist_final_check(cb)) {
+      free(rel_res_v);
+      cleanup(false);
+      return -1;
+   }
    *prel_res = normr2 / normb;
    *piter = iter;
    *prel_res_v = rel_res_v;
@@ -1099,7 +1104,7 @@ bool library_operator(const void* fn)
           fn == (const void*)&Nfft4GPAmdPrecondNysDvp || fn == (const void*)&Nfft4GPAmdPrecondFsaiSolve ||
           fn == (const void*)&Nfft4GPAmdPrecondFsaiDvp || fn == (const void*)&Nfft4GPAmdDistMatSymv ||
           fn == (const void*)&Nfft4GPAmdDistGradMatSymv || fn == (const void*)&Nfft4GPAmdDistNysSolve ||
-          fn == (const void*)&Nfft4GPAmdDistAfnSolve ||
+          fn == (const void*)&Nfft4GPAmdDistAfnSolve || fn == (const void*)&Nfft4GPPrecondNysSolve ||
           fn == (const void*)&Nfft4GPAmdPrecondAFNSolve || fn == (const void*)&Nfft4GPAmdPrecondAFNDvp;
 }
 }  // namespace nfft4gp_amd

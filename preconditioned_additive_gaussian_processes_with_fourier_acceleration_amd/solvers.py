@@ -102,6 +102,32 @@ class NystromPrecond:
             pass
 
 
+class ReferenceNystrom:
+    """A precond_nys built by the reference's own Nfft4GPPrecondNysSetupWithKernel (nys.c:518-660), applied
+    on the GPU through this library's Nfft4GPPrecondNysSolve (the reference's name, nys.c:115-173), which
+    reads the struct's _n, _k, _perm, _eta, _U, _s (nys.h:24-55) and mirrors the factors into HBM once.
+    ``ptr`` is the struct's address; the struct stays the caller's."""
+
+    def __init__(self, ptr: int, n: int):
+        self.h, self.n = int(ptr), int(n)
+
+    def solve(self, x, rhs):
+        _check_len("x", x, self.n)
+        _check_len("rhs", rhs, self.n)
+        if _lib.lib().Nfft4GPPrecondNysSolve(self.h, self.n, _ptr(x)[0], _ptr(rhs)[0]):
+            raise RuntimeError("Nfft4GPPrecondNysSolve failed")
+        return x
+
+    @property
+    def solve_fnptr(self) -> int:
+        return _lib.fnptr("Nfft4GPPrecondNysSolve")
+
+    def free(self):
+        """drop the HBM mirror (the struct itself is the reference's to free)"""
+        if self.h:
+            _lib.lib().Nfft4GPAmdPrecondNysMirrorRelease(self.h)
+
+
 class _Apply:
     """Common part of the HBM-resident preconditioner handles (func_solve + free)."""
 

@@ -1,5 +1,5 @@
-/* struct_offsets.c -- offsetof / sizeof of every field of nfft4gp_kernel (SRC/linearalg/kernels.h:65-95) and
- * str_adj (INC/_external.h:28-51).  Compiled twice by tests/test_dropin.py: once against the reference's
+/* struct_offsets.c -- offsetof / sizeof of every field of nfft4gp_kernel (SRC/linearalg/kernels.h:65-95),
+ * str_adj (INC/_external.h:28-51) and precond_nys (SRC/preconds/nys.h:24-55).  Compiled twice by tests/test_dropin.py: once against the reference's
  * own declarations (-DUSE_REF, /root/reference in this container) and once against include/nfft4gp_amd.h;
  * the two outputs must be identical. */
 #include <stddef.h>
@@ -10,6 +10,7 @@
  * extracts the struct's text from it into a scratch ref_str_adj.h at run time */
 typedef struct fastsum_plan_ fastsum_plan;
 #include "ref_str_adj.h"
+#include "nys.h" /* SRC/preconds */
 #else
 #include "nfft4gp_amd.h"
 #endif
@@ -51,5 +52,27 @@ int main(void)
    F(str_adj, _kernel_scale);
    F(str_adj, _fastsum_original);
    F(str_adj, _fastsum_derivative);
+   printf("precond_nys %zu\n", sizeof(precond_nys));
+   F(precond_nys, _k_setup);
+   F(precond_nys, _own_perm);
+   F(precond_nys, _perm);
+   F(precond_nys, _n);
+   F(precond_nys, _tits);
+   F(precond_nys, _titt);
+   F(precond_nys, _tset);
+   F(precond_nys, _tlogdet);
+   F(precond_nys, _tdvp);
+   F(precond_nys, _nys_opt);
+   F(precond_nys, _k);
+   F(precond_nys, _eta);
+   F(precond_nys, _f2);
+   F(precond_nys, _U);
+   F(precond_nys, _s);
+   F(precond_nys, _work);
+   F(precond_nys, _K);
+   F(precond_nys, _dU);
+   F(precond_nys, _dK);
+   F(precond_nys, _chol_K11);
+   F(precond_nys, _dvp_nosolve);
    return 0;
 }

@@ -61,14 +61,15 @@ def test_struct_layouts_equal_the_reference(tmp_path):
     (tmp_path / "ref_str_adj.h").write_text(m.group(0) + "\n")
     ref = tmp_path / "ref_off"
     ours = tmp_path / "amd_off"
-    _cc(["gcc", "-std=gnu11", "-fopenmp", "-DUSE_REF", f"-I{REFERENCE}/SRC/linearalg", f"-I{tmp_path}",
+    _cc(["gcc", "-std=gnu11", "-fopenmp", "-DUSE_REF", f"-I{REFERENCE}/SRC/linearalg",
+         f"-I{REFERENCE}/SRC/preconds", f"-I{tmp_path}",
          os.path.join(SRC, "struct_offsets.c"), "-o", str(ref)])
     _cc(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{ROOT}/include", os.path.join(SRC, "struct_offsets.c"), "-o",
          str(ours)])
     a = _cc([str(ref)]).stdout
     b = _cc([str(ours)]).stdout
     assert a == b
-    assert "nfft4gp_kernel 176" in b and len(b.splitlines()) == 34
+    assert "nfft4gp_kernel 176" in b and "precond_nys 144" in b and len(b.splitlines()) == 56
 
 
 def test_exports_are_exactly_the_header_names():
@@ -112,3 +113,65 @@ def test_dropin_driver_runs(tmp_path, amd_first, case):
                        text=True, timeout=240)
     print(r.stdout)
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
+
+
+def build_nys_driver(out_dir, amd_first=True):
+    exe = os.path.join(out_dir, "nys_dropin_" + ("amd_first" if amd_first else "ref_first"))
+    libs = [f"-L{PKG}", "-lnfft4gp_amd", f"-L{REF_DIR}", "-lnfft4gp_ref"]
+    if not amd_first:
+        libs = libs[2:] + libs[:2]
+    _cc(["gcc", "-std=c11", "-O2", "-Wall", "-Werror", f"-I{ROOT}/include", os.path.join(SRC, "nys_dropin.c"),
+         "-o", exe, *libs, f"-Wl,-rpath,{PKG}", f"-Wl,-rpath,{REF_DIR}", "-ldl", "-lm"])
+    return exe
+
+
+@pytest.mark.skipif(not os.path.exists(REF_LIB), reason="oracle/_ref not built")
+def test_nys_dropin_driver_links_in_both_orders(tmp_path):
+    for amd_first in (True, False):
+        exe = build_nys_driver(str(tmp_path), amd_first)
+        syms = _cc(["nm", "-D", "--undefined-only", exe]).stdout
+        assert "Nfft4GPPrecondNysSolve" in syms and "Nfft4GPPrecondNysSetupWithKernel" in syms
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_LIB), reason="oracle/_ref not built")
+def test_nys_solve_under_the_reference_name(tmp_path):
+    """&Nfft4GPPrecondNysSolve on a precond_nys the reference's own
+    Nfft4GPPrecondNysSetupWithKernel built (pcg_synth: dense additive Gaussian, 4 x 1-D windows, n = 1500,
+    l = 0.1, k = 32, the fixture's permutation), handed to Nfft4GPSolverPcg with the reference's dense
+    operator.  Linked amd-first the apply is this library's GPU apply reading the reference's struct: it must
+    equal the reference's own Solve in the same process to 1e-12, the fixture's apply to 1e-10, and the PCG
+    must match pcg_synth's Nystrom run under test_pcg_matches_golden's bounds.  With require_grad the
+    reference's Dvp (whose applies, nys.c:289/:312, then reach this library's Solve) must equal the ref-first
+    run's to 1e-10."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "pcg_synth.npz"), allow_pickle=False)
+    X = np.asfortranarray(z["X"])
+    n, d = X.shape
+    k = int(z["nys_k"])
+    X.ravel(order="F").tofile(str(tmp_path / "X.bin"))
+    np.asarray(z["b"], np.float64).tofile(str(tmp_path / "b.bin"))
+    np.asarray(z["nys_perm"], np.int32).tofile(str(tmp_path / "perm.bin"))
+    np.asarray(z["nys_rhs"], np.float64).tofile(str(tmp_path / "rhs.bin"))
+    res = {}
+    for amd_first in (True, False):
+        exe = build_nys_driver(str(tmp_path), amd_first)
+        r = subprocess.run([exe, str(tmp_path), str(n), str(d), str(k), str(float(z["f"])), str(float(z["l"])),
+                            str(float(z["mu"])), "1"], capture_output=True, text=True, timeout=240)
+        print(r.stdout, r.stderr)
+        assert r.returncode == 0 and "DONE" in r.stdout, (r.returncode, r.stdout + r.stderr)
+        lib = "libnfft4gp_amd.so" if amd_first else "libnfft4gp_ref.so"
+        assert f"Nfft4GPPrecondNysSolve from {lib}" in r.stdout
+        res[amd_first] = np.fromfile(str(tmp_path / "out.bin"), dtype=np.float64)
+    rel = lambda a, b: np.linalg.norm(a - b) / np.linalg.norm(b)  # noqa: E731
+    for amd_first, o in res.items():
+        apply_, apply_ref, x = o[:n], o[n:2 * n], o[2 * n:3 * n]
+        iters, relres, tits = int(o[3 * n]), o[3 * n + 1], int(o[3 * n + 2])
+        assert rel(apply_, apply_ref) <= 1e-12
+        assert rel(apply_, z["nys_out"]) <= 1e-10
+        it_ref = int(z["pcgnys_iters"])
+        assert iters > 0 and abs(iters - it_ref) <= max(2, it_ref // 20), (amd_first, iters, it_ref)
+        assert relres <= 1e-6 and rel(x, z["pcgnys_x"]) < 1e-5
+        assert tits >= iters  # every PCG iteration applied the preconditioner through the drop-in name
+    dvp_amd, dvp_ref = res[True][3 * n + 3:6 * n + 3], res[False][3 * n + 3:6 * n + 3]
+    assert np.all(np.isfinite(dvp_ref)) and np.linalg.norm(dvp_ref) > 0
+    assert rel(dvp_amd, dvp_ref) <= 1e-10

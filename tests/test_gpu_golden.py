@@ -141,6 +141,58 @@ def test_pcg_host_vectors_with_reference_operator(torch_cuda):
     assert rel(x, z["pcg_x"]) < 1e-5
 
 
+def test_reference_nys_struct_through_the_reference_name(torch_cuda):
+    """Nfft4GPPrecondNysSolve (the reference's name, nys.c:115-173) on the precond_nys the reference's own
+    setup built (oracle/_ref, nys.c:518-660): device and host vectors equal the reference's Solve to 1e-12;
+    PCG with it matches pcg_synth's Nystrom run; a re-setup of the same struct at another l is seen (the
+    HBM mirror is rebuilt, not reused) and k = 0 gives rhs / eta."""
+    torch = torch_cuda
+    import oracle as O
+    if not O.ref_available():
+        pytest.skip("oracle/_ref not built")
+    z = load("pcg_synth")
+    dense = O.RefDenseAdditive(np.asarray(z["X"]), np.asarray(z["windows"], np.int32), int(z["nw"]), int(z["dw"]))
+    nys = O.RefNystrom(dense, float(z["f"]), float(z["l"]), float(z["mu"]), int(z["nys_k"]), z["nys_perm"])
+    pre = amd.ReferenceNystrom(nys.h, nys.n)
+    r = np.asarray(z["nys_rhs"])
+    want = nys.solve(np.zeros(nys.n), r.copy())
+    assert rel(want, z["nys_out"]) <= 1e-12
+    xd = torch.zeros(r.size, dtype=torch.float64, device="cuda")
+    pre.solve(xd, torch.tensor(r, device="cuda"))
+    assert rel(xd.cpu().numpy(), want) <= 1e-12
+    xh = np.zeros(r.size)
+    pre.solve(xh, r.copy())
+    assert rel(xh, want) <= 1e-12
+    tits = nys.st._tits
+    op = RefDenseOp(z)
+    b = torch.tensor(np.asarray(z["b"]), device="cuda")
+    x = torch.zeros(op.n, dtype=torch.float64, device="cuda")
+    x, rr, hist, it = amd.pcg(op, b, x, maxits=1000, tol=1e-6, precond=pre)
+    it_ref = int(z["pcgnys_iters"])
+    assert it > 0 and abs(it - it_ref) <= max(2, it_ref // 20), (it, it_ref)
+    assert rr <= 1e-6 and rel(x.cpu().numpy(), z["pcgnys_x"]) < 1e-5
+    assert nys.st._tits - tits >= it  # _tits counts the applies (nys.c:170)
+    # Reset + re-setup of the same struct (the loss's cycle, gp_loss.c:161 / :300; nys.c:76-100, :518-660) at
+    # l = 0.2: new factors, possibly at the same addresses
+    nys.lib.Nfft4GPPrecondNysReset.argtypes = [C.c_void_p]
+    nys.lib.Nfft4GPPrecondNysReset(C.c_void_p(nys.h))
+    dense.st._params[1] = 0.2
+    fk = C.cast(nys.lib.Nfft4GPKernelAdditiveKernel, C.c_void_p)
+    assert nys.lib.Nfft4GPPrecondNysSetupWithKernel(O._d(dense._data), dense.n, dense.n, dense.d, fk, dense.h, 0,
+                                                    nys.h) == 0
+    want2 = nys.solve(np.zeros(nys.n), r.copy())
+    assert rel(want2, want) > 1e-6
+    pre.solve(xd, torch.tensor(r, device="cuda"))
+    assert rel(xd.cpu().numpy(), want2) <= 1e-12
+    # k = 0: x = rhs / eta
+    k_saved = nys.st._k
+    nys.st._k = 0
+    pre.solve(xd, torch.tensor(r, device="cuda"))
+    assert rel(xd.cpu().numpy(), r / nys.st._eta) <= 1e-15
+    nys.st._k = k_saved
+    pre.free()
+
+
 # ---- FSAI (fsai.c:106-123) and AFN (afn.c:82-143) applies ----------------------------------------
 class DenseGaussHostOp(DenseHostOp):
     """func_symmatvec on host vectors for the precond_synth fixture: the reference's dense Gaussian

@@ -361,3 +361,39 @@ def test_fgmres_lucky_breakdown(torch_cuda, ortho):
     assert np.all(np.isfinite(xv)) and np.isfinite(rr)
     assert it == 1 and rr <= 1e-10, (it, rr)
     assert rel(xv, b.cpu().numpy()) <= 1e-14
+
+
+def test_one_launch_sweeps_recover_after_a_wait_gives_up(torch_cuda, case):
+    """after a one-launch sweep's wait gives up (k_mgs_chain in FGMRES, k_lanczos_local in the
+    Lanczos quadrature), that solve fails, and LATER solves in the process must run (as launch chains) and
+    give the clean results.  The fault is injected by setting the kernels' error word, the state a timed-out
+    wait leaves (Nfft4GPAmdDebugChainFault)."""
+    torch = torch_cuda
+    z, k, op = case
+    L = amd.lib()
+    L.Nfft4GPAmdDebugChainFault.restype = C.c_int
+    L.Nfft4GPAmdDebugChainFault.argtypes = [C.c_int]
+    b = torch.tensor(np.asarray(z["b"]), device="cuda")
+    R = np.asarray(k["rademacher"], dtype=np.float64)
+    try:
+        x0, r0, h0, i0 = amd.fgmres(op, b, torch.zeros_like(b), kdim=100, maxits=400, tol=1e-8)
+        v0, g0 = amd.logdet(op, int(k["maxits"]), int(k["nvecs"]), R)
+        assert L.Nfft4GPAmdDebugChainFault(1) == 0
+        with pytest.raises(RuntimeError):
+            amd.fgmres(op, b, torch.zeros_like(b), kdim=100, maxits=400, tol=1e-8)
+        x1, r1, h1, i1 = amd.fgmres(op, b, torch.zeros_like(b), kdim=100, maxits=400, tol=1e-8)
+        assert i1 == i0
+        torch.testing.assert_close(x1, x0, rtol=0, atol=0)  # the k_gs_step chain is bitwise the one-launch sweep
+        v1, g1 = amd.logdet(op, int(k["maxits"]), int(k["nvecs"]), R)  # block_gs in place of the local pass
+        assert v1 == pytest.approx(v0, rel=1e-12)
+        assert L.Nfft4GPAmdDebugChainFault(1) == 1  # the sweeps had been switched off by the FGMRES failure
+        with pytest.raises(RuntimeError):
+            amd.logdet(op, int(k["maxits"]), int(k["nvecs"]), R)
+        v2, g2 = amd.logdet(op, int(k["maxits"]), int(k["nvecs"]), R)
+        assert v2 == pytest.approx(v0, rel=1e-12)
+        np.testing.assert_allclose(g2, g0, rtol=1e-10)
+        x2, _, _, i2 = amd.fgmres(op, b, torch.zeros_like(b), kdim=100, maxits=400, tol=1e-8)
+        assert i2 == i0
+        torch.testing.assert_close(x2, x0, rtol=0, atol=0)
+    finally:
+        L.Nfft4GPAmdDebugChainFault(0)
