@@ -145,6 +145,41 @@ def physical_cores_allowed():
     return len(cores) or len(allowed)
 
 
+def cpu_quota():
+    """CPUs the cgroup's CFS quota grants this process (cgroup v2 cpu.max, else v1 cpu.cfs_quota_us /
+    cpu.cfs_period_us), or None when there is no quota."""
+    paths = []
+    try:
+        with open("/proc/self/cgroup") as fh:
+            for line in fh:
+                parts = line.strip().split(":", 2)
+                if len(parts) == 3 and (parts[1] == "" or "cpu" in parts[1].split(",")):
+                    paths.append((parts[1], parts[2]))
+    except OSError:
+        pass
+    for ctl, rel in paths:
+        if ctl == "":  # v2
+            for base in (os.path.join("/sys/fs/cgroup", rel.lstrip("/")), "/sys/fs/cgroup"):
+                try:
+                    quota, period = open(os.path.join(base, "cpu.max")).read().split()[:2]
+                    if quota != "max":
+                        return float(quota) / float(period)
+                    break
+                except (OSError, ValueError):
+                    continue
+        else:  # v1
+            for base in (os.path.join("/sys/fs/cgroup/cpu", rel.lstrip("/")), "/sys/fs/cgroup/cpu"):
+                try:
+                    quota = int(open(os.path.join(base, "cpu.cfs_quota_us")).read())
+                    period = int(open(os.path.join(base, "cpu.cfs_period_us")).read())
+                    if quota > 0 and period > 0:
+                        return quota / period
+                    break
+                except (OSError, ValueError):
+                    continue
+    return None
+
+
 def cpu_baseline(n, d, threads=16, timeout=600):
     """Oracle (C + OpenMP restatement of nfft_interface.c + NFFT3 fastsum, oracle/nfft4gp_oracle.c, with
     NFFT3's PRE_PSI taps and a 1-D fast path) on this host's cores, in a child process whose OpenMP threads
@@ -154,7 +189,13 @@ def cpu_baseline(n, d, threads=16, timeout=600):
     multi-thread runs (the strongest CPU figure this host gives), with both reported beside it."""
     so = _native_oracle()
     allcores = physical_cores_allowed()
-    counts = [threads] + ([allcores] if allcores != threads else []) + [1]
+    quota = cpu_quota()
+    # never more threads than the CFS quota grants: above it the threads time-share the quota and the run is
+    # slower than fewer threads (round 5's 128-thread leg on a 16-CPU share ran below one thread)
+    cap = max(1, int(quota)) if quota else None
+    share = min(threads, cap) if cap else threads
+    usable = min(allcores, cap) if cap else allcores
+    counts = [share] + ([usable] if usable != share else []) + [1]
     env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores")
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--n", str(n), "--d", str(d),
            "--cpu-threads", ",".join(str(c) for c in counts)] + (["--cpu-oracle-so", so] if so else [])
@@ -168,6 +209,7 @@ def cpu_baseline(n, d, threads=16, timeout=600):
     best = min(multi, key=lambda x: x["median_s"])
     host = host_info()
     host["physical_cores_allowed"] = allcores
+    host["cpu_quota_cpus"] = quota
     host["omp_env"] = {k: env.get(k) for k in ("OMP_NUM_THREADS", "OMP_PROC_BIND", "OMP_PLACES")}
 
     def rec(x):
@@ -184,13 +226,15 @@ def cpu_baseline(n, d, threads=16, timeout=600):
         "min_s": best["min_s"],
         "max_s": best["max_s"],
         "box_share": rec(multi[0]),
-        "all_physical_cores": rec(multi[1]) if len(multi) > 1 else rec(multi[0]),
+        "all_usable_cores": rec(multi[1]) if len(multi) > 1 else rec(multi[0]),
         "one_thread": rec(single),
+        "multi_thread_slower_than_one": any(m["median_s"] > single["median_s"] for m in multi),
         "host": host,
         "sample": f"median of 5-15 timed matvecs of the full workload (n={n}, {d} windows) after one warm-up per "
                   f"thread count, OpenMP threads bound one per physical core (close, cores) in a child process: "
-                  f"{threads} threads (the box's CPU share), {allcores} threads (every physical core of the "
-                  f"affinity mask) and 1; value = the faster multi-thread median; setup (PRE_PSI taps, bhat) "
+                  f"{share} threads (the box's CPU share{', capped by the CFS quota of %.1f CPUs' % quota if quota else ''}), "
+                  f"{usable} threads (the physical cores of the affinity mask, {allcores}, capped by the quota) and 1; "
+                  f"value = the faster multi-thread median; setup (PRE_PSI taps, bhat) "
                   f"{res['setup_s']:.1f}s untimed; -march=native={so is not None}",
     }
 
@@ -282,13 +326,15 @@ def launcher_selftest(fail_rank):
         print(json.dumps({"selftest": True, "world": int(rec["WORLD_SIZE"])}), flush=True)
 
 
-def kernel_only(n, d, nys_rank=0):
+def kernel_only(n, d, nys_rank=0, precision=64):
     """Child mode for the PMC passes: setup + one matvec + a few launches of each kernel (and, with
     nys_rank > 0, one rank-k Nystrom setup for its MFMA GEMM k_gemm_f64)."""
     import torch
     import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
     X, x_host = make_problem(n, d)
     op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    if precision != 64:
+        op.set_precision(precision)
     assert op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) == 0
     xd = torch.tensor(x_host, device="cuda")
     yd = torch.zeros(n, dtype=torch.float64, device="cuda")
@@ -302,7 +348,7 @@ def kernel_only(n, d, nys_rank=0):
     torch.cuda.synchronize()
 
 
-def pmc_traffic(n, d, timeout=600):
+def pmc_traffic(n, d, timeout=600, precision=64):
     """HBM bytes per launch of k_spread / k_interp from rocprofv3 PMC counters, one counter per pass
     (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass), on a child process running --kernel-only.
     FETCH_SIZE is doubled (gfx950 tallies 128-B reads at 64 B, MI355X_MICROARCH.md 'HBM');
@@ -319,7 +365,8 @@ def pmc_traffic(n, d, timeout=600):
         d_out = os.path.join(base, counter.lower())
         shutil.rmtree(d_out, ignore_errors=True)
         cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", d_out, "-o", "pmc", "--",
-               sys.executable, os.path.abspath(__file__), "--kernel-only", "--n", str(n), "--d", str(d)]
+               sys.executable, os.path.abspath(__file__), "--kernel-only", "--n", str(n), "--d", str(d),
+               "--kernel-only-precision", str(precision)]
         r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=timeout)
         if r.returncode != 0:
             return None
@@ -526,6 +573,86 @@ def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000
             key + "_f32_iters": iters32, key + "_f32_rel_res": relres32, key + "_f32_apply_ms": 1e3 * t_apply32}
 
 
+def run_config_e(torch, steps, warmup, traffic=True, n=10_000_000, d=64):
+    """BASELINE configs[4]'s operator on one GPU, under the same clock as the headline: n = 1e7 points, 64 1-D
+    windows (Gaussian f = 1, l = 1, mu = 0.01), the additive matvec with x, y in HBM, out of the 256 MB
+    Infinity Cache (the layout is 2.8-3.5 GB per pass).  Two legs: the fp64 default records and the 32-bit
+    records configs[4] grants (fp32 coordinates, fp64 accumulation; Nfft4GPAmdSetPrecision).  Each leg: pre-warm,
+    W warmup, K timed matvecs between synchronisations, then the same K with dispatch-attached hipEvents for the
+    per-kernel durations, and a roofline for k_spread and k_interp against SURVEY 8(d)'s configs[4] bytes:
+    fp32 coordinates, n (4d + 4) for the spread pass (coordinates + v) and n (4d + 8) for the interpolation pass
+    (coordinates + y written); the PMC HBM bytes per launch beside them."""
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    t0 = time.time()
+    X, x_host = make_problem(n, d)
+    gen_s = time.time() - t0
+    win = np.arange(d, dtype=np.int32)
+    xd = torch.tensor(x_host, device="cuda")
+    yd = torch.zeros(n, dtype=torch.float64, device="cuda")
+    survey = {"spread": n * (4 * d + 4), "interp": n * (4 * d + 8)}
+    out = {"workload": f"BASELINE configs[4] operator on 1 GPU: additive NFFT matvec, n={n}, d={d}, {d} x 1-D windows, "
+                       f"Gaussian f=1 l=1 mu=0.01 (synthetic: numpy PCG64 seed 906)",
+           "n": n, "d": d, "steps": steps, "warmup": warmup, "data_gen_s": gen_s,
+           "survey_bytes_per_matvec": n * (8 * d + 12),
+           "survey_bytes_def": "SURVEY 8(d) configs[4]: n (4*2d + 4 + 8), fp32 coordinates and v, fp64 y"}
+    for bits in (64, 32):
+        t0 = time.time()
+        op = amd.NFFTAdditiveKernel(X, win, d, 1)
+        if bits == 32:
+            op.set_precision(32)
+        if op.setup(amd.GAUSSIAN, f=1.0, l=1.0, mu=0.01) != 0:
+            raise SystemExit("config E setup failed")
+        torch.cuda.synchronize()
+        setup_s = time.time() - t0
+        t_end = time.perf_counter() + 0.5
+        while time.perf_counter() < t_end:
+            for _ in range(20):
+                op.matsymv(xd, 1.0, 0.0, yd)
+            torch.cuda.synchronize()
+        for _ in range(warmup):
+            op.matsymv(xd, 1.0, 0.0, yd)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            op.matsymv(xd, 1.0, 0.0, yd)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        op.timing(True)
+        torch.cuda.synchronize()
+        for _ in range(steps):
+            op.matsymv(xd, 1.0, 0.0, yd)
+        torch.cuda.synchronize()
+        avg = {k: ms / max(c, 1) for k, (ms, c) in op.timing_query().items()}
+        op.timing(False)
+        info = op.layout_info()
+        op.free()
+        pmc = None
+        if traffic:
+            try:
+                pmc = pmc_traffic(n, d, precision=bits)
+            except Exception:
+                pmc = None
+        rl = {}
+        for k in ("spread", "interp"):
+            a = survey[k] / (avg[k] * 1e-3) / 1e9
+            tr = pmc.get(k, {}).get("traffic") if pmc else None
+            rl["k_" + k] = {"bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": a / HBM_PEAK_GBS, "traffic": tr, "algorithmic_bytes_per_launch": survey[k],
+                            "avg_launch_ms": avg[k],
+                            "achieved_pmc": tr / (avg[k] * 1e-3) / 1e9 if tr else None,
+                            "frac_pmc": tr / (avg[k] * 1e-3) / 1e9 / HBM_PEAK_GBS if tr else None}
+        dom = "k_spread" if avg["spread"] >= avg["interp"] else "k_interp"
+        out[f"f{bits}"] = {
+            "value": steps / el, "unit": "matvecs/s", "ms_per_step": 1e3 * el / steps,
+            "frac_of_survey_bytes": out["survey_bytes_per_matvec"] / (el / steps) / 1e9 / HBM_PEAK_GBS,
+            "records": "fp64 default, 5 B per (point, window)" if bits == 64 else
+                       "32-bit records (fp32 coordinates, fp64 accumulation), 4 B per (point, window)",
+            "setup_s": setup_s, "kernels_ms": avg, "layout": info,
+            "roofline": dict(rl[dom], kernel=dom), "roofline_per_kernel": rl,
+            "traffic_unit": "bytes per launch (2 x FETCH_SIZE + WRITE_SIZE)"}
+    return out
+
+
 class _StdoutToStderr:
     """The reference's loss prints progress with printf (gp_loss.c 'Transform ...'); the bench's stdout must
     carry only the JSON line, so C-level stdout goes to stderr inside this block."""
@@ -640,6 +767,11 @@ def main():
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-oracle-so", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--kernel-only-nys", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--kernel-only-precision", type=int, default=64, help=argparse.SUPPRESS)
+    ap.add_argument("--precision", type=int, default=64, choices=[32, 64],
+                    help="N = 1 headline leg: the fp64 records (default) or the 32-bit records (A/B at other sizes)")
+    ap.add_argument("--no-config-e", action="store_true",
+                    help="N = 1: skip the BASELINE configs[4]-size matvec leg (n = 1e7, 64 windows)")
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--launcher-selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     if "--cpu-baseline-child" in sys.argv:  # the child's --cpu-threads is a list "16,1"
@@ -651,7 +783,7 @@ def main():
         return
     args = ap.parse_args()
     if args.kernel_only:
-        kernel_only(args.n, args.d, args.kernel_only_nys)
+        kernel_only(args.n, args.d, args.kernel_only_nys, args.kernel_only_precision)
         return
     mode, nranks = resolve_world(args.gpus)
     if mode == "spawn":
@@ -689,6 +821,8 @@ def main():
     comm = None
     if world == 1:
         op = amd.NFFTAdditiveKernel(X, win, d, 1)
+        if args.precision == 32:
+            op.set_precision(32)
         rb, re = 0, n
     else:
         from preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd.dist import (
@@ -898,7 +1032,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": "f64" if args.precision == 64 else "f32 records, f64 accumulation",
         "data": "synthetic: X ~ U[0,1)^d, x ~ U(-0.5,0.5), numpy PCG64 seed 906",
         "config": {"workload": f"additive NFFT matvec, n={n}, d={d}, {d} x 1-D windows, Gaussian f=1 l=1 "
                                f"mu=0.01 ({cfg_tag})" + (f"; {world} GPUs, {args.partition} sharded" if world > 1 else ""),
@@ -951,6 +1085,8 @@ def main():
         # survey-defined whole-matvec bytes (fp64 coords: 8n(2d+2)) for reference
         result["matvec_bytes_survey_def"] = 8 * n * (2 * d + 2)
         result["pcie_inclusive_matvecs_per_s"] = pcie_rate
+        if not args.no_config_e:
+            result["config_e"] = run_config_e(torch, args.steps, args.warmup, traffic=not args.no_traffic)
         if not args.no_cpu_baseline:
             try:
                 result["cpu_baseline"] = cpu_baseline(n, d, threads=args.cpu_threads)

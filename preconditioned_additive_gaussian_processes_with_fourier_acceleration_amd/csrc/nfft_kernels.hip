@@ -211,7 +211,8 @@ __device__ __forceinline__ uint32_t det_interp_exp(const double* __restrict__ hb
 }
 
 // at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
-template <int THREADS, bool TIMELINE = false, int MOMT = 1, bool DET = false, int REC = 5>
+// PIPE (A/B, NFFT4GP_AMD_SPREAD_VARIANT=3): the next tile's loads issued before the current tile's moments
+template <int THREADS, bool TIMELINE = false, int MOMT = 1, bool DET = false, int REC = 5, bool PIPE = false>
 __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restrict__ meta,
                                                       const uint32_t* __restrict__ lo,
                                                       const uint32_t* __restrict__ qarr,
@@ -240,7 +241,7 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    constexpr int nwaves = THREADS / 64;
 
    // the first run's loads and the alpha slice are in flight together
-   TileRegs cur;
+   TileRegs cur, nxt;
    const int t1 = tile_off[b * ngroups + g + 1];
    int t = tile_off[b * ngroups + g] + wave;
    if (t < t1) load_tile<REC>(cur, meta, lo, qarr, t, lane);
@@ -251,16 +252,21 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces have landed
    __syncthreads();
    if (TIMELINE) stamp(1);
-   // DET: biased exponent of C_0 (C_d: + 31 d), known before the wave's first flush
-   uint32_t bC0 = 0, lcm = 0;
+   // DET: the rounding grids C_d (biased exponent of C_0, + 31 d), wave-uniform, formed once before the runs (the
+   // wait is for the other waves' maxima of the slice, published right after the barrier)
+   double Cd[kNC];
    if (DET) {
       det_max_publish<THREADS>(s_alpha, min(B, n - base), s_red);
       const int cm = cmax[b * ngroups + g];
-      lcm = max(cm > 1 ? 32u - (uint32_t)__clz(cm - 1) : 0u, 6u) + 1u;
+      const uint32_t lcm = max(cm > 1 ? 32u - (uint32_t)__clz(cm - 1) : 0u, 6u) + 1u;
+      const uint32_t bC0 = det_max_wait<THREADS>(s_red) + lcm;
+#pragma unroll
+      for (int d = 0; d < kNC; d++) Cd[d] = det_grid(REC == 4 ? bC0 : bC0 + 31u * d);
    }
 
    const int c0 = g * CG;
    for (; t < t1; t += nwaves) {
+      if (PIPE && t + nwaves < t1) load_tile<REC>(nxt, meta, lo, qarr, t + nwaves, lane);
       double acc[kNC];
       if constexpr (REC == 4) {
          // the 32-bit mode (BASELINE configs[4]: fp32 matvec, fp64 accumulation): a run's moments in fp32, two
@@ -302,14 +308,16 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
       const int comp_local = (int)(cur.mt >> 6) - c0;
       const int cell = (int)(cur.mt & 63u);
       double* dst = s_mom + mom_index<MOMT>(comp_local, cell, 0);
-      if (DET && bC0 == 0) bC0 = det_max_wait<THREADS>(s_red) + lcm;
 #pragma unroll
       for (int d = 0; d < kNC; d++) {
          // (32-bit mode: moments in u, |u| <= 1/2, so one grid for every degree)
-         const double a = DET ? det_round(acc[d], det_grid(REC == 4 ? bC0 : bC0 + 31u * d)) : acc[d];
+         const double a = DET ? det_round(acc[d], Cd[d]) : acc[d];
          atomicAdd(dst + mom_index<MOMT>(0, 0, d), a);  // ds_add_f64
       }
-      if (t + nwaves < t1) load_tile<REC>(cur, meta, lo, qarr, t + nwaves, lane);
+      if (PIPE)
+         cur = nxt;
+      else if (t + nwaves < t1)
+         load_tile<REC>(cur, meta, lo, qarr, t + nwaves, lane);
    }
    __syncthreads();
    if (TIMELINE) stamp(2);
@@ -697,7 +705,10 @@ constexpr int kEpMax = 8;  // epilogue values per thread held in registers (B <=
 // DOT (non-GRAD only): also forms (y_out, x) -- the (q, p) of a CG step when y = A p -- with a
 // deterministic grid-wide sum written to *dot_out by the last block (reduce.hpp)
 // DET: the y adds rounded on the grid of det_interp_exp (hb: the bounds of H, and of Hd at hb + nw)
-template <bool GRAD, int THREADS, bool DOT = false, bool DET = false, int REC = 5>
+// V (A/B variants, NFFT4GP_AMD_INTERP_VARIANT): bit 0 = the next tile's loads issued before the current tile's H
+// loads and Horner (two tile register sets: two tiles in flight per wave); bit 1 = no epilogue x / y prefetch into
+// registers (kEpMax doubles each), so the main loop holds 32 fewer VGPRs
+template <bool GRAD, int THREADS, bool DOT = false, bool DET = false, int REC = 5, int V = 0>
 __global__ __launch_bounds__(THREADS) void k_interp(
     const uint16_t* __restrict__ meta, const uint32_t* __restrict__ lo, const uint32_t* __restrict__ qarr,
     const int* __restrict__ tile_off, const double* __restrict__ H, const double* __restrict__ Hd,
@@ -718,15 +729,17 @@ __global__ __launch_bounds__(THREADS) void k_interp(
    constexpr int nwaves = THREADS / 64;
    const int t0 = tile_off[b * ngroups];
    const int t1 = tile_off[(b + 1) * ngroups];
-   TileRegs cur;
+   constexpr bool PIPE = (V & 1) != 0;
+   constexpr int kEp = (V & 2) ? 1 : kEpMax;
+   TileRegs cur, nxt;
    int t = t0 + wave;
    if (t < t1) load_tile<REC>(cur, meta, lo, qarr, t, lane);
    // the epilogue's x (mu term) and, when beta != 0, y are fetched now, behind the first run
-   const bool ep_regs = B <= kEpMax * THREADS;
-   double xe[kEpMax], ye[kEpMax];
+   const bool ep_regs = !(V & 2) && B <= kEpMax * THREADS;
+   double xe[kEp], ye[kEp];
    if (ep_regs) {
 #pragma unroll
-      for (int k = 0; k < kEpMax; k++) {
+      for (int k = 0; k < kEp; k++) {
          const int j = tid + k * THREADS;
          xe[k] = (j < nloc) ? x[(size_t)base + j] : 0.0;
          ye[k] = (!GRAD && beta != 0.0 && j < nloc) ? y[(size_t)base + j] : 0.0;
@@ -745,6 +758,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
 
    for (; t < t1; t += nwaves) {
       const int tn = t + nwaves;
+      if (PIPE && tn < t1) load_tile<REC>(nxt, meta, lo, qarr, tn, lane);
       const size_t hoff = (size_t)cur.mt * kNC;  // (comp*64 + cell) * kNC: meta is comp<<6|cell
       double hc[kNC], hdc[GRAD ? kNC : 1];
 #pragma unroll
@@ -773,7 +787,10 @@ __global__ __launch_bounds__(THREADS) void k_interp(
             lds_add(off + 8u * (uint32_t)Bp, DET ? det_round(vd, Cyd) : vd);  // s_yd follows it
          }
       }
-      if (tn < t1) load_tile<REC>(cur, meta, lo, qarr, tn, lane);
+      if (PIPE)
+         cur = nxt;
+      else if (tn < t1)
+         load_tile<REC>(cur, meta, lo, qarr, tn, lane);
    }
    __syncthreads();
 
@@ -783,7 +800,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
    double* y1 = y + n;
    double* y2 = y + 2 * (size_t)n;
 #pragma unroll
-   for (int k = 0; k < kEpMax; k++) {
+   for (int k = 0; k < kEp; k++) {
       // registers path: k-th value of this thread; fallback (B > kEpMax*THREADS): strided loop below
       if (!ep_regs) break;
       const int j = tid + k * THREADS;
@@ -991,15 +1008,16 @@ typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, cons
 // spread's tail) were removed in round 4; DESIGN.md 3.5 keeps their numbers.
 constexpr int kSpreadThreads = 512;
 // [record 5 / 4][plain / deterministic][variant]
-static const SpreadFn kSpreadFns[2][2][3] = {
-    {{k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>, k_spread<kSpreadThreads, false, 0>},
+static const SpreadFn kSpreadFns[2][2][4] = {
+    {{k_spread<kSpreadThreads>, k_spread<kSpreadThreads, true>, k_spread<kSpreadThreads, false, 0>,
+      k_spread<kSpreadThreads, false, 1, false, 5, true>},
      {k_spread<kSpreadThreads, false, 1, true>, k_spread<kSpreadThreads, true, 1, true>,
-      k_spread<kSpreadThreads, false, 0, true>}},
+      k_spread<kSpreadThreads, false, 0, true>, k_spread<kSpreadThreads, false, 1, true, 5, true>}},
     {{k_spread<kSpreadThreads, false, 1, false, 4>, k_spread<kSpreadThreads, true, 1, false, 4>,
-      k_spread<kSpreadThreads, false, 0, false, 4>},
+      k_spread<kSpreadThreads, false, 0, false, 4>, k_spread<kSpreadThreads, false, 1, false, 4, true>},
      {k_spread<kSpreadThreads, false, 1, true, 4>, k_spread<kSpreadThreads, true, 1, true, 4>,
-      k_spread<kSpreadThreads, false, 0, true, 4>}}};
-constexpr int kNumSpreadVariants = 3;
+      k_spread<kSpreadThreads, false, 0, true, 4>, k_spread<kSpreadThreads, false, 1, true, 4, true>}}};
+constexpr int kNumSpreadVariants = 4;
 static SpreadFn spread_fn(const AdditivePlan& P)
 {
    const int v = std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1);
@@ -1019,8 +1037,30 @@ static InterpFn interp_fn_t(bool grad, bool dot, bool det)
    if (dot) return det ? k_interp<false, T, true, true, REC> : k_interp<false, T, true, false, REC>;
    return det ? k_interp<false, T, false, true, REC> : k_interp<false, T, false, false, REC>;
 }
+// the plain interpolation's A/B variants (k_interp's V: 1 two tiles in flight, 2 no epilogue prefetch, 3 both)
+template <int T, int REC>
+static InterpFn interp_plain_variant(int v)
+{
+   switch (v) {
+   case 1: return k_interp<false, T, false, false, REC, 1>;
+   case 2: return k_interp<false, T, false, false, REC, 2>;
+   case 3: return k_interp<false, T, false, false, REC, 3>;
+   default: return k_interp<false, T, false, false, REC, 0>;
+   }
+}
+static int interp_variant()
+{
+   static const int v = getenv("NFFT4GP_AMD_INTERP_VARIANT") ? atoi(getenv("NFFT4GP_AMD_INTERP_VARIANT")) & 3 : 0;
+   return v;
+}
 static InterpFn interp_fn(bool grad, bool dot, bool small, bool det, int rec)
 {
+   if (!grad && !dot && !det && interp_variant()) {
+      if (rec == 4) return small ? interp_plain_variant<512, 4>(interp_variant())
+                                 : interp_plain_variant<kInterpThreads, 4>(interp_variant());
+      return small ? interp_plain_variant<512, 5>(interp_variant())
+                   : interp_plain_variant<kInterpThreads, 5>(interp_variant());
+   }
    if (rec == 4) return small ? interp_fn_t<512, 4>(grad, dot, det) : interp_fn_t<kInterpThreads, 4>(grad, dot, det);
    return small ? interp_fn_t<512, 5>(grad, dot, det) : interp_fn_t<kInterpThreads, 5>(grad, dot, det);
 }

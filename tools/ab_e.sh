@@ -1,0 +1,16 @@
+# A/B of environment settings on BASELINE configs[4]'s operator (n = 1e7, 64 1-D windows) in both record
+# precisions and on config C, one box, two reps:
+#   bash tools/ab_e.sh "NFFT4GP_AMD_INTERP_VARIANT=0 NFFT4GP_AMD_INTERP_VARIANT=2"
+set -o pipefail
+mkdir -p gpurun_out
+SETS="$1"; shift
+for rep in 1 2; do
+  for cfg in "--n 10000000 --d 64 --steps 100 --precision 32" "--n 10000000 --d 64 --steps 100" "--steps 500"; do
+    i=0
+    for kv in $SETS; do
+      i=$((i+1))
+      env $(echo "$kv" | tr ',' ' ') timeout -k 10 300 python bench.py --no-cpu-baseline --no-traffic --no-pcg --no-config-e $cfg "$@" > gpurun_out/abe_$i.json 2> gpurun_out/abe_$i.err || { echo BENCH_FAIL $kv $cfg; tail -20 gpurun_out/abe_$i.err; exit 1; }
+      python -c "import json;d=json.load(open('gpurun_out/abe_$i.json'));print('$kv [$cfg] rep $rep', round(d['ms_per_step']*1e3,1), {k:round(x*1e3,2) for k,x in d['kernels_ms'].items()})"
+    done
+  done
+done

@@ -8,7 +8,7 @@ for rep in 1 2; do
   i=0
   for kv in $SETS; do
     i=$((i+1))
-    env $(echo "$kv" | tr ',' ' ') timeout -k 10 300 python bench.py --no-cpu-baseline --no-traffic --no-pcg "$@" > gpurun_out/ab_$i.json 2> gpurun_out/ab_$i.err || { echo BENCH_FAIL $kv; tail -20 gpurun_out/ab_$i.err; exit 1; }
+    env $(echo "$kv" | tr ',' ' ') timeout -k 10 300 python bench.py --no-cpu-baseline --no-traffic --no-pcg --no-config-e "$@" > gpurun_out/ab_$i.json 2> gpurun_out/ab_$i.err || { echo BENCH_FAIL $kv; tail -20 gpurun_out/ab_$i.err; exit 1; }
     python -c "import json;d=json.load(open('gpurun_out/ab_$i.json'));print('$kv rep $rep', round(d['ms_per_step']*1e3,1), {k:round(x*1e3,2) for k,x in d['kernels_ms'].items()})"
   done
 done
