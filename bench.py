@@ -725,18 +725,22 @@ def peer_enable_verified(op, xd, dist):
     y_ref = op.matsymv(xd).clone()
     if not op.enable_peer():
         return {"enabled": False, "reason": "Nfft4GPAmdDistPeerEnable refused (a rank could not export or open)"}
-    ok, rel = True, None
+    ok, rel, err = True, None, None
     try:
         y_p = op.matsymv(xd)
+        op.check()
         rel = float(torch.linalg.norm(y_p - y_ref) / torch.linalg.norm(y_ref))
-    except RuntimeError:
-        ok = False
+    except RuntimeError as e:
+        ok, err = False, str(e)
     t = torch.tensor([rel if rel is not None else float("inf")], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     rel = float(t.item())
     if not agree(ok) or not rel <= 1e-12:
-        op.disable_peer()
-        return {"enabled": True, "verified": False, "max_rel_diff_vs_allreduce": rel}
+        # the exchange opened on every rank but its matvec timed out or differs from the all-reduce's: that is a
+        # defect, not a configuration the bench may quietly route around
+        raise SystemExit(f"bench: the peer-memory exchange failed its check on rank {int(os.environ.get('RANK', 0))}: "
+                         f"{'timed out (' + err + ')' if err else 'matvec differs from the all-reduce by %.3g' % rel}; "
+                         f"rerun with --no-peer to measure the all-reduce path")
     return {"enabled": True, "verified": True, "max_rel_diff_vs_allreduce": rel,
             "how": "rank-order sum of every rank's IPC-shared grid slots inside the grid kernel (dist.hip), no "
                    "all-reduce; 16 KB of epoch-stamped words read per rank"}
@@ -977,6 +981,8 @@ def main():
     # per-kernel durations of the roofline
     elapsed, _ = timed(False)
     elapsed_inst, kern_avg = timed(True)
+    if peer is not None and peer.get("verified"):
+        op.check()  # a peer wait that gave up in the timed steps fails the bench (raises), loudly
     per_rank = rank_times(kern_avg, elapsed_inst) if world > 1 else None
     rows_allreduce = None
     if peer is not None and peer.get("verified"):

@@ -181,6 +181,7 @@ _SIGS = {
     "Nfft4GPAmdDistPeerEnable": (C.c_int, [vp]),
     "Nfft4GPAmdDistPeerActive": (C.c_int, [vp]),
     "Nfft4GPAmdDistPeerDisable": (C.c_int, [vp]),
+    "Nfft4GPAmdDistCheck": (C.c_int, [vp]),
     "Nfft4GPAmdSetFgmresOrtho": (None, [C.c_int]),
     "Nfft4GPAmdFgmresSecondPasses": (C.c_longlong, []),
     "Nfft4GPAmdDistGradMatSymv": (C.c_int, [vp, C.c_int, C.c_double, vp, C.c_double, vp]),

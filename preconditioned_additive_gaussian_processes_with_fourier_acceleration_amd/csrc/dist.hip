@@ -726,8 +726,14 @@ int Nfft4GPAmdDistPeerEnable(void* dop)
    // two grid slots of (low, high) words with the epoch (nfft_kernels.hip), then two scalar slots (k_peer_scalars)
    const size_t bytes = 2 * gcount * 16 + 2 * (size_t)kPeerScal * 16;
    constexpr size_t HB = sizeof(hipIpcMemHandle_t);
-   bool ok = hipMalloc((void**)&P->local, bytes) == hipSuccess && hipMemsetAsync(P->local, 0, bytes, s) == hipSuccess &&
-             hipStreamSynchronize(s) == hipSuccess;
+   // uncached device memory (hipDeviceMallocUncached, MTYPE UC): every store and load of the exchange words, the
+   // owner's and the peers' over xGMI, goes to the owning device's memory, so no cache level of either device can
+   // hold a stale epoch word; the coherence of the exchange then needs no rule about which caches a system-scope
+   // access bypasses on coarse-grained memory.  NFFT4GP_AMD_PEER_CACHED=1: plain hipMalloc (A/B)
+   static const bool cached = getenv("NFFT4GP_AMD_PEER_CACHED") && atoi(getenv("NFFT4GP_AMD_PEER_CACHED")) != 0;
+   bool ok = (cached ? hipMalloc((void**)&P->local, bytes)
+                     : hipExtMallocWithFlags((void**)&P->local, bytes, hipDeviceMallocUncached)) == hipSuccess &&
+             hipMemsetAsync(P->local, 0, bytes, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
    hipIpcMemHandle_t mine;
    memset(&mine, 0, sizeof(mine));
    if (ok && world > 1 && hipIpcGetMemHandle(&mine, P->local) != hipSuccess) {

@@ -210,7 +210,9 @@ struct AdditivePlan {
    // layout
    int B = kMaxBlock, CG = 3, ngroups = 0, nblocks = 0;  // CG = 3: 3 spread workgroups fit a CU's LDS
    int rec = 5;  // layout record: 5 bytes per (point, window) (fp64 default) or 4 (Nfft4GPAmdSetPrecision 32)
-   int spread_variant = 0;  // 0: the spread; 1: the same with timeline stamps; 2: round-4 moment table (A/B)
+   // -1 (auto): 0 or 3 by the layout's size; 0: the spread; 1: the same with timeline stamps; 2: round-4 moment
+   // table (A/B); 3: the next tile loaded before the current one's moments
+   int spread_variant = -1;
    // deterministic 1-D matvec: the spread's moment flushes and the interpolation's y adds are rounded to a grid on
    // which every sum is exact, so results do not depend on the order of the LDS atomics (Nfft4GPAmdSetDeterministic)
    bool det = false;

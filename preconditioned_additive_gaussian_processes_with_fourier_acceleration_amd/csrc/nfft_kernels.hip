@@ -211,7 +211,7 @@ __device__ __forceinline__ uint32_t det_interp_exp(const double* __restrict__ hb
 }
 
 // at most 80 VGPRs, so three 512-thread workgroups (24 waves) share a CU
-// PIPE (A/B, NFFT4GP_AMD_SPREAD_VARIANT=3): the next tile's loads issued before the current tile's moments
+// PIPE (variant 3, layouts past the Infinity Cache): the next tile's loads issued before the current tile's moments
 template <int THREADS, bool TIMELINE = false, int MOMT = 1, bool DET = false, int REC = 5, bool PIPE = false>
 __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restrict__ meta,
                                                       const uint32_t* __restrict__ lo,
@@ -759,7 +759,8 @@ __global__ __launch_bounds__(THREADS) void k_interp(
    for (; t < t1; t += nwaves) {
       const int tn = t + nwaves;
       if (PIPE && tn < t1) load_tile<REC>(nxt, meta, lo, qarr, tn, lane);
-      const size_t hoff = (size_t)cur.mt * kNC;  // (comp*64 + cell) * kNC: meta is comp<<6|cell
+      // (V & 16: timing probe only, wrong sums: every run reads window 0's H, 4 KB that stay in L1)
+      const size_t hoff = (size_t)((V & 16) ? (cur.mt & 63u) : cur.mt) * kNC;  // (comp*64 + cell) * kNC
       double hc[kNC], hdc[GRAD ? kNC : 1];
 #pragma unroll
       for (int d = 0; d < kNC; d += 2) {
@@ -779,7 +780,14 @@ __global__ __launch_bounds__(THREADS) void k_interp(
          double v = hc[kNC - 1];
 #pragma unroll
          for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
-         lds_add(off, DET ? det_round(v, Cy) : v);  // s_y is the first dynamic slice
+         if (V & 4)  // timing probe only (wrong sums): a plain ds_write_b64 in place of the atomic
+            *lds_at(off) = v;
+         else if (V & 8)  // timing probe only (wrong sums): ds_add_u64 of the double's bits
+            (void)__hip_atomic_fetch_add((__attribute__((address_space(3))) unsigned long long*)(size_t)off,
+                                         (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+         else
+            lds_add(off, DET ? det_round(v, Cy) : v);  // s_y is the first dynamic slice
          if (GRAD) {
             double vd = hdc[kNC - 1];
 #pragma unroll
@@ -1018,9 +1026,15 @@ static const SpreadFn kSpreadFns[2][2][4] = {
      {k_spread<kSpreadThreads, false, 1, true, 4>, k_spread<kSpreadThreads, true, 1, true, 4>,
       k_spread<kSpreadThreads, false, 0, true, 4>, k_spread<kSpreadThreads, false, 1, true, 4, true>}}};
 constexpr int kNumSpreadVariants = 4;
+// a layout past the 256 MB Infinity Cache streams from HBM: the spread then loads each wave's next tile before the
+// current tile's moments (variant 3; E32 606 -> 584 us, E64 739 -> 719), which costs 1.8 % on a cache-resident
+// layout (config C, 175 MB), so the choice follows the layout's size (profiles/r06_matvec_variants_ab.txt)
+constexpr size_t kInfinityCacheBytes = 256ull << 20;
 static SpreadFn spread_fn(const AdditivePlan& P)
 {
-   const int v = std::min(std::max(P.spread_variant, 0), kNumSpreadVariants - 1);
+   int v = P.spread_variant;
+   if (v < 0) v = P.dl.bytes > kInfinityCacheBytes ? 3 : 0;
+   v = std::min(v, kNumSpreadVariants - 1);
    return kSpreadFns[P.rec == 4 ? 1 : 0][P.det ? 1 : 0][v];
 }
 
@@ -1045,12 +1059,16 @@ static InterpFn interp_plain_variant(int v)
    case 1: return k_interp<false, T, false, false, REC, 1>;
    case 2: return k_interp<false, T, false, false, REC, 2>;
    case 3: return k_interp<false, T, false, false, REC, 3>;
+   case 4: return k_interp<false, T, false, false, REC, 4>;
+   case 8: return k_interp<false, T, false, false, REC, 8>;
+   case 16: return k_interp<false, T, false, false, REC, 16>;
+   case 17: return k_interp<false, T, false, false, REC, 17>;
    default: return k_interp<false, T, false, false, REC, 0>;
    }
 }
 static int interp_variant()
 {
-   static const int v = getenv("NFFT4GP_AMD_INTERP_VARIANT") ? atoi(getenv("NFFT4GP_AMD_INTERP_VARIANT")) & 3 : 0;
+   static const int v = getenv("NFFT4GP_AMD_INTERP_VARIANT") ? atoi(getenv("NFFT4GP_AMD_INTERP_VARIANT")) & 31 : 0;
    return v;
 }
 static InterpFn interp_fn(bool grad, bool dot, bool small, bool det, int rec)

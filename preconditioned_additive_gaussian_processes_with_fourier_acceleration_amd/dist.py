@@ -225,6 +225,13 @@ class DistributedAdditiveKernel:
         if _lib.lib().Nfft4GPAmdDistPeerDisable(self.h) != 0:
             raise RuntimeError("Nfft4GPAmdDistPeerDisable failed")
 
+    def check(self):
+        """Synchronise and raise if a peer exchange of this operator timed out in the work enqueued so far
+        (Nfft4GPAmdDistCheck): its results are then not to be used."""
+        from . import _lib
+        if _lib.lib().Nfft4GPAmdDistCheck(self.h) != 0:
+            raise RuntimeError("a peer exchange of the distributed operator timed out (Nfft4GPAmdDistCheck)")
+
     @property
     def peer_active(self) -> bool:
         from . import _lib
