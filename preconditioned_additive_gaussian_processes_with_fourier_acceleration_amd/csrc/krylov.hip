@@ -211,6 +211,115 @@ __global__ __launch_bounds__(T) void k_mgs_chain(double* __restrict__ w, const d
    }
 }
 
+// The MGS sweep in ONE launch for vectors too long for k_mgs_chain's one-pass grid (config E, n = 1e7): w stays
+// in registers across the whole sweep -- S strided passes of 4 elements per thread, exactly the elements and the
+// order k_gs_step<1024, 4> visits on the same grid -- while v_{j-1} is re-read for each update instead of being
+// held (w, v_{j-1} and v_j would not fit the register file at this n).  Step j: w -= h_{j-1} v_{j-1}, then
+// (w, v_j) (the last step ||w||^2), summed by reduce.hpp's last arriver and published into the preset hd[j] as
+// k_mgs_chain does (bounded waits, *err).  Per element and per reduction the arithmetic of the per-projection
+// chain on this grid (Ctx::mgs_grid): bitwise equal to it.  Moves 2 vectors per projection against the chain's
+// 4 (w read and written, v_{j-1}, v_j).
+template <int T, int S>
+__global__ __launch_bounds__(T) void k_mgs_wide(double* __restrict__ w, const double* __restrict__ V, size_t n, int i,
+                                                double* __restrict__ hd, double* __restrict__ part,
+                                                unsigned int* __restrict__ ticket, int* __restrict__ err)
+{
+   constexpr int E = 4;
+   __shared__ double s_h;
+   __shared__ int s_fail;
+   // element (p, e) of this thread is c(p, e) + threadIdx.x with c wave-uniform: the loads take a scalar base and
+   // one 32-bit lane offset, so no per-element 64-bit address stays live across the sweep
+   const size_t stride = (size_t)gridDim.x * T * E;
+   const size_t c0 = (size_t)blockIdx.x * T * E;
+   const unsigned tid = threadIdx.x;
+   auto cbase = [&](int p, int e) -> size_t { return c0 + (size_t)p * stride + (size_t)e * T; };
+   double wv[S][E];
+#pragma unroll
+   for (int p = 0; p < S; p++)
+#pragma unroll
+      for (int e = 0; e < E; e++) {
+         const size_t c = cbase(p, e);
+         wv[p][e] = c + tid < n ? (w + c)[tid] : 0.0;
+      }
+   if (threadIdx.x == 0) s_fail = 0;
+   for (int j = 0; j <= i; j++) {
+      const double* u = j > 0 ? V + (size_t)(j - 1) * n : nullptr;
+      const double* v = j < i ? V + (size_t)j * n : nullptr;
+      const double h = j > 0 ? s_h : 0.0;
+      double acc = 0.0;
+#pragma unroll
+      for (int p = 0; p < S; p++) {
+         if (cbase(p, 0) + tid < n) {  // gs_body's grid-stride loop has ended for this thread past here
+            double uv[E], vv[E];
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+               const size_t c = cbase(p, e);
+               const bool in = c + tid < n;
+               uv[e] = (u && in) ? (u + c)[tid] : 0.0;
+               vv[e] = (v && in) ? (v + c)[tid] : 0.0;
+            }
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+               if (u) wv[p][e] = fma(-h, uv[e], wv[p][e]);
+               acc = v ? fma(wv[p][e], vv[e], acc) : fma(wv[p][e], wv[p][e], acc);
+            }
+         }
+         // one pass's 8 loads in flight per thread: hoisting every pass's loads above the arithmetic would need
+         // 16 S VGPRs beside w's 8 S
+         asm volatile("" ::: "memory");
+      }
+      acc = block_sum0<T>(acc);
+      double tot;
+      unsigned long long* slot = reinterpret_cast<unsigned long long*>(hd + j);
+      if (grid_total<T>(acc, part, ticket, &tot)) {
+         if (threadIdx.x == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ticket resets land before the publish
+            __hip_atomic_store(slot, (unsigned long long)__double_as_longlong(tot), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            s_h = tot;
+         }
+      } else if (threadIdx.x == 0) {
+         unsigned long long b = kChainUnset;
+         for (long spin = 0; spin < (1l << 22); spin++) {
+            b = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (b != kChainUnset) break;
+            __builtin_amdgcn_s_sleep(1);
+         }
+         if (b != kChainUnset) {
+            s_h = __longlong_as_double((long long)b);
+         } else {
+            s_fail = 1;
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+         }
+      }
+      __syncthreads();
+      if (s_fail) return;
+   }
+#pragma unroll
+   for (int p = 0; p < S; p++)
+#pragma unroll
+      for (int e = 0; e < E; e++) {
+         const size_t c = cbase(p, e);
+         if (c + tid < n) (w + c)[tid] = wv[p][e];
+      }
+}
+
+// k_mgs_wide's instantiations: passes S per thread
+constexpr int kWideS[] = {2, 4, 6, 8, 10, 12};
+typedef void (*MgsWideFn)(double*, const double*, size_t, int, double*, double*, unsigned int*, int*);
+static MgsWideFn mgs_wide_fn(int S)
+{
+   switch (S) {
+   case 2: return k_mgs_wide<1024, 2>;
+   case 4: return k_mgs_wide<1024, 4>;
+   case 6: return k_mgs_wide<1024, 6>;
+   case 8: return k_mgs_wide<1024, 8>;
+   case 10: return k_mgs_wide<1024, 10>;
+   case 12: return k_mgs_wide<1024, 12>;
+   default: return nullptr;
+   }
+}
+
 // mgs2's local pass in ONE launch (what Ctx::block_gs(w, V + j0 n, Z + j0 n, ml, h, 1) does in three: h[0..ml) =
 // [v_j0, v_j0+1]^T w, h[ml + 1] = ||w||^2 before, w -= Z_loc h, h[ml] = ||w||^2 after).  The ml + 1 grid-wide sums
 // of the first half are reduce.hpp's last-arriver sums (one partials / ticket pair each), published into hd
@@ -740,6 +849,7 @@ struct KScratch {
    int* chain = nullptr;      // k_mgs_chain: [1] error word
    int* hchain_err = nullptr; // pinned read-back of the error word
    int chain_occ = -1;        // resident workgroups of k_mgs_chain per CU x CUs (0: unusable)
+   int wide_occ[6] = {-1, -1, -1, -1, -1, -1};  // the same for k_mgs_wide<1024, kWideS[x]>
    // set once a one-launch sweep's wait has given up in this process: the sweeps then run as launch chains
    // (k_gs_step / block_gs), which cannot wait on other workgroups
    bool chain_off = false;
@@ -809,6 +919,13 @@ struct KScratch {
          if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
              hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_mgs_chain<1024, 4>, 1024, 0) == hipSuccess)
             chain_occ = occ * prop.multiProcessorCount;
+         for (int x = 0; x < 6; x++) {
+            wide_occ[x] = 0;
+            occ = 0;
+            if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mgs_wide_fn(kWideS[x]), 1024, 0) == hipSuccess)
+               wide_occ[x] = occ * prop.multiProcessorCount;
+         }
       }
       return 0;
    }
@@ -826,12 +943,34 @@ struct Ctx {
    {
       return comm ? comm->allreduce(d, (size_t)count, s) : 0;
    }
-   // w -= h u (u optional), *out = (w, v) or ||w||^2
-   int gs(double* w, const double* u, const double* hprev, const double* v, double* out)
+   // the MGS sweep's form for this n (comm == NULL): 0 k_mgs_chain (one pass of 4 elements per thread covers n with
+   // a resident grid), S > 0 k_mgs_wide<1024, S> on *grid workgroups (the smallest S of kWideS whose resident grid
+   // covers n in S passes), -1 neither (the per-projection chain on its usual grid)
+   int mgs_form(unsigned* grid)
+   {
+      *grid = (unsigned)std::max<size_t>(1, std::min<size_t>((n + 4095) / 4096, kKMaxBlocks));
+      if (comm || g_k.ensure_chain()) return -1;
+      if ((size_t)*grid * 4096 >= n && (int)*grid <= g_k.chain_occ) return 0;
+      const char* e = getenv("NFFT4GP_AMD_MGS_WIDE");
+      if (e && atoi(e) == 0) return -1;
+      for (int x = 0; x < 6; x++) {
+         const size_t per = (size_t)kWideS[x] * 4096;
+         const size_t g = (n + per - 1) / per;
+         if (g <= (size_t)g_k.wide_occ[x] && g <= (size_t)kKMaxBlocks) {
+            *grid = (unsigned)g;
+            return kWideS[x];
+         }
+      }
+      return -1;
+   }
+   // w -= h u (u optional), *out = (w, v) or ||w||^2; grid 0: the usual grid, else that many workgroups
+   // (grid-stride over n: the MGS sweep's grid when k_mgs_wide serves this n, so the two forms are bitwise equal)
+   int gs(double* w, const double* u, const double* hprev, const double* v, double* out, unsigned grid_in = 0)
    {
       // 1024 threads x 4 elements: a quarter of the 256-thread partials for the last block to add (8.35 us per
       // projection at n = 1e6 against 9.16; 1024 x 8: 10.7, 512 x 4: 8.49 -- round 3, tools/ab_gs.sh, removed)
-      const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((n + 4095) / 4096, kKMaxBlocks));
+      const unsigned grid =
+          grid_in ? grid_in : (unsigned)std::max<size_t>(1, std::min<size_t>((n + 4095) / 4096, kKMaxBlocks));
       hipLaunchKernelGGL((k_gs_step<1024, 4>), dim3(grid), dim3(1024), 0, s, w, u, hprev, v, n, g_k.part, g_k.ticket,
                          out);
       NFFT4GP_HIP_CHECK(hipGetLastError());
@@ -842,13 +981,18 @@ struct Ctx {
    int mgs_chain(double* w, const double* V, int i, double* hd)
    {
       if (comm || g_k.ensure_chain()) return comm ? 1 : -1;
-      const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((n + 4095) / 4096, kKMaxBlocks));
+      unsigned grid = 0;
+      const int form = mgs_form(&grid);
       const char* e = getenv("NFFT4GP_AMD_MGS_CHAIN");
       const bool off = e && atoi(e) == 0;
-      if (off || g_k.chain_off || (size_t)grid * 4096 < n || (int)grid > g_k.chain_occ) return 1;
+      if (off || g_k.chain_off || form < 0) return 1;
       NFFT4GP_HIP_CHECK(hipMemsetAsync(hd, 0xFF, sizeof(double) * (i + 1), s));  // kChainUnset
-      hipLaunchKernelGGL((k_mgs_chain<1024, 4>), dim3(grid), dim3(1024), 0, s, w, V, n, i, hd, g_k.part, g_k.ticket,
-                         g_k.chain + 1);
+      if (form > 0)
+         hipLaunchKernelGGL(mgs_wide_fn(form), dim3(grid), dim3(1024), 0, s, w, V, n, i, hd, g_k.part, g_k.ticket,
+                            g_k.chain + 1);
+      else
+         hipLaunchKernelGGL((k_mgs_chain<1024, 4>), dim3(grid), dim3(1024), 0, s, w, V, n, i, hd, g_k.part,
+                            g_k.ticket, g_k.chain + 1);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       // the error word comes back with the step's scalars (the caller's read synchronises)
       NFFT4GP_HIP_CHECK(hipMemcpyAsync(g_k.hchain_err, g_k.chain + 1, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1374,11 +1518,14 @@ int fgmres_dev(Callbacks& cb, double* x, const double* rhs, int kdim, int maxits
             const int rc = c.mgs_chain(w, V, i, hd);
             if (rc < 0) return fail();
             if (rc > 0) {
+               // the per-projection chain, on the grid of the one-launch form this n would take (bitwise equal)
+               unsigned mg = 0;
+               if (c.mgs_form(&mg) < 0) mg = 0;
                for (int j = 0; j < i; j++)
                   if (c.gs(w, j ? V + (size_t)(j - 1) * n : nullptr, j ? hd + j - 1 : nullptr, V + (size_t)j * n,
-                           hd + j))
+                           hd + j, mg))
                      return fail();
-               if (c.gs(w, V + (size_t)(i - 1) * n, hd + i - 1, nullptr, hd + i)) return fail();
+               if (c.gs(w, V + (size_t)(i - 1) * n, hd + i - 1, nullptr, hd + i, mg)) return fail();
             }
             if (c.read(hd, i + 1, hcol.data())) return fail();
             if (rc == 0 && c.chain_failed()) return fail();

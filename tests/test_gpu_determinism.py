@@ -94,3 +94,37 @@ def test_fgmres_mgs_sweep_in_one_launch_is_bitwise(torch_cuda, config_c_op, monk
     assert r1 == r2
     np.testing.assert_array_equal(h1, h2)
     assert torch.equal(x1, x2)
+
+
+@pytest.mark.parametrize("n", [1_500_000, 10_000_000], ids=["n1.5e6_S2", "n1e7_S10"])
+def test_fgmres_mgs_sweep_wide_is_bitwise(torch_cuda, monkeypatch, n):
+    """Past k_mgs_chain's one-pass grid (n > ~1e6) the MGS sweep runs as k_mgs_wide: w in registers over S strided
+    passes, v_{j-1} re-read for each update.  Against one k_gs_step launch per projection on the same grid
+    (NFFT4GP_AMD_MGS_CHAIN=0) the same per-element and per-reduction arithmetic: the same bits.  BASELINE
+    configs[4]'s n = 1e7 takes S = 10 passes; 4 windows keep the operator cheap, deterministic mode keeps the two
+    runs' matvecs equal."""
+    torch = torch_cuda
+    rng = np.random.default_rng(909)
+    d = 4
+    X = rng.random((n, d))
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    assert op.setup(amd.GAUSSIAN, f=1.0, l=0.1, mu=0.01) == 0
+    op.set_deterministic(True)
+    amd.lib().Nfft4GPAmdSetFgmresOrtho(0)
+    b = torch.tensor(rng.random(n) - 0.5, device="cuda")
+    runs = []
+    try:
+        for chain in ("1", "0"):
+            monkeypatch.setenv("NFFT4GP_AMD_MGS_CHAIN", chain)
+            x = torch.zeros(n, dtype=torch.float64, device="cuda")
+            _, relres, hist, it = amd.fgmres(op, b, x, kdim=30, maxits=30, tol=1e-14)
+            torch.cuda.synchronize()
+            runs.append((x, relres, np.asarray(hist), it))
+    finally:
+        op.free()
+    (x1, r1, h1, i1), (x2, r2, h2, i2) = runs
+    print(f"n {n}: FGMRES(30) rel res {r1:.6e} / {r2:.6e}")
+    assert i1 == i2 and i1 > 0
+    assert r1 == r2
+    np.testing.assert_array_equal(h1, h2)
+    assert torch.equal(x1, x2)
