@@ -705,10 +705,7 @@ constexpr int kEpMax = 8;  // epilogue values per thread held in registers (B <=
 // DOT (non-GRAD only): also forms (y_out, x) -- the (q, p) of a CG step when y = A p -- with a
 // deterministic grid-wide sum written to *dot_out by the last block (reduce.hpp)
 // DET: the y adds rounded on the grid of det_interp_exp (hb: the bounds of H, and of Hd at hb + nw)
-// V (A/B variants, NFFT4GP_AMD_INTERP_VARIANT): bit 0 = the next tile's loads issued before the current tile's H
-// loads and Horner (two tile register sets: two tiles in flight per wave); bit 1 = no epilogue x / y prefetch into
-// registers (kEpMax doubles each), so the main loop holds 32 fewer VGPRs
-template <bool GRAD, int THREADS, bool DOT = false, bool DET = false, int REC = 5, int V = 0>
+template <bool GRAD, int THREADS, bool DOT = false, bool DET = false, int REC = 5>
 __global__ __launch_bounds__(THREADS) void k_interp(
     const uint16_t* __restrict__ meta, const uint32_t* __restrict__ lo, const uint32_t* __restrict__ qarr,
     const int* __restrict__ tile_off, const double* __restrict__ H, const double* __restrict__ Hd,
@@ -729,17 +726,15 @@ __global__ __launch_bounds__(THREADS) void k_interp(
    constexpr int nwaves = THREADS / 64;
    const int t0 = tile_off[b * ngroups];
    const int t1 = tile_off[(b + 1) * ngroups];
-   constexpr bool PIPE = (V & 1) != 0;
-   constexpr int kEp = (V & 2) ? 1 : kEpMax;
-   TileRegs cur, nxt;
+   TileRegs cur;
    int t = t0 + wave;
    if (t < t1) load_tile<REC>(cur, meta, lo, qarr, t, lane);
    // the epilogue's x (mu term) and, when beta != 0, y are fetched now, behind the first run
-   const bool ep_regs = !(V & 2) && B <= kEpMax * THREADS;
-   double xe[kEp], ye[kEp];
+   const bool ep_regs = B <= kEpMax * THREADS;
+   double xe[kEpMax], ye[kEpMax];
    if (ep_regs) {
 #pragma unroll
-      for (int k = 0; k < kEp; k++) {
+      for (int k = 0; k < kEpMax; k++) {
          const int j = tid + k * THREADS;
          xe[k] = (j < nloc) ? x[(size_t)base + j] : 0.0;
          ye[k] = (!GRAD && beta != 0.0 && j < nloc) ? y[(size_t)base + j] : 0.0;
@@ -758,9 +753,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
 
    for (; t < t1; t += nwaves) {
       const int tn = t + nwaves;
-      if (PIPE && tn < t1) load_tile<REC>(nxt, meta, lo, qarr, tn, lane);
-      // (V & 16: timing probe only, wrong sums: every run reads window 0's H, 4 KB that stay in L1)
-      const size_t hoff = (size_t)((V & 16) ? (cur.mt & 63u) : cur.mt) * kNC;  // (comp*64 + cell) * kNC
+      const size_t hoff = (size_t)cur.mt * kNC;  // (comp*64 + cell) * kNC: meta is comp<<6|cell
       double hc[kNC], hdc[GRAD ? kNC : 1];
 #pragma unroll
       for (int d = 0; d < kNC; d += 2) {
@@ -780,14 +773,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
          double v = hc[kNC - 1];
 #pragma unroll
          for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
-         if (V & 4)  // timing probe only (wrong sums): a plain ds_write_b64 in place of the atomic
-            *lds_at(off) = v;
-         else if (V & 8)  // timing probe only (wrong sums): ds_add_u64 of the double's bits
-            (void)__hip_atomic_fetch_add((__attribute__((address_space(3))) unsigned long long*)(size_t)off,
-                                         (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-         else
-            lds_add(off, DET ? det_round(v, Cy) : v);  // s_y is the first dynamic slice
+         lds_add(off, DET ? det_round(v, Cy) : v);  // s_y is the first dynamic slice
          if (GRAD) {
             double vd = hdc[kNC - 1];
 #pragma unroll
@@ -795,10 +781,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
             lds_add(off + 8u * (uint32_t)Bp, DET ? det_round(vd, Cyd) : vd);  // s_yd follows it
          }
       }
-      if (PIPE)
-         cur = nxt;
-      else if (tn < t1)
-         load_tile<REC>(cur, meta, lo, qarr, tn, lane);
+      if (tn < t1) load_tile<REC>(cur, meta, lo, qarr, tn, lane);
    }
    __syncthreads();
 
@@ -808,7 +791,7 @@ __global__ __launch_bounds__(THREADS) void k_interp(
    double* y1 = y + n;
    double* y2 = y + 2 * (size_t)n;
 #pragma unroll
-   for (int k = 0; k < kEp; k++) {
+   for (int k = 0; k < kEpMax; k++) {
       // registers path: k-th value of this thread; fallback (B > kEpMax*THREADS): strided loop below
       if (!ep_regs) break;
       const int j = tid + k * THREADS;
@@ -871,6 +854,159 @@ __global__ __launch_bounds__(THREADS) void k_interp(
                                 s_scr + THREADS / 64) &&
           threadIdx.x == 0)
          *dot_out = tot;
+   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// the plain interpolation with the window group's H rows staged in LDS
+// ------------------------------------------------------------------------------------------------
+// k_interp gathers each run's 8 coefficients H[comp][cell][0..7] from global memory: 64 B per run from a table of
+// nw x 4 KB that L1 cannot hold beside the layout stream, so at config E the gather costs ~20 % of the kernel (a
+// probe that read one window's 4 KB for every run ran 671 -> 535 us).  Here a workgroup walks its block's tiles
+// group by group (tile_off orders them so) and reads the coefficients from LDS: two slots of CG windows x 64 cells x
+// 8 degrees ([window][degree][cell], windows kHlWin = 513 doubles apart so two windows' even cells fall on
+// different banks).  Groups 0 and 1 are staged by the whole workgroup before the loop; afterwards the LAST wave to
+// leave group g (an LDS counter per group) stages group g + 2 into g's slot and publishes it (ready[slot] = g + 2,
+// release), and a wave entering group g >= 2 waits for that (acquire, s_sleep, bounded).  A wave waits only for a
+// group every wave has left two groups before, and the stager stages before it waits for anything, so the waves
+// never wait on one another in a cycle.  Same arithmetic as k_interp's plain path (bitwise equal results).
+constexpr int kHlWin = kNC * kNos + 1;
+
+__host__ __device__ constexpr size_t hl_lds_bytes(int B, int CG, int ngroups)
+{
+   return sizeof(double) * ((size_t)B + kPad) + sizeof(double) * 2 * (size_t)CG * kHlWin +
+          sizeof(int) * (3 + 2 * (size_t)ngroups);
+}
+
+// one wave stages group g's H rows (windows [g CG, min((g + 1) CG, nw))) into slot `slot` of s_H
+__device__ __forceinline__ void hl_stage_wave(double* s_H, const double* __restrict__ H, int g, int slot, int CG, int nw,
+                                              int lane)
+{
+   const int c0 = g * CG;
+   const int ncomp = min(CG, nw - c0);
+   const double2* src = reinterpret_cast<const double2*>(H + (size_t)c0 * kNos * kNC);
+   double* dst = s_H + (size_t)slot * CG * kHlWin;
+   const int pairs = ncomp * kNos * kNC / 2;
+#pragma unroll 4
+   for (int i = lane; i < pairs; i += 64) {
+      const double2 v = src[i];
+      const int e = 2 * i;                       // element of [cl][cell][d]
+      const int cl = e / (kNos * kNC);
+      const int cell = (e / kNC) & (kNos - 1);
+      const int d = e & (kNC - 1);
+      double* row = dst + cl * kHlWin + cell;
+      row[d * kNos] = v.x;
+      row[(d + 1) * kNos] = v.y;
+   }
+}
+
+template <int THREADS, bool DET = false, int REC = 5>
+__global__ __launch_bounds__(THREADS) void k_interp_hl(const uint16_t* __restrict__ meta, const uint32_t* __restrict__ lo,
+                                                       const uint32_t* __restrict__ qarr, const int* __restrict__ tile_off,
+                                                       const double* __restrict__ H, const double* __restrict__ x,
+                                                       double* __restrict__ y, int n, int B, int ngroups, int CG, int nw,
+                                                       double alpha, double beta, double f, double mu,
+                                                       const double* __restrict__ hb)
+{
+   extern __shared__ __attribute__((aligned(16))) double smem[];
+   const int Bp = B + kPad;
+   double* s_y = smem;  // the first dynamic slice (lds_add addresses it absolutely)
+   double* s_H = smem + Bp;
+   int* s_ready = reinterpret_cast<int*>(s_H + 2 * (size_t)CG * kHlWin);
+   int* s_done = s_ready + 2;
+   int* s_toff = s_done + ngroups;  // the block's group boundaries tile_off[b ngroups .. (b + 1) ngroups]
+   const int b = blockIdx.x;
+   const int tid = threadIdx.x;
+   const int base = b * B;
+   const int nloc = min(B, n - base);
+   const int lane = tid & 63;
+   const int wave = tid >> 6;
+   constexpr int nwaves = THREADS / 64;
+   const int gbase = b * ngroups;
+   const int t0 = tile_off[gbase];
+   const int t1 = tile_off[gbase + ngroups];
+   TileRegs cur;
+   int t = t0 + wave;
+   if (t < t1) load_tile<REC>(cur, meta, lo, qarr, t, lane);
+   const bool ep_regs = B <= kEpMax * THREADS;
+   double xe[kEpMax], ye[kEpMax];
+   if (ep_regs) {
+#pragma unroll
+      for (int k = 0; k < kEpMax; k++) {
+         const int j = tid + k * THREADS;
+         xe[k] = (j < nloc) ? x[(size_t)base + j] : 0.0;
+         ye[k] = (beta != 0.0 && j < nloc) ? y[(size_t)base + j] : 0.0;
+      }
+   }
+   for (int i = tid; i < Bp; i += THREADS) s_y[i] = 0.0;
+   for (int i = tid; i < ngroups; i += THREADS) s_done[i] = 0;
+   for (int i = tid; i <= ngroups; i += THREADS) s_toff[i] = tile_off[gbase + i];
+   if (tid < 2) s_ready[tid] = tid;
+   // groups 0 and 1, one wave each (more waves when there are: every wave w < 2 stages group w)
+   if (wave < 2 && wave < ngroups) hl_stage_wave(s_H, H, wave, wave, CG, nw, lane);
+   const double Cy = DET ? det_grid(det_interp_exp(hb, nw)) : 0.0;
+   __syncthreads();
+
+   int g = 0;
+   int gend = s_toff[1];
+   // wave leaves group gl: count it; the last one stages group gl + 2 into gl's slot and publishes it
+   auto leave = [&](int gl) {
+      int old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(s_done + gl, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+      old = __builtin_amdgcn_readfirstlane(old);
+      if (old == nwaves - 1 && gl + 2 < ngroups) {
+         hl_stage_wave(s_H, H, gl + 2, gl & 1, CG, nw, lane);
+         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+         if (lane == 0) __hip_atomic_store(s_ready + (gl & 1), gl + 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+   };
+   for (; t < t1; t += nwaves) {
+      while (t >= gend) {
+         leave(g);
+         g++;
+         gend = s_toff[g + 1];
+         if (g >= 2) {
+            for (long spin = 0; spin < (1l << 24); spin++) {
+               if (__hip_atomic_load(s_ready + (g & 1), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == g) break;
+               __builtin_amdgcn_s_sleep(1);
+            }
+         }
+      }
+      const int cl = (int)(cur.mt >> 6) - g * CG;
+      const int cell = (int)(cur.mt & 63u);
+      const double* hrow = s_H + ((size_t)(g & 1) * CG + cl) * kHlWin + cell;
+      double hc[kNC];
+#pragma unroll
+      for (int d = 0; d < kNC; d++) hc[d] = hrow[d * kNos];
+#pragma unroll
+      for (int r = 0; r < kR; r++) {
+         const uint32_t off = slot_off<REC>(cur, r);
+         const double u = q_to_s(cur.qq[r]);
+         double v = hc[kNC - 1];
+#pragma unroll
+         for (int d = kNC - 2; d >= 0; d--) v = fma(v, u, hc[d]);
+         lds_add(off, DET ? det_round(v, Cy) : v);
+      }
+      if (t + nwaves < t1) load_tile<REC>(cur, meta, lo, qarr, t + nwaves, lane);
+   }
+   for (; g < ngroups; g++) leave(g);  // the groups this wave has no (more) tiles in
+   __syncthreads();
+
+   const double ff = f * f;
+#pragma unroll
+   for (int k = 0; k < kEpMax; k++) {
+      if (!ep_regs) break;
+      const int j = tid + k * THREADS;
+      if (j >= nloc) break;
+      const double v = ff * (s_y[j] + mu * xe[k]);
+      y[(size_t)base + j] = (beta == 0.0) ? alpha * v : fma(beta, ye[k], alpha * v);
+   }
+   if (!ep_regs) {
+      for (int j = tid; j < nloc; j += THREADS) {
+         const size_t gj = (size_t)base + j;
+         const double v = ff * (s_y[j] + mu * x[gj]);
+         y[gj] = (beta == 0.0) ? alpha * v : fma(beta, y[gj], alpha * v);
+      }
    }
 }
 
@@ -1051,34 +1187,8 @@ static InterpFn interp_fn_t(bool grad, bool dot, bool det)
    if (dot) return det ? k_interp<false, T, true, true, REC> : k_interp<false, T, true, false, REC>;
    return det ? k_interp<false, T, false, true, REC> : k_interp<false, T, false, false, REC>;
 }
-// the plain interpolation's A/B variants (k_interp's V: 1 two tiles in flight, 2 no epilogue prefetch, 3 both)
-template <int T, int REC>
-static InterpFn interp_plain_variant(int v)
-{
-   switch (v) {
-   case 1: return k_interp<false, T, false, false, REC, 1>;
-   case 2: return k_interp<false, T, false, false, REC, 2>;
-   case 3: return k_interp<false, T, false, false, REC, 3>;
-   case 4: return k_interp<false, T, false, false, REC, 4>;
-   case 8: return k_interp<false, T, false, false, REC, 8>;
-   case 16: return k_interp<false, T, false, false, REC, 16>;
-   case 17: return k_interp<false, T, false, false, REC, 17>;
-   default: return k_interp<false, T, false, false, REC, 0>;
-   }
-}
-static int interp_variant()
-{
-   static const int v = getenv("NFFT4GP_AMD_INTERP_VARIANT") ? atoi(getenv("NFFT4GP_AMD_INTERP_VARIANT")) & 31 : 0;
-   return v;
-}
 static InterpFn interp_fn(bool grad, bool dot, bool small, bool det, int rec)
 {
-   if (!grad && !dot && !det && interp_variant()) {
-      if (rec == 4) return small ? interp_plain_variant<512, 4>(interp_variant())
-                                 : interp_plain_variant<kInterpThreads, 4>(interp_variant());
-      return small ? interp_plain_variant<512, 5>(interp_variant())
-                   : interp_plain_variant<kInterpThreads, 5>(interp_variant());
-   }
    if (rec == 4) return small ? interp_fn_t<512, 4>(grad, dot, det) : interp_fn_t<kInterpThreads, 4>(grad, dot, det);
    return small ? interp_fn_t<512, 5>(grad, dot, det) : interp_fn_t<kInterpThreads, 5>(grad, dot, det);
 }
@@ -1110,9 +1220,32 @@ static bool static_lds_zero(const void* fn)
 }
 
 // every interpolation kernel the launchers pick
+typedef void (*InterpHlFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, const double*,
+                           double*, int, int, int, int, int, double, double, double, double, const double*);
+static InterpHlFn interp_hl_fn(bool small, bool det, int rec)
+{
+   if (rec == 4)
+      return small ? (det ? k_interp_hl<512, true, 4> : k_interp_hl<512, false, 4>)
+                   : (det ? k_interp_hl<1024, true, 4> : k_interp_hl<1024, false, 4>);
+   return small ? (det ? k_interp_hl<512, true, 5> : k_interp_hl<512, false, 5>)
+                : (det ? k_interp_hl<1024, true, 5> : k_interp_hl<1024, false, 5>);
+}
+// k_interp_hl for layouts past the Infinity Cache (config E: 785 -> 717 us fp64, 671 -> 652 us in the 32-bit mode);
+// on a cache-resident layout (config C) its one-wave stagings stall the waves, which there run about one tile per
+// group (31 -> 42 us), so k_interp stays.  NFFT4GP_AMD_INTERP_HL=0 / 1 forces either
+// (profiles/r06_matvec_variants_ab.txt)
+static bool interp_hl_on(const AdditivePlan& P)
+{
+   static const int v = getenv("NFFT4GP_AMD_INTERP_HL") ? atoi(getenv("NFFT4GP_AMD_INTERP_HL")) : -1;
+   return v < 0 ? P.dl.bytes > kInfinityCacheBytes : v != 0;
+}
+
 static std::vector<const void*> interp_kernels()
 {
    std::vector<const void*> v;
+   for (int sm = 0; sm < 2; sm++)
+      for (int det = 0; det < 2; det++)
+         for (int rec = 4; rec <= 5; rec++) v.push_back((const void*)interp_hl_fn(sm, det, rec));
    for (int g = 0; g < 2; g++)
       for (int d = 0; d < 2; d++)
          for (int sm = 0; sm < 2; sm++)
@@ -1258,6 +1391,14 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
    // config C; profiles/r04_interp_threads_ab.txt).  NFFT4GP_AMD_INTERP_THREADS=512 / 1024 forces either.
    static const int forced = getenv("NFFT4GP_AMD_INTERP_THREADS") ? atoi(getenv("NFFT4GP_AMD_INTERP_THREADS")) : 0;
    const bool small = forced == 512 || (forced != 1024 && P.nblocks >= 512);
+   if (!grad && !d_dot && interp_hl_on(P) && P.ngroups >= 1) {
+      launch_ev(interp_hl_fn(small, P.det, P.rec), dim3(P.nblocks), dim3(small ? 512 : kInterpThreads),
+                hl_lds_bytes(P.B, P.CG, P.ngroups), stream, P.kev ? P.kev + 4 : nullptr, P.dl.meta, P.dl.lo, P.dl.q,
+                P.dl.tile_off, (const double*)P.d_H, d_x, d_y, P.n, P.B, P.ngroups, P.CG, P.nw, alpha, beta, P.f,
+                P.mu * P.diag, (const double*)P.d_hb);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   }
    const InterpFn fn = interp_fn(grad, d_dot != nullptr, small, P.det, P.rec);
    launch_ev(fn, dim3(P.nblocks), dim3(small ? 512 : kInterpThreads), interp_lds_bytes(P, grad), stream,
              P.kev ? P.kev + 4 : nullptr, P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const double*)P.d_H,
