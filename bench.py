@@ -573,7 +573,7 @@ def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000
             key + "_f32_iters": iters32, key + "_f32_rel_res": relres32, key + "_f32_apply_ms": 1e3 * t_apply32}
 
 
-def run_config_e(torch, steps, warmup, traffic=True, n=10_000_000, d=64):
+def run_config_e(torch, steps, warmup, traffic=True, n=10_000_000, d=64, precisions=(64, 32), tag="configs[4]"):
     """BASELINE configs[4]'s operator on one GPU, under the same clock as the headline: n = 1e7 points, 64 1-D
     windows (Gaussian f = 1, l = 1, mu = 0.01), the additive matvec with x, y in HBM, out of the 256 MB
     Infinity Cache (the layout is 2.8-3.5 GB per pass).  Two legs: the fp64 default records and the 32-bit
@@ -590,12 +590,16 @@ def run_config_e(torch, steps, warmup, traffic=True, n=10_000_000, d=64):
     xd = torch.tensor(x_host, device="cuda")
     yd = torch.zeros(n, dtype=torch.float64, device="cuda")
     survey = {"spread": n * (4 * d + 4), "interp": n * (4 * d + 8)}
-    out = {"workload": f"BASELINE configs[4] operator on 1 GPU: additive NFFT matvec, n={n}, d={d}, {d} x 1-D windows, "
+    out = {"workload": f"BASELINE {tag} operator on 1 GPU: additive NFFT matvec, n={n}, d={d}, {d} x 1-D windows, "
                        f"Gaussian f=1 l=1 mu=0.01 (synthetic: numpy PCG64 seed 906)",
            "n": n, "d": d, "steps": steps, "warmup": warmup, "data_gen_s": gen_s,
            "survey_bytes_per_matvec": n * (8 * d + 12),
-           "survey_bytes_def": "SURVEY 8(d) configs[4]: n (4*2d + 4 + 8), fp32 coordinates and v, fp64 y"}
-    for bits in (64, 32):
+           "survey_bytes_def": "SURVEY 8(d) configs[4]'s form: n (4*2d + 4 + 8), fp32 coordinates and v, fp64 y"}
+    if tag != "configs[4]":  # SURVEY 8(d)'s fp64 form for the fp64 configs: 8 n (d + 1) per pass
+        survey = {"spread": 8 * n * (d + 1), "interp": 8 * n * (d + 1)}
+        out["survey_bytes_per_matvec"] = 8 * n * (2 * d + 2)
+        out["survey_bytes_def"] = "SURVEY 8(d): 8 n (2d + 2), fp64 coordinates and vectors"
+    for bits in precisions:
         t0 = time.time()
         op = amd.NFFTAdditiveKernel(X, win, d, 1)
         if bits == 32:
@@ -1093,6 +1097,9 @@ def main():
         result["pcie_inclusive_matvecs_per_s"] = pcie_rate
         if not args.no_config_e:
             result["config_e"] = run_config_e(torch, args.steps, args.warmup, traffic=not args.no_traffic)
+            # BASELINE configs[1]'s operator (n = 1e5, 8 windows, fp64): cache-resident and launch-bound
+            result["config_b"] = run_config_e(torch, max(args.steps, 200), args.warmup, traffic=False, n=100_000, d=8,
+                                              precisions=(64,), tag="configs[1]")
         if not args.no_cpu_baseline:
             try:
                 result["cpu_baseline"] = cpu_baseline(n, d, threads=args.cpu_threads)
