@@ -229,6 +229,8 @@ struct AdditivePlan {
    double* d_dot_part = nullptr;         // [nblocks] fused matvec-dot partials
    unsigned int* d_dot_ticket = nullptr; // arrival counters (reduce.hpp)
    double* d_part2 = nullptr; // two-vector matvec: both vectors' partial grids [2][nblocks][nw][64]
+   double* d_gsum = nullptr;  // the spread's grids summed by global atomics [nw][64] (launch_spread_grid), zero between
+                              // matvecs (k_grid clears what it read)
    double* d_H2 = nullptr;    // [2][nw][64][kNC]
    double* d_xs = nullptr;    // staging (host pointer calls)
    double* d_ys = nullptr;    // staging 3n
@@ -247,6 +249,9 @@ int upload_tap_coeffs();
 // launchers (nfft_kernels.hip); all enqueue on `stream`
 int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream);
 int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int grad, hipStream_t stream);
+// a whole handle's spread and grid step: the spread's partial grids summed by k_grid in a fixed order, or (not
+// deterministic, few blocks) added by the spread itself into P.d_gsum with global atomics, which k_grid reads and clears
+int launch_spread_grid(AdditivePlan& P, const double* d_x, int grad, hipStream_t stream);
 int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int grad, hipStream_t stream);
 // the peer-memory exchange of the row split (dist.hip, Nfft4GPAmdDistPeerEnable): every rank's buffer holds
 // two grid slots (epoch parity) of slot_doubles entries, each entry two 64-bit words carrying the epoch

@@ -167,6 +167,7 @@ void free_plan(PlanExt* E)
    dfree(P.d_H);
    dfree(P.d_Hd);
    dfree(P.d_hb);
+   dfree(P.d_gsum);
    dfree(P.d_C);
    dfree(P.d_xs);
    dfree(P.d_ys);
@@ -383,12 +384,16 @@ int plan_apply_dev(PlanExt* E, int grad, double alpha, const double* d_x, double
    const bool mdt = P.timing && P.md.on;  // multi-feature windows: events recorded around each launch
    int rc = 0;
    if (mdt) (void)hipEventRecord(rec.ev[0], s);
-   rc = P.md.on ? md_spread(P, d_x, P.md.d_grid, s) : launch_spread(P, d_x, P.d_part, s);
-   if (mdt) {
-      (void)hipEventRecord(rec.ev[1], s);
-      (void)hipEventRecord(rec.ev[2], s);
+   if (P.md.on) {
+      rc = md_spread(P, d_x, P.md.d_grid, s);
+      if (mdt) {
+         (void)hipEventRecord(rec.ev[1], s);
+         (void)hipEventRecord(rec.ev[2], s);
+      }
+      if (!rc) rc = md_grid(P, P.md.d_grid, grad, s);
+   } else {
+      rc = launch_spread_grid(P, d_x, grad, s);
    }
-   if (!rc) rc = P.md.on ? md_grid(P, P.md.d_grid, grad, s) : launch_grid(P, P.d_part, P.nparts, grad, s);
    if (mdt) {
       (void)hipEventRecord(rec.ev[3], s);
       (void)hipEventRecord(rec.ev[4], s);
@@ -608,8 +613,7 @@ int additive_matvec_dot(void* str, const double* d_x, double* d_y, double* d_dot
       if (md_spread(P, d_x, P.md.d_grid, s) || md_grid(P, P.md.d_grid, 0, s)) return -1;
       return md_interp(P, 0, 1.0, d_x, 0.0, d_y, s, d_dot);
    }
-   if (launch_spread(P, d_x, P.d_part, s)) return -1;
-   if (launch_grid(P, P.d_part, P.nparts, 0, s)) return -1;
+   if (launch_spread_grid(P, d_x, 0, s)) return -1;
    return launch_interp(P, 0, 1.0, d_x, 0.0, d_y, s, d_dot);
 }
 }  // namespace nfft4gp_amd
@@ -641,7 +645,7 @@ int additive_matvec_chunked(void* str, double alpha, const double* d_x, double* 
    AdditivePlan& P = E->P;
    if (P.md.on || P.timing || P.row_begin != 0 || P.row_end != P.n_global || P.nblocks == 0) return -1;
    hipStream_t s = current_stream();
-   if (launch_spread(P, d_x, P.d_part, s) || launch_grid(P, P.d_part, P.nparts, 0, s)) return -1;
+   if (launch_spread_grid(P, d_x, 0, s)) return -1;
    nchunks = std::max(1, std::min(nchunks, P.nblocks));
    for (int c = 0; c < nchunks; c++) {
       const int b0 = (int)((long long)P.nblocks * c / nchunks), b1 = (int)((long long)P.nblocks * (c + 1) / nchunks);

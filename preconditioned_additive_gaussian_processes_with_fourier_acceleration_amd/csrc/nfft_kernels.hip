@@ -218,7 +218,8 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
                                                       const uint32_t* __restrict__ qarr,
                                                       const int* __restrict__ tile_off, const int* __restrict__ cmax,
                                                       const double* __restrict__ x, int n, int B, int nblocks,
-                                                      int ngroups, int CG, int nw, double* __restrict__ part)
+                                                      int ngroups, int CG, int nw, double* __restrict__ part,
+                                                      double* __restrict__ gsum)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = B + kPad;
@@ -336,7 +337,10 @@ __global__ __launch_bounds__(THREADS, 6) void k_spread(const uint16_t* __restric
          for (int d = 0; d < kNC; d++)
             v = fma((REC == 4 ? c_taps_u : c_taps)[tp * kNC + d], mrow[mom_index<MOMT>(0, 0, d)], v);
       }
-      part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
+      if (gsum)
+         atomicAdd(gsum + (size_t)(c0 + cl) * kNos + gi, v);  // launch_spread_grid's atomic sum
+      else
+         part[((size_t)(c0 + cl) * nblocks + b) * kNos + gi] = v;  // [comp][block][cell]
    }
    if (TIMELINE) {
       __syncthreads();
@@ -424,7 +428,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
                                                       const double* __restrict__ w, const double* __restrict__ wd,
                                                       double* __restrict__ H, double* __restrict__ Hd, int grad,
                                                       int from_sum, long long part_rs = 0, long long h_rs = 0,
-                                                      double* __restrict__ hb = nullptr)
+                                                      double* __restrict__ hb = nullptr, int clear_sum = 0)
 {
    __shared__ double s_red[kGridThreads];
    __shared__ double s_g[kNos];
@@ -439,7 +443,11 @@ __global__ __launch_bounds__(kGridThreads) void k_grid(const double* __restrict_
    double ct[kTaps];
    grid_tail_coeffs(ct);
    if (from_sum) {
-      if (tid < kNos) s_g[tid] = part[(size_t)comp * kNos + tid];
+      if (tid < kNos) {
+         s_g[tid] = part[(size_t)comp * kNos + tid];
+         // launch_spread_grid's atomic sums start from zero at the next matvec
+         if (clear_sum) const_cast<double*>(part)[(size_t)comp * kNos + tid] = 0.0;
+      }
    } else {
       // 16 strands per cell over this window's contiguous partial grids; each strand issues up to
       // kPer loads before its first add (one memory latency for nparts <= 256); fixed order ->
@@ -1145,7 +1153,7 @@ int upload_tap_coeffs()
 }
 
 typedef void (*SpreadFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const int*, const double*, int,
-                         int, int, int, int, int, double*);
+                         int, int, int, int, int, double*, double*);
 // 0: the spread; 1: the same with per-workgroup s_memrealtime stamps (tools/timeline_spread.py); 2: the round-4
 // moment table (MOMT 0, A/B).  Variants that measured slower or neutral (prefetching runs, persistent workgroups,
 // several groups per workgroup, the fold in two chains, register-staged alpha, the row shards' block sum in the
@@ -1290,7 +1298,8 @@ static bool abs_lds_ok()
    return ok;
 }
 
-int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream)
+static int launch_spread_to(const AdditivePlan& P, const double* d_x, double* d_part, double* d_gsum,
+                            hipStream_t stream)
 {
    if (P.dl.ntiles == 0 || P.n == 0) return 0;
    raise_lds_limit_once();
@@ -1299,7 +1308,42 @@ int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipS
    const int gridx = ((P.nblocks + 7) / 8) * 8 * P.ngroups;
    launch_ev(fn, dim3(gridx), dim3(kSpreadThreads), spread_lds_bytes(P), stream, P.kev ? P.kev + 0 : nullptr,
              P.dl.meta, P.dl.lo, P.dl.q, P.dl.tile_off, (const int*)P.dl.cmax, d_x, P.n, P.B, P.nblocks, P.ngroups,
-             P.CG, P.nw, d_part);
+             P.CG, P.nw, d_part, d_gsum);
+   NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int launch_spread(const AdditivePlan& P, const double* d_x, double* d_part, hipStream_t stream)
+{
+   return launch_spread_to(P, d_x, d_part, nullptr, stream);
+}
+
+// The atomic grid sum: each spread workgroup adds its CG x 64 grid values into d_gsum (device-scope fp64 atomics,
+// executed at the memory side) instead of writing a partial grid, and k_grid reads the nw x 64 sums (and clears
+// them for the next matvec) instead of summing nblocks partial grids per window -- at config C 246 x 64 loads per
+// window, most of k_grid's 5 us.  The sums' order then follows the workgroups' arrival, so deterministic mode keeps
+// the partials; with many blocks (config E: 2461 adds per address) the adds would contend, so they keep them too.
+constexpr int kAtomicGridMaxBlocks = 512;
+static bool grid_atomic(const AdditivePlan& P)
+{
+   static const int v = getenv("NFFT4GP_AMD_GRID_ATOMIC") ? atoi(getenv("NFFT4GP_AMD_GRID_ATOMIC")) : -1;
+   if (P.det || v == 0) return false;
+   return v > 0 || P.nblocks <= kAtomicGridMaxBlocks;
+}
+
+int launch_spread_grid(AdditivePlan& P, const double* d_x, int grad, hipStream_t stream)
+{
+   if (!grid_atomic(P) || P.nblocks == 0) {
+      if (launch_spread(P, d_x, P.d_part, stream)) return -1;
+      return launch_grid(P, P.d_part, P.nparts, grad, stream);
+   }
+   if (!P.d_gsum) {
+      NFFT4GP_HIP_CHECK(hipMalloc((void**)&P.d_gsum, sizeof(double) * (size_t)P.nw * kNos));
+      NFFT4GP_HIP_CHECK(hipMemsetAsync(P.d_gsum, 0, sizeof(double) * (size_t)P.nw * kNos, stream));
+   }
+   if (launch_spread_to(P, d_x, nullptr, P.d_gsum, stream)) return -1;
+   launch_ev(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, P.kev ? P.kev + 2 : nullptr, (const double*)P.d_gsum, 1,
+             (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 1, 0ll, 0ll, (double*)nullptr, 1);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -1308,7 +1352,7 @@ int launch_grid(const AdditivePlan& P, const double* d_part, int nparts, int gra
 {
    launch_ev(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, P.kev ? P.kev + 2 : nullptr, d_part, nparts,
              (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 0, 0ll, 0ll,
-             P.det ? P.d_hb : (double*)nullptr);
+             P.det ? P.d_hb : (double*)nullptr, 0);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -1317,7 +1361,7 @@ int launch_grid_from_sum(const AdditivePlan& P, const double* d_gridsum, int gra
 {
    launch_ev(k_grid, dim3(P.nw), dim3(kGridThreads), 0, stream, P.kev ? P.kev + 2 : nullptr, d_gridsum, 1,
              (const double*)P.d_w, (const double*)P.d_wd, P.d_H, P.d_Hd, grad, 1, 0ll, 0ll,
-             P.det ? P.d_hb : (double*)nullptr);
+             P.det ? P.d_hb : (double*)nullptr, 0);
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;
 }
@@ -1446,7 +1490,7 @@ int launch_matvec2(AdditivePlan& P, double alpha, const double* x0, const double
    // P.d_hb holds [vector][H, Hd][nw]: the grid writes each vector's H bound at hb + 2 nw y
    hipLaunchKernelGGL(k_grid, dim3(P.nw, 2), dim3(kGridThreads), 0, stream, (const double*)P.d_part2, P.nparts,
                       (const double*)P.d_w, (const double*)P.d_wd, P.d_H2, P.d_Hd, 0, 0, (long long)part_rs,
-                      (long long)h_rs, P.det ? P.d_hb : (double*)nullptr);
+                      (long long)h_rs, P.det ? P.d_hb : (double*)nullptr, 0);
    const size_t lds_i = sizeof(double) * 2 * ((size_t)P.B + kPad);
    // 1024 threads: 512-thread workgroups at config E's 2461 blocks measured the same loss (1.700 s either way,
    // profiles/r05_interp2_ab.txt); NFFT4GP_AMD_INTERP2_THREADS=512 selects them
