@@ -880,10 +880,10 @@ __global__ __launch_bounds__(THREADS) void k_interp(
 // never wait on one another in a cycle.  Same arithmetic as k_interp's plain path (bitwise equal results).
 constexpr int kHlWin = kNC * kNos + 1;
 
-__host__ __device__ constexpr size_t hl_lds_bytes(int B, int CG, int ngroups)
+__host__ __device__ constexpr size_t hl_lds_bytes(int B, int CG, int ngroups, int ns)
 {
-   return sizeof(double) * ((size_t)B + kPad) + sizeof(double) * 2 * (size_t)CG * kHlWin +
-          sizeof(int) * (3 + 2 * (size_t)ngroups);
+   return sizeof(double) * ((size_t)B + kPad) + sizeof(double) * (size_t)ns * CG * kHlWin +
+          sizeof(int) * (1 + (size_t)ns + 2 * (size_t)ngroups);
 }
 
 // one wave stages group g's H rows (windows [g CG, min((g + 1) CG, nw))) into slot `slot` of s_H
@@ -914,14 +914,14 @@ __global__ __launch_bounds__(THREADS) void k_interp_hl(const uint16_t* __restric
                                                        const double* __restrict__ H, const double* __restrict__ x,
                                                        double* __restrict__ y, int n, int B, int ngroups, int CG, int nw,
                                                        double alpha, double beta, double f, double mu,
-                                                       const double* __restrict__ hb)
+                                                       const double* __restrict__ hb, int ns)
 {
    extern __shared__ __attribute__((aligned(16))) double smem[];
    const int Bp = B + kPad;
    double* s_y = smem;  // the first dynamic slice (lds_add addresses it absolutely)
-   double* s_H = smem + Bp;
-   int* s_ready = reinterpret_cast<int*>(s_H + 2 * (size_t)CG * kHlWin);
-   int* s_done = s_ready + 2;
+   double* s_H = smem + Bp;  // ns slots (2 <= ns <= nwaves): group g in slot g % ns
+   int* s_ready = reinterpret_cast<int*>(s_H + (size_t)ns * CG * kHlWin);
+   int* s_done = s_ready + ns;
    int* s_toff = s_done + ngroups;  // the block's group boundaries tile_off[b ngroups .. (b + 1) ngroups]
    const int b = blockIdx.x;
    const int tid = threadIdx.x;
@@ -949,23 +949,24 @@ __global__ __launch_bounds__(THREADS) void k_interp_hl(const uint16_t* __restric
    for (int i = tid; i < Bp; i += THREADS) s_y[i] = 0.0;
    for (int i = tid; i < ngroups; i += THREADS) s_done[i] = 0;
    for (int i = tid; i <= ngroups; i += THREADS) s_toff[i] = tile_off[gbase + i];
-   if (tid < 2) s_ready[tid] = tid;
-   // groups 0 and 1, one wave each (more waves when there are: every wave w < 2 stages group w)
-   if (wave < 2 && wave < ngroups) hl_stage_wave(s_H, H, wave, wave, CG, nw, lane);
+   if (tid < ns) s_ready[tid] = tid;
+   // groups 0 .. ns - 1, one wave each
+   if (wave < ns && wave < ngroups) hl_stage_wave(s_H, H, wave, wave, CG, nw, lane);
    const double Cy = DET ? det_grid(det_interp_exp(hb, nw)) : 0.0;
    __syncthreads();
 
-   int g = 0;
+   int g = 0, gslot = 0;
    int gend = s_toff[1];
-   // wave leaves group gl: count it; the last one stages group gl + 2 into gl's slot and publishes it
+   // wave leaves group gl: count it; the last one stages group gl + ns into gl's slot and publishes it
    auto leave = [&](int gl) {
       int old = 0;
       if (lane == 0) old = __hip_atomic_fetch_add(s_done + gl, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
       old = __builtin_amdgcn_readfirstlane(old);
-      if (old == nwaves - 1 && gl + 2 < ngroups) {
-         hl_stage_wave(s_H, H, gl + 2, gl & 1, CG, nw, lane);
+      if (old == nwaves - 1 && gl + ns < ngroups) {
+         const int sl = gl % ns;
+         hl_stage_wave(s_H, H, gl + ns, sl, CG, nw, lane);
          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-         if (lane == 0) __hip_atomic_store(s_ready + (gl & 1), gl + 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+         if (lane == 0) __hip_atomic_store(s_ready + sl, gl + ns, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
    };
    for (; t < t1; t += nwaves) {
@@ -973,16 +974,17 @@ __global__ __launch_bounds__(THREADS) void k_interp_hl(const uint16_t* __restric
          leave(g);
          g++;
          gend = s_toff[g + 1];
-         if (g >= 2) {
+         gslot = g % ns;
+         if (g >= ns) {
             for (long spin = 0; spin < (1l << 24); spin++) {
-               if (__hip_atomic_load(s_ready + (g & 1), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == g) break;
+               if (__hip_atomic_load(s_ready + gslot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == g) break;
                __builtin_amdgcn_s_sleep(1);
             }
          }
       }
       const int cl = (int)(cur.mt >> 6) - g * CG;
       const int cell = (int)(cur.mt & 63u);
-      const double* hrow = s_H + ((size_t)(g & 1) * CG + cl) * kHlWin + cell;
+      const double* hrow = s_H + ((size_t)gslot * CG + cl) * kHlWin + cell;
       double hc[kNC];
 #pragma unroll
       for (int d = 0; d < kNC; d++) hc[d] = hrow[d * kNos];
@@ -1229,7 +1231,7 @@ static bool static_lds_zero(const void* fn)
 
 // every interpolation kernel the launchers pick
 typedef void (*InterpHlFn)(const uint16_t*, const uint32_t*, const uint32_t*, const int*, const double*, const double*,
-                           double*, int, int, int, int, int, double, double, double, double, const double*);
+                           double*, int, int, int, int, int, double, double, double, double, const double*, int);
 static InterpHlFn interp_hl_fn(bool small, bool det, int rec)
 {
    if (rec == 4)
@@ -1436,10 +1438,13 @@ int launch_interp(const AdditivePlan& P, int grad, double alpha, const double* d
    static const int forced = getenv("NFFT4GP_AMD_INTERP_THREADS") ? atoi(getenv("NFFT4GP_AMD_INTERP_THREADS")) : 0;
    const bool small = forced == 512 || (forced != 1024 && P.nblocks >= 512);
    if (!grad && !d_dot && interp_hl_on(P) && P.ngroups >= 1) {
+      // staging slots: 2 on 512-thread workgroups (two per CU fit 2 x 81 KB of LDS), up to 6 on 1024
+      static const int slots_env = getenv("NFFT4GP_AMD_HL_SLOTS") ? atoi(getenv("NFFT4GP_AMD_HL_SLOTS")) : 0;
+      const int ns = std::max(2, std::min(slots_env > 0 ? slots_env : 2, small ? 2 : 6));
       launch_ev(interp_hl_fn(small, P.det, P.rec), dim3(P.nblocks), dim3(small ? 512 : kInterpThreads),
-                hl_lds_bytes(P.B, P.CG, P.ngroups), stream, P.kev ? P.kev + 4 : nullptr, P.dl.meta, P.dl.lo, P.dl.q,
-                P.dl.tile_off, (const double*)P.d_H, d_x, d_y, P.n, P.B, P.ngroups, P.CG, P.nw, alpha, beta, P.f,
-                P.mu * P.diag, (const double*)P.d_hb);
+                hl_lds_bytes(P.B, P.CG, P.ngroups, ns), stream, P.kev ? P.kev + 4 : nullptr, P.dl.meta, P.dl.lo,
+                P.dl.q, P.dl.tile_off, (const double*)P.d_H, d_x, d_y, P.n, P.B, P.ngroups, P.CG, P.nw, alpha, beta,
+                P.f, P.mu * P.diag, (const double*)P.d_hb, ns);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return 0;
    }
