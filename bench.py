@@ -573,7 +573,8 @@ def run_pcg_afn(op, X, torch, n, k, lfil=20, rng_seed=906, tol=1e-6, maxits=3000
             key + "_f32_iters": iters32, key + "_f32_rel_res": relres32, key + "_f32_apply_ms": 1e3 * t_apply32}
 
 
-def run_config_e(torch, steps, warmup, traffic=True, n=10_000_000, d=64, precisions=(64, 32), tag="configs[4]"):
+def run_config_e(torch, steps, warmup, traffic=True, n=10_000_000, d=64, precisions=(64, 32), tag="configs[4]",
+                 with_loss=True):
     """BASELINE configs[4]'s operator on one GPU, under the same clock as the headline: n = 1e7 points, 64 1-D
     windows (Gaussian f = 1, l = 1, mu = 0.01), the additive matvec with x, y in HBM, out of the 256 MB
     Infinity Cache (the layout is 2.8-3.5 GB per pass).  Two legs: the fp64 default records and the 32-bit
@@ -589,6 +590,11 @@ def run_config_e(torch, steps, warmup, traffic=True, n=10_000_000, d=64, precisi
     win = np.arange(d, dtype=np.int32)
     xd = torch.tensor(x_host, device="cuda")
     yd = torch.zeros(n, dtype=torch.float64, device="cuda")
+    y_loss = R_loss = None
+    if with_loss:  # the loss leg's labels and its fixed Rademacher probes (probe-major = column-major n x nvecs)
+        rng = np.random.default_rng(909)
+        y_loss = rng.random(n) - 0.5
+        R_loss = torch.tensor(np.where(rng.random((10, n)) < 0.5, -1.0, 1.0), device="cuda")
     survey = {"spread": n * (4 * d + 4), "interp": n * (4 * d + 8)}
     out = {"workload": f"BASELINE {tag} operator on 1 GPU: additive NFFT matvec, n={n}, d={d}, {d} x 1-D windows, "
                        f"Gaussian f=1 l=1 mu=0.01 (synthetic: numpy PCG64 seed 906)",
@@ -629,6 +635,9 @@ def run_config_e(torch, steps, warmup, traffic=True, n=10_000_000, d=64, precisi
         avg = {k: ms / max(c, 1) for k, (ms, c) in op.timing_query().items()}
         op.timing(False)
         info = op.layout_info()
+        loss_rec = None
+        if with_loss:
+            loss_rec = config_e_loss(op, torch, X, y_loss, R_loss, d)
         op.free()
         pmc = None
         if traffic:
@@ -654,7 +663,26 @@ def run_config_e(torch, steps, warmup, traffic=True, n=10_000_000, d=64, precisi
             "setup_s": setup_s, "kernels_ms": avg, "layout": info,
             "roofline": dict(rl[dom], kernel=dom), "roofline_per_kernel": rl,
             "traffic_unit": "bytes per launch (2 x FETCH_SIZE + WRITE_SIZE)"}
+        if loss_rec is not None:
+            out[f"f{bits}"]["loss"] = loss_rec
     return out
+
+
+def config_e_loss(op, torch, X, y, R, d, maxits=50, nvecs=10, l=0.1):
+    """BASELINE configs[4]'s step on one GPU: one Nfft4GPGpLoss (gp_loss.c:96-307: FGMRES for K^-1 y with the
+    reference's MGS, nvecs Rademacher probes x maxits Lanczos steps, the gradient matvecs) on the leg's handle
+    at (f, l, mu) = (1, 0.1, 0.01), identity transform (l = 0.1: the NFFT operator is SPD there)."""
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    win = np.arange(d, dtype=np.int32)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    with _StdoutToStderr():
+        loss, grad = amd.gp_loss(X, win, d, 1, y, (1.0, l, 0.01), maxits=maxits, nvecs=nvecs, rademacher=R,
+                                 tol=1e-6, transform=3, op=op)
+        torch.cuda.synchronize()
+    t = time.time() - t0
+    return {"time_s": t, "value": loss, "grad": [float(g) for g in grad], "maxits": maxits, "nvecs": nvecs, "l": l,
+            "fgmres_ortho": "modified Gram-Schmidt (the reference's)"}
 
 
 class _StdoutToStderr:
@@ -1099,7 +1127,7 @@ def main():
             result["config_e"] = run_config_e(torch, args.steps, args.warmup, traffic=not args.no_traffic)
             # BASELINE configs[1]'s operator (n = 1e5, 8 windows, fp64): cache-resident and launch-bound
             result["config_b"] = run_config_e(torch, max(args.steps, 200), args.warmup, traffic=False, n=100_000, d=8,
-                                              precisions=(64,), tag="configs[1]")
+                                              precisions=(64,), tag="configs[1]", with_loss=False)
         if not args.no_cpu_baseline:
             try:
                 result["cpu_baseline"] = cpu_baseline(n, d, threads=args.cpu_threads)
