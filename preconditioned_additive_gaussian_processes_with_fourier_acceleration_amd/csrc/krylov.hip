@@ -522,7 +522,9 @@ int bd_grid(size_t n)
 // FOLD: k_block_reduce folded in -- the partials are stored at agent scope, the last arriving workgroup of each
 // column group (reduce.hpp's per-XCD tickets, one ticket array per group) sums them in k_block_reduce's order
 // and writes h[0..m) (h[m + 1] for the norm column): one launch instead of two, the same bits
-template <bool FOLD = false>
+// VEC = 2: each thread reads two consecutive rows per column as one 16-byte load (the host picks it when n is even
+// and w, V are 16-byte aligned, so every column is)
+template <bool FOLD = false, int VEC = 1>
 __global__ __launch_bounds__(kBDThreads) void k_block_dots(const double* __restrict__ w, const double* __restrict__ V,
                                                            size_t n, int m, int with_norm, double* __restrict__ part,
                                                            int ldp, const double* __restrict__ c_after = nullptr,
@@ -539,13 +541,28 @@ __global__ __launch_bounds__(kBDThreads) void k_block_dots(const double* __restr
 #pragma unroll
    for (int j = 0; j < kBD; j++) acc[j] = 0.0;
    const size_t stride = (size_t)gridDim.x * kBDThreads;
-   for (size_t r = (size_t)blockIdx.x * kBDThreads + threadIdx.x; r < n; r += stride) {
-      const double wr = w[r];
-      double v[kBD];
+   if constexpr (VEC == 1) {
+      for (size_t r = (size_t)blockIdx.x * kBDThreads + threadIdx.x; r < n; r += stride) {
+         const double wr = w[r];
+         double v[kBD];
 #pragma unroll
-      for (int j = 0; j < kBD; j++) v[j] = j < nv && j < cnt ? V[(size_t)(g0 + j) * n + r] : (j < cnt ? wr : 0.0);
+         for (int j = 0; j < kBD; j++) v[j] = j < nv && j < cnt ? V[(size_t)(g0 + j) * n + r] : (j < cnt ? wr : 0.0);
 #pragma unroll
-      for (int j = 0; j < kBD; j++) acc[j] = fma(v[j], wr, acc[j]);
+         for (int j = 0; j < kBD; j++) acc[j] = fma(v[j], wr, acc[j]);
+      }
+   } else {
+      const size_t n2 = n / 2;
+      const double2* __restrict__ w2 = reinterpret_cast<const double2*>(w);
+      for (size_t r = (size_t)blockIdx.x * kBDThreads + threadIdx.x; r < n2; r += stride) {
+         const double2 wr = w2[r];
+         double2 v[kBD];
+#pragma unroll
+         for (int j = 0; j < kBD; j++)
+            v[j] = j < nv && j < cnt ? reinterpret_cast<const double2*>(V + (size_t)(g0 + j) * n)[r]
+                                     : (j < cnt ? wr : make_double2(0.0, 0.0));
+#pragma unroll
+         for (int j = 0; j < kBD; j++) acc[j] = fma(v[j].y, wr.y, fma(v[j].x, wr.x, acc[j]));
+      }
    }
    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -636,6 +653,9 @@ __global__ __launch_bounds__(1024) void k_block_reduce(const double* __restrict_
 // (fixed-order grid reduction).  c_after / c_before (optional device scalars, the squared norms after and
 // before the previous pass): the pass runs only when the DGKS test sqrt(after) < 0.7071 sqrt(before) holds --
 // the same in every workgroup -- and *c_flag records the decision (1 / 0) for the host
+// VEC = 2: two consecutive rows per 16-byte load (n even, w and Z 16-byte aligned); w's rows get the same bits,
+// only the norm's summation order differs
+template <int VEC = 1>
 __global__ __launch_bounds__(kKThreads) void k_block_update(double* __restrict__ w, const double* __restrict__ Z,
                                                             size_t n, const double* __restrict__ h, int m,
                                                             double* __restrict__ part,
@@ -654,6 +674,60 @@ __global__ __launch_bounds__(kKThreads) void k_block_update(double* __restrict__
    for (int j = threadIdx.x; j < m; j += kKThreads) s_h[j] = h[j];
    __syncthreads();
    double acc = 0.0;
+   if constexpr (VEC == 2) {
+      constexpr int E2 = kKEPT / 2;  // pairs per thread per step
+      const size_t n2 = n / 2;
+      double2* __restrict__ w2 = reinterpret_cast<double2*>(w);
+      const size_t stride2 = (size_t)gridDim.x * kKThreads * E2;
+      for (size_t p0 = (size_t)blockIdx.x * kKThreads * E2 + threadIdx.x; p0 < n2; p0 += stride2) {
+         double2 wv[E2];
+         bool in[E2];
+#pragma unroll
+         for (int e = 0; e < E2; e++) {
+            const size_t p = p0 + (size_t)e * kKThreads;
+            in[e] = p < n2;
+            wv[e] = in[e] ? w2[p] : make_double2(0.0, 0.0);
+         }
+         int j = 0;
+         for (; j + 4 <= m; j += 4) {
+            double2 z[4][E2];
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+#pragma unroll
+               for (int e = 0; e < E2; e++)
+                  z[q][e] = in[e] ? reinterpret_cast<const double2*>(Z + (size_t)(j + q) * n)[p0 + (size_t)e * kKThreads]
+                                  : make_double2(0.0, 0.0);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+               const double hj = s_h[j + q];
+#pragma unroll
+               for (int e = 0; e < E2; e++) {
+                  wv[e].x = fma(-hj, z[q][e].x, wv[e].x);
+                  wv[e].y = fma(-hj, z[q][e].y, wv[e].y);
+               }
+            }
+         }
+         for (; j < m; j++) {
+            const double hj = s_h[j];
+#pragma unroll
+            for (int e = 0; e < E2; e++) {
+               const double2 z = in[e] ? reinterpret_cast<const double2*>(Z + (size_t)j * n)[p0 + (size_t)e * kKThreads]
+                                       : make_double2(0.0, 0.0);
+               wv[e].x = fma(-hj, z.x, wv[e].x);
+               wv[e].y = fma(-hj, z.y, wv[e].y);
+            }
+         }
+#pragma unroll
+         for (int e = 0; e < E2; e++) {
+            if (in[e]) w2[p0 + (size_t)e * kKThreads] = wv[e];
+            acc = fma(wv[e].y, wv[e].y, fma(wv[e].x, wv[e].x, acc));
+         }
+      }
+      acc = block_sum0<kKThreads>(acc);
+      double tot;
+      if (grid_total<kKThreads>(acc, part, ticket, &tot) && threadIdx.x == 0) *out = tot;
+      return;
+   }
    const size_t stride = (size_t)gridDim.x * kKThreads * kKEPT;
    for (size_t i0 = (size_t)blockIdx.x * kKThreads * kKEPT + threadIdx.x; i0 < n; i0 += stride) {
       double wv[kKEPT];
@@ -1058,31 +1132,64 @@ struct Ctx {
       const char* e = getenv("NFFT4GP_AMD_BD_FOLD");
       return !(e && atoi(e) == 0);
    }
+   // the block passes' 16-byte row pairs: n even and every vector 16-byte aligned (then so is every column);
+   // NFFT4GP_AMD_BD_VEC=0 keeps one row per load
+   bool bd_vec(const void* a, const void* b, const void* c2) const
+   {
+      const char* e = getenv("NFFT4GP_AMD_BD_VEC");
+      if (e && atoi(e) == 0) return false;
+      return n % 2 == 0 && (((uintptr_t)a | (uintptr_t)b | (uintptr_t)c2) & 15) == 0;
+   }
+   // h[0..mc) = V^T w (column m, when mc = m + 1, is w itself: h[m + 1]) in k_block_dots (+ k_block_reduce
+   // unless folded); after / before: the DGKS gate of a second pass
+   void block_dots(const double* w, const double* V, int m, int with_norm, double* h, bool vec,
+                   const double* after = nullptr, const double* before = nullptr)
+   {
+      const int nb = bd_grid(n);
+      const int mc = m + with_norm;
+      const dim3 grid(nb, (mc + kBD - 1) / kBD);
+      if (fold_reduce()) {
+         if (vec)
+            hipLaunchKernelGGL((k_block_dots<true, 2>), grid, dim3(kBDThreads), 0, s, w, V, n, m, with_norm, g_k.bpart,
+                               KScratch::kScal, after, before, h, g_k.bd_tickets);
+         else
+            hipLaunchKernelGGL((k_block_dots<true, 1>), grid, dim3(kBDThreads), 0, s, w, V, n, m, with_norm, g_k.bpart,
+                               KScratch::kScal, after, before, h, g_k.bd_tickets);
+      } else {
+         if (vec)
+            hipLaunchKernelGGL((k_block_dots<false, 2>), grid, dim3(kBDThreads), 0, s, w, V, n, m, with_norm,
+                               g_k.bpart, KScratch::kScal, after, before, (double*)nullptr, (unsigned int*)nullptr);
+         else
+            hipLaunchKernelGGL((k_block_dots<false, 1>), grid, dim3(kBDThreads), 0, s, w, V, n, m, with_norm,
+                               g_k.bpart, KScratch::kScal, after, before, (double*)nullptr, (unsigned int*)nullptr);
+         hipLaunchKernelGGL(k_block_reduce, dim3((mc + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, mc,
+                            m, h);
+      }
+   }
+   // w -= Z h (m columns), *out = ||w||^2; after / before / flag: the DGKS gate of a second pass
+   void block_update(double* w, const double* Z, int m, const double* h, double* out, bool vec,
+                     const double* after = nullptr, const double* before = nullptr, double* flag = nullptr)
+   {
+      if (vec)
+         hipLaunchKernelGGL(k_block_update<2>, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, Z, n, h, m,
+                            g_k.part, g_k.ticket, out, after, before, flag);
+      else
+         hipLaunchKernelGGL(k_block_update<1>, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, Z, n, h, m,
+                            g_k.part, g_k.ticket, out, after, before, flag);
+   }
    // one classical Gram-Schmidt pass: h[0..m) = V^T w, w -= Z h, h[m] = ||w||^2 afterwards (device
    // scalars); with_norm: also h[m + 1] = ||w||^2 before the update (from the dot pass)
    int block_gs(double* w, const double* V, const double* Z, int m, double* h, int with_norm = 0)
    {
       if (m <= 0 || m + 2 > KScratch::kScal) return -1;
       if (g_k.ensure_bpart()) return -1;
-      const int nb = bd_grid(n);
-      const int mc = m + with_norm;
+      const bool vec = bd_vec(w, V, Z);
       // h[m], h[m + 1] take part in the all-reduce below even when this pass does not write them
       if (comm) NFFT4GP_HIP_CHECK(hipMemsetAsync(h + m, 0, sizeof(double) * 2, s));
-      if (fold_reduce()) {
-         hipLaunchKernelGGL(k_block_dots<true>, dim3(nb, (mc + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m,
-                            with_norm, g_k.bpart, KScratch::kScal, (const double*)nullptr, (const double*)nullptr, h,
-                            g_k.bd_tickets);
-      } else {
-         hipLaunchKernelGGL(k_block_dots<false>, dim3(nb, (mc + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m,
-                            with_norm, g_k.bpart, KScratch::kScal, (const double*)nullptr, (const double*)nullptr,
-                            (double*)nullptr, (unsigned int*)nullptr);
-         hipLaunchKernelGGL(k_block_reduce, dim3((mc + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, mc,
-                            m, h);
-      }
+      block_dots(w, V, m, with_norm, h, vec);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       if (red(h, m + 2)) return -1;  // the projections and the norm before them, summed over the row shards
-      hipLaunchKernelGGL(k_block_update, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, Z, n, h, m,
-                         g_k.part, g_k.ticket, h + m, nullptr, nullptr, nullptr);
+      block_update(w, Z, m, h, h + m, vec);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return red(h + m, 1);
    }
@@ -1095,22 +1202,13 @@ struct Ctx {
    {
       if (m <= 0 || 2 * m + 4 > KScratch::kScal) return -1;
       if (block_gs(w, V, V, m, h, 1)) return -1;
-      const int nb = bd_grid(n);
+      const bool vec = bd_vec(w, V, V);
       const double* after = h + m;
       const double* before = h + m + 1;
-      if (fold_reduce()) {
-         hipLaunchKernelGGL(k_block_dots<true>, dim3(nb, (m + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m, 0,
-                            g_k.bpart, KScratch::kScal, after, before, h + m + 2, g_k.bd_tickets);
-      } else {
-         hipLaunchKernelGGL(k_block_dots<false>, dim3(nb, (m + kBD - 1) / kBD), dim3(kBDThreads), 0, s, w, V, n, m, 0,
-                            g_k.bpart, KScratch::kScal, after, before, (double*)nullptr, (unsigned int*)nullptr);
-         hipLaunchKernelGGL(k_block_reduce, dim3((m + 63) / 64), dim3(1024), 0, s, g_k.bpart, nb, KScratch::kScal, m, m,
-                            h + m + 2);
-      }
+      block_dots(w, V, m, 0, h + m + 2, vec, after, before);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       if (red(h + m + 2, m)) return -1;
-      hipLaunchKernelGGL(k_block_update, dim3(kgrid(n)), dim3(kKThreads), sizeof(double) * m, s, w, V, n, h + m + 2,
-                         m, g_k.part, g_k.ticket, h + 2 * m + 2, after, before, h + 2 * m + 3);
+      block_update(w, V, m, h + m + 2, h + 2 * m + 2, vec, after, before, h + 2 * m + 3);
       NFFT4GP_HIP_CHECK(hipGetLastError());
       return red(h + 2 * m + 2, 1);
    }
@@ -2594,6 +2692,31 @@ extern "C" int Nfft4GPAmdDebugChainFault(int mode)
    *g_k.hchain_err = 0;
    g_k.chain_off = false;
    return was_off;
+}
+
+// Timing probe for tools/reorth_probe.py: `reps` classical Gram-Schmidt passes (Ctx::block_gs, the Lanczos
+// re-orthogonalisation's pass) of the device vector w against m device columns V (dots) / Z (updates) on the
+// library's stream; *ms = average pass time (hipEvents), h_out (m + 2 doubles, optional) = the last pass's scalars
+extern "C" int Nfft4GPAmdDebugBlockGs(double* w, const double* V, const double* Z, long long n, int m, int with_norm,
+                                      int reps, float* ms, double* h_out)
+{
+   if (!need_device("Nfft4GPAmdDebugBlockGs") || n <= 0 || m <= 0 || reps <= 0 || g_k.ensure()) return -1;
+   Ctx c{current_stream(), (size_t)n, nullptr};
+   hipEvent_t e0, e1;
+   NFFT4GP_HIP_CHECK(hipEventCreate(&e0));
+   NFFT4GP_HIP_CHECK(hipEventCreate(&e1));
+   int rc = c.block_gs(w, V, Z, m, g_k.scal, with_norm);  // warm-up
+   NFFT4GP_HIP_CHECK(hipEventRecord(e0, c.s));
+   for (int r = 0; r < reps && rc == 0; r++) rc = c.block_gs(w, V, Z, m, g_k.scal, with_norm);
+   NFFT4GP_HIP_CHECK(hipEventRecord(e1, c.s));
+   NFFT4GP_HIP_CHECK(hipEventSynchronize(e1));
+   float t = 0.f;
+   NFFT4GP_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+   if (ms) *ms = t / reps;
+   (void)hipEventDestroy(e0);
+   (void)hipEventDestroy(e1);
+   if (rc == 0 && h_out) rc = c.read(g_k.scal, m + 2, h_out);
+   return rc;
 }
 
 extern "C" {

@@ -45,3 +45,26 @@ def test_multi_matches_single(torch_cuda, nv, nw, dw, beta, n):
     h = np.zeros(n)
     assert L.Nfft4GPAmdAdditiveMatSymvMulti(op.h, n, 1, 1.0, h.ctypes.data, n, 0.0, h.ctypes.data, n) != 0
     assert L.Nfft4GPAmdAdditiveMatSymvMulti(op.h, n, 2, 1.0, V.data_ptr(), n - 1, 0.0, Y2.data_ptr(), n) != 0
+
+
+def test_multi_past_the_infinity_cache_is_bitwise(torch_cuda):
+    """A layout past the 256 MB Infinity Cache (n = 4e6, 64 windows: ~1.4 GB): the single-vector matvec takes
+    k_interp_hl (H rows staged in LDS) and the pair k_interp2; in deterministic mode both equal k_interp's bits."""
+    import torch
+
+    n, d = 4_000_000, 64
+    rng = np.random.default_rng(41)
+    X = rng.random((n, d))
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    del X
+    assert op.setup(amd.GAUSSIAN, f=1.0, l=0.5, mu=0.01) == 0
+    op.set_deterministic(True)
+    V = torch.tensor(rng.random((2, n)) - 0.5, device="cuda")
+    Y1 = torch.empty_like(V)
+    Y2 = torch.empty_like(V)
+    for v in range(2):
+        op.matsymv(V[v], 0.9, 0.0, Y1[v])
+    L = _lib.lib()
+    assert L.Nfft4GPAmdAdditiveMatSymvMulti(op.h, n, 2, 0.9, V.data_ptr(), n, 0.0, Y2.data_ptr(), n) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(Y1, Y2)
