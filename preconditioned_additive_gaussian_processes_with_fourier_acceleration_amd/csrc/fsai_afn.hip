@@ -172,6 +172,125 @@ __global__ __launch_bounds__(256) void k_a12_part(const TK* __restrict__ K12, in
    }
 }
 
+// The two K12 passes in one when S^{-1} = schur_scale I (schur_opt 0): y2[j] = schur_scale (rp2[j] - K12[:, j]^T y)
+// needs only column j, and the second pass adds K12[:, j] y2[j], so each column is read from HBM once and used
+// twice from registers.  A wave takes 4 columns at a time (k_a12t's dot: the same lane-strided sum and shuffle tree,
+// so y2 has k_a12t + k_scale_into's bits), then adds the 4 columns times their y2 into its lanes' row sums (rows
+// lane + 64 m); the workgroup's part[blk] adds its 4 waves' sums in wave order.  Fixed order: the same bits every
+// run (the K12 y2 sum in another order than k_a12_part's).  MI rows per lane (k <= 64 MI; EXACT: k = 64 MI).
+template <typename TK, int MI, bool EXACT>
+__device__ __forceinline__ void a12_fused_body(const TK* __restrict__ K12, int k, int n2, int cols,
+                                               const double* __restrict__ y, const double* __restrict__ rp2,
+                                               double scale, double* __restrict__ y2, double* __restrict__ part)
+{
+   extern __shared__ double s_y[];  // [k] y, then [4][k] the waves' row sums
+   double* s_acc = s_y + k;
+   for (int i = threadIdx.x; i < k; i += 256) s_y[i] = y[i];
+   __syncthreads();
+   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+   const int j0 = blockIdx.x * cols, j1 = min(n2, j0 + cols);
+   double yl[MI], acc[MI];
+#pragma unroll
+   for (int m = 0; m < MI; m++) {
+      const int i = lane + 64 * m;
+      yl[m] = i < k ? s_y[i] : 0.0;
+      acc[m] = 0.0;
+   }
+   for (int jw = j0 + wave * kA12tCols; jw < j1; jw += 4 * kA12tCols) {
+      const int nc = min(kA12tCols, j1 - jw);
+      const TK* col = K12 + (size_t)jw * k;
+      // every load unconditional, so all 4 MI of them are in flight together: an element past the column's k rows
+      // or past the workgroup's columns reads a valid entry instead and is never used (its row's sum is not
+      // stored; such a column's y2 is 0)
+      TK v[kA12tCols][MI];
+#pragma unroll
+      for (int c = 0; c < kA12tCols; c++) {
+         const TK* cc = col + (size_t)min(c, nc - 1) * k;  // a column past the workgroup's re-reads its last one
+         if (EXACT) {  // k = 64 MI: one base per column, immediate row offsets
+#pragma unroll
+            for (int m = 0; m < MI; m++) v[c][m] = cc[lane + 64 * m];
+         } else {
+#pragma unroll
+            for (int m = 0; m < MI; m++) v[c][m] = cc[min(lane + 64 * m, k - 1)];
+         }
+      }
+      double r[kA12tCols];
+#pragma unroll
+      for (int c = 0; c < kA12tCols; c++) {
+         r[c] = 0.0;
+#pragma unroll
+         for (int m = 0; m < MI; m++)
+            if (lane + 64 * m < k) r[c] = fma((double)v[c][m], yl[m], r[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < kA12tCols; c++) {
+         double t = r[c];
+         for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
+         double yv = 0.0;
+         if (lane == 0 && c < nc) {
+            yv = scale * (rp2[jw + c] - t);
+            y2[jw + c] = yv;
+         }
+         yv = __shfl(yv, 0, 64);
+#pragma unroll
+         for (int m = 0; m < MI; m++) acc[m] = fma((double)v[c][m], yv, acc[m]);
+      }
+   }
+#pragma unroll
+   for (int m = 0; m < MI; m++) {
+      const int i = lane + 64 * m;
+      if (i < k) s_acc[(size_t)wave * k + i] = acc[m];
+   }
+   __syncthreads();
+   for (int i = threadIdx.x; i < k; i += 256)
+      part[(size_t)blockIdx.x * k + i] = ((s_acc[i] + s_acc[(size_t)k + i]) + s_acc[2 * (size_t)k + i]) +
+                                         s_acc[3 * (size_t)k + i];
+}
+
+// fp64 storage: 133 VGPRs, 3 waves per SIMD; fp32 storage held to 128 VGPRs (4 waves per SIMD: 0.505 -> 0.472 ms per
+// apply at k = 512, n = 1e6, where the same bound costs fp64 0.797 -> 0.821; profiles/r06_afn_fused.txt)
+template <int MI, bool EXACT>
+__global__ __launch_bounds__(256) void k_a12_fused_f64(const double* __restrict__ K12, int k, int n2, int cols,
+                                                       const double* __restrict__ y, const double* __restrict__ rp2,
+                                                       double scale, double* __restrict__ y2, double* __restrict__ part)
+{
+   a12_fused_body<double, MI, EXACT>(K12, k, n2, cols, y, rp2, scale, y2, part);
+}
+template <int MI, bool EXACT>
+__global__ __launch_bounds__(256, 4) void k_a12_fused_f32(const float* __restrict__ K12, int k, int n2, int cols,
+                                                          const double* __restrict__ y, const double* __restrict__ rp2,
+                                                          double scale, double* __restrict__ y2, double* __restrict__ part)
+{
+   a12_fused_body<float, MI, EXACT>(K12, k, n2, cols, y, rp2, scale, y2, part);
+}
+
+// the fused pass for k <= 1024 (K12f: the fp32 copy, else K12); false when k is larger or NFFT4GP_AMD_AFN_FUSED=0
+bool a12_fused(const double* K12, const float* K12f, int k, int n2, int cols, int nblk, const double* y,
+               const double* rp2, double scale, double* y2, double* part, hipStream_t s)
+{
+   const char* fe = getenv("NFFT4GP_AMD_AFN_FUSED");
+   if (k > 1024 || (fe && atoi(fe) == 0)) return false;
+   const size_t lds = sizeof(double) * 5 * (size_t)k;
+#define NFFT4GP_A12F(KER, MIv, M)                                                                                    \
+   if (k == 64 * MIv)                                                                                                 \
+      hipLaunchKernelGGL((KER<MIv, true>), dim3(nblk), dim3(256), lds, s, M, k, n2, cols, y, rp2, scale, y2, part);   \
+   else                                                                                                               \
+      hipLaunchKernelGGL((KER<MIv, false>), dim3(nblk), dim3(256), lds, s, M, k, n2, cols, y, rp2, scale, y2, part)
+#define NFFT4GP_A12F_MI(KER, M)                                                                                      \
+   if (k <= 128) NFFT4GP_A12F(KER, 2, M);                                                                             \
+   else if (k <= 256) NFFT4GP_A12F(KER, 4, M);                                                                        \
+   else if (k <= 512) NFFT4GP_A12F(KER, 8, M);                                                                        \
+   else NFFT4GP_A12F(KER, 16, M)
+   if (K12f) {
+      NFFT4GP_A12F_MI(k_a12_fused_f32, K12f);
+   } else {
+      NFFT4GP_A12F_MI(k_a12_fused_f64, K12);
+   }
+#undef NFFT4GP_A12F_MI
+#undef NFFT4GP_A12F
+   return true;
+}
+
 // rp[i] -= sum_blk part[blk][i]: a workgroup per 16 outputs, 64 strands over the partials (strand s takes
 // blk = s mod 64, four rotating accumulators, all its loads independent), strands added in order in LDS.
 // Fixed order, so the same bits every run.
@@ -310,6 +429,15 @@ int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
    // y = A11 \ rp = L^{-T} (L^{-1} rp)
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->LinvT, k, A->rp, A->t);
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y);
+   // S^{-1} = schur_scale I: both K12 passes in one (k_a12_fused_*; NFFT4GP_AMD_AFN_FUSED=0 keeps the two)
+   if (!A->S && a12_fused(A->K12, A->K12f, k, n2, A->cols, A->nblk, A->y, rp2, A->schur_scale, y2, A->part, s)) {
+      hipLaunchKernelGGL(k_a12_reduce, dim3((k + 15) / 16), dim3(1024), 0, s, A->part, A->nblk, k, A->rp);
+      hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->LinvT, k, A->rp, A->t);
+      hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y);
+      hipLaunchKernelGGL(k_scatter, dim3(g), dim3(256), 0, s, A->y, A->perm, n, dx);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   }
    // rp2 -= A12^T y
    const dim3 ga((n2 + 4 * kA12tCols - 1) / (4 * kA12tCols));
    if (A->K12f) {
@@ -545,8 +673,12 @@ int afn_shard_apply(AfnShard* S, double* x, const double* r, hipStream_t s)
    // y1 = A11 \ rp1
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, S->LinvT, k, S->rp1, S->t);
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, S->Linv, k, S->t, S->y1);
+   // S^{-1} = schur_scale I: this rank's columns in one K12 pass (y2 and the partials of K12 y2)
+   const bool fused = !S->fsai && m2 > 0 &&
+                      a12_fused(S->K12, nullptr, k, m2, S->cols, S->nblk, S->y1, S->rp2, S->schur_scale, S->y2,
+                                S->part, s);
    // rp2 -= A12^T y1 on this rank's columns
-   if (m2 > 0) {
+   if (m2 > 0 && !fused) {
       const dim3 ga((m2 + 4 * kA12tCols - 1) / (4 * kA12tCols));
       if (k <= kA12tLdsMax)
          hipLaunchKernelGGL(k_a12t<true>, ga, dim3(256), sizeof(double) * k, s, (const double*)S->K12, k, m2, S->y1,
@@ -582,14 +714,15 @@ int afn_shard_apply(AfnShard* S, double* x, const double* r, hipStream_t s)
             hipLaunchKernelGGL(k_csr_staged, dim3(S->GT.nparts), dim3(kCsrT), 0, s, S->GT.ia, S->GT.ja, S->GT.aa,
                                S->gbuf, S->y2, S->GT.part);
       }
-   } else if (m2 > 0) {
+   } else if (m2 > 0 && !fused) {
       hipLaunchKernelGGL(k_scale_into, dim3(g2), dim3(256), 0, s, S->rp2, m2, S->schur_scale, S->y2);
    }
    // rp1 -= A12 y2: this rank's columns' partial sum (negated by k_a12_reduce), summed over the ranks
    NFFT4GP_HIP_CHECK(hipMemsetAsync(S->w, 0, sizeof(double) * k, s));
    if (m2 > 0) {
-      hipLaunchKernelGGL(k_a12_part<double>, dim3(S->nblk), dim3(256), 0, s, (const double*)S->K12, k, m2, S->cols,
-                         S->y2, S->part);
+      if (!fused)
+         hipLaunchKernelGGL(k_a12_part<double>, dim3(S->nblk), dim3(256), 0, s, (const double*)S->K12, k, m2, S->cols,
+                            S->y2, S->part);
       hipLaunchKernelGGL(k_a12_reduce, dim3((k + 15) / 16), dim3(1024), 0, s, S->part, S->nblk, k, S->w);
    }
    if (S->comm->allreduce(S->w, (size_t)k, s)) return -1;

@@ -355,3 +355,28 @@ def test_afn_fp32_k12_storage_pcg(torch_cuda):
         with pytest.raises(ValueError):
             pre.set_storage(16)
         pre.free()
+
+
+@pytest.mark.parametrize("k,storage", [(256, 64), (600, 64), (1000, 32)])
+def test_afn_noise_apply_in_one_k12_pass(torch_cuda, monkeypatch, k, storage):
+    """S^{-1} = I / noise (schur_opt 0): the apply streams K12 once (k_a12_fused: each column's dot, y2 and its
+    share of K12 y2 from the same registers).  Equal to the two-pass apply (NFFT4GP_AMD_AFN_FUSED=0) to rounding --
+    the K12 y2 sum runs in another fixed order -- and the same bits on every call; 2-16 rows per lane, both
+    storages and a ragged last workgroup (n2 odd)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(k)
+    n, d, f, l, mu = 20001 + 2 * k, 6, 1.0, 0.3, 0.02
+    X = np.asfortranarray(rng.random((n, d)))
+    pre = amd.AfnPrecond.setup(X, k, f, l, mu, perm_opt="fps", schur="noise")
+    assert pre.info()[0] == k
+    if storage == 32:
+        pre.set_storage(32)
+    r = torch.tensor(rng.random(n) - 0.5, device="cuda")
+    z = [torch.zeros(n, dtype=torch.float64, device="cuda") for _ in range(3)]
+    pre.solve(z[0], r.clone())
+    pre.solve(z[1], r.clone())
+    monkeypatch.setenv("NFFT4GP_AMD_AFN_FUSED", "0")
+    pre.solve(z[2], r.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(z[0], z[1])
+    assert ((z[0] - z[2]).norm() / z[2].norm()).item() < 1e-13
