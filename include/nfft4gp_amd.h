@@ -427,6 +427,14 @@ void *Nfft4GPAmdAfnSetup(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int
  * quirk), the FPS order and the KNN pattern still come from data. */
 void *Nfft4GPAmdAfnSetupSchur(const NFFT4GP_DOUBLE *data, int n, int ldim, int d, int k, int perm_opt,
                               const int *perm, int schur_opt, int schur_lfil, int kernel, void *fkernel_params);
+/* The AFN apply's two K12 products (K12^T y1 and K12 y2, afn.c:82-143) as matvecs of this library's additive
+ * NFFT handle op (whole rows, set up over the AFN's n points with its kernel -- the handle the AFN was built
+ * from): the landmark (Schur) part of the permuted vector placed at its points, zero elsewhere, through
+ * Nfft4GPAdditiveNFFTMatSymv's operator and read back at the other part's points (the operator's mu term meets
+ * only zeros there).  The products then carry the NFFT operator's approximation of the dense kernel
+ *  instead of the stored K12's values, at two matvecs per apply instead of two passes over
+ * k (n - k) doubles.  op NULL: back to the stored K12.  op must stay alive while the AFN applies.  0 / -1. */
+int Nfft4GPAmdAfnSetOperator(void *afn, void *op);
 /* the AFN handle's rank, permutation (n) and Schur-complement FSAI (CSR, n - k rows); any output may be
  * NULL; returns the FSAI's nnz (0 without one), -1 on error */
 int Nfft4GPAmdAfnInfo(void *afn, int *k, int *perm, int *ia, int *ja, NFFT4GP_DOUBLE *aa);

@@ -196,6 +196,7 @@ _SIGS = {
                                     vp, C.c_int, C.c_int, vp]),
     "Nfft4GPAmdAfnShardInfo": (C.c_int, [vp, ip, ip, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
     "Nfft4GPAmdAfnSetStorage": (C.c_int, [vp, C.c_int]),
+    "Nfft4GPAmdAfnSetOperator": (C.c_int, [vp, vp]),
     "Nfft4GPAmdPrecondAFNSetStorage": (C.c_int, [vp, C.c_int]),
     "Nfft4GPAmdDistAfnSolve": (C.c_int, [vp, C.c_int, vp, vp]),
     "Nfft4GPAmdDistAfnFree": (None, [vp]),

@@ -46,7 +46,28 @@ struct AfnDev {
    bool own_S = false;
    double *rp = nullptr, *y = nullptr, *t = nullptr, *part = nullptr;
    int nblk = 0, cols = 1;  // A12 y2: workgroups, columns per workgroup
+   // Nfft4GPAmdAfnSetOperator: K12^T y and K12 y2 as matvecs of this library's additive handle (whole rows, the
+   // AFN's points and kernel) instead of passes over the stored K12; u, w: its input and output (n each)
+   void* op = nullptr;
+   double *u = nullptr, *w = nullptr;
 };
+
+// u[perm[i]] = y[i] for the landmark part (which 0: i < k) or the Schur part (which 1: i >= k) of the permuted y,
+// 0 at every other point: the additive operator's input for K12^T y1 (which 0) or K12 y2 (which 1)
+__global__ void k_afn_place(const double* __restrict__ y, const int* __restrict__ perm, int n, int k, int which,
+                            double* __restrict__ u)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) u[perm[i]] = (which ? i >= k : i < k) ? y[i] : 0.0;
+}
+
+// rp[i] -= w[perm[i]], i in [i0, i1): the operator's output read back at the other part's points
+__global__ void k_afn_sub(const double* __restrict__ w, const int* __restrict__ perm, int i0, int i1,
+                          double* __restrict__ rp)
+{
+   const int i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < i1) rp[i] -= w[perm[i]];
+}
 
 // y = A x, a thread per CSR row summing in the row's stored order, unfused (matops.c:239-248); the
 // entries and their gathers go through LDS a workgroup-wide chunk at a time (csr.hpp)
@@ -429,6 +450,28 @@ int afn_apply_obj(void* obj, double* dx, const double* drhs, hipStream_t s)
    // y = A11 \ rp = L^{-T} (L^{-1} rp)
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->LinvT, k, A->rp, A->t);
    hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y);
+   if (A->op) {
+      // K12^T y1 = (A u)[Schur points] with u = y1 at the landmarks and 0 elsewhere: the operator's kernel part is
+      // the AFN's kernel, and its mu term meets only zeros at the points read back; then K12 y2 the same way
+      hipLaunchKernelGGL(k_afn_place, dim3(g), dim3(256), 0, s, (const double*)A->y, A->perm, n, k, 0, A->u);
+      const double* xin[1] = {A->u};
+      double* yout[1] = {A->w};
+      if (additive_matvec_multi(A->op, 1, 1.0, xin, 0.0, yout)) return -1;
+      hipLaunchKernelGGL(k_afn_sub, dim3((n2 + 255) / 256), dim3(256), 0, s, (const double*)A->w, A->perm, k, n, A->rp);
+      if (A->S) {
+         if (fsai_apply_dev(A->S, y2, rp2, s)) return -1;
+      } else {
+         hipLaunchKernelGGL(k_scale_into, dim3((n2 + 255) / 256), dim3(256), 0, s, rp2, n2, A->schur_scale, y2);
+      }
+      hipLaunchKernelGGL(k_afn_place, dim3(g), dim3(256), 0, s, (const double*)A->y, A->perm, n, k, 1, A->u);
+      if (additive_matvec_multi(A->op, 1, 1.0, xin, 0.0, yout)) return -1;
+      hipLaunchKernelGGL(k_afn_sub, dim3((k + 255) / 256), dim3(256), 0, s, (const double*)A->w, A->perm, 0, k, A->rp);
+      hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->LinvT, k, A->rp, A->t);
+      hipLaunchKernelGGL(k_trmv, dim3(gk), dim3(256), 0, s, A->Linv, k, A->t, A->y);
+      hipLaunchKernelGGL(k_scatter, dim3(g), dim3(256), 0, s, A->y, A->perm, n, dx);
+      NFFT4GP_HIP_CHECK(hipGetLastError());
+      return 0;
+   }
    // S^{-1} = schur_scale I: both K12 passes in one (k_a12_fused_*; NFFT4GP_AMD_AFN_FUSED=0 keeps the two)
    if (!A->S && a12_fused(A->K12, A->K12f, k, n2, A->cols, A->nblk, A->y, rp2, A->schur_scale, y2, A->part, s)) {
       hipLaunchKernelGGL(k_a12_reduce, dim3((k + 15) / 16), dim3(1024), 0, s, A->part, A->nblk, k, A->rp);
@@ -918,7 +961,7 @@ void Nfft4GPAmdAfnFree(void* afn)
    AfnDev* A = (AfnDev*)afn;
    if (!A) return;
    for (void* p : {(void*)A->perm, (void*)A->Linv, (void*)A->LinvT, (void*)A->K12, (void*)A->K12f, (void*)A->rp,
-                   (void*)A->y, (void*)A->t, (void*)A->part})
+                   (void*)A->y, (void*)A->t, (void*)A->part, (void*)A->u, (void*)A->w})
       (void)hipFree(p);
    // the Schur complement's FSAI handle stays with its creator (Nfft4GPAmdFsaiFree) unless the AFN was
    // set up on the device (Nfft4GPAmdAfnSetup), which owns it
@@ -950,6 +993,27 @@ int Nfft4GPAmdAfnSetStorage(void* afn, int bits)
    NFFT4GP_HIP_CHECK(hipMalloc((void**)&A->K12f, sizeof(float) * std::max<size_t>(1, count)));
    hipLaunchKernelGGL(k_afn_to_f32, dim3(4096), dim3(256), 0, s, (const double*)A->K12, count, A->K12f);
    NFFT4GP_HIP_CHECK(hipGetLastError());
+   return 0;
+}
+
+int Nfft4GPAmdAfnSetOperator(void* afn, void* op)
+{
+   AfnDev* A = (AfnDev*)afn;
+   if (!A) return -1;
+   if (!op) {
+      A->op = nullptr;
+      return 0;
+   }
+   int nl = 0, ng = 0, rb = 0;
+   if (additive_rows(op, &nl, &ng, &rb) || nl != A->n || ng != A->n) {
+      fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetOperator: needs this library's additive handle over the AFN's "
+                      "%d points (whole rows, after its setup)\n", A->n);
+      return -1;
+   }
+   if (A->k == 0 || A->k == A->n) return 0;  // no K12 products (afn.c:101-110)
+   if (!A->u) NFFT4GP_HIP_CHECK(hipMalloc((void**)&A->u, sizeof(double) * A->n));
+   if (!A->w) NFFT4GP_HIP_CHECK(hipMalloc((void**)&A->w, sizeof(double) * A->n));
+   A->op = op;
    return 0;
 }
 

@@ -238,6 +238,15 @@ class AfnPrecond(_Apply):
             raise ValueError("storage bits must be 32 or 64")
         return self
 
+    def set_operator(self, op):
+        """K12^T y and K12 y2 as matvecs of ``op`` (the NFFTAdditiveKernel this AFN was built from, after its
+        setup) instead of passes over the stored K12 -- the kernel part of the same operator, to its NFFT accuracy;
+        None: back to the stored K12.  Nfft4GPAmdAfnSetOperator; ``op`` must outlive this object's applies."""
+        if _lib.lib().Nfft4GPAmdAfnSetOperator(self.h, op.h if op is not None else None):
+            raise ValueError("Nfft4GPAmdAfnSetOperator failed (see stderr)")
+        self._op = op
+        return self
+
     def info(self):
         """(k, perm, (ia, ja, aa) of the Schur complement's FSAI or None)"""
         L = _lib.lib()
@@ -293,6 +302,18 @@ class PrecondAFN(_Apply):
         Nfft4GPAmdPrecondAFNSetStorage; the gradient-capable branches keep fp64."""
         if _lib.lib().Nfft4GPAmdPrecondAFNSetStorage(self.h, int(bits)):
             raise ValueError("storage bits must be 32 or 64")
+        return self
+
+    def set_operator(self, op):
+        """The AFN branch's K12 products as matvecs of ``op`` (AfnPrecond.set_operator); no effect on the
+        Nystrom / FSAI branches.  Nfft4GPAmdPrecondAFNInfo + Nfft4GPAmdAfnSetOperator."""
+        L = _lib.lib()
+        kind, afn = C.c_int(), C.c_void_p()
+        L.Nfft4GPAmdPrecondAFNInfo(self.h, C.byref(kind), None, C.byref(afn), None)
+        if kind.value == 0 and afn.value:
+            if L.Nfft4GPAmdAfnSetOperator(afn, op.h if op is not None else None):
+                raise ValueError("Nfft4GPAmdAfnSetOperator failed (see stderr)")
+            self._op = op
         return self
 
     def dvp(self, x, mask=None):

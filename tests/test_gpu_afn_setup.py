@@ -380,3 +380,40 @@ def test_afn_noise_apply_in_one_k12_pass(torch_cuda, monkeypatch, k, storage):
     torch.cuda.synchronize()
     assert torch.equal(z[0], z[1])
     assert ((z[0] - z[2]).norm() / z[2].norm()).item() < 1e-13
+
+
+@pytest.mark.parametrize("schur", ["noise", "fsai"])
+def test_afn_k12_products_through_the_operator(torch_cuda, schur):
+    """Nfft4GPAmdAfnSetOperator: the apply's K12^T y1 and K12 y2 as matvecs of the additive handle the AFN was
+    built from.  The apply then carries the NFFT operator's approximation of the dense kernel: equal to the
+    stored-K12 apply to the operator's accuracy, and PCG to 1e-8 takes the same iterations within 2 %."""
+    torch = torch_cuda
+    rng = np.random.default_rng(77)
+    n, d, l, mu, k = 20000, 8, 0.3, 0.01, 256
+    X = np.asfortranarray(rng.random((n, d)))
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    assert op.setup(amd.GAUSSIAN, f=1.0, l=l, mu=mu) == 0
+    pre = amd.AfnPrecond.setup(X, k, 1.0, l, mu, perm_opt="fps", schur_lfil=20, op=op, schur=schur)
+    r = torch.tensor(rng.random(n) - 0.5, device="cuda")
+    z_dense = torch.zeros(n, dtype=torch.float64, device="cuda")
+    pre.solve(z_dense, r.clone())
+    b = torch.tensor(rng.random(n) - 0.5, device="cuda")
+    _, rr0, _, it0 = amd.pcg(op, b, torch.zeros_like(b), maxits=3000, tol=1e-8, precond=pre)
+    pre.set_operator(op)
+    z_op = torch.zeros(n, dtype=torch.float64, device="cuda")
+    pre.solve(z_op, r.clone())
+    torch.cuda.synchronize()
+    err = ((z_op - z_dense).norm() / z_dense.norm()).item()
+    assert err < 1e-6, err
+    _, rr1, _, it1 = amd.pcg(op, b, torch.zeros_like(b), maxits=3000, tol=1e-8, precond=pre)
+    assert rr1 <= 1e-8 and abs(it1 - it0) <= max(2, it0 // 50), (it0, it1)
+    pre.set_operator(None)
+    z_back = torch.zeros(n, dtype=torch.float64, device="cuda")
+    pre.solve(z_back, r.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(z_back, z_dense)
+    # a handle over other points is refused
+    op2 = amd.NFFTAdditiveKernel(X[: n // 2].copy(order="F"), np.arange(d, dtype=np.int32), d, 1)
+    assert op2.setup(amd.GAUSSIAN, f=1.0, l=l, mu=mu) == 0
+    with pytest.raises(ValueError):
+        pre.set_operator(op2)
