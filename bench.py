@@ -691,6 +691,22 @@ def run_config_e(torch, steps, warmup, traffic=True, n=10_000_000, d=64, precisi
     return out
 
 
+def config_b_pcg(torch, n=100_000, d=8, k=256):
+    """BASELINE configs[1]'s solve: PCG to 1e-6 at n = 1e5, 8 1-D windows, l = 0.1, without a preconditioner, with
+    the rank-256 Nystrom and with the rank-256 AFN (Schur FSAI and I/mu; each also with its K12 products through
+    the operator), the same legs as config C's."""
+    import preconditioned_additive_gaussian_processes_with_fourier_acceleration_amd as amd
+    X, _ = make_problem(n, d)
+    op = amd.NFFTAdditiveKernel(X, np.arange(d, dtype=np.int32), d, 1)
+    out = {}
+    out.update(run_pcg_single(op, torch, n))
+    out.update(run_pcg_nystrom(op, torch, n, k))
+    out.update(run_pcg_afn(op, X, torch, n, k, schur="fsai"))
+    out.update(run_pcg_afn(op, X, torch, n, k, schur="noise"))
+    op.free()
+    return {kk: v for kk, v in out.items() if not kk.startswith("nys_setup_mfma")}
+
+
 def config_e_loss(op, torch, X, y, R, d, maxits=50, nvecs=10, l=0.1):
     """BASELINE configs[4]'s step on one GPU: one Nfft4GPGpLoss (gp_loss.c:96-307: FGMRES for K^-1 y with the
     reference's MGS, nvecs Rademacher probes x maxits Lanczos steps, the gradient matvecs) on the leg's handle
@@ -1151,6 +1167,8 @@ def main():
             # BASELINE configs[1]'s operator (n = 1e5, 8 windows, fp64): cache-resident and launch-bound
             result["config_b"] = run_config_e(torch, max(args.steps, 200), args.warmup, traffic=False, n=100_000, d=8,
                                               precisions=(64,), tag="configs[1]", with_loss=False)
+            if not args.no_pcg:
+                result["config_b"].update(config_b_pcg(torch))
         if not args.no_cpu_baseline:
             try:
                 result["cpu_baseline"] = cpu_baseline(n, d, threads=args.cpu_threads)
