@@ -25,6 +25,8 @@
 //   this library: the caller picks k.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -729,6 +731,15 @@ void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm
       if (AG) afn_grad_free(AG);
       return nullptr;
    };
+   // NFFT4GP_AMD_VERBOSE: the setup's phases on stderr (stream synchronised at each stamp)
+   const bool verbose = getenv("NFFT4GP_AMD_VERBOSE") != nullptr;
+   const auto tv0 = std::chrono::steady_clock::now();
+   auto stamp = [&](const char* what) {
+      if (!verbose) return;
+      (void)hipStreamSynchronize(s);
+      fprintf(stderr, "nfft4gp_amd: AFN setup %-28s %8.1f ms\n", what,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tv0).count());
+   };
    if (dalloc(&dX, (size_t)ldim * d)) return fail("allocation");
    const hipMemcpyKind kind = is_device_ptr(data) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
    if (hipMemcpy(dX, data, sizeof(double) * (size_t)ldim * d, kind) != hipSuccess) return fail("upload");
@@ -746,6 +757,7 @@ void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm
          hperm.assign(perm, perm + n);
       }
    }
+   stamp("upload + ordering");
    if (dalloc(&dperm, n) || hipMemcpy(dperm, hperm.data(), sizeof(int) * n, hipMemcpyHostToDevice) != hipSuccess ||
        dalloc(&Xp, (size_t)n * d))
       return fail("allocation");
@@ -779,6 +791,7 @@ void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm
       if (info < 0) return fail("Cholesky / triangular inverse of K11");
       if (gout && chol_factor_dev(Lf, k, dinfo, s)) return fail("Cholesky of K11");
    }
+   stamp("gather + K11 + Cholesky");
    if (n2 > 0 && k > 0) {
       // K12 = K(X1, X2) (afn.c:436), W = L11^{-1} K12 (afn.c:443, dtrtrs; the Schur FSAI's kernel)
       if (dalloc(&K12, (size_t)k * n2) || (schur_opt == 3 && dalloc(&W, (size_t)k * n2))) return fail("allocation");
@@ -818,6 +831,7 @@ void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm
       }
       if (hipGetLastError() != hipSuccess) return fail("gradient kernels");
    }
+   stamp("K12 + W = L11^-1 K12");
    if (n2 > 0 && schur_opt == 3) {
       // FSAI of the Schur complement on X2 (afn.c:445-473): KNN on the points' coordinates, values of the
       // Schur-complement kernel on the kernel coordinates
@@ -833,28 +847,48 @@ void* afn_setup_impl(const double* data, int n, int ldim, int d, int k, int perm
          }
       KernelSpec K2 = Kp;
       K2.Xk = additive ? Xkp + k : nullptr;  // column c of the last n2 points: Xkp + c*n + k + i
+      // without gradients the CSR stays in HBM and the handle (L^T included) is formed there
+      void* keep[3] = {nullptr, nullptr, nullptr};
       const int rc = fsai_kernel_csr(X2, n2, n2, d, schur_lfil, K2, W, k > 0 ? k : 0, gout ? 1 : 0, ia, ja, aa, da, s,
-                                     PB, PC);
+                                     PB, PC, gout ? nullptr : keep);
       (void)hipStreamSynchronize(s);
       (void)hipFree(X2);
       if (rc) return fail("Schur-complement FSAI");
-      if (gout && !std::all_of(da.begin(), da.end(), [](double v) { return std::isfinite(v); })) {
-         fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: the Schur FSAI's gradients are not finite\n");
-         *breakdown = true;
-         return fail(nullptr);
-      }
-      if (!std::all_of(aa.begin(), aa.end(), [](double v) { return std::isfinite(v); })) {
-         fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: the Schur complement's FSAI broke down (non-positive "
-                         "pivot)\n");
-         *breakdown = true;
-         return fail(nullptr);
-      }
-      S = Nfft4GPAmdFsaiCreate(n2, ia.data(), ja.data(), aa.data());
-      if (!S) return fail("FSAI upload");
-      if (gout) {
-         AG = new AfnGrad();
-         AG->S = fsai_grad_create(n2, ia.data(), ja.data(), aa.data(), da.data());
-         if (!AG->S) return fail("FSAI (gradients) upload");
+      if (keep[0]) {
+         const long long bad = count_nonfinite((const double*)keep[2], (size_t)ia[n2], s);
+         if (bad != 0) {
+            for (void* p : keep) (void)hipFree(p);
+            if (bad < 0) return fail("Schur-complement FSAI check");
+            fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: the Schur complement's FSAI broke down (non-positive "
+                            "pivot)\n");
+            *breakdown = true;
+            return fail(nullptr);
+         }
+         stamp("Schur FSAI (KNN, rows)");
+         S = fsai_create_from_device(n2, (int*)keep[0], (int*)keep[1], (double*)keep[2], ia, s);
+         if (!S) return fail("FSAI handle");
+         stamp("FSAI handle (L^T on the device)");
+      } else {
+         if (gout && !std::all_of(da.begin(), da.end(), [](double v) { return std::isfinite(v); })) {
+            fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: the Schur FSAI's gradients are not finite\n");
+            *breakdown = true;
+            return fail(nullptr);
+         }
+         if (!std::all_of(aa.begin(), aa.end(), [](double v) { return std::isfinite(v); })) {
+            fprintf(stderr, "nfft4gp_amd: Nfft4GPAmdAfnSetup: the Schur complement's FSAI broke down (non-positive "
+                            "pivot)\n");
+            *breakdown = true;
+            return fail(nullptr);
+         }
+         stamp("Schur FSAI (KNN, rows)");
+         S = Nfft4GPAmdFsaiCreate(n2, ia.data(), ja.data(), aa.data());
+         if (!S) return fail("FSAI upload");
+         stamp("FSAI handle (L^T, upload)");
+         if (gout) {
+            AG = new AfnGrad();
+            AG->S = fsai_grad_create(n2, ia.data(), ja.data(), aa.data(), da.data());
+            if (!AG->S) return fail("FSAI (gradients) upload");
+         }
       }
    }
    if (gout) {

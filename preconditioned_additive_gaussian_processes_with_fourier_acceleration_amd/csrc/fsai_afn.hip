@@ -10,6 +10,7 @@
 //                    x(perm) = [y; y2].  A11 \ . uses L11^{-1} (two triangular products) instead of the
 //                    reference's Cholesky solves.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -849,6 +850,117 @@ void* afn_shard_from_parts(int n_local, int k, int n2, Comm* comm, const std::ve
       return nullptr;
    }
    return S;
+}
+
+// ---- the FSAI handle from a device CSR: L^T by one radix sort of (column, row) keys -------------------------------
+// key of entry p of row i: column ja[p] above, row i below, so the sorted order is L^T's rows (the columns of L) with
+// each one's entries in ascending row order -- the order fsai_create's host counting sort produces
+__global__ void k_csr_tkeys(const int* __restrict__ ia, const int* __restrict__ ja, int n,
+                            unsigned long long* __restrict__ keys, int* __restrict__ vals, int* __restrict__ tcnt)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= n) return;
+   for (int p = ia[i]; p < ia[i + 1]; p++) {
+      keys[p] = ((unsigned long long)(unsigned)ja[p] << 32) | (unsigned)i;
+      vals[p] = p;
+      atomicAdd(tcnt + ja[p] + 1, 1);  // counts: any order gives the same sums
+   }
+}
+
+__global__ void k_csr_tfill(const unsigned long long* __restrict__ keys, const int* __restrict__ vals,
+                            const double* __restrict__ aa, size_t nnz, int* __restrict__ tja, double* __restrict__ taa)
+{
+   const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+   if (p >= nnz) return;
+   tja[p] = (int)(unsigned)(keys[p] & 0xFFFFFFFFull);
+   taa[p] = aa[vals[p]];
+}
+
+__global__ void k_count_nonfinite(const double* __restrict__ a, size_t count, unsigned long long* __restrict__ out)
+{
+   unsigned long long c = 0;
+   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x)
+      c += isfinite(a[i]) ? 0ull : 1ull;
+   if (c) atomicAdd(out, c);
+}
+
+long long count_nonfinite(const double* d, size_t count, hipStream_t s)
+{
+   unsigned long long* dc = nullptr;
+   unsigned long long h = 0;
+   if (hipMalloc((void**)&dc, sizeof(unsigned long long)) != hipSuccess) return -1;
+   bool ok = hipMemsetAsync(dc, 0, sizeof(unsigned long long), s) == hipSuccess;
+   if (ok && count) hipLaunchKernelGGL(k_count_nonfinite, dim3(1024), dim3(256), 0, s, d, count, dc);
+   ok = ok && hipMemcpyAsync(&h, dc, sizeof(h), hipMemcpyDeviceToHost, s) == hipSuccess &&
+        hipStreamSynchronize(s) == hipSuccess;
+   (void)hipFree(dc);
+   return ok ? (long long)h : -1;
+}
+
+void* fsai_create_from_device(int n, int* dia, int* dja, double* daa, const std::vector<int>& hia, hipStream_t s)
+{
+   FsaiDev* F = new FsaiDev();
+   F->n = n;
+   F->ia = dia;
+   F->ja = dja;
+   F->aa = daa;
+   const size_t nnz = (size_t)hia[n];
+   unsigned long long *k_in = nullptr, *k_out = nullptr;
+   int *v_in = nullptr, *v_out = nullptr;
+   void* tmp = nullptr;
+   size_t tmp_bytes = 0;
+   auto done = [&](bool ok) -> void* {
+      (void)hipStreamSynchronize(s);
+      for (void* p : {(void*)k_in, (void*)k_out, (void*)v_in, (void*)v_out, tmp}) (void)hipFree(p);
+      if (!ok) {
+         fprintf(stderr, "nfft4gp_amd: FSAI handle on the device: allocation or sort failed\n");
+         fsai_free(F);
+         return nullptr;
+      }
+      return F;
+   };
+   if (hipMalloc((void**)&F->tia, sizeof(int) * ((size_t)n + 1)) != hipSuccess ||
+       hipMalloc((void**)&F->tja, sizeof(int) * std::max<size_t>(1, nnz)) != hipSuccess ||
+       hipMalloc((void**)&F->taa, sizeof(double) * std::max<size_t>(1, nnz)) != hipSuccess ||
+       hipMalloc((void**)&F->work, sizeof(double) * std::max(1, n)) != hipSuccess ||
+       hipMalloc((void**)&k_in, sizeof(unsigned long long) * std::max<size_t>(1, nnz)) != hipSuccess ||
+       hipMalloc((void**)&k_out, sizeof(unsigned long long) * std::max<size_t>(1, nnz)) != hipSuccess ||
+       hipMalloc((void**)&v_in, sizeof(int) * std::max<size_t>(1, nnz)) != hipSuccess ||
+       hipMalloc((void**)&v_out, sizeof(int) * std::max<size_t>(1, nnz)) != hipSuccess ||
+       hipMemsetAsync(F->tia, 0, sizeof(int) * ((size_t)n + 1), s) != hipSuccess)
+      return done(false);
+   hipLaunchKernelGGL(k_csr_tkeys, dim3((n + 255) / 256), dim3(256), 0, s, (const int*)dia, (const int*)dja, n, k_in,
+                      v_in, F->tia);
+   int end_bit = 32;
+   while (end_bit < 64 && (1ull << (end_bit - 32)) < (unsigned long long)n) end_bit++;
+   if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, (int)nnz, 0, end_bit, s) !=
+           hipSuccess ||
+       hipMalloc(&tmp, std::max<size_t>(1, tmp_bytes)) != hipSuccess ||
+       hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (int)nnz, 0, end_bit, s) !=
+           hipSuccess)
+      return done(false);
+   (void)hipFree(tmp);
+   tmp = nullptr;
+   tmp_bytes = 0;
+   // tia: counts -> pointers (inclusive sum over tia[1..n])
+   if (hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, F->tia + 1, F->tia + 1, n, s) != hipSuccess ||
+       hipMalloc(&tmp, std::max<size_t>(1, tmp_bytes)) != hipSuccess ||
+       hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, F->tia + 1, F->tia + 1, n, s) != hipSuccess)
+      return done(false);
+   if (nnz)
+      hipLaunchKernelGGL(k_csr_tfill, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, (const unsigned long long*)k_out,
+                         (const int*)v_out, (const double*)daa, nnz, F->tja, F->taa);
+   // the workgroups' row spans of L and L^T (csr_partition, on the host pointers)
+   std::vector<int> htia((size_t)n + 1);
+   if (hipGetLastError() != hipSuccess ||
+       hipMemcpyAsync(htia.data(), F->tia, sizeof(int) * ((size_t)n + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess)
+      return done(false);
+   const std::vector<int> p = csr_partition(n, hia.data()), tp = csr_partition(n, htia.data());
+   F->nparts = (int)p.size() - 1;
+   F->ntparts = (int)tp.size() - 1;
+   if (up(&F->part, p.data(), p.size()) || up(&F->tpart, tp.data(), tp.size())) return done(false);
+   return done(true);
 }
 
 // an AFN apply object from factors already in HBM (afn_setup.hip); takes ownership of d_perm, d_Linv,

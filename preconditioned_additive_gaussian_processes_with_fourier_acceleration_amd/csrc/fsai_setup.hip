@@ -1793,7 +1793,7 @@ int kernel_spec_of(void* fkernel_params, func_kernel fkernel, int kernel, int n,
 // gradients), copied to host CSR.  dW (kw x n, optional): the Schur-complement kernel of the AFN setup.
 int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const KernelSpec& Ks, const double* dW, int kw,
                     int require_grad, std::vector<int>& hia, std::vector<int>& hja, std::vector<double>& haa,
-                    std::vector<double>& hda, hipStream_t s, const double* dGB, const double* dGC)
+                    std::vector<double>& hda, hipStream_t s, const double* dGB, const double* dGC, void** keep)
 {
    if (n <= 0 || ldim < n || d <= 0 || d > kMaxDims || lfil < 1 || lfil > kFsaiMaxK || (dW && kw <= 0)) {
       fprintf(stderr, "nfft4gp_amd: FSAI setup needs 1 <= lfil <= %d and at most %d features\n", kFsaiMaxK,
@@ -1834,6 +1834,19 @@ int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const Ke
    auto rows_kernel = fsai_rows_kernel(lfil);
    hipLaunchKernelGGL(rows_kernel, dim3(n), dim3(64), 0, s, Xk, ldk, dia, dja, P, dW, kw, require_grad ? 1 : 0, nnz,
                       daa, dda, dGB, dGC, (const int*)nullptr);
+   if (keep && !require_grad) {  // the caller builds the handle on the device
+      if (hipGetLastError() != hipSuccess) return cleanup(-1);
+      keep[0] = dia;
+      keep[1] = dja;
+      keep[2] = daa;
+      dia = nullptr;
+      dja = nullptr;
+      daa = nullptr;
+      hja.clear();
+      haa.clear();
+      hda.clear();
+      return cleanup(0);
+   }
    haa.assign((size_t)nnz, 0.0);
    hda.assign(require_grad ? 3 * (size_t)nnz : 0, 0.0);
    if (hipGetLastError() != hipSuccess ||

@@ -375,10 +375,17 @@ struct KernelSpec {
 // K; host CSR out; dW (kw x n): the Schur-complement kernel K - W'W
 // With require_grad and dW: dGB (2 kw x n panels L11^{-1} dK12_g) and dGC (3 panels GdK11G_g W) give the
 // Schur kernel's gradients (fsai_setup.hip k_fsai_rows)
+// keep (no gradients): the CSR stays on the device (keep[0] = ia, keep[1] = ja, keep[2] = aa, owned by the caller);
+// only ia comes back to the host then
 int fsai_kernel_csr(const double* dX, int n, int ldim, int d, int lfil, const KernelSpec& K, const double* dW, int kw,
                     int require_grad, std::vector<int>& ia, std::vector<int>& ja, std::vector<double>& aa,
                     std::vector<double>& da, hipStream_t s, const double* dGB = nullptr,
-                    const double* dGC = nullptr);
+                    const double* dGC = nullptr, void** keep = nullptr);
+// an Nfft4GPAmdFsaiCreate handle from a CSR already in HBM (fsai_afn.hip): takes ownership of dia / dja / daa; hia
+// is the host copy of dia; L^T is formed on the device.  NULL on error (the arrays are freed then)
+void* fsai_create_from_device(int n, int* dia, int* dja, double* daa, const std::vector<int>& hia, hipStream_t s);
+// the number of non-finite values among count doubles (device)
+long long count_nonfinite(const double* d, size_t count, hipStream_t s);
 // a row shard's rows of the FSAI (fsai_setup.hip): the pattern of the listed rows (ascending) -- KNN over their
 // earlier points only -- and the values of a range of pattern rows, W's column of each entry from dwcol
 int fsai_pattern_rows(const double* dX, int n, int ldim, int d, int lfil, const std::vector<int>& rows,
