@@ -296,6 +296,7 @@ class PrecondAFN(_Apply):
         kind, k = C.c_int(), C.c_int()
         L.Nfft4GPAmdPrecondAFNInfo(self.h, C.byref(kind), C.byref(k), None, None)
         self.kind, self.k = self.KINDS[kind.value], k.value
+        self.require_grad = bool(require_grad)
 
     def set_storage(self, bits: int):
         """The AFN's K12 / the Nystrom branch's U read in fp64 (64) or as an fp32 copy (32; fp64 accumulation),
@@ -306,7 +307,10 @@ class PrecondAFN(_Apply):
 
     def set_operator(self, op):
         """The AFN branch's K12 products as matvecs of ``op`` (AfnPrecond.set_operator); no effect on the
-        Nystrom / FSAI branches.  Nfft4GPAmdPrecondAFNInfo + Nfft4GPAmdAfnSetOperator."""
+        Nystrom / FSAI branches, nor with require_grad (as set_storage: Dvp, Trace and Logdet describe the stored
+        factors, so the solve keeps them).  Nfft4GPAmdPrecondAFNInfo + Nfft4GPAmdAfnSetOperator."""
+        if self.require_grad:
+            return self
         L = _lib.lib()
         kind, afn = C.c_int(), C.c_void_p()
         L.Nfft4GPAmdPrecondAFNInfo(self.h, C.byref(kind), None, C.byref(afn), None)
