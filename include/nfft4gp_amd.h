@@ -433,7 +433,8 @@ void *Nfft4GPAmdAfnSetupSchur(const NFFT4GP_DOUBLE *data, int n, int ldim, int d
  * Nfft4GPAdditiveNFFTMatSymv's operator and read back at the other part's points (the operator's mu term meets
  * only zeros there).  The products then carry the NFFT operator's approximation of the dense kernel
  *  instead of the stored K12's values, at two matvecs per apply instead of two passes over
- * k (n - k) doubles.  op NULL: back to the stored K12.  op must stay alive while the AFN applies.  0 / -1. */
+ * k (n - k) doubles.  op NULL: back to the stored K12.  op must stay alive while the AFN applies.  An AFN
+ * set up with gradients keeps the stored K12 (its Dvp / Trace / Logdet describe those factors).  0 / -1. */
 int Nfft4GPAmdAfnSetOperator(void *afn, void *op);
 /* the AFN handle's rank, permutation (n) and Schur-complement FSAI (CSR, n - k rows); any output may be
  * NULL; returns the FSAI's nnz (0 without one), -1 on error */
