@@ -59,7 +59,7 @@ def analyse(path):
     gaps.sort(reverse=True)
     by = {}
     for s, e, name in win:
-        key = name.split("(")[0][-60:]
+        key = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][-60:]
         by[key] = by.get(key, 0) + (e - s)
     out = {"span_ms": (t1 - t0) / 1e6, "busy_ms": busy / 1e6, "idle_ms": (t1 - t0 - busy) / 1e6,
            "kernels": len(win), "gaps_over_20us": sum(1 for g in gaps if g[0] > 20000),
