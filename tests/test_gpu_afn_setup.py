@@ -419,3 +419,43 @@ def test_afn_k12_products_through_the_operator(torch_cuda, schur):
     assert op2.setup(amd.GAUSSIAN, f=1.0, l=l, mu=mu) == 0
     with pytest.raises(ValueError):
         pre.set_operator(op2)
+
+
+@pytest.mark.parametrize("k", [0, 300])
+def test_device_built_fsai_handle_matches_the_host_build(torch_cuda, k):
+    """The AFN setup forms its Schur FSAI handle in HBM (L^T by a radix sort of (column, row) keys); the handle
+    built on the host from the same CSR (Nfft4GPAmdFsaiCreate's counting sort) applies with the same bits.
+    k = 0: the AFN is that FSAI alone; k > 0: the Schur part of the apply is compared through an AfnPrecond
+    assembled on the host from the device setup's own pieces."""
+    torch = torch_cuda
+    rng = np.random.default_rng(123 + k)
+    n, d, f, l, mu = 6000, 3, 1.0, 0.2, 0.01
+    X = np.asfortranarray(rng.random((n, d)))
+    pre = amd.AfnPrecond.setup(X, k, f, l, mu, perm_opt="identity", schur_lfil=20)
+    kk, perm, csr = pre.info()
+    assert kk == k and csr is not None
+    ia, ja, aa = csr
+    host = amd.FsaiPrecond(ia, ja, aa)
+    m = n - k
+    r = torch.tensor(rng.random(m) - 0.5, device="cuda")
+    z_host = torch.zeros(m, dtype=torch.float64, device="cuda")
+    host.solve(z_host, r.clone())
+    if k == 0:
+        z_dev = torch.zeros(m, dtype=torch.float64, device="cuda")
+        pre.solve(z_dev, r.clone())
+        torch.cuda.synchronize()
+        assert torch.equal(z_dev, z_host)
+    else:
+        # M^{-1} applied to a vector that is zero on the landmarks and r on the Schur points, with the landmark
+        # block's contribution removed, is the FSAI of the Schur part: compare against a host-built AFN instead
+        K11 = O.gaussian_block(X, f, l, perm[:k], perm[:k]) + mu * f * f * np.eye(k)
+        L11 = np.linalg.cholesky(K11)
+        K12 = O.gaussian_block(X, f, l, perm[:k], perm[k:])
+        ref = amd.AfnPrecond(perm, L11, K12, host)
+        b = torch.tensor(rng.random(n) - 0.5, device="cuda")
+        z1 = torch.zeros(n, dtype=torch.float64, device="cuda")
+        z2 = torch.zeros(n, dtype=torch.float64, device="cuda")
+        pre.solve(z1, b.clone())
+        ref.solve(z2, b.clone())
+        torch.cuda.synchronize()
+        assert ((z1 - z2).norm() / z2.norm()).item() < 1e-9
