@@ -31,9 +31,12 @@ def test_library_exports_every_header_symbol():
 
 
 def test_library_is_gfx950_code_object():
+    """Every device code object in the library targets gfx950 (bundle target ids); rocPRIM's host code carries
+    other architectures' names only as strings of its run-time config lookup."""
+    import re
     blob = open(amd._lib.LIB_PATH, "rb").read()
-    assert b"amdgcn-amd-amdhsa--gfx950" in blob
-    assert b"gfx942" not in blob and b"gfx90a" not in blob
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-f]+)", blob))
+    assert targets == {b"gfx950"}, targets
 
 
 def test_struct_layout_matches_reference():
