@@ -153,7 +153,8 @@ struct DevLayout {
 };
 
 // multi-dimensional windows (nfft_md.hip): per-component 64^d grids, dims <= kMdMaxDim
-constexpr int kMdMaxDim = 4;     // 4-feature windows: 64^4 grids (134 MB each), the untiled spread / interp
+constexpr int kMdMaxDim = 5;     // up to 5-feature windows: 64^5 grids (8.6 GB each, ~77 GB of buffers per
+                                 // 5-feature window), the untiled spread / interp from 4 features on
 constexpr int kMdTiledMaxDim = 3;  // the tiled kernels' LDS footprint (17^d doubles) fits up to 3 features
 struct MdComp {
    int d = 0;
@@ -174,7 +175,8 @@ struct MdPlan {
    double* d_grid = nullptr; // [nw][G] spread grid
    double2* d_F[2] = {nullptr, nullptr};  // forward ping-pong [nw][Cmax]
    double2* d_Mo[2] = {nullptr, nullptr}; // modes x bhat (chain 0: K, chain 1: K') [nw][M]
-   double2* d_B[4] = {nullptr, nullptr, nullptr, nullptr};  // backward ping-pong, 2 per chain
+   double2* d_B[4] = {nullptr, nullptr, nullptr, nullptr};  // backward ping-pong, 2 per chain; chain 0's
+                                                            // two alias d_F (free once the modes are formed)
    double* d_h[2] = {nullptr, nullptr};   // interpolation grids [nw][G]
    double* d_bh = nullptr;   // [nw][M]  weight * bhat * prod 1/phihut (second deconvolution)
    double* d_bhd = nullptr;  // [nw][M]  the same for the derivative kernel, times dscale

@@ -1,5 +1,5 @@
-// nfft_md.hip -- the additive operator for windows of 2 or 3 features (TEST1's bike / poletele windows,
-// BASELINE config A), and any handle mixing them with 1-D windows.
+// nfft_md.hip -- the additive operator for windows of 2 to 5 features (TEST1's bike / poletele windows of 2 and
+// 3, BASELINE config A), and any handle mixing them with 1-D windows.
 //
 // Same algorithm as the 1-D path (NFFT3 fastsum with N = 32, n_os = 64, m = 4, nfft_interface.c:216-256,
 // :426, :533-534; see window.cpp), on 64^d grids:
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_spread_tiled(const MdCo
    const int d = cp.d;
    int foot = 1;
    for (int t = 0; t < d; t++) foot *= kMdFoot;
-   int lo[kMdMaxDim];
+   int lo[kMdTiledMaxDim];
    {
       int rem = it.y;
       for (int t = 0; t < d; t++) {
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(kMdLinesThreads) void k_md_spread_lines(const MdCom
    const int grp = tid / lines, line = tid - grp * lines;
    const bool active = grp < groups;
    const int yl = line % kMdFoot, zl = line / kMdFoot;
-   int lo[kMdMaxDim];
+   int lo[kMdTiledMaxDim];
    {
       int rem = it.y;
       for (int t = 0; t < d; t++) {
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(kMdSpreadThreads) void k_md_interp_tiled(const MdCo
    const int d = cp.d;
    int foot = 1;
    for (int t = 0; t < d; t++) foot *= kMdFoot;
-   int lo[kMdMaxDim];
+   int lo[kMdTiledMaxDim];
    {
       int rem = it.y;
       for (int t = 0; t < d; t++) {
@@ -726,6 +726,7 @@ void md_free(AdditivePlan& P)
    dfree_md(D.d_u);
    dfree_md(D.d_psi);
    dfree_md(D.d_grid);
+   D.d_B[0] = D.d_B[1] = nullptr;  // aliases of d_F
    for (auto& p : D.d_F) dfree_md(p);
    for (auto& p : D.d_Mo) dfree_md(p);
    for (auto& p : D.d_B) dfree_md(p);
@@ -810,12 +811,15 @@ int md_build_points(AdditivePlan& P, const std::vector<std::vector<double>>& xs)
    const size_t nw = (size_t)P.nw;
    if (dalloc(&D.d_comps, nw) || dalloc(&D.d_u, u.size()) || dalloc(&D.d_psi, psi.size()) ||
        dalloc(&D.d_grid, nw * D.G) || dalloc(&D.d_F[0], nw * D.Cmax) || dalloc(&D.d_F[1], nw * D.Cmax) ||
-       dalloc(&D.d_Mo[0], nw * D.M) || dalloc(&D.d_Mo[1], nw * D.M) || dalloc(&D.d_B[0], nw * D.Cmax) ||
-       dalloc(&D.d_B[1], nw * D.Cmax) || dalloc(&D.d_B[2], nw * D.Cmax) || dalloc(&D.d_B[3], nw * D.Cmax) ||
+       dalloc(&D.d_Mo[0], nw * D.M) || dalloc(&D.d_Mo[1], nw * D.M) || dalloc(&D.d_B[2], nw * D.Cmax) ||
+       dalloc(&D.d_B[3], nw * D.Cmax) ||
        dalloc(&D.d_h[0], nw * D.G) || dalloc(&D.d_h[1], nw * D.G) || dalloc(&D.d_bh, nw * D.M) ||
        dalloc(&D.d_bhd, nw * D.M) || dalloc(&D.d_dot_part, (size_t)kMdInterpBlocks) ||
        dalloc(&D.d_dot_ticket, (size_t)kTicketWords) || dalloc(&D.d_xmax, 1))
       return -1;
+   // the backward passes of chain 0 run in the forward passes' buffers: k_md_modes has read them by then
+   D.d_B[0] = D.d_F[0];
+   D.d_B[1] = D.d_F[1];
    // the spread's fixed-point grids (16 B per cell): every window's at once, or -- windows beyond the tiled
    // kernels (4 features: 64^4 cells) whose set would pass 256 MB -- one window's, reused window by window
    D.gfix_per_window = D.maxd > kMdTiledMaxDim && nw > 1 && 16.0 * (double)nw * (double)D.G > 256.0 * (1 << 20);

@@ -11,7 +11,9 @@
 //       w[s] = sum_{k=-N/2}^{N/2-1} bhat_k / phihut_k^2 cos(2 pi k s / n_os).
 #include <cmath>
 #include <complex>
+#include <algorithm>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "internal.h"
@@ -155,16 +157,29 @@ void bhat_nd(int kind, int d, double c, std::vector<double>& bhat)
    }
    std::complex<double> tw[kBand];
    for (int m = 0; m < N; m++) tw[m] = std::polar(1.0, -2.0 * kPi * (double)m / (double)N);
+   // 5-feature windows have 32^5 modes (5 passes of 1.1e9 complex products): the passes are split over up to
+   // 16 host threads by output index (each output's sum is unchanged, so are the bits)
+   const int nth = nm >= (1 << 20) ? std::max(1, std::min(16, (int)std::thread::hardware_concurrency())) : 1;
    int stride = 1;
    for (int t = 0; t < d; t++) {
-      for (int j = 0; j < nm; j++) {
-         const int lo = j % stride, kt = (j / stride) % N, hi = j / (stride * N);
-         std::complex<double> acc = 0.0;
-         for (int l = 0; l < N; l++) {
-            const int m = ((((kt - N / 2) * (l - N / 2)) % N) + N) % N;  // exact phase reduction
-            acc += a[lo + stride * (l + N * hi)] * tw[m];
+      auto pass = [&](int j0, int j1) {
+         for (int j = j0; j < j1; j++) {
+            const int lo = j % stride, kt = (j / stride) % N, hi = j / (stride * N);
+            std::complex<double> acc = 0.0;
+            for (int l = 0; l < N; l++) {
+               const int m = ((((kt - N / 2) * (l - N / 2)) % N) + N) % N;  // exact phase reduction
+               acc += a[lo + stride * (l + N * hi)] * tw[m];
+            }
+            b[j] = acc;
          }
-         b[j] = acc;
+      };
+      if (nth == 1) {
+         pass(0, nm);
+      } else {
+         std::vector<std::thread> th;
+         const int per = (nm + nth - 1) / nth;
+         for (int i = 0; i < nth; i++) th.emplace_back(pass, std::min(nm, i * per), std::min(nm, (i + 1) * per));
+         for (auto& x : th) x.join();
       }
       a.swap(b);
       stride *= N;

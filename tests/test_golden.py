@@ -202,3 +202,22 @@ def test_fps_restatement_matches_compiled_reference(n, d, k, tol):
     p, dist = fps_par1(X, k, tol)
     np.testing.assert_array_equal(p, p_ref)
     np.testing.assert_array_equal(dist, d_ref)
+
+
+def test_oracle_constant_feature_slice():
+    """The slice property tests/test_gpu_md.py uses to pin the 5-feature path, measured on the oracle one and two
+    levels down: a window with one more, constant feature is the smaller window's fastsum up to the window
+    function's error along the extra axis (2 -> 3 features: 4.98e-8, gradient 5.9e-8), not bit for bit."""
+    rng = np.random.default_rng(404)
+    n = 300
+    X = rng.random((n, 2))
+    x = rng.random(n) - 0.5
+    a = OracleAdditiveNFFT(X, np.arange(2, dtype=np.int32), 1, 2)
+    b = OracleAdditiveNFFT(np.hstack([X, np.full((n, 1), 0.37)]), np.arange(3, dtype=np.int32), 1, 3)
+    a.setup(0, 1.0, 1.0, 0.01)
+    b.setup(0, 1.0, 1.0, 0.01)
+    r = np.linalg.norm(b.matsymv(x) - a.matsymv(x)) / np.linalg.norm(a.matsymv(x))
+    ga, gb = a.gradmatsymv(x), b.gradmatsymv(x)
+    rg = [np.linalg.norm(gb[i * n:(i + 1) * n] - ga[i * n:(i + 1) * n]) / np.linalg.norm(ga[i * n:(i + 1) * n])
+          for i in range(3)]
+    assert 1e-9 < r < 1e-7 and max(rg) < 1e-7, (r, rg)

@@ -159,11 +159,12 @@ def test_single_component_api(torch_cuda):
     assert rel(g, orc.gradmatsymv(x)) <= TOL_TIGHT
 
 
-def test_window_of_five_features_fails_loudly(torch_cuda):
-    """Windows of 1-4 features run (test_gpu_md.py); 5 features is refused with -1 and a message."""
-    n, d = 1000, 5
+def test_window_of_six_features_fails_loudly(torch_cuda):
+    """Windows of 1-5 features run (test_gpu_md.py); 6 features (a 64^6 grid: 550 GB) is refused with -1 and a
+    message."""
+    n, d = 1000, 6
     X, _ = make(n, d)
-    op = amd.NFFTAdditiveKernel(X, np.arange(5, dtype=np.int32), 1, 5)
+    op = amd.NFFTAdditiveKernel(X, np.arange(6, dtype=np.int32), 1, 6)
     assert op.setup(amd.GAUSSIAN, 1.0, 1.0, 0.01) == -1
 
 
