@@ -510,14 +510,21 @@ __global__ __launch_bounds__(kMdThreads) void k_md_combine(int nw, const double*
 }
 
 // forward pass along axis t: in [32^t][64][64^(d-t-1)] (real grid when t == 0) -> out [32^t][32][...]
+// The twiddle index ((k - 16) l) & 63 differs across a wave's lanes (k, or l in the backward pass): the 64
+// twiddles are staged in LDS once per workgroup (bike 0.335 -> 0.310 ms, 5 features 236 -> 229 ms per matvec
+// against per-lane loads from the constant table, profiles/r06_md_twiddles_ab.txt; same bits).
 __global__ __launch_bounds__(kMdThreads) void k_md_fwd(const MdComp* __restrict__ comps, int t,
                                                        const double* __restrict__ grid, long long G,
                                                        double2* __restrict__ F0, double2* __restrict__ F1,
                                                        long long Cmax)
 {
+   __shared__ double2 s_tw[kNos];
    const int c = blockIdx.y;
    const int d = comps[c].d;
-   if (t >= d) return;
+   if (t >= d) return;  // uniform over the workgroup
+   if (threadIdx.x < kNos) s_tw[threadIdx.x] = c_tw[threadIdx.x];
+   __syncthreads();
+   const double2* tw = s_tw;
    const int lo = ipow_i(kBand, t), hi = ipow_i(kNos, d - t - 1);
    const int e = blockIdx.x * kMdThreads + threadIdx.x;
    if (e >= lo * kBand * hi) return;
@@ -527,7 +534,7 @@ __global__ __launch_bounds__(kMdThreads) void k_md_fwd(const MdComp* __restrict_
       const double* in = grid + (long long)c * G;
       for (int l = 0; l < kNos; l++) {
          const double v = in[lo_i + (long long)lo * (l + kNos * h)];
-         const double2 w = c_tw[((k - kBand / 2) * l) & (kNos - 1)];
+         const double2 w = tw[((k - kBand / 2) * l) & (kNos - 1)];
          acc.x = fma(v, w.x, acc.x);
          acc.y = fma(v, w.y, acc.y);
       }
@@ -535,7 +542,7 @@ __global__ __launch_bounds__(kMdThreads) void k_md_fwd(const MdComp* __restrict_
       const double2* in = ((t - 1) & 1 ? F1 : F0) + (long long)c * Cmax;
       for (int l = 0; l < kNos; l++) {
          const double2 v = in[lo_i + (long long)lo * (l + kNos * h)];
-         const double2 w = c_tw[((k - kBand / 2) * l) & (kNos - 1)];
+         const double2 w = tw[((k - kBand / 2) * l) & (kNos - 1)];
          acc.x = fma(v.x, w.x, fma(-v.y, w.y, acc.x));
          acc.y = fma(v.x, w.y, fma(v.y, w.x, acc.y));
       }
@@ -543,6 +550,86 @@ __global__ __launch_bounds__(kMdThreads) void k_md_fwd(const MdComp* __restrict_
    double2* out = (t & 1 ? F1 : F0) + (long long)c * Cmax;
    const double s = c_phinv[k];
    out[lo_i + (long long)lo * (k + kBand * h)] = make_double2(acc.x * s, acc.y * s);
+}
+
+// Passes t >= 1 with one thread per line: the per-output kernels above give each of a line's 32 (forward) or
+// 64 (backward) outputs its own thread, lo = 32^t / 64^t threads apart, so every input is fetched 32 / 64 times
+// from L2 or HBM (5 features: 34 ms per backward pass, 550 GB of requests; 230 -> 68 ms per matvec).  Here thread (lo_i, h) reads its
+// line once -- lanes run along lo_i, so loads and stores are coalesced -- and forms all the line's outputs:
+// the forward keeps 32 accumulators, the backward keeps the 32 inputs, in registers.  Every output is the
+// same fma chain in the same order as in the per-output kernels, so the bits are the same.
+__global__ __launch_bounds__(kMdThreads) void k_md_fwd_lines(const MdComp* __restrict__ comps, int t,
+                                                             double2* __restrict__ F0, double2* __restrict__ F1,
+                                                             long long Cmax)
+{
+   __shared__ double2 s_tw[kNos];
+   const int c = blockIdx.y;
+   const int d = comps[c].d;
+   if (t >= d) return;  // uniform over the workgroup
+   if (threadIdx.x < kNos) s_tw[threadIdx.x] = c_tw[threadIdx.x];
+   __syncthreads();
+   const int lo = ipow_i(kBand, t), hi = ipow_i(kNos, d - t - 1);
+   const int e = blockIdx.x * kMdThreads + threadIdx.x;
+   if (e >= lo * hi) return;
+   const int lo_i = e % lo, h = e / lo;
+   const double2* in = ((t - 1) & 1 ? F1 : F0) + (long long)c * Cmax + lo_i + (long long)lo * kNos * h;
+   double2 acc[kBand];
+#pragma unroll
+   for (int k = 0; k < kBand; k++) acc[k] = make_double2(0.0, 0.0);
+   for (int l = 0; l < kNos; l++) {
+      const double2 v = in[(long long)lo * l];
+#pragma unroll
+      for (int k = 0; k < kBand; k++) {
+         const double2 w = s_tw[((k - kBand / 2) * l) & (kNos - 1)];
+         acc[k].x = fma(v.x, w.x, fma(-v.y, w.y, acc[k].x));
+         acc[k].y = fma(v.x, w.y, fma(v.y, w.x, acc[k].y));
+      }
+   }
+   double2* out = (t & 1 ? F1 : F0) + (long long)c * Cmax + lo_i + (long long)lo * kBand * h;
+#pragma unroll
+   for (int k = 0; k < kBand; k++) {
+      const double sc = c_phinv[k];
+      out[(long long)lo * k] = make_double2(acc[k].x * sc, acc[k].y * sc);
+   }
+}
+
+__global__ __launch_bounds__(kMdThreads) void k_md_bwd_lines(const MdComp* __restrict__ comps, int t,
+                                                             double2* __restrict__ B0, double2* __restrict__ B1,
+                                                             double2* __restrict__ B2, double2* __restrict__ B3,
+                                                             long long Cmax, double* __restrict__ h0,
+                                                             double* __restrict__ h1, long long G)
+{
+   __shared__ double2 s_tw[kNos];
+   const int c = blockIdx.y, chain = blockIdx.z;
+   const int d = comps[c].d;
+   if (t >= d) return;  // uniform over the workgroup
+   if (threadIdx.x < kNos) s_tw[threadIdx.x] = c_tw[threadIdx.x];
+   __syncthreads();
+   const int lo = ipow_i(kNos, t), hi = ipow_i(kBand, d - t - 1);
+   const int e = blockIdx.x * kMdThreads + threadIdx.x;
+   if (e >= lo * hi) return;
+   const int lo_i = e % lo, h = e / lo;
+   double2* Ba = chain ? B2 : B0;
+   double2* Bb = chain ? B3 : B1;
+   const double2* in = ((t - 1) & 1 ? Bb : Ba) + (long long)c * Cmax + lo_i + (long long)lo * kBand * h;
+   double2 v[kBand];
+#pragma unroll
+   for (int k = 0; k < kBand; k++) v[k] = in[(long long)lo * k];
+   const long long o = lo_i + (long long)lo * kNos * h;
+#pragma unroll 1
+   for (int l = 0; l < kNos; l++) {
+      double2 acc = {0.0, 0.0};
+#pragma unroll
+      for (int k = 0; k < kBand; k++) {
+         const double2 w = s_tw[((k - kBand / 2) * l) & (kNos - 1)];  // conjugated below
+         acc.x = fma(v[k].x, w.x, fma(v[k].y, w.y, acc.x));
+         acc.y = fma(v[k].y, w.x, fma(-v[k].x, w.y, acc.y));
+      }
+      if (t == d - 1)
+         (chain ? h1 : h0)[(long long)c * G + o + (long long)lo * l] = acc.x;
+      else
+         ((t & 1) ? Bb : Ba)[(long long)c * Cmax + o + (long long)lo * l] = acc;
+   }
 }
 
 // modes: chain 0 = a * bh, chain 1 = a * bhd
@@ -577,9 +664,13 @@ __global__ __launch_bounds__(kMdThreads) void k_md_bwd(const MdComp* __restrict_
                                                        long long Cmax, double* __restrict__ h0,
                                                        double* __restrict__ h1, long long G)
 {
+   __shared__ double2 s_tw[kNos];
    const int c = blockIdx.y, chain = blockIdx.z;
    const int d = comps[c].d;
-   if (t >= d) return;
+   if (t >= d) return;  // uniform over the workgroup
+   if (threadIdx.x < kNos) s_tw[threadIdx.x] = c_tw[threadIdx.x];
+   __syncthreads();
+   const double2* tw = s_tw;
    const int lo = ipow_i(kNos, t), hi = ipow_i(kBand, d - t - 1);
    const int e = blockIdx.x * kMdThreads + threadIdx.x;
    if (e >= lo * kNos * hi) return;
@@ -590,7 +681,7 @@ __global__ __launch_bounds__(kMdThreads) void k_md_bwd(const MdComp* __restrict_
    double2 acc = {0.0, 0.0};
    for (int k = 0; k < kBand; k++) {
       const double2 v = in[lo_i + (long long)lo * (k + kBand * h)];
-      const double2 w = c_tw[((k - kBand / 2) * l) & (kNos - 1)];  // conjugated below
+      const double2 w = tw[((k - kBand / 2) * l) & (kNos - 1)];  // conjugated below
       acc.x = fma(v.x, w.x, fma(v.y, w.y, acc.x));
       acc.y = fma(v.y, w.x, fma(-v.x, w.y, acc.y));
    }
@@ -1023,13 +1114,23 @@ static int md_spread_untiled(const AdditivePlan& P, const double* d_x, double ps
 int md_grid(const AdditivePlan& P, const double* d_grid, int grad, hipStream_t s)
 {
    const MdPlan& D = P.md;
+   // passes t >= 1 one thread per line once the grids pass the Infinity Cache (4 and 5 features: 64^4 complex
+   // cells are 268 MB); 2- and 3-feature grids (4 MB) serve the per-output kernels' re-reads from L2 and keep
+   // their parallelism (bike 0.31 vs 0.52 ms per matvec).  NFFT4GP_AMD_MD_LINES_DFT=0 / 2 forces one per output /
+   // per line; the bits are the same (profiles/r06_md_lines_dft_ab.txt).
+   static const int lines_env = getenv("NFFT4GP_AMD_MD_LINES_DFT") ? atoi(getenv("NFFT4GP_AMD_MD_LINES_DFT")) : 1;
+   const bool lines_dft = lines_env == 2 || (lines_env == 1 && D.maxd >= 4);
    for (int t = 0; t < D.maxd; t++) {
       // largest pass over the components: 32^(t+1) 64^(maxd-t-1) outputs
       long long outs = 1;
       for (int a = 0; a <= t; a++) outs *= kBand;
       for (int a = t + 1; a < D.maxd; a++) outs *= kNos;
-      hipLaunchKernelGGL(k_md_fwd, dim3((unsigned)((outs + kMdThreads - 1) / kMdThreads), P.nw), dim3(kMdThreads), 0,
-                         s, D.d_comps, t, d_grid, D.G, D.d_F[0], D.d_F[1], D.Cmax);
+      if (t > 0 && lines_dft)  // one thread per line of 64 inputs
+         hipLaunchKernelGGL(k_md_fwd_lines, dim3((unsigned)((outs / kBand + kMdThreads - 1) / kMdThreads), P.nw),
+                            dim3(kMdThreads), 0, s, D.d_comps, t, D.d_F[0], D.d_F[1], D.Cmax);
+      else
+         hipLaunchKernelGGL(k_md_fwd, dim3((unsigned)((outs + kMdThreads - 1) / kMdThreads), P.nw), dim3(kMdThreads), 0,
+                            s, D.d_comps, t, d_grid, D.G, D.d_F[0], D.d_F[1], D.Cmax);
    }
    hipLaunchKernelGGL(k_md_modes, dim3((unsigned)((D.M + kMdThreads - 1) / kMdThreads), P.nw), dim3(kMdThreads), 0, s,
                       D.d_comps, D.d_F[0], D.d_F[1], D.Cmax, D.d_bh, D.d_bhd, D.M, grad, D.d_Mo[0], D.d_Mo[1]);
@@ -1037,9 +1138,15 @@ int md_grid(const AdditivePlan& P, const double* d_grid, int grad, hipStream_t s
       long long outs = 1;
       for (int a = 0; a <= t; a++) outs *= kNos;
       for (int a = t + 1; a < D.maxd; a++) outs *= kBand;
-      hipLaunchKernelGGL(k_md_bwd, dim3((unsigned)((outs + kMdThreads - 1) / kMdThreads), P.nw, grad ? 2 : 1),
-                         dim3(kMdThreads), 0, s, D.d_comps, t, D.d_Mo[0], D.d_Mo[1], D.M, D.d_B[0], D.d_B[1],
-                         D.d_B[2], D.d_B[3], D.Cmax, D.d_h[0], D.d_h[1], D.G);
+      if (t > 0 && lines_dft)  // one thread per line of 32 modes
+         hipLaunchKernelGGL(k_md_bwd_lines, dim3((unsigned)((outs / kNos + kMdThreads - 1) / kMdThreads), P.nw,
+                                                 grad ? 2 : 1),
+                            dim3(kMdThreads), 0, s, D.d_comps, t, D.d_B[0], D.d_B[1], D.d_B[2], D.d_B[3], D.Cmax,
+                            D.d_h[0], D.d_h[1], D.G);
+      else
+         hipLaunchKernelGGL(k_md_bwd, dim3((unsigned)((outs + kMdThreads - 1) / kMdThreads), P.nw, grad ? 2 : 1),
+                            dim3(kMdThreads), 0, s, D.d_comps, t, D.d_Mo[0], D.d_Mo[1], D.M, D.d_B[0], D.d_B[1],
+                            D.d_B[2], D.d_B[3], D.Cmax, D.d_h[0], D.d_h[1], D.G);
    }
    NFFT4GP_HIP_CHECK(hipGetLastError());
    return 0;

@@ -1,7 +1,7 @@
 """Multi-feature windows (nfft_md.hip): matvec time per configuration, hipEvent-timed over repeated
 matvecs on the library stream.
-    python tools/md_probe.py
-Configurations: n points, nw windows of dw features (2-D / 3-D windows; TEST1's bike is 3 x 3-D)."""
+    python tools/md_probe.py [n,nw,dw ...]
+Configurations (default below, or the ones given): n points, nw windows of dw features (2-D / 3-D windows; TEST1's bike is 3 x 3-D)."""
 import json
 import os
 import sys
@@ -20,7 +20,8 @@ def main():
     s = torch.cuda.Stream()
     torch.cuda.set_stream(s)
     amd.lib().Nfft4GPAmdSetStream(s.cuda_stream)
-    for n, nw, dw in CONFIGS:
+    configs = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]] or CONFIGS
+    for n, nw, dw in configs:
         rng = np.random.default_rng(n + nw)
         X = np.asfortranarray(rng.random((n, nw * dw)))
         win = np.arange(nw * dw, dtype=np.int32)
